@@ -1,0 +1,284 @@
+"""MI355X VP9 hybrid decoder — Python host bindings.
+
+The product is the C-ABI shared library ``libvp9hip.so`` (include/vp9hip.h): host
+runtime + gfx950 HIP kernels for the VP9 pixel path (inverse transforms, intra
+prediction, motion compensation, loop filter). This module only binds it with
+ctypes and mirrors the reference's decode API for this path
+(``avcodec_send_packet`` / ``avcodec_receive_frame``, libavcodec/avcodec.c:707-717;
+the VP9 decoder's frame loop vp9.c:1606-1863) at the pass-1 packet level.
+
+There is no CPU fallback: if the HIP library cannot be loaded, every entry point
+raises :class:`Vp9HipUnavailable`.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libvp9hip.so")
+
+# AVERROR codes (include/vp9hip.h)
+EINVAL = -22
+ENOMEM = -12
+ENOSYS = -38
+EINVALIDDATA = -1094995529
+EEXTERNAL = -542398533
+
+BS_64x64, BS_64x32, BS_32x64, BS_32x32, BS_32x16, BS_16x32, BS_16x16, BS_16x8, BS_8x16, \
+    BS_8x8, BS_8x4, BS_4x8, BS_4x4 = range(13)
+
+
+class Vp9HipUnavailable(RuntimeError):
+    pass
+
+
+class Vp9HipError(RuntimeError):
+    def __init__(self, fn, code):
+        super().__init__("%s failed with AVERROR %d" % (fn, code))
+        self.code = code
+
+
+class Block(ctypes.Structure):
+    """vp9h_block (include/vp9hip.h) == VP9Block (vp9dec.h:89-97)."""
+    _fields_ = [("row", ctypes.c_uint16), ("col", ctypes.c_uint16), ("bs", ctypes.c_uint8),
+                ("tx", ctypes.c_uint8), ("uvtx", ctypes.c_uint8), ("skip", ctypes.c_uint8),
+                ("intra", ctypes.c_uint8), ("comp", ctypes.c_uint8), ("seg_id", ctypes.c_uint8),
+                ("filter", ctypes.c_uint8), ("mode", ctypes.c_uint8 * 4), ("uvmode", ctypes.c_uint8),
+                ("ref", ctypes.c_uint8 * 2), ("pad0", ctypes.c_uint8),
+                ("mv", ctypes.c_int16 * 16)]
+
+
+class FramePacket(ctypes.Structure):
+    """vp9h_frame: one pass-1 frame packet."""
+    _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32), ("bpp", ctypes.c_uint8),
+                ("ss_h", ctypes.c_uint8), ("ss_v", ctypes.c_uint8), ("keyframe", ctypes.c_uint8),
+                ("intraonly", ctypes.c_uint8), ("lossless", ctypes.c_uint8),
+                ("filter_level", ctypes.c_uint8), ("sharpness", ctypes.c_uint8),
+                ("log2_tile_cols", ctypes.c_uint8), ("log2_tile_rows", ctypes.c_uint8),
+                ("pad0", ctypes.c_uint8 * 2), ("lflvl", ctypes.c_uint8 * 64),
+                ("ref_w", ctypes.c_int32 * 3), ("ref_h", ctypes.c_int32 * 3),
+                ("nblocks", ctypes.c_uint32), ("neobs", ctypes.c_uint32), ("ncoefs", ctypes.c_uint64),
+                ("blocks", ctypes.POINTER(Block)), ("eobs", ctypes.POINTER(ctypes.c_uint16)),
+                ("coefs", ctypes.c_void_p)]
+
+
+class SynthParams(ctypes.Structure):
+    """vp9h_synth_params."""
+    _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32), ("bpp", ctypes.c_int32),
+                ("ss_h", ctypes.c_int32), ("ss_v", ctypes.c_int32), ("log2_tile_cols", ctypes.c_int32),
+                ("inter", ctypes.c_int32), ("compound", ctypes.c_int32), ("q_idx", ctypes.c_int32),
+                ("lossless", ctypes.c_int32), ("filter_level", ctypes.c_int32),
+                ("sharpness", ctypes.c_int32), ("bilinear", ctypes.c_int32),
+                ("coef_stress", ctypes.c_int32), ("p_zero_eob", ctypes.c_float),
+                ("p_skip", ctypes.c_float), ("seed", ctypes.c_uint64)]
+
+
+_lib_handle = None
+
+# Exported symbols of include/vp9hip.h (checked by the CPU test suite).
+ABI_SYMBOLS = ["vp9hip_open", "vp9hip_close", "vp9hip_configure", "vp9hip_submit_frame",
+               "vp9hip_stage_batch", "vp9hip_run_batch", "vp9hip_sync", "vp9hip_download_frame",
+               "vp9hip_upload_frame", "vp9hip_flush", "vp9hip_last_timing",
+               "vp9hip_synth_defaults", "vp9hip_synth_frame", "vp9hip_synth_free"]
+
+
+def lib():
+    """Load libvp9hip.so (fails loudly: there is no CPU fallback)."""
+    global _lib_handle
+    if _lib_handle is not None:
+        return _lib_handle
+    if not os.path.exists(LIB_PATH):
+        raise Vp9HipUnavailable("libvp9hip.so not built: run __graft_entry__.build() (%s)" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    vp = ctypes.c_void_p
+    L.vp9hip_open.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
+    L.vp9hip_close.argtypes = [vp]
+    L.vp9hip_close.restype = None
+    L.vp9hip_configure.argtypes = [vp] + [ctypes.c_int] * 6
+    L.vp9hip_submit_frame.argtypes = [vp, ctypes.POINTER(FramePacket), ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+    L.vp9hip_stage_batch.argtypes = [vp, ctypes.POINTER(FramePacket), ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+    L.vp9hip_run_batch.argtypes = [vp]
+    L.vp9hip_sync.argtypes = [vp]
+    L.vp9hip_download_frame.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
+                                        ctypes.POINTER(ctypes.c_ssize_t)]
+    L.vp9hip_upload_frame.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
+                                      ctypes.POINTER(ctypes.c_ssize_t)]
+    L.vp9hip_flush.argtypes = [vp]
+    L.vp9hip_last_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),
+                                     ctypes.POINTER(ctypes.c_int), ctypes.c_int]
+    L.vp9hip_alg_bytes.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.c_int]
+    L.vp9hip_set_timing.argtypes = [vp, ctypes.c_int]
+    L.vp9hip_synth_defaults.argtypes = [ctypes.POINTER(SynthParams), ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    L.vp9hip_synth_defaults.restype = None
+    L.vp9hip_synth_frame.argtypes = [ctypes.POINTER(FramePacket), ctypes.POINTER(SynthParams)]
+    L.vp9hip_synth_free.argtypes = [ctypes.POINTER(FramePacket)]
+    L.vp9hip_synth_free.restype = None
+    _lib_handle = L
+    return L
+
+
+def _check(fn, r):
+    if r < 0:
+        raise Vp9HipError(fn, r)
+    return r
+
+
+def synth_params(width, height, bpp=8, **kw):
+    """§8(d) default stream settings, overridable by keyword."""
+    p = SynthParams()
+    lib().vp9hip_synth_defaults(ctypes.byref(p), width, height, bpp)
+    for k, v in kw.items():
+        if not hasattr(p, k):
+            raise KeyError(k)
+        setattr(p, k, v)
+    return p
+
+
+class SynthFrame:
+    """A pass-1 frame packet generated by vp9hip_synth_frame (owns its C arrays)."""
+
+    def __init__(self, params):
+        self.params = params
+        self.pkt = FramePacket()
+        _check("vp9hip_synth_frame", lib().vp9hip_synth_frame(ctypes.byref(self.pkt), ctypes.byref(params)))
+
+    def __del__(self):
+        if getattr(self, "pkt", None) is not None and _lib_handle is not None:
+            _lib_handle.vp9hip_synth_free(ctypes.byref(self.pkt))
+            self.pkt = None
+
+    @property
+    def nbytes_coefs(self):
+        return self.pkt.ncoefs * (2 if self.pkt.bpp == 8 else 4)
+
+    def blocks(self):
+        return [self.pkt.blocks[i] for i in range(self.pkt.nblocks)]
+
+
+def alloc_planes(width, height, bpp, ss_h=1, ss_v=1, pad=64):
+    """Host planes padded to 64 luma pixels (the layout the oracle expects)."""
+    dt = np.uint8 if bpp == 8 else np.uint16
+    W = (width + pad - 1) // pad * pad
+    H = (height + pad - 1) // pad * pad
+    return [np.zeros((H, W), dt), np.zeros((H >> ss_v, W >> ss_h), dt), np.zeros((H >> ss_v, W >> ss_h), dt)]
+
+
+def visible(planes, width, height, ss_h=1, ss_v=1):
+    cw, ch = (width + ss_h) >> ss_h, (height + ss_v) >> ss_v
+    return [planes[0][:height, :width], planes[1][:ch, :cw], planes[2][:ch, :cw]]
+
+
+class Device:
+    """A vp9hip context on one GPU (vp9hip_open / vp9hip_configure)."""
+
+    def __init__(self, device=0):
+        self._c = ctypes.c_void_p()
+        _check("vp9hip_open", lib().vp9hip_open(device, ctypes.byref(self._c)))
+        self.w = self.h = 0
+        self.bpp = 8
+
+    def close(self):
+        if self._c:
+            lib().vp9hip_close(self._c)
+            self._c = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def configure(self, width, height, bpp=8, nbufs=4, ss_h=1, ss_v=1):
+        _check("vp9hip_configure", lib().vp9hip_configure(self._c, width, height, bpp, ss_h, ss_v, nbufs))
+        self.w, self.h, self.bpp, self.ss_h, self.ss_v = width, height, bpp, ss_h, ss_v
+
+    def submit(self, frame, out_buf, refs=(0, 0, 0)):
+        r = (ctypes.c_int * 3)(*refs)
+        pkt = frame.pkt if isinstance(frame, SynthFrame) else frame
+        _check("vp9hip_submit_frame", lib().vp9hip_submit_frame(self._c, ctypes.byref(pkt), out_buf, r))
+
+    def stage_batch(self, frames, out_bufs):
+        arr = (FramePacket * len(frames))(*[f.pkt if isinstance(f, SynthFrame) else f for f in frames])
+        ob = (ctypes.c_int * len(out_bufs))(*out_bufs)
+        self._staged = (arr, frames)   # keep host packets alive
+        _check("vp9hip_stage_batch", lib().vp9hip_stage_batch(self._c, arr, len(frames), ob))
+
+    def run_batch(self):
+        _check("vp9hip_run_batch", lib().vp9hip_run_batch(self._c))
+
+    def sync(self):
+        _check("vp9hip_sync", lib().vp9hip_sync(self._c))
+
+    def set_timing(self, on):
+        _check("vp9hip_set_timing", lib().vp9hip_set_timing(self._c, int(bool(on))))
+
+    def timing(self):
+        names = (ctypes.c_char_p * 8)()
+        ms = (ctypes.c_double * 8)()
+        cnt = (ctypes.c_int * 8)()
+        n = _check("vp9hip_last_timing", lib().vp9hip_last_timing(self._c, names, ms, cnt, 8))
+        return {names[i].decode(): (ms[i], cnt[i]) for i in range(n)}
+
+    def alg_bytes(self):
+        b = (ctypes.c_double * 8)()
+        n = _check("vp9hip_alg_bytes", lib().vp9hip_alg_bytes(self._c, b, 8))
+        return [b[i] for i in range(n)]
+
+    def _plane_args(self, planes):
+        ptrs = (ctypes.c_void_p * 3)(*[p.ctypes.data for p in planes])
+        ls = (ctypes.c_ssize_t * 3)(*[p.strides[0] for p in planes])
+        return ptrs, ls
+
+    def download(self, buf):
+        planes = alloc_planes(self.w, self.h, self.bpp, self.ss_h, self.ss_v)
+        ptrs, ls = self._plane_args(planes)
+        _check("vp9hip_download_frame", lib().vp9hip_download_frame(self._c, buf, ptrs, ls))
+        return planes
+
+    def upload(self, buf, planes):
+        planes = [np.ascontiguousarray(p) for p in planes]
+        ptrs, ls = self._plane_args(planes)
+        _check("vp9hip_upload_frame", lib().vp9hip_upload_frame(self._c, buf, ptrs, ls))
+
+    def flush(self):
+        _check("vp9hip_flush", lib().vp9hip_flush(self._c))
+
+
+class Decoder:
+    """send_packet / receive_frame mirror of the reference decode loop for this path.
+
+    Packets are pass-1 frame packets; VP9 reference slots follow the frame
+    header's refresh mask semantics (vp9.c:1839-1859) in the simplified form
+    used here: every decoded frame becomes LAST for the next inter frame.
+    """
+
+    def __init__(self, device=0, nbufs=4):
+        self.dev = Device(device)
+        self.nbufs = nbufs
+        self._configured = None
+        self._queue = []
+        self._last = None
+        self._next = 0
+
+    def send_packet(self, frame):
+        pkt = frame.pkt if isinstance(frame, SynthFrame) else frame
+        cfg = (pkt.width, pkt.height, pkt.bpp)
+        if self._configured != cfg:
+            self.dev.configure(pkt.width, pkt.height, pkt.bpp, self.nbufs, pkt.ss_h, pkt.ss_v)
+            self._configured = cfg
+            self._last = None
+        out = self._next
+        self._next = (self._next + 1) % self.nbufs
+        ref = self._last if self._last is not None else out
+        self.dev.submit(pkt, out, (ref, ref, ref))
+        self._last = out
+        self._queue.append(out)
+
+    def receive_frame(self):
+        """Returns the next decoded frame as visible numpy planes, or None (EAGAIN)."""
+        if not self._queue:
+            return None
+        buf = self._queue.pop(0)
+        w, h, bpp = self._configured
+        return visible(self.dev.download(buf), w, h)

@@ -1,0 +1,941 @@
+// gfx950 (MI355X) kernels of the VP9 hybrid decoder pixel path.
+//
+//   k_recon  — one workgroup (4 waves) per 64x64 superblock: intra prediction +
+//              inverse transform + residual add for every tx block of the SB, in
+//              host-computed dependency levels, entirely in LDS; superblocks are
+//              launched along an SB wavefront (left/top/top-left dependencies only,
+//              tile columns independent: vp9recon.c:45-47).
+//   k_lf     — one workgroup per SB: the in-loop deblocking filter of
+//              ff_vp9_loopfilter_sb (vp9lpf.c:183-230) on a 72x72 LDS tile, one lane
+//              per pixel row (column edges) then one lane per pixel column (row
+//              edges); SBs launched along the t = x + 2y wavefront that reproduces the
+//              reference's raster order.
+//   k_mc     — sub-pel motion compensation (vp9dsp_template.c:1969-2361) with
+//              edge clamping (videodsp_template.c:27-105), one thread per pixel.
+//
+// Arithmetic restates vp9dsp_template.c bit-exactly: 8-bit transforms run in
+// wrapping 32-bit arithmetic with int16 intermediates (dctint int / dctcoef int16,
+// vp9dsp_8bpp.c), high bit depth in int64 with int32 intermediates.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define VP9T_STORAGE static __constant__ const
+#include "vp9_tables.h"
+#include "vp9hip_work.h"
+
+#define DEV __device__ __forceinline__
+
+// ------------------------------------------------------------------ helpers
+DEV int clipbd(int v, int bd) { int m = (1 << bd) - 1; return v < 0 ? 0 : (v > m ? m : v); }
+DEV int iabs(int v) { return v < 0 ? -v : v; }
+
+DEV void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Transform arithmetic policy. 8-bit: uint32 bit patterns (defined wrap-around,
+// identical to the reference's `x * 11585U` products cast back to int) with an
+// arithmetic rounding shift. High bit depth: int64.
+struct M32 {
+    typedef uint32_t T;
+    static DEV T in(int32_t v) { return (uint32_t) v; }
+    static DEV T r14(T v) { return (uint32_t) ((int32_t) (v + 8192u) >> 14); }
+};
+struct M64 {
+    typedef int64_t T;
+    static DEV T in(int32_t v) { return (int64_t) v; }
+    static DEV T r14(T v) { return (v + 8192) >> 14; }
+};
+
+#define R(x) M::r14(x)
+#define C(k) ((T) (k))
+
+// vp9dsp_template.c:1202-1216
+template <class M> DEV void idct4(typename M::T *io)
+{
+    typedef typename M::T T;
+    T t0 = R((io[0] + io[2]) * C(11585)), t1 = R((io[0] - io[2]) * C(11585));
+    T t2 = R(io[1] * C(6270) - io[3] * C(15137)), t3 = R(io[1] * C(15137) + io[3] * C(6270));
+    io[0] = t0 + t3; io[1] = t1 + t2; io[2] = t1 - t2; io[3] = t0 - t3;
+}
+// vp9dsp_template.c:1218-1232
+template <class M> DEV void iadst4(typename M::T *io)
+{
+    typedef typename M::T T;
+    T t0 = C(5283) * io[0] + C(15212) * io[2] + C(9929) * io[3];
+    T t1 = C(9929) * io[0] - C(5283) * io[2] - C(15212) * io[3];
+    T t2 = C(13377) * (io[0] - io[2] + io[3]);
+    T t3 = C(13377) * io[1];
+    io[0] = R(t0 + t3); io[1] = R(t1 + t3); io[2] = R(t2); io[3] = R(t0 + t1 - t3);
+}
+// vp9dsp_template.c:1236-1270
+template <class M> DEV void idct8(typename M::T *io)
+{
+    typedef typename M::T T;
+    T t0a = R((io[0] + io[4]) * C(11585)), t1a = R((io[0] - io[4]) * C(11585));
+    T t2a = R(io[2] * C(6270) - io[6] * C(15137)), t3a = R(io[2] * C(15137) + io[6] * C(6270));
+    T t4a = R(io[1] * C(3196) - io[7] * C(16069)), t5a = R(io[5] * C(13623) - io[3] * C(9102));
+    T t6a = R(io[5] * C(9102) + io[3] * C(13623)), t7a = R(io[1] * C(16069) + io[7] * C(3196));
+    T t0 = t0a + t3a, t1 = t1a + t2a, t2 = t1a - t2a, t3 = t0a - t3a;
+    T t4 = t4a + t5a, t7 = t7a + t6a;
+    t5a = t4a - t5a; t6a = t7a - t6a;
+    T t5 = R((t6a - t5a) * C(11585)), t6 = R((t6a + t5a) * C(11585));
+    io[0] = t0 + t7; io[1] = t1 + t6; io[2] = t2 + t5; io[3] = t3 + t4;
+    io[4] = t3 - t4; io[5] = t2 - t5; io[6] = t1 - t6; io[7] = t0 - t7;
+}
+// vp9dsp_template.c:1272-1314
+template <class M> DEV void iadst8(typename M::T *io)
+{
+    typedef typename M::T T;
+    T t0a = C(16305) * io[7] + C(1606) * io[0], t1a = C(1606) * io[7] - C(16305) * io[0];
+    T t2a = C(14449) * io[5] + C(7723) * io[2], t3a = C(7723) * io[5] - C(14449) * io[2];
+    T t4a = C(10394) * io[3] + C(12665) * io[4], t5a = C(12665) * io[3] - C(10394) * io[4];
+    T t6a = C(4756) * io[1] + C(15679) * io[6], t7a = C(15679) * io[1] - C(4756) * io[6];
+    T t0 = R(t0a + t4a), t1 = R(t1a + t5a), t2 = R(t2a + t6a), t3 = R(t3a + t7a);
+    T t4 = R(t0a - t4a), t5 = R(t1a - t5a), t6 = R(t2a - t6a), t7 = R(t3a - t7a);
+    t4a = C(15137) * t4 + C(6270) * t5;
+    t5a = C(6270) * t4 - C(15137) * t5;
+    t6a = C(15137) * t7 - C(6270) * t6;
+    t7a = C(6270) * t7 + C(15137) * t6;
+    io[0] = t0 + t2;
+    io[7] = C(0) - (t1 + t3);
+    t2 = t0 - t2;
+    t3 = t1 - t3;
+    io[1] = C(0) - R(t4a + t6a);
+    io[6] = R(t5a + t7a);
+    t6 = R(t4a - t6a);
+    t7 = R(t5a - t7a);
+    io[3] = C(0) - R((t2 + t3) * C(11585));
+    io[4] = R((t2 - t3) * C(11585));
+    io[2] = R((t6 + t7) * C(11585));
+    io[5] = C(0) - R((t6 - t7) * C(11585));
+}
+// vp9dsp_template.c:1318-1404
+template <class M> DEV void idct16(typename M::T *io)
+{
+    typedef typename M::T T;
+    T t0, t1, t2, t3, t4, t5, t6, t7, t8, t9, t10, t11, t12, t13, t14, t15;
+    T t0a, t1a, t2a, t3a, t4a, t5a, t6a, t7a, t8a, t9a, t10a, t11a, t12a, t13a, t14a, t15a;
+    t0a = R((io[0] + io[8]) * C(11585));
+    t1a = R((io[0] - io[8]) * C(11585));
+    t2a = R(io[4] * C(6270) - io[12] * C(15137));
+    t3a = R(io[4] * C(15137) + io[12] * C(6270));
+    t4a = R(io[2] * C(3196) - io[14] * C(16069));
+    t7a = R(io[2] * C(16069) + io[14] * C(3196));
+    t5a = R(io[10] * C(13623) - io[6] * C(9102));
+    t6a = R(io[10] * C(9102) + io[6] * C(13623));
+    t8a = R(io[1] * C(1606) - io[15] * C(16305));
+    t15a = R(io[1] * C(16305) + io[15] * C(1606));
+    t9a = R(io[9] * C(12665) - io[7] * C(10394));
+    t14a = R(io[9] * C(10394) + io[7] * C(12665));
+    t10a = R(io[5] * C(7723) - io[11] * C(14449));
+    t13a = R(io[5] * C(14449) + io[11] * C(7723));
+    t11a = R(io[13] * C(15679) - io[3] * C(4756));
+    t12a = R(io[13] * C(4756) + io[3] * C(15679));
+    t0 = t0a + t3a; t1 = t1a + t2a; t2 = t1a - t2a; t3 = t0a - t3a;
+    t4 = t4a + t5a; t5 = t4a - t5a; t6 = t7a - t6a; t7 = t7a + t6a;
+    t8 = t8a + t9a; t9 = t8a - t9a; t10 = t11a - t10a; t11 = t11a + t10a;
+    t12 = t12a + t13a; t13 = t12a - t13a; t14 = t15a - t14a; t15 = t15a + t14a;
+    t5a = R((t6 - t5) * C(11585));
+    t6a = R((t6 + t5) * C(11585));
+    t9a = R(t14 * C(6270) - t9 * C(15137));
+    t14a = R(t14 * C(15137) + t9 * C(6270));
+    t10a = R(C(0) - (t13 * C(15137) + t10 * C(6270)));
+    t13a = R(t13 * C(6270) - t10 * C(15137));
+    t0a = t0 + t7; t1a = t1 + t6a; t2a = t2 + t5a; t3a = t3 + t4;
+    t4 = t3 - t4; t5 = t2 - t5a; t6 = t1 - t6a; t7 = t0 - t7;
+    t8a = t8 + t11; t9 = t9a + t10a; t10 = t9a - t10a; t11a = t8 - t11;
+    t12a = t15 - t12; t13 = t14a - t13a; t14 = t14a + t13a; t15a = t15 + t12;
+    t10a = R((t13 - t10) * C(11585));
+    t13a = R((t13 + t10) * C(11585));
+    t11 = R((t12a - t11a) * C(11585));
+    t12 = R((t12a + t11a) * C(11585));
+    io[0] = t0a + t15a; io[1] = t1a + t14; io[2] = t2a + t13a; io[3] = t3a + t12;
+    io[4] = t4 + t11; io[5] = t5 + t10a; io[6] = t6 + t9; io[7] = t7 + t8a;
+    io[8] = t7 - t8a; io[9] = t6 - t9; io[10] = t5 - t10a; io[11] = t4 - t11;
+    io[12] = t3a - t12; io[13] = t2a - t13a; io[14] = t1a - t14; io[15] = t0a - t15a;
+}
+// vp9dsp_template.c:1406-1507
+template <class M> DEV void iadst16(typename M::T *io)
+{
+    typedef typename M::T T;
+    T t0, t1, t2, t3, t4, t5, t6, t7, t8, t9, t10, t11, t12, t13, t14, t15;
+    T t0a, t1a, t2a, t3a, t4a, t5a, t6a, t7a, t8a, t9a, t10a, t11a, t12a, t13a, t14a, t15a;
+    t0 = io[15] * C(16364) + io[0] * C(804);
+    t1 = io[15] * C(804) - io[0] * C(16364);
+    t2 = io[13] * C(15893) + io[2] * C(3981);
+    t3 = io[13] * C(3981) - io[2] * C(15893);
+    t4 = io[11] * C(14811) + io[4] * C(7005);
+    t5 = io[11] * C(7005) - io[4] * C(14811);
+    t6 = io[9] * C(13160) + io[6] * C(9760);
+    t7 = io[9] * C(9760) - io[6] * C(13160);
+    t8 = io[7] * C(11003) + io[8] * C(12140);
+    t9 = io[7] * C(12140) - io[8] * C(11003);
+    t10 = io[5] * C(8423) + io[10] * C(14053);
+    t11 = io[5] * C(14053) - io[10] * C(8423);
+    t12 = io[3] * C(5520) + io[12] * C(15426);
+    t13 = io[3] * C(15426) - io[12] * C(5520);
+    t14 = io[1] * C(2404) + io[14] * C(16207);
+    t15 = io[1] * C(16207) - io[14] * C(2404);
+    t0a = R(t0 + t8); t1a = R(t1 + t9); t2a = R(t2 + t10); t3a = R(t3 + t11);
+    t4a = R(t4 + t12); t5a = R(t5 + t13); t6a = R(t6 + t14); t7a = R(t7 + t15);
+    t8a = R(t0 - t8); t9a = R(t1 - t9); t10a = R(t2 - t10); t11a = R(t3 - t11);
+    t12a = R(t4 - t12); t13a = R(t5 - t13); t14a = R(t6 - t14); t15a = R(t7 - t15);
+    t8 = t8a * C(16069) + t9a * C(3196);
+    t9 = t8a * C(3196) - t9a * C(16069);
+    t10 = t10a * C(9102) + t11a * C(13623);
+    t11 = t10a * C(13623) - t11a * C(9102);
+    t12 = t13a * C(16069) - t12a * C(3196);
+    t13 = t13a * C(3196) + t12a * C(16069);
+    t14 = t15a * C(9102) - t14a * C(13623);
+    t15 = t15a * C(13623) + t14a * C(9102);
+    t0 = t0a + t4a; t1 = t1a + t5a; t2 = t2a + t6a; t3 = t3a + t7a;
+    t4 = t0a - t4a; t5 = t1a - t5a; t6 = t2a - t6a; t7 = t3a - t7a;
+    t8a = R(t8 + t12); t9a = R(t9 + t13); t10a = R(t10 + t14); t11a = R(t11 + t15);
+    t12a = R(t8 - t12); t13a = R(t9 - t13); t14a = R(t10 - t14); t15a = R(t11 - t15);
+    t4a = t4 * C(15137) + t5 * C(6270);
+    t5a = t4 * C(6270) - t5 * C(15137);
+    t6a = t7 * C(15137) - t6 * C(6270);
+    t7a = t7 * C(6270) + t6 * C(15137);
+    t12 = t12a * C(15137) + t13a * C(6270);
+    t13 = t12a * C(6270) - t13a * C(15137);
+    t14 = t15a * C(15137) - t14a * C(6270);
+    t15 = t15a * C(6270) + t14a * C(15137);
+    io[0] = t0 + t2;
+    io[15] = C(0) - (t1 + t3);
+    t2a = t0 - t2;
+    t3a = t1 - t3;
+    io[3] = C(0) - R(t4a + t6a);
+    io[12] = R(t5a + t7a);
+    t6 = R(t4a - t6a);
+    t7 = R(t5a - t7a);
+    io[1] = C(0) - (t8a + t10a);
+    io[14] = t9a + t11a;
+    t10 = t8a - t10a;
+    t11 = t9a - t11a;
+    io[2] = R(t12 + t14);
+    io[13] = C(0) - R(t13 + t15);
+    t14a = R(t12 - t14);
+    t15a = R(t13 - t15);
+    io[7] = R((C(0) - (t2a + t3a)) * C(11585));
+    io[8] = R((t2a - t3a) * C(11585));
+    io[4] = R((t7 + t6) * C(11585));
+    io[11] = R((t7 - t6) * C(11585));
+    io[6] = R((t11 + t10) * C(11585));
+    io[9] = R((t11 - t10) * C(11585));
+    io[5] = R((C(0) - (t14a + t15a)) * C(11585));
+    io[10] = R((t14a - t15a) * C(11585));
+}
+// vp9dsp_template.c:1511-1715
+template <class M> DEV void idct32(typename M::T *io)
+{
+    typedef typename M::T T;
+    T t0a = R((io[0] + io[16]) * C(11585));
+    T t1a = R((io[0] - io[16]) * C(11585));
+    T t2a = R(io[8] * C(6270) - io[24] * C(15137));
+    T t3a = R(io[8] * C(15137) + io[24] * C(6270));
+    T t4a = R(io[4] * C(3196) - io[28] * C(16069));
+    T t7a = R(io[4] * C(16069) + io[28] * C(3196));
+    T t5a = R(io[20] * C(13623) - io[12] * C(9102));
+    T t6a = R(io[20] * C(9102) + io[12] * C(13623));
+    T t8a = R(io[2] * C(1606) - io[30] * C(16305));
+    T t15a = R(io[2] * C(16305) + io[30] * C(1606));
+    T t9a = R(io[18] * C(12665) - io[14] * C(10394));
+    T t14a = R(io[18] * C(10394) + io[14] * C(12665));
+    T t10a = R(io[10] * C(7723) - io[22] * C(14449));
+    T t13a = R(io[10] * C(14449) + io[22] * C(7723));
+    T t11a = R(io[26] * C(15679) - io[6] * C(4756));
+    T t12a = R(io[26] * C(4756) + io[6] * C(15679));
+    T t16a = R(io[1] * C(804) - io[31] * C(16364));
+    T t31a = R(io[1] * C(16364) + io[31] * C(804));
+    T t17a = R(io[17] * C(12140) - io[15] * C(11003));
+    T t30a = R(io[17] * C(11003) + io[15] * C(12140));
+    T t18a = R(io[9] * C(7005) - io[23] * C(14811));
+    T t29a = R(io[9] * C(14811) + io[23] * C(7005));
+    T t19a = R(io[25] * C(15426) - io[7] * C(5520));
+    T t28a = R(io[25] * C(5520) + io[7] * C(15426));
+    T t20a = R(io[5] * C(3981) - io[27] * C(15893));
+    T t27a = R(io[5] * C(15893) + io[27] * C(3981));
+    T t21a = R(io[21] * C(14053) - io[11] * C(8423));
+    T t26a = R(io[21] * C(8423) + io[11] * C(14053));
+    T t22a = R(io[13] * C(9760) - io[19] * C(13160));
+    T t25a = R(io[13] * C(13160) + io[19] * C(9760));
+    T t23a = R(io[29] * C(16207) - io[3] * C(2404));
+    T t24a = R(io[29] * C(2404) + io[3] * C(16207));
+
+    T t0 = t0a + t3a, t1 = t1a + t2a, t2 = t1a - t2a, t3 = t0a - t3a;
+    T t4 = t4a + t5a, t5 = t4a - t5a, t6 = t7a - t6a, t7 = t7a + t6a;
+    T t8 = t8a + t9a, t9 = t8a - t9a, t10 = t11a - t10a, t11 = t11a + t10a;
+    T t12 = t12a + t13a, t13 = t12a - t13a, t14 = t15a - t14a, t15 = t15a + t14a;
+    T t16 = t16a + t17a, t17 = t16a - t17a, t18 = t19a - t18a, t19 = t19a + t18a;
+    T t20 = t20a + t21a, t21 = t20a - t21a, t22 = t23a - t22a, t23 = t23a + t22a;
+    T t24 = t24a + t25a, t25 = t24a - t25a, t26 = t27a - t26a, t27 = t27a + t26a;
+    T t28 = t28a + t29a, t29 = t28a - t29a, t30 = t31a - t30a, t31 = t31a + t30a;
+
+    t5a = R((t6 - t5) * C(11585));
+    t6a = R((t6 + t5) * C(11585));
+    t9a = R(t14 * C(6270) - t9 * C(15137));
+    t14a = R(t14 * C(15137) + t9 * C(6270));
+    t10a = R(C(0) - (t13 * C(15137) + t10 * C(6270)));
+    t13a = R(t13 * C(6270) - t10 * C(15137));
+    t17a = R(t30 * C(3196) - t17 * C(16069));
+    t30a = R(t30 * C(16069) + t17 * C(3196));
+    t18a = R(C(0) - (t29 * C(16069) + t18 * C(3196)));
+    t29a = R(t29 * C(3196) - t18 * C(16069));
+    t21a = R(t26 * C(13623) - t21 * C(9102));
+    t26a = R(t26 * C(9102) + t21 * C(13623));
+    t22a = R(C(0) - (t25 * C(9102) + t22 * C(13623)));
+    t25a = R(t25 * C(13623) - t22 * C(9102));
+
+    t0a = t0 + t7; t1a = t1 + t6a; t2a = t2 + t5a; t3a = t3 + t4;
+    t4a = t3 - t4; t5 = t2 - t5a; t6 = t1 - t6a; t7a = t0 - t7;
+    t8a = t8 + t11; t9 = t9a + t10a; t10 = t9a - t10a; t11a = t8 - t11;
+    t12a = t15 - t12; t13 = t14a - t13a; t14 = t14a + t13a; t15a = t15 + t12;
+    t16a = t16 + t19; t17 = t17a + t18a; t18 = t17a - t18a; t19a = t16 - t19;
+    t20a = t23 - t20; t21 = t22a - t21a; t22 = t22a + t21a; t23a = t23 + t20;
+    t24a = t24 + t27; t25 = t25a + t26a; t26 = t25a - t26a; t27a = t24 - t27;
+    t28a = t31 - t28; t29 = t30a - t29a; t30 = t30a + t29a; t31a = t31 + t28;
+
+    t10a = R((t13 - t10) * C(11585));
+    t13a = R((t13 + t10) * C(11585));
+    t11 = R((t12a - t11a) * C(11585));
+    t12 = R((t12a + t11a) * C(11585));
+    t18a = R(t29 * C(6270) - t18 * C(15137));
+    t29a = R(t29 * C(15137) + t18 * C(6270));
+    t19 = R(t28a * C(6270) - t19a * C(15137));
+    t28 = R(t28a * C(15137) + t19a * C(6270));
+    t20 = R(C(0) - (t27a * C(15137) + t20a * C(6270)));
+    t27 = R(t27a * C(6270) - t20a * C(15137));
+    t21a = R(C(0) - (t26 * C(15137) + t21 * C(6270)));
+    t26a = R(t26 * C(6270) - t21 * C(15137));
+
+    t0 = t0a + t15a; t1 = t1a + t14; t2 = t2a + t13a; t3 = t3a + t12;
+    t4 = t4a + t11; t5a = t5 + t10a; t6a = t6 + t9; t7 = t7a + t8a;
+    t8 = t7a - t8a; t9a = t6 - t9; t10 = t5 - t10a; t11a = t4a - t11;
+    t12a = t3a - t12; t13 = t2a - t13a; t14a = t1a - t14; t15 = t0a - t15a;
+    t16 = t16a + t23a; t17a = t17 + t22; t18 = t18a + t21a; t19a = t19 + t20;
+    t20a = t19 - t20; t21 = t18a - t21a; t22a = t17 - t22; t23 = t16a - t23a;
+    t24 = t31a - t24a; t25a = t30 - t25; t26 = t29a - t26a; t27a = t28 - t27;
+    t28a = t28 + t27; t29 = t29a + t26a; t30a = t30 + t25; t31 = t31a + t24a;
+
+    t20 = R((t27a - t20a) * C(11585));
+    t27 = R((t27a + t20a) * C(11585));
+    t21a = R((t26 - t21) * C(11585));
+    t26a = R((t26 + t21) * C(11585));
+    t22 = R((t25a - t22a) * C(11585));
+    t25 = R((t25a + t22a) * C(11585));
+    t23a = R((t24 - t23) * C(11585));
+    t24a = R((t24 + t23) * C(11585));
+
+    io[0] = t0 + t31; io[1] = t1 + t30a; io[2] = t2 + t29; io[3] = t3 + t28a;
+    io[4] = t4 + t27; io[5] = t5a + t26a; io[6] = t6a + t25; io[7] = t7 + t24a;
+    io[8] = t8 + t23a; io[9] = t9a + t22; io[10] = t10 + t21a; io[11] = t11a + t20;
+    io[12] = t12a + t19a; io[13] = t13 + t18; io[14] = t14a + t17a; io[15] = t15 + t16;
+    io[16] = t15 - t16; io[17] = t14a - t17a; io[18] = t13 - t18; io[19] = t12a - t19a;
+    io[20] = t11a - t20; io[21] = t10 - t21a; io[22] = t9a - t22; io[23] = t8 - t23a;
+    io[24] = t7 - t24a; io[25] = t6a - t25; io[26] = t5a - t26a; io[27] = t4 - t27;
+    io[28] = t3 - t28a; io[29] = t2 - t29; io[30] = t1 - t30a; io[31] = t0 - t31;
+}
+#undef R
+#undef C
+
+// iwht4_1d (vp9dsp_template.c:1719-1748), int temporaries
+DEV void iwht4(int32_t *io, int pass)
+{
+    uint32_t t0, t1, t2, t3, t4;
+    if (pass == 0) { t0 = io[0] >> 2; t1 = io[3] >> 2; t2 = io[1] >> 2; t3 = io[2] >> 2; }
+    else { t0 = io[0]; t1 = io[3]; t2 = io[1]; t3 = io[2]; }
+    t0 += t2; t3 -= t1; t4 = (uint32_t) ((int32_t) (t0 - t3) >> 1); t1 = t4 - t1; t2 = t4 - t2; t0 -= t1; t3 += t2;
+    io[0] = (int32_t) t0; io[1] = (int32_t) t1; io[2] = (int32_t) t2; io[3] = (int32_t) t3;
+}
+
+// One 1-D inverse transform of length 4<<tx on `v` (kind: 0 dct, 1 adst).
+template <class M> DEV void tx1d(typename M::T *v, int tx, int adst)
+{
+    switch (tx) {
+    case 0: if (adst) iadst4<M>(v); else idct4<M>(v); break;
+    case 1: if (adst) iadst8<M>(v); else idct8<M>(v); break;
+    case 2: if (adst) iadst16<M>(v); else idct16<M>(v); break;
+    default: idct32<M>(v); break;
+    }
+}
+
+// ------------------------------------------------------------ intra predict
+// Edge array layout per wave (`e`): e[0..n) = left column bottom-to-top (top-to-
+// bottom for HOR_UP), e[n] = top-left, e[n+1 ..] = top row incl. top-right.
+// Per-pixel closed forms of the predictors of vp9dsp_template.c:28-1106.
+#define A2(a, b) (((a) + (b) + 1) >> 1)
+#define A3(a, b, c) (((a) + 2 * (b) + (c) + 2) >> 2)
+
+DEV int pred_px(int mode, int n, int x, int y, const uint16_t *e, int dc, int bd)
+{
+    const uint16_t *L = e, *T = e + n + 1;
+    switch (mode) {
+    case 0: return T[x];                                           // VERT
+    case 1: return L[n - 1 - y];                                   // HOR
+    case 9: return clipbd(T[x] + L[n - 1 - y] - T[-1], bd);        // TM_VP8
+    case 3: {                                                      // DIAG_DOWN_LEFT
+        int k = x + y;
+        if (n == 4) return k < 6 ? A3(T[k], T[k + 1], T[k + 2]) : T[7];
+        if (k < n - 2) return A3(T[k], T[k + 1], T[k + 2]);
+        if (k == n - 2) return (T[n - 2] + T[n - 1] * 3 + 2) >> 2;
+        return T[n - 1];
+    }
+    case 4: { int j = n - 1 - y + x; return A3(e[j], e[j + 1], e[j + 2]); }   // DIAG_DOWN_RIGHT
+    case 5: {                                                      // VERT_RIGHT
+        int h = n >> 1, m = h - 1 - (y >> 1) + x;
+        if (!(y & 1)) {
+            if (m <= h - 2) return A3(e[2 * m + 2], e[2 * m + 3], e[2 * m + 4]);
+            return A2(e[n + m - h + 1], e[n + m - h + 2]);
+        }
+        if (m <= h - 2) return A3(e[2 * m + 1], e[2 * m + 2], e[2 * m + 3]);
+        return A3(e[n + m - h], e[n + m - h + 1], e[n + m - h + 2]);
+    }
+    case 6: {                                                      // HOR_DOWN
+        int m = 2 * n - 2 - 2 * y + x;
+        if (m >= 2 * n) { int i = m - 2 * n; return A3(e[n + i], e[n + i + 1], e[n + i + 2]); }
+        int i = m >> 1;
+        return (m & 1) ? A3(e[i], e[i + 1], e[i + 2]) : A2(e[i], e[i + 1]);
+    }
+    case 7: {                                                      // VERT_LEFT
+        int k = (y >> 1) + x;
+        if (n == 4) return (y & 1) ? A3(T[k], T[k + 1], T[k + 2]) : A2(T[k], T[k + 1]);
+        if (x >= n - (y >> 1) - 1) return T[n - 1];
+        if (!(y & 1)) return A2(T[k], T[k + 1]);
+        return k < n - 2 ? A3(T[k], T[k + 1], T[k + 2]) : (T[n - 2] + T[n - 1] * 3 + 2) >> 2;
+    }
+    case 8: {                                                      // HOR_UP (L top-to-bottom)
+        if (y >= (n >> 1) && x >= 2 * n - 2 - 2 * y) return L[n - 1];
+        int m = 2 * y + x, i = m >> 1;
+        if (!(m & 1)) return A2(L[i], L[i + 1]);
+        return i < n - 2 ? A3(L[i], L[i + 1], L[i + 2]) : (L[n - 2] + L[n - 1] * 3 + 2) >> 2;
+    }
+    default: return dc;                                            // DC variants
+    }
+}
+
+// ------------------------------------------------------------- k_recon
+// LDS tile per plane: row 0 / column 0 hold the top row / left column outside
+// the SB; pixel (x, y) of the SB lives at [(y + 1) * PITCH + x + 1].
+#define LP 66            // luma tile pitch (65 used)
+#define CP 34            // chroma tile pitch (33 used, 4:2:0)
+#define LT_SIZE (65 * LP)
+#define CT_SIZE (33 * CP)
+
+template <typename PIX, class M, typename COEF>
+__global__ __launch_bounds__(256) void k_recon(const uint32_t *__restrict__ list, const SBRec *__restrict__ sbs,
+                                               const TxJob *__restrict__ jobs, const uint16_t *__restrict__ lvls,
+                                               const FrameDesc *__restrict__ frames,
+                                               const COEF *__restrict__ coefs)
+{
+    typedef typename M::T T;
+    __shared__ uint16_t tile[LT_SIZE + 2 * CT_SIZE];
+    __shared__ int32_t cbuf[4][32 * 32];
+    __shared__ int32_t tbuf[4][32 * 33];
+    __shared__ uint16_t ebuf[4][80];
+
+    const SBRec sb = sbs[list[blockIdx.x]];
+    const FrameDesc &fd = frames[sb.frame];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int bd = fd.bd;
+#define TPL(p) (tile + ((p) == 0 ? 0 : (p) == 1 ? LT_SIZE : LT_SIZE + CT_SIZE))
+#define TPCH(p) ((p) ? CP : LP)
+
+    // ---- load the SB neighbourhood (pre-loop-filter reconstruction) ----
+    for (int p = 0; p < 3; p++) {
+        const int sz = p ? 32 : 64, ps = p ? 1 : 0;
+        const PIX *g = (const PIX *) fd.plane[p];
+        const int pitch = fd.pitch[p ? 1 : 0];
+        const int x0 = sb.sbx * sz, y0 = sb.sby * sz;
+        uint16_t *t = TPL(p);
+        const int tpch = TPCH(p);
+        (void) ps;
+        // top row (y0 - 1), x0 - 1 .. x0 + sz - 1
+        if (y0 > 0)
+            for (int i = tid; i < sz + 1; i += 256) {
+                int gx = x0 - 1 + i;
+                t[i] = gx >= 0 ? g[(size_t) (y0 - 1) * pitch + gx] : 0;
+            }
+        if (x0 > 0)
+            for (int i = tid; i < sz; i += 256) t[(i + 1) * tpch] = g[(size_t) (y0 + i) * pitch + x0 - 1];
+        if (sb.flags & 1)
+            for (int i = tid; i < sz * sz; i += 256) {
+                int yy = i / sz, xx = i - yy * sz;
+                t[(yy + 1) * tpch + xx + 1] = g[(size_t) (y0 + yy) * pitch + x0 + xx];
+            }
+    }
+    __syncthreads();
+
+    const uint16_t *lv = lvls + sb.lvl0;
+    for (int l = 0; l < sb.nlev; l++) {
+        const int j0 = sb.job0 + lv[l], j1 = sb.job0 + lv[l + 1];
+        for (int j = j0 + wave; j < j1; j += 4) {
+            const TxJob jb = jobs[j];
+            const int p = jb.ptx & 3, tx = jb.ptx >> 2, ts = tx & 3, n = 4 << ts;
+            uint16_t *t = TPL(p);
+            const int tpch = TPCH(p);
+            const int px = jb.x4 * 4, py = jb.y4 * 4;                 // in-SB position
+            uint16_t *o = t + (py + 1) * tpch + px + 1;              // top-left pixel of the tx block
+            int32_t *cb = cbuf[wave];
+            int32_t *tb = tbuf[wave];
+            uint16_t *e = ebuf[wave];
+
+            if (jb.mode != 0xff) {
+                // ---- edges: check_intra_mode (vp9recon.c:37-221) ----
+                const int sz = p ? 32 : 64;
+                const int gx = sb.sbx * sz + px, gy = sb.sby * sz + py;   // plane position
+                const int tile_x0 = p ? sb.tile_x0 * 4 : sb.tile_x0 * 8;
+                const int have_top = gy > 0, have_left = gx > tile_x0, have_right = jb.flags & 1;
+                const int w8 = fd.w8[p ? 1 : 0], h8 = fd.h8[p ? 1 : 0];
+                const int have_t = w8 - gx, have_l = h8 - gy;
+                int mode = jb.mode;
+                // mode_conv[mode][have_left][have_top]
+                switch (mode) {
+                case 0: if (!have_top) mode = 13; break;
+                case 1: if (!have_left) mode = 14; break;
+                case 2: mode = have_left ? (have_top ? 2 : 10) : (have_top ? 11 : 12); break;
+                case 3: case 7: if (!have_top) mode = 13; break;
+                case 8: if (!have_left) mode = 14; break;
+                case 9: mode = have_left ? (have_top ? 9 : 1) : (have_top ? 0 : 14); break;
+                default: break;
+                }
+                const bool need_top = mode == 0 || mode == 2 || mode == 3 || mode == 4 || mode == 5 ||
+                                      mode == 6 || mode == 7 || mode == 9 || mode == 11;
+                const bool need_left = mode == 1 || mode == 2 || mode == 4 || mode == 5 || mode == 6 ||
+                                       mode == 8 || mode == 9 || mode == 10;
+                const bool need_tl = mode == 4 || mode == 5 || mode == 6 || mode == 9;
+                const bool need_tr = mode == 3 || mode == 7;
+                const int base = 128 << (bd - 8);
+                uint16_t *T_ = e + n + 1;
+                if (need_top) {
+                    if (lane < n) {
+                        int v;
+                        if (!have_top) v = base - 1;
+                        else v = o[-tpch + (lane < have_t ? lane : have_t - 1)];
+                        T_[lane] = v;
+                    }
+                    if (ts == 0 && need_tr && lane >= 4 && lane < 8) {
+                        int v;
+                        if (have_top && have_right && 8 <= have_t) v = o[-tpch + lane];
+                        else if (!have_top) v = base - 1;                      // replicate a[3]
+                        else v = o[-tpch + (3 < have_t ? 3 : have_t - 1)];
+                        T_[lane] = v;
+                    }
+                    if (need_tl && lane == 0)
+                        T_[-1] = (have_left && have_top) ? o[-tpch - 1] : base + (have_top ? 1 : -1);
+                }
+                if (need_left && lane < n) {
+                    int v;
+                    if (!have_left) v = base + 1;
+                    else if (mode == 8) v = o[(lane < have_l ? lane : have_l - 1) * tpch - 1];
+                    else {
+                        // l[n-1-i] = pixel row i; rows >= have replicate the bottom-most available
+                        int i = n - 1 - lane;
+                        v = o[(i < have_l ? i : have_l - 1) * tpch - 1];
+                    }
+                    e[lane] = v;
+                }
+                wave_sync();
+                int dc = 0;
+                if (mode == 2) {
+                    int s = 0; for (int i = 0; i < n; i++) s += e[i] + T_[i];
+                    dc = (s + n) >> (ts + 3);
+                } else if (mode == 10) {
+                    int s = 0; for (int i = 0; i < n; i++) s += e[i];
+                    dc = (s + (n >> 1)) >> (ts + 2);
+                } else if (mode == 11) {
+                    int s = 0; for (int i = 0; i < n; i++) s += T_[i];
+                    dc = (s + (n >> 1)) >> (ts + 2);
+                } else if (mode >= 12) {
+                    dc = base + (mode == 13 ? -1 : mode == 14 ? 1 : 0);
+                }
+                for (int i = lane; i < n * n; i += 64) {
+                    int yy = i >> (ts + 2), xx = i & (n - 1);
+                    o[yy * tpch + xx] = pred_px(mode, n, xx, yy, e, dc, bd);
+                }
+                wave_sync();
+            }
+
+            if (jb.eob) {
+                const int eob = jb.eob;
+                if (tx == 4) {
+                    // lossless WHT 4x4 (vp9dsp_template.c:1750)
+                    for (int i = lane; i < 16; i += 64) cb[i] = 0;
+                    wave_sync();
+                    if (lane < eob) cb[vp9t_scan_default_4x4[lane]] = (int32_t) coefs[jb.coef + lane];
+                    wave_sync();
+                    if (lane < 4) {
+                        int32_t v[4];
+                        for (int k = 0; k < 4; k++) v[k] = cb[k * 4 + lane];
+                        iwht4(v, 0);
+                        for (int k = 0; k < 4; k++) tb[lane * 5 + k] = (COEF) v[k];
+                    }
+                    wave_sync();
+                    if (lane < 4) {
+                        int32_t v[4];
+                        for (int k = 0; k < 4; k++) v[k] = tb[k * 5 + lane];
+                        iwht4(v, 1);
+                        for (int k = 0; k < 4; k++) {
+                            uint16_t *q = o + k * tpch + lane;
+                            *q = clipbd(*q + (COEF) v[k], bd);
+                        }
+                    }
+                    wave_sync();
+                } else {
+                    const int txtp = ts == 3 ? 0 : jb.txtp;
+                    const int bits = ts == 3 ? 6 : ts + 4;
+                    if (txtp == 0 && eob == 1) {
+                        // DC-only shortcut (vp9dsp_template.c:1165-1178)
+                        T c0 = M::in((int32_t) coefs[jb.coef]);
+                        T t1 = M::r14(c0 * (T) 11585);
+                        int32_t tdc = (int32_t) M::r14(t1 * (T) 11585);
+                        int add = (int32_t) ((uint32_t) tdc + (1u << (bits - 1))) >> bits;
+                        for (int i = lane; i < n * n; i += 64) {
+                            uint16_t *q = o + (i >> (ts + 2)) * tpch + (i & (n - 1));
+                            *q = clipbd(*q + add, bd);
+                        }
+                        wave_sync();
+                    } else {
+                        const int16_t *scan = ts == 0 ? (txtp == 1 ? vp9t_scan_col_4x4 : txtp == 2 ? vp9t_scan_row_4x4 : vp9t_scan_default_4x4)
+                                            : ts == 1 ? (txtp == 1 ? vp9t_scan_col_8x8 : txtp == 2 ? vp9t_scan_row_8x8 : vp9t_scan_default_8x8)
+                                            : ts == 2 ? (txtp == 1 ? vp9t_scan_col_16x16 : txtp == 2 ? vp9t_scan_row_16x16 : vp9t_scan_default_16x16)
+                                            : vp9t_scan_default_32x32;
+                        for (int i = lane; i < n * n; i += 64) cb[i] = 0;
+                        wave_sync();
+                        for (int i = lane; i < eob; i += 64) cb[scan[i]] = (int32_t) coefs[jb.coef + i];
+                        wave_sync();
+                        // pass 1: column c -> tmp row c (type_a: ADST for txtp 1, 3)
+                        if (lane < n) {
+                            T v[32];
+                            for (int k = 0; k < n; k++) v[k] = M::in(cb[k * n + lane]);
+                            tx1d<M>(v, ts, txtp & 1);
+                            for (int k = 0; k < n; k++) tb[lane * (n + 1) + k] = (COEF) (int64_t) v[k];
+                        }
+                        wave_sync();
+                        // pass 2: output column c (type_b: ADST for txtp 2, 3)
+                        if (lane < n) {
+                            T v[32];
+                            for (int k = 0; k < n; k++) v[k] = M::in(tb[k * (n + 1) + lane]);
+                            tx1d<M>(v, ts, txtp >> 1);
+                            for (int k = 0; k < n; k++) {
+                                int32_t ov = (COEF) (int64_t) v[k];
+                                int add = (int32_t) ((uint32_t) ov + (1u << (bits - 1))) >> bits;
+                                uint16_t *q = o + k * tpch + lane;
+                                *q = clipbd(*q + add, bd);
+                            }
+                        }
+                        wave_sync();
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+
+    // ---- store the SB interior ----
+    for (int p = 0; p < 3; p++) {
+        const int sz = p ? 32 : 64;
+        PIX *g = (PIX *) fd.plane[p];
+        const int pitch = fd.pitch[p ? 1 : 0];
+        const int x0 = sb.sbx * sz, y0 = sb.sby * sz;
+        const uint16_t *t = TPL(p);
+        const int tpch = TPCH(p);
+        for (int i = tid; i < sz * sz; i += 256) {
+            int yy = i / sz, xx = i - yy * sz;
+            g[(size_t) (y0 + yy) * pitch + x0 + xx] = (PIX) t[(yy + 1) * tpch + xx + 1];
+        }
+    }
+}
+
+// --------------------------------------------------------------- k_lf
+// loop_filter (vp9dsp_template.c:1780-1889) on one line of 16 pixels around an
+// edge; `p` points at q0, `s` is the step across the edge.
+DEV void lf_line(uint16_t *p, int s, int wd, int L, int sharp, int bd)
+{
+    int limit = L;
+    if (sharp > 0) { limit >>= (sharp + 3) >> 2; limit = limit < 9 - sharp ? limit : 9 - sharp; }
+    limit = limit > 1 ? limit : 1;                                 // vp9.c:674-685
+    int E = (2 * (L + 2) + limit) << (bd - 8), I = limit << (bd - 8), H = (L >> 4) << (bd - 8);
+    int F = 1 << (bd - 8);
+    int p3 = p[-4 * s], p2 = p[-3 * s], p1 = p[-2 * s], p0 = p[-s];
+    int q0 = p[0], q1 = p[s], q2 = p[2 * s], q3 = p[3 * s];
+    bool fm = iabs(p3 - p2) <= I && iabs(p2 - p1) <= I && iabs(p1 - p0) <= I &&
+              iabs(q1 - q0) <= I && iabs(q2 - q1) <= I && iabs(q3 - q2) <= I &&
+              iabs(p0 - q0) * 2 + (iabs(p1 - q1) >> 1) <= E;
+    if (!fm) return;
+    bool flat8in = false, flat8out = false;
+    if (wd >= 8)
+        flat8in = iabs(p3 - p0) <= F && iabs(p2 - p0) <= F && iabs(p1 - p0) <= F &&
+                  iabs(q1 - q0) <= F && iabs(q2 - q0) <= F && iabs(q3 - q0) <= F;
+    if (wd >= 16 && flat8in) {
+        int p7 = p[-8 * s], p6 = p[-7 * s], p5 = p[-6 * s], p4 = p[-5 * s];
+        int q4 = p[4 * s], q5 = p[5 * s], q6 = p[6 * s], q7 = p[7 * s];
+        flat8out = iabs(p7 - p0) <= F && iabs(p6 - p0) <= F && iabs(p5 - p0) <= F &&
+                   iabs(p4 - p0) <= F && iabs(q4 - q0) <= F && iabs(q5 - q0) <= F &&
+                   iabs(q6 - q0) <= F && iabs(q7 - q0) <= F;
+        if (flat8out) {
+            // 15-tap: running window sum over {p7..q7} with edge replication
+            int v[16] = { p7, p6, p5, p4, p3, p2, p1, p0, q0, q1, q2, q3, q4, q5, q6, q7 };
+            int sum = p7 * 7 + p6 * 2 + p5 + p4 + p3 + p2 + p1 + p0 + q0;   // output index 1
+            int out[16];
+            for (int k = 1; k < 15; k++) {
+                out[k] = (sum + 8) >> 4;
+                // slide: window [k-7, k+7] (+ v[k] twice) -> [k-6, k+8] (+ v[k+1] twice)
+                int lo = k - 7 < 0 ? 0 : k - 7, hi = k + 8 > 15 ? 15 : k + 8;
+                sum += v[hi] - v[lo] + v[k + 1] - v[k];
+            }
+            for (int k = 1; k < 15; k++) p[(k - 8) * s] = out[k];
+            return;
+        }
+    }
+    if (wd >= 8 && flat8in) {
+        p[-3 * s] = (p3 + p3 + p3 + 2 * p2 + p1 + p0 + q0 + 4) >> 3;
+        p[-2 * s] = (p3 + p3 + p2 + 2 * p1 + p0 + q0 + q1 + 4) >> 3;
+        p[-1 * s] = (p3 + p2 + p1 + 2 * p0 + q0 + q1 + q2 + 4) >> 3;
+        p[0] = (p2 + p1 + p0 + 2 * q0 + q1 + q2 + q3 + 4) >> 3;
+        p[1 * s] = (p1 + p0 + q0 + 2 * q1 + q2 + q3 + q3 + 4) >> 3;
+        p[2 * s] = (p0 + q0 + q1 + 2 * q2 + q3 + q3 + q3 + 4) >> 3;
+        return;
+    }
+    const int mx = (1 << (bd - 1)) - 1, mn = -(1 << (bd - 1));
+    bool hev = iabs(p1 - p0) > H || iabs(q1 - q0) > H;
+    if (hev) {
+        int f = p1 - q1; f = f < mn ? mn : f > mx ? mx : f;
+        f = 3 * (q0 - p0) + f; f = f < mn ? mn : f > mx ? mx : f;
+        int f1 = (f + 4 < mx ? f + 4 : mx) >> 3, f2 = (f + 3 < mx ? f + 3 : mx) >> 3;
+        p[-s] = clipbd(p0 + f2, bd);
+        p[0] = clipbd(q0 - f1, bd);
+    } else {
+        int f = 3 * (q0 - p0); f = f < mn ? mn : f > mx ? mx : f;
+        int f1 = (f + 4 < mx ? f + 4 : mx) >> 3, f2 = (f + 3 < mx ? f + 3 : mx) >> 3;
+        p[-s] = clipbd(p0 + f2, bd);
+        p[0] = clipbd(q0 - f1, bd);
+        f = (f1 + 1) >> 1;
+        p[-2 * s] = clipbd(p1 + f, bd);
+        p[s] = clipbd(q1 - f, bd);
+    }
+}
+
+#define FLP 74           // luma LF tile pitch (72 used)
+#define FCP 42           // chroma LF tile pitch (40 used)
+
+template <typename PIX>
+__global__ __launch_bounds__(128) void k_lf(const uint32_t *__restrict__ list, const LFRec *__restrict__ recs,
+                                            const FrameDesc *__restrict__ frames)
+{
+    __shared__ uint16_t lt[72 * FLP];
+    __shared__ uint16_t ct[2][40 * FCP];
+    __shared__ uint8_t lvl[64];
+    __shared__ uint8_t msk[2][2][8][4];
+
+    const LFRec &rec = recs[list[blockIdx.x]];
+    const FrameDesc &fd = frames[rec.frame];
+    const int tid = threadIdx.x, bd = fd.bd, sharp = fd.sharp;
+    const int sbx = rec.sbx, sby = rec.sby;
+    if (tid < 64) lvl[tid] = rec.level[tid];
+    if (tid < 128) ((uint8_t *) msk)[tid] = ((const uint8_t *) rec.mask)[tid];
+
+    // load: luma rows [y0-8, y0+64) x cols [x0-8, x0+64), chroma [-8, 32)
+    for (int p = 0; p < 3; p++) {
+        const int sz = p ? 32 : 64, tw = sz + 8, tpch = p ? FCP : FLP;
+        uint16_t *t = p ? ct[p - 1] : lt;
+        const PIX *g = (const PIX *) fd.plane[p];
+        const int pitch = fd.pitch[p ? 1 : 0];
+        const int x0 = sbx * sz - 8, y0 = sby * sz - 8;
+        for (int i = tid; i < tw * tw; i += 128) {
+            int yy = i / tw, xx = i - yy * tw;
+            int gx = x0 + xx, gy = y0 + yy;
+            t[yy * tpch + xx] = (gx >= 0 && gy >= 0) ? g[(size_t) gy * pitch + gx] : 0;
+        }
+    }
+    __syncthreads();
+
+    const int col = sbx * 8, row = sby * 8;   // SB position in 8x8 units
+    // ---- column edges (filter_plane_cols, vp9lpf.c:31-104): one lane per pixel row ----
+    {
+        int p, r;
+        if (tid < 64) { p = 0; r = tid; } else { p = 1 + ((tid - 64) >> 5); r = (tid - 64) & 31; }
+        const int ss = p ? 1 : 0;
+        uint16_t *t = p ? ct[p - 1] : lt;
+        const int tpch = p ? FCP : FLP;
+        uint16_t *rowp = t + (r + 8) * tpch + 8;             // pixel (0, r) of the SB plane
+        const uint8_t(*mask)[4] = msk[p ? 1 : 0][0];
+        // band of 8 rows; pair (hmask1 = first band, hmask2 = second)
+        const int band = r >> 3, half = band & 1, y = (band >> 1) * (2 << ss);
+        const uint8_t *hm1 = mask[y], *hm2 = mask[y + 1 + ss];
+        const int lrow1 = y, lrow2 = y + (1 << ss);          // level rows (l, l[8 << ss_v])
+        const unsigned h1 = hm1[0] | hm1[1] | hm1[2], h2 = hm2[1] | hm2[2];
+        for (int k = 0; k < 8; k++) {
+            const unsigned x = 1u << k;
+            const int ex = ss ? 4 * k : 8 * k;                // edge position in the plane row
+            const int lc = ss ? (k & ~1) : k;                 // level column
+            if (col || k > 0) {
+                int wd = 0, L = 0;
+                if (!half) {
+                    if (h1 & x) { wd = (hm1[0] & x) ? 16 : (hm1[1] & x) ? 8 : 4; L = lvl[lrow1 * 8 + lc]; }
+                } else {
+                    if (h1 & x) {
+                        if (hm1[0] & x) { if (hm2[0] & x) { wd = 16; L = lvl[lrow1 * 8 + lc]; } }
+                        else if (h2 & x) { wd = (hm2[1] & x) ? 8 : 4; L = lvl[lrow2 * 8 + lc]; }
+                    } else if (h2 & x) { wd = (hm2[1] & x) ? 8 : 4; L = lvl[lrow2 * 8 + lc]; }
+                }
+                if (wd) lf_line(rowp + ex, 1, wd, L, sharp, bd);
+            }
+            if (!ss) {
+                const unsigned in = half ? hm2[3] : hm1[3];
+                if (in & x) lf_line(rowp + ex + 4, 1, 4, lvl[(half ? lrow2 : lrow1) * 8 + lc], sharp, bd);
+            }
+        }
+    }
+    __syncthreads();
+    // ---- row edges (filter_plane_rows, vp9lpf.c:106-181): one lane per pixel column ----
+    {
+        int p, c;
+        if (tid < 64) { p = 0; c = tid; } else { p = 1 + ((tid - 64) >> 5); c = (tid - 64) & 31; }
+        const int ss = p ? 1 : 0;
+        uint16_t *t = p ? ct[p - 1] : lt;
+        const int tpch = p ? FCP : FLP;
+        uint16_t *colp = t + 8 * tpch + 8 + c;               // pixel (c, 0) of the SB plane
+        const uint8_t(*mask)[4] = msk[p ? 1 : 0][1];
+        const int chunk = c >> 4, half = (c >> 3) & 1;
+        const unsigned x = 1u << (chunk * (2 << ss)), x2 = x << (1 + ss);
+        const int lc1 = chunk * (2 << ss), lc2 = lc1 + 1 + ss;
+        for (int y = 0; y < 8; y++) {
+            const uint8_t *vm_ = mask[y];
+            const unsigned vm = vm_[0] | vm_[1] | vm_[2], vm3 = vm_[3];
+            const int lr = ss ? (y & ~1) : y;
+            const int ey = ss ? 4 * y : 8 * y;
+            if (row || y) {
+                int wd = 0, L = 0;
+                if (!half) {
+                    if (vm & x) { wd = (vm_[0] & x) ? 16 : (vm_[1] & x) ? 8 : 4; L = lvl[lr * 8 + lc1]; }
+                } else {
+                    if (vm & x) {
+                        if (vm_[0] & x) { if (vm_[0] & x2) { wd = 16; L = lvl[lr * 8 + lc1]; } }
+                        else if (vm & x2) { wd = (vm_[1] & x2) ? 8 : 4; L = lvl[lr * 8 + lc2]; }
+                    } else if (vm & x2) { wd = (vm_[1] & x2) ? 8 : 4; L = lvl[lr * 8 + lc2]; }
+                }
+                if (wd) lf_line(colp + ey * tpch, tpch, wd, L, sharp, bd);
+            }
+            if (!ss) {
+                if (!half) { if (vm3 & x) lf_line(colp + (ey + 4) * tpch, tpch, 4, lvl[lr * 8 + lc1], sharp, bd); }
+                else { if (vm3 & x2) lf_line(colp + (ey + 4) * tpch, tpch, 4, lvl[lr * 8 + lc2], sharp, bd); }
+            }
+        }
+    }
+    __syncthreads();
+    // ---- store the modified region: rows [0,sz) x cols [-8,sz) and rows [-8,0) x cols [0,sz) ----
+    for (int p = 0; p < 3; p++) {
+        const int sz = p ? 32 : 64, tw = sz + 8, tpch = p ? FCP : FLP;
+        const uint16_t *t = p ? ct[p - 1] : lt;
+        PIX *g = (PIX *) fd.plane[p];
+        const int pitch = fd.pitch[p ? 1 : 0];
+        const int x0 = sbx * sz - 8, y0 = sby * sz - 8;
+        const int wlim = fd.w8[p ? 1 : 0], hlim = fd.h8[p ? 1 : 0];
+        for (int i = tid; i < tw * tw; i += 128) {
+            int yy = i / tw, xx = i - yy * tw;
+            if (yy < 8 && xx < 8) continue;
+            int gx = x0 + xx, gy = y0 + yy;
+            if (gx >= 0 && gy >= 0 && gx < wlim && gy < hlim) g[(size_t) gy * pitch + gx] = (PIX) t[yy * tpch + xx];
+        }
+    }
+}
+
+// --------------------------------------------------------------- k_mc
+template <typename PIX>
+DEV int mc_ref(const PIX *r, int pitch, int w, int h, int x, int y)
+{
+    x = x < 0 ? 0 : x >= w ? w - 1 : x;
+    y = y < 0 ? 0 : y >= h ? h - 1 : y;
+    return r[(size_t) y * pitch + x];
+}
+
+template <typename PIX>
+DEV int mc_sample(const PIX *r, int pitch, int w, int h, int X, int Y, int mx, int my, int filter, int bd)
+{
+    if (!mx && !my) return mc_ref(r, pitch, w, h, X, Y);
+    if (filter == 3) {   // bilinear (vp9dsp_template.c:2150-2227)
+        if (mx && my) {
+            int a0 = mc_ref(r, pitch, w, h, X, Y), a1 = mc_ref(r, pitch, w, h, X + 1, Y);
+            int b0 = mc_ref(r, pitch, w, h, X, Y + 1), b1 = mc_ref(r, pitch, w, h, X + 1, Y + 1);
+            int t0 = a0 + ((mx * (a1 - a0) + 8) >> 4), t1 = b0 + ((mx * (b1 - b0) + 8) >> 4);
+            return t0 + ((my * (t1 - t0) + 8) >> 4);
+        }
+        int a0 = mc_ref(r, pitch, w, h, X, Y);
+        int a1 = mx ? mc_ref(r, pitch, w, h, X + 1, Y) : mc_ref(r, pitch, w, h, X, Y + 1);
+        int m = mx ? mx : my;
+        return a0 + ((m * (a1 - a0) + 8) >> 4);
+    }
+    const int16_t *fx = vp9t_subpel_filters[filter][mx], *fy = vp9t_subpel_filters[filter][my];
+    if (mx && my) {   // 2-D: pixel-clipped horizontal pass (vp9dsp_template.c:2076-2113)
+        int acc = 0;
+        for (int k = 0; k < 8; k++) {
+            int s = 0;
+            for (int t = 0; t < 8; t++) s += fx[t] * mc_ref(r, pitch, w, h, X - 3 + t, Y - 3 + k);
+            acc += fy[k] * clipbd((s + 64) >> 7, bd);
+        }
+        return clipbd((acc + 64) >> 7, bd);
+    }
+    int s = 0;
+    if (mx) for (int t = 0; t < 8; t++) s += fx[t] * mc_ref(r, pitch, w, h, X - 3 + t, Y);
+    else    for (int t = 0; t < 8; t++) s += fy[t] * mc_ref(r, pitch, w, h, X, Y - 3 + t);
+    return clipbd((s + 64) >> 7, bd);
+}
+
+template <typename PIX>
+__global__ __launch_bounds__(256) void k_mc(const McUnit *__restrict__ units, int nunits,
+                                            const FrameDesc *__restrict__ frames)
+{
+    const McUnit u = units[blockIdx.x];
+    const FrameDesc &fd = frames[u.frame];
+    const int p = u.plane, c = p ? 1 : 0, bd = fd.bd;
+    PIX *dst = (PIX *) fd.plane[p];
+    const int pitch = fd.pitch[c];
+    for (int i = threadIdx.x; i < u.w * u.h; i += 256) {
+        int yy = i / u.w, xx = i - yy * u.w;
+        int out = 0;
+        for (int k = 0; k < u.nref; k++) {
+            const int rf = u.ref[k];
+            const PIX *r = (const PIX *) fd.ref[rf][p];
+            int dx = u.d16[k][0], dy = u.d16[k][1];
+            int X = u.x + xx + (dx >> 4), Y = u.y + yy + (dy >> 4);
+            int v = mc_sample<PIX>(r, pitch, fd.refw[rf][c], fd.refh[rf][c], X, Y, dx & 15, dy & 15, u.filter, bd);
+            out = k ? (out + v + 1) >> 1 : v;
+        }
+        dst[(size_t) (u.y + yy) * pitch + u.x + xx] = (PIX) out;
+    }
+}
+
+// ------------------------------------------------------------ launchers
+extern "C" {
+int vp9hip_launch_recon(int hb, hipStream_t st, int nsb, const uint32_t *list, const SBRec *sbs,
+                        const TxJob *jobs, const uint16_t *lvls, const FrameDesc *frames, const void *coefs)
+{
+    if (nsb <= 0) return 0;
+    if (hb)
+        hipLaunchKernelGGL((k_recon<uint16_t, M64, int32_t>), dim3(nsb), dim3(256), 0, st,
+                           list, sbs, jobs, lvls, frames, (const int32_t *) coefs);
+    else
+        hipLaunchKernelGGL((k_recon<uint8_t, M32, int16_t>), dim3(nsb), dim3(256), 0, st,
+                           list, sbs, jobs, lvls, frames, (const int16_t *) coefs);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int vp9hip_launch_lf(int hb, hipStream_t st, int nsb, const uint32_t *list, const LFRec *recs,
+                     const FrameDesc *frames)
+{
+    if (nsb <= 0) return 0;
+    if (hb) hipLaunchKernelGGL(k_lf<uint16_t>, dim3(nsb), dim3(128), 0, st, list, recs, frames);
+    else    hipLaunchKernelGGL(k_lf<uint8_t>, dim3(nsb), dim3(128), 0, st, list, recs, frames);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int vp9hip_launch_mc(int hb, hipStream_t st, int n, const McUnit *units, const FrameDesc *frames)
+{
+    if (n <= 0) return 0;
+    if (hb) hipLaunchKernelGGL(k_mc<uint16_t>, dim3(n), dim3(256), 0, st, units, n, frames);
+    else    hipLaunchKernelGGL(k_mc<uint8_t>, dim3(n), dim3(256), 0, st, units, n, frames);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+}

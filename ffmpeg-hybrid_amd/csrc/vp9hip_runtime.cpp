@@ -1,0 +1,670 @@
+// Host runtime of the MI355X VP9 hybrid decoder: implements the C-ABI of
+// include/vp9hip.h on top of the gfx950 kernels in vp9hip_kernels.hip.
+//
+// From each pass-1 frame packet it builds, on the host:
+//   * per-superblock transform-block job lists, topologically levelled by the
+//     intra dependencies of check_intra_mode (vp9recon.c:37-221) so one SB is
+//     reconstructed by one workgroup in LDS;
+//   * the loop-filter level/mask record of every SB (VP9Filter, restating
+//     vp9block.c:1142-1262 and 1438-1452);
+//   * motion-compensation rectangles restating inter_pred's sub-8x8 MV rules
+//     (vp9_mc_template.c:30-464);
+//   * launch schedules: the intra SB wavefront (t = x_in_tile + y) and the LF SB
+//     wavefront (t = x + 2y) that reproduces the reference's SB-raster LF order
+//     (vp9.c:1419-1429).
+// Everything is uploaded into one HBM arena per staged batch; run launches only.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#pragma clang diagnostic ignored "-Wunused-result"
+#pragma clang diagnostic ignored "-Wunused-value"
+
+#include "../../include/vp9hip.h"
+#include "vp9_tables.h"
+#include "vp9hip_work.h"
+
+extern "C" {
+int vp9hip_launch_recon(int hb, hipStream_t st, int nsb, const uint32_t *list, const SBRec *sbs,
+                        const TxJob *jobs, const uint16_t *lvls, const FrameDesc *frames, const void *coefs);
+int vp9hip_launch_lf(int hb, hipStream_t st, int nsb, const uint32_t *list, const LFRec *recs,
+                     const FrameDesc *frames);
+int vp9hip_launch_mc(int hb, hipStream_t st, int n, const McUnit *units, const FrameDesc *frames);
+}
+
+namespace {
+
+enum { K_MC, K_RECON, K_LF, K_N };
+const char *const kname[K_N] = { "k_mc", "k_recon", "k_lf" };
+
+// ff_vp9_intra_txfm_type (vp9data.c:437-452)
+const uint8_t intra_txfm_type[14] = { 2, 1, 0, 0, 3, 2, 1, 2, 1, 3, 0, 0, 0, 0 };
+
+struct Launch { int kind; uint32_t off; uint32_t n; };
+
+struct Staged {
+    // host images (kept for rebuilds / inspection)
+    std::vector<FrameDesc> frames;
+    std::vector<SBRec> sbs;
+    std::vector<TxJob> jobs;
+    std::vector<uint16_t> lvls;
+    std::vector<LFRec> lfs;
+    std::vector<McUnit> mcs;
+    std::vector<uint32_t> lists;        // concatenated SB index lists of all launches
+    std::vector<Launch> launches;
+    std::vector<uint8_t> coefs;         // concatenated coefficient streams (bytes)
+    double alg_bytes[K_N] = { 0, 0, 0 };
+    // device arena
+    uint8_t *arena = nullptr;
+    size_t arena_cap = 0;
+    size_t o_frames = 0, o_sbs = 0, o_jobs = 0, o_lvls = 0, o_lfs = 0, o_mcs = 0, o_lists = 0, o_coefs = 0;
+    bool ready = false;
+};
+
+} // namespace
+
+struct vp9hip_ctx {
+    int dev = 0;
+    hipStream_t st = nullptr;
+    int w = 0, h = 0, bpp = 8, ss_h = 1, ss_v = 1, hb = 0, bypp = 1;
+    int cols = 0, rows = 0, sb_cols = 0, sb_rows = 0;
+    int pitch[2] = { 0, 0 };
+    size_t plane_off[3] = { 0, 0, 0 }, buf_bytes = 0;
+    std::vector<uint8_t *> bufs;
+    Staged stg;
+    // timing of the last run
+    bool timing = true;
+    std::vector<hipEvent_t> ev;
+    double kms[K_N] = { 0, 0, 0 };
+    int kcount[K_N] = { 0, 0, 0 };
+};
+
+#define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+    fprintf(stderr, "vp9hip: %s failed: %s\n", #x, hipGetErrorString(e_)); return VP9HIP_EEXTERNAL; } } while (0)
+
+extern "C" int vp9hip_open(int device, vp9hip_ctx **out)
+{
+    if (!out) return VP9HIP_EINVAL;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return VP9HIP_ENOSYS;
+    vp9hip_ctx *c = new vp9hip_ctx;
+    c->dev = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return VP9HIP_EEXTERNAL;
+    }
+    *out = c;
+    return 0;
+}
+
+static void free_bufs(vp9hip_ctx *c)
+{
+    for (auto *b : c->bufs) hipFree(b);
+    c->bufs.clear();
+}
+
+extern "C" void vp9hip_close(vp9hip_ctx *c)
+{
+    if (!c) return;
+    hipSetDevice(c->dev);
+    hipStreamSynchronize(c->st);
+    free_bufs(c);
+    if (c->stg.arena) hipFree(c->stg.arena);
+    for (auto e : c->ev) hipEventDestroy(e);
+    hipStreamDestroy(c->st);
+    delete c;
+}
+
+extern "C" int vp9hip_configure(vp9hip_ctx *c, int width, int height, int bpp, int ss_h, int ss_v, int nbufs)
+{
+    if (!c || width <= 0 || height <= 0 || nbufs <= 0 || width > 16384 || height > 16384) return VP9HIP_EINVAL;
+    if (bpp != 8 && bpp != 10 && bpp != 12) return VP9HIP_EINVAL;
+    if (ss_h != 1 || ss_v != 1) return VP9HIP_ENOSYS;   // 4:2:0 only on the device path (profiles 0/2)
+    hipSetDevice(c->dev);
+    hipStreamSynchronize(c->st);
+    free_bufs(c);
+    c->w = width; c->h = height; c->bpp = bpp; c->ss_h = ss_h; c->ss_v = ss_v;
+    c->hb = bpp > 8; c->bypp = c->hb ? 2 : 1;
+    c->cols = (width + 7) >> 3; c->rows = (height + 7) >> 3;
+    c->sb_cols = (width + 63) >> 6; c->sb_rows = (height + 63) >> 6;
+    c->pitch[0] = c->sb_cols * 64;
+    c->pitch[1] = c->sb_cols * 64 >> ss_h;
+    size_t hy = (size_t) c->sb_rows * 64, hc = hy >> ss_v;
+    c->plane_off[0] = 0;
+    c->plane_off[1] = (size_t) c->pitch[0] * hy * c->bypp;
+    c->plane_off[2] = c->plane_off[1] + (size_t) c->pitch[1] * hc * c->bypp;
+    c->buf_bytes = c->plane_off[2] + (size_t) c->pitch[1] * hc * c->bypp;
+    for (int i = 0; i < nbufs; i++) {
+        uint8_t *b = nullptr;
+        if (hipMalloc(&b, c->buf_bytes) != hipSuccess) { free_bufs(c); return VP9HIP_ENOMEM; }
+        hipMemsetAsync(b, 0, c->buf_bytes, c->st);
+        c->bufs.push_back(b);
+    }
+    c->stg.ready = false;
+    return hipStreamSynchronize(c->st) == hipSuccess ? 0 : VP9HIP_EEXTERNAL;
+}
+
+// --------------------------------------------------------------------------
+// loop-filter masks: restates mask_edges (vp9block.c:1142-1262)
+static void lf_mask_edges(uint8_t (*mask)[8][4], int ss_h, int ss_v, int row7, int col7, int w, int h,
+                          int col_end, int row_end, int tx, int skip_inter)
+{
+    static const unsigned wide_col[2] = { 0x11, 0x01 }, wide_row[2] = { 0x03, 0x07 };
+    if (tx == 0 && (ss_v | ss_h)) {
+        if (h == ss_v) { if (row7 & 1) return; if (!row_end) h += 1; }
+        if (w == ss_h) { if (col7 & 1) return; if (!col_end) w += 1; }
+    }
+    const unsigned t = 1u << col7, m_col = (t << w) - t;
+    if (tx == 0 && !skip_inter) {
+        const unsigned m8 = m_col & wide_col[ss_h], m4 = m_col - m8;
+        for (int y = row7; y < h + row7; y++) {
+            const int id = 2 - !(y & wide_row[ss_v]);
+            mask[0][y][1] |= m8;
+            mask[0][y][2] |= m4;
+            mask[1][y][id] |= ((ss_h & ss_v) && (col_end & 1) && (y & 1)) ? (t << (w - 1)) - t : m_col;
+            if (!ss_h) mask[0][y][3] |= m_col;
+            if (!ss_v) mask[1][y][3] |= (ss_h && (col_end & 1)) ? (t << (w - 1)) - t : m_col;
+        }
+        return;
+    }
+    if (!skip_inter) {
+        static const unsigned masks[4] = { 0xff, 0x55, 0x11, 0x01 };
+        const int id = tx == 1;
+        int l2 = tx + ss_h - 1;
+        const unsigned m_row = m_col & masks[l2];
+        if (ss_h && tx > 1 && (w ^ (w - 1)) == 1) {
+            const unsigned m16 = ((t << (w - 1)) - t) & masks[l2], m8 = m_row - m16;
+            for (int y = row7; y < h + row7; y++) { mask[0][y][0] |= m16; mask[0][y][1] |= m8; }
+        } else {
+            for (int y = row7; y < h + row7; y++) mask[0][y][id] |= m_row;
+        }
+        l2 = tx + ss_v - 1;
+        const int step = 1 << l2;
+        int y;
+        if (ss_v && tx > 1 && (h ^ (h - 1)) == 1) {
+            for (y = row7; y < h + row7 - 1; y += step) mask[1][y][0] |= m_col;
+            if (y - row7 == h - 1) mask[1][y][1] |= m_col;
+        } else {
+            for (y = row7; y < h + row7; y += step) mask[1][y][id] |= m_col;
+        }
+    } else if (tx != 0) {
+        mask[1][row7][(tx == 1) || (h == ss_v)] |= m_col;
+        const int id = (tx == 1) || (w == ss_h);
+        for (int y = row7; y < h + row7; y++) mask[0][y][id] |= t;
+    } else {
+        const unsigned t8 = t & wide_col[ss_h], t4 = t - t8;
+        for (int y = row7; y < h + row7; y++) { mask[0][y][2] |= t4; mask[0][y][1] |= t8; }
+        mask[1][row7][2 - !(row7 & wide_row[ss_v])] |= m_col;
+    }
+}
+
+static inline int rdiv(int a, int b) { return (a >= 0 ? a + (b >> 1) : a - (b >> 1)) / b; }
+
+// --------------------------------------------------------------------------
+// Per-frame work building
+namespace {
+
+struct FrameBuild {
+    const vp9h_frame *f;
+    int frame_idx;
+    int cols, rows, sb_cols, sb_rows;
+    int ss_h, ss_v, coef_size;
+    uint64_t coef_base;          // element offset of this frame's coefficients in the batch stream
+};
+
+struct PendingJob { TxJob j; int level; };
+
+} // namespace
+
+// Build jobs/levels/LF/MC for one frame. Appends to stg. Returns 0 or error.
+static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<uint32_t> &recon_parallel,
+                       std::vector<std::vector<uint32_t>> &recon_steps, std::vector<std::vector<uint32_t>> &lf_steps)
+{
+    const vp9h_frame *f = fb.f;
+    const int ss_h = fb.ss_h, ss_v = fb.ss_v, cols = fb.cols, rows = fb.rows;
+    const int lossless = f->lossless;
+    const uint16_t *eob = f->eobs;
+    const uint16_t *eob_end = f->eobs + f->neobs;
+    uint64_t coef = fb.coef_base;           // running element index
+    uint32_t bi = 0;
+    const int log2 = f->log2_tile_cols;
+
+    std::vector<PendingJob> pj;
+    pj.reserve(1024);
+    int8_t lmap[3][16 * 16];
+
+    while (bi < f->nblocks) {
+        const vp9h_block *b0 = &f->blocks[bi];
+        const int sbx = b0->col >> 3, sby = b0->row >> 3;
+        // tile column of this SB (vp9.c:1244-1250)
+        int tile_x0 = 0, tile_sb0 = 0;
+        for (int ti = 0; ti < (1 << log2); ti++) {
+            int s0 = std::min((ti * fb.sb_cols) >> log2, fb.sb_cols), s1 = std::min(((ti + 1) * fb.sb_cols) >> log2, fb.sb_cols);
+            if (sbx >= s0 && sbx < s1) { tile_x0 = s0 << 3; tile_sb0 = s0; }
+        }
+        LFRec lf;
+        memset(&lf, 0, sizeof(lf));
+        lf.frame = fb.frame_idx; lf.sbx = sbx; lf.sby = sby;
+        pj.clear();
+        memset(lmap, -1, sizeof(lmap));
+        bool has_intra = false;
+
+        for (; bi < f->nblocks; bi++) {
+            const vp9h_block *b = &f->blocks[bi];
+            if ((b->col >> 3) != sbx || (b->row >> 3) != sby) break;
+            if (b->bs >= VP9H_N_BS || b->tx > 3 || b->uvtx > 3) return VP9HIP_EINVALIDDATA;
+            const int bw8 = vp9t_bwh[1][b->bs][0], bh8 = vp9t_bwh[1][b->bs][1];
+            const int w4 = bw8 << 1, h4 = bh8 << 1;
+            int end_x = std::min(2 * (cols - b->col), w4), end_y = std::min(2 * (rows - b->row), h4);
+            if (b->intra) has_intra = true;
+
+            for (int p = 0; p < 3; p++) {
+                const int sh = p ? ss_h : 0, sv = p ? ss_v : 0;
+                const int txs = p ? b->uvtx : b->tx, step = 1 << txs;
+                const int pw4 = w4 >> sh, ex = end_x >> sh, ey = end_y >> sv;
+                const int bx = (b->col * 8 >> sh), by = (b->row * 8 >> sv);     // plane pixel pos
+                const int sbsz = 64 >> sh, sbszv = 64 >> sv;
+                const int ux_sb = (bx - sbx * sbsz) >> 2, uy_sb = (by - sby * sbszv) >> 2;
+                const int units = sbsz >> 2;  // units per row of this plane's SB (16 luma, 8 chroma)
+                for (int y = 0; y < ey; y += step)
+                    for (int x = 0; x < ex; x += step) {
+                        int e = 0;
+                        if (!b->skip) {
+                            if (eob >= eob_end) return VP9HIP_EINVALIDDATA;
+                            e = *eob++;
+                        }
+                        if (!b->intra && !e) continue;
+                        TxJob j;
+                        memset(&j, 0, sizeof(j));
+                        int mode = 0xff, txtp = 0;
+                        if (b->intra) {
+                            mode = p ? b->uvmode : b->mode[b->bs > VP9H_BS_8x8 && b->tx == 0 ? y * 2 + x : 0];
+                            if (mode > 9) return VP9HIP_EINVALIDDATA;
+                            txtp = p ? 0 : intra_txfm_type[mode];
+                        }
+                        const int tcode = lossless ? 4 : txs;
+                        j.ptx = (uint8_t) (p | (tcode << 2));
+                        j.txtp = (uint8_t) txtp;
+                        j.mode = (uint8_t) mode;
+                        j.flags = (x < pw4 - 1) ? 1 : 0;
+                        j.x4 = (uint8_t) (ux_sb + x);
+                        j.y4 = (uint8_t) (uy_sb + y);
+                        j.eob = (uint16_t) e;
+                        j.coef = (uint32_t) coef;
+                        coef += e;
+                        // dependency level within the SB plane
+                        int lvl = -1;
+                        const int ux0 = ux_sb + x, uy0 = uy_sb + y, n4 = step;
+                        int8_t *lm = lmap[p];
+                        if (b->intra) {
+                            const int trx = (txs == 0 && (j.flags & 1)) ? 1 : 0;
+                            if (uy0 > 0)
+                                for (int u = ux0 - 1; u < ux0 + n4 + trx; u++)
+                                    if (u >= 0 && u < units) lvl = std::max<int>(lvl, lm[(uy0 - 1) * 16 + u]);
+                            if (ux0 > 0)
+                                for (int v = uy0; v < uy0 + n4; v++)
+                                    if (v < units) lvl = std::max<int>(lvl, lm[v * 16 + ux0 - 1]);
+                        }
+                        lvl += 1;
+                        for (int v = uy0; v < uy0 + n4 && v < units; v++)
+                            for (int u = ux0; u < ux0 + n4 && u < units; u++) lm[v * 16 + u] = (int8_t) lvl;
+                        pj.push_back({ j, lvl });
+                    }
+            }
+
+            // inter prediction units (vp9_mc_template.c:30-464), 4:2:0
+            if (!b->intra) {
+                McUnit u;
+                memset(&u, 0, sizeof(u));
+                u.frame = fb.frame_idx;
+                u.filter = b->filter;
+                u.nref = b->comp ? 2 : 1;
+                u.ref[0] = b->ref[0];
+                u.ref[1] = b->ref[1];
+                auto luma = [&](int x, int y, int w, int hh, int bidx) {
+                    McUnit m = u;
+                    m.plane = 0; m.x = x; m.y = y; m.w = w; m.h = hh;
+                    for (int k = 0; k < m.nref; k++) { m.d16[k][0] = b->mv[bidx][k][0] * 2; m.d16[k][1] = b->mv[bidx][k][1] * 2; }
+                    s.mcs.push_back(m);
+                };
+                auto chroma = [&](int x, int y, int w, int hh, const int16_t mv[2][2]) {
+                    for (int p = 1; p < 3; p++) {
+                        McUnit m = u;
+                        m.plane = p; m.x = x; m.y = y; m.w = w; m.h = hh;
+                        for (int k = 0; k < m.nref; k++) { m.d16[k][0] = mv[k][0]; m.d16[k][1] = mv[k][1]; }
+                        s.mcs.push_back(m);
+                    }
+                };
+                const int lx = b->col * 8, ly = b->row * 8, cx = b->col * 4, cy = b->row * 4;
+                int16_t uv[2][2];
+                if (b->bs > VP9H_BS_8x8) {
+                    if (b->bs == VP9H_BS_8x4) {
+                        luma(lx, ly, 8, 4, 0); luma(lx, ly + 4, 8, 4, 2);
+                        for (int k = 0; k < 2; k++) for (int d = 0; d < 2; d++) uv[k][d] = rdiv(b->mv[0][k][d] + b->mv[2][k][d], 2);
+                    } else if (b->bs == VP9H_BS_4x8) {
+                        luma(lx, ly, 4, 8, 0); luma(lx + 4, ly, 4, 8, 1);
+                        for (int k = 0; k < 2; k++) for (int d = 0; d < 2; d++) uv[k][d] = rdiv(b->mv[0][k][d] + b->mv[1][k][d], 2);
+                    } else {
+                        luma(lx, ly, 4, 4, 0); luma(lx + 4, ly, 4, 4, 1);
+                        luma(lx, ly + 4, 4, 4, 2); luma(lx + 4, ly + 4, 4, 4, 3);
+                        for (int k = 0; k < 2; k++) for (int d = 0; d < 2; d++)
+                            uv[k][d] = rdiv(b->mv[0][k][d] + b->mv[1][k][d] + b->mv[2][k][d] + b->mv[3][k][d], 4);
+                    }
+                    chroma(cx, cy, 4, 4, uv);
+                } else {
+                    const int bw = vp9t_bwh[0][b->bs][0] * 4, bh = vp9t_bwh[0][b->bs][1] * 4;
+                    luma(lx, ly, bw, bh, 0);
+                    for (int k = 0; k < 2; k++) for (int d = 0; d < 2; d++) uv[k][d] = b->mv[0][k][d];
+                    chroma(cx, cy, vp9t_bwh[1][b->bs][0] * 4, vp9t_bwh[1][b->bs][1] * 4, uv);
+                }
+            }
+
+            // LF level + masks (vp9block.c:1438-1452)
+            int lvl;
+            if (f->filter_level && b->seg_id < 8 &&
+                (lvl = f->lflvl[b->seg_id][b->intra ? 0 : b->ref[0] + 1][b->mode[3] != VP9H_ZEROMV]) > 0) {
+                const int x_end = std::min(cols - b->col, bw8), y_end = std::min(rows - b->row, bh8);
+                const int skip_inter = !b->intra && b->skip, col7 = b->col & 7, row7 = b->row & 7;
+                for (int yy = 0; yy < bh8; yy++)
+                    for (int xx = 0; xx < bw8; xx++) lf.level[(row7 + yy) * 8 + col7 + xx] = (uint8_t) lvl;
+                lf_mask_edges(lf.mask[0], 0, 0, row7, col7, x_end, y_end, 0, 0, b->tx, skip_inter);
+                lf_mask_edges(lf.mask[1], ss_h, ss_v, row7, col7, x_end, y_end,
+                              (cols & 1) && b->col + bw8 >= cols ? cols & 7 : 0,
+                              (rows & 1) && b->row + bh8 >= rows ? rows & 7 : 0, b->uvtx, skip_inter);
+            }
+        }
+
+        // sort jobs by level (stable), emit SB record
+        int nlev = 0;
+        for (auto &q : pj) nlev = std::max(nlev, q.level + 1);
+        SBRec sr;
+        memset(&sr, 0, sizeof(sr));
+        sr.frame = fb.frame_idx; sr.sbx = sbx; sr.sby = sby;
+        sr.job0 = (uint32_t) s.jobs.size();
+        sr.lvl0 = (uint32_t) s.lvls.size();
+        sr.nlev = (uint16_t) nlev;
+        sr.tile_x0 = (uint16_t) tile_x0;
+        sr.flags = f->keyframe || f->intraonly ? 0 : 1;
+        std::vector<int> cnt(nlev + 1, 0);
+        for (auto &q : pj) cnt[q.level + 1]++;
+        for (int l = 0; l < nlev; l++) cnt[l + 1] += cnt[l];
+        for (int l = 0; l <= nlev; l++) s.lvls.push_back((uint16_t) cnt[l]);
+        size_t base = s.jobs.size();
+        s.jobs.resize(base + pj.size());
+        std::vector<int> pos(cnt.begin(), cnt.end());
+        for (auto &q : pj) s.jobs[base + pos[q.level]++] = q.j;
+        uint32_t sbi = (uint32_t) s.sbs.size();
+        s.sbs.push_back(sr);
+        if (!pj.empty() || sr.flags == 0) {
+            if (has_intra) {
+                int d = (sbx - tile_sb0) + sby;
+                if ((int) recon_steps.size() <= d) recon_steps.resize(d + 1);
+                recon_steps[d].push_back(sbi);
+            } else {
+                recon_parallel.push_back(sbi);
+            }
+        }
+        if (f->filter_level) {
+            uint32_t li = (uint32_t) s.lfs.size();
+            s.lfs.push_back(lf);
+            int d = sbx + 2 * sby;
+            if ((int) lf_steps.size() <= d) lf_steps.resize(d + 1);
+            lf_steps[d].push_back(li);
+        }
+        (void) has_intra;
+    }
+    if (eob != eob_end) return VP9HIP_EINVALIDDATA;
+    if (coef - fb.coef_base != f->ncoefs) return VP9HIP_EINVALIDDATA;
+    return 0;
+}
+
+static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bufs, const int *ref_bufs /*n*3 or null*/)
+{
+    if (!c || !pkts || n <= 0 || !out_bufs) return VP9HIP_EINVAL;
+    if (c->bufs.empty()) return VP9HIP_EINVAL;
+    hipSetDevice(c->dev);
+    HIPCHK(hipStreamSynchronize(c->st));      // the previous batch may still read the arena
+    Staged &s = c->stg;
+    s.frames.clear(); s.sbs.clear(); s.jobs.clear(); s.lvls.clear(); s.lfs.clear(); s.mcs.clear();
+    s.lists.clear(); s.launches.clear(); s.coefs.clear();
+    for (int k = 0; k < K_N; k++) s.alg_bytes[k] = 0;
+    s.ready = false;
+
+    const int csz = c->hb ? 4 : 2;
+    std::vector<uint32_t> par;
+    std::vector<std::vector<uint32_t>> rsteps, lsteps;
+    uint64_t coef_base = 0;
+    double pix_bytes = (double) c->w * c->h * c->bypp * (1.0 + 2.0 / ((1 << c->ss_h) * (1 << c->ss_v)));
+    for (int i = 0; i < n; i++) {
+        const vp9h_frame *f = &pkts[i];
+        if (f->width != c->w || f->height != c->h || f->bpp != c->bpp || f->ss_h != c->ss_h || f->ss_v != c->ss_v)
+            return VP9HIP_EINVAL;
+        if (out_bufs[i] < 0 || out_bufs[i] >= (int) c->bufs.size()) return VP9HIP_EINVAL;
+        const bool intra = f->keyframe || f->intraonly;
+        if (!intra && n != 1) return VP9HIP_EINVAL;     // inter frames are staged one at a time
+        FrameDesc fd;
+        memset(&fd, 0, sizeof(fd));
+        uint8_t *ob = c->bufs[out_bufs[i]];
+        for (int p = 0; p < 3; p++) fd.plane[p] = (uint64_t) (ob + c->plane_off[p]);
+        fd.pitch[0] = c->pitch[0]; fd.pitch[1] = c->pitch[1];
+        fd.w8[0] = c->cols * 8; fd.h8[0] = c->rows * 8;
+        fd.w8[1] = c->cols * 8 >> c->ss_h; fd.h8[1] = c->rows * 8 >> c->ss_v;
+        fd.sb_cols = c->sb_cols; fd.sb_rows = c->sb_rows;
+        fd.bd = c->bpp;
+        fd.sharp = f->sharpness;
+        if (!intra) {
+            if (!ref_bufs) return VP9HIP_EINVAL;
+            for (int r = 0; r < 3; r++) {
+                int rb = ref_bufs[i * 3 + r];
+                if (rb < 0 || rb >= (int) c->bufs.size()) return VP9HIP_EINVAL;
+                if (f->ref_w[r] != c->w || f->ref_h[r] != c->h) return VP9HIP_ENOSYS;  // scaled MC: not yet on device
+                for (int p = 0; p < 3; p++) fd.ref[r][p] = (uint64_t) (c->bufs[rb] + c->plane_off[p]);
+                fd.refw[r][0] = f->ref_w[r]; fd.refh[r][0] = f->ref_h[r];
+                fd.refw[r][1] = (f->ref_w[r] + c->ss_h) >> c->ss_h; fd.refh[r][1] = (f->ref_h[r] + c->ss_v) >> c->ss_v;
+            }
+        }
+        s.frames.push_back(fd);
+        FrameBuild fb;
+        fb.f = f; fb.frame_idx = i;
+        fb.cols = c->cols; fb.rows = c->rows; fb.sb_cols = c->sb_cols; fb.sb_rows = c->sb_rows;
+        fb.ss_h = c->ss_h; fb.ss_v = c->ss_v; fb.coef_size = csz;
+        fb.coef_base = coef_base;
+        size_t mc0 = s.mcs.size();
+        int r = build_frame(c, s, fb, par, rsteps, lsteps);
+        if (r < 0) return r;
+        size_t cb = (size_t) f->ncoefs * csz;
+        size_t off = s.coefs.size();
+        s.coefs.resize(off + cb);
+        if (cb) memcpy(s.coefs.data() + off, f->coefs, cb);
+        coef_base += f->ncoefs;
+        if (coef_base > 0xffffffffull) return VP9HIP_ENOMEM;
+        // algorithmic bytes: recon writes P and reads C (+P for inter SBs),
+        // LF reads + writes P, MC reads R*P and writes the predicted pixels
+        s.alg_bytes[K_RECON] += (double) cb + pix_bytes * (intra ? 1.0 : 2.0);
+        if (f->filter_level) s.alg_bytes[K_LF] += 2.0 * pix_bytes;
+        for (size_t m = mc0; m < s.mcs.size(); m++)
+            s.alg_bytes[K_MC] += (double) s.mcs[m].w * s.mcs[m].h * c->bypp * (1 + s.mcs[m].nref);
+    }
+    // launch schedule: MC, recon (parallel SBs, then the intra wavefront), LF wavefront
+    if (!s.mcs.empty()) s.launches.push_back({ K_MC, 0, (uint32_t) s.mcs.size() });
+    auto add_list = [&](int kind, const std::vector<uint32_t> &v) {
+        if (v.empty()) return;
+        s.launches.push_back({ kind, (uint32_t) s.lists.size(), (uint32_t) v.size() });
+        s.lists.insert(s.lists.end(), v.begin(), v.end());
+    };
+    add_list(K_RECON, par);
+    for (auto &v : rsteps) add_list(K_RECON, v);
+    for (auto &v : lsteps) add_list(K_LF, v);
+
+    // upload into one arena
+    auto al = [](size_t x) { return (x + 255) & ~(size_t) 255; };
+    size_t o = 0;
+    s.o_frames = o; o = al(o + s.frames.size() * sizeof(FrameDesc));
+    s.o_sbs = o; o = al(o + s.sbs.size() * sizeof(SBRec));
+    s.o_jobs = o; o = al(o + s.jobs.size() * sizeof(TxJob));
+    s.o_lvls = o; o = al(o + s.lvls.size() * sizeof(uint16_t));
+    s.o_lfs = o; o = al(o + s.lfs.size() * sizeof(LFRec));
+    s.o_mcs = o; o = al(o + s.mcs.size() * sizeof(McUnit));
+    s.o_lists = o; o = al(o + s.lists.size() * sizeof(uint32_t));
+    s.o_coefs = o; o = al(o + s.coefs.size() + 64);
+    if (o > s.arena_cap) {
+        if (s.arena) hipFree(s.arena);
+        s.arena = nullptr;
+        s.arena_cap = 0;
+        if (hipMalloc(&s.arena, o) != hipSuccess) return VP9HIP_ENOMEM;
+        s.arena_cap = o;
+    }
+    auto up = [&](size_t off, const void *src, size_t bytes) -> int {
+        if (!bytes) return 0;
+        return hipMemcpyAsync(s.arena + off, src, bytes, hipMemcpyHostToDevice, c->st) == hipSuccess ? 0 : -1;
+    };
+    if (up(s.o_frames, s.frames.data(), s.frames.size() * sizeof(FrameDesc)) ||
+        up(s.o_sbs, s.sbs.data(), s.sbs.size() * sizeof(SBRec)) ||
+        up(s.o_jobs, s.jobs.data(), s.jobs.size() * sizeof(TxJob)) ||
+        up(s.o_lvls, s.lvls.data(), s.lvls.size() * sizeof(uint16_t)) ||
+        up(s.o_lfs, s.lfs.data(), s.lfs.size() * sizeof(LFRec)) ||
+        up(s.o_mcs, s.mcs.data(), s.mcs.size() * sizeof(McUnit)) ||
+        up(s.o_lists, s.lists.data(), s.lists.size() * sizeof(uint32_t)) ||
+        up(s.o_coefs, s.coefs.data(), s.coefs.size()))
+        return VP9HIP_EEXTERNAL;
+    HIPCHK(hipStreamSynchronize(c->st));
+    s.ready = true;
+    return 0;
+}
+
+extern "C" int vp9hip_stage_batch(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bufs)
+{
+    return stage(c, pkts, n, out_bufs, nullptr);
+}
+
+extern "C" int vp9hip_run_batch(vp9hip_ctx *c)
+{
+    if (!c || !c->stg.ready) return VP9HIP_EINVAL;
+    hipSetDevice(c->dev);
+    Staged &s = c->stg;
+    const FrameDesc *fr = (const FrameDesc *) (s.arena + s.o_frames);
+    const uint32_t *lists = (const uint32_t *) (s.arena + s.o_lists);
+    size_t nl = s.launches.size();
+    if (c->timing && c->ev.size() < 2 * nl) {
+        size_t old = c->ev.size();
+        c->ev.resize(2 * nl);
+        for (size_t i = old; i < c->ev.size(); i++) HIPCHK(hipEventCreate(&c->ev[i]));
+    }
+    for (size_t i = 0; i < nl; i++) {
+        const Launch &L = s.launches[i];
+        if (c->timing) HIPCHK(hipEventRecord(c->ev[2 * i], c->st));
+        int r = 0;
+        switch (L.kind) {
+        case K_MC:
+            r = vp9hip_launch_mc(c->hb, c->st, (int) L.n, (const McUnit *) (s.arena + s.o_mcs), fr);
+            break;
+        case K_RECON:
+            r = vp9hip_launch_recon(c->hb, c->st, (int) L.n, lists + L.off, (const SBRec *) (s.arena + s.o_sbs),
+                                    (const TxJob *) (s.arena + s.o_jobs), (const uint16_t *) (s.arena + s.o_lvls),
+                                    fr, s.arena + s.o_coefs);
+            break;
+        case K_LF:
+            r = vp9hip_launch_lf(c->hb, c->st, (int) L.n, lists + L.off, (const LFRec *) (s.arena + s.o_lfs), fr);
+            break;
+        }
+        if (r) return VP9HIP_EEXTERNAL;
+        if (c->timing) HIPCHK(hipEventRecord(c->ev[2 * i + 1], c->st));
+    }
+    return 0;
+}
+
+extern "C" int vp9hip_sync(vp9hip_ctx *c)
+{
+    if (!c) return VP9HIP_EINVAL;
+    hipSetDevice(c->dev);
+    HIPCHK(hipStreamSynchronize(c->st));
+    if (c->timing && c->stg.ready) {
+        for (int k = 0; k < K_N; k++) { c->kms[k] = 0; c->kcount[k] = 0; }
+        for (size_t i = 0; i < c->stg.launches.size() && 2 * i + 1 < c->ev.size(); i++) {
+            float ms = 0;
+            if (hipEventElapsedTime(&ms, c->ev[2 * i], c->ev[2 * i + 1]) == hipSuccess) {
+                c->kms[c->stg.launches[i].kind] += ms;
+                c->kcount[c->stg.launches[i].kind]++;
+            }
+        }
+    }
+    return 0;
+}
+
+extern "C" int vp9hip_submit_frame(vp9hip_ctx *c, const vp9h_frame *pkt, int out_buf, const int ref_buf[3])
+{
+    int r = stage(c, pkt, 1, &out_buf, ref_buf);
+    if (r < 0) return r;
+    return vp9hip_run_batch(c);
+}
+
+extern "C" int vp9hip_download_frame(vp9hip_ctx *c, int buf, uint8_t *const planes[3], const ptrdiff_t linesize[3])
+{
+    if (!c || buf < 0 || buf >= (int) c->bufs.size() || !planes) return VP9HIP_EINVAL;
+    hipSetDevice(c->dev);
+    HIPCHK(hipStreamSynchronize(c->st));
+    for (int p = 0; p < 3; p++) {
+        int pw = p ? (c->w + c->ss_h) >> c->ss_h : c->w, ph = p ? (c->h + c->ss_v) >> c->ss_v : c->h;
+        HIPCHK(hipMemcpy2DAsync(planes[p], linesize[p], c->bufs[buf] + c->plane_off[p],
+                                (size_t) c->pitch[p ? 1 : 0] * c->bypp, (size_t) pw * c->bypp, ph,
+                                hipMemcpyDeviceToHost, c->st));
+    }
+    HIPCHK(hipStreamSynchronize(c->st));
+    return 0;
+}
+
+extern "C" int vp9hip_upload_frame(vp9hip_ctx *c, int buf, const uint8_t *const planes[3], const ptrdiff_t linesize[3])
+{
+    if (!c || buf < 0 || buf >= (int) c->bufs.size() || !planes) return VP9HIP_EINVAL;
+    hipSetDevice(c->dev);
+    for (int p = 0; p < 3; p++) {
+        int pw = p ? (c->w + c->ss_h) >> c->ss_h : c->w, ph = p ? (c->h + c->ss_v) >> c->ss_v : c->h;
+        HIPCHK(hipMemcpy2DAsync(c->bufs[buf] + c->plane_off[p], (size_t) c->pitch[p ? 1 : 0] * c->bypp,
+                                planes[p], linesize[p], (size_t) pw * c->bypp, ph, hipMemcpyHostToDevice, c->st));
+    }
+    HIPCHK(hipStreamSynchronize(c->st));
+    return 0;
+}
+
+extern "C" int vp9hip_flush(vp9hip_ctx *c)
+{
+    if (!c) return VP9HIP_EINVAL;
+    hipSetDevice(c->dev);
+    HIPCHK(hipStreamSynchronize(c->st));
+    c->stg.ready = false;
+    return 0;
+}
+
+extern "C" int vp9hip_last_timing(vp9hip_ctx *c, const char **names, double *ms, int *launches, int cap)
+{
+    if (!c) return VP9HIP_EINVAL;
+    int n = 0;
+    for (int k = 0; k < K_N && n < cap; k++, n++) {
+        if (names) names[n] = kname[k];
+        if (ms) ms[n] = c->kms[k];
+        if (launches) launches[n] = c->kcount[k];
+    }
+    return n;
+}
+
+// Algorithmic bytes of the staged batch per kernel class (same order as timing).
+extern "C" int vp9hip_alg_bytes(vp9hip_ctx *c, double *bytes, int cap)
+{
+    if (!c) return VP9HIP_EINVAL;
+    int n = 0;
+    for (int k = 0; k < K_N && n < cap; k++, n++) bytes[n] = c->stg.alg_bytes[k];
+    return n;
+}
+
+extern "C" int vp9hip_set_timing(vp9hip_ctx *c, int on)
+{
+    if (!c) return VP9HIP_EINVAL;
+    c->timing = on != 0;
+    return 0;
+}
+
+extern "C" int vp9hip_abi_version(void) { return VP9HIP_ABI_VERSION; }

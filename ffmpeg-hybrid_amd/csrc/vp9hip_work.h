@@ -1,0 +1,72 @@
+/*
+ * Device work lists built by the host runtime from pass-1 packets and consumed by
+ * the gfx950 kernels. Internal to libvp9hip (not part of the C-ABI).
+ *
+ * HBM layout per frame buffer: three planes, luma padded to 64 x 64 superblocks,
+ * chroma to the matching subsampled size; pitch in pixels. Pixels are uint8_t
+ * (bpp 8) or uint16_t (bpp 10/12). Nothing outside the 8-aligned frame area is
+ * ever read (intra edge rules vp9recon.c:103,192; LF masks vp9block.c:1442; MC
+ * clamps to the visible size, videodsp_template.c:27-105), so the padding needs no
+ * border extension.
+ */
+#ifndef VP9HIP_WORK_H
+#define VP9HIP_WORK_H
+#include <stdint.h>
+
+/* Per-frame descriptor (device array, indexed by SBRec.frame / McUnit.frame). */
+typedef struct FrameDesc {
+    uint64_t plane[3];        /* device pointers                                      */
+    uint64_t ref[3][3];       /* [LAST/GOLDEN/ALTREF][plane] device pointers           */
+    int32_t  pitch[2];        /* luma / chroma pitch (pixels)                         */
+    int32_t  w8[2], h8[2];    /* 8-aligned plane size (cols*8 >> ss)                  */
+    int32_t  refw[3][2], refh[3][2]; /* visible ref plane sizes (MC clamp)           */
+    int32_t  sb_cols, sb_rows;
+    int32_t  bd;              /* bit depth                                            */
+    int32_t  sharp;           /* LF sharpness                                         */
+} FrameDesc;
+
+/* One transform block job (16 bytes). */
+typedef struct TxJob {
+    uint8_t  ptx;             /* plane | tx << 2   (tx 0..3, 4 = lossless WHT)          */
+    uint8_t  txtp;            /* DCT_DCT 0, DCT_ADST 1, ADST_DCT 2, ADST_ADST 3          */
+    uint8_t  mode;            /* intra mode before edge substitution; 0xff = residual only */
+    uint8_t  flags;           /* bit0 have_right (vp9recon.c:47)                        */
+    uint8_t  x4, y4;          /* position inside the SB plane, 4-pixel units            */
+    uint16_t eob;
+    uint32_t coef;            /* element offset of the scan-order coefficients          */
+    uint32_t pad;
+} TxJob;
+
+/* One superblock of reconstruction work. */
+typedef struct SBRec {
+    uint32_t frame;
+    uint16_t sbx, sby;
+    uint32_t job0;            /* first TxJob (jobs sorted by dependency level)          */
+    uint32_t lvl0;            /* first entry of the level-start table (nlev + 1 u16)    */
+    uint16_t nlev;
+    uint16_t tile_x0;         /* tile column start, 8x8 units (vp9.c:1244-1250)         */
+    uint32_t flags;           /* bit0: load SB interior first (inter frame)             */
+} SBRec;
+
+/* Loop-filter data of one SB: VP9Filter (vp9dec.h:83-87) + position. */
+typedef struct LFRec {
+    uint32_t frame;
+    uint16_t sbx, sby;
+    uint8_t  level[64];
+    uint8_t  mask[2][2][8][4];
+} LFRec;
+
+/* One motion-compensated rectangle of one plane (<= 64 x 64). */
+typedef struct McUnit {
+    uint32_t frame;
+    uint16_t x, y;            /* plane pixel position                                   */
+    uint8_t  w, h;
+    uint8_t  plane;
+    uint8_t  filter;          /* 0..2 8-tap smooth/regular/sharp, 3 bilinear            */
+    uint8_t  nref;            /* 1 or 2 (compound: second ref averaged)                 */
+    uint8_t  ref[2];
+    uint8_t  pad;
+    int16_t  d16[2][2];       /* [ref][x,y] offset in 1/16 plane pel                    */
+} McUnit;
+
+#endif

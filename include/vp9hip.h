@@ -1,0 +1,183 @@
+/*
+ * vp9hip.h — C-ABI boundary of the MI355X VP9 hybrid decoder.
+ *
+ * The host (entropy decode, header parse) produces one "pass-1 frame packet" per
+ * frame; the device (gfx950 HIP kernels) runs the whole per-superblock pixel path:
+ * inverse transforms, intra prediction, motion compensation and the loop filter.
+ *
+ * The packet mirrors the reference decoder's 2-pass buffers
+ * (/root/reference/libavcodec/vp9.c:335-353, vp9block.c:1352-1362): one VP9Block
+ * per coded block (vp9dec.h:89-97), the per-tx-block eobs and the dequantized
+ * coefficients in scan order (vp9block.c:805-923), plus the frame-header values the
+ * pixel path reads (vp9.c:669-791: LF level / sharpness / lossless / tiling).
+ *
+ * Entry points replace, one for one, the hooks the reference's hybrid path calls:
+ *   vp9hip_open/close      <- ff_vp9_webgpu_init/uninit      (vp9_webgpu.h:370-375; vp9.c:1905-1917, 1281-1292)
+ *   vp9hip_submit_frame    <- ff_vp9_webgpu_begin/end_frame  (vp9_webgpu.h:470-480; vp9.c:1319-1324, 1840-1845)
+ *                             and FFHWAccel.start_frame/decode_slice/end_frame (hwaccel_internal.h:34-166; vp9.c:1694-1713)
+ *   vp9hip_download_frame  <- the end_frame readback         (vp9_webgpu.c:2995-3056)
+ *   vp9hip_flush           <- FFHWAccel.flush                (hwaccel_internal.h:165; vp9.c:1865-1883)
+ * Errors are FFmpeg-style negative AVERROR codes (VP9HIP_E*).
+ * A context is not thread-safe; use one host thread per context.
+ */
+#ifndef VP9HIP_H
+#define VP9HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VP9HIP_ABI_VERSION 1
+
+/* FFmpeg AVERROR values used by the boundary (libavutil/error.h). */
+#define VP9HIP_EINVAL       (-22)          /* AVERROR(EINVAL)   */
+#define VP9HIP_ENOMEM       (-12)          /* AVERROR(ENOMEM)   */
+#define VP9HIP_ENOSYS       (-38)          /* AVERROR(ENOSYS)   */
+#define VP9HIP_EINVALIDDATA (-1094995529)  /* AVERROR_INVALIDDATA */
+#define VP9HIP_EEXTERNAL    (-542398533)   /* AVERROR_EXTERNAL (HIP runtime failure) */
+
+/* enum BlockSize (vp9shared.h:86-101) */
+enum { VP9H_BS_64x64, VP9H_BS_64x32, VP9H_BS_32x64, VP9H_BS_32x32, VP9H_BS_32x16,
+       VP9H_BS_16x32, VP9H_BS_16x16, VP9H_BS_16x8, VP9H_BS_8x16, VP9H_BS_8x8,
+       VP9H_BS_8x4, VP9H_BS_4x8, VP9H_BS_4x4, VP9H_N_BS };
+/* enum TxfmMode (vp9.h:27-35) */
+enum { VP9H_TX_4X4, VP9H_TX_8X8, VP9H_TX_16X16, VP9H_TX_32X32 };
+/* enum FilterMode (vp9.h:64-71) */
+enum { VP9H_FILTER_SMOOTH, VP9H_FILTER_REGULAR, VP9H_FILTER_SHARP, VP9H_FILTER_BILINEAR };
+/* intra modes 0..9 (vp9.h:45-62), inter modes (vp9shared.h:43-48) */
+enum { VP9H_NEARESTMV = 10, VP9H_NEARMV = 11, VP9H_ZEROMV = 12, VP9H_NEWMV = 13 };
+
+/* One coded block in decode order (VP9Block, vp9dec.h:89-97). 52 bytes. */
+typedef struct vp9h_block {
+    uint16_t row, col;      /* position in 8x8 units (vp9block.c:1276-1279)            */
+    uint8_t  bs;            /* VP9H_BS_*                                               */
+    uint8_t  tx, uvtx;      /* luma / chroma transform size (vp9block.c:1291)         */
+    uint8_t  skip;          /* final skip flag, after vp9block.c:1310-1314             */
+    uint8_t  intra, comp;   /* intra block; compound prediction                       */
+    uint8_t  seg_id;        /* segment (selects LF level)                              */
+    uint8_t  filter;        /* VP9H_FILTER_* for inter blocks                          */
+    uint8_t  mode[4];       /* luma mode per 4x4 sub-block (intra 0..9, inter 10..13)  */
+    uint8_t  uvmode;        /* chroma intra mode                                       */
+    uint8_t  ref[2];        /* 0=LAST 1=GOLDEN 2=ALTREF                                */
+    uint8_t  pad0;
+    int16_t  mv[4][2][2];   /* [b_idx][ref][x,y] in 1/8 luma pel                       */
+} vp9h_block;
+
+/*
+ * One frame of pass-1 output.
+ * eobs: for every block with skip == 0, one uint16 per transform block that lies
+ *   inside the frame (end_x/end_y clipping of vp9recon.c:243-244), in the reference's
+ *   loop order: luma tx blocks row-major, then U, then V (vp9recon.c:269-357).
+ *   Blocks with skip == 1 store nothing.
+ * coefs: for every tx block with eob > 0, `eob` dequantized coefficients in scan
+ *   order (the values decode_coeffs_b_generic stores at coef[scan[i]],
+ *   vp9block.c:905-917): int16 for bpp == 8, int32 for bpp > 8.
+ */
+typedef struct vp9h_frame {
+    int32_t  width, height;        /* visible size                                    */
+    uint8_t  bpp;                  /* 8, 10, 12                                       */
+    uint8_t  ss_h, ss_v;           /* chroma subsampling                              */
+    uint8_t  keyframe, intraonly;
+    uint8_t  lossless;             /* WHT 4x4 everywhere (vp9.c:704-705)              */
+    uint8_t  filter_level;         /* s->s.h.filter.level                             */
+    uint8_t  sharpness;            /* s->s.h.filter.sharpness                         */
+    uint8_t  log2_tile_cols;
+    uint8_t  log2_tile_rows;
+    uint8_t  pad0[2];
+    uint8_t  lflvl[8][4][2];       /* segmentation.feat[s].lflvl (vp9.c:767-791)       */
+    int32_t  ref_w[3], ref_h[3];   /* visible size of LAST/GOLDEN/ALTREF (MC clamp)   */
+    uint32_t nblocks;
+    uint32_t neobs;
+    uint64_t ncoefs;
+    const vp9h_block *blocks;
+    const uint16_t   *eobs;
+    const void       *coefs;
+} vp9h_frame;
+
+/* ---- device context ---------------------------------------------------- */
+typedef struct vp9hip_ctx vp9hip_ctx;
+
+/* Open a context on HIP device `device`. Returns 0 or a negative error. */
+int  vp9hip_open(int device, vp9hip_ctx **out);
+void vp9hip_close(vp9hip_ctx *ctx);
+
+/* Allocate `nbufs` device frame buffers of w x h (padded to 64 internally). */
+int  vp9hip_configure(vp9hip_ctx *ctx, int width, int height, int bpp, int ss_h, int ss_v,
+                      int nbufs);
+
+/*
+ * Queue one frame: `out_buf` receives the reconstruction, ref_buf[0..2] are the
+ * device buffers holding LAST/GOLDEN/ALTREF (ignored for intra frames).
+ * The packet is copied (staged) before return; execution is asynchronous.
+ */
+int  vp9hip_submit_frame(vp9hip_ctx *ctx, const vp9h_frame *pkt, int out_buf,
+                         const int ref_buf[3]);
+
+/*
+ * Batched form for independent (intra-only) frames: stage all packets into device
+ * memory once (vp9hip_stage_batch), then run the pixel path over all of them with
+ * frames interleaved in each wavefront launch (vp9hip_run_batch). run may be
+ * repeated; the inputs stay resident in HBM.
+ */
+int  vp9hip_stage_batch(vp9hip_ctx *ctx, const vp9h_frame *pkts, int n, const int *out_bufs);
+int  vp9hip_run_batch(vp9hip_ctx *ctx);
+
+/* Wait for all queued work. */
+int  vp9hip_sync(vp9hip_ctx *ctx);
+
+/* Copy device buffer `buf` into host planes (linesize in bytes). Synchronous. */
+int  vp9hip_download_frame(vp9hip_ctx *ctx, int buf, uint8_t *const planes[3],
+                           const ptrdiff_t linesize[3]);
+/* Upload host planes into device buffer `buf` (test hook for reference frames). */
+int  vp9hip_upload_frame(vp9hip_ctx *ctx, int buf, const uint8_t *const planes[3],
+                         const ptrdiff_t linesize[3]);
+
+/* Drop queued work and staged batches (FFHWAccel.flush). */
+int  vp9hip_flush(vp9hip_ctx *ctx);
+
+/*
+ * Per-kernel timing of the last run (HIP events on the execution stream):
+ * names[i] / ms[i] / launches[i] for up to `cap` kernel classes. Returns count.
+ */
+int  vp9hip_last_timing(vp9hip_ctx *ctx, const char **names, double *ms, int *launches, int cap);
+
+/* ---- synthetic pass-1 generator (test / bench input) -------------------- */
+/*
+ * Generates a pseudo-random but structurally legal frame packet. Defaults follow the
+ * stream settings of SURVEY.md §8(d): random partitions (P(split) 0.5 at 64/32, 0.3
+ * at 16, 10 % sub-8x8), uniform intra modes, skip 0.2, TX_MODE_SELECT, per tx block
+ * eob uniform in [1, min(n,64)] with geometric(0.6) magnitudes and random sign,
+ * base_q_idx 60 (no deltas), filter level 36, sharpness 0, LF deltas at the libvpx
+ * defaults. inter != 0: LAST-ref inter frame (50 % NEWMV, MVs uniform in +-64 px,
+ * 10 % intra blocks). The packet owns heap arrays; release with vp9hip_synth_free.
+ */
+typedef struct vp9h_synth_params {
+    int32_t  width, height;
+    int32_t  bpp;              /* 8 / 10 / 12                                   */
+    int32_t  ss_h, ss_v;       /* 1,1 = 4:2:0                                   */
+    int32_t  log2_tile_cols;
+    int32_t  inter;            /* 0 = keyframe; 1 = inter frame on LAST         */
+    int32_t  compound;         /* inter: allow compound LAST+ALTREF blocks      */
+    int32_t  q_idx;            /* base_q_idx (0 + lossless -> WHT)              */
+    int32_t  lossless;
+    int32_t  filter_level;
+    int32_t  sharpness;
+    int32_t  bilinear;         /* frame-level bilinear MC filter                */
+    int32_t  coef_stress;      /* 1: coefficients uniform over the full range   */
+    float    p_zero_eob;       /* chance that a tx block codes eob 0            */
+    float    p_skip;           /* default 0.2                                   */
+    uint64_t seed;
+} vp9h_synth_params;
+
+/* Fill p with the §8(d) defaults for a w x h bpp stream. */
+void vp9hip_synth_defaults(vp9h_synth_params *p, int width, int height, int bpp);
+int  vp9hip_synth_frame(vp9h_frame *out, const vp9h_synth_params *p);
+void vp9hip_synth_free(vp9h_frame *f);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VP9HIP_H */

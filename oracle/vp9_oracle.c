@@ -1,0 +1,891 @@
+/*
+ * ORACLE — test infrastructure only (see vp9_oracle.h). Scalar restatement of the
+ * reference libavcodec VP9 reconstruction:
+ *   check_intra_mode / intra_recon        vp9recon.c:37-364
+ *   mc_{luma,chroma}_unscaled, inter_pred vp9recon.c:376-467, vp9_mc_template.c:30-464
+ *   inter_recon                           vp9recon.c:655-764
+ *   mask_edges + LF level                 vp9block.c:1142-1262, 1438-1452
+ *   filter_plane_cols/rows, loopfilter_sb vp9lpf.c:31-230
+ *   SB-row loop with intra_pred_data      vp9.c:1351-1435
+ * It walks the pass-1 packet exactly as the reference's pass-2 (decode_sb_mem,
+ * vp9.c:1195-1242) walks its VP9Block array.
+ */
+#include <stdlib.h>
+#include <string.h>
+
+#include "vp9_oracle.h"
+#include "../ffmpeg-hybrid_amd/csrc/vp9_tables.h"
+
+#define OB 8
+#include "vp9o_dsp_tmpl.h"
+#undef OB
+#define OB 16
+#include "vp9o_dsp_tmpl.h"
+#undef OB
+
+#define MIN(a, b) ((a) < (b) ? (a) : (b))
+#define MAX(a, b) ((a) > (b) ? (a) : (b))
+
+enum { DCT_DCT, DCT_ADST, ADST_DCT, ADST_ADST };
+enum { VERT_PRED, HOR_PRED, DC_PRED, DIAG_DOWN_LEFT_PRED, DIAG_DOWN_RIGHT_PRED, VERT_RIGHT_PRED,
+       HOR_DOWN_PRED, VERT_LEFT_PRED, HOR_UP_PRED, TM_VP8_PRED, LEFT_DC_PRED, TOP_DC_PRED,
+       DC_128_PRED, DC_127_PRED, DC_129_PRED };
+
+/* ff_vp9_intra_txfm_type (vp9data.c:437-452) */
+static const uint8_t intra_txfm_type[14] = {
+    ADST_DCT, DCT_ADST, DCT_DCT, DCT_DCT, ADST_ADST, ADST_DCT, DCT_ADST, ADST_DCT, DCT_ADST,
+    ADST_ADST, DCT_DCT, DCT_DCT, DCT_DCT, DCT_DCT };
+
+const int16_t *vp9o_scan(int tx, int txtp)
+{
+    /* ff_vp9_scans (vp9data.c:600-618) */
+    static const int16_t *const scans[5][4] = {
+        { vp9t_scan_default_4x4, vp9t_scan_col_4x4, vp9t_scan_row_4x4, vp9t_scan_default_4x4 },
+        { vp9t_scan_default_8x8, vp9t_scan_col_8x8, vp9t_scan_row_8x8, vp9t_scan_default_8x8 },
+        { vp9t_scan_default_16x16, vp9t_scan_col_16x16, vp9t_scan_row_16x16, vp9t_scan_default_16x16 },
+        { vp9t_scan_default_32x32, vp9t_scan_default_32x32, vp9t_scan_default_32x32, vp9t_scan_default_32x32 },
+        { vp9t_scan_default_4x4, vp9t_scan_default_4x4, vp9t_scan_default_4x4, vp9t_scan_default_4x4 },
+    };
+    return scans[tx][txtp];
+}
+
+/* ---- public DSP entry points (unit tests) ------------------------------ */
+void vp9o_itxfm_add(int bpp, void *dst, ptrdiff_t stride, void *coef, int eob, int tx, int txtp)
+{
+    if (bpp == 8) itxfm_add_8(dst, stride, coef, eob, tx, txtp, 8);
+    else          itxfm_add_16(dst, stride, coef, eob, tx, txtp, bpp);
+}
+void vp9o_intra_pred(int bpp, void *dst, ptrdiff_t stride, const void *left, const void *top,
+                     int tx, int mode)
+{
+    if (bpp == 8) ipred_8(dst, stride, left, top, tx, mode, 8);
+    else          ipred_16(dst, stride, left, top, tx, mode, bpp);
+}
+/* kind 0: loop_filter_8[wd1][dir]; 1: loop_filter_16[dir]; 2: mix2[wd1][wd2][dir] */
+void vp9o_loop_filter(int bpp, void *dst, ptrdiff_t stride, int kind, int wd1, int wd2, int dir,
+                      int E, int I, int H)
+{
+    if (bpp == 8) {
+        if (kind == 0) lf8_8(dst, stride, wd1, dir, E, I, H, 8);
+        else if (kind == 1) lf16_8(dst, stride, dir, E, I, H, 8);
+        else lfmix2_8(dst, stride, wd1, wd2, dir, E, I, H, 8);
+    } else {
+        if (kind == 0) lf8_16(dst, stride, wd1, dir, E, I, H, bpp);
+        else if (kind == 1) lf16_16(dst, stride, dir, E, I, H, bpp);
+        else lfmix2_16(dst, stride, wd1, wd2, dir, E, I, H, bpp);
+    }
+}
+void vp9o_mc(int bpp, void *dst, ptrdiff_t ds, const void *src, ptrdiff_t ss, int w, int h,
+             int mx, int my, int filter, int avg)
+{
+    if (bpp == 8) mc_8(dst, ds, src, ss, w, h, mx, my, filter, avg, 8);
+    else          mc_16(dst, ds, src, ss, w, h, mx, my, filter, avg, bpp);
+}
+
+/* ---- frame context ----------------------------------------------------- */
+typedef struct VP9Filter {
+    uint8_t level[8 * 8];
+    uint8_t mask[2][2][8][4];   /* [y/uv][col/row][row][16,8,4,inner4] (vp9dec.h:83-87) */
+} VP9Filter;
+
+typedef struct OCtx {
+    const vp9h_frame *f;
+    int bd, bypp;                /* bit depth, bytes per pixel */
+    int ss_h, ss_v;
+    int cols, rows, sb_cols, sb_rows;
+    uint8_t lim_lut[64], mblim_lut[64];
+    VP9Filter *lflvl;
+    uint8_t *plane[3];           /* byte pointers */
+    ptrdiff_t ls[3];             /* bytes */
+    const vp9o_planes *refs;
+    uint8_t *ipd[3];             /* intra_pred_data (vp9.c:285-291) */
+    uint8_t *ipd_base[3];
+    int tile_col_start;          /* 8x8 units */
+    int tile_col_end;
+    /* the current block's eobs and coefficients */
+    int n_eob[3];
+    const uint16_t *eob[3];
+    const uint8_t *coef[3];      /* per plane cursor into the coefficient stream */
+    uint8_t edge[160 * 160 * 2];
+} OCtx;
+
+static inline int rd_px(const uint8_t *p, int i, int bypp) { return bypp == 1 ? p[i] : ((const uint16_t *) p)[i]; }
+static inline void wr_px(uint8_t *p, int i, int v, int bypp) { if (bypp == 1) p[i] = v; else ((uint16_t *) p)[i] = v; }
+
+static void itx(OCtx *c, uint8_t *dst, ptrdiff_t ls_bytes, void *blk, int eob, int tx, int txtp)
+{
+    if (c->bypp == 1) itxfm_add_8(dst, ls_bytes, blk, eob, tx, txtp, 8);
+    else itxfm_add_16((uint16_t *) dst, ls_bytes / 2, blk, eob, tx, txtp, c->bd);
+}
+
+/* Expand the next `eob` scan-order coefficients of plane p into a dense block. */
+static void load_coefs(OCtx *c, int p, void *blk, int eob, int tx, int txtp)
+{
+    const int16_t *scan = vp9o_scan(tx, txtp);
+    int sz = 4 << (tx & 3), i;
+    if (c->bypp == 1) {
+        int16_t *b = blk; const int16_t *s = (const int16_t *) c->coef[p];
+        memset(b, 0, sz * sz * 2);
+        for (i = 0; i < eob; i++) b[scan[i]] = s[i];
+        c->coef[p] += eob * 2;
+    } else {
+        int32_t *b = blk; const int32_t *s = (const int32_t *) c->coef[p];
+        memset(b, 0, sz * sz * 4);
+        for (i = 0; i < eob; i++) b[scan[i]] = s[i];
+        c->coef[p] += eob * 4;
+    }
+}
+
+/* check_intra_mode, vp9recon.c:37-221. Byte-addressed like the reference. */
+static int check_intra_mode(OCtx *c, int mode, uint8_t **a, uint8_t *dst_edge, ptrdiff_t stride_edge,
+                            uint8_t *dst_inner, ptrdiff_t stride_inner, uint8_t *l, int col, int x,
+                            int w, int row, int y, int tx, int p, int ss_h, int ss_v)
+{
+    static const uint8_t mode_conv[10][2][2] = {
+        [VERT_PRED]            = { { DC_127_PRED, VERT_PRED }, { DC_127_PRED, VERT_PRED } },
+        [HOR_PRED]             = { { DC_129_PRED, DC_129_PRED }, { HOR_PRED, HOR_PRED } },
+        [DC_PRED]              = { { DC_128_PRED, TOP_DC_PRED }, { LEFT_DC_PRED, DC_PRED } },
+        [DIAG_DOWN_LEFT_PRED]  = { { DC_127_PRED, DIAG_DOWN_LEFT_PRED }, { DC_127_PRED, DIAG_DOWN_LEFT_PRED } },
+        [DIAG_DOWN_RIGHT_PRED] = { { DIAG_DOWN_RIGHT_PRED, DIAG_DOWN_RIGHT_PRED }, { DIAG_DOWN_RIGHT_PRED, DIAG_DOWN_RIGHT_PRED } },
+        [VERT_RIGHT_PRED]      = { { VERT_RIGHT_PRED, VERT_RIGHT_PRED }, { VERT_RIGHT_PRED, VERT_RIGHT_PRED } },
+        [HOR_DOWN_PRED]        = { { HOR_DOWN_PRED, HOR_DOWN_PRED }, { HOR_DOWN_PRED, HOR_DOWN_PRED } },
+        [VERT_LEFT_PRED]       = { { DC_127_PRED, VERT_LEFT_PRED }, { DC_127_PRED, VERT_LEFT_PRED } },
+        [HOR_UP_PRED]          = { { DC_129_PRED, DC_129_PRED }, { HOR_UP_PRED, HOR_UP_PRED } },
+        [TM_VP8_PRED]          = { { DC_129_PRED, VERT_PRED }, { HOR_PRED, TM_VP8_PRED } },
+    };
+    /* needs_left, needs_top, needs_topleft, needs_topright, invert_left */
+    static const uint8_t edges[15][5] = {
+        [VERT_PRED] = { 0, 1, 0, 0, 0 }, [HOR_PRED] = { 1, 0, 0, 0, 0 }, [DC_PRED] = { 1, 1, 0, 0, 0 },
+        [DIAG_DOWN_LEFT_PRED] = { 0, 1, 0, 1, 0 }, [DIAG_DOWN_RIGHT_PRED] = { 1, 1, 1, 0, 0 },
+        [VERT_RIGHT_PRED] = { 1, 1, 1, 0, 0 }, [HOR_DOWN_PRED] = { 1, 1, 1, 0, 0 },
+        [VERT_LEFT_PRED] = { 0, 1, 0, 1, 0 }, [HOR_UP_PRED] = { 1, 0, 0, 0, 1 },
+        [TM_VP8_PRED] = { 1, 1, 1, 0, 0 }, [LEFT_DC_PRED] = { 1, 0, 0, 0, 0 },
+        [TOP_DC_PRED] = { 0, 1, 0, 0, 0 }, [DC_128_PRED] = { 0 }, [DC_127_PRED] = { 0 }, [DC_129_PRED] = { 0 },
+    };
+    const int bypp = c->bypp, bd = c->bd;
+    int have_top = row > 0 || y > 0;
+    int have_left = col > c->tile_col_start || x > 0;
+    int have_right = x < w - 1;
+    int i;
+
+    mode = mode_conv[mode][have_left][have_top];
+    if (edges[mode][1]) {
+        uint8_t *top = NULL, *topleft = NULL;
+        int n_px_need = 4 << tx, n_px_have = (((c->cols - col) << !ss_h) - x) * 4;
+        int n_px_need_tr = 0;
+
+        if (tx == 0 && edges[mode][3] && have_right)
+            n_px_need_tr = 4;
+        if (have_top) {
+            top = !(row & 7) && !y ? c->ipd[p] + (col * (8 >> ss_h) + x * 4) * bypp
+                : y == 0 ? &dst_edge[-stride_edge] : &dst_inner[-stride_inner];
+            if (have_left)
+                topleft = !(row & 7) && !y ? c->ipd[p] + (col * (8 >> ss_h) + x * 4) * bypp
+                    : y == 0 || x == 0 ? &dst_edge[-stride_edge] : &dst_inner[-stride_inner];
+        }
+        if (have_top && (!edges[mode][2] || (have_left && top == topleft)) &&
+            (tx != 0 || !edges[mode][3] || have_right) && n_px_need + n_px_need_tr <= n_px_have) {
+            *a = top;
+        } else {
+            if (have_top) {
+                if (n_px_need <= n_px_have) {
+                    memcpy(*a, top, n_px_need * bypp);
+                } else {
+                    memcpy(*a, top, n_px_have * bypp);
+                    for (i = n_px_have; i < n_px_need; i++)
+                        wr_px(*a, i, rd_px(*a, n_px_have - 1, bypp), bypp);
+                }
+            } else {
+                for (i = 0; i < n_px_need; i++) wr_px(*a, i, (128 << (bd - 8)) - 1, bypp);
+            }
+            if (edges[mode][2]) {
+                if (have_left && have_top)
+                    wr_px(*a, -1, rd_px(topleft, -1, bypp), bypp);
+                else
+                    wr_px(*a, -1, (128 << (bd - 8)) + (have_top ? +1 : -1), bypp);
+            }
+            if (tx == 0 && edges[mode][3]) {
+                if (have_top && have_right && n_px_need + n_px_need_tr <= n_px_have)
+                    memcpy(&(*a)[4 * bypp], &top[4 * bypp], 4 * bypp);
+                else
+                    for (i = 4; i < 8; i++) wr_px(*a, i, rd_px(*a, 3, bypp), bypp);
+            }
+        }
+    }
+    if (edges[mode][0]) {
+        if (have_left) {
+            int n_px_need = 4 << tx, n_px_have = (((c->rows - row) << !ss_v) - y) * 4;
+            uint8_t *dst = x == 0 ? dst_edge : dst_inner;
+            ptrdiff_t stride = x == 0 ? stride_edge : stride_inner;
+            if (edges[mode][4]) {
+                if (n_px_need <= n_px_have) {
+                    for (i = 0; i < n_px_need; i++) wr_px(l, i, rd_px(&dst[i * stride], -1, bypp), bypp);
+                } else {
+                    for (i = 0; i < n_px_have; i++) wr_px(l, i, rd_px(&dst[i * stride], -1, bypp), bypp);
+                    for (i = n_px_have; i < n_px_need; i++) wr_px(l, i, rd_px(l, n_px_have - 1, bypp), bypp);
+                }
+            } else {
+                if (n_px_need <= n_px_have) {
+                    for (i = 0; i < n_px_need; i++)
+                        wr_px(l, n_px_need - 1 - i, rd_px(&dst[i * stride], -1, bypp), bypp);
+                } else {
+                    for (i = 0; i < n_px_have; i++)
+                        wr_px(l, n_px_need - 1 - i, rd_px(&dst[i * stride], -1, bypp), bypp);
+                    for (i = 0; i < n_px_need - n_px_have; i++)
+                        wr_px(l, i, rd_px(l, n_px_need - n_px_have, bypp), bypp);
+                }
+            }
+        } else {
+            for (i = 0; i < (4 << tx); i++) wr_px(l, i, (128 << (bd - 8)) + 1, bypp);
+        }
+    }
+    return mode;
+}
+
+static void ipred(OCtx *c, uint8_t *dst, ptrdiff_t ls, const uint8_t *l, const uint8_t *a, int tx, int mode)
+{
+    if (c->bypp == 1) ipred_8(dst, ls, l, a, tx, mode, 8);
+    else ipred_16((uint16_t *) dst, ls / 2, (const uint16_t *) l, (const uint16_t *) a, tx, mode, c->bd);
+}
+
+/* intra_recon, vp9recon.c:235-364 (dst_edge == dst_inner: buffers are padded, so the
+ * emulated-overhang path of vp9block.c:1365-1436 never triggers). */
+static void intra_recon(OCtx *c, const vp9h_block *b)
+{
+    const int bypp = c->bypp;
+    int row = b->row, col = b->col;
+    int w4 = vp9t_bwh[1][b->bs][0] << 1, step1d = 1 << b->tx, n;
+    int h4 = vp9t_bwh[1][b->bs][1] << 1, x, y, step = 1 << (b->tx * 2);
+    int end_x = MIN(2 * (c->cols - col), w4);
+    int end_y = MIN(2 * (c->rows - row), h4);
+    int tx = 4 * c->f->lossless + b->tx, uvtx = b->uvtx + 4 * c->f->lossless;
+    int uvstep1d = 1 << b->uvtx, p, k = 0;
+    ptrdiff_t ls = c->ls[0];
+    uint8_t *dst = c->plane[0] + row * 8 * ls + col * 8 * bypp;
+    uint8_t a_buf[64 + 160] __attribute__((aligned(16))), l[128] __attribute__((aligned(16)));
+    int32_t blk[32 * 32];
+
+    for (n = 0, y = 0; y < end_y; y += step1d) {
+        uint8_t *ptr = dst;
+        for (x = 0; x < end_x; x += step1d, ptr += 4 * step1d * bypp, n += step) {
+            int mode = b->mode[b->bs > VP9H_BS_8x8 && b->tx == 0 ? y * 2 + x : 0];
+            uint8_t *a = &a_buf[64];
+            int txtp = intra_txfm_type[mode];
+            int eob = b->skip ? 0 : c->eob[0][k++];
+            mode = check_intra_mode(c, mode, &a, ptr, ls, ptr, ls, l, col, x, w4, row, y, b->tx, 0, 0, 0);
+            ipred(c, ptr, ls, l, a, b->tx, mode);
+            if (eob) {
+                load_coefs(c, 0, blk, eob, tx, txtp);
+                itx(c, ptr, ls, blk, eob, tx, txtp);
+            }
+        }
+        dst += 4 * step1d * ls;
+    }
+
+    w4 >>= c->ss_h; end_x >>= c->ss_h; end_y >>= c->ss_v;
+    step = 1 << (b->uvtx * 2);
+    ls = c->ls[1];
+    for (p = 0; p < 2; p++) {
+        k = 0;
+        dst = c->plane[1 + p] + row * (8 >> c->ss_v) * ls + col * (8 >> c->ss_h) * bypp;
+        for (n = 0, y = 0; y < end_y; y += uvstep1d) {
+            uint8_t *ptr = dst;
+            for (x = 0; x < end_x; x += uvstep1d, ptr += 4 * uvstep1d * bypp, n += step) {
+                int mode = b->uvmode;
+                uint8_t *a = &a_buf[64];
+                int eob = b->skip ? 0 : c->eob[1 + p][k++];
+                mode = check_intra_mode(c, mode, &a, ptr, ls, ptr, ls, l, col, x, w4, row, y,
+                                        b->uvtx, p + 1, c->ss_h, c->ss_v);
+                ipred(c, ptr, ls, l, a, b->uvtx, mode);
+                if (eob) {
+                    load_coefs(c, 1 + p, blk, eob, uvtx, DCT_DCT);
+                    itx(c, ptr, ls, blk, eob, uvtx, DCT_DCT);
+                }
+            }
+            dst += 4 * uvstep1d * ls;
+        }
+    }
+}
+
+/* ---- MC ------------------------------------------------------------------ */
+static void mcf(OCtx *c, uint8_t *dst, ptrdiff_t ds, const uint8_t *src, ptrdiff_t ss,
+                int bw, int bh, int mx, int my, int filter, int avg)
+{
+    if (c->bypp == 1) mc_8(dst, ds, src, ss, bw, bh, mx, my, filter, avg, 8);
+    else mc_16((uint16_t *) dst, ds / 2, (const uint16_t *) src, ss / 2, bw, bh, mx, my, filter, avg, c->bd);
+}
+
+static void emu(OCtx *c, uint8_t *buf, const uint8_t *src, ptrdiff_t sls, int bw, int bh, int sx, int sy,
+                int w, int h)
+{
+    if (c->bypp == 1) emu_edge_8(buf, src, 160, sls, bw, bh, sx, sy, w, h);
+    else emu_edge_16((uint16_t *) buf, (const uint16_t *) src, 160, sls / 2, bw, bh, sx, sy, w, h);
+}
+
+/* mc_luma_unscaled, vp9recon.c:376-414 (edge buffer stride: 160 pixels) */
+static void mc_luma(OCtx *c, uint8_t *dst, ptrdiff_t dst_stride, const uint8_t *ref, ptrdiff_t ref_stride,
+                    ptrdiff_t y, ptrdiff_t x, const int16_t *mv, int bw, int bh, int w, int h,
+                    int filter, int avg)
+{
+    const int bypp = c->bypp;
+    int mx = mv[0], my = mv[1];
+    y += my >> 3;
+    x += mx >> 3;
+    ref += y * ref_stride + x * bypp;
+    mx &= 7;
+    my &= 7;
+    if (x < !!mx * 3 || y < !!my * 3 || x + !!mx * 4 > w - bw || y + !!my * 5 > h - bh) {
+        emu(c, c->edge, ref - !!my * 3 * ref_stride - !!mx * 3 * bypp, ref_stride,
+            bw + !!mx * 7, bh + !!my * 7, x - !!mx * 3, y - !!my * 3, w, h);
+        ref = c->edge + (!!my * 3 * 160 + !!mx * 3) * bypp;
+        ref_stride = 160 * bypp;
+    }
+    mcf(c, dst, dst_stride, ref, ref_stride, bw, bh, mx << 1, my << 1, filter, avg);
+}
+
+/* mc_chroma_unscaled, vp9recon.c:416-467 */
+static void mc_chroma(OCtx *c, uint8_t *dst_u, uint8_t *dst_v, ptrdiff_t dst_stride,
+                      const uint8_t *ref_u, const uint8_t *ref_v, ptrdiff_t src_stride,
+                      ptrdiff_t y, ptrdiff_t x, const int16_t *mv, int bw, int bh, int w, int h,
+                      int filter, int avg)
+{
+    const int bypp = c->bypp;
+    int mx = mv[0] * (1 << !c->ss_h), my = mv[1] * (1 << !c->ss_v);
+    y += my >> 4;
+    x += mx >> 4;
+    ref_u += y * src_stride + x * bypp;
+    ref_v += y * src_stride + x * bypp;
+    mx &= 15;
+    my &= 15;
+    if (x < !!mx * 3 || y < !!my * 3 || x + !!mx * 4 > w - bw || y + !!my * 5 > h - bh) {
+        emu(c, c->edge, ref_u - !!my * 3 * src_stride - !!mx * 3 * bypp, src_stride,
+            bw + !!mx * 7, bh + !!my * 7, x - !!mx * 3, y - !!my * 3, w, h);
+        mcf(c, dst_u, dst_stride, c->edge + (!!my * 3 * 160 + !!mx * 3) * bypp, 160 * bypp, bw, bh, mx, my, filter, avg);
+        emu(c, c->edge, ref_v - !!my * 3 * src_stride - !!mx * 3 * bypp, src_stride,
+            bw + !!mx * 7, bh + !!my * 7, x - !!mx * 3, y - !!my * 3, w, h);
+        mcf(c, dst_v, dst_stride, c->edge + (!!my * 3 * 160 + !!mx * 3) * bypp, 160 * bypp, bw, bh, mx, my, filter, avg);
+    } else {
+        mcf(c, dst_u, dst_stride, ref_u, src_stride, bw, bh, mx, my, filter, avg);
+        mcf(c, dst_v, dst_stride, ref_v, src_stride, bw, bh, mx, my, filter, avg);
+    }
+}
+
+static inline int rdiv(int a, int b) { return (a >= 0 ? a + (b >> 1) : a - (b >> 1)) / b; }  /* ROUNDED_DIV */
+
+static void mv_avg2(int16_t *o, const int16_t *a, const int16_t *b)
+{ o[0] = rdiv(a[0] + b[0], 2); o[1] = rdiv(a[1] + b[1], 2); }
+static void mv_avg4(int16_t *o, const int16_t *a, const int16_t *b, const int16_t *cc, const int16_t *d)
+{ o[0] = rdiv(a[0] + b[0] + cc[0] + d[0], 4); o[1] = rdiv(a[1] + b[1] + cc[1] + d[1], 4); }
+
+/* inter_pred, vp9_mc_template.c:30-464 (unscaled). i = 0 first ref (put), 1 second (avg). */
+static int inter_pred(OCtx *c, const vp9h_block *b)
+{
+    const int bypp = c->bypp, ss_h = c->ss_h, ss_v = c->ss_v;
+    int row = b->row, col = b->col, i;
+    ptrdiff_t ls_y = c->ls[0], ls_uv = c->ls[1];
+    uint8_t *dy = c->plane[0] + row * 8 * ls_y + col * 8 * bypp;
+    uint8_t *du = c->plane[1] + row * (8 >> ss_v) * ls_uv + col * (8 >> ss_h) * bypp;
+    uint8_t *dv = c->plane[2] + row * (8 >> ss_v) * ls_uv + col * (8 >> ss_h) * bypp;
+
+    for (i = 0; i < 1 + b->comp; i++) {
+        const vp9o_planes *r = &c->refs[b->ref[i]];
+        const uint8_t *ry = r->data[0], *ru = r->data[1], *rv = r->data[2];
+        ptrdiff_t rls = r->stride[0] * bypp, rls_uv = r->stride[1] * bypp;
+        int w1 = r->w, h1 = r->h, f = b->filter;
+        int16_t uvmv[2];
+        if (r->w != c->f->width || r->h != c->f->height)
+            return VP9HIP_ENOSYS;  /* scaled references: not restated in this round */
+
+        if (b->bs > VP9H_BS_8x8) {
+            if (b->bs == VP9H_BS_8x4) {
+                mc_luma(c, dy, ls_y, ry, rls, row << 3, col << 3, b->mv[0][i], 8, 4, w1, h1, f, i);
+                mc_luma(c, dy + 4 * ls_y, ls_y, ry, rls, (row << 3) + 4, col << 3, b->mv[2][i], 8, 4, w1, h1, f, i);
+                w1 = (w1 + ss_h) >> ss_h;
+                if (ss_v) {
+                    h1 = (h1 + 1) >> 1;
+                    mv_avg2(uvmv, b->mv[0][i], b->mv[2][i]);
+                    mc_chroma(c, du, dv, ls_uv, ru, rv, rls_uv, row << 2, col << (3 - ss_h), uvmv,
+                              8 >> ss_h, 4, w1, h1, f, i);
+                } else {
+                    mc_chroma(c, du, dv, ls_uv, ru, rv, rls_uv, row << 3, col << (3 - ss_h), b->mv[0][i],
+                              8 >> ss_h, 4, w1, h1, f, i);
+                    /* BUG compat: libvpx uses the wrong block index for 4:2:2 (vp9_mc_template.c:107-114) */
+                    if (ss_h == 0) { uvmv[0] = b->mv[2][i][0]; uvmv[1] = b->mv[2][i][1]; }
+                    else mv_avg2(uvmv, b->mv[0][i], b->mv[2][i]);
+                    mc_chroma(c, du + 4 * ls_uv, dv + 4 * ls_uv, ls_uv, ru, rv, rls_uv, (row << 3) + 4,
+                              col << (3 - ss_h), uvmv, 8 >> ss_h, 4, w1, h1, f, i);
+                }
+            } else if (b->bs == VP9H_BS_4x8) {
+                mc_luma(c, dy, ls_y, ry, rls, row << 3, col << 3, b->mv[0][i], 4, 8, w1, h1, f, i);
+                mc_luma(c, dy + 4 * bypp, ls_y, ry, rls, row << 3, (col << 3) + 4, b->mv[1][i], 4, 8, w1, h1, f, i);
+                h1 = (h1 + ss_v) >> ss_v;
+                if (ss_h) {
+                    w1 = (w1 + 1) >> 1;
+                    mv_avg2(uvmv, b->mv[0][i], b->mv[1][i]);
+                    mc_chroma(c, du, dv, ls_uv, ru, rv, rls_uv, row << (3 - ss_v), col << 2, uvmv,
+                              4, 8 >> ss_v, w1, h1, f, i);
+                } else {
+                    mc_chroma(c, du, dv, ls_uv, ru, rv, rls_uv, row << (3 - ss_v), col << 3, b->mv[0][i],
+                              4, 8 >> ss_v, w1, h1, f, i);
+                    mc_chroma(c, du + 4 * bypp, dv + 4 * bypp, ls_uv, ru, rv, rls_uv, row << (3 - ss_v),
+                              (col << 3) + 4, b->mv[1][i], 4, 8 >> ss_v, w1, h1, f, i);
+                }
+            } else {
+                mc_luma(c, dy, ls_y, ry, rls, row << 3, col << 3, b->mv[0][i], 4, 4, w1, h1, f, i);
+                mc_luma(c, dy + 4 * bypp, ls_y, ry, rls, row << 3, (col << 3) + 4, b->mv[1][i], 4, 4, w1, h1, f, i);
+                mc_luma(c, dy + 4 * ls_y, ls_y, ry, rls, (row << 3) + 4, col << 3, b->mv[2][i], 4, 4, w1, h1, f, i);
+                mc_luma(c, dy + 4 * ls_y + 4 * bypp, ls_y, ry, rls, (row << 3) + 4, (col << 3) + 4,
+                        b->mv[3][i], 4, 4, w1, h1, f, i);
+                if (ss_v) {
+                    h1 = (h1 + 1) >> 1;
+                    if (ss_h) {
+                        w1 = (w1 + 1) >> 1;
+                        mv_avg4(uvmv, b->mv[0][i], b->mv[1][i], b->mv[2][i], b->mv[3][i]);
+                        mc_chroma(c, du, dv, ls_uv, ru, rv, rls_uv, row << 2, col << 2, uvmv, 4, 4, w1, h1, f, i);
+                    } else {
+                        mv_avg2(uvmv, b->mv[0][i], b->mv[2][i]);
+                        mc_chroma(c, du, dv, ls_uv, ru, rv, rls_uv, row << 2, col << 3, uvmv, 4, 4, w1, h1, f, i);
+                        mv_avg2(uvmv, b->mv[1][i], b->mv[3][i]);
+                        mc_chroma(c, du + 4 * bypp, dv + 4 * bypp, ls_uv, ru, rv, rls_uv, row << 2,
+                                  (col << 3) + 4, uvmv, 4, 4, w1, h1, f, i);
+                    }
+                } else {
+                    if (ss_h) {
+                        w1 = (w1 + 1) >> 1;
+                        mv_avg2(uvmv, b->mv[0][i], b->mv[1][i]);
+                        mc_chroma(c, du, dv, ls_uv, ru, rv, rls_uv, row << 3, col << 2, uvmv, 4, 4, w1, h1, f, i);
+                        /* BUG compat (vp9_mc_template.c:296-305) */
+                        mv_avg2(uvmv, b->mv[1][i], b->mv[2][i]);
+                        mc_chroma(c, du + 4 * ls_uv, dv + 4 * ls_uv, ls_uv, ru, rv, rls_uv, (row << 3) + 4,
+                                  col << 2, uvmv, 4, 4, w1, h1, f, i);
+                    } else {
+                        mc_chroma(c, du, dv, ls_uv, ru, rv, rls_uv, row << 3, col << 3, b->mv[0][i], 4, 4, w1, h1, f, i);
+                        mc_chroma(c, du + 4 * bypp, dv + 4 * bypp, ls_uv, ru, rv, rls_uv, row << 3,
+                                  (col << 3) + 4, b->mv[1][i], 4, 4, w1, h1, f, i);
+                        mc_chroma(c, du + 4 * ls_uv, dv + 4 * ls_uv, ls_uv, ru, rv, rls_uv, (row << 3) + 4,
+                                  col << 3, b->mv[2][i], 4, 4, w1, h1, f, i);
+                        mc_chroma(c, du + 4 * ls_uv + 4 * bypp, dv + 4 * ls_uv + 4 * bypp, ls_uv, ru, rv,
+                                  rls_uv, (row << 3) + 4, (col << 3) + 4, b->mv[3][i], 4, 4, w1, h1, f, i);
+                    }
+                }
+            }
+        } else {
+            int bw = vp9t_bwh[0][b->bs][0] * 4, bh = vp9t_bwh[0][b->bs][1] * 4;
+            int uvbw = vp9t_bwh[ss_h][b->bs][0] * 4, uvbh = vp9t_bwh[ss_v][b->bs][1] * 4;
+            mc_luma(c, dy, ls_y, ry, rls, row << 3, col << 3, b->mv[0][i], bw, bh, w1, h1, f, i);
+            w1 = (w1 + ss_h) >> ss_h;
+            h1 = (h1 + ss_v) >> ss_v;
+            mc_chroma(c, du, dv, ls_uv, ru, rv, rls_uv, row << (3 - ss_v), col << (3 - ss_h), b->mv[0][i],
+                      uvbw, uvbh, w1, h1, f, i);
+        }
+    }
+    return 0;
+}
+
+/* inter_recon residual loop, vp9recon.c:707-763 */
+static void inter_residual(OCtx *c, const vp9h_block *b)
+{
+    const int bypp = c->bypp;
+    int row = b->row, col = b->col;
+    int w4 = vp9t_bwh[1][b->bs][0] << 1, step1d = 1 << b->tx, n;
+    int h4 = vp9t_bwh[1][b->bs][1] << 1, x, y, step = 1 << (b->tx * 2);
+    int end_x = MIN(2 * (c->cols - col), w4);
+    int end_y = MIN(2 * (c->rows - row), h4);
+    int tx = 4 * c->f->lossless + b->tx, uvtx = b->uvtx + 4 * c->f->lossless;
+    int uvstep1d = 1 << b->uvtx, p, k = 0;
+    ptrdiff_t ls = c->ls[0];
+    uint8_t *dst = c->plane[0] + row * 8 * ls + col * 8 * bypp;
+    int32_t blk[32 * 32];
+
+    for (n = 0, y = 0; y < end_y; y += step1d) {
+        uint8_t *ptr = dst;
+        for (x = 0; x < end_x; x += step1d, ptr += 4 * step1d * bypp, n += step) {
+            int eob = c->eob[0][k++];
+            if (eob) {
+                load_coefs(c, 0, blk, eob, tx, DCT_DCT);
+                itx(c, ptr, ls, blk, eob, tx, DCT_DCT);
+            }
+        }
+        dst += 4 * ls * step1d;
+    }
+    end_x >>= c->ss_h;
+    end_y >>= c->ss_v;
+    step = 1 << (b->uvtx * 2);
+    ls = c->ls[1];
+    for (p = 0; p < 2; p++) {
+        k = 0;
+        dst = c->plane[1 + p] + row * (8 >> c->ss_v) * ls + col * (8 >> c->ss_h) * bypp;
+        for (n = 0, y = 0; y < end_y; y += uvstep1d) {
+            uint8_t *ptr = dst;
+            for (x = 0; x < end_x; x += uvstep1d, ptr += 4 * uvstep1d * bypp, n += step) {
+                int eob = c->eob[1 + p][k++];
+                if (eob) {
+                    load_coefs(c, 1 + p, blk, eob, uvtx, DCT_DCT);
+                    itx(c, ptr, ls, blk, eob, uvtx, DCT_DCT);
+                }
+            }
+            dst += 4 * uvstep1d * ls;
+        }
+    }
+}
+
+/* ---- loop-filter masks (vp9block.c:1142-1262) ------------------------------ */
+static void mask_edges(uint8_t (*mask)[8][4], int ss_h, int ss_v, int row_and_7, int col_and_7,
+                       int w, int h, int col_end, int row_end, int tx, int skip_inter)
+{
+    static const unsigned wide_filter_col_mask[2] = { 0x11, 0x01 };
+    static const unsigned wide_filter_row_mask[2] = { 0x03, 0x07 };
+
+    if (tx == 0 && (ss_v | ss_h)) {
+        if (h == ss_v) {
+            if (row_and_7 & 1) return;
+            if (!row_end) h += 1;
+        }
+        if (w == ss_h) {
+            if (col_and_7 & 1) return;
+            if (!col_end) w += 1;
+        }
+    }
+    if (tx == 0 && !skip_inter) {
+        int t = 1 << col_and_7, m_col = (t << w) - t, y;
+        int m_row_8 = m_col & wide_filter_col_mask[ss_h], m_row_4 = m_col - m_row_8;
+        for (y = row_and_7; y < h + row_and_7; y++) {
+            int col_mask_id = 2 - !(y & wide_filter_row_mask[ss_v]);
+            mask[0][y][1] |= m_row_8;
+            mask[0][y][2] |= m_row_4;
+            if ((ss_h & ss_v) && (col_end & 1) && (y & 1))
+                mask[1][y][col_mask_id] |= (t << (w - 1)) - t;
+            else
+                mask[1][y][col_mask_id] |= m_col;
+            if (!ss_h)
+                mask[0][y][3] |= m_col;
+            if (!ss_v) {
+                if (ss_h && (col_end & 1))
+                    mask[1][y][3] |= (t << (w - 1)) - t;
+                else
+                    mask[1][y][3] |= m_col;
+            }
+        }
+    } else {
+        int y, t = 1 << col_and_7, m_col = (t << w) - t;
+        if (!skip_inter) {
+            int mask_id = (tx == 1);
+            int l2 = tx + ss_h - 1, step1d;
+            static const unsigned masks[4] = { 0xff, 0x55, 0x11, 0x01 };
+            int m_row = m_col & masks[l2];
+            if (ss_h && tx > 1 && (w ^ (w - 1)) == 1) {
+                int m_row_16 = ((t << (w - 1)) - t) & masks[l2];
+                int m_row_8 = m_row - m_row_16;
+                for (y = row_and_7; y < h + row_and_7; y++) {
+                    mask[0][y][0] |= m_row_16;
+                    mask[0][y][1] |= m_row_8;
+                }
+            } else {
+                for (y = row_and_7; y < h + row_and_7; y++)
+                    mask[0][y][mask_id] |= m_row;
+            }
+            l2 = tx + ss_v - 1;
+            step1d = 1 << l2;
+            if (ss_v && tx > 1 && (h ^ (h - 1)) == 1) {
+                for (y = row_and_7; y < h + row_and_7 - 1; y += step1d)
+                    mask[1][y][0] |= m_col;
+                if (y - row_and_7 == h - 1)
+                    mask[1][y][1] |= m_col;
+            } else {
+                for (y = row_and_7; y < h + row_and_7; y += step1d)
+                    mask[1][y][mask_id] |= m_col;
+            }
+        } else if (tx != 0) {
+            int mask_id;
+            mask_id = (tx == 1) || (h == ss_v);
+            mask[1][row_and_7][mask_id] |= m_col;
+            mask_id = (tx == 1) || (w == ss_h);
+            for (y = row_and_7; y < h + row_and_7; y++)
+                mask[0][y][mask_id] |= t;
+        } else {
+            int t8 = t & wide_filter_col_mask[ss_h], t4 = t - t8;
+            for (y = row_and_7; y < h + row_and_7; y++) {
+                mask[0][y][2] |= t4;
+                mask[0][y][1] |= t8;
+            }
+            mask[1][row_and_7][2 - !(row_and_7 & wide_filter_row_mask[ss_v])] |= m_col;
+        }
+    }
+}
+
+static void lf8(OCtx *c, uint8_t *p, ptrdiff_t ls, int wd, int dir, int E, int I, int H)
+{
+    if (c->bypp == 1) lf8_8(p, ls, wd, dir, E, I, H, 8);
+    else lf8_16((uint16_t *) p, ls / 2, wd, dir, E, I, H, c->bd);
+}
+static void lf16(OCtx *c, uint8_t *p, ptrdiff_t ls, int dir, int E, int I, int H)
+{
+    if (c->bypp == 1) lf16_8(p, ls, dir, E, I, H, 8);
+    else lf16_16((uint16_t *) p, ls / 2, dir, E, I, H, c->bd);
+}
+static void lfmix(OCtx *c, uint8_t *p, ptrdiff_t ls, int w1, int w2, int dir, int E, int I, int H)
+{
+    if (c->bypp == 1) lfmix2_8(p, ls, w1, w2, dir, E, I, H, 8);
+    else lfmix2_16((uint16_t *) p, ls / 2, w1, w2, dir, E, I, H, c->bd);
+}
+
+/* filter_plane_cols, vp9lpf.c:31-104 */
+static void filter_plane_cols(OCtx *c, int col, int ss_h, int ss_v, uint8_t *lvl, uint8_t (*mask)[4],
+                              uint8_t *dst, ptrdiff_t ls)
+{
+    int y, x, bypp = c->bypp;
+    for (y = 0; y < 8; y += 2 << ss_v, dst += 16 * ls, lvl += 16 << ss_v) {
+        uint8_t *ptr = dst, *l = lvl, *hmask1 = mask[y], *hmask2 = mask[y + 1 + ss_v];
+        unsigned hm1 = hmask1[0] | hmask1[1] | hmask1[2], hm13 = hmask1[3];
+        unsigned hm2 = hmask2[1] | hmask2[2], hm23 = hmask2[3];
+        unsigned hm = hm1 | hm2 | hm13 | hm23;
+        for (x = 1; hm & ~(x - 1); x <<= 1, ptr += 8 * bypp >> ss_h) {
+            if (col || x > 1) {
+                if (hm1 & x) {
+                    int L = *l, H = L >> 4;
+                    int E = c->mblim_lut[L], I = c->lim_lut[L];
+                    if (hmask1[0] & x) {
+                        if (hmask2[0] & x) lf16(c, ptr, ls, 0, E, I, H);
+                        else lf8(c, ptr, ls, 2, 0, E, I, H);
+                    } else if (hm2 & x) {
+                        L = l[8 << ss_v];
+                        H |= (L >> 4) << 8;
+                        E |= c->mblim_lut[L] << 8;
+                        I |= c->lim_lut[L] << 8;
+                        lfmix(c, ptr, ls, !!(hmask1[1] & x), !!(hmask2[1] & x), 0, E, I, H);
+                    } else {
+                        lf8(c, ptr, ls, !!(hmask1[1] & x), 0, E, I, H);
+                    }
+                } else if (hm2 & x) {
+                    int L = l[8 << ss_v], H = L >> 4;
+                    int E = c->mblim_lut[L], I = c->lim_lut[L];
+                    lf8(c, ptr + 8 * ls, ls, !!(hmask2[1] & x), 0, E, I, H);
+                }
+            }
+            if (ss_h) {
+                if (x & 0xAA) l += 2;
+            } else {
+                if (hm13 & x) {
+                    int L = *l, H = L >> 4;
+                    int E = c->mblim_lut[L], I = c->lim_lut[L];
+                    if (hm23 & x) {
+                        L = l[8 << ss_v];
+                        H |= (L >> 4) << 8;
+                        E |= c->mblim_lut[L] << 8;
+                        I |= c->lim_lut[L] << 8;
+                        lfmix(c, ptr + 4 * bypp, ls, 0, 0, 0, E, I, H);
+                    } else {
+                        lf8(c, ptr + 4 * bypp, ls, 0, 0, E, I, H);
+                    }
+                } else if (hm23 & x) {
+                    int L = l[8 << ss_v], H = L >> 4;
+                    int E = c->mblim_lut[L], I = c->lim_lut[L];
+                    lf8(c, ptr + 8 * ls + 4 * bypp, ls, 0, 0, E, I, H);
+                }
+                l++;
+            }
+        }
+    }
+}
+
+/* filter_plane_rows, vp9lpf.c:106-181 */
+static void filter_plane_rows(OCtx *c, int row, int ss_h, int ss_v, uint8_t *lvl, uint8_t (*mask)[4],
+                              uint8_t *dst, ptrdiff_t ls)
+{
+    int y, x, bypp = c->bypp;
+    for (y = 0; y < 8; y++, dst += 8 * ls >> ss_v) {
+        uint8_t *ptr = dst, *l = lvl, *vmask = mask[y];
+        unsigned vm = vmask[0] | vmask[1] | vmask[2], vm3 = vmask[3];
+        for (x = 1; vm & ~(x - 1); x <<= (2 << ss_h), ptr += 16 * bypp, l += 2 << ss_h) {
+            if (row || y) {
+                if (vm & x) {
+                    int L = *l, H = L >> 4;
+                    int E = c->mblim_lut[L], I = c->lim_lut[L];
+                    if (vmask[0] & x) {
+                        if (vmask[0] & (x << (1 + ss_h))) lf16(c, ptr, ls, 1, E, I, H);
+                        else lf8(c, ptr, ls, 2, 1, E, I, H);
+                    } else if (vm & (x << (1 + ss_h))) {
+                        L = l[1 + ss_h];
+                        H |= (L >> 4) << 8;
+                        E |= c->mblim_lut[L] << 8;
+                        I |= c->lim_lut[L] << 8;
+                        lfmix(c, ptr, ls, !!(vmask[1] & x), !!(vmask[1] & (x << (1 + ss_h))), 1, E, I, H);
+                    } else {
+                        lf8(c, ptr, ls, !!(vmask[1] & x), 1, E, I, H);
+                    }
+                } else if (vm & (x << (1 + ss_h))) {
+                    int L = l[1 + ss_h], H = L >> 4;
+                    int E = c->mblim_lut[L], I = c->lim_lut[L];
+                    lf8(c, ptr + 8 * bypp, ls, !!(vmask[1] & (x << (1 + ss_h))), 1, E, I, H);
+                }
+            }
+            if (!ss_v) {
+                if (vm3 & x) {
+                    int L = *l, H = L >> 4;
+                    int E = c->mblim_lut[L], I = c->lim_lut[L];
+                    if (vm3 & (x << (1 + ss_h))) {
+                        L = l[1 + ss_h];
+                        H |= (L >> 4) << 8;
+                        E |= c->mblim_lut[L] << 8;
+                        I |= c->lim_lut[L] << 8;
+                        lfmix(c, ptr + ls * 4, ls, 0, 0, 1, E, I, H);
+                    } else {
+                        lf8(c, ptr + ls * 4, ls, 0, 1, E, I, H);
+                    }
+                } else if (vm3 & (x << (1 + ss_h))) {
+                    int L = l[1 + ss_h], H = L >> 4;
+                    int E = c->mblim_lut[L], I = c->lim_lut[L];
+                    lf8(c, ptr + ls * 4 + 8 * bypp, ls, 0, 1, E, I, H);
+                }
+            }
+        }
+        if (ss_v) {
+            if (y & 1) lvl += 16;
+        } else {
+            lvl += 8;
+        }
+    }
+}
+
+/* ff_vp9_loopfilter_sb, vp9lpf.c:183-230 */
+static void loopfilter_sb(OCtx *c, VP9Filter *lflvl, int row, int col)
+{
+    const int bypp = c->bypp;
+    uint8_t *dst = c->plane[0] + row * 8 * c->ls[0] + col * 8 * bypp;
+    uint8_t (*uv_masks)[8][4] = lflvl->mask[c->ss_h | c->ss_v];
+    int p;
+    filter_plane_cols(c, col, 0, 0, lflvl->level, lflvl->mask[0][0], dst, c->ls[0]);
+    filter_plane_rows(c, row, 0, 0, lflvl->level, lflvl->mask[0][1], dst, c->ls[0]);
+    for (p = 0; p < 2; p++) {
+        dst = c->plane[1 + p] + row * (8 >> c->ss_v) * c->ls[1] + col * (8 >> c->ss_h) * bypp;
+        filter_plane_cols(c, col, c->ss_h, c->ss_v, lflvl->level, uv_masks[0], dst, c->ls[1]);
+        filter_plane_rows(c, row, c->ss_h, c->ss_v, lflvl->level, uv_masks[1], dst, c->ls[1]);
+    }
+}
+
+/* count the tx blocks (inside the frame) of one plane of a block */
+static int n_txb(OCtx *c, const vp9h_block *b, int uv)
+{
+    int w4 = vp9t_bwh[1][b->bs][0] << 1, h4 = vp9t_bwh[1][b->bs][1] << 1;
+    int end_x = MIN(2 * (c->cols - b->col), w4), end_y = MIN(2 * (c->rows - b->row), h4);
+    int s = 1 << (uv ? b->uvtx : b->tx);
+    if (uv) { end_x >>= c->ss_h; end_y >>= c->ss_v; }
+    return ((end_x + s - 1) / s) * ((end_y + s - 1) / s);
+}
+
+int vp9o_decode_frame(const vp9h_frame *f, vp9o_planes *cur, const vp9o_planes *refs)
+{
+    OCtx *c = calloc(1, sizeof(*c));
+    const uint16_t *eobp = f->eobs;
+    const uint8_t *coefp = f->coefs;
+    int i, p, ret = 0, sharp = f->sharpness;
+    uint32_t bi;
+    if (!c) return VP9HIP_ENOMEM;
+    c->f = f;
+    c->bd = f->bpp;
+    c->bypp = f->bpp > 8 ? 2 : 1;
+    c->ss_h = f->ss_h;
+    c->ss_v = f->ss_v;
+    c->cols = (f->width + 7) >> 3;
+    c->rows = (f->height + 7) >> 3;
+    c->sb_cols = (f->width + 63) >> 6;
+    c->sb_rows = (f->height + 63) >> 6;
+    c->refs = refs;
+    for (p = 0; p < 3; p++) {
+        c->plane[p] = cur->data[p];
+        c->ls[p] = cur->stride[p] * c->bypp;
+    }
+    /* lim/mblim LUT, vp9.c:673-686 */
+    for (i = 1; i <= 63; i++) {
+        int limit = i;
+        if (sharp > 0) {
+            limit >>= (sharp + 3) >> 2;
+            limit = MIN(limit, 9 - sharp);
+        }
+        limit = MAX(limit, 1);
+        c->lim_lut[i] = limit;
+        c->mblim_lut[i] = 2 * (i + 2) + limit;
+    }
+    c->lflvl = calloc(c->sb_cols, sizeof(VP9Filter));
+    for (p = 0; p < 3; p++) c->ipd_base[p] = calloc(c->sb_cols * 64 * 2 + 64, 1);
+    if (!c->lflvl || !c->ipd_base[0] || !c->ipd_base[1] || !c->ipd_base[2]) { ret = VP9HIP_ENOMEM; goto end; }
+    for (p = 0; p < 3; p++) c->ipd[p] = c->ipd_base[p] + 32;
+
+    {
+        int prev_sb = -1;
+        for (bi = 0; bi < f->nblocks; bi++) {
+            const vp9h_block *b = &f->blocks[bi];
+            int sbr = b->row >> 3, sbc = b->col >> 3;
+            VP9Filter *lflvl = &c->lflvl[sbc];
+            int lvl, ti, log2 = f->log2_tile_cols;
+
+            if (sbr * c->sb_cols + sbc != prev_sb) {
+                /* new superblock: reset masks (vp9.c:1381-1383); tile col bounds (vp9.c:1244-1250) */
+                memset(lflvl->mask, 0, sizeof(lflvl->mask));
+                prev_sb = sbr * c->sb_cols + sbc;
+                for (ti = 0; ti < (1 << log2); ti++) {
+                    int s0 = MIN((ti * c->sb_cols) >> log2, c->sb_cols);
+                    int s1 = MIN(((ti + 1) * c->sb_cols) >> log2, c->sb_cols);
+                    if (sbc >= s0 && sbc < s1) { c->tile_col_start = s0 << 3; c->tile_col_end = s1 << 3; }
+                }
+            }
+            /* gather this block's eobs + coefficient cursors */
+            for (p = 0; p < 3; p++) {
+                c->n_eob[p] = b->skip ? 0 : n_txb(c, b, p > 0);
+                c->eob[p] = eobp;
+                eobp += c->n_eob[p];
+            }
+            if ((uint64_t)(eobp - f->eobs) > f->neobs) { ret = VP9HIP_EINVALIDDATA; goto end; }
+            for (p = 0; p < 3; p++) {
+                c->coef[p] = coefp;
+                for (i = 0; i < c->n_eob[p]; i++) coefp += c->eob[p][i] * (c->bypp == 1 ? 2 : 4);
+            }
+
+            if (b->intra) {
+                intra_recon(c, b);
+            } else {
+                if (!refs) { ret = VP9HIP_EINVAL; goto end; }
+                if ((ret = inter_pred(c, b)) < 0) goto end;
+                if (!b->skip) inter_residual(c, b);
+            }
+
+            /* LF level + masks, vp9block.c:1438-1452 */
+            if (f->filter_level &&
+                (lvl = f->lflvl[b->seg_id][b->intra ? 0 : b->ref[0] + 1][b->mode[3] != VP9H_ZEROMV]) > 0) {
+                int w4 = vp9t_bwh[1][b->bs][0], h4 = vp9t_bwh[1][b->bs][1];
+                int x_end = MIN(c->cols - b->col, w4), y_end = MIN(c->rows - b->row, h4);
+                int skip_inter = !b->intra && b->skip, col7 = b->col & 7, row7 = b->row & 7, yy, xx;
+                for (yy = 0; yy < h4; yy++)
+                    for (xx = 0; xx < w4; xx++) lflvl->level[(row7 + yy) * 8 + col7 + xx] = lvl;
+                mask_edges(lflvl->mask[0], 0, 0, row7, col7, x_end, y_end, 0, 0, b->tx, skip_inter);
+                if (c->ss_h || c->ss_v)
+                    mask_edges(lflvl->mask[1], c->ss_h, c->ss_v, row7, col7, x_end, y_end,
+                               c->cols & 1 && b->col + w4 >= c->cols ? c->cols & 7 : 0,
+                               c->rows & 1 && b->row + h4 >= c->rows ? c->rows & 7 : 0,
+                               b->uvtx, skip_inter);
+            }
+
+            /* end of an SB row (all tile columns): vp9.c:1404-1429 */
+            if (bi + 1 == f->nblocks || (f->blocks[bi + 1].row >> 3) != sbr) {
+                int row = sbr << 3, col;
+                if (row + 8 < c->rows) {
+                    memcpy(c->ipd[0], c->plane[0] + (row * 8 + 63) * c->ls[0], 8 * c->cols * c->bypp);
+                    memcpy(c->ipd[1], c->plane[1] + ((row * 8 >> c->ss_v) + (64 >> c->ss_v) - 1) * c->ls[1],
+                           8 * c->cols * c->bypp >> c->ss_h);
+                    memcpy(c->ipd[2], c->plane[2] + ((row * 8 >> c->ss_v) + (64 >> c->ss_v) - 1) * c->ls[1],
+                           8 * c->cols * c->bypp >> c->ss_h);
+                }
+                if (f->filter_level)
+                    for (col = 0; col < c->cols; col += 8)
+                        loopfilter_sb(c, &c->lflvl[col >> 3], row, col);
+            }
+        }
+    }
+    if ((uint64_t)(coefp - (const uint8_t *) f->coefs) != f->ncoefs * (c->bypp == 1 ? 2 : 4))
+        ret = VP9HIP_EINVALIDDATA;
+end:
+    for (p = 0; p < 3; p++) free(c->ipd_base[p]);
+    free(c->lflvl);
+    free(c);
+    return ret;
+}
