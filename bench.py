@@ -1,0 +1,157 @@
+#!/usr/bin/env python3
+"""Benchmark: decoded frames/s of the VP9 pixel path on MI355X (BASELINE.json metric).
+
+Workload (config C3 of BASELINE.md): 3840x2160 VP9 Profile-0 8-bit, 4 tile columns,
+all keyframes, 120 frames per stream, synthetic pass-1 packets with the SURVEY.md
+§8(d) stream statistics (seed 0x56503900 + config index 2 + rank).
+
+One step = reconstruct + loop-filter the whole 120-frame stream on the GPU with all
+inputs (pass-1 packets -> device work lists + coefficients) already resident in HBM.
+Multi-GPU: one process per GPU; frames are independent (keyframes reset all state,
+vp9.c:565,882-892), so every rank decodes its own stream with no data-path
+collective (weak scaling); the barrier and the max-over-ranks timing reduction use
+torch.distributed (gloo, control plane only).
+
+Prints one JSON line (rank 0) with the driver's fields plus "roofline" (dominant
+kernel, algorithmic bytes / HIP-event kernel time vs the 8 TB/s HBM peak) and
+"cpu_baseline" (the scalar C oracle on a bounded sample of the same frames).
+"""
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+W, H, BPP, LOG2_TILE_COLS = 3840, 2160, 8, 2
+CONFIG_INDEX = 2               # C3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--frames", type=int, default=120)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+
+    v = importlib.import_module("ffmpeg-hybrid_amd")
+    seed0 = 0x56503900 + CONFIG_INDEX
+    t0 = time.time()
+    frames = [v.SynthFrame(v.synth_params(W, H, BPP, seed=seed0 + rank * 100003 + i, log2_tile_cols=LOG2_TILE_COLS))
+              for i in range(args.frames)]
+    t_gen = time.time() - t0
+
+    dev = v.Device(local_rank)
+    dev.configure(W, H, BPP, nbufs=args.frames)
+    t0 = time.time()
+    dev.stage_batch(frames, list(range(args.frames)))
+    t_stage = time.time() - t0
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    dev.set_timing(True)
+    for _ in range(args.warmup):
+        dev.run_batch()
+    dev.sync()
+
+    barrier()
+    dev.sync()
+    ksum = {}
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        dev.run_batch()
+        dev.sync()          # per-step sync also collects the per-launch HIP-event times
+        for k, (ms, n) in dev.timing().items():
+            a = ksum.setdefault(k, [0.0, 0])
+            a[0] += ms
+            a[1] += n
+    dev.sync()
+    barrier()
+    elapsed = time.perf_counter() - t0
+
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    alg = dev.alg_bytes()           # per step, per kernel class: [mc, recon, lf]
+    names = ["k_mc", "k_recon", "k_lf"]
+    total_frames = args.frames * args.steps * world
+    fps = total_frames / elapsed
+    ms_per_step = elapsed * 1000.0 / args.steps
+
+    # dominant kernel (largest device time)
+    dom = max(names, key=lambda k: ksum.get(k, [0.0, 0])[0])
+    kms, kn = ksum[dom]
+    kidx = names.index(dom)
+    launches_per_step = kn / args.steps
+    bytes_per_launch = alg[kidx] / launches_per_step if launches_per_step else 0.0
+    avg_launch_s = (kms / 1000.0) / kn if kn else float("nan")
+    achieved = bytes_per_launch / avg_launch_s / 1e9 if kn else 0.0
+    kernel_ms_per_frame = sum(x[0] for x in ksum.values()) / (args.frames * args.steps)
+    frame_bytes = sum(alg) / args.frames
+    roofline = {
+        "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+        "kernel": dom, "launches_per_step": int(launches_per_step),
+        "alg_bytes_per_launch": round(bytes_per_launch),
+        "avg_launch_us": round(avg_launch_s * 1e6, 2),
+        "all_kernels_frac": round(frame_bytes / (kernel_ms_per_frame / 1000.0) / 1e9 / HBM_PEAK_GBS, 5),
+        "kernel_ms": {k: round(ksum[k][0] / args.steps, 3) for k in ksum},
+    }
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle  # CPU baseline leg only: the scalar C restatement, timed
+        out = v.alloc_planes(W, H, BPP)
+        n = 0
+        t0 = time.perf_counter()
+        while n < len(frames) and (time.perf_counter() - t0 < args.cpu_seconds or n < 2):
+            oracle.decode_frame(frames[n].pkt, out)
+            n += 1
+        dt = time.perf_counter() - t0
+        cpu = {"value": round(n / dt, 3), "unit": "frames/s", "cores": 1, "kind": "port",
+               "sample": "%d of the 120 C3 frames, scalar C oracle, reconstruction + loop filter from the same "
+                         "pass-1 packets (host entropy decode excluded), 1 thread" % n}
+
+    out = {
+        "metric": "decoded frames/sec (bit-exact) 4K VP9 Profile-0 @ 1/2/4/8 MI355X; % HBM roofline",
+        "value": round(fps, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+        "config": {"workload": "C3: 3840x2160 VP9 Profile-0 8-bit, 4 tile columns, all keyframes, "
+                               "%d frames per GPU per step, pass-1 packets resident in HBM" % args.frames,
+                   "global_batch": args.frames * world, "frames_per_gpu": args.frames,
+                   "parallelism": "frame-sharded x%d (independent keyframes, no collective)" % world,
+                   "host_gen_s": round(t_gen, 2), "host_stage_s": round(t_stage, 2)},
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    dev.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

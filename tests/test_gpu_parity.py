@@ -88,7 +88,7 @@ def test_inter_parity(v9, orc, gpu, w, h, bpp, kw):
 
 def test_batch_interleaved_keyframes(v9, orc, gpu):
     """Independent keyframes decoded in one batch (frames interleaved per wavefront launch)."""
-    w, h, n = 384, 200, 5
+    w, h, n = 512, 200, 5
     frames = [v9.SynthFrame(v9.synth_params(w, h, 8, seed=100 + i, log2_tile_cols=i % 2)) for i in range(n)]
     gpu.configure(w, h, 8, nbufs=n)
     gpu.stage_batch(frames, list(range(n)))
