@@ -1,0 +1,99 @@
+"""CPU: the C-ABI library, the synthetic pass-1 generator and oracle regression fixtures."""
+import ctypes
+import json
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_library_exports_every_declared_symbol(v9):
+    hdr = open(os.path.join(ROOT, "include", "vp9hip.h")).read()
+    declared = sorted(set(re.findall(r"\b(vp9hip_\w+)\s*\(", hdr)))
+    assert declared, "no entry points found in include/vp9hip.h"
+    L = v9.lib()
+    for sym in declared:
+        assert hasattr(L, sym), sym
+    nm = subprocess.run(["nm", "-D", "--defined-only", v9.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (vp9hip_\w+)", nm))
+    assert set(declared) <= exported
+    assert set(v9.ABI_SYMBOLS) <= exported
+
+
+def test_struct_layouts_match_header(v9):
+    # vp9h_block is 52 bytes (include/vp9hip.h); the Python mirror must agree
+    assert ctypes.sizeof(v9.Block) == 52
+    assert ctypes.sizeof(v9.SynthParams) == 72
+
+
+def test_no_device_is_an_error_not_a_fallback(v9):
+    """Without a GPU the product path fails loudly (no CPU fallback)."""
+    try:
+        import torch
+        if torch.cuda.is_available():
+            pytest.skip("GPU present")
+    except ImportError:
+        pass
+    with pytest.raises(v9.Vp9HipError):
+        v9.Device(0)
+
+
+def _coverage(pkt, w, h):
+    cols, rows = (w + 7) >> 3, (h + 7) >> 3
+    cov = np.zeros((rows, cols), np.int32)
+    bwh = [(8, 8), (8, 4), (4, 8), (4, 4), (4, 2), (2, 4), (2, 2), (2, 1), (1, 2), (1, 1), (1, 1), (1, 1), (1, 1)]
+    for i in range(pkt.nblocks):
+        b = pkt.blocks[i]
+        bw, bh = bwh[b.bs]
+        cov[b.row:min(b.row + bh, rows), b.col:min(b.col + bw, cols)] += 1
+        # blocks never straddle a superblock (decode_sb, vp9.c:1115-1193)
+        assert b.row // 8 == (b.row + bh - 1) // 8 and b.col // 8 == (b.col + bw - 1) // 8
+    return cov
+
+
+@pytest.mark.parametrize("w,h,kw", [(352, 288, {}), (200, 130, {}), (66, 66, {}),
+                                    (512, 256, {"log2_tile_cols": 1}), (3840, 64, {"log2_tile_cols": 2})])
+def test_synth_partition_covers_frame_once(v9, w, h, kw):
+    f = v9.SynthFrame(v9.synth_params(w, h, 8, seed=5, **kw))
+    cov = _coverage(f.pkt, w, h)
+    assert (cov == 1).all()
+
+
+def test_synth_deterministic_and_seeded(v9):
+    a = v9.SynthFrame(v9.synth_params(352, 288, 8, seed=9))
+    b = v9.SynthFrame(v9.synth_params(352, 288, 8, seed=9))
+    c = v9.SynthFrame(v9.synth_params(352, 288, 8, seed=10))
+    raw = lambda f: (ctypes.string_at(f.pkt.blocks, 52 * f.pkt.nblocks),
+                     ctypes.string_at(f.pkt.coefs, f.nbytes_coefs))
+    assert raw(a) == raw(b)
+    assert raw(a) != raw(c)
+
+
+def test_synth_rejects_illegal_tiling(v9):
+    # 384 px -> 6 SB columns: only log2_tile_cols 0 is legal (vp9.c:800-810)
+    with pytest.raises(v9.Vp9HipError):
+        v9.SynthFrame(v9.synth_params(384, 64, 8, log2_tile_cols=1))
+
+
+def test_synth_statistics_follow_survey(v9):
+    """§8(d): skip 0.2, eob uniform in [1, min(n, 64)], q_idx 60 dequantization."""
+    f = v9.SynthFrame(v9.synth_params(1920, 1080, 8, seed=3))
+    bl = f.blocks()
+    skip = np.mean([b.skip for b in bl])
+    assert 0.15 < skip < 0.25
+    eobs = np.ctypeslib.as_array(f.pkt.eobs, (f.pkt.neobs,))
+    assert eobs.min() >= 1 and eobs.max() <= 64
+
+
+def test_oracle_regression_framemd5(v9, orc):
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(ROOT, "tests", "golden", "make_golden.py"))
+    mg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mg)
+    want = json.load(open(os.path.join(ROOT, "tests", "golden", "oracle_framemd5.json")))
+    got = mg.compute()
+    assert got == want
