@@ -352,15 +352,13 @@ DEV void iwht4(int32_t *io, int pass)
     io[0] = (int32_t) t0; io[1] = (int32_t) t1; io[2] = (int32_t) t2; io[3] = (int32_t) t3;
 }
 
-// One 1-D inverse transform of length 4<<tx on `v` (kind: 0 dct, 1 adst).
-template <class M> DEV void tx1d(typename M::T *v, int tx, int adst)
+// One 1-D inverse transform of compile-time length N (adst: 0 dct, 1 adst).
+template <int N, class M> DEV void tx1n(typename M::T *v, int adst)
 {
-    switch (tx) {
-    case 0: if (adst) iadst4<M>(v); else idct4<M>(v); break;
-    case 1: if (adst) iadst8<M>(v); else idct8<M>(v); break;
-    case 2: if (adst) iadst16<M>(v); else idct16<M>(v); break;
-    default: idct32<M>(v); break;
-    }
+    if (N == 4) { if (adst) iadst4<M>(v); else idct4<M>(v); }
+    else if (N == 8) { if (adst) iadst8<M>(v); else idct8<M>(v); }
+    else if (N == 16) { if (adst) iadst16<M>(v); else idct16<M>(v); }
+    else idct32<M>(v);
 }
 
 // ------------------------------------------------------------ intra predict
@@ -418,221 +416,317 @@ DEV int pred_px(int mode, int n, int x, int y, const uint16_t *e, int dc, int bd
 }
 
 // ------------------------------------------------------------- k_recon
-// LDS tile per plane: row 0 / column 0 hold the top row / left column outside
-// the SB; pixel (x, y) of the SB lives at [(y + 1) * PITCH + x + 1].
-#define LP 66            // luma tile pitch (65 used)
-#define CP 34            // chroma tile pitch (33 used, 4:2:0)
+// One wavefront reconstructs one 64x64 superblock (luma + 4:2:0 chroma) in LDS. The
+// host groups the SB's tx blocks into passes of independent jobs of one size (same
+// dependency level): a pass runs 64/n jobs side by side, n lanes per job (one per
+// transform column; 32x32 jobs run alone on 32 lanes), so an SB takes ~40 passes
+// instead of ~155 sequential jobs. A tile's row 0 / column 0 hold the pixels above /
+// left of the SB. Pixel (x, y) of plane p lives at tile_p[(y + 1) * pitch_p + x + 1].
+#define LP 68            // luma tile pitch (65 used)
+#define CP 36            // chroma tile pitch (33 used, 4:2:0)
 #define LT_SIZE (65 * LP)
 #define CT_SIZE (33 * CP)
+#define KPF 8            // coefficients prefetched per lane per pass (more: loaded in place)
 
-template <typename PIX, class M, typename COEF>
-__global__ __launch_bounds__(256) void k_recon(const uint32_t *__restrict__ list, const SBRec *__restrict__ sbs,
-                                               const TxJob *__restrict__ jobs, const uint16_t *__restrict__ lvls,
-                                               const FrameDesc *__restrict__ frames,
-                                               const COEF *__restrict__ coefs)
+DEV const int16_t *scan_for(int tcode, int txtp)
+{
+    const int ts = tcode & 3;
+    if (tcode == 4) return vp9t_scan_default_4x4;                 // lossless (vp9data.c:600-618)
+    return ts == 0 ? (txtp == 1 ? vp9t_scan_col_4x4 : txtp == 2 ? vp9t_scan_row_4x4 : vp9t_scan_default_4x4)
+         : ts == 1 ? (txtp == 1 ? vp9t_scan_col_8x8 : txtp == 2 ? vp9t_scan_row_8x8 : vp9t_scan_default_8x8)
+         : ts == 2 ? (txtp == 1 ? vp9t_scan_col_16x16 : txtp == 2 ? vp9t_scan_row_16x16 : vp9t_scan_default_16x16)
+         : vp9t_scan_default_32x32;
+}
+
+// Lane geometry of a pass: groups of G = n lanes (64 for 32x32), one job per group.
+struct PassGeo {
+    int tcode, ts, n, lg, grp, li, nj, first;
+    DEV PassGeo(int w, int lane)
+    {
+        tcode = PASS_TX(w); ts = tcode & 3; n = 4 << ts;
+        lg = ts == 3 ? 6 : ts + 2;
+        grp = lane >> lg; li = lane & ((1 << lg) - 1);
+        nj = PASS_NJOBS(w); first = PASS_FIRST(w);
+    }
+    DEV bool active() const { return grp < nj; }
+};
+
+// Issue this lane's coefficient loads for a pass: coefficient k = li + m * G of its job.
+template <typename COEF>
+DEV void fetch_coefs(int w, int lane, const TxJob *lj, const COEF *__restrict__ coefs, uint32_t coef0,
+                     int32_t (&cv)[KPF], int16_t (&cp)[KPF])
+{
+    const PassGeo g(w, lane);
+#pragma unroll
+    for (int m = 0; m < KPF; m++) { cv[m] = 0; cp[m] = 0; }
+    if (!g.active()) return;
+    const TxJob jb = lj[g.first + g.grp];
+    const int eob = JOB_EOB(jb);
+    const COEF *src = coefs + coef0 + JOB_COFF(jb);
+    const int16_t *scan = scan_for(g.tcode, JOB_TXTP(jb));
+#pragma unroll
+    for (int m = 0; m < KPF; m++) {
+        const int k = g.li + (m << g.lg);
+        if (k < eob) { cv[m] = (int32_t) src[k]; cp[m] = scan[k]; }
+    }
+}
+
+// Column pass (type_a) of one job: lane c < nzc transforms column c of the job's
+// coefficient block (rows >= nzr are zero) into row c of its tmp block.
+template <int N, class M, typename COEF>
+DEV void itx_cols(const COEF *cb, COEF *tb, int li, int nzc, int nzr, int adst)
 {
     typedef typename M::T T;
-    __shared__ uint16_t tile[LT_SIZE + 2 * CT_SIZE];
-    __shared__ int32_t cbuf[4][32 * 32];
-    __shared__ int32_t tbuf[4][32 * 33];
-    __shared__ uint16_t ebuf[4][80];
+    if (li < nzc) {
+        T v[N];
+#pragma unroll
+        for (int k = 0; k < N; k++) v[k] = k < nzr ? M::in(cb[k * N + li]) : (T) 0;
+        tx1n<N, M>(v, adst);
+#pragma unroll
+        for (int k = 0; k < N; k++) tb[li * (N + 1) + k] = (COEF) (int64_t) v[k];
+    }
+}
+
+// Row pass (type_b) + add: lane i transforms tmp column i and adds output column i.
+template <int N, class M, typename COEF, typename PIX>
+DEV void itx_rows(const COEF *tb, PIX *o, int tpch, int li, int nzc, int adst, int bits, int bd)
+{
+    typedef typename M::T T;
+    if (li < N) {
+        T v[N];
+#pragma unroll
+        for (int k = 0; k < N; k++) v[k] = k < nzc ? M::in(tb[k * (N + 1) + li]) : (T) 0;
+        tx1n<N, M>(v, adst);
+#pragma unroll
+        for (int k = 0; k < N; k++) {
+            const int32_t ov = (COEF) (int64_t) v[k];
+            const int add = (int32_t) ((uint32_t) ov + (1u << (bits - 1))) >> bits;
+            PIX *q = o + k * tpch + li;
+            *q = (PIX) clipbd(*q + add, bd);
+        }
+    }
+}
+
+template <int N, class M, typename COEF, typename PIX>
+DEV void itx_pass(COEF *cbg, COEF *tbg, PIX *o, int tpch, int li, bool full, int nzc, int nzr, int txtp,
+                  int bits, int bd)
+{
+    if (full) itx_cols<N, M, COEF>(cbg, tbg, li, nzc, nzr, txtp & 1);
+    wave_sync();
+    if (full) itx_rows<N, M, COEF, PIX>(tbg, o, tpch, li, nzc, txtp >> 1, bits, bd);
+}
+
+template <typename PIX, class M, typename COEF>
+__global__ __launch_bounds__(64) void k_recon(const uint32_t *__restrict__ list, const SBRec *__restrict__ sbs,
+                                              const TxJob *__restrict__ jobs, const uint16_t *__restrict__ passes,
+                                              const FrameDesc *__restrict__ frames,
+                                              const COEF *__restrict__ coefs)
+{
+    typedef typename M::T T;
+    __shared__ PIX tile[LT_SIZE + 2 * CT_SIZE];
+    __shared__ COEF cb[1024];                  // per job n*n, <= 1024 per pass
+    __shared__ COEF tb[1088];                  // per job n*(n+1)
+    __shared__ uint16_t eb[256];               // per job 2n+8 edge pixels
+    __shared__ TxJob lj[MAX_SB_JOBS];
+    __shared__ uint16_t lp[MAX_SB_JOBS];
 
     const SBRec sb = sbs[list[blockIdx.x]];
     const FrameDesc &fd = frames[sb.frame];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int lane = threadIdx.x;
     const int bd = fd.bd;
 #define TPL(p) (tile + ((p) == 0 ? 0 : (p) == 1 ? LT_SIZE : LT_SIZE + CT_SIZE))
 #define TPCH(p) ((p) ? CP : LP)
 
-    // ---- load the SB neighbourhood (pre-loop-filter reconstruction) ----
+    // ---- prologue: job list, pass words, SB neighbourhood (pre-loop-filter pixels) ----
+    for (int i = lane; i < sb.njobs; i += 64) lj[i] = jobs[sb.job0 + i];
+    for (int i = lane; i < sb.npass; i += 64) lp[i] = passes[sb.pass0 + i];
     for (int p = 0; p < 3; p++) {
-        const int sz = p ? 32 : 64, ps = p ? 1 : 0;
+        const int sz = p ? 32 : 64;
         const PIX *g = (const PIX *) fd.plane[p];
         const int pitch = fd.pitch[p ? 1 : 0];
         const int x0 = sb.sbx * sz, y0 = sb.sby * sz;
-        uint16_t *t = TPL(p);
+        PIX *t = TPL(p);
         const int tpch = TPCH(p);
-        (void) ps;
-        // top row (y0 - 1), x0 - 1 .. x0 + sz - 1
         if (y0 > 0)
-            for (int i = tid; i < sz + 1; i += 256) {
-                int gx = x0 - 1 + i;
+            for (int i = lane; i < sz + 1; i += 64) {
+                const int gx = x0 - 1 + i;
                 t[i] = gx >= 0 ? g[(size_t) (y0 - 1) * pitch + gx] : 0;
             }
         if (x0 > 0)
-            for (int i = tid; i < sz; i += 256) t[(i + 1) * tpch] = g[(size_t) (y0 + i) * pitch + x0 - 1];
+            for (int i = lane; i < sz; i += 64) t[(i + 1) * tpch] = g[(size_t) (y0 + i) * pitch + x0 - 1];
         if (sb.flags & 1)
-            for (int i = tid; i < sz * sz; i += 256) {
-                int yy = i / sz, xx = i - yy * sz;
+            for (int i = lane; i < sz * sz; i += 64) {
+                const int yy = i / sz, xx = i - yy * sz;
                 t[(yy + 1) * tpch + xx + 1] = g[(size_t) (y0 + yy) * pitch + x0 + xx];
             }
     }
-    __syncthreads();
+    wave_sync();
 
-    const uint16_t *lv = lvls + sb.lvl0;
-    for (int l = 0; l < sb.nlev; l++) {
-        const int j0 = sb.job0 + lv[l], j1 = sb.job0 + lv[l + 1];
-        for (int j = j0 + wave; j < j1; j += 4) {
-            const TxJob jb = jobs[j];
-            const int p = jb.ptx & 3, tx = jb.ptx >> 2, ts = tx & 3, n = 4 << ts;
-            uint16_t *t = TPL(p);
-            const int tpch = TPCH(p);
-            const int px = jb.x4 * 4, py = jb.y4 * 4;                 // in-SB position
-            uint16_t *o = t + (py + 1) * tpch + px + 1;              // top-left pixel of the tx block
-            int32_t *cb = cbuf[wave];
-            int32_t *tb = tbuf[wave];
-            uint16_t *e = ebuf[wave];
+    const int npass = sb.npass;
+    int32_t cv[KPF], cvn[KPF];
+    int16_t cp[KPF], cpn[KPF];
+    if (npass) fetch_coefs<COEF>(lp[0], lane, lj, coefs, sb.coef0, cv, cp);
 
-            if (jb.mode != 0xff) {
-                // ---- edges: check_intra_mode (vp9recon.c:37-221) ----
-                const int sz = p ? 32 : 64;
-                const int gx = sb.sbx * sz + px, gy = sb.sby * sz + py;   // plane position
-                const int tile_x0 = p ? sb.tile_x0 * 4 : sb.tile_x0 * 8;
-                const int have_top = gy > 0, have_left = gx > tile_x0, have_right = jb.flags & 1;
-                const int w8 = fd.w8[p ? 1 : 0], h8 = fd.h8[p ? 1 : 0];
-                const int have_t = w8 - gx, have_l = h8 - gy;
-                int mode = jb.mode;
-                // mode_conv[mode][have_left][have_top]
-                switch (mode) {
-                case 0: if (!have_top) mode = 13; break;
-                case 1: if (!have_left) mode = 14; break;
-                case 2: mode = have_left ? (have_top ? 2 : 10) : (have_top ? 11 : 12); break;
-                case 3: case 7: if (!have_top) mode = 13; break;
-                case 8: if (!have_left) mode = 14; break;
-                case 9: mode = have_left ? (have_top ? 9 : 1) : (have_top ? 0 : 14); break;
-                default: break;
-                }
-                const bool need_top = mode == 0 || mode == 2 || mode == 3 || mode == 4 || mode == 5 ||
-                                      mode == 6 || mode == 7 || mode == 9 || mode == 11;
-                const bool need_left = mode == 1 || mode == 2 || mode == 4 || mode == 5 || mode == 6 ||
-                                       mode == 8 || mode == 9 || mode == 10;
-                const bool need_tl = mode == 4 || mode == 5 || mode == 6 || mode == 9;
-                const bool need_tr = mode == 3 || mode == 7;
-                const int base = 128 << (bd - 8);
-                uint16_t *T_ = e + n + 1;
+    for (int pi = 0; pi < npass; pi++) {
+        const int w = __builtin_amdgcn_readfirstlane(lp[pi]);
+        // prefetch the next pass's coefficients while this one runs
+        if (pi + 1 < npass) fetch_coefs<COEF>(lp[pi + 1], lane, lj, coefs, sb.coef0, cvn, cpn);
+
+        const PassGeo g(w, lane);
+        const int n = g.n, ts = g.ts, li = g.li;
+        const bool act = g.active();
+        const TxJob jb = lj[g.first + (act ? g.grp : 0)];
+        const int p = JOB_PLANE(jb);
+        PIX *t = TPL(p);
+        const int tpch = TPCH(p);
+        const int px = (jb.pos & 15) * 4, py = (jb.pos >> 4) * 4;
+        PIX *o = t + (py + 1) * tpch + px + 1;
+        const int eob = act ? JOB_EOB(jb) : 0;
+        const bool intra = act && jb.mode != 0xff;
+
+        // ---- intra prediction: check_intra_mode (vp9recon.c:37-221) + ipred ----
+        uint16_t *e = eb + g.grp * (2 * n + 8);
+        int mode = jb.mode;
+        const int base = 128 << (bd - 8);
+        if (intra) {
+            const int sz = p ? 32 : 64;
+            const int gx = sb.sbx * sz + px, gy = sb.sby * sz + py;
+            const int tile_x0 = p ? sb.tile_x0 * 4 : sb.tile_x0 * 8;
+            const int have_top = gy > 0, have_left = gx > tile_x0, have_right = JOB_HR(jb);
+            const int have_t = fd.w8[p ? 1 : 0] - gx, have_l = fd.h8[p ? 1 : 0] - gy;
+            switch (mode) {            // mode_conv[mode][have_left][have_top]
+            case 0: if (!have_top) mode = 13; break;
+            case 1: if (!have_left) mode = 14; break;
+            case 2: mode = have_left ? (have_top ? 2 : 10) : (have_top ? 11 : 12); break;
+            case 3: case 7: if (!have_top) mode = 13; break;
+            case 8: if (!have_left) mode = 14; break;
+            case 9: mode = have_left ? (have_top ? 9 : 1) : (have_top ? 0 : 14); break;
+            default: break;
+            }
+            const bool need_top = mode == 0 || mode == 2 || mode == 3 || mode == 4 || mode == 5 ||
+                                  mode == 6 || mode == 7 || mode == 9 || mode == 11;
+            const bool need_left = mode == 1 || mode == 2 || mode == 4 || mode == 5 || mode == 6 ||
+                                   mode == 8 || mode == 9 || mode == 10;
+            const bool need_tl = mode == 4 || mode == 5 || mode == 6 || mode == 9;
+            const bool need_tr = mode == 3 || mode == 7;
+            uint16_t *T_ = e + n + 1;
+            if (li < n) {
                 if (need_top) {
-                    if (lane < n) {
+                    T_[li] = !have_top ? base - 1 : o[-tpch + (li < have_t ? li : have_t - 1)];
+                    if (ts == 0 && need_tr) {
                         int v;
-                        if (!have_top) v = base - 1;
-                        else v = o[-tpch + (lane < have_t ? lane : have_t - 1)];
-                        T_[lane] = v;
-                    }
-                    if (ts == 0 && need_tr && lane >= 4 && lane < 8) {
-                        int v;
-                        if (have_top && have_right && 8 <= have_t) v = o[-tpch + lane];
-                        else if (!have_top) v = base - 1;                      // replicate a[3]
+                        if (have_top && have_right && 8 <= have_t) v = o[-tpch + 4 + li];
+                        else if (!have_top) v = base - 1;
                         else v = o[-tpch + (3 < have_t ? 3 : have_t - 1)];
-                        T_[lane] = v;
+                        T_[4 + li] = v;
                     }
-                    if (need_tl && lane == 0)
+                    if (need_tl && li == 0)
                         T_[-1] = (have_left && have_top) ? o[-tpch - 1] : base + (have_top ? 1 : -1);
                 }
-                if (need_left && lane < n) {
+                if (need_left) {
                     int v;
                     if (!have_left) v = base + 1;
-                    else if (mode == 8) v = o[(lane < have_l ? lane : have_l - 1) * tpch - 1];
+                    else if (mode == 8) v = o[(li < have_l ? li : have_l - 1) * tpch - 1];
                     else {
-                        // l[n-1-i] = pixel row i; rows >= have replicate the bottom-most available
-                        int i = n - 1 - lane;
+                        const int i = n - 1 - li;
                         v = o[(i < have_l ? i : have_l - 1) * tpch - 1];
                     }
-                    e[lane] = v;
-                }
-                wave_sync();
-                int dc = 0;
-                if (mode == 2) {
-                    int s = 0; for (int i = 0; i < n; i++) s += e[i] + T_[i];
-                    dc = (s + n) >> (ts + 3);
-                } else if (mode == 10) {
-                    int s = 0; for (int i = 0; i < n; i++) s += e[i];
-                    dc = (s + (n >> 1)) >> (ts + 2);
-                } else if (mode == 11) {
-                    int s = 0; for (int i = 0; i < n; i++) s += T_[i];
-                    dc = (s + (n >> 1)) >> (ts + 2);
-                } else if (mode >= 12) {
-                    dc = base + (mode == 13 ? -1 : mode == 14 ? 1 : 0);
-                }
-                for (int i = lane; i < n * n; i += 64) {
-                    int yy = i >> (ts + 2), xx = i & (n - 1);
-                    o[yy * tpch + xx] = pred_px(mode, n, xx, yy, e, dc, bd);
-                }
-                wave_sync();
-            }
-
-            if (jb.eob) {
-                const int eob = jb.eob;
-                if (tx == 4) {
-                    // lossless WHT 4x4 (vp9dsp_template.c:1750)
-                    for (int i = lane; i < 16; i += 64) cb[i] = 0;
-                    wave_sync();
-                    if (lane < eob) cb[vp9t_scan_default_4x4[lane]] = (int32_t) coefs[jb.coef + lane];
-                    wave_sync();
-                    if (lane < 4) {
-                        int32_t v[4];
-                        for (int k = 0; k < 4; k++) v[k] = cb[k * 4 + lane];
-                        iwht4(v, 0);
-                        for (int k = 0; k < 4; k++) tb[lane * 5 + k] = (COEF) v[k];
-                    }
-                    wave_sync();
-                    if (lane < 4) {
-                        int32_t v[4];
-                        for (int k = 0; k < 4; k++) v[k] = tb[k * 5 + lane];
-                        iwht4(v, 1);
-                        for (int k = 0; k < 4; k++) {
-                            uint16_t *q = o + k * tpch + lane;
-                            *q = clipbd(*q + (COEF) v[k], bd);
-                        }
-                    }
-                    wave_sync();
-                } else {
-                    const int txtp = ts == 3 ? 0 : jb.txtp;
-                    const int bits = ts == 3 ? 6 : ts + 4;
-                    if (txtp == 0 && eob == 1) {
-                        // DC-only shortcut (vp9dsp_template.c:1165-1178)
-                        T c0 = M::in((int32_t) coefs[jb.coef]);
-                        T t1 = M::r14(c0 * (T) 11585);
-                        int32_t tdc = (int32_t) M::r14(t1 * (T) 11585);
-                        int add = (int32_t) ((uint32_t) tdc + (1u << (bits - 1))) >> bits;
-                        for (int i = lane; i < n * n; i += 64) {
-                            uint16_t *q = o + (i >> (ts + 2)) * tpch + (i & (n - 1));
-                            *q = clipbd(*q + add, bd);
-                        }
-                        wave_sync();
-                    } else {
-                        const int16_t *scan = ts == 0 ? (txtp == 1 ? vp9t_scan_col_4x4 : txtp == 2 ? vp9t_scan_row_4x4 : vp9t_scan_default_4x4)
-                                            : ts == 1 ? (txtp == 1 ? vp9t_scan_col_8x8 : txtp == 2 ? vp9t_scan_row_8x8 : vp9t_scan_default_8x8)
-                                            : ts == 2 ? (txtp == 1 ? vp9t_scan_col_16x16 : txtp == 2 ? vp9t_scan_row_16x16 : vp9t_scan_default_16x16)
-                                            : vp9t_scan_default_32x32;
-                        for (int i = lane; i < n * n; i += 64) cb[i] = 0;
-                        wave_sync();
-                        for (int i = lane; i < eob; i += 64) cb[scan[i]] = (int32_t) coefs[jb.coef + i];
-                        wave_sync();
-                        // pass 1: column c -> tmp row c (type_a: ADST for txtp 1, 3)
-                        if (lane < n) {
-                            T v[32];
-                            for (int k = 0; k < n; k++) v[k] = M::in(cb[k * n + lane]);
-                            tx1d<M>(v, ts, txtp & 1);
-                            for (int k = 0; k < n; k++) tb[lane * (n + 1) + k] = (COEF) (int64_t) v[k];
-                        }
-                        wave_sync();
-                        // pass 2: output column c (type_b: ADST for txtp 2, 3)
-                        if (lane < n) {
-                            T v[32];
-                            for (int k = 0; k < n; k++) v[k] = M::in(tb[k * (n + 1) + lane]);
-                            tx1d<M>(v, ts, txtp >> 1);
-                            for (int k = 0; k < n; k++) {
-                                int32_t ov = (COEF) (int64_t) v[k];
-                                int add = (int32_t) ((uint32_t) ov + (1u << (bits - 1))) >> bits;
-                                uint16_t *q = o + k * tpch + lane;
-                                *q = clipbd(*q + add, bd);
-                            }
-                        }
-                        wave_sync();
-                    }
+                    e[li] = v;
                 }
             }
         }
-        __syncthreads();
+        wave_sync();
+        if (intra) {
+            const uint16_t *T_ = e + n + 1;
+            int dc = 0;
+            if (mode == 2) {
+                int sum = 0; for (int i = 0; i < n; i++) sum += e[i] + T_[i];
+                dc = (sum + n) >> (ts + 3);
+            } else if (mode == 10) {
+                int sum = 0; for (int i = 0; i < n; i++) sum += e[i];
+                dc = (sum + (n >> 1)) >> (ts + 2);
+            } else if (mode == 11) {
+                int sum = 0; for (int i = 0; i < n; i++) sum += T_[i];
+                dc = (sum + (n >> 1)) >> (ts + 2);
+            } else if (mode >= 12) {
+                dc = base + (mode == 13 ? -1 : mode == 14 ? 1 : 0);
+            }
+            for (int i = li; i < n * n; i += (1 << g.lg)) {
+                const int yy = i >> (ts + 2), xx = i & (n - 1);
+                o[yy * tpch + xx] = (PIX) pred_px(mode, n, xx, yy, e, dc, bd);
+            }
+        }
+        wave_sync();
+
+        // ---- residual: inverse transform + add (vp9dsp_template.c:1139-1750) ----
+        const int tcode = g.tcode;
+        const int txtp = JOB_TXTP(jb);
+        const int bits = ts == 3 ? 6 : ts + 4;
+        const int dcv = __shfl(cv[0], lane & ~((1 << g.lg) - 1));
+        const bool dconly = eob == 1 && txtp == 0 && tcode != 4;
+        if (dconly) {
+            // DC-only shortcut (vp9dsp_template.c:1165-1178)
+            const T t1 = M::r14(M::in(dcv) * (T) 11585);
+            const int32_t tdc = (int32_t) M::r14(t1 * (T) 11585);
+            const int add = (int32_t) ((uint32_t) tdc + (1u << (bits - 1))) >> bits;
+            for (int i = li; i < n * n; i += (1 << g.lg)) {
+                PIX *q = o + (i >> (ts + 2)) * tpch + (i & (n - 1));
+                *q = (PIX) clipbd(*q + add, bd);
+            }
+        }
+        // any full transform in this pass? (uniform)
+        const bool full = eob > 0 && !dconly;
+        if (__any(full)) {
+            const int nzc = tcode == 4 ? 4 : JOB_NZC(jb), nzr = tcode == 4 ? 4 : JOB_NZR(jb);
+            COEF *cbg = cb + g.grp * n * n;
+            COEF *tbg = tb + g.grp * n * (n + 1);
+            if (full)
+                for (int i = li; i < nzr * nzc; i += (1 << g.lg)) {
+                    const int r = i / nzc, c = i - r * nzc;
+                    cbg[r * n + c] = 0;
+                }
+            wave_sync();
+            if (full) {
+#pragma unroll
+                for (int m = 0; m < KPF; m++)
+                    if (li + (m << g.lg) < eob) cbg[cp[m]] = (COEF) cv[m];
+                if (eob > (KPF << g.lg)) {
+                    const int16_t *scan = scan_for(tcode, txtp);
+                    const COEF *src = coefs + sb.coef0 + JOB_COFF(jb);
+                    for (int k = li + (KPF << g.lg); k < eob; k += (1 << g.lg)) cbg[scan[k]] = src[k];
+                }
+            }
+            wave_sync();
+            if (tcode == 4) {
+                // lossless WHT 4x4 (vp9dsp_template.c:1719-1750)
+                if (full) {
+                    int32_t v[4];
+                    for (int k = 0; k < 4; k++) v[k] = cbg[k * 4 + li];
+                    iwht4(v, 0);
+                    for (int k = 0; k < 4; k++) tbg[li * 5 + k] = (COEF) v[k];
+                }
+                wave_sync();
+                if (full) {
+                    int32_t v[4];
+                    for (int k = 0; k < 4; k++) v[k] = tbg[k * 5 + li];
+                    iwht4(v, 1);
+                    for (int k = 0; k < 4; k++) {
+                        PIX *q = o + k * tpch + li;
+                        *q = (PIX) clipbd(*q + (COEF) v[k], bd);
+                    }
+                }
+            } else {
+                switch (ts) {
+                case 0: itx_pass<4, M, COEF, PIX>(cbg, tbg, o, tpch, li, full, nzc, nzr, txtp, bits, bd); break;
+                case 1: itx_pass<8, M, COEF, PIX>(cbg, tbg, o, tpch, li, full, nzc, nzr, txtp, bits, bd); break;
+                case 2: itx_pass<16, M, COEF, PIX>(cbg, tbg, o, tpch, li, full, nzc, nzr, txtp, bits, bd); break;
+                default: itx_pass<32, M, COEF, PIX>(cbg, tbg, o, tpch, li, full, nzc, nzr, 0, bits, bd); break;
+                }
+            }
+        }
+        wave_sync();
+#pragma unroll
+        for (int m = 0; m < KPF; m++) { cv[m] = cvn[m]; cp[m] = cpn[m]; }
     }
 
     // ---- store the SB interior ----
@@ -641,13 +735,15 @@ __global__ __launch_bounds__(256) void k_recon(const uint32_t *__restrict__ list
         PIX *g = (PIX *) fd.plane[p];
         const int pitch = fd.pitch[p ? 1 : 0];
         const int x0 = sb.sbx * sz, y0 = sb.sby * sz;
-        const uint16_t *t = TPL(p);
+        const PIX *t = TPL(p);
         const int tpch = TPCH(p);
-        for (int i = tid; i < sz * sz; i += 256) {
-            int yy = i / sz, xx = i - yy * sz;
-            g[(size_t) (y0 + yy) * pitch + x0 + xx] = (PIX) t[(yy + 1) * tpch + xx + 1];
+        for (int i = lane; i < sz * sz; i += 64) {
+            const int yy = i / sz, xx = i - yy * sz;
+            g[(size_t) (y0 + yy) * pitch + x0 + xx] = t[(yy + 1) * tpch + xx + 1];
         }
     }
+#undef TPL
+#undef TPCH
 }
 
 // --------------------------------------------------------------- k_lf
@@ -912,15 +1008,15 @@ __global__ __launch_bounds__(256) void k_mc(const McUnit *__restrict__ units, in
 // ------------------------------------------------------------ launchers
 extern "C" {
 int vp9hip_launch_recon(int hb, hipStream_t st, int nsb, const uint32_t *list, const SBRec *sbs,
-                        const TxJob *jobs, const uint16_t *lvls, const FrameDesc *frames, const void *coefs)
+                        const TxJob *jobs, const uint16_t *passes, const FrameDesc *frames, const void *coefs)
 {
     if (nsb <= 0) return 0;
     if (hb)
-        hipLaunchKernelGGL((k_recon<uint16_t, M64, int32_t>), dim3(nsb), dim3(256), 0, st,
-                           list, sbs, jobs, lvls, frames, (const int32_t *) coefs);
+        hipLaunchKernelGGL((k_recon<uint16_t, M64, int32_t>), dim3(nsb), dim3(64), 0, st,
+                           list, sbs, jobs, passes, frames, (const int32_t *) coefs);
     else
-        hipLaunchKernelGGL((k_recon<uint8_t, M32, int16_t>), dim3(nsb), dim3(256), 0, st,
-                           list, sbs, jobs, lvls, frames, (const int16_t *) coefs);
+        hipLaunchKernelGGL((k_recon<uint8_t, M32, int16_t>), dim3(nsb), dim3(64), 0, st,
+                           list, sbs, jobs, passes, frames, (const int16_t *) coefs);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int vp9hip_launch_lf(int hb, hipStream_t st, int nsb, const uint32_t *list, const LFRec *recs,

@@ -30,7 +30,7 @@
 
 extern "C" {
 int vp9hip_launch_recon(int hb, hipStream_t st, int nsb, const uint32_t *list, const SBRec *sbs,
-                        const TxJob *jobs, const uint16_t *lvls, const FrameDesc *frames, const void *coefs);
+                        const TxJob *jobs, const uint16_t *passes, const FrameDesc *frames, const void *coefs);
 int vp9hip_launch_lf(int hb, hipStream_t st, int nsb, const uint32_t *list, const LFRec *recs,
                      const FrameDesc *frames);
 int vp9hip_launch_mc(int hb, hipStream_t st, int n, const McUnit *units, const FrameDesc *frames);
@@ -51,7 +51,7 @@ struct Staged {
     std::vector<FrameDesc> frames;
     std::vector<SBRec> sbs;
     std::vector<TxJob> jobs;
-    std::vector<uint16_t> lvls;
+    std::vector<uint16_t> passes;
     std::vector<LFRec> lfs;
     std::vector<McUnit> mcs;
     std::vector<uint32_t> lists;        // concatenated SB index lists of all launches
@@ -61,7 +61,7 @@ struct Staged {
     // device arena
     uint8_t *arena = nullptr;
     size_t arena_cap = 0;
-    size_t o_frames = 0, o_sbs = 0, o_jobs = 0, o_lvls = 0, o_lfs = 0, o_mcs = 0, o_lists = 0, o_coefs = 0;
+    size_t o_frames = 0, o_sbs = 0, o_jobs = 0, o_passes = 0, o_lfs = 0, o_mcs = 0, o_lists = 0, o_coefs = 0;
     bool ready = false;
 };
 
@@ -204,6 +204,36 @@ static void lf_mask_edges(uint8_t (*mask)[8][4], int ss_h, int ss_v, int row7, i
 
 static inline int rdiv(int a, int b) { return (a >= 0 ? a + (b >> 1) : a - (b >> 1)) / b; }
 
+// Bounding box (columns, rows) of the coefficient positions scan[0 .. eob-1] for every
+// (tx, txtp, eob): the kernels transform only columns that can hold a nonzero value.
+static uint8_t g_nz[5][4][1025][2];
+static void init_nz()
+{
+    static bool done = false;
+    if (done) return;
+    static const int16_t *const scans[5][4] = {
+        { vp9t_scan_default_4x4, vp9t_scan_col_4x4, vp9t_scan_row_4x4, vp9t_scan_default_4x4 },
+        { vp9t_scan_default_8x8, vp9t_scan_col_8x8, vp9t_scan_row_8x8, vp9t_scan_default_8x8 },
+        { vp9t_scan_default_16x16, vp9t_scan_col_16x16, vp9t_scan_row_16x16, vp9t_scan_default_16x16 },
+        { vp9t_scan_default_32x32, vp9t_scan_default_32x32, vp9t_scan_default_32x32, vp9t_scan_default_32x32 },
+        { vp9t_scan_default_4x4, vp9t_scan_default_4x4, vp9t_scan_default_4x4, vp9t_scan_default_4x4 },
+    };
+    for (int tx = 0; tx < 5; tx++)
+        for (int tp = 0; tp < 4; tp++) {
+            const int n = 4 << (tx & 3);
+            int mc = 0, mr = 0;
+            g_nz[tx][tp][0][0] = g_nz[tx][tp][0][1] = 0;
+            for (int i = 0; i < n * n; i++) {
+                const int rc = scans[tx][tp][i];
+                mc = std::max(mc, rc % n + 1);
+                mr = std::max(mr, rc / n + 1);
+                g_nz[tx][tp][i + 1][0] = (uint8_t) mc;
+                g_nz[tx][tp][i + 1][1] = (uint8_t) mr;
+            }
+        }
+    done = true;
+}
+
 // --------------------------------------------------------------------------
 // Per-frame work building
 namespace {
@@ -216,7 +246,10 @@ struct FrameBuild {
     uint64_t coef_base;          // element offset of this frame's coefficients in the batch stream
 };
 
-struct PendingJob { TxJob j; int level; };
+struct PendingJob {
+    int level, plane, tcode, txtp, mode, hr, x4, y4, eob, nzc, nzr;
+    uint64_t src;               // element offset of the job's coefficients in the packet
+};
 
 } // namespace
 
@@ -229,7 +262,7 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<uin
     const int lossless = f->lossless;
     const uint16_t *eob = f->eobs;
     const uint16_t *eob_end = f->eobs + f->neobs;
-    uint64_t coef = fb.coef_base;           // running element index
+    uint64_t coef = 0;                      // running element index within the frame's coefficients
     uint32_t bi = 0;
     const int log2 = f->log2_tile_cols;
 
@@ -278,30 +311,29 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<uin
                             e = *eob++;
                         }
                         if (!b->intra && !e) continue;
-                        TxJob j;
-                        memset(&j, 0, sizeof(j));
+                        PendingJob q;
                         int mode = 0xff, txtp = 0;
                         if (b->intra) {
                             mode = p ? b->uvmode : b->mode[b->bs > VP9H_BS_8x8 && b->tx == 0 ? y * 2 + x : 0];
                             if (mode > 9) return VP9HIP_EINVALIDDATA;
-                            txtp = p ? 0 : intra_txfm_type[mode];
+                            txtp = p || txs == 3 ? 0 : intra_txfm_type[mode];
                         }
                         const int tcode = lossless ? 4 : txs;
-                        j.ptx = (uint8_t) (p | (tcode << 2));
-                        j.txtp = (uint8_t) txtp;
-                        j.mode = (uint8_t) mode;
-                        j.flags = (x < pw4 - 1) ? 1 : 0;
-                        j.x4 = (uint8_t) (ux_sb + x);
-                        j.y4 = (uint8_t) (uy_sb + y);
-                        j.eob = (uint16_t) e;
-                        j.coef = (uint32_t) coef;
+                        if (e > (16 << (2 * txs))) return VP9HIP_EINVALIDDATA;
+                        q.plane = p; q.tcode = tcode; q.txtp = txtp; q.mode = mode;
+                        q.hr = (x < pw4 - 1) ? 1 : 0;
+                        q.x4 = ux_sb + x; q.y4 = uy_sb + y;
+                        q.eob = e;
+                        q.nzc = e ? g_nz[tcode][txtp][e][0] : 1;
+                        q.nzr = e ? g_nz[tcode][txtp][e][1] : 1;
+                        q.src = coef;
                         coef += e;
                         // dependency level within the SB plane
                         int lvl = -1;
                         const int ux0 = ux_sb + x, uy0 = uy_sb + y, n4 = step;
                         int8_t *lm = lmap[p];
                         if (b->intra) {
-                            const int trx = (txs == 0 && (j.flags & 1)) ? 1 : 0;
+                            const int trx = (txs == 0 && q.hr) ? 1 : 0;
                             if (uy0 > 0)
                                 for (int u = ux0 - 1; u < ux0 + n4 + trx; u++)
                                     if (u >= 0 && u < units) lvl = std::max<int>(lvl, lm[(uy0 - 1) * 16 + u]);
@@ -312,7 +344,8 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<uin
                         lvl += 1;
                         for (int v = uy0; v < uy0 + n4 && v < units; v++)
                             for (int u = ux0; u < ux0 + n4 && u < units; u++) lm[v * 16 + u] = (int8_t) lvl;
-                        pj.push_back({ j, lvl });
+                        q.level = lvl;
+                        pj.push_back(q);
                     }
             }
 
@@ -378,25 +411,50 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<uin
             }
         }
 
-        // sort jobs by level (stable), emit SB record
-        int nlev = 0;
-        for (auto &q : pj) nlev = std::max(nlev, q.level + 1);
+        // group jobs into passes: same level and tx code, up to 64/n jobs; sorted by
+        // (level, tx, txtp, mode) so a pass runs few distinct code paths
+        if (pj.size() > MAX_SB_JOBS) return VP9HIP_EINVALIDDATA;
+        std::stable_sort(pj.begin(), pj.end(), [](const PendingJob &a, const PendingJob &b) {
+            if (a.level != b.level) return a.level < b.level;
+            if (a.tcode != b.tcode) return a.tcode < b.tcode;
+            if (a.txtp != b.txtp) return a.txtp < b.txtp;
+            return a.mode < b.mode;
+        });
         SBRec sr;
         memset(&sr, 0, sizeof(sr));
         sr.frame = fb.frame_idx; sr.sbx = sbx; sr.sby = sby;
         sr.job0 = (uint32_t) s.jobs.size();
-        sr.lvl0 = (uint32_t) s.lvls.size();
-        sr.nlev = (uint16_t) nlev;
+        sr.pass0 = (uint32_t) s.passes.size();
+        sr.coef0 = (uint32_t) (s.coefs.size() / fb.coef_size);
         sr.tile_x0 = (uint16_t) tile_x0;
+        sr.njobs = (uint16_t) pj.size();
         sr.flags = f->keyframe || f->intraonly ? 0 : 1;
-        std::vector<int> cnt(nlev + 1, 0);
-        for (auto &q : pj) cnt[q.level + 1]++;
-        for (int l = 0; l < nlev; l++) cnt[l + 1] += cnt[l];
-        for (int l = 0; l <= nlev; l++) s.lvls.push_back((uint16_t) cnt[l]);
-        size_t base = s.jobs.size();
-        s.jobs.resize(base + pj.size());
-        std::vector<int> pos(cnt.begin(), cnt.end());
-        for (auto &q : pj) s.jobs[base + pos[q.level]++] = q.j;
+        for (size_t k = 0; k < pj.size();) {
+            const int tcode = pj[k].tcode, n = 4 << (tcode & 3);
+            const int cap = n == 32 ? 1 : 64 / n;
+            size_t e = k + 1;
+            while (e < pj.size() && (int) (e - k) < cap && pj[e].level == pj[k].level && pj[e].tcode == tcode) e++;
+            s.passes.push_back((uint16_t) ((k << 7) | ((e - k - 1) << 3) | tcode));
+            k = e;
+        }
+        sr.npass = (uint16_t) (s.passes.size() - sr.pass0);
+        // jobs + their coefficients in pass order
+        uint32_t coff = 0;
+        for (auto &q : pj) {
+            TxJob j;
+            j.ptx = (uint8_t) (q.plane | q.tcode << 2 | q.hr << 5 | q.txtp << 6);
+            j.mode = (uint8_t) q.mode;
+            j.pos = (uint8_t) (q.x4 | q.y4 << 4);
+            j.nzc = (uint8_t) (q.nzc - 1);
+            j.ec = (uint32_t) q.eob | (uint32_t) (q.nzr - 1) << 11 | coff << 16;
+            if (q.eob) {
+                const size_t nb = (size_t) q.eob * fb.coef_size, dst = s.coefs.size();
+                s.coefs.resize(dst + nb);
+                memcpy(s.coefs.data() + dst, (const uint8_t *) f->coefs + q.src * fb.coef_size, nb);
+            }
+            coff += q.eob;
+            s.jobs.push_back(j);
+        }
         uint32_t sbi = (uint32_t) s.sbs.size();
         s.sbs.push_back(sr);
         if (!pj.empty() || sr.flags == 0) {
@@ -418,7 +476,7 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<uin
         (void) has_intra;
     }
     if (eob != eob_end) return VP9HIP_EINVALIDDATA;
-    if (coef - fb.coef_base != f->ncoefs) return VP9HIP_EINVALIDDATA;
+    if (coef != f->ncoefs) return VP9HIP_EINVALIDDATA;
     return 0;
 }
 
@@ -429,12 +487,13 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     hipSetDevice(c->dev);
     HIPCHK(hipStreamSynchronize(c->st));      // the previous batch may still read the arena
     Staged &s = c->stg;
-    s.frames.clear(); s.sbs.clear(); s.jobs.clear(); s.lvls.clear(); s.lfs.clear(); s.mcs.clear();
+    s.frames.clear(); s.sbs.clear(); s.jobs.clear(); s.passes.clear(); s.lfs.clear(); s.mcs.clear();
     s.lists.clear(); s.launches.clear(); s.coefs.clear();
     for (int k = 0; k < K_N; k++) s.alg_bytes[k] = 0;
     s.ready = false;
 
     const int csz = c->hb ? 4 : 2;
+    init_nz();
     std::vector<uint32_t> par;
     std::vector<std::vector<uint32_t>> rsteps, lsteps;
     uint64_t coef_base = 0;
@@ -477,9 +536,6 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
         int r = build_frame(c, s, fb, par, rsteps, lsteps);
         if (r < 0) return r;
         size_t cb = (size_t) f->ncoefs * csz;
-        size_t off = s.coefs.size();
-        s.coefs.resize(off + cb);
-        if (cb) memcpy(s.coefs.data() + off, f->coefs, cb);
         coef_base += f->ncoefs;
         if (coef_base > 0xffffffffull) return VP9HIP_ENOMEM;
         // algorithmic bytes: recon writes P and reads C (+P for inter SBs),
@@ -506,7 +562,7 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     s.o_frames = o; o = al(o + s.frames.size() * sizeof(FrameDesc));
     s.o_sbs = o; o = al(o + s.sbs.size() * sizeof(SBRec));
     s.o_jobs = o; o = al(o + s.jobs.size() * sizeof(TxJob));
-    s.o_lvls = o; o = al(o + s.lvls.size() * sizeof(uint16_t));
+    s.o_passes = o; o = al(o + s.passes.size() * sizeof(uint16_t));
     s.o_lfs = o; o = al(o + s.lfs.size() * sizeof(LFRec));
     s.o_mcs = o; o = al(o + s.mcs.size() * sizeof(McUnit));
     s.o_lists = o; o = al(o + s.lists.size() * sizeof(uint32_t));
@@ -525,7 +581,7 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     if (up(s.o_frames, s.frames.data(), s.frames.size() * sizeof(FrameDesc)) ||
         up(s.o_sbs, s.sbs.data(), s.sbs.size() * sizeof(SBRec)) ||
         up(s.o_jobs, s.jobs.data(), s.jobs.size() * sizeof(TxJob)) ||
-        up(s.o_lvls, s.lvls.data(), s.lvls.size() * sizeof(uint16_t)) ||
+        up(s.o_passes, s.passes.data(), s.passes.size() * sizeof(uint16_t)) ||
         up(s.o_lfs, s.lfs.data(), s.lfs.size() * sizeof(LFRec)) ||
         up(s.o_mcs, s.mcs.data(), s.mcs.size() * sizeof(McUnit)) ||
         up(s.o_lists, s.lists.data(), s.lists.size() * sizeof(uint32_t)) ||
@@ -564,7 +620,7 @@ extern "C" int vp9hip_run_batch(vp9hip_ctx *c)
             break;
         case K_RECON:
             r = vp9hip_launch_recon(c->hb, c->st, (int) L.n, lists + L.off, (const SBRec *) (s.arena + s.o_sbs),
-                                    (const TxJob *) (s.arena + s.o_jobs), (const uint16_t *) (s.arena + s.o_lvls),
+                                    (const TxJob *) (s.arena + s.o_jobs), (const uint16_t *) (s.arena + s.o_passes),
                                     fr, s.arena + s.o_coefs);
             break;
         case K_LF:

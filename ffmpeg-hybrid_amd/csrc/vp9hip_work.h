@@ -25,28 +25,46 @@ typedef struct FrameDesc {
     int32_t  sharp;           /* LF sharpness                                         */
 } FrameDesc;
 
-/* One transform block job (16 bytes). */
+/* One transform block job (8 bytes, so a whole SB's job list fits in LDS). */
 typedef struct TxJob {
-    uint8_t  ptx;             /* plane | tx << 2   (tx 0..3, 4 = lossless WHT)          */
-    uint8_t  txtp;            /* DCT_DCT 0, DCT_ADST 1, ADST_DCT 2, ADST_ADST 3          */
+    uint8_t  ptx;             /* plane (2b) | tx << 2 (3b: 0..3, 4 = lossless WHT) |
+                                 have_right << 5 (vp9recon.c:47) | txtp << 6               */
     uint8_t  mode;            /* intra mode before edge substitution; 0xff = residual only */
-    uint8_t  flags;           /* bit0 have_right (vp9recon.c:47)                        */
-    uint8_t  x4, y4;          /* position inside the SB plane, 4-pixel units            */
-    uint16_t eob;
-    uint32_t coef;            /* element offset of the scan-order coefficients          */
-    uint32_t pad;
+    uint8_t  pos;             /* x4 | y4 << 4: position inside the SB plane, 4-pixel units */
+    uint8_t  nzc;             /* columns that can be nonzero minus 1 (bounding box of
+                                 scan[0 .. eob-1]; a zero column transforms to zero)        */
+    uint32_t ec;              /* eob (11b) | (nzr - 1) << 11 (5b) | coefficient offset
+                                 relative to SBRec.coef0 << 16                             */
 } TxJob;
 
-/* One superblock of reconstruction work. */
+#define JOB_PLANE(j) ((j).ptx & 3)
+#define JOB_TX(j) (((j).ptx >> 2) & 7)
+#define JOB_HR(j) (((j).ptx >> 5) & 1)
+#define JOB_TXTP(j) ((j).ptx >> 6)
+#define JOB_EOB(j) ((j).ec & 2047)
+#define JOB_NZR(j) ((((j).ec >> 11) & 31) + 1)
+#define JOB_NZC(j) ((j).nzc + 1)
+#define JOB_COFF(j) ((j).ec >> 16)
+
+/* One superblock of reconstruction work. Its jobs are grouped into "passes": a pass
+ * holds up to 64/n independent jobs (same dependency level, same tx code), so one
+ * wavefront runs them side by side, n lanes (one per transform column) per job. */
 typedef struct SBRec {
     uint32_t frame;
     uint16_t sbx, sby;
-    uint32_t job0;            /* first TxJob (jobs sorted by dependency level)          */
-    uint32_t lvl0;            /* first entry of the level-start table (nlev + 1 u16)    */
-    uint16_t nlev;
+    uint32_t job0;            /* first TxJob (jobs in pass order)                       */
+    uint32_t pass0;           /* first pass word                                        */
+    uint32_t coef0;           /* first coefficient element (coefficients in job order)  */
+    uint16_t npass, njobs;
     uint16_t tile_x0;         /* tile column start, 8x8 units (vp9.c:1244-1250)         */
-    uint32_t flags;           /* bit0: load SB interior first (inter frame)             */
+    uint16_t flags;           /* bit0: load SB interior first (inter frame)             */
 } SBRec;
+
+/* pass word (u16): first job (relative to job0) << 7 | (njobs - 1) << 3 | tx code */
+#define PASS_FIRST(w) ((w) >> 7)
+#define PASS_NJOBS(w) ((((w) >> 3) & 15) + 1)
+#define PASS_TX(w) ((w) & 7)
+#define MAX_SB_JOBS 384
 
 /* Loop-filter data of one SB: VP9Filter (vp9dec.h:83-87) + position. */
 typedef struct LFRec {
