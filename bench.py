@@ -92,8 +92,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    alg = dev.alg_bytes()           # per step, per kernel class: [mc, recon, lf]
-    names = ["k_mc", "k_recon", "k_lf"]
+    alg = dev.alg_bytes()           # per step, per kernel class
+    names = list(alg.keys())
     total_frames = args.frames * args.steps * world
     fps = total_frames / elapsed
     ms_per_step = elapsed * 1000.0 / args.steps
@@ -101,13 +101,12 @@ def main():
     # dominant kernel (largest device time)
     dom = max(names, key=lambda k: ksum.get(k, [0.0, 0])[0])
     kms, kn = ksum[dom]
-    kidx = names.index(dom)
     launches_per_step = kn / args.steps
-    bytes_per_launch = alg[kidx] / launches_per_step if launches_per_step else 0.0
+    bytes_per_launch = alg[dom] / launches_per_step if launches_per_step else 0.0
     avg_launch_s = (kms / 1000.0) / kn if kn else float("nan")
     achieved = bytes_per_launch / avg_launch_s / 1e9 if kn else 0.0
     kernel_ms_per_frame = sum(x[0] for x in ksum.values()) / (args.frames * args.steps)
-    frame_bytes = sum(alg) / args.frames
+    frame_bytes = sum(alg.values()) / args.frames
     roofline = {
         "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,

@@ -221,9 +221,11 @@ class Device:
         return {names[i].decode(): (ms[i], cnt[i]) for i in range(n)}
 
     def alg_bytes(self):
+        """Algorithmic bytes of the staged batch per kernel class, keyed like timing()."""
         b = (ctypes.c_double * 8)()
         n = _check("vp9hip_alg_bytes", lib().vp9hip_alg_bytes(self._c, b, 8))
-        return [b[i] for i in range(n)]
+        names = list(self.timing().keys())
+        return {names[i]: b[i] for i in range(n)}
 
     def _plane_args(self, planes):
         ptrs = (ctypes.c_void_p * 3)(*[p.ctypes.data for p in planes])

@@ -415,18 +415,14 @@ DEV int pred_px(int mode, int n, int x, int y, const uint16_t *e, int dc, int bd
     }
 }
 
-// ------------------------------------------------------------- k_recon
-// One wavefront reconstructs one 64x64 superblock (luma + 4:2:0 chroma) in LDS. The
-// host groups the SB's tx blocks into passes of independent jobs of one size (same
-// dependency level): a pass runs 64/n jobs side by side, n lanes per job (one per
-// transform column; 32x32 jobs run alone on 32 lanes), so an SB takes ~40 passes
-// instead of ~155 sequential jobs. A tile's row 0 / column 0 hold the pixels above /
-// left of the SB. Pixel (x, y) of plane p lives at tile_p[(y + 1) * pitch_p + x + 1].
-#define LP 68            // luma tile pitch (65 used)
-#define CP 36            // chroma tile pitch (33 used, 4:2:0)
-#define LT_SIZE (65 * LP)
-#define CT_SIZE (33 * CP)
-#define KPF 8            // coefficients prefetched per lane per pass (more: loaded in place)
+// ------------------------------------------------------------- k_resid
+// Inverse transform of every coded tx block of a batch (vp9dsp_template.c:1139-1750),
+// one launch per tx code, no dependencies: a wave holds 64/N jobs, N lanes per job
+// (one per column). The residual (out + (1 << (bits - 1))) >> bits is either added in
+// place onto the motion-compensated prediction (inter blocks) or stored column-major
+// as int16 for k_pred (intra blocks; 10/12-bit values saturate to int16, which leaves
+// clip(pred + r) unchanged since |pred| < 4096).
+#define RWAVES 4
 
 DEV const int16_t *scan_for(int tcode, int txtp)
 {
@@ -438,96 +434,249 @@ DEV const int16_t *scan_for(int tcode, int txtp)
          : vp9t_scan_default_32x32;
 }
 
-// Lane geometry of a pass: groups of G = n lanes (64 for 32x32), one job per group.
-struct PassGeo {
-    int tcode, ts, n, lg, grp, li, nj, first;
-    DEV PassGeo(int w, int lane)
-    {
-        tcode = PASS_TX(w); ts = tcode & 3; n = 4 << ts;
-        lg = ts == 3 ? 6 : ts + 2;
-        grp = lane >> lg; li = lane & ((1 << lg) - 1);
-        nj = PASS_NJOBS(w); first = PASS_FIRST(w);
-    }
-    DEV bool active() const { return grp < nj; }
-};
-
-// Issue this lane's coefficient loads for a pass: coefficient k = li + m * G of its job.
-template <typename COEF>
-DEV void fetch_coefs(int w, int lane, const TxJob *lj, const COEF *__restrict__ coefs, uint32_t coef0,
-                     int32_t (&cv)[KPF], int16_t (&cp)[KPF])
+template <int N> DEV void store_col(int16_t *dst, const int (&r)[N])
 {
-    const PassGeo g(w, lane);
+    uint32_t w[N / 2];
 #pragma unroll
-    for (int m = 0; m < KPF; m++) { cv[m] = 0; cp[m] = 0; }
-    if (!g.active()) return;
-    const TxJob jb = lj[g.first + g.grp];
-    const int eob = JOB_EOB(jb);
-    const COEF *src = coefs + coef0 + JOB_COFF(jb);
-    const int16_t *scan = scan_for(g.tcode, JOB_TXTP(jb));
+    for (int k = 0; k < N / 2; k++) w[k] = ((uint32_t) r[2 * k] & 0xffff) | ((uint32_t) r[2 * k + 1] << 16);
+    if (N == 4) *(uint2 *) dst = make_uint2(w[0], w[1]);
+    else
 #pragma unroll
-    for (int m = 0; m < KPF; m++) {
-        const int k = g.li + (m << g.lg);
-        if (k < eob) { cv[m] = (int32_t) src[k]; cp[m] = scan[k]; }
+        for (int k = 0; k < N / 8; k++) ((uint4 *) dst)[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+}
+
+template <int N, int TCODE, typename PIX, class M, typename COEF>
+__global__ __launch_bounds__(64 * RWAVES) void k_resid(const RJob *__restrict__ jobs, int njobs,
+                                                       const FrameDesc *__restrict__ frames,
+                                                       const COEF *__restrict__ coefs, int16_t *__restrict__ resid)
+{
+    typedef typename M::T T;
+    constexpr int CAP = 64 / N;
+    constexpr int LG = N == 4 ? 2 : N == 8 ? 3 : N == 16 ? 4 : 5;
+    constexpr int TS = LG - 2;
+    constexpr int BITS = N == 32 ? 6 : TS + 4;
+    __shared__ COEF cbs[RWAVES][CAP * N * N];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int grp = lane >> LG, li = lane & (N - 1);
+    const int j = (blockIdx.x * RWAVES + wave) * CAP + grp;
+    const bool act = j < njobs;
+    COEF *cb = cbs[wave] + grp * N * N;
+
+    RJob r;
+    if (act) r = jobs[j];
+    else { r.coef = 0; r.dst = 0; r.eob = 0; r.frame = 0; r.ptx = 0; r.nzc = 1; r.nzr = 1; }
+    const int eob = r.eob, txtp = TCODE == 3 || TCODE == 4 ? 0 : RJ_TXTP(r);
+    const int nzc = TCODE == 4 ? 4 : r.nzc, nzr = TCODE == 4 ? 4 : r.nzr;   // the WHT reads every row
+    const COEF *src = coefs + r.coef;
+    const bool dconly = TCODE != 4 && act && eob == 1 && txtp == 0;
+    const bool full = act && !dconly;
+
+    // zero the nonzero bounding box, then scatter scan-order coefficients
+    if (full)
+        for (int k = 0; k < nzr; k++) cb[k * N + li] = 0;
+    wave_sync();
+    if (full) {
+        const int16_t *scan = scan_for(TCODE, txtp);
+        for (int k0 = 0; k0 < eob; k0 += 8 * N) {
+            COEF c[8];
+            int pos[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int k = k0 + li + u * N;
+                if (k < eob) { c[u] = src[k]; pos[u] = scan[k]; }
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                if (k0 + li + u * N < eob) cb[pos[u]] = c[u];
+        }
+    }
+    wave_sync();
+
+    int res[N];
+    if (TCODE == 4) {
+        // lossless WHT (vp9dsp_template.c:1719-1750); in-place transpose through LDS
+        int32_t v[4];
+        if (full) for (int k = 0; k < 4; k++) v[k] = cb[k * 4 + li];
+        wave_sync();
+        if (full) { iwht4(v, 0); for (int k = 0; k < 4; k++) cb[li * 4 + k] = (COEF) v[k]; }
+        wave_sync();
+        if (full) { for (int k = 0; k < 4; k++) v[k] = cb[k * 4 + li]; iwht4(v, 1); }
+#pragma unroll
+        for (int k = 0; k < N; k++) res[k] = full ? (int) (COEF) v[k & 3] : 0;
+    } else {
+        T v[N];
+        // column pass (type_a): lane c < nzc transforms column c into row c
+        const bool colp = full && li < nzc;
+#pragma unroll
+        for (int k = 0; k < N; k++) v[k] = colp && k < nzr ? M::in(cb[k * N + li]) : (T) 0;
+        wave_sync();
+        if (colp) {
+            tx1n<N, M>(v, txtp & 1);
+#pragma unroll
+            for (int k = 0; k < N; k++) cb[li * N + k] = (COEF) (int64_t) v[k];
+        }
+        wave_sync();
+        // row pass (type_b): lane i transforms column i of the transposed block
+        if (full) {
+#pragma unroll
+            for (int k = 0; k < N; k++) v[k] = k < nzc ? M::in(cb[k * N + li]) : (T) 0;
+            tx1n<N, M>(v, txtp >> 1);
+#pragma unroll
+            for (int k = 0; k < N; k++) {
+                const int32_t ov = (COEF) (int64_t) v[k];
+                res[k] = (int32_t) ((uint32_t) ov + (1u << (BITS - 1))) >> BITS;
+            }
+        } else {
+            // DC-only shortcut (vp9dsp_template.c:1165-1178)
+            int add = 0;
+            if (dconly) {
+                const T t1 = M::r14(M::in((int32_t) src[0]) * (T) 11585);
+                const int32_t tdc = (int32_t) M::r14(t1 * (T) 11585);
+                add = (int32_t) ((uint32_t) tdc + (1u << (BITS - 1))) >> BITS;
+            }
+#pragma unroll
+            for (int k = 0; k < N; k++) res[k] = add;
+        }
+    }
+    if (!act) return;
+    if (RJ_INPLACE(r)) {
+        const FrameDesc &fd = frames[r.frame];
+        const int p = RJ_PLANE(r);
+        PIX *q = (PIX *) fd.plane[p] + r.dst + li;
+        const int pitch = fd.pitch[p ? 1 : 0], bd = fd.bd;
+#pragma unroll
+        for (int k = 0; k < N; k++) q[(size_t) k * pitch] = (PIX) clipbd(q[(size_t) k * pitch] + res[k], bd);
+    } else {
+#pragma unroll
+        for (int k = 0; k < N; k++) res[k] = res[k] < -32768 ? -32768 : res[k] > 32767 ? 32767 : res[k];
+        store_col<N>(resid + (size_t) r.dst * 16 + li * N, res);
     }
 }
 
-// Column pass (type_a) of one job: lane c < nzc transforms column c of the job's
-// coefficient block (rows >= nzr are zero) into row c of its tmp block.
-template <int N, class M, typename COEF>
-DEV void itx_cols(const COEF *cb, COEF *tb, int li, int nzc, int nzr, int adst)
+// ------------------------------------------------------------- k_pred
+// One wavefront predicts one 64x64 superblock (luma + 4:2:0 chroma) in LDS. The host
+// packs the SB's intra tx blocks into passes of independent jobs of one size (same
+// dependency level): 64/n jobs side by side, n lanes per job, lane = pixel column.
+// Each pass: edges (check_intra_mode, vp9recon.c:37-221) -> predictor
+// (vp9dsp_template.c:28-1106) -> + residual from k_resid -> clip. A tile's row 0 /
+// column 0 hold the pixels above / left of the SB; pixel (x, y) of plane p lives at
+// tile_p[(y + 1) * pitch_p + x + 1].
+#define LP 68            // luma tile pitch (65 used)
+#define CP 36            // chroma tile pitch (33 used, 4:2:0)
+#define LT_SIZE (65 * LP)
+#define CT_SIZE (33 * CP)
+
+// A lane's residual column (<= 32 int16) in named registers (no array: stays out of scratch).
+struct RCol { uint4 a, b, c, d; };
+DEV uint32_t rword(const RCol &r, int k)
 {
-    typedef typename M::T T;
-    if (li < nzc) {
-        T v[N];
-#pragma unroll
-        for (int k = 0; k < N; k++) v[k] = k < nzr ? M::in(cb[k * N + li]) : (T) 0;
-        tx1n<N, M>(v, adst);
-#pragma unroll
-        for (int k = 0; k < N; k++) tb[li * (N + 1) + k] = (COEF) (int64_t) v[k];
+    switch (k) {
+    case 0: return r.a.x; case 1: return r.a.y; case 2: return r.a.z; case 3: return r.a.w;
+    case 4: return r.b.x; case 5: return r.b.y; case 6: return r.b.z; case 7: return r.b.w;
+    case 8: return r.c.x; case 9: return r.c.y; case 10: return r.c.z; case 11: return r.c.w;
+    case 12: return r.d.x; case 13: return r.d.y; case 14: return r.d.z; default: return r.d.w;
     }
 }
 
-// Row pass (type_b) + add: lane i transforms tmp column i and adds output column i.
-template <int N, class M, typename COEF, typename PIX>
-DEV void itx_rows(const COEF *tb, PIX *o, int tpch, int li, int nzc, int adst, int bits, int bd)
+// load this lane's residual column of the job it serves in pass word w
+DEV void fetch_resid(int w, int lane, const PJob *lj, const int16_t *__restrict__ resid, RCol &rv)
 {
-    typedef typename M::T T;
-    if (li < N) {
-        T v[N];
+    const int ts = PASS_TS(w), lg = ts + 2, grp = lane >> lg, li = lane & ((1 << lg) - 1);
+    if (grp >= PASS_NJOBS(w)) return;
+    const PJob jb = lj[PASS_FIRST(w) + grp];
+    if (!PJ_RES(jb)) return;
+    const uint4 *s = (const uint4 *) (resid + (size_t) jb.roff * 16 + (li << lg));
+    if (ts == 0) { const uint2 x = *(const uint2 *) s; rv.a.x = x.x; rv.a.y = x.y; return; }
+    rv.a = s[0];
+    if (ts >= 2) rv.b = s[1];
+    if (ts == 3) { rv.c = s[2]; rv.d = s[3]; }
+}
+
+#define PCASE(m) case m: for (int y = 0; y < N; y++) o[y * tpch + x] = (PIX) pred_px(m, N, x, y, e, dc, bd); break;
+// predictor column x of an N x N block into the tile, then + residual, clipped
+template <int N, typename PIX>
+DEV void pred_col(int mode, int x, const uint16_t *e, int dc, int bd, bool has_res, const RCol &rv,
+                  PIX *o, int tpch)
+{
+    switch (mode) {
+    PCASE(0) PCASE(1) PCASE(3) PCASE(4) PCASE(5) PCASE(6) PCASE(7) PCASE(8) PCASE(9)
+    default:
+        for (int y = 0; y < N; y++) o[y * tpch + x] = (PIX) dc;
+    }
+    if (has_res) {
 #pragma unroll
-        for (int k = 0; k < N; k++) v[k] = k < nzc ? M::in(tb[k * (N + 1) + li]) : (T) 0;
-        tx1n<N, M>(v, adst);
+        for (int y = 0; y < N; y++)
+            o[y * tpch + x] = (PIX) clipbd(o[y * tpch + x] + (int) (int16_t) (rword(rv, y >> 1) >> ((y & 1) * 16)), bd);
+    }
+}
+#undef PCASE
+
+// Load the pixels above / left of an SB (and, for inter frames, its interior: the
+// MC prediction + inter residuals) into the LDS tile. All global loads of a batch are
+// issued before any LDS write so their latencies overlap.
+template <typename PIX>
+DEV void load_sb_tile(const FrameDesc &fd, int sbx, int sby, bool interior, int lane, PIX *tile)
+{
+    const PIX *gy = (const PIX *) fd.plane[0], *gu = (const PIX *) fd.plane[1], *gv = (const PIX *) fd.plane[2];
+    const int py = fd.pitch[0], pc = fd.pitch[1];
+    const int lx = sbx * 64, ly = sby * 64, cx = sbx * 32, cy = sby * 32;
+    // borders: luma top (65), luma left (64), chroma top (33 + 33), chroma left (32 + 32)
+    // lanes 0..32 read U top x = -1..31, lanes 33..63 V top x = -1..29, lanes 0..1 V x = 30..31
+    PIX v0 = 0, v1 = 0, v2 = 0, v3 = 0, v4 = 0, v5 = 0;
+    const bool top = ly > 0, left = lx > 0;
+    const PIX *gc = lane < 33 ? gu : gv;
+    const int ci = lane < 33 ? lane : lane - 33;
+    if (top) {
+        if (lx - 1 + lane >= 0) v0 = gy[(size_t) (ly - 1) * py + lx - 1 + lane];
+        if (lane == 0) v4 = gy[(size_t) (ly - 1) * py + lx + 63];
+        if (cx - 1 + ci >= 0) v2 = gc[(size_t) (cy - 1) * pc + cx - 1 + ci];
+        if (lane < 2) v5 = gv[(size_t) (cy - 1) * pc + cx + 30 + lane];
+    }
+    if (left) {
+        v1 = gy[(size_t) (ly + lane) * py + lx - 1];
+        v3 = (lane < 32 ? gu : gv)[(size_t) (cy + (lane & 31)) * pc + cx - 1];
+    }
+    PIX *tu = tile + LT_SIZE, *tv = tile + LT_SIZE + CT_SIZE;
+    if (top) {
+        tile[lane] = v0;
+        if (lane == 0) tile[64] = v4;
+        (lane < 33 ? tu : tv)[ci] = v2;
+        if (lane < 2) tv[31 + lane] = v5;
+    }
+    if (left) { tile[(lane + 1) * LP] = v1; (lane < 32 ? tu : tv)[((lane & 31) + 1) * CP] = v3; }
+    if (!interior) return;
+    // interior: 64 luma rows + 2 x 32 chroma rows, 16 independent loads per lane per batch
+    for (int i0 = 0; i0 < 64 * 64 + 2 * 32 * 32; i0 += 64 * 16) {
+        PIX t[16];
 #pragma unroll
-        for (int k = 0; k < N; k++) {
-            const int32_t ov = (COEF) (int64_t) v[k];
-            const int add = (int32_t) ((uint32_t) ov + (1u << (bits - 1))) >> bits;
-            PIX *q = o + k * tpch + li;
-            *q = (PIX) clipbd(*q + add, bd);
+        for (int u = 0; u < 16; u++) {
+            const int i = i0 + u * 64 + lane;
+            if (i < 4096) t[u] = gy[(size_t) (ly + (i >> 6)) * py + lx + (i & 63)];
+            else {
+                const int c = i - 4096, pl = c >> 10, r = (c >> 5) & 31, x = c & 31;
+                t[u] = (pl ? gv : gu)[(size_t) (cy + r) * pc + cx + x];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+            const int i = i0 + u * 64 + lane;
+            if (i < 4096) tile[((i >> 6) + 1) * LP + (i & 63) + 1] = t[u];
+            else {
+                const int c = i - 4096, pl = c >> 10, r = (c >> 5) & 31, x = c & 31;
+                tile[LT_SIZE + pl * CT_SIZE + (r + 1) * CP + x + 1] = t[u];
+            }
         }
     }
 }
 
-template <int N, class M, typename COEF, typename PIX>
-DEV void itx_pass(COEF *cbg, COEF *tbg, PIX *o, int tpch, int li, bool full, int nzc, int nzr, int txtp,
-                  int bits, int bd)
+template <typename PIX>
+__global__ __launch_bounds__(64) void k_pred(const uint32_t *__restrict__ list, const SBRec *__restrict__ sbs,
+                                             const PJob *__restrict__ jobs, const uint16_t *__restrict__ passes,
+                                             const FrameDesc *__restrict__ frames, const int16_t *__restrict__ resid)
 {
-    if (full) itx_cols<N, M, COEF>(cbg, tbg, li, nzc, nzr, txtp & 1);
-    wave_sync();
-    if (full) itx_rows<N, M, COEF, PIX>(tbg, o, tpch, li, nzc, txtp >> 1, bits, bd);
-}
-
-template <typename PIX, class M, typename COEF>
-__global__ __launch_bounds__(64) void k_recon(const uint32_t *__restrict__ list, const SBRec *__restrict__ sbs,
-                                              const TxJob *__restrict__ jobs, const uint16_t *__restrict__ passes,
-                                              const FrameDesc *__restrict__ frames,
-                                              const COEF *__restrict__ coefs)
-{
-    typedef typename M::T T;
     __shared__ PIX tile[LT_SIZE + 2 * CT_SIZE];
-    __shared__ COEF cb[1024];                  // per job n*n, <= 1024 per pass
-    __shared__ COEF tb[1088];                  // per job n*(n+1)
     __shared__ uint16_t eb[256];               // per job 2n+8 edge pixels
-    __shared__ TxJob lj[MAX_SB_JOBS];
+    __shared__ PJob lj[MAX_SB_JOBS];
     __shared__ uint16_t lp[MAX_SB_JOBS];
 
     const SBRec sb = sbs[list[blockIdx.x]];
@@ -540,59 +689,38 @@ __global__ __launch_bounds__(64) void k_recon(const uint32_t *__restrict__ list,
     // ---- prologue: job list, pass words, SB neighbourhood (pre-loop-filter pixels) ----
     for (int i = lane; i < sb.njobs; i += 64) lj[i] = jobs[sb.job0 + i];
     for (int i = lane; i < sb.npass; i += 64) lp[i] = passes[sb.pass0 + i];
-    for (int p = 0; p < 3; p++) {
-        const int sz = p ? 32 : 64;
-        const PIX *g = (const PIX *) fd.plane[p];
-        const int pitch = fd.pitch[p ? 1 : 0];
-        const int x0 = sb.sbx * sz, y0 = sb.sby * sz;
-        PIX *t = TPL(p);
-        const int tpch = TPCH(p);
-        if (y0 > 0)
-            for (int i = lane; i < sz + 1; i += 64) {
-                const int gx = x0 - 1 + i;
-                t[i] = gx >= 0 ? g[(size_t) (y0 - 1) * pitch + gx] : 0;
-            }
-        if (x0 > 0)
-            for (int i = lane; i < sz; i += 64) t[(i + 1) * tpch] = g[(size_t) (y0 + i) * pitch + x0 - 1];
-        if (sb.flags & 1)
-            for (int i = lane; i < sz * sz; i += 64) {
-                const int yy = i / sz, xx = i - yy * sz;
-                t[(yy + 1) * tpch + xx + 1] = g[(size_t) (y0 + yy) * pitch + x0 + xx];
-            }
-    }
+    load_sb_tile<PIX>(fd, sb.sbx, sb.sby, sb.flags & 1, lane, tile);
     wave_sync();
 
     const int npass = sb.npass;
-    int32_t cv[KPF], cvn[KPF];
-    int16_t cp[KPF], cpn[KPF];
-    if (npass) fetch_coefs<COEF>(lp[0], lane, lj, coefs, sb.coef0, cv, cp);
+    RCol rv, rvn;
+    rv.a = rv.b = rv.c = rv.d = make_uint4(0, 0, 0, 0);
+    rvn = rv;
+    if (npass) fetch_resid(lp[0], lane, lj, resid, rv);
 
     for (int pi = 0; pi < npass; pi++) {
         const int w = __builtin_amdgcn_readfirstlane(lp[pi]);
-        // prefetch the next pass's coefficients while this one runs
-        if (pi + 1 < npass) fetch_coefs<COEF>(lp[pi + 1], lane, lj, coefs, sb.coef0, cvn, cpn);
+        if (pi + 1 < npass) fetch_resid(lp[pi + 1], lane, lj, resid, rvn);   // prefetch
 
-        const PassGeo g(w, lane);
-        const int n = g.n, ts = g.ts, li = g.li;
-        const bool act = g.active();
-        const TxJob jb = lj[g.first + (act ? g.grp : 0)];
-        const int p = JOB_PLANE(jb);
+        const int ts = PASS_TS(w), n = 4 << ts, lg = ts + 2;
+        const int grp = lane >> lg, li = lane & (n - 1);
+        const bool act = grp < PASS_NJOBS(w);
+        const PJob jb = lj[PASS_FIRST(w) + (act ? grp : 0)];
+        const int p = PJ_PLANE(jb);
         PIX *t = TPL(p);
         const int tpch = TPCH(p);
         const int px = (jb.pos & 15) * 4, py = (jb.pos >> 4) * 4;
         PIX *o = t + (py + 1) * tpch + px + 1;
-        const int eob = act ? JOB_EOB(jb) : 0;
-        const bool intra = act && jb.mode != 0xff;
 
-        // ---- intra prediction: check_intra_mode (vp9recon.c:37-221) + ipred ----
-        uint16_t *e = eb + g.grp * (2 * n + 8);
+        // ---- edges: check_intra_mode (vp9recon.c:37-221) ----
+        uint16_t *e = eb + grp * (2 * n + 8);
         int mode = jb.mode;
         const int base = 128 << (bd - 8);
-        if (intra) {
+        if (act) {
             const int sz = p ? 32 : 64;
             const int gx = sb.sbx * sz + px, gy = sb.sby * sz + py;
             const int tile_x0 = p ? sb.tile_x0 * 4 : sb.tile_x0 * 8;
-            const int have_top = gy > 0, have_left = gx > tile_x0, have_right = JOB_HR(jb);
+            const int have_top = gy > 0, have_left = gx > tile_x0, have_right = PJ_HR(jb);
             const int have_t = fd.w8[p ? 1 : 0] - gx, have_l = fd.h8[p ? 1 : 0] - gy;
             switch (mode) {            // mode_conv[mode][have_left][have_top]
             case 0: if (!have_top) mode = 13; break;
@@ -610,33 +738,31 @@ __global__ __launch_bounds__(64) void k_recon(const uint32_t *__restrict__ list,
             const bool need_tl = mode == 4 || mode == 5 || mode == 6 || mode == 9;
             const bool need_tr = mode == 3 || mode == 7;
             uint16_t *T_ = e + n + 1;
-            if (li < n) {
-                if (need_top) {
-                    T_[li] = !have_top ? base - 1 : o[-tpch + (li < have_t ? li : have_t - 1)];
-                    if (ts == 0 && need_tr) {
-                        int v;
-                        if (have_top && have_right && 8 <= have_t) v = o[-tpch + 4 + li];
-                        else if (!have_top) v = base - 1;
-                        else v = o[-tpch + (3 < have_t ? 3 : have_t - 1)];
-                        T_[4 + li] = v;
-                    }
-                    if (need_tl && li == 0)
-                        T_[-1] = (have_left && have_top) ? o[-tpch - 1] : base + (have_top ? 1 : -1);
-                }
-                if (need_left) {
+            if (need_top) {
+                T_[li] = !have_top ? base - 1 : o[-tpch + (li < have_t ? li : have_t - 1)];
+                if (ts == 0 && need_tr) {
                     int v;
-                    if (!have_left) v = base + 1;
-                    else if (mode == 8) v = o[(li < have_l ? li : have_l - 1) * tpch - 1];
-                    else {
-                        const int i = n - 1 - li;
-                        v = o[(i < have_l ? i : have_l - 1) * tpch - 1];
-                    }
-                    e[li] = v;
+                    if (have_top && have_right && 8 <= have_t) v = o[-tpch + 4 + li];
+                    else if (!have_top) v = base - 1;
+                    else v = o[-tpch + (3 < have_t ? 3 : have_t - 1)];
+                    T_[4 + li] = v;
                 }
+                if (need_tl && li == 0)
+                    T_[-1] = (have_left && have_top) ? o[-tpch - 1] : base + (have_top ? 1 : -1);
+            }
+            if (need_left) {
+                int v;
+                if (!have_left) v = base + 1;
+                else if (mode == 8) v = o[(li < have_l ? li : have_l - 1) * tpch - 1];
+                else {
+                    const int i = n - 1 - li;
+                    v = o[(i < have_l ? i : have_l - 1) * tpch - 1];
+                }
+                e[li] = v;
             }
         }
         wave_sync();
-        if (intra) {
+        if (act) {
             const uint16_t *T_ = e + n + 1;
             int dc = 0;
             if (mode == 2) {
@@ -651,82 +777,16 @@ __global__ __launch_bounds__(64) void k_recon(const uint32_t *__restrict__ list,
             } else if (mode >= 12) {
                 dc = base + (mode == 13 ? -1 : mode == 14 ? 1 : 0);
             }
-            for (int i = li; i < n * n; i += (1 << g.lg)) {
-                const int yy = i >> (ts + 2), xx = i & (n - 1);
-                o[yy * tpch + xx] = (PIX) pred_px(mode, n, xx, yy, e, dc, bd);
+            const bool hr = PJ_RES(jb);
+            switch (ts) {
+            case 0: pred_col<4, PIX>(mode, li, e, dc, bd, hr, rv, o, tpch); break;
+            case 1: pred_col<8, PIX>(mode, li, e, dc, bd, hr, rv, o, tpch); break;
+            case 2: pred_col<16, PIX>(mode, li, e, dc, bd, hr, rv, o, tpch); break;
+            default: pred_col<32, PIX>(mode, li, e, dc, bd, hr, rv, o, tpch); break;
             }
         }
         wave_sync();
-
-        // ---- residual: inverse transform + add (vp9dsp_template.c:1139-1750) ----
-        const int tcode = g.tcode;
-        const int txtp = JOB_TXTP(jb);
-        const int bits = ts == 3 ? 6 : ts + 4;
-        const int dcv = __shfl(cv[0], lane & ~((1 << g.lg) - 1));
-        const bool dconly = eob == 1 && txtp == 0 && tcode != 4;
-        if (dconly) {
-            // DC-only shortcut (vp9dsp_template.c:1165-1178)
-            const T t1 = M::r14(M::in(dcv) * (T) 11585);
-            const int32_t tdc = (int32_t) M::r14(t1 * (T) 11585);
-            const int add = (int32_t) ((uint32_t) tdc + (1u << (bits - 1))) >> bits;
-            for (int i = li; i < n * n; i += (1 << g.lg)) {
-                PIX *q = o + (i >> (ts + 2)) * tpch + (i & (n - 1));
-                *q = (PIX) clipbd(*q + add, bd);
-            }
-        }
-        // any full transform in this pass? (uniform)
-        const bool full = eob > 0 && !dconly;
-        if (__any(full)) {
-            const int nzc = tcode == 4 ? 4 : JOB_NZC(jb), nzr = tcode == 4 ? 4 : JOB_NZR(jb);
-            COEF *cbg = cb + g.grp * n * n;
-            COEF *tbg = tb + g.grp * n * (n + 1);
-            if (full)
-                for (int i = li; i < nzr * nzc; i += (1 << g.lg)) {
-                    const int r = i / nzc, c = i - r * nzc;
-                    cbg[r * n + c] = 0;
-                }
-            wave_sync();
-            if (full) {
-#pragma unroll
-                for (int m = 0; m < KPF; m++)
-                    if (li + (m << g.lg) < eob) cbg[cp[m]] = (COEF) cv[m];
-                if (eob > (KPF << g.lg)) {
-                    const int16_t *scan = scan_for(tcode, txtp);
-                    const COEF *src = coefs + sb.coef0 + JOB_COFF(jb);
-                    for (int k = li + (KPF << g.lg); k < eob; k += (1 << g.lg)) cbg[scan[k]] = src[k];
-                }
-            }
-            wave_sync();
-            if (tcode == 4) {
-                // lossless WHT 4x4 (vp9dsp_template.c:1719-1750)
-                if (full) {
-                    int32_t v[4];
-                    for (int k = 0; k < 4; k++) v[k] = cbg[k * 4 + li];
-                    iwht4(v, 0);
-                    for (int k = 0; k < 4; k++) tbg[li * 5 + k] = (COEF) v[k];
-                }
-                wave_sync();
-                if (full) {
-                    int32_t v[4];
-                    for (int k = 0; k < 4; k++) v[k] = tbg[k * 5 + li];
-                    iwht4(v, 1);
-                    for (int k = 0; k < 4; k++) {
-                        PIX *q = o + k * tpch + li;
-                        *q = (PIX) clipbd(*q + (COEF) v[k], bd);
-                    }
-                }
-            } else {
-                switch (ts) {
-                case 0: itx_pass<4, M, COEF, PIX>(cbg, tbg, o, tpch, li, full, nzc, nzr, txtp, bits, bd); break;
-                case 1: itx_pass<8, M, COEF, PIX>(cbg, tbg, o, tpch, li, full, nzc, nzr, txtp, bits, bd); break;
-                case 2: itx_pass<16, M, COEF, PIX>(cbg, tbg, o, tpch, li, full, nzc, nzr, txtp, bits, bd); break;
-                default: itx_pass<32, M, COEF, PIX>(cbg, tbg, o, tpch, li, full, nzc, nzr, 0, bits, bd); break;
-                }
-            }
-        }
-        wave_sync();
-#pragma unroll
-        for (int m = 0; m < KPF; m++) { cv[m] = cvn[m]; cp[m] = cpn[m]; }
+        rv = rvn;
     }
 
     // ---- store the SB interior ----
@@ -1006,17 +1066,40 @@ __global__ __launch_bounds__(256) void k_mc(const McUnit *__restrict__ units, in
 }
 
 // ------------------------------------------------------------ launchers
+template <int N, int TC>
+static void launch_resid_n(int hb, hipStream_t st, int n, const RJob *jobs, const FrameDesc *frames,
+                           const void *coefs, int16_t *resid)
+{
+    const int per = RWAVES * (64 / N);
+    const int nb = (n + per - 1) / per;
+    if (hb)
+        hipLaunchKernelGGL((k_resid<N, TC, uint16_t, M64, int32_t>), dim3(nb), dim3(64 * RWAVES), 0, st,
+                           jobs, n, frames, (const int32_t *) coefs, resid);
+    else
+        hipLaunchKernelGGL((k_resid<N, TC, uint8_t, M32, int16_t>), dim3(nb), dim3(64 * RWAVES), 0, st,
+                           jobs, n, frames, (const int16_t *) coefs, resid);
+}
 extern "C" {
-int vp9hip_launch_recon(int hb, hipStream_t st, int nsb, const uint32_t *list, const SBRec *sbs,
-                        const TxJob *jobs, const uint16_t *passes, const FrameDesc *frames, const void *coefs)
+int vp9hip_launch_resid(int hb, hipStream_t st, int tcode, int n, const RJob *jobs, const FrameDesc *frames,
+                        const void *coefs, int16_t *resid)
+{
+    if (n <= 0) return 0;
+    switch (tcode) {
+    case 0: launch_resid_n<4, 0>(hb, st, n, jobs, frames, coefs, resid); break;
+    case 1: launch_resid_n<8, 1>(hb, st, n, jobs, frames, coefs, resid); break;
+    case 2: launch_resid_n<16, 2>(hb, st, n, jobs, frames, coefs, resid); break;
+    case 3: launch_resid_n<32, 3>(hb, st, n, jobs, frames, coefs, resid); break;
+    case 4: launch_resid_n<4, 4>(hb, st, n, jobs, frames, coefs, resid); break;
+    default: return -1;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int vp9hip_launch_pred(int hb, hipStream_t st, int nsb, const uint32_t *list, const SBRec *sbs,
+                       const PJob *jobs, const uint16_t *passes, const FrameDesc *frames, const int16_t *resid)
 {
     if (nsb <= 0) return 0;
-    if (hb)
-        hipLaunchKernelGGL((k_recon<uint16_t, M64, int32_t>), dim3(nsb), dim3(64), 0, st,
-                           list, sbs, jobs, passes, frames, (const int32_t *) coefs);
-    else
-        hipLaunchKernelGGL((k_recon<uint8_t, M32, int16_t>), dim3(nsb), dim3(64), 0, st,
-                           list, sbs, jobs, passes, frames, (const int16_t *) coefs);
+    if (hb) hipLaunchKernelGGL(k_pred<uint16_t>, dim3(nsb), dim3(64), 0, st, list, sbs, jobs, passes, frames, resid);
+    else    hipLaunchKernelGGL(k_pred<uint8_t>, dim3(nsb), dim3(64), 0, st, list, sbs, jobs, passes, frames, resid);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int vp9hip_launch_lf(int hb, hipStream_t st, int nsb, const uint32_t *list, const LFRec *recs,

@@ -2,9 +2,11 @@
 // include/vp9hip.h on top of the gfx950 kernels in vp9hip_kernels.hip.
 //
 // From each pass-1 frame packet it builds, on the host:
-//   * per-superblock transform-block job lists, topologically levelled by the
-//     intra dependencies of check_intra_mode (vp9recon.c:37-221) so one SB is
-//     reconstructed by one workgroup in LDS;
+//   * residual jobs: every coded tx block of the batch, bucketed by tx size and type,
+//     for the dependency-free inverse-transform kernel k_resid;
+//   * per-superblock intra prediction job lists, topologically levelled by the
+//     intra dependencies of check_intra_mode (vp9recon.c:37-221) and packed into
+//     passes of independent jobs, so one SB is predicted by one wavefront in LDS;
 //   * the loop-filter level/mask record of every SB (VP9Filter, restating
 //     vp9block.c:1142-1262 and 1438-1452);
 //   * motion-compensation rectangles restating inter_pred's sub-8x8 MV rules
@@ -29,8 +31,10 @@
 #include "vp9hip_work.h"
 
 extern "C" {
-int vp9hip_launch_recon(int hb, hipStream_t st, int nsb, const uint32_t *list, const SBRec *sbs,
-                        const TxJob *jobs, const uint16_t *passes, const FrameDesc *frames, const void *coefs);
+int vp9hip_launch_resid(int hb, hipStream_t st, int tcode, int n, const RJob *jobs, const FrameDesc *frames,
+                        const void *coefs, int16_t *resid);
+int vp9hip_launch_pred(int hb, hipStream_t st, int nsb, const uint32_t *list, const SBRec *sbs,
+                       const PJob *jobs, const uint16_t *passes, const FrameDesc *frames, const int16_t *resid);
 int vp9hip_launch_lf(int hb, hipStream_t st, int nsb, const uint32_t *list, const LFRec *recs,
                      const FrameDesc *frames);
 int vp9hip_launch_mc(int hb, hipStream_t st, int n, const McUnit *units, const FrameDesc *frames);
@@ -38,30 +42,35 @@ int vp9hip_launch_mc(int hb, hipStream_t st, int n, const McUnit *units, const F
 
 namespace {
 
-enum { K_MC, K_RECON, K_LF, K_N };
-const char *const kname[K_N] = { "k_mc", "k_recon", "k_lf" };
+enum { K_MC, K_RESID, K_PRED, K_LF, K_N };
+const char *const kname[K_N] = { "k_mc", "k_resid", "k_pred", "k_lf" };
 
 // ff_vp9_intra_txfm_type (vp9data.c:437-452)
 const uint8_t intra_txfm_type[14] = { 2, 1, 0, 0, 3, 2, 1, 2, 1, 3, 0, 0, 0, 0 };
 
-struct Launch { int kind; uint32_t off; uint32_t n; };
+struct Launch { int kind; uint32_t off; uint32_t n; int arg; };
 
 struct Staged {
     // host images (kept for rebuilds / inspection)
     std::vector<FrameDesc> frames;
     std::vector<SBRec> sbs;
-    std::vector<TxJob> jobs;
+    std::vector<PJob> pjobs;
     std::vector<uint16_t> passes;
+    std::vector<RJob> rbucket[5][4];    // residual jobs by (tx code, txtp)
+    std::vector<RJob> rjobs;            // concatenated buckets
+    uint64_t resid16 = 0;               // residual scratch size, 16-element units
     std::vector<LFRec> lfs;
     std::vector<McUnit> mcs;
     std::vector<uint32_t> lists;        // concatenated SB index lists of all launches
     std::vector<Launch> launches;
     std::vector<uint8_t> coefs;         // concatenated coefficient streams (bytes)
-    double alg_bytes[K_N] = { 0, 0, 0 };
+    double alg_bytes[K_N] = { 0, 0, 0, 0 };
     // device arena
     uint8_t *arena = nullptr;
     size_t arena_cap = 0;
-    size_t o_frames = 0, o_sbs = 0, o_jobs = 0, o_passes = 0, o_lfs = 0, o_mcs = 0, o_lists = 0, o_coefs = 0;
+    size_t o_frames = 0, o_sbs = 0, o_pjobs = 0, o_passes = 0, o_rjobs = 0, o_lfs = 0, o_mcs = 0, o_lists = 0, o_coefs = 0;
+    int16_t *resid = nullptr;           // intra residual scratch (column-major n x n blocks)
+    size_t resid_cap = 0;               // bytes
     bool ready = false;
 };
 
@@ -79,8 +88,8 @@ struct vp9hip_ctx {
     // timing of the last run
     bool timing = true;
     std::vector<hipEvent_t> ev;
-    double kms[K_N] = { 0, 0, 0 };
-    int kcount[K_N] = { 0, 0, 0 };
+    double kms[K_N] = { 0, 0, 0, 0 };
+    int kcount[K_N] = { 0, 0, 0, 0 };
 };
 
 #define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
@@ -114,6 +123,7 @@ extern "C" void vp9hip_close(vp9hip_ctx *c)
     hipStreamSynchronize(c->st);
     free_bufs(c);
     if (c->stg.arena) hipFree(c->stg.arena);
+    if (c->stg.resid) hipFree(c->stg.resid);
     for (auto e : c->ev) hipEventDestroy(e);
     hipStreamDestroy(c->st);
     delete c;
@@ -243,23 +253,22 @@ struct FrameBuild {
     int frame_idx;
     int cols, rows, sb_cols, sb_rows;
     int ss_h, ss_v, coef_size;
+    int pitch[2];
     uint64_t coef_base;          // element offset of this frame's coefficients in the batch stream
 };
 
-struct PendingJob {
-    int level, plane, tcode, txtp, mode, hr, x4, y4, eob, nzc, nzr;
-    uint64_t src;               // element offset of the job's coefficients in the packet
-};
+struct PendingJob { PJob j; int level, ts; };
 
 } // namespace
 
 // Build jobs/levels/LF/MC for one frame. Appends to stg. Returns 0 or error.
-static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<uint32_t> &recon_parallel,
-                       std::vector<std::vector<uint32_t>> &recon_steps, std::vector<std::vector<uint32_t>> &lf_steps)
+static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std::vector<uint32_t>> &pred_steps,
+                       std::vector<std::vector<uint32_t>> &lf_steps)
 {
     const vp9h_frame *f = fb.f;
     const int ss_h = fb.ss_h, ss_v = fb.ss_v, cols = fb.cols, rows = fb.rows;
     const int lossless = f->lossless;
+    const bool intra_frame = f->keyframe || f->intraonly;
     const uint16_t *eob = f->eobs;
     const uint16_t *eob_end = f->eobs + f->neobs;
     uint64_t coef = 0;                      // running element index within the frame's coefficients
@@ -284,7 +293,6 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<uin
         lf.frame = fb.frame_idx; lf.sbx = sbx; lf.sby = sby;
         pj.clear();
         memset(lmap, -1, sizeof(lmap));
-        bool has_intra = false;
 
         for (; bi < f->nblocks; bi++) {
             const vp9h_block *b = &f->blocks[bi];
@@ -293,7 +301,6 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<uin
             const int bw8 = vp9t_bwh[1][b->bs][0], bh8 = vp9t_bwh[1][b->bs][1];
             const int w4 = bw8 << 1, h4 = bh8 << 1;
             int end_x = std::min(2 * (cols - b->col), w4), end_y = std::min(2 * (rows - b->row), h4);
-            if (b->intra) has_intra = true;
 
             for (int p = 0; p < 3; p++) {
                 const int sh = p ? ss_h : 0, sv = p ? ss_v : 0;
@@ -310,8 +317,6 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<uin
                             if (eob >= eob_end) return VP9HIP_EINVALIDDATA;
                             e = *eob++;
                         }
-                        if (!b->intra && !e) continue;
-                        PendingJob q;
                         int mode = 0xff, txtp = 0;
                         if (b->intra) {
                             mode = p ? b->uvmode : b->mode[b->bs > VP9H_BS_8x8 && b->tx == 0 ? y * 2 + x : 0];
@@ -320,27 +325,45 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<uin
                         }
                         const int tcode = lossless ? 4 : txs;
                         if (e > (16 << (2 * txs))) return VP9HIP_EINVALIDDATA;
-                        q.plane = p; q.tcode = tcode; q.txtp = txtp; q.mode = mode;
-                        q.hr = (x < pw4 - 1) ? 1 : 0;
-                        q.x4 = ux_sb + x; q.y4 = uy_sb + y;
-                        q.eob = e;
-                        q.nzc = e ? g_nz[tcode][txtp][e][0] : 1;
-                        q.nzr = e ? g_nz[tcode][txtp][e][1] : 1;
-                        q.src = coef;
-                        coef += e;
-                        // dependency level within the SB plane
-                        int lvl = -1;
                         const int ux0 = ux_sb + x, uy0 = uy_sb + y, n4 = step;
-                        int8_t *lm = lmap[p];
-                        if (b->intra) {
-                            const int trx = (txs == 0 && q.hr) ? 1 : 0;
-                            if (uy0 > 0)
-                                for (int u = ux0 - 1; u < ux0 + n4 + trx; u++)
-                                    if (u >= 0 && u < units) lvl = std::max<int>(lvl, lm[(uy0 - 1) * 16 + u]);
-                            if (ux0 > 0)
-                                for (int v = uy0; v < uy0 + n4; v++)
-                                    if (v < units) lvl = std::max<int>(lvl, lm[v * 16 + ux0 - 1]);
+                        uint32_t roff = 0;
+                        if (e) {
+                            RJob r;
+                            memset(&r, 0, sizeof(r));
+                            r.coef = (uint32_t) (fb.coef_base + coef);
+                            r.eob = (uint16_t) e;
+                            r.frame = (uint16_t) fb.frame_idx;
+                            r.ptx = (uint8_t) (p | tcode << 2 | (b->intra ? 0 : 1) << 5 | txtp << 6);
+                            r.nzc = g_nz[tcode][txtp][e][0];
+                            r.nzr = g_nz[tcode][txtp][e][1];
+                            if (b->intra) {
+                                roff = (uint32_t) s.resid16;
+                                r.dst = roff;
+                                s.resid16 += (uint64_t) 1 << (2 * txs);
+                            } else {
+                                r.dst = (uint32_t) ((size_t) (by + y * 4) * fb.pitch[p ? 1 : 0] + bx + x * 4);
+                            }
+                            s.rbucket[tcode][txtp].push_back(r);
                         }
+                        coef += e;
+                        if (!b->intra) continue;
+                        // intra: prediction job, levelled by the pixels its edges read
+                        PendingJob q;
+                        q.j.ptx = (uint8_t) (p | txs << 2 | ((x < pw4 - 1) ? 1 : 0) << 4 | (e ? 1 : 0) << 5);
+                        q.j.mode = (uint8_t) mode;
+                        q.j.pos = (uint8_t) (ux0 | uy0 << 4);
+                        q.j.pad = 0;
+                        q.j.roff = roff;
+                        q.ts = txs;
+                        int lvl = -1;
+                        int8_t *lm = lmap[p];
+                        const int trx = (txs == 0 && (x < pw4 - 1)) ? 1 : 0;
+                        if (uy0 > 0)
+                            for (int u = ux0 - 1; u < ux0 + n4 + trx; u++)
+                                if (u >= 0 && u < units) lvl = std::max<int>(lvl, lm[(uy0 - 1) * 16 + u]);
+                        if (ux0 > 0)
+                            for (int v = uy0; v < uy0 + n4; v++)
+                                if (v < units) lvl = std::max<int>(lvl, lm[v * 16 + ux0 - 1]);
                         lvl += 1;
                         for (int v = uy0; v < uy0 + n4 && v < units; v++)
                             for (int u = ux0; u < ux0 + n4 && u < units; u++) lm[v * 16 + u] = (int8_t) lvl;
@@ -411,60 +434,37 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<uin
             }
         }
 
-        // group jobs into passes: same level and tx code, up to 64/n jobs; sorted by
-        // (level, tx, txtp, mode) so a pass runs few distinct code paths
+        // group intra jobs into passes: same level and size, up to 64/n jobs; sorted
+        // by (level, size, mode) so a pass runs few distinct predictor paths
         if (pj.size() > MAX_SB_JOBS) return VP9HIP_EINVALIDDATA;
-        std::stable_sort(pj.begin(), pj.end(), [](const PendingJob &a, const PendingJob &b) {
-            if (a.level != b.level) return a.level < b.level;
-            if (a.tcode != b.tcode) return a.tcode < b.tcode;
-            if (a.txtp != b.txtp) return a.txtp < b.txtp;
-            return a.mode < b.mode;
-        });
-        SBRec sr;
-        memset(&sr, 0, sizeof(sr));
-        sr.frame = fb.frame_idx; sr.sbx = sbx; sr.sby = sby;
-        sr.job0 = (uint32_t) s.jobs.size();
-        sr.pass0 = (uint32_t) s.passes.size();
-        sr.coef0 = (uint32_t) (s.coefs.size() / fb.coef_size);
-        sr.tile_x0 = (uint16_t) tile_x0;
-        sr.njobs = (uint16_t) pj.size();
-        sr.flags = f->keyframe || f->intraonly ? 0 : 1;
-        for (size_t k = 0; k < pj.size();) {
-            const int tcode = pj[k].tcode, n = 4 << (tcode & 3);
-            const int cap = n == 32 ? 1 : 64 / n;
-            size_t e = k + 1;
-            while (e < pj.size() && (int) (e - k) < cap && pj[e].level == pj[k].level && pj[e].tcode == tcode) e++;
-            s.passes.push_back((uint16_t) ((k << 7) | ((e - k - 1) << 3) | tcode));
-            k = e;
-        }
-        sr.npass = (uint16_t) (s.passes.size() - sr.pass0);
-        // jobs + their coefficients in pass order
-        uint32_t coff = 0;
-        for (auto &q : pj) {
-            TxJob j;
-            j.ptx = (uint8_t) (q.plane | q.tcode << 2 | q.hr << 5 | q.txtp << 6);
-            j.mode = (uint8_t) q.mode;
-            j.pos = (uint8_t) (q.x4 | q.y4 << 4);
-            j.nzc = (uint8_t) (q.nzc - 1);
-            j.ec = (uint32_t) q.eob | (uint32_t) (q.nzr - 1) << 11 | coff << 16;
-            if (q.eob) {
-                const size_t nb = (size_t) q.eob * fb.coef_size, dst = s.coefs.size();
-                s.coefs.resize(dst + nb);
-                memcpy(s.coefs.data() + dst, (const uint8_t *) f->coefs + q.src * fb.coef_size, nb);
+        if (!pj.empty()) {
+            std::stable_sort(pj.begin(), pj.end(), [](const PendingJob &a, const PendingJob &b) {
+                if (a.level != b.level) return a.level < b.level;
+                if (a.ts != b.ts) return a.ts < b.ts;
+                return a.j.mode < b.j.mode;
+            });
+            SBRec sr;
+            memset(&sr, 0, sizeof(sr));
+            sr.frame = fb.frame_idx; sr.sbx = sbx; sr.sby = sby;
+            sr.job0 = (uint32_t) s.pjobs.size();
+            sr.pass0 = (uint32_t) s.passes.size();
+            sr.tile_x0 = (uint16_t) tile_x0;
+            sr.njobs = (uint16_t) pj.size();
+            sr.flags = intra_frame ? 0 : 1;
+            for (size_t k = 0; k < pj.size();) {
+                const int ts = pj[k].ts, cap = 64 >> (ts + 2);
+                size_t e = k + 1;
+                while (e < pj.size() && (int) (e - k) < cap && pj[e].level == pj[k].level && pj[e].ts == ts) e++;
+                s.passes.push_back((uint16_t) ((k << 7) | ((e - k - 1) << 3) | ts));
+                k = e;
             }
-            coff += q.eob;
-            s.jobs.push_back(j);
-        }
-        uint32_t sbi = (uint32_t) s.sbs.size();
-        s.sbs.push_back(sr);
-        if (!pj.empty() || sr.flags == 0) {
-            if (has_intra) {
-                int d = (sbx - tile_sb0) + sby;
-                if ((int) recon_steps.size() <= d) recon_steps.resize(d + 1);
-                recon_steps[d].push_back(sbi);
-            } else {
-                recon_parallel.push_back(sbi);
-            }
+            sr.npass = (uint16_t) (s.passes.size() - sr.pass0);
+            for (auto &q : pj) s.pjobs.push_back(q.j);
+            uint32_t sbi = (uint32_t) s.sbs.size();
+            s.sbs.push_back(sr);
+            int d = (sbx - tile_sb0) + sby;
+            if ((int) pred_steps.size() <= d) pred_steps.resize(d + 1);
+            pred_steps[d].push_back(sbi);
         }
         if (f->filter_level) {
             uint32_t li = (uint32_t) s.lfs.size();
@@ -473,7 +473,6 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<uin
             if ((int) lf_steps.size() <= d) lf_steps.resize(d + 1);
             lf_steps[d].push_back(li);
         }
-        (void) has_intra;
     }
     if (eob != eob_end) return VP9HIP_EINVALIDDATA;
     if (coef != f->ncoefs) return VP9HIP_EINVALIDDATA;
@@ -487,15 +486,16 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     hipSetDevice(c->dev);
     HIPCHK(hipStreamSynchronize(c->st));      // the previous batch may still read the arena
     Staged &s = c->stg;
-    s.frames.clear(); s.sbs.clear(); s.jobs.clear(); s.passes.clear(); s.lfs.clear(); s.mcs.clear();
+    s.frames.clear(); s.sbs.clear(); s.pjobs.clear(); s.passes.clear(); s.lfs.clear(); s.mcs.clear();
+    s.rjobs.clear(); s.resid16 = 0;
+    for (auto &bt : s.rbucket) for (auto &bk : bt) bk.clear();
     s.lists.clear(); s.launches.clear(); s.coefs.clear();
     for (int k = 0; k < K_N; k++) s.alg_bytes[k] = 0;
     s.ready = false;
 
     const int csz = c->hb ? 4 : 2;
     init_nz();
-    std::vector<uint32_t> par;
-    std::vector<std::vector<uint32_t>> rsteps, lsteps;
+    std::vector<std::vector<uint32_t>> psteps, lsteps;
     uint64_t coef_base = 0;
     double pix_bytes = (double) c->w * c->h * c->bypp * (1.0 + 2.0 / ((1 << c->ss_h) * (1 << c->ss_v)));
     for (int i = 0; i < n; i++) {
@@ -531,38 +531,56 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
         fb.f = f; fb.frame_idx = i;
         fb.cols = c->cols; fb.rows = c->rows; fb.sb_cols = c->sb_cols; fb.sb_rows = c->sb_rows;
         fb.ss_h = c->ss_h; fb.ss_v = c->ss_v; fb.coef_size = csz;
+        fb.pitch[0] = c->pitch[0]; fb.pitch[1] = c->pitch[1];
         fb.coef_base = coef_base;
         size_t mc0 = s.mcs.size();
-        int r = build_frame(c, s, fb, par, rsteps, lsteps);
+        int r = build_frame(c, s, fb, psteps, lsteps);
         if (r < 0) return r;
         size_t cb = (size_t) f->ncoefs * csz;
+        size_t off = s.coefs.size();
+        s.coefs.resize(off + cb);
+        if (cb) memcpy(s.coefs.data() + off, f->coefs, cb);
         coef_base += f->ncoefs;
         if (coef_base > 0xffffffffull) return VP9HIP_ENOMEM;
-        // algorithmic bytes: recon writes P and reads C (+P for inter SBs),
+        // algorithmic bytes: reconstruction reads C and writes P (k_resid
+        // owns C, k_pred owns P; inter residuals read + write their pixels in k_resid),
         // LF reads + writes P, MC reads R*P and writes the predicted pixels
-        s.alg_bytes[K_RECON] += (double) cb + pix_bytes * (intra ? 1.0 : 2.0);
+        s.alg_bytes[K_RESID] += (double) cb;
+        if (intra) s.alg_bytes[K_PRED] += pix_bytes;
         if (f->filter_level) s.alg_bytes[K_LF] += 2.0 * pix_bytes;
         for (size_t m = mc0; m < s.mcs.size(); m++)
             s.alg_bytes[K_MC] += (double) s.mcs[m].w * s.mcs[m].h * c->bypp * (1 + s.mcs[m].nref);
     }
-    // launch schedule: MC, recon (parallel SBs, then the intra wavefront), LF wavefront
-    if (!s.mcs.empty()) s.launches.push_back({ K_MC, 0, (uint32_t) s.mcs.size() });
+    // residual jobs in (tx code, txtp) buckets; inter residual pixels are algorithmic
+    // reads + writes of k_resid
+    for (int t = 0; t < 5; t++) {
+        const uint32_t off = (uint32_t) s.rjobs.size();
+        for (int tp = 0; tp < 4; tp++) {
+            for (auto &r : s.rbucket[t][tp])
+                if (r.ptx & 32) s.alg_bytes[K_RESID] += 2.0 * (16 << (2 * (t & 3))) * c->bypp;
+            s.rjobs.insert(s.rjobs.end(), s.rbucket[t][tp].begin(), s.rbucket[t][tp].end());
+        }
+        if (s.rjobs.size() > off) s.launches.push_back({ K_RESID, off, (uint32_t) (s.rjobs.size() - off), t });
+    }
+    // launch schedule: MC, residuals, the intra SB wavefront, the LF wavefront
+    if (!s.mcs.empty()) s.launches.insert(s.launches.begin(), { K_MC, 0, (uint32_t) s.mcs.size(), 0 });
     auto add_list = [&](int kind, const std::vector<uint32_t> &v) {
         if (v.empty()) return;
-        s.launches.push_back({ kind, (uint32_t) s.lists.size(), (uint32_t) v.size() });
+        s.launches.push_back({ kind, (uint32_t) s.lists.size(), (uint32_t) v.size(), 0 });
         s.lists.insert(s.lists.end(), v.begin(), v.end());
     };
-    add_list(K_RECON, par);
-    for (auto &v : rsteps) add_list(K_RECON, v);
+    for (auto &v : psteps) add_list(K_PRED, v);
     for (auto &v : lsteps) add_list(K_LF, v);
+    if (s.resid16 > 0xffffffffull) return VP9HIP_ENOMEM;
 
     // upload into one arena
     auto al = [](size_t x) { return (x + 255) & ~(size_t) 255; };
     size_t o = 0;
     s.o_frames = o; o = al(o + s.frames.size() * sizeof(FrameDesc));
     s.o_sbs = o; o = al(o + s.sbs.size() * sizeof(SBRec));
-    s.o_jobs = o; o = al(o + s.jobs.size() * sizeof(TxJob));
+    s.o_pjobs = o; o = al(o + s.pjobs.size() * sizeof(PJob));
     s.o_passes = o; o = al(o + s.passes.size() * sizeof(uint16_t));
+    s.o_rjobs = o; o = al(o + s.rjobs.size() * sizeof(RJob));
     s.o_lfs = o; o = al(o + s.lfs.size() * sizeof(LFRec));
     s.o_mcs = o; o = al(o + s.mcs.size() * sizeof(McUnit));
     s.o_lists = o; o = al(o + s.lists.size() * sizeof(uint32_t));
@@ -574,14 +592,23 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
         if (hipMalloc(&s.arena, o) != hipSuccess) return VP9HIP_ENOMEM;
         s.arena_cap = o;
     }
+    const size_t rbytes = (size_t) s.resid16 * 32 + 256;
+    if (rbytes > s.resid_cap) {
+        if (s.resid) hipFree(s.resid);
+        s.resid = nullptr;
+        s.resid_cap = 0;
+        if (hipMalloc(&s.resid, rbytes) != hipSuccess) return VP9HIP_ENOMEM;
+        s.resid_cap = rbytes;
+    }
     auto up = [&](size_t off, const void *src, size_t bytes) -> int {
         if (!bytes) return 0;
         return hipMemcpyAsync(s.arena + off, src, bytes, hipMemcpyHostToDevice, c->st) == hipSuccess ? 0 : -1;
     };
     if (up(s.o_frames, s.frames.data(), s.frames.size() * sizeof(FrameDesc)) ||
         up(s.o_sbs, s.sbs.data(), s.sbs.size() * sizeof(SBRec)) ||
-        up(s.o_jobs, s.jobs.data(), s.jobs.size() * sizeof(TxJob)) ||
+        up(s.o_pjobs, s.pjobs.data(), s.pjobs.size() * sizeof(PJob)) ||
         up(s.o_passes, s.passes.data(), s.passes.size() * sizeof(uint16_t)) ||
+        up(s.o_rjobs, s.rjobs.data(), s.rjobs.size() * sizeof(RJob)) ||
         up(s.o_lfs, s.lfs.data(), s.lfs.size() * sizeof(LFRec)) ||
         up(s.o_mcs, s.mcs.data(), s.mcs.size() * sizeof(McUnit)) ||
         up(s.o_lists, s.lists.data(), s.lists.size() * sizeof(uint32_t)) ||
@@ -618,10 +645,14 @@ extern "C" int vp9hip_run_batch(vp9hip_ctx *c)
         case K_MC:
             r = vp9hip_launch_mc(c->hb, c->st, (int) L.n, (const McUnit *) (s.arena + s.o_mcs), fr);
             break;
-        case K_RECON:
-            r = vp9hip_launch_recon(c->hb, c->st, (int) L.n, lists + L.off, (const SBRec *) (s.arena + s.o_sbs),
-                                    (const TxJob *) (s.arena + s.o_jobs), (const uint16_t *) (s.arena + s.o_passes),
-                                    fr, s.arena + s.o_coefs);
+        case K_RESID:
+            r = vp9hip_launch_resid(c->hb, c->st, L.arg, (int) L.n, (const RJob *) (s.arena + s.o_rjobs) + L.off, fr,
+                                    s.arena + s.o_coefs, s.resid);
+            break;
+        case K_PRED:
+            r = vp9hip_launch_pred(c->hb, c->st, (int) L.n, lists + L.off, (const SBRec *) (s.arena + s.o_sbs),
+                                   (const PJob *) (s.arena + s.o_pjobs), (const uint16_t *) (s.arena + s.o_passes),
+                                   fr, s.resid);
             break;
         case K_LF:
             r = vp9hip_launch_lf(c->hb, c->st, (int) L.n, lists + L.off, (const LFRec *) (s.arena + s.o_lfs), fr);

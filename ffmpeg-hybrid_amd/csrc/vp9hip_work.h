@@ -25,45 +25,57 @@ typedef struct FrameDesc {
     int32_t  sharp;           /* LF sharpness                                         */
 } FrameDesc;
 
-/* One transform block job (8 bytes, so a whole SB's job list fits in LDS). */
-typedef struct TxJob {
-    uint8_t  ptx;             /* plane (2b) | tx << 2 (3b: 0..3, 4 = lossless WHT) |
-                                 have_right << 5 (vp9recon.c:47) | txtp << 6               */
-    uint8_t  mode;            /* intra mode before edge substitution; 0xff = residual only */
+/* Residual job (k_resid): one tx block with coefficients, 16 bytes. The residual
+ * (out + (1 << (bits - 1))) >> bits of itxfm_add (vp9dsp_template.c:1139-1180) depends
+ * on the coefficients only, so every tx block of a batch is transformed in parallel;
+ * intra residuals go to a scratch buffer (column-major n x n int16) that k_pred adds
+ * after prediction, inter residuals are added in place onto the MC prediction. */
+typedef struct RJob {
+    uint32_t coef;            /* element offset of the scan-order coefficients          */
+    uint32_t dst;             /* intra: residual offset / 16 (int16 elements);
+                                 inter: pixel offset y * pitch + x in plane of `frame`  */
+    uint16_t eob;
+    uint16_t frame;
+    uint8_t  ptx;             /* plane | tx code << 2 (0..3, 4 = WHT) | inplace << 5 | txtp << 6 */
+    uint8_t  nzc, nzr;        /* bounding box of scan[0 .. eob-1] (a zero column transforms to zero) */
+    uint8_t  pad;
+} RJob;
+
+#define RJ_PLANE(j) ((j).ptx & 3)
+#define RJ_INPLACE(j) (((j).ptx >> 5) & 1)
+#define RJ_TXTP(j) ((j).ptx >> 6)
+
+/* Intra prediction job (k_pred), 8 bytes, so a whole SB's list fits in LDS. */
+typedef struct PJob {
+    uint8_t  ptx;             /* plane | ts << 2 | have_right << 4 (vp9recon.c:47) | has_residual << 5 */
+    uint8_t  mode;            /* intra mode before edge substitution                       */
     uint8_t  pos;             /* x4 | y4 << 4: position inside the SB plane, 4-pixel units */
-    uint8_t  nzc;             /* columns that can be nonzero minus 1 (bounding box of
-                                 scan[0 .. eob-1]; a zero column transforms to zero)        */
-    uint32_t ec;              /* eob (11b) | (nzr - 1) << 11 (5b) | coefficient offset
-                                 relative to SBRec.coef0 << 16                             */
-} TxJob;
+    uint8_t  pad;
+    uint32_t roff;            /* residual offset / 16                                      */
+} PJob;
 
-#define JOB_PLANE(j) ((j).ptx & 3)
-#define JOB_TX(j) (((j).ptx >> 2) & 7)
-#define JOB_HR(j) (((j).ptx >> 5) & 1)
-#define JOB_TXTP(j) ((j).ptx >> 6)
-#define JOB_EOB(j) ((j).ec & 2047)
-#define JOB_NZR(j) ((((j).ec >> 11) & 31) + 1)
-#define JOB_NZC(j) ((j).nzc + 1)
-#define JOB_COFF(j) ((j).ec >> 16)
+#define PJ_PLANE(j) ((j).ptx & 3)
+#define PJ_TS(j) (((j).ptx >> 2) & 3)
+#define PJ_HR(j) (((j).ptx >> 4) & 1)
+#define PJ_RES(j) (((j).ptx >> 5) & 1)
 
-/* One superblock of reconstruction work. Its jobs are grouped into "passes": a pass
- * holds up to 64/n independent jobs (same dependency level, same tx code), so one
- * wavefront runs them side by side, n lanes (one per transform column) per job. */
+/* One superblock of intra work. Its jobs are grouped into "passes": a pass holds up
+ * to 64/n independent jobs (same dependency level, same tx size n), so one wavefront
+ * runs them side by side, one lane per pixel column. */
 typedef struct SBRec {
     uint32_t frame;
     uint16_t sbx, sby;
-    uint32_t job0;            /* first TxJob (jobs in pass order)                       */
+    uint32_t job0;            /* first PJob (jobs in pass order)                        */
     uint32_t pass0;           /* first pass word                                        */
-    uint32_t coef0;           /* first coefficient element (coefficients in job order)  */
     uint16_t npass, njobs;
     uint16_t tile_x0;         /* tile column start, 8x8 units (vp9.c:1244-1250)         */
     uint16_t flags;           /* bit0: load SB interior first (inter frame)             */
 } SBRec;
 
-/* pass word (u16): first job (relative to job0) << 7 | (njobs - 1) << 3 | tx code */
+/* pass word (u16): first job (relative to job0) << 7 | (njobs - 1) << 3 | ts */
 #define PASS_FIRST(w) ((w) >> 7)
 #define PASS_NJOBS(w) ((((w) >> 3) & 15) + 1)
-#define PASS_TX(w) ((w) & 7)
+#define PASS_TS(w) ((w) & 3)
 #define MAX_SB_JOBS 384
 
 /* Loop-filter data of one SB: VP9Filter (vp9dec.h:83-87) + position. */
