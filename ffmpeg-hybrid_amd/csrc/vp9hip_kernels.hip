@@ -875,6 +875,48 @@ DEV void lf_line(uint16_t *p, int s, int wd, int L, int sharp, int bd)
     }
 }
 
+// 8-pixel chunk <-> 8 uint16 of the LF tile (tile rows are 4-byte aligned)
+template <typename PIX> struct Chunk8;
+template <> struct Chunk8<uint8_t> {
+    typedef uint2 T;
+    static DEV T zero() { return make_uint2(0, 0); }
+    static DEV void to_lds(T v, uint16_t *t)
+    {
+        uint32_t *d = (uint32_t *) t;
+        d[0] = (v.x & 0xff) | ((v.x & 0xff00) << 8);
+        d[1] = ((v.x >> 16) & 0xff) | ((v.x >> 8) & 0xff0000);
+        d[2] = (v.y & 0xff) | ((v.y & 0xff00) << 8);
+        d[3] = ((v.y >> 16) & 0xff) | ((v.y >> 8) & 0xff0000);
+    }
+    static DEV T from_lds(const uint16_t *t)
+    {
+        const uint32_t *s = (const uint32_t *) t;
+        return make_uint2((s[0] & 0xff) | ((s[0] >> 8) & 0xff00) | ((s[1] & 0xff) << 16) | ((s[1] & 0xff0000) << 8),
+                          (s[2] & 0xff) | ((s[2] >> 8) & 0xff00) | ((s[3] & 0xff) << 16) | ((s[3] & 0xff0000) << 8));
+    }
+};
+template <> struct Chunk8<uint16_t> {
+    typedef uint4 T;
+    static DEV T zero() { return make_uint4(0, 0, 0, 0); }
+    static DEV void to_lds(T v, uint16_t *t)
+    {
+        uint32_t *d = (uint32_t *) t;
+        d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+    }
+    static DEV T from_lds(const uint16_t *t)
+    {
+        const uint32_t *s = (const uint32_t *) t;
+        return make_uint4(s[0], s[1], s[2], s[3]);
+    }
+};
+
+// chunk index -> (plane, tile row, chunk column): luma 72 rows x 9, then U, V 40 x 5
+DEV void lf_chunk(int ci, int &p, int &r, int &k)
+{
+    if (ci < 648) { p = 0; r = ci / 9; k = ci - r * 9; }
+    else { const int c = ci - 648; p = 1 + (c >= 200); const int cc = c - (p - 1) * 200; r = cc / 5; k = cc - r * 5; }
+}
+
 #define FLP 74           // luma LF tile pitch (72 used)
 #define FCP 42           // chroma LF tile pitch (40 used)
 
@@ -894,17 +936,29 @@ __global__ __launch_bounds__(128) void k_lf(const uint32_t *__restrict__ list, c
     if (tid < 64) lvl[tid] = rec.level[tid];
     if (tid < 128) ((uint8_t *) msk)[tid] = ((const uint8_t *) rec.mask)[tid];
 
-    // load: luma rows [y0-8, y0+64) x cols [x0-8, x0+64), chroma [-8, 32)
-    for (int p = 0; p < 3; p++) {
-        const int sz = p ? 32 : 64, tw = sz + 8, tpch = p ? FCP : FLP;
-        uint16_t *t = p ? ct[p - 1] : lt;
-        const PIX *g = (const PIX *) fd.plane[p];
-        const int pitch = fd.pitch[p ? 1 : 0];
-        const int x0 = sbx * sz - 8, y0 = sby * sz - 8;
-        for (int i = tid; i < tw * tw; i += 128) {
-            int yy = i / tw, xx = i - yy * tw;
-            int gx = x0 + xx, gy = y0 + yy;
-            t[yy * tpch + xx] = (gx >= 0 && gy >= 0) ? g[(size_t) gy * pitch + gx] : 0;
+    // load: luma rows [y0-8, y0+64) x cols [x0-8, x0+64), chroma [-8, 32), in aligned
+    // 8-pixel chunks (luma 72 x 9, chroma 2 x 40 x 5 = 1048 chunks, <= 9 per thread), all
+    // global loads of a thread in flight before its LDS writes
+    typedef typename Chunk8<PIX>::T CT;
+    CT v[9];
+#pragma unroll
+    for (int u = 0; u < 9; u++) {
+        const int ci = tid + u * 128;
+        int p, r, k;
+        lf_chunk(ci, p, r, k);
+        const int gx = (p ? sbx * 32 : sbx * 64) - 8 + 8 * k, gy = (p ? sby * 32 : sby * 64) - 8 + r;
+        v[u] = Chunk8<PIX>::zero();
+        if (ci < 1048 && gx >= 0 && gy >= 0)
+            v[u] = *(const CT *) ((const PIX *) fd.plane[p] + (size_t) gy * fd.pitch[p ? 1 : 0] + gx);
+    }
+#pragma unroll
+    for (int u = 0; u < 9; u++) {
+        const int ci = tid + u * 128;
+        int p, r, k;
+        lf_chunk(ci, p, r, k);
+        if (ci < 1048) {
+            uint16_t *t = p ? ct[p - 1] + r * FCP : lt + r * FLP;
+            Chunk8<PIX>::to_lds(v[u], t + 8 * k);
         }
     }
     __syncthreads();
@@ -983,19 +1037,18 @@ __global__ __launch_bounds__(128) void k_lf(const uint32_t *__restrict__ list, c
         }
     }
     __syncthreads();
-    // ---- store the modified region: rows [0,sz) x cols [-8,sz) and rows [-8,0) x cols [0,sz) ----
-    for (int p = 0; p < 3; p++) {
-        const int sz = p ? 32 : 64, tw = sz + 8, tpch = p ? FCP : FLP;
-        const uint16_t *t = p ? ct[p - 1] : lt;
-        PIX *g = (PIX *) fd.plane[p];
-        const int pitch = fd.pitch[p ? 1 : 0];
-        const int x0 = sbx * sz - 8, y0 = sby * sz - 8;
-        const int wlim = fd.w8[p ? 1 : 0], hlim = fd.h8[p ? 1 : 0];
-        for (int i = tid; i < tw * tw; i += 128) {
-            int yy = i / tw, xx = i - yy * tw;
-            if (yy < 8 && xx < 8) continue;
-            int gx = x0 + xx, gy = y0 + yy;
-            if (gx >= 0 && gy >= 0 && gx < wlim && gy < hlim) g[(size_t) gy * pitch + gx] = (PIX) t[yy * tpch + xx];
+    // ---- store the modified region: rows [0,sz) x cols [-8,sz) and rows [-8,0) x cols [0,sz).
+    // Other SBs of the same wavefront step never touch this region, so whole chunks are
+    // written back (pixels beyond the 8-aligned frame size are unchanged padding). ----
+#pragma unroll
+    for (int u = 0; u < 9; u++) {
+        const int ci = tid + u * 128;
+        int p, r, k;
+        lf_chunk(ci, p, r, k);
+        const int gx = (p ? sbx * 32 : sbx * 64) - 8 + 8 * k, gy = (p ? sby * 32 : sby * 64) - 8 + r;
+        if (ci < 1048 && gx >= 0 && gy >= 0 && (r >= 8 || k > 0)) {
+            const uint16_t *t = p ? ct[p - 1] + r * FCP : lt + r * FLP;
+            *(CT *) ((PIX *) fd.plane[p] + (size_t) gy * fd.pitch[p ? 1 : 0] + gx) = Chunk8<PIX>::from_lds(t + 8 * k);
         }
     }
 }

@@ -9,7 +9,7 @@ from collections import defaultdict
 
 
 def short(name):
-    for k in ("k_recon", "k_lf", "k_mc"):
+    for k in ("k_resid", "k_pred", "k_recon", "k_lf", "k_mc"):
         if k in name:
             return k
     return name[:40]
@@ -24,7 +24,7 @@ def main(d):
         for r in csv.DictReader(open(f)):
             acc[short(r["Kernel_Name"])]["duration_us"].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     for k, cs in sorted(acc.items()):
-        if k not in ("k_recon", "k_lf", "k_mc"):
+        if not k.startswith("k_"):
             continue
         print(k)
         for c, v in sorted(cs.items()):
