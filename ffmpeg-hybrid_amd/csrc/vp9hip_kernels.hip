@@ -557,10 +557,11 @@ __global__ __launch_bounds__(64 * RWAVES) void k_resid(const RJob *__restrict__ 
 // One wavefront predicts one 64x64 superblock (luma + 4:2:0 chroma) in LDS. The host
 // packs the SB's intra tx blocks into passes of independent jobs of one size (same
 // dependency level): 64/n jobs side by side, n lanes per job, lane = pixel column.
-// Each pass: edges (check_intra_mode, vp9recon.c:37-221) -> predictor
-// (vp9dsp_template.c:28-1106) -> + residual from k_resid -> clip. A tile's row 0 /
-// column 0 hold the pixels above / left of the SB; pixel (x, y) of plane p lives at
-// tile_p[(y + 1) * pitch_p + x + 1].
+// A pass is branch-free: edges are filled from host-resolved clamps (check_intra_mode,
+// vp9recon.c:37-221), every predictor pixel is one formula-table word
+// (vp9dsp_template.c:28-1106 restated per pixel), then + residual from k_resid, clip.
+// A tile's row 0 / column 0 hold the pixels above / left of the SB; pixel (x, y) of
+// plane p lives at tile_p[(y + 1) * pitch_p + x + 1].
 #define LP 68            // luma tile pitch (65 used)
 #define CP 36            // chroma tile pitch (33 used, 4:2:0)
 #define LT_SIZE (65 * LP)
@@ -570,12 +571,10 @@ __global__ __launch_bounds__(64 * RWAVES) void k_resid(const RJob *__restrict__ 
 struct RCol { uint4 a, b, c, d; };
 DEV uint32_t rword(const RCol &r, int k)
 {
-    switch (k) {
-    case 0: return r.a.x; case 1: return r.a.y; case 2: return r.a.z; case 3: return r.a.w;
-    case 4: return r.b.x; case 5: return r.b.y; case 6: return r.b.z; case 7: return r.b.w;
-    case 8: return r.c.x; case 9: return r.c.y; case 10: return r.c.z; case 11: return r.c.w;
-    case 12: return r.d.x; case 13: return r.d.y; case 14: return r.d.z; default: return r.d.w;
-    }
+    return k == 0 ? r.a.x : k == 1 ? r.a.y : k == 2 ? r.a.z : k == 3 ? r.a.w :
+           k == 4 ? r.b.x : k == 5 ? r.b.y : k == 6 ? r.b.z : k == 7 ? r.b.w :
+           k == 8 ? r.c.x : k == 9 ? r.c.y : k == 10 ? r.c.z : k == 11 ? r.c.w :
+           k == 12 ? r.d.x : k == 13 ? r.d.y : k == 14 ? r.d.z : r.d.w;
 }
 
 // load this lane's residual column of the job it serves in pass word w
@@ -592,25 +591,6 @@ DEV void fetch_resid(int w, int lane, const PJob *lj, const int16_t *__restrict_
     if (ts == 3) { rv.c = s[2]; rv.d = s[3]; }
 }
 
-#define PCASE(m) case m: for (int y = 0; y < N; y++) o[y * tpch + x] = (PIX) pred_px(m, N, x, y, e, dc, bd); break;
-// predictor column x of an N x N block into the tile, then + residual, clipped
-template <int N, typename PIX>
-DEV void pred_col(int mode, int x, const uint16_t *e, int dc, int bd, bool has_res, const RCol &rv,
-                  PIX *o, int tpch)
-{
-    switch (mode) {
-    PCASE(0) PCASE(1) PCASE(3) PCASE(4) PCASE(5) PCASE(6) PCASE(7) PCASE(8) PCASE(9)
-    default:
-        for (int y = 0; y < N; y++) o[y * tpch + x] = (PIX) dc;
-    }
-    if (has_res) {
-#pragma unroll
-        for (int y = 0; y < N; y++)
-            o[y * tpch + x] = (PIX) clipbd(o[y * tpch + x] + (int) (int16_t) (rword(rv, y >> 1) >> ((y & 1) * 16)), bd);
-    }
-}
-#undef PCASE
-
 // Load the pixels above / left of an SB (and, for inter frames, its interior: the
 // MC prediction + inter residuals) into the LDS tile. All global loads of a batch are
 // issued before any LDS write so their latencies overlap.
@@ -620,7 +600,6 @@ DEV void load_sb_tile(const FrameDesc &fd, int sbx, int sby, bool interior, int 
     const PIX *gy = (const PIX *) fd.plane[0], *gu = (const PIX *) fd.plane[1], *gv = (const PIX *) fd.plane[2];
     const int py = fd.pitch[0], pc = fd.pitch[1];
     const int lx = sbx * 64, ly = sby * 64, cx = sbx * 32, cy = sby * 32;
-    // borders: luma top (65), luma left (64), chroma top (33 + 33), chroma left (32 + 32)
     // lanes 0..32 read U top x = -1..31, lanes 33..63 V top x = -1..29, lanes 0..1 V x = 30..31
     PIX v0 = 0, v1 = 0, v2 = 0, v3 = 0, v4 = 0, v5 = 0;
     const bool top = ly > 0, left = lx > 0;
@@ -669,10 +648,72 @@ DEV void load_sb_tile(const FrameDesc &fd, int sbx, int sby, bool interior, int 
     }
 }
 
+// One pass of N x N jobs: lane li of group grp predicts column li of its job.
+template <int N, typename PIX>
+DEV void pred_pass(const PJob &jb, bool act, int li, int grp, PIX *tile, uint16_t *eb, int bd,
+                   const RCol &rv, const uint32_t *__restrict__ ptab)
+{
+    constexpr int TS = N == 4 ? 0 : N == 8 ? 1 : N == 16 ? 2 : 3;
+    constexpr int TOFF = N == 4 ? 0 : N == 8 ? 16 : N == 16 ? 80 : 336;
+    const int p = PJ_PLANE(jb);
+    const int tpch = p ? CP : LP;
+    PIX *o = tile + (p == 0 ? 0 : p == 1 ? LT_SIZE : LT_SIZE + CT_SIZE) + (PJ_Y4(jb) * 4 + 1) * tpch + PJ_X4(jb) * 4 + 1;
+    const int ms = PJ_MSLOT(jb);
+    // formula words of this column (L1/L2-resident table), issued first
+    uint32_t f[N];
+    const uint32_t *tb = ptab + (ms < 9 ? ms : 9) * PTAB_SLOT + TOFF + li;
+#pragma unroll
+    for (int y = 0; y < N; y++) f[y] = act ? tb[y * N] : 0;
+
+    // edges, branch-free (fills: vp9recon.c:103-210)
+    const int base = 128 << (bd - 8);
+    const int htop = PJ_HTOP(jb), hleft = PJ_HLEFT(jb), ct = PJ_CT(jb), cl = PJ_CL(jb);
+    const int tv = htop ? (int) o[-tpch + (li < ct ? li : ct)] : base - 1;
+    const int lr = N - 1 - li < cl ? N - 1 - li : cl;
+    const int lv = hleft ? (int) o[lr * tpch - 1] : base + 1;
+    uint16_t *e = eb + grp * (2 * N + 8);
+    if (act) {
+        e[li] = lv;
+        e[N + 1 + li] = tv;
+        if (N == 4) e[N + 5 + li] = htop ? (PJ_TRREAL(jb) ? o[-tpch + 4 + li] : o[-tpch + ct]) : base - 1;
+        if (li == 0) e[N] = (hleft && htop) ? o[-tpch - 1] : base + (htop ? 1 : -1);
+    }
+    // DC sums over the group's N lanes
+    int sl = lv, st = tv;
+#pragma unroll
+    for (int m = 1; m < N; m <<= 1) { sl += __shfl_xor(sl, m); st += __shfl_xor(st, m); }
+    const int dc = ms == 9 ? (sl + st + N) >> (TS + 3) : ms == 10 ? (sl + (N >> 1)) >> (TS + 2) :
+                   ms == 11 ? (st + (N >> 1)) >> (TS + 2) : ms == 12 ? base : ms == 13 ? base - 1 : base + 1;
+    wave_sync();
+    if (act) {
+        const int mx = (1 << bd) - 1;
+        const bool hr = PJ_RES(jb);
+#pragma unroll
+        for (int y = 0; y < N; y++) {
+            const uint32_t w = f[y];
+            int v;
+            if (w >> 27) v = dc;
+            else {
+                const int a = e[w & 127], b = e[(w >> 7) & 127], c = e[(w >> 14) & 127];
+                const int wb = (w >> 21) & 3, wc = (w >> 23) & 3, s = (w >> 25) & 3;
+                v = (a + wb * b + (wc == 2 ? -c : wc * c) + ((1 << s) >> 1)) >> s;
+                v = v < 0 ? 0 : v > mx ? mx : v;
+            }
+            if (hr) {
+                const int r = (int16_t) (rword(rv, y >> 1) >> ((y & 1) * 16));
+                v += r;
+                v = v < 0 ? 0 : v > mx ? mx : v;
+            }
+            o[y * tpch + li] = (PIX) v;
+        }
+    }
+}
+
 template <typename PIX>
 __global__ __launch_bounds__(64) void k_pred(const uint32_t *__restrict__ list, const SBRec *__restrict__ sbs,
                                              const PJob *__restrict__ jobs, const uint16_t *__restrict__ passes,
-                                             const FrameDesc *__restrict__ frames, const int16_t *__restrict__ resid)
+                                             const FrameDesc *__restrict__ frames, const int16_t *__restrict__ resid,
+                                             const uint32_t *__restrict__ ptab)
 {
     __shared__ PIX tile[LT_SIZE + 2 * CT_SIZE];
     __shared__ uint16_t eb[256];               // per job 2n+8 edge pixels
@@ -683,8 +724,6 @@ __global__ __launch_bounds__(64) void k_pred(const uint32_t *__restrict__ list, 
     const FrameDesc &fd = frames[sb.frame];
     const int lane = threadIdx.x;
     const int bd = fd.bd;
-#define TPL(p) (tile + ((p) == 0 ? 0 : (p) == 1 ? LT_SIZE : LT_SIZE + CT_SIZE))
-#define TPCH(p) ((p) ? CP : LP)
 
     // ---- prologue: job list, pass words, SB neighbourhood (pre-loop-filter pixels) ----
     for (int i = lane; i < sb.njobs; i += 64) lj[i] = jobs[sb.job0 + i];
@@ -700,90 +739,16 @@ __global__ __launch_bounds__(64) void k_pred(const uint32_t *__restrict__ list, 
 
     for (int pi = 0; pi < npass; pi++) {
         const int w = __builtin_amdgcn_readfirstlane(lp[pi]);
-        if (pi + 1 < npass) fetch_resid(lp[pi + 1], lane, lj, resid, rvn);   // prefetch
-
-        const int ts = PASS_TS(w), n = 4 << ts, lg = ts + 2;
-        const int grp = lane >> lg, li = lane & (n - 1);
+        if (pi + 1 < npass) fetch_resid(lp[pi + 1], lane, lj, resid, rvn);   // prefetch the next pass
+        const int ts = PASS_TS(w), lg = ts + 2;
+        const int grp = lane >> lg, li = lane & ((1 << lg) - 1);
         const bool act = grp < PASS_NJOBS(w);
         const PJob jb = lj[PASS_FIRST(w) + (act ? grp : 0)];
-        const int p = PJ_PLANE(jb);
-        PIX *t = TPL(p);
-        const int tpch = TPCH(p);
-        const int px = (jb.pos & 15) * 4, py = (jb.pos >> 4) * 4;
-        PIX *o = t + (py + 1) * tpch + px + 1;
-
-        // ---- edges: check_intra_mode (vp9recon.c:37-221) ----
-        uint16_t *e = eb + grp * (2 * n + 8);
-        int mode = jb.mode;
-        const int base = 128 << (bd - 8);
-        if (act) {
-            const int sz = p ? 32 : 64;
-            const int gx = sb.sbx * sz + px, gy = sb.sby * sz + py;
-            const int tile_x0 = p ? sb.tile_x0 * 4 : sb.tile_x0 * 8;
-            const int have_top = gy > 0, have_left = gx > tile_x0, have_right = PJ_HR(jb);
-            const int have_t = fd.w8[p ? 1 : 0] - gx, have_l = fd.h8[p ? 1 : 0] - gy;
-            switch (mode) {            // mode_conv[mode][have_left][have_top]
-            case 0: if (!have_top) mode = 13; break;
-            case 1: if (!have_left) mode = 14; break;
-            case 2: mode = have_left ? (have_top ? 2 : 10) : (have_top ? 11 : 12); break;
-            case 3: case 7: if (!have_top) mode = 13; break;
-            case 8: if (!have_left) mode = 14; break;
-            case 9: mode = have_left ? (have_top ? 9 : 1) : (have_top ? 0 : 14); break;
-            default: break;
-            }
-            const bool need_top = mode == 0 || mode == 2 || mode == 3 || mode == 4 || mode == 5 ||
-                                  mode == 6 || mode == 7 || mode == 9 || mode == 11;
-            const bool need_left = mode == 1 || mode == 2 || mode == 4 || mode == 5 || mode == 6 ||
-                                   mode == 8 || mode == 9 || mode == 10;
-            const bool need_tl = mode == 4 || mode == 5 || mode == 6 || mode == 9;
-            const bool need_tr = mode == 3 || mode == 7;
-            uint16_t *T_ = e + n + 1;
-            if (need_top) {
-                T_[li] = !have_top ? base - 1 : o[-tpch + (li < have_t ? li : have_t - 1)];
-                if (ts == 0 && need_tr) {
-                    int v;
-                    if (have_top && have_right && 8 <= have_t) v = o[-tpch + 4 + li];
-                    else if (!have_top) v = base - 1;
-                    else v = o[-tpch + (3 < have_t ? 3 : have_t - 1)];
-                    T_[4 + li] = v;
-                }
-                if (need_tl && li == 0)
-                    T_[-1] = (have_left && have_top) ? o[-tpch - 1] : base + (have_top ? 1 : -1);
-            }
-            if (need_left) {
-                int v;
-                if (!have_left) v = base + 1;
-                else if (mode == 8) v = o[(li < have_l ? li : have_l - 1) * tpch - 1];
-                else {
-                    const int i = n - 1 - li;
-                    v = o[(i < have_l ? i : have_l - 1) * tpch - 1];
-                }
-                e[li] = v;
-            }
-        }
-        wave_sync();
-        if (act) {
-            const uint16_t *T_ = e + n + 1;
-            int dc = 0;
-            if (mode == 2) {
-                int sum = 0; for (int i = 0; i < n; i++) sum += e[i] + T_[i];
-                dc = (sum + n) >> (ts + 3);
-            } else if (mode == 10) {
-                int sum = 0; for (int i = 0; i < n; i++) sum += e[i];
-                dc = (sum + (n >> 1)) >> (ts + 2);
-            } else if (mode == 11) {
-                int sum = 0; for (int i = 0; i < n; i++) sum += T_[i];
-                dc = (sum + (n >> 1)) >> (ts + 2);
-            } else if (mode >= 12) {
-                dc = base + (mode == 13 ? -1 : mode == 14 ? 1 : 0);
-            }
-            const bool hr = PJ_RES(jb);
-            switch (ts) {
-            case 0: pred_col<4, PIX>(mode, li, e, dc, bd, hr, rv, o, tpch); break;
-            case 1: pred_col<8, PIX>(mode, li, e, dc, bd, hr, rv, o, tpch); break;
-            case 2: pred_col<16, PIX>(mode, li, e, dc, bd, hr, rv, o, tpch); break;
-            default: pred_col<32, PIX>(mode, li, e, dc, bd, hr, rv, o, tpch); break;
-            }
+        switch (ts) {
+        case 0: pred_pass<4, PIX>(jb, act, li, grp, tile, eb, bd, rv, ptab); break;
+        case 1: pred_pass<8, PIX>(jb, act, li, grp, tile, eb, bd, rv, ptab); break;
+        case 2: pred_pass<16, PIX>(jb, act, li, grp, tile, eb, bd, rv, ptab); break;
+        default: pred_pass<32, PIX>(jb, act, li, grp, tile, eb, bd, rv, ptab); break;
         }
         wave_sync();
         rv = rvn;
@@ -795,15 +760,13 @@ __global__ __launch_bounds__(64) void k_pred(const uint32_t *__restrict__ list, 
         PIX *g = (PIX *) fd.plane[p];
         const int pitch = fd.pitch[p ? 1 : 0];
         const int x0 = sb.sbx * sz, y0 = sb.sby * sz;
-        const PIX *t = TPL(p);
-        const int tpch = TPCH(p);
+        const PIX *t = tile + (p == 0 ? 0 : p == 1 ? LT_SIZE : LT_SIZE + CT_SIZE);
+        const int tpch = p ? CP : LP;
         for (int i = lane; i < sz * sz; i += 64) {
             const int yy = i / sz, xx = i - yy * sz;
             g[(size_t) (y0 + yy) * pitch + x0 + xx] = t[(yy + 1) * tpch + xx + 1];
         }
     }
-#undef TPL
-#undef TPCH
 }
 
 // --------------------------------------------------------------- k_lf
@@ -1148,11 +1111,12 @@ int vp9hip_launch_resid(int hb, hipStream_t st, int tcode, int n, const RJob *jo
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int vp9hip_launch_pred(int hb, hipStream_t st, int nsb, const uint32_t *list, const SBRec *sbs,
-                       const PJob *jobs, const uint16_t *passes, const FrameDesc *frames, const int16_t *resid)
+                       const PJob *jobs, const uint16_t *passes, const FrameDesc *frames, const int16_t *resid,
+                       const uint32_t *ptab)
 {
     if (nsb <= 0) return 0;
-    if (hb) hipLaunchKernelGGL(k_pred<uint16_t>, dim3(nsb), dim3(64), 0, st, list, sbs, jobs, passes, frames, resid);
-    else    hipLaunchKernelGGL(k_pred<uint8_t>, dim3(nsb), dim3(64), 0, st, list, sbs, jobs, passes, frames, resid);
+    if (hb) hipLaunchKernelGGL(k_pred<uint16_t>, dim3(nsb), dim3(64), 0, st, list, sbs, jobs, passes, frames, resid, ptab);
+    else    hipLaunchKernelGGL(k_pred<uint8_t>, dim3(nsb), dim3(64), 0, st, list, sbs, jobs, passes, frames, resid, ptab);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int vp9hip_launch_lf(int hb, hipStream_t st, int nsb, const uint32_t *list, const LFRec *recs,

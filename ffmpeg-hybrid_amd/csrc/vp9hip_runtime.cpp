@@ -34,7 +34,8 @@ extern "C" {
 int vp9hip_launch_resid(int hb, hipStream_t st, int tcode, int n, const RJob *jobs, const FrameDesc *frames,
                         const void *coefs, int16_t *resid);
 int vp9hip_launch_pred(int hb, hipStream_t st, int nsb, const uint32_t *list, const SBRec *sbs,
-                       const PJob *jobs, const uint16_t *passes, const FrameDesc *frames, const int16_t *resid);
+                       const PJob *jobs, const uint16_t *passes, const FrameDesc *frames, const int16_t *resid,
+                       const uint32_t *ptab);
 int vp9hip_launch_lf(int hb, hipStream_t st, int nsb, const uint32_t *list, const LFRec *recs,
                      const FrameDesc *frames);
 int vp9hip_launch_mc(int hb, hipStream_t st, int n, const McUnit *units, const FrameDesc *frames);
@@ -84,6 +85,7 @@ struct vp9hip_ctx {
     int pitch[2] = { 0, 0 };
     size_t plane_off[3] = { 0, 0, 0 }, buf_bytes = 0;
     std::vector<uint8_t *> bufs;
+    uint32_t *ptab = nullptr;           // intra predictor formula table (device)
     Staged stg;
     // timing of the last run
     bool timing = true;
@@ -124,9 +126,83 @@ extern "C" void vp9hip_close(vp9hip_ctx *c)
     free_bufs(c);
     if (c->stg.arena) hipFree(c->stg.arena);
     if (c->stg.resid) hipFree(c->stg.resid);
+    if (c->ptab) hipFree(c->ptab);
     for (auto e : c->ev) hipEventDestroy(e);
     hipStreamDestroy(c->st);
     delete c;
+}
+
+// --------------------------------------------------------------------------
+// Intra predictor formula table (vp9dsp_template.c:28-1106 restated per pixel). Edge
+// array e: e[0..n) left column bottom-to-top, e[n] top-left, e[n+1 ..] top row with the
+// 4x4 top-right. Kinds: copy, avg2 (a+b+1)>>1, avg3 (a+2b+c+2)>>2, avg31 (a+3b+2)>>2,
+// tm clip(a+b-c), dc.
+enum { PF_COPY, PF_AVG2, PF_AVG3, PF_AVG31, PF_TM, PF_DC };
+static uint32_t pf_enc(int kind, int i0 = 0, int i1 = 0, int i2 = 0)
+{
+    static const int wb[6] = { 0, 1, 2, 3, 1, 0 }, wc[6] = { 0, 0, 1, 0, 2, 0 }, sh[6] = { 0, 1, 2, 2, 0, 0 };
+    return (uint32_t) i0 | (uint32_t) i1 << 7 | (uint32_t) i2 << 14 | (uint32_t) wb[kind] << 21 |
+           (uint32_t) wc[kind] << 23 | (uint32_t) sh[kind] << 25 | (uint32_t) (kind == PF_DC) << 27;
+}
+static uint32_t pix_formula(int slot, int n, int x, int y)
+{
+    const int T = n + 1, h = n >> 1;        // T[k] = e[T + k]; HU left top-to-bottom L[i] = e[n - 1 - i]
+    switch (slot) {
+    case 0: return pf_enc(PF_COPY, T + x);                                       // VERT
+    case 1: return pf_enc(PF_COPY, n - 1 - y);                                   // HOR
+    case 8: return pf_enc(PF_TM, T + x, n - 1 - y, n);                           // TM_VP8
+    case 2: {                                                                    // DIAG_DOWN_LEFT
+        const int k = x + y;
+        if (n == 4) return k < 6 ? pf_enc(PF_AVG3, T + k, T + k + 1, T + k + 2) : pf_enc(PF_COPY, T + 7);
+        if (k < n - 2) return pf_enc(PF_AVG3, T + k, T + k + 1, T + k + 2);
+        if (k == n - 2) return pf_enc(PF_AVG31, T + n - 2, T + n - 1);
+        return pf_enc(PF_COPY, T + n - 1);
+    }
+    case 3: { const int j = n - 1 - y + x; return pf_enc(PF_AVG3, j, j + 1, j + 2); }   // DIAG_DOWN_RIGHT
+    case 4: {                                                                    // VERT_RIGHT
+        const int m = h - 1 - (y >> 1) + x;
+        if (!(y & 1)) {
+            if (m <= h - 2) return pf_enc(PF_AVG3, 2 * m + 2, 2 * m + 3, 2 * m + 4);
+            return pf_enc(PF_AVG2, n + m - h + 1, n + m - h + 2);
+        }
+        if (m <= h - 2) return pf_enc(PF_AVG3, 2 * m + 1, 2 * m + 2, 2 * m + 3);
+        return pf_enc(PF_AVG3, n + m - h, n + m - h + 1, n + m - h + 2);
+    }
+    case 5: {                                                                    // HOR_DOWN
+        const int m = 2 * n - 2 - 2 * y + x;
+        if (m >= 2 * n) { const int i = m - 2 * n; return pf_enc(PF_AVG3, n + i, n + i + 1, n + i + 2); }
+        const int i = m >> 1;
+        return (m & 1) ? pf_enc(PF_AVG3, i, i + 1, i + 2) : pf_enc(PF_AVG2, i, i + 1);
+    }
+    case 6: {                                                                    // VERT_LEFT
+        const int k = (y >> 1) + x;
+        if (n == 4) return (y & 1) ? pf_enc(PF_AVG3, T + k, T + k + 1, T + k + 2) : pf_enc(PF_AVG2, T + k, T + k + 1);
+        if (x >= n - (y >> 1) - 1) return pf_enc(PF_COPY, T + n - 1);
+        if (!(y & 1)) return pf_enc(PF_AVG2, T + k, T + k + 1);
+        return k < n - 2 ? pf_enc(PF_AVG3, T + k, T + k + 1, T + k + 2) : pf_enc(PF_AVG31, T + n - 2, T + n - 1);
+    }
+    case 7: {                                                                    // HOR_UP
+        auto L = [n](int i) { return n - 1 - i; };
+        if (y >= h && x >= 2 * n - 2 - 2 * y) return pf_enc(PF_COPY, L(n - 1));
+        const int m = 2 * y + x, i = m >> 1;
+        if (!(m & 1)) return pf_enc(PF_AVG2, L(i), L(i + 1));
+        return i < n - 2 ? pf_enc(PF_AVG3, L(i), L(i + 1), L(i + 2)) : pf_enc(PF_AVG31, L(n - 2), L(n - 1));
+    }
+    default: return pf_enc(PF_DC);
+    }
+}
+static int upload_ptab(vp9hip_ctx *c)
+{
+    if (c->ptab) return 0;
+    std::vector<uint32_t> t(PTAB_SIZE);
+    for (int slot = 0; slot < 10; slot++)
+        for (int ts = 0, off = 0; ts < 4; off += 16 << (2 * ts), ts++) {
+            const int n = 4 << ts;
+            for (int y = 0; y < n; y++)
+                for (int x = 0; x < n; x++) t[slot * PTAB_SLOT + off + y * n + x] = pix_formula(slot, n, x, y);
+        }
+    if (hipMalloc(&c->ptab, t.size() * 4) != hipSuccess) return VP9HIP_ENOMEM;
+    return hipMemcpy(c->ptab, t.data(), t.size() * 4, hipMemcpyHostToDevice) == hipSuccess ? 0 : VP9HIP_EEXTERNAL;
 }
 
 extern "C" int vp9hip_configure(vp9hip_ctx *c, int width, int height, int bpp, int ss_h, int ss_v, int nbufs)
@@ -155,6 +231,8 @@ extern "C" int vp9hip_configure(vp9hip_ctx *c, int width, int height, int bpp, i
         c->bufs.push_back(b);
     }
     c->stg.ready = false;
+    int r = upload_ptab(c);
+    if (r) return r;
     return hipStreamSynchronize(c->st) == hipSuccess ? 0 : VP9HIP_EEXTERNAL;
 }
 
@@ -347,13 +425,34 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
                         }
                         coef += e;
                         if (!b->intra) continue;
-                        // intra: prediction job, levelled by the pixels its edges read
+                        // intra: prediction job, levelled by the pixels its edges read; the
+                        // edge availability of check_intra_mode (vp9recon.c:37-221) is resolved here
                         PendingJob q;
-                        q.j.ptx = (uint8_t) (p | txs << 2 | ((x < pw4 - 1) ? 1 : 0) << 4 | (e ? 1 : 0) << 5);
-                        q.j.mode = (uint8_t) mode;
-                        q.j.pos = (uint8_t) (ux0 | uy0 << 4);
-                        q.j.pad = 0;
-                        q.j.roff = roff;
+                        {
+                            const int n = 4 << txs;
+                            const int gx = bx + x * 4, gy = by + y * 4;      // plane pixel position
+                            const int tx0 = p ? tile_x0 * 8 >> ss_h : tile_x0 * 8;
+                            const int have_top = gy > 0, have_left = gx > tx0, have_right = x < pw4 - 1;
+                            const int have_t = (p ? cols * 8 >> ss_h : cols * 8) - gx;
+                            const int have_l = (p ? rows * 8 >> ss_v : rows * 8) - gy;
+                            int m = mode;
+                            switch (m) {            // mode_conv[mode][have_left][have_top] (vp9recon.c:49-87)
+                            case 0: if (!have_top) m = 13; break;
+                            case 1: if (!have_left) m = 14; break;
+                            case 2: m = have_left ? (have_top ? 2 : 10) : (have_top ? 11 : 12); break;
+                            case 3: case 7: if (!have_top) m = 13; break;
+                            case 8: if (!have_left) m = 14; break;
+                            case 9: m = have_left ? (have_top ? 9 : 1) : (have_top ? 0 : 14); break;
+                            default: break;
+                            }
+                            static const uint8_t slot_of[15] = { 0, 1, 9, 2, 3, 4, 5, 6, 7, 8, 10, 11, 12, 13, 14 };
+                            const int ct = std::min(n, have_t) - 1, cl = std::min(n, have_l) - 1;
+                            const int trreal = txs == 0 && have_top && have_right && have_t >= 8;
+                            q.j.a = (uint32_t) p | (uint32_t) txs << 2 | (uint32_t) (e ? 1 : 0) << 4 | (uint32_t) trreal << 5 |
+                                    (uint32_t) have_top << 6 | (uint32_t) have_left << 7 | (uint32_t) slot_of[m] << 8 |
+                                    (uint32_t) ux0 << 12 | (uint32_t) uy0 << 16 | (uint32_t) ct << 20 | (uint32_t) cl << 25;
+                            q.j.roff = roff;
+                        }
                         q.ts = txs;
                         int lvl = -1;
                         int8_t *lm = lmap[p];
@@ -441,7 +540,7 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
             std::stable_sort(pj.begin(), pj.end(), [](const PendingJob &a, const PendingJob &b) {
                 if (a.level != b.level) return a.level < b.level;
                 if (a.ts != b.ts) return a.ts < b.ts;
-                return a.j.mode < b.j.mode;
+                return ((a.j.a >> 8) & 15) < ((b.j.a >> 8) & 15);
             });
             SBRec sr;
             memset(&sr, 0, sizeof(sr));
@@ -652,7 +751,7 @@ extern "C" int vp9hip_run_batch(vp9hip_ctx *c)
         case K_PRED:
             r = vp9hip_launch_pred(c->hb, c->st, (int) L.n, lists + L.off, (const SBRec *) (s.arena + s.o_sbs),
                                    (const PJob *) (s.arena + s.o_pjobs), (const uint16_t *) (s.arena + s.o_passes),
-                                   fr, s.resid);
+                                   fr, s.resid, c->ptab);
             break;
         case K_LF:
             r = vp9hip_launch_lf(c->hb, c->st, (int) L.n, lists + L.off, (const LFRec *) (s.arena + s.o_lfs), fr);

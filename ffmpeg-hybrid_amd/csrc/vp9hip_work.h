@@ -45,19 +45,38 @@ typedef struct RJob {
 #define RJ_INPLACE(j) (((j).ptx >> 5) & 1)
 #define RJ_TXTP(j) ((j).ptx >> 6)
 
-/* Intra prediction job (k_pred), 8 bytes, so a whole SB's list fits in LDS. */
+/* Intra prediction job (k_pred), 8 bytes, so a whole SB's list fits in LDS. The host
+ * resolves check_intra_mode (vp9recon.c:37-221) ahead of time: the final mode after
+ * mode_conv and the edge clamps n_px_have (vp9recon.c:103,192) are stored, so the
+ * kernel's edge fill is branch-free.
+ *   a:  plane (2b) | ts << 2 (2b) | has_residual << 4 | top_right_real << 5 |
+ *       have_top << 6 | have_left << 7 | mslot << 8 (4b) | x4 << 12 | y4 << 16 |
+ *       ct << 20 (5b: last valid top column) | cl << 25 (5b: last valid left row)
+ *   mslot: 0 V, 1 H, 2 DL, 3 DR, 4 VR, 5 HD, 6 VL, 7 HU, 8 TM, 9 DC, 10 LEFT_DC,
+ *          11 TOP_DC, 12 DC_128, 13 DC_127, 14 DC_129 */
 typedef struct PJob {
-    uint8_t  ptx;             /* plane | ts << 2 | have_right << 4 (vp9recon.c:47) | has_residual << 5 */
-    uint8_t  mode;            /* intra mode before edge substitution                       */
-    uint8_t  pos;             /* x4 | y4 << 4: position inside the SB plane, 4-pixel units */
-    uint8_t  pad;
-    uint32_t roff;            /* residual offset / 16                                      */
+    uint32_t a;
+    uint32_t roff;            /* residual offset / 16 (absolute in the batch)              */
 } PJob;
 
-#define PJ_PLANE(j) ((j).ptx & 3)
-#define PJ_TS(j) (((j).ptx >> 2) & 3)
-#define PJ_HR(j) (((j).ptx >> 4) & 1)
-#define PJ_RES(j) (((j).ptx >> 5) & 1)
+#define PJ_PLANE(j) ((j).a & 3)
+#define PJ_TS(j) (((j).a >> 2) & 3)
+#define PJ_RES(j) (((j).a >> 4) & 1)
+#define PJ_TRREAL(j) (((j).a >> 5) & 1)
+#define PJ_HTOP(j) (((j).a >> 6) & 1)
+#define PJ_HLEFT(j) (((j).a >> 7) & 1)
+#define PJ_MSLOT(j) (((j).a >> 8) & 15)
+#define PJ_X4(j) (((j).a >> 12) & 15)
+#define PJ_Y4(j) (((j).a >> 16) & 15)
+#define PJ_CT(j) (((j).a >> 20) & 31)
+#define PJ_CL(j) (((j).a >> 25) & 31)
+
+/* Intra predictor formula table: for (table slot 0..9, ts, y, x) one word
+ *   i0 | i1 << 7 | i2 << 14 | wb << 21 | wc << 23 (1: +1, 2: -1) | s << 25 | dc << 27
+ * pixel = dc ? DC : clip((e[i0] + wb * e[i1] + wc * e[i2] + ((1 << s) >> 1)) >> s) over the
+ * job's edge array e (left column bottom-to-top, top-left, top row + top-right). */
+#define PTAB_SLOT 1360        /* 16 + 64 + 256 + 1024 entries per slot */
+#define PTAB_SIZE (10 * PTAB_SLOT)
 
 /* One superblock of intra work. Its jobs are grouped into "passes": a pass holds up
  * to 64/n independent jobs (same dependency level, same tx size n), so one wavefront
