@@ -284,3 +284,15 @@ class Decoder:
         buf = self._queue.pop(0)
         w, h, bpp = self._configured
         return visible(self.dev.download(buf), w, h)
+
+
+PLAN_STAT_NAMES = ("sbs", "passes", "pjobs", "rjobs", "passes_4x4", "passes_8x8", "passes_16x16",
+                   "passes_32x32", "lane_use", "max_passes_sb", "lf_records", "mc_units", "pred_steps",
+                   "lf_steps")
+
+
+def plan_stats(frame):
+    """Host-only work-planning statistics of one pass-1 packet (vp9hip_plan_stats)."""
+    out = (ctypes.c_double * 14)()
+    _check("vp9hip_plan_stats", lib().vp9hip_plan_stats(ctypes.byref(frame.pkt), out, 14))
+    return dict(zip(PLAN_STAT_NAMES, list(out)))

@@ -567,28 +567,24 @@ __global__ __launch_bounds__(64 * RWAVES) void k_resid(const RJob *__restrict__ 
 #define LT_SIZE (65 * LP)
 #define CT_SIZE (33 * CP)
 
-// A lane's residual column (<= 32 int16) in named registers (no array: stays out of scratch).
-struct RCol { uint4 a, b, c, d; };
-DEV uint32_t rword(const RCol &r, int k)
+// Prefetched per-lane inputs of one pass: the lane's job record and the first 8 rows
+// of its residual column (named fields, so the set stays in registers). Two sets
+// alternate across passes; the load is unconditional (clamped address), so no
+// control-flow join forces an early s_waitcnt.
+struct PSet { uint32_t ja, jr; uint4 r0; };
+DEV uint32_t pr_word(const PSet &s, int k)
 {
-    return k == 0 ? r.a.x : k == 1 ? r.a.y : k == 2 ? r.a.z : k == 3 ? r.a.w :
-           k == 4 ? r.b.x : k == 5 ? r.b.y : k == 6 ? r.b.z : k == 7 ? r.b.w :
-           k == 8 ? r.c.x : k == 9 ? r.c.y : k == 10 ? r.c.z : k == 11 ? r.c.w :
-           k == 12 ? r.d.x : k == 13 ? r.d.y : k == 14 ? r.d.z : r.d.w;
+    return k == 0 ? s.r0.x : k == 1 ? s.r0.y : k == 2 ? s.r0.z : s.r0.w;
 }
 
-// load this lane's residual column of the job it serves in pass word w
-DEV void fetch_resid(int w, int lane, const PJob *lj, const int16_t *__restrict__ resid, RCol &rv)
+DEV void prefetch_pass(int w, int lane, const PJob *lj, const int16_t *__restrict__ resid, PSet &ps)
 {
-    const int ts = PASS_TS(w), lg = ts + 2, grp = lane >> lg, li = lane & ((1 << lg) - 1);
-    if (grp >= PASS_NJOBS(w)) return;
-    const PJob jb = lj[PASS_FIRST(w) + grp];
-    if (!PJ_RES(jb)) return;
-    const uint4 *s = (const uint4 *) (resid + (size_t) jb.roff * 16 + (li << lg));
-    if (ts == 0) { const uint2 x = *(const uint2 *) s; rv.a.x = x.x; rv.a.y = x.y; return; }
-    rv.a = s[0];
-    if (ts >= 2) rv.b = s[1];
-    if (ts == 3) { rv.c = s[2]; rv.d = s[3]; }
+    const int ts = PASS_TS(w), lg = ts + 2;
+    const int grp = lane >> lg, li = lane & ((1 << lg) - 1), nj = PASS_NJOBS(w);
+    const PJob jb = lj[PASS_FIRST(w) + (grp < nj ? grp : nj - 1)];
+    ps.ja = jb.a;
+    ps.jr = jb.roff;
+    ps.r0 = *(const uint4 *) (resid + (PJ_RES(jb) ? (size_t) jb.roff * 16 + (li << lg) : 0));
 }
 
 // Load the pixels above / left of an SB (and, for inter frames, its interior: the
@@ -651,110 +647,155 @@ DEV void load_sb_tile(const FrameDesc &fd, int sbx, int sby, bool interior, int 
 // One pass of N x N jobs: lane li of group grp predicts column li of its job.
 template <int N, typename PIX>
 DEV void pred_pass(const PJob &jb, bool act, int li, int grp, PIX *tile, uint16_t *eb, int bd,
-                   const RCol &rv, const uint32_t *__restrict__ ptab)
+                   const PSet &ps, const uint32_t *ltab, const int16_t *__restrict__ resid,
+                   const uint32_t *__restrict__ ptab, int dbg)
 {
     constexpr int TS = N == 4 ? 0 : N == 8 ? 1 : N == 16 ? 2 : 3;
     constexpr int TOFF = N == 4 ? 0 : N == 8 ? 16 : N == 16 ? 80 : 336;
     const int p = PJ_PLANE(jb);
     const int tpch = p ? CP : LP;
     PIX *o = tile + (p == 0 ? 0 : p == 1 ? LT_SIZE : LT_SIZE + CT_SIZE) + (PJ_Y4(jb) * 4 + 1) * tpch + PJ_X4(jb) * 4 + 1;
-    const int ms = PJ_MSLOT(jb);
-    // formula words of this column (L1/L2-resident table), issued first
+    const int ms = PJ_MSLOT(jb), slot = ms < 9 ? ms : 9;
+    // formula words of this column: 4x4 / 8x8 from the LDS copy, larger from L1/L2;
+    // residual rows >= 8 of 16x16 / 32x32 loaded here
     uint32_t f[N];
-    const uint32_t *tb = ptab + (ms < 9 ? ms : 9) * PTAB_SLOT + TOFF + li;
+    uint32_t rx[N > 8 ? (N - 8) / 2 : 1];
+    if (N <= 8) {
 #pragma unroll
-    for (int y = 0; y < N; y++) f[y] = act ? tb[y * N] : 0;
+        for (int y = 0; y < N; y++) f[y] = ltab[slot * 80 + TOFF + y * N + li];
+    } else {
+        const uint32_t *tb = ptab + slot * PTAB_SLOT + TOFF + li;
+#pragma unroll
+        for (int y = 0; y < N; y++) f[y] = tb[y * N];
+        const uint32_t *r = (const uint32_t *) (resid + (PJ_RES(jb) ? (size_t) jb.roff * 16 + li * N : 0));
+#pragma unroll
+        for (int k = 4; k < N / 2; k++) rx[k - 4] = r[k];
+    }
 
-    // edges, branch-free (fills: vp9recon.c:103-210)
+    // edges (fills: vp9recon.c:103-210): every load hits a valid tile address, the
+    // host-resolved availability selects between pixel and fill value (no branches)
     const int base = 128 << (bd - 8);
     const int htop = PJ_HTOP(jb), hleft = PJ_HLEFT(jb), ct = PJ_CT(jb), cl = PJ_CL(jb);
-    const int tv = htop ? (int) o[-tpch + (li < ct ? li : ct)] : base - 1;
-    const int lr = N - 1 - li < cl ? N - 1 - li : cl;
-    const int lv = hleft ? (int) o[lr * tpch - 1] : base + 1;
-    uint16_t *e = eb + grp * (2 * N + 8);
-    if (act) {
-        e[li] = lv;
-        e[N + 1 + li] = tv;
-        if (N == 4) e[N + 5 + li] = htop ? (PJ_TRREAL(jb) ? o[-tpch + 4 + li] : o[-tpch + ct]) : base - 1;
-        if (li == 0) e[N] = (hleft && htop) ? o[-tpch - 1] : base + (htop ? 1 : -1);
+    const PIX *orow = o - tpch;
+    const int t_px = orow[li < ct ? li : ct];
+    const int l_px = o[(N - 1 - li < cl ? N - 1 - li : cl) * tpch - 1];
+    const int tl_px = orow[-1];
+    const int tv = htop ? t_px : base - 1;
+    const int lv = hleft ? l_px : base + 1;
+    const int tl = (hleft & htop) ? tl_px : base + (htop ? 1 : -1);
+    int tr = 0;
+    if (N == 4) {
+        const int tr_px = orow[PJ_TRREAL(jb) ? 4 + li : ct];
+        tr = htop ? tr_px : base - 1;
     }
-    // DC sums over the group's N lanes
-    int sl = lv, st = tv;
+    uint16_t *e = eb + grp * (2 * N + 8);
+    if (act && !(dbg & 16)) {
+        e[li] = (uint16_t) lv;
+        e[N + 1 + li] = (uint16_t) tv;
+        if (N == 4) e[N + 5 + li] = (uint16_t) tr;
+        e[N] = (uint16_t) tl;                  // every lane of the group writes the same value
+    }
+    // DC sums over the group's N lanes (only when the pass holds a DC/LEFT_DC/TOP_DC job)
+    int dc = ms == 12 ? base : ms == 13 ? base - 1 : base + 1;
+    if (__any(act && ms >= 9 && ms <= 11)) {
+        int sl = lv, st = tv;
 #pragma unroll
-    for (int m = 1; m < N; m <<= 1) { sl += __shfl_xor(sl, m); st += __shfl_xor(st, m); }
-    const int dc = ms == 9 ? (sl + st + N) >> (TS + 3) : ms == 10 ? (sl + (N >> 1)) >> (TS + 2) :
-                   ms == 11 ? (st + (N >> 1)) >> (TS + 2) : ms == 12 ? base : ms == 13 ? base - 1 : base + 1;
+        for (int m = 1; m < N; m <<= 1) { sl += __shfl_xor(sl, m); st += __shfl_xor(st, m); }
+        const int d9 = (sl + st + N) >> (TS + 3), d10 = (sl + (N >> 1)) >> (TS + 2), d11 = (st + (N >> 1)) >> (TS + 2);
+        dc = ms == 9 ? d9 : ms == 10 ? d10 : ms == 11 ? d11 : dc;
+    }
     wave_sync();
-    if (act) {
+    if (act && !(dbg & 8)) {
         const int mx = (1 << bd) - 1;
-        const bool hr = PJ_RES(jb);
+        const int hr = PJ_RES(jb);
 #pragma unroll
         for (int y = 0; y < N; y++) {
             const uint32_t w = f[y];
-            int v;
-            if (w >> 27) v = dc;
-            else {
-                const int a = e[w & 127], b = e[(w >> 7) & 127], c = e[(w >> 14) & 127];
-                const int wb = (w >> 21) & 3, wc = (w >> 23) & 3, s = (w >> 25) & 3;
-                v = (a + wb * b + (wc == 2 ? -c : wc * c) + ((1 << s) >> 1)) >> s;
-                v = v < 0 ? 0 : v > mx ? mx : v;
-            }
-            if (hr) {
-                const int r = (int16_t) (rword(rv, y >> 1) >> ((y & 1) * 16));
-                v += r;
-                v = v < 0 ? 0 : v > mx ? mx : v;
-            }
+            const int a = e[w & 127], b = e[(w >> 7) & 127], c = e[(w >> 14) & 127];
+            const int wb = (w >> 21) & 3, s = (w >> 25) & 3;
+            const int wc = __builtin_amdgcn_sbfe((int) w, 23, 2);
+            int v = (a + wb * b + wc * c + ((1 << s) >> 1)) >> s;
+            v = min(max(v, 0), mx);
+            v = (w >> 27) ? dc : v;
+            const uint32_t rw = y < 8 ? pr_word(ps, y >> 1) : rx[y < 8 ? 0 : (y >> 1) - 4];
+            const int r = (int) (int16_t) (rw >> ((y & 1) * 16));
+            v += hr ? r : 0;
+            v = min(max(v, 0), mx);
             o[y * tpch + li] = (PIX) v;
         }
     }
 }
 
 template <typename PIX>
+DEV void run_pass(int w, int lane, PIX *tile, uint16_t *eb, int bd, const PSet &ps, const uint32_t *ltab,
+                  const int16_t *__restrict__ resid, const uint32_t *__restrict__ ptab, int dbg)
+{
+    const int ts = PASS_TS(w), lg = ts + 2;
+    const int grp = lane >> lg, li = lane & ((1 << lg) - 1);
+    const bool act = grp < PASS_NJOBS(w);
+    PJob jb;
+    jb.a = ps.ja;
+    jb.roff = ps.jr;
+    switch (ts) {
+    case 0: pred_pass<4, PIX>(jb, act, li, grp, tile, eb, bd, ps, ltab, resid, ptab, dbg); break;
+    case 1: pred_pass<8, PIX>(jb, act, li, grp, tile, eb, bd, ps, ltab, resid, ptab, dbg); break;
+    case 2: pred_pass<16, PIX>(jb, act, li, grp, tile, eb, bd, ps, ltab, resid, ptab, dbg); break;
+    default: pred_pass<32, PIX>(jb, act, li, grp, tile, eb, bd, ps, ltab, resid, ptab, dbg); break;
+    }
+    wave_sync();
+}
+
+template <typename PIX>
 __global__ __launch_bounds__(64) void k_pred(const uint32_t *__restrict__ list, const SBRec *__restrict__ sbs,
                                              const PJob *__restrict__ jobs, const uint16_t *__restrict__ passes,
                                              const FrameDesc *__restrict__ frames, const int16_t *__restrict__ resid,
-                                             const uint32_t *__restrict__ ptab)
+                                             const uint32_t *__restrict__ ptab, int dbg)
 {
     __shared__ PIX tile[LT_SIZE + 2 * CT_SIZE];
     __shared__ uint16_t eb[256];               // per job 2n+8 edge pixels
     __shared__ PJob lj[MAX_SB_JOBS];
     __shared__ uint16_t lp[MAX_SB_JOBS];
+    __shared__ uint32_t ltab[10 * 80];         // formula words of 4x4 and 8x8, all slots
 
     const SBRec sb = sbs[list[blockIdx.x]];
     const FrameDesc &fd = frames[sb.frame];
     const int lane = threadIdx.x;
     const int bd = fd.bd;
 
-    // ---- prologue: job list, pass words, SB neighbourhood (pre-loop-filter pixels) ----
+    // ---- prologue: job list, pass words, formula words, SB neighbourhood (pre-LF pixels) ----
+    {
+        uint32_t t[13];
+#pragma unroll
+        for (int u = 0; u < 13; u++) {
+            const int i = lane + 64 * u;
+            t[u] = i < 800 ? ptab[(i / 80) * PTAB_SLOT + i % 80] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 13; u++)
+            if (lane + 64 * u < 800) ltab[lane + 64 * u] = t[u];
+    }
     for (int i = lane; i < sb.njobs; i += 64) lj[i] = jobs[sb.job0 + i];
     for (int i = lane; i < sb.npass; i += 64) lp[i] = passes[sb.pass0 + i];
-    load_sb_tile<PIX>(fd, sb.sbx, sb.sby, sb.flags & 1, lane, tile);
+    if (!(dbg & 4)) load_sb_tile<PIX>(fd, sb.sbx, sb.sby, sb.flags & 1, lane, tile);
     wave_sync();
 
-    const int npass = sb.npass;
-    RCol rv, rvn;
-    rv.a = rv.b = rv.c = rv.d = make_uint4(0, 0, 0, 0);
-    rvn = rv;
-    if (npass) fetch_resid(lp[0], lane, lj, resid, rv);
-
-    for (int pi = 0; pi < npass; pi++) {
-        const int w = __builtin_amdgcn_readfirstlane(lp[pi]);
-        if (pi + 1 < npass) fetch_resid(lp[pi + 1], lane, lj, resid, rvn);   // prefetch the next pass
-        const int ts = PASS_TS(w), lg = ts + 2;
-        const int grp = lane >> lg, li = lane & ((1 << lg) - 1);
-        const bool act = grp < PASS_NJOBS(w);
-        const PJob jb = lj[PASS_FIRST(w) + (act ? grp : 0)];
-        switch (ts) {
-        case 0: pred_pass<4, PIX>(jb, act, li, grp, tile, eb, bd, rv, ptab); break;
-        case 1: pred_pass<8, PIX>(jb, act, li, grp, tile, eb, bd, rv, ptab); break;
-        case 2: pred_pass<16, PIX>(jb, act, li, grp, tile, eb, bd, rv, ptab); break;
-        default: pred_pass<32, PIX>(jb, act, li, grp, tile, eb, bd, rv, ptab); break;
-        }
-        wave_sync();
-        rv = rvn;
+    // passes, two prefetch sets alternating (loop unrolled by two: no register copies)
+    const int npass = (dbg & 1) ? 0 : sb.npass;
+    PSet A, B;
+    if (npass) prefetch_pass(lp[0], lane, lj, resid, A);
+    for (int pi = 0; pi < npass; pi += 2) {
+        const int w0 = __builtin_amdgcn_readfirstlane(lp[pi]);
+        const bool two = pi + 1 < npass;
+        const int w1 = two ? __builtin_amdgcn_readfirstlane(lp[pi + 1]) : w0;
+        if (two) prefetch_pass(w1, lane, lj, resid, B);
+        run_pass<PIX>(w0, lane, tile, eb, bd, A, ltab, resid, ptab, dbg);
+        if (!two) break;
+        if (pi + 2 < npass) prefetch_pass(lp[pi + 2], lane, lj, resid, A);
+        run_pass<PIX>(w1, lane, tile, eb, bd, B, ltab, resid, ptab, dbg);
     }
 
     // ---- store the SB interior ----
+    if (!(dbg & 2))
     for (int p = 0; p < 3; p++) {
         const int sz = p ? 32 : 64;
         PIX *g = (PIX *) fd.plane[p];
@@ -1112,11 +1153,11 @@ int vp9hip_launch_resid(int hb, hipStream_t st, int tcode, int n, const RJob *jo
 }
 int vp9hip_launch_pred(int hb, hipStream_t st, int nsb, const uint32_t *list, const SBRec *sbs,
                        const PJob *jobs, const uint16_t *passes, const FrameDesc *frames, const int16_t *resid,
-                       const uint32_t *ptab)
+                       const uint32_t *ptab, int dbg)
 {
     if (nsb <= 0) return 0;
-    if (hb) hipLaunchKernelGGL(k_pred<uint16_t>, dim3(nsb), dim3(64), 0, st, list, sbs, jobs, passes, frames, resid, ptab);
-    else    hipLaunchKernelGGL(k_pred<uint8_t>, dim3(nsb), dim3(64), 0, st, list, sbs, jobs, passes, frames, resid, ptab);
+    if (hb) hipLaunchKernelGGL(k_pred<uint16_t>, dim3(nsb), dim3(64), 0, st, list, sbs, jobs, passes, frames, resid, ptab, dbg);
+    else    hipLaunchKernelGGL(k_pred<uint8_t>, dim3(nsb), dim3(64), 0, st, list, sbs, jobs, passes, frames, resid, ptab, dbg);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int vp9hip_launch_lf(int hb, hipStream_t st, int nsb, const uint32_t *list, const LFRec *recs,

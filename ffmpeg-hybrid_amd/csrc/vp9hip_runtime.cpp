@@ -19,6 +19,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -35,7 +36,7 @@ int vp9hip_launch_resid(int hb, hipStream_t st, int tcode, int n, const RJob *jo
                         const void *coefs, int16_t *resid);
 int vp9hip_launch_pred(int hb, hipStream_t st, int nsb, const uint32_t *list, const SBRec *sbs,
                        const PJob *jobs, const uint16_t *passes, const FrameDesc *frames, const int16_t *resid,
-                       const uint32_t *ptab);
+                       const uint32_t *ptab, int dbg);
 int vp9hip_launch_lf(int hb, hipStream_t st, int nsb, const uint32_t *list, const LFRec *recs,
                      const FrameDesc *frames);
 int vp9hip_launch_mc(int hb, hipStream_t st, int n, const McUnit *units, const FrameDesc *frames);
@@ -86,6 +87,7 @@ struct vp9hip_ctx {
     size_t plane_off[3] = { 0, 0, 0 }, buf_bytes = 0;
     std::vector<uint8_t *> bufs;
     uint32_t *ptab = nullptr;           // intra predictor formula table (device)
+    int dbg = 0;                        // VP9HIP_DEBUG: ablation switches for profiling only
     Staged stg;
     // timing of the last run
     bool timing = true;
@@ -104,6 +106,7 @@ extern "C" int vp9hip_open(int device, vp9hip_ctx **out)
     if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return VP9HIP_ENOSYS;
     vp9hip_ctx *c = new vp9hip_ctx;
     c->dev = device;
+    if (const char *d = getenv("VP9HIP_DEBUG")) c->dbg = atoi(d);
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return VP9HIP_EEXTERNAL;
@@ -140,7 +143,8 @@ extern "C" void vp9hip_close(vp9hip_ctx *c)
 enum { PF_COPY, PF_AVG2, PF_AVG3, PF_AVG31, PF_TM, PF_DC };
 static uint32_t pf_enc(int kind, int i0 = 0, int i1 = 0, int i2 = 0)
 {
-    static const int wb[6] = { 0, 1, 2, 3, 1, 0 }, wc[6] = { 0, 0, 1, 0, 2, 0 }, sh[6] = { 0, 1, 2, 2, 0, 0 };
+    // wc is a 2-bit two's complement weight (3 = -1)
+    static const int wb[6] = { 0, 1, 2, 3, 1, 0 }, wc[6] = { 0, 0, 1, 0, 3, 0 }, sh[6] = { 0, 1, 2, 2, 0, 0 };
     return (uint32_t) i0 | (uint32_t) i1 << 7 | (uint32_t) i2 << 14 | (uint32_t) wb[kind] << 21 |
            (uint32_t) wc[kind] << 23 | (uint32_t) sh[kind] << 25 | (uint32_t) (kind == PF_DC) << 27;
 }
@@ -751,7 +755,7 @@ extern "C" int vp9hip_run_batch(vp9hip_ctx *c)
         case K_PRED:
             r = vp9hip_launch_pred(c->hb, c->st, (int) L.n, lists + L.off, (const SBRec *) (s.arena + s.o_sbs),
                                    (const PJob *) (s.arena + s.o_pjobs), (const uint16_t *) (s.arena + s.o_passes),
-                                   fr, s.resid, c->ptab);
+                                   fr, s.resid, c->ptab, c->dbg);
             break;
         case K_LF:
             r = vp9hip_launch_lf(c->hb, c->st, (int) L.n, lists + L.off, (const LFRec *) (s.arena + s.o_lfs), fr);
@@ -854,3 +858,46 @@ extern "C" int vp9hip_set_timing(vp9hip_ctx *c, int on)
 }
 
 extern "C" int vp9hip_abi_version(void) { return VP9HIP_ABI_VERSION; }
+
+// Host-only planning statistics of one frame (no device needed): used by the CPU tests
+// and to size kernels. out[]: 0 SBs with intra work, 1 passes, 2 intra jobs, 3 residual
+// jobs, 4..7 passes per tx size, 8 sum of jobs over passes / capacity (lane use),
+// 9 max passes in one SB, 10 LF records, 11 MC units, 12 intra wavefront steps,
+// 13 LF wavefront steps.
+extern "C" int vp9hip_plan_stats(const vp9h_frame *f, double *out, int cap)
+{
+    if (!f || !out || cap < 14) return VP9HIP_EINVAL;
+    if (f->ss_h != 1 || f->ss_v != 1) return VP9HIP_ENOSYS;
+    init_nz();
+    Staged s;
+    FrameBuild fb;
+    fb.f = f; fb.frame_idx = 0;
+    fb.cols = (f->width + 7) >> 3; fb.rows = (f->height + 7) >> 3;
+    fb.sb_cols = (f->width + 63) >> 6; fb.sb_rows = (f->height + 63) >> 6;
+    fb.ss_h = f->ss_h; fb.ss_v = f->ss_v; fb.coef_size = f->bpp > 8 ? 4 : 2;
+    fb.pitch[0] = fb.sb_cols * 64; fb.pitch[1] = fb.sb_cols * 32;
+    fb.coef_base = 0;
+    std::vector<std::vector<uint32_t>> ps, ls;
+    int r = build_frame(nullptr, s, fb, ps, ls);
+    if (r < 0) return r;
+    for (int i = 0; i < 14; i++) out[i] = 0;
+    out[0] = (double) s.sbs.size();
+    out[1] = (double) s.passes.size();
+    out[2] = (double) s.pjobs.size();
+    size_t nr = 0;
+    for (auto &bt : s.rbucket) for (auto &bk : bt) nr += bk.size();
+    out[3] = (double) nr;
+    double used = 0, capsum = 0;
+    for (uint16_t w : s.passes) {
+        out[4 + PASS_TS(w)] += 1;
+        used += PASS_NJOBS(w);
+        capsum += 64 >> (PASS_TS(w) + 2);
+    }
+    out[8] = capsum ? used / capsum : 0;
+    for (auto &sb : s.sbs) out[9] = std::max(out[9], (double) sb.npass);
+    out[10] = (double) s.lfs.size();
+    out[11] = (double) s.mcs.size();
+    out[12] = (double) ps.size();
+    out[13] = (double) ls.size();
+    return 0;
+}

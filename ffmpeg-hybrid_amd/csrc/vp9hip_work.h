@@ -72,7 +72,7 @@ typedef struct PJob {
 #define PJ_CL(j) (((j).a >> 25) & 31)
 
 /* Intra predictor formula table: for (table slot 0..9, ts, y, x) one word
- *   i0 | i1 << 7 | i2 << 14 | wb << 21 | wc << 23 (1: +1, 2: -1) | s << 25 | dc << 27
+ *   i0 | i1 << 7 | i2 << 14 | wb << 21 | wc << 23 (2-bit signed: 1 = +1, 3 = -1) | s << 25 | dc << 27
  * pixel = dc ? DC : clip((e[i0] + wb * e[i1] + wc * e[i2] + ((1 << s) >> 1)) >> s) over the
  * job's edge array e (left column bottom-to-top, top-left, top row + top-right). */
 #define PTAB_SLOT 1360        /* 16 + 64 + 256 + 1024 entries per slot */

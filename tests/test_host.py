@@ -97,3 +97,20 @@ def test_oracle_regression_framemd5(v9, orc):
     want = json.load(open(os.path.join(ROOT, "tests", "golden", "oracle_framemd5.json")))
     got = mg.compute()
     assert got == want
+
+
+def test_planner_stats_c3_frame(v9):
+    """Host planner on a 4K frame (no GPU): every tx block becomes a job, passes pack
+    independent jobs of one size (<= 64/n), the wavefront step counts follow the
+    SB grid (intra: x_in_tile + y, LF: x + 2y)."""
+    f = v9.SynthFrame(v9.synth_params(3840, 2160, 8, seed=0x56503902, log2_tile_cols=2))
+    st = v9.plan_stats(f)
+    assert st["sbs"] == 60 * 34
+    # keyframe: a prediction job per tx block (skip blocks too), a residual job per eob > 0
+    eobs = np.ctypeslib.as_array(f.pkt.eobs, (f.pkt.neobs,))
+    assert st["rjobs"] == int((eobs > 0).sum())
+    assert st["pjobs"] >= f.pkt.neobs
+    assert st["passes"] >= 26 * st["sbs"] * 0.9
+    assert 0 < st["lane_use"] <= 1
+    assert st["pred_steps"] == 15 + 34 - 1     # 4 tile columns of 15 SBs
+    assert st["lf_steps"] == 60 + 2 * 33
