@@ -29,6 +29,29 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 W, H, BPP, LOG2_TILE_COLS = 3840, 2160, 8, 2
 CONFIG_INDEX = 2               # C3
+SEED0 = 0x56503900 + CONFIG_INDEX
+TRAFFIC_PROFILE = "r01d"       # rocprofv3 PMC pass of this workload (tools/profile.sh)
+
+
+def frame_seed(rank, i):
+    """Seed of frame i of rank `rank`: every rank decodes its own, distinct frames."""
+    return SEED0 + rank * 100003 + i
+
+
+def reduce_elapsed(elapsed, dist):
+    """Max over ranks of the timed region (the slowest rank defines the job time)."""
+    if dist is None:
+        return elapsed
+    import torch
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def aggregate(frames_per_rank, steps, world, elapsed_max):
+    """Whole-job throughput: all frames of all ranks over the max-over-ranks time."""
+    total = frames_per_rank * steps * world
+    return total / elapsed_max, elapsed_max * 1000.0 / steps
 
 
 def main():
@@ -50,9 +73,8 @@ def main():
         dist.init_process_group("gloo")
 
     v = importlib.import_module("ffmpeg-hybrid_amd")
-    seed0 = 0x56503900 + CONFIG_INDEX
     t0 = time.time()
-    frames = [v.SynthFrame(v.synth_params(W, H, BPP, seed=seed0 + rank * 100003 + i, log2_tile_cols=LOG2_TILE_COLS))
+    frames = [v.SynthFrame(v.synth_params(W, H, BPP, seed=frame_seed(rank, i), log2_tile_cols=LOG2_TILE_COLS))
               for i in range(args.frames)]
     t_gen = time.time() - t0
 
@@ -86,17 +108,11 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
 
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = reduce_elapsed(elapsed, dist)
 
     alg = dev.alg_bytes()           # per step, per kernel class
     names = list(alg.keys())
-    total_frames = args.frames * args.steps * world
-    fps = total_frames / elapsed
-    ms_per_step = elapsed * 1000.0 / args.steps
+    fps, ms_per_step = aggregate(args.frames, args.steps, world, elapsed)
 
     # dominant kernel (largest device time)
     dom = max(names, key=lambda k: ksum.get(k, [0.0, 0])[0])
@@ -107,9 +123,17 @@ def main():
     achieved = bytes_per_launch / avg_launch_s / 1e9 if kn else 0.0
     kernel_ms_per_frame = sum(x[0] for x in ksum.values()) / (args.frames * args.steps)
     frame_bytes = sum(alg.values()) / args.frames
+    # HBM traffic per launch of the same kernel on the same workload, from the committed
+    # rocprofv3 PMC pass (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; tools/traffic.py)
+    traffic, traffic_src = None, None
+    tf = os.path.join(ROOT, "profiles", TRAFFIC_PROFILE, "traffic.json")
+    if os.path.exists(tf):
+        per = json.load(open(tf))["per_launch"].get(dom)
+        if per:
+            traffic, traffic_src = round(per["traffic_bytes"]), "profiles/%s/traffic.json" % TRAFFIC_PROFILE
     roofline = {
         "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-        "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+        "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": traffic_src,
         "kernel": dom, "launches_per_step": int(launches_per_step),
         "alg_bytes_per_launch": round(bytes_per_launch),
         "avg_launch_us": round(avg_launch_s * 1e6, 2),

@@ -79,7 +79,8 @@ _lib_handle = None
 # Exported symbols of include/vp9hip.h (checked by the CPU test suite).
 ABI_SYMBOLS = ["vp9hip_open", "vp9hip_close", "vp9hip_configure", "vp9hip_submit_frame",
                "vp9hip_stage_batch", "vp9hip_run_batch", "vp9hip_sync", "vp9hip_download_frame",
-               "vp9hip_upload_frame", "vp9hip_flush", "vp9hip_last_timing",
+               "vp9hip_upload_frame", "vp9hip_flush", "vp9hip_last_timing", "vp9hip_set_timing",
+               "vp9hip_alg_bytes", "vp9hip_plan_stats", "vp9hip_abi_version",
                "vp9hip_synth_defaults", "vp9hip_synth_frame", "vp9hip_synth_free"]
 
 

@@ -144,6 +144,20 @@ int  vp9hip_flush(vp9hip_ctx *ctx);
  */
 int  vp9hip_last_timing(vp9hip_ctx *ctx, const char **names, double *ms, int *launches, int cap);
 
+/* Per-launch HIP-event timing on/off (default on). */
+int  vp9hip_set_timing(vp9hip_ctx *ctx, int on);
+
+/* Algorithmic bytes (B = C + P(1+R) + 2P[LF]) of the staged batch,
+ * per kernel class in vp9hip_last_timing order. Returns count. */
+int  vp9hip_alg_bytes(vp9hip_ctx *ctx, double *bytes, int cap);
+
+/* Host-only planning statistics of one packet (no device needed), 14 values:
+ * SBs with intra work, passes, intra jobs, residual jobs, passes per tx size (4),
+ * lane use, max passes per SB, LF records, MC units, intra / LF wavefront steps. */
+int  vp9hip_plan_stats(const vp9h_frame *pkt, double *out, int cap);
+
+int  vp9hip_abi_version(void);
+
 /* ---- synthetic pass-1 generator (test / bench input) -------------------- */
 /*
  * Generates a pseudo-random but structurally legal frame packet. Defaults follow the

@@ -1,0 +1,42 @@
+#!/usr/bin/env python3
+"""Per-kernel HBM traffic per launch from tools/profile.sh PMC passes.
+
+FETCH_SIZE / WRITE_SIZE are kilobytes per dispatch (rocprofv3). On gfx950 FETCH_SIZE
+counts 64 B per 128-B request of wide streaming reads (MI355X_MICROARCH.md, HBM
+section), so `fetch_corrected` doubles it; both are reported.
+Usage: traffic.py gpurun_out/prof_TAG [out.json]"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def short(name):
+    for k in ("k_resid", "k_pred", "k_lf", "k_mc"):
+        if k in name:
+            return k
+    return None
+
+
+def main(d, out=None):
+    acc = defaultdict(lambda: defaultdict(list))
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            k = short(r["Kernel_Name"])
+            if k and r["Counter_Name"] in ("FETCH_SIZE", "WRITE_SIZE"):
+                acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]) * 1024.0)
+    res = {}
+    for k, c in acc.items():
+        fe = sum(c["FETCH_SIZE"]) / max(1, len(c["FETCH_SIZE"]))
+        wr = sum(c["WRITE_SIZE"]) / max(1, len(c["WRITE_SIZE"]))
+        res[k] = {"fetch_bytes": fe, "fetch_corrected": 2 * fe, "write_bytes": wr,
+                  "traffic_bytes": 2 * fe + wr, "launches": len(c["FETCH_SIZE"])}
+    print(json.dumps(res, indent=1))
+    if out:
+        json.dump({"source": d, "per_launch": res}, open(out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
