@@ -50,7 +50,8 @@ const char *const kname[K_N] = { "k_mc", "k_resid", "k_pred", "k_lf" };
 // ff_vp9_intra_txfm_type (vp9data.c:437-452)
 const uint8_t intra_txfm_type[14] = { 2, 1, 0, 0, 3, 2, 1, 2, 1, 3, 0, 0, 0, 0 };
 
-struct Launch { int kind; uint32_t off; uint32_t n; int arg; };
+struct Launch { int kind; uint32_t off; uint32_t n; int arg; int grp; };
+#define MAX_GROUPS 4                    // independent frame groups = concurrent launch chains
 
 struct Staged {
     // host images (kept for rebuilds / inspection)
@@ -58,7 +59,8 @@ struct Staged {
     std::vector<SBRec> sbs;
     std::vector<PJob> pjobs;
     std::vector<uint16_t> passes;
-    std::vector<RJob> rbucket[5][4];    // residual jobs by (tx code, txtp)
+    std::vector<RJob> rbucket[MAX_GROUPS][5][4];    // residual jobs by (group, tx code, txtp)
+    int ngroups = 1;
     std::vector<RJob> rjobs;            // concatenated buckets
     uint64_t resid16 = 0;               // residual scratch size, 16-element units
     std::vector<LFRec> lfs;
@@ -80,7 +82,10 @@ struct Staged {
 
 struct vp9hip_ctx {
     int dev = 0;
-    hipStream_t st = nullptr;
+    hipStream_t st = nullptr;           // main stream: uploads, downloads, group 0
+    hipStream_t xst[MAX_GROUPS - 1] = {};   // groups 1.. of a batch (joined back into st)
+    hipEvent_t fork_ev = nullptr, join_ev[MAX_GROUPS - 1] = {};
+    int max_groups = 2;                 // VP9HIP_STREAMS overrides (1..4); 2 measured best at C3
     int w = 0, h = 0, bpp = 8, ss_h = 1, ss_v = 1, hb = 0, bypp = 1;
     int cols = 0, rows = 0, sb_cols = 0, sb_rows = 0;
     int pitch[2] = { 0, 0 };
@@ -107,7 +112,13 @@ extern "C" int vp9hip_open(int device, vp9hip_ctx **out)
     vp9hip_ctx *c = new vp9hip_ctx;
     c->dev = device;
     if (const char *d = getenv("VP9HIP_DEBUG")) c->dbg = atoi(d);
-    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) {
+    if (const char *g = getenv("VP9HIP_STREAMS")) c->max_groups = std::max(1, std::min(MAX_GROUPS, atoi(g)));
+    bool ok = hipSetDevice(device) == hipSuccess && hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) == hipSuccess &&
+              hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) == hipSuccess;
+    for (int i = 0; ok && i < MAX_GROUPS - 1; i++)
+        ok = hipStreamCreateWithFlags(&c->xst[i], hipStreamNonBlocking) == hipSuccess &&
+             hipEventCreateWithFlags(&c->join_ev[i], hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
         delete c;
         return VP9HIP_EEXTERNAL;
     }
@@ -132,6 +143,11 @@ extern "C" void vp9hip_close(vp9hip_ctx *c)
     if (c->ptab) hipFree(c->ptab);
     for (auto e : c->ev) hipEventDestroy(e);
     hipStreamDestroy(c->st);
+    for (int i = 0; i < MAX_GROUPS - 1; i++) {
+        if (c->xst[i]) hipStreamDestroy(c->xst[i]);
+        if (c->join_ev[i]) hipEventDestroy(c->join_ev[i]);
+    }
+    if (c->fork_ev) hipEventDestroy(c->fork_ev);
     delete c;
 }
 
@@ -336,6 +352,7 @@ struct FrameBuild {
     int cols, rows, sb_cols, sb_rows;
     int ss_h, ss_v, coef_size;
     int pitch[2];
+    int group;                   // frame group (launch chain) of this frame
     uint64_t coef_base;          // element offset of this frame's coefficients in the batch stream
 };
 
@@ -425,7 +442,7 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
                             } else {
                                 r.dst = (uint32_t) ((size_t) (by + y * 4) * fb.pitch[p ? 1 : 0] + bx + x * 4);
                             }
-                            s.rbucket[tcode][txtp].push_back(r);
+                            s.rbucket[fb.group][tcode][txtp].push_back(r);
                         }
                         coef += e;
                         if (!b->intra) continue;
@@ -591,14 +608,17 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     Staged &s = c->stg;
     s.frames.clear(); s.sbs.clear(); s.pjobs.clear(); s.passes.clear(); s.lfs.clear(); s.mcs.clear();
     s.rjobs.clear(); s.resid16 = 0;
-    for (auto &bt : s.rbucket) for (auto &bk : bt) bk.clear();
+    for (auto &bg : s.rbucket) for (auto &bt : bg) for (auto &bk : bt) bk.clear();
     s.lists.clear(); s.launches.clear(); s.coefs.clear();
     for (int k = 0; k < K_N; k++) s.alg_bytes[k] = 0;
     s.ready = false;
 
     const int csz = c->hb ? 4 : 2;
     init_nz();
-    std::vector<std::vector<uint32_t>> psteps, lsteps;
+    // independent frames are split into groups, one launch chain (HIP stream) each
+    const int G = std::max(1, std::min(c->max_groups, n));
+    s.ngroups = G;
+    std::vector<std::vector<uint32_t>> psteps[MAX_GROUPS], lsteps[MAX_GROUPS];
     uint64_t coef_base = 0;
     double pix_bytes = (double) c->w * c->h * c->bypp * (1.0 + 2.0 / ((1 << c->ss_h) * (1 << c->ss_v)));
     for (int i = 0; i < n; i++) {
@@ -637,7 +657,8 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
         fb.pitch[0] = c->pitch[0]; fb.pitch[1] = c->pitch[1];
         fb.coef_base = coef_base;
         size_t mc0 = s.mcs.size();
-        int r = build_frame(c, s, fb, psteps, lsteps);
+        fb.group = i % G;
+        int r = build_frame(c, s, fb, psteps[fb.group], lsteps[fb.group]);
         if (r < 0) return r;
         size_t cb = (size_t) f->ncoefs * csz;
         size_t off = s.coefs.size();
@@ -654,26 +675,27 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
         for (size_t m = mc0; m < s.mcs.size(); m++)
             s.alg_bytes[K_MC] += (double) s.mcs[m].w * s.mcs[m].h * c->bypp * (1 + s.mcs[m].nref);
     }
-    // residual jobs in (tx code, txtp) buckets; inter residual pixels are algorithmic
-    // reads + writes of k_resid
-    for (int t = 0; t < 5; t++) {
-        const uint32_t off = (uint32_t) s.rjobs.size();
-        for (int tp = 0; tp < 4; tp++) {
-            for (auto &r : s.rbucket[t][tp])
-                if (r.ptx & 32) s.alg_bytes[K_RESID] += 2.0 * (16 << (2 * (t & 3))) * c->bypp;
-            s.rjobs.insert(s.rjobs.end(), s.rbucket[t][tp].begin(), s.rbucket[t][tp].end());
+    // per group: residual jobs in (tx code, txtp) buckets, then the intra SB wavefront,
+    // then the LF wavefront; inter residual pixels are algorithmic reads + writes of k_resid
+    if (!s.mcs.empty()) s.launches.push_back({ K_MC, 0, (uint32_t) s.mcs.size(), 0, 0 });
+    for (int g = 0; g < G; g++) {
+        for (int t = 0; t < 5; t++) {
+            const uint32_t off = (uint32_t) s.rjobs.size();
+            for (int tp = 0; tp < 4; tp++) {
+                for (auto &r : s.rbucket[g][t][tp])
+                    if (r.ptx & 32) s.alg_bytes[K_RESID] += 2.0 * (16 << (2 * (t & 3))) * c->bypp;
+                s.rjobs.insert(s.rjobs.end(), s.rbucket[g][t][tp].begin(), s.rbucket[g][t][tp].end());
+            }
+            if (s.rjobs.size() > off) s.launches.push_back({ K_RESID, off, (uint32_t) (s.rjobs.size() - off), t, g });
         }
-        if (s.rjobs.size() > off) s.launches.push_back({ K_RESID, off, (uint32_t) (s.rjobs.size() - off), t });
+        auto add_list = [&](int kind, const std::vector<uint32_t> &v) {
+            if (v.empty()) return;
+            s.launches.push_back({ kind, (uint32_t) s.lists.size(), (uint32_t) v.size(), 0, g });
+            s.lists.insert(s.lists.end(), v.begin(), v.end());
+        };
+        for (auto &v : psteps[g]) add_list(K_PRED, v);
+        for (auto &v : lsteps[g]) add_list(K_LF, v);
     }
-    // launch schedule: MC, residuals, the intra SB wavefront, the LF wavefront
-    if (!s.mcs.empty()) s.launches.insert(s.launches.begin(), { K_MC, 0, (uint32_t) s.mcs.size(), 0 });
-    auto add_list = [&](int kind, const std::vector<uint32_t> &v) {
-        if (v.empty()) return;
-        s.launches.push_back({ kind, (uint32_t) s.lists.size(), (uint32_t) v.size(), 0 });
-        s.lists.insert(s.lists.end(), v.begin(), v.end());
-    };
-    for (auto &v : psteps) add_list(K_PRED, v);
-    for (auto &v : lsteps) add_list(K_LF, v);
     if (s.resid16 > 0xffffffffull) return VP9HIP_ENOMEM;
 
     // upload into one arena
@@ -740,29 +762,40 @@ extern "C" int vp9hip_run_batch(vp9hip_ctx *c)
         c->ev.resize(2 * nl);
         for (size_t i = old; i < c->ev.size(); i++) HIPCHK(hipEventCreate(&c->ev[i]));
     }
+    // fork: groups 1.. start after everything queued on the main stream (uploads)
+    if (s.ngroups > 1) {
+        HIPCHK(hipEventRecord(c->fork_ev, c->st));
+        for (int g = 1; g < s.ngroups; g++) HIPCHK(hipStreamWaitEvent(c->xst[g - 1], c->fork_ev, 0));
+    }
     for (size_t i = 0; i < nl; i++) {
         const Launch &L = s.launches[i];
-        if (c->timing) HIPCHK(hipEventRecord(c->ev[2 * i], c->st));
+        hipStream_t st = L.grp ? c->xst[L.grp - 1] : c->st;
+        if (c->timing) HIPCHK(hipEventRecord(c->ev[2 * i], st));
         int r = 0;
         switch (L.kind) {
         case K_MC:
-            r = vp9hip_launch_mc(c->hb, c->st, (int) L.n, (const McUnit *) (s.arena + s.o_mcs), fr);
+            r = vp9hip_launch_mc(c->hb, st, (int) L.n, (const McUnit *) (s.arena + s.o_mcs), fr);
             break;
         case K_RESID:
-            r = vp9hip_launch_resid(c->hb, c->st, L.arg, (int) L.n, (const RJob *) (s.arena + s.o_rjobs) + L.off, fr,
+            r = vp9hip_launch_resid(c->hb, st, L.arg, (int) L.n, (const RJob *) (s.arena + s.o_rjobs) + L.off, fr,
                                     s.arena + s.o_coefs, s.resid);
             break;
         case K_PRED:
-            r = vp9hip_launch_pred(c->hb, c->st, (int) L.n, lists + L.off, (const SBRec *) (s.arena + s.o_sbs),
+            r = vp9hip_launch_pred(c->hb, st, (int) L.n, lists + L.off, (const SBRec *) (s.arena + s.o_sbs),
                                    (const PJob *) (s.arena + s.o_pjobs), (const uint16_t *) (s.arena + s.o_passes),
                                    fr, s.resid, c->ptab, c->dbg);
             break;
         case K_LF:
-            r = vp9hip_launch_lf(c->hb, c->st, (int) L.n, lists + L.off, (const LFRec *) (s.arena + s.o_lfs), fr);
+            r = vp9hip_launch_lf(c->hb, st, (int) L.n, lists + L.off, (const LFRec *) (s.arena + s.o_lfs), fr);
             break;
         }
         if (r) return VP9HIP_EEXTERNAL;
-        if (c->timing) HIPCHK(hipEventRecord(c->ev[2 * i + 1], c->st));
+        if (c->timing) HIPCHK(hipEventRecord(c->ev[2 * i + 1], st));
+    }
+    // join: the main stream (downloads, sync, the next stage) waits for every group
+    for (int g = 1; g < s.ngroups; g++) {
+        HIPCHK(hipEventRecord(c->join_ev[g - 1], c->xst[g - 1]));
+        HIPCHK(hipStreamWaitEvent(c->st, c->join_ev[g - 1], 0));
     }
     return 0;
 }
@@ -877,6 +910,7 @@ extern "C" int vp9hip_plan_stats(const vp9h_frame *f, double *out, int cap)
     fb.ss_h = f->ss_h; fb.ss_v = f->ss_v; fb.coef_size = f->bpp > 8 ? 4 : 2;
     fb.pitch[0] = fb.sb_cols * 64; fb.pitch[1] = fb.sb_cols * 32;
     fb.coef_base = 0;
+    fb.group = 0;
     std::vector<std::vector<uint32_t>> ps, ls;
     int r = build_frame(nullptr, s, fb, ps, ls);
     if (r < 0) return r;
@@ -885,7 +919,7 @@ extern "C" int vp9hip_plan_stats(const vp9h_frame *f, double *out, int cap)
     out[1] = (double) s.passes.size();
     out[2] = (double) s.pjobs.size();
     size_t nr = 0;
-    for (auto &bt : s.rbucket) for (auto &bk : bt) nr += bk.size();
+    for (auto &bt : s.rbucket[0]) for (auto &bk : bt) nr += bk.size();
     out[3] = (double) nr;
     double used = 0, capsum = 0;
     for (uint16_t w : s.passes) {
