@@ -34,11 +34,11 @@
 extern "C" {
 int vp9hip_launch_resid(int hb, hipStream_t st, int tcode, int n, const RJob *jobs, const FrameDesc *frames,
                         const void *coefs, int16_t *resid);
-int vp9hip_launch_pred(int hb, hipStream_t st, int nsb, const uint32_t *list, const SBRec *sbs,
-                       const PJob *jobs, const uint16_t *passes, const FrameDesc *frames, const int16_t *resid,
+int vp9hip_launch_pred(int hb, hipStream_t st, int nwg, const uint32_t *list, const WGRec *wgs, const SBRec *sbs,
+                       const PJob *jobs, const uint32_t *passes, const FrameDesc *frames, const int16_t *resid,
                        const uint32_t *ptab, int dbg);
 int vp9hip_launch_lf(int hb, hipStream_t st, int nsb, const uint32_t *list, const LFRec *recs,
-                     const FrameDesc *frames);
+                     const FrameDesc *frames, int dbg);
 int vp9hip_launch_mc(int hb, hipStream_t st, int n, const McUnit *units, const FrameDesc *frames);
 }
 
@@ -57,8 +57,14 @@ struct Staged {
     // host images (kept for rebuilds / inspection)
     std::vector<FrameDesc> frames;
     std::vector<SBRec> sbs;
-    std::vector<PJob> pjobs;
-    std::vector<uint16_t> passes;
+    std::vector<PJob> pjobs;            // merged per workgroup, pass order (device)
+    std::vector<uint32_t> passes;       // pass words (device)
+    std::vector<WGRec> wgs;             // k_pred workgroups (device)
+    // per-SB intra jobs before merging (host): sorted by (level, ts, mode)
+    struct SBHost { uint32_t job0, njobs, lv0, nlev; };
+    std::vector<SBHost> sbh;
+    std::vector<PJob> sbjobs;
+    std::vector<uint32_t> sblv;         // level starts (relative to job0), nlev + 1 per SB
     std::vector<RJob> rbucket[MAX_GROUPS][5][4];    // residual jobs by (group, tx code, txtp)
     int ngroups = 1;
     std::vector<RJob> rjobs;            // concatenated buckets
@@ -72,10 +78,12 @@ struct Staged {
     // device arena
     uint8_t *arena = nullptr;
     size_t arena_cap = 0;
-    size_t o_frames = 0, o_sbs = 0, o_pjobs = 0, o_passes = 0, o_rjobs = 0, o_lfs = 0, o_mcs = 0, o_lists = 0, o_coefs = 0;
+    size_t o_frames = 0, o_sbs = 0, o_pjobs = 0, o_passes = 0, o_wgs = 0, o_rjobs = 0, o_lfs = 0, o_mcs = 0, o_lists = 0,
+           o_coefs = 0;
     int16_t *resid = nullptr;           // intra residual scratch (column-major n x n blocks)
     size_t resid_cap = 0;               // bytes
     bool ready = false;
+    hipGraphExec_t graph = nullptr;     // captured launch sequence of this batch (timing off)
 };
 
 } // namespace
@@ -93,6 +101,7 @@ struct vp9hip_ctx {
     std::vector<uint8_t *> bufs;
     uint32_t *ptab = nullptr;           // intra predictor formula table (device)
     int dbg = 0;                        // VP9HIP_DEBUG: ablation switches for profiling only
+    bool use_graph = true;              // VP9HIP_GRAPH=0 disables graph replay
     Staged stg;
     // timing of the last run
     bool timing = true;
@@ -112,6 +121,7 @@ extern "C" int vp9hip_open(int device, vp9hip_ctx **out)
     vp9hip_ctx *c = new vp9hip_ctx;
     c->dev = device;
     if (const char *d = getenv("VP9HIP_DEBUG")) c->dbg = atoi(d);
+    if (const char *g = getenv("VP9HIP_GRAPH")) c->use_graph = atoi(g) != 0;
     if (const char *g = getenv("VP9HIP_STREAMS")) c->max_groups = std::max(1, std::min(MAX_GROUPS, atoi(g)));
     bool ok = hipSetDevice(device) == hipSuccess && hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) == hipSuccess;
@@ -140,6 +150,7 @@ extern "C" void vp9hip_close(vp9hip_ctx *c)
     free_bufs(c);
     if (c->stg.arena) hipFree(c->stg.arena);
     if (c->stg.resid) hipFree(c->stg.resid);
+    if (c->stg.graph) hipGraphExecDestroy(c->stg.graph);
     if (c->ptab) hipFree(c->ptab);
     for (auto e : c->ev) hipEventDestroy(e);
     hipStreamDestroy(c->st);
@@ -566,20 +577,19 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
             SBRec sr;
             memset(&sr, 0, sizeof(sr));
             sr.frame = fb.frame_idx; sr.sbx = sbx; sr.sby = sby;
-            sr.job0 = (uint32_t) s.pjobs.size();
-            sr.pass0 = (uint32_t) s.passes.size();
             sr.tile_x0 = (uint16_t) tile_x0;
-            sr.njobs = (uint16_t) pj.size();
             sr.flags = intra_frame ? 0 : 1;
-            for (size_t k = 0; k < pj.size();) {
-                const int ts = pj[k].ts, cap = 64 >> (ts + 2);
-                size_t e = k + 1;
-                while (e < pj.size() && (int) (e - k) < cap && pj[e].level == pj[k].level && pj[e].ts == ts) e++;
-                s.passes.push_back((uint16_t) ((k << 7) | ((e - k - 1) << 3) | ts));
-                k = e;
+            Staged::SBHost h;
+            h.job0 = (uint32_t) s.sbjobs.size();
+            h.njobs = (uint32_t) pj.size();
+            h.lv0 = (uint32_t) s.sblv.size();
+            for (size_t k = 0; k < pj.size(); k++) {
+                if (k == 0 || pj[k].level != pj[k - 1].level) s.sblv.push_back((uint32_t) k);
+                s.sbjobs.push_back(pj[k].j);
             }
-            sr.npass = (uint16_t) (s.passes.size() - sr.pass0);
-            for (auto &q : pj) s.pjobs.push_back(q.j);
+            s.sblv.push_back((uint32_t) pj.size());
+            h.nlev = (uint32_t) (s.sblv.size() - h.lv0 - 1);
+            s.sbh.push_back(h);
             uint32_t sbi = (uint32_t) s.sbs.size();
             s.sbs.push_back(sr);
             int d = (sbx - tile_sb0) + sby;
@@ -599,6 +609,76 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
     return 0;
 }
 
+// Zip the dependency levels of up to PRED_K superblocks into shared passes (one k_pred
+// wavefront). Each SB advances through its levels in order; a pass takes jobs of one tx
+// size from the current level of any SBs, up to 64/n jobs. Greedy: the size whose pass
+// is fullest wins, ties broken by how many SBs it lets finish their level.
+static int g_pass_cap[4] = { 16, 8, 4, 2 };     // jobs per pass by tx size
+static int merge_wg(Staged &s, const uint32_t *sbl, int k)
+{
+    WGRec wg;
+    memset(&wg, 0xff, sizeof(wg));
+    wg.job0 = (uint32_t) s.pjobs.size();
+    wg.pass0 = (uint32_t) s.passes.size();
+    struct Cur { uint32_t lev, pos[4], end[4]; } cur[PRED_K];
+    auto open_level = [&](int i) {
+        const Staged::SBHost &h = s.sbh[sbl[i]];
+        Cur &c = cur[i];
+        for (int t = 0; t < 4; t++) c.pos[t] = c.end[t] = 0;
+        if (c.lev >= h.nlev) return;
+        const uint32_t b = s.sblv[h.lv0 + c.lev], e = s.sblv[h.lv0 + c.lev + 1];
+        for (uint32_t j = b; j < e; j++) {          // jobs of a level are sorted by ts
+            const int t = PJ_TS(s.sbjobs[h.job0 + j]);
+            if (c.end[t] == 0) c.pos[t] = j;
+            c.end[t] = j + 1;
+        }
+    };
+    for (int i = 0; i < k; i++) { wg.sb[i] = sbl[i]; cur[i].lev = 0; open_level(i); }
+    for (;;) {
+        int best = -1;
+        double score = 0;
+        for (int t = 0; t < 4; t++) {
+            const int cap = g_pass_cap[t];
+            int tot = 0, fin = 0;
+            for (int i = 0; i < k; i++) {
+                const int n = (int) (cur[i].end[t] - cur[i].pos[t]);
+                if (!n) continue;
+                tot += n;
+                bool only = n <= cap;
+                for (int u = 0; u < 4; u++) if (u != t && cur[i].end[u] > cur[i].pos[u]) only = false;
+                fin += only;
+            }
+            if (!tot) continue;
+            const double sc = (double) std::min(tot, cap) / cap + 0.25 * fin;
+            if (sc > score) { score = sc; best = t; }
+        }
+        if (best < 0) break;
+        const int cap = g_pass_cap[best];
+        const uint32_t first = (uint32_t) (s.pjobs.size() - wg.job0);
+        int taken = 0;
+        for (int i = 0; i < k && taken < cap; i++) {
+            Cur &c = cur[i];
+            const Staged::SBHost &h = s.sbh[sbl[i]];
+            while (c.pos[best] < c.end[best] && taken < cap) {
+                PJob p = s.sbjobs[h.job0 + c.pos[best]++];
+                p.a |= (uint32_t) i << 30;
+                s.pjobs.push_back(p);
+                taken++;
+            }
+            bool empty = true;
+            for (int t = 0; t < 4; t++) if (c.end[t] > c.pos[t]) empty = false;
+            if (empty && c.lev < h.nlev) { c.lev++; open_level(i); }
+        }
+        s.passes.push_back(first << 8 | (uint32_t) (taken - 1) << 3 | (uint32_t) best);
+    }
+    const size_t nj = s.pjobs.size() - wg.job0, np = s.passes.size() - wg.pass0;
+    if (nj > PRED_K * MAX_SB_JOBS || np > PRED_K * MAX_SB_JOBS) return VP9HIP_EINVALIDDATA;
+    wg.njobs = (uint16_t) nj;
+    wg.npass = (uint16_t) np;
+    s.wgs.push_back(wg);
+    return 0;
+}
+
 static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bufs, const int *ref_bufs /*n*3 or null*/)
 {
     if (!c || !pkts || n <= 0 || !out_bufs) return VP9HIP_EINVAL;
@@ -606,7 +686,9 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     hipSetDevice(c->dev);
     HIPCHK(hipStreamSynchronize(c->st));      // the previous batch may still read the arena
     Staged &s = c->stg;
+    if (s.graph) { hipGraphExecDestroy(s.graph); s.graph = nullptr; }
     s.frames.clear(); s.sbs.clear(); s.pjobs.clear(); s.passes.clear(); s.lfs.clear(); s.mcs.clear();
+    s.wgs.clear(); s.sbh.clear(); s.sbjobs.clear(); s.sblv.clear();
     s.rjobs.clear(); s.resid16 = 0;
     for (auto &bg : s.rbucket) for (auto &bt : bg) for (auto &bk : bt) bk.clear();
     s.lists.clear(); s.launches.clear(); s.coefs.clear();
@@ -693,7 +775,16 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
             s.launches.push_back({ kind, (uint32_t) s.lists.size(), (uint32_t) v.size(), 0, g });
             s.lists.insert(s.lists.end(), v.begin(), v.end());
         };
-        for (auto &v : psteps[g]) add_list(K_PRED, v);
+        for (auto &v : psteps[g]) {
+            // SBs of a step -> workgroups of PRED_K (any frames: they are independent)
+            std::vector<uint32_t> wl;
+            for (size_t i = 0; i < v.size(); i += PRED_K) {
+                wl.push_back((uint32_t) s.wgs.size());
+                int r = merge_wg(s, v.data() + i, (int) std::min<size_t>(PRED_K, v.size() - i));
+                if (r) return r;
+            }
+            add_list(K_PRED, wl);
+        }
         for (auto &v : lsteps[g]) add_list(K_LF, v);
     }
     if (s.resid16 > 0xffffffffull) return VP9HIP_ENOMEM;
@@ -704,7 +795,8 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     s.o_frames = o; o = al(o + s.frames.size() * sizeof(FrameDesc));
     s.o_sbs = o; o = al(o + s.sbs.size() * sizeof(SBRec));
     s.o_pjobs = o; o = al(o + s.pjobs.size() * sizeof(PJob));
-    s.o_passes = o; o = al(o + s.passes.size() * sizeof(uint16_t));
+    s.o_passes = o; o = al(o + s.passes.size() * sizeof(uint32_t));
+    s.o_wgs = o; o = al(o + s.wgs.size() * sizeof(WGRec));
     s.o_rjobs = o; o = al(o + s.rjobs.size() * sizeof(RJob));
     s.o_lfs = o; o = al(o + s.lfs.size() * sizeof(LFRec));
     s.o_mcs = o; o = al(o + s.mcs.size() * sizeof(McUnit));
@@ -732,7 +824,8 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     if (up(s.o_frames, s.frames.data(), s.frames.size() * sizeof(FrameDesc)) ||
         up(s.o_sbs, s.sbs.data(), s.sbs.size() * sizeof(SBRec)) ||
         up(s.o_pjobs, s.pjobs.data(), s.pjobs.size() * sizeof(PJob)) ||
-        up(s.o_passes, s.passes.data(), s.passes.size() * sizeof(uint16_t)) ||
+        up(s.o_passes, s.passes.data(), s.passes.size() * sizeof(uint32_t)) ||
+        up(s.o_wgs, s.wgs.data(), s.wgs.size() * sizeof(WGRec)) ||
         up(s.o_rjobs, s.rjobs.data(), s.rjobs.size() * sizeof(RJob)) ||
         up(s.o_lfs, s.lfs.data(), s.lfs.size() * sizeof(LFRec)) ||
         up(s.o_mcs, s.mcs.data(), s.mcs.size() * sizeof(McUnit)) ||
@@ -749,10 +842,32 @@ extern "C" int vp9hip_stage_batch(vp9hip_ctx *c, const vp9h_frame *pkts, int n, 
     return stage(c, pkts, n, out_bufs, nullptr);
 }
 
+static int enqueue_batch(vp9hip_ctx *c);
+
+// Run the staged batch. Without per-launch timing the ~300 launches of a 4K batch are
+// captured once into a HIP graph (both frame-group streams) and replayed.
 extern "C" int vp9hip_run_batch(vp9hip_ctx *c)
 {
     if (!c || !c->stg.ready) return VP9HIP_EINVAL;
     hipSetDevice(c->dev);
+    Staged &s = c->stg;
+    if (c->timing || !c->use_graph) return enqueue_batch(c);
+    if (!s.graph) {
+        hipGraph_t g = nullptr;
+        HIPCHK(hipStreamBeginCapture(c->st, hipStreamCaptureModeThreadLocal));
+        int r = enqueue_batch(c);
+        hipError_t e = hipStreamEndCapture(c->st, &g);
+        if (r || e != hipSuccess) { if (g) hipGraphDestroy(g); return r ? r : VP9HIP_EEXTERNAL; }
+        e = hipGraphInstantiate(&s.graph, g, nullptr, nullptr, 0);
+        hipGraphDestroy(g);
+        if (e != hipSuccess) { s.graph = nullptr; return VP9HIP_EEXTERNAL; }
+    }
+    HIPCHK(hipGraphLaunch(s.graph, c->st));
+    return 0;
+}
+
+static int enqueue_batch(vp9hip_ctx *c)
+{
     Staged &s = c->stg;
     const FrameDesc *fr = (const FrameDesc *) (s.arena + s.o_frames);
     const uint32_t *lists = (const uint32_t *) (s.arena + s.o_lists);
@@ -781,12 +896,12 @@ extern "C" int vp9hip_run_batch(vp9hip_ctx *c)
                                     s.arena + s.o_coefs, s.resid);
             break;
         case K_PRED:
-            r = vp9hip_launch_pred(c->hb, st, (int) L.n, lists + L.off, (const SBRec *) (s.arena + s.o_sbs),
-                                   (const PJob *) (s.arena + s.o_pjobs), (const uint16_t *) (s.arena + s.o_passes),
-                                   fr, s.resid, c->ptab, c->dbg);
+            r = vp9hip_launch_pred(c->hb, st, (int) L.n, lists + L.off, (const WGRec *) (s.arena + s.o_wgs),
+                                   (const SBRec *) (s.arena + s.o_sbs), (const PJob *) (s.arena + s.o_pjobs),
+                                   (const uint32_t *) (s.arena + s.o_passes), fr, s.resid, c->ptab, c->dbg);
             break;
         case K_LF:
-            r = vp9hip_launch_lf(c->hb, st, (int) L.n, lists + L.off, (const LFRec *) (s.arena + s.o_lfs), fr);
+            r = vp9hip_launch_lf(c->hb, st, (int) L.n, lists + L.off, (const LFRec *) (s.arena + s.o_lfs), fr, c->dbg >> 16);
             break;
         }
         if (r) return VP9HIP_EEXTERNAL;
@@ -915,6 +1030,16 @@ extern "C" int vp9hip_plan_stats(const vp9h_frame *f, double *out, int cap)
     int r = build_frame(nullptr, s, fb, ps, ls);
     if (r < 0) return r;
     for (int i = 0; i < 14; i++) out[i] = 0;
+    // workgroups of K SBs from the same intra wavefront step (K = 1 unless VP9HIP_PLAN_K)
+    int K = 1;
+    if (const char *e = getenv("VP9HIP_PLAN_K")) K = std::max(1, std::min(PRED_K, atoi(e)));
+    if (const char *e = getenv("VP9HIP_PLAN_CAP"))
+        sscanf(e, "%d,%d,%d,%d", &g_pass_cap[0], &g_pass_cap[1], &g_pass_cap[2], &g_pass_cap[3]);
+    for (auto &v : ps)
+        for (size_t i = 0; i < v.size(); i += K) {
+            r = merge_wg(s, v.data() + i, (int) std::min<size_t>(K, v.size() - i));
+            if (r) return r;
+        }
     out[0] = (double) s.sbs.size();
     out[1] = (double) s.passes.size();
     out[2] = (double) s.pjobs.size();
@@ -922,13 +1047,13 @@ extern "C" int vp9hip_plan_stats(const vp9h_frame *f, double *out, int cap)
     for (auto &bt : s.rbucket[0]) for (auto &bk : bt) nr += bk.size();
     out[3] = (double) nr;
     double used = 0, capsum = 0;
-    for (uint16_t w : s.passes) {
+    for (uint32_t w : s.passes) {
         out[4 + PASS_TS(w)] += 1;
         used += PASS_NJOBS(w);
-        capsum += 64 >> (PASS_TS(w) + 2);
+        capsum += g_pass_cap[PASS_TS(w)];
     }
     out[8] = capsum ? used / capsum : 0;
-    for (auto &sb : s.sbs) out[9] = std::max(out[9], (double) sb.npass);
+    for (auto &wg : s.wgs) out[9] = std::max(out[9], (double) wg.npass);
     out[10] = (double) s.lfs.size();
     out[11] = (double) s.mcs.size();
     out[12] = (double) ps.size();

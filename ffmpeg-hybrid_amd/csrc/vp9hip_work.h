@@ -78,24 +78,32 @@ typedef struct PJob {
 #define PTAB_SLOT 1360        /* 16 + 64 + 256 + 1024 entries per slot */
 #define PTAB_SIZE (10 * PTAB_SLOT)
 
-/* One superblock of intra work. Its jobs are grouped into "passes": a pass holds up
- * to 64/n independent jobs (same dependency level, same tx size n), so one wavefront
- * runs them side by side, one lane per pixel column. */
+/* One superblock of intra work (geometry only; its jobs live in a WGRec). */
 typedef struct SBRec {
     uint32_t frame;
     uint16_t sbx, sby;
-    uint32_t job0;            /* first PJob (jobs in pass order)                        */
-    uint32_t pass0;           /* first pass word                                        */
-    uint16_t npass, njobs;
     uint16_t tile_x0;         /* tile column start, 8x8 units (vp9.c:1244-1250)         */
     uint16_t flags;           /* bit0: load SB interior first (inter frame)             */
 } SBRec;
 
-/* pass word (u16): first job (relative to job0) << 7 | (njobs - 1) << 3 | ts */
-#define PASS_FIRST(w) ((w) >> 7)
-#define PASS_NJOBS(w) ((((w) >> 3) & 15) + 1)
+/* One k_pred workgroup: up to PRED_K superblocks of the same wavefront step (any frames)
+ * predicted by one wavefront. The host zips the SBs' dependency levels into shared
+ * passes: a pass holds up to 64/n independent jobs of one size n, from any of the
+ * SBs (each SB's jobs in a pass are of one level, levels in order). */
+#define PRED_K 1
+typedef struct WGRec {
+    uint32_t job0;            /* first PJob (merged, pass order)                        */
+    uint32_t pass0;           /* first pass word                                        */
+    uint16_t njobs, npass;
+    uint32_t sb[PRED_K];      /* SBRec index per slot, 0xffffffff = empty              */
+} WGRec;
+
+/* pass word (u32): first job (relative to job0) << 8 | (njobs - 1) << 3 | ts */
+#define PASS_FIRST(w) ((w) >> 8)
+#define PASS_NJOBS(w) ((((w) >> 3) & 31) + 1)
 #define PASS_TS(w) ((w) & 3)
 #define MAX_SB_JOBS 384
+#define PJ_SLOT(j) ((j).a >> 30)
 
 /* Loop-filter data of one SB: VP9Filter (vp9dec.h:83-87) + position. */
 typedef struct LFRec {
