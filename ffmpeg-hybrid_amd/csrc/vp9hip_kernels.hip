@@ -568,6 +568,30 @@ __global__ __launch_bounds__(64 * RWAVES) void k_resid(const RJob *__restrict__ 
 #define CT_SIZE (33 * CP)
 #define TILE_ELEMS (LT_SIZE + 2 * CT_SIZE)
 
+// Lane map of a mixed pass (pass word: first << 14 | c4 << 9 | c8 << 5 | c16 << 2 | c32):
+// lanes [0, 32 c32) serve 32x32 jobs, then 16x16, 8x8, 4x4 -- every group aligned to its
+// size n, one lane per pixel column.
+struct LaneMap { int ts, li, jidx, gstart; bool act; };
+DEV LaneMap lane_map(uint32_t w, int lane)
+{
+    const int c32 = w & 3, c16 = (w >> 2) & 7, c8 = (w >> 5) & 15, c4 = (w >> 9) & 31;
+    const int b32 = 32 * c32, b16 = b32 + 16 * c16, b8 = b16 + 8 * c8, b4 = b8 + 4 * c4;
+    LaneMap m;
+    const int ts = lane < b32 ? 3 : lane < b16 ? 2 : lane < b8 ? 1 : 0;
+    const int base = ts == 3 ? 0 : ts == 2 ? b32 : ts == 1 ? b16 : b8;
+    const int j0 = ts == 3 ? 0 : ts == 2 ? c32 : ts == 1 ? c32 + c16 : c32 + c16 + c8;
+    const int lg = ts + 2, rel = lane - base;
+    m.ts = ts;
+    m.li = rel & ((1 << lg) - 1);
+    m.jidx = j0 + (rel >> lg);
+    m.gstart = lane - m.li;
+    m.act = lane < b4;
+    if (!m.act) m.jidx = 0;
+    return m;
+}
+#define PASS_FIRST_M(w) ((w) >> 14)
+#define PASS_MAXN(w) (((w) & 3) ? 32 : (((w) >> 2) & 7) ? 16 : (((w) >> 5) & 15) ? 8 : 4)
+
 // Prefetched per-lane inputs of one pass: the lane's job record and the first 8 rows
 // of its residual column (named fields, so the set stays in registers). Two sets
 // alternate across passes; the load is unconditional (clamped address), so no
@@ -580,12 +604,11 @@ DEV uint32_t pr_word(const PSet &s, int k)
 
 DEV void prefetch_pass(uint32_t w, int lane, const PJob *lj, const int16_t *__restrict__ resid, PSet &ps)
 {
-    const int ts = PASS_TS(w), lg = ts + 2;
-    const int grp = lane >> lg, li = lane & ((1 << lg) - 1), nj = PASS_NJOBS(w);
-    const PJob jb = lj[PASS_FIRST(w) + (grp < nj ? grp : nj - 1)];
+    const LaneMap m = lane_map(w, lane);
+    const PJob jb = lj[PASS_FIRST_M(w) + m.jidx];
     ps.ja = jb.a;
     ps.jr = jb.roff;
-    ps.r0 = *(const uint4 *) (resid + (PJ_RES(jb) ? (size_t) jb.roff * 16 + (li << lg) : 0));
+    ps.r0 = *(const uint4 *) (resid + (PJ_RES(jb) ? (size_t) jb.roff * 16 + (m.li << (m.ts + 2)) : 0));
 }
 
 // Load the pixels above / left of an SB (and, for inter frames, its interior: the
@@ -646,32 +669,38 @@ DEV void load_sb_tile(const FrameDesc &fd, int sbx, int sby, bool interior, int 
 }
 
 // One pass of N x N jobs: lane li of group grp predicts column li of its job.
-template <int N, typename PIX>
-DEV void pred_pass(const PJob &jb, bool act, int li, int grp, PIX *tile, uint16_t *eb, int bd,
-                   const PSet &ps, const uint32_t *ltab, const int16_t *__restrict__ resid,
-                   const uint32_t *__restrict__ ptab, int dbg)
+// One mixed pass: lane li of an n x n job predicts pixel column li (rows 0..n-1); the
+// row loop runs to the pass's largest n (MAXN, unrolled), rows >= n are masked.
+template <int MAXN, typename PIX>
+DEV void pred_pass(uint32_t w, int lane, PIX *tile, uint16_t *eb, int bd, const PSet &ps, const uint32_t *ltab,
+                   const int16_t *__restrict__ resid, const uint32_t *__restrict__ ptab, int dbg)
 {
-    constexpr int TS = N == 4 ? 0 : N == 8 ? 1 : N == 16 ? 2 : 3;
-    constexpr int TOFF = N == 4 ? 0 : N == 8 ? 16 : N == 16 ? 80 : 336;
+    const LaneMap m = lane_map(w, lane);
+    PJob jb;
+    jb.a = ps.ja;
+    jb.roff = ps.jr;
+    const int ts = m.ts, n = 4 << ts, li = m.li;
+    const bool act = m.act;
     const int p = PJ_PLANE(jb);
     const int tpch = p ? CP : LP;
     PIX *o = tile + PJ_SLOT(jb) * TILE_ELEMS + (p == 0 ? 0 : p == 1 ? LT_SIZE : LT_SIZE + CT_SIZE) +
              (PJ_Y4(jb) * 4 + 1) * tpch + PJ_X4(jb) * 4 + 1;
     const int ms = PJ_MSLOT(jb), slot = ms < 9 ? ms : 9;
-    // formula words of this column: 4x4 / 8x8 from the LDS copy, larger from L1/L2;
+    const int toff = ts == 0 ? 0 : ts == 1 ? 16 : ts == 2 ? 80 : 336;
+    // formula words of this column: rows of 4x4 / 8x8 from the LDS copy, larger from L1/L2;
     // residual rows >= 8 of 16x16 / 32x32 loaded here
-    uint32_t f[N];
-    uint32_t rx[N > 8 ? (N - 8) / 2 : 1];
-    if (N <= 8) {
+    uint32_t f[MAXN];
+    uint32_t rx[MAXN > 8 ? (MAXN - 8) / 2 : 1];
+    if (MAXN <= 8) {
 #pragma unroll
-        for (int y = 0; y < N; y++) f[y] = ltab[slot * 80 + TOFF + y * N + li];
+        for (int y = 0; y < MAXN; y++) f[y] = ltab[slot * 80 + toff + (y < n ? y : 0) * n + li];
     } else {
-        const uint32_t *tb = ptab + slot * PTAB_SLOT + TOFF + li;
+        const uint32_t *tl = ts <= 1 ? ltab + slot * 80 + toff + li : ptab + slot * PTAB_SLOT + toff + li;
 #pragma unroll
-        for (int y = 0; y < N; y++) f[y] = tb[y * N];
-        const uint32_t *r = (const uint32_t *) (resid + (PJ_RES(jb) ? (size_t) jb.roff * 16 + li * N : 0));
+        for (int y = 0; y < MAXN; y++) f[y] = tl[(y < n ? y : 0) * n];
+        const uint32_t *r = (const uint32_t *) (resid + (PJ_RES(jb) && ts >= 2 ? (size_t) jb.roff * 16 + li * n : 0));
 #pragma unroll
-        for (int k = 4; k < N / 2; k++) rx[k - 4] = r[k];
+        for (int k = 4; k < MAXN / 2; k++) rx[k - 4] = r[k < n / 2 ? k : 0];
     }
 
     // edges (fills: vp9recon.c:103-210): every load hits a valid tile address, the
@@ -680,30 +709,30 @@ DEV void pred_pass(const PJob &jb, bool act, int li, int grp, PIX *tile, uint16_
     const int htop = PJ_HTOP(jb), hleft = PJ_HLEFT(jb), ct = PJ_CT(jb), cl = PJ_CL(jb);
     const PIX *orow = o - tpch;
     const int t_px = orow[li < ct ? li : ct];
-    const int l_px = o[(N - 1 - li < cl ? N - 1 - li : cl) * tpch - 1];
+    const int l_px = o[(n - 1 - li < cl ? n - 1 - li : cl) * tpch - 1];
     const int tl_px = orow[-1];
+    const int tr_px = orow[PJ_TRREAL(jb) ? 4 + li : ct];
     const int tv = htop ? t_px : base - 1;
     const int lv = hleft ? l_px : base + 1;
     const int tl = (hleft & htop) ? tl_px : base + (htop ? 1 : -1);
-    int tr = 0;
-    if (N == 4) {
-        const int tr_px = orow[PJ_TRREAL(jb) ? 4 + li : ct];
-        tr = htop ? tr_px : base - 1;
-    }
-    uint16_t *e = eb + grp * (2 * N + 8);
+    const int tr = htop ? tr_px : base - 1;
+    uint16_t *e = eb + 2 * m.gstart + 8 * m.jidx;
     if (act && !(dbg & 16)) {
         e[li] = (uint16_t) lv;
-        e[N + 1 + li] = (uint16_t) tv;
-        if (N == 4) e[N + 5 + li] = (uint16_t) tr;
-        e[N] = (uint16_t) tl;                  // every lane of the group writes the same value
+        e[n + 1 + li] = (uint16_t) tv;
+        if (ts == 0) e[n + 5 + li] = (uint16_t) tr;
+        e[n] = (uint16_t) tl;                  // every lane of the group writes the same value
     }
-    // DC sums over the group's N lanes (only when the pass holds a DC/LEFT_DC/TOP_DC job)
+    // DC sums over the job's n lanes (only when the pass holds a DC/LEFT_DC/TOP_DC job)
     int dc = ms == 12 ? base : ms == 13 ? base - 1 : base + 1;
     if (__any(act && ms >= 9 && ms <= 11)) {
         int sl = lv, st = tv;
 #pragma unroll
-        for (int m = 1; m < N; m <<= 1) { sl += __shfl_xor(sl, m); st += __shfl_xor(st, m); }
-        const int d9 = (sl + st + N) >> (TS + 3), d10 = (sl + (N >> 1)) >> (TS + 2), d11 = (st + (N >> 1)) >> (TS + 2);
+        for (int k = 1; k < MAXN; k <<= 1) {
+            const int a = __shfl_xor(sl, k), b = __shfl_xor(st, k);
+            if (k < n) { sl += a; st += b; }
+        }
+        const int d9 = (sl + st + n) >> (ts + 3), d10 = (sl + (n >> 1)) >> (ts + 2), d11 = (st + (n >> 1)) >> (ts + 2);
         dc = ms == 9 ? d9 : ms == 10 ? d10 : ms == 11 ? d11 : dc;
     }
     wave_sync();
@@ -711,14 +740,15 @@ DEV void pred_pass(const PJob &jb, bool act, int li, int grp, PIX *tile, uint16_
         const int mx = (1 << bd) - 1;
         const int hr = PJ_RES(jb);
 #pragma unroll
-        for (int y = 0; y < N; y++) {
-            const uint32_t w = f[y];
-            const int a = e[w & 127], b = e[(w >> 7) & 127], c = e[(w >> 14) & 127];
-            const int wb = (w >> 21) & 3, s = (w >> 25) & 3;
-            const int wc = __builtin_amdgcn_sbfe((int) w, 23, 2);
+        for (int y = 0; y < MAXN; y++) {
+            if (MAXN > 4 && y >= n) continue;
+            const uint32_t fw = f[y];
+            const int a = e[fw & 127], b = e[(fw >> 7) & 127], c = e[(fw >> 14) & 127];
+            const int wb = (fw >> 21) & 3, s = (fw >> 25) & 3;
+            const int wc = __builtin_amdgcn_sbfe((int) fw, 23, 2);
             int v = (a + wb * b + wc * c + ((1 << s) >> 1)) >> s;
             v = min(max(v, 0), mx);
-            v = (w >> 27) ? dc : v;
+            v = (fw >> 27) ? dc : v;
             const uint32_t rw = y < 8 ? pr_word(ps, y >> 1) : rx[y < 8 ? 0 : (y >> 1) - 4];
             const int r = (int) (int16_t) (rw >> ((y & 1) * 16));
             v += hr ? r : 0;
@@ -732,17 +762,11 @@ template <typename PIX>
 DEV void run_pass(uint32_t w, int lane, PIX *tile, uint16_t *eb, int bd, const PSet &ps, const uint32_t *ltab,
                   const int16_t *__restrict__ resid, const uint32_t *__restrict__ ptab, int dbg)
 {
-    const int ts = PASS_TS(w), lg = ts + 2;
-    const int grp = lane >> lg, li = lane & ((1 << lg) - 1);
-    const bool act = grp < PASS_NJOBS(w);
-    PJob jb;
-    jb.a = ps.ja;
-    jb.roff = ps.jr;
-    switch (ts) {
-    case 0: pred_pass<4, PIX>(jb, act, li, grp, tile, eb, bd, ps, ltab, resid, ptab, dbg); break;
-    case 1: pred_pass<8, PIX>(jb, act, li, grp, tile, eb, bd, ps, ltab, resid, ptab, dbg); break;
-    case 2: pred_pass<16, PIX>(jb, act, li, grp, tile, eb, bd, ps, ltab, resid, ptab, dbg); break;
-    default: pred_pass<32, PIX>(jb, act, li, grp, tile, eb, bd, ps, ltab, resid, ptab, dbg); break;
+    switch (PASS_MAXN(w)) {
+    case 4: pred_pass<4, PIX>(w, lane, tile, eb, bd, ps, ltab, resid, ptab, dbg); break;
+    case 8: pred_pass<8, PIX>(w, lane, tile, eb, bd, ps, ltab, resid, ptab, dbg); break;
+    case 16: pred_pass<16, PIX>(w, lane, tile, eb, bd, ps, ltab, resid, ptab, dbg); break;
+    default: pred_pass<32, PIX>(w, lane, tile, eb, bd, ps, ltab, resid, ptab, dbg); break;
     }
     wave_sync();
 }

@@ -613,72 +613,6 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
 // wavefront). Each SB advances through its levels in order; a pass takes jobs of one tx
 // size from the current level of any SBs, up to 64/n jobs. Greedy: the size whose pass
 // is fullest wins, ties broken by how many SBs it lets finish their level.
-static int g_pass_cap[4] = { 16, 8, 4, 2 };     // jobs per pass by tx size
-static int merge_wg(Staged &s, const uint32_t *sbl, int k)
-{
-    WGRec wg;
-    memset(&wg, 0xff, sizeof(wg));
-    wg.job0 = (uint32_t) s.pjobs.size();
-    wg.pass0 = (uint32_t) s.passes.size();
-    struct Cur { uint32_t lev, pos[4], end[4]; } cur[PRED_K];
-    auto open_level = [&](int i) {
-        const Staged::SBHost &h = s.sbh[sbl[i]];
-        Cur &c = cur[i];
-        for (int t = 0; t < 4; t++) c.pos[t] = c.end[t] = 0;
-        if (c.lev >= h.nlev) return;
-        const uint32_t b = s.sblv[h.lv0 + c.lev], e = s.sblv[h.lv0 + c.lev + 1];
-        for (uint32_t j = b; j < e; j++) {          // jobs of a level are sorted by ts
-            const int t = PJ_TS(s.sbjobs[h.job0 + j]);
-            if (c.end[t] == 0) c.pos[t] = j;
-            c.end[t] = j + 1;
-        }
-    };
-    for (int i = 0; i < k; i++) { wg.sb[i] = sbl[i]; cur[i].lev = 0; open_level(i); }
-    for (;;) {
-        int best = -1;
-        double score = 0;
-        for (int t = 0; t < 4; t++) {
-            const int cap = g_pass_cap[t];
-            int tot = 0, fin = 0;
-            for (int i = 0; i < k; i++) {
-                const int n = (int) (cur[i].end[t] - cur[i].pos[t]);
-                if (!n) continue;
-                tot += n;
-                bool only = n <= cap;
-                for (int u = 0; u < 4; u++) if (u != t && cur[i].end[u] > cur[i].pos[u]) only = false;
-                fin += only;
-            }
-            if (!tot) continue;
-            const double sc = (double) std::min(tot, cap) / cap + 0.25 * fin;
-            if (sc > score) { score = sc; best = t; }
-        }
-        if (best < 0) break;
-        const int cap = g_pass_cap[best];
-        const uint32_t first = (uint32_t) (s.pjobs.size() - wg.job0);
-        int taken = 0;
-        for (int i = 0; i < k && taken < cap; i++) {
-            Cur &c = cur[i];
-            const Staged::SBHost &h = s.sbh[sbl[i]];
-            while (c.pos[best] < c.end[best] && taken < cap) {
-                PJob p = s.sbjobs[h.job0 + c.pos[best]++];
-                p.a |= (uint32_t) i << 30;
-                s.pjobs.push_back(p);
-                taken++;
-            }
-            bool empty = true;
-            for (int t = 0; t < 4; t++) if (c.end[t] > c.pos[t]) empty = false;
-            if (empty && c.lev < h.nlev) { c.lev++; open_level(i); }
-        }
-        s.passes.push_back(first << 8 | (uint32_t) (taken - 1) << 3 | (uint32_t) best);
-    }
-    const size_t nj = s.pjobs.size() - wg.job0, np = s.passes.size() - wg.pass0;
-    if (nj > PRED_K * MAX_SB_JOBS || np > PRED_K * MAX_SB_JOBS) return VP9HIP_EINVALIDDATA;
-    wg.njobs = (uint16_t) nj;
-    wg.npass = (uint16_t) np;
-    s.wgs.push_back(wg);
-    return 0;
-}
-
 static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bufs, const int *ref_bufs /*n*3 or null*/)
 {
     if (!c || !pkts || n <= 0 || !out_bufs) return VP9HIP_EINVAL;
@@ -778,9 +712,9 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
         for (auto &v : psteps[g]) {
             // SBs of a step -> workgroups of PRED_K (any frames: they are independent)
             std::vector<uint32_t> wl;
-            for (size_t i = 0; i < v.size(); i += PRED_K) {
+            for (size_t i = 0; i < v.size(); i++) {
                 wl.push_back((uint32_t) s.wgs.size());
-                int r = merge_wg(s, v.data() + i, (int) std::min<size_t>(PRED_K, v.size() - i));
+                int r = merge_mixed(s, v[i]);
                 if (r) return r;
             }
             add_list(K_PRED, wl);
@@ -1030,29 +964,26 @@ extern "C" int vp9hip_plan_stats(const vp9h_frame *f, double *out, int cap)
     int r = build_frame(nullptr, s, fb, ps, ls);
     if (r < 0) return r;
     for (int i = 0; i < 14; i++) out[i] = 0;
-    // workgroups of K SBs from the same intra wavefront step (K = 1 unless VP9HIP_PLAN_K)
-    int K = 1;
-    if (const char *e = getenv("VP9HIP_PLAN_K")) K = std::max(1, std::min(PRED_K, atoi(e)));
-    if (const char *e = getenv("VP9HIP_PLAN_CAP"))
-        sscanf(e, "%d,%d,%d,%d", &g_pass_cap[0], &g_pass_cap[1], &g_pass_cap[2], &g_pass_cap[3]);
+    // one k_pred workgroup per SB, mixed-size passes (as staged for the device)
     for (auto &v : ps)
-        for (size_t i = 0; i < v.size(); i += K) {
-            r = merge_wg(s, v.data() + i, (int) std::min<size_t>(K, v.size() - i));
+        for (uint32_t sbi : v) {
+            r = merge_mixed(s, sbi);
             if (r) return r;
         }
+    for (int i = 0; i < 14; i++) out[i] = 0;
     out[0] = (double) s.sbs.size();
     out[1] = (double) s.passes.size();
     out[2] = (double) s.pjobs.size();
     size_t nr = 0;
     for (auto &bt : s.rbucket[0]) for (auto &bk : bt) nr += bk.size();
     out[3] = (double) nr;
-    double used = 0, capsum = 0;
+    double lanes = 0;
     for (uint32_t w : s.passes) {
-        out[4 + PASS_TS(w)] += 1;
-        used += PASS_NJOBS(w);
-        capsum += g_pass_cap[PASS_TS(w)];
+        const int c4 = (w >> 9) & 31, c8 = (w >> 5) & 15, c16 = (w >> 2) & 7, c32 = w & 3;
+        out[4] += c4; out[5] += c8; out[6] += c16; out[7] += c32;      // jobs per tx size
+        lanes += 4 * c4 + 8 * c8 + 16 * c16 + 32 * c32;
     }
-    out[8] = capsum ? used / capsum : 0;
+    out[8] = s.passes.empty() ? 0 : lanes / (64.0 * s.passes.size());
     for (auto &wg : s.wgs) out[9] = std::max(out[9], (double) wg.npass);
     out[10] = (double) s.lfs.size();
     out[11] = (double) s.mcs.size();

@@ -90,7 +90,7 @@ typedef struct SBRec {
  * predicted by one wavefront. The host zips the SBs' dependency levels into shared
  * passes: a pass holds up to 64/n independent jobs of one size n, from any of the
  * SBs (each SB's jobs in a pass are of one level, levels in order). */
-#define PRED_K 1
+#define PRED_K 1          /* slots per workgroup (the kernel supports more; 1 measured best) */
 typedef struct WGRec {
     uint32_t job0;            /* first PJob (merged, pass order)                        */
     uint32_t pass0;           /* first pass word                                        */
