@@ -287,8 +287,8 @@ class Decoder:
         return visible(self.dev.download(buf), w, h)
 
 
-PLAN_STAT_NAMES = ("sbs", "passes", "pjobs", "rjobs", "passes_4x4", "passes_8x8", "passes_16x16",
-                   "passes_32x32", "lane_use", "max_passes_sb", "lf_records", "mc_units", "pred_steps",
+PLAN_STAT_NAMES = ("sbs", "passes", "pjobs", "rjobs", "jobs_4x4", "jobs_8x8", "jobs_16x16",
+                   "jobs_32x32", "lane_use", "max_passes_sb", "lf_records", "mc_units", "pred_steps",
                    "lf_steps")
 
 

@@ -609,10 +609,47 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
     return 0;
 }
 
-// Zip the dependency levels of up to PRED_K superblocks into shared passes (one k_pred
-// wavefront). Each SB advances through its levels in order; a pass takes jobs of one tx
-// size from the current level of any SBs, up to 64/n jobs. Greedy: the size whose pass
-// is fullest wins, ties broken by how many SBs it lets finish their level.
+// Mixed-size packing of one SB's intra jobs: a pass takes jobs of one dependency level
+// of any sizes, 64 lanes = n lanes per n x n job; jobs in a pass are ordered 32x32,
+// 16x16, 8x8, 4x4 so every job's lane group is aligned to its size. Pass word:
+// first << 14 | c4 << 9 | c8 << 5 | c16 << 2 | c32 (job counts per size).
+static int merge_mixed(Staged &s, uint32_t sbi)
+{
+    WGRec wg;
+    memset(&wg, 0xff, sizeof(wg));
+    wg.job0 = (uint32_t) s.pjobs.size();
+    wg.pass0 = (uint32_t) s.passes.size();
+    wg.sb[0] = sbi;
+    const Staged::SBHost &h = s.sbh[sbi];
+    for (uint32_t l = 0; l < h.nlev; l++) {
+        const uint32_t b = s.sblv[h.lv0 + l], e = s.sblv[h.lv0 + l + 1];
+        std::vector<uint32_t> by[4];
+        for (uint32_t j = b; j < e; j++) by[PJ_TS(s.sbjobs[h.job0 + j])].push_back(h.job0 + j);
+        size_t pos[4] = { 0, 0, 0, 0 };
+        for (;;) {
+            int lanes = 0, cnt[4] = { 0, 0, 0, 0 };
+            const uint32_t first = (uint32_t) (s.pjobs.size() - wg.job0);
+            for (int t = 3; t >= 0; t--) {
+                const int n = 4 << t;
+                while (pos[t] < by[t].size() && lanes + n <= 64) {
+                    s.pjobs.push_back(s.sbjobs[by[t][pos[t]++]]);
+                    lanes += n;
+                    cnt[t]++;
+                }
+            }
+            if (!lanes) break;
+            s.passes.push_back(first << 14 | (uint32_t) cnt[0] << 9 | (uint32_t) cnt[1] << 5 | (uint32_t) cnt[2] << 2 |
+                               (uint32_t) cnt[3]);
+        }
+    }
+    const size_t nj = s.pjobs.size() - wg.job0, np = s.passes.size() - wg.pass0;
+    if (nj > MAX_SB_JOBS || np > MAX_SB_JOBS) return VP9HIP_EINVALIDDATA;
+    wg.njobs = (uint16_t) nj;
+    wg.npass = (uint16_t) np;
+    s.wgs.push_back(wg);
+    return 0;
+}
+
 static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bufs, const int *ref_bufs /*n*3 or null*/)
 {
     if (!c || !pkts || n <= 0 || !out_bufs) return VP9HIP_EINVAL;
@@ -943,9 +980,8 @@ extern "C" int vp9hip_abi_version(void) { return VP9HIP_ABI_VERSION; }
 
 // Host-only planning statistics of one frame (no device needed): used by the CPU tests
 // and to size kernels. out[]: 0 SBs with intra work, 1 passes, 2 intra jobs, 3 residual
-// jobs, 4..7 passes per tx size, 8 sum of jobs over passes / capacity (lane use),
-// 9 max passes in one SB, 10 LF records, 11 MC units, 12 intra wavefront steps,
-// 13 LF wavefront steps.
+// jobs, 4..7 intra jobs per tx size, 8 lane use (job lanes / 64 per pass), 9 max passes
+// in one SB, 10 LF records, 11 MC units, 12 intra wavefront steps, 13 LF wavefront steps.
 extern "C" int vp9hip_plan_stats(const vp9h_frame *f, double *out, int cap)
 {
     if (!f || !out || cap < 14) return VP9HIP_EINVAL;

@@ -152,7 +152,7 @@ int  vp9hip_set_timing(vp9hip_ctx *ctx, int on);
 int  vp9hip_alg_bytes(vp9hip_ctx *ctx, double *bytes, int cap);
 
 /* Host-only planning statistics of one packet (no device needed), 14 values:
- * SBs with intra work, passes, intra jobs, residual jobs, passes per tx size (4),
+ * SBs with intra work, passes, intra jobs, residual jobs, intra jobs per tx size (4),
  * lane use, max passes per SB, LF records, MC units, intra / LF wavefront steps. */
 int  vp9hip_plan_stats(const vp9h_frame *pkt, double *out, int cap);
 

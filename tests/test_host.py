@@ -110,7 +110,8 @@ def test_planner_stats_c3_frame(v9):
     eobs = np.ctypeslib.as_array(f.pkt.eobs, (f.pkt.neobs,))
     assert st["rjobs"] == int((eobs > 0).sum())
     assert st["pjobs"] >= f.pkt.neobs
-    assert st["passes"] >= 26 * st["sbs"] * 0.9
+    assert st["passes"] >= 20 * st["sbs"]        # bounded below by the intra dependency depth
+    assert st["jobs_4x4"] + st["jobs_8x8"] + st["jobs_16x16"] + st["jobs_32x32"] == st["pjobs"]
     assert 0 < st["lane_use"] <= 1
     assert st["pred_steps"] == 15 + 34 - 1     # 4 tile columns of 15 SBs
     assert st["lf_steps"] == 60 + 2 * 33
