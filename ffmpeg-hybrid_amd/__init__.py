@@ -78,7 +78,8 @@ _lib_handle = None
 
 # Exported symbols of include/vp9hip.h (checked by the CPU test suite).
 ABI_SYMBOLS = ["vp9hip_open", "vp9hip_close", "vp9hip_configure", "vp9hip_submit_frame",
-               "vp9hip_stage_batch", "vp9hip_run_batch", "vp9hip_sync", "vp9hip_download_frame",
+               "vp9hip_stage_batch", "vp9hip_stage_batch_refs", "vp9hip_run_batch", "vp9hip_sync",
+               "vp9hip_download_frame",
                "vp9hip_upload_frame", "vp9hip_flush", "vp9hip_last_timing", "vp9hip_set_timing",
                "vp9hip_alg_bytes", "vp9hip_plan_stats", "vp9hip_abi_version",
                "vp9hip_synth_defaults", "vp9hip_synth_frame", "vp9hip_synth_free"]
@@ -99,6 +100,8 @@ def lib():
     L.vp9hip_configure.argtypes = [vp] + [ctypes.c_int] * 6
     L.vp9hip_submit_frame.argtypes = [vp, ctypes.POINTER(FramePacket), ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
     L.vp9hip_stage_batch.argtypes = [vp, ctypes.POINTER(FramePacket), ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+    L.vp9hip_stage_batch_refs.argtypes = [vp, ctypes.POINTER(FramePacket), ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                          ctypes.POINTER(ctypes.c_int)]
     L.vp9hip_run_batch.argtypes = [vp]
     L.vp9hip_sync.argtypes = [vp]
     L.vp9hip_download_frame.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
@@ -199,11 +202,20 @@ class Device:
         pkt = frame.pkt if isinstance(frame, SynthFrame) else frame
         _check("vp9hip_submit_frame", lib().vp9hip_submit_frame(self._c, ctypes.byref(pkt), out_buf, r))
 
-    def stage_batch(self, frames, out_bufs):
+    def stage_batch(self, frames, out_bufs, ref_bufs=None):
+        """Stage a batch; ref_bufs: per frame (LAST, GOLDEN, ALTREF) buffer ids or None
+        (keyframes). Dependent frames are chained, independent chains run concurrently."""
         arr = (FramePacket * len(frames))(*[f.pkt if isinstance(f, SynthFrame) else f for f in frames])
         ob = (ctypes.c_int * len(out_bufs))(*out_bufs)
         self._staged = (arr, frames)   # keep host packets alive
-        _check("vp9hip_stage_batch", lib().vp9hip_stage_batch(self._c, arr, len(frames), ob))
+        if ref_bufs is None:
+            _check("vp9hip_stage_batch", lib().vp9hip_stage_batch(self._c, arr, len(frames), ob))
+            return
+        flat = []
+        for r in ref_bufs:
+            flat += list(r) if r is not None else [0, 0, 0]
+        rb = (ctypes.c_int * len(flat))(*flat)
+        _check("vp9hip_stage_batch_refs", lib().vp9hip_stage_batch_refs(self._c, arr, len(frames), ob, rb))
 
     def run_batch(self):
         _check("vp9hip_run_batch", lib().vp9hip_run_batch(self._c))

@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <functional>
+#include <array>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -65,7 +67,8 @@ struct Staged {
     std::vector<SBHost> sbh;
     std::vector<PJob> sbjobs;
     std::vector<uint32_t> sblv;         // level starts (relative to job0), nlev + 1 per SB
-    std::vector<RJob> rbucket[MAX_GROUPS][5][4];    // residual jobs by (group, tx code, txtp)
+    // residual jobs by (phase, tx code, txtp); a phase = (stream group, chain position)
+    std::vector<std::array<std::array<std::vector<RJob>, 4>, 5>> rbucket;
     int ngroups = 1;
     std::vector<RJob> rjobs;            // concatenated buckets
     uint64_t resid16 = 0;               // residual scratch size, 16-element units
@@ -363,7 +366,7 @@ struct FrameBuild {
     int cols, rows, sb_cols, sb_rows;
     int ss_h, ss_v, coef_size;
     int pitch[2];
-    int group;                   // frame group (launch chain) of this frame
+    int phase;                   // (stream group, chain position) of this frame
     uint64_t coef_base;          // element offset of this frame's coefficients in the batch stream
 };
 
@@ -453,7 +456,7 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
                             } else {
                                 r.dst = (uint32_t) ((size_t) (by + y * 4) * fb.pitch[p ? 1 : 0] + bx + x * 4);
                             }
-                            s.rbucket[fb.group][tcode][txtp].push_back(r);
+                            s.rbucket[fb.phase][tcode][txtp].push_back(r);
                         }
                         coef += e;
                         if (!b->intra) continue;
@@ -661,17 +664,48 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     s.frames.clear(); s.sbs.clear(); s.pjobs.clear(); s.passes.clear(); s.lfs.clear(); s.mcs.clear();
     s.wgs.clear(); s.sbh.clear(); s.sbjobs.clear(); s.sblv.clear();
     s.rjobs.clear(); s.resid16 = 0;
-    for (auto &bg : s.rbucket) for (auto &bt : bg) for (auto &bk : bt) bk.clear();
+    s.rbucket.clear();
     s.lists.clear(); s.launches.clear(); s.coefs.clear();
     for (int k = 0; k < K_N; k++) s.alg_bytes[k] = 0;
     s.ready = false;
 
     const int csz = c->hb ? 4 : 2;
     init_nz();
-    // independent frames are split into groups, one launch chain (HIP stream) each
-    const int G = std::max(1, std::min(c->max_groups, n));
+    // Frame dependencies inside the batch: an inter frame follows the frames whose output
+    // it references, and a frame overwriting a buffer follows every earlier frame that
+    // reads or writes that buffer. Dependent frames form chains; chains are spread over G
+    // stream groups, and within a group frames of equal chain position ("phase") are
+    // interleaved in every launch (a keyframe batch is one phase per group).
+    std::vector<int> pos(n, 0), comp(n);
+    for (int i = 0; i < n; i++) comp[i] = i;
+    std::function<int(int)> find = [&](int x) { return comp[x] == x ? x : comp[x] = find(comp[x]); };
+    for (int i = 0; i < n; i++) {
+        const vp9h_frame *f = &pkts[i];
+        const bool inter = !(f->keyframe || f->intraonly);
+        if (inter && !ref_bufs) return VP9HIP_EINVAL;
+        for (int j = 0; j < i; j++) {
+            bool dep = out_bufs[j] == out_bufs[i];
+            for (int r = 0; r < 3 && !dep; r++) {
+                if (inter && ref_bufs[i * 3 + r] == out_bufs[j]) dep = true;
+                const bool jinter = !(pkts[j].keyframe || pkts[j].intraonly);
+                if (jinter && ref_bufs[j * 3 + r] == out_bufs[i]) dep = true;
+            }
+            if (dep) { pos[i] = std::max(pos[i], pos[j] + 1); comp[find(i)] = find(j); }
+        }
+    }
+    std::vector<int> roots;
+    for (int i = 0; i < n; i++) if (find(i) == i) roots.push_back(i);
+    const int G = std::max(1, std::min<int>(c->max_groups, (int) roots.size()));
     s.ngroups = G;
-    std::vector<std::vector<uint32_t>> psteps[MAX_GROUPS], lsteps[MAX_GROUPS];
+    std::vector<int> grp(n);
+    for (int i = 0; i < n; i++)
+        grp[i] = (int) (std::lower_bound(roots.begin(), roots.end(), find(i)) - roots.begin()) % G;
+    int maxpos = 0;
+    for (int i = 0; i < n; i++) maxpos = std::max(maxpos, pos[i]);
+    const int NP = G * (maxpos + 1);                   // phase id = g * (maxpos + 1) + pos
+    s.rbucket.assign(NP, {});
+    std::vector<std::vector<std::vector<uint32_t>>> psteps(NP), lsteps(NP);
+    std::vector<std::vector<std::pair<uint32_t, uint32_t>>> mcr(NP);   // MC unit ranges per phase
     uint64_t coef_base = 0;
     double pix_bytes = (double) c->w * c->h * c->bypp * (1.0 + 2.0 / ((1 << c->ss_h) * (1 << c->ss_v)));
     for (int i = 0; i < n; i++) {
@@ -680,7 +714,6 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
             return VP9HIP_EINVAL;
         if (out_bufs[i] < 0 || out_bufs[i] >= (int) c->bufs.size()) return VP9HIP_EINVAL;
         const bool intra = f->keyframe || f->intraonly;
-        if (!intra && n != 1) return VP9HIP_EINVAL;     // inter frames are staged one at a time
         FrameDesc fd;
         memset(&fd, 0, sizeof(fd));
         uint8_t *ob = c->bufs[out_bufs[i]];
@@ -692,10 +725,10 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
         fd.bd = c->bpp;
         fd.sharp = f->sharpness;
         if (!intra) {
-            if (!ref_bufs) return VP9HIP_EINVAL;
             for (int r = 0; r < 3; r++) {
                 int rb = ref_bufs[i * 3 + r];
                 if (rb < 0 || rb >= (int) c->bufs.size()) return VP9HIP_EINVAL;
+                if (rb == out_bufs[i]) return VP9HIP_EINVAL;                       // in-place MC
                 if (f->ref_w[r] != c->w || f->ref_h[r] != c->h) return VP9HIP_ENOSYS;  // scaled MC: not yet on device
                 for (int p = 0; p < 3; p++) fd.ref[r][p] = (uint64_t) (c->bufs[rb] + c->plane_off[p]);
                 fd.refw[r][0] = f->ref_w[r]; fd.refh[r][0] = f->ref_h[r];
@@ -709,10 +742,11 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
         fb.ss_h = c->ss_h; fb.ss_v = c->ss_v; fb.coef_size = csz;
         fb.pitch[0] = c->pitch[0]; fb.pitch[1] = c->pitch[1];
         fb.coef_base = coef_base;
-        size_t mc0 = s.mcs.size();
-        fb.group = i % G;
-        int r = build_frame(c, s, fb, psteps[fb.group], lsteps[fb.group]);
+        fb.phase = grp[i] * (maxpos + 1) + pos[i];
+        const size_t mc0 = s.mcs.size();
+        int r = build_frame(c, s, fb, psteps[fb.phase], lsteps[fb.phase]);
         if (r < 0) return r;
+        if (s.mcs.size() > mc0) mcr[fb.phase].push_back({ (uint32_t) mc0, (uint32_t) (s.mcs.size() - mc0) });
         size_t cb = (size_t) f->ncoefs * csz;
         size_t off = s.coefs.size();
         s.coefs.resize(off + cb);
@@ -728,36 +762,37 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
         for (size_t m = mc0; m < s.mcs.size(); m++)
             s.alg_bytes[K_MC] += (double) s.mcs[m].w * s.mcs[m].h * c->bypp * (1 + s.mcs[m].nref);
     }
-    // per group: residual jobs in (tx code, txtp) buckets, then the intra SB wavefront,
-    // then the LF wavefront; inter residual pixels are algorithmic reads + writes of k_resid
-    if (!s.mcs.empty()) s.launches.push_back({ K_MC, 0, (uint32_t) s.mcs.size(), 0, 0 });
-    for (int g = 0; g < G; g++) {
-        for (int t = 0; t < 5; t++) {
-            const uint32_t off = (uint32_t) s.rjobs.size();
-            for (int tp = 0; tp < 4; tp++) {
-                for (auto &r : s.rbucket[g][t][tp])
-                    if (r.ptx & 32) s.alg_bytes[K_RESID] += 2.0 * (16 << (2 * (t & 3))) * c->bypp;
-                s.rjobs.insert(s.rjobs.end(), s.rbucket[g][t][tp].begin(), s.rbucket[g][t][tp].end());
+    // launch schedule per group, phases in chain order: MC, residuals by (tx code, txtp),
+    // the intra SB wavefront, the LF wavefront; inter residual pixels are algorithmic
+    // reads + writes of k_resid
+    for (int g = 0; g < G; g++)
+        for (int ph = g * (maxpos + 1); ph < (g + 1) * (maxpos + 1); ph++) {
+            for (auto &mr : mcr[ph]) s.launches.push_back({ K_MC, mr.first, mr.second, 0, g });
+            for (int t = 0; t < 5; t++) {
+                const uint32_t off = (uint32_t) s.rjobs.size();
+                for (int tp = 0; tp < 4; tp++) {
+                    for (auto &r : s.rbucket[ph][t][tp])
+                        if (r.ptx & 32) s.alg_bytes[K_RESID] += 2.0 * (16 << (2 * (t & 3))) * c->bypp;
+                    s.rjobs.insert(s.rjobs.end(), s.rbucket[ph][t][tp].begin(), s.rbucket[ph][t][tp].end());
+                }
+                if (s.rjobs.size() > off) s.launches.push_back({ K_RESID, off, (uint32_t) (s.rjobs.size() - off), t, g });
             }
-            if (s.rjobs.size() > off) s.launches.push_back({ K_RESID, off, (uint32_t) (s.rjobs.size() - off), t, g });
-        }
-        auto add_list = [&](int kind, const std::vector<uint32_t> &v) {
-            if (v.empty()) return;
-            s.launches.push_back({ kind, (uint32_t) s.lists.size(), (uint32_t) v.size(), 0, g });
-            s.lists.insert(s.lists.end(), v.begin(), v.end());
-        };
-        for (auto &v : psteps[g]) {
-            // SBs of a step -> workgroups of PRED_K (any frames: they are independent)
-            std::vector<uint32_t> wl;
-            for (size_t i = 0; i < v.size(); i++) {
-                wl.push_back((uint32_t) s.wgs.size());
-                int r = merge_mixed(s, v[i]);
-                if (r) return r;
+            auto add_list = [&](int kind, const std::vector<uint32_t> &v) {
+                if (v.empty()) return;
+                s.launches.push_back({ kind, (uint32_t) s.lists.size(), (uint32_t) v.size(), 0, g });
+                s.lists.insert(s.lists.end(), v.begin(), v.end());
+            };
+            for (auto &v : psteps[ph]) {
+                std::vector<uint32_t> wl;             // one workgroup per SB of the step
+                for (size_t i = 0; i < v.size(); i++) {
+                    wl.push_back((uint32_t) s.wgs.size());
+                    int r = merge_mixed(s, v[i]);
+                    if (r) return r;
+                }
+                add_list(K_PRED, wl);
             }
-            add_list(K_PRED, wl);
+            for (auto &v : lsteps[ph]) add_list(K_LF, v);
         }
-        for (auto &v : lsteps[g]) add_list(K_LF, v);
-    }
     if (s.resid16 > 0xffffffffull) return VP9HIP_ENOMEM;
 
     // upload into one arena
@@ -813,6 +848,12 @@ extern "C" int vp9hip_stage_batch(vp9hip_ctx *c, const vp9h_frame *pkts, int n, 
     return stage(c, pkts, n, out_bufs, nullptr);
 }
 
+extern "C" int vp9hip_stage_batch_refs(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bufs,
+                                       const int *ref_bufs)
+{
+    return stage(c, pkts, n, out_bufs, ref_bufs);
+}
+
 static int enqueue_batch(vp9hip_ctx *c);
 
 // Run the staged batch. Without per-launch timing the ~300 launches of a 4K batch are
@@ -860,7 +901,7 @@ static int enqueue_batch(vp9hip_ctx *c)
         int r = 0;
         switch (L.kind) {
         case K_MC:
-            r = vp9hip_launch_mc(c->hb, st, (int) L.n, (const McUnit *) (s.arena + s.o_mcs), fr);
+            r = vp9hip_launch_mc(c->hb, st, (int) L.n, (const McUnit *) (s.arena + s.o_mcs) + L.off, fr);
             break;
         case K_RESID:
             r = vp9hip_launch_resid(c->hb, st, L.arg, (int) L.n, (const RJob *) (s.arena + s.o_rjobs) + L.off, fr,
@@ -995,7 +1036,8 @@ extern "C" int vp9hip_plan_stats(const vp9h_frame *f, double *out, int cap)
     fb.ss_h = f->ss_h; fb.ss_v = f->ss_v; fb.coef_size = f->bpp > 8 ? 4 : 2;
     fb.pitch[0] = fb.sb_cols * 64; fb.pitch[1] = fb.sb_cols * 32;
     fb.coef_base = 0;
-    fb.group = 0;
+    fb.phase = 0;
+    s.rbucket.resize(1);
     std::vector<std::vector<uint32_t>> ps, ls;
     int r = build_frame(nullptr, s, fb, ps, ls);
     if (r < 0) return r;

@@ -124,6 +124,13 @@ int  vp9hip_submit_frame(vp9hip_ctx *ctx, const vp9h_frame *pkt, int out_buf,
  */
 int  vp9hip_stage_batch(vp9hip_ctx *ctx, const vp9h_frame *pkts, int n, const int *out_bufs);
 int  vp9hip_run_batch(vp9hip_ctx *ctx);
+/*
+ * Batch with inter frames: ref_bufs[3*i .. 3*i+2] are the LAST/GOLDEN/ALTREF buffers of
+ * frame i (ignored for keyframes). Frames that reference (or overwrite) the output of an
+ * earlier frame of the batch run after it; independent chains run concurrently.
+ */
+int  vp9hip_stage_batch_refs(vp9hip_ctx *ctx, const vp9h_frame *pkts, int n, const int *out_bufs,
+                             const int *ref_bufs);
 
 /* Wait for all queued work. */
 int  vp9hip_sync(vp9hip_ctx *ctx);

@@ -117,3 +117,32 @@ def test_decoder_api_sequence(v9, orc):
             assert np.array_equal(a, b)
         prev = ref
     dec.dev.close()
+
+
+def test_batch_gop_chains(v9, orc, gpu):
+    """Two independent GOPs (key + 3 P frames, compound/bilinear refs to earlier frames)
+    staged as ONE batch: chained frames run in order, the two chains concurrently."""
+    w, h = 256, 136
+    frames, outs, refs = [], [], []
+    for c in range(2):
+        base = 4 * c
+        frames.append(v9.SynthFrame(v9.synth_params(w, h, 8, seed=500 + 10 * c)))
+        outs.append(base)
+        refs.append(None)
+        for k in range(1, 4):
+            kw = {"compound": 1} if k == 2 else {"bilinear": 1} if k == 3 else {}
+            frames.append(v9.SynthFrame(v9.synth_params(w, h, 8, seed=501 + 10 * c + k, inter=1, **kw)))
+            outs.append(base + k)
+            refs.append((base + k - 1, base + k - 1, base))   # LAST = previous, ALTREF = keyframe
+    order = [0, 4, 1, 5, 2, 6, 3, 7]                           # interleave the two chains
+    gpu.configure(w, h, 8, nbufs=8)
+    gpu.stage_batch([frames[i] for i in order], [outs[i] for i in order], [refs[i] for i in order])
+    gpu.run_batch()
+    gpu.sync()
+    dec = {}
+    for i in range(8):
+        out = v9.alloc_planes(w, h, 8)
+        r = refs[i]
+        orc.decode_frame(frames[i].pkt, out, None if r is None else [dec[r[0]], dec[r[1]], dec[r[2]]])
+        dec[outs[i]] = out
+        _cmp(v9, gpu.download(outs[i]), out, w, h, "gop frame %d" % i)
