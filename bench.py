@@ -1,9 +1,12 @@
 #!/usr/bin/env python3
 """Benchmark: decoded frames/s of the VP9 pixel path on MI355X (BASELINE.json metric).
 
-Workload (config C3 of BASELINE.md): 3840x2160 VP9 Profile-0 8-bit, 4 tile columns,
-all keyframes, 120 frames per stream, synthetic pass-1 packets with the SURVEY.md
-§8(d) stream statistics (seed 0x56503900 + config index 2 + rank).
+Workload (config C3 of BASELINE.md, the default): 3840x2160 VP9 Profile-0 8-bit, 4 tile
+columns, all keyframes, 120 frames per stream, synthetic pass-1 packets with the
+SURVEY.md §8(d) stream statistics (seed 0x56503900 + config index + rank).
+--config C2 / C4 / C5 measure the other BASELINE.md shapes (1080p GOPs of key + 31 P,
+4K 10-bit keyframes, 8K 10-bit GOPs); P frames chain on the previous frame (LAST,
+GOLDEN) and the GOP's keyframe (ALTREF), GOPs are independent chains.
 
 One step = reconstruct + loop-filter the whole 120-frame stream on the GPU with all
 inputs (pass-1 packets -> device work lists + coefficients) already resident in HBM.
@@ -27,15 +30,28 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# (index, w, h, bpp, log2 tile cols, GOP length (1 = all keyframes), frames)
+CONFIGS = {
+    "C2": (1, 1920, 1080, 8, 0, 32, 120),
+    "C3": (2, 3840, 2160, 8, 2, 1, 120),
+    "C4": (3, 3840, 2160, 10, 2, 1, 120),
+    "C5": (4, 7680, 4320, 10, 3, 32, 60),
+}
 W, H, BPP, LOG2_TILE_COLS = 3840, 2160, 8, 2
 CONFIG_INDEX = 2               # C3
 SEED0 = 0x56503900 + CONFIG_INDEX
-TRAFFIC_PROFILE = "r01d"       # rocprofv3 PMC pass of this workload (tools/profile.sh)
+TRAFFIC_PROFILE = "r01d"       # rocprofv3 PMC pass of C3 (tools/profile.sh)
 
 
-def frame_seed(rank, i):
+def frame_seed(rank, i, config_index=CONFIG_INDEX):
     """Seed of frame i of rank `rank`: every rank decodes its own, distinct frames."""
-    return SEED0 + rank * 100003 + i
+    return 0x56503900 + config_index + rank * 100003 + i
+
+
+def gop_refs(n, gop):
+    """Reference buffers per frame: keyframes (i % gop == 0) none; P frames LAST = GOLDEN =
+    previous frame, ALTREF = the GOP's keyframe. Frame i writes buffer i."""
+    return [None if i % gop == 0 else (i - 1, i - 1, i - i % gop) for i in range(n)]
 
 
 def reduce_elapsed(elapsed, dist):
@@ -59,7 +75,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--frames", type=int, default=120)
+    ap.add_argument("--config", default="C3", choices=sorted(CONFIGS))
+    ap.add_argument("--frames", type=int, default=None, help="frames per GPU (default: the config's)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--timed-events", action="store_true",
@@ -75,15 +92,20 @@ def main():
         dist.init_process_group("gloo")
 
     v = importlib.import_module("ffmpeg-hybrid_amd")
+    cidx, W, H, BPP, LOG2_TILE_COLS, gop, nf = CONFIGS[args.config]
+    if args.frames is None:
+        args.frames = nf
+    refs = gop_refs(args.frames, gop)
     t0 = time.time()
-    frames = [v.SynthFrame(v.synth_params(W, H, BPP, seed=frame_seed(rank, i), log2_tile_cols=LOG2_TILE_COLS))
+    frames = [v.SynthFrame(v.synth_params(W, H, BPP, seed=frame_seed(rank, i, cidx), log2_tile_cols=LOG2_TILE_COLS,
+                                          inter=int(refs[i] is not None)))
               for i in range(args.frames)]
     t_gen = time.time() - t0
 
     dev = v.Device(local_rank)
     dev.configure(W, H, BPP, nbufs=args.frames)
     t0 = time.time()
-    dev.stage_batch(frames, list(range(args.frames)))
+    dev.stage_batch(frames, list(range(args.frames)), None if gop == 1 else refs)
     t_stage = time.time() - t0
 
     def barrier():
@@ -138,7 +160,7 @@ def main():
     # rocprofv3 PMC pass (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; tools/traffic.py)
     traffic, traffic_src = None, None
     tf = os.path.join(ROOT, "profiles", TRAFFIC_PROFILE, "traffic.json")
-    if os.path.exists(tf):
+    if os.path.exists(tf) and args.config == "C3":
         per = json.load(open(tf))["per_launch"].get(dom)
         if per:
             traffic, traffic_src = round(per["traffic_bytes"]), "profiles/%s/traffic.json" % TRAFFIC_PROFILE
@@ -161,26 +183,35 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle  # CPU baseline leg only: the scalar C restatement, timed
-        out = v.alloc_planes(W, H, BPP)
+        outs = {}
         n = 0
         t0 = time.perf_counter()
         while n < len(frames) and (time.perf_counter() - t0 < args.cpu_seconds or n < 2):
-            oracle.decode_frame(frames[n].pkt, out)
+            out = v.alloc_planes(W, H, BPP)
+            r = refs[n]
+            oracle.decode_frame(frames[n].pkt, out, None if r is None else [outs[r[0]], outs[r[1]], outs[r[2]]])
+            outs[n] = out
+            for k in [k for k in outs if k < n - gop]:     # keep only what later frames reference
+                del outs[k]
             n += 1
         dt = time.perf_counter() - t0
         cpu = {"value": round(n / dt, 3), "unit": "frames/s", "cores": 1, "kind": "port",
-               "sample": "%d of the 120 C3 frames, scalar C oracle, reconstruction + loop filter from the same "
-                         "pass-1 packets (host entropy decode excluded), 1 thread" % n}
+               "sample": "%d of the %d %s frames (in decode order), scalar C oracle, reconstruction + loop filter "
+                         "from the same pass-1 packets (host entropy decode excluded), 1 thread"
+                         % (n, len(frames), args.config)}
 
     out = {
         "metric": "decoded frames/sec (bit-exact) 4K VP9 Profile-0 @ 1/2/4/8 MI355X; % HBM roofline",
         "value": round(fps, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-        "config": {"workload": "C3: 3840x2160 VP9 Profile-0 8-bit, 4 tile columns, all keyframes, "
-                               "%d frames per GPU per step, pass-1 packets resident in HBM" % args.frames,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8" if BPP == 8 else "u16", "data": "synthetic",
+        "config": {"workload": "%s: %dx%d VP9 Profile-%d %d-bit, %d tile columns, %s, %d frames per GPU per step, "
+                               "pass-1 packets resident in HBM"
+                               % (args.config, W, H, 0 if BPP == 8 else 2, BPP, 1 << LOG2_TILE_COLS,
+                                  "all keyframes" if gop == 1 else "GOPs of key + %d P" % (gop - 1), args.frames),
                    "global_batch": args.frames * world, "frames_per_gpu": args.frames,
-                   "parallelism": "frame-sharded x%d (independent keyframes, no collective)" % world,
+                   "parallelism": "frame-sharded x%d (independent %s, no collective)"
+                                  % (world, "keyframes" if gop == 1 else "GOPs"),
                    "streams_per_gpu": streams,
                    "host_gen_s": round(t_gen, 2), "host_stage_s": round(t_stage, 2)},
         "roofline": roofline,
