@@ -10,8 +10,9 @@
 //              per pixel row (column edges) then one lane per pixel column (row
 //              edges); SBs launched along the t = x + 2y wavefront that reproduces the
 //              reference's raster order.
-//   k_mc     — sub-pel motion compensation (vp9dsp_template.c:1969-2361) with
-//              edge clamping (videodsp_template.c:27-105), one thread per pixel.
+//   k_mc     — sub-pel motion compensation, unscaled and scaled references
+//              (vp9dsp_template.c:1969-2569), edge clamping (videodsp_template.c:27-105),
+//              one thread per pixel.
 //
 // Arithmetic restates vp9dsp_template.c bit-exactly: 8-bit transforms run in
 // wrapping 32-bit arithmetic with int16 intermediates (dctint int / dctcoef int16,
@@ -1299,10 +1300,11 @@ __global__ __launch_bounds__(256) void k_mc(const McUnit *__restrict__ units, in
         int out = 0;
         for (int k = 0; k < u.nref; k++) {
             const int rf = u.ref[k];
+            const McRef m = u.r[k];
             const PIX *r = (const PIX *) fd.ref[rf][p];
-            int dx = u.d16[k][0], dy = u.d16[k][1];
-            int X = u.x + xx + (dx >> 4), Y = u.y + yy + (dy >> 4);
-            int v = mc_sample<PIX>(r, pitch, fd.refw[rf][c], fd.refh[rf][c], X, Y, dx & 15, dy & 15, u.filter, bd);
+            const int px = m.mx + xx * m.dx, py = m.my + yy * m.dy;
+            const int v = mc_sample<PIX>(r, pitch, fd.refw[rf][c], fd.refh[rf][c], m.ix + (px >> 4), m.iy + (py >> 4),
+                                         px & 15, py & 15, u.filter, bd);
             out = k ? (out + v + 1) >> 1 : v;
         }
         dst[(size_t) (u.y + yy) * pitch + u.x + xx] = (PIX) out;

@@ -102,6 +102,7 @@ struct vp9hip_ctx {
     int pitch[2] = { 0, 0 };
     size_t plane_off[3] = { 0, 0, 0 }, buf_bytes = 0;
     std::vector<uint8_t *> bufs;
+    std::vector<std::pair<int, int>> buf_wh;   // visible size of the frame each buffer holds
     uint32_t *ptab = nullptr;           // intra predictor formula table (device)
     int dbg = 0;                        // VP9HIP_DEBUG: ablation switches for profiling only
     bool use_graph = true;              // VP9HIP_GRAPH=0 disables graph replay
@@ -143,6 +144,7 @@ static void free_bufs(vp9hip_ctx *c)
 {
     for (auto *b : c->bufs) hipFree(b);
     c->bufs.clear();
+    c->buf_wh.clear();
 }
 
 extern "C" void vp9hip_close(vp9hip_ctx *c)
@@ -263,6 +265,7 @@ extern "C" int vp9hip_configure(vp9hip_ctx *c, int width, int height, int bpp, i
         if (hipMalloc(&b, c->buf_bytes) != hipSuccess) { free_bufs(c); return VP9HIP_ENOMEM; }
         hipMemsetAsync(b, 0, c->buf_bytes, c->st);
         c->bufs.push_back(b);
+        c->buf_wh.push_back({ width, height });
     }
     c->stg.ready = false;
     int r = upload_ptab(c);
@@ -367,12 +370,65 @@ struct FrameBuild {
     int ss_h, ss_v, coef_size;
     int pitch[2];
     int phase;                   // (stream group, chain position) of this frame
+    int scale[3][2], step[3][2]; // reference scale factors (vp9.c:845-880), 0 = unscaled
+    int refw[3][2], refh[3][2];  // visible reference plane sizes
     uint64_t coef_base;          // element offset of this frame's coefficients in the batch stream
 };
 
 struct PendingJob { PJob j; int level, ts; };
 
 } // namespace
+
+#define SCALE_INVALID 0xFFFF
+static inline int scale_mv(int n, int scale) { return (int) (((int64_t) n * scale) >> 14); }
+static inline int clampi(int v, int lo, int hi) { return v < lo ? lo : v > hi ? hi : v; }
+
+// MC reference parameters of one luma unit at plane position (x, y): mc_luma_unscaled
+// (vp9recon.c:376-414) or the scaled branch of mc_luma_scaled (vp9recon.c:492-541).
+static McRef mc_luma_ref(const FrameBuild &fb, int rf, int x, int y, const int16_t *mv, int px, int py, int pw, int ph,
+                         int bw, int bh)
+{
+    McRef m;
+    if (!fb.scale[rf][0]) {
+        m.ix = x + (mv[0] >> 3); m.iy = y + (mv[1] >> 3);
+        m.mx = (uint8_t) ((mv[0] & 7) << 1); m.my = (uint8_t) ((mv[1] & 7) << 1);
+        m.dx = m.dy = 16;
+        return m;
+    }
+    const int mvx = clampi(mv[0], -(x + pw - px + 4) * 8, (fb.cols * 8 - x + px + 3) * 8);
+    const int mvy = clampi(mv[1], -(y + ph - py + 4) * 8, (fb.rows * 8 - y + py + 3) * 8);
+    const int mx = scale_mv(mvx * 2, fb.scale[rf][0]) + scale_mv(x * 16, fb.scale[rf][0]);
+    const int my = scale_mv(mvy * 2, fb.scale[rf][1]) + scale_mv(y * 16, fb.scale[rf][1]);
+    m.ix = mx >> 4; m.iy = my >> 4;
+    m.mx = (uint8_t) (mx & 15); m.my = (uint8_t) (my & 15);
+    m.dx = (uint8_t) fb.step[rf][0]; m.dy = (uint8_t) fb.step[rf][1];
+    (void) bw; (void) bh;
+    return m;
+}
+
+// Chroma (4:2:0): mc_chroma_unscaled (vp9recon.c:416-467) or mc_chroma_scaled with the
+// libvpx rounding of webm issue 820 (vp9recon.c:543-628).
+static McRef mc_chroma_ref(const FrameBuild &fb, int rf, int x, int y, const int16_t *mv, int px, int py, int pw, int ph,
+                           int bw, int bh)
+{
+    McRef m;
+    if (!fb.scale[rf][0]) {
+        m.ix = x + (mv[0] >> 4); m.iy = y + (mv[1] >> 4);
+        m.mx = (uint8_t) (mv[0] & 15); m.my = (uint8_t) (mv[1] & 15);
+        m.dx = m.dy = 16;
+        return m;
+    }
+    const int sx = fb.scale[rf][0], sy = fb.scale[rf][1];
+    const int mvx = clampi(mv[0], -(x + pw - px + 4) * 16, (fb.cols * 4 - x + px + 3) * 16);
+    const int mvy = clampi(mv[1], -(y + ph - py + 4) * 16, (fb.rows * 4 - y + py + 3) * 16);
+    const int mx = scale_mv(mvx, sx) + (scale_mv(x * 16, sx) & ~15) + (scale_mv(x * 32, sx) & 15);
+    const int my = scale_mv(mvy, sy) + (scale_mv(y * 16, sy) & ~15) + (scale_mv(y * 32, sy) & 15);
+    m.ix = mx >> 4; m.iy = my >> 4;
+    m.mx = (uint8_t) (mx & 15); m.my = (uint8_t) (my & 15);
+    m.dx = (uint8_t) fb.step[rf][0]; m.dy = (uint8_t) fb.step[rf][1];
+    (void) bw; (void) bh;
+    return m;
+}
 
 // Build jobs/levels/LF/MC for one frame. Appends to stg. Returns 0 or error.
 static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std::vector<uint32_t>> &pred_steps,
@@ -508,6 +564,11 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
 
             // inter prediction units (vp9_mc_template.c:30-464), 4:2:0
             if (!b->intra) {
+                const int r0 = b->ref[0], r1 = b->comp ? b->ref[1] : r0;
+                if (b->ref[0] > 2 || (b->comp && b->ref[1] > 2)) return VP9HIP_EINVALIDDATA;
+                if (fb.scale[r0][0] == SCALE_INVALID || fb.scale[r1][0] == SCALE_INVALID) return VP9HIP_EINVALIDDATA;
+                // the SCALED template when any reference is scaled (vp9recon.c:670-680)
+                const bool scaled_tpl = fb.scale[r0][0] || (b->comp && fb.scale[r1][0]);
                 McUnit u;
                 memset(&u, 0, sizeof(u));
                 u.frame = fb.frame_idx;
@@ -515,41 +576,56 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
                 u.nref = b->comp ? 2 : 1;
                 u.ref[0] = b->ref[0];
                 u.ref[1] = b->ref[1];
-                auto luma = [&](int x, int y, int w, int hh, int bidx) {
+                // (x, y) plane position, (px, py, pw, ph) of mc_{luma,chroma}_dir
+                auto emit = [&](int plane, int x, int y, int w, int hh, const int16_t (*mv)[2], int px, int py, int pw,
+                                int ph) {
                     McUnit m = u;
-                    m.plane = 0; m.x = x; m.y = y; m.w = w; m.h = hh;
-                    for (int k = 0; k < m.nref; k++) { m.d16[k][0] = b->mv[bidx][k][0] * 2; m.d16[k][1] = b->mv[bidx][k][1] * 2; }
+                    m.plane = plane; m.x = x; m.y = y; m.w = w; m.h = hh;
+                    for (int k = 0; k < m.nref; k++) {
+                        const int rf = b->ref[k];
+                        m.r[k] = plane ? mc_chroma_ref(fb, rf, x, y, mv[k], px, py, pw, ph, w, hh)
+                                       : mc_luma_ref(fb, rf, x, y, mv[k], px, py, pw, ph, w, hh);
+                    }
                     s.mcs.push_back(m);
                 };
-                auto chroma = [&](int x, int y, int w, int hh, const int16_t mv[2][2]) {
-                    for (int p = 1; p < 3; p++) {
-                        McUnit m = u;
-                        m.plane = p; m.x = x; m.y = y; m.w = w; m.h = hh;
-                        for (int k = 0; k < m.nref; k++) { m.d16[k][0] = mv[k][0]; m.d16[k][1] = mv[k][1]; }
-                        s.mcs.push_back(m);
-                    }
+                auto chroma2 = [&](int x, int y, int w, int hh, const int16_t (*mv)[2], int px, int py, int pw, int ph) {
+                    emit(1, x, y, w, hh, mv, px, py, pw, ph);
+                    emit(2, x, y, w, hh, mv, px, py, pw, ph);
                 };
                 const int lx = b->col * 8, ly = b->row * 8, cx = b->col * 4, cy = b->row * 4;
                 int16_t uv[2][2];
-                if (b->bs > VP9H_BS_8x8) {
+                if (b->bs > VP9H_BS_8x8 && scaled_tpl) {
+                    // four 4x4 luma blocks, one 4x4 chroma block with the 4-MV average
+                    static const int sub[4][2] = { { 0, 0 }, { 4, 0 }, { 0, 4 }, { 4, 4 } };
+                    for (int k = 0; k < 4; k++)
+                        emit(0, lx + sub[k][0], ly + sub[k][1], 4, 4, b->mv[k], sub[k][0], sub[k][1], 8, 8);
+                    for (int k = 0; k < 2; k++) for (int d = 0; d < 2; d++)
+                        uv[k][d] = rdiv(b->mv[0][k][d] + b->mv[1][k][d] + b->mv[2][k][d] + b->mv[3][k][d], 4);
+                    chroma2(cx, cy, 4, 4, uv, 0, 0, 4, 4);
+                } else if (b->bs > VP9H_BS_8x8) {
                     if (b->bs == VP9H_BS_8x4) {
-                        luma(lx, ly, 8, 4, 0); luma(lx, ly + 4, 8, 4, 2);
+                        emit(0, lx, ly, 8, 4, b->mv[0], 0, 0, 0, 0);
+                        emit(0, lx, ly + 4, 8, 4, b->mv[2], 0, 0, 0, 0);
                         for (int k = 0; k < 2; k++) for (int d = 0; d < 2; d++) uv[k][d] = rdiv(b->mv[0][k][d] + b->mv[2][k][d], 2);
                     } else if (b->bs == VP9H_BS_4x8) {
-                        luma(lx, ly, 4, 8, 0); luma(lx + 4, ly, 4, 8, 1);
+                        emit(0, lx, ly, 4, 8, b->mv[0], 0, 0, 0, 0);
+                        emit(0, lx + 4, ly, 4, 8, b->mv[1], 0, 0, 0, 0);
                         for (int k = 0; k < 2; k++) for (int d = 0; d < 2; d++) uv[k][d] = rdiv(b->mv[0][k][d] + b->mv[1][k][d], 2);
                     } else {
-                        luma(lx, ly, 4, 4, 0); luma(lx + 4, ly, 4, 4, 1);
-                        luma(lx, ly + 4, 4, 4, 2); luma(lx + 4, ly + 4, 4, 4, 3);
+                        emit(0, lx, ly, 4, 4, b->mv[0], 0, 0, 0, 0);
+                        emit(0, lx + 4, ly, 4, 4, b->mv[1], 0, 0, 0, 0);
+                        emit(0, lx, ly + 4, 4, 4, b->mv[2], 0, 0, 0, 0);
+                        emit(0, lx + 4, ly + 4, 4, 4, b->mv[3], 0, 0, 0, 0);
                         for (int k = 0; k < 2; k++) for (int d = 0; d < 2; d++)
                             uv[k][d] = rdiv(b->mv[0][k][d] + b->mv[1][k][d] + b->mv[2][k][d] + b->mv[3][k][d], 4);
                     }
-                    chroma(cx, cy, 4, 4, uv);
+                    chroma2(cx, cy, 4, 4, uv, 0, 0, 4, 4);
                 } else {
                     const int bw = vp9t_bwh[0][b->bs][0] * 4, bh = vp9t_bwh[0][b->bs][1] * 4;
-                    luma(lx, ly, bw, bh, 0);
+                    const int uvbw = vp9t_bwh[1][b->bs][0] * 4, uvbh = vp9t_bwh[1][b->bs][1] * 4;
+                    emit(0, lx, ly, bw, bh, b->mv[0], 0, 0, bw, bh);
                     for (int k = 0; k < 2; k++) for (int d = 0; d < 2; d++) uv[k][d] = b->mv[0][k][d];
-                    chroma(cx, cy, vp9t_bwh[1][b->bs][0] * 4, vp9t_bwh[1][b->bs][1] * 4, uv);
+                    chroma2(cx, cy, uvbw, uvbh, uv, 0, 0, uvbw, uvbh);
                 }
             }
 
@@ -707,11 +783,15 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     std::vector<std::vector<std::vector<uint32_t>>> psteps(NP), lsteps(NP);
     std::vector<std::vector<std::pair<uint32_t, uint32_t>>> mcr(NP);   // MC unit ranges per phase
     uint64_t coef_base = 0;
-    double pix_bytes = (double) c->w * c->h * c->bypp * (1.0 + 2.0 / ((1 << c->ss_h) * (1 << c->ss_v)));
+
     for (int i = 0; i < n; i++) {
         const vp9h_frame *f = &pkts[i];
-        if (f->width != c->w || f->height != c->h || f->bpp != c->bpp || f->ss_h != c->ss_h || f->ss_v != c->ss_v)
+        // frames up to the configured size share the buffers (reference scaling, vp9.c:845-880)
+        if (f->width <= 0 || f->height <= 0 || f->width > c->w || f->height > c->h || f->bpp != c->bpp ||
+            f->ss_h != c->ss_h || f->ss_v != c->ss_v)
             return VP9HIP_EINVAL;
+        const int cols = (f->width + 7) >> 3, rows = (f->height + 7) >> 3;
+        const double pix_bytes = (double) f->width * f->height * c->bypp * (1.0 + 2.0 / ((1 << c->ss_h) * (1 << c->ss_v)));
         if (out_bufs[i] < 0 || out_bufs[i] >= (int) c->bufs.size()) return VP9HIP_EINVAL;
         const bool intra = f->keyframe || f->intraonly;
         FrameDesc fd;
@@ -719,9 +799,9 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
         uint8_t *ob = c->bufs[out_bufs[i]];
         for (int p = 0; p < 3; p++) fd.plane[p] = (uint64_t) (ob + c->plane_off[p]);
         fd.pitch[0] = c->pitch[0]; fd.pitch[1] = c->pitch[1];
-        fd.w8[0] = c->cols * 8; fd.h8[0] = c->rows * 8;
-        fd.w8[1] = c->cols * 8 >> c->ss_h; fd.h8[1] = c->rows * 8 >> c->ss_v;
-        fd.sb_cols = c->sb_cols; fd.sb_rows = c->sb_rows;
+        fd.w8[0] = cols * 8; fd.h8[0] = rows * 8;
+        fd.w8[1] = cols * 8 >> c->ss_h; fd.h8[1] = rows * 8 >> c->ss_v;
+        fd.sb_cols = (f->width + 63) >> 6; fd.sb_rows = (f->height + 63) >> 6;
         fd.bd = c->bpp;
         fd.sharp = f->sharpness;
         if (!intra) {
@@ -729,16 +809,38 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
                 int rb = ref_bufs[i * 3 + r];
                 if (rb < 0 || rb >= (int) c->bufs.size()) return VP9HIP_EINVAL;
                 if (rb == out_bufs[i]) return VP9HIP_EINVAL;                       // in-place MC
-                if (f->ref_w[r] != c->w || f->ref_h[r] != c->h) return VP9HIP_ENOSYS;  // scaled MC: not yet on device
+                if (f->ref_w[r] <= 0 || f->ref_h[r] <= 0 || f->ref_w[r] > c->w || f->ref_h[r] > c->h)
+                    return VP9HIP_EINVAL;
                 for (int p = 0; p < 3; p++) fd.ref[r][p] = (uint64_t) (c->bufs[rb] + c->plane_off[p]);
                 fd.refw[r][0] = f->ref_w[r]; fd.refh[r][0] = f->ref_h[r];
                 fd.refw[r][1] = (f->ref_w[r] + c->ss_h) >> c->ss_h; fd.refh[r][1] = (f->ref_h[r] + c->ss_v) >> c->ss_v;
             }
         }
         s.frames.push_back(fd);
+        c->buf_wh[out_bufs[i]] = { f->width, f->height };
         FrameBuild fb;
         fb.f = f; fb.frame_idx = i;
-        fb.cols = c->cols; fb.rows = c->rows; fb.sb_cols = c->sb_cols; fb.sb_rows = c->sb_rows;
+        fb.cols = cols; fb.rows = rows; fb.sb_cols = fd.sb_cols; fb.sb_rows = fd.sb_rows;
+        memset(fb.scale, 0, sizeof(fb.scale));
+        memset(fb.step, 0, sizeof(fb.step));
+        if (!intra) {
+            // reference scale factors (vp9.c:845-880)
+            int valid = 0;
+            for (int r = 0; r < 3; r++) {
+                const int rw = f->ref_w[r], rh = f->ref_h[r], w = f->width, h = f->height;
+                if (rw == w && rh == h) { valid++; continue; }
+                if (w * 2 < rw || h * 2 < rh || w > 16 * rw || h > 16 * rh) {
+                    fb.scale[r][0] = fb.scale[r][1] = SCALE_INVALID;
+                    continue;
+                }
+                fb.scale[r][0] = (rw << 14) / w;
+                fb.scale[r][1] = (rh << 14) / h;
+                fb.step[r][0] = 16 * fb.scale[r][0] >> 14;
+                fb.step[r][1] = 16 * fb.scale[r][1] >> 14;
+                valid++;
+            }
+            if (!valid) return VP9HIP_EINVALIDDATA;
+        }
         fb.ss_h = c->ss_h; fb.ss_v = c->ss_v; fb.coef_size = csz;
         fb.pitch[0] = c->pitch[0]; fb.pitch[1] = c->pitch[1];
         fb.coef_base = coef_base;
@@ -958,7 +1060,8 @@ extern "C" int vp9hip_download_frame(vp9hip_ctx *c, int buf, uint8_t *const plan
     hipSetDevice(c->dev);
     HIPCHK(hipStreamSynchronize(c->st));
     for (int p = 0; p < 3; p++) {
-        int pw = p ? (c->w + c->ss_h) >> c->ss_h : c->w, ph = p ? (c->h + c->ss_v) >> c->ss_v : c->h;
+        const int bw = c->buf_wh[buf].first, bh = c->buf_wh[buf].second;
+        int pw = p ? (bw + c->ss_h) >> c->ss_h : bw, ph = p ? (bh + c->ss_v) >> c->ss_v : bh;
         HIPCHK(hipMemcpy2DAsync(planes[p], linesize[p], c->bufs[buf] + c->plane_off[p],
                                 (size_t) c->pitch[p ? 1 : 0] * c->bypp, (size_t) pw * c->bypp, ph,
                                 hipMemcpyDeviceToHost, c->st));
@@ -972,7 +1075,8 @@ extern "C" int vp9hip_upload_frame(vp9hip_ctx *c, int buf, const uint8_t *const 
     if (!c || buf < 0 || buf >= (int) c->bufs.size() || !planes) return VP9HIP_EINVAL;
     hipSetDevice(c->dev);
     for (int p = 0; p < 3; p++) {
-        int pw = p ? (c->w + c->ss_h) >> c->ss_h : c->w, ph = p ? (c->h + c->ss_v) >> c->ss_v : c->h;
+        const int bw = c->buf_wh[buf].first, bh = c->buf_wh[buf].second;
+        int pw = p ? (bw + c->ss_h) >> c->ss_h : bw, ph = p ? (bh + c->ss_v) >> c->ss_v : bh;
         HIPCHK(hipMemcpy2DAsync(c->bufs[buf] + c->plane_off[p], (size_t) c->pitch[p ? 1 : 0] * c->bypp,
                                 planes[p], linesize[p], (size_t) pw * c->bypp, ph, hipMemcpyHostToDevice, c->st));
     }

@@ -113,7 +113,19 @@ typedef struct LFRec {
     uint8_t  mask[2][2][8][4];
 } LFRec;
 
-/* One motion-compensated rectangle of one plane (<= 64 x 64). */
+/* One motion-compensated rectangle of one plane (<= 64 x 64) and its references. Per
+ * reference, output pixel (i, j) samples the reference at x = ix + ((mx + i dx) >> 4),
+ * phase (mx + i dx) & 15 (y likewise): the stepping of do_scaled_8tap / do_scaled_bilin
+ * (vp9dsp_template.c:2363-2482). Unscaled references use dx = dy = 16, for which the
+ * always-2-D scaled filter equals the 1-D / 2-D / copy selection of the unscaled MC
+ * exactly (an identity phase is exact). Reads clamp to the reference's visible size
+ * (emulated_edge_mc, videodsp_template.c:27-105). */
+typedef struct McRef {
+    int32_t  ix, iy;          /* integer reference position of output pixel (0, 0)      */
+    uint8_t  mx, my;          /* its 1/16-pel phase                                     */
+    uint8_t  dx, dy;          /* phase step per output pixel (16 = unscaled)            */
+} McRef;
+
 typedef struct McUnit {
     uint32_t frame;
     uint16_t x, y;            /* plane pixel position                                   */
@@ -123,7 +135,7 @@ typedef struct McUnit {
     uint8_t  nref;            /* 1 or 2 (compound: second ref averaged)                 */
     uint8_t  ref[2];
     uint8_t  pad;
-    int16_t  d16[2][2];       /* [ref][x,y] offset in 1/16 plane pel                    */
+    McRef    r[2];
 } McUnit;
 
 #endif

@@ -42,6 +42,9 @@ def lib():
         _L.vp9o_mc.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_ssize_t, ctypes.c_void_p,
                                ctypes.c_ssize_t] + [ctypes.c_int] * 6
         _L.vp9o_mc.restype = None
+        _L.vp9o_mc_scaled.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_ssize_t, ctypes.c_void_p,
+                                      ctypes.c_ssize_t] + [ctypes.c_int] * 8
+        _L.vp9o_mc_scaled.restype = None
         _L.vp9o_scan.argtypes = [ctypes.c_int, ctypes.c_int]
         _L.vp9o_scan.restype = ctypes.POINTER(ctypes.c_int16)
     return _L
@@ -92,6 +95,11 @@ def intra_pred(bpp, dst, left, top_with_tl, tx, mode):
 
 def loop_filter(bpp, buf, off, stride, kind, wd1, wd2, direction, E, I, H):
     lib().vp9o_loop_filter(bpp, buf.ctypes.data + off * buf.itemsize, stride, kind, wd1, wd2, direction, E, I, H)
+
+
+def mc_scaled(bpp, dst, src, off, sstride, w, h, mx, my, dx, dy, filt, avg):
+    lib().vp9o_mc_scaled(bpp, dst.ctypes.data, dst.strides[0] // dst.itemsize, src.ctypes.data + off * src.itemsize,
+                         sstride, w, h, mx, my, dx, dy, filt, avg)
 
 
 def mc(bpp, dst, src, off, sstride, w, h, mx, my, filt, avg):

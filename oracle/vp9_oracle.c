@@ -3,6 +3,8 @@
  * reference libavcodec VP9 reconstruction:
  *   check_intra_mode / intra_recon        vp9recon.c:37-364
  *   mc_{luma,chroma}_unscaled, inter_pred vp9recon.c:376-467, vp9_mc_template.c:30-464
+ *   mc_{luma,chroma}_scaled + the SCALED template, vp9recon.c:492-680; do_scaled_8tap /
+ *   do_scaled_bilin vp9dsp_template.c:2363-2482; mvscale / mvstep vp9.c:845-880
  *   inter_recon                           vp9recon.c:655-764
  *   mask_edges + LF level                 vp9block.c:1142-1262, 1438-1452
  *   filter_plane_cols/rows, loopfilter_sb vp9lpf.c:31-230
@@ -75,6 +77,13 @@ void vp9o_loop_filter(int bpp, void *dst, ptrdiff_t stride, int kind, int wd1, i
         else lfmix2_16(dst, stride, wd1, wd2, dir, E, I, H, bpp);
     }
 }
+void vp9o_mc_scaled(int bpp, void *dst, ptrdiff_t ds, const void *src, ptrdiff_t ss, int w, int h,
+                    int mx, int my, int dx, int dy, int filter, int avg)
+{
+    if (bpp == 8) mc_scaled_8(dst, ds, src, ss, w, h, mx, my, dx, dy, filter, avg, 8);
+    else          mc_scaled_16(dst, ds, src, ss, w, h, mx, my, dx, dy, filter, avg, bpp);
+}
+
 void vp9o_mc(int bpp, void *dst, ptrdiff_t ds, const void *src, ptrdiff_t ss, int w, int h,
              int mx, int my, int filter, int avg)
 {
@@ -107,6 +116,8 @@ typedef struct OCtx {
     const uint16_t *eob[3];
     const uint8_t *coef[3];      /* per plane cursor into the coefficient stream */
     uint8_t edge[160 * 160 * 2];
+    uint8_t sedge[288 * 136 * 2];  /* scaled-MC edge buffer (stride 288, vp9recon.c:532-539) */
+    int mvscale[3][2], mvstep[3][2];  /* vp9.c:855-872; REF_INVALID_SCALE = 0xFFFF */
 } OCtx;
 
 static inline int rd_px(const uint8_t *p, int i, int bypp) { return bypp == 1 ? p[i] : ((const uint16_t *) p)[i]; }
@@ -315,11 +326,16 @@ static void mcf(OCtx *c, uint8_t *dst, ptrdiff_t ds, const uint8_t *src, ptrdiff
     else mc_16((uint16_t *) dst, ds / 2, (const uint16_t *) src, ss / 2, bw, bh, mx, my, filter, avg, c->bd);
 }
 
+static void emu_s(OCtx *c, uint8_t *buf, int bstride, const uint8_t *src, ptrdiff_t sls, int bw, int bh,
+                  int sx, int sy, int w, int h)
+{
+    if (c->bypp == 1) emu_edge_8(buf, src, bstride, sls, bw, bh, sx, sy, w, h);
+    else emu_edge_16((uint16_t *) buf, (const uint16_t *) src, bstride, sls / 2, bw, bh, sx, sy, w, h);
+}
 static void emu(OCtx *c, uint8_t *buf, const uint8_t *src, ptrdiff_t sls, int bw, int bh, int sx, int sy,
                 int w, int h)
 {
-    if (c->bypp == 1) emu_edge_8(buf, src, 160, sls, bw, bh, sx, sy, w, h);
-    else emu_edge_16((uint16_t *) buf, (const uint16_t *) src, 160, sls / 2, bw, bh, sx, sy, w, h);
+    emu_s(c, buf, 160, src, sls, bw, bh, sx, sy, w, h);
 }
 
 /* mc_luma_unscaled, vp9recon.c:376-414 (edge buffer stride: 160 pixels) */
@@ -370,6 +386,87 @@ static void mc_chroma(OCtx *c, uint8_t *dst_u, uint8_t *dst_v, ptrdiff_t dst_str
     }
 }
 
+#define REF_INVALID_SCALE 0xFFFF
+static inline int clipi(int v, int lo, int hi) { return v < lo ? lo : v > hi ? hi : v; }
+static inline int scale_mv(int n, int scale) { return (int) (((int64_t) n * scale) >> 14); }
+
+static void smcf(OCtx *c, uint8_t *dst, ptrdiff_t ds, const uint8_t *src, ptrdiff_t ss,
+                 int bw, int bh, int mx, int my, int dx, int dy, int filter, int avg)
+{
+    if (c->bypp == 1) mc_scaled_8(dst, ds, src, ss, bw, bh, mx, my, dx, dy, filter, avg, 8);
+    else mc_scaled_16((uint16_t *) dst, ds / 2, (const uint16_t *) src, ss / 2, bw, bh, mx, my, dx, dy, filter, avg, c->bd);
+}
+
+/* mc_luma_scaled, vp9recon.c:492-541 (scaled branch; the unscaled branch is mc_luma) */
+static void mc_luma_scaled(OCtx *c, uint8_t *dst, ptrdiff_t dst_stride, const uint8_t *ref, ptrdiff_t ref_stride,
+                           ptrdiff_t y, ptrdiff_t x, const int16_t *in_mv, int px, int py, int pw, int ph,
+                           int bw, int bh, int w, int h, int filter, int avg, const int *scale, const int *step)
+{
+    const int bypp = c->bypp;
+    int mvx = clipi(in_mv[0], -(int) (x + pw - px + 4) * 8, (c->cols * 8 - (int) x + px + 3) * 8);
+    int mvy = clipi(in_mv[1], -(int) (y + ph - py + 4) * 8, (c->rows * 8 - (int) y + py + 3) * 8);
+    /* libvpx scales position and MV separately (vp9recon.c:515-520) */
+    int mx = scale_mv(mvx * 2, scale[0]) + scale_mv((int) x * 16, scale[0]);
+    int my = scale_mv(mvy * 2, scale[1]) + scale_mv((int) y * 16, scale[1]);
+    y = my >> 4;
+    x = mx >> 4;
+    ref += y * ref_stride + x * bypp;
+    mx &= 15;
+    my &= 15;
+    const int refbw_m1 = ((bw - 1) * step[0] + mx) >> 4, refbh_m1 = ((bh - 1) * step[1] + my) >> 4;
+    if (x < 3 || y < 3 || x + 4 >= w - refbw_m1 || y + 5 >= h - refbh_m1) {
+        emu_s(c, c->sedge, 288, ref - 3 * ref_stride - 3 * bypp, ref_stride, refbw_m1 + 8, refbh_m1 + 8,
+              (int) x - 3, (int) y - 3, w, h);
+        ref = c->sedge + (3 * 288 + 3) * bypp;
+        ref_stride = 288 * bypp;
+    }
+    smcf(c, dst, dst_stride, ref, ref_stride, bw, bh, mx, my, step[0], step[1], filter, avg);
+}
+
+/* mc_chroma_scaled, vp9recon.c:543-628 (4:2:0 / 4:2:2 / 4:4:0 rounding quirks kept) */
+static void mc_chroma_scaled(OCtx *c, uint8_t *dst_u, uint8_t *dst_v, ptrdiff_t dst_stride,
+                             const uint8_t *ref_u, const uint8_t *ref_v, ptrdiff_t src_stride,
+                             ptrdiff_t y, ptrdiff_t x, const int16_t *in_mv, int px, int py, int pw, int ph,
+                             int bw, int bh, int w, int h, int filter, int avg, const int *scale, const int *step)
+{
+    const int bypp = c->bypp;
+    int mx, my, mvx, mvy;
+    if (c->ss_h) {
+        mvx = clipi(in_mv[0], -(int) (x + pw - px + 4) * 16, (c->cols * 4 - (int) x + px + 3) * 16);
+        mx = scale_mv(mvx, scale[0]) + (scale_mv((int) x * 16, scale[0]) & ~15) + (scale_mv((int) x * 32, scale[0]) & 15);
+    } else {
+        mvx = clipi(in_mv[0], -(int) (x + pw - px + 4) * 8, (c->cols * 8 - (int) x + px + 3) * 8);
+        mx = scale_mv(mvx * 2, scale[0]) + scale_mv((int) x * 16, scale[0]);
+    }
+    if (c->ss_v) {
+        mvy = clipi(in_mv[1], -(int) (y + ph - py + 4) * 16, (c->rows * 4 - (int) y + py + 3) * 16);
+        my = scale_mv(mvy, scale[1]) + (scale_mv((int) y * 16, scale[1]) & ~15) + (scale_mv((int) y * 32, scale[1]) & 15);
+    } else {
+        mvy = clipi(in_mv[1], -(int) (y + ph - py + 4) * 8, (c->rows * 8 - (int) y + py + 3) * 8);
+        my = scale_mv(mvy * 2, scale[1]) + scale_mv((int) y * 16, scale[1]);
+    }
+    y = my >> 4;
+    x = mx >> 4;
+    ref_u += y * src_stride + x * bypp;
+    ref_v += y * src_stride + x * bypp;
+    mx &= 15;
+    my &= 15;
+    const int refbw_m1 = ((bw - 1) * step[0] + mx) >> 4, refbh_m1 = ((bh - 1) * step[1] + my) >> 4;
+    if (x < 3 || y < 3 || x + 4 >= w - refbw_m1 || y + 5 >= h - refbh_m1) {
+        emu_s(c, c->sedge, 288, ref_u - 3 * src_stride - 3 * bypp, src_stride, refbw_m1 + 8, refbh_m1 + 8,
+              (int) x - 3, (int) y - 3, w, h);
+        smcf(c, dst_u, dst_stride, c->sedge + (3 * 288 + 3) * bypp, 288 * bypp, bw, bh, mx, my, step[0], step[1],
+             filter, avg);
+        emu_s(c, c->sedge, 288, ref_v - 3 * src_stride - 3 * bypp, src_stride, refbw_m1 + 8, refbh_m1 + 8,
+              (int) x - 3, (int) y - 3, w, h);
+        smcf(c, dst_v, dst_stride, c->sedge + (3 * 288 + 3) * bypp, 288 * bypp, bw, bh, mx, my, step[0], step[1],
+             filter, avg);
+    } else {
+        smcf(c, dst_u, dst_stride, ref_u, src_stride, bw, bh, mx, my, step[0], step[1], filter, avg);
+        smcf(c, dst_v, dst_stride, ref_v, src_stride, bw, bh, mx, my, step[0], step[1], filter, avg);
+    }
+}
+
 static inline int rdiv(int a, int b) { return (a >= 0 ? a + (b >> 1) : a - (b >> 1)) / b; }  /* ROUNDED_DIV */
 
 static void mv_avg2(int16_t *o, const int16_t *a, const int16_t *b)
@@ -377,9 +474,100 @@ static void mv_avg2(int16_t *o, const int16_t *a, const int16_t *b)
 static void mv_avg4(int16_t *o, const int16_t *a, const int16_t *b, const int16_t *cc, const int16_t *d)
 { o[0] = rdiv(a[0] + b[0] + cc[0] + d[0], 4); o[1] = rdiv(a[1] + b[1] + cc[1] + d[1], 4); }
 
+/* The SCALED instance of inter_pred (vp9_mc_template.c with SCALED 1, used when any of
+ * the block's references is scaled, vp9recon.c:670-680): every sub-8x8 block is done as
+ * four 4x4 luma blocks; each call falls back to the unscaled MC when that reference has
+ * the current frame's size (vp9recon.c:503-507). */
+static void mcl_dir(OCtx *c, int i, uint8_t *dst, ptrdiff_t ls, const vp9o_planes *r, ptrdiff_t rls,
+                    int y, int x, const int16_t *mv, int px, int py, int pw, int ph, int bw, int bh, int w, int h,
+                    int f, int ref)
+{
+    if (r->w == c->f->width && r->h == c->f->height)
+        mc_luma(c, dst, ls, r->data[0], rls, y, x, mv, bw, bh, w, h, f, i);
+    else
+        mc_luma_scaled(c, dst, ls, r->data[0], rls, y, x, mv, px, py, pw, ph, bw, bh, w, h, f, i,
+                       c->mvscale[ref], c->mvstep[ref]);
+}
+static void mcc_dir(OCtx *c, int i, uint8_t *du, uint8_t *dv, ptrdiff_t ls, const vp9o_planes *r, ptrdiff_t rls,
+                    int y, int x, const int16_t *mv, int px, int py, int pw, int ph, int bw, int bh, int w, int h,
+                    int f, int ref)
+{
+    if (r->w == c->f->width && r->h == c->f->height)
+        mc_chroma(c, du, dv, ls, r->data[1], r->data[2], rls, y, x, mv, bw, bh, w, h, f, i);
+    else
+        mc_chroma_scaled(c, du, dv, ls, r->data[1], r->data[2], rls, y, x, mv, px, py, pw, ph, bw, bh, w, h, f, i,
+                         c->mvscale[ref], c->mvstep[ref]);
+}
+
+static int inter_pred_scaled(OCtx *c, const vp9h_block *b)
+{
+    const int bypp = c->bypp, ss_h = c->ss_h, ss_v = c->ss_v;
+    int row = b->row, col = b->col, i;
+    ptrdiff_t ls_y = c->ls[0], ls_uv = c->ls[1];
+    uint8_t *dy = c->plane[0] + row * 8 * ls_y + col * 8 * bypp;
+    uint8_t *du = c->plane[1] + row * (8 >> ss_v) * ls_uv + col * (8 >> ss_h) * bypp;
+    uint8_t *dv = c->plane[2] + row * (8 >> ss_v) * ls_uv + col * (8 >> ss_h) * bypp;
+
+    for (i = 0; i < 1 + b->comp; i++) {
+        const int ref = b->ref[i];
+        const vp9o_planes *r = &c->refs[ref];
+        ptrdiff_t rls = r->stride[0] * bypp, rls_uv = r->stride[1] * bypp;
+        int w1 = r->w, h1 = r->h, f = b->filter;
+        int16_t uvmv[2];
+        if (b->bs > VP9H_BS_8x8) {
+            static const int sub[4][2] = { { 0, 0 }, { 4, 0 }, { 0, 4 }, { 4, 4 } };
+            for (int k = 0; k < 4; k++)
+                mcl_dir(c, i, dy + sub[k][1] * ls_y + sub[k][0] * bypp, ls_y, r, rls, (row << 3) + sub[k][1],
+                        (col << 3) + sub[k][0], b->mv[k][i], sub[k][0], sub[k][1], 8, 8, 4, 4, w1, h1, f, ref);
+            if (ss_v) {
+                h1 = (h1 + 1) >> 1;
+                if (ss_h) {
+                    w1 = (w1 + 1) >> 1;
+                    mv_avg4(uvmv, b->mv[0][i], b->mv[1][i], b->mv[2][i], b->mv[3][i]);
+                    mcc_dir(c, i, du, dv, ls_uv, r, rls_uv, row << 2, col << 2, uvmv, 0, 0, 4, 4, 4, 4, w1, h1, f, ref);
+                } else {
+                    mv_avg2(uvmv, b->mv[0][i], b->mv[2][i]);
+                    mcc_dir(c, i, du, dv, ls_uv, r, rls_uv, row << 2, col << 3, uvmv, 0, 0, 8, 4, 4, 4, w1, h1, f, ref);
+                    mv_avg2(uvmv, b->mv[1][i], b->mv[3][i]);
+                    mcc_dir(c, i, du + 4 * bypp, dv + 4 * bypp, ls_uv, r, rls_uv, row << 2, (col << 3) + 4, uvmv,
+                            4, 0, 8, 4, 4, 4, w1, h1, f, ref);
+                }
+            } else {
+                if (ss_h) {
+                    w1 = (w1 + 1) >> 1;
+                    mv_avg2(uvmv, b->mv[0][i], b->mv[1][i]);
+                    mcc_dir(c, i, du, dv, ls_uv, r, rls_uv, row << 3, col << 2, uvmv, 0, 0, 4, 8, 4, 4, w1, h1, f, ref);
+                    mv_avg2(uvmv, b->mv[1][i], b->mv[2][i]);     /* BUG compat (vp9_mc_template.c:296-305) */
+                    mcc_dir(c, i, du + 4 * ls_uv, dv + 4 * ls_uv, ls_uv, r, rls_uv, (row << 3) + 4, col << 2, uvmv,
+                            0, 4, 4, 8, 4, 4, w1, h1, f, ref);
+                } else {
+                    for (int k = 0; k < 4; k++)
+                        mcc_dir(c, i, du + sub[k][1] * ls_uv + sub[k][0] * bypp, dv + sub[k][1] * ls_uv + sub[k][0] * bypp,
+                                ls_uv, r, rls_uv, (row << 3) + sub[k][1], (col << 3) + sub[k][0], b->mv[k][i],
+                                sub[k][0], sub[k][1], 8, 8, 4, 4, w1, h1, f, ref);
+                }
+            }
+        } else {
+            int bw = vp9t_bwh[0][b->bs][0] * 4, bh = vp9t_bwh[0][b->bs][1] * 4;
+            int uvbw = vp9t_bwh[ss_h][b->bs][0] * 4, uvbh = vp9t_bwh[ss_v][b->bs][1] * 4;
+            mcl_dir(c, i, dy, ls_y, r, rls, row << 3, col << 3, b->mv[0][i], 0, 0, bw, bh, bw, bh, w1, h1, f, ref);
+            w1 = (w1 + ss_h) >> ss_h;
+            h1 = (h1 + ss_v) >> ss_v;
+            mcc_dir(c, i, du, dv, ls_uv, r, rls_uv, row << (3 - ss_v), col << (3 - ss_h), b->mv[0][i],
+                    0, 0, uvbw, uvbh, uvbw, uvbh, w1, h1, f, ref);
+        }
+    }
+    return 0;
+}
+
 /* inter_pred, vp9_mc_template.c:30-464 (unscaled). i = 0 first ref (put), 1 second (avg). */
 static int inter_pred(OCtx *c, const vp9h_block *b)
 {
+    /* inter_recon (vp9recon.c:659-680): invalid scale -> error, any scaled ref -> SCALED template */
+    if (c->mvscale[b->ref[0]][0] == REF_INVALID_SCALE || (b->comp && c->mvscale[b->ref[1]][0] == REF_INVALID_SCALE))
+        return VP9HIP_EINVALIDDATA;
+    if (c->mvscale[b->ref[0]][0] || (b->comp && c->mvscale[b->ref[1]][0]))
+        return inter_pred_scaled(c, b);
     const int bypp = c->bypp, ss_h = c->ss_h, ss_v = c->ss_v;
     int row = b->row, col = b->col, i;
     ptrdiff_t ls_y = c->ls[0], ls_uv = c->ls[1];
@@ -393,8 +581,6 @@ static int inter_pred(OCtx *c, const vp9h_block *b)
         ptrdiff_t rls = r->stride[0] * bypp, rls_uv = r->stride[1] * bypp;
         int w1 = r->w, h1 = r->h, f = b->filter;
         int16_t uvmv[2];
-        if (r->w != c->f->width || r->h != c->f->height)
-            return VP9HIP_ENOSYS;  /* scaled references: not restated in this round */
 
         if (b->bs > VP9H_BS_8x8) {
             if (b->bs == VP9H_BS_8x4) {
@@ -791,6 +977,26 @@ int vp9o_decode_frame(const vp9h_frame *f, vp9o_planes *cur, const vp9o_planes *
     c->sb_cols = (f->width + 63) >> 6;
     c->sb_rows = (f->height + 63) >> 6;
     c->refs = refs;
+    /* reference scale factors (vp9.c:845-880) */
+    if (refs && !f->keyframe && !f->intraonly) {
+        int valid = 0;
+        for (i = 0; i < 3; i++) {
+            const int w = f->width, h = f->height, refw = refs[i].w, refh = refs[i].h;
+            if (refw == w && refh == h) {
+                c->mvscale[i][0] = c->mvscale[i][1] = 0;
+            } else if (w * 2 < refw || h * 2 < refh || w > 16 * refw || h > 16 * refh) {
+                c->mvscale[i][0] = c->mvscale[i][1] = REF_INVALID_SCALE;
+                continue;
+            } else {
+                c->mvscale[i][0] = (refw << 14) / w;
+                c->mvscale[i][1] = (refh << 14) / h;
+                c->mvstep[i][0] = 16 * c->mvscale[i][0] >> 14;
+                c->mvstep[i][1] = 16 * c->mvscale[i][1] >> 14;
+            }
+            valid++;
+        }
+        if (!valid) { free(c); return VP9HIP_EINVALIDDATA; }
+    }
     for (p = 0; p < 3; p++) {
         c->plane[p] = cur->data[p];
         c->ls[p] = cur->stride[p] * c->bypp;

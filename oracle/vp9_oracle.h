@@ -38,6 +38,9 @@ void vp9o_intra_pred(int bpp, void *dst, ptrdiff_t stride, const void *left, con
                      int tx, int mode);
 void vp9o_loop_filter(int bpp, void *dst, ptrdiff_t stride, int kind, int wd1, int wd2, int dir,
                       int E, int I, int H);
+/* scaled MC (do_scaled_8tap / do_scaled_bilin, vp9dsp_template.c:2363-2482) */
+void vp9o_mc_scaled(int bpp, void *dst, ptrdiff_t ds, const void *src, ptrdiff_t ss, int w, int h,
+                    int mx, int my, int dx, int dy, int filter, int avg);
 void vp9o_mc(int bpp, void *dst, ptrdiff_t ds, const void *src, ptrdiff_t ss, int w, int h,
              int mx, int my, int filter, int avg);
 /* scan table access: returns pointer to the scan for tx (0..3, 4 = lossless) / txtp */

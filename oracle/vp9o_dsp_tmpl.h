@@ -733,6 +733,71 @@ static void F(mc)(PIX *dst, ptrdiff_t ds, const PIX *src, ptrdiff_t ss, int w, i
             }
     }
 }
+/* Scaled MC, vp9dsp_template.c:2363-2482 (do_scaled_8tap_c / do_scaled_bilin_c): the
+ * horizontal pass steps the source phase by dx per output pixel into a pixel-clipped
+ * 64-wide tmp, the vertical pass steps by dy. 12-bit bilinear uses the 10-bit code
+ * (ff_vp9dsp_scaled_mc_init, vp9dsp_template.c:2533-2541), identical for uint16 pixels. */
+static void F(mc_scaled)(PIX *dst, ptrdiff_t ds, const PIX *src, ptrdiff_t ss, int w, int h,
+                         int mx, int my, int dx, int dy, int filter, int avg, int bd)
+{
+    int x, y;
+    if (filter == 3) {
+        static PIX tmp[64 * 129];
+        int tmp_h = (((h - 1) * dy + my) >> 4) + 2;
+        PIX *tp = tmp;
+        do {
+            int imx = mx, ioff = 0;
+            for (x = 0; x < w; x++) {
+                tp[x] = BILIN(src, ioff, imx, 1);
+                imx += dx;
+                ioff += imx >> 4;
+                imx &= 0xf;
+            }
+            tp += 64;
+            src += ss;
+        } while (--tmp_h);
+        tp = tmp;
+        for (y = 0; y < h; y++) {
+            for (x = 0; x < w; x++) {
+                int v = BILIN(tp, x, my, 64);
+                dst[x] = avg ? (dst[x] + v + 1) >> 1 : v;
+            }
+            my += dy;
+            tp += (my >> 4) * 64;
+            my &= 0xf;
+            dst += ds;
+        }
+        return;
+    }
+    static PIX tmp[64 * 135];
+    const int16_t (*filters)[8] = vp9t_subpel_filters[filter];
+    int tmp_h = (((h - 1) * dy + my) >> 4) + 8;
+    PIX *tp = tmp;
+    src -= ss * 3;
+    do {
+        int imx = mx, ioff = 0;
+        for (x = 0; x < w; x++) {
+            tp[x] = FILT8(src, ioff, filters[imx], 1);
+            imx += dx;
+            ioff += imx >> 4;
+            imx &= 0xf;
+        }
+        tp += 64;
+        src += ss;
+    } while (--tmp_h);
+    tp = tmp + 64 * 3;
+    for (y = 0; y < h; y++) {
+        const int16_t *fy = filters[my];
+        for (x = 0; x < w; x++) {
+            int v = FILT8(tp, x, fy, 64);
+            dst[x] = avg ? (dst[x] + v + 1) >> 1 : v;
+        }
+        my += dy;
+        tp += (my >> 4) * 64;
+        my &= 0xf;
+        dst += ds;
+    }
+}
 #undef FILT8
 #undef BILIN
 

@@ -146,3 +146,36 @@ def test_batch_gop_chains(v9, orc, gpu):
         orc.decode_frame(frames[i].pkt, out, None if r is None else [dec[r[0]], dec[r[1]], dec[r[2]]])
         dec[outs[i]] = out
         _cmp(v9, gpu.download(outs[i]), out, w, h, "gop frame %d" % i)
+
+
+SCALED = [
+    # (reference size, frame size, bpp, extra params): down- and up-scaled references
+    ((352, 288), (240, 200), 8, {}),
+    ((176, 144), (352, 288), 8, {"compound": 1}),
+    ((200, 130), (320, 208), 8, {"bilinear": 1}),
+    ((256, 256), (200, 136), 10, {"compound": 1}),
+]
+
+
+@pytest.mark.parametrize("rs,fs,bpp,kw", SCALED)
+def test_scaled_reference_parity(v9, orc, gpu, rs, fs, bpp, kw):
+    """Reference scaling (vp9recon.c:492-628, vp9.c:845-880): a keyframe at one size,
+    an inter frame at another size predicting from it."""
+    (rw, rh), (w, h) = rs, fs
+    key = v9.SynthFrame(v9.synth_params(rw, rh, bpp, seed=900))
+    gpu.configure(max(rw, w), max(rh, h), bpp, nbufs=2)
+    gpu.stage_batch([key], [0])
+    gpu.run_batch()
+    kref = v9.alloc_planes(rw, rh, bpp)
+    orc.decode_frame(key.pkt, kref)
+    _cmp(v9, gpu.download(0), kref, rw, rh, "scaled-test keyframe")
+    for seed in (901, 902):
+        f = v9.SynthFrame(v9.synth_params(w, h, bpp, seed=seed, inter=1, **kw))
+        for r in range(3):
+            f.pkt.ref_w[r], f.pkt.ref_h[r] = rw, rh
+        gpu.stage_batch([f], [1], [(0, 0, 0)])
+        gpu.run_batch()
+        gpu.sync()
+        out = v9.alloc_planes(w, h, bpp)
+        orc.decode_frame(f.pkt, out, [kref, kref, kref], [(rw, rh)] * 3)
+        _cmp(v9, gpu.download(1), out, w, h, "scaled ref %dx%d -> %dx%d@%d %s seed %d" % (rw, rh, w, h, bpp, kw, seed))

@@ -250,3 +250,36 @@ def test_mc_properties(orc, filt):
     d = np.zeros((64, 64), np.uint16)
     orc.mc(10, d, ramp, 3 * 72 + 3, 72, 8, 8, 4, 0, 3, 0)
     assert (d[:8, :8] == ramp[3:11, 3:11] + 2).all()
+
+
+@pytest.mark.parametrize("filt", [0, 1, 2, 3])
+def test_mc_scaled_unit_step_equals_unscaled(orc, filt):
+    """do_scaled_8tap / do_scaled_bilin (vp9dsp_template.c:2363-2482) always run the 2-D
+    filter; at step 16 (scale 1.0) they must equal the unscaled 1-D/2-D/copy paths
+    (vp9dsp_template.c:1969-2361) -- the identity phase is exact."""
+    for bpp in (8, 10):
+        dt = _dt(bpp)
+        src = RNG.integers(0, 1 << bpp, (96, 96)).astype(dt)
+        for mx, my in ((0, 0), (6, 0), (0, 10), (3, 13), (15, 1)):
+            for avg in (0, 1):
+                a = RNG.integers(0, 1 << bpp, (64, 64)).astype(dt)
+                b = a.copy()
+                off = 8 * 96 + 8
+                orc.mc(bpp, a, src, off, 96, 16, 8, mx, my, filt, avg)
+                orc.mc_scaled(bpp, b, src, off, 96, 16, 8, mx, my, 16, 16, filt, avg)
+                assert np.array_equal(a, b), (bpp, mx, my, filt, avg)
+
+
+def test_mc_scaled_constant_and_step():
+    """A constant reference stays constant at any scale; at step 32 (2x downscale) with
+    phase 0 the full-pel source samples are every other pixel."""
+    import oracle as orc
+    for filt in range(4):
+        src = np.full((160, 160), 77, np.uint8)
+        d = np.zeros((64, 64), np.uint8)
+        orc.mc_scaled(8, d, src, 8 * 160 + 8, 160, 16, 16, 5, 11, 24, 21, filt, 0)
+        assert (d[:16, :16] == 77).all()
+    src = RNG.integers(0, 256, (160, 160)).astype(np.uint8)
+    d = np.zeros((64, 64), np.uint8)
+    orc.mc_scaled(8, d, src, 8 * 160 + 8, 160, 16, 16, 0, 0, 32, 32, 1, 0)
+    assert np.array_equal(d[:16, :16], src[8:40:2, 8:40:2])
