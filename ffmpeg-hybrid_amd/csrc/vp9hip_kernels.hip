@@ -772,35 +772,45 @@ DEV void run_pass(uint32_t w, int lane, PIX *tile, uint16_t *eb, int bd, const P
     wave_sync();
 }
 
-template <typename PIX>
-__global__ __launch_bounds__(64) void k_pred(const uint32_t *__restrict__ list, const WGRec *__restrict__ wgs,
-                                             const SBRec *__restrict__ sbs, const PJob *__restrict__ jobs,
-                                             const uint32_t *__restrict__ passes, const FrameDesc *__restrict__ frames,
-                                             const int16_t *__restrict__ resid, const uint32_t *__restrict__ ptab, int dbg)
-{
-    __shared__ PIX tile[PRED_K * TILE_ELEMS];
-    __shared__ uint16_t eb[256];               // per job 2n+8 edge pixels
-    __shared__ PJob lj[PRED_K * MAX_SB_JOBS];
-    __shared__ uint32_t lp[PRED_K * MAX_SB_JOBS];
-    __shared__ uint32_t ltab[10 * 80];         // formula words of 4x4 and 8x8, all slots
+// LDS of one k_pred workgroup (one wavefront).
+template <typename PIX> struct PredLds {
+    PIX tile[PRED_K * TILE_ELEMS];
+    uint16_t eb[256];                 // per job 2n+8 edge pixels
+    PJob lj[PRED_K * MAX_SB_JOBS];
+    uint32_t lp[PRED_K * MAX_SB_JOBS];
+    uint32_t ltab[10 * 80];           // formula words of 4x4 and 8x8, all slots
+};
 
-    const WGRec *wgp = wgs + list[blockIdx.x];
+template <typename PIX>
+DEV void load_ltab(uint32_t *ltab, const uint32_t *__restrict__ ptab, int lane)
+{
+    uint32_t t[13];
+#pragma unroll
+    for (int u = 0; u < 13; u++) {
+        const int i = lane + 64 * u;
+        t[u] = i < 800 ? ptab[(i / 80) * PTAB_SLOT + i % 80] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < 13; u++)
+        if (lane + 64 * u < 800) ltab[lane + 64 * u] = t[u];
+}
+
+// Intra prediction of one workgroup record (the ltab copy must be loaded).
+template <typename PIX>
+DEV void pred_wg(const WGRec *wgp, const SBRec *__restrict__ sbs, const PJob *__restrict__ jobs,
+                 const uint32_t *__restrict__ passes, const FrameDesc *__restrict__ frames,
+                 const int16_t *__restrict__ resid, const uint32_t *__restrict__ ptab, PredLds<PIX> &S, int lane,
+                 int dbg)
+{
+    PIX *tile = S.tile;
+    uint16_t *eb = S.eb;
+    PJob *lj = S.lj;
+    uint32_t *lp = S.lp;
+    const uint32_t *ltab = S.ltab;
     const uint32_t wjob0 = wgp->job0, wpass0 = wgp->pass0, wnjobs = wgp->njobs, wnpass = wgp->npass;
-    const int lane = threadIdx.x;
     const int bd = frames[sbs[wgp->sb[0]].frame].bd;
 
-    // ---- prologue: formula words, job list, pass words, SB neighbourhoods (pre-LF pixels) ----
-    {
-        uint32_t t[13];
-#pragma unroll
-        for (int u = 0; u < 13; u++) {
-            const int i = lane + 64 * u;
-            t[u] = i < 800 ? ptab[(i / 80) * PTAB_SLOT + i % 80] : 0;
-        }
-#pragma unroll
-        for (int u = 0; u < 13; u++)
-            if (lane + 64 * u < 800) ltab[lane + 64 * u] = t[u];
-    }
+    // ---- prologue: job list, pass words, SB neighbourhoods (pre-LF pixels) ----
     for (int i = lane; i < wnjobs; i += 64) lj[i] = jobs[wjob0 + i];
     for (int i = lane; i < wnpass; i += 64) lp[i] = passes[wpass0 + i];
 #pragma unroll 1
@@ -849,6 +859,17 @@ __global__ __launch_bounds__(64) void k_pred(const uint32_t *__restrict__ list, 
             }
         }
     }
+}
+
+template <typename PIX>
+__global__ __launch_bounds__(64) void k_pred(const uint32_t *__restrict__ list, const WGRec *__restrict__ wgs,
+                                             const SBRec *__restrict__ sbs, const PJob *__restrict__ jobs,
+                                             const uint32_t *__restrict__ passes, const FrameDesc *__restrict__ frames,
+                                             const int16_t *__restrict__ resid, const uint32_t *__restrict__ ptab, int dbg)
+{
+    __shared__ PredLds<PIX> S;
+    load_ltab<PIX>(S.ltab, ptab, threadIdx.x);
+    pred_wg<PIX>(wgs + list[blockIdx.x], sbs, jobs, passes, frames, resid, ptab, S, threadIdx.x, dbg);
 }
 
 // --------------------------------------------------------------- k_lf
@@ -1035,30 +1056,39 @@ DEV void lf_reg(int (&px)[NPX], int wd, int L, int sharp, int bd)
 #define FLP 74           // luma LF tile pitch (72 used)
 #define FCP 42           // chroma LF tile pitch (40 used)
 
-template <typename PIX>
-__global__ __launch_bounds__(128) void k_lf(const uint32_t *__restrict__ list, const LFRec *__restrict__ recs,
-                                            const FrameDesc *__restrict__ frames, int dbg)
-{
-    __shared__ uint16_t lt[72 * FLP];
-    __shared__ uint16_t ct[2][40 * FCP];
-    __shared__ uint8_t lvl[64];
-    __shared__ uint8_t msk[2][2][8][4];
+// One SB of loop filter by NT threads (128: two waves, luma / chroma in parallel; 64: one
+// wave, luma then chroma). Same arithmetic and edge order either way (planes are
+// independent, vp9lpf.c:183-230).
+struct LfLds {
+    uint16_t lt[72 * FLP];
+    uint16_t ct[2][40 * FCP];
+    uint8_t lvl[64];
+    uint8_t msk[2][2][8][4];
+};
 
-    const LFRec &rec = recs[list[blockIdx.x]];
+template <typename PIX, int NT>
+DEV void lf_sb(const LFRec &rec, const FrameDesc *__restrict__ frames, LfLds &S, int lane, int dbg)
+{
+#define LF_SYNC() do { if (NT == 64) wave_sync(); else __syncthreads(); } while (0)
+    uint16_t *lt = S.lt;
+    uint16_t (*ct)[40 * FCP] = S.ct;
+    uint8_t *lvl = S.lvl;
+    uint8_t (*msk)[2][8][4] = S.msk;
     const FrameDesc &fd = frames[rec.frame];
-    const int tid = threadIdx.x, bd = fd.bd, sharp = fd.sharp;
+    const int bd = fd.bd, sharp = fd.sharp;
     const int sbx = rec.sbx, sby = rec.sby;
-    if (tid < 64) lvl[tid] = rec.level[tid];
-    if (tid < 128) ((uint8_t *) msk)[tid] = ((const uint8_t *) rec.mask)[tid];
+    for (int i = lane; i < 64; i += NT) lvl[i] = rec.level[i];
+    for (int i = lane; i < 128; i += NT) ((uint8_t *) msk)[i] = ((const uint8_t *) rec.mask)[i];
 
     // load: luma rows [y0-8, y0+64) x cols [x0-8, x0+64), chroma [-8, 32), in aligned
     // 8-pixel chunks (luma 72 x 9, chroma 2 x 40 x 5 = 1048 chunks, <= 9 per thread), all
     // global loads of a thread in flight before its LDS writes
     typedef typename Chunk8<PIX>::T CT;
-    CT v[9];
+    constexpr int NU = (1048 + NT - 1) / NT;
+    CT v[NU];
 #pragma unroll
-    for (int u = 0; u < 9; u++) {
-        const int ci = tid + u * 128;
+    for (int u = 0; u < NU; u++) {
+        const int ci = lane + u * NT;
         int p, r, k;
         lf_chunk(ci, p, r, k);
         const int gx = (p ? sbx * 32 : sbx * 64) - 8 + 8 * k, gy = (p ? sby * 32 : sby * 64) - 8 + r;
@@ -1067,8 +1097,8 @@ __global__ __launch_bounds__(128) void k_lf(const uint32_t *__restrict__ list, c
             v[u] = *(const CT *) ((const PIX *) fd.plane[p] + (size_t) gy * fd.pitch[p ? 1 : 0] + gx);
     }
 #pragma unroll
-    for (int u = 0; u < 9; u++) {
-        const int ci = tid + u * 128;
+    for (int u = 0; u < NU; u++) {
+        const int ci = lane + u * NT;
         int p, r, k;
         lf_chunk(ci, p, r, k);
         if (ci < 1048) {
@@ -1076,12 +1106,13 @@ __global__ __launch_bounds__(128) void k_lf(const uint32_t *__restrict__ list, c
             Chunk8<PIX>::to_lds(v[u], t + 8 * k);
         }
     }
-    __syncthreads();
+    LF_SYNC();
 
     const int col = sbx * 8, row = sby * 8;   // SB position in 8x8 units
     if (!(dbg & 1)) {
     // ---- column edges (filter_plane_cols, vp9lpf.c:31-104): one lane per pixel row, the
     //      row in registers (luma x = -8..63, chroma x = -8..31), edges left to right ----
+    for (int tid = lane; tid < 128; tid += NT) {
     if (tid < 64) {
         const int r = tid;
         uint16_t *rowp = lt + (r + 8) * FLP;
@@ -1156,9 +1187,11 @@ __global__ __launch_bounds__(128) void k_lf(const uint32_t *__restrict__ list, c
 #pragma unroll
         for (int i = 0; i < 20; i++) ((uint32_t *) rowp)[i] = (uint32_t) px[2 * i] | (uint32_t) px[2 * i + 1] << 16;
     }
-    __syncthreads();
+    }
+    LF_SYNC();
     // ---- row edges (filter_plane_rows, vp9lpf.c:106-181): one lane per pixel column, the
     //      column in registers (rows -8..63 / -8..31), edges top to bottom ----
+    for (int tid = lane; tid < 128; tid += NT) {
     if (tid < 64) {
         const int c = tid;
         uint16_t *colp = lt + 8 + c;
@@ -1227,14 +1260,15 @@ __global__ __launch_bounds__(128) void k_lf(const uint32_t *__restrict__ list, c
 #pragma unroll
         for (int i = 1; i < 40; i++) colp[i * FCP] = (uint16_t) px[i];
     }
-    __syncthreads();
+    }
+    LF_SYNC();
     }
     // ---- store the modified region: rows [0,sz) x cols [-8,sz) and rows [-8,0) x cols [0,sz).
     // Other SBs of the same wavefront step never touch this region, so whole chunks are
     // written back (pixels beyond the 8-aligned frame size are unchanged padding). ----
 #pragma unroll
-    for (int u = 0; u < 9; u++) {
-        const int ci = tid + u * 128;
+    for (int u = 0; u < NU; u++) {
+        const int ci = lane + u * NT;
         int p, r, k;
         lf_chunk(ci, p, r, k);
         const int gx = (p ? sbx * 32 : sbx * 64) - 8 + 8 * k, gy = (p ? sby * 32 : sby * 64) - 8 + r;
@@ -1243,6 +1277,15 @@ __global__ __launch_bounds__(128) void k_lf(const uint32_t *__restrict__ list, c
             *(CT *) ((PIX *) fd.plane[p] + (size_t) gy * fd.pitch[p ? 1 : 0] + gx) = Chunk8<PIX>::from_lds(t + 8 * k);
         }
     }
+#undef LF_SYNC
+}
+
+template <typename PIX>
+__global__ __launch_bounds__(128) void k_lf(const uint32_t *__restrict__ list, const LFRec *__restrict__ recs,
+                                            const FrameDesc *__restrict__ frames, int dbg)
+{
+    __shared__ LfLds S;
+    lf_sb<PIX, 128>(recs[list[blockIdx.x]], frames, S, threadIdx.x, dbg);
 }
 
 // --------------------------------------------------------------- k_mc
