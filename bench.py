@@ -81,6 +81,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--timed-events", action="store_true",
                     help="per-launch HIP events inside the timed steps (no graph replay)")
+    ap.add_argument("--shard", choices=["frames", "tiles"], default="frames",
+                    help="frames: every rank decodes its own stream (weak scaling, default); tiles: all ranks "
+                         "decode ONE stream, each its tile columns, pre-LF stripes all-gathered (strong scaling)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -92,6 +95,8 @@ def main():
         dist.init_process_group("gloo")
 
     v = importlib.import_module("ffmpeg-hybrid_amd")
+    if args.shard == "tiles":
+        return bench_tiles(args, v, dist, world, rank, local_rank)
     cidx, W, H, BPP, LOG2_TILE_COLS, gop, nf = CONFIGS[args.config]
     if args.frames is None:
         args.frames = nf
@@ -216,6 +221,66 @@ def main():
                    "host_gen_s": round(t_gen, 2), "host_stage_s": round(t_stage, 2)},
         "roofline": roofline,
         "cpu_baseline": cpu,
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    dev.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def bench_tiles(args, v, dist, world, rank, local_rank):
+    """--shard tiles: one stream over all ranks (tileshard.py). Every
+    rank stages the same frames and reconstructs its tile columns. Per chain position
+    the pre-LF stripes go through one RCCL all-gather (an nccl group beside the gloo
+    control group), then every rank loop-filters the whole frame."""
+    import torch
+    ts = importlib.import_module("ffmpeg-hybrid_amd.tileshard")
+    cidx, W, H, BPP, log2, gop, nf = CONFIGS[args.config]
+    if args.frames is None:
+        args.frames = nf
+    refs = gop_refs(args.frames, gop)
+    frames = [v.SynthFrame(v.synth_params(W, H, BPP, seed=frame_seed(0, i, cidx), log2_tile_cols=log2,
+                                          inter=int(refs[i] is not None))) for i in range(args.frames)]
+    torch.cuda.set_device(local_rank)
+    group = dist.new_group(backend="nccl") if dist is not None else None
+    lo, hi = ts.tile_ranges(1 << log2, world)[rank]
+    dev = v.Device(local_rank)
+    dev.configure(W, H, BPP, nbufs=args.frames)
+    dev.stage_batch(frames, list(range(args.frames)), refs, tiles=(lo, hi))
+    dev.set_timing(False)
+    sh = ts.TileShard(dev, 1 << log2, rank, world, group=group, device="cuda:%d" % local_rank)
+    for _ in range(args.warmup):
+        sh.run()
+    if dist is not None:
+        dist.barrier()
+    dev.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        sh.run()
+    dev.sync()
+    if dist is not None:
+        dist.barrier()
+    elapsed = reduce_elapsed(time.perf_counter() - t0, dist)
+    fps, ms_per_step = aggregate(args.frames, args.steps, 1, elapsed)     # one stream: strong scaling
+    step_bytes = sum(dev.alg_bytes().values())
+    sent, recvd = zip(*sh.bytes_per_phase())
+    achieved = step_bytes / (ms_per_step / 1000.0) / 1e9
+    out = {
+        "metric": "decoded frames/sec (bit-exact) 4K VP9 Profile-0 @ 1/2/4/8 MI355X; % HBM roofline",
+        "value": round(fps, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "u8" if BPP == 8 else "u16", "data": "synthetic",
+        "config": {"workload": "%s: %dx%d %d-bit, %d tile columns, %s, ONE %d-frame stream over all GPUs"
+                               % (args.config, W, H, BPP, 1 << log2,
+                                  "all keyframes" if gop == 1 else "GOPs of key + %d P" % (gop - 1), args.frames),
+                   "parallelism": "tile-sharded x%d: tile columns %d..%d on rank %d, RCCL all-gather of pre-LF "
+                                  "stripes per chain position, redundant full-frame LF" % (world, lo, hi - 1, rank),
+                   "exchange_bytes_per_phase": {"sent": max(sent), "received": max(recvd)}},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                     "kernel": "whole step on rank 0 (algorithmic bytes of its share / step wall time)"},
+        "cpu_baseline": None,
     }
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -82,6 +82,8 @@ ABI_SYMBOLS = ["vp9hip_open", "vp9hip_close", "vp9hip_configure", "vp9hip_submit
                "vp9hip_download_frame",
                "vp9hip_upload_frame", "vp9hip_flush", "vp9hip_last_timing", "vp9hip_set_timing",
                "vp9hip_alg_bytes", "vp9hip_plan_stats", "vp9hip_abi_version",
+               "vp9hip_stage_batch_tiles", "vp9hip_batch_phases", "vp9hip_phase_frames", "vp9hip_run_phase",
+               "vp9hip_stripe",
                "vp9hip_synth_defaults", "vp9hip_synth_frame", "vp9hip_synth_free"]
 
 
@@ -102,6 +104,13 @@ def lib():
     L.vp9hip_stage_batch.argtypes = [vp, ctypes.POINTER(FramePacket), ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
     L.vp9hip_stage_batch_refs.argtypes = [vp, ctypes.POINTER(FramePacket), ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                                           ctypes.POINTER(ctypes.c_int)]
+    L.vp9hip_stage_batch_tiles.argtypes = [vp, ctypes.POINTER(FramePacket), ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                           ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_int]
+    L.vp9hip_batch_phases.argtypes = [vp]
+    L.vp9hip_phase_frames.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_int]
+    L.vp9hip_run_phase.argtypes = [vp, ctypes.c_int, ctypes.c_int]
+    L.vp9hip_stripe.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+    L.vp9hip_stripe.restype = ctypes.c_int64
     L.vp9hip_run_batch.argtypes = [vp]
     L.vp9hip_sync.argtypes = [vp]
     L.vp9hip_download_frame.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
@@ -202,20 +211,49 @@ class Device:
         pkt = frame.pkt if isinstance(frame, SynthFrame) else frame
         _check("vp9hip_submit_frame", lib().vp9hip_submit_frame(self._c, ctypes.byref(pkt), out_buf, r))
 
-    def stage_batch(self, frames, out_bufs, ref_bufs=None):
+    def stage_batch(self, frames, out_bufs, ref_bufs=None, tiles=None):
         """Stage a batch; ref_bufs: per frame (LAST, GOLDEN, ALTREF) buffer ids or None
-        (keyframes). Dependent frames are chained, independent chains run concurrently."""
+        (keyframes). Dependent frames are chained, independent chains run concurrently.
+        tiles=(lo, hi): reconstruct only tile columns [lo, hi) (a shard of a tile-sharded
+        stream, run with run_phase; see tileshard.py)."""
         arr = (FramePacket * len(frames))(*[f.pkt if isinstance(f, SynthFrame) else f for f in frames])
         ob = (ctypes.c_int * len(out_bufs))(*out_bufs)
         self._staged = (arr, frames)   # keep host packets alive
-        if ref_bufs is None:
+        if ref_bufs is None and tiles is None:
             _check("vp9hip_stage_batch", lib().vp9hip_stage_batch(self._c, arr, len(frames), ob))
             return
         flat = []
-        for r in ref_bufs:
+        for r in (ref_bufs if ref_bufs is not None else [None] * len(frames)):
             flat += list(r) if r is not None else [0, 0, 0]
         rb = (ctypes.c_int * len(flat))(*flat)
+        if tiles is not None:
+            _check("vp9hip_stage_batch_tiles",
+                   lib().vp9hip_stage_batch_tiles(self._c, arr, len(frames), ob, rb, int(tiles[0]), int(tiles[1])))
+            return
         _check("vp9hip_stage_batch_refs", lib().vp9hip_stage_batch_refs(self._c, arr, len(frames), ob, rb))
+
+    PART_RECON, PART_LF = 0, 1
+
+    def phases(self):
+        """Number of phases (chain positions) of the staged batch."""
+        return _check("vp9hip_batch_phases", lib().vp9hip_batch_phases(self._c))
+
+    def phase_frames(self, phase):
+        """Batch indices of the frames in `phase`."""
+        n = _check("vp9hip_phase_frames", lib().vp9hip_phase_frames(self._c, phase, None, 0))
+        a = (ctypes.c_int * max(n, 1))()
+        _check("vp9hip_phase_frames", lib().vp9hip_phase_frames(self._c, phase, a, n))
+        return list(a[:n])
+
+    def run_phase(self, phase, part):
+        _check("vp9hip_run_phase", lib().vp9hip_run_phase(self._c, phase, part))
+
+    def stripe(self, frame, tile_lo, tile_hi, dev_ptr=None, to_frame=False):
+        """Pack / unpack the pre-LF columns of tile columns [lo, hi) of batch frame `frame`
+        to / from device memory at dev_ptr (an int address); returns the byte count."""
+        return _check("vp9hip_stripe", lib().vp9hip_stripe(self._c, frame, tile_lo, tile_hi,
+                                                           ctypes.c_void_p(dev_ptr) if dev_ptr else None,
+                                                           int(bool(to_frame))))
 
     def run_batch(self):
         _check("vp9hip_run_batch", lib().vp9hip_run_batch(self._c))

@@ -52,7 +52,8 @@ const char *const kname[K_N] = { "k_mc", "k_resid", "k_pred", "k_lf" };
 // ff_vp9_intra_txfm_type (vp9data.c:437-452)
 const uint8_t intra_txfm_type[14] = { 2, 1, 0, 0, 3, 2, 1, 2, 1, 3, 0, 0, 0, 0 };
 
-struct Launch { int kind; uint32_t off; uint32_t n; int arg; int grp; };
+struct Launch { int kind; uint32_t off; uint32_t n; int arg; int grp; int ph; int part; };
+enum { PART_RECON, PART_LF };           // a phase's reconstruction launches, then its loop filter
 #define MAX_GROUPS 4                    // independent frame groups = concurrent launch chains
 
 struct Staged {
@@ -76,6 +77,10 @@ struct Staged {
     std::vector<McUnit> mcs;
     std::vector<uint32_t> lists;        // concatenated SB index lists of all launches
     std::vector<Launch> launches;
+    int nphases = 0;
+    std::vector<int> frame_phase;       // phase of each batch frame
+    std::vector<int> frame_log2;        // log2 tile columns of each batch frame
+    int tile_lo = 0, tile_hi = 64;      // tile columns this context reconstructs (sharded batches)
     std::vector<uint8_t> coefs;         // concatenated coefficient streams (bytes)
     double alg_bytes[K_N] = { 0, 0, 0, 0 };
     // device arena
@@ -110,6 +115,7 @@ struct vp9hip_ctx {
     // timing of the last run
     bool timing = true;
     std::vector<hipEvent_t> ev;
+    bool timed_run = false;             // the last run recorded per-launch events
     double kms[K_N] = { 0, 0, 0, 0 };
     int kcount[K_N] = { 0, 0, 0, 0 };
 };
@@ -370,6 +376,7 @@ struct FrameBuild {
     int ss_h, ss_v, coef_size;
     int pitch[2];
     int phase;                   // (stream group, chain position) of this frame
+    int tile_lo = 0, tile_hi = 64;   // tile columns to reconstruct (default: all)
     int scale[3][2], step[3][2]; // reference scale factors (vp9.c:845-880), 0 = unscaled
     int refw[3][2], refh[3][2];  // visible reference plane sizes
     uint64_t coef_base;          // element offset of this frame's coefficients in the batch stream
@@ -452,11 +459,14 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
         const vp9h_block *b0 = &f->blocks[bi];
         const int sbx = b0->col >> 3, sby = b0->row >> 3;
         // tile column of this SB (vp9.c:1244-1250)
-        int tile_x0 = 0, tile_sb0 = 0;
+        int tile_x0 = 0, tile_sb0 = 0, tile = 0;
         for (int ti = 0; ti < (1 << log2); ti++) {
             int s0 = std::min((ti * fb.sb_cols) >> log2, fb.sb_cols), s1 = std::min(((ti + 1) * fb.sb_cols) >> log2, fb.sb_cols);
-            if (sbx >= s0 && sbx < s1) { tile_x0 = s0 << 3; tile_sb0 = s0; }
+            if (sbx >= s0 && sbx < s1) { tile_x0 = s0 << 3; tile_sb0 = s0; tile = ti; }
         }
+        // sharded batches reconstruct their own tile columns only; every SB keeps its LF
+        // record (the loop filter runs over the whole frame on every shard)
+        const bool mine = tile >= fb.tile_lo && tile < fb.tile_hi;
         LFRec lf;
         memset(&lf, 0, sizeof(lf));
         lf.frame = fb.frame_idx; lf.sbx = sbx; lf.sby = sby;
@@ -496,7 +506,7 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
                         if (e > (16 << (2 * txs))) return VP9HIP_EINVALIDDATA;
                         const int ux0 = ux_sb + x, uy0 = uy_sb + y, n4 = step;
                         uint32_t roff = 0;
-                        if (e) {
+                        if (e && mine) {
                             RJob r;
                             memset(&r, 0, sizeof(r));
                             r.coef = (uint32_t) (fb.coef_base + coef);
@@ -515,7 +525,7 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
                             s.rbucket[fb.phase][tcode][txtp].push_back(r);
                         }
                         coef += e;
-                        if (!b->intra) continue;
+                        if (!b->intra || !mine) continue;
                         // intra: prediction job, levelled by the pixels its edges read; the
                         // edge availability of check_intra_mode (vp9recon.c:37-221) is resolved here
                         PendingJob q;
@@ -563,7 +573,7 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
             }
 
             // inter prediction units (vp9_mc_template.c:30-464), 4:2:0
-            if (!b->intra) {
+            if (!b->intra && mine) {
                 const int r0 = b->ref[0], r1 = b->comp ? b->ref[1] : r0;
                 if (b->ref[0] > 2 || (b->comp && b->ref[1] > 2)) return VP9HIP_EINVALIDDATA;
                 if (fb.scale[r0][0] == SCALE_INVALID || fb.scale[r1][0] == SCALE_INVALID) return VP9HIP_EINVALIDDATA;
@@ -729,7 +739,8 @@ static int merge_mixed(Staged &s, uint32_t sbi)
     return 0;
 }
 
-static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bufs, const int *ref_bufs /*n*3 or null*/)
+static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bufs, const int *ref_bufs /*n*3 or null*/,
+                 int tile_lo = 0, int tile_hi = 64, int max_groups = 0)
 {
     if (!c || !pkts || n <= 0 || !out_bufs) return VP9HIP_EINVAL;
     if (c->bufs.empty()) return VP9HIP_EINVAL;
@@ -742,6 +753,8 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     s.rjobs.clear(); s.resid16 = 0;
     s.rbucket.clear();
     s.lists.clear(); s.launches.clear(); s.coefs.clear();
+    s.frame_phase.assign(n, 0); s.frame_log2.assign(n, 0);
+    s.tile_lo = tile_lo; s.tile_hi = tile_hi;
     for (int k = 0; k < K_N; k++) s.alg_bytes[k] = 0;
     s.ready = false;
 
@@ -771,7 +784,7 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     }
     std::vector<int> roots;
     for (int i = 0; i < n; i++) if (find(i) == i) roots.push_back(i);
-    const int G = std::max(1, std::min<int>(c->max_groups, (int) roots.size()));
+    const int G = std::max(1, std::min<int>(max_groups > 0 ? max_groups : c->max_groups, (int) roots.size()));
     s.ngroups = G;
     std::vector<int> grp(n);
     for (int i = 0; i < n; i++)
@@ -779,6 +792,7 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     int maxpos = 0;
     for (int i = 0; i < n; i++) maxpos = std::max(maxpos, pos[i]);
     const int NP = G * (maxpos + 1);                   // phase id = g * (maxpos + 1) + pos
+    s.nphases = NP;
     s.rbucket.assign(NP, {});
     std::vector<std::vector<std::vector<uint32_t>>> psteps(NP), lsteps(NP);
     std::vector<std::vector<std::pair<uint32_t, uint32_t>>> mcr(NP);   // MC unit ranges per phase
@@ -845,6 +859,9 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
         fb.pitch[0] = c->pitch[0]; fb.pitch[1] = c->pitch[1];
         fb.coef_base = coef_base;
         fb.phase = grp[i] * (maxpos + 1) + pos[i];
+        fb.tile_lo = tile_lo; fb.tile_hi = tile_hi;
+        s.frame_phase[i] = fb.phase;
+        s.frame_log2[i] = f->log2_tile_cols;
         const size_t mc0 = s.mcs.size();
         int r = build_frame(c, s, fb, psteps[fb.phase], lsteps[fb.phase]);
         if (r < 0) return r;
@@ -869,7 +886,7 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     // reads + writes of k_resid
     for (int g = 0; g < G; g++)
         for (int ph = g * (maxpos + 1); ph < (g + 1) * (maxpos + 1); ph++) {
-            for (auto &mr : mcr[ph]) s.launches.push_back({ K_MC, mr.first, mr.second, 0, g });
+            for (auto &mr : mcr[ph]) s.launches.push_back({ K_MC, mr.first, mr.second, 0, g, ph, PART_RECON });
             for (int t = 0; t < 5; t++) {
                 const uint32_t off = (uint32_t) s.rjobs.size();
                 for (int tp = 0; tp < 4; tp++) {
@@ -877,11 +894,13 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
                         if (r.ptx & 32) s.alg_bytes[K_RESID] += 2.0 * (16 << (2 * (t & 3))) * c->bypp;
                     s.rjobs.insert(s.rjobs.end(), s.rbucket[ph][t][tp].begin(), s.rbucket[ph][t][tp].end());
                 }
-                if (s.rjobs.size() > off) s.launches.push_back({ K_RESID, off, (uint32_t) (s.rjobs.size() - off), t, g });
+                if (s.rjobs.size() > off)
+                    s.launches.push_back({ K_RESID, off, (uint32_t) (s.rjobs.size() - off), t, g, ph, PART_RECON });
             }
             auto add_list = [&](int kind, const std::vector<uint32_t> &v) {
                 if (v.empty()) return;
-                s.launches.push_back({ kind, (uint32_t) s.lists.size(), (uint32_t) v.size(), 0, g });
+                s.launches.push_back({ kind, (uint32_t) s.lists.size(), (uint32_t) v.size(), 0, g, ph,
+                                       kind == K_LF ? PART_LF : PART_RECON });
                 s.lists.insert(s.lists.end(), v.begin(), v.end());
             };
             for (auto &v : psteps[ph]) {
@@ -980,12 +999,32 @@ extern "C" int vp9hip_run_batch(vp9hip_ctx *c)
     return 0;
 }
 
-static int enqueue_batch(vp9hip_ctx *c)
+static int launch_one(vp9hip_ctx *c, const Launch &L, hipStream_t st)
 {
     Staged &s = c->stg;
     const FrameDesc *fr = (const FrameDesc *) (s.arena + s.o_frames);
     const uint32_t *lists = (const uint32_t *) (s.arena + s.o_lists);
+    switch (L.kind) {
+    case K_MC:
+        return vp9hip_launch_mc(c->hb, st, (int) L.n, (const McUnit *) (s.arena + s.o_mcs) + L.off, fr);
+    case K_RESID:
+        return vp9hip_launch_resid(c->hb, st, L.arg, (int) L.n, (const RJob *) (s.arena + s.o_rjobs) + L.off, fr,
+                                   s.arena + s.o_coefs, s.resid);
+    case K_PRED:
+        return vp9hip_launch_pred(c->hb, st, (int) L.n, lists + L.off, (const WGRec *) (s.arena + s.o_wgs),
+                                  (const SBRec *) (s.arena + s.o_sbs), (const PJob *) (s.arena + s.o_pjobs),
+                                  (const uint32_t *) (s.arena + s.o_passes), fr, s.resid, c->ptab, c->dbg);
+    case K_LF:
+        return vp9hip_launch_lf(c->hb, st, (int) L.n, lists + L.off, (const LFRec *) (s.arena + s.o_lfs), fr, c->dbg >> 16);
+    }
+    return -1;
+}
+
+static int enqueue_batch(vp9hip_ctx *c)
+{
+    Staged &s = c->stg;
     size_t nl = s.launches.size();
+    c->timed_run = c->timing;
     if (c->timing && c->ev.size() < 2 * nl) {
         size_t old = c->ev.size();
         c->ev.resize(2 * nl);
@@ -1000,25 +1039,7 @@ static int enqueue_batch(vp9hip_ctx *c)
         const Launch &L = s.launches[i];
         hipStream_t st = L.grp ? c->xst[L.grp - 1] : c->st;
         if (c->timing) HIPCHK(hipEventRecord(c->ev[2 * i], st));
-        int r = 0;
-        switch (L.kind) {
-        case K_MC:
-            r = vp9hip_launch_mc(c->hb, st, (int) L.n, (const McUnit *) (s.arena + s.o_mcs) + L.off, fr);
-            break;
-        case K_RESID:
-            r = vp9hip_launch_resid(c->hb, st, L.arg, (int) L.n, (const RJob *) (s.arena + s.o_rjobs) + L.off, fr,
-                                    s.arena + s.o_coefs, s.resid);
-            break;
-        case K_PRED:
-            r = vp9hip_launch_pred(c->hb, st, (int) L.n, lists + L.off, (const WGRec *) (s.arena + s.o_wgs),
-                                   (const SBRec *) (s.arena + s.o_sbs), (const PJob *) (s.arena + s.o_pjobs),
-                                   (const uint32_t *) (s.arena + s.o_passes), fr, s.resid, c->ptab, c->dbg);
-            break;
-        case K_LF:
-            r = vp9hip_launch_lf(c->hb, st, (int) L.n, lists + L.off, (const LFRec *) (s.arena + s.o_lfs), fr, c->dbg >> 16);
-            break;
-        }
-        if (r) return VP9HIP_EEXTERNAL;
+        if (launch_one(c, L, st)) return VP9HIP_EEXTERNAL;
         if (c->timing) HIPCHK(hipEventRecord(c->ev[2 * i + 1], st));
     }
     // join: the main stream (downloads, sync, the next stage) waits for every group
@@ -1029,12 +1050,78 @@ static int enqueue_batch(vp9hip_ctx *c)
     return 0;
 }
 
+// ---- tile-column sharding of one stream over several devices ----
+extern "C" int vp9hip_stage_batch_tiles(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bufs,
+                                        const int *ref_bufs, int tile_lo, int tile_hi)
+{
+    if (tile_lo < 0 || tile_hi < tile_lo || tile_hi > 64) return VP9HIP_EINVAL;
+    return stage(c, pkts, n, out_bufs, ref_bufs, tile_lo, tile_hi, 1);   // one group: phases in chain order
+}
+
+extern "C" int vp9hip_batch_phases(vp9hip_ctx *c)
+{
+    if (!c || !c->stg.ready) return VP9HIP_EINVAL;
+    return c->stg.nphases;
+}
+
+extern "C" int vp9hip_phase_frames(vp9hip_ctx *c, int phase, int *frames, int cap)
+{
+    if (!c || !c->stg.ready || phase < 0 || phase >= c->stg.nphases || cap < 0) return VP9HIP_EINVAL;
+    int n = 0;
+    for (int i = 0; i < (int) c->stg.frame_phase.size(); i++)
+        if (c->stg.frame_phase[i] == phase) {
+            if (frames && n < cap) frames[n] = i;
+            n++;
+        }
+    return n;
+}
+
+// Enqueue one part of one phase: PART_RECON (MC, residuals, intra of this context's
+// tile columns) or PART_LF (the loop filter of the whole frames).
+extern "C" int vp9hip_run_phase(vp9hip_ctx *c, int phase, int part)
+{
+    if (!c || !c->stg.ready || phase < 0 || phase >= c->stg.nphases || (part != PART_RECON && part != PART_LF))
+        return VP9HIP_EINVAL;
+    hipSetDevice(c->dev);
+    c->timed_run = false;
+    for (const Launch &L : c->stg.launches)
+        if (L.ph == phase && L.part == part && launch_one(c, L, c->st)) return VP9HIP_EEXTERNAL;
+    return 0;
+}
+
+// Copy the pixel columns of tile columns [tile_lo, tile_hi) of batch frame `frame` (all
+// 8-aligned rows; Y, then U, then V, each packed row by row) between the frame's buffer
+// and contiguous device memory `dev`: to_frame = 0 packs, 1 unpacks. dev == NULL only
+// returns the byte count. Tile columns follow set_tile_offset (vp9.c:1244-1250).
+extern "C" int64_t vp9hip_stripe(vp9hip_ctx *c, int frame, int tile_lo, int tile_hi, void *dev, int to_frame)
+{
+    if (!c || !c->stg.ready || frame < 0 || frame >= (int) c->stg.frames.size() || tile_lo < 0 || tile_hi < tile_lo)
+        return VP9HIP_EINVAL;
+    const FrameDesc &fd = c->stg.frames[frame];
+    const int log2 = c->stg.frame_log2[frame], nt = 1 << log2;
+    auto sbx = [&](int t) { return std::min(std::min(t, nt) * fd.sb_cols >> log2, fd.sb_cols); };
+    const int x0 = std::min(sbx(tile_lo) * 64, (int) fd.w8[0]), x1 = std::min(sbx(tile_hi) * 64, (int) fd.w8[0]);
+    int64_t off = 0;
+    for (int p = 0; p < 3; p++) {
+        const int sh = p ? c->ss_h : 0, h = p ? fd.h8[1] : fd.h8[0];
+        const size_t w = (size_t) ((x1 >> sh) - (x0 >> sh)) * c->bypp, pitch = (size_t) fd.pitch[p ? 1 : 0] * c->bypp;
+        if (dev && w && h) {
+            uint8_t *fp = (uint8_t *) fd.plane[p] + (size_t) (x0 >> sh) * c->bypp, *dp = (uint8_t *) dev + off;
+            hipError_t e = to_frame ? hipMemcpy2DAsync(fp, pitch, dp, w, w, h, hipMemcpyDeviceToDevice, c->st)
+                                    : hipMemcpy2DAsync(dp, w, fp, pitch, w, h, hipMemcpyDeviceToDevice, c->st);
+            if (e != hipSuccess) return VP9HIP_EEXTERNAL;
+        }
+        off += (int64_t) w * h;
+    }
+    return off;
+}
+
 extern "C" int vp9hip_sync(vp9hip_ctx *c)
 {
     if (!c) return VP9HIP_EINVAL;
     hipSetDevice(c->dev);
     HIPCHK(hipStreamSynchronize(c->st));
-    if (c->timing && c->stg.ready) {
+    if (c->timing && c->timed_run && c->stg.ready) {
         for (int k = 0; k < K_N; k++) { c->kms[k] = 0; c->kcount[k] = 0; }
         for (size_t i = 0; i < c->stg.launches.size() && 2 * i + 1 < c->ev.size(); i++) {
             float ms = 0;

@@ -132,6 +132,38 @@ int  vp9hip_run_batch(vp9hip_ctx *ctx);
 int  vp9hip_stage_batch_refs(vp9hip_ctx *ctx, const vp9h_frame *pkts, int n, const int *out_bufs,
                              const int *ref_bufs);
 
+/*
+ * Tile-column sharding of ONE stream over several devices (one context per device).
+ * Every context stages the same packets. Its reconstruction covers only tile columns
+ * [tile_lo, tile_hi), which is MC, residuals and intra; tile columns decode
+ * independently (vp9.c:1244-1250, vp9recon.c:46). Its loop filter covers the whole
+ * frame. Per phase (vp9hip_batch_phases, the frames of one chain position,
+ * vp9hip_phase_frames):
+ *   1. vp9hip_run_phase(ctx, ph, VP9HIP_PART_RECON);
+ *   2. exchange the pre-LF stripes of that phase's frames (vp9hip_stripe pack, an
+ *      all-gather, vp9hip_stripe unpack of the other shards' columns);
+ *   3. vp9hip_run_phase(ctx, ph, VP9HIP_PART_LF).
+ * Every device then holds the full post-LF frames that later phases reference.
+ * The device form of the reference's slice-threaded tile decode: tile-column jobs
+ * (decode_tiles_mt, vp9.c:1442-1520), then the loop filter over the whole frame
+ * (loopfilter_proc, vp9.c:1522-1551; dispatched at vp9.c:1806).
+ */
+#define VP9HIP_PART_RECON 0
+#define VP9HIP_PART_LF    1
+int  vp9hip_stage_batch_tiles(vp9hip_ctx *ctx, const vp9h_frame *pkts, int n, const int *out_bufs,
+                              const int *ref_bufs, int tile_lo, int tile_hi);
+int  vp9hip_batch_phases(vp9hip_ctx *ctx);
+/* Batch indices of the frames in `phase` (up to cap written); returns their count. */
+int  vp9hip_phase_frames(vp9hip_ctx *ctx, int phase, int *frames, int cap);
+int  vp9hip_run_phase(vp9hip_ctx *ctx, int phase, int part);
+/*
+ * Pack (to_frame = 0) or unpack (1) the pixel columns of tile columns [tile_lo, tile_hi)
+ * of batch frame `frame`, all 8-aligned rows, Y then U then V, between its device
+ * buffer and contiguous device memory `dev`. The copy is asynchronous on the context's
+ * stream. Returns the byte count, which is all it does when dev is NULL.
+ */
+int64_t vp9hip_stripe(vp9hip_ctx *ctx, int frame, int tile_lo, int tile_hi, void *dev, int to_frame);
+
 /* Wait for all queued work. */
 int  vp9hip_sync(vp9hip_ctx *ctx);
 
