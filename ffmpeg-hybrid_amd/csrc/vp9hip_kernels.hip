@@ -594,22 +594,32 @@ DEV LaneMap lane_map(uint32_t w, int lane)
 #define PASS_MAXN(w) (((w) & 3) ? 32 : (((w) >> 2) & 7) ? 16 : (((w) >> 5) & 15) ? 8 : 4)
 
 // Prefetched per-lane inputs of one pass: the lane's job record and the first 8 rows
-// of its residual column (named fields, so the set stays in registers). Two sets
-// alternate across passes; the load is unconditional (clamped address), so no
+// of its residual column (named fields, so the set stays in registers). The job records
+// (global, L1/L2) are read two passes ahead, the residual rows (whose address needs the
+// job record) one pass ahead; every load is unconditional (clamped pass index), so no
 // control-flow join forces an early s_waitcnt.
 struct PSet { uint32_t ja, jr; uint4 r0; };
+struct JSet { uint32_t ja, jr, lt; };     // job record + (li | ts << 8) of the lane
 DEV uint32_t pr_word(const PSet &s, int k)
 {
     return k == 0 ? s.r0.x : k == 1 ? s.r0.y : k == 2 ? s.r0.z : s.r0.w;
 }
 
-DEV void prefetch_pass(uint32_t w, int lane, const PJob *lj, const int16_t *__restrict__ resid, PSet &ps)
+DEV void load_job(uint32_t w, int lane, const PJob *__restrict__ lj, JSet &j)
 {
     const LaneMap m = lane_map(w, lane);
     const PJob jb = lj[PASS_FIRST_M(w) + m.jidx];
-    ps.ja = jb.a;
-    ps.jr = jb.roff;
-    ps.r0 = *(const uint4 *) (resid + (PJ_RES(jb) ? (size_t) jb.roff * 16 + (m.li << (m.ts + 2)) : 0));
+    j.ja = jb.a;
+    j.jr = jb.roff;
+    j.lt = (uint32_t) m.li | (uint32_t) m.ts << 8;
+}
+
+DEV void load_resid(const JSet &j, const int16_t *__restrict__ resid, PSet &ps)
+{
+    ps.ja = j.ja;
+    ps.jr = j.jr;
+    const uint32_t li = j.lt & 255, ts = j.lt >> 8;
+    ps.r0 = *(const uint4 *) (resid + (((j.ja >> 4) & 1) ? (size_t) j.jr * 16 + (li << (ts + 2)) : 0));
 }
 
 // Load the pixels above / left of an SB (and, for inter frames, its interior: the
@@ -776,8 +786,6 @@ DEV void run_pass(uint32_t w, int lane, PIX *tile, uint16_t *eb, int bd, const P
 template <typename PIX> struct PredLds {
     PIX tile[PRED_K * TILE_ELEMS];
     uint16_t eb[256];                 // per job 2n+8 edge pixels
-    PJob lj[PRED_K * MAX_SB_JOBS];
-    uint32_t lp[PRED_K * MAX_SB_JOBS];
     uint32_t ltab[10 * 80];           // formula words of 4x4 and 8x8, all slots
 };
 
@@ -804,15 +812,13 @@ DEV void pred_wg(const WGRec *wgp, const SBRec *__restrict__ sbs, const PJob *__
 {
     PIX *tile = S.tile;
     uint16_t *eb = S.eb;
-    PJob *lj = S.lj;
-    uint32_t *lp = S.lp;
     const uint32_t *ltab = S.ltab;
     const uint32_t wjob0 = wgp->job0, wpass0 = wgp->pass0, wnjobs = wgp->njobs, wnpass = wgp->npass;
+    const PJob *lj = jobs + wjob0;         // job records: read a pass ahead (L1/L2)
+    const uint32_t *lp = passes + wpass0;  // pass words: wave-uniform scalar loads
     const int bd = frames[sbs[wgp->sb[0]].frame].bd;
 
     // ---- prologue: job list, pass words, SB neighbourhoods (pre-LF pixels) ----
-    for (int i = lane; i < wnjobs; i += 64) lj[i] = jobs[wjob0 + i];
-    for (int i = lane; i < wnpass; i += 64) lp[i] = passes[wpass0 + i];
 #pragma unroll 1
     for (int k = 0; k < PRED_K; k++) {
         const uint32_t sbi = __builtin_amdgcn_readfirstlane(wgp->sb[k]);
@@ -823,20 +829,28 @@ DEV void pred_wg(const WGRec *wgp, const SBRec *__restrict__ sbs, const PJob *__
     }
     wave_sync();
 
-    // passes, two prefetch sets alternating (loop unrolled by two: no register copies)
+    // passes: residual sets A / B alternate (loop unrolled by two), job records J run a
+    // pass ahead of them; pass words are wave-uniform scalar loads (index clamped)
     const int npass = (dbg & 1) ? 0 : wnpass;
-    PSet A, B;
-    if (npass) prefetch_pass(lp[0], lane, lj, resid, A);
-    for (int pi = 0; pi < npass; pi += 2) {
-        const uint32_t w0 = __builtin_amdgcn_readfirstlane(lp[pi]);
-        const bool two = pi + 1 < npass;
-        const uint32_t w1 = two ? __builtin_amdgcn_readfirstlane(lp[pi + 1]) : w0;
-        if (two) prefetch_pass(w1, lane, lj, resid, B);
-        run_pass<PIX>(w0, lane, tile, eb, bd, A, ltab, resid, ptab, dbg);
-        if (!two) break;
-        if (pi + 2 < npass) prefetch_pass(lp[pi + 2], lane, lj, resid, A);
-        run_pass<PIX>(w1, lane, tile, eb, bd, B, ltab, resid, ptab, dbg);
+#define LPW(k) __builtin_amdgcn_readfirstlane(lp[(k) < npass ? (k) : npass - 1])
+    if (npass) {
+        PSet A, B;
+        JSet J;
+        load_job(LPW(0), lane, lj, J);
+        load_resid(J, resid, A);
+        load_job(LPW(1), lane, lj, J);
+        for (int pi = 0; pi < npass; pi += 2) {
+            const uint32_t w0 = LPW(pi), w1 = LPW(pi + 1);
+            load_resid(J, resid, B);
+            load_job(LPW(pi + 2), lane, lj, J);
+            run_pass<PIX>(w0, lane, tile, eb, bd, A, ltab, resid, ptab, dbg);
+            if (pi + 1 >= npass) break;
+            load_resid(J, resid, A);
+            load_job(LPW(pi + 3), lane, lj, J);
+            run_pass<PIX>(w1, lane, tile, eb, bd, B, ltab, resid, ptab, dbg);
+        }
     }
+#undef LPW
 
     // ---- store the SB interiors ----
     if (!(dbg & 2))
