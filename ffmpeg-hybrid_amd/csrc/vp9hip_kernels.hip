@@ -563,8 +563,8 @@ __global__ __launch_bounds__(64 * RWAVES) void k_resid(const RJob *__restrict__ 
 // (vp9dsp_template.c:28-1106 restated per pixel), then + residual from k_resid, clip.
 // A tile's row 0 / column 0 hold the pixels above / left of the SB; pixel (x, y) of
 // plane p lives at tile_p[(y + 1) * pitch_p + x + 1].
-#define LP 68            // luma tile pitch (65 used)
-#define CP 36            // chroma tile pitch (33 used, 4:2:0)
+#define LP 65            // luma tile pitch
+#define CP 33            // chroma tile pitch (4:2:0)
 #define LT_SIZE (65 * LP)
 #define CT_SIZE (33 * CP)
 #define TILE_ELEMS (LT_SIZE + 2 * CT_SIZE)
