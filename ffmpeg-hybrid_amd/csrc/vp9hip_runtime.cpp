@@ -555,13 +555,24 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
                             q.j.roff = roff;
                         }
                         q.ts = txs;
+                        // level = 1 + the levels of the tx blocks whose pixels this job's
+                        // (substituted) mode reads: the edges[] needs of vp9recon.c:71-97.
+                        // Pixels a mode does not read impose no order (the kernel may load
+                        // them into its edge buffer; no formula of that mode uses them).
                         int lvl = -1;
                         int8_t *lm = lmap[p];
-                        const int trx = (txs == 0 && (x < pw4 - 1)) ? 1 : 0;
-                        if (uy0 > 0)
-                            for (int u = ux0 - 1; u < ux0 + n4 + trx; u++)
+                        const int msub = (int) ((q.j.a >> 8) & 15);   // slot (slot_of) of the substituted mode
+                        static const uint8_t needs[15] = {            // by slot: 1 left, 2 top, 4 top-left, 8 top-right
+                            2, 1, 2 | 8, 1 | 2 | 4, 1 | 2 | 4, 1 | 2 | 4, 2 | 8, 1, 1 | 2 | 4,   // V H D45 D135 D117 D153 D63 D207 TM
+                            1 | 2, 1, 2, 0, 0, 0 };                                            // DC LEFT_DC TOP_DC DC_128/127/129
+                        const int nd = needs[msub];
+                        const int trx = (txs == 0 && (x < pw4 - 1) && (nd & 8)) ? 1 : 0;
+                        if (uy0 > 0) {
+                            const int u0 = (nd & 4) ? ux0 - 1 : ux0, u1 = (nd & 2) ? ux0 + n4 + trx : ux0;
+                            for (int u = u0; u < u1; u++)
                                 if (u >= 0 && u < units) lvl = std::max<int>(lvl, lm[(uy0 - 1) * 16 + u]);
-                        if (ux0 > 0)
+                        }
+                        if (ux0 > 0 && (nd & 1))
                             for (int v = uy0; v < uy0 + n4; v++)
                                 if (v < units) lvl = std::max<int>(lvl, lm[v * 16 + ux0 - 1]);
                         lvl += 1;
