@@ -24,6 +24,7 @@ ENOMEM = -12
 ENOSYS = -38
 EINVALIDDATA = -1094995529
 EEXTERNAL = -542398533
+EBUG = -558323010
 
 BS_64x64, BS_64x32, BS_32x64, BS_32x32, BS_32x16, BS_16x32, BS_16x16, BS_16x8, BS_8x16, \
     BS_8x8, BS_8x4, BS_4x8, BS_4x4 = range(13)
@@ -339,11 +340,11 @@ class Decoder:
 
 PLAN_STAT_NAMES = ("sbs", "passes", "pjobs", "rjobs", "jobs_4x4", "jobs_8x8", "jobs_16x16",
                    "jobs_32x32", "lane_use", "max_passes_sb", "lf_records", "mc_units", "pred_steps",
-                   "lf_steps")
+                   "lf_steps", "levels")
 
 
 def plan_stats(frame):
     """Host-only work-planning statistics of one pass-1 packet (vp9hip_plan_stats)."""
-    out = (ctypes.c_double * 14)()
-    _check("vp9hip_plan_stats", lib().vp9hip_plan_stats(ctypes.byref(frame.pkt), out, 14))
+    out = (ctypes.c_double * len(PLAN_STAT_NAMES))()
+    _check("vp9hip_plan_stats", lib().vp9hip_plan_stats(ctypes.byref(frame.pkt), out, len(PLAN_STAT_NAMES)))
     return dict(zip(PLAN_STAT_NAMES, list(out)))

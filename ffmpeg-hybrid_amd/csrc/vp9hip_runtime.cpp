@@ -63,11 +63,13 @@ struct Staged {
     std::vector<PJob> pjobs;            // merged per workgroup, pass order (device)
     std::vector<uint32_t> passes;       // pass words (device)
     std::vector<WGRec> wgs;             // k_pred workgroups (device)
-    // per-SB intra jobs before merging (host): sorted by (level, ts, mode)
-    struct SBHost { uint32_t job0, njobs, lv0, nlev; };
+    // per-SB intra jobs before pass packing (host), in decode order, with the SB-local
+    // indices of the jobs whose pixels each one reads (jdep0[k] .. jdep0[k + 1])
+    struct SBHost { uint32_t job0, njobs, nlev; };
     std::vector<SBHost> sbh;
     std::vector<PJob> sbjobs;
-    std::vector<uint32_t> sblv;         // level starts (relative to job0), nlev + 1 per SB
+    std::vector<uint32_t> jdep0;        // per job, plus one end marker per SB
+    std::vector<uint16_t> jdeps;
     // residual jobs by (phase, tx code, txtp); a phase = (stream group, chain position)
     std::vector<std::array<std::array<std::vector<RJob>, 4>, 5>> rbucket;
     int ngroups = 1;
@@ -382,7 +384,7 @@ struct FrameBuild {
     uint64_t coef_base;          // element offset of this frame's coefficients in the batch stream
 };
 
-struct PendingJob { PJob j; int level, ts; };
+struct PendingJob { PJob j; int level, ts; uint32_t d0, nd; };   // deps: pdeps[d0 .. d0 + nd)
 
 } // namespace
 
@@ -454,6 +456,8 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
     std::vector<PendingJob> pj;
     pj.reserve(1024);
     int8_t lmap[3][16 * 16];
+    int16_t jmap[3][16 * 16];              // SB-local job index that writes each 4x4 unit
+    std::vector<uint16_t> pdeps;
 
     while (bi < f->nblocks) {
         const vp9h_block *b0 = &f->blocks[bi];
@@ -472,6 +476,8 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
         lf.frame = fb.frame_idx; lf.sbx = sbx; lf.sby = sby;
         pj.clear();
         memset(lmap, -1, sizeof(lmap));
+        memset(jmap, -1, sizeof(jmap));
+        pdeps.clear();
 
         for (; bi < f->nblocks; bi++) {
             const vp9h_block *b = &f->blocks[bi];
@@ -561,6 +567,15 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
                         // them into its edge buffer; no formula of that mode uses them).
                         int lvl = -1;
                         int8_t *lm = lmap[p];
+                        int16_t *jm = jmap[p];
+                        q.d0 = (uint32_t) pdeps.size();
+                        auto dep = [&](int unit) {
+                            lvl = std::max<int>(lvl, lm[unit]);
+                            const int j = jm[unit];
+                            if (j < 0) return;
+                            for (size_t k = q.d0; k < pdeps.size(); k++) if (pdeps[k] == j) return;
+                            pdeps.push_back((uint16_t) j);
+                        };
                         const int msub = (int) ((q.j.a >> 8) & 15);   // slot (slot_of) of the substituted mode
                         static const uint8_t needs[15] = {            // by slot: 1 left, 2 top, 4 top-left, 8 top-right
                             2, 1, 2 | 8, 1 | 2 | 4, 1 | 2 | 4, 1 | 2 | 4, 2 | 8, 1, 1 | 2 | 4,   // V H D45 D135 D117 D153 D63 D207 TM
@@ -570,14 +585,18 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
                         if (uy0 > 0) {
                             const int u0 = (nd & 4) ? ux0 - 1 : ux0, u1 = (nd & 2) ? ux0 + n4 + trx : ux0;
                             for (int u = u0; u < u1; u++)
-                                if (u >= 0 && u < units) lvl = std::max<int>(lvl, lm[(uy0 - 1) * 16 + u]);
+                                if (u >= 0 && u < units) dep((uy0 - 1) * 16 + u);
                         }
                         if (ux0 > 0 && (nd & 1))
                             for (int v = uy0; v < uy0 + n4; v++)
-                                if (v < units) lvl = std::max<int>(lvl, lm[v * 16 + ux0 - 1]);
+                                if (v < units) dep(v * 16 + ux0 - 1);
+                        q.nd = (uint32_t) pdeps.size() - q.d0;
                         lvl += 1;
                         for (int v = uy0; v < uy0 + n4 && v < units; v++)
-                            for (int u = ux0; u < ux0 + n4 && u < units; u++) lm[v * 16 + u] = (int8_t) lvl;
+                            for (int u = ux0; u < ux0 + n4 && u < units; u++) {
+                                lm[v * 16 + u] = (int8_t) lvl;
+                                jm[v * 16 + u] = (int16_t) pj.size();
+                            }
                         q.level = lvl;
                         pj.push_back(q);
                     }
@@ -665,15 +684,10 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
             }
         }
 
-        // group intra jobs into passes: same level and size, up to 64/n jobs; sorted
-        // by (level, size, mode) so a pass runs few distinct predictor paths
+        // intra jobs of the SB, in decode order with their producer lists; pass packing
+        // (list scheduling) happens in merge_mixed
         if (pj.size() > MAX_SB_JOBS) return VP9HIP_EINVALIDDATA;
         if (!pj.empty()) {
-            std::stable_sort(pj.begin(), pj.end(), [](const PendingJob &a, const PendingJob &b) {
-                if (a.level != b.level) return a.level < b.level;
-                if (a.ts != b.ts) return a.ts < b.ts;
-                return ((a.j.a >> 8) & 15) < ((b.j.a >> 8) & 15);
-            });
             SBRec sr;
             memset(&sr, 0, sizeof(sr));
             sr.frame = fb.frame_idx; sr.sbx = sbx; sr.sby = sby;
@@ -682,13 +696,14 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
             Staged::SBHost h;
             h.job0 = (uint32_t) s.sbjobs.size();
             h.njobs = (uint32_t) pj.size();
-            h.lv0 = (uint32_t) s.sblv.size();
+            h.nlev = 0;
             for (size_t k = 0; k < pj.size(); k++) {
-                if (k == 0 || pj[k].level != pj[k - 1].level) s.sblv.push_back((uint32_t) k);
                 s.sbjobs.push_back(pj[k].j);
+                s.jdep0.push_back((uint32_t) s.jdeps.size());
+                s.jdeps.insert(s.jdeps.end(), pdeps.begin() + pj[k].d0, pdeps.begin() + pj[k].d0 + pj[k].nd);
+                h.nlev = std::max<uint32_t>(h.nlev, (uint32_t) pj[k].level + 1);
             }
-            s.sblv.push_back((uint32_t) pj.size());
-            h.nlev = (uint32_t) (s.sblv.size() - h.lv0 - 1);
+            s.jdep0.push_back((uint32_t) s.jdeps.size());
             s.sbh.push_back(h);
             uint32_t sbi = (uint32_t) s.sbs.size();
             s.sbs.push_back(sr);
@@ -709,8 +724,9 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
     return 0;
 }
 
-// Mixed-size packing of one SB's intra jobs: a pass takes jobs of one dependency level
-// of any sizes, 64 lanes = n lanes per n x n job; jobs in a pass are ordered 32x32,
+// Pass packing of one SB's intra jobs by list scheduling: every pass takes ready jobs
+// (all producers in earlier passes), highest remaining critical path first, up to 64
+// lanes (n lanes per n x n job, any sizes mixed). Jobs in a pass are ordered 32x32,
 // 16x16, 8x8, 4x4 so every job's lane group is aligned to its size. Pass word:
 // first << 14 | c4 << 9 | c8 << 5 | c16 << 2 | c32 (job counts per size).
 static int merge_mixed(Staged &s, uint32_t sbi)
@@ -721,26 +737,50 @@ static int merge_mixed(Staged &s, uint32_t sbi)
     wg.pass0 = (uint32_t) s.passes.size();
     wg.sb[0] = sbi;
     const Staged::SBHost &h = s.sbh[sbi];
-    for (uint32_t l = 0; l < h.nlev; l++) {
-        const uint32_t b = s.sblv[h.lv0 + l], e = s.sblv[h.lv0 + l + 1];
-        std::vector<uint32_t> by[4];
-        for (uint32_t j = b; j < e; j++) by[PJ_TS(s.sbjobs[h.job0 + j])].push_back(h.job0 + j);
-        size_t pos[4] = { 0, 0, 0, 0 };
-        for (;;) {
-            int lanes = 0, cnt[4] = { 0, 0, 0, 0 };
-            const uint32_t first = (uint32_t) (s.pjobs.size() - wg.job0);
-            for (int t = 3; t >= 0; t--) {
-                const int n = 4 << t;
-                while (pos[t] < by[t].size() && lanes + n <= 64) {
-                    s.pjobs.push_back(s.sbjobs[by[t][pos[t]++]]);
-                    lanes += n;
-                    cnt[t]++;
-                }
-            }
-            if (!lanes) break;
-            s.passes.push_back(first << 14 | (uint32_t) cnt[0] << 9 | (uint32_t) cnt[1] << 5 | (uint32_t) cnt[2] << 2 |
-                               (uint32_t) cnt[3]);
+    const int N = (int) h.njobs;
+    // the SB's jobs are consecutive, so their producer lists are too: job k's list is
+    // jdep0[job0 + k + sbi] .. (one end marker per earlier SB shifts the index by sbi)
+    const uint32_t *d0 = s.jdep0.data() + h.job0 + sbi;
+    std::vector<std::vector<uint16_t>> succ(N);
+    std::vector<int> indeg(N), height(N, 1);
+    for (int k = 0; k < N; k++) {
+        indeg[k] = (int) (d0[k + 1] - d0[k]);
+        for (uint32_t e = d0[k]; e < d0[k + 1]; e++) succ[s.jdeps[e]].push_back((uint16_t) k);
+    }
+    for (int k = N - 1; k >= 0; k--)                      // producers precede consumers
+        for (uint16_t c : succ[k]) height[k] = std::max(height[k], height[c] + 1);
+    std::vector<int> ready, next;
+    for (int k = 0; k < N; k++) if (!indeg[k]) ready.push_back(k);
+    int done = 0;
+    while (done < N) {
+        if (ready.empty()) return VP9HIP_EBUG;
+        std::sort(ready.begin(), ready.end(), [&](int a, int b) {
+            if (height[a] != height[b]) return height[a] > height[b];
+            return a < b;
+        });
+        int lanes = 0, cnt[4] = { 0, 0, 0, 0 };
+        std::vector<int> take;
+        next.clear();
+        for (int k : ready) {
+            const int n = 4 << PJ_TS(s.sbjobs[h.job0 + k]);
+            if (lanes + n <= 64) { take.push_back(k); lanes += n; }
+            else next.push_back(k);
         }
+        std::stable_sort(take.begin(), take.end(), [&](int a, int b) {
+            return PJ_TS(s.sbjobs[h.job0 + a]) > PJ_TS(s.sbjobs[h.job0 + b]);
+        });
+        const uint32_t first = (uint32_t) (s.pjobs.size() - wg.job0);
+        for (int k : take) {
+            s.pjobs.push_back(s.sbjobs[h.job0 + k]);
+            cnt[PJ_TS(s.sbjobs[h.job0 + k])]++;
+        }
+        s.passes.push_back(first << 14 | (uint32_t) cnt[0] << 9 | (uint32_t) cnt[1] << 5 | (uint32_t) cnt[2] << 2 |
+                           (uint32_t) cnt[3]);
+        for (int k : take)
+            for (uint16_t c : succ[k])
+                if (--indeg[c] == 0) next.push_back(c);
+        done += (int) take.size();
+        ready.swap(next);
     }
     const size_t nj = s.pjobs.size() - wg.job0, np = s.passes.size() - wg.pass0;
     if (nj > MAX_SB_JOBS || np > MAX_SB_JOBS) return VP9HIP_EINVALIDDATA;
@@ -760,7 +800,7 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     Staged &s = c->stg;
     if (s.graph) { hipGraphExecDestroy(s.graph); s.graph = nullptr; }
     s.frames.clear(); s.sbs.clear(); s.pjobs.clear(); s.passes.clear(); s.lfs.clear(); s.mcs.clear();
-    s.wgs.clear(); s.sbh.clear(); s.sbjobs.clear(); s.sblv.clear();
+    s.wgs.clear(); s.sbh.clear(); s.sbjobs.clear(); s.jdep0.clear(); s.jdeps.clear();
     s.rjobs.clear(); s.resid16 = 0;
     s.rbucket.clear();
     s.lists.clear(); s.launches.clear(); s.coefs.clear();
@@ -1227,7 +1267,7 @@ extern "C" int vp9hip_abi_version(void) { return VP9HIP_ABI_VERSION; }
 // in one SB, 10 LF records, 11 MC units, 12 intra wavefront steps, 13 LF wavefront steps.
 extern "C" int vp9hip_plan_stats(const vp9h_frame *f, double *out, int cap)
 {
-    if (!f || !out || cap < 14) return VP9HIP_EINVAL;
+    if (!f || !out || cap < 15) return VP9HIP_EINVAL;
     if (f->ss_h != 1 || f->ss_v != 1) return VP9HIP_ENOSYS;
     init_nz();
     Staged s;
@@ -1243,14 +1283,13 @@ extern "C" int vp9hip_plan_stats(const vp9h_frame *f, double *out, int cap)
     std::vector<std::vector<uint32_t>> ps, ls;
     int r = build_frame(nullptr, s, fb, ps, ls);
     if (r < 0) return r;
-    for (int i = 0; i < 14; i++) out[i] = 0;
     // one k_pred workgroup per SB, mixed-size passes (as staged for the device)
     for (auto &v : ps)
         for (uint32_t sbi : v) {
             r = merge_mixed(s, sbi);
             if (r) return r;
         }
-    for (int i = 0; i < 14; i++) out[i] = 0;
+    for (int i = 0; i < 15; i++) out[i] = 0;
     out[0] = (double) s.sbs.size();
     out[1] = (double) s.passes.size();
     out[2] = (double) s.pjobs.size();
@@ -1269,5 +1308,6 @@ extern "C" int vp9hip_plan_stats(const vp9h_frame *f, double *out, int cap)
     out[11] = (double) s.mcs.size();
     out[12] = (double) ps.size();
     out[13] = (double) ls.size();
+    for (auto &h : s.sbh) out[14] += h.nlev;                           // dependency levels (pass lower bound)
     return 0;
 }

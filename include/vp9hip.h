@@ -38,6 +38,7 @@ extern "C" {
 #define VP9HIP_ENOSYS       (-38)          /* AVERROR(ENOSYS)   */
 #define VP9HIP_EINVALIDDATA (-1094995529)  /* AVERROR_INVALIDDATA */
 #define VP9HIP_EEXTERNAL    (-542398533)   /* AVERROR_EXTERNAL (HIP runtime failure) */
+#define VP9HIP_EBUG         (-558323010)   /* AVERROR_BUG (internal invariant broken) */
 
 /* enum BlockSize (vp9shared.h:86-101) */
 enum { VP9H_BS_64x64, VP9H_BS_64x32, VP9H_BS_32x64, VP9H_BS_32x32, VP9H_BS_32x16,
@@ -190,9 +191,10 @@ int  vp9hip_set_timing(vp9hip_ctx *ctx, int on);
  * per kernel class in vp9hip_last_timing order. Returns count. */
 int  vp9hip_alg_bytes(vp9hip_ctx *ctx, double *bytes, int cap);
 
-/* Host-only planning statistics of one packet (no device needed), 14 values:
+/* Host-only planning statistics of one packet (no device needed), 15 values:
  * SBs with intra work, passes, intra jobs, residual jobs, intra jobs per tx size (4),
- * lane use, max passes per SB, LF records, MC units, intra / LF wavefront steps. */
+ * lane use, max passes per SB, LF records, MC units, intra / LF wavefront steps,
+ * intra dependency levels (summed over SBs: the lower bound of the passes). */
 int  vp9hip_plan_stats(const vp9h_frame *pkt, double *out, int cap);
 
 int  vp9hip_abi_version(void);
