@@ -28,7 +28,6 @@
 
 // ------------------------------------------------------------------ helpers
 DEV int clipbd(int v, int bd) { int m = (1 << bd) - 1; return v < 0 ? 0 : (v > m ? m : v); }
-DEV int iabs(int v) { return v < 0 ? -v : v; }
 
 DEV void wave_sync()
 {
@@ -886,75 +885,6 @@ __global__ __launch_bounds__(64) void k_pred(const uint32_t *__restrict__ list, 
     pred_wg<PIX>(wgs + list[blockIdx.x], sbs, jobs, passes, frames, resid, ptab, S, threadIdx.x, dbg);
 }
 
-// --------------------------------------------------------------- k_lf
-// loop_filter (vp9dsp_template.c:1780-1889) on one line of 16 pixels around an
-// edge; `p` points at q0, `s` is the step across the edge.
-DEV void lf_line(uint16_t *p, int s, int wd, int L, int sharp, int bd)
-{
-    int limit = L;
-    if (sharp > 0) { limit >>= (sharp + 3) >> 2; limit = limit < 9 - sharp ? limit : 9 - sharp; }
-    limit = limit > 1 ? limit : 1;                                 // vp9.c:674-685
-    int E = (2 * (L + 2) + limit) << (bd - 8), I = limit << (bd - 8), H = (L >> 4) << (bd - 8);
-    int F = 1 << (bd - 8);
-    int p3 = p[-4 * s], p2 = p[-3 * s], p1 = p[-2 * s], p0 = p[-s];
-    int q0 = p[0], q1 = p[s], q2 = p[2 * s], q3 = p[3 * s];
-    bool fm = iabs(p3 - p2) <= I && iabs(p2 - p1) <= I && iabs(p1 - p0) <= I &&
-              iabs(q1 - q0) <= I && iabs(q2 - q1) <= I && iabs(q3 - q2) <= I &&
-              iabs(p0 - q0) * 2 + (iabs(p1 - q1) >> 1) <= E;
-    if (!fm) return;
-    bool flat8in = false, flat8out = false;
-    if (wd >= 8)
-        flat8in = iabs(p3 - p0) <= F && iabs(p2 - p0) <= F && iabs(p1 - p0) <= F &&
-                  iabs(q1 - q0) <= F && iabs(q2 - q0) <= F && iabs(q3 - q0) <= F;
-    if (wd >= 16 && flat8in) {
-        int p7 = p[-8 * s], p6 = p[-7 * s], p5 = p[-6 * s], p4 = p[-5 * s];
-        int q4 = p[4 * s], q5 = p[5 * s], q6 = p[6 * s], q7 = p[7 * s];
-        flat8out = iabs(p7 - p0) <= F && iabs(p6 - p0) <= F && iabs(p5 - p0) <= F &&
-                   iabs(p4 - p0) <= F && iabs(q4 - q0) <= F && iabs(q5 - q0) <= F &&
-                   iabs(q6 - q0) <= F && iabs(q7 - q0) <= F;
-        if (flat8out) {
-            // 15-tap: running window sum over {p7..q7} with edge replication
-            int v[16] = { p7, p6, p5, p4, p3, p2, p1, p0, q0, q1, q2, q3, q4, q5, q6, q7 };
-            int sum = p7 * 7 + p6 * 2 + p5 + p4 + p3 + p2 + p1 + p0 + q0;   // output index 1
-            int out[16];
-            for (int k = 1; k < 15; k++) {
-                out[k] = (sum + 8) >> 4;
-                // slide: window [k-7, k+7] (+ v[k] twice) -> [k-6, k+8] (+ v[k+1] twice)
-                int lo = k - 7 < 0 ? 0 : k - 7, hi = k + 8 > 15 ? 15 : k + 8;
-                sum += v[hi] - v[lo] + v[k + 1] - v[k];
-            }
-            for (int k = 1; k < 15; k++) p[(k - 8) * s] = out[k];
-            return;
-        }
-    }
-    if (wd >= 8 && flat8in) {
-        p[-3 * s] = (p3 + p3 + p3 + 2 * p2 + p1 + p0 + q0 + 4) >> 3;
-        p[-2 * s] = (p3 + p3 + p2 + 2 * p1 + p0 + q0 + q1 + 4) >> 3;
-        p[-1 * s] = (p3 + p2 + p1 + 2 * p0 + q0 + q1 + q2 + 4) >> 3;
-        p[0] = (p2 + p1 + p0 + 2 * q0 + q1 + q2 + q3 + 4) >> 3;
-        p[1 * s] = (p1 + p0 + q0 + 2 * q1 + q2 + q3 + q3 + 4) >> 3;
-        p[2 * s] = (p0 + q0 + q1 + 2 * q2 + q3 + q3 + q3 + 4) >> 3;
-        return;
-    }
-    const int mx = (1 << (bd - 1)) - 1, mn = -(1 << (bd - 1));
-    bool hev = iabs(p1 - p0) > H || iabs(q1 - q0) > H;
-    if (hev) {
-        int f = p1 - q1; f = f < mn ? mn : f > mx ? mx : f;
-        f = 3 * (q0 - p0) + f; f = f < mn ? mn : f > mx ? mx : f;
-        int f1 = (f + 4 < mx ? f + 4 : mx) >> 3, f2 = (f + 3 < mx ? f + 3 : mx) >> 3;
-        p[-s] = clipbd(p0 + f2, bd);
-        p[0] = clipbd(q0 - f1, bd);
-    } else {
-        int f = 3 * (q0 - p0); f = f < mn ? mn : f > mx ? mx : f;
-        int f1 = (f + 4 < mx ? f + 4 : mx) >> 3, f2 = (f + 3 < mx ? f + 3 : mx) >> 3;
-        p[-s] = clipbd(p0 + f2, bd);
-        p[0] = clipbd(q0 - f1, bd);
-        f = (f1 + 1) >> 1;
-        p[-2 * s] = clipbd(p1 + f, bd);
-        p[s] = clipbd(q1 - f, bd);
-    }
-}
-
 // 8-pixel chunk <-> 8 uint16 of the LF tile (tile rows are 4-byte aligned)
 template <typename PIX> struct Chunk8;
 template <> struct Chunk8<uint8_t> {
@@ -997,8 +927,13 @@ DEV void lf_chunk(int ci, int &p, int &r, int &k)
     else { const int c = ci - 648; p = 1 + (c >= 200); const int cc = c - (p - 1) * 200; r = cc / 5; k = cc - r * 5; }
 }
 
-// The same filter on a line held in registers: q0 = px[C], compile-time positions, so
-// a row's chain of edges (vp9lpf.c:31-104 order) runs without LDS round trips.
+// --------------------------------------------------------------- k_lf
+DEV int ad16(int a, int b) { return (int) __builtin_amdgcn_sad_u16((uint32_t) a, (uint32_t) b, 0u); }
+DEV int max3i(int a, int b, int c) { return max(max(a, b), c); }
+
+// loop_filter (vp9dsp_template.c:1780-1889) on a line held in registers: q0 = px[C],
+// compile-time positions, so a row's chain of edges (vp9lpf.c:31-104 order) runs
+// without LDS round trips.
 template <int C, int NPX>
 DEV void lf_reg(int (&px)[NPX], int wd, int L, int sharp, int bd)
 {
@@ -1009,22 +944,22 @@ DEV void lf_reg(int (&px)[NPX], int wd, int L, int sharp, int bd)
     const int F = 1 << (bd - 8);
     const int p3 = px[C - 4], p2 = px[C - 3], p1 = px[C - 2], p0 = px[C - 1];
     const int q0 = px[C], q1 = px[C + 1], q2 = px[C + 2], q3 = px[C + 3];
-    const bool fm = iabs(p3 - p2) <= I && iabs(p2 - p1) <= I && iabs(p1 - p0) <= I &&
-                    iabs(q1 - q0) <= I && iabs(q2 - q1) <= I && iabs(q3 - q2) <= I &&
-                    iabs(p0 - q0) * 2 + (iabs(p1 - q1) >> 1) <= E;
+    // decisions branch-free: |a - b| is one v_sad_u16 (pixels < 2^12), reductions by max3,
+    // one compare per condition (the reference's && chains compile to a branch per term)
+    const int ap1p0 = ad16(p1, p0), aq1q0 = ad16(q1, q0);
+    const int mi = max3i(max3i(ad16(p3, p2), ad16(p2, p1), ap1p0), max3i(aq1q0, ad16(q2, q1), ad16(q3, q2)), 0);
+    const bool fm = (mi <= I) & (ad16(p0, q0) * 2 + (ad16(p1, q1) >> 1) <= E);
     if (!fm) return;
-    bool flat8in = false;
-    if (wd >= 8)
-        flat8in = iabs(p3 - p0) <= F && iabs(p2 - p0) <= F && iabs(p1 - p0) <= F &&
-                  iabs(q1 - q0) <= F && iabs(q2 - q0) <= F && iabs(q3 - q0) <= F;
+    const bool flat8in = (wd >= 8) &
+                         (max3i(max3i(ad16(p3, p0), ad16(p2, p0), ap1p0), max3i(aq1q0, ad16(q2, q0), ad16(q3, q0)), 0) <= F);
     if (C >= 8 && C + 7 < NPX && wd >= 16 && flat8in) {
         const int p7 = px[C - 8 >= 0 ? C - 8 : 0], p6 = px[C - 7 >= 0 ? C - 7 : 0], p5 = px[C - 6 >= 0 ? C - 6 : 0],
                   p4 = px[C - 5 >= 0 ? C - 5 : 0];
         const int q4 = px[C + 4 < NPX ? C + 4 : NPX - 1], q5 = px[C + 5 < NPX ? C + 5 : NPX - 1],
                   q6 = px[C + 6 < NPX ? C + 6 : NPX - 1], q7 = px[C + 7 < NPX ? C + 7 : NPX - 1];
-        const bool flat8out = iabs(p7 - p0) <= F && iabs(p6 - p0) <= F && iabs(p5 - p0) <= F &&
-                              iabs(p4 - p0) <= F && iabs(q4 - q0) <= F && iabs(q5 - q0) <= F &&
-                              iabs(q6 - q0) <= F && iabs(q7 - q0) <= F;
+        const bool flat8out = max3i(max3i(ad16(p7, p0), ad16(p6, p0), ad16(p5, p0)),
+                                    max3i(ad16(p4, p0), ad16(q4, q0), ad16(q5, q0)),
+                                    max3i(ad16(q6, q0), ad16(q7, q0), 0)) <= F;
         if (flat8out) {
             // 15-tap (vp9dsp_template.c:1836-1857): running window sum with edge replication
             const int v[16] = { p7, p6, p5, p4, p3, p2, p1, p0, q0, q1, q2, q3, q4, q5, q6, q7 };
@@ -1049,7 +984,7 @@ DEV void lf_reg(int (&px)[NPX], int wd, int L, int sharp, int bd)
         return;
     }
     const int mx = (1 << (bd - 1)) - 1, mn = -(1 << (bd - 1));
-    const bool hev = iabs(p1 - p0) > H || iabs(q1 - q0) > H;
+    const bool hev = (ap1p0 > H) | (aq1q0 > H);
     if (hev) {
         int f = p1 - q1; f = f < mn ? mn : f > mx ? mx : f;
         f = 3 * (q0 - p0) + f; f = f < mn ? mn : f > mx ? mx : f;
