@@ -934,14 +934,14 @@ DEV int max3i(int a, int b, int c) { return max(max(a, b), c); }
 // loop_filter (vp9dsp_template.c:1780-1889) on a line held in registers: q0 = px[C],
 // compile-time positions, so a row's chain of edges (vp9lpf.c:31-104 order) runs
 // without LDS round trips.
+// `code` = filter width (1: 4, 2: 8, 3: 16), `eih` = the E | I << 12 | H << 22 word of
+// the edge's level (lf_lut).
 template <int C, int NPX>
-DEV void lf_reg(int (&px)[NPX], int wd, int L, int sharp, int bd)
+DEV void lf_reg(int (&px)[NPX], int code, uint32_t eih, int bd)
 {
-    int limit = L;
-    if (sharp > 0) { limit >>= (sharp + 3) >> 2; limit = limit < 9 - sharp ? limit : 9 - sharp; }
-    limit = limit > 1 ? limit : 1;                                 // vp9.c:674-685
-    const int E = (2 * (L + 2) + limit) << (bd - 8), I = limit << (bd - 8), H = (L >> 4) << (bd - 8);
+    const int E = eih & 4095, I = (eih >> 12) & 1023, H = eih >> 22;
     const int F = 1 << (bd - 8);
+    const int wd = 4 << (code - 1);
     const int p3 = px[C - 4], p2 = px[C - 3], p1 = px[C - 2], p0 = px[C - 1];
     const int q0 = px[C], q1 = px[C + 1], q2 = px[C + 2], q3 = px[C + 3];
     // decisions branch-free: |a - b| is one v_sad_u16 (pixels < 2^12), reductions by max3,
@@ -1011,9 +1011,20 @@ DEV void lf_reg(int (&px)[NPX], int wd, int L, int sharp, int bd)
 struct LfLds {
     uint16_t lt[72 * FLP];
     uint16_t ct[2][40 * FCP];
-    uint8_t lvl[64];
-    uint8_t msk[2][2][8][4];
+    uint32_t prog[LF_PROG_BYTES / 4];     // the SB's edge decisions (LFRec.prog)
+    uint32_t lut[64];                     // level -> E | I << 12 | H << 22
 };
+
+// E / I / H of a filter level (vp9.c:669-687 limit LUTs; loop_filter's F / E / I / H
+// scaling by bit depth, vp9dsp_template.c:1780-1800)
+DEV uint32_t lf_eih(int L, int sharp, int bd)
+{
+    int limit = L;
+    if (sharp > 0) { limit >>= (sharp + 3) >> 2; limit = limit < 9 - sharp ? limit : 9 - sharp; }
+    limit = limit > 1 ? limit : 1;
+    const uint32_t E = (2 * (L + 2) + limit) << (bd - 8), I = limit << (bd - 8), H = (L >> 4) << (bd - 8);
+    return E | I << 12 | H << 22;
+}
 
 template <typename PIX, int NT>
 DEV void lf_sb(const LFRec &rec, const FrameDesc *__restrict__ frames, LfLds &S, int lane, int dbg)
@@ -1021,13 +1032,12 @@ DEV void lf_sb(const LFRec &rec, const FrameDesc *__restrict__ frames, LfLds &S,
 #define LF_SYNC() do { if (NT == 64) wave_sync(); else __syncthreads(); } while (0)
     uint16_t *lt = S.lt;
     uint16_t (*ct)[40 * FCP] = S.ct;
-    uint8_t *lvl = S.lvl;
-    uint8_t (*msk)[2][8][4] = S.msk;
+    const uint32_t *lut = S.lut;
     const FrameDesc &fd = frames[rec.frame];
     const int bd = fd.bd, sharp = fd.sharp;
     const int sbx = rec.sbx, sby = rec.sby;
-    for (int i = lane; i < 64; i += NT) lvl[i] = rec.level[i];
-    for (int i = lane; i < 128; i += NT) ((uint8_t *) msk)[i] = ((const uint8_t *) rec.mask)[i];
+    for (int i = lane; i < LF_PROG_BYTES / 4; i += NT) S.prog[i] = ((const uint32_t *) rec.prog)[i];
+    for (int i = lane; i < 64; i += NT) S.lut[i] = lf_eih(i, sharp, bd);
 
     // load: luma rows [y0-8, y0+64) x cols [x0-8, x0+64), chroma [-8, 32), in aligned
     // 8-pixel chunks (luma 72 x 9, chroma 2 x 40 x 5 = 1048 chunks, <= 9 per thread), all
@@ -1057,7 +1067,6 @@ DEV void lf_sb(const LFRec &rec, const FrameDesc *__restrict__ frames, LfLds &S,
     }
     LF_SYNC();
 
-    const int col = sbx * 8, row = sby * 8;   // SB position in 8x8 units
     if (!(dbg & 1)) {
     // ---- column edges (filter_plane_cols, vp9lpf.c:31-104): one lane per pixel row, the
     //      row in registers (luma x = -8..63, chroma x = -8..31), edges left to right ----
@@ -1071,28 +1080,15 @@ DEV void lf_sb(const LFRec &rec, const FrameDesc *__restrict__ frames, LfLds &S,
             const uint32_t w = ((const uint32_t *) rowp)[i];
             px[2 * i] = w & 0xffff; px[2 * i + 1] = w >> 16;
         }
-        const uint8_t(*mask)[4] = msk[0][0];
-        const int band = r >> 3, half = band & 1, y = (band >> 1) * 2;
-        const uint8_t *hm1 = mask[y], *hm2 = mask[y + 1];
-        const int lrow1 = y, lrow2 = y + 1;
-        const unsigned h1 = hm1[0] | hm1[1] | hm1[2], h2 = hm2[1] | hm2[2];
+        // edge bytes of this row's band: (main, inner) for edges 0..7
+        const uint32_t *pw = S.prog + (LFP_YC + (r >> 3) * 16) / 4;
+        const uint32_t pw0 = pw[0], pw1 = pw[1], pw2 = pw[2], pw3 = pw[3];
 #define LF_COL_EDGE(k)                                                                                   \
         {                                                                                                \
-            const unsigned x = 1u << (k);                                                                \
-            if (col || (k) > 0) {                                                                        \
-                int wd = 0, L = 0;                                                                       \
-                if (!half) {                                                                             \
-                    if (h1 & x) { wd = (hm1[0] & x) ? 16 : (hm1[1] & x) ? 8 : 4; L = lvl[lrow1 * 8 + (k)]; } \
-                } else {                                                                                 \
-                    if (h1 & x) {                                                                        \
-                        if (hm1[0] & x) { if (hm2[0] & x) { wd = 16; L = lvl[lrow1 * 8 + (k)]; } }        \
-                        else if (h2 & x) { wd = (hm2[1] & x) ? 8 : 4; L = lvl[lrow2 * 8 + (k)]; }         \
-                    } else if (h2 & x) { wd = (hm2[1] & x) ? 8 : 4; L = lvl[lrow2 * 8 + (k)]; }           \
-                }                                                                                        \
-                if (wd) lf_reg<8 * (k) + 8>(px, wd, L, sharp, bd);                                       \
-            }                                                                                            \
-            const unsigned in = half ? hm2[3] : hm1[3];                                                  \
-            if (in & x) lf_reg<8 * (k) + 12>(px, 4, lvl[(half ? lrow2 : lrow1) * 8 + (k)], sharp, bd);   \
+            const uint32_t ww = (k) < 2 ? pw0 : (k) < 4 ? pw1 : (k) < 6 ? pw2 : pw3;                     \
+            const uint32_t m = (ww >> (16 * ((k) & 1))) & 255, in = (ww >> (16 * ((k) & 1) + 8)) & 255;  \
+            if (m >> 6) lf_reg<8 * (k) + 8>(px, m >> 6, lut[m & 63], bd);                                \
+            if (in) lf_reg<8 * (k) + 12>(px, 1, lut[in & 63], bd);                                       \
         }
         LF_COL_EDGE(0) LF_COL_EDGE(1) LF_COL_EDGE(2) LF_COL_EDGE(3)
         LF_COL_EDGE(4) LF_COL_EDGE(5) LF_COL_EDGE(6) LF_COL_EDGE(7)
@@ -1110,25 +1106,12 @@ DEV void lf_sb(const LFRec &rec, const FrameDesc *__restrict__ frames, LfLds &S,
         }
 #pragma unroll
         for (int i = 40; i < 48; i++) px[i] = 0;
-        const uint8_t(*mask)[4] = msk[1][0];
-        const int band = r >> 3, half = band & 1, y = (band >> 1) * 4;
-        const uint8_t *hm1 = mask[y], *hm2 = mask[y + 2];
-        const int lrow1 = y, lrow2 = y + 2;
-        const unsigned h1 = hm1[0] | hm1[1] | hm1[2], h2 = hm2[1] | hm2[2];
+        const uint32_t *pw = S.prog + (LFP_CC + (r >> 3) * 8) / 4;
+        const uint32_t pc0 = pw[0], pc1 = pw[1];
 #define LF_COL_EDGE_UV(k)                                                                                \
-        if (col || (k) > 0) {                                                                            \
-            const unsigned x = 1u << (k);                                                                \
-            const int lc = (k) & ~1;                                                                     \
-            int wd = 0, L = 0;                                                                           \
-            if (!half) {                                                                                 \
-                if (h1 & x) { wd = (hm1[0] & x) ? 16 : (hm1[1] & x) ? 8 : 4; L = lvl[lrow1 * 8 + lc]; }  \
-            } else {                                                                                     \
-                if (h1 & x) {                                                                            \
-                    if (hm1[0] & x) { if (hm2[0] & x) { wd = 16; L = lvl[lrow1 * 8 + lc]; } }            \
-                    else if (h2 & x) { wd = (hm2[1] & x) ? 8 : 4; L = lvl[lrow2 * 8 + lc]; }             \
-                } else if (h2 & x) { wd = (hm2[1] & x) ? 8 : 4; L = lvl[lrow2 * 8 + lc]; }               \
-            }                                                                                            \
-            if (wd) lf_reg<4 * (k) + 8>(px, wd, L, sharp, bd);                                           \
+        {                                                                                                \
+            const uint32_t m = (((k) < 4 ? pc0 : pc1) >> (8 * ((k) & 3))) & 255;                         \
+            if (m >> 6) lf_reg<4 * (k) + 8>(px, m >> 6, lut[m & 63], bd);                                \
         }
         LF_COL_EDGE_UV(0) LF_COL_EDGE_UV(1) LF_COL_EDGE_UV(2) LF_COL_EDGE_UV(3)
         LF_COL_EDGE_UV(4) LF_COL_EDGE_UV(5) LF_COL_EDGE_UV(6) LF_COL_EDGE_UV(7)
@@ -1147,28 +1130,14 @@ DEV void lf_sb(const LFRec &rec, const FrameDesc *__restrict__ frames, LfLds &S,
         int px[72];
 #pragma unroll
         for (int i = 0; i < 72; i++) px[i] = colp[i * FLP];
-        const uint8_t(*mask)[4] = msk[0][1];
-        const int chunk = c >> 4, half = (c >> 3) & 1;
-        const unsigned x = 1u << (chunk * 2), x2 = x << 1;
-        const int lc1 = chunk * 2, lc2 = lc1 + 1;
+        const uint32_t *pw = S.prog + (LFP_YR + (c >> 3) * 16) / 4;
+        const uint32_t pw0 = pw[0], pw1 = pw[1], pw2 = pw[2], pw3 = pw[3];
 #define LF_ROW_EDGE(yy)                                                                                  \
         {                                                                                                \
-            const uint8_t *vm_ = mask[yy];                                                               \
-            const unsigned vm = vm_[0] | vm_[1] | vm_[2], vm3 = vm_[3];                                  \
-            if (row || (yy)) {                                                                           \
-                int wd = 0, L = 0;                                                                       \
-                if (!half) {                                                                             \
-                    if (vm & x) { wd = (vm_[0] & x) ? 16 : (vm_[1] & x) ? 8 : 4; L = lvl[(yy) * 8 + lc1]; } \
-                } else {                                                                                 \
-                    if (vm & x) {                                                                        \
-                        if (vm_[0] & x) { if (vm_[0] & x2) { wd = 16; L = lvl[(yy) * 8 + lc1]; } }        \
-                        else if (vm & x2) { wd = (vm_[1] & x2) ? 8 : 4; L = lvl[(yy) * 8 + lc2]; }       \
-                    } else if (vm & x2) { wd = (vm_[1] & x2) ? 8 : 4; L = lvl[(yy) * 8 + lc2]; }         \
-                }                                                                                        \
-                if (wd) lf_reg<8 * (yy) + 8>(px, wd, L, sharp, bd);                                      \
-            }                                                                                            \
-            if (!half) { if (vm3 & x) lf_reg<8 * (yy) + 12>(px, 4, lvl[(yy) * 8 + lc1], sharp, bd); }   \
-            else { if (vm3 & x2) lf_reg<8 * (yy) + 12>(px, 4, lvl[(yy) * 8 + lc2], sharp, bd); }         \
+            const uint32_t ww = (yy) < 2 ? pw0 : (yy) < 4 ? pw1 : (yy) < 6 ? pw2 : pw3;                  \
+            const uint32_t m = (ww >> (16 * ((yy) & 1))) & 255, in = (ww >> (16 * ((yy) & 1) + 8)) & 255; \
+            if (m >> 6) lf_reg<8 * (yy) + 8>(px, m >> 6, lut[m & 63], bd);                               \
+            if (in) lf_reg<8 * (yy) + 12>(px, 1, lut[in & 63], bd);                                      \
         }
         LF_ROW_EDGE(0) LF_ROW_EDGE(1) LF_ROW_EDGE(2) LF_ROW_EDGE(3)
         LF_ROW_EDGE(4) LF_ROW_EDGE(5) LF_ROW_EDGE(6) LF_ROW_EDGE(7)
@@ -1183,25 +1152,12 @@ DEV void lf_sb(const LFRec &rec, const FrameDesc *__restrict__ frames, LfLds &S,
         for (int i = 0; i < 40; i++) px[i] = colp[i * FCP];
 #pragma unroll
         for (int i = 40; i < 48; i++) px[i] = 0;
-        const uint8_t(*mask)[4] = msk[1][1];
-        const int chunk = c >> 4, half = (c >> 3) & 1;
-        const unsigned x = 1u << (chunk * 4), x2 = x << 2;
-        const int lc1 = chunk * 4, lc2 = lc1 + 2;
+        const uint32_t *pw = S.prog + (LFP_CR + (c >> 3) * 8) / 4;
+        const uint32_t pc0 = pw[0], pc1 = pw[1];
 #define LF_ROW_EDGE_UV(yy)                                                                               \
-        if (row || (yy)) {                                                                               \
-            const uint8_t *vm_ = mask[yy];                                                               \
-            const unsigned vm = vm_[0] | vm_[1] | vm_[2];                                                \
-            const int lr = (yy) & ~1;                                                                    \
-            int wd = 0, L = 0;                                                                           \
-            if (!half) {                                                                                 \
-                if (vm & x) { wd = (vm_[0] & x) ? 16 : (vm_[1] & x) ? 8 : 4; L = lvl[lr * 8 + lc1]; }    \
-            } else {                                                                                     \
-                if (vm & x) {                                                                            \
-                    if (vm_[0] & x) { if (vm_[0] & x2) { wd = 16; L = lvl[lr * 8 + lc1]; } }              \
-                    else if (vm & x2) { wd = (vm_[1] & x2) ? 8 : 4; L = lvl[lr * 8 + lc2]; }             \
-                } else if (vm & x2) { wd = (vm_[1] & x2) ? 8 : 4; L = lvl[lr * 8 + lc2]; }               \
-            }                                                                                            \
-            if (wd) lf_reg<4 * (yy) + 8>(px, wd, L, sharp, bd);                                          \
+        {                                                                                                \
+            const uint32_t m = (((yy) < 4 ? pc0 : pc1) >> (8 * ((yy) & 3))) & 255;                       \
+            if (m >> 6) lf_reg<4 * (yy) + 8>(px, m >> 6, lut[m & 63], bd);                               \
         }
         LF_ROW_EDGE_UV(0) LF_ROW_EDGE_UV(1) LF_ROW_EDGE_UV(2) LF_ROW_EDGE_UV(3)
         LF_ROW_EDGE_UV(4) LF_ROW_EDGE_UV(5) LF_ROW_EDGE_UV(6) LF_ROW_EDGE_UV(7)

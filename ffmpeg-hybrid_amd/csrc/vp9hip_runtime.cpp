@@ -439,6 +439,72 @@ static McRef mc_chroma_ref(const FrameBuild &fb, int rf, int x, int y, const int
     return m;
 }
 
+// Filter width code | level of one edge (LFRec.prog)
+static inline uint8_t lf_byte(int wd, int L)
+{
+    return wd ? (uint8_t) ((wd == 16 ? 3 : wd == 8 ? 2 : 1) << 6 | L) : 0;
+}
+
+// The LF program of one SB: which filter (width, level) every edge of every 8-line band
+// gets, exactly as filter_plane_cols / filter_plane_rows select it from the masks,
+// including the mix2 pairing of two 8-line halves (vp9lpf.c:31-181, loopfilter_sb
+// 183-230). col0 / row0: the SB is at the frame's left / top edge (no outer edge there).
+static void lf_program(const uint8_t *lvl, const uint8_t (*msk)[2][8][4], bool col0, bool row0, uint8_t *prog)
+{
+    memset(prog, 0, LF_PROG_BYTES);
+    for (int pl = 0; pl < 2; pl++) {
+        const int nb = pl ? 4 : 8;                  // bands of 8 pixel lines
+        const int dy = pl ? 2 : 1;                  // mask rows per 8 pixel lines (4:2:0)
+        // column edges (filter_plane_cols): band of pixel rows, edges left to right
+        for (int band = 0; band < nb; band++) {
+            const int half = band & 1, y = (band >> 1) * 2 * dy;
+            const uint8_t *hm1 = msk[pl][0][y], *hm2 = msk[pl][0][y + dy];
+            const unsigned h1 = hm1[0] | hm1[1] | hm1[2], h2 = hm2[1] | hm2[2];
+            for (int k = 0; k < 8; k++) {
+                const unsigned x = 1u << k;
+                const int lc = pl ? k & ~1 : k;
+                int wd = 0, L = 0;
+                if (!col0 || k > 0) {
+                    if (!half) {
+                        if (h1 & x) { wd = (hm1[0] & x) ? 16 : (hm1[1] & x) ? 8 : 4; L = lvl[y * 8 + lc]; }
+                    } else if (h1 & x) {
+                        if (hm1[0] & x) { if (hm2[0] & x) { wd = 16; L = lvl[y * 8 + lc]; } }
+                        else if (h2 & x) { wd = (hm2[1] & x) ? 8 : 4; L = lvl[(y + dy) * 8 + lc]; }
+                    } else if (h2 & x) { wd = (hm2[1] & x) ? 8 : 4; L = lvl[(y + dy) * 8 + lc]; }
+                }
+                if (pl) { prog[LFP_CC + band * 8 + k] = lf_byte(wd, L); continue; }
+                prog[LFP_YC + band * 16 + k * 2] = lf_byte(wd, L);
+                const unsigned in = half ? hm2[3] : hm1[3];
+                if (in & x) prog[LFP_YC + band * 16 + k * 2 + 1] = (uint8_t) (0x40 | lvl[(half ? y + 1 : y) * 8 + k]);
+            }
+        }
+        // row edges (filter_plane_rows): band of pixel columns, edges top to bottom
+        for (int band = 0; band < nb; band++) {
+            const int chunk = band >> 1, half = band & 1;
+            const unsigned x = 1u << (chunk * 2 * dy), x2 = x << dy;
+            const int lc1 = chunk * 2 * dy, lc2 = lc1 + dy;
+            for (int yy = 0; yy < 8; yy++) {
+                const uint8_t *vm_ = msk[pl][1][yy];
+                const unsigned vm = vm_[0] | vm_[1] | vm_[2], vm3 = vm_[3];
+                const int lr = pl ? yy & ~1 : yy;
+                int wd = 0, L = 0;
+                if (!row0 || yy) {
+                    if (!half) {
+                        if (vm & x) { wd = (vm_[0] & x) ? 16 : (vm_[1] & x) ? 8 : 4; L = lvl[lr * 8 + lc1]; }
+                    } else if (vm & x) {
+                        if (vm_[0] & x) { if (vm_[0] & x2) { wd = 16; L = lvl[lr * 8 + lc1]; } }
+                        else if (vm & x2) { wd = (vm_[1] & x2) ? 8 : 4; L = lvl[lr * 8 + lc2]; }
+                    } else if (vm & x2) { wd = (vm_[1] & x2) ? 8 : 4; L = lvl[lr * 8 + lc2]; }
+                }
+                if (pl) { prog[LFP_CR + band * 8 + yy] = lf_byte(wd, L); continue; }
+                prog[LFP_YR + band * 16 + yy * 2] = lf_byte(wd, L);
+                if (!half ? (vm3 & x) : (vm3 & x2))
+                    prog[LFP_YR + band * 16 + yy * 2 + 1] = (uint8_t) (0x40 | lvl[yy * 8 + (half ? lc2 : lc1)]);
+            }
+        }
+    }
+}
+
 // Build jobs/levels/LF/MC for one frame. Appends to stg. Returns 0 or error.
 static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std::vector<uint32_t>> &pred_steps,
                        std::vector<std::vector<uint32_t>> &lf_steps)
@@ -474,6 +540,9 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
         LFRec lf;
         memset(&lf, 0, sizeof(lf));
         lf.frame = fb.frame_idx; lf.sbx = sbx; lf.sby = sby;
+        uint8_t lf_level[64], lf_mask[2][2][8][4];           // VP9Filter of the SB (vp9dec.h:83-87)
+        memset(lf_level, 0, sizeof(lf_level));
+        memset(lf_mask, 0, sizeof(lf_mask));
         pj.clear();
         memset(lmap, -1, sizeof(lmap));
         memset(jmap, -1, sizeof(jmap));
@@ -676,9 +745,9 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
                 const int x_end = std::min(cols - b->col, bw8), y_end = std::min(rows - b->row, bh8);
                 const int skip_inter = !b->intra && b->skip, col7 = b->col & 7, row7 = b->row & 7;
                 for (int yy = 0; yy < bh8; yy++)
-                    for (int xx = 0; xx < bw8; xx++) lf.level[(row7 + yy) * 8 + col7 + xx] = (uint8_t) lvl;
-                lf_mask_edges(lf.mask[0], 0, 0, row7, col7, x_end, y_end, 0, 0, b->tx, skip_inter);
-                lf_mask_edges(lf.mask[1], ss_h, ss_v, row7, col7, x_end, y_end,
+                    for (int xx = 0; xx < bw8; xx++) lf_level[(row7 + yy) * 8 + col7 + xx] = (uint8_t) lvl;
+                lf_mask_edges(lf_mask[0], 0, 0, row7, col7, x_end, y_end, 0, 0, b->tx, skip_inter);
+                lf_mask_edges(lf_mask[1], ss_h, ss_v, row7, col7, x_end, y_end,
                               (cols & 1) && b->col + bw8 >= cols ? cols & 7 : 0,
                               (rows & 1) && b->row + bh8 >= rows ? rows & 7 : 0, b->uvtx, skip_inter);
             }
@@ -713,6 +782,7 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
         }
         if (f->filter_level) {
             uint32_t li = (uint32_t) s.lfs.size();
+            lf_program(lf_level, lf_mask, sbx == 0, sby == 0, lf.prog);
             s.lfs.push_back(lf);
             int d = sbx + 2 * sby;
             if ((int) lf_steps.size() <= d) lf_steps.resize(d + 1);

@@ -105,12 +105,21 @@ typedef struct WGRec {
 #define MAX_SB_JOBS 384
 #define PJ_SLOT(j) ((j).a >> 30)
 
-/* Loop-filter data of one SB: VP9Filter (vp9dec.h:83-87) + position. */
+/* Loop-filter program of one SB: the edge decisions of filter_plane_cols / _rows
+ * (vp9lpf.c:31-181), resolved on the host from the SB's VP9Filter levels and masks
+ * (vp9dec.h:83-87, vp9block.c:1438-1452). One byte per (band, edge): band = pixel row
+ * >> 3 for column edges, pixel column >> 3 for row edges (the decisions are uniform
+ * over 8 lines); main edge = width code (1: 4, 2: 8, 3: 16) << 6 | level, 0 = none;
+ * luma inner 4-wide edge = 0x40 | level, 0 = none. */
+#define LFP_YC 0                 /* luma column edges: band * 16 + edge * 2 + {main, inner} */
+#define LFP_YR 128               /* luma row edges:    band * 16 + edge * 2 + {main, inner} */
+#define LFP_CC 256               /* chroma column edges: band * 8 + edge (U and V alike)    */
+#define LFP_CR 288               /* chroma row edges:    band * 8 + edge                    */
+#define LF_PROG_BYTES 320
 typedef struct LFRec {
     uint32_t frame;
     uint16_t sbx, sby;
-    uint8_t  level[64];
-    uint8_t  mask[2][2][8][4];
+    uint8_t  prog[LF_PROG_BYTES];
 } LFRec;
 
 /* One motion-compensated rectangle of one plane (<= 64 x 64) and its references. Per
