@@ -40,7 +40,7 @@ CONFIGS = {
 W, H, BPP, LOG2_TILE_COLS = 3840, 2160, 8, 2
 CONFIG_INDEX = 2               # C3
 SEED0 = 0x56503900 + CONFIG_INDEX
-TRAFFIC_PROFILE = "r01d"       # rocprofv3 PMC pass of C3 (tools/profile.sh)
+TRAFFIC_PROFILE = "r01e"       # rocprofv3 PMC pass of C3 (tools/profile.sh)
 
 
 def frame_seed(rank, i, config_index=CONFIG_INDEX):
