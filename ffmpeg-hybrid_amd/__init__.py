@@ -340,7 +340,7 @@ class Decoder:
 
 PLAN_STAT_NAMES = ("sbs", "passes", "pjobs", "rjobs", "jobs_4x4", "jobs_8x8", "jobs_16x16",
                    "jobs_32x32", "lane_use", "max_passes_sb", "lf_records", "mc_units", "pred_steps",
-                   "lf_steps", "levels")
+                   "lf_steps", "levels", "pass_rows")
 
 
 def plan_stats(frame):

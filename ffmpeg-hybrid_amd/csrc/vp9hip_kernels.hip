@@ -29,6 +29,14 @@
 // ------------------------------------------------------------------ helpers
 DEV int clipbd(int v, int bd) { int m = (1 << bd) - 1; return v < 0 ? 0 : (v > m ? m : v); }
 
+// clamp to [0, mx] in one v_med3_i32 (mx wave-uniform)
+DEV int med3_0(int v, int mx)
+{
+    int r;
+    asm("v_med3_i32 %0, %1, 0, %2" : "=v"(r) : "v"(v), "s"(mx));
+    return r;
+}
+
 DEV void wave_sync()
 {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -733,7 +741,8 @@ DEV void pred_pass(uint32_t w, int lane, PIX *tile, uint16_t *eb, int bd, const 
         if (ts == 0) e[n + 5 + li] = (uint16_t) tr;
         e[n] = (uint16_t) tl;                  // every lane of the group writes the same value
     }
-    // DC sums over the job's n lanes (only when the pass holds a DC/LEFT_DC/TOP_DC job)
+    // DC family: sums over the job's n lanes (only when the pass holds a DC / LEFT_DC /
+    // TOP_DC job), the value stored at edge index 2n + 7 for the formula table's copy
     int dc = ms == 12 ? base : ms == 13 ? base - 1 : base + 1;
     if (__any(act && ms >= 9 && ms <= 11)) {
         int sl = lv, st = tv;
@@ -745,24 +754,24 @@ DEV void pred_pass(uint32_t w, int lane, PIX *tile, uint16_t *eb, int bd, const 
         const int d9 = (sl + st + n) >> (ts + 3), d10 = (sl + (n >> 1)) >> (ts + 2), d11 = (st + (n >> 1)) >> (ts + 2);
         dc = ms == 9 ? d9 : ms == 10 ? d10 : ms == 11 ? d11 : dc;
     }
+    if (act && ms >= 9 && li == 0 && !(dbg & 16)) e[2 * n + 7] = (uint16_t) dc;
     wave_sync();
     if (act && !(dbg & 8)) {
         const int mx = (1 << bd) - 1;
         const int hr = PJ_RES(jb);
+        const char *e8 = (const char *) e;
 #pragma unroll
         for (int y = 0; y < MAXN; y++) {
             if (MAXN > 4 && y >= n) continue;
             const uint32_t fw = f[y];
-            const int a = e[fw & 127], b = e[(fw >> 7) & 127], c = e[(fw >> 14) & 127];
-            const int wb = (fw >> 21) & 3, s = (fw >> 25) & 3;
-            const int wc = __builtin_amdgcn_sbfe((int) fw, 23, 2);
-            int v = (a + wb * b + wc * c + ((1 << s) >> 1)) >> s;
-            v = min(max(v, 0), mx);
-            v = (fw >> 27) ? dc : v;
+            const int a = *(const uint16_t *) (e8 + (fw & 255)), b = *(const uint16_t *) (e8 + ((fw >> 8) & 255)),
+                      c = *(const uint16_t *) (e8 + ((fw >> 16) & 255));
+            const int wb = (fw >> 24) & 3, s = (fw >> 28) & 3, rnd = fw >> 30;
+            const int wc = __builtin_amdgcn_sbfe((int) fw, 26, 2);
+            int v = med3_0(((a + rnd) + wb * b + wc * c) >> s, mx);
             const uint32_t rw = y < 8 ? pr_word(ps, y >> 1) : rx[y < 8 ? 0 : (y >> 1) - 4];
             const int r = (int) (int16_t) (rw >> ((y & 1) * 16));
-            v += hr ? r : 0;
-            v = min(max(v, 0), mx);
+            v = med3_0(v + (hr ? r : 0), mx);
             o[y * tpch + li] = (PIX) v;
         }
     }

@@ -181,12 +181,15 @@ extern "C" void vp9hip_close(vp9hip_ctx *c)
 // 4x4 top-right. Kinds: copy, avg2 (a+b+1)>>1, avg3 (a+2b+c+2)>>2, avg31 (a+3b+2)>>2,
 // tm clip(a+b-c), dc.
 enum { PF_COPY, PF_AVG2, PF_AVG3, PF_AVG31, PF_TM, PF_DC };
+// Formula word: byte offsets (2 * index) of the three edge samples a, b, c in bits 0-23,
+// then wb (2 bits), wc (2-bit two's complement, 3 = -1), shift s, rounding (1 << s) >> 1:
+// pixel = (a + rnd + wb * b + wc * c) >> s. DC predictors copy edge index 2n + 7, where
+// the kernel stores the job's DC value.
 static uint32_t pf_enc(int kind, int i0 = 0, int i1 = 0, int i2 = 0)
 {
-    // wc is a 2-bit two's complement weight (3 = -1)
     static const int wb[6] = { 0, 1, 2, 3, 1, 0 }, wc[6] = { 0, 0, 1, 0, 3, 0 }, sh[6] = { 0, 1, 2, 2, 0, 0 };
-    return (uint32_t) i0 | (uint32_t) i1 << 7 | (uint32_t) i2 << 14 | (uint32_t) wb[kind] << 21 |
-           (uint32_t) wc[kind] << 23 | (uint32_t) sh[kind] << 25 | (uint32_t) (kind == PF_DC) << 27;
+    return (uint32_t) (2 * i0) | (uint32_t) (2 * i1) << 8 | (uint32_t) (2 * i2) << 16 | (uint32_t) wb[kind] << 24 |
+           (uint32_t) wc[kind] << 26 | (uint32_t) sh[kind] << 28 | (uint32_t) ((1 << sh[kind]) >> 1) << 30;
 }
 static uint32_t pix_formula(int slot, int n, int x, int y)
 {
@@ -232,7 +235,7 @@ static uint32_t pix_formula(int slot, int n, int x, int y)
         if (!(m & 1)) return pf_enc(PF_AVG2, L(i), L(i + 1));
         return i < n - 2 ? pf_enc(PF_AVG3, L(i), L(i + 1), L(i + 2)) : pf_enc(PF_AVG31, L(n - 2), L(n - 1));
     }
-    default: return pf_enc(PF_DC);
+    default: return pf_enc(PF_COPY, 2 * n + 7);                                  // DC family
     }
 }
 static int upload_ptab(vp9hip_ctx *c)
@@ -1337,7 +1340,7 @@ extern "C" int vp9hip_abi_version(void) { return VP9HIP_ABI_VERSION; }
 // in one SB, 10 LF records, 11 MC units, 12 intra wavefront steps, 13 LF wavefront steps.
 extern "C" int vp9hip_plan_stats(const vp9h_frame *f, double *out, int cap)
 {
-    if (!f || !out || cap < 15) return VP9HIP_EINVAL;
+    if (!f || !out || cap < 16) return VP9HIP_EINVAL;
     if (f->ss_h != 1 || f->ss_v != 1) return VP9HIP_ENOSYS;
     init_nz();
     Staged s;
@@ -1359,7 +1362,7 @@ extern "C" int vp9hip_plan_stats(const vp9h_frame *f, double *out, int cap)
             r = merge_mixed(s, sbi);
             if (r) return r;
         }
-    for (int i = 0; i < 15; i++) out[i] = 0;
+    for (int i = 0; i < 16; i++) out[i] = 0;
     out[0] = (double) s.sbs.size();
     out[1] = (double) s.passes.size();
     out[2] = (double) s.pjobs.size();
@@ -1371,6 +1374,7 @@ extern "C" int vp9hip_plan_stats(const vp9h_frame *f, double *out, int cap)
         const int c4 = (w >> 9) & 31, c8 = (w >> 5) & 15, c16 = (w >> 2) & 7, c32 = w & 3;
         out[4] += c4; out[5] += c8; out[6] += c16; out[7] += c32;      // jobs per tx size
         lanes += 4 * c4 + 8 * c8 + 16 * c16 + 32 * c32;
+        out[15] += c32 ? 32 : c16 ? 16 : c8 ? 8 : 4;                     // pixel rows the pass loops over
     }
     out[8] = s.passes.empty() ? 0 : lanes / (64.0 * s.passes.size());
     for (auto &wg : s.wgs) out[9] = std::max(out[9], (double) wg.npass);

@@ -191,10 +191,11 @@ int  vp9hip_set_timing(vp9hip_ctx *ctx, int on);
  * per kernel class in vp9hip_last_timing order. Returns count. */
 int  vp9hip_alg_bytes(vp9hip_ctx *ctx, double *bytes, int cap);
 
-/* Host-only planning statistics of one packet (no device needed), 15 values:
+/* Host-only planning statistics of one packet (no device needed), 16 values:
  * SBs with intra work, passes, intra jobs, residual jobs, intra jobs per tx size (4),
  * lane use, max passes per SB, LF records, MC units, intra / LF wavefront steps,
- * intra dependency levels (summed over SBs: the lower bound of the passes). */
+ * intra dependency levels (summed over SBs: the lower bound of the passes), pixel rows
+ * the passes loop over (each pass: its largest job size). */
 int  vp9hip_plan_stats(const vp9h_frame *pkt, double *out, int cap);
 
 int  vp9hip_abi_version(void);
