@@ -84,7 +84,7 @@ ABI_SYMBOLS = ["vp9hip_open", "vp9hip_close", "vp9hip_configure", "vp9hip_submit
                "vp9hip_upload_frame", "vp9hip_flush", "vp9hip_last_timing", "vp9hip_set_timing",
                "vp9hip_alg_bytes", "vp9hip_plan_stats", "vp9hip_abi_version",
                "vp9hip_stage_batch_tiles", "vp9hip_batch_phases", "vp9hip_phase_frames", "vp9hip_run_phase",
-               "vp9hip_stripe",
+               "vp9hip_stripe", "vp9hip_frame_device",
                "vp9hip_synth_defaults", "vp9hip_synth_frame", "vp9hip_synth_free"]
 
 
@@ -112,6 +112,9 @@ def lib():
     L.vp9hip_run_phase.argtypes = [vp, ctypes.c_int, ctypes.c_int]
     L.vp9hip_stripe.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
     L.vp9hip_stripe.restype = ctypes.c_int64
+    L.vp9hip_frame_device.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_ssize_t),
+                                       ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                                       ctypes.POINTER(ctypes.c_void_p)]
     L.vp9hip_run_batch.argtypes = [vp]
     L.vp9hip_sync.argtypes = [vp]
     L.vp9hip_download_frame.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
@@ -289,6 +292,34 @@ class Device:
         ptrs, ls = self._plane_args(planes)
         _check("vp9hip_download_frame", lib().vp9hip_download_frame(self._c, buf, ptrs, ls))
         return planes
+
+    def frame_device(self, buf):
+        """Device planes of buffer `buf` without a copy: ([ptr] * 3, [pitch bytes] * 3,
+        (width, height), hipStream_t handle) -- vp9hip_frame_device."""
+        ptrs = (ctypes.c_void_p * 3)()
+        ls = (ctypes.c_ssize_t * 3)()
+        w, h, st = ctypes.c_int(), ctypes.c_int(), ctypes.c_void_p()
+        _check("vp9hip_frame_device", lib().vp9hip_frame_device(self._c, buf, ptrs, ls, ctypes.byref(w), ctypes.byref(h),
+                                                                ctypes.byref(st)))
+        return list(ptrs), list(ls), (w.value, h.value), st.value
+
+    def frame_tensors(self, buf, device=None):
+        """Zero-copy torch views (uint8 / int16 storage of the u16 samples) of buffer
+        `buf`'s visible planes, via __cuda_array_interface__. Call sync() first (or order
+        consumers after the context's stream)."""
+        import torch
+        ptrs, ls, (w, h), _ = self.frame_device(buf)
+        bpp = 1 if self.bpp == 8 else 2
+        out = []
+        for p in range(3):
+            pw = w if p == 0 else (w + self.ss_h) >> self.ss_h
+            ph = h if p == 0 else (h + self.ss_v) >> self.ss_v
+
+            class _View:
+                __cuda_array_interface__ = {"shape": (ph, pw), "typestr": "|u1" if bpp == 1 else "<i2",
+                                            "data": (ptrs[p], False), "strides": (ls[p], bpp), "version": 2}
+            out.append(torch.as_tensor(_View(), device=device or "cuda"))
+        return out
 
     def upload(self, buf, planes):
         planes = [np.ascontiguousarray(p) for p in planes]

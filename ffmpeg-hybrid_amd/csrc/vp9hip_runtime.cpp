@@ -1295,6 +1295,26 @@ extern "C" int vp9hip_upload_frame(vp9hip_ctx *c, int buf, const uint8_t *const 
     return 0;
 }
 
+// Zero-copy export of a decoded frame: device pointers of the three
+// planes, their pitches in bytes, the visible size, and the context's stream, which
+// orders every kernel that writes the buffer. A consumer that enqueues on that stream
+// (or waits for vp9hip_sync) reads the finished frame without a D2H copy. The pointers
+// stay valid until vp9hip_configure / vp9hip_close; the content until the buffer is
+// written again.
+extern "C" int vp9hip_frame_device(vp9hip_ctx *c, int buf, void *planes[3], ptrdiff_t linesize[3], int *width,
+                                   int *height, void **stream)
+{
+    if (!c || buf < 0 || buf >= (int) c->bufs.size() || !planes || !linesize) return VP9HIP_EINVAL;
+    for (int p = 0; p < 3; p++) {
+        planes[p] = c->bufs[buf] + c->plane_off[p];
+        linesize[p] = (ptrdiff_t) c->pitch[p ? 1 : 0] * c->bypp;
+    }
+    if (width) *width = c->buf_wh[buf].first;
+    if (height) *height = c->buf_wh[buf].second;
+    if (stream) *stream = (void *) c->st;
+    return 0;
+}
+
 extern "C" int vp9hip_flush(vp9hip_ctx *c)
 {
     if (!c) return VP9HIP_EINVAL;

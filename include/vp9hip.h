@@ -171,6 +171,17 @@ int  vp9hip_sync(vp9hip_ctx *ctx);
 /* Copy device buffer `buf` into host planes (linesize in bytes). Synchronous. */
 int  vp9hip_download_frame(vp9hip_ctx *ctx, int buf, uint8_t *const planes[3],
                            const ptrdiff_t linesize[3]);
+/*
+ * Zero-copy export of device buffer `buf` (replaces the D2H of vp9hip_download_frame for
+ * consumers on the GPU; the hwcontext frame export of SURVEY 8f rank 2,
+ * hwaccel_internal.h:146, libavutil/hwcontext.h:26-44): device pointers and byte
+ * pitches of the three planes, the visible size, and the context's hipStream_t, which
+ * orders every write of the buffer. Work enqueued on that stream, or after
+ * vp9hip_sync, sees the finished frame. Pointers stay valid until vp9hip_configure /
+ * vp9hip_close.
+ */
+int  vp9hip_frame_device(vp9hip_ctx *ctx, int buf, void *planes[3], ptrdiff_t linesize[3],
+                         int *width, int *height, void **stream);
 /* Upload host planes into device buffer `buf` (test hook for reference frames). */
 int  vp9hip_upload_frame(vp9hip_ctx *ctx, int buf, const uint8_t *const planes[3],
                          const ptrdiff_t linesize[3]);

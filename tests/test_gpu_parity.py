@@ -179,3 +179,24 @@ def test_scaled_reference_parity(v9, orc, gpu, rs, fs, bpp, kw):
         out = v9.alloc_planes(w, h, bpp)
         orc.decode_frame(f.pkt, out, [kref, kref, kref], [(rw, rh)] * 3)
         _cmp(v9, gpu.download(1), out, w, h, "scaled ref %dx%d -> %dx%d@%d %s seed %d" % (rw, rh, w, h, bpp, kw, seed))
+
+
+@pytest.mark.parametrize("bpp", [8, 10])
+def test_zero_copy_export_matches_download(v9, orc, gpu, bpp):
+    """vp9hip_frame_device: torch views of the device planes hold the
+    oracle's frame, at the buffer's own addresses (no copy)."""
+    import torch
+    w, h = 200, 130
+    f = v9.SynthFrame(v9.synth_params(w, h, bpp, seed=77))
+    gpu.configure(w, h, bpp, nbufs=2)
+    gpu.submit(f, 1)
+    gpu.sync()
+    ptrs, ls, (vw, vh), stream = gpu.frame_device(1)
+    assert (vw, vh) == (w, h) and stream
+    views = gpu.frame_tensors(1, device="cuda:0")
+    assert [t.data_ptr() for t in views] == ptrs
+    ref = v9.alloc_planes(w, h, bpp)
+    orc.decode_frame(f.pkt, ref)
+    for t, r in zip(views, v9.visible(ref, w, h)):
+        assert t.shape == r.shape
+        assert np.array_equal(t.cpu().numpy().astype(r.dtype), r)
