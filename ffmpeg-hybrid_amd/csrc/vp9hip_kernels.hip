@@ -895,24 +895,13 @@ __global__ __launch_bounds__(64) void k_pred(const uint32_t *__restrict__ list, 
 }
 
 // 8-pixel chunk <-> 8 uint16 of the LF tile (tile rows are 4-byte aligned)
+// 8 pixels between a global chunk and an LDS tile row of PIX (rows dword-aligned)
 template <typename PIX> struct Chunk8;
 template <> struct Chunk8<uint8_t> {
     typedef uint2 T;
     static DEV T zero() { return make_uint2(0, 0); }
-    static DEV void to_lds(T v, uint16_t *t)
-    {
-        uint32_t *d = (uint32_t *) t;
-        d[0] = (v.x & 0xff) | ((v.x & 0xff00) << 8);
-        d[1] = ((v.x >> 16) & 0xff) | ((v.x >> 8) & 0xff0000);
-        d[2] = (v.y & 0xff) | ((v.y & 0xff00) << 8);
-        d[3] = ((v.y >> 16) & 0xff) | ((v.y >> 8) & 0xff0000);
-    }
-    static DEV T from_lds(const uint16_t *t)
-    {
-        const uint32_t *s = (const uint32_t *) t;
-        return make_uint2((s[0] & 0xff) | ((s[0] >> 8) & 0xff00) | ((s[1] & 0xff) << 16) | ((s[1] & 0xff0000) << 8),
-                          (s[2] & 0xff) | ((s[2] >> 8) & 0xff00) | ((s[3] & 0xff) << 16) | ((s[3] & 0xff0000) << 8));
-    }
+    static DEV void to_lds(T v, uint8_t *t) { uint32_t *d = (uint32_t *) t; d[0] = v.x; d[1] = v.y; }
+    static DEV T from_lds(const uint8_t *t) { const uint32_t *s = (const uint32_t *) t; return make_uint2(s[0], s[1]); }
 };
 template <> struct Chunk8<uint16_t> {
     typedef uint4 T;
@@ -1011,15 +1000,37 @@ DEV void lf_reg(int (&px)[NPX], int code, uint32_t eih, int bd)
     }
 }
 
-#define FLP 74           // luma LF tile pitch (72 used)
-#define FCP 42           // chroma LF tile pitch (40 used)
+// LF tile pitches in pixels: 72 / 40 used, rows dword-aligned with an odd dword count
+// (lanes of the column pass read dword i of consecutive rows: no bank conflicts)
+template <typename PIX> struct LfP {
+    static constexpr int YP = sizeof(PIX) == 1 ? 76 : 74, UVP = sizeof(PIX) == 1 ? 44 : 42;
+    static constexpr int PPW = 4 / sizeof(PIX);     // pixels per dword
+};
+template <typename PIX, int N> DEV void lf_unpack(const uint32_t *w, int (&px)[N], int i0, int i1, int o)
+{
+#pragma unroll
+    for (int i = i0; i < i1; i++)
+#pragma unroll
+        for (int j = 0; j < LfP<PIX>::PPW; j++)
+            px[o + (i - i0) * LfP<PIX>::PPW + j] = (w[i] >> (8 * sizeof(PIX) * j)) & ((1u << (8 * sizeof(PIX))) - 1);
+}
+template <typename PIX, int N> DEV void lf_pack(uint32_t *w, const int (&px)[N], int i0, int i1, int o)
+{
+#pragma unroll
+    for (int i = i0; i < i1; i++) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int j = 0; j < LfP<PIX>::PPW; j++) v |= (uint32_t) px[o + (i - i0) * LfP<PIX>::PPW + j] << (8 * sizeof(PIX) * j);
+        w[i] = v;
+    }
+}
 
 // One SB of loop filter by NT threads (128: two waves, luma / chroma in parallel; 64: one
 // wave, luma then chroma). Same arithmetic and edge order either way (planes are
 // independent, vp9lpf.c:183-230).
-struct LfLds {
-    uint16_t lt[72 * FLP];
-    uint16_t ct[2][40 * FCP];
+template <typename PIX> struct LfLds {
+    PIX lt[72 * LfP<PIX>::YP];
+    PIX ct[2][40 * LfP<PIX>::UVP];
     uint32_t prog[LF_PROG_BYTES / 4];     // the SB's edge decisions (LFRec.prog)
     uint32_t lut[64];                     // level -> E | I << 12 | H << 22
 };
@@ -1036,11 +1047,12 @@ DEV uint32_t lf_eih(int L, int sharp, int bd)
 }
 
 template <typename PIX, int NT>
-DEV void lf_sb(const LFRec &rec, const FrameDesc *__restrict__ frames, LfLds &S, int lane, int dbg)
+DEV void lf_sb(const LFRec &rec, const FrameDesc *__restrict__ frames, LfLds<PIX> &S, int lane, int dbg)
 {
 #define LF_SYNC() do { if (NT == 64) wave_sync(); else __syncthreads(); } while (0)
-    uint16_t *lt = S.lt;
-    uint16_t (*ct)[40 * FCP] = S.ct;
+    constexpr int FLP = LfP<PIX>::YP, FCP = LfP<PIX>::UVP, PPW = LfP<PIX>::PPW;
+    PIX *lt = S.lt;
+    PIX (*ct)[40 * FCP] = S.ct;
     const uint32_t *lut = S.lut;
     const FrameDesc &fd = frames[rec.frame];
     const int bd = fd.bd, sharp = fd.sharp;
@@ -1070,7 +1082,7 @@ DEV void lf_sb(const LFRec &rec, const FrameDesc *__restrict__ frames, LfLds &S,
         int p, r, k;
         lf_chunk(ci, p, r, k);
         if (ci < 1048) {
-            uint16_t *t = p ? ct[p - 1] + r * FCP : lt + r * FLP;
+            PIX *t = p ? ct[p - 1] + r * FCP : lt + r * FLP;
             Chunk8<PIX>::to_lds(v[u], t + 8 * k);
         }
     }
@@ -1082,37 +1094,34 @@ DEV void lf_sb(const LFRec &rec, const FrameDesc *__restrict__ frames, LfLds &S,
     for (int tid = lane; tid < 128; tid += NT) {
     if (tid < 64) {
         const int r = tid;
-        uint16_t *rowp = lt + (r + 8) * FLP;
-        int px[72];
-#pragma unroll
-        for (int i = 0; i < 36; i++) {
-            const uint32_t w = ((const uint32_t *) rowp)[i];
-            px[2 * i] = w & 0xffff; px[2 * i + 1] = w >> 16;
-        }
+        uint32_t *rowp = (uint32_t *) (lt + (r + 8) * FLP);      // 72 pixels: 72 / PPW dwords
         // edge bytes of this row's band: (main, inner) for edges 0..7
         const uint32_t *pw = S.prog + (LFP_YC + (r >> 3) * 16) / 4;
         const uint32_t pw0 = pw[0], pw1 = pw[1], pw2 = pw[2], pw3 = pw[3];
-#define LF_COL_EDGE(k)                                                                                   \
+        // the row in two register halves (an edge touches 8 pixels either side): x = -8..31
+        // for edges 0-3, then x = 24..63 for edges 4-7 (x = 24..31 carried over)
+        int px[40];
+        lf_unpack<PIX>(rowp, px, 0, 40 / PPW, 0);
+#define LF_COL_EDGE(k, C0)                                                                               \
         {                                                                                                \
             const uint32_t ww = (k) < 2 ? pw0 : (k) < 4 ? pw1 : (k) < 6 ? pw2 : pw3;                     \
             const uint32_t m = (ww >> (16 * ((k) & 1))) & 255, in = (ww >> (16 * ((k) & 1) + 8)) & 255;  \
-            if (m >> 6) lf_reg<8 * (k) + 8>(px, m >> 6, lut[m & 63], bd);                                \
-            if (in) lf_reg<8 * (k) + 12>(px, 1, lut[in & 63], bd);                                       \
+            if (m >> 6) lf_reg<8 * (k) + 8 - (C0)>(px, m >> 6, lut[m & 63], bd);                         \
+            if (in) lf_reg<8 * (k) + 12 - (C0)>(px, 1, lut[in & 63], bd);                                \
         }
-        LF_COL_EDGE(0) LF_COL_EDGE(1) LF_COL_EDGE(2) LF_COL_EDGE(3)
-        LF_COL_EDGE(4) LF_COL_EDGE(5) LF_COL_EDGE(6) LF_COL_EDGE(7)
-#undef LF_COL_EDGE
+        LF_COL_EDGE(0, 0) LF_COL_EDGE(1, 0) LF_COL_EDGE(2, 0) LF_COL_EDGE(3, 0)
+        lf_pack<PIX>(rowp, px, 0, 32 / PPW, 0);
 #pragma unroll
-        for (int i = 0; i < 36; i++) ((uint32_t *) rowp)[i] = (uint32_t) px[2 * i] | (uint32_t) px[2 * i + 1] << 16;
+        for (int i = 0; i < 8; i++) px[i] = px[32 + i];
+        lf_unpack<PIX>(rowp, px, 40 / PPW, 72 / PPW, 8);
+        LF_COL_EDGE(4, 32) LF_COL_EDGE(5, 32) LF_COL_EDGE(6, 32) LF_COL_EDGE(7, 32)
+#undef LF_COL_EDGE
+        lf_pack<PIX>(rowp, px, 32 / PPW, 72 / PPW, 0);
     } else {
         const int p = 1 + ((tid - 64) >> 5), r = (tid - 64) & 31;
-        uint16_t *rowp = ct[p - 1] + (r + 8) * FCP;
+        uint32_t *rowp = (uint32_t *) (ct[p - 1] + (r + 8) * FCP);
         int px[48];
-#pragma unroll
-        for (int i = 0; i < 20; i++) {
-            const uint32_t w = ((const uint32_t *) rowp)[i];
-            px[2 * i] = w & 0xffff; px[2 * i + 1] = w >> 16;
-        }
+        lf_unpack<PIX>(rowp, px, 0, 40 / PPW, 0);
 #pragma unroll
         for (int i = 40; i < 48; i++) px[i] = 0;
         const uint32_t *pw = S.prog + (LFP_CC + (r >> 3) * 8) / 4;
@@ -1125,8 +1134,7 @@ DEV void lf_sb(const LFRec &rec, const FrameDesc *__restrict__ frames, LfLds &S,
         LF_COL_EDGE_UV(0) LF_COL_EDGE_UV(1) LF_COL_EDGE_UV(2) LF_COL_EDGE_UV(3)
         LF_COL_EDGE_UV(4) LF_COL_EDGE_UV(5) LF_COL_EDGE_UV(6) LF_COL_EDGE_UV(7)
 #undef LF_COL_EDGE_UV
-#pragma unroll
-        for (int i = 0; i < 20; i++) ((uint32_t *) rowp)[i] = (uint32_t) px[2 * i] | (uint32_t) px[2 * i + 1] << 16;
+        lf_pack<PIX>(rowp, px, 0, 40 / PPW, 0);
     }
     }
     LF_SYNC();
@@ -1135,27 +1143,33 @@ DEV void lf_sb(const LFRec &rec, const FrameDesc *__restrict__ frames, LfLds &S,
     for (int tid = lane; tid < 128; tid += NT) {
     if (tid < 64) {
         const int c = tid;
-        uint16_t *colp = lt + 8 + c;
-        int px[72];
+        PIX *colp = lt + 8 + c;
+        int px[40];                    // rows -8..31, then 24..63 (as the column pass)
 #pragma unroll
-        for (int i = 0; i < 72; i++) px[i] = colp[i * FLP];
+        for (int i = 0; i < 40; i++) px[i] = colp[i * FLP];
         const uint32_t *pw = S.prog + (LFP_YR + (c >> 3) * 16) / 4;
         const uint32_t pw0 = pw[0], pw1 = pw[1], pw2 = pw[2], pw3 = pw[3];
-#define LF_ROW_EDGE(yy)                                                                                  \
+#define LF_ROW_EDGE(yy, C0)                                                                              \
         {                                                                                                \
             const uint32_t ww = (yy) < 2 ? pw0 : (yy) < 4 ? pw1 : (yy) < 6 ? pw2 : pw3;                  \
             const uint32_t m = (ww >> (16 * ((yy) & 1))) & 255, in = (ww >> (16 * ((yy) & 1) + 8)) & 255; \
-            if (m >> 6) lf_reg<8 * (yy) + 8>(px, m >> 6, lut[m & 63], bd);                               \
-            if (in) lf_reg<8 * (yy) + 12>(px, 1, lut[in & 63], bd);                                      \
+            if (m >> 6) lf_reg<8 * (yy) + 8 - (C0)>(px, m >> 6, lut[m & 63], bd);                        \
+            if (in) lf_reg<8 * (yy) + 12 - (C0)>(px, 1, lut[in & 63], bd);                               \
         }
-        LF_ROW_EDGE(0) LF_ROW_EDGE(1) LF_ROW_EDGE(2) LF_ROW_EDGE(3)
-        LF_ROW_EDGE(4) LF_ROW_EDGE(5) LF_ROW_EDGE(6) LF_ROW_EDGE(7)
+        LF_ROW_EDGE(0, 0) LF_ROW_EDGE(1, 0) LF_ROW_EDGE(2, 0) LF_ROW_EDGE(3, 0)
+#pragma unroll
+        for (int i = 1; i < 32; i++) colp[i * FLP] = (PIX) px[i];
+#pragma unroll
+        for (int i = 0; i < 8; i++) px[i] = px[32 + i];
+#pragma unroll
+        for (int i = 8; i < 40; i++) px[i] = colp[(32 + i) * FLP];
+        LF_ROW_EDGE(4, 32) LF_ROW_EDGE(5, 32) LF_ROW_EDGE(6, 32) LF_ROW_EDGE(7, 32)
 #undef LF_ROW_EDGE
 #pragma unroll
-        for (int i = 1; i < 72; i++) colp[i * FLP] = (uint16_t) px[i];
+        for (int i = 0; i < 40; i++) colp[(32 + i) * FLP] = (PIX) px[i];
     } else {
         const int p = 1 + ((tid - 64) >> 5), c = (tid - 64) & 31;
-        uint16_t *colp = ct[p - 1] + 8 + c;
+        PIX *colp = ct[p - 1] + 8 + c;
         int px[48];
 #pragma unroll
         for (int i = 0; i < 40; i++) px[i] = colp[i * FCP];
@@ -1172,7 +1186,7 @@ DEV void lf_sb(const LFRec &rec, const FrameDesc *__restrict__ frames, LfLds &S,
         LF_ROW_EDGE_UV(4) LF_ROW_EDGE_UV(5) LF_ROW_EDGE_UV(6) LF_ROW_EDGE_UV(7)
 #undef LF_ROW_EDGE_UV
 #pragma unroll
-        for (int i = 1; i < 40; i++) colp[i * FCP] = (uint16_t) px[i];
+        for (int i = 1; i < 40; i++) colp[i * FCP] = (PIX) px[i];
     }
     }
     LF_SYNC();
@@ -1187,7 +1201,7 @@ DEV void lf_sb(const LFRec &rec, const FrameDesc *__restrict__ frames, LfLds &S,
         lf_chunk(ci, p, r, k);
         const int gx = (p ? sbx * 32 : sbx * 64) - 8 + 8 * k, gy = (p ? sby * 32 : sby * 64) - 8 + r;
         if (!(dbg & 2) && ci < 1048 && gx >= 0 && gy >= 0 && (r >= 8 || k > 0)) {
-            const uint16_t *t = p ? ct[p - 1] + r * FCP : lt + r * FLP;
+            const PIX *t = p ? ct[p - 1] + r * FCP : lt + r * FLP;
             *(CT *) ((PIX *) fd.plane[p] + (size_t) gy * fd.pitch[p ? 1 : 0] + gx) = Chunk8<PIX>::from_lds(t + 8 * k);
         }
     }
@@ -1198,7 +1212,7 @@ template <typename PIX>
 __global__ __launch_bounds__(128) void k_lf(const uint32_t *__restrict__ list, const LFRec *__restrict__ recs,
                                             const FrameDesc *__restrict__ frames, int dbg)
 {
-    __shared__ LfLds S;
+    __shared__ LfLds<PIX> S;
     lf_sb<PIX, 128>(recs[list[blockIdx.x]], frames, S, threadIdx.x, dbg);
 }
 
