@@ -570,6 +570,9 @@ __global__ __launch_bounds__(64 * RWAVES) void k_resid(const RJob *__restrict__ 
 // (vp9dsp_template.c:28-1106 restated per pixel), then + residual from k_resid, clip.
 // A tile's row 0 / column 0 hold the pixels above / left of the SB; pixel (x, y) of
 // plane p lives at tile_p[(y + 1) * pitch_p + x + 1].
+#ifndef PRED_LTAB_LDS
+#define PRED_LTAB_LDS 1       // 4x4 / 8x8 formula words: LDS copy (1) or the global table via L1 (0)
+#endif
 #define LP 65            // luma tile pitch
 #define CP 33            // chroma tile pitch (4:2:0)
 #define LT_SIZE (65 * LP)
@@ -662,11 +665,12 @@ DEV void load_sb_tile(const FrameDesc &fd, int sbx, int sby, bool interior, int 
     }
     if (left) { tile[(lane + 1) * LP] = v1; (lane < 32 ? tu : tv)[((lane & 31) + 1) * CP] = v3; }
     if (!interior) return;
-    // interior: 64 luma rows + 2 x 32 chroma rows, 16 independent loads per lane per batch
-    for (int i0 = 0; i0 < 64 * 64 + 2 * 32 * 32; i0 += 64 * 16) {
-        PIX t[16];
+    // interior: 64 luma rows + 2 x 32 chroma rows, 8 independent loads per lane per batch
+    // (16 in flight raised the kernel's register allocation by 40 VGPRs)
+    for (int i0 = 0; i0 < 64 * 64 + 2 * 32 * 32; i0 += 64 * 8) {
+        PIX t[8];
 #pragma unroll
-        for (int u = 0; u < 16; u++) {
+        for (int u = 0; u < 8; u++) {
             const int i = i0 + u * 64 + lane;
             if (i < 4096) t[u] = gy[(size_t) (ly + (i >> 6)) * py + lx + (i & 63)];
             else {
@@ -675,7 +679,7 @@ DEV void load_sb_tile(const FrameDesc &fd, int sbx, int sby, bool interior, int 
             }
         }
 #pragma unroll
-        for (int u = 0; u < 16; u++) {
+        for (int u = 0; u < 8; u++) {
             const int i = i0 + u * 64 + lane;
             if (i < 4096) tile[((i >> 6) + 1) * LP + (i & 63) + 1] = t[u];
             else {
@@ -705,20 +709,22 @@ DEV void pred_pass(uint32_t w, int lane, PIX *tile, uint16_t *eb, int bd, const 
              (PJ_Y4(jb) * 4 + 1) * tpch + PJ_X4(jb) * 4 + 1;
     const int ms = PJ_MSLOT(jb), slot = ms < 9 ? ms : 9;
     const int toff = ts == 0 ? 0 : ts == 1 ? 16 : ts == 2 ? 80 : 336;
-    // formula words of this column: rows of 4x4 / 8x8 from the LDS copy, larger from L1/L2;
-    // residual rows >= 8 of 16x16 / 32x32 loaded here
-    uint32_t f[MAXN];
-    uint32_t rx[MAXN > 8 ? (MAXN - 8) / 2 : 1];
-    if (MAXN <= 8) {
+    // formula words of this column: rows of 4x4 / 8x8 from the LDS copy, larger from L1/L2.
+    // Rows 0-7 here; rows >= 8 of 16x16 / 32x32 (formula + residual words) per 8-row chunk,
+    // one chunk ahead, so at most two chunks are live
+    constexpr int F0 = MAXN < 8 ? MAXN : 8;
+    uint32_t f[F0];
+    const uint32_t *ftab = PRED_LTAB_LDS && (ts <= 1 || MAXN <= 8) ? ltab + slot * 80 + toff + li
+                                                                   : ptab + slot * PTAB_SLOT + toff + li;
 #pragma unroll
-        for (int y = 0; y < MAXN; y++) f[y] = ltab[slot * 80 + toff + (y < n ? y : 0) * n + li];
-    } else {
-        const uint32_t *tl = ts <= 1 ? ltab + slot * 80 + toff + li : ptab + slot * PTAB_SLOT + toff + li;
+    for (int y = 0; y < F0; y++) f[y] = ftab[(y < n ? y : 0) * n];
+    const uint32_t *rr = (const uint32_t *) (resid + (PJ_RES(jb) && ts >= 2 ? (size_t) jb.roff * 16 + li * n : 0));
+    uint32_t fa[8], ra[4], fb[8], rb[4];
+    if (MAXN > 8) {
 #pragma unroll
-        for (int y = 0; y < MAXN; y++) f[y] = tl[(y < n ? y : 0) * n];
-        const uint32_t *r = (const uint32_t *) (resid + (PJ_RES(jb) && ts >= 2 ? (size_t) jb.roff * 16 + li * n : 0));
+        for (int y = 0; y < 8; y++) fa[y] = ftab[(8 + y < n ? 8 + y : 0) * n];
 #pragma unroll
-        for (int k = 4; k < MAXN / 2; k++) rx[k - 4] = r[k < n / 2 ? k : 0];
+        for (int k = 0; k < 4; k++) ra[k] = rr[4 + k < n / 2 ? 4 + k : 0];
     }
 
     // edges (fills: vp9recon.c:103-210): every load hits a valid tile address, the
@@ -762,14 +768,21 @@ DEV void pred_pass(uint32_t w, int lane, PIX *tile, uint16_t *eb, int bd, const 
         const char *e8 = (const char *) e;
 #pragma unroll
         for (int y = 0; y < MAXN; y++) {
+            if (MAXN > 8 && (y & 7) == 0 && y >= 8 && y + 8 < MAXN) {   // prefetch the chunk after this one
+                uint32_t *fn = ((y >> 3) & 1) ? fb : fa, *rn = ((y >> 3) & 1) ? rb : ra;
+#pragma unroll
+                for (int k = 0; k < 8; k++) fn[k] = ftab[(y + 8 + k < n ? y + 8 + k : 0) * n];
+#pragma unroll
+                for (int k = 0; k < 4; k++) rn[k] = rr[(y + 8) / 2 + k < n / 2 ? (y + 8) / 2 + k : 0];
+            }
             if (MAXN > 4 && y >= n) continue;
-            const uint32_t fw = f[y];
+            const uint32_t fw = y < 8 ? f[y < F0 ? y : 0] : ((y >> 3) & 1) ? fa[y & 7] : fb[y & 7];
             const int a = *(const uint16_t *) (e8 + (fw & 255)), b = *(const uint16_t *) (e8 + ((fw >> 8) & 255)),
                       c = *(const uint16_t *) (e8 + ((fw >> 16) & 255));
             const int wb = (fw >> 24) & 3, s = (fw >> 28) & 3, rnd = fw >> 30;
             const int wc = __builtin_amdgcn_sbfe((int) fw, 26, 2);
             int v = med3_0(((a + rnd) + wb * b + wc * c) >> s, mx);
-            const uint32_t rw = y < 8 ? pr_word(ps, y >> 1) : rx[y < 8 ? 0 : (y >> 1) - 4];
+            const uint32_t rw = y < 8 ? pr_word(ps, y >> 1) : ((y >> 3) & 1) ? ra[(y >> 1) & 3] : rb[(y >> 1) & 3];
             const int r = (int) (int16_t) (rw >> ((y & 1) * 16));
             v = med3_0(v + (hr ? r : 0), mx);
             o[y * tpch + li] = (PIX) v;
@@ -794,7 +807,9 @@ DEV void run_pass(uint32_t w, int lane, PIX *tile, uint16_t *eb, int bd, const P
 template <typename PIX> struct PredLds {
     PIX tile[PRED_K * TILE_ELEMS];
     uint16_t eb[256];                 // per job 2n+8 edge pixels
+#if PRED_LTAB_LDS
     uint32_t ltab[10 * 80];           // formula words of 4x4 and 8x8, all slots
+#endif
 };
 
 template <typename PIX>
@@ -820,7 +835,11 @@ DEV void pred_wg(const WGRec *wgp, const SBRec *__restrict__ sbs, const PJob *__
 {
     PIX *tile = S.tile;
     uint16_t *eb = S.eb;
+#if PRED_LTAB_LDS
     const uint32_t *ltab = S.ltab;
+#else
+    const uint32_t *ltab = nullptr;
+#endif
     const uint32_t wjob0 = wgp->job0, wpass0 = wgp->pass0, wnjobs = wgp->njobs, wnpass = wgp->npass;
     const PJob *lj = jobs + wjob0;         // job records: read a pass ahead (L1/L2)
     const uint32_t *lp = passes + wpass0;  // pass words: wave-uniform scalar loads
@@ -890,7 +909,9 @@ __global__ __launch_bounds__(64) void k_pred(const uint32_t *__restrict__ list, 
                                              const int16_t *__restrict__ resid, const uint32_t *__restrict__ ptab, int dbg)
 {
     __shared__ PredLds<PIX> S;
+#if PRED_LTAB_LDS
     load_ltab<PIX>(S.ltab, ptab, threadIdx.x);
+#endif
     pred_wg<PIX>(wgs + list[blockIdx.x], sbs, jobs, passes, frames, resid, ptab, S, threadIdx.x, dbg);
 }
 
@@ -1120,10 +1141,8 @@ DEV void lf_sb(const LFRec &rec, const FrameDesc *__restrict__ frames, LfLds<PIX
     } else {
         const int p = 1 + ((tid - 64) >> 5), r = (tid - 64) & 31;
         uint32_t *rowp = (uint32_t *) (ct[p - 1] + (r + 8) * FCP);
-        int px[48];
+        int px[40];
         lf_unpack<PIX>(rowp, px, 0, 40 / PPW, 0);
-#pragma unroll
-        for (int i = 40; i < 48; i++) px[i] = 0;
         const uint32_t *pw = S.prog + (LFP_CC + (r >> 3) * 8) / 4;
         const uint32_t pc0 = pw[0], pc1 = pw[1];
 #define LF_COL_EDGE_UV(k)                                                                                \
@@ -1170,11 +1189,9 @@ DEV void lf_sb(const LFRec &rec, const FrameDesc *__restrict__ frames, LfLds<PIX
     } else {
         const int p = 1 + ((tid - 64) >> 5), c = (tid - 64) & 31;
         PIX *colp = ct[p - 1] + 8 + c;
-        int px[48];
+        int px[40];
 #pragma unroll
         for (int i = 0; i < 40; i++) px[i] = colp[i * FCP];
-#pragma unroll
-        for (int i = 40; i < 48; i++) px[i] = 0;
         const uint32_t *pw = S.prog + (LFP_CR + (c >> 3) * 8) / 4;
         const uint32_t pc0 = pw[0], pc1 = pw[1];
 #define LF_ROW_EDGE_UV(yy)                                                                               \
