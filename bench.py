@@ -151,7 +151,7 @@ def main():
     alg = dev.alg_bytes()           # per step, per kernel class
     names = list(alg.keys())
     fps, ms_per_step = aggregate(args.frames, args.steps, world, elapsed)
-    streams = max(1, min(4, int(os.environ.get("VP9HIP_STREAMS", "2")), args.frames))
+    streams = dev.groups()          # frame groups = concurrent HIP streams of the batch
 
     # dominant kernel (largest device time)
     dom = max(names, key=lambda k: ksum.get(k, [0.0, 0])[0])

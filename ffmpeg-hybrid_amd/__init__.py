@@ -84,7 +84,7 @@ ABI_SYMBOLS = ["vp9hip_open", "vp9hip_close", "vp9hip_configure", "vp9hip_submit
                "vp9hip_upload_frame", "vp9hip_flush", "vp9hip_last_timing", "vp9hip_set_timing",
                "vp9hip_alg_bytes", "vp9hip_plan_stats", "vp9hip_abi_version",
                "vp9hip_stage_batch_tiles", "vp9hip_batch_phases", "vp9hip_phase_frames", "vp9hip_run_phase",
-               "vp9hip_stripe", "vp9hip_frame_device",
+               "vp9hip_stripe", "vp9hip_frame_device", "vp9hip_batch_groups",
                "vp9hip_synth_defaults", "vp9hip_synth_frame", "vp9hip_synth_free"]
 
 
@@ -108,6 +108,7 @@ def lib():
     L.vp9hip_stage_batch_tiles.argtypes = [vp, ctypes.POINTER(FramePacket), ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                                            ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_int]
     L.vp9hip_batch_phases.argtypes = [vp]
+    L.vp9hip_batch_groups.argtypes = [vp]
     L.vp9hip_phase_frames.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_int]
     L.vp9hip_run_phase.argtypes = [vp, ctypes.c_int, ctypes.c_int]
     L.vp9hip_stripe.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
@@ -241,6 +242,10 @@ class Device:
     def phases(self):
         """Number of phases (chain positions) of the staged batch."""
         return _check("vp9hip_batch_phases", lib().vp9hip_batch_phases(self._c))
+
+    def groups(self):
+        """Frame groups (concurrent HIP streams) of the staged batch."""
+        return _check("vp9hip_batch_groups", lib().vp9hip_batch_groups(self._c))
 
     def phase_frames(self, phase):
         """Batch indices of the frames in `phase`."""

@@ -103,7 +103,7 @@ struct vp9hip_ctx {
     hipStream_t st = nullptr;           // main stream: uploads, downloads, group 0
     hipStream_t xst[MAX_GROUPS - 1] = {};   // groups 1.. of a batch (joined back into st)
     hipEvent_t fork_ev = nullptr, join_ev[MAX_GROUPS - 1] = {};
-    int max_groups = 2;                 // VP9HIP_STREAMS overrides (1..4); 2 measured best at C3
+    int max_groups = 3;                 // VP9HIP_STREAMS overrides (1..4); 3 measured best at C3, with even chain splits
     int w = 0, h = 0, bpp = 8, ss_h = 1, ss_v = 1, hb = 0, bypp = 1;
     int cols = 0, rows = 0, sb_cols = 0, sb_rows = 0;
     int pitch[2] = { 0, 0 };
@@ -908,7 +908,11 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     }
     std::vector<int> roots;
     for (int i = 0; i < n; i++) if (find(i) == i) roots.push_back(i);
-    const int G = std::max(1, std::min<int>(max_groups > 0 ? max_groups : c->max_groups, (int) roots.size()));
+    // G groups: as many as allowed, but chains split evenly (unless there are many: 4 GOP
+    // chains over 3 streams run 2/1/1 and the pair sets the time)
+    const int nroots = (int) roots.size();
+    int G = std::max(1, std::min<int>(max_groups > 0 ? max_groups : c->max_groups, nroots));
+    while (G > 1 && nroots % G && nroots < 16 * G) G--;
     s.ngroups = G;
     std::vector<int> grp(n);
     for (int i = 0; i < n; i++)
@@ -1186,6 +1190,13 @@ extern "C" int vp9hip_batch_phases(vp9hip_ctx *c)
 {
     if (!c || !c->stg.ready) return VP9HIP_EINVAL;
     return c->stg.nphases;
+}
+
+// Frame groups (concurrent HIP streams) of the staged batch.
+extern "C" int vp9hip_batch_groups(vp9hip_ctx *c)
+{
+    if (!c || !c->stg.ready) return VP9HIP_EINVAL;
+    return c->stg.ngroups;
 }
 
 extern "C" int vp9hip_phase_frames(vp9hip_ctx *c, int phase, int *frames, int cap)

@@ -154,6 +154,8 @@ int  vp9hip_stage_batch_refs(vp9hip_ctx *ctx, const vp9h_frame *pkts, int n, con
 int  vp9hip_stage_batch_tiles(vp9hip_ctx *ctx, const vp9h_frame *pkts, int n, const int *out_bufs,
                               const int *ref_bufs, int tile_lo, int tile_hi);
 int  vp9hip_batch_phases(vp9hip_ctx *ctx);
+/* Frame groups of the staged batch: independent chains run on that many HIP streams. */
+int  vp9hip_batch_groups(vp9hip_ctx *ctx);
 /* Batch indices of the frames in `phase` (up to cap written); returns their count. */
 int  vp9hip_phase_frames(vp9hip_ctx *ctx, int phase, int *frames, int cap);
 int  vp9hip_run_phase(vp9hip_ctx *ctx, int phase, int part);
