@@ -85,6 +85,7 @@ ABI_SYMBOLS = ["vp9hip_open", "vp9hip_close", "vp9hip_configure", "vp9hip_submit
                "vp9hip_alg_bytes", "vp9hip_plan_stats", "vp9hip_abi_version",
                "vp9hip_stage_batch_tiles", "vp9hip_batch_phases", "vp9hip_phase_frames", "vp9hip_run_phase",
                "vp9hip_stripe", "vp9hip_frame_device", "vp9hip_batch_groups",
+               "vp9h_decode_frame", "vp9h_encode_frame", "vp9h_frame_free", "vp9h_buffer_free",
                "vp9hip_synth_defaults", "vp9hip_synth_frame", "vp9hip_synth_free"]
 
 
@@ -132,6 +133,13 @@ def lib():
     L.vp9hip_synth_frame.argtypes = [ctypes.POINTER(FramePacket), ctypes.POINTER(SynthParams)]
     L.vp9hip_synth_free.argtypes = [ctypes.POINTER(FramePacket)]
     L.vp9hip_synth_free.restype = None
+    L.vp9h_decode_frame.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(FramePacket)]
+    L.vp9h_encode_frame.argtypes = [ctypes.POINTER(FramePacket), ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
+                                    ctypes.POINTER(ctypes.c_size_t)]
+    L.vp9h_frame_free.argtypes = [ctypes.POINTER(FramePacket)]
+    L.vp9h_frame_free.restype = None
+    L.vp9h_buffer_free.argtypes = [ctypes.c_void_p]
+    L.vp9h_buffer_free.restype = None
     _lib_handle = L
     return L
 
@@ -174,6 +182,33 @@ class SynthFrame:
         return [self.pkt.blocks[i] for i in range(self.pkt.nblocks)]
 
 
+def encode_frame(frame, base_q_idx):
+    """Write a pass-1 packet (SynthFrame or FramePacket) as a VP9 frame bitstream
+    (vp9h_encode_frame): returns bytes."""
+    pkt = frame.pkt if hasattr(frame, "pkt") else frame
+    buf, n = ctypes.c_void_p(), ctypes.c_size_t()
+    _check("vp9h_encode_frame", lib().vp9h_encode_frame(ctypes.byref(pkt), base_q_idx, ctypes.byref(buf), ctypes.byref(n)))
+    try:
+        return ctypes.string_at(buf.value, n.value)
+    finally:
+        lib().vp9h_buffer_free(buf)
+
+
+class DecodedFrame:
+    """The pass-1 packet of one VP9 frame bitstream, parsed on the host by
+    vp9h_decode_frame (owns its C arrays); usable wherever a SynthFrame is."""
+
+    def __init__(self, data):
+        self._data = bytes(data)
+        self.pkt = FramePacket()
+        _check("vp9h_decode_frame", lib().vp9h_decode_frame(self._data, len(self._data), ctypes.byref(self.pkt)))
+
+    def __del__(self):
+        if getattr(self, "pkt", None) is not None and _lib_handle is not None:
+            _lib_handle.vp9h_frame_free(ctypes.byref(self.pkt))
+            self.pkt = None
+
+
 def alloc_planes(width, height, bpp, ss_h=1, ss_v=1, pad=64):
     """Host planes padded to 64 luma pixels (the layout the oracle expects)."""
     dt = np.uint8 if bpp == 8 else np.uint16
@@ -185,6 +220,11 @@ def alloc_planes(width, height, bpp, ss_h=1, ss_v=1, pad=64):
 def visible(planes, width, height, ss_h=1, ss_v=1):
     cw, ch = (width + ss_h) >> ss_h, (height + ss_v) >> ss_v
     return [planes[0][:height, :width], planes[1][:ch, :cw], planes[2][:ch, :cw]]
+
+
+def decode_frame(data):
+    """Host entropy decode of one VP9 frame -> DecodedFrame (pass-1 packet)."""
+    return DecodedFrame(data)
 
 
 class Device:
@@ -213,7 +253,7 @@ class Device:
 
     def submit(self, frame, out_buf, refs=(0, 0, 0)):
         r = (ctypes.c_int * 3)(*refs)
-        pkt = frame.pkt if isinstance(frame, SynthFrame) else frame
+        pkt = frame.pkt if hasattr(frame, "pkt") else frame
         _check("vp9hip_submit_frame", lib().vp9hip_submit_frame(self._c, ctypes.byref(pkt), out_buf, r))
 
     def stage_batch(self, frames, out_bufs, ref_bufs=None, tiles=None):
@@ -221,7 +261,7 @@ class Device:
         (keyframes). Dependent frames are chained, independent chains run concurrently.
         tiles=(lo, hi): reconstruct only tile columns [lo, hi) (a shard of a tile-sharded
         stream, run with run_phase; see tileshard.py)."""
-        arr = (FramePacket * len(frames))(*[f.pkt if isinstance(f, SynthFrame) else f for f in frames])
+        arr = (FramePacket * len(frames))(*[f.pkt if hasattr(f, "pkt") else f for f in frames])
         ob = (ctypes.c_int * len(out_bufs))(*out_bufs)
         self._staged = (arr, frames)   # keep host packets alive
         if ref_bufs is None and tiles is None:
@@ -352,7 +392,7 @@ class Decoder:
         self._next = 0
 
     def send_packet(self, frame):
-        pkt = frame.pkt if isinstance(frame, SynthFrame) else frame
+        pkt = frame.pkt if hasattr(frame, "pkt") else frame
         cfg = (pkt.width, pkt.height, pkt.bpp)
         if self._configured != cfg:
             self.dev.configure(pkt.width, pkt.height, pkt.bpp, self.nbufs, pkt.ss_h, pkt.ss_v)

@@ -246,6 +246,22 @@ void vp9hip_synth_defaults(vp9h_synth_params *p, int width, int height, int bpp)
 int  vp9hip_synth_frame(vp9h_frame *out, const vp9h_synth_params *p);
 void vp9hip_synth_free(vp9h_frame *f);
 
+/* ---- host bitstream side: VP9 frame <-> pass-1 packet ----------
+ * vp9h_decode_frame parses one frame's compressed data (uncompressed + compressed
+ * header, tiles) into a pass-1 packet: the host entropy decode whose output the device
+ * path consumes. It follows decode_frame_header / decode_tiles / decode_sb /
+ * ff_vp9_decode_block of the reference (vp9.c:519-1395, vp9block.c:80-1130). The packet
+ * owns heap arrays; release them with vp9h_frame_free.
+ * vp9h_encode_frame writes a pass-1 packet as a VP9 bitstream (the synthetic stream
+ * generator): default probabilities, frame_parallel, tx_mode = TX_MODE_SELECT, libvpx's
+ * default LF deltas. Release the buffer with vp9h_buffer_free.
+ * This version: keyframes and intra-only frames, profiles 0 / 2 (4:2:0); inter frames
+ * and backward probability adaptation return VP9HIP_ENOSYS. */
+int  vp9h_decode_frame(const uint8_t *data, size_t size, vp9h_frame *out);
+int  vp9h_encode_frame(const vp9h_frame *pkt, int base_q_idx, uint8_t **out, size_t *size);
+void vp9h_frame_free(vp9h_frame *f);
+void vp9h_buffer_free(uint8_t *p);
+
 #ifdef __cplusplus
 }
 #endif

@@ -13,13 +13,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def test_library_exports_every_declared_symbol(v9):
     hdr = open(os.path.join(ROOT, "include", "vp9hip.h")).read()
-    declared = sorted(set(re.findall(r"\b(vp9hip_\w+)\s*\(", hdr)))
+    declared = sorted(set(re.findall(r"\b(vp9h(?:ip)?_\w+)\s*\(", hdr)))
     assert declared, "no entry points found in include/vp9hip.h"
     L = v9.lib()
     for sym in declared:
         assert hasattr(L, sym), sym
     nm = subprocess.run(["nm", "-D", "--defined-only", v9.LIB_PATH], capture_output=True, text=True).stdout
-    exported = set(re.findall(r" T (vp9hip_\w+)", nm))
+    exported = set(re.findall(r" T (vp9h(?:ip)?_\w+)", nm))
     assert set(declared) <= exported
     assert set(v9.ABI_SYMBOLS) <= exported
 
