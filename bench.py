@@ -184,6 +184,8 @@ def main():
         "kernel_ms": {k: round(ksum[k][0] / args.steps, 3) for k in ksum},
     }
 
+    host = host_entropy_rate(v, frames, gop, args) if rank == 0 and world == 1 and not args.no_cpu_baseline else None
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -221,12 +223,40 @@ def main():
                    "host_gen_s": round(t_gen, 2), "host_stage_s": round(t_stage, 2)},
         "roofline": roofline,
         "cpu_baseline": cpu,
+        "host_entropy": host,
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
     dev.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def host_entropy_rate(v, frames, gop, args):
+    """The host side of the hybrid split: the frames as VP9 bitstreams
+    (vp9h_encode_frame), parsed back into pass-1 packets by vp9h_decode_frame, timed on
+    this box's cores (1 thread, then a frame-parallel pool: ctypes drops the GIL). Not
+    `value` (the GPU path is timed with packets resident); the rate at which the host
+    front end could feed it. Keyframe streams only in this version."""
+    import concurrent.futures
+    if gop != 1:
+        return {"note": "inter-frame bitstreams are not parsed by this version"}
+    streams = [v.encode_frame(f, f.params.q_idx) for f in frames[:min(len(frames), 16)]]
+    t0 = time.perf_counter()
+    n = 0
+    while time.perf_counter() - t0 < args.cpu_seconds / 2 or n < len(streams):
+        v.decode_frame(streams[n % len(streams)])
+        n += 1
+    one = n / (time.perf_counter() - t0)
+    threads = min(16, os.cpu_count() or 1)             # the box's CPU share
+    with concurrent.futures.ThreadPoolExecutor(threads) as ex:
+        t0 = time.perf_counter()
+        reps = max(1, int(one * args.cpu_seconds / 2 * threads / len(streams) / 4) + 1)
+        list(ex.map(v.decode_frame, streams * reps))
+        many = len(streams) * reps / (time.perf_counter() - t0)
+    return {"fps_1_thread": round(one, 2), "fps_threads": round(many, 2), "threads": threads,
+            "bytes_per_frame": int(sum(map(len, streams)) / len(streams)),
+            "sample": "%d synthetic %s frames as VP9 bitstreams, parsed to pass-1 packets" % (len(streams), args.config)}
 
 
 def bench_tiles(args, v, dist, world, rank, local_rank):

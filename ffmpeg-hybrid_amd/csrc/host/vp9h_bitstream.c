@@ -32,41 +32,67 @@
 
 /* ------------------------------------------------------------------ bool coder */
 typedef struct BoolDec {
-    const uint8_t *p, *end;
-    uint32_t value;      /* 2-byte window, RFC 6386 7.3 */
+    const uint8_t *start, *p, *end;
+    uint64_t value;      /* the next bits of the stream, left-aligned (bit 63 first) */
+    int bits;            /* valid bits in value */
     uint32_t range;
-    int bit_count;
-    int overrun;         /* bytes requested past the end (vpx_rac_is_end, vpx_rac.h:47-52) */
+    int pad;             /* zero bytes filled in past the end */
 } BoolDec;
 
-static uint8_t bd_next(BoolDec *d)
+/* top the window up to >= 57 valid bits: 8 bytes at a time while the stream lasts */
+static void bd_fill(BoolDec *d)
 {
-    if (d->p < d->end) return *d->p++;
-    d->overrun++;
-    return 0;
+    if (d->end - d->p >= 8) {
+        uint64_t be;
+        memcpy(&be, d->p, 8);
+        be = __builtin_bswap64(be);
+        const int nbytes = (64 - d->bits) >> 3;
+        if (nbytes < 8) be &= ~0ull << (64 - 8 * nbytes);
+        d->value |= be >> d->bits;
+        d->p += nbytes;
+        d->bits += 8 * nbytes;
+        return;
+    }
+    while (d->bits <= 56) {
+        uint64_t byte = 0;
+        if (d->p < d->end) byte = *d->p++;
+        else d->pad++;
+        d->value |= byte << (56 - d->bits);
+        d->bits += 8;
+    }
 }
 
 static void bd_init(BoolDec *d, const uint8_t *p, size_t n)
 {
-    d->p = p; d->end = p + n;
-    d->value = (uint32_t) bd_next(d) << 8;
-    d->value |= bd_next(d);
+    d->start = d->p = p; d->end = p + n;
+    d->value = 0; d->bits = 0; d->pad = 0;
     d->range = 255;
-    d->bit_count = 0;
-    d->overrun = 0;
+    bd_fill(d);
 }
 
-static int bd_read(BoolDec *d, int prob)
+/* bytes the byte-serial coder of RFC 6386 7.3 (2-byte window, one byte per 8 shifts) would
+ * have requested past the end: the vpx_rac_is_end test (vpx_rac.h:47-52) */
+static int bd_overrun(const BoolDec *d)
 {
-    const uint32_t split = 1 + (((d->range - 1) * (uint32_t) prob) >> 8), SPLIT = split << 8;
-    int bit;
-    if (d->value >= SPLIT) { bit = 1; d->range -= split; d->value -= SPLIT; }
-    else { bit = 0; d->range = split; }
-    while (d->range < 128) {
-        d->value <<= 1;
-        d->range <<= 1;
-        if (++d->bit_count == 8) { d->bit_count = 0; d->value |= bd_next(d); }
-    }
+    const int64_t shifted = 8 * ((int64_t) (d->p - d->start) + d->pad) - d->bits;
+    const int64_t over = 2 + shifted / 8 - (int64_t) (d->end - d->start);
+    return over > 0 ? (int) over : 0;
+}
+
+/* one bool (vpx_rac_get_prob, vpx_rac.h:87-110): compare the top byte with the split,
+ * renormalise by the leading zeros of the range */
+static inline __attribute__((always_inline)) int bd_read(BoolDec *d, int prob)
+{
+    if (d->bits < 16) bd_fill(d);
+    const uint32_t split = 1 + (((d->range - 1) * (uint32_t) prob) >> 8);
+    const uint64_t big = (uint64_t) split << 56;
+    const int bit = d->value >= big;                 /* selects, not a branch: bits are noisy */
+    d->range = bit ? d->range - split : split;
+    d->value -= bit ? big : 0;
+    const int sh = __builtin_clz(d->range) - 24;
+    d->range <<= sh;
+    d->value <<= sh;
+    d->bits -= sh;
     return bit;
 }
 
@@ -128,9 +154,14 @@ static void be_flush(BoolEnc *e)
 /* one coder, either direction: bc_bool returns the bit read, or writes `bit` */
 typedef struct BC { int enc; BoolDec d; BoolEnc e; } BC;
 
-static inline int bc_bool(BC *c, int prob, int bit)
+static inline __attribute__((always_inline)) int bc_bool(BC *c, int prob, int bit)
 {
     if (c->enc) { be_write(&c->e, prob, bit); return bit; }
+    return bd_read(&c->d, prob);
+}
+static inline __attribute__((always_inline)) int bc_bool_e(BC *c, const int enc, int prob, int bit)
+{
+    if (enc) { be_write(&c->e, prob, bit); return bit; }
     return bd_read(&c->d, prob);
 }
 static int bc_uint(BC *c, int bits, int v)
@@ -352,9 +383,10 @@ static int enc_value(const Walk *w, int stored, int q, int tx32)
 }
 
 /* one tx block's tokens (decode_coeffs_b_generic, vp9block.c:806-923): returns the eob */
-static int walk_tokens(Walk *w, int n_coeffs, int tx32, const uint8_t (*p)[6][11], int nnz, const int16_t *scan,
-                       const int16_t (*nb)[2], const int16_t *band_counts, const int *qmul, int eob_in,
-                       const uint8_t *cin, int csz)
+static inline __attribute__((always_inline)) int
+walk_tokens_t(Walk *w, int n_coeffs, int tx32, const uint8_t (*p)[6][11], int nnz, const int16_t *scan,
+              const int16_t (*nb)[2], const int16_t *band_counts, const int *qmul, int eob_in,
+              const uint8_t *cin, int csz, const int enc)
 {
     BC *c = w->c;
     const int bpp = w->h.bpp;
@@ -363,7 +395,7 @@ static int walk_tokens(Walk *w, int n_coeffs, int tx32, const uint8_t (*p)[6][11
     uint8_t cache[1024];
     /* encoder: the values to send */
     int vals[1024];
-    if (c->enc)
+    if (enc)
         for (int k = 0; k < eob_in; k++) {
             int32_t s;
             if (csz == 2) { int16_t t; memcpy(&t, cin + 2 * k, 2); s = t; } else memcpy(&s, cin + 4 * k, 4);
@@ -376,71 +408,74 @@ static int walk_tokens(Walk *w, int n_coeffs, int tx32, const uint8_t (*p)[6][11
             if ((csz == 2 ? (int32_t) (int16_t) back : back) != s) { w->err = 1; return 0; }
         }
     const size_t c0 = w->nc;
-    if (!c->enc) {
+    if (!enc) {
         w->coefs = grow(w->coefs, &w->cc, w->nc + (size_t) n_coeffs * csz, 1, &w->err);
         if (w->err) return 0;
     }
     do {
         /* more coefficients? */
-        if (!bc_bool(c, tp[0], i < eob_in)) break;
+        if (!bc_bool_e(c, enc, tp[0], i < eob_in)) break;
     skip_eob:
         {
-            const int v = c->enc ? vals[i] : 0, av = v < 0 ? -v : v;
-            if (!bc_bool(c, tp[1], av != 0)) {                       /* ZERO */
+            const int v = enc ? vals[i] : 0, av = v < 0 ? -v : v;
+            if (!bc_bool_e(c, enc, tp[1], av != 0)) {                       /* ZERO */
                 if (!--band_left) band_left = band_counts[++band];
                 cache[scan[i]] = 0;
                 nnz = (1 + cache[nb[i][0]] + cache[nb[i][1]]) >> 1;
                 tp = p[band][nnz];
-                if (!c->enc) { int32_t z = 0; memcpy(w->coefs + c0 + (size_t) i * csz, &z, csz); }
+                if (!enc) {
+                    if (csz == 2) { const int16_t z = 0; memcpy(w->coefs + c0 + (size_t) i * 2, &z, 2); }
+                    else { const int32_t z = 0; memcpy(w->coefs + c0 + (size_t) i * 4, &z, 4); }
+                }
                 if (++i == n_coeffs) break;
                 goto skip_eob;
             }
             const int rc = scan[i];
             int val;
-            if (!bc_bool(c, tp[2], av > 1)) { val = 1; cache[rc] = 1; }
-            else if (!bc_bool(c, tp[3], av > 4)) {
-                if (!bc_bool(c, tp[4], av > 2)) { val = 2; cache[rc] = 2; }
-                else { val = 3 + bc_bool(c, tp[5], av == 4); cache[rc] = 3; }
-            } else if (!bc_bool(c, tp[6], av > 10)) {
+            if (!bc_bool_e(c, enc, tp[2], av > 1)) { val = 1; cache[rc] = 1; }
+            else if (!bc_bool_e(c, enc, tp[3], av > 4)) {
+                if (!bc_bool_e(c, enc, tp[4], av > 2)) { val = 2; cache[rc] = 2; }
+                else { val = 3 + bc_bool_e(c, enc, tp[5], av == 4); cache[rc] = 3; }
+            } else if (!bc_bool_e(c, enc, tp[6], av > 10)) {
                 cache[rc] = 4;
-                if (!bc_bool(c, tp[7], av > 6)) val = 5 + bc_bool(c, 159, av == 6);
+                if (!bc_bool_e(c, enc, tp[7], av > 6)) val = 5 + bc_bool_e(c, enc, 159, av == 6);
                 else {
                     const int e = av - 7;
-                    val = 7 + (bc_bool(c, 165, (e >> 1) & 1) << 1);
-                    val += bc_bool(c, 145, e & 1);
+                    val = 7 + (bc_bool_e(c, enc, 165, (e >> 1) & 1) << 1);
+                    val += bc_bool_e(c, enc, 145, e & 1);
                 }
             } else {
                 cache[rc] = 5;
-                if (!bc_bool(c, tp[8], av > 34)) {
-                    if (!bc_bool(c, tp[9], av > 18)) {
+                if (!bc_bool_e(c, enc, tp[8], av > 34)) {
+                    if (!bc_bool_e(c, enc, tp[9], av > 18)) {
                         const int e = av - 11;
-                        val = 11 + (bc_bool(c, 173, (e >> 2) & 1) << 2);
-                        val += bc_bool(c, 148, (e >> 1) & 1) << 1;
-                        val += bc_bool(c, 140, e & 1);
+                        val = 11 + (bc_bool_e(c, enc, 173, (e >> 2) & 1) << 2);
+                        val += bc_bool_e(c, enc, 148, (e >> 1) & 1) << 1;
+                        val += bc_bool_e(c, enc, 140, e & 1);
                     } else {
                         const int e = av - 19;
-                        val = 19 + (bc_bool(c, 176, (e >> 3) & 1) << 3);
-                        val += bc_bool(c, 155, (e >> 2) & 1) << 2;
-                        val += bc_bool(c, 140, (e >> 1) & 1) << 1;
-                        val += bc_bool(c, 135, e & 1);
+                        val = 19 + (bc_bool_e(c, enc, 176, (e >> 3) & 1) << 3);
+                        val += bc_bool_e(c, enc, 155, (e >> 2) & 1) << 2;
+                        val += bc_bool_e(c, enc, 140, (e >> 1) & 1) << 1;
+                        val += bc_bool_e(c, enc, 135, e & 1);
                     }
-                } else if (!bc_bool(c, tp[10], av > 66)) {
+                } else if (!bc_bool_e(c, enc, tp[10], av > 66)) {
                     const int e = av - 35;
-                    val = 35 + (bc_bool(c, 180, (e >> 4) & 1) << 4);
-                    val += bc_bool(c, 157, (e >> 3) & 1) << 3;
-                    val += bc_bool(c, 141, (e >> 2) & 1) << 2;
-                    val += bc_bool(c, 134, (e >> 1) & 1) << 1;
-                    val += bc_bool(c, 130, e & 1);
+                    val = 35 + (bc_bool_e(c, enc, 180, (e >> 4) & 1) << 4);
+                    val += bc_bool_e(c, enc, 157, (e >> 3) & 1) << 3;
+                    val += bc_bool_e(c, enc, 141, (e >> 2) & 1) << 2;
+                    val += bc_bool_e(c, enc, 134, (e >> 1) & 1) << 1;
+                    val += bc_bool_e(c, enc, 130, e & 1);
                 } else {
                     /* CAT6: 14 extra bits at 8-bit, 16 at 10-bit, 18 at 12-bit */
                     const int nbits = bpp == 12 ? 18 : bpp == 10 ? 16 : 14, e = av - 67;
                     val = 67;
-                    for (int k = nbits - 1; k >= 0; k--) val += bc_bool(c, cat6_probs[17 - k], (e >> k) & 1) << k;
+                    for (int k = nbits - 1; k >= 0; k--) val += bc_bool_e(c, enc, cat6_probs[17 - k], (e >> k) & 1) << k;
                 }
             }
             if (!--band_left) band_left = band_counts[++band];
-            const int neg = bc_bool(c, 128, v < 0);
-            if (!c->enc) {
+            const int neg = bc_bool_e(c, enc, 128, v < 0);
+            if (!enc) {
                 const int32_t sv = neg ? -val : val;
                 int32_t st = tx32 ? (int32_t) ((int) ((unsigned) sv * (unsigned) qmul[i > 0]) / 2)
                                   : (int32_t) ((unsigned) sv * (unsigned) qmul[i > 0]);
@@ -451,8 +486,18 @@ static int walk_tokens(Walk *w, int n_coeffs, int tx32, const uint8_t (*p)[6][11
             tp = p[band][nnz];
         }
     } while (++i < n_coeffs);
-    if (!c->enc) w->nc += (size_t) i * csz;
+    if (!enc) w->nc += (size_t) i * csz;
     return i;
+}
+
+/* the walker's direction as a constant, so the decode loop carries no encoder branches */
+static int walk_tokens(Walk *w, int n_coeffs, int tx32, const uint8_t (*p)[6][11], int nnz, const int16_t *scan,
+                       const int16_t (*nb)[2], const int16_t *band_counts, const int *qmul, int eob_in,
+                       const uint8_t *cin, int csz)
+{
+    if (w->c->enc)
+        return walk_tokens_t(w, n_coeffs, tx32, p, nnz, scan, nb, band_counts, qmul, eob_in, cin, csz, 1);
+    return walk_tokens_t(w, n_coeffs, tx32, p, nnz, scan, nb, band_counts, qmul, eob_in, cin, csz, 0);
 }
 
 static const int16_t band_counts[4][6] = {
@@ -889,7 +934,7 @@ static int walk_tiles(Walk *w, BC *coders)
                 w->c = &coders[tr * ntc + tc];
                 for (int col = c0; col < c1; col += 8) {
                     /* a tile whose data ran out is invalid (vp9.c:1383-1385) */
-                    if (!w->c->enc && w->c->d.overrun > 10) { w->err = 1; return -1; }
+                    if (!w->c->enc && bd_overrun(&w->c->d) > 10) { w->err = 1; return -1; }
                     walk_sb(w, row, col, 0);
                     if (w->err) return -1;
                 }
