@@ -75,6 +75,28 @@ class SynthParams(ctypes.Structure):
                 ("p_skip", ctypes.c_float), ("seed", ctypes.c_uint64)]
 
 
+class FrameInfo(ctypes.Structure):
+    """vp9h_frame_info: the frame header's reference bookkeeping."""
+    _fields_ = [("show_existing_frame", ctypes.c_int32), ("show_slot", ctypes.c_int32),
+                ("show_frame", ctypes.c_int32), ("refresh_mask", ctypes.c_int32),
+                ("ref_slot", ctypes.c_int32 * 3), ("sign_bias", ctypes.c_int32 * 3),
+                ("error_res", ctypes.c_int32), ("refresh_ctx", ctypes.c_int32), ("parallel", ctypes.c_int32),
+                ("ctx_id", ctypes.c_int32), ("allow_hp", ctypes.c_int32), ("interp", ctypes.c_int32),
+                ("comp_mode", ctypes.c_int32), ("tx_mode", ctypes.c_int32),
+                ("header_size", ctypes.c_uint32), ("compressed_header_size", ctypes.c_uint32)]
+
+
+class EncParams(ctypes.Structure):
+    """vp9h_enc_params: the encoder's per-frame choices."""
+    _fields_ = [("base_q_idx", ctypes.c_int32), ("show_existing_frame", ctypes.c_int32),
+                ("show_slot", ctypes.c_int32), ("show_frame", ctypes.c_int32), ("error_res", ctypes.c_int32),
+                ("refresh_mask", ctypes.c_int32), ("ref_slot", ctypes.c_int32 * 3),
+                ("sign_bias", ctypes.c_int32 * 3), ("refresh_ctx", ctypes.c_int32), ("parallel", ctypes.c_int32),
+                ("ctx_id", ctypes.c_int32), ("reset_ctx", ctypes.c_int32), ("allow_hp", ctypes.c_int32),
+                ("interp", ctypes.c_int32), ("comp_mode", ctypes.c_int32), ("tx_mode", ctypes.c_int32),
+                ("prob_updates", ctypes.c_int32), ("keep_modes", ctypes.c_int32)]
+
+
 _lib_handle = None
 
 # Exported symbols of include/vp9hip.h (checked by the CPU test suite).
@@ -86,6 +108,8 @@ ABI_SYMBOLS = ["vp9hip_open", "vp9hip_close", "vp9hip_configure", "vp9hip_submit
                "vp9hip_stage_batch_tiles", "vp9hip_batch_phases", "vp9hip_phase_frames", "vp9hip_run_phase",
                "vp9hip_stripe", "vp9hip_frame_device", "vp9hip_batch_groups",
                "vp9h_decode_frame", "vp9h_encode_frame", "vp9h_frame_free", "vp9h_buffer_free",
+               "vp9h_stream_open", "vp9h_stream_close", "vp9h_stream_decode", "vp9h_stream_encode",
+               "vp9h_enc_defaults", "vp9h_superframe_split",
                "vp9hip_synth_defaults", "vp9hip_synth_frame", "vp9hip_synth_free"]
 
 
@@ -140,6 +164,18 @@ def lib():
     L.vp9h_frame_free.restype = None
     L.vp9h_buffer_free.argtypes = [ctypes.c_void_p]
     L.vp9h_buffer_free.restype = None
+    L.vp9h_stream_open.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+    L.vp9h_stream_close.argtypes = [ctypes.c_void_p]
+    L.vp9h_stream_close.restype = None
+    L.vp9h_stream_decode.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(FramePacket),
+                                     ctypes.POINTER(FrameInfo)]
+    L.vp9h_stream_encode.argtypes = [ctypes.c_void_p, ctypes.POINTER(FramePacket), ctypes.POINTER(EncParams),
+                                     ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t),
+                                     ctypes.POINTER(FramePacket)]
+    L.vp9h_enc_defaults.argtypes = [ctypes.POINTER(EncParams)]
+    L.vp9h_enc_defaults.restype = None
+    L.vp9h_superframe_split.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t),
+                                        ctypes.POINTER(ctypes.c_size_t), ctypes.c_int]
     _lib_handle = L
     return L
 
@@ -207,6 +243,96 @@ class DecodedFrame:
         if getattr(self, "pkt", None) is not None and _lib_handle is not None:
             _lib_handle.vp9h_frame_free(ctypes.byref(self.pkt))
             self.pkt = None
+
+
+class _OwnedPacket:
+    """A pass-1 packet whose arrays the library allocated (vp9h_frame_free)."""
+
+    def __init__(self):
+        self.pkt = FramePacket()
+
+    def __del__(self):
+        if getattr(self, "pkt", None) is not None and _lib_handle is not None:
+            _lib_handle.vp9h_frame_free(ctypes.byref(self.pkt))
+            self.pkt = None
+
+    def blocks(self):
+        return [self.pkt.blocks[i] for i in range(self.pkt.nblocks)]
+
+
+def enc_params(**kw):
+    """vp9h_enc_defaults, overridable by keyword (ref_slot / sign_bias take 3-sequences)."""
+    p = EncParams()
+    lib().vp9h_enc_defaults(ctypes.byref(p))
+    for k, v in kw.items():
+        if not hasattr(p, k):
+            raise KeyError(k)
+        if k in ("ref_slot", "sign_bias"):
+            v = (ctypes.c_int32 * 3)(*v)
+        setattr(p, k, v)
+    return p
+
+
+class Stream:
+    """A stream's host parse state (vp9h_stream): decode or encode frames in order."""
+
+    def __init__(self):
+        self._s = ctypes.c_void_p()
+        _check("vp9h_stream_open", lib().vp9h_stream_open(ctypes.byref(self._s)))
+
+    def close(self):
+        if self._s:
+            lib().vp9h_stream_close(self._s)
+            self._s = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def decode(self, data):
+        """One frame of compressed data -> (packet or None for show_existing_frame, FrameInfo)."""
+        data = bytes(data)
+        out, info = _OwnedPacket(), FrameInfo()
+        _check("vp9h_stream_decode", lib().vp9h_stream_decode(self._s, data, len(data), ctypes.byref(out.pkt),
+                                                               ctypes.byref(info)))
+        return (None if info.show_existing_frame else out), info
+
+    def encode(self, frame, params=None, **kw):
+        """Write one frame (a packet, or None with show_existing_frame=1): returns
+        (bytes, coded packet or None)."""
+        p = params if params is not None else enc_params(**kw)
+        pkt = None if frame is None else (frame.pkt if hasattr(frame, "pkt") else frame)
+        buf, n = ctypes.c_void_p(), ctypes.c_size_t()
+        coded = _OwnedPacket()
+        _check("vp9h_stream_encode", lib().vp9h_stream_encode(self._s, ctypes.byref(pkt) if pkt is not None else None,
+                                                               ctypes.byref(p), ctypes.byref(buf), ctypes.byref(n),
+                                                               ctypes.byref(coded.pkt)))
+        try:
+            data = ctypes.string_at(buf.value, n.value)
+        finally:
+            lib().vp9h_buffer_free(buf)
+        return data, (coded if pkt is not None else None)
+
+
+def superframe_split(data):
+    """The frames of a superframe (vp9h_superframe_split), as bytes objects."""
+    data = bytes(data)
+    offs, sizes = (ctypes.c_size_t * 8)(), (ctypes.c_size_t * 8)()
+    n = _check("vp9h_superframe_split", lib().vp9h_superframe_split(data, len(data), offs, sizes, 8))
+    return [data[offs[i]:offs[i] + sizes[i]] for i in range(n)]
+
+
+def superframe_join(frames):
+    """Pack frames into one superframe with the index vp9_superframe_split reads."""
+    if len(frames) == 1:
+        return bytes(frames[0])
+    mx = max(len(f) for f in frames)
+    ln = 1 if mx < 1 << 8 else 2 if mx < 1 << 16 else 3 if mx < 1 << 24 else 4
+    marker = 0xc0 | (ln - 1) << 3 | (len(frames) - 1)
+    idx = bytes([marker]) + b"".join(len(f).to_bytes(ln, "little") for f in frames) + bytes([marker])
+    return b"".join(bytes(f) for f in frames) + idx
 
 
 def alloc_planes(width, height, bpp, ss_h=1, ss_v=1, pad=64):

@@ -255,12 +255,81 @@ void vp9hip_synth_free(vp9h_frame *f);
  * vp9h_encode_frame writes a pass-1 packet as a VP9 bitstream (the synthetic stream
  * generator): default probabilities, frame_parallel, tx_mode = TX_MODE_SELECT, libvpx's
  * default LF deltas. Release the buffer with vp9h_buffer_free.
- * This version: keyframes and intra-only frames, profiles 0 / 2 (4:2:0); inter frames
- * and backward probability adaptation return VP9HIP_ENOSYS. */
+ * These one-frame forms take keyframes and intra-only frames (no reference state);
+ * streams with inter frames go through a vp9h_stream below. Profiles 0 / 2 (4:2:0). */
 int  vp9h_decode_frame(const uint8_t *data, size_t size, vp9h_frame *out);
 int  vp9h_encode_frame(const vp9h_frame *pkt, int base_q_idx, uint8_t **out, size_t *size);
 void vp9h_frame_free(vp9h_frame *f);
 void vp9h_buffer_free(uint8_t *p);
+
+/*
+ * A stream's host parse state (VP9Context's frame-to-frame state: the 4 saved probability
+ * contexts prob_ctx, the 8 reference slots' sizes, the last frame's MV pairs and the
+ * segmentation-map reference, vp9.c:1616-1686; the persistent header s->s.h). One
+ * vp9h_stream either decodes or encodes one stream, frame by frame, in order.
+ */
+typedef struct vp9h_stream vp9h_stream;
+int  vp9h_stream_open(vp9h_stream **out);
+void vp9h_stream_close(vp9h_stream *s);
+
+/* What the frame header decided beyond the packet (reference slot bookkeeping for the
+ * device buffers, vp9.c:1686-1691, 1845-1849). */
+typedef struct vp9h_frame_info {
+    int32_t show_existing_frame;   /* 1: no packet; output reference slot show_slot        */
+    int32_t show_slot;
+    int32_t show_frame;            /* 0: decoded into the slots but not output             */
+    int32_t refresh_mask;          /* slots that receive this frame                        */
+    int32_t ref_slot[3];           /* LAST / GOLDEN / ALTREF slots (inter frames)           */
+    int32_t sign_bias[3];
+    int32_t error_res, refresh_ctx, parallel, ctx_id;
+    int32_t allow_hp, interp, comp_mode, tx_mode;
+    uint32_t header_size, compressed_header_size;
+} vp9h_frame_info;
+
+/* Parse one frame (one superframe part) of the stream: the packet, or for
+ * show_existing_frame only `info` (out is left empty). */
+int  vp9h_stream_decode(vp9h_stream *s, const uint8_t *data, size_t size, vp9h_frame *out,
+                        vp9h_frame_info *info);
+
+/* Encoder choices for one frame (vp9h_enc_defaults: the SURVEY 8(d) stream settings). */
+typedef struct vp9h_enc_params {
+    int32_t base_q_idx;
+    int32_t show_existing_frame, show_slot;   /* 1: write a show_existing_frame header only */
+    int32_t show_frame;
+    int32_t error_res;
+    int32_t refresh_mask;          /* -1: keyframes / intra-only all slots, inter slot 0   */
+    int32_t ref_slot[3];
+    int32_t sign_bias[3];          /* default 0, 0, 1: compound prediction allowed          */
+    int32_t refresh_ctx, parallel, ctx_id, reset_ctx;
+    int32_t allow_hp;
+    int32_t interp;                /* -1: fixed if every inter block shares one filter      */
+    int32_t comp_mode;             /* -1: switchable when the packet has compound blocks    */
+    int32_t tx_mode;               /* -1: TX_MODE_SELECT                                    */
+    int32_t prob_updates;          /* 0: none; else the seed of random forward updates      */
+    int32_t keep_modes;            /* 1: code the packet's inter modes, taking the MVs they  */
+                                   /*    predict (NEAREST / NEAR / ZERO); 0: keep the MVs    */
+} vp9h_enc_params;
+void vp9h_enc_defaults(vp9h_enc_params *p);
+
+/*
+ * Write one frame. `coded` (optional) receives the packet exactly as written, which is
+ * what vp9h_stream_decode returns for the bitstream. It differs from `pkt` only where
+ * the syntax cannot say what the packet says:
+ *   - an inter mode whose predicted MV is not the packet's MV becomes NEWMV (keep_modes:
+ *     the mode stays and the MV becomes the predicted one);
+ *   - a low-precision MV difference loses its odd 1/8-pel step (vp9mvs.c:302-318);
+ *   - a skipped inter block takes the largest transform size (vp9block.c:213-215);
+ *   - an inter block <= 8x8 without coefficients becomes skip (vp9block.c:1310-1314);
+ *   - fields the syntax does not carry are zero (intra blocks' MVs / refs / filter,
+ *     single-reference blocks' second MV and reference).
+ */
+int  vp9h_stream_encode(vp9h_stream *s, const vp9h_frame *pkt, const vp9h_enc_params *p,
+                        uint8_t **out, size_t *size, vp9h_frame *coded);
+
+/* Split a superframe into its frames (vp9_superframe_split_bsf,
+ * bsf/vp9_superframe_split.c:40-95): up to cap (offset, size) pairs; returns the frame
+ * count (1 for a plain frame) or a negative error. */
+int  vp9h_superframe_split(const uint8_t *data, size_t size, size_t *offsets, size_t *sizes, int cap);
 
 #ifdef __cplusplus
 }
