@@ -39,6 +39,7 @@ CONFIGS = {
 }
 W, H, BPP, LOG2_TILE_COLS = 3840, 2160, 8, 2
 CONFIG_INDEX = 2               # C3
+CHROMA = {"420": (1, 1), "422": (1, 0), "440": (0, 1), "444": (0, 0)}   # (ss_h, ss_v)
 SEED0 = 0x56503900 + CONFIG_INDEX
 TRAFFIC_PROFILE = "r01e"       # rocprofv3 PMC pass of C3 (tools/profile.sh)
 
@@ -81,6 +82,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--timed-events", action="store_true",
                     help="per-launch HIP events inside the timed steps (no graph replay)")
+    ap.add_argument("--chroma", choices=sorted(CHROMA), default="420",
+                    help="chroma format (profiles 1/3: 422, 440, 444); the BASELINE configs are 4:2:0")
     ap.add_argument("--shard", choices=["frames", "tiles"], default="frames",
                     help="frames: every rank decodes its own stream (weak scaling, default); tiles: all ranks "
                          "decode ONE stream, each its tile columns, pre-LF stripes all-gathered (strong scaling)")
@@ -102,13 +105,14 @@ def main():
         args.frames = nf
     refs = gop_refs(args.frames, gop)
     t0 = time.time()
+    ssh, ssv = CHROMA[args.chroma]
     frames = [v.SynthFrame(v.synth_params(W, H, BPP, seed=frame_seed(rank, i, cidx), log2_tile_cols=LOG2_TILE_COLS,
-                                          inter=int(refs[i] is not None)))
+                                          inter=int(refs[i] is not None), ss_h=ssh, ss_v=ssv))
               for i in range(args.frames)]
     t_gen = time.time() - t0
 
     dev = v.Device(local_rank)
-    dev.configure(W, H, BPP, nbufs=args.frames)
+    dev.configure(W, H, BPP, nbufs=args.frames, ss_h=ssh, ss_v=ssv)
     t0 = time.time()
     dev.stage_batch(frames, list(range(args.frames)), None if gop == 1 else refs)
     t_stage = time.time() - t0
@@ -165,7 +169,7 @@ def main():
     # rocprofv3 PMC pass (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; tools/traffic.py)
     traffic, traffic_src = None, None
     tf = os.path.join(ROOT, "profiles", TRAFFIC_PROFILE, "traffic.json")
-    if os.path.exists(tf) and args.config == "C3":
+    if os.path.exists(tf) and args.config == "C3" and args.chroma == "420":
         per = json.load(open(tf))["per_launch"].get(dom)
         if per:
             traffic, traffic_src = round(per["traffic_bytes"]), "profiles/%s/traffic.json" % TRAFFIC_PROFILE
@@ -194,7 +198,7 @@ def main():
         n = 0
         t0 = time.perf_counter()
         while n < len(frames) and (time.perf_counter() - t0 < args.cpu_seconds or n < 2):
-            out = v.alloc_planes(W, H, BPP)
+            out = v.alloc_planes(W, H, BPP, ssh, ssv)
             r = refs[n]
             oracle.decode_frame(frames[n].pkt, out, None if r is None else [outs[r[0]], outs[r[1]], outs[r[2]]])
             outs[n] = out
@@ -212,9 +216,11 @@ def main():
         "value": round(fps, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8" if BPP == 8 else "u16", "data": "synthetic",
-        "config": {"workload": "%s: %dx%d VP9 Profile-%d %d-bit, %d tile columns, %s, %d frames per GPU per step, "
+        "config": {"workload": "%s: %dx%d VP9 Profile-%d %d-bit%s, %d tile columns, %s, %d frames per GPU per step, "
                                "pass-1 packets resident in HBM"
-                               % (args.config, W, H, 0 if BPP == 8 else 2, BPP, 1 << LOG2_TILE_COLS,
+                               % (args.config, W, H, (0 if BPP == 8 else 2) | (args.chroma != "420"), BPP,
+                                  "" if args.chroma == "420" else " 4:%s:%s" % (args.chroma[1], args.chroma[2]),
+                                  1 << LOG2_TILE_COLS,
                                   "all keyframes" if gop == 1 else "GOPs of key + %d P" % (gop - 1), args.frames),
                    "global_batch": args.frames * world, "frames_per_gpu": args.frames,
                    "parallelism": "frame-sharded x%d (independent %s, no collective)"

@@ -24,7 +24,7 @@
  *   backward adaptation      ff_vp9_adapt_probs, vp9prob.c:25-290
  *   bool coder               vpx_rac.h:34-135; the encoder is the RFC 6386 section 7 one
  *   superframes              bsf/vp9_superframe_split.c:40-95
- * Scope: profiles 0 and 2 (4:2:0, 8/10/12-bit). Profiles 1 / 3 return AVERROR(ENOSYS).
+ * Scope: profiles 0-3 (4:2:0 / 4:2:2 / 4:4:0 / 4:4:4, 8/10/12-bit; RGB parses as 4:4:4).
  * The encoder never sends loop-filter delta updates or segmentation.
  */
 #include <stdlib.h>
@@ -352,7 +352,7 @@ typedef struct Hdr {
 struct vp9h_stream {
     Hdr h;
     SavedCtx ctx[4];
-    struct { int valid, w, h, bpp; } slot[8];
+    struct { int valid, w, h, bpp, ss_h, ss_v; } slot[8];
     int last_keyframe;
     Side *cur;                           /* CUR_FRAME: the last decoded frame */
     Side *segref;                        /* REF_FRAME_SEGMAP */
@@ -1516,16 +1516,29 @@ static void set_qmul_lf(Walk *w)
     }
 }
 
-/* color config (read_colorspace_details, vp9.c:459-517) for 4:2:0 streams */
+/* color config (read_colorspace_details, vp9.c:457-517). Profiles 1 / 3 code the
+ * subsampling (4:2:2 / 4:4:0 / 4:4:4; 8-bit 4:2:0 is refused there, 10/12-bit 4:2:0 in
+ * profile 3 is accepted, as in the reference) or RGB (4:4:4). The encoder writes BT.709
+ * YUV with the packet's subsampling. Returns 0 or -1 (invalid). */
 static int walk_color(Bits *b, Hdr *h, int prof)
 {
     int bits = 0;
     if (prof >= 2) bits = 1 + bits_rw(b, 1, h->bpp == 12);
     h->bpp = 8 + 2 * bits;
-    if (bits_rw(b, 3, 2) == 7) return -2;                        /* sRGB: 4:4:4 only */
+    if (bits_rw(b, 3, 2) == 7) {                                  /* RGB: profiles 1 / 3 only */
+        if (!(prof & 1)) return -1;
+        h->ss_h = h->ss_v = 0;
+        return bits_rw(b, 1, 0) ? -1 : 0;                         /* reserved bit */
+    }
     bits_rw(b, 1, 0);                                             /* color range */
-    if (prof == 1 || prof == 3) return -2;                        /* 4:2:2 / 4:4:0 / 4:4:4 */
-    h->ss_h = h->ss_v = 1;
+    if (prof & 1) {
+        h->ss_h = bits_rw(b, 1, h->ss_h);
+        h->ss_v = bits_rw(b, 1, h->ss_v);
+        if (!bits && h->ss_h && h->ss_v) return -1;               /* YUV 4:2:0 in profile 1 */
+        if (bits_rw(b, 1, 0)) return -1;                          /* reserved bit */
+    } else {
+        h->ss_h = h->ss_v = 1;
+    }
     return 0;
 }
 
@@ -1556,7 +1569,7 @@ static long walk_uncompressed(Walk *w, Bits *b, int *existing)
     int fw, fh;
     if (h->keyframe) {
         if (bits_rw(b, 24, 0x498342) != 0x498342) return -1;     /* sync code */
-        if (walk_color(b, h, prof) < 0) return -2;
+        if (walk_color(b, h, prof) < 0) return -1;
         h->refreshmask = 0xff;
         fw = bits_rw(b, 16, h->w - 1) + 1;
         fh = bits_rw(b, 16, h->h - 1) + 1;
@@ -1567,7 +1580,7 @@ static long walk_uncompressed(Walk *w, Bits *b, int *existing)
         if (h->intraonly) {
             if (bits_rw(b, 24, 0x498342) != 0x498342) return -1;
             if (prof >= 1) {
-                if (walk_color(b, h, prof) < 0) return -2;
+                if (walk_color(b, h, prof) < 0) return -1;
             } else {
                 h->ss_h = h->ss_v = 1;
                 h->bpp = 8;
@@ -1611,9 +1624,14 @@ static long walk_uncompressed(Walk *w, Bits *b, int *existing)
                 else if (h->signbias[0] == h->signbias[2]) { h->fixcompref = 1; h->varcompref[0] = 0; h->varcompref[1] = 2; }
                 else { h->fixcompref = 0; h->varcompref[0] = 1; h->varcompref[1] = 2; }
             }
-            /* the bit depth of an inter frame is its references' */
+            /* the format of an inter frame is its references' (all must match, vp9.c:606-616
+             * via update_size's pixel format) */
             h->bpp = st->slot[h->refidx[0]].bpp;
-            h->ss_h = h->ss_v = 1;
+            h->ss_h = st->slot[h->refidx[0]].ss_h;
+            h->ss_v = st->slot[h->refidx[0]].ss_v;
+            for (int i = 1; i < 3; i++)
+                if (st->slot[h->refidx[i]].bpp != h->bpp || st->slot[h->refidx[i]].ss_h != h->ss_h ||
+                    st->slot[h->refidx[i]].ss_v != h->ss_v) return -1;
         }
     }
     h->w = fw; h->h = fh;
@@ -1989,6 +2007,7 @@ static void end_frame(Walk *w)
     for (int i = 0; i < 8; i++)
         if (h->refreshmask & (1 << i)) {
             st->slot[i].valid = 1; st->slot[i].w = h->w; st->slot[i].h = h->h; st->slot[i].bpp = h->bpp;
+            st->slot[i].ss_h = h->ss_h; st->slot[i].ss_v = h->ss_v;
         }
     side_unref(&st->cur);
     st->cur = w->side;
@@ -2204,18 +2223,18 @@ int vp9h_stream_encode(vp9h_stream *st, const vp9h_frame *pkt, const vp9h_enc_pa
         return 0;
     }
     if (!pkt || ep->base_q_idx < 0 || ep->base_q_idx > 255) return VP9HIP_EINVAL;
-    if (pkt->ss_h != 1 || pkt->ss_v != 1 || (pkt->bpp != 8 && pkt->bpp != 10 && pkt->bpp != 12)) return VP9HIP_ENOSYS;
+    if (pkt->ss_h > 1 || pkt->ss_v > 1 || (pkt->bpp != 8 && pkt->bpp != 10 && pkt->bpp != 12)) return VP9HIP_ENOSYS;
     const int inter = !pkt->keyframe && !pkt->intraonly;
     const int retain = st->segref && (!st->h.seg_enabled || !st->h.seg_update_map);
     const int last_keyframe = h->keyframe, last_invisible = h->invisible;
     /* the frame header this packet needs */
-    h->profile = pkt->bpp > 8 ? 2 : 0;
+    h->profile = (pkt->bpp > 8 ? 2 : 0) | !(pkt->ss_h && pkt->ss_v);   /* profiles 1 / 3: not 4:2:0 */
     h->keyframe = pkt->keyframe;
     h->intraonly = pkt->intraonly && !pkt->keyframe;
     h->invisible = !ep->show_frame;
     if (h->intraonly) h->invisible = 1;                       /* intra_only is coded in hidden frames only */
     h->errorres = ep->error_res;
-    h->w = pkt->width; h->h = pkt->height; h->bpp = pkt->bpp;
+    h->w = pkt->width; h->h = pkt->height; h->bpp = pkt->bpp; h->ss_h = pkt->ss_h; h->ss_v = pkt->ss_v;
     h->refreshctx = ep->refresh_ctx; h->parallel = ep->parallel;
     h->ctxid_raw = ep->ctx_id & 3;
     h->resetctx = ep->reset_ctx & 3;
@@ -2231,7 +2250,8 @@ int vp9h_stream_encode(vp9h_stream *st, const vp9h_frame *pkt, const vp9h_enc_pa
         for (int i = 0; i < 3; i++) {
             h->refidx[i] = ep->ref_slot[i] & 7;
             h->signbias[i] = !!ep->sign_bias[i];
-            if (!st->slot[h->refidx[i]].valid || st->slot[h->refidx[i]].bpp != pkt->bpp) return VP9HIP_EINVAL;
+            if (!st->slot[h->refidx[i]].valid || st->slot[h->refidx[i]].bpp != pkt->bpp ||
+                st->slot[h->refidx[i]].ss_h != pkt->ss_h || st->slot[h->refidx[i]].ss_v != pkt->ss_v) return VP9HIP_EINVAL;
         }
         h->hp = !!ep->allow_hp;
         /* one filter for every inter block: a fixed filter mode, else switchable */

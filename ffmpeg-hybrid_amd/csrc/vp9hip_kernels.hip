@@ -574,10 +574,15 @@ __global__ __launch_bounds__(64 * RWAVES) void k_resid(const RJob *__restrict__ 
 #define PRED_LTAB_LDS 1       // 4x4 / 8x8 formula words: LDS copy (1) or the global table via L1 (0)
 #endif
 #define LP 65            // luma tile pitch
-#define CP 33            // chroma tile pitch (4:2:0)
 #define LT_SIZE (65 * LP)
-#define CT_SIZE (33 * CP)
-#define TILE_ELEMS (LT_SIZE + 2 * CT_SIZE)
+// chroma tile geometry of a subsampling (4:2:0 = Geo<1, 1>): CW x CH pixels per SB,
+// tile pitch CP, CT elements per chroma tile, TILE elements per SB (Y, U, V)
+template <int SSH, int SSV> struct Geo {
+    static constexpr int SH = SSH, SV = SSV;
+    static constexpr int CW = 64 >> SSH, CH = 64 >> SSV, CP = CW + 1, CT = (CH + 1) * CP;
+    static constexpr int TILE = LT_SIZE + 2 * CT;
+};
+typedef Geo<1, 1> G420;
 
 // Lane map of a mixed pass (pass word: first << 14 | c4 << 9 | c8 << 5 | c16 << 2 | c32):
 // lanes [0, 32 c32) serve 32x32 jobs, then 16x16, 8x8, 4x4 -- every group aligned to its
@@ -635,9 +640,31 @@ DEV void load_resid(const JSet &j, const int16_t *__restrict__ resid, PSet &ps)
 // Load the pixels above / left of an SB (and, for inter frames, its interior: the
 // MC prediction + inter residuals) into the LDS tile. All global loads of a batch are
 // issued before any LDS write so their latencies overlap.
-template <typename PIX>
+template <typename PIX, class G>
 DEV void load_sb_tile(const FrameDesc &fd, int sbx, int sby, bool interior, int lane, PIX *tile)
 {
+    if (G::SH != 1 || G::SV != 1) {
+        // 4:2:2 / 4:4:0 / 4:4:4: plain loops (same tile layout, chroma CW x CH)
+        const int lx = sbx * 64, ly = sby * 64, cx = sbx * G::CW, cy = sby * G::CH;
+        const int py = fd.pitch[0], pc = fd.pitch[1];
+        for (int p = 0; p < 3; p++) {
+            const PIX *g = (const PIX *) fd.plane[p];
+            const int pitch = p ? pc : py, x0 = p ? cx : lx, y0 = p ? cy : ly;
+            const int w = p ? G::CW : 64, h = p ? G::CH : 64, tp = p ? G::CP : LP;
+            PIX *t = tile + (p == 0 ? 0 : p == 1 ? LT_SIZE : LT_SIZE + G::CT);
+            if (y0 > 0)
+                for (int i = lane; i <= w; i += 64) t[i] = x0 - 1 + i >= 0 ? g[(size_t) (y0 - 1) * pitch + x0 - 1 + i] : 0;
+            if (x0 > 0)
+                for (int i = lane; i < h; i += 64) t[(i + 1) * tp] = g[(size_t) (y0 + i) * pitch + x0 - 1];
+            if (interior)
+                for (int i = lane; i < w * h; i += 64) {
+                    const int yy = i / w, xx = i - yy * w;
+                    t[(yy + 1) * tp + xx + 1] = g[(size_t) (y0 + yy) * pitch + x0 + xx];
+                }
+        }
+        return;
+    }
+    constexpr int CP = G::CP, CT_SIZE = G::CT;
     const PIX *gy = (const PIX *) fd.plane[0], *gu = (const PIX *) fd.plane[1], *gv = (const PIX *) fd.plane[2];
     const int py = fd.pitch[0], pc = fd.pitch[1];
     const int lx = sbx * 64, ly = sby * 64, cx = sbx * 32, cy = sby * 32;
@@ -693,7 +720,7 @@ DEV void load_sb_tile(const FrameDesc &fd, int sbx, int sby, bool interior, int 
 // One pass of N x N jobs: lane li of group grp predicts column li of its job.
 // One mixed pass: lane li of an n x n job predicts pixel column li (rows 0..n-1); the
 // row loop runs to the pass's largest n (MAXN, unrolled), rows >= n are masked.
-template <int MAXN, typename PIX>
+template <int MAXN, typename PIX, class G>
 DEV void pred_pass(uint32_t w, int lane, PIX *tile, uint16_t *eb, int bd, const PSet &ps, const uint32_t *ltab,
                    const int16_t *__restrict__ resid, const uint32_t *__restrict__ ptab, int dbg)
 {
@@ -704,8 +731,8 @@ DEV void pred_pass(uint32_t w, int lane, PIX *tile, uint16_t *eb, int bd, const 
     const int ts = m.ts, n = 4 << ts, li = m.li;
     const bool act = m.act;
     const int p = PJ_PLANE(jb);
-    const int tpch = p ? CP : LP;
-    PIX *o = tile + PJ_SLOT(jb) * TILE_ELEMS + (p == 0 ? 0 : p == 1 ? LT_SIZE : LT_SIZE + CT_SIZE) +
+    const int tpch = p ? G::CP : LP;
+    PIX *o = tile + PJ_SLOT(jb) * G::TILE + (p == 0 ? 0 : p == 1 ? LT_SIZE : LT_SIZE + G::CT) +
              (PJ_Y4(jb) * 4 + 1) * tpch + PJ_X4(jb) * 4 + 1;
     const int ms = PJ_MSLOT(jb), slot = ms < 9 ? ms : 9;
     const int toff = ts == 0 ? 0 : ts == 1 ? 16 : ts == 2 ? 80 : 336;
@@ -790,22 +817,22 @@ DEV void pred_pass(uint32_t w, int lane, PIX *tile, uint16_t *eb, int bd, const 
     }
 }
 
-template <typename PIX>
+template <typename PIX, class G>
 DEV void run_pass(uint32_t w, int lane, PIX *tile, uint16_t *eb, int bd, const PSet &ps, const uint32_t *ltab,
                   const int16_t *__restrict__ resid, const uint32_t *__restrict__ ptab, int dbg)
 {
     switch (PASS_MAXN(w)) {
-    case 4: pred_pass<4, PIX>(w, lane, tile, eb, bd, ps, ltab, resid, ptab, dbg); break;
-    case 8: pred_pass<8, PIX>(w, lane, tile, eb, bd, ps, ltab, resid, ptab, dbg); break;
-    case 16: pred_pass<16, PIX>(w, lane, tile, eb, bd, ps, ltab, resid, ptab, dbg); break;
-    default: pred_pass<32, PIX>(w, lane, tile, eb, bd, ps, ltab, resid, ptab, dbg); break;
+    case 4: pred_pass<4, PIX, G>(w, lane, tile, eb, bd, ps, ltab, resid, ptab, dbg); break;
+    case 8: pred_pass<8, PIX, G>(w, lane, tile, eb, bd, ps, ltab, resid, ptab, dbg); break;
+    case 16: pred_pass<16, PIX, G>(w, lane, tile, eb, bd, ps, ltab, resid, ptab, dbg); break;
+    default: pred_pass<32, PIX, G>(w, lane, tile, eb, bd, ps, ltab, resid, ptab, dbg); break;
     }
     wave_sync();
 }
 
 // LDS of one k_pred workgroup (one wavefront).
-template <typename PIX> struct PredLds {
-    PIX tile[PRED_K * TILE_ELEMS];
+template <typename PIX, class G> struct PredLds {
+    PIX tile[PRED_K * G::TILE];
     uint16_t eb[256];                 // per job 2n+8 edge pixels
 #if PRED_LTAB_LDS
     uint32_t ltab[10 * 80];           // formula words of 4x4 and 8x8, all slots
@@ -827,10 +854,10 @@ DEV void load_ltab(uint32_t *ltab, const uint32_t *__restrict__ ptab, int lane)
 }
 
 // Intra prediction of one workgroup record (the ltab copy must be loaded).
-template <typename PIX>
+template <typename PIX, class G>
 DEV void pred_wg(const WGRec *wgp, const SBRec *__restrict__ sbs, const PJob *__restrict__ jobs,
                  const uint32_t *__restrict__ passes, const FrameDesc *__restrict__ frames,
-                 const int16_t *__restrict__ resid, const uint32_t *__restrict__ ptab, PredLds<PIX> &S, int lane,
+                 const int16_t *__restrict__ resid, const uint32_t *__restrict__ ptab, PredLds<PIX, G> &S, int lane,
                  int dbg)
 {
     PIX *tile = S.tile;
@@ -851,7 +878,7 @@ DEV void pred_wg(const WGRec *wgp, const SBRec *__restrict__ sbs, const PJob *__
         const uint32_t sbi = __builtin_amdgcn_readfirstlane(wgp->sb[k]);
         if (sbi != 0xffffffffu) {
             const SBRec sb = sbs[sbi];
-            if (!(dbg & 4)) load_sb_tile<PIX>(frames[sb.frame], sb.sbx, sb.sby, sb.flags & 1, lane, tile + k * TILE_ELEMS);
+            if (!(dbg & 4)) load_sb_tile<PIX, G>(frames[sb.frame], sb.sbx, sb.sby, sb.flags & 1, lane, tile + k * G::TILE);
         }
     }
     wave_sync();
@@ -870,11 +897,11 @@ DEV void pred_wg(const WGRec *wgp, const SBRec *__restrict__ sbs, const PJob *__
             const uint32_t w0 = LPW(pi), w1 = LPW(pi + 1);
             load_resid(J, resid, B);
             load_job(LPW(pi + 2), lane, lj, J);
-            run_pass<PIX>(w0, lane, tile, eb, bd, A, ltab, resid, ptab, dbg);
+            run_pass<PIX, G>(w0, lane, tile, eb, bd, A, ltab, resid, ptab, dbg);
             if (pi + 1 >= npass) break;
             load_resid(J, resid, A);
             load_job(LPW(pi + 3), lane, lj, J);
-            run_pass<PIX>(w1, lane, tile, eb, bd, B, ltab, resid, ptab, dbg);
+            run_pass<PIX, G>(w1, lane, tile, eb, bd, B, ltab, resid, ptab, dbg);
         }
     }
 #undef LPW
@@ -888,31 +915,31 @@ DEV void pred_wg(const WGRec *wgp, const SBRec *__restrict__ sbs, const PJob *__
         const SBRec sb = sbs[sbi];
         const FrameDesc &fd = frames[sb.frame];
         for (int p = 0; p < 3; p++) {
-            const int sz = p ? 32 : 64;
+            const int sw = p ? G::CW : 64, sh = p ? G::CH : 64;
             PIX *g = (PIX *) fd.plane[p];
             const int pitch = fd.pitch[p ? 1 : 0];
-            const int x0 = sb.sbx * sz, y0 = sb.sby * sz;
-            const PIX *t = tile + k * TILE_ELEMS + (p == 0 ? 0 : p == 1 ? LT_SIZE : LT_SIZE + CT_SIZE);
-            const int tpch = p ? CP : LP;
-            for (int i = lane; i < sz * sz; i += 64) {
-                const int yy = i / sz, xx = i - yy * sz;
+            const int x0 = sb.sbx * sw, y0 = sb.sby * sh;
+            const PIX *t = tile + k * G::TILE + (p == 0 ? 0 : p == 1 ? LT_SIZE : LT_SIZE + G::CT);
+            const int tpch = p ? G::CP : LP;
+            for (int i = lane; i < sw * sh; i += 64) {
+                const int yy = i / sw, xx = i - yy * sw;
                 g[(size_t) (y0 + yy) * pitch + x0 + xx] = t[(yy + 1) * tpch + xx + 1];
             }
         }
     }
 }
 
-template <typename PIX>
+template <typename PIX, class G>
 __global__ __launch_bounds__(64) void k_pred(const uint32_t *__restrict__ list, const WGRec *__restrict__ wgs,
                                              const SBRec *__restrict__ sbs, const PJob *__restrict__ jobs,
                                              const uint32_t *__restrict__ passes, const FrameDesc *__restrict__ frames,
                                              const int16_t *__restrict__ resid, const uint32_t *__restrict__ ptab, int dbg)
 {
-    __shared__ PredLds<PIX> S;
+    __shared__ PredLds<PIX, G> S;
 #if PRED_LTAB_LDS
     load_ltab<PIX>(S.ltab, ptab, threadIdx.x);
 #endif
-    pred_wg<PIX>(wgs + list[blockIdx.x], sbs, jobs, passes, frames, resid, ptab, S, threadIdx.x, dbg);
+    pred_wg<PIX, G>(wgs + list[blockIdx.x], sbs, jobs, passes, frames, resid, ptab, S, threadIdx.x, dbg);
 }
 
 // 8-pixel chunk <-> 8 uint16 of the LF tile (tile rows are 4-byte aligned)
@@ -939,11 +966,25 @@ template <> struct Chunk8<uint16_t> {
     }
 };
 
-// chunk index -> (plane, tile row, chunk column): luma 72 rows x 9, then U, V 40 x 5
-DEV void lf_chunk(int ci, int &p, int &r, int &k)
+// LF tile geometry: luma 72 x 72 (x, y = -8..63), chroma (CW + 8) x (CH + 8); pitches in
+// pixels, rows dword-aligned with an odd dword count (lanes of the column pass read
+// dword i of consecutive rows: no bank conflicts)
+template <typename PIX, class G> struct LfP {
+    static constexpr int YP = sizeof(PIX) == 1 ? 76 : 74;
+    static constexpr int UVP = G::CW + 8 + (sizeof(PIX) == 1 ? 4 : 2);
+    static constexpr int PPW = 4 / sizeof(PIX);     // pixels per dword
+    static constexpr int CK = G::CW / 8 + 1;        // 8-pixel chunks per chroma tile row
+    static constexpr int CR = G::CH + 8;            // chroma tile rows
+    static constexpr int NCHUNK = 648 + 2 * CR * CK;
+    static constexpr int PROG = LF_PROG_OF(G::SH, G::SV);
+};
+
+// chunk index -> (plane, tile row, chunk column): luma 72 rows x 9, then U, V CR x CK
+template <typename PIX, class G> DEV void lf_chunk(int ci, int &p, int &r, int &k)
 {
+    typedef LfP<PIX, G> L;
     if (ci < 648) { p = 0; r = ci / 9; k = ci - r * 9; }
-    else { const int c = ci - 648; p = 1 + (c >= 200); const int cc = c - (p - 1) * 200; r = cc / 5; k = cc - r * 5; }
+    else { const int c = ci - 648; p = 1 + (c >= L::CR * L::CK); const int cc = c - (p - 1) * L::CR * L::CK; r = cc / L::CK; k = cc - r * L::CK; }
 }
 
 // --------------------------------------------------------------- k_lf
@@ -1021,39 +1062,114 @@ DEV void lf_reg(int (&px)[NPX], int code, uint32_t eih, int bd)
     }
 }
 
-// LF tile pitches in pixels: 72 / 40 used, rows dword-aligned with an odd dword count
-// (lanes of the column pass read dword i of consecutive rows: no bank conflicts)
-template <typename PIX> struct LfP {
-    static constexpr int YP = sizeof(PIX) == 1 ? 76 : 74, UVP = sizeof(PIX) == 1 ? 44 : 42;
-    static constexpr int PPW = 4 / sizeof(PIX);     // pixels per dword
-};
 template <typename PIX, int N> DEV void lf_unpack(const uint32_t *w, int (&px)[N], int i0, int i1, int o)
 {
+    constexpr int PPW = 4 / sizeof(PIX);
 #pragma unroll
     for (int i = i0; i < i1; i++)
 #pragma unroll
-        for (int j = 0; j < LfP<PIX>::PPW; j++)
-            px[o + (i - i0) * LfP<PIX>::PPW + j] = (w[i] >> (8 * sizeof(PIX) * j)) & ((1u << (8 * sizeof(PIX))) - 1);
+        for (int j = 0; j < PPW; j++)
+            px[o + (i - i0) * PPW + j] = (w[i] >> (8 * sizeof(PIX) * j)) & ((1u << (8 * sizeof(PIX))) - 1);
 }
 template <typename PIX, int N> DEV void lf_pack(uint32_t *w, const int (&px)[N], int i0, int i1, int o)
 {
+    constexpr int PPW = 4 / sizeof(PIX);
 #pragma unroll
     for (int i = i0; i < i1; i++) {
         uint32_t v = 0;
 #pragma unroll
-        for (int j = 0; j < LfP<PIX>::PPW; j++) v |= (uint32_t) px[o + (i - i0) * LfP<PIX>::PPW + j] << (8 * sizeof(PIX) * j);
+        for (int j = 0; j < PPW; j++) v |= (uint32_t) px[o + (i - i0) * PPW + j] << (8 * sizeof(PIX) * j);
         w[i] = v;
     }
 }
 
-// One SB of loop filter by NT threads (128: two waves, luma / chroma in parallel; 64: one
-// wave, luma then chroma). Same arithmetic and edge order either way (planes are
-// independent, vp9lpf.c:183-230).
-template <typename PIX> struct LfLds {
-    PIX lt[72 * LfP<PIX>::YP];
-    PIX ct[2][40 * LfP<PIX>::UVP];
-    uint32_t prog[LF_PROG_BYTES / 4];     // the SB's edge decisions (LFRec.prog)
-    uint32_t lut[64];                     // level -> E | I << 12 | H << 22
+// Edge chains of one line held in registers (vp9lpf.c:31-181 order), program words pw
+// of the line's band. "wide": a 64-pixel plane dimension, line x = -8..63, 8 edges 8
+// apart each with an inner 4-wide edge, processed in two 40-pixel register halves
+// (an edge touches 8 pixels either side: x = -8..31 for edges 0-3, then x = 24..63 for
+// edges 4-7, x = 24..31 carried over). "narrow": a subsampled 32-pixel chroma dimension,
+// x = -8..31, 8 edges 4 apart.
+#define LF_EDGE_WIDE(k, C0)                                                                              \
+    {                                                                                                    \
+        const uint32_t ww = (k) < 2 ? pw0 : (k) < 4 ? pw1 : (k) < 6 ? pw2 : pw3;                         \
+        const uint32_t m = (ww >> (16 * ((k) & 1))) & 255, in = (ww >> (16 * ((k) & 1) + 8)) & 255;      \
+        if (m >> 6) lf_reg<8 * (k) + 8 - (C0)>(px, m >> 6, lut[m & 63], bd);                             \
+        if (in) lf_reg<8 * (k) + 12 - (C0)>(px, 1, lut[in & 63], bd);                                    \
+    }
+#define LF_EDGE_NARROW(k)                                                                                \
+    {                                                                                                    \
+        const uint32_t m = (((k) < 4 ? pc0 : pc1) >> (8 * ((k) & 3))) & 255;                             \
+        if (m >> 6) lf_reg<4 * (k) + 8>(px, m >> 6, lut[m & 63], bd);                                    \
+    }
+// column edges of one pixel row (packed dwords in LDS)
+template <typename PIX>
+DEV void lf_line_row_wide(uint32_t *rowp, const uint32_t *pw, const uint32_t *lut, int bd)
+{
+    constexpr int PPW = 4 / sizeof(PIX);
+    const uint32_t pw0 = pw[0], pw1 = pw[1], pw2 = pw[2], pw3 = pw[3];
+    int px[40];
+    lf_unpack<PIX>(rowp, px, 0, 40 / PPW, 0);
+    LF_EDGE_WIDE(0, 0) LF_EDGE_WIDE(1, 0) LF_EDGE_WIDE(2, 0) LF_EDGE_WIDE(3, 0)
+    lf_pack<PIX>(rowp, px, 0, 32 / PPW, 0);
+#pragma unroll
+    for (int i = 0; i < 8; i++) px[i] = px[32 + i];
+    lf_unpack<PIX>(rowp, px, 40 / PPW, 72 / PPW, 8);
+    LF_EDGE_WIDE(4, 32) LF_EDGE_WIDE(5, 32) LF_EDGE_WIDE(6, 32) LF_EDGE_WIDE(7, 32)
+    lf_pack<PIX>(rowp, px, 32 / PPW, 72 / PPW, 0);
+}
+template <typename PIX>
+DEV void lf_line_row_narrow(uint32_t *rowp, const uint32_t *pw, const uint32_t *lut, int bd)
+{
+    constexpr int PPW = 4 / sizeof(PIX);
+    int px[40];
+    lf_unpack<PIX>(rowp, px, 0, 40 / PPW, 0);
+    const uint32_t pc0 = pw[0], pc1 = pw[1];
+    LF_EDGE_NARROW(0) LF_EDGE_NARROW(1) LF_EDGE_NARROW(2) LF_EDGE_NARROW(3)
+    LF_EDGE_NARROW(4) LF_EDGE_NARROW(5) LF_EDGE_NARROW(6) LF_EDGE_NARROW(7)
+    lf_pack<PIX>(rowp, px, 0, 40 / PPW, 0);
+}
+// row edges of one pixel column (tile pitch P)
+template <typename PIX, int P>
+DEV void lf_line_col_wide(PIX *colp, const uint32_t *pw, const uint32_t *lut, int bd)
+{
+    int px[40];                    // rows -8..31, then 24..63 (as the column pass)
+#pragma unroll
+    for (int i = 0; i < 40; i++) px[i] = colp[i * P];
+    const uint32_t pw0 = pw[0], pw1 = pw[1], pw2 = pw[2], pw3 = pw[3];
+    LF_EDGE_WIDE(0, 0) LF_EDGE_WIDE(1, 0) LF_EDGE_WIDE(2, 0) LF_EDGE_WIDE(3, 0)
+#pragma unroll
+    for (int i = 1; i < 32; i++) colp[i * P] = (PIX) px[i];
+#pragma unroll
+    for (int i = 0; i < 8; i++) px[i] = px[32 + i];
+#pragma unroll
+    for (int i = 8; i < 40; i++) px[i] = colp[(32 + i) * P];
+    LF_EDGE_WIDE(4, 32) LF_EDGE_WIDE(5, 32) LF_EDGE_WIDE(6, 32) LF_EDGE_WIDE(7, 32)
+#pragma unroll
+    for (int i = 0; i < 40; i++) colp[(32 + i) * P] = (PIX) px[i];
+}
+template <typename PIX, int P>
+DEV void lf_line_col_narrow(PIX *colp, const uint32_t *pw, const uint32_t *lut, int bd)
+{
+    int px[40];
+#pragma unroll
+    for (int i = 0; i < 40; i++) px[i] = colp[i * P];
+    const uint32_t pc0 = pw[0], pc1 = pw[1];
+    LF_EDGE_NARROW(0) LF_EDGE_NARROW(1) LF_EDGE_NARROW(2) LF_EDGE_NARROW(3)
+    LF_EDGE_NARROW(4) LF_EDGE_NARROW(5) LF_EDGE_NARROW(6) LF_EDGE_NARROW(7)
+#pragma unroll
+    for (int i = 1; i < 40; i++) colp[i * P] = (PIX) px[i];
+}
+#undef LF_EDGE_WIDE
+#undef LF_EDGE_NARROW
+
+// One SB of loop filter by NT threads (128 for 4:2:0: luma and chroma lines in parallel).
+// Planes are independent (vp9lpf.c:183-230), so lanes take luma and chroma lines
+// together; each plane filters all column edges, then all row edges.
+template <typename PIX, class G> struct LfLds {
+    PIX lt[72 * LfP<PIX, G>::YP];
+    PIX ct[2][LfP<PIX, G>::CR * LfP<PIX, G>::UVP];
+    uint32_t prog[LfP<PIX, G>::PROG / 4];    // the SB's edge decisions (LFRec.prog)
+    uint32_t lut[64];                         // level -> E | I << 12 | H << 22
 };
 
 // E / I / H of a filter level (vp9.c:669-687 limit LUTs; loop_filter's F / E / I / H
@@ -1067,42 +1183,43 @@ DEV uint32_t lf_eih(int L, int sharp, int bd)
     return E | I << 12 | H << 22;
 }
 
-template <typename PIX, int NT>
-DEV void lf_sb(const LFRec &rec, const FrameDesc *__restrict__ frames, LfLds<PIX> &S, int lane, int dbg)
+template <typename PIX, class G, int NT>
+DEV void lf_sb(const LFRec &rec, const FrameDesc *__restrict__ frames, LfLds<PIX, G> &S, int lane, int dbg)
 {
 #define LF_SYNC() do { if (NT == 64) wave_sync(); else __syncthreads(); } while (0)
-    constexpr int FLP = LfP<PIX>::YP, FCP = LfP<PIX>::UVP, PPW = LfP<PIX>::PPW;
+    typedef LfP<PIX, G> L;
+    constexpr int FLP = L::YP, FCP = L::UVP, CW = G::CW, CH = G::CH;
     PIX *lt = S.lt;
-    PIX (*ct)[40 * FCP] = S.ct;
+    PIX (*ct)[L::CR * FCP] = S.ct;
     const uint32_t *lut = S.lut;
     const FrameDesc &fd = frames[rec.frame];
     const int bd = fd.bd, sharp = fd.sharp;
     const int sbx = rec.sbx, sby = rec.sby;
-    for (int i = lane; i < LF_PROG_BYTES / 4; i += NT) S.prog[i] = ((const uint32_t *) rec.prog)[i];
+    for (int i = lane; i < L::PROG / 4; i += NT) S.prog[i] = ((const uint32_t *) rec.prog)[i];
     for (int i = lane; i < 64; i += NT) S.lut[i] = lf_eih(i, sharp, bd);
 
-    // load: luma rows [y0-8, y0+64) x cols [x0-8, x0+64), chroma [-8, 32), in aligned
-    // 8-pixel chunks (luma 72 x 9, chroma 2 x 40 x 5 = 1048 chunks, <= 9 per thread), all
-    // global loads of a thread in flight before its LDS writes
+    // load: luma rows [y0-8, y0+64) x cols [x0-8, x0+64), chroma [-8, CH) x [-8, CW), in
+    // aligned 8-pixel chunks (4:2:0: luma 72 x 9, chroma 2 x 40 x 5 = 1048 chunks, <= 9 per
+    // thread), all global loads of a thread in flight before its LDS writes
     typedef typename Chunk8<PIX>::T CT;
-    constexpr int NU = (1048 + NT - 1) / NT;
+    constexpr int NU = (L::NCHUNK + NT - 1) / NT;
     CT v[NU];
 #pragma unroll
     for (int u = 0; u < NU; u++) {
         const int ci = lane + u * NT;
         int p, r, k;
-        lf_chunk(ci, p, r, k);
-        const int gx = (p ? sbx * 32 : sbx * 64) - 8 + 8 * k, gy = (p ? sby * 32 : sby * 64) - 8 + r;
+        lf_chunk<PIX, G>(ci, p, r, k);
+        const int gx = (p ? sbx * CW : sbx * 64) - 8 + 8 * k, gy = (p ? sby * CH : sby * 64) - 8 + r;
         v[u] = Chunk8<PIX>::zero();
-        if (!(dbg & 4) && ci < 1048 && gx >= 0 && gy >= 0)
+        if (!(dbg & 4) && ci < L::NCHUNK && gx >= 0 && gy >= 0)
             v[u] = *(const CT *) ((const PIX *) fd.plane[p] + (size_t) gy * fd.pitch[p ? 1 : 0] + gx);
     }
 #pragma unroll
     for (int u = 0; u < NU; u++) {
         const int ci = lane + u * NT;
         int p, r, k;
-        lf_chunk(ci, p, r, k);
-        if (ci < 1048) {
+        lf_chunk<PIX, G>(ci, p, r, k);
+        if (ci < L::NCHUNK) {
             PIX *t = p ? ct[p - 1] + r * FCP : lt + r * FLP;
             Chunk8<PIX>::to_lds(v[u], t + 8 * k);
         }
@@ -1110,114 +1227,43 @@ DEV void lf_sb(const LFRec &rec, const FrameDesc *__restrict__ frames, LfLds<PIX
     LF_SYNC();
 
     if (!(dbg & 1)) {
-    // ---- column edges (filter_plane_cols, vp9lpf.c:31-104): one lane per pixel row, the
-    //      row in registers (luma x = -8..63, chroma x = -8..31), edges left to right ----
-    for (int tid = lane; tid < 128; tid += NT) {
-    if (tid < 64) {
-        const int r = tid;
-        uint32_t *rowp = (uint32_t *) (lt + (r + 8) * FLP);      // 72 pixels: 72 / PPW dwords
-        // edge bytes of this row's band: (main, inner) for edges 0..7
-        const uint32_t *pw = S.prog + (LFP_YC + (r >> 3) * 16) / 4;
-        const uint32_t pw0 = pw[0], pw1 = pw[1], pw2 = pw[2], pw3 = pw[3];
-        // the row in two register halves (an edge touches 8 pixels either side): x = -8..31
-        // for edges 0-3, then x = 24..63 for edges 4-7 (x = 24..31 carried over)
-        int px[40];
-        lf_unpack<PIX>(rowp, px, 0, 40 / PPW, 0);
-#define LF_COL_EDGE(k, C0)                                                                               \
-        {                                                                                                \
-            const uint32_t ww = (k) < 2 ? pw0 : (k) < 4 ? pw1 : (k) < 6 ? pw2 : pw3;                     \
-            const uint32_t m = (ww >> (16 * ((k) & 1))) & 255, in = (ww >> (16 * ((k) & 1) + 8)) & 255;  \
-            if (m >> 6) lf_reg<8 * (k) + 8 - (C0)>(px, m >> 6, lut[m & 63], bd);                         \
-            if (in) lf_reg<8 * (k) + 12 - (C0)>(px, 1, lut[in & 63], bd);                                \
+    // ---- column edges (filter_plane_cols, vp9lpf.c:31-104): one lane per pixel row ----
+    for (int tid = lane; tid < 64 + 2 * CH; tid += NT) {
+        if (tid < 64) {
+            lf_line_row_wide<PIX>((uint32_t *) (lt + (tid + 8) * FLP), S.prog + (LFP_YC + (tid >> 3) * 16) / 4, lut, bd);
+        } else {
+            const int p = 1 + (tid - 64 >= CH), r = tid - 64 - (p - 1) * CH;
+            uint32_t *rowp = (uint32_t *) (ct[p - 1] + (r + 8) * FCP);
+            const uint32_t *pw = S.prog + (LFP_CC + (r >> 3) * LFP_CSTRIDE(G::SH)) / 4;
+            if (G::SH) lf_line_row_narrow<PIX>(rowp, pw, lut, bd);
+            else lf_line_row_wide<PIX>(rowp, pw, lut, bd);
         }
-        LF_COL_EDGE(0, 0) LF_COL_EDGE(1, 0) LF_COL_EDGE(2, 0) LF_COL_EDGE(3, 0)
-        lf_pack<PIX>(rowp, px, 0, 32 / PPW, 0);
-#pragma unroll
-        for (int i = 0; i < 8; i++) px[i] = px[32 + i];
-        lf_unpack<PIX>(rowp, px, 40 / PPW, 72 / PPW, 8);
-        LF_COL_EDGE(4, 32) LF_COL_EDGE(5, 32) LF_COL_EDGE(6, 32) LF_COL_EDGE(7, 32)
-#undef LF_COL_EDGE
-        lf_pack<PIX>(rowp, px, 32 / PPW, 72 / PPW, 0);
-    } else {
-        const int p = 1 + ((tid - 64) >> 5), r = (tid - 64) & 31;
-        uint32_t *rowp = (uint32_t *) (ct[p - 1] + (r + 8) * FCP);
-        int px[40];
-        lf_unpack<PIX>(rowp, px, 0, 40 / PPW, 0);
-        const uint32_t *pw = S.prog + (LFP_CC + (r >> 3) * 8) / 4;
-        const uint32_t pc0 = pw[0], pc1 = pw[1];
-#define LF_COL_EDGE_UV(k)                                                                                \
-        {                                                                                                \
-            const uint32_t m = (((k) < 4 ? pc0 : pc1) >> (8 * ((k) & 3))) & 255;                         \
-            if (m >> 6) lf_reg<4 * (k) + 8>(px, m >> 6, lut[m & 63], bd);                                \
-        }
-        LF_COL_EDGE_UV(0) LF_COL_EDGE_UV(1) LF_COL_EDGE_UV(2) LF_COL_EDGE_UV(3)
-        LF_COL_EDGE_UV(4) LF_COL_EDGE_UV(5) LF_COL_EDGE_UV(6) LF_COL_EDGE_UV(7)
-#undef LF_COL_EDGE_UV
-        lf_pack<PIX>(rowp, px, 0, 40 / PPW, 0);
-    }
     }
     LF_SYNC();
-    // ---- row edges (filter_plane_rows, vp9lpf.c:106-181): one lane per pixel column, the
-    //      column in registers (rows -8..63 / -8..31), edges top to bottom ----
-    for (int tid = lane; tid < 128; tid += NT) {
-    if (tid < 64) {
-        const int c = tid;
-        PIX *colp = lt + 8 + c;
-        int px[40];                    // rows -8..31, then 24..63 (as the column pass)
-#pragma unroll
-        for (int i = 0; i < 40; i++) px[i] = colp[i * FLP];
-        const uint32_t *pw = S.prog + (LFP_YR + (c >> 3) * 16) / 4;
-        const uint32_t pw0 = pw[0], pw1 = pw[1], pw2 = pw[2], pw3 = pw[3];
-#define LF_ROW_EDGE(yy, C0)                                                                              \
-        {                                                                                                \
-            const uint32_t ww = (yy) < 2 ? pw0 : (yy) < 4 ? pw1 : (yy) < 6 ? pw2 : pw3;                  \
-            const uint32_t m = (ww >> (16 * ((yy) & 1))) & 255, in = (ww >> (16 * ((yy) & 1) + 8)) & 255; \
-            if (m >> 6) lf_reg<8 * (yy) + 8 - (C0)>(px, m >> 6, lut[m & 63], bd);                        \
-            if (in) lf_reg<8 * (yy) + 12 - (C0)>(px, 1, lut[in & 63], bd);                               \
+    // ---- row edges (filter_plane_rows, vp9lpf.c:106-181): one lane per pixel column ----
+    for (int tid = lane; tid < 64 + 2 * CW; tid += NT) {
+        if (tid < 64) {
+            lf_line_col_wide<PIX, FLP>(lt + 8 + tid, S.prog + (LFP_YR + (tid >> 3) * 16) / 4, lut, bd);
+        } else {
+            const int p = 1 + (tid - 64 >= CW), c = tid - 64 - (p - 1) * CW;
+            PIX *colp = ct[p - 1] + 8 + c;
+            const uint32_t *pw = S.prog + (LFP_CR(G::SH, G::SV) + (c >> 3) * LFP_CSTRIDE(G::SV)) / 4;
+            if (G::SV) lf_line_col_narrow<PIX, FCP>(colp, pw, lut, bd);
+            else lf_line_col_wide<PIX, FCP>(colp, pw, lut, bd);
         }
-        LF_ROW_EDGE(0, 0) LF_ROW_EDGE(1, 0) LF_ROW_EDGE(2, 0) LF_ROW_EDGE(3, 0)
-#pragma unroll
-        for (int i = 1; i < 32; i++) colp[i * FLP] = (PIX) px[i];
-#pragma unroll
-        for (int i = 0; i < 8; i++) px[i] = px[32 + i];
-#pragma unroll
-        for (int i = 8; i < 40; i++) px[i] = colp[(32 + i) * FLP];
-        LF_ROW_EDGE(4, 32) LF_ROW_EDGE(5, 32) LF_ROW_EDGE(6, 32) LF_ROW_EDGE(7, 32)
-#undef LF_ROW_EDGE
-#pragma unroll
-        for (int i = 0; i < 40; i++) colp[(32 + i) * FLP] = (PIX) px[i];
-    } else {
-        const int p = 1 + ((tid - 64) >> 5), c = (tid - 64) & 31;
-        PIX *colp = ct[p - 1] + 8 + c;
-        int px[40];
-#pragma unroll
-        for (int i = 0; i < 40; i++) px[i] = colp[i * FCP];
-        const uint32_t *pw = S.prog + (LFP_CR + (c >> 3) * 8) / 4;
-        const uint32_t pc0 = pw[0], pc1 = pw[1];
-#define LF_ROW_EDGE_UV(yy)                                                                               \
-        {                                                                                                \
-            const uint32_t m = (((yy) < 4 ? pc0 : pc1) >> (8 * ((yy) & 3))) & 255;                       \
-            if (m >> 6) lf_reg<4 * (yy) + 8>(px, m >> 6, lut[m & 63], bd);                               \
-        }
-        LF_ROW_EDGE_UV(0) LF_ROW_EDGE_UV(1) LF_ROW_EDGE_UV(2) LF_ROW_EDGE_UV(3)
-        LF_ROW_EDGE_UV(4) LF_ROW_EDGE_UV(5) LF_ROW_EDGE_UV(6) LF_ROW_EDGE_UV(7)
-#undef LF_ROW_EDGE_UV
-#pragma unroll
-        for (int i = 1; i < 40; i++) colp[i * FCP] = (PIX) px[i];
-    }
     }
     LF_SYNC();
     }
-    // ---- store the modified region: rows [0,sz) x cols [-8,sz) and rows [-8,0) x cols [0,sz).
+    // ---- store the modified region: rows [0,h) x cols [-8,w) and rows [-8,0) x cols [0,w).
     // Other SBs of the same wavefront step never touch this region, so whole chunks are
     // written back (pixels beyond the 8-aligned frame size are unchanged padding). ----
 #pragma unroll
     for (int u = 0; u < NU; u++) {
         const int ci = lane + u * NT;
         int p, r, k;
-        lf_chunk(ci, p, r, k);
-        const int gx = (p ? sbx * 32 : sbx * 64) - 8 + 8 * k, gy = (p ? sby * 32 : sby * 64) - 8 + r;
-        if (!(dbg & 2) && ci < 1048 && gx >= 0 && gy >= 0 && (r >= 8 || k > 0)) {
+        lf_chunk<PIX, G>(ci, p, r, k);
+        const int gx = (p ? sbx * CW : sbx * 64) - 8 + 8 * k, gy = (p ? sby * CH : sby * 64) - 8 + r;
+        if (!(dbg & 2) && ci < L::NCHUNK && gx >= 0 && gy >= 0 && (r >= 8 || k > 0)) {
             const PIX *t = p ? ct[p - 1] + r * FCP : lt + r * FLP;
             *(CT *) ((PIX *) fd.plane[p] + (size_t) gy * fd.pitch[p ? 1 : 0] + gx) = Chunk8<PIX>::from_lds(t + 8 * k);
         }
@@ -1225,12 +1271,15 @@ DEV void lf_sb(const LFRec &rec, const FrameDesc *__restrict__ frames, LfLds<PIX
 #undef LF_SYNC
 }
 
-template <typename PIX>
-__global__ __launch_bounds__(128) void k_lf(const uint32_t *__restrict__ list, const LFRec *__restrict__ recs,
-                                            const FrameDesc *__restrict__ frames, int dbg)
+// threads per k_lf workgroup: 128 for 4:2:0, 192 when a chroma dimension is 64
+template <class G> struct LfNT { static constexpr int NT = (G::SH && G::SV) ? 128 : 192; };
+
+template <typename PIX, class G>
+__global__ __launch_bounds__(LfNT<G>::NT) void k_lf(const uint32_t *__restrict__ list, const LFRec *__restrict__ recs,
+                                                    const FrameDesc *__restrict__ frames, int dbg)
 {
-    __shared__ LfLds<PIX> S;
-    lf_sb<PIX, 128>(recs[list[blockIdx.x]], frames, S, threadIdx.x, dbg);
+    __shared__ LfLds<PIX, G> S;
+    lf_sb<PIX, G, LfNT<G>::NT>(recs[list[blockIdx.x]], frames, S, threadIdx.x, dbg);
 }
 
 // --------------------------------------------------------------- k_mc
@@ -1313,6 +1362,41 @@ static void launch_resid_n(int hb, hipStream_t st, int n, const RJob *jobs, cons
         hipLaunchKernelGGL((k_resid<N, TC, uint8_t, M32, int16_t>), dim3(nb), dim3(64 * RWAVES), 0, st,
                            jobs, n, frames, (const int16_t *) coefs, resid);
 }
+template <typename PIX, class G>
+static void launch_pred_g(hipStream_t st, int nwg, size_t pad, const uint32_t *list, const WGRec *wgs, const SBRec *sbs,
+                          const PJob *jobs, const uint32_t *passes, const FrameDesc *frames, const int16_t *resid,
+                          const uint32_t *ptab, int dbg)
+{
+    hipLaunchKernelGGL((k_pred<PIX, G>), dim3(nwg), dim3(64), pad, st, list, wgs, sbs, jobs, passes, frames, resid, ptab, dbg);
+}
+template <typename PIX>
+static void launch_pred_p(int ss, hipStream_t st, int nwg, size_t pad, const uint32_t *list, const WGRec *wgs,
+                          const SBRec *sbs, const PJob *jobs, const uint32_t *passes, const FrameDesc *frames,
+                          const int16_t *resid, const uint32_t *ptab, int dbg)
+{
+    switch (ss) {
+    case 3: launch_pred_g<PIX, Geo<1, 1>>(st, nwg, pad, list, wgs, sbs, jobs, passes, frames, resid, ptab, dbg); break;
+    case 1: launch_pred_g<PIX, Geo<1, 0>>(st, nwg, pad, list, wgs, sbs, jobs, passes, frames, resid, ptab, dbg); break;
+    case 2: launch_pred_g<PIX, Geo<0, 1>>(st, nwg, pad, list, wgs, sbs, jobs, passes, frames, resid, ptab, dbg); break;
+    default: launch_pred_g<PIX, Geo<0, 0>>(st, nwg, pad, list, wgs, sbs, jobs, passes, frames, resid, ptab, dbg); break;
+    }
+}
+template <typename PIX, class G>
+static void launch_lf_g(hipStream_t st, int nsb, const uint32_t *list, const LFRec *recs, const FrameDesc *frames, int dbg)
+{
+    hipLaunchKernelGGL((k_lf<PIX, G>), dim3(nsb), dim3(LfNT<G>::NT), 0, st, list, recs, frames, dbg);
+}
+template <typename PIX>
+static void launch_lf_p(int ss, hipStream_t st, int nsb, const uint32_t *list, const LFRec *recs, const FrameDesc *frames,
+                        int dbg)
+{
+    switch (ss) {
+    case 3: launch_lf_g<PIX, Geo<1, 1>>(st, nsb, list, recs, frames, dbg); break;
+    case 1: launch_lf_g<PIX, Geo<1, 0>>(st, nsb, list, recs, frames, dbg); break;
+    case 2: launch_lf_g<PIX, Geo<0, 1>>(st, nsb, list, recs, frames, dbg); break;
+    default: launch_lf_g<PIX, Geo<0, 0>>(st, nsb, list, recs, frames, dbg); break;
+    }
+}
 extern "C" {
 int vp9hip_launch_resid(int hb, hipStream_t st, int tcode, int n, const RJob *jobs, const FrameDesc *frames,
                         const void *coefs, int16_t *resid)
@@ -1328,22 +1412,23 @@ int vp9hip_launch_resid(int hb, hipStream_t st, int tcode, int n, const RJob *jo
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
-int vp9hip_launch_pred(int hb, hipStream_t st, int nwg, const uint32_t *list, const WGRec *wgs, const SBRec *sbs,
+// fmt: bit 0 high bit depth, bit 1 ss_h, bit 2 ss_v
+int vp9hip_launch_pred(int fmt, hipStream_t st, int nwg, const uint32_t *list, const WGRec *wgs, const SBRec *sbs,
                        const PJob *jobs, const uint32_t *passes, const FrameDesc *frames, const int16_t *resid,
                        const uint32_t *ptab, int dbg)
 {
     if (nwg <= 0) return 0;
     const size_t pad = (size_t) ((dbg >> 8) & 255) * 1024;     // profiling: occupancy sweep via LDS padding
-    if (hb) hipLaunchKernelGGL(k_pred<uint16_t>, dim3(nwg), dim3(64), pad, st, list, wgs, sbs, jobs, passes, frames, resid, ptab, dbg);
-    else    hipLaunchKernelGGL(k_pred<uint8_t>, dim3(nwg), dim3(64), pad, st, list, wgs, sbs, jobs, passes, frames, resid, ptab, dbg);
+    if (fmt & 1) launch_pred_p<uint16_t>(fmt >> 1, st, nwg, pad, list, wgs, sbs, jobs, passes, frames, resid, ptab, dbg);
+    else         launch_pred_p<uint8_t>(fmt >> 1, st, nwg, pad, list, wgs, sbs, jobs, passes, frames, resid, ptab, dbg);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
-int vp9hip_launch_lf(int hb, hipStream_t st, int nsb, const uint32_t *list, const LFRec *recs,
+int vp9hip_launch_lf(int fmt, hipStream_t st, int nsb, const uint32_t *list, const LFRec *recs,
                      const FrameDesc *frames, int dbg)
 {
     if (nsb <= 0) return 0;
-    if (hb) hipLaunchKernelGGL(k_lf<uint16_t>, dim3(nsb), dim3(128), 0, st, list, recs, frames, dbg);
-    else    hipLaunchKernelGGL(k_lf<uint8_t>, dim3(nsb), dim3(128), 0, st, list, recs, frames, dbg);
+    if (fmt & 1) launch_lf_p<uint16_t>(fmt >> 1, st, nsb, list, recs, frames, dbg);
+    else         launch_lf_p<uint8_t>(fmt >> 1, st, nsb, list, recs, frames, dbg);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int vp9hip_launch_mc(int hb, hipStream_t st, int n, const McUnit *units, const FrameDesc *frames)

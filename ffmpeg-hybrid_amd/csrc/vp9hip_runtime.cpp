@@ -36,10 +36,10 @@
 extern "C" {
 int vp9hip_launch_resid(int hb, hipStream_t st, int tcode, int n, const RJob *jobs, const FrameDesc *frames,
                         const void *coefs, int16_t *resid);
-int vp9hip_launch_pred(int hb, hipStream_t st, int nwg, const uint32_t *list, const WGRec *wgs, const SBRec *sbs,
+int vp9hip_launch_pred(int fmt, hipStream_t st, int nwg, const uint32_t *list, const WGRec *wgs, const SBRec *sbs,
                        const PJob *jobs, const uint32_t *passes, const FrameDesc *frames, const int16_t *resid,
                        const uint32_t *ptab, int dbg);
-int vp9hip_launch_lf(int hb, hipStream_t st, int nsb, const uint32_t *list, const LFRec *recs,
+int vp9hip_launch_lf(int fmt, hipStream_t st, int nsb, const uint32_t *list, const LFRec *recs,
                      const FrameDesc *frames, int dbg);
 int vp9hip_launch_mc(int hb, hipStream_t st, int n, const McUnit *units, const FrameDesc *frames);
 }
@@ -256,7 +256,7 @@ extern "C" int vp9hip_configure(vp9hip_ctx *c, int width, int height, int bpp, i
 {
     if (!c || width <= 0 || height <= 0 || nbufs <= 0 || width > 16384 || height > 16384) return VP9HIP_EINVAL;
     if (bpp != 8 && bpp != 10 && bpp != 12) return VP9HIP_EINVAL;
-    if (ss_h != 1 || ss_v != 1) return VP9HIP_ENOSYS;   // 4:2:0 only on the device path (profiles 0/2)
+    if (ss_h < 0 || ss_h > 1 || ss_v < 0 || ss_v > 1) return VP9HIP_EINVAL;   // 4:2:0 / 4:2:2 / 4:4:0 / 4:4:4
     hipSetDevice(c->dev);
     hipStreamSynchronize(c->st);
     free_bufs(c);
@@ -418,23 +418,37 @@ static McRef mc_luma_ref(const FrameBuild &fb, int rf, int x, int y, const int16
     return m;
 }
 
-// Chroma (4:2:0): mc_chroma_unscaled (vp9recon.c:416-467) or mc_chroma_scaled with the
-// libvpx rounding of webm issue 820 (vp9recon.c:543-628).
+// Chroma: mc_chroma_unscaled (vp9recon.c:416-467; mv * 2 on a non-subsampled axis) or
+// mc_chroma_scaled with the libvpx rounding of webm issue 820 on subsampled axes
+// (vp9recon.c:543-628).
 static McRef mc_chroma_ref(const FrameBuild &fb, int rf, int x, int y, const int16_t *mv, int px, int py, int pw, int ph,
                            int bw, int bh)
 {
     McRef m;
+    const int ssh = fb.ss_h, ssv = fb.ss_v;
     if (!fb.scale[rf][0]) {
-        m.ix = x + (mv[0] >> 4); m.iy = y + (mv[1] >> 4);
-        m.mx = (uint8_t) (mv[0] & 15); m.my = (uint8_t) (mv[1] & 15);
+        const int mx = mv[0] * (1 << !ssh), my = mv[1] * (1 << !ssv);
+        m.ix = x + (mx >> 4); m.iy = y + (my >> 4);
+        m.mx = (uint8_t) (mx & 15); m.my = (uint8_t) (my & 15);
         m.dx = m.dy = 16;
         return m;
     }
     const int sx = fb.scale[rf][0], sy = fb.scale[rf][1];
-    const int mvx = clampi(mv[0], -(x + pw - px + 4) * 16, (fb.cols * 4 - x + px + 3) * 16);
-    const int mvy = clampi(mv[1], -(y + ph - py + 4) * 16, (fb.rows * 4 - y + py + 3) * 16);
-    const int mx = scale_mv(mvx, sx) + (scale_mv(x * 16, sx) & ~15) + (scale_mv(x * 32, sx) & 15);
-    const int my = scale_mv(mvy, sy) + (scale_mv(y * 16, sy) & ~15) + (scale_mv(y * 32, sy) & 15);
+    int mx, my;
+    if (ssh) {
+        const int mvx = clampi(mv[0], -(x + pw - px + 4) * 16, (fb.cols * 4 - x + px + 3) * 16);
+        mx = scale_mv(mvx, sx) + (scale_mv(x * 16, sx) & ~15) + (scale_mv(x * 32, sx) & 15);
+    } else {
+        const int mvx = clampi(mv[0], -(x + pw - px + 4) * 8, (fb.cols * 8 - x + px + 3) * 8);
+        mx = scale_mv(mvx * 2, sx) + scale_mv(x * 16, sx);
+    }
+    if (ssv) {
+        const int mvy = clampi(mv[1], -(y + ph - py + 4) * 16, (fb.rows * 4 - y + py + 3) * 16);
+        my = scale_mv(mvy, sy) + (scale_mv(y * 16, sy) & ~15) + (scale_mv(y * 32, sy) & 15);
+    } else {
+        const int mvy = clampi(mv[1], -(y + ph - py + 4) * 8, (fb.rows * 8 - y + py + 3) * 8);
+        my = scale_mv(mvy * 2, sy) + scale_mv(y * 16, sy);
+    }
     m.ix = mx >> 4; m.iy = my >> 4;
     m.mx = (uint8_t) (mx & 15); m.my = (uint8_t) (my & 15);
     m.dx = (uint8_t) fb.step[rf][0]; m.dy = (uint8_t) fb.step[rf][1];
@@ -451,21 +465,25 @@ static inline uint8_t lf_byte(int wd, int L)
 // The LF program of one SB: which filter (width, level) every edge of every 8-line band
 // gets, exactly as filter_plane_cols / filter_plane_rows select it from the masks,
 // including the mix2 pairing of two 8-line halves (vp9lpf.c:31-181, loopfilter_sb
-// 183-230). col0 / row0: the SB is at the frame's left / top edge (no outer edge there).
-static void lf_program(const uint8_t *lvl, const uint8_t (*msk)[2][8][4], bool col0, bool row0, uint8_t *prog)
+// 183-230). Chroma uses mask[ss_h | ss_v] (vp9lpf.c:189) with the plane's subsampling.
+// col0 / row0: the SB is at the frame's left / top edge (no outer edge there).
+static void lf_program(const uint8_t *lvl, const uint8_t (*msk)[2][8][4], int ss_h, int ss_v, bool col0, bool row0,
+                       uint8_t *prog)
 {
     memset(prog, 0, LF_PROG_BYTES);
     for (int pl = 0; pl < 2; pl++) {
-        const int nb = pl ? 4 : 8;                  // bands of 8 pixel lines
-        const int dy = pl ? 2 : 1;                  // mask rows per 8 pixel lines (4:2:0)
+        const int sh = pl ? ss_h : 0, sv = pl ? ss_v : 0;
+        const uint8_t (*m)[8][4] = msk[pl ? (ss_h | ss_v) : 0];
+        const int cbase = pl ? LFP_CC : LFP_YC, rbase = pl ? LFP_CR(ss_h, ss_v) : LFP_YR;
+        const int dy = 1 << sv, dh = 1 << sh;       // mask rows / columns per 8 pixel lines
         // column edges (filter_plane_cols): band of pixel rows, edges left to right
-        for (int band = 0; band < nb; band++) {
+        for (int band = 0; band < (8 >> sv); band++) {
             const int half = band & 1, y = (band >> 1) * 2 * dy;
-            const uint8_t *hm1 = msk[pl][0][y], *hm2 = msk[pl][0][y + dy];
+            const uint8_t *hm1 = m[0][y], *hm2 = m[0][y + dy];
             const unsigned h1 = hm1[0] | hm1[1] | hm1[2], h2 = hm2[1] | hm2[2];
             for (int k = 0; k < 8; k++) {
                 const unsigned x = 1u << k;
-                const int lc = pl ? k & ~1 : k;
+                const int lc = sh ? k & ~1 : k;
                 int wd = 0, L = 0;
                 if (!col0 || k > 0) {
                     if (!half) {
@@ -475,21 +493,21 @@ static void lf_program(const uint8_t *lvl, const uint8_t (*msk)[2][8][4], bool c
                         else if (h2 & x) { wd = (hm2[1] & x) ? 8 : 4; L = lvl[(y + dy) * 8 + lc]; }
                     } else if (h2 & x) { wd = (hm2[1] & x) ? 8 : 4; L = lvl[(y + dy) * 8 + lc]; }
                 }
-                if (pl) { prog[LFP_CC + band * 8 + k] = lf_byte(wd, L); continue; }
-                prog[LFP_YC + band * 16 + k * 2] = lf_byte(wd, L);
+                if (sh) { prog[cbase + band * 8 + k] = lf_byte(wd, L); continue; }
+                prog[cbase + band * 16 + k * 2] = lf_byte(wd, L);
                 const unsigned in = half ? hm2[3] : hm1[3];
-                if (in & x) prog[LFP_YC + band * 16 + k * 2 + 1] = (uint8_t) (0x40 | lvl[(half ? y + 1 : y) * 8 + k]);
+                if (in & x) prog[cbase + band * 16 + k * 2 + 1] = (uint8_t) (0x40 | lvl[(half ? y + dy : y) * 8 + k]);
             }
         }
         // row edges (filter_plane_rows): band of pixel columns, edges top to bottom
-        for (int band = 0; band < nb; band++) {
+        for (int band = 0; band < (8 >> sh); band++) {
             const int chunk = band >> 1, half = band & 1;
-            const unsigned x = 1u << (chunk * 2 * dy), x2 = x << dy;
-            const int lc1 = chunk * 2 * dy, lc2 = lc1 + dy;
+            const unsigned x = 1u << (chunk * 2 * dh), x2 = x << dh;
+            const int lc1 = chunk * 2 * dh, lc2 = lc1 + dh;
             for (int yy = 0; yy < 8; yy++) {
-                const uint8_t *vm_ = msk[pl][1][yy];
+                const uint8_t *vm_ = m[1][yy];
                 const unsigned vm = vm_[0] | vm_[1] | vm_[2], vm3 = vm_[3];
-                const int lr = pl ? yy & ~1 : yy;
+                const int lr = sv ? yy & ~1 : yy;
                 int wd = 0, L = 0;
                 if (!row0 || yy) {
                     if (!half) {
@@ -499,10 +517,10 @@ static void lf_program(const uint8_t *lvl, const uint8_t (*msk)[2][8][4], bool c
                         else if (vm & x2) { wd = (vm_[1] & x2) ? 8 : 4; L = lvl[lr * 8 + lc2]; }
                     } else if (vm & x2) { wd = (vm_[1] & x2) ? 8 : 4; L = lvl[lr * 8 + lc2]; }
                 }
-                if (pl) { prog[LFP_CR + band * 8 + yy] = lf_byte(wd, L); continue; }
-                prog[LFP_YR + band * 16 + yy * 2] = lf_byte(wd, L);
+                if (sv) { prog[rbase + band * 8 + yy] = lf_byte(wd, L); continue; }
+                prog[rbase + band * 16 + yy * 2] = lf_byte(wd, L);
                 if (!half ? (vm3 & x) : (vm3 & x2))
-                    prog[LFP_YR + band * 16 + yy * 2 + 1] = (uint8_t) (0x40 | lvl[yy * 8 + (half ? lc2 : lc1)]);
+                    prog[rbase + band * 16 + yy * 2 + 1] = (uint8_t) (0x40 | lvl[yy * 8 + (half ? lc2 : lc1)]);
             }
         }
     }
@@ -566,7 +584,7 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
                 const int bx = (b->col * 8 >> sh), by = (b->row * 8 >> sv);     // plane pixel pos
                 const int sbsz = 64 >> sh, sbszv = 64 >> sv;
                 const int ux_sb = (bx - sbx * sbsz) >> 2, uy_sb = (by - sby * sbszv) >> 2;
-                const int units = sbsz >> 2;  // units per row of this plane's SB (16 luma, 8 chroma)
+                const int units = sbsz >> 2, unitsv = sbszv >> 2;   // 4x4 units of this plane's SB (16 luma)
                 for (int y = 0; y < ey; y += step)
                     for (int x = 0; x < ex; x += step) {
                         int e = 0;
@@ -661,10 +679,10 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
                         }
                         if (ux0 > 0 && (nd & 1))
                             for (int v = uy0; v < uy0 + n4; v++)
-                                if (v < units) dep(v * 16 + ux0 - 1);
+                                if (v < unitsv) dep(v * 16 + ux0 - 1);
                         q.nd = (uint32_t) pdeps.size() - q.d0;
                         lvl += 1;
-                        for (int v = uy0; v < uy0 + n4 && v < units; v++)
+                        for (int v = uy0; v < uy0 + n4 && v < unitsv; v++)
                             for (int u = ux0; u < ux0 + n4 && u < units; u++) {
                                 lm[v * 16 + u] = (int8_t) lvl;
                                 jm[v * 16 + u] = (int16_t) pj.size();
@@ -674,7 +692,7 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
                     }
             }
 
-            // inter prediction units (vp9_mc_template.c:30-464), 4:2:0
+            // inter prediction units (vp9_mc_template.c:30-464)
             if (!b->intra && mine) {
                 const int r0 = b->ref[0], r1 = b->comp ? b->ref[1] : r0;
                 if (b->ref[0] > 2 || (b->comp && b->ref[1] > 2)) return VP9HIP_EINVALIDDATA;
@@ -704,40 +722,69 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
                     emit(1, x, y, w, hh, mv, px, py, pw, ph);
                     emit(2, x, y, w, hh, mv, px, py, pw, ph);
                 };
-                const int lx = b->col * 8, ly = b->row * 8, cx = b->col * 4, cy = b->row * 4;
+                const int lx = b->col * 8, ly = b->row * 8, cx = b->col * (8 >> ss_h), cy = b->row * (8 >> ss_v);
                 int16_t uv[2][2];
+                // ROUNDED_DIV_MVx2 / x4 chroma MVs of sub-8x8 blocks (vp9_mc_template.c:24-28)
+                auto avg2 = [&](int i0, int i1) {
+                    for (int k = 0; k < 2; k++) for (int d = 0; d < 2; d++) uv[k][d] = (int16_t) rdiv(b->mv[i0][k][d] + b->mv[i1][k][d], 2);
+                    return uv;
+                };
+                auto avg4 = [&]() {
+                    for (int k = 0; k < 2; k++) for (int d = 0; d < 2; d++)
+                        uv[k][d] = (int16_t) rdiv(b->mv[0][k][d] + b->mv[1][k][d] + b->mv[2][k][d] + b->mv[3][k][d], 4);
+                    return uv;
+                };
+                static const int sub[4][2] = { { 0, 0 }, { 4, 0 }, { 0, 4 }, { 4, 4 } };
                 if (b->bs > VP9H_BS_8x8 && scaled_tpl) {
-                    // four 4x4 luma blocks, one 4x4 chroma block with the 4-MV average
-                    static const int sub[4][2] = { { 0, 0 }, { 4, 0 }, { 0, 4 }, { 4, 4 } };
+                    // SCALED template (vp9_mc_template.c, SCALED == 1): four 4x4 luma blocks;
+                    // chroma 4x4 blocks with averaged MVs per subsampled axis
                     for (int k = 0; k < 4; k++)
                         emit(0, lx + sub[k][0], ly + sub[k][1], 4, 4, b->mv[k], sub[k][0], sub[k][1], 8, 8);
-                    for (int k = 0; k < 2; k++) for (int d = 0; d < 2; d++)
-                        uv[k][d] = rdiv(b->mv[0][k][d] + b->mv[1][k][d] + b->mv[2][k][d] + b->mv[3][k][d], 4);
-                    chroma2(cx, cy, 4, 4, uv, 0, 0, 4, 4);
-                } else if (b->bs > VP9H_BS_8x8) {
-                    if (b->bs == VP9H_BS_8x4) {
-                        emit(0, lx, ly, 8, 4, b->mv[0], 0, 0, 0, 0);
-                        emit(0, lx, ly + 4, 8, 4, b->mv[2], 0, 0, 0, 0);
-                        for (int k = 0; k < 2; k++) for (int d = 0; d < 2; d++) uv[k][d] = rdiv(b->mv[0][k][d] + b->mv[2][k][d], 2);
-                    } else if (b->bs == VP9H_BS_4x8) {
-                        emit(0, lx, ly, 4, 8, b->mv[0], 0, 0, 0, 0);
-                        emit(0, lx + 4, ly, 4, 8, b->mv[1], 0, 0, 0, 0);
-                        for (int k = 0; k < 2; k++) for (int d = 0; d < 2; d++) uv[k][d] = rdiv(b->mv[0][k][d] + b->mv[1][k][d], 2);
+                    if (ss_v && ss_h) chroma2(cx, cy, 4, 4, avg4(), 0, 0, 4, 4);
+                    else if (ss_v) {
+                        chroma2(cx, cy, 4, 4, avg2(0, 2), 0, 0, 8, 4);
+                        chroma2(cx + 4, cy, 4, 4, avg2(1, 3), 4, 0, 8, 4);
+                    } else if (ss_h) {
+                        chroma2(cx, cy, 4, 4, avg2(0, 1), 0, 0, 4, 8);
+                        chroma2(cx, cy + 4, 4, 4, avg2(1, 2), 0, 4, 4, 8);   // libvpx bug replica (296-305)
                     } else {
-                        emit(0, lx, ly, 4, 4, b->mv[0], 0, 0, 0, 0);
-                        emit(0, lx + 4, ly, 4, 4, b->mv[1], 0, 0, 0, 0);
-                        emit(0, lx, ly + 4, 4, 4, b->mv[2], 0, 0, 0, 0);
-                        emit(0, lx + 4, ly + 4, 4, 4, b->mv[3], 0, 0, 0, 0);
-                        for (int k = 0; k < 2; k++) for (int d = 0; d < 2; d++)
-                            uv[k][d] = rdiv(b->mv[0][k][d] + b->mv[1][k][d] + b->mv[2][k][d] + b->mv[3][k][d], 4);
+                        for (int k = 0; k < 4; k++)
+                            chroma2(cx + sub[k][0], cy + sub[k][1], 4, 4, b->mv[k], sub[k][0], sub[k][1], 8, 8);
                     }
-                    chroma2(cx, cy, 4, 4, uv, 0, 0, 4, 4);
+                } else if (b->bs == VP9H_BS_8x4) {
+                    emit(0, lx, ly, 8, 4, b->mv[0], 0, 0, 0, 0);
+                    emit(0, lx, ly + 4, 8, 4, b->mv[2], 0, 0, 0, 0);
+                    if (ss_v) chroma2(cx, cy, 8 >> ss_h, 4, avg2(0, 2), 0, 0, 0, 0);
+                    else {
+                        chroma2(cx, cy, 8 >> ss_h, 4, b->mv[0], 0, 0, 0, 0);
+                        // libvpx uses the wrong block index for 4:4:4 (vp9_mc_template.c:107-114)
+                        chroma2(cx, cy + 4, 8 >> ss_h, 4, ss_h ? avg2(0, 2) : b->mv[2], 0, 0, 0, 0);
+                    }
+                } else if (b->bs == VP9H_BS_4x8) {
+                    emit(0, lx, ly, 4, 8, b->mv[0], 0, 0, 0, 0);
+                    emit(0, lx + 4, ly, 4, 8, b->mv[1], 0, 0, 0, 0);
+                    if (ss_h) chroma2(cx, cy, 4, 8 >> ss_v, avg2(0, 1), 0, 0, 0, 0);
+                    else {
+                        chroma2(cx, cy, 4, 8 >> ss_v, b->mv[0], 0, 0, 0, 0);
+                        chroma2(cx + 4, cy, 4, 8 >> ss_v, b->mv[1], 0, 0, 0, 0);
+                    }
+                } else if (b->bs > VP9H_BS_8x8) {
+                    for (int k = 0; k < 4; k++) emit(0, lx + sub[k][0], ly + sub[k][1], 4, 4, b->mv[k], 0, 0, 0, 0);
+                    if (ss_v && ss_h) chroma2(cx, cy, 4, 4, avg4(), 0, 0, 0, 0);
+                    else if (ss_v) {
+                        chroma2(cx, cy, 4, 4, avg2(0, 2), 0, 0, 0, 0);
+                        chroma2(cx + 4, cy, 4, 4, avg2(1, 3), 0, 0, 0, 0);
+                    } else if (ss_h) {
+                        chroma2(cx, cy, 4, 4, avg2(0, 1), 0, 0, 0, 0);
+                        chroma2(cx, cy + 4, 4, 4, avg2(1, 2), 0, 0, 0, 0);   // libvpx bug replica (296-305)
+                    } else {
+                        for (int k = 0; k < 4; k++) chroma2(cx + sub[k][0], cy + sub[k][1], 4, 4, b->mv[k], 0, 0, 0, 0);
+                    }
                 } else {
                     const int bw = vp9t_bwh[0][b->bs][0] * 4, bh = vp9t_bwh[0][b->bs][1] * 4;
-                    const int uvbw = vp9t_bwh[1][b->bs][0] * 4, uvbh = vp9t_bwh[1][b->bs][1] * 4;
+                    const int uvbw = vp9t_bwh[ss_h][b->bs][0] * 4, uvbh = vp9t_bwh[ss_v][b->bs][1] * 4;
                     emit(0, lx, ly, bw, bh, b->mv[0], 0, 0, bw, bh);
-                    for (int k = 0; k < 2; k++) for (int d = 0; d < 2; d++) uv[k][d] = b->mv[0][k][d];
-                    chroma2(cx, cy, uvbw, uvbh, uv, 0, 0, uvbw, uvbh);
+                    chroma2(cx, cy, uvbw, uvbh, b->mv[0], 0, 0, uvbw, uvbh);
                 }
             }
 
@@ -785,7 +832,7 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
         }
         if (f->filter_level) {
             uint32_t li = (uint32_t) s.lfs.size();
-            lf_program(lf_level, lf_mask, sbx == 0, sby == 0, lf.prog);
+            lf_program(lf_level, lf_mask, ss_h, ss_v, sbx == 0, sby == 0, lf.prog);
             s.lfs.push_back(lf);
             int d = sbx + 2 * sby;
             if ((int) lf_steps.size() <= d) lf_steps.resize(d + 1);
@@ -1139,11 +1186,11 @@ static int launch_one(vp9hip_ctx *c, const Launch &L, hipStream_t st)
         return vp9hip_launch_resid(c->hb, st, L.arg, (int) L.n, (const RJob *) (s.arena + s.o_rjobs) + L.off, fr,
                                    s.arena + s.o_coefs, s.resid);
     case K_PRED:
-        return vp9hip_launch_pred(c->hb, st, (int) L.n, lists + L.off, (const WGRec *) (s.arena + s.o_wgs),
+        return vp9hip_launch_pred(c->hb | c->ss_h << 1 | c->ss_v << 2, st, (int) L.n, lists + L.off, (const WGRec *) (s.arena + s.o_wgs),
                                   (const SBRec *) (s.arena + s.o_sbs), (const PJob *) (s.arena + s.o_pjobs),
                                   (const uint32_t *) (s.arena + s.o_passes), fr, s.resid, c->ptab, c->dbg);
     case K_LF:
-        return vp9hip_launch_lf(c->hb, st, (int) L.n, lists + L.off, (const LFRec *) (s.arena + s.o_lfs), fr, c->dbg >> 16);
+        return vp9hip_launch_lf(c->hb | c->ss_h << 1 | c->ss_v << 2, st, (int) L.n, lists + L.off, (const LFRec *) (s.arena + s.o_lfs), fr, c->dbg >> 16);
     }
     return -1;
 }
@@ -1372,7 +1419,7 @@ extern "C" int vp9hip_abi_version(void) { return VP9HIP_ABI_VERSION; }
 extern "C" int vp9hip_plan_stats(const vp9h_frame *f, double *out, int cap)
 {
     if (!f || !out || cap < 16) return VP9HIP_EINVAL;
-    if (f->ss_h != 1 || f->ss_v != 1) return VP9HIP_ENOSYS;
+    if (f->ss_h > 1 || f->ss_v > 1) return VP9HIP_EINVAL;
     init_nz();
     Staged s;
     FrameBuild fb;
@@ -1380,7 +1427,7 @@ extern "C" int vp9hip_plan_stats(const vp9h_frame *f, double *out, int cap)
     fb.cols = (f->width + 7) >> 3; fb.rows = (f->height + 7) >> 3;
     fb.sb_cols = (f->width + 63) >> 6; fb.sb_rows = (f->height + 63) >> 6;
     fb.ss_h = f->ss_h; fb.ss_v = f->ss_v; fb.coef_size = f->bpp > 8 ? 4 : 2;
-    fb.pitch[0] = fb.sb_cols * 64; fb.pitch[1] = fb.sb_cols * 32;
+    fb.pitch[0] = fb.sb_cols * 64; fb.pitch[1] = fb.sb_cols * 64 >> f->ss_h;
     fb.coef_base = 0;
     fb.phase = 0;
     s.rbucket.resize(1);

@@ -102,7 +102,7 @@ typedef struct WGRec {
 #define PASS_FIRST(w) ((w) >> 8)
 #define PASS_NJOBS(w) ((((w) >> 3) & 31) + 1)
 #define PASS_TS(w) ((w) & 3)
-#define MAX_SB_JOBS 384
+#define MAX_SB_JOBS 768          /* 3 planes x 256 4x4 jobs (4:4:4) */
 #define PJ_SLOT(j) ((j).a >> 30)
 
 /* Loop-filter program of one SB: the edge decisions of filter_plane_cols / _rows
@@ -110,12 +110,18 @@ typedef struct WGRec {
  * (vp9dec.h:83-87, vp9block.c:1438-1452). One byte per (band, edge): band = pixel row
  * >> 3 for column edges, pixel column >> 3 for row edges (the decisions are uniform
  * over 8 lines); main edge = width code (1: 4, 2: 8, 3: 16) << 6 | level, 0 = none;
- * luma inner 4-wide edge = 0x40 | level, 0 = none. */
+ * inner 4-wide edge = 0x40 | level, 0 = none.
+ * A plane dimension of 64 pixels (luma; chroma without subsampling on that axis) has
+ * 8 edges 8 pixels apart, each with (main, inner) bytes: 16 bytes per band. A subsampled
+ * chroma dimension (32 pixels) has 8 edges 4 pixels apart, main only: 8 bytes per band.
+ * U and V share the chroma program (one mask set, vp9lpf.c:189). */
 #define LFP_YC 0                 /* luma column edges: band * 16 + edge * 2 + {main, inner} */
 #define LFP_YR 128               /* luma row edges:    band * 16 + edge * 2 + {main, inner} */
-#define LFP_CC 256               /* chroma column edges: band * 8 + edge (U and V alike)    */
-#define LFP_CR 288               /* chroma row edges:    band * 8 + edge                    */
-#define LF_PROG_BYTES 320
+#define LFP_CC 256               /* chroma column edges: band * LFP_CSTRIDE(ss_h) + ...     */
+#define LFP_CSTRIDE(ss) ((ss) ? 8 : 16)
+#define LFP_CR(ss_h, ss_v) (LFP_CC + (8 >> (ss_v)) * LFP_CSTRIDE(ss_h))       /* chroma row edges */
+#define LF_PROG_OF(ss_h, ss_v) (LFP_CR(ss_h, ss_v) + (8 >> (ss_h)) * LFP_CSTRIDE(ss_v))
+#define LF_PROG_BYTES 512        /* LF_PROG_OF(0, 0): 4:2:0 uses the first 320 */
 typedef struct LFRec {
     uint32_t frame;
     uint16_t sbx, sby;

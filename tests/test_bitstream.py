@@ -39,7 +39,7 @@ def _same(a, b):
     assert np.array_equal(A[1], B[1]), "eobs differ"
     assert A[2] == B[2], "coefficients differ"
     assert bytes(a.lflvl) == bytes(b.lflvl)
-    for k in ("width", "height", "bpp", "lossless", "filter_level", "sharpness", "log2_tile_cols", "keyframe", "intraonly"):
+    for k in ("width", "height", "bpp", "ss_h", "ss_v", "lossless", "filter_level", "sharpness", "log2_tile_cols", "keyframe", "intraonly"):
         assert getattr(a, k) == getattr(b, k), k
 
 
@@ -69,6 +69,48 @@ def test_keyframe_round_trip(v9, w, h, bpp, kw):
         assert data[1:4] == b"\x49\x83\x42" or bpp > 8             # sync code right after (profile 0)
         d = v9.decode_frame(data)
         _same(f.pkt, d.pkt)
+
+
+@pytest.mark.parametrize("bpp", [8, 10, 12])
+@pytest.mark.parametrize("ssh,ssv", [(1, 0), (0, 1), (0, 0)])
+def test_profile_1_3_round_trip(v9, bpp, ssh, ssv):
+    """Profiles 1 / 3: the colour config codes the subsampling
+    (read_colorspace_details, vp9.c:457-517); chroma uvtx, nnz contexts and token
+    counts follow it (vp9block.c:1291, 965-1130)."""
+    for (w, h, kw) in [(200, 130, {}), (512, 136, {"log2_tile_cols": 1}), (66, 74, {"lossless": 1, "q_idx": 0})]:
+        f = v9.SynthFrame(v9.synth_params(w, h, bpp, seed=61, ss_h=ssh, ss_v=ssv, **kw))
+        data = v9.encode_frame(f, f.params.q_idx)
+        profile = (data[0] >> 5 & 1) | (data[0] >> 4 & 1) << 1
+        assert profile == (1 if bpp == 8 else 3)
+        d = v9.decode_frame(data)
+        assert (d.pkt.ss_h, d.pkt.ss_v) == (ssh, ssv)
+        _same(f.pkt, d.pkt)
+
+
+def _set_bits(data, pos, vals):
+    b = bytearray(data)
+    for i, v in enumerate(vals):
+        k = pos + i
+        b[k >> 3] = (b[k >> 3] & ~(0x80 >> (k & 7))) | (v << (7 - (k & 7)))
+    return bytes(b)
+
+
+def test_colour_config_refusals(v9):
+    """read_colorspace_details (vp9.c:457-517): 8-bit 4:2:0 in profile 1, the reserved bit,
+    and RGB in profile 0 are invalid data."""
+    f = v9.SynthFrame(v9.synth_params(200, 130, 8, seed=62, ss_h=1, ss_v=0))
+    data = v9.encode_frame(f, 60)
+    # profile 1 keyframe: marker 2, profile 2, show_existing, type, show, error_res 4,
+    # sync 24 -> colour space at bit 32, range 35, ss_h 36, ss_v 37, reserved 38
+    assert v9.decode_frame(data).pkt.ss_v == 0
+    for pos, vals in ((36, [1, 1]), (38, [1])):
+        with pytest.raises(v9.Vp9HipError) as e:
+            v9.decode_frame(_set_bits(data, pos, vals))
+        assert e.value.code == v9.EINVALIDDATA
+    k0 = v9.encode_frame(v9.SynthFrame(v9.synth_params(200, 130, 8, seed=63)), 60)
+    with pytest.raises(v9.Vp9HipError) as e:
+        v9.decode_frame(_set_bits(k0, 32, [1, 1, 1]))      # RGB in profile 0
+    assert e.value.code == v9.EINVALIDDATA
 
 
 def test_4k_tiles_round_trip(v9):

@@ -52,7 +52,7 @@ def _arrays(p):
 
 def same_packet(a, b):
     """Decoded == coded, field by field."""
-    for k in ("width", "height", "bpp", "keyframe", "intraonly", "lossless", "filter_level", "sharpness",
+    for k in ("width", "height", "bpp", "ss_h", "ss_v", "keyframe", "intraonly", "lossless", "filter_level", "sharpness",
               "log2_tile_cols", "log2_tile_rows", "nblocks", "neobs", "ncoefs"):
         assert getattr(a, k) == getattr(b, k), k
     assert bytes(a.lflvl) == bytes(b.lflvl)
@@ -104,7 +104,7 @@ def check_legalized(orig, coded, stats, keep_modes=False):
 
 def _frames(v9, w, h, n, bpp=8, seed=700, **kw):
     """Keyframe + n - 1 inter frames (LAST = previous, GOLDEN = key, ALTREF = previous)."""
-    key = {k: x for k, x in kw.items() if k in ("log2_tile_cols", "lossless", "q_idx")}
+    key = {k: x for k, x in kw.items() if k in ("log2_tile_cols", "lossless", "q_idx", "ss_h", "ss_v")}
     fr = [v9.SynthFrame(v9.synth_params(w, h, bpp, seed=seed, **key))]
     for i in range(1, n):
         fr.append(v9.SynthFrame(v9.synth_params(w, h, bpp, seed=seed + i, inter=1, **kw)))
@@ -141,6 +141,11 @@ STREAMS = [
     ("tiles", dict(w=1024, h=136, n=3, log2_tile_cols=2), None),
     ("ten_bit", dict(w=176, h=144, n=4, bpp=10, compound=1), None),
     ("twelve_bit", dict(w=136, h=72, n=3, bpp=12), None),
+    # profiles 1 / 3: subsampling coded in the colour config
+    ("yuv422", dict(w=200, h=130, n=4, compound=1, ss_h=1, ss_v=0), None),
+    ("yuv440", dict(w=200, h=130, n=4, ss_h=0, ss_v=1), lambda i: {"refresh_ctx": 1, "parallel": 0}),
+    ("yuv444_10bit", dict(w=176, h=144, n=4, bpp=10, compound=1, ss_h=0, ss_v=0), None),
+    ("yuv444_12bit", dict(w=136, h=72, n=3, bpp=12, ss_h=0, ss_v=0), None),
     ("prob_updates", dict(w=352, h=288, n=5, compound=1), lambda i: {"prob_updates": 11 + i}),
     ("backward_adaptation", dict(w=352, h=288, n=6, compound=1),
      lambda i: {"refresh_ctx": 1, "parallel": 0, "ctx_id": i % 4}),
@@ -281,15 +286,16 @@ print(ok, err)
 
 
 @pytest.mark.gpu
-def test_inter_bitstream_to_gpu_matches_oracle(v9, orc, gpu):
+@pytest.mark.parametrize("ssh,ssv", [(1, 1), (1, 0), (0, 0)])
+def test_inter_bitstream_to_gpu_matches_oracle(v9, orc, gpu, ssh, ssv):
     """Host decode of an inter stream (compound, adaptation), then the MI355X pixel path
     with the decoded reference slots, bit-exact against the oracle's decode of the coded
-    packets."""
+    packets (4:2:0 and the profile 1 formats)."""
     w, h = 352, 288
-    frames = _frames(v9, w, h, 5, compound=1)
+    frames = _frames(v9, w, h, 5, compound=1, ss_h=ssh, ss_v=ssv)
     datas, coded = encode_stream(v9, frames, lambda i: {"refresh_ctx": 1, "parallel": 0})
     dec = v9.Stream()
-    gpu.configure(w, h, 8, nbufs=8)
+    gpu.configure(w, h, 8, nbufs=8, ss_h=ssh, ss_v=ssv)
     slots = [None] * 8          # reference slot -> device buffer (frame index)
     oracle = []
     for i, d in enumerate(datas):
@@ -297,7 +303,7 @@ def test_inter_bitstream_to_gpu_matches_oracle(v9, orc, gpu):
         refs = [slots[s] if slots[s] is not None else 0 for s in info.ref_slot]
         gpu.submit(p, i, refs)
         ref_planes = None if i == 0 else [oracle[r] for r in refs]
-        out = v9.alloc_planes(w, h, 8)
+        out = v9.alloc_planes(w, h, 8, ssh, ssv)
         orc.decode_frame(coded[i].pkt, out, ref_planes)
         oracle.append(out)
         for s in range(8):
@@ -306,5 +312,5 @@ def test_inter_bitstream_to_gpu_matches_oracle(v9, orc, gpu):
     gpu.sync()
     for i in range(len(datas)):
         got = gpu.download(i)
-        for a, b in zip(v9.visible(got, w, h), v9.visible(oracle[i], w, h)):
+        for a, b in zip(v9.visible(got, w, h, ssh, ssv), v9.visible(oracle[i], w, h, ssh, ssv)):
             assert np.array_equal(a, b), "frame %d" % i
