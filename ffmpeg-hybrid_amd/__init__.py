@@ -22,6 +22,8 @@ LIB_PATH = os.path.join(_HERE, "libvp9hip.so")
 EINVAL = -22
 ENOMEM = -12
 ENOSYS = -38
+EAGAIN = -11
+EOF = -541478725
 EINVALIDDATA = -1094995529
 EEXTERNAL = -542398533
 EBUG = -558323010
@@ -110,7 +112,12 @@ ABI_SYMBOLS = ["vp9hip_open", "vp9hip_close", "vp9hip_configure", "vp9hip_submit
                "vp9h_decode_frame", "vp9h_encode_frame", "vp9h_frame_free", "vp9h_buffer_free",
                "vp9h_stream_open", "vp9h_stream_close", "vp9h_stream_decode", "vp9h_stream_encode",
                "vp9h_enc_defaults", "vp9h_superframe_split",
-               "vp9hip_synth_defaults", "vp9hip_synth_frame", "vp9hip_synth_free"]
+               "vp9hip_synth_defaults", "vp9hip_synth_frame", "vp9hip_synth_free",
+               "vp9h_ivf_probe", "vp9h_ivf_read_header", "vp9h_ivf_read_frame", "vp9h_ivf_write_header",
+               "vp9h_ivf_write_frame_header",
+               "vp9hip_decoder_defaults", "vp9hip_decoder_open", "vp9hip_decoder_close", "vp9hip_decoder_context",
+               "vp9hip_decoder_send_packet", "vp9hip_decoder_receive_frame", "vp9hip_decoder_release",
+               "vp9hip_decoder_flush"]
 
 
 def lib():
@@ -176,8 +183,45 @@ def lib():
     L.vp9h_enc_defaults.restype = None
     L.vp9h_superframe_split.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t),
                                         ctypes.POINTER(ctypes.c_size_t), ctypes.c_int]
+    L.vp9h_ivf_probe.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    L.vp9h_ivf_read_header.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(IvfHeader)]
+    L.vp9h_ivf_read_frame.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t),
+                                      ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint32),
+                                      ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int)]
+    L.vp9h_ivf_write_header.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32,
+                                        ctypes.c_uint32]
+    L.vp9h_ivf_write_frame_header.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int64]
+    L.vp9h_ivf_write_frame_header.restype = None
+    L.vp9hip_decoder_defaults.argtypes = [ctypes.POINTER(DecoderParams)]
+    L.vp9hip_decoder_defaults.restype = None
+    L.vp9hip_decoder_open.argtypes = [ctypes.POINTER(DecoderParams), ctypes.POINTER(vp)]
+    L.vp9hip_decoder_close.argtypes = [vp]
+    L.vp9hip_decoder_close.restype = None
+    L.vp9hip_decoder_context.argtypes = [vp]
+    L.vp9hip_decoder_context.restype = vp
+    L.vp9hip_decoder_send_packet.argtypes = [vp, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int64]
+    L.vp9hip_decoder_receive_frame.argtypes = [vp, ctypes.POINTER(DecodedFrameInfo)]
+    L.vp9hip_decoder_release.argtypes = [vp, ctypes.c_int]
+    L.vp9hip_decoder_flush.argtypes = [vp]
     _lib_handle = L
     return L
+
+
+class IvfHeader(ctypes.Structure):
+    _fields_ = [("fourcc", ctypes.c_char * 5), ("width", ctypes.c_int32), ("height", ctypes.c_int32),
+                ("time_base_den", ctypes.c_uint32), ("time_base_num", ctypes.c_uint32),
+                ("nb_frames", ctypes.c_uint32), ("header_size", ctypes.c_uint32)]
+
+
+class DecoderParams(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("max_batch", ctypes.c_int32), ("extra_bufs", ctypes.c_int32),
+                ("max_width", ctypes.c_int32), ("max_height", ctypes.c_int32)]
+
+
+class DecodedFrameInfo(ctypes.Structure):
+    _fields_ = [("buf", ctypes.c_int32), ("width", ctypes.c_int32), ("height", ctypes.c_int32),
+                ("bpp", ctypes.c_int32), ("ss_h", ctypes.c_int32), ("ss_v", ctypes.c_int32),
+                ("pts", ctypes.c_int64)]
 
 
 def _check(fn, r):
@@ -501,12 +545,11 @@ class Device:
         _check("vp9hip_flush", lib().vp9hip_flush(self._c))
 
 
-class Decoder:
-    """send_packet / receive_frame mirror of the reference decode loop for this path.
+class PacketDecoder:
+    """send_packet / receive_frame over pass-1 frame packets (no bitstream parse).
 
-    Packets are pass-1 frame packets; VP9 reference slots follow the frame
-    header's refresh mask semantics (vp9.c:1839-1859) in the simplified form
-    used here: every decoded frame becomes LAST for the next inter frame.
+    Reference slots are simplified: every decoded frame becomes LAST, GOLDEN and
+    ALTREF of the next inter frame. Bitstreams go through Decoder.
     """
 
     def __init__(self, device=0, nbufs=4):
@@ -538,6 +581,146 @@ class Decoder:
         buf = self._queue.pop(0)
         w, h, bpp = self._configured
         return visible(self.dev.download(buf), w, h)
+
+
+class Decoder:
+    """avcodec_send_packet / avcodec_receive_frame for AV_CODEC_ID_VP9 (vp9hip_decoder):
+    compressed VP9 packets in, decoded frames out. The host parses each frame
+    (vp9h_stream), the MI355X reconstructs them in batches of up to max_batch frames.
+
+    send_packet(data, pts) -> None; raises Vp9HipError with code EAGAIN when frames must
+    be received first. send_packet(None) drains. receive_frame() -> (planes, info) with
+    visible numpy planes (download=True) or a device-buffer handle, None when more input
+    is needed (EAGAIN) or after the drain (EOF, which also sets .eof).
+    """
+
+    def __init__(self, device=0, max_batch=16, extra_bufs=4, max_width=0, max_height=0):
+        self.params = DecoderParams()
+        lib().vp9hip_decoder_defaults(ctypes.byref(self.params))
+        self.params.device, self.params.max_batch, self.params.extra_bufs = device, max_batch, extra_bufs
+        self.params.max_width, self.params.max_height = max_width, max_height
+        self._d = ctypes.c_void_p()
+        _check("vp9hip_decoder_open", lib().vp9hip_decoder_open(ctypes.byref(self.params), ctypes.byref(self._d)))
+        self.eof = False
+
+    def close(self):
+        if self._d:
+            lib().vp9hip_decoder_close(self._d)
+            self._d = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def send_packet(self, data, pts=0):
+        if data is None:
+            _check("vp9hip_decoder_send_packet", lib().vp9hip_decoder_send_packet(self._d, None, 0, 0))
+            return
+        data = bytes(data)
+        _check("vp9hip_decoder_send_packet", lib().vp9hip_decoder_send_packet(self._d, data, len(data), pts))
+
+    def receive_frame(self, download=True):
+        """Next output frame: (visible planes, DecodedFrameInfo) with download=True, else
+        (None, info) with info.buf valid until release(info.buf). None: EAGAIN / EOF."""
+        info = DecodedFrameInfo()
+        r = lib().vp9hip_decoder_receive_frame(self._d, ctypes.byref(info))
+        if r == EAGAIN:
+            return None
+        if r == EOF:
+            self.eof = True
+            return None
+        _check("vp9hip_decoder_receive_frame", r)
+        if not download:
+            return None, info
+        planes = alloc_planes(info.width, info.height, info.bpp, info.ss_h, info.ss_v)
+        ptrs = (ctypes.c_void_p * 3)(*[p.ctypes.data for p in planes])
+        ls = (ctypes.c_ssize_t * 3)(*[p.strides[0] for p in planes])
+        try:
+            _check("vp9hip_download_frame", lib().vp9hip_download_frame(self.context(), info.buf, ptrs, ls))
+        finally:
+            self.release(info.buf)
+        return visible(planes, info.width, info.height, info.ss_h, info.ss_v), info
+
+    def release(self, buf):
+        _check("vp9hip_decoder_release", lib().vp9hip_decoder_release(self._d, buf))
+
+    def context(self):
+        return ctypes.c_void_p(lib().vp9hip_decoder_context(self._d))
+
+    def flush(self):
+        _check("vp9hip_decoder_flush", lib().vp9hip_decoder_flush(self._d))
+        self.eof = False
+
+    def decode(self, packets, download=True):
+        """Decode an iterable of (data, pts) or data: yields receive_frame results in
+        output order, draining at the end (the ffmpeg -i ... -f null - loop)."""
+        for item in packets:
+            data, pts = item if isinstance(item, tuple) else (item, 0)
+            while True:
+                try:
+                    self.send_packet(data, pts)
+                    break
+                except Vp9HipError as e:
+                    if e.code != EAGAIN:
+                        raise
+                    got = self.receive_frame(download)
+                    if got is None:
+                        raise
+                    yield got
+            while True:
+                got = self.receive_frame(download)
+                if got is None:
+                    break
+                yield got
+        self.send_packet(None)
+        while True:
+            got = self.receive_frame(download)
+            if got is None:
+                break
+            yield got
+
+
+# ---- IVF (libavformat/ivfdec.c, ivfenc.c) -------------------------------------------
+def ivf_probe(data):
+    data = bytes(data[:32])
+    return lib().vp9h_ivf_probe(data, len(data))
+
+
+def ivf_read(data):
+    """IVF bytes -> (IvfHeader, [(pts, frame bytes)]). A short last frame is returned
+    as far as it goes (av_get_packet)."""
+    data = bytes(data)
+    h = IvfHeader()
+    _check("vp9h_ivf_read_header", lib().vp9h_ivf_read_header(data, len(data), ctypes.byref(h)))
+    frames = []
+    pos = ctypes.c_size_t(32)
+    ptr, n, pts, tr = ctypes.c_void_p(), ctypes.c_uint32(), ctypes.c_int64(), ctypes.c_int()
+    base = ctypes.cast(ctypes.c_char_p(data), ctypes.c_void_p).value
+    while True:
+        r = lib().vp9h_ivf_read_frame(data, len(data), ctypes.byref(pos), ctypes.byref(ptr), ctypes.byref(n),
+                                      ctypes.byref(pts), ctypes.byref(tr))
+        if r == EOF:
+            break
+        _check("vp9h_ivf_read_frame", r)
+        off = ptr.value - base
+        frames.append((pts.value, data[off:off + n.value]))
+    return h, frames
+
+
+def ivf_write(frames, width, height, time_base=(1, 30)):
+    """[(pts, bytes)] or [bytes] -> IVF bytes (fourcc VP90, frame count filled in)."""
+    hdr = ctypes.create_string_buffer(32)
+    _check("vp9h_ivf_write_header", lib().vp9h_ivf_write_header(hdr, width, height, time_base[1], time_base[0],
+                                                                 len(frames)))
+    out = [hdr.raw]
+    fh = ctypes.create_string_buffer(12)
+    for i, f in enumerate(frames):
+        pts, data = f if isinstance(f, tuple) else (i, f)
+        lib().vp9h_ivf_write_frame_header(fh, len(data), pts)
+        out += [fh.raw, bytes(data)]
+    return b"".join(out)
 
 
 PLAN_STAT_NAMES = ("sbs", "passes", "pjobs", "rjobs", "jobs_4x4", "jobs_8x8", "jobs_16x16",

@@ -2215,10 +2215,11 @@ int vp9h_stream_encode(vp9h_stream *st, const vp9h_frame *pkt, const vp9h_enc_pa
         w0.st = st; w0.h = h;
         int slot = ep->show_slot;
         if (walk_uncompressed(&w0, &b, &slot) != -3 || b.err) { free(b.buf); return VP9HIP_EINVAL; }
-        *out = malloc(1);
+        const size_t n = (b.bit + 7) >> 3;        /* 1 byte; 2 in profile 3 (its reserved bit) */
+        *out = malloc(n);
         if (!*out) { free(b.buf); return VP9HIP_ENOMEM; }
-        (*out)[0] = b.buf[0];
-        *out_size = 1;
+        memcpy(*out, b.buf, n);
+        *out_size = n;
         free(b.buf);
         return 0;
     }

@@ -39,6 +39,8 @@ extern "C" {
 #define VP9HIP_EINVALIDDATA (-1094995529)  /* AVERROR_INVALIDDATA */
 #define VP9HIP_EEXTERNAL    (-542398533)   /* AVERROR_EXTERNAL (HIP runtime failure) */
 #define VP9HIP_EBUG         (-558323010)   /* AVERROR_BUG (internal invariant broken) */
+#define VP9HIP_EAGAIN       (-11)          /* AVERROR(EAGAIN)   */
+#define VP9HIP_EOF          (-541478725)   /* AVERROR_EOF       */
 
 /* enum BlockSize (vp9shared.h:86-101) */
 enum { VP9H_BS_64x64, VP9H_BS_64x32, VP9H_BS_32x64, VP9H_BS_32x32, VP9H_BS_32x16,
@@ -256,7 +258,7 @@ void vp9hip_synth_free(vp9h_frame *f);
  * generator): default probabilities, frame_parallel, tx_mode = TX_MODE_SELECT, libvpx's
  * default LF deltas. Release the buffer with vp9h_buffer_free.
  * These one-frame forms take keyframes and intra-only frames (no reference state);
- * streams with inter frames go through a vp9h_stream below. Profiles 0 / 2 (4:2:0). */
+ * streams with inter frames go through a vp9h_stream below. Profiles 0-3. */
 int  vp9h_decode_frame(const uint8_t *data, size_t size, vp9h_frame *out);
 int  vp9h_encode_frame(const vp9h_frame *pkt, int base_q_idx, uint8_t **out, size_t *size);
 void vp9h_frame_free(vp9h_frame *f);
@@ -330,6 +332,59 @@ int  vp9h_stream_encode(vp9h_stream *s, const vp9h_frame *pkt, const vp9h_enc_pa
  * bsf/vp9_superframe_split.c:40-95): up to cap (offset, size) pairs; returns the frame
  * count (1 for a plain frame) or a negative error. */
 int  vp9h_superframe_split(const uint8_t *data, size_t size, size_t *offsets, size_t *sizes, int cap);
+
+/* ---- IVF container (libavformat/ivfdec.c, ivfenc.c) ------------- */
+typedef struct vp9h_ivf_header {
+    char     fourcc[5];            /* "VP90" for VP9, NUL-terminated                        */
+    int32_t  width, height;
+    uint32_t time_base_den, time_base_num;
+    uint32_t nb_frames;
+    uint32_t header_size;
+} vp9h_ivf_header;
+/* ivfdec.c probe (:27-34): 98 (AVPROBE_SCORE_MAX - 2) for an IVF header, else 0. */
+int  vp9h_ivf_probe(const uint8_t *buf, size_t size);
+/* ivfdec.c read_header (:36-77): AVERROR_INVALIDDATA for a zero time base. */
+int  vp9h_ivf_read_header(const uint8_t *buf, size_t size, vp9h_ivf_header *h);
+/* ivfdec.c read_packet (:79-90): the frame at *pos (32 = the first), advancing *pos.
+ * Returns 0, or VP9HIP_EOF at the end; a short last frame sets *truncated. */
+int  vp9h_ivf_read_frame(const uint8_t *buf, size_t size, size_t *pos, const uint8_t **data, uint32_t *frame_size,
+                         int64_t *pts, int *truncated);
+/* ivfenc.c write_header (:54-73) with fourcc VP90, and write_packet's frame header (:75-88). */
+int  vp9h_ivf_write_header(uint8_t out[32], int width, int height, uint32_t time_base_den, uint32_t time_base_num,
+                           uint32_t nb_frames);
+void vp9h_ivf_write_frame_header(uint8_t out[12], uint32_t frame_size, int64_t pts);
+
+/* ---- bitstream decoder: avcodec_send_packet / avcodec_receive_frame for VP9 -------------
+ * The decode loop of vp9_decode_frame (vp9.c:1558-1865) over the host parse (vp9h_stream)
+ * and the device path (vp9hip_ctx): superframes split, show_existing_frame, hidden frames,
+ * reference slots by refresh mask. Frames are reconstructed in batches of up to
+ * max_batch frames (decoder delay, like frame threading); send_packet(NULL) drains.
+ * Errors: VP9HIP_EAGAIN from send_packet = read frames first (no free buffer);
+ * from receive_frame = send more input; VP9HIP_EOF after a drain. */
+typedef struct vp9hip_decoder vp9hip_decoder;
+typedef struct vp9hip_decoder_params {
+    int32_t device;
+    int32_t max_batch;             /* frames per GPU batch (decoder delay), default 16        */
+    int32_t extra_bufs;            /* output frames the caller may hold at once, default 4     */
+    int32_t max_width, max_height; /* buffer size; 0: the first keyframe's (larger inter      */
+                                   /* frames, e.g. reference scaling up, need it set)         */
+} vp9hip_decoder_params;
+typedef struct vp9hip_decoded_frame {
+    int32_t buf;                   /* device buffer of vp9hip_decoder_context()              */
+    int32_t width, height, bpp, ss_h, ss_v;
+    int64_t pts;
+} vp9hip_decoded_frame;
+void vp9hip_decoder_defaults(vp9hip_decoder_params *p);
+int  vp9hip_decoder_open(const vp9hip_decoder_params *p, vp9hip_decoder **out);
+void vp9hip_decoder_close(vp9hip_decoder *d);
+/* The device context holding the frames: vp9hip_download_frame / vp9hip_frame_device. */
+vp9hip_ctx *vp9hip_decoder_context(vp9hip_decoder *d);
+int  vp9hip_decoder_send_packet(vp9hip_decoder *d, const uint8_t *data, size_t size, int64_t pts);
+/* The next output frame; its buffer stays valid until vp9hip_decoder_release. */
+int  vp9hip_decoder_receive_frame(vp9hip_decoder *d, vp9hip_decoded_frame *out);
+int  vp9hip_decoder_release(vp9hip_decoder *d, int buf);
+/* avcodec_flush_buffers: drop queued frames and reference state (seek). */
+int  vp9hip_decoder_flush(vp9hip_decoder *d);
 
 #ifdef __cplusplus
 }

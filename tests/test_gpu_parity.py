@@ -104,7 +104,7 @@ def test_batch_interleaved_keyframes(v9, orc, gpu):
 def test_decoder_api_sequence(v9, orc):
     """send_packet / receive_frame over a key + 3 inter frames."""
     w, h = 160, 96
-    dec = v9.Decoder(0, nbufs=3)
+    dec = v9.PacketDecoder(0, nbufs=3)
     pkts = [v9.SynthFrame(v9.synth_params(w, h, 8, seed=40))] + \
            [v9.SynthFrame(v9.synth_params(w, h, 8, seed=41 + i, inter=1)) for i in range(3)]
     prev = None
