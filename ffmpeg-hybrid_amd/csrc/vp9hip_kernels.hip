@@ -1282,6 +1282,29 @@ __global__ __launch_bounds__(LfNT<G>::NT) void k_lf(const uint32_t *__restrict__
     lf_sb<PIX, G, LfNT<G>::NT>(recs[list[blockIdx.x]], frames, S, threadIdx.x, dbg);
 }
 
+// Fused launch of one intra diagonal and one LF diagonal (runtime schedule: LF diagonal
+// t - 3 with intra diagonal t touch disjoint pixels): workgroups [0, npred) predict one SB
+// each with wave 0 (wave 1 exits), the rest loop-filter one SB each.
+template <typename PIX, class G>
+__global__ __launch_bounds__(LfNT<G>::NT) void k_plf(const uint32_t *__restrict__ plist, int npred,
+                                                     const uint32_t *__restrict__ llist, const WGRec *__restrict__ wgs,
+                                                     const SBRec *__restrict__ sbs, const PJob *__restrict__ jobs,
+                                                     const uint32_t *__restrict__ passes, const LFRec *__restrict__ recs,
+                                                     const FrameDesc *__restrict__ frames, const int16_t *__restrict__ resid,
+                                                     const uint32_t *__restrict__ ptab, int dbg)
+{
+    __shared__ union PlfLds { PredLds<PIX, G> p; LfLds<PIX, G> l; } S;
+    if ((int) blockIdx.x < npred) {
+        if (threadIdx.x >= 64) return;
+#if PRED_LTAB_LDS
+        load_ltab<PIX>(S.p.ltab, ptab, threadIdx.x);
+#endif
+        pred_wg<PIX, G>(wgs + plist[blockIdx.x], sbs, jobs, passes, frames, resid, ptab, S.p, threadIdx.x, dbg);
+    } else {
+        lf_sb<PIX, G, LfNT<G>::NT>(recs[llist[blockIdx.x - npred]], frames, S.l, threadIdx.x, dbg >> 16);
+    }
+}
+
 // --------------------------------------------------------------- k_mc
 template <typename PIX>
 DEV int mc_ref(const PIX *r, int pitch, int w, int h, int x, int y)
@@ -1397,6 +1420,26 @@ static void launch_lf_p(int ss, hipStream_t st, int nsb, const uint32_t *list, c
     default: launch_lf_g<PIX, Geo<0, 0>>(st, nsb, list, recs, frames, dbg); break;
     }
 }
+template <typename PIX, class G>
+static void launch_plf_g(hipStream_t st, int npred, const uint32_t *plist, int nlf, const uint32_t *llist, const WGRec *wgs,
+                         const SBRec *sbs, const PJob *jobs, const uint32_t *passes, const LFRec *recs,
+                         const FrameDesc *frames, const int16_t *resid, const uint32_t *ptab, int dbg)
+{
+    hipLaunchKernelGGL((k_plf<PIX, G>), dim3(npred + nlf), dim3(LfNT<G>::NT), 0, st, plist, npred, llist, wgs, sbs, jobs,
+                       passes, recs, frames, resid, ptab, dbg);
+}
+template <typename PIX>
+static void launch_plf_p(int ss, hipStream_t st, int npred, const uint32_t *plist, int nlf, const uint32_t *llist,
+                         const WGRec *wgs, const SBRec *sbs, const PJob *jobs, const uint32_t *passes, const LFRec *recs,
+                         const FrameDesc *frames, const int16_t *resid, const uint32_t *ptab, int dbg)
+{
+    switch (ss) {
+    case 3: launch_plf_g<PIX, Geo<1, 1>>(st, npred, plist, nlf, llist, wgs, sbs, jobs, passes, recs, frames, resid, ptab, dbg); break;
+    case 1: launch_plf_g<PIX, Geo<1, 0>>(st, npred, plist, nlf, llist, wgs, sbs, jobs, passes, recs, frames, resid, ptab, dbg); break;
+    case 2: launch_plf_g<PIX, Geo<0, 1>>(st, npred, plist, nlf, llist, wgs, sbs, jobs, passes, recs, frames, resid, ptab, dbg); break;
+    default: launch_plf_g<PIX, Geo<0, 0>>(st, npred, plist, nlf, llist, wgs, sbs, jobs, passes, recs, frames, resid, ptab, dbg); break;
+    }
+}
 extern "C" {
 int vp9hip_launch_resid(int hb, hipStream_t st, int tcode, int n, const RJob *jobs, const FrameDesc *frames,
                         const void *coefs, int16_t *resid)
@@ -1429,6 +1472,15 @@ int vp9hip_launch_lf(int fmt, hipStream_t st, int nsb, const uint32_t *list, con
     if (nsb <= 0) return 0;
     if (fmt & 1) launch_lf_p<uint16_t>(fmt >> 1, st, nsb, list, recs, frames, dbg);
     else         launch_lf_p<uint8_t>(fmt >> 1, st, nsb, list, recs, frames, dbg);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int vp9hip_launch_plf(int fmt, hipStream_t st, int npred, const uint32_t *plist, int nlf, const uint32_t *llist,
+                      const WGRec *wgs, const SBRec *sbs, const PJob *jobs, const uint32_t *passes, const LFRec *recs,
+                      const FrameDesc *frames, const int16_t *resid, const uint32_t *ptab, int dbg)
+{
+    if (npred + nlf <= 0) return 0;
+    if (fmt & 1) launch_plf_p<uint16_t>(fmt >> 1, st, npred, plist, nlf, llist, wgs, sbs, jobs, passes, recs, frames, resid, ptab, dbg);
+    else         launch_plf_p<uint8_t>(fmt >> 1, st, npred, plist, nlf, llist, wgs, sbs, jobs, passes, recs, frames, resid, ptab, dbg);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int vp9hip_launch_mc(int hb, hipStream_t st, int n, const McUnit *units, const FrameDesc *frames)

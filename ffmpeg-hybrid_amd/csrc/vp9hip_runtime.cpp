@@ -42,19 +42,28 @@ int vp9hip_launch_pred(int fmt, hipStream_t st, int nwg, const uint32_t *list, c
 int vp9hip_launch_lf(int fmt, hipStream_t st, int nsb, const uint32_t *list, const LFRec *recs,
                      const FrameDesc *frames, int dbg);
 int vp9hip_launch_mc(int hb, hipStream_t st, int n, const McUnit *units, const FrameDesc *frames);
+int vp9hip_launch_plf(int fmt, hipStream_t st, int npred, const uint32_t *plist, int nlf, const uint32_t *llist,
+                      const WGRec *wgs, const SBRec *sbs, const PJob *jobs, const uint32_t *passes, const LFRec *recs,
+                      const FrameDesc *frames, const int16_t *resid, const uint32_t *ptab, int dbg);
 }
 
 namespace {
 
-enum { K_MC, K_RESID, K_PRED, K_LF, K_N };
-const char *const kname[K_N] = { "k_mc", "k_resid", "k_pred", "k_lf" };
+enum { K_MC, K_RESID, K_PRED, K_LF, K_PLF, K_N };
+const char *const kname[K_N] = { "k_mc", "k_resid", "k_pred", "k_lf", "k_plf" };
 
 // ff_vp9_intra_txfm_type (vp9data.c:437-452)
 const uint8_t intra_txfm_type[14] = { 2, 1, 0, 0, 3, 2, 1, 2, 1, 3, 0, 0, 0, 0 };
 
-struct Launch { int kind; uint32_t off; uint32_t n; int arg; int grp; int ph; int part; };
+// step: wavefront diagonal of a K_PRED (x_in_tile + y) or K_LF (x + 2y) launch; K_PLF
+// (intra diagonal `step` + LF diagonal step - PLF_LAG in one launch): off / n the intra
+// workgroups, off2 / n2 the LF SBs
+struct Launch { int kind; uint32_t off; uint32_t n; int arg; int grp; int ph; int part; int step;
+                uint32_t off2 = 0, n2 = 0; };
+#define PLF_LAG 3   // see the schedule in stage()
 enum { PART_RECON, PART_LF };           // a phase's reconstruction launches, then its loop filter
-#define MAX_GROUPS 4                    // independent frame groups = concurrent launch chains
+#define MAX_GROUPS 8                    // independent frame groups = concurrent launch chains
+#define LF_LAG 2                        // LF diagonal j needs intra diagonals <= j + LF_LAG (see enqueue_batch)
 
 struct Staged {
     // host images (kept for rebuilds / inspection)
@@ -84,7 +93,7 @@ struct Staged {
     std::vector<int> frame_log2;        // log2 tile columns of each batch frame
     int tile_lo = 0, tile_hi = 64;      // tile columns this context reconstructs (sharded batches)
     std::vector<uint8_t> coefs;         // concatenated coefficient streams (bytes)
-    double alg_bytes[K_N] = { 0, 0, 0, 0 };
+    double alg_bytes[K_N] = { 0, 0, 0, 0, 0 };
     // device arena
     uint8_t *arena = nullptr;
     size_t arena_cap = 0;
@@ -102,8 +111,13 @@ struct vp9hip_ctx {
     int dev = 0;
     hipStream_t st = nullptr;           // main stream: uploads, downloads, group 0
     hipStream_t xst[MAX_GROUPS - 1] = {};   // groups 1.. of a batch (joined back into st)
-    hipEvent_t fork_ev = nullptr, join_ev[MAX_GROUPS - 1] = {};
-    int max_groups = 3;                 // VP9HIP_STREAMS overrides (1..4); 3 measured best at C3, with even chain splits
+    hipStream_t lst[MAX_GROUPS] = {};       // per group: its loop-filter launches (lf_overlap)
+    hipEvent_t fork_ev = nullptr, join_ev[2 * MAX_GROUPS] = {};
+    hipEvent_t lf_done[MAX_GROUPS] = {};
+    std::vector<hipEvent_t> sev;            // recon -> LF step events (lf_overlap)
+    int max_groups = 3;                 // VP9HIP_STREAMS overrides (1..8); 3 measured best at C3, with even chain splits
+    bool lf_overlap = false;            // VP9HIP_LF_OVERLAP=1: LF on a second stream per group (measured slower)
+    bool fuse_plf = true;               // VP9HIP_PLF=0: no fused intra + LF launches
     int w = 0, h = 0, bpp = 8, ss_h = 1, ss_v = 1, hb = 0, bypp = 1;
     int cols = 0, rows = 0, sb_cols = 0, sb_rows = 0;
     int pitch[2] = { 0, 0 };
@@ -118,8 +132,8 @@ struct vp9hip_ctx {
     bool timing = true;
     std::vector<hipEvent_t> ev;
     bool timed_run = false;             // the last run recorded per-launch events
-    double kms[K_N] = { 0, 0, 0, 0 };
-    int kcount[K_N] = { 0, 0, 0, 0 };
+    double kms[K_N] = { 0, 0, 0, 0, 0 };
+    int kcount[K_N] = { 0, 0, 0, 0, 0 };
 };
 
 #define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
@@ -135,8 +149,14 @@ extern "C" int vp9hip_open(int device, vp9hip_ctx **out)
     if (const char *d = getenv("VP9HIP_DEBUG")) c->dbg = atoi(d);
     if (const char *g = getenv("VP9HIP_GRAPH")) c->use_graph = atoi(g) != 0;
     if (const char *g = getenv("VP9HIP_STREAMS")) c->max_groups = std::max(1, std::min(MAX_GROUPS, atoi(g)));
+    if (const char *g = getenv("VP9HIP_LF_OVERLAP")) c->lf_overlap = atoi(g) != 0;
+    if (const char *g = getenv("VP9HIP_PLF")) c->fuse_plf = atoi(g) != 0;
     bool ok = hipSetDevice(device) == hipSuccess && hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) == hipSuccess;
+    for (int i = 0; ok && i < MAX_GROUPS; i++)
+        ok = hipStreamCreateWithFlags(&c->lst[i], hipStreamNonBlocking) == hipSuccess &&
+             hipEventCreateWithFlags(&c->lf_done[i], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&c->join_ev[MAX_GROUPS + i], hipEventDisableTiming) == hipSuccess;
     for (int i = 0; ok && i < MAX_GROUPS - 1; i++)
         ok = hipStreamCreateWithFlags(&c->xst[i], hipStreamNonBlocking) == hipSuccess &&
              hipEventCreateWithFlags(&c->join_ev[i], hipEventDisableTiming) == hipSuccess;
@@ -171,6 +191,12 @@ extern "C" void vp9hip_close(vp9hip_ctx *c)
         if (c->xst[i]) hipStreamDestroy(c->xst[i]);
         if (c->join_ev[i]) hipEventDestroy(c->join_ev[i]);
     }
+    for (int i = 0; i < MAX_GROUPS; i++) {
+        if (c->lst[i]) hipStreamDestroy(c->lst[i]);
+        if (c->lf_done[i]) hipEventDestroy(c->lf_done[i]);
+        if (c->join_ev[MAX_GROUPS + i]) hipEventDestroy(c->join_ev[MAX_GROUPS + i]);
+    }
+    for (auto e : c->sev) hipEventDestroy(e);
     if (c->fork_ev) hipEventDestroy(c->fork_ev);
     delete c;
 }
@@ -910,9 +936,20 @@ static int merge_mixed(Staged &s, uint32_t sbi)
     return 0;
 }
 
-static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bufs, const int *ref_bufs /*n*3 or null*/,
-                 int tile_lo = 0, int tile_hi = 64, int max_groups = 0)
+// Pixel bytes of SB (sbx, sby) of frame f (all planes, visible area): its share of the
+// frame's algorithmic bytes P.
+static double sb_bytes(const vp9hip_ctx *c, const vp9h_frame &f, int sbx, int sby)
 {
+    const int w = std::min(64, f.width - sbx * 64), h = std::min(64, f.height - sby * 64);
+    return (double) w * h * c->bypp * (1.0 + 2.0 / ((1 << c->ss_h) * (1 << c->ss_v)));
+}
+
+static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bufs, const int *ref_bufs /*n*3 or null*/,
+                 int tile_lo = 0, int tile_hi = 64, int max_groups = 0, bool tiled = false)
+{
+    // fused intra + LF launches need the LF of a phase in the same launch sequence as its
+    // reconstruction (not for tile-sharded batches: recon, exchange, then LF)
+    const bool fuse = c->fuse_plf && !tiled;
     if (!c || !pkts || n <= 0 || !out_bufs) return VP9HIP_EINVAL;
     if (c->bufs.empty()) return VP9HIP_EINVAL;
     hipSetDevice(c->dev);
@@ -1061,7 +1098,7 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     // reads + writes of k_resid
     for (int g = 0; g < G; g++)
         for (int ph = g * (maxpos + 1); ph < (g + 1) * (maxpos + 1); ph++) {
-            for (auto &mr : mcr[ph]) s.launches.push_back({ K_MC, mr.first, mr.second, 0, g, ph, PART_RECON });
+            for (auto &mr : mcr[ph]) s.launches.push_back({ K_MC, mr.first, mr.second, 0, g, ph, PART_RECON, 0 });
             for (int t = 0; t < 5; t++) {
                 const uint32_t off = (uint32_t) s.rjobs.size();
                 for (int tp = 0; tp < 4; tp++) {
@@ -1070,24 +1107,65 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
                     s.rjobs.insert(s.rjobs.end(), s.rbucket[ph][t][tp].begin(), s.rbucket[ph][t][tp].end());
                 }
                 if (s.rjobs.size() > off)
-                    s.launches.push_back({ K_RESID, off, (uint32_t) (s.rjobs.size() - off), t, g, ph, PART_RECON });
+                    s.launches.push_back({ K_RESID, off, (uint32_t) (s.rjobs.size() - off), t, g, ph, PART_RECON, 0 });
             }
-            auto add_list = [&](int kind, const std::vector<uint32_t> &v) {
+            auto add_list = [&](int kind, const std::vector<uint32_t> &v, int step) {
                 if (v.empty()) return;
                 s.launches.push_back({ kind, (uint32_t) s.lists.size(), (uint32_t) v.size(), 0, g, ph,
-                                       kind == K_LF ? PART_LF : PART_RECON });
+                                       kind == K_LF ? PART_LF : PART_RECON, step });
                 s.lists.insert(s.lists.end(), v.begin(), v.end());
             };
-            for (auto &v : psteps[ph]) {
-                std::vector<uint32_t> wl;             // one workgroup per SB of the step
-                for (size_t i = 0; i < v.size(); i++) {
-                    wl.push_back((uint32_t) s.wgs.size());
+            std::vector<std::vector<uint32_t>> wls(psteps[ph].size());
+            for (size_t d = 0; d < psteps[ph].size(); d++) {
+                const auto &v = psteps[ph][d];
+                for (size_t i = 0; i < v.size(); i++) {   // one workgroup per SB of the step
+                    wls[d].push_back((uint32_t) s.wgs.size());
                     int r = merge_mixed(s, v[i]);
                     if (r) return r;
                 }
-                add_list(K_PRED, wl);
             }
-            for (auto &v : lsteps[ph]) add_list(K_LF, v);
+            if (!fuse) {
+                for (size_t d = 0; d < wls.size(); d++) add_list(K_PRED, wls[d], (int) d);
+                for (size_t d = 0; d < lsteps[ph].size(); d++) add_list(K_LF, lsteps[ph][d], (int) d);
+                continue;
+            }
+            // Fused schedule: launch t runs intra diagonal t and LF diagonal t - PLF_LAG.
+            // LF of SB (x, y) (diagonal x + 2y = j) rewrites pre-LF pixels of SBs
+            // (x - 1 .. x, y - 1 .. y) that the intra blocks of SBs (x - 1 .. x + 1, y .. y + 1)
+            // read; those are on intra diagonals <= x_in_tile + y + 2 <= j + 2, i.e. in earlier
+            // launches. Conversely the intra diagonal t reads SBs on diagonals t - 1, t - 2,
+            // whose pixels no LF SB of diagonal t - 3 touches (that needs x - x_in_tile + y < 0).
+            // This is the ordering the reference gets from its pre-LF intra_pred_data row
+            // (vp9.c:1404-1416), without a second copy.
+            const int np = (int) wls.size(), nlf = (int) lsteps[ph].size();
+            const int nt = std::max(np, nlf ? nlf + PLF_LAG : 0);
+            for (int t = 0; t < nt; t++) {
+                const std::vector<uint32_t> *pv = t < np && !wls[t].empty() ? &wls[t] : nullptr;
+                const int j = t - PLF_LAG;
+                const std::vector<uint32_t> *lv = j >= 0 && j < nlf && !lsteps[ph][j].empty() ? &lsteps[ph][j] : nullptr;
+                if (pv && lv) {
+                    Launch L = { K_PLF, (uint32_t) s.lists.size(), (uint32_t) pv->size(), 0, g, ph, PART_RECON, t };
+                    s.lists.insert(s.lists.end(), pv->begin(), pv->end());
+                    L.off2 = (uint32_t) s.lists.size();
+                    L.n2 = (uint32_t) lv->size();
+                    s.lists.insert(s.lists.end(), lv->begin(), lv->end());
+                    s.launches.push_back(L);
+                    // algorithmic bytes of the fused launch move from K_PRED / K_LF to K_PLF
+                    for (uint32_t w : *pv) {
+                        const SBRec &sb = s.sbs[s.wgs[w].sb[0]];
+                        const vp9h_frame &f = pkts[sb.frame];
+                        if (!(f.keyframe || f.intraonly)) continue;
+                        const double b = sb_bytes(c, f, sb.sbx, sb.sby);
+                        s.alg_bytes[K_PRED] -= b; s.alg_bytes[K_PLF] += b;
+                    }
+                    for (uint32_t li : *lv) {
+                        const LFRec &lr = s.lfs[li];
+                        const double b = 2.0 * sb_bytes(c, pkts[lr.frame], lr.sbx, lr.sby);
+                        s.alg_bytes[K_LF] -= b; s.alg_bytes[K_PLF] += b;
+                    }
+                } else if (pv) add_list(K_PRED, *pv, t);
+                else if (lv) add_list(K_LF, *lv, j);
+            }
         }
     if (s.resid16 > 0xffffffffull) return VP9HIP_ENOMEM;
 
@@ -1191,10 +1269,26 @@ static int launch_one(vp9hip_ctx *c, const Launch &L, hipStream_t st)
                                   (const uint32_t *) (s.arena + s.o_passes), fr, s.resid, c->ptab, c->dbg);
     case K_LF:
         return vp9hip_launch_lf(c->hb | c->ss_h << 1 | c->ss_v << 2, st, (int) L.n, lists + L.off, (const LFRec *) (s.arena + s.o_lfs), fr, c->dbg >> 16);
+    case K_PLF:
+        return vp9hip_launch_plf(c->hb | c->ss_h << 1 | c->ss_v << 2, st, (int) L.n, lists + L.off, (int) L.n2,
+                                 lists + L.off2, (const WGRec *) (s.arena + s.o_wgs), (const SBRec *) (s.arena + s.o_sbs),
+                                 (const PJob *) (s.arena + s.o_pjobs), (const uint32_t *) (s.arena + s.o_passes),
+                                 (const LFRec *) (s.arena + s.o_lfs), fr, s.resid, c->ptab, c->dbg);
     }
     return -1;
 }
 
+// Enqueue the staged launches: group g runs on its own stream (group 0 on the main
+// stream), forked from and joined back into the main stream.
+// lf_overlap: a group's loop filter runs on a second stream of its own, overlapping the
+// intra wavefront of the same phase. LF of SB (x, y) rewrites pre-LF pixels that intra
+// prediction reads: the last row / column of SB (x, y) and of its left / upper neighbours
+// (SB (x, y)'s left and top edges). Their readers are the intra blocks of SBs (x - 1 .. x + 1,
+// y .. y + 1), on intra diagonals <= x_in_tile + y + 2 <= (x + 2y) + LF_LAG. So LF diagonal j
+// (x + 2y = j) starts after intra diagonal j + LF_LAG (and after MC / residuals); the LF
+// stream is in order (the x + 2y wavefront), and the next phase's reconstruction (whose MC
+// reads post-LF references) waits for the phase's last LF launch. This is the ordering
+// the reference gets from its intra_pred_data backup of the pre-LF SB row (vp9.c:1404-1416).
 static int enqueue_batch(vp9hip_ctx *c)
 {
     Staged &s = c->stg;
@@ -1205,23 +1299,72 @@ static int enqueue_batch(vp9hip_ctx *c)
         c->ev.resize(2 * nl);
         for (size_t i = old; i < c->ev.size(); i++) HIPCHK(hipEventCreate(&c->ev[i]));
     }
-    // fork: groups 1.. start after everything queued on the main stream (uploads)
-    if (s.ngroups > 1) {
+    const bool ovl = c->lf_overlap;
+    auto rstream = [&](int g) { return g ? c->xst[g - 1] : c->st; };
+    // fork: every stream of the batch starts after what is queued on the main stream
+    if (s.ngroups > 1 || ovl) {
         HIPCHK(hipEventRecord(c->fork_ev, c->st));
         for (int g = 1; g < s.ngroups; g++) HIPCHK(hipStreamWaitEvent(c->xst[g - 1], c->fork_ev, 0));
+        if (ovl)
+            for (int g = 0; g < s.ngroups; g++) HIPCHK(hipStreamWaitEvent(c->lst[g], c->fork_ev, 0));
     }
+    // recon -> LF dependencies: for each LF launch, the recon launch (same group and phase)
+    // it must follow; events are recorded after those recon launches only
+    std::vector<int> lf_dep(nl, -1), rec_ev(nl, -1);
+    int nev = 0;
+    if (ovl) {
+        for (size_t i = 0; i < nl; i++) {
+            const Launch &L = s.launches[i];
+            if (L.kind != K_LF) continue;
+            int dep = -1;
+            for (size_t k = 0; k < nl; k++) {           // launches of the phase precede its LF
+                const Launch &R = s.launches[k];
+                if (R.ph != L.ph || R.kind == K_LF) continue;
+                if (R.kind != K_PRED || R.step <= L.step + LF_LAG) dep = (int) k;
+            }
+            lf_dep[i] = dep;
+            if (dep >= 0 && rec_ev[dep] < 0) rec_ev[dep] = nev++;
+        }
+        while ((int) c->sev.size() < nev) {
+            hipEvent_t e;
+            HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            c->sev.push_back(e);
+        }
+    }
+    std::vector<int> waited(s.ngroups, -1), last_lf_ph(s.ngroups, -1), rec_ph(s.ngroups, -1);
     for (size_t i = 0; i < nl; i++) {
         const Launch &L = s.launches[i];
-        hipStream_t st = L.grp ? c->xst[L.grp - 1] : c->st;
+        const bool lf = ovl && L.kind == K_LF;
+        hipStream_t st = lf ? c->lst[L.grp] : rstream(L.grp);
+        if (lf) {
+            if (lf_dep[i] >= 0 && lf_dep[i] != waited[L.grp]) {
+                HIPCHK(hipStreamWaitEvent(st, c->sev[rec_ev[lf_dep[i]]], 0));
+                waited[L.grp] = lf_dep[i];
+            }
+            last_lf_ph[L.grp] = L.ph;
+        } else if (ovl && rec_ph[L.grp] != L.ph) {
+            // a new phase's reconstruction follows the previous phase's loop filter
+            rec_ph[L.grp] = L.ph;
+            if (last_lf_ph[L.grp] >= 0) {
+                HIPCHK(hipEventRecord(c->lf_done[L.grp], c->lst[L.grp]));
+                HIPCHK(hipStreamWaitEvent(st, c->lf_done[L.grp], 0));
+            }
+        }
         if (c->timing) HIPCHK(hipEventRecord(c->ev[2 * i], st));
         if (launch_one(c, L, st)) return VP9HIP_EEXTERNAL;
         if (c->timing) HIPCHK(hipEventRecord(c->ev[2 * i + 1], st));
+        if (!lf && ovl && rec_ev[i] >= 0) HIPCHK(hipEventRecord(c->sev[rec_ev[i]], st));
     }
-    // join: the main stream (downloads, sync, the next stage) waits for every group
+    // join: the main stream (downloads, sync, the next stage) waits for every stream
     for (int g = 1; g < s.ngroups; g++) {
         HIPCHK(hipEventRecord(c->join_ev[g - 1], c->xst[g - 1]));
         HIPCHK(hipStreamWaitEvent(c->st, c->join_ev[g - 1], 0));
     }
+    if (ovl)
+        for (int g = 0; g < s.ngroups; g++) {
+            HIPCHK(hipEventRecord(c->join_ev[MAX_GROUPS + g], c->lst[g]));
+            HIPCHK(hipStreamWaitEvent(c->st, c->join_ev[MAX_GROUPS + g], 0));
+        }
     return 0;
 }
 
@@ -1230,7 +1373,7 @@ extern "C" int vp9hip_stage_batch_tiles(vp9hip_ctx *c, const vp9h_frame *pkts, i
                                         const int *ref_bufs, int tile_lo, int tile_hi)
 {
     if (tile_lo < 0 || tile_hi < tile_lo || tile_hi > 64) return VP9HIP_EINVAL;
-    return stage(c, pkts, n, out_bufs, ref_bufs, tile_lo, tile_hi, 1);   // one group: phases in chain order
+    return stage(c, pkts, n, out_bufs, ref_bufs, tile_lo, tile_hi, 1, true);   // one group: phases in chain order
 }
 
 extern "C" int vp9hip_batch_phases(vp9hip_ctx *c)
