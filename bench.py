@@ -106,9 +106,11 @@ def main():
     refs = gop_refs(args.frames, gop)
     t0 = time.time()
     ssh, ssv = CHROMA[args.chroma]
-    frames = [v.SynthFrame(v.synth_params(W, H, BPP, seed=frame_seed(rank, i, cidx), log2_tile_cols=LOG2_TILE_COLS,
-                                          inter=int(refs[i] is not None), ss_h=ssh, ss_v=ssv))
-              for i in range(args.frames)]
+    import concurrent.futures    # the C generator releases the GIL: frames in parallel
+    with concurrent.futures.ThreadPoolExecutor(min(16, os.cpu_count() or 1)) as ex:
+        frames = list(ex.map(lambda i: v.SynthFrame(v.synth_params(
+            W, H, BPP, seed=frame_seed(rank, i, cidx), log2_tile_cols=LOG2_TILE_COLS,
+            inter=int(refs[i] is not None), ss_h=ssh, ss_v=ssv)), range(args.frames)))
     t_gen = time.time() - t0
 
     dev = v.Device(local_rank)

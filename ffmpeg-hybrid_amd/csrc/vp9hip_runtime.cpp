@@ -18,7 +18,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <functional>
+#include <thread>
 #include <array>
 #include <cstdio>
 #include <cstdlib>
@@ -936,6 +938,44 @@ static int merge_mixed(Staged &s, uint32_t sbi)
     return 0;
 }
 
+// The work plan of one frame, built on its own (host threads in parallel): the Staged
+// images with frame-local indices, the intra diagonals' workgroups and LF diagonals' SBs.
+struct FramePlan {
+    Staged s;
+    std::vector<std::vector<uint32_t>> wsteps, lsteps;
+    int err = 0;
+};
+
+static int plan_frame(FrameBuild fb, FramePlan &fp)
+{
+    fp.s.rbucket.resize(1);
+    fb.phase = 0;
+    std::vector<std::vector<uint32_t>> ps;
+    int r = build_frame(nullptr, fp.s, fb, ps, fp.lsteps);
+    if (r < 0) return r;
+    fp.wsteps.resize(ps.size());
+    for (size_t d = 0; d < ps.size(); d++)
+        for (uint32_t sbi : ps[d]) {
+            fp.wsteps[d].push_back((uint32_t) fp.s.wgs.size());
+            r = merge_mixed(fp.s, sbi);
+            if (r) return r;
+        }
+    return 0;
+}
+
+// Host threads for batch planning: VP9HIP_HOST_THREADS, default min(16, hardware threads)
+// (16 = the CPU share of one GPU on the MI355X boxes).
+static int host_threads()
+{
+    static int n = 0;
+    if (!n) {
+        const char *e = getenv("VP9HIP_HOST_THREADS");
+        n = e ? atoi(e) : (int) std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+        n = std::max(1, std::min(64, n));
+    }
+    return n;
+}
+
 // Pixel bytes of SB (sbx, sby) of frame f (all planes, visible area): its share of the
 // frame's algorithmic bytes P.
 static double sb_bytes(const vp9hip_ctx *c, const vp9h_frame &f, int sbx, int sby)
@@ -1006,10 +1046,10 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     const int NP = G * (maxpos + 1);                   // phase id = g * (maxpos + 1) + pos
     s.nphases = NP;
     s.rbucket.assign(NP, {});
-    std::vector<std::vector<std::vector<uint32_t>>> psteps(NP), lsteps(NP);
-    std::vector<std::vector<std::pair<uint32_t, uint32_t>>> mcr(NP);   // MC unit ranges per phase
+    // per frame: validate, frame descriptor, reference scaling (sequential, cheap)
+    std::vector<FrameBuild> fbs(n);
+    std::vector<size_t> coef_off(n + 1, 0);
     uint64_t coef_base = 0;
-
     for (int i = 0; i < n; i++) {
         const vp9h_frame *f = &pkts[i];
         // frames up to the configured size share the buffers (reference scaling, vp9.c:845-880)
@@ -1017,7 +1057,6 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
             f->ss_h != c->ss_h || f->ss_v != c->ss_v)
             return VP9HIP_EINVAL;
         const int cols = (f->width + 7) >> 3, rows = (f->height + 7) >> 3;
-        const double pix_bytes = (double) f->width * f->height * c->bypp * (1.0 + 2.0 / ((1 << c->ss_h) * (1 << c->ss_v)));
         if (out_bufs[i] < 0 || out_bufs[i] >= (int) c->bufs.size()) return VP9HIP_EINVAL;
         const bool intra = f->keyframe || f->intraonly;
         FrameDesc fd;
@@ -1044,7 +1083,7 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
         }
         s.frames.push_back(fd);
         c->buf_wh[out_bufs[i]] = { f->width, f->height };
-        FrameBuild fb;
+        FrameBuild &fb = fbs[i];
         fb.f = f; fb.frame_idx = i;
         fb.cols = cols; fb.rows = rows; fb.sb_cols = fd.sb_cols; fb.sb_rows = fd.sb_rows;
         memset(fb.scale, 0, sizeof(fb.scale));
@@ -1074,24 +1113,79 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
         fb.tile_lo = tile_lo; fb.tile_hi = tile_hi;
         s.frame_phase[i] = fb.phase;
         s.frame_log2[i] = f->log2_tile_cols;
-        const size_t mc0 = s.mcs.size();
-        int r = build_frame(c, s, fb, psteps[fb.phase], lsteps[fb.phase]);
-        if (r < 0) return r;
-        if (s.mcs.size() > mc0) mcr[fb.phase].push_back({ (uint32_t) mc0, (uint32_t) (s.mcs.size() - mc0) });
-        size_t cb = (size_t) f->ncoefs * csz;
-        size_t off = s.coefs.size();
-        s.coefs.resize(off + cb);
-        if (cb) memcpy(s.coefs.data() + off, f->coefs, cb);
+        coef_off[i + 1] = coef_off[i] + (size_t) f->ncoefs * csz;
         coef_base += f->ncoefs;
         if (coef_base > 0xffffffffull) return VP9HIP_ENOMEM;
         // algorithmic bytes: reconstruction reads C and writes P (k_resid
         // owns C, k_pred owns P; inter residuals read + write their pixels in k_resid),
         // LF reads + writes P, MC reads R*P and writes the predicted pixels
-        s.alg_bytes[K_RESID] += (double) cb;
+        const double pix_bytes = (double) f->width * f->height * c->bypp * (1.0 + 2.0 / ((1 << c->ss_h) * (1 << c->ss_v)));
+        s.alg_bytes[K_RESID] += (double) f->ncoefs * csz;
         if (intra) s.alg_bytes[K_PRED] += pix_bytes;
         if (f->filter_level) s.alg_bytes[K_LF] += 2.0 * pix_bytes;
-        for (size_t m = mc0; m < s.mcs.size(); m++)
-            s.alg_bytes[K_MC] += (double) s.mcs[m].w * s.mcs[m].h * c->bypp * (1 + s.mcs[m].nref);
+    }
+
+    // work planning of every frame (independent), on host threads: jobs, dependency
+    // levels and pass packing, LF programs, MC units, coefficient copy
+    std::vector<FramePlan> plans(n);
+    s.coefs.resize(coef_off[n]);
+    {
+        std::atomic<int> next(0);
+        auto worker = [&]() {
+            for (int i; (i = next.fetch_add(1)) < n;) {
+                plans[i].err = plan_frame(fbs[i], plans[i]);
+                if (coef_off[i + 1] > coef_off[i]) memcpy(s.coefs.data() + coef_off[i], pkts[i].coefs, coef_off[i + 1] - coef_off[i]);
+            }
+        };
+        const int nt = std::min(n, host_threads());
+        std::vector<std::thread> pool;
+        for (int t = 1; t < nt; t++) pool.emplace_back(worker);
+        worker();
+        for (auto &t : pool) t.join();
+    }
+    // merge in frame order: local indices -> batch indices
+    std::vector<std::vector<std::vector<uint32_t>>> wsteps(NP), lsteps(NP);   // per phase: WG / LF lists
+    std::vector<std::vector<std::pair<uint32_t, uint32_t>>> mcr(NP);           // MC unit ranges per phase
+    for (int i = 0; i < n; i++) {
+        FramePlan &fp = plans[i];
+        if (fp.err < 0) return fp.err;
+        const int ph = fbs[i].phase;
+        Staged &l = fp.s;
+        const uint32_t sb_off = (uint32_t) s.sbs.size(), job_off = (uint32_t) s.pjobs.size();
+        const uint32_t pass_off = (uint32_t) s.passes.size(), wg_off = (uint32_t) s.wgs.size();
+        const uint32_t lf_off = (uint32_t) s.lfs.size(), mc_off = (uint32_t) s.mcs.size();
+        const uint64_t res_off = s.resid16;
+        if (res_off + l.resid16 > 0xffffffffull) return VP9HIP_ENOMEM;
+        s.sbs.insert(s.sbs.end(), l.sbs.begin(), l.sbs.end());
+        for (PJob j : l.pjobs) {
+            if (PJ_RES(j)) j.roff += (uint32_t) res_off;
+            s.pjobs.push_back(j);
+        }
+        s.passes.insert(s.passes.end(), l.passes.begin(), l.passes.end());
+        for (WGRec w : l.wgs) {
+            w.job0 += job_off; w.pass0 += pass_off; w.sb[0] += sb_off;
+            s.wgs.push_back(w);
+        }
+        for (int t = 0; t < 5; t++)
+            for (int tp = 0; tp < 4; tp++)
+                for (RJob r : l.rbucket[0][t][tp]) {
+                    if (!(r.ptx & 32)) r.dst += (uint32_t) res_off;      // intra: residual scratch offset
+                    s.rbucket[ph][t][tp].push_back(r);
+                }
+        s.resid16 += l.resid16;
+        s.lfs.insert(s.lfs.end(), l.lfs.begin(), l.lfs.end());
+        if (!l.mcs.empty()) {
+            s.mcs.insert(s.mcs.end(), l.mcs.begin(), l.mcs.end());
+            mcr[ph].push_back({ mc_off, (uint32_t) l.mcs.size() });
+        }
+        for (const McUnit &m : l.mcs) s.alg_bytes[K_MC] += (double) m.w * m.h * c->bypp * (1 + m.nref);
+        if (wsteps[ph].size() < fp.wsteps.size()) wsteps[ph].resize(fp.wsteps.size());
+        for (size_t d = 0; d < fp.wsteps.size(); d++)
+            for (uint32_t w : fp.wsteps[d]) wsteps[ph][d].push_back(w + wg_off);
+        if (lsteps[ph].size() < fp.lsteps.size()) lsteps[ph].resize(fp.lsteps.size());
+        for (size_t d = 0; d < fp.lsteps.size(); d++)
+            for (uint32_t li : fp.lsteps[d]) lsteps[ph][d].push_back(li + lf_off);
+        fp = FramePlan();                        // release the frame's host images early
     }
     // launch schedule per group, phases in chain order: MC, residuals by (tx code, txtp),
     // the intra SB wavefront, the LF wavefront; inter residual pixels are algorithmic
@@ -1115,15 +1209,7 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
                                        kind == K_LF ? PART_LF : PART_RECON, step });
                 s.lists.insert(s.lists.end(), v.begin(), v.end());
             };
-            std::vector<std::vector<uint32_t>> wls(psteps[ph].size());
-            for (size_t d = 0; d < psteps[ph].size(); d++) {
-                const auto &v = psteps[ph][d];
-                for (size_t i = 0; i < v.size(); i++) {   // one workgroup per SB of the step
-                    wls[d].push_back((uint32_t) s.wgs.size());
-                    int r = merge_mixed(s, v[i]);
-                    if (r) return r;
-                }
-            }
+            const std::vector<std::vector<uint32_t>> &wls = wsteps[ph];   // one workgroup per SB
             if (!fuse) {
                 for (size_t d = 0; d < wls.size(); d++) add_list(K_PRED, wls[d], (int) d);
                 for (size_t d = 0; d < lsteps[ph].size(); d++) add_list(K_LF, lsteps[ph][d], (int) d);
