@@ -111,7 +111,7 @@ ABI_SYMBOLS = ["vp9hip_open", "vp9hip_close", "vp9hip_configure", "vp9hip_submit
                "vp9hip_stripe", "vp9hip_frame_device", "vp9hip_batch_groups",
                "vp9h_decode_frame", "vp9h_encode_frame", "vp9h_frame_free", "vp9h_buffer_free",
                "vp9h_stream_open", "vp9h_stream_close", "vp9h_stream_decode", "vp9h_stream_encode",
-               "vp9h_enc_defaults", "vp9h_superframe_split",
+               "vp9h_enc_defaults", "vp9h_superframe_split", "vp9h_frame_type",
                "vp9hip_synth_defaults", "vp9hip_synth_frame", "vp9hip_synth_free",
                "vp9h_ivf_probe", "vp9h_ivf_read_header", "vp9h_ivf_read_frame", "vp9h_ivf_write_header",
                "vp9h_ivf_write_frame_header",
@@ -183,6 +183,7 @@ def lib():
     L.vp9h_enc_defaults.restype = None
     L.vp9h_superframe_split.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t),
                                         ctypes.POINTER(ctypes.c_size_t), ctypes.c_int]
+    L.vp9h_frame_type.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
     L.vp9h_ivf_probe.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
     L.vp9h_ivf_read_header.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(IvfHeader)]
     L.vp9h_ivf_read_frame.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t),
@@ -215,7 +216,7 @@ class IvfHeader(ctypes.Structure):
 
 class DecoderParams(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("max_batch", ctypes.c_int32), ("extra_bufs", ctypes.c_int32),
-                ("max_width", ctypes.c_int32), ("max_height", ctypes.c_int32)]
+                ("max_width", ctypes.c_int32), ("max_height", ctypes.c_int32), ("parse_threads", ctypes.c_int32)]
 
 
 class DecodedFrameInfo(ctypes.Structure):
@@ -594,11 +595,13 @@ class Decoder:
     is needed (EAGAIN) or after the drain (EOF, which also sets .eof).
     """
 
-    def __init__(self, device=0, max_batch=16, extra_bufs=4, max_width=0, max_height=0):
+    def __init__(self, device=0, max_batch=16, extra_bufs=4, max_width=0, max_height=0, parse_threads=None):
         self.params = DecoderParams()
         lib().vp9hip_decoder_defaults(ctypes.byref(self.params))
         self.params.device, self.params.max_batch, self.params.extra_bufs = device, max_batch, extra_bufs
         self.params.max_width, self.params.max_height = max_width, max_height
+        if parse_threads is not None:
+            self.params.parse_threads = parse_threads
         self._d = ctypes.c_void_p()
         _check("vp9hip_decoder_open", lib().vp9hip_decoder_open(ctypes.byref(self.params), ctypes.byref(self._d)))
         self.eof = False
@@ -680,6 +683,13 @@ class Decoder:
             if got is None:
                 break
             yield got
+
+
+def vp9h_type(data):
+    """Frame type from the header's first bits (vp9h_frame_type): 0 key, 1 other, 2
+    show_existing_frame, or a negative AVERROR."""
+    data = bytes(data)
+    return lib().vp9h_frame_type(data, len(data))
 
 
 # ---- IVF (libavformat/ivfdec.c, ivfenc.c) -------------------------------------------

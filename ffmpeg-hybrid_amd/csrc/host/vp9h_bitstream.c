@@ -2056,7 +2056,7 @@ static void fill_packet(Walk *w, vp9h_frame *out)
     memset(out, 0, sizeof(*out));
     out->width = h->w; out->height = h->h; out->bpp = (uint8_t) h->bpp;
     out->ss_h = (uint8_t) h->ss_h; out->ss_v = (uint8_t) h->ss_v;
-    out->keyframe = (uint8_t) h->keyframe; out->intraonly = (uint8_t) h->intraonly;
+    out->keyframe = (uint8_t) h->keyframe; out->intraonly = (uint8_t) (h->intraonly && !h->keyframe);  /* stale after a keyframe */
     out->lossless = (uint8_t) h->lossless;
     out->filter_level = (uint8_t) h->filter_level; out->sharpness = (uint8_t) h->sharpness;
     out->log2_tile_cols = (uint8_t) h->log2_tile_cols; out->log2_tile_rows = (uint8_t) h->log2_tile_rows;
@@ -2373,6 +2373,23 @@ void vp9h_buffer_free(uint8_t *p) { free(p); }
 /* ------------------------------------------------------------------ container side */
 /* vp9_superframe_split_bsf (bsf/vp9_superframe_split.c:40-95): the frames of a
  * superframe, from the index at its end; one frame otherwise */
+/* The frame type from the first header bits (vp9.c:521-545): 0 keyframe, 1 other frame,
+ * 2 show_existing_frame; AVERROR_INVALIDDATA for a bad marker / profile. A keyframe's
+ * parse depends on no earlier frame (contexts, loop-filter deltas, segmentation and the
+ * reference slots are all reset, vp9.c:557-569, 882-892), which lets a decoder parse it
+ * on a fresh vp9h_stream in parallel with the frames before it. */
+int vp9h_frame_type(const uint8_t *data, size_t size)
+{
+    if (!data || size < 1) return VP9HIP_EINVALIDDATA;
+    const unsigned b = (unsigned) data[0] << 8 | (size > 1 ? data[1] : 0);
+    if ((b >> 14) != 2) return VP9HIP_EINVALIDDATA;                 /* frame marker */
+    const int prof = (b >> 13 & 1) | (b >> 12 & 1) << 1;
+    int pos = 12;                                                    /* next bit (from the top) */
+    if (prof == 3 && (b >> --pos & 1)) return VP9HIP_EINVALIDDATA;  /* reserved bit */
+    if (b >> --pos & 1) return 2;                                    /* show_existing_frame */
+    return (b >> --pos & 1) ? 1 : 0;                                 /* frame_type: 0 = key */
+}
+
 int vp9h_superframe_split(const uint8_t *data, size_t size, size_t *offsets, size_t *sizes, int cap)
 {
     if (!data || size < 1) return VP9HIP_EINVAL;

@@ -9,47 +9,77 @@
 //   - every decoded frame goes to the slots of its refresh mask (vp9.c:1686-1691,
 //     1845-1849); hidden frames (show_frame = 0) are decoded but not output;
 //   - inter frames read their LAST / GOLDEN / ALTREF slots (s->s.h.refidx).
-// Frames are parsed on the host as packets arrive and reconstructed on the GPU in
-// batches of up to max_batch frames (vp9hip_stage_batch_refs: reference chains in
-// order, independent chains concurrently); the parse of the next batch overlaps the
-// GPU work of the previous one. receive_frame hands out frames whose batch has been
-// submitted, in output order. Like libavcodec's frame threading, this adds decoder delay
-// (up to max_batch frames); flushing (send_packet with data = NULL) drains it.
+//
+// Pipeline:
+//   1. host parse on a pool of threads. Frames of one parse chain parse in order on one
+//      vp9h_stream; a keyframe starts a new chain on a fresh vp9h_stream, because its
+//      parse depends on no earlier frame (vp9h_frame_type). All-keyframe streams thus
+//      parse frame-parallel, GOP streams GOP-parallel (the reference's frame threads get
+//      the same freedom from ff_thread_finish_setup after the header, vp9.c:1736);
+//   2. in decode order, on the caller's thread: reference slots, device buffers, and
+//      batches of up to max_batch frames staged and launched on the GPU
+//      (vp9hip_stage_batch_refs: reference chains in order, independent chains
+//      concurrently; the batch planning itself runs on host threads);
+//   3. receive_frame hands out frames whose batch has been launched, in output order.
+// Like libavcodec's frame threading this adds decoder delay (up to max_batch frames plus
+// the frames in parse); flushing (send_packet with data = NULL) drains it.
+#include <condition_variable>
 #include <cstring>
 #include <deque>
+#include <memory>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../../include/vp9hip.h"
 
 namespace {
+struct ParseJob;
+struct Chain {                         // one parse state: its frames parse in order
+    vp9h_stream *st = nullptr;
+    std::deque<ParseJob *> q;          // queued, not started
+    bool scheduled = false;            // on the run queue or being run by a worker
+    ~Chain() { if (st) vp9h_stream_close(st); }
+};
+struct ParseJob {
+    std::vector<uint8_t> data;
+    int64_t pts = 0;
+    std::shared_ptr<Chain> chain;
+    vp9h_frame pkt;
+    vp9h_frame_info info;
+    int ret = 0;
+    bool done = false;
+    ParseJob() { memset(&pkt, 0, sizeof(pkt)); memset(&info, 0, sizeof(info)); }
+};
 struct Pending { vp9h_frame pkt; int out; int refs[3]; };   // refs: -1 for keyframes / intra-only
 struct Out { int buf; int64_t pts; bool submitted; };
+const int STALL = 1;                   // consume: no free device buffer until frames are released
 }
 
 struct vp9hip_decoder {
     vp9hip_decoder_params p;
     vp9hip_ctx *ctx = nullptr;
-    vp9h_stream *st = nullptr;
     bool configured = false, draining = false;
     int cw = 0, ch = 0, cbpp = 0, css_h = 0, css_v = 0, nbufs = 0;
     int slot[8];
     std::vector<int> pins, busy, bw, bh;   // per device buffer
     std::vector<Pending> batch;
     std::deque<Out> outq;
-    int64_t decoded = 0;
+    // parse pipeline
+    std::deque<std::unique_ptr<ParseJob>> inflight;   // decode order
+    std::shared_ptr<Chain> chain;                     // the chain of the next non-key frame
+    std::mutex mu;
+    std::condition_variable cv_work, cv_done;
+    std::deque<std::shared_ptr<Chain>> runq;
+    std::vector<std::thread> workers;
+    bool stop = false;
+    int max_inflight = 0;
 };
 
 static int slot_refs(const vp9hip_decoder *d, int b)
 {
     int n = 0;
     for (int s = 0; s < 8; s++) n += d->slot[s] == b;
-    return n;
-}
-
-static int free_buffers(const vp9hip_decoder *d)
-{
-    int n = 0;
-    for (int b = 0; b < d->nbufs; b++) n += !d->pins[b] && !d->busy[b] && !slot_refs(d, b);
     return n;
 }
 
@@ -60,6 +90,73 @@ static int alloc_buffer(vp9hip_decoder *d)
     return -1;
 }
 
+// ---- parse workers ----
+static void parse_one(ParseJob *j)
+{
+    j->ret = vp9h_stream_decode(j->chain->st, j->data.data(), j->data.size(), &j->pkt, &j->info);
+}
+
+static void worker_main(vp9hip_decoder *d)
+{
+    std::unique_lock<std::mutex> lk(d->mu);
+    for (;;) {
+        d->cv_work.wait(lk, [&] { return d->stop || !d->runq.empty(); });
+        if (d->stop) return;
+        std::shared_ptr<Chain> c = d->runq.front();
+        d->runq.pop_front();
+        while (!c->q.empty()) {                       // the chain's frames, in order
+            ParseJob *j = c->q.front();
+            c->q.pop_front();
+            lk.unlock();
+            parse_one(j);
+            lk.lock();
+            j->done = true;
+            d->cv_done.notify_all();
+        }
+        c->scheduled = false;
+    }
+}
+
+static void enqueue_parse(vp9hip_decoder *d, std::unique_ptr<ParseJob> j)
+{
+    ParseJob *raw = j.get();
+    if (d->workers.empty()) {                         // no pool: parse now, in order
+        parse_one(raw);
+        raw->done = true;
+        d->inflight.push_back(std::move(j));
+        return;
+    }
+    std::lock_guard<std::mutex> lk(d->mu);
+    d->inflight.push_back(std::move(j));
+    Chain *c = raw->chain.get();
+    c->q.push_back(raw);
+    if (!c->scheduled) {
+        c->scheduled = true;
+        d->runq.push_back(raw->chain);
+        d->cv_work.notify_one();
+    }
+}
+
+static bool front_done(vp9hip_decoder *d, bool block)
+{
+    if (d->inflight.empty()) return false;
+    if (d->workers.empty()) return true;
+    std::unique_lock<std::mutex> lk(d->mu);
+    if (block) d->cv_done.wait(lk, [&] { return d->inflight.front()->done; });
+    return d->inflight.front()->done;
+}
+
+static void wait_all_parsed(vp9hip_decoder *d)
+{
+    if (d->workers.empty()) return;
+    std::unique_lock<std::mutex> lk(d->mu);
+    d->cv_done.wait(lk, [&] {
+        for (auto &j : d->inflight) if (!j->done) return false;
+        return true;
+    });
+}
+
+// ---- device side ----
 // Stage + launch the pending frames as one batch.
 static int submit(vp9hip_decoder *d)
 {
@@ -101,11 +198,84 @@ static int configure(vp9hip_decoder *d, const vp9h_frame &f)
     return 0;
 }
 
+// One parsed frame, in decode order: slots, buffer, batch. 0, STALL (no free buffer;
+// the job stays queued) or an error.
+static int consume_one(vp9hip_decoder *d, ParseJob &j)
+{
+    if (j.ret < 0) return j.ret;
+    vp9h_frame &f = j.pkt;
+    const vp9h_frame_info &info = j.info;
+    if (info.show_existing_frame) {
+        const int b = d->configured ? d->slot[info.show_slot & 7] : -1;
+        if (b < 0) return VP9HIP_EINVALIDDATA;
+        d->pins[b]++;
+        d->outq.push_back({ b, j.pts, d->batch.empty() });
+        return 0;
+    }
+    const bool intra = f.keyframe || f.intraonly;
+    if (!d->configured || f.bpp != d->cbpp || f.ss_h != d->css_h || f.ss_v != d->css_v ||
+        f.width > d->cw || f.height > d->ch) {
+        // a new format or size: only at an intra frame with nothing outstanding
+        int r = submit(d);
+        if (r < 0) return r;
+        bool idle = true;
+        for (int b = 0; b < d->nbufs && idle; b++) idle = !d->pins[b];
+        if (!intra) return d->configured ? VP9HIP_ENOSYS : VP9HIP_EINVALIDDATA;
+        if (!idle) return STALL;          // frames of the old format are still out: receive / release them
+        r = configure(d, f);
+        if (r < 0) return r;
+    }
+    int out = alloc_buffer(d);
+    if (out < 0) {                        // the batch's busy buffers come back when it is launched
+        int r = submit(d);
+        if (r < 0) return r;
+        out = alloc_buffer(d);
+        if (out < 0) return STALL;
+    }
+    Pending q;
+    q.pkt = f;
+    q.out = out;
+    for (int i = 0; i < 3; i++) {
+        q.refs[i] = intra ? -1 : d->slot[info.ref_slot[i] & 7];
+        if (!intra && q.refs[i] < 0) return VP9HIP_EINVALIDDATA;
+    }
+    memset(&f, 0, sizeof(f));            // the batch owns the packet now
+    d->busy[q.out]++;
+    for (int i = 0; i < 3; i++)
+        if (q.refs[i] >= 0) d->busy[q.refs[i]]++;
+    d->bw[q.out] = q.pkt.width; d->bh[q.out] = q.pkt.height;
+    for (int s = 0; s < 8; s++)
+        if (info.refresh_mask & (1 << s)) d->slot[s] = q.out;
+    d->batch.push_back(q);
+    if (info.show_frame) {
+        d->pins[q.out]++;
+        d->outq.push_back({ q.out, j.pts, false });
+    }
+    if ((int) d->batch.size() >= d->p.max_batch) return submit(d);
+    return 0;
+}
+
+// Consume parsed frames in decode order; block: wait for their parse. Returns 0 when the
+// parsed front is consumed (or nothing is ready), STALL, or an error.
+static int consume(vp9hip_decoder *d, bool block, size_t keep = 0)
+{
+    while (d->inflight.size() > keep && front_done(d, block)) {
+        int r = consume_one(d, *d->inflight.front());
+        if (r == STALL) return STALL;
+        vp9h_frame_free(&d->inflight.front()->pkt);
+        d->inflight.pop_front();
+        if (r < 0) return r;
+    }
+    return 0;
+}
+
+// ---- C-ABI ----
 extern "C" void vp9hip_decoder_defaults(vp9hip_decoder_params *p)
 {
     memset(p, 0, sizeof(*p));
     p->max_batch = 16;
     p->extra_bufs = 4;
+    p->parse_threads = (int) std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
 }
 
 extern "C" int vp9hip_decoder_open(const vp9hip_decoder_params *params, vp9hip_decoder **out)
@@ -116,19 +286,36 @@ extern "C" int vp9hip_decoder_open(const vp9hip_decoder_params *params, vp9hip_d
     if (params) d->p = *params; else vp9hip_decoder_defaults(&d->p);
     if (d->p.max_batch <= 0) d->p.max_batch = 1;
     if (d->p.max_batch > 256) d->p.max_batch = 256;
+    if (d->p.parse_threads < 0) d->p.parse_threads = 0;
+    if (d->p.parse_threads > 64) d->p.parse_threads = 64;
+    d->max_inflight = std::max(2 * d->p.parse_threads, d->p.max_batch) + 1;
     for (int s = 0; s < 8; s++) d->slot[s] = -1;
     int r = vp9hip_open(d->p.device, &d->ctx);
-    if (r >= 0) r = vp9h_stream_open(&d->st);
     if (r < 0) { vp9hip_decoder_close(d); return r; }
+    for (int t = 0; t < d->p.parse_threads; t++) d->workers.emplace_back(worker_main, d);
     *out = d;
     return 0;
+}
+
+static void drop_inflight(vp9hip_decoder *d)
+{
+    wait_all_parsed(d);
+    for (auto &j : d->inflight) vp9h_frame_free(&j->pkt);
+    d->inflight.clear();
 }
 
 extern "C" void vp9hip_decoder_close(vp9hip_decoder *d)
 {
     if (!d) return;
+    drop_inflight(d);
+    {
+        std::lock_guard<std::mutex> lk(d->mu);
+        d->stop = true;
+    }
+    d->cv_work.notify_all();
+    for (auto &t : d->workers) t.join();
     for (auto &f : d->batch) vp9h_frame_free(&f.pkt);
-    if (d->st) vp9h_stream_close(d->st);
+    d->chain.reset();
     if (d->ctx) vp9hip_close(d->ctx);
     delete d;
 }
@@ -138,80 +325,52 @@ extern "C" vp9hip_ctx *vp9hip_decoder_context(vp9hip_decoder *d) { return d ? d-
 extern "C" int vp9hip_decoder_send_packet(vp9hip_decoder *d, const uint8_t *data, size_t size, int64_t pts)
 {
     if (!d) return VP9HIP_EINVAL;
-    if (!data || !size) {                      // flush: drain the decoder delay
+    if (!data || !size) {                      // flush: drain the decoder delay (receive_frame does it)
         d->draining = true;
-        return submit(d);
+        int r = consume(d, false);
+        return r < 0 ? r : 0;
     }
     if (d->draining) return VP9HIP_EOF;
     size_t offs[8], sizes[8];
     const int nf = vp9h_superframe_split(data, size, offs, sizes, 8);
     if (nf < 0) return nf;
-    // every frame of the packet may need a buffer: ask for output to be read first
-    // (avcodec_send_packet's EAGAIN) instead of parsing what cannot be placed
-    if (d->configured && free_buffers(d) < nf) {
-        int r = submit(d);
+    // bound the frames in flight: consume parsed ones first; a stall (no free device
+    // buffer) asks the caller to receive frames (avcodec_send_packet's EAGAIN)
+    if (d->inflight.size() + nf > (size_t) d->max_inflight) {
+        int r = consume(d, true, d->max_inflight > nf ? d->max_inflight - nf : 0);
         if (r < 0) return r;
-        if (free_buffers(d) < nf) return VP9HIP_EAGAIN;
+        if (r == STALL) return VP9HIP_EAGAIN;
     }
     for (int k = 0; k < nf; k++) {
-        vp9h_frame f;
-        vp9h_frame_info info;
-        memset(&f, 0, sizeof(f));
-        int r = vp9h_stream_decode(d->st, data + offs[k], sizes[k], &f, &info);
-        if (r < 0) return r;
-        if (info.show_existing_frame) {
-            const int b = d->configured ? d->slot[info.show_slot & 7] : -1;
-            if (b < 0) return VP9HIP_EINVALIDDATA;
-            d->pins[b]++;
-            d->outq.push_back({ b, pts, d->batch.empty() });
-            continue;
-        }
-        const bool intra = f.keyframe || f.intraonly;
-        if (!d->configured || f.bpp != d->cbpp || f.ss_h != d->css_h || f.ss_v != d->css_v ||
-            f.width > d->cw || f.height > d->ch) {
-            // a new format or size: only at a keyframe with nothing outstanding
-            bool idle = d->batch.empty();
-            for (int b = 0; b < d->nbufs && idle; b++) idle = !d->pins[b];
-            if (!intra || !idle) { vp9h_frame_free(&f); return d->configured ? VP9HIP_ENOSYS : VP9HIP_EINVALIDDATA; }
-            r = configure(d, f);
-            if (r < 0) { vp9h_frame_free(&f); return r; }
-        }
-        Pending q;
-        q.pkt = f;
-        q.out = alloc_buffer(d);
-        if (q.out < 0) { vp9h_frame_free(&f); return VP9HIP_EBUG; }
-        for (int i = 0; i < 3; i++) {
-            q.refs[i] = intra ? -1 : d->slot[info.ref_slot[i] & 7];
-            if (!intra && q.refs[i] < 0) { vp9h_frame_free(&f); return VP9HIP_EINVALIDDATA; }
-        }
-        d->busy[q.out]++;
-        for (int i = 0; i < 3; i++)
-            if (q.refs[i] >= 0) d->busy[q.refs[i]]++;
-        d->bw[q.out] = f.width; d->bh[q.out] = f.height;
-        for (int s = 0; s < 8; s++)
-            if (info.refresh_mask & (1 << s)) d->slot[s] = q.out;
-        d->batch.push_back(q);
-        d->decoded++;
-        if (info.show_frame) {
-            d->pins[q.out]++;
-            d->outq.push_back({ q.out, pts, false });
-        }
-        if ((int) d->batch.size() >= d->p.max_batch) {
-            r = submit(d);
+        const int type = vp9h_frame_type(data + offs[k], sizes[k]);
+        if (type < 0) return type;
+        std::unique_ptr<ParseJob> j(new ParseJob());
+        j->data.assign(data + offs[k], data + offs[k] + sizes[k]);
+        j->pts = pts;
+        if (type == 0 || !d->chain) {          // a keyframe parses on a fresh stream
+            std::shared_ptr<Chain> c = std::make_shared<Chain>();
+            int r = vp9h_stream_open(&c->st);
             if (r < 0) return r;
+            d->chain = c;
         }
+        j->chain = d->chain;
+        enqueue_parse(d, std::move(j));
     }
-    return 0;
+    int r = consume(d, false);
+    return r < 0 ? r : 0;
 }
 
 extern "C" int vp9hip_decoder_receive_frame(vp9hip_decoder *d, vp9hip_decoded_frame *out)
 {
     if (!d || !out) return VP9HIP_EINVAL;
-    if (!d->outq.empty() && !d->outq.front().submitted && d->draining) {
-        int r = submit(d);
+    int r = consume(d, d->draining);
+    if (r < 0) return r;
+    if (d->draining) {                         // everything parsed that can be placed: launch it
+        r = submit(d);
         if (r < 0) return r;
     }
-    if (d->outq.empty()) return d->draining ? VP9HIP_EOF : VP9HIP_EAGAIN;
+    if (d->outq.empty())
+        return d->draining && d->inflight.empty() && d->batch.empty() ? VP9HIP_EOF : VP9HIP_EAGAIN;
     if (!d->outq.front().submitted) return VP9HIP_EAGAIN;
     const Out o = d->outq.front();
     d->outq.pop_front();
@@ -238,6 +397,8 @@ extern "C" int vp9hip_decoder_release(vp9hip_decoder *d, int buf)
 extern "C" int vp9hip_decoder_flush(vp9hip_decoder *d)
 {
     if (!d) return VP9HIP_EINVAL;
+    drop_inflight(d);
+    d->chain.reset();
     for (auto &f : d->batch) {
         vp9h_frame_free(&f.pkt);
         d->busy[f.out]--;
@@ -248,10 +409,6 @@ extern "C" int vp9hip_decoder_flush(vp9hip_decoder *d)
     for (auto &o : d->outq) d->pins[o.buf]--;
     d->outq.clear();
     for (int s = 0; s < 8; s++) d->slot[s] = -1;
-    vp9h_stream_close(d->st);
-    d->st = nullptr;
     d->draining = false;
-    int r = vp9h_stream_open(&d->st);
-    if (r < 0) return r;
     return d->ctx ? vp9hip_flush(d->ctx) : 0;
 }

@@ -328,6 +328,10 @@ void vp9h_enc_defaults(vp9h_enc_params *p);
 int  vp9h_stream_encode(vp9h_stream *s, const vp9h_frame *pkt, const vp9h_enc_params *p,
                         uint8_t **out, size_t *size, vp9h_frame *coded);
 
+/* The frame type from the first header bits: 0 keyframe (its parse needs no earlier
+ * frame), 1 other frame, 2 show_existing_frame, or AVERROR_INVALIDDATA. */
+int  vp9h_frame_type(const uint8_t *data, size_t size);
+
 /* Split a superframe into its frames (vp9_superframe_split_bsf,
  * bsf/vp9_superframe_split.c:40-95): up to cap (offset, size) pairs; returns the frame
  * count (1 for a plain frame) or a negative error. */
@@ -359,6 +363,7 @@ void vp9h_ivf_write_frame_header(uint8_t out[12], uint32_t frame_size, int64_t p
  * and the device path (vp9hip_ctx): superframes split, show_existing_frame, hidden frames,
  * reference slots by refresh mask. Frames are reconstructed in batches of up to
  * max_batch frames (decoder delay, like frame threading); send_packet(NULL) drains.
+ * The host parse runs on parse_threads threads ahead of the caller.
  * Errors: VP9HIP_EAGAIN from send_packet = read frames first (no free buffer);
  * from receive_frame = send more input; VP9HIP_EOF after a drain. */
 typedef struct vp9hip_decoder vp9hip_decoder;
@@ -368,6 +373,9 @@ typedef struct vp9hip_decoder_params {
     int32_t extra_bufs;            /* output frames the caller may hold at once, default 4     */
     int32_t max_width, max_height; /* buffer size; 0: the first keyframe's (larger inter      */
                                    /* frames, e.g. reference scaling up, need it set)         */
+    int32_t parse_threads;         /* host parse threads (0: parse in the caller's thread);    */
+                                   /* a keyframe starts a new parse chain, so keyframe-only   */
+                                   /* streams parse frame-parallel, GOPs GOP-parallel         */
 } vp9hip_decoder_params;
 typedef struct vp9hip_decoded_frame {
     int32_t buf;                   /* device buffer of vp9hip_decoder_context()              */

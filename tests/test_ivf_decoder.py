@@ -119,13 +119,31 @@ def _same(a, b, what):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("max_batch", [1, 3, 16])
-def test_decoder_ivf_stream_matches_oracle(v9, orc, max_batch):
+@pytest.mark.parametrize("max_batch,threads", [(1, 0), (3, 4), (16, 16), (4, 1)])
+def test_decoder_ivf_stream_matches_oracle(v9, orc, max_batch, threads):
     pkts = _stream(v9)
     _, frames = v9.ivf_read(v9.ivf_write(pkts, 200, 130))
     ref = _oracle_outputs(v9, orc, [d for _, d in frames])
-    got = _decode_all(v9, [d for _, d in frames], max_batch=max_batch)
-    _same(got, ref, "batch %d" % max_batch)
+    got = _decode_all(v9, [d for _, d in frames], max_batch=max_batch, parse_threads=threads)
+    _same(got, ref, "batch %d threads %d" % (max_batch, threads))
+
+
+@pytest.mark.gpu
+def test_decoder_parallel_gops_and_keyframes(v9, orc):
+    """Keyframes start new parse chains (vp9h_frame_type == 0): three GOPs and a run of
+    keyframes parse concurrently on the pool, outputs stay in order and bit-exact."""
+    pkts = []
+    for g in range(3):
+        fr = _frames(v9, 136, 72, 4, seed=800 + 10 * g, compound=1)
+        enc = v9.Stream()
+        pkts += [enc.encode(f, **({} if i == 0 else dict(ref_slot=(0, 0, 0), refresh_mask=2 if i % 2 else 4)))[0]
+                 for i, f in enumerate(fr)]
+    for k in range(6):
+        pkts.append(v9.encode_frame(v9.SynthFrame(v9.synth_params(136, 72, 8, seed=900 + k)), 60))
+    assert [v9.vp9h_type(d) for d in pkts] == ([0, 1, 1, 1] * 3 + [0] * 6)
+    ref = _oracle_outputs(v9, orc, pkts)
+    for threads, batch in ((8, 5), (2, 16)):
+        _same(_decode_all(v9, pkts, max_batch=batch, parse_threads=threads), ref, "threads %d" % threads)
 
 
 @pytest.mark.gpu
@@ -139,13 +157,13 @@ def test_decoder_formats(v9, orc, bpp, ssh, ssv):
 def test_decoder_eagain_flush_and_restart(v9, orc):
     """send_packet's EAGAIN when no buffer is free (frames held by the caller), receive's
     EAGAIN inside the decoder delay, flush (seek) then a new keyframe."""
-    fr = _frames(v9, 136, 72, 17)
+    fr = _frames(v9, 136, 72, 30)
     enc = v9.Stream()
     long_gop = [enc.encode(fr[0])[0]] + [enc.encode(f, ref_slot=(1 if i else 0, 0, 0), refresh_mask=2)[0]
                                          for i, f in enumerate(fr[1:])]
     pkts = _stream(v9)
     ref = _oracle_outputs(v9, orc, pkts)
-    dec = v9.Decoder(0, max_batch=4, extra_bufs=1)      # 8 slots + 4 + 1 = 13 buffers
+    dec = v9.Decoder(0, max_batch=4, extra_bufs=1, parse_threads=1)   # 13 buffers, <= 5 frames in parse
     held = []
     sent = 0
     with pytest.raises(v9.Vp9HipError) as e:
@@ -169,17 +187,14 @@ def test_decoder_eagain_flush_and_restart(v9, orc):
 
 @pytest.mark.gpu
 def test_decoder_rejects_inter_without_keyframe(v9):
+    """The parse runs ahead on the pool, so the error surfaces on the call that consumes
+    the frame (send_packet or receive_frame), as with libavcodec's frame threads."""
     pkts = _stream(v9)
-    dec = v9.Decoder(0)
-    with pytest.raises(v9.Vp9HipError) as e:
-        dec.send_packet(pkts[1])
-    assert e.value.code == v9.EINVALIDDATA
-    dec.close()
-
-
-def test_show_existing_frame_profile_3(v9, orc):
-    """In profile 3 the header has a reserved bit after the profile (vp9.c:527-531), so a
-    show_existing_frame header needs 9 bits: 2 bytes. The CPU decode loop outputs it."""
-    pkts = _stream(v9, 136, 72, 10, 0, 0)
-    assert len(pkts[4]) == 2 and pkts[4][0] >> 4 & 3 == 3
-    assert len(_oracle_outputs(v9, orc, pkts)) == 6
+    for threads in (0, 4):
+        dec = v9.Decoder(0, parse_threads=threads)
+        with pytest.raises(v9.Vp9HipError) as e:
+            dec.send_packet(pkts[1])
+            dec.send_packet(None)
+            dec.receive_frame()
+        assert e.value.code == v9.EINVALIDDATA
+        dec.close()
