@@ -190,7 +190,13 @@ def main():
         "kernel_ms": {k: round(ksum[k][0] / args.steps, 3) for k in ksum},
     }
 
-    host = host_entropy_rate(v, frames, gop, args) if rank == 0 and world == 1 and not args.no_cpu_baseline else None
+    host = e2e = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sample = encode_sample(v, frames, gop, min(len(frames), max(gop, 16)))
+        host = host_entropy_rate(v, sample, gop, args)
+        dev.close()                                     # free the batch's HBM before the decoder runs
+        dev = None
+        e2e = e2e_rate(v, sample, args, local_rank)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -232,24 +238,23 @@ def main():
         "roofline": roofline,
         "cpu_baseline": cpu,
         "host_entropy": host,
+        "e2e_decoder": e2e,
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
-    dev.close()
+    if dev is not None:
+        dev.close()
     if dist is not None:
         dist.destroy_process_group()
 
 
-def host_entropy_rate(v, frames, gop, args):
-    """The host side of the hybrid split: the frames as a VP9 stream
-    (vp9h_stream_encode), parsed back into pass-1 packets by vp9h_stream_decode, timed on
-    this box's cores: 1 thread, then a pool decoding independent GOPs (keyframe to
-    keyframe) in parallel (ctypes drops the GIL). Not `value` (the GPU path is timed with
-    packets resident); the rate at which the host front end could feed it."""
+def encode_sample(v, frames, gop, n):
+    """The first n frames as VP9 streams (vp9h_stream_encode), one per GOP (keyframe to
+    keyframe; LAST = ALTREF = the previous frame, GOLDEN = the keyframe), GOPs encoded in
+    parallel (ctypes drops the GIL)."""
     import concurrent.futures
-    n = min(len(frames), max(gop, 16))
-    gops = []
-    for g0 in range(0, n, gop):
+
+    def enc_gop(g0):
         enc, datas = v.Stream(), []
         for i in range(g0, min(n, g0 + gop)):
             kw = {}
@@ -257,7 +262,19 @@ def host_entropy_rate(v, frames, gop, args):
                 prev = (i - 1 - g0) % 8
                 kw = {"ref_slot": (prev, 0, prev), "refresh_mask": 1 << ((i - g0) % 8)}
             datas.append(enc.encode(frames[i], base_q_idx=frames[i].params.q_idx, **kw)[0])
-        gops.append(datas)
+        return datas
+
+    with concurrent.futures.ThreadPoolExecutor(min(16, os.cpu_count() or 1)) as ex:
+        return list(ex.map(enc_gop, range(0, n, gop)))
+
+
+def host_entropy_rate(v, gops, gop, args):
+    """The host side of the hybrid split: the sample stream parsed back
+    into pass-1 packets by vp9h_stream_decode, timed on this box's cores: 1 thread, then a
+    pool decoding independent GOPs (keyframe to keyframe) in parallel. Not `value` (the GPU
+    path is timed with packets resident); the rate at which the host front end could feed it."""
+    import concurrent.futures
+    n = sum(len(g) for g in gops)
 
     def decode_gop(datas):
         dec = v.Stream()
@@ -280,6 +297,36 @@ def host_entropy_rate(v, frames, gop, args):
             "bytes_per_frame": int(sum(len(d) for g in gops for d in g) / n),
             "sample": "%d synthetic %s frames as a VP9 stream (%s), parsed to pass-1 packets"
                       % (n, args.config, "keyframes" if gop == 1 else "GOPs of %d" % gop)}
+
+
+def e2e_rate(v, gops, args, device):
+    """Whole decoder, bitstream in -> frames in HBM out: vp9hip_decoder (host parse on a
+    thread pool, batched planning + H2D staging, GPU reconstruction), the sample stream sent
+    `reps` times, frames received as device buffers and released. Not `value`: this one
+    includes the host parse and the PCIe copy of every frame's packet."""
+    pkts = [d for g in gops for d in g]
+    threads = min(16, os.cpu_count() or 1)
+    dec = v.Decoder(device, max_batch=16, parse_threads=threads)
+
+    def run(reps):
+        n = 0
+        for _, info in dec.decode(pkts * reps, download=False):
+            dec.release(info.buf)
+            n += 1
+        dec.flush()
+        return n
+
+    t0 = time.perf_counter()
+    run(1)                                              # configure + warm-up
+    dt = time.perf_counter() - t0
+    reps = max(1, int(args.cpu_seconds / 2 / max(dt, 1e-3)))
+    t0 = time.perf_counter()
+    n = run(reps)
+    dt = time.perf_counter() - t0
+    dec.close()
+    return {"fps": round(n / dt, 2), "frames": n, "parse_threads": threads, "max_batch": 16,
+            "sample": "the %d-frame %s sample stream sent %d times through vp9hip_decoder "
+                      "(send_packet / receive_frame, device frames)" % (len(pkts), args.config, reps)}
 
 
 def bench_tiles(args, v, dist, world, rank, local_rank):

@@ -886,47 +886,57 @@ static int merge_mixed(Staged &s, uint32_t sbi)
     wg.sb[0] = sbi;
     const Staged::SBHost &h = s.sbh[sbi];
     const int N = (int) h.njobs;
+    const PJob *jobs = s.sbjobs.data() + h.job0;
     // the SB's jobs are consecutive, so their producer lists are too: job k's list is
     // jdep0[job0 + k + sbi] .. (one end marker per earlier SB shifts the index by sbi)
     const uint32_t *d0 = s.jdep0.data() + h.job0 + sbi;
-    std::vector<std::vector<uint16_t>> succ(N);
-    std::vector<int> indeg(N), height(N, 1);
-    for (int k = 0; k < N; k++) {
-        indeg[k] = (int) (d0[k + 1] - d0[k]);
-        for (uint32_t e = d0[k]; e < d0[k + 1]; e++) succ[s.jdeps[e]].push_back((uint16_t) k);
+    // scratch reused across SBs of this thread (no allocations per SB or pass):
+    // successor lists in CSR form, in-degrees, heights (longest path to a sink)
+    thread_local std::vector<int> indeg, height, soff, ready, next, take;
+    thread_local std::vector<uint16_t> succ;
+    indeg.assign(N, 0); height.assign(N, 1); soff.assign(N + 1, 0);
+    const uint32_t e0 = d0[0], e1 = d0[N];
+    for (uint32_t e = e0; e < e1; e++) soff[s.jdeps[e] + 1]++;
+    for (int k = 0; k < N; k++) soff[k + 1] += soff[k];
+    succ.resize(e1 - e0);
+    {
+        thread_local std::vector<int> fill;
+        fill.assign(soff.begin(), soff.end() - 1);
+        for (int k = 0; k < N; k++) {
+            indeg[k] = (int) (d0[k + 1] - d0[k]);
+            for (uint32_t e = d0[k]; e < d0[k + 1]; e++) succ[fill[s.jdeps[e]]++] = (uint16_t) k;
+        }
     }
     for (int k = N - 1; k >= 0; k--)                      // producers precede consumers
-        for (uint16_t c : succ[k]) height[k] = std::max(height[k], height[c] + 1);
-    std::vector<int> ready, next;
+        for (int e = soff[k]; e < soff[k + 1]; e++) height[k] = std::max(height[k], height[succ[e]] + 1);
+    ready.clear();
     for (int k = 0; k < N; k++) if (!indeg[k]) ready.push_back(k);
     int done = 0;
     while (done < N) {
         if (ready.empty()) return VP9HIP_EBUG;
+        // highest remaining critical path first, then decode order
         std::sort(ready.begin(), ready.end(), [&](int a, int b) {
             if (height[a] != height[b]) return height[a] > height[b];
             return a < b;
         });
         int lanes = 0, cnt[4] = { 0, 0, 0, 0 };
-        std::vector<int> take;
+        take.clear();
         next.clear();
         for (int k : ready) {
-            const int n = 4 << PJ_TS(s.sbjobs[h.job0 + k]);
+            const int n = 4 << PJ_TS(jobs[k]);
             if (lanes + n <= 64) { take.push_back(k); lanes += n; }
             else next.push_back(k);
         }
-        std::stable_sort(take.begin(), take.end(), [&](int a, int b) {
-            return PJ_TS(s.sbjobs[h.job0 + a]) > PJ_TS(s.sbjobs[h.job0 + b]);
-        });
+        // lane groups by size, largest first (stable: decode order within a size)
         const uint32_t first = (uint32_t) (s.pjobs.size() - wg.job0);
-        for (int k : take) {
-            s.pjobs.push_back(s.sbjobs[h.job0 + k]);
-            cnt[PJ_TS(s.sbjobs[h.job0 + k])]++;
-        }
+        for (int ts = 3; ts >= 0; ts--)
+            for (int k : take)
+                if ((int) PJ_TS(jobs[k]) == ts) { s.pjobs.push_back(jobs[k]); cnt[ts]++; }
         s.passes.push_back(first << 14 | (uint32_t) cnt[0] << 9 | (uint32_t) cnt[1] << 5 | (uint32_t) cnt[2] << 2 |
                            (uint32_t) cnt[3]);
         for (int k : take)
-            for (uint16_t c : succ[k])
-                if (--indeg[c] == 0) next.push_back(c);
+            for (int e = soff[k]; e < soff[k + 1]; e++)
+                if (--indeg[succ[e]] == 0) next.push_back(succ[e]);
         done += (int) take.size();
         ready.swap(next);
     }
