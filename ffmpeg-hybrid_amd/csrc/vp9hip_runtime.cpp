@@ -19,6 +19,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <functional>
 #include <thread>
 #include <array>
@@ -96,6 +97,10 @@ struct Staged {
     int tile_lo = 0, tile_hi = 64;      // tile columns this context reconstructs (sharded batches)
     std::vector<uint8_t> coefs;         // concatenated coefficient streams (bytes)
     double alg_bytes[K_N] = { 0, 0, 0, 0, 0 };
+    // record counts of the arena (the host images above are not kept for these)
+    uint32_t n_sbs = 0, n_pjobs = 0, n_passes = 0, n_wgs = 0, n_rjobs = 0, n_lfs = 0, n_mcs = 0;
+    uint8_t *pinned = nullptr;          // pinned host image of the arena (one DMA per stage)
+    size_t pinned_cap = 0;
     // device arena
     uint8_t *arena = nullptr;
     size_t arena_cap = 0;
@@ -185,6 +190,7 @@ extern "C" void vp9hip_close(vp9hip_ctx *c)
     free_bufs(c);
     if (c->stg.arena) hipFree(c->stg.arena);
     if (c->stg.resid) hipFree(c->stg.resid);
+    if (c->stg.pinned) hipHostFree(c->stg.pinned);
     if (c->stg.graph) hipGraphExecDestroy(c->stg.graph);
     if (c->ptab) hipFree(c->ptab);
     for (auto e : c->ev) hipEventDestroy(e);
@@ -1000,6 +1006,12 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     // fused intra + LF launches need the LF of a phase in the same launch sequence as its
     // reconstruction (not for tile-sharded batches: recon, exchange, then LF)
     const bool fuse = c->fuse_plf && !tiled;
+    // VP9HIP_STAGE_TRACE=1: host time of the staging steps on stderr
+    static const bool stage_trace = getenv("VP9HIP_STAGE_TRACE") && atoi(getenv("VP9HIP_STAGE_TRACE"));
+    double st_ms[6] = { 0, 0, 0, 0, 0, 0 };
+    auto st_t0 = std::chrono::steady_clock::now();
+#define STAGE_T(k) do { auto t_ = std::chrono::steady_clock::now(); \
+        st_ms[k] = std::chrono::duration<double, std::milli>(t_ - st_t0).count(); st_t0 = t_; } while (0)
     if (!c || !pkts || n <= 0 || !out_bufs) return VP9HIP_EINVAL;
     if (c->bufs.empty()) return VP9HIP_EINVAL;
     hipSetDevice(c->dev);
@@ -1055,7 +1067,6 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     for (int i = 0; i < n; i++) maxpos = std::max(maxpos, pos[i]);
     const int NP = G * (maxpos + 1);                   // phase id = g * (maxpos + 1) + pos
     s.nphases = NP;
-    s.rbucket.assign(NP, {});
     // per frame: validate, frame descriptor, reference scaling (sequential, cheap)
     std::vector<FrameBuild> fbs(n);
     std::vector<size_t> coef_off(n + 1, 0);
@@ -1135,16 +1146,15 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
         if (f->filter_level) s.alg_bytes[K_LF] += 2.0 * pix_bytes;
     }
 
+    STAGE_T(0);
     // work planning of every frame (independent), on host threads: jobs, dependency
     // levels and pass packing, LF programs, MC units, coefficient copy
     std::vector<FramePlan> plans(n);
-    s.coefs.resize(coef_off[n]);
     {
         std::atomic<int> next(0);
         auto worker = [&]() {
             for (int i; (i = next.fetch_add(1)) < n;) {
                 plans[i].err = plan_frame(fbs[i], plans[i]);
-                if (coef_off[i + 1] > coef_off[i]) memcpy(s.coefs.data() + coef_off[i], pkts[i].coefs, coef_off[i + 1] - coef_off[i]);
             }
         };
         const int nt = std::min(n, host_threads());
@@ -1153,66 +1163,74 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
         worker();
         for (auto &t : pool) t.join();
     }
-    // merge in frame order: local indices -> batch indices
+    STAGE_T(1);
+    // merge: batch offsets of every frame's records (prefix sums in frame order; residual
+    // jobs in launch order: group, phase, tx code, txtp, frame). The records themselves
+    // are written, with their index fixups, straight into the pinned arena image below.
+    for (int i = 0; i < n; i++)
+        if (plans[i].err < 0) return plans[i].err;
+    struct Off { uint32_t sb, job, pass, wg, lf, mc; uint64_t res; uint32_t rj[5][4]; };
+    std::vector<Off> off(n);
+    Off tot = {};
+    for (int i = 0; i < n; i++) {
+        const Staged &l = plans[i].s;
+        off[i] = tot;
+        tot.sb += (uint32_t) l.sbs.size(); tot.job += (uint32_t) l.pjobs.size(); tot.pass += (uint32_t) l.passes.size();
+        tot.wg += (uint32_t) l.wgs.size(); tot.lf += (uint32_t) l.lfs.size(); tot.mc += (uint32_t) l.mcs.size();
+        tot.res += l.resid16;
+    }
+    if (tot.res > 0xffffffffull) return VP9HIP_ENOMEM;
+    s.resid16 = tot.res;
+    std::vector<std::vector<int>> phase_frames(NP);
+    for (int i = 0; i < n; i++) phase_frames[fbs[i].phase].push_back(i);
+    std::vector<std::array<std::pair<uint32_t, uint32_t>, 5>> rj_range(NP);   // per phase, tx code: (off, n)
+    uint32_t tot_rj = 0;
+    for (int ph = 0; ph < NP; ph++)                    // phase ids are group-major, chain order
+        for (int t = 0; t < 5; t++) {
+            rj_range[ph][t].first = tot_rj;
+            for (int tp = 0; tp < 4; tp++)
+                for (int i : phase_frames[ph]) {
+                    off[i].rj[t][tp] = tot_rj;
+                    tot_rj += (uint32_t) plans[i].s.rbucket[0][t][tp].size();
+                }
+            rj_range[ph][t].second = tot_rj - rj_range[ph][t].first;
+        }
+    // per workgroup / LF record: the algorithmic pixel bytes its SB moves (fused launches)
+    std::vector<double> wg_bytes(tot.wg, 0.0), lf_bytes(tot.lf, 0.0);
+    for (int i = 0; i < n; i++) {
+        const Staged &l = plans[i].s;
+        const bool intra = pkts[i].keyframe || pkts[i].intraonly;
+        for (size_t k = 0; k < l.wgs.size() && intra; k++) {
+            const SBRec &sb = l.sbs[l.wgs[k].sb[0]];
+            wg_bytes[off[i].wg + k] = sb_bytes(c, pkts[i], sb.sbx, sb.sby);
+        }
+        for (size_t k = 0; k < l.lfs.size(); k++)
+            lf_bytes[off[i].lf + k] = 2.0 * sb_bytes(c, pkts[i], l.lfs[k].sbx, l.lfs[k].sby);
+    }
     std::vector<std::vector<std::vector<uint32_t>>> wsteps(NP), lsteps(NP);   // per phase: WG / LF lists
     std::vector<std::vector<std::pair<uint32_t, uint32_t>>> mcr(NP);           // MC unit ranges per phase
     for (int i = 0; i < n; i++) {
         FramePlan &fp = plans[i];
-        if (fp.err < 0) return fp.err;
         const int ph = fbs[i].phase;
-        Staged &l = fp.s;
-        const uint32_t sb_off = (uint32_t) s.sbs.size(), job_off = (uint32_t) s.pjobs.size();
-        const uint32_t pass_off = (uint32_t) s.passes.size(), wg_off = (uint32_t) s.wgs.size();
-        const uint32_t lf_off = (uint32_t) s.lfs.size(), mc_off = (uint32_t) s.mcs.size();
-        const uint64_t res_off = s.resid16;
-        if (res_off + l.resid16 > 0xffffffffull) return VP9HIP_ENOMEM;
-        s.sbs.insert(s.sbs.end(), l.sbs.begin(), l.sbs.end());
-        for (PJob j : l.pjobs) {
-            if (PJ_RES(j)) j.roff += (uint32_t) res_off;
-            s.pjobs.push_back(j);
-        }
-        s.passes.insert(s.passes.end(), l.passes.begin(), l.passes.end());
-        for (WGRec w : l.wgs) {
-            w.job0 += job_off; w.pass0 += pass_off; w.sb[0] += sb_off;
-            s.wgs.push_back(w);
-        }
-        for (int t = 0; t < 5; t++)
-            for (int tp = 0; tp < 4; tp++)
-                for (RJob r : l.rbucket[0][t][tp]) {
-                    if (!(r.ptx & 32)) r.dst += (uint32_t) res_off;      // intra: residual scratch offset
-                    s.rbucket[ph][t][tp].push_back(r);
-                }
-        s.resid16 += l.resid16;
-        s.lfs.insert(s.lfs.end(), l.lfs.begin(), l.lfs.end());
-        if (!l.mcs.empty()) {
-            s.mcs.insert(s.mcs.end(), l.mcs.begin(), l.mcs.end());
-            mcr[ph].push_back({ mc_off, (uint32_t) l.mcs.size() });
-        }
-        for (const McUnit &m : l.mcs) s.alg_bytes[K_MC] += (double) m.w * m.h * c->bypp * (1 + m.nref);
+        if (!fp.s.mcs.empty()) mcr[ph].push_back({ off[i].mc, (uint32_t) fp.s.mcs.size() });
+        for (const McUnit &m : fp.s.mcs) s.alg_bytes[K_MC] += (double) m.w * m.h * c->bypp * (1 + m.nref);
         if (wsteps[ph].size() < fp.wsteps.size()) wsteps[ph].resize(fp.wsteps.size());
         for (size_t d = 0; d < fp.wsteps.size(); d++)
-            for (uint32_t w : fp.wsteps[d]) wsteps[ph][d].push_back(w + wg_off);
+            for (uint32_t w : fp.wsteps[d]) wsteps[ph][d].push_back(w + off[i].wg);
         if (lsteps[ph].size() < fp.lsteps.size()) lsteps[ph].resize(fp.lsteps.size());
         for (size_t d = 0; d < fp.lsteps.size(); d++)
-            for (uint32_t li : fp.lsteps[d]) lsteps[ph][d].push_back(li + lf_off);
-        fp = FramePlan();                        // release the frame's host images early
+            for (uint32_t li : fp.lsteps[d]) lsteps[ph][d].push_back(li + off[i].lf);
     }
+    STAGE_T(2);
     // launch schedule per group, phases in chain order: MC, residuals by (tx code, txtp),
     // the intra SB wavefront, the LF wavefront; inter residual pixels are algorithmic
     // reads + writes of k_resid
     for (int g = 0; g < G; g++)
         for (int ph = g * (maxpos + 1); ph < (g + 1) * (maxpos + 1); ph++) {
             for (auto &mr : mcr[ph]) s.launches.push_back({ K_MC, mr.first, mr.second, 0, g, ph, PART_RECON, 0 });
-            for (int t = 0; t < 5; t++) {
-                const uint32_t off = (uint32_t) s.rjobs.size();
-                for (int tp = 0; tp < 4; tp++) {
-                    for (auto &r : s.rbucket[ph][t][tp])
-                        if (r.ptx & 32) s.alg_bytes[K_RESID] += 2.0 * (16 << (2 * (t & 3))) * c->bypp;
-                    s.rjobs.insert(s.rjobs.end(), s.rbucket[ph][t][tp].begin(), s.rbucket[ph][t][tp].end());
-                }
-                if (s.rjobs.size() > off)
-                    s.launches.push_back({ K_RESID, off, (uint32_t) (s.rjobs.size() - off), t, g, ph, PART_RECON, 0 });
-            }
+            for (int t = 0; t < 5; t++)                 // residual jobs placed by the merge
+                if (rj_range[ph][t].second)
+                    s.launches.push_back({ K_RESID, rj_range[ph][t].first, rj_range[ph][t].second, t, g, ph, PART_RECON, 0 });
             auto add_list = [&](int kind, const std::vector<uint32_t> &v, int step) {
                 if (v.empty()) return;
                 s.launches.push_back({ kind, (uint32_t) s.lists.size(), (uint32_t) v.size(), 0, g, ph,
@@ -1247,43 +1265,44 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
                     s.lists.insert(s.lists.end(), lv->begin(), lv->end());
                     s.launches.push_back(L);
                     // algorithmic bytes of the fused launch move from K_PRED / K_LF to K_PLF
-                    for (uint32_t w : *pv) {
-                        const SBRec &sb = s.sbs[s.wgs[w].sb[0]];
-                        const vp9h_frame &f = pkts[sb.frame];
-                        if (!(f.keyframe || f.intraonly)) continue;
-                        const double b = sb_bytes(c, f, sb.sbx, sb.sby);
-                        s.alg_bytes[K_PRED] -= b; s.alg_bytes[K_PLF] += b;
-                    }
-                    for (uint32_t li : *lv) {
-                        const LFRec &lr = s.lfs[li];
-                        const double b = 2.0 * sb_bytes(c, pkts[lr.frame], lr.sbx, lr.sby);
-                        s.alg_bytes[K_LF] -= b; s.alg_bytes[K_PLF] += b;
-                    }
+                    for (uint32_t w : *pv) { s.alg_bytes[K_PRED] -= wg_bytes[w]; s.alg_bytes[K_PLF] += wg_bytes[w]; }
+                    for (uint32_t li : *lv) { s.alg_bytes[K_LF] -= lf_bytes[li]; s.alg_bytes[K_PLF] += lf_bytes[li]; }
                 } else if (pv) add_list(K_PRED, *pv, t);
                 else if (lv) add_list(K_LF, *lv, j);
             }
         }
     if (s.resid16 > 0xffffffffull) return VP9HIP_ENOMEM;
 
-    // upload into one arena
+    STAGE_T(3);
+    // upload: one arena; its host image is built in pinned memory (every frame writes its
+    // records there with the batch index fixups, in parallel) and copied with one DMA
     auto al = [](size_t x) { return (x + 255) & ~(size_t) 255; };
     size_t o = 0;
     s.o_frames = o; o = al(o + s.frames.size() * sizeof(FrameDesc));
-    s.o_sbs = o; o = al(o + s.sbs.size() * sizeof(SBRec));
-    s.o_pjobs = o; o = al(o + s.pjobs.size() * sizeof(PJob));
-    s.o_passes = o; o = al(o + s.passes.size() * sizeof(uint32_t));
-    s.o_wgs = o; o = al(o + s.wgs.size() * sizeof(WGRec));
-    s.o_rjobs = o; o = al(o + s.rjobs.size() * sizeof(RJob));
-    s.o_lfs = o; o = al(o + s.lfs.size() * sizeof(LFRec));
-    s.o_mcs = o; o = al(o + s.mcs.size() * sizeof(McUnit));
+    s.o_sbs = o; o = al(o + (size_t) tot.sb * sizeof(SBRec));
+    s.o_pjobs = o; o = al(o + (size_t) tot.job * sizeof(PJob));
+    s.o_passes = o; o = al(o + (size_t) tot.pass * sizeof(uint32_t));
+    s.o_wgs = o; o = al(o + (size_t) tot.wg * sizeof(WGRec));
+    s.o_rjobs = o; o = al(o + (size_t) tot_rj * sizeof(RJob));
+    s.o_lfs = o; o = al(o + (size_t) tot.lf * sizeof(LFRec));
+    s.o_mcs = o; o = al(o + (size_t) tot.mc * sizeof(McUnit));
     s.o_lists = o; o = al(o + s.lists.size() * sizeof(uint32_t));
-    s.o_coefs = o; o = al(o + s.coefs.size() + 64);
+    s.o_coefs = o; o = al(o + coef_off[n] + 64);
+    s.n_sbs = tot.sb; s.n_pjobs = tot.job; s.n_passes = tot.pass; s.n_wgs = tot.wg; s.n_rjobs = tot_rj;
+    s.n_lfs = tot.lf; s.n_mcs = tot.mc;
     if (o > s.arena_cap) {
         if (s.arena) hipFree(s.arena);
         s.arena = nullptr;
         s.arena_cap = 0;
         if (hipMalloc(&s.arena, o) != hipSuccess) return VP9HIP_ENOMEM;
         s.arena_cap = o;
+    }
+    if (o > s.pinned_cap) {
+        if (s.pinned) hipHostFree(s.pinned);
+        s.pinned = nullptr;
+        s.pinned_cap = 0;
+        if (hipHostMalloc((void **) &s.pinned, o, hipHostMallocDefault) != hipSuccess) return VP9HIP_ENOMEM;
+        s.pinned_cap = o;
     }
     const size_t rbytes = (size_t) s.resid16 * 32 + 256;
     if (rbytes > s.resid_cap) {
@@ -1293,22 +1312,66 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
         if (hipMalloc(&s.resid, rbytes) != hipSuccess) return VP9HIP_ENOMEM;
         s.resid_cap = rbytes;
     }
-    auto up = [&](size_t off, const void *src, size_t bytes) -> int {
-        if (!bytes) return 0;
-        return hipMemcpyAsync(s.arena + off, src, bytes, hipMemcpyHostToDevice, c->st) == hipSuccess ? 0 : -1;
-    };
-    if (up(s.o_frames, s.frames.data(), s.frames.size() * sizeof(FrameDesc)) ||
-        up(s.o_sbs, s.sbs.data(), s.sbs.size() * sizeof(SBRec)) ||
-        up(s.o_pjobs, s.pjobs.data(), s.pjobs.size() * sizeof(PJob)) ||
-        up(s.o_passes, s.passes.data(), s.passes.size() * sizeof(uint32_t)) ||
-        up(s.o_wgs, s.wgs.data(), s.wgs.size() * sizeof(WGRec)) ||
-        up(s.o_rjobs, s.rjobs.data(), s.rjobs.size() * sizeof(RJob)) ||
-        up(s.o_lfs, s.lfs.data(), s.lfs.size() * sizeof(LFRec)) ||
-        up(s.o_mcs, s.mcs.data(), s.mcs.size() * sizeof(McUnit)) ||
-        up(s.o_lists, s.lists.data(), s.lists.size() * sizeof(uint32_t)) ||
-        up(s.o_coefs, s.coefs.data(), s.coefs.size()))
-        return VP9HIP_EEXTERNAL;
+    uint8_t *img = s.pinned;
+    memcpy(img + s.o_frames, s.frames.data(), s.frames.size() * sizeof(FrameDesc));
+    if (!s.lists.empty()) memcpy(img + s.o_lists, s.lists.data(), s.lists.size() * sizeof(uint32_t));
+    std::vector<double> inplace_bytes(n, 0.0);
+    {
+        std::atomic<int> next(0);
+        auto worker = [&]() {
+            for (int i; (i = next.fetch_add(1)) < n;) {
+                const Staged &l = plans[i].s;
+                const Off &q = off[i];
+                const uint32_t res = (uint32_t) q.res;
+                if (!l.sbs.empty()) memcpy((SBRec *) (img + s.o_sbs) + q.sb, l.sbs.data(), l.sbs.size() * sizeof(SBRec));
+                PJob *pj = (PJob *) (img + s.o_pjobs) + q.job;
+                for (size_t k = 0; k < l.pjobs.size(); k++) {
+                    PJob j = l.pjobs[k];
+                    if (PJ_RES(j)) j.roff += res;
+                    pj[k] = j;
+                }
+                if (!l.passes.empty())
+                    memcpy((uint32_t *) (img + s.o_passes) + q.pass, l.passes.data(), l.passes.size() * sizeof(uint32_t));
+                WGRec *wg = (WGRec *) (img + s.o_wgs) + q.wg;
+                for (size_t k = 0; k < l.wgs.size(); k++) {
+                    WGRec w = l.wgs[k];
+                    w.job0 += q.job; w.pass0 += q.pass; w.sb[0] += q.sb;
+                    wg[k] = w;
+                }
+                if (!l.lfs.empty()) memcpy((LFRec *) (img + s.o_lfs) + q.lf, l.lfs.data(), l.lfs.size() * sizeof(LFRec));
+                if (!l.mcs.empty()) memcpy((McUnit *) (img + s.o_mcs) + q.mc, l.mcs.data(), l.mcs.size() * sizeof(McUnit));
+                double ib = 0;
+                for (int t = 0; t < 5; t++)
+                    for (int tp = 0; tp < 4; tp++) {
+                        const std::vector<RJob> &bk = l.rbucket[0][t][tp];
+                        RJob *dst = (RJob *) (img + s.o_rjobs) + q.rj[t][tp];
+                        for (size_t k = 0; k < bk.size(); k++) {
+                            RJob r = bk[k];
+                            if (!(r.ptx & 32)) r.dst += res;          // intra: residual scratch offset
+                            else ib += 2.0 * (16 << (2 * (t & 3))) * c->bypp;   // inter: pixels read + written
+                            dst[k] = r;
+                        }
+                    }
+                inplace_bytes[i] = ib;
+                if (coef_off[i + 1] > coef_off[i])
+                    memcpy(img + s.o_coefs + coef_off[i], pkts[i].coefs, coef_off[i + 1] - coef_off[i]);
+                plans[i] = FramePlan();                  // release the frame's host images
+            }
+        };
+        const int nt = std::min(n, host_threads());
+        std::vector<std::thread> pool;
+        for (int t = 1; t < nt; t++) pool.emplace_back(worker);
+        worker();
+        for (auto &t : pool) t.join();
+    }
+    for (int i = 0; i < n; i++) s.alg_bytes[K_RESID] += inplace_bytes[i];
+    HIPCHK(hipMemcpyAsync(s.arena, img, o, hipMemcpyHostToDevice, c->st));
+    STAGE_T(4);
     HIPCHK(hipStreamSynchronize(c->st));
+    STAGE_T(5);
+    if (stage_trace)
+        fprintf(stderr, "vp9hip stage: %d frames: setup %.1f plan %.1f merge %.1f schedule %.1f upload %.1f sync %.1f ms\n",
+                n, st_ms[0], st_ms[1], st_ms[2], st_ms[3], st_ms[4], st_ms[5]);
     s.ready = true;
     return 0;
 }
