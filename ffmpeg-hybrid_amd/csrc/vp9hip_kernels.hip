@@ -453,22 +453,21 @@ template <int N> DEV void store_col(int16_t *dst, const int (&r)[N])
         for (int k = 0; k < N / 8; k++) ((uint4 *) dst)[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
 }
 
+// One wave of residual work: jobs [wj * 64/N, (wj + 1) * 64/N) of `jobs`, n lanes per
+// job; cbw = the wave's LDS block (64 N coefficients).
 template <int N, int TCODE, typename PIX, class M, typename COEF>
-__global__ __launch_bounds__(64 * RWAVES) void k_resid(const RJob *__restrict__ jobs, int njobs,
-                                                       const FrameDesc *__restrict__ frames,
-                                                       const COEF *__restrict__ coefs, int16_t *__restrict__ resid)
+DEV void resid_wave(const RJob *__restrict__ jobs, int njobs, int wj, int lane, const FrameDesc *__restrict__ frames,
+                    const COEF *__restrict__ coefs, int16_t *__restrict__ resid, COEF *cbw)
 {
     typedef typename M::T T;
     constexpr int CAP = 64 / N;
     constexpr int LG = N == 4 ? 2 : N == 8 ? 3 : N == 16 ? 4 : 5;
     constexpr int TS = LG - 2;
     constexpr int BITS = N == 32 ? 6 : TS + 4;
-    __shared__ COEF cbs[RWAVES][CAP * N * N];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int grp = lane >> LG, li = lane & (N - 1);
-    const int j = (blockIdx.x * RWAVES + wave) * CAP + grp;
+    const int j = wj * CAP + grp;
     const bool act = j < njobs;
-    COEF *cb = cbs[wave] + grp * N * N;
+    COEF *cb = cbw + grp * N * N;
 
     RJob r;
     if (act) r = jobs[j];
@@ -559,6 +558,17 @@ __global__ __launch_bounds__(64 * RWAVES) void k_resid(const RJob *__restrict__ 
         for (int k = 0; k < N; k++) res[k] = res[k] < -32768 ? -32768 : res[k] > 32767 ? 32767 : res[k];
         store_col<N>(resid + (size_t) r.dst * 16 + li * N, res);
     }
+}
+
+template <int N, int TCODE, typename PIX, class M, typename COEF>
+__global__ __launch_bounds__(64 * RWAVES) void k_resid(const RJob *__restrict__ jobs, int njobs,
+                                                       const FrameDesc *__restrict__ frames,
+                                                       const COEF *__restrict__ coefs, int16_t *__restrict__ resid)
+{
+    __shared__ COEF cbs[RWAVES][64 * N];
+    const int wave = threadIdx.x >> 6;
+    resid_wave<N, TCODE, PIX, M, COEF>(jobs, njobs, blockIdx.x * RWAVES + wave, threadIdx.x & 63, frames, coefs, resid,
+                                       cbs[wave]);
 }
 
 // ------------------------------------------------------------- k_pred
@@ -1282,27 +1292,59 @@ __global__ __launch_bounds__(LfNT<G>::NT) void k_lf(const uint32_t *__restrict__
     lf_sb<PIX, G, LfNT<G>::NT>(recs[list[blockIdx.x]], frames, S, threadIdx.x, dbg);
 }
 
-// Fused launch of one intra diagonal and one LF diagonal (runtime schedule: LF diagonal
-// t - 3 with intra diagonal t touch disjoint pixels): workgroups [0, npred) predict one SB
-// each with wave 0 (wave 1 exits), the rest loop-filter one SB each.
+// Residual arithmetic types per pixel type: 8-bit int16 coefficients / 32-bit math,
+// high bit depth int32 coefficients / 64-bit math (vp9dsp_template.c dctcoef / dctint)
+template <typename PIX> struct RT;
+template <> struct RT<uint8_t> { typedef M32 M; typedef int16_t C; };
+template <> struct RT<uint16_t> { typedef M64 M; typedef int32_t C; };
+
+// Fused wavefront launch (runtime schedule, stage()): launch t holds intra diagonal t, LF
+// diagonal t - 3 (disjoint pixels) and the residuals of intra diagonal t + 1.
+// Workgroups [0, npred) predict one SB each with wave 0 (the other waves exit), the next
+// nlf loop-filter one SB each, the rest run residual jobs by transform code, NT/64 waves
+// of 64/n jobs each.
 template <typename PIX, class G>
-__global__ __launch_bounds__(LfNT<G>::NT) void k_plf(const uint32_t *__restrict__ plist, int npred,
+__global__ __launch_bounds__(LfNT<G>::NT) void k_plf(PlfLaunch a, const uint32_t *__restrict__ plist,
                                                      const uint32_t *__restrict__ llist, const WGRec *__restrict__ wgs,
                                                      const SBRec *__restrict__ sbs, const PJob *__restrict__ jobs,
                                                      const uint32_t *__restrict__ passes, const LFRec *__restrict__ recs,
-                                                     const FrameDesc *__restrict__ frames, const int16_t *__restrict__ resid,
+                                                     const RJob *__restrict__ rjobs, const FrameDesc *__restrict__ frames,
+                                                     const void *__restrict__ coefs, int16_t *__restrict__ resid,
                                                      const uint32_t *__restrict__ ptab, int dbg)
 {
-    __shared__ union PlfLds { PredLds<PIX, G> p; LfLds<PIX, G> l; } S;
-    if ((int) blockIdx.x < npred) {
+    typedef typename RT<PIX>::M M;
+    typedef typename RT<PIX>::C COEF;
+    constexpr int NW = LfNT<G>::NT / 64;
+    __shared__ union PlfLds { PredLds<PIX, G> p; LfLds<PIX, G> l; COEF r[NW][64 * 32]; } S;
+    const int b = blockIdx.x;
+    if (b < (int) a.npred) {
         if (threadIdx.x >= 64) return;
 #if PRED_LTAB_LDS
         load_ltab<PIX>(S.p.ltab, ptab, threadIdx.x);
 #endif
-        pred_wg<PIX, G>(wgs + plist[blockIdx.x], sbs, jobs, passes, frames, resid, ptab, S.p, threadIdx.x, dbg);
-    } else {
-        lf_sb<PIX, G, LfNT<G>::NT>(recs[llist[blockIdx.x - npred]], frames, S.l, threadIdx.x, dbg >> 16);
+        pred_wg<PIX, G>(wgs + plist[b], sbs, jobs, passes, frames, resid, ptab, S.p, threadIdx.x, dbg);
+        return;
     }
+    if (b < (int) (a.npred + a.nlf)) {
+        lf_sb<PIX, G, LfNT<G>::NT>(recs[llist[b - a.npred]], frames, S.l, threadIdx.x, dbg >> 16);
+        return;
+    }
+    // residual workgroups: transform code k owns ceil(rn[k] / (NW * 64 / n)) of them
+    int rb = b - (int) (a.npred + a.nlf);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const COEF *cf = (const COEF *) coefs;
+#define RES_CASE(K, N, TC)                                                                                  \
+    {                                                                                                       \
+        const int nwg = ((int) a.rn[K] + NW * (64 / N) - 1) / (NW * (64 / N));                             \
+        if (rb < nwg) {                                                                                     \
+            resid_wave<N, TC, PIX, M, COEF>(rjobs + a.roff[K], a.rn[K], rb * NW + wave, lane, frames, cf,    \
+                                            resid, S.r[wave]);                                              \
+            return;                                                                                         \
+        }                                                                                                   \
+        rb -= nwg;                                                                                          \
+    }
+    RES_CASE(0, 4, 0) RES_CASE(1, 8, 1) RES_CASE(2, 16, 2) RES_CASE(3, 32, 3) RES_CASE(4, 4, 4)
+#undef RES_CASE
 }
 
 // --------------------------------------------------------------- k_mc
@@ -1421,23 +1463,29 @@ static void launch_lf_p(int ss, hipStream_t st, int nsb, const uint32_t *list, c
     }
 }
 template <typename PIX, class G>
-static void launch_plf_g(hipStream_t st, int npred, const uint32_t *plist, int nlf, const uint32_t *llist, const WGRec *wgs,
-                         const SBRec *sbs, const PJob *jobs, const uint32_t *passes, const LFRec *recs,
-                         const FrameDesc *frames, const int16_t *resid, const uint32_t *ptab, int dbg)
+static void launch_plf_g(hipStream_t st, const PlfLaunch &pl, const uint32_t *plist, const uint32_t *llist, const WGRec *wgs,
+                         const SBRec *sbs, const PJob *jobs, const uint32_t *passes, const LFRec *recs, const RJob *rjobs,
+                         const FrameDesc *frames, const void *coefs, int16_t *resid, const uint32_t *ptab, int dbg)
 {
-    hipLaunchKernelGGL((k_plf<PIX, G>), dim3(npred + nlf), dim3(LfNT<G>::NT), 0, st, plist, npred, llist, wgs, sbs, jobs,
-                       passes, recs, frames, resid, ptab, dbg);
+    constexpr int NW = LfNT<G>::NT / 64;
+    static const int n_of[5] = { 4, 8, 16, 32, 4 };
+    int nblk = (int) (pl.npred + pl.nlf);
+    for (int k = 0; k < 5; k++) nblk += ((int) pl.rn[k] + NW * (64 / n_of[k]) - 1) / (NW * (64 / n_of[k]));
+    if (nblk <= 0) return;
+    hipLaunchKernelGGL((k_plf<PIX, G>), dim3(nblk), dim3(LfNT<G>::NT), 0, st, pl, plist, llist, wgs, sbs, jobs, passes,
+                       recs, rjobs, frames, coefs, resid, ptab, dbg);
 }
 template <typename PIX>
-static void launch_plf_p(int ss, hipStream_t st, int npred, const uint32_t *plist, int nlf, const uint32_t *llist,
+static void launch_plf_p(int ss, hipStream_t st, const PlfLaunch &pl, const uint32_t *plist, const uint32_t *llist,
                          const WGRec *wgs, const SBRec *sbs, const PJob *jobs, const uint32_t *passes, const LFRec *recs,
-                         const FrameDesc *frames, const int16_t *resid, const uint32_t *ptab, int dbg)
+                         const RJob *rjobs, const FrameDesc *frames, const void *coefs, int16_t *resid,
+                         const uint32_t *ptab, int dbg)
 {
     switch (ss) {
-    case 3: launch_plf_g<PIX, Geo<1, 1>>(st, npred, plist, nlf, llist, wgs, sbs, jobs, passes, recs, frames, resid, ptab, dbg); break;
-    case 1: launch_plf_g<PIX, Geo<1, 0>>(st, npred, plist, nlf, llist, wgs, sbs, jobs, passes, recs, frames, resid, ptab, dbg); break;
-    case 2: launch_plf_g<PIX, Geo<0, 1>>(st, npred, plist, nlf, llist, wgs, sbs, jobs, passes, recs, frames, resid, ptab, dbg); break;
-    default: launch_plf_g<PIX, Geo<0, 0>>(st, npred, plist, nlf, llist, wgs, sbs, jobs, passes, recs, frames, resid, ptab, dbg); break;
+    case 3: launch_plf_g<PIX, Geo<1, 1>>(st, pl, plist, llist, wgs, sbs, jobs, passes, recs, rjobs, frames, coefs, resid, ptab, dbg); break;
+    case 1: launch_plf_g<PIX, Geo<1, 0>>(st, pl, plist, llist, wgs, sbs, jobs, passes, recs, rjobs, frames, coefs, resid, ptab, dbg); break;
+    case 2: launch_plf_g<PIX, Geo<0, 1>>(st, pl, plist, llist, wgs, sbs, jobs, passes, recs, rjobs, frames, coefs, resid, ptab, dbg); break;
+    default: launch_plf_g<PIX, Geo<0, 0>>(st, pl, plist, llist, wgs, sbs, jobs, passes, recs, rjobs, frames, coefs, resid, ptab, dbg); break;
     }
 }
 extern "C" {
@@ -1474,13 +1522,13 @@ int vp9hip_launch_lf(int fmt, hipStream_t st, int nsb, const uint32_t *list, con
     else         launch_lf_p<uint8_t>(fmt >> 1, st, nsb, list, recs, frames, dbg);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
-int vp9hip_launch_plf(int fmt, hipStream_t st, int npred, const uint32_t *plist, int nlf, const uint32_t *llist,
+int vp9hip_launch_plf(int fmt, hipStream_t st, const PlfLaunch *pl, const uint32_t *plist, const uint32_t *llist,
                       const WGRec *wgs, const SBRec *sbs, const PJob *jobs, const uint32_t *passes, const LFRec *recs,
-                      const FrameDesc *frames, const int16_t *resid, const uint32_t *ptab, int dbg)
+                      const RJob *rjobs, const FrameDesc *frames, const void *coefs, int16_t *resid, const uint32_t *ptab,
+                      int dbg)
 {
-    if (npred + nlf <= 0) return 0;
-    if (fmt & 1) launch_plf_p<uint16_t>(fmt >> 1, st, npred, plist, nlf, llist, wgs, sbs, jobs, passes, recs, frames, resid, ptab, dbg);
-    else         launch_plf_p<uint8_t>(fmt >> 1, st, npred, plist, nlf, llist, wgs, sbs, jobs, passes, recs, frames, resid, ptab, dbg);
+    if (fmt & 1) launch_plf_p<uint16_t>(fmt >> 1, st, *pl, plist, llist, wgs, sbs, jobs, passes, recs, rjobs, frames, coefs, resid, ptab, dbg);
+    else         launch_plf_p<uint8_t>(fmt >> 1, st, *pl, plist, llist, wgs, sbs, jobs, passes, recs, rjobs, frames, coefs, resid, ptab, dbg);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int vp9hip_launch_mc(int hb, hipStream_t st, int n, const McUnit *units, const FrameDesc *frames)

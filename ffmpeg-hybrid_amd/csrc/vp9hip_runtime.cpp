@@ -45,9 +45,10 @@ int vp9hip_launch_pred(int fmt, hipStream_t st, int nwg, const uint32_t *list, c
 int vp9hip_launch_lf(int fmt, hipStream_t st, int nsb, const uint32_t *list, const LFRec *recs,
                      const FrameDesc *frames, int dbg);
 int vp9hip_launch_mc(int hb, hipStream_t st, int n, const McUnit *units, const FrameDesc *frames);
-int vp9hip_launch_plf(int fmt, hipStream_t st, int npred, const uint32_t *plist, int nlf, const uint32_t *llist,
+int vp9hip_launch_plf(int fmt, hipStream_t st, const PlfLaunch *pl, const uint32_t *plist, const uint32_t *llist,
                       const WGRec *wgs, const SBRec *sbs, const PJob *jobs, const uint32_t *passes, const LFRec *recs,
-                      const FrameDesc *frames, const int16_t *resid, const uint32_t *ptab, int dbg);
+                      const RJob *rjobs, const FrameDesc *frames, const void *coefs, int16_t *resid, const uint32_t *ptab,
+                      int dbg);
 }
 
 namespace {
@@ -62,8 +63,14 @@ const uint8_t intra_txfm_type[14] = { 2, 1, 0, 0, 3, 2, 1, 2, 1, 3, 0, 0, 0, 0 }
 // (intra diagonal `step` + LF diagonal step - PLF_LAG in one launch): off / n the intra
 // workgroups, off2 / n2 the LF SBs
 struct Launch { int kind; uint32_t off; uint32_t n; int arg; int grp; int ph; int part; int step;
-                uint32_t off2 = 0, n2 = 0; };
+                uint32_t off2 = 0, n2 = 0;
+                uint32_t roff[5] = { 0, 0, 0, 0, 0 }, rn[5] = { 0, 0, 0, 0, 0 };   // K_PLF residual jobs by tx code
+};
 #define PLF_LAG 3   // see the schedule in stage()
+// Residuals run inside the fused launches (one intra diagonal ahead) for phases of fewer
+// frames than this; wide phases (keyframe batches) keep their separate k_resid launches:
+// measured C2 +6.5 % fused, C3 -2 %, C4 -8 %
+#define RES_FUSE_MAX_FRAMES 8
 enum { PART_RECON, PART_LF };           // a phase's reconstruction launches, then its loop filter
 #define MAX_GROUPS 8                    // independent frame groups = concurrent launch chains
 #define LF_LAG 2                        // LF diagonal j needs intra diagonals <= j + LF_LAG (see enqueue_batch)
@@ -419,6 +426,7 @@ struct FrameBuild {
     int scale[3][2], step[3][2]; // reference scale factors (vp9.c:845-880), 0 = unscaled
     int refw[3][2], refh[3][2];  // visible reference plane sizes
     uint64_t coef_base;          // element offset of this frame's coefficients in the batch stream
+    bool by_diag = false;        // residual buckets per intra diagonal of the SB (fused schedule)
 };
 
 struct PendingJob { PJob j; int level, ts; uint32_t d0, nd; };   // deps: pdeps[d0 .. d0 + nd)
@@ -592,6 +600,9 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
         // sharded batches reconstruct their own tile columns only; every SB keeps its LF
         // record (the loop filter runs over the whole frame on every shard)
         const bool mine = tile >= fb.tile_lo && tile < fb.tile_hi;
+        // residual bucket: per intra diagonal of the SB (fused schedule) or the phase
+        const int rbi = fb.by_diag ? (sbx - tile_sb0) + sby : fb.phase;
+        if ((int) s.rbucket.size() <= rbi) s.rbucket.resize(rbi + 1);
         LFRec lf;
         memset(&lf, 0, sizeof(lf));
         lf.frame = fb.frame_idx; lf.sbx = sbx; lf.sby = sby;
@@ -652,7 +663,7 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
                             } else {
                                 r.dst = (uint32_t) ((size_t) (by + y * 4) * fb.pitch[p ? 1 : 0] + bx + x * 4);
                             }
-                            s.rbucket[fb.phase][tcode][txtp].push_back(r);
+                            s.rbucket[rbi][tcode][txtp].push_back(r);
                         }
                         coef += e;
                         if (!b->intra || !mine) continue;
@@ -965,7 +976,7 @@ struct FramePlan {
 static int plan_frame(FrameBuild fb, FramePlan &fp)
 {
     fp.s.rbucket.resize(1);
-    fb.phase = 0;
+    fb.phase = 0;                                // non-fused: one bucket set (index 0)
     std::vector<std::vector<uint32_t>> ps;
     int r = build_frame(nullptr, fp.s, fb, ps, fp.lsteps);
     if (r < 0) return r;
@@ -1067,6 +1078,11 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     for (int i = 0; i < n; i++) maxpos = std::max(maxpos, pos[i]);
     const int NP = G * (maxpos + 1);                   // phase id = g * (maxpos + 1) + pos
     s.nphases = NP;
+    // residuals fused into the wavefront launches: per phase (RES_FUSE_MAX_FRAMES)
+    std::vector<int> phase_n(NP, 0);
+    for (int i = 0; i < n; i++) phase_n[grp[i] * (maxpos + 1) + pos[i]]++;
+    std::vector<char> res_fused(NP);
+    for (int ph = 0; ph < NP; ph++) res_fused[ph] = fuse && phase_n[ph] < RES_FUSE_MAX_FRAMES;
     // per frame: validate, frame descriptor, reference scaling (sequential, cheap)
     std::vector<FrameBuild> fbs(n);
     std::vector<size_t> coef_off(n + 1, 0);
@@ -1132,6 +1148,7 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
         fb.coef_base = coef_base;
         fb.phase = grp[i] * (maxpos + 1) + pos[i];
         fb.tile_lo = tile_lo; fb.tile_hi = tile_hi;
+        fb.by_diag = res_fused[fb.phase];
         s.frame_phase[i] = fb.phase;
         s.frame_log2[i] = f->log2_tile_cols;
         coef_off[i + 1] = coef_off[i] + (size_t) f->ncoefs * csz;
@@ -1169,7 +1186,7 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     // are written, with their index fixups, straight into the pinned arena image below.
     for (int i = 0; i < n; i++)
         if (plans[i].err < 0) return plans[i].err;
-    struct Off { uint32_t sb, job, pass, wg, lf, mc; uint64_t res; uint32_t rj[5][4]; };
+    struct Off { uint32_t sb, job, pass, wg, lf, mc; uint64_t res; };
     std::vector<Off> off(n);
     Off tot = {};
     for (int i = 0; i < n; i++) {
@@ -1183,18 +1200,27 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     s.resid16 = tot.res;
     std::vector<std::vector<int>> phase_frames(NP);
     for (int i = 0; i < n; i++) phase_frames[fbs[i].phase].push_back(i);
-    std::vector<std::array<std::pair<uint32_t, uint32_t>, 5>> rj_range(NP);   // per phase, tx code: (off, n)
+    // residual jobs per (phase, bucket = intra diagonal when fused, tx code): (off, n)
+    std::vector<std::vector<std::array<std::pair<uint32_t, uint32_t>, 5>>> rj_range(NP);
+    std::vector<std::vector<std::array<std::array<uint32_t, 4>, 5>>> rj_off(n);   // per frame, bucket
+    for (int i = 0; i < n; i++) rj_off[i].resize(plans[i].s.rbucket.size());
     uint32_t tot_rj = 0;
-    for (int ph = 0; ph < NP; ph++)                    // phase ids are group-major, chain order
-        for (int t = 0; t < 5; t++) {
-            rj_range[ph][t].first = tot_rj;
-            for (int tp = 0; tp < 4; tp++)
-                for (int i : phase_frames[ph]) {
-                    off[i].rj[t][tp] = tot_rj;
-                    tot_rj += (uint32_t) plans[i].s.rbucket[0][t][tp].size();
-                }
-            rj_range[ph][t].second = tot_rj - rj_range[ph][t].first;
-        }
+    for (int ph = 0; ph < NP; ph++) {                  // phase ids are group-major, chain order
+        size_t nb = 0;
+        for (int i : phase_frames[ph]) nb = std::max(nb, plans[i].s.rbucket.size());
+        rj_range[ph].resize(nb);
+        for (size_t d = 0; d < nb; d++)
+            for (int t = 0; t < 5; t++) {
+                rj_range[ph][d][t].first = tot_rj;
+                for (int tp = 0; tp < 4; tp++)
+                    for (int i : phase_frames[ph]) {
+                        if (d >= plans[i].s.rbucket.size()) continue;
+                        rj_off[i][d][t][tp] = tot_rj;
+                        tot_rj += (uint32_t) plans[i].s.rbucket[d][t][tp].size();
+                    }
+                rj_range[ph][d][t].second = tot_rj - rj_range[ph][d][t].first;
+            }
+    }
     // per workgroup / LF record: the algorithmic pixel bytes its SB moves (fused launches)
     std::vector<double> wg_bytes(tot.wg, 0.0), lf_bytes(tot.lf, 0.0);
     for (int i = 0; i < n; i++) {
@@ -1228,9 +1254,11 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     for (int g = 0; g < G; g++)
         for (int ph = g * (maxpos + 1); ph < (g + 1) * (maxpos + 1); ph++) {
             for (auto &mr : mcr[ph]) s.launches.push_back({ K_MC, mr.first, mr.second, 0, g, ph, PART_RECON, 0 });
-            for (int t = 0; t < 5; t++)                 // residual jobs placed by the merge
-                if (rj_range[ph][t].second)
-                    s.launches.push_back({ K_RESID, rj_range[ph][t].first, rj_range[ph][t].second, t, g, ph, PART_RECON, 0 });
+            if (!res_fused[ph])                          // residual jobs placed by the merge
+                for (auto &rr : rj_range[ph])
+                    for (int t = 0; t < 5; t++)
+                        if (rr[t].second)
+                            s.launches.push_back({ K_RESID, rr[t].first, rr[t].second, t, g, ph, PART_RECON, 0 });
             auto add_list = [&](int kind, const std::vector<uint32_t> &v, int step) {
                 if (v.empty()) return;
                 s.launches.push_back({ kind, (uint32_t) s.lists.size(), (uint32_t) v.size(), 0, g, ph,
@@ -1251,24 +1279,37 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
             // whose pixels no LF SB of diagonal t - 3 touches (that needs x - x_in_tile + y < 0).
             // This is the ordering the reference gets from its pre-LF intra_pred_data row
             // (vp9.c:1404-1416), without a second copy.
+            // The residuals of intra diagonal t + 1 (inverse transforms, incl. inter
+            // residuals added onto the MC prediction) run in launch t too, so no separate
+            // residual pass precedes the wavefront: launch -1 holds diagonal 0's alone.
             const int np = (int) wls.size(), nlf = (int) lsteps[ph].size();
-            const int nt = std::max(np, nlf ? nlf + PLF_LAG : 0);
-            for (int t = 0; t < nt; t++) {
-                const std::vector<uint32_t> *pv = t < np && !wls[t].empty() ? &wls[t] : nullptr;
+            const int nres = res_fused[ph] ? (int) rj_range[ph].size() : 0;
+            const int nt = std::max(std::max(np, nlf ? nlf + PLF_LAG : 0), nres - 1);
+            for (int t = -1; t < nt; t++) {
+                const std::vector<uint32_t> *pv = t >= 0 && t < np && !wls[t].empty() ? &wls[t] : nullptr;
                 const int j = t - PLF_LAG;
                 const std::vector<uint32_t> *lv = j >= 0 && j < nlf && !lsteps[ph][j].empty() ? &lsteps[ph][j] : nullptr;
-                if (pv && lv) {
-                    Launch L = { K_PLF, (uint32_t) s.lists.size(), (uint32_t) pv->size(), 0, g, ph, PART_RECON, t };
+                const std::array<std::pair<uint32_t, uint32_t>, 5> *rr = t + 1 < nres ? &rj_range[ph][t + 1] : nullptr;
+                bool res = false;
+                for (int k = 0; rr && k < 5; k++) res |= (*rr)[k].second > 0;
+                if (!pv && !res) {
+                    if (lv) add_list(K_LF, *lv, j);
+                    continue;
+                }
+                Launch L = { K_PLF, (uint32_t) s.lists.size(), 0, 0, g, ph, PART_RECON, t };
+                if (pv) {
+                    L.n = (uint32_t) pv->size();
                     s.lists.insert(s.lists.end(), pv->begin(), pv->end());
-                    L.off2 = (uint32_t) s.lists.size();
+                    for (uint32_t w : *pv) { s.alg_bytes[K_PRED] -= wg_bytes[w]; s.alg_bytes[K_PLF] += wg_bytes[w]; }
+                }
+                L.off2 = (uint32_t) s.lists.size();
+                if (lv) {
                     L.n2 = (uint32_t) lv->size();
                     s.lists.insert(s.lists.end(), lv->begin(), lv->end());
-                    s.launches.push_back(L);
-                    // algorithmic bytes of the fused launch move from K_PRED / K_LF to K_PLF
-                    for (uint32_t w : *pv) { s.alg_bytes[K_PRED] -= wg_bytes[w]; s.alg_bytes[K_PLF] += wg_bytes[w]; }
                     for (uint32_t li : *lv) { s.alg_bytes[K_LF] -= lf_bytes[li]; s.alg_bytes[K_PLF] += lf_bytes[li]; }
-                } else if (pv) add_list(K_PRED, *pv, t);
-                else if (lv) add_list(K_LF, *lv, j);
+                }
+                for (int k = 0; res && k < 5; k++) { L.roff[k] = (*rr)[k].first; L.rn[k] = (*rr)[k].second; }
+                s.launches.push_back(L);
             }
         }
     if (s.resid16 > 0xffffffffull) return VP9HIP_ENOMEM;
@@ -1341,10 +1382,11 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
                 if (!l.lfs.empty()) memcpy((LFRec *) (img + s.o_lfs) + q.lf, l.lfs.data(), l.lfs.size() * sizeof(LFRec));
                 if (!l.mcs.empty()) memcpy((McUnit *) (img + s.o_mcs) + q.mc, l.mcs.data(), l.mcs.size() * sizeof(McUnit));
                 double ib = 0;
+                for (size_t d = 0; d < l.rbucket.size(); d++)
                 for (int t = 0; t < 5; t++)
                     for (int tp = 0; tp < 4; tp++) {
-                        const std::vector<RJob> &bk = l.rbucket[0][t][tp];
-                        RJob *dst = (RJob *) (img + s.o_rjobs) + q.rj[t][tp];
+                        const std::vector<RJob> &bk = l.rbucket[d][t][tp];
+                        RJob *dst = (RJob *) (img + s.o_rjobs) + rj_off[i][d][t][tp];
                         for (size_t k = 0; k < bk.size(); k++) {
                             RJob r = bk[k];
                             if (!(r.ptx & 32)) r.dst += res;          // intra: residual scratch offset
@@ -1365,6 +1407,12 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
         for (auto &t : pool) t.join();
     }
     for (int i = 0; i < n; i++) s.alg_bytes[K_RESID] += inplace_bytes[i];
+    for (int i = 0; i < n; i++)                  // residuals that run inside the k_plf launches
+        if (res_fused[fbs[i].phase]) {
+            const double b = (double) pkts[i].ncoefs * csz + inplace_bytes[i];
+            s.alg_bytes[K_RESID] -= b;
+            s.alg_bytes[K_PLF] += b;
+        }
     HIPCHK(hipMemcpyAsync(s.arena, img, o, hipMemcpyHostToDevice, c->st));
     STAGE_T(4);
     HIPCHK(hipStreamSynchronize(c->st));
@@ -1428,11 +1476,16 @@ static int launch_one(vp9hip_ctx *c, const Launch &L, hipStream_t st)
                                   (const uint32_t *) (s.arena + s.o_passes), fr, s.resid, c->ptab, c->dbg);
     case K_LF:
         return vp9hip_launch_lf(c->hb | c->ss_h << 1 | c->ss_v << 2, st, (int) L.n, lists + L.off, (const LFRec *) (s.arena + s.o_lfs), fr, c->dbg >> 16);
-    case K_PLF:
-        return vp9hip_launch_plf(c->hb | c->ss_h << 1 | c->ss_v << 2, st, (int) L.n, lists + L.off, (int) L.n2,
-                                 lists + L.off2, (const WGRec *) (s.arena + s.o_wgs), (const SBRec *) (s.arena + s.o_sbs),
+    case K_PLF: {
+        PlfLaunch pl;
+        pl.npred = L.n; pl.nlf = L.n2;
+        for (int k = 0; k < 5; k++) { pl.roff[k] = L.roff[k]; pl.rn[k] = L.rn[k]; }
+        return vp9hip_launch_plf(c->hb | c->ss_h << 1 | c->ss_v << 2, st, &pl, lists + L.off, lists + L.off2,
+                                 (const WGRec *) (s.arena + s.o_wgs), (const SBRec *) (s.arena + s.o_sbs),
                                  (const PJob *) (s.arena + s.o_pjobs), (const uint32_t *) (s.arena + s.o_passes),
-                                 (const LFRec *) (s.arena + s.o_lfs), fr, s.resid, c->ptab, c->dbg);
+                                 (const LFRec *) (s.arena + s.o_lfs), (const RJob *) (s.arena + s.o_rjobs), fr,
+                                 s.arena + s.o_coefs, s.resid, c->ptab, c->dbg);
+    }
     }
     return -1;
 }

@@ -128,6 +128,14 @@ typedef struct LFRec {
     uint8_t  prog[LF_PROG_BYTES];
 } LFRec;
 
+/* One fused wavefront launch (k_plf): `npred` intra workgroups (one SB each), `nlf` LF
+ * SBs, and per transform code (4x4, 8x8, 16x16, 32x32, WHT) rn[k] residual jobs starting
+ * at RJob roff[k] (the residuals of the next intra diagonal). */
+typedef struct PlfLaunch {
+    uint32_t npred, nlf;
+    uint32_t roff[5], rn[5];
+} PlfLaunch;
+
 /* One motion-compensated rectangle of one plane (<= 64 x 64) and its references. Per
  * reference, output pixel (i, j) samples the reference at x = ix + ((mx + i dx) >> 4),
  * phase (mx + i dx) & 15 (y likewise): the stepping of do_scaled_8tap / do_scaled_bilin

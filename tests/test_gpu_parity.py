@@ -101,6 +101,21 @@ def test_batch_interleaved_keyframes(v9, orc, gpu):
         _cmp(v9, gpu.download(i), ref, w, h, "batch frame %d" % i)
 
 
+def test_wide_batch_separate_residual_launches(v9, orc, gpu):
+    """A batch wide enough (>= 8 frames per phase) that residuals run as their own k_resid
+    launches before the fused intra + LF wavefront (narrow phases fuse them too)."""
+    w, h, n = 200, 136, 27
+    frames = [v9.SynthFrame(v9.synth_params(w, h, 8, seed=300 + i)) for i in range(n)]
+    gpu.configure(w, h, 8, nbufs=n)
+    gpu.stage_batch(frames, list(range(n)))
+    gpu.run_batch()
+    gpu.sync()
+    for i in (0, 7, 13, 26):
+        ref = v9.alloc_planes(w, h, 8)
+        orc.decode_frame(frames[i].pkt, ref)
+        _cmp(v9, gpu.download(i), ref, w, h, "wide batch frame %d" % i)
+
+
 def test_decoder_api_sequence(v9, orc):
     """send_packet / receive_frame over a key + 3 inter frames."""
     w, h = 160, 96
