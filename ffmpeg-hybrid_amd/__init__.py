@@ -106,7 +106,7 @@ ABI_SYMBOLS = ["vp9hip_open", "vp9hip_close", "vp9hip_configure", "vp9hip_submit
                "vp9hip_stage_batch", "vp9hip_stage_batch_refs", "vp9hip_run_batch", "vp9hip_sync",
                "vp9hip_download_frame",
                "vp9hip_upload_frame", "vp9hip_flush", "vp9hip_last_timing", "vp9hip_set_timing",
-               "vp9hip_alg_bytes", "vp9hip_plan_stats", "vp9hip_abi_version",
+               "vp9hip_alg_bytes", "vp9hip_plan_stats", "vp9hip_abi_version", "vp9hip_set_graph",
                "vp9hip_stage_batch_tiles", "vp9hip_batch_phases", "vp9hip_phase_frames", "vp9hip_run_phase",
                "vp9hip_stripe", "vp9hip_frame_device", "vp9hip_batch_groups",
                "vp9h_decode_frame", "vp9h_encode_frame", "vp9h_frame_free", "vp9h_buffer_free",

@@ -187,7 +187,9 @@ static int configure(vp9hip_decoder *d, const vp9h_frame &f)
     const int w = d->p.max_width > 0 ? d->p.max_width : f.width;
     const int h = d->p.max_height > 0 ? d->p.max_height : f.height;
     if (f.width > w || f.height > h) return VP9HIP_ENOSYS;
-    const int nb = 8 + d->p.max_batch + (d->p.extra_bufs > 0 ? d->p.extra_bufs : 4);
+    // 8 reference slots, the batch being filled, the launched batch's frames still to be
+    // received, and the frames the caller holds
+    const int nb = 8 + 2 * d->p.max_batch + (d->p.extra_bufs > 0 ? d->p.extra_bufs : 4);
     int r = vp9hip_configure(d->ctx, w, h, f.bpp, f.ss_h, f.ss_v, nb);
     if (r < 0) return r;
     d->configured = true;
@@ -292,6 +294,8 @@ extern "C" int vp9hip_decoder_open(const vp9hip_decoder_params *params, vp9hip_d
     for (int s = 0; s < 8; s++) d->slot[s] = -1;
     int r = vp9hip_open(d->p.device, &d->ctx);
     if (r < 0) { vp9hip_decoder_close(d); return r; }
+    vp9hip_set_timing(d->ctx, 0);             // every batch runs once: plain launches, no events
+    vp9hip_set_graph(d->ctx, 0);
     for (int t = 0; t < d->p.parse_threads; t++) d->workers.emplace_back(worker_main, d);
     *out = d;
     return 0;
@@ -363,8 +367,11 @@ extern "C" int vp9hip_decoder_send_packet(vp9hip_decoder *d, const uint8_t *data
 extern "C" int vp9hip_decoder_receive_frame(vp9hip_decoder *d, vp9hip_decoded_frame *out)
 {
     if (!d || !out) return VP9HIP_EINVAL;
-    int r = consume(d, d->draining);
-    if (r < 0) return r;
+    int r = 0;
+    if (d->outq.empty() || !d->outq.front().submitted) {   // nothing to hand out yet: make progress
+        r = consume(d, d->draining);
+        if (r < 0) return r;
+    }
     if (d->draining) {                         // everything parsed that can be placed: launch it
         r = submit(d);
         if (r < 0) return r;

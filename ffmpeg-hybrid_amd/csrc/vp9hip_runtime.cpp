@@ -861,13 +861,18 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
             h.job0 = (uint32_t) s.sbjobs.size();
             h.njobs = (uint32_t) pj.size();
             h.nlev = 0;
+            // each job's producers were appended to pdeps right after the previous job's,
+            // so the SB's lists go over in one block
+            const uint32_t jd = (uint32_t) s.jdeps.size();
+            s.jdeps.insert(s.jdeps.end(), pdeps.begin(), pdeps.end());
+            const size_t j0 = s.sbjobs.size();
+            s.sbjobs.resize(j0 + pj.size());
             for (size_t k = 0; k < pj.size(); k++) {
-                s.sbjobs.push_back(pj[k].j);
-                s.jdep0.push_back((uint32_t) s.jdeps.size());
-                s.jdeps.insert(s.jdeps.end(), pdeps.begin() + pj[k].d0, pdeps.begin() + pj[k].d0 + pj[k].nd);
+                s.sbjobs[j0 + k] = pj[k].j;
+                s.jdep0.push_back(jd + pj[k].d0);
                 h.nlev = std::max<uint32_t>(h.nlev, (uint32_t) pj[k].level + 1);
             }
-            s.jdep0.push_back((uint32_t) s.jdeps.size());
+            s.jdep0.push_back(jd + (uint32_t) pdeps.size());
             s.sbh.push_back(h);
             uint32_t sbi = (uint32_t) s.sbs.size();
             s.sbs.push_back(sr);
@@ -909,7 +914,7 @@ static int merge_mixed(Staged &s, uint32_t sbi)
     const uint32_t *d0 = s.jdep0.data() + h.job0 + sbi;
     // scratch reused across SBs of this thread (no allocations per SB or pass):
     // successor lists in CSR form, in-degrees, heights (longest path to a sink)
-    thread_local std::vector<int> indeg, height, soff, ready, next, take;
+    thread_local std::vector<int> indeg, height, soff, ready, next, take, fresh;
     thread_local std::vector<uint16_t> succ;
     indeg.assign(N, 0); height.assign(N, 1); soff.assign(N + 1, 0);
     const uint32_t e0 = d0[0], e1 = d0[N];
@@ -926,16 +931,15 @@ static int merge_mixed(Staged &s, uint32_t sbi)
     }
     for (int k = N - 1; k >= 0; k--)                      // producers precede consumers
         for (int e = soff[k]; e < soff[k + 1]; e++) height[k] = std::max(height[k], height[succ[e]] + 1);
+    // ready list kept in priority order: highest remaining critical path first, then
+    // decode order; each pass merges its newly ready jobs into the leftovers
+    auto before = [&](int a, int b) { return height[a] != height[b] ? height[a] > height[b] : a < b; };
     ready.clear();
     for (int k = 0; k < N; k++) if (!indeg[k]) ready.push_back(k);
+    std::sort(ready.begin(), ready.end(), before);
     int done = 0;
     while (done < N) {
         if (ready.empty()) return VP9HIP_EBUG;
-        // highest remaining critical path first, then decode order
-        std::sort(ready.begin(), ready.end(), [&](int a, int b) {
-            if (height[a] != height[b]) return height[a] > height[b];
-            return a < b;
-        });
         int lanes = 0, cnt[4] = { 0, 0, 0, 0 };
         take.clear();
         next.clear();
@@ -951,11 +955,14 @@ static int merge_mixed(Staged &s, uint32_t sbi)
                 if ((int) PJ_TS(jobs[k]) == ts) { s.pjobs.push_back(jobs[k]); cnt[ts]++; }
         s.passes.push_back(first << 14 | (uint32_t) cnt[0] << 9 | (uint32_t) cnt[1] << 5 | (uint32_t) cnt[2] << 2 |
                            (uint32_t) cnt[3]);
+        fresh.clear();
         for (int k : take)
             for (int e = soff[k]; e < soff[k + 1]; e++)
-                if (--indeg[succ[e]] == 0) next.push_back(succ[e]);
+                if (--indeg[succ[e]] == 0) fresh.push_back(succ[e]);
+        std::sort(fresh.begin(), fresh.end(), before);
         done += (int) take.size();
-        ready.swap(next);
+        ready.resize(next.size() + fresh.size());
+        std::merge(next.begin(), next.end(), fresh.begin(), fresh.end(), ready.begin(), before);
     }
     const size_t nj = s.pjobs.size() - wg.job0, np = s.passes.size() - wg.pass0;
     if (nj > MAX_SB_JOBS || np > MAX_SB_JOBS) return VP9HIP_EINVALIDDATA;
@@ -1762,6 +1769,13 @@ extern "C" int vp9hip_set_timing(vp9hip_ctx *c, int on)
 {
     if (!c) return VP9HIP_EINVAL;
     c->timing = on != 0;
+    return 0;
+}
+
+extern "C" int vp9hip_set_graph(vp9hip_ctx *c, int on)
+{
+    if (!c) return VP9HIP_EINVAL;
+    c->use_graph = on != 0;
     return 0;
 }
 

@@ -201,6 +201,10 @@ int  vp9hip_last_timing(vp9hip_ctx *ctx, const char **names, double *ms, int *la
 
 /* Per-launch HIP-event timing on/off (default on). */
 int  vp9hip_set_timing(vp9hip_ctx *ctx, int on);
+/* Graph replay of a staged batch (default on): run_batch captures the batch's launch
+ * sequence into a HIP graph once and replays it. Off: every run_batch enqueues the
+ * launches directly (cheaper for a batch that runs once, e.g. the decoder's). */
+int  vp9hip_set_graph(vp9hip_ctx *ctx, int on);
 
 /* Algorithmic bytes (B = C + P(1+R) + 2P[LF]) of the staged batch,
  * per kernel class in vp9hip_last_timing order. Returns count. */
@@ -369,7 +373,8 @@ void vp9h_ivf_write_frame_header(uint8_t out[12], uint32_t frame_size, int64_t p
 typedef struct vp9hip_decoder vp9hip_decoder;
 typedef struct vp9hip_decoder_params {
     int32_t device;
-    int32_t max_batch;             /* frames per GPU batch (decoder delay), default 16        */
+    int32_t max_batch;             /* frames per GPU batch (decoder delay), default 16; the  */
+                                   /* decoder holds 8 + 2 max_batch + extra_bufs buffers      */
     int32_t extra_bufs;            /* output frames the caller may hold at once, default 4     */
     int32_t max_width, max_height; /* buffer size; 0: the first keyframe's (larger inter      */
                                    /* frames, e.g. reference scaling up, need it set)         */

@@ -163,7 +163,7 @@ def test_decoder_eagain_flush_and_restart(v9, orc):
                                          for i, f in enumerate(fr[1:])]
     pkts = _stream(v9)
     ref = _oracle_outputs(v9, orc, pkts)
-    dec = v9.Decoder(0, max_batch=4, extra_bufs=1, parse_threads=1)   # 13 buffers, <= 5 frames in parse
+    dec = v9.Decoder(0, max_batch=4, extra_bufs=1, parse_threads=1)   # 17 buffers, <= 5 frames in parse
     held = []
     sent = 0
     with pytest.raises(v9.Vp9HipError) as e:
