@@ -952,49 +952,49 @@ __global__ __launch_bounds__(64) void k_pred(const uint32_t *__restrict__ list, 
     pred_wg<PIX, G>(wgs + list[blockIdx.x], sbs, jobs, passes, frames, resid, ptab, S, threadIdx.x, dbg);
 }
 
-// 8-pixel chunk <-> 8 uint16 of the LF tile (tile rows are 4-byte aligned)
-// 8 pixels between a global chunk and an LDS tile row of PIX (rows dword-aligned)
-template <typename PIX> struct Chunk8;
-template <> struct Chunk8<uint8_t> {
-    typedef uint2 T;
-    static DEV T zero() { return make_uint2(0, 0); }
-    static DEV void to_lds(T v, uint8_t *t) { uint32_t *d = (uint32_t *) t; d[0] = v.x; d[1] = v.y; }
-    static DEV T from_lds(const uint8_t *t) { const uint32_t *s = (const uint32_t *) t; return make_uint2(s[0], s[1]); }
-};
-template <> struct Chunk8<uint16_t> {
+// 16-byte chunks between global memory and the LF tile (16 pixels at 8-bit, 8 at 16-bit):
+// one dwordx4 load / store each, 16-byte aligned in the frame buffer
+struct Chunk16 {
     typedef uint4 T;
     static DEV T zero() { return make_uint4(0, 0, 0, 0); }
-    static DEV void to_lds(T v, uint16_t *t)
+    static DEV void to_lds(T v, void *t)
     {
         uint32_t *d = (uint32_t *) t;
         d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
     }
-    static DEV T from_lds(const uint16_t *t)
+    static DEV T from_lds(const void *t)
     {
         const uint32_t *s = (const uint32_t *) t;
         return make_uint4(s[0], s[1], s[2], s[3]);
     }
 };
 
-// LF tile geometry: luma 72 x 72 (x, y = -8..63), chroma (CW + 8) x (CH + 8); pitches in
-// pixels, rows dword-aligned with an odd dword count (lanes of the column pass read
-// dword i of consecutive rows: no bank conflicts)
+// LF tile geometry. A tile row starts XL pixels left of the SB (16 at 8-bit, 8 at 16-bit,
+// so chunks stay 16-byte aligned) and holds XL + 64 (luma) / XL + CW (chroma) pixels; the
+// filters see x = -8 .. at offset XO = XL - 8. Rows: y = -8 .. 63 (luma) / CH - 1. Pitches
+// in pixels, rows dword-aligned with an odd dword count (lanes of the column pass read
+// dword i of consecutive rows: no bank conflicts).
 template <typename PIX, class G> struct LfP {
-    static constexpr int YP = sizeof(PIX) == 1 ? 76 : 74;
-    static constexpr int UVP = G::CW + 8 + (sizeof(PIX) == 1 ? 4 : 2);
+    static constexpr int CPX = 16 / sizeof(PIX);    // pixels per chunk
+    static constexpr int XL = CPX;                  // left halo loaded (8 used)
+    static constexpr int XO = XL - 8;               // tile offset of x = -8
+    static constexpr int YP = sizeof(PIX) == 1 ? 84 : 74;
+    static constexpr int UVP = G::CW + XL + (sizeof(PIX) == 1 ? 4 : 2);
     static constexpr int PPW = 4 / sizeof(PIX);     // pixels per dword
-    static constexpr int CK = G::CW / 8 + 1;        // 8-pixel chunks per chroma tile row
+    static constexpr int YK = (64 + XL) / CPX;      // chunks per luma tile row
+    static constexpr int CK = (G::CW + XL) / CPX;   // chunks per chroma tile row
     static constexpr int CR = G::CH + 8;            // chroma tile rows
-    static constexpr int NCHUNK = 648 + 2 * CR * CK;
+    static constexpr int NY = 72 * YK;
+    static constexpr int NCHUNK = NY + 2 * CR * CK;
     static constexpr int PROG = LF_PROG_OF(G::SH, G::SV);
 };
 
-// chunk index -> (plane, tile row, chunk column): luma 72 rows x 9, then U, V CR x CK
+// chunk index -> (plane, tile row, chunk column): luma 72 rows x YK, then U, V CR x CK
 template <typename PIX, class G> DEV void lf_chunk(int ci, int &p, int &r, int &k)
 {
     typedef LfP<PIX, G> L;
-    if (ci < 648) { p = 0; r = ci / 9; k = ci - r * 9; }
-    else { const int c = ci - 648; p = 1 + (c >= L::CR * L::CK); const int cc = c - (p - 1) * L::CR * L::CK; r = cc / L::CK; k = cc - r * L::CK; }
+    if (ci < L::NY) { p = 0; r = ci / L::YK; k = ci - r * L::YK; }
+    else { const int c = ci - L::NY; p = 1 + (c >= L::CR * L::CK); const int cc = c - (p - 1) * L::CR * L::CK; r = cc / L::CK; k = cc - r * L::CK; }
 }
 
 // --------------------------------------------------------------- k_lf
@@ -1208,10 +1208,11 @@ DEV void lf_sb(const LFRec &rec, const FrameDesc *__restrict__ frames, LfLds<PIX
     for (int i = lane; i < L::PROG / 4; i += NT) S.prog[i] = ((const uint32_t *) rec.prog)[i];
     for (int i = lane; i < 64; i += NT) S.lut[i] = lf_eih(i, sharp, bd);
 
-    // load: luma rows [y0-8, y0+64) x cols [x0-8, x0+64), chroma [-8, CH) x [-8, CW), in
-    // aligned 8-pixel chunks (4:2:0: luma 72 x 9, chroma 2 x 40 x 5 = 1048 chunks, <= 9 per
-    // thread), all global loads of a thread in flight before its LDS writes
-    typedef typename Chunk8<PIX>::T CT;
+    // load: luma rows [y0-8, y0+64) x cols [x0-XL, x0+64), chroma [-8, CH) x [-XL, CW), in
+    // aligned 16-byte chunks (4:2:0 8-bit: luma 72 x 5, chroma 2 x 40 x 3 = 600 chunks, <= 5
+    // per thread), all global loads of a thread in flight before its LDS writes
+    typedef Chunk16::T CT;
+    constexpr int CPX = L::CPX, XL = L::XL, XO = L::XO;
     constexpr int NU = (L::NCHUNK + NT - 1) / NT;
     CT v[NU];
 #pragma unroll
@@ -1219,8 +1220,8 @@ DEV void lf_sb(const LFRec &rec, const FrameDesc *__restrict__ frames, LfLds<PIX
         const int ci = lane + u * NT;
         int p, r, k;
         lf_chunk<PIX, G>(ci, p, r, k);
-        const int gx = (p ? sbx * CW : sbx * 64) - 8 + 8 * k, gy = (p ? sby * CH : sby * 64) - 8 + r;
-        v[u] = Chunk8<PIX>::zero();
+        const int gx = (p ? sbx * CW : sbx * 64) - XL + CPX * k, gy = (p ? sby * CH : sby * 64) - 8 + r;
+        v[u] = Chunk16::zero();
         if (!(dbg & 4) && ci < L::NCHUNK && gx >= 0 && gy >= 0)
             v[u] = *(const CT *) ((const PIX *) fd.plane[p] + (size_t) gy * fd.pitch[p ? 1 : 0] + gx);
     }
@@ -1231,7 +1232,7 @@ DEV void lf_sb(const LFRec &rec, const FrameDesc *__restrict__ frames, LfLds<PIX
         lf_chunk<PIX, G>(ci, p, r, k);
         if (ci < L::NCHUNK) {
             PIX *t = p ? ct[p - 1] + r * FCP : lt + r * FLP;
-            Chunk8<PIX>::to_lds(v[u], t + 8 * k);
+            Chunk16::to_lds(v[u], t + CPX * k);
         }
     }
     LF_SYNC();
@@ -1240,10 +1241,10 @@ DEV void lf_sb(const LFRec &rec, const FrameDesc *__restrict__ frames, LfLds<PIX
     // ---- column edges (filter_plane_cols, vp9lpf.c:31-104): one lane per pixel row ----
     for (int tid = lane; tid < 64 + 2 * CH; tid += NT) {
         if (tid < 64) {
-            lf_line_row_wide<PIX>((uint32_t *) (lt + (tid + 8) * FLP), S.prog + (LFP_YC + (tid >> 3) * 16) / 4, lut, bd);
+            lf_line_row_wide<PIX>((uint32_t *) (lt + (tid + 8) * FLP + XO), S.prog + (LFP_YC + (tid >> 3) * 16) / 4, lut, bd);
         } else {
             const int p = 1 + (tid - 64 >= CH), r = tid - 64 - (p - 1) * CH;
-            uint32_t *rowp = (uint32_t *) (ct[p - 1] + (r + 8) * FCP);
+            uint32_t *rowp = (uint32_t *) (ct[p - 1] + (r + 8) * FCP + XO);
             const uint32_t *pw = S.prog + (LFP_CC + (r >> 3) * LFP_CSTRIDE(G::SH)) / 4;
             if (G::SH) lf_line_row_narrow<PIX>(rowp, pw, lut, bd);
             else lf_line_row_wide<PIX>(rowp, pw, lut, bd);
@@ -1253,10 +1254,10 @@ DEV void lf_sb(const LFRec &rec, const FrameDesc *__restrict__ frames, LfLds<PIX
     // ---- row edges (filter_plane_rows, vp9lpf.c:106-181): one lane per pixel column ----
     for (int tid = lane; tid < 64 + 2 * CW; tid += NT) {
         if (tid < 64) {
-            lf_line_col_wide<PIX, FLP>(lt + 8 + tid, S.prog + (LFP_YR + (tid >> 3) * 16) / 4, lut, bd);
+            lf_line_col_wide<PIX, FLP>(lt + XL + tid, S.prog + (LFP_YR + (tid >> 3) * 16) / 4, lut, bd);
         } else {
             const int p = 1 + (tid - 64 >= CW), c = tid - 64 - (p - 1) * CW;
-            PIX *colp = ct[p - 1] + 8 + c;
+            PIX *colp = ct[p - 1] + XL + c;
             const uint32_t *pw = S.prog + (LFP_CR(G::SH, G::SV) + (c >> 3) * LFP_CSTRIDE(G::SV)) / 4;
             if (G::SV) lf_line_col_narrow<PIX, FCP>(colp, pw, lut, bd);
             else lf_line_col_wide<PIX, FCP>(colp, pw, lut, bd);
@@ -1272,10 +1273,10 @@ DEV void lf_sb(const LFRec &rec, const FrameDesc *__restrict__ frames, LfLds<PIX
         const int ci = lane + u * NT;
         int p, r, k;
         lf_chunk<PIX, G>(ci, p, r, k);
-        const int gx = (p ? sbx * CW : sbx * 64) - 8 + 8 * k, gy = (p ? sby * CH : sby * 64) - 8 + r;
+        const int gx = (p ? sbx * CW : sbx * 64) - XL + CPX * k, gy = (p ? sby * CH : sby * 64) - 8 + r;
         if (!(dbg & 2) && ci < L::NCHUNK && gx >= 0 && gy >= 0 && (r >= 8 || k > 0)) {
             const PIX *t = p ? ct[p - 1] + r * FCP : lt + r * FLP;
-            *(CT *) ((PIX *) fd.plane[p] + (size_t) gy * fd.pitch[p ? 1 : 0] + gx) = Chunk8<PIX>::from_lds(t + 8 * k);
+            *(CT *) ((PIX *) fd.plane[p] + (size_t) gy * fd.pitch[p ? 1 : 0] + gx) = Chunk16::from_lds(t + CPX * k);
         }
     }
 #undef LF_SYNC
