@@ -579,17 +579,19 @@ __global__ __launch_bounds__(64 * RWAVES) void k_resid(const RJob *__restrict__ 
 // vp9recon.c:37-221), every predictor pixel is one formula-table word
 // (vp9dsp_template.c:28-1106 restated per pixel), then + residual from k_resid, clip.
 // A tile's row 0 / column 0 hold the pixels above / left of the SB; pixel (x, y) of
-// plane p lives at tile_p[(y + 1) * pitch_p + x + 1].
+// plane p lives at tile_p[(y + 1) * pitch_p + x + PX0]: pixel rows start 4-pixel aligned,
+// so the SB interior moves between LDS and HBM in 16-byte chunks.
 #ifndef PRED_LTAB_LDS
 #define PRED_LTAB_LDS 1       // 4x4 / 8x8 formula words: LDS copy (1) or the global table via L1 (0)
 #endif
-#define LP 65            // luma tile pitch
+#define LP 68            // luma tile pitch (17 dwords at 8-bit: column reads are bank-conflict free)
+#define PX0 4            // tile column of pixel x = 0 (x = -1 at column 3)
 #define LT_SIZE (65 * LP)
 // chroma tile geometry of a subsampling (4:2:0 = Geo<1, 1>): CW x CH pixels per SB,
 // tile pitch CP, CT elements per chroma tile, TILE elements per SB (Y, U, V)
 template <int SSH, int SSV> struct Geo {
     static constexpr int SH = SSH, SV = SSV;
-    static constexpr int CW = 64 >> SSH, CH = 64 >> SSV, CP = CW + 1, CT = (CH + 1) * CP;
+    static constexpr int CW = 64 >> SSH, CH = 64 >> SSV, CP = CW + PX0, CT = (CH + 1) * CP;
     static constexpr int TILE = LT_SIZE + 2 * CT;
 };
 typedef Geo<1, 1> G420;
@@ -650,6 +652,65 @@ DEV void load_resid(const JSet &j, const int16_t *__restrict__ resid, PSet &ps)
 // Load the pixels above / left of an SB (and, for inter frames, its interior: the
 // MC prediction + inter residuals) into the LDS tile. All global loads of a batch are
 // issued before any LDS write so their latencies overlap.
+// 16-byte chunks between global memory and an LDS tile (16 pixels at 8-bit, 8 at 16-bit):
+// one dwordx4 load / store each, 16-byte aligned in the frame buffer
+struct Chunk16 {
+    typedef uint4 T;
+    static DEV T zero() { return make_uint4(0, 0, 0, 0); }
+    static DEV void to_lds(T v, void *t)
+    {
+        uint32_t *d = (uint32_t *) t;
+        d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+    }
+    static DEV T from_lds(const void *t)
+    {
+        const uint32_t *s = (const uint32_t *) t;
+        return make_uint4(s[0], s[1], s[2], s[3]);
+    }
+};
+
+// The SB interior (all planes) between HBM and the LDS tile in 16-byte chunks (16 px at
+// 8-bit, 8 at 16-bit): STORE = false loads (inter frames: MC prediction + inter residuals),
+// true stores the reconstructed SB. All loads of a lane are issued before its LDS writes.
+template <typename PIX, class G, bool STORE>
+DEV void sb_interior(const FrameDesc &fd, int sbx, int sby, int lane, PIX *tile)
+{
+    constexpr int CPX = 16 / sizeof(PIX);
+    constexpr int YK = 64 / CPX, CKX = G::CW / CPX;              // chunks per row
+    constexpr int NY = 64 * YK, NC = G::CH * CKX, NT = NY + 2 * NC;
+    constexpr int NB = 2;                                         // 16-byte loads in flight per lane (VGPR budget)
+    auto where = [&](int c, PIX *&g, PIX *&t) {
+        int p, r, k;
+        if (c < NY) { p = 0; r = c / YK; k = c - r * YK; }
+        else { const int cc = c - NY; p = 1 + (cc >= NC); const int q = cc - (p - 1) * NC; r = q / CKX; k = q - r * CKX; }
+        g = (PIX *) fd.plane[p] + (size_t) ((p ? sby * G::CH : sby * 64) + r) * fd.pitch[p ? 1 : 0] +
+            (p ? sbx * G::CW : sbx * 64) + k * CPX;
+        t = tile + (p == 0 ? 0 : p == 1 ? LT_SIZE : LT_SIZE + G::CT) + (r + 1) * (p ? G::CP : LP) + PX0 + k * CPX;
+    };
+#pragma unroll 1
+    for (int c0 = 0; c0 < NT; c0 += 64 * NB) {
+        uint4 v[NB];
+#pragma unroll
+        for (int u = 0; u < NB; u++) {
+            const int c = c0 + lane + 64 * u;
+            if (c >= NT) break;
+            PIX *g, *t;
+            where(c, g, t);
+            if (STORE) *(uint4 *) g = Chunk16::from_lds(t);
+            else v[u] = *(const uint4 *) g;
+        }
+        if (STORE) continue;
+#pragma unroll
+        for (int u = 0; u < NB; u++) {
+            const int c = c0 + lane + 64 * u;
+            if (c >= NT) break;
+            PIX *g, *t;
+            where(c, g, t);
+            Chunk16::to_lds(v[u], t);
+        }
+    }
+}
+
 template <typename PIX, class G>
 DEV void load_sb_tile(const FrameDesc &fd, int sbx, int sby, bool interior, int lane, PIX *tile)
 {
@@ -663,15 +724,11 @@ DEV void load_sb_tile(const FrameDesc &fd, int sbx, int sby, bool interior, int 
             const int w = p ? G::CW : 64, h = p ? G::CH : 64, tp = p ? G::CP : LP;
             PIX *t = tile + (p == 0 ? 0 : p == 1 ? LT_SIZE : LT_SIZE + G::CT);
             if (y0 > 0)
-                for (int i = lane; i <= w; i += 64) t[i] = x0 - 1 + i >= 0 ? g[(size_t) (y0 - 1) * pitch + x0 - 1 + i] : 0;
+                for (int i = lane; i <= w; i += 64) t[i + PX0 - 1] = x0 - 1 + i >= 0 ? g[(size_t) (y0 - 1) * pitch + x0 - 1 + i] : 0;
             if (x0 > 0)
-                for (int i = lane; i < h; i += 64) t[(i + 1) * tp] = g[(size_t) (y0 + i) * pitch + x0 - 1];
-            if (interior)
-                for (int i = lane; i < w * h; i += 64) {
-                    const int yy = i / w, xx = i - yy * w;
-                    t[(yy + 1) * tp + xx + 1] = g[(size_t) (y0 + yy) * pitch + x0 + xx];
-                }
+                for (int i = lane; i < h; i += 64) t[(i + 1) * tp + PX0 - 1] = g[(size_t) (y0 + i) * pitch + x0 - 1];
         }
+        if (interior) sb_interior<PIX, G, false>(fd, sbx, sby, lane, tile);
         return;
     }
     constexpr int CP = G::CP, CT_SIZE = G::CT;
@@ -695,36 +752,13 @@ DEV void load_sb_tile(const FrameDesc &fd, int sbx, int sby, bool interior, int 
     }
     PIX *tu = tile + LT_SIZE, *tv = tile + LT_SIZE + CT_SIZE;
     if (top) {
-        tile[lane] = v0;
-        if (lane == 0) tile[64] = v4;
-        (lane < 33 ? tu : tv)[ci] = v2;
-        if (lane < 2) tv[31 + lane] = v5;
+        tile[PX0 - 1 + lane] = v0;
+        if (lane == 0) tile[PX0 + 63] = v4;
+        (lane < 33 ? tu : tv)[PX0 - 1 + ci] = v2;
+        if (lane < 2) tv[PX0 + 30 + lane] = v5;
     }
-    if (left) { tile[(lane + 1) * LP] = v1; (lane < 32 ? tu : tv)[((lane & 31) + 1) * CP] = v3; }
-    if (!interior) return;
-    // interior: 64 luma rows + 2 x 32 chroma rows, 8 independent loads per lane per batch
-    // (16 in flight raised the kernel's register allocation by 40 VGPRs)
-    for (int i0 = 0; i0 < 64 * 64 + 2 * 32 * 32; i0 += 64 * 8) {
-        PIX t[8];
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-            const int i = i0 + u * 64 + lane;
-            if (i < 4096) t[u] = gy[(size_t) (ly + (i >> 6)) * py + lx + (i & 63)];
-            else {
-                const int c = i - 4096, pl = c >> 10, r = (c >> 5) & 31, x = c & 31;
-                t[u] = (pl ? gv : gu)[(size_t) (cy + r) * pc + cx + x];
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-            const int i = i0 + u * 64 + lane;
-            if (i < 4096) tile[((i >> 6) + 1) * LP + (i & 63) + 1] = t[u];
-            else {
-                const int c = i - 4096, pl = c >> 10, r = (c >> 5) & 31, x = c & 31;
-                tile[LT_SIZE + pl * CT_SIZE + (r + 1) * CP + x + 1] = t[u];
-            }
-        }
-    }
+    if (left) { tile[(lane + 1) * LP + PX0 - 1] = v1; (lane < 32 ? tu : tv)[((lane & 31) + 1) * CP + PX0 - 1] = v3; }
+    if (interior) sb_interior<PIX, G, false>(fd, sbx, sby, lane, tile);
 }
 
 // One pass of N x N jobs: lane li of group grp predicts column li of its job.
@@ -743,7 +777,7 @@ DEV void pred_pass(uint32_t w, int lane, PIX *tile, uint16_t *eb, int bd, const 
     const int p = PJ_PLANE(jb);
     const int tpch = p ? G::CP : LP;
     PIX *o = tile + PJ_SLOT(jb) * G::TILE + (p == 0 ? 0 : p == 1 ? LT_SIZE : LT_SIZE + G::CT) +
-             (PJ_Y4(jb) * 4 + 1) * tpch + PJ_X4(jb) * 4 + 1;
+             (PJ_Y4(jb) * 4 + 1) * tpch + PJ_X4(jb) * 4 + PX0;
     const int ms = PJ_MSLOT(jb), slot = ms < 9 ? ms : 9;
     const int toff = ts == 0 ? 0 : ts == 1 ? 16 : ts == 2 ? 80 : 336;
     // formula words of this column: rows of 4x4 / 8x8 from the LDS copy, larger from L1/L2.
@@ -923,19 +957,7 @@ DEV void pred_wg(const WGRec *wgp, const SBRec *__restrict__ sbs, const PJob *__
         const uint32_t sbi = __builtin_amdgcn_readfirstlane(wgp->sb[k]);
         if (sbi == 0xffffffffu) continue;
         const SBRec sb = sbs[sbi];
-        const FrameDesc &fd = frames[sb.frame];
-        for (int p = 0; p < 3; p++) {
-            const int sw = p ? G::CW : 64, sh = p ? G::CH : 64;
-            PIX *g = (PIX *) fd.plane[p];
-            const int pitch = fd.pitch[p ? 1 : 0];
-            const int x0 = sb.sbx * sw, y0 = sb.sby * sh;
-            const PIX *t = tile + k * G::TILE + (p == 0 ? 0 : p == 1 ? LT_SIZE : LT_SIZE + G::CT);
-            const int tpch = p ? G::CP : LP;
-            for (int i = lane; i < sw * sh; i += 64) {
-                const int yy = i / sw, xx = i - yy * sw;
-                g[(size_t) (y0 + yy) * pitch + x0 + xx] = t[(yy + 1) * tpch + xx + 1];
-            }
-        }
+        sb_interior<PIX, G, true>(frames[sb.frame], sb.sbx, sb.sby, lane, tile + k * G::TILE);
     }
 }
 
@@ -951,23 +973,6 @@ __global__ __launch_bounds__(64) void k_pred(const uint32_t *__restrict__ list, 
 #endif
     pred_wg<PIX, G>(wgs + list[blockIdx.x], sbs, jobs, passes, frames, resid, ptab, S, threadIdx.x, dbg);
 }
-
-// 16-byte chunks between global memory and the LF tile (16 pixels at 8-bit, 8 at 16-bit):
-// one dwordx4 load / store each, 16-byte aligned in the frame buffer
-struct Chunk16 {
-    typedef uint4 T;
-    static DEV T zero() { return make_uint4(0, 0, 0, 0); }
-    static DEV void to_lds(T v, void *t)
-    {
-        uint32_t *d = (uint32_t *) t;
-        d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
-    }
-    static DEV T from_lds(const void *t)
-    {
-        const uint32_t *s = (const uint32_t *) t;
-        return make_uint4(s[0], s[1], s[2], s[3]);
-    }
-};
 
 // LF tile geometry. A tile row starts XL pixels left of the SB (16 at 8-bit, 8 at 16-bit,
 // so chunks stay 16-byte aligned) and holds XL + 64 (luma) / XL + CW (chroma) pixels; the
