@@ -1198,6 +1198,47 @@ DEV uint32_t lf_eih(int L, int sharp, int bd)
     return E | I << 12 | H << 22;
 }
 
+// The filter passes of one SB over its LDS tile: all column edges of every plane (lanes =
+// pixel rows), then all row edges (lanes = pixel columns). Ends with a barrier.
+template <typename PIX, class G, int NT>
+DEV void lf_passes(LfLds<PIX, G> &S, int lane, int bd)
+{
+#define LF_SYNC() do { if (NT == 64) wave_sync(); else __syncthreads(); } while (0)
+    typedef LfP<PIX, G> L;
+    constexpr int FLP = L::YP, FCP = L::UVP, CW = G::CW, CH = G::CH;
+    constexpr int XL = L::XL, XO = L::XO;
+    PIX *lt = S.lt;
+    PIX (*ct)[L::CR * FCP] = S.ct;
+    const uint32_t *lut = S.lut;
+    // ---- column edges (filter_plane_cols, vp9lpf.c:31-104): one lane per pixel row ----
+    for (int tid = lane; tid < 64 + 2 * CH; tid += NT) {
+        if (tid < 64) {
+            lf_line_row_wide<PIX>((uint32_t *) (lt + (tid + 8) * FLP + XO), S.prog + (LFP_YC + (tid >> 3) * 16) / 4, lut, bd);
+        } else {
+            const int p = 1 + (tid - 64 >= CH), r = tid - 64 - (p - 1) * CH;
+            uint32_t *rowp = (uint32_t *) (ct[p - 1] + (r + 8) * FCP + XO);
+            const uint32_t *pw = S.prog + (LFP_CC + (r >> 3) * LFP_CSTRIDE(G::SH)) / 4;
+            if (G::SH) lf_line_row_narrow<PIX>(rowp, pw, lut, bd);
+            else lf_line_row_wide<PIX>(rowp, pw, lut, bd);
+        }
+    }
+    LF_SYNC();
+    // ---- row edges (filter_plane_rows, vp9lpf.c:106-181): one lane per pixel column ----
+    for (int tid = lane; tid < 64 + 2 * CW; tid += NT) {
+        if (tid < 64) {
+            lf_line_col_wide<PIX, FLP>(lt + XL + tid, S.prog + (LFP_YR + (tid >> 3) * 16) / 4, lut, bd);
+        } else {
+            const int p = 1 + (tid - 64 >= CW), c = tid - 64 - (p - 1) * CW;
+            PIX *colp = ct[p - 1] + XL + c;
+            const uint32_t *pw = S.prog + (LFP_CR(G::SH, G::SV) + (c >> 3) * LFP_CSTRIDE(G::SV)) / 4;
+            if (G::SV) lf_line_col_narrow<PIX, FCP>(colp, pw, lut, bd);
+            else lf_line_col_wide<PIX, FCP>(colp, pw, lut, bd);
+        }
+    }
+    LF_SYNC();
+#undef LF_SYNC
+}
+
 template <typename PIX, class G, int NT>
 DEV void lf_sb(const LFRec &rec, const FrameDesc *__restrict__ frames, LfLds<PIX, G> &S, int lane, int dbg)
 {
@@ -1242,34 +1283,7 @@ DEV void lf_sb(const LFRec &rec, const FrameDesc *__restrict__ frames, LfLds<PIX
     }
     LF_SYNC();
 
-    if (!(dbg & 1)) {
-    // ---- column edges (filter_plane_cols, vp9lpf.c:31-104): one lane per pixel row ----
-    for (int tid = lane; tid < 64 + 2 * CH; tid += NT) {
-        if (tid < 64) {
-            lf_line_row_wide<PIX>((uint32_t *) (lt + (tid + 8) * FLP + XO), S.prog + (LFP_YC + (tid >> 3) * 16) / 4, lut, bd);
-        } else {
-            const int p = 1 + (tid - 64 >= CH), r = tid - 64 - (p - 1) * CH;
-            uint32_t *rowp = (uint32_t *) (ct[p - 1] + (r + 8) * FCP + XO);
-            const uint32_t *pw = S.prog + (LFP_CC + (r >> 3) * LFP_CSTRIDE(G::SH)) / 4;
-            if (G::SH) lf_line_row_narrow<PIX>(rowp, pw, lut, bd);
-            else lf_line_row_wide<PIX>(rowp, pw, lut, bd);
-        }
-    }
-    LF_SYNC();
-    // ---- row edges (filter_plane_rows, vp9lpf.c:106-181): one lane per pixel column ----
-    for (int tid = lane; tid < 64 + 2 * CW; tid += NT) {
-        if (tid < 64) {
-            lf_line_col_wide<PIX, FLP>(lt + XL + tid, S.prog + (LFP_YR + (tid >> 3) * 16) / 4, lut, bd);
-        } else {
-            const int p = 1 + (tid - 64 >= CW), c = tid - 64 - (p - 1) * CW;
-            PIX *colp = ct[p - 1] + XL + c;
-            const uint32_t *pw = S.prog + (LFP_CR(G::SH, G::SV) + (c >> 3) * LFP_CSTRIDE(G::SV)) / 4;
-            if (G::SV) lf_line_col_narrow<PIX, FCP>(colp, pw, lut, bd);
-            else lf_line_col_wide<PIX, FCP>(colp, pw, lut, bd);
-        }
-    }
-    LF_SYNC();
-    }
+    if (!(dbg & 1)) lf_passes<PIX, G, NT>(S, lane, bd);
     // ---- store the modified region: rows [0,h) x cols [-8,w) and rows [-8,0) x cols [0,w).
     // Other SBs of the same wavefront step never touch this region, so whole chunks are
     // written back (pixels beyond the 8-aligned frame size are unchanged padding). ----
@@ -1296,6 +1310,197 @@ __global__ __launch_bounds__(LfNT<G>::NT) void k_lf(const uint32_t *__restrict__
 {
     __shared__ LfLds<PIX, G> S;
     lf_sb<PIX, G, LfNT<G>::NT>(recs[list[blockIdx.x]], frames, S, threadIdx.x, dbg);
+}
+
+// ------------------------------------------------------------- k_lfr
+// Row-pipelined loop filter: one workgroup filters one SB row of one frame, SB by SB left to
+// right (the raster SB order of ff_vp9_loopfilter_sb's callers, vp9.c:1522-1551 /
+// vp9lpf.c:183-230), instead of one launch per x + 2y wavefront diagonal.
+// - The left halo (x = -XL..-1) of SB c is the previous SB's right columns, already final
+//   for this row and still in LDS: copied within LDS, never re-read from HBM.
+// - The top halo (y = -8..-1) is the bottom of SB row r - 1, finished by another workgroup
+//   of this launch. SB (r, c) needs row r - 1 through SB c + 1 (whose left-edge column
+//   filtering rewrites x = 64c + 57..63 of that row), i.e. progress[r - 1] >= c + 2.
+//   Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, Valid forms row 1): every
+//   byte of the bottom 8 rows is stored sc1 (write-through) and drained by every storing
+//   wave before the barrier and ONE lane's sc1 progress store; the consumer polls with sc1
+//   loads and loads those rows only with sc1 loads. Every other load reads bytes written by
+//   earlier launches, or by this launch only after the load (row r + 1 rewrites row r's
+//   bottom rows once row r has published them).
+// - Workgroups take their task (frame, SB row) from a ticket counter in the order they
+//   start, and tasks are numbered rows-major, so a workgroup waits only on tasks already
+//   held by running workgroups: no assumption about dispatch order or XCD placement.
+//   Spins are bounded (timeout word ctr[2]). The last workgroup to finish zeroes the
+//   counters for the next launch (graph replay).
+// A task may start at SB column c0 > 0 (the SBs left of it filtered by earlier diagonal
+// launches: the k_plf launches of the same phase); its first left halo then comes from HBM.
+// progress[] holds absolute SB columns + 1; a dep task starting at c0' has SBs < c0' done.
+// Task table (lists): tasks[k] = offset of task k's record {dep task or ~0u, ncols, c0,
+// dep's c0, LFRec index of SB c0 .. ncols - 1}. ctr: {ticket, done, timeouts, 0,
+// progress[ntasks]}.
+typedef __attribute__((address_space(1))) uint64_t gu64;
+typedef __attribute__((address_space(1))) uint32_t gu32;
+DEV uint64_t ld_sc1(const void *p) { return __hip_atomic_load((gu64 *) p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+DEV void st_sc1(void *p, uint64_t v) { __hip_atomic_store((gu64 *) p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+// k_lfr pieces: chunk (p, r, k) of SB (sbx, sby) in its plane. Plane bases are offsets from
+// plane 0 chosen by selects (an indexed array of pointers would live in scratch).
+struct LfrPlanes {
+    uint64_t b0, d1, d2;
+    int pit0, pit1;
+};
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) v4u gv4u;        // global_ (not flat_) loads / stores
+template <typename PIX, class G> DEV PIX *lfr_addr(const LfrPlanes &P, int sbx, int sby, int p, int r, int k)
+{
+    typedef LfP<PIX, G> L;
+    const int gx = (p ? sbx * G::CW : sbx * 64) - L::XL + L::CPX * k, gy = (p ? sby * G::CH : sby * 64) - 8 + r;
+    const uint64_t a = P.b0 + (p == 1 ? P.d1 : 0) + (p == 2 ? P.d2 : 0);
+    return (PIX *) a + (ptrdiff_t) gy * (p ? P.pit1 : P.pit0) + gx;
+}
+// issue the plain loads of SB (sbx, sby)'s interior chunks (and its left halo from HBM when
+// `halo`), all in flight before any use
+template <typename PIX, class G, int NT, int NU>
+DEV void lfr_issue(Chunk16::T (&v)[NU], const LfrPlanes &P, int sbx, int sby, int lane, bool halo)
+{
+    typedef LfP<PIX, G> L;
+#pragma unroll
+    for (int u = 0; u < NU; u++) {
+        const int ci = lane + u * NT;
+        int p, r, k;
+        lf_chunk<PIX, G>(ci, p, r, k);
+        if (ci < L::NCHUNK && r >= 8 && (k > 0 || halo)) {
+            const v4u x = *(const gv4u *) lfr_addr<PIX, G>(P, sbx, sby, p, r, k);
+            v[u] = make_uint4(x.x, x.y, x.z, x.w);
+        }
+    }
+}
+
+// PF: the next SB's interior loads are issued before this SB's filtering (in registers)
+template <typename PIX, class G, bool PF>
+__global__ __launch_bounds__(LfNT<G>::NT) void k_lfr(const uint32_t *__restrict__ tasks, const LFRec *__restrict__ recs,
+                                                     const FrameDesc *__restrict__ frames, uint32_t *ctr, int ntasks)
+{
+    constexpr int NT = LfNT<G>::NT;
+    typedef LfP<PIX, G> L;
+    typedef Chunk16::T CT;
+    constexpr int FLP = L::YP, FCP = L::UVP, CW = G::CW, CPX = L::CPX;
+    constexpr int NU = (L::NCHUNK + NT - 1) / NT;
+    __shared__ LfLds<PIX, G> S;
+    __shared__ uint32_t s_task, s_last;
+    const int lane = threadIdx.x;
+    uint32_t *const progress = ctr + 4;
+    // the row chain is the latency path of the phase: its waves issue first on their SIMDs
+    __builtin_amdgcn_s_setprio(3);
+    if (lane == 0) s_task = atomicAdd(&ctr[0], 1u);
+    __syncthreads();
+    const uint32_t *T = tasks + tasks[s_task];
+    const uint32_t dep = T[0], ncols = T[1], c0 = T[2];
+    uint32_t seen = T[3];                                  // lane 0: dep's columns known done
+    const LFRec &rec0 = recs[T[4]];
+    const FrameDesc &fd = frames[rec0.frame];
+    const int bd = fd.bd, sby = rec0.sby;
+    LfrPlanes P;
+    P.b0 = fd.plane[0]; P.d1 = fd.plane[1] - P.b0; P.d2 = fd.plane[2] - P.b0;
+    P.pit0 = fd.pitch[0]; P.pit1 = fd.pitch[1];
+    for (int i = lane; i < 64; i += NT) S.lut[i] = lf_eih(i, fd.sharp, bd);
+    CT v[NU];
+#pragma unroll
+    for (int u = 0; u < NU; u++) v[u] = Chunk16::zero();
+    lfr_issue<PIX, G, NT, NU>(v, P, c0, sby, lane, c0 > 0);
+    for (uint32_t c = c0; c < ncols; c++) {
+        const int sbx = (int) c;
+        const LFRec &rec = recs[T[4 + c - c0]];
+        if (!PF && c > c0) lfr_issue<PIX, G, NT, NU>(v, P, sbx, sby, lane, false);
+        // left halo (x < 0): this workgroup's previous tile, read from LDS before the barrier
+        // below (SB c0's came from HBM with its interior)
+        if (c > c0) {
+#pragma unroll
+            for (int u = 0; u < NU; u++) {
+                const int ci = lane + u * NT;
+                int p, r, k;
+                lf_chunk<PIX, G>(ci, p, r, k);
+                if (ci < L::NCHUNK && r >= 8 && k == 0) {
+                    const PIX *t = p ? S.ct[p - 1] + r * FCP : S.lt + r * FLP;
+                    v[u] = Chunk16::from_lds(t + (p ? CW : 64));          // x = 64 - XL .. 63 (CW for chroma)
+                }
+            }
+        }
+        if (lane == 0 && dep != ~0u) {
+            const uint32_t need = c + 2 < ncols ? c + 2 : ncols;
+            for (uint32_t n = 0; seen < need; n++) {
+                seen = __hip_atomic_load((gu32 *) &progress[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (seen >= need) break;
+                if (n > (1u << 22)) { atomicAdd(&ctr[2], 1u); seen = need; break; }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        __syncthreads();
+        // top halo (y = -8..-1, x >= 0): rows row r - 1 handed off, sc1 loads only
+#pragma unroll
+        for (int u = 0; u < NU; u++) {
+            const int ci = lane + u * NT;
+            int p, r, k;
+            lf_chunk<PIX, G>(ci, p, r, k);
+            if (ci >= L::NCHUNK || r >= 8 || k == 0 || sby == 0) continue;
+            const PIX *g = lfr_addr<PIX, G>(P, sbx, sby, p, r, k);
+            const uint64_t lo = ld_sc1(g), hi = ld_sc1((const char *) g + 8);
+            v[u] = make_uint4((uint32_t) lo, (uint32_t) (lo >> 32), (uint32_t) hi, (uint32_t) (hi >> 32));
+        }
+        for (int i = lane; i < L::PROG / 4; i += NT) S.prog[i] = ((const uint32_t *) rec.prog)[i];
+#pragma unroll
+        for (int u = 0; u < NU; u++) {
+            const int ci = lane + u * NT;
+            int p, r, k;
+            lf_chunk<PIX, G>(ci, p, r, k);
+            if (ci < L::NCHUNK && (r >= 8 || k > 0)) {
+                PIX *t = p ? S.ct[p - 1] + r * FCP : S.lt + r * FLP;
+                Chunk16::to_lds(v[u], t + CPX * k);
+            }
+        }
+        __syncthreads();
+        // the next SB's interior loads run under this SB's filtering
+        if (PF && c + 1 < ncols) lfr_issue<PIX, G, NT, NU>(v, P, sbx + 1, sby, lane, false);
+        lf_passes<PIX, G, NT>(S, lane, bd);
+        // the bottom 8 rows (handed to row r + 1) first: sc1 stores, drained by every wave,
+        // then the progress word; the rest of rows [0, h) x cols [-XL, w) and rows [-8, 0) x
+        // cols [0, w) after it
+#pragma unroll
+        for (int u = 0; u < NU; u++) {
+            const int ci = lane + u * NT;
+            int p, r, k;
+            lf_chunk<PIX, G>(ci, p, r, k);
+            if (ci >= L::NCHUNK || r < (p ? L::CR : 72) - 8 || (k == 0 && sbx == 0)) continue;
+            const PIX *t = p ? S.ct[p - 1] + r * FCP : S.lt + r * FLP;
+            PIX *g = lfr_addr<PIX, G>(P, sbx, sby, p, r, k);
+            const CT w = Chunk16::from_lds(t + CPX * k);
+            st_sc1(g, (uint64_t) w.x | (uint64_t) w.y << 32);
+            st_sc1((char *) g + 8, (uint64_t) w.z | (uint64_t) w.w << 32);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (lane == 0) __hip_atomic_store((gu32 *) &progress[s_task], c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int u = 0; u < NU; u++) {
+            const int ci = lane + u * NT;
+            int p, r, k;
+            lf_chunk<PIX, G>(ci, p, r, k);
+            if (ci >= L::NCHUNK || r >= (p ? L::CR : 72) - 8 || (k == 0 && (sbx == 0 || r < 8)) || (r < 8 && sby == 0))
+                continue;
+            const PIX *t = p ? S.ct[p - 1] + r * FCP : S.lt + r * FLP;
+            const CT w = Chunk16::from_lds(t + CPX * k);
+            v4u x; x.x = w.x; x.y = w.y; x.z = w.z; x.w = w.w;
+            *(gv4u *) lfr_addr<PIX, G>(P, sbx, sby, p, r, k) = x;
+        }
+    }
+    // the last workgroup to finish resets the counters (every ticket is taken by then)
+    if (lane == 0) s_last = atomicAdd(&ctr[1], 1u) == (uint32_t) ntasks - 1;
+    __syncthreads();
+    if (s_last) {
+        for (int i = lane; i < ntasks; i += NT) progress[i] = 0;
+        if (lane == 0) { ctr[0] = 0; ctr[1] = 0; }
+    }
 }
 
 // Residual arithmetic types per pixel type: 8-bit int16 coefficients / 32-bit math,
@@ -1457,6 +1662,24 @@ static void launch_lf_g(hipStream_t st, int nsb, const uint32_t *list, const LFR
 {
     hipLaunchKernelGGL((k_lf<PIX, G>), dim3(nsb), dim3(LfNT<G>::NT), 0, st, list, recs, frames, dbg);
 }
+template <typename PIX, class G>
+static void launch_lfr_g(hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs, const FrameDesc *frames, uint32_t *ctr)
+{
+    static const bool pf = getenv("VP9HIP_LFR_PF") && atoi(getenv("VP9HIP_LFR_PF"));
+    if (pf) hipLaunchKernelGGL((k_lfr<PIX, G, true>), dim3(ntasks), dim3(LfNT<G>::NT), 0, st, tasks, recs, frames, ctr, ntasks);
+    else    hipLaunchKernelGGL((k_lfr<PIX, G, false>), dim3(ntasks), dim3(LfNT<G>::NT), 0, st, tasks, recs, frames, ctr, ntasks);
+}
+template <typename PIX>
+static void launch_lfr_p(int ss, hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs, const FrameDesc *frames,
+                         uint32_t *ctr)
+{
+    switch (ss) {
+    case 3: launch_lfr_g<PIX, Geo<1, 1>>(st, ntasks, tasks, recs, frames, ctr); break;
+    case 1: launch_lfr_g<PIX, Geo<1, 0>>(st, ntasks, tasks, recs, frames, ctr); break;
+    case 2: launch_lfr_g<PIX, Geo<0, 1>>(st, ntasks, tasks, recs, frames, ctr); break;
+    default: launch_lfr_g<PIX, Geo<0, 0>>(st, ntasks, tasks, recs, frames, ctr); break;
+    }
+}
 template <typename PIX>
 static void launch_lf_p(int ss, hipStream_t st, int nsb, const uint32_t *list, const LFRec *recs, const FrameDesc *frames,
                         int dbg)
@@ -1526,6 +1749,14 @@ int vp9hip_launch_lf(int fmt, hipStream_t st, int nsb, const uint32_t *list, con
     if (nsb <= 0) return 0;
     if (fmt & 1) launch_lf_p<uint16_t>(fmt >> 1, st, nsb, list, recs, frames, dbg);
     else         launch_lf_p<uint8_t>(fmt >> 1, st, nsb, list, recs, frames, dbg);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int vp9hip_launch_lfr(int fmt, hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs,
+                      const FrameDesc *frames, uint32_t *ctr)
+{
+    if (ntasks <= 0) return 0;
+    if (fmt & 1) launch_lfr_p<uint16_t>(fmt >> 1, st, ntasks, tasks, recs, frames, ctr);
+    else         launch_lfr_p<uint8_t>(fmt >> 1, st, ntasks, tasks, recs, frames, ctr);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int vp9hip_launch_plf(int fmt, hipStream_t st, const PlfLaunch *pl, const uint32_t *plist, const uint32_t *llist,

@@ -45,6 +45,8 @@ int vp9hip_launch_pred(int fmt, hipStream_t st, int nwg, const uint32_t *list, c
 int vp9hip_launch_lf(int fmt, hipStream_t st, int nsb, const uint32_t *list, const LFRec *recs,
                      const FrameDesc *frames, int dbg);
 int vp9hip_launch_mc(int hb, hipStream_t st, int n, const McUnit *units, const FrameDesc *frames);
+int vp9hip_launch_lfr(int fmt, hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs,
+                      const FrameDesc *frames, uint32_t *ctr);
 int vp9hip_launch_plf(int fmt, hipStream_t st, const PlfLaunch *pl, const uint32_t *plist, const uint32_t *llist,
                       const WGRec *wgs, const SBRec *sbs, const PJob *jobs, const uint32_t *passes, const LFRec *recs,
                       const RJob *rjobs, const FrameDesc *frames, const void *coefs, int16_t *resid, const uint32_t *ptab,
@@ -53,15 +55,16 @@ int vp9hip_launch_plf(int fmt, hipStream_t st, const PlfLaunch *pl, const uint32
 
 namespace {
 
-enum { K_MC, K_RESID, K_PRED, K_LF, K_PLF, K_N };
-const char *const kname[K_N] = { "k_mc", "k_resid", "k_pred", "k_lf", "k_plf" };
+enum { K_MC, K_RESID, K_PRED, K_LF, K_PLF, K_LFR, K_N };
+const char *const kname[K_N] = { "k_mc", "k_resid", "k_pred", "k_lf", "k_plf", "k_lfr" };
 
 // ff_vp9_intra_txfm_type (vp9data.c:437-452)
 const uint8_t intra_txfm_type[14] = { 2, 1, 0, 0, 3, 2, 1, 2, 1, 3, 0, 0, 0, 0 };
 
 // step: wavefront diagonal of a K_PRED (x_in_tile + y) or K_LF (x + 2y) launch; K_PLF
 // (intra diagonal `step` + LF diagonal step - PLF_LAG in one launch): off / n the intra
-// workgroups, off2 / n2 the LF SBs
+// workgroups, off2 / n2 the LF SBs; K_LFR (row-pipelined loop filter of a phase): off / n
+// its task table, arg its counter block (uint32 index into the arena's counter words)
 struct Launch { int kind; uint32_t off; uint32_t n; int arg; int grp; int ph; int part; int step;
                 uint32_t off2 = 0, n2 = 0;
                 uint32_t roff[5] = { 0, 0, 0, 0, 0 }, rn[5] = { 0, 0, 0, 0, 0 };   // K_PLF residual jobs by tx code
@@ -71,6 +74,11 @@ struct Launch { int kind; uint32_t off; uint32_t n; int arg; int grp; int ph; in
 // frames than this; wide phases (keyframe batches) keep their separate k_resid launches:
 // measured C2 +6.5 % fused, C3 -2 %, C4 -8 %
 #define RES_FUSE_MAX_FRAMES 8
+// The loop filter of phases of fewer frames than this runs as one row-pipelined k_lfr launch
+// (its tail after the fused diagonals); wide phases keep diagonal launches: measured C2
+// +8-10 %, C3 -6 % with k_lfr everywhere (its long-lived workgroups crowd the other groups'
+// intra wavefronts)
+#define LFR_MAX_FRAMES 8
 enum { PART_RECON, PART_LF };           // a phase's reconstruction launches, then its loop filter
 #define MAX_GROUPS 8                    // independent frame groups = concurrent launch chains
 #define LF_LAG 2                        // LF diagonal j needs intra diagonals <= j + LF_LAG (see enqueue_batch)
@@ -103,16 +111,17 @@ struct Staged {
     std::vector<int> frame_log2;        // log2 tile columns of each batch frame
     int tile_lo = 0, tile_hi = 64;      // tile columns this context reconstructs (sharded batches)
     std::vector<uint8_t> coefs;         // concatenated coefficient streams (bytes)
-    double alg_bytes[K_N] = { 0, 0, 0, 0, 0 };
+    double alg_bytes[K_N] = {};
     // record counts of the arena (the host images above are not kept for these)
     uint32_t n_sbs = 0, n_pjobs = 0, n_passes = 0, n_wgs = 0, n_rjobs = 0, n_lfs = 0, n_mcs = 0;
+    uint32_t n_ctr = 0;                 // k_lfr counter words (zero between launches)
     uint8_t *pinned = nullptr;          // pinned host image of the arena (one DMA per stage)
     size_t pinned_cap = 0;
     // device arena
     uint8_t *arena = nullptr;
     size_t arena_cap = 0;
     size_t o_frames = 0, o_sbs = 0, o_pjobs = 0, o_passes = 0, o_wgs = 0, o_rjobs = 0, o_lfs = 0, o_mcs = 0, o_lists = 0,
-           o_coefs = 0;
+           o_coefs = 0, o_ctr = 0;
     int16_t *resid = nullptr;           // intra residual scratch (column-major n x n blocks)
     size_t resid_cap = 0;               // bytes
     bool ready = false;
@@ -132,6 +141,8 @@ struct vp9hip_ctx {
     int max_groups = 3;                 // VP9HIP_STREAMS overrides (1..8); 3 measured best at C3, with even chain splits
     bool lf_overlap = false;            // VP9HIP_LF_OVERLAP=1: LF on a second stream per group (measured slower)
     bool fuse_plf = true;               // VP9HIP_PLF=0: no fused intra + LF launches
+    int lf_rows = 1;                    // VP9HIP_LFROW: 0 LF as diagonal launches only, 1 k_lfr for
+                                        // narrow phases (LFR_MAX_FRAMES), 2 k_lfr for every phase
     int w = 0, h = 0, bpp = 8, ss_h = 1, ss_v = 1, hb = 0, bypp = 1;
     int cols = 0, rows = 0, sb_cols = 0, sb_rows = 0;
     int pitch[2] = { 0, 0 };
@@ -146,8 +157,8 @@ struct vp9hip_ctx {
     bool timing = true;
     std::vector<hipEvent_t> ev;
     bool timed_run = false;             // the last run recorded per-launch events
-    double kms[K_N] = { 0, 0, 0, 0, 0 };
-    int kcount[K_N] = { 0, 0, 0, 0, 0 };
+    double kms[K_N] = {};
+    int kcount[K_N] = {};
 };
 
 #define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
@@ -165,6 +176,7 @@ extern "C" int vp9hip_open(int device, vp9hip_ctx **out)
     if (const char *g = getenv("VP9HIP_STREAMS")) c->max_groups = std::max(1, std::min(MAX_GROUPS, atoi(g)));
     if (const char *g = getenv("VP9HIP_LF_OVERLAP")) c->lf_overlap = atoi(g) != 0;
     if (const char *g = getenv("VP9HIP_PLF")) c->fuse_plf = atoi(g) != 0;
+    if (const char *g = getenv("VP9HIP_LFROW")) c->lf_rows = atoi(g);
     bool ok = hipSetDevice(device) == hipSuccess && hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) == hipSuccess;
     for (int i = 0; ok && i < MAX_GROUPS; i++)
@@ -1024,6 +1036,9 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     // fused intra + LF launches need the LF of a phase in the same launch sequence as its
     // reconstruction (not for tile-sharded batches: recon, exchange, then LF)
     const bool fuse = c->fuse_plf && !tiled;
+    // the loop filter of a phase as one row-pipelined k_lfr launch (after the phase's
+    // reconstruction) instead of x + 2y diagonal launches
+    const bool lfr_any = c->lf_rows > 0 && !tiled;
     // VP9HIP_STAGE_TRACE=1: host time of the staging steps on stderr
     static const bool stage_trace = getenv("VP9HIP_STAGE_TRACE") && atoi(getenv("VP9HIP_STAGE_TRACE"));
     double st_ms[6] = { 0, 0, 0, 0, 0, 0 };
@@ -1040,7 +1055,7 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     s.wgs.clear(); s.sbh.clear(); s.sbjobs.clear(); s.jdep0.clear(); s.jdeps.clear();
     s.rjobs.clear(); s.resid16 = 0;
     s.rbucket.clear();
-    s.lists.clear(); s.launches.clear(); s.coefs.clear();
+    s.lists.clear(); s.launches.clear(); s.coefs.clear(); s.n_ctr = 0;
     s.frame_phase.assign(n, 0); s.frame_log2.assign(n, 0);
     s.tile_lo = tile_lo; s.tile_hi = tile_hi;
     for (int k = 0; k < K_N; k++) s.alg_bytes[k] = 0;
@@ -1273,9 +1288,69 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
                 s.lists.insert(s.lists.end(), v.begin(), v.end());
             };
             const std::vector<std::vector<uint32_t>> &wls = wsteps[ph];   // one workgroup per SB
+            const bool lfr = lfr_any && (c->lf_rows > 1 || (int) phase_frames[ph].size() < LFR_MAX_FRAMES);
+            // k_lfr task table of the phase: one task per (frame, SB row), rows-major, each
+            // naming the task of the row above (dep) and its SBs' LF records left to right
+            // j0: LF diagonals x + 2y < j0 ran in earlier (fused) launches
+            auto add_lfr = [&](int j0) {
+                std::vector<std::vector<std::vector<uint32_t>>> grid;      // per frame: [row][col]
+                int maxr = 0;
+                for (int i : phase_frames[ph]) {
+                    const std::vector<LFRec> &lf = plans[i].s.lfs;
+                    if (lf.empty()) continue;
+                    int nr = 0, nc = 0;
+                    for (const LFRec &r : lf) { nr = std::max(nr, r.sby + 1); nc = std::max(nc, r.sbx + 1); }
+                    std::vector<std::vector<uint32_t>> gr(nr, std::vector<uint32_t>(nc, ~0u));
+                    for (size_t k = 0; k < lf.size(); k++) gr[lf[k].sby][lf[k].sbx] = off[i].lf + (uint32_t) k;
+                    for (auto &row : gr)
+                        for (uint32_t v : row)
+                            if (v == ~0u) return VP9HIP_EINVALIDDATA;
+                    grid.push_back(std::move(gr));
+                    maxr = std::max(maxr, nr);
+                }
+                if (grid.empty()) return 0;
+                std::vector<std::vector<uint32_t>> tid(grid.size());   // task of (frame, row) or ~0u
+                std::vector<uint32_t> recs;
+                std::vector<uint32_t> offs;
+                auto start = [&](int r) { return std::max(0, j0 - 2 * r); };
+                for (int r = 0; r < maxr; r++)
+                    for (size_t f = 0; f < grid.size(); f++) {
+                        if (r >= (int) grid[f].size()) continue;
+                        const int nc = (int) grid[f][r].size(), c0 = start(r);
+                        if (c0 >= nc) { tid[f].push_back(~0u); continue; }
+                        tid[f].push_back((uint32_t) offs.size());
+                        offs.push_back((uint32_t) recs.size());
+                        const uint32_t dep = r ? tid[f][r - 1] : ~0u;
+                        recs.push_back(dep);
+                        recs.push_back((uint32_t) nc);
+                        recs.push_back((uint32_t) c0);
+                        recs.push_back(dep != ~0u ? (uint32_t) start(r - 1) : 0u);
+                        recs.insert(recs.end(), grid[f][r].begin() + c0, grid[f][r].end());
+                    }
+                if (offs.empty()) return 0;
+                const uint32_t nt = (uint32_t) offs.size();
+                Launch L = { K_LFR, (uint32_t) s.lists.size(), nt, (int) s.n_ctr, g, ph, PART_LF, 0 };
+                for (uint32_t &o : offs) o += nt;
+                s.lists.insert(s.lists.end(), offs.begin(), offs.end());
+                s.lists.insert(s.lists.end(), recs.begin(), recs.end());
+                s.n_ctr += 4 + nt;
+                s.launches.push_back(L);
+                for (int i : phase_frames[ph])
+                    for (size_t k = 0; k < plans[i].s.lfs.size(); k++) {
+                        const LFRec &r = plans[i].s.lfs[k];
+                        if (r.sbx + 2 * r.sby < j0) continue;
+                        s.alg_bytes[K_LF] -= lf_bytes[off[i].lf + k];
+                        s.alg_bytes[K_LFR] += lf_bytes[off[i].lf + k];
+                    }
+                return 0;
+            };
             if (!fuse) {
                 for (size_t d = 0; d < wls.size(); d++) add_list(K_PRED, wls[d], (int) d);
-                for (size_t d = 0; d < lsteps[ph].size(); d++) add_list(K_LF, lsteps[ph][d], (int) d);
+                if (lfr) {
+                    if (int e = add_lfr(0)) return e;
+                } else {
+                    for (size_t d = 0; d < lsteps[ph].size(); d++) add_list(K_LF, lsteps[ph][d], (int) d);
+                }
                 continue;
             }
             // Fused schedule: launch t runs intra diagonal t and LF diagonal t - PLF_LAG.
@@ -1289,8 +1364,12 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
             // The residuals of intra diagonal t + 1 (inverse transforms, incl. inter
             // residuals added onto the MC prediction) run in launch t too, so no separate
             // residual pass precedes the wavefront: launch -1 holds diagonal 0's alone.
-            const int np = (int) wls.size(), nlf = (int) lsteps[ph].size();
+            const int np = (int) wls.size();
             const int nres = res_fused[ph] ? (int) rj_range[ph].size() : 0;
+            // with k_lfr, LF diagonals fuse into the launches the intra wavefront needs anyway
+            // and k_lfr filters the rest
+            const int jlfr = std::max(0, std::max(np, nres - 1) - PLF_LAG);
+            const int nlf = lfr ? std::min(jlfr, (int) lsteps[ph].size()) : (int) lsteps[ph].size();
             const int nt = std::max(std::max(np, nlf ? nlf + PLF_LAG : 0), nres - 1);
             for (int t = -1; t < nt; t++) {
                 const std::vector<uint32_t> *pv = t >= 0 && t < np && !wls[t].empty() ? &wls[t] : nullptr;
@@ -1318,6 +1397,8 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
                 for (int k = 0; res && k < 5; k++) { L.roff[k] = (*rr)[k].first; L.rn[k] = (*rr)[k].second; }
                 s.launches.push_back(L);
             }
+            if (lfr)
+                if (int e = add_lfr(nlf)) return e;
         }
     if (s.resid16 > 0xffffffffull) return VP9HIP_ENOMEM;
 
@@ -1335,6 +1416,7 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     s.o_lfs = o; o = al(o + (size_t) tot.lf * sizeof(LFRec));
     s.o_mcs = o; o = al(o + (size_t) tot.mc * sizeof(McUnit));
     s.o_lists = o; o = al(o + s.lists.size() * sizeof(uint32_t));
+    s.o_ctr = o; o = al(o + (size_t) s.n_ctr * sizeof(uint32_t));
     s.o_coefs = o; o = al(o + coef_off[n] + 64);
     s.n_sbs = tot.sb; s.n_pjobs = tot.job; s.n_passes = tot.pass; s.n_wgs = tot.wg; s.n_rjobs = tot_rj;
     s.n_lfs = tot.lf; s.n_mcs = tot.mc;
@@ -1363,6 +1445,7 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     uint8_t *img = s.pinned;
     memcpy(img + s.o_frames, s.frames.data(), s.frames.size() * sizeof(FrameDesc));
     if (!s.lists.empty()) memcpy(img + s.o_lists, s.lists.data(), s.lists.size() * sizeof(uint32_t));
+    memset(img + s.o_ctr, 0, (size_t) s.n_ctr * sizeof(uint32_t));
     std::vector<double> inplace_bytes(n, 0.0);
     {
         std::atomic<int> next(0);
@@ -1481,6 +1564,9 @@ static int launch_one(vp9hip_ctx *c, const Launch &L, hipStream_t st)
         return vp9hip_launch_pred(c->hb | c->ss_h << 1 | c->ss_v << 2, st, (int) L.n, lists + L.off, (const WGRec *) (s.arena + s.o_wgs),
                                   (const SBRec *) (s.arena + s.o_sbs), (const PJob *) (s.arena + s.o_pjobs),
                                   (const uint32_t *) (s.arena + s.o_passes), fr, s.resid, c->ptab, c->dbg);
+    case K_LFR:
+        return vp9hip_launch_lfr(c->hb | c->ss_h << 1 | c->ss_v << 2, st, (int) L.n, lists + L.off,
+                                 (const LFRec *) (s.arena + s.o_lfs), fr, (uint32_t *) (s.arena + s.o_ctr) + L.arg);
     case K_LF:
         return vp9hip_launch_lf(c->hb | c->ss_h << 1 | c->ss_v << 2, st, (int) L.n, lists + L.off, (const LFRec *) (s.arena + s.o_lfs), fr, c->dbg >> 16);
     case K_PLF: {

@@ -215,3 +215,41 @@ def test_zero_copy_export_matches_download(v9, orc, gpu, bpp):
     for t, r in zip(views, v9.visible(ref, w, h)):
         assert t.shape == r.shape
         assert np.array_equal(t.cpu().numpy().astype(r.dtype), r)
+
+
+@pytest.mark.parametrize("mode,bpp", [("0", 8), ("2", 8), ("2", 10), ("1", 10)])
+def test_loop_filter_schedules(v9, orc, monkeypatch, mode, bpp):
+    """Both loop-filter schedules (vp9lpf.c:183-230 in raster SB order): VP9HIP_LFROW=0 runs
+    x + 2y diagonal launches only; 2 runs the row-pipelined k_lfr for every phase (its rows
+    start after the diagonals fused with the intra wavefront, workgroups hand the bottom SB
+    rows to the next row through sc1 stores / loads); 1 (default) k_lfr for narrow phases.
+    A wide keyframe batch and a narrow GOP, several SB rows and columns, 2 tile columns."""
+    monkeypatch.setenv("VP9HIP_LFROW", mode)
+    dev = v9.Device(0)
+    try:
+        w, h, n = 520, 300, 9
+        frames = [v9.SynthFrame(v9.synth_params(w, h, bpp, seed=500 + i, log2_tile_cols=1)) for i in range(n)]
+        dev.configure(w, h, bpp, nbufs=n)
+        dev.stage_batch(frames, list(range(n)))
+        for _ in range(2):      # graph replay: k_lfr counters reset by the launch itself
+            dev.run_batch()
+            dev.sync()
+        for i in (0, 4, 8):
+            ref = v9.alloc_planes(w, h, bpp)
+            orc.decode_frame(frames[i].pkt, ref)
+            _cmp(v9, dev.download(i), ref, w, h, "LFROW=%s keyframe batch frame %d" % (mode, i))
+        # key + 2 inter frames, one chain (phases of one frame)
+        key = v9.SynthFrame(v9.synth_params(w, h, bpp, seed=600))
+        p1 = v9.SynthFrame(v9.synth_params(w, h, bpp, seed=601, inter=1))
+        dev.configure(w, h, bpp, nbufs=2)
+        dev.submit(key, 0)
+        dev.submit(p1, 1, (0, 0, 0))
+        dev.sync()
+        r0 = v9.alloc_planes(w, h, bpp)
+        orc.decode_frame(key.pkt, r0)
+        r1 = v9.alloc_planes(w, h, bpp)
+        orc.decode_frame(p1.pkt, r1, [r0, r0, r0])
+        _cmp(v9, dev.download(0), r0, w, h, "LFROW=%s key" % mode)
+        _cmp(v9, dev.download(1), r1, w, h, "LFROW=%s inter" % mode)
+    finally:
+        dev.close()
