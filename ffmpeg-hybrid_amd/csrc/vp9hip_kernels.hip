@@ -1200,7 +1200,7 @@ DEV uint32_t lf_eih(int L, int sharp, int bd)
 
 // The filter passes of one SB over its LDS tile: all column edges of every plane (lanes =
 // pixel rows), then all row edges (lanes = pixel columns). Ends with a barrier.
-template <typename PIX, class G, int NT>
+template <typename PIX, class G, int NT, int PASSES = 3>
 DEV void lf_passes(LfLds<PIX, G> &S, int lane, int bd)
 {
 #define LF_SYNC() do { if (NT == 64) wave_sync(); else __syncthreads(); } while (0)
@@ -1211,6 +1211,7 @@ DEV void lf_passes(LfLds<PIX, G> &S, int lane, int bd)
     PIX (*ct)[L::CR * FCP] = S.ct;
     const uint32_t *lut = S.lut;
     // ---- column edges (filter_plane_cols, vp9lpf.c:31-104): one lane per pixel row ----
+    if (PASSES & 1) {
     for (int tid = lane; tid < 64 + 2 * CH; tid += NT) {
         if (tid < 64) {
             lf_line_row_wide<PIX>((uint32_t *) (lt + (tid + 8) * FLP + XO), S.prog + (LFP_YC + (tid >> 3) * 16) / 4, lut, bd);
@@ -1223,7 +1224,9 @@ DEV void lf_passes(LfLds<PIX, G> &S, int lane, int bd)
         }
     }
     LF_SYNC();
+    }
     // ---- row edges (filter_plane_rows, vp9lpf.c:106-181): one lane per pixel column ----
+    if (PASSES & 2) {
     for (int tid = lane; tid < 64 + 2 * CW; tid += NT) {
         if (tid < 64) {
             lf_line_col_wide<PIX, FLP>(lt + XL + tid, S.prog + (LFP_YR + (tid >> 3) * 16) / 4, lut, bd);
@@ -1236,6 +1239,7 @@ DEV void lf_passes(LfLds<PIX, G> &S, int lane, int bd)
         }
     }
     LF_SYNC();
+    }
 #undef LF_SYNC
 }
 
@@ -1320,7 +1324,10 @@ __global__ __launch_bounds__(LfNT<G>::NT) void k_lf(const uint32_t *__restrict__
 //   for this row and still in LDS: copied within LDS, never re-read from HBM.
 // - The top halo (y = -8..-1) is the bottom of SB row r - 1, finished by another workgroup
 //   of this launch. SB (r, c) needs row r - 1 through SB c + 1 (whose left-edge column
-//   filtering rewrites x = 64c + 57..63 of that row), i.e. progress[r - 1] >= c + 2.
+//   filtering rewrites x = 64c + 57..63 of that row). progress[r] = p says the bottom
+//   rows of SBs 0..p-1 are final: row r publishes p = c right after SB c's column pass
+//   (SB c - 1's last columns are then final and stored), before its row pass, and p = ncols
+//   after its last SB; SB (r + 1, c) waits for progress[r] >= c + 1.
 //   Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, Valid forms row 1): every
 //   byte of the bottom 8 rows is stored sc1 (write-through) and drained by every storing
 //   wave before the barrier and ONE lane's sc1 progress store; the consumer polls with sc1
@@ -1334,9 +1341,10 @@ __global__ __launch_bounds__(LfNT<G>::NT) void k_lf(const uint32_t *__restrict__
 //   counters for the next launch (graph replay).
 // A task may start at SB column c0 > 0 (the SBs left of it filtered by earlier diagonal
 // launches: the k_plf launches of the same phase); its first left halo then comes from HBM.
-// progress[] holds absolute SB columns + 1; a dep task starting at c0' has SBs < c0' done.
+// progress[] counts absolute SB columns; a dep task starting at c0' > 0 has the bottom rows
+// of SBs < c0' - 1 final before the launch.
 // Task table (lists): tasks[k] = offset of task k's record {dep task or ~0u, ncols, c0,
-// dep's c0, LFRec index of SB c0 .. ncols - 1}. ctr: {ticket, done, timeouts, 0,
+// dep's final columns at the start, LFRec index of SB c0 .. ncols - 1}. ctr: {ticket, done, timeouts, 0,
 // progress[ntasks]}.
 typedef __attribute__((address_space(1))) uint64_t gu64;
 typedef __attribute__((address_space(1))) uint32_t gu32;
@@ -1427,7 +1435,7 @@ __global__ __launch_bounds__(LfNT<G>::NT) void k_lfr(const uint32_t *__restrict_
             }
         }
         if (lane == 0 && dep != ~0u) {
-            const uint32_t need = c + 2 < ncols ? c + 2 : ncols;
+            const uint32_t need = c + 1;
             for (uint32_t n = 0; seen < need; n++) {
                 seen = __hip_atomic_load((gu32 *) &progress[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (seen >= need) break;
@@ -1462,36 +1470,54 @@ __global__ __launch_bounds__(LfNT<G>::NT) void k_lfr(const uint32_t *__restrict_
         __syncthreads();
         // the next SB's interior loads run under this SB's filtering
         if (PF && c + 1 < ncols) lfr_issue<PIX, G, NT, NU>(v, P, sbx + 1, sby, lane, false);
-        lf_passes<PIX, G, NT>(S, lane, bd);
-        // the bottom 8 rows (handed to row r + 1) first: sc1 stores, drained by every wave,
-        // then the progress word; the rest of rows [0, h) x cols [-XL, w) and rows [-8, 0) x
-        // cols [0, w) after it
+        lf_passes<PIX, G, NT, 1>(S, lane, bd);
+        // SB c - 1's bottom rows are final now (this SB's left-edge column filtering was the
+        // last to touch them): its last XL columns of them sc1, drained by every wave, then
+        // the progress word, ahead of this SB's row pass. Those bytes are not stored again.
+        if (sbx > 0) {
 #pragma unroll
-        for (int u = 0; u < NU; u++) {
-            const int ci = lane + u * NT;
-            int p, r, k;
-            lf_chunk<PIX, G>(ci, p, r, k);
-            if (ci >= L::NCHUNK || r < (p ? L::CR : 72) - 8 || (k == 0 && sbx == 0)) continue;
-            const PIX *t = p ? S.ct[p - 1] + r * FCP : S.lt + r * FLP;
-            PIX *g = lfr_addr<PIX, G>(P, sbx, sby, p, r, k);
-            const CT w = Chunk16::from_lds(t + CPX * k);
-            st_sc1(g, (uint64_t) w.x | (uint64_t) w.y << 32);
-            st_sc1((char *) g + 8, (uint64_t) w.z | (uint64_t) w.w << 32);
+            for (int u = 0; u < NU; u++) {
+                const int ci = lane + u * NT;
+                int p, r, k;
+                lf_chunk<PIX, G>(ci, p, r, k);
+                if (ci >= L::NCHUNK || r < (p ? L::CR : 72) - 8 || k != 0) continue;
+                const PIX *t = p ? S.ct[p - 1] + r * FCP : S.lt + r * FLP;
+                PIX *g = lfr_addr<PIX, G>(P, sbx, sby, p, r, k);
+                const CT w = Chunk16::from_lds(t);
+                st_sc1(g, (uint64_t) w.x | (uint64_t) w.y << 32);
+                st_sc1((char *) g + 8, (uint64_t) w.z | (uint64_t) w.w << 32);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (lane == 0) __hip_atomic_store((gu32 *) &progress[s_task], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (lane == 0) __hip_atomic_store((gu32 *) &progress[s_task], c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        lf_passes<PIX, G, NT, 2>(S, lane, bd);
+        // store rows [0, h) x cols [-XL, w) and rows [-8, 0) x cols [0, w), except the bytes
+        // published above; the bottom rows sc1 (row r + 1 reads them)
 #pragma unroll
         for (int u = 0; u < NU; u++) {
             const int ci = lane + u * NT;
             int p, r, k;
             lf_chunk<PIX, G>(ci, p, r, k);
-            if (ci >= L::NCHUNK || r >= (p ? L::CR : 72) - 8 || (k == 0 && (sbx == 0 || r < 8)) || (r < 8 && sby == 0))
+            if (ci >= L::NCHUNK || (k == 0 && (sbx == 0 || r < 8 || r >= (p ? L::CR : 72) - 8)) || (r < 8 && sby == 0))
                 continue;
+            if (r >= (p ? L::CR : 72) - 8) {
+                const PIX *t = p ? S.ct[p - 1] + r * FCP : S.lt + r * FLP;
+                PIX *g = lfr_addr<PIX, G>(P, sbx, sby, p, r, k);
+                const CT w = Chunk16::from_lds(t + CPX * k);
+                st_sc1(g, (uint64_t) w.x | (uint64_t) w.y << 32);
+                st_sc1((char *) g + 8, (uint64_t) w.z | (uint64_t) w.w << 32);
+                continue;
+            }
             const PIX *t = p ? S.ct[p - 1] + r * FCP : S.lt + r * FLP;
             const CT w = Chunk16::from_lds(t + CPX * k);
             v4u x; x.x = w.x; x.y = w.y; x.z = w.z; x.w = w.w;
             *(gv4u *) lfr_addr<PIX, G>(P, sbx, sby, p, r, k) = x;
+        }
+        if (c + 1 == ncols) {                   // the row's last SB: its bottom rows are final
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (lane == 0) __hip_atomic_store((gu32 *) &progress[s_task], ncols, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     // the last workgroup to finish resets the counters (every ticket is taken by then)

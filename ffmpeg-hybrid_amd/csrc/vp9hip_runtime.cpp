@@ -141,6 +141,7 @@ struct vp9hip_ctx {
     int max_groups = 3;                 // VP9HIP_STREAMS overrides (1..8); 3 measured best at C3, with even chain splits
     bool lf_overlap = false;            // VP9HIP_LF_OVERLAP=1: LF on a second stream per group (measured slower)
     bool fuse_plf = true;               // VP9HIP_PLF=0: no fused intra + LF launches
+    bool level_sched = true;            // VP9HIP_LEVELS=0: inter frames' intra SBs by diagonal
     int lf_rows = 1;                    // VP9HIP_LFROW: 0 LF as diagonal launches only, 1 k_lfr for
                                         // narrow phases (LFR_MAX_FRAMES), 2 k_lfr for every phase
     int w = 0, h = 0, bpp = 8, ss_h = 1, ss_v = 1, hb = 0, bypp = 1;
@@ -177,6 +178,7 @@ extern "C" int vp9hip_open(int device, vp9hip_ctx **out)
     if (const char *g = getenv("VP9HIP_LF_OVERLAP")) c->lf_overlap = atoi(g) != 0;
     if (const char *g = getenv("VP9HIP_PLF")) c->fuse_plf = atoi(g) != 0;
     if (const char *g = getenv("VP9HIP_LFROW")) c->lf_rows = atoi(g);
+    if (const char *g = getenv("VP9HIP_LEVELS")) c->level_sched = atoi(g) != 0;
     bool ok = hipSetDevice(device) == hipSuccess && hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) == hipSuccess;
     for (int i = 0; ok && i < MAX_GROUPS; i++)
@@ -439,6 +441,7 @@ struct FrameBuild {
     int refw[3][2], refh[3][2];  // visible reference plane sizes
     uint64_t coef_base;          // element offset of this frame's coefficients in the batch stream
     bool by_diag = false;        // residual buckets per intra diagonal of the SB (fused schedule)
+    bool levels = false;         // inter frame: SB steps by intra dependency level, not diagonal
 };
 
 struct PendingJob { PJob j; int level, ts; uint32_t d0, nd; };   // deps: pdeps[d0 .. d0 + nd)
@@ -596,6 +599,21 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
 
     std::vector<PendingJob> pj;
     pj.reserve(1024);
+    // level schedule (inter frames): the SB level of the intra job that produced each 4x4
+    // unit of the frame (per plane), -1 for inter-predicted units. An SB's level is 1 + the
+    // highest level among the units of OTHER SBs its intra jobs read (left, top, top-left:
+    // above-right reads stay inside the block's columns, vp9recon.c:71-97 / 103-121), 0
+    // when they read only inter pixels, which MC and the residual launches finish before
+    // the first intra launch.
+    const bool levels = fb.levels && !intra_frame;
+    thread_local std::vector<int16_t> umap[3];
+    int uw[3] = { 0, 0, 0 };
+    if (levels)
+        for (int p = 0; p < 3; p++) {
+            const int u = (64 >> (p ? ss_h : 0)) >> 2, v = (64 >> (p ? ss_v : 0)) >> 2;
+            uw[p] = fb.sb_cols * u;
+            umap[p].assign((size_t) uw[p] * fb.sb_rows * v, -1);
+        }
     int8_t lmap[3][16 * 16];
     int16_t jmap[3][16 * 16];              // SB-local job index that writes each 4x4 unit
     std::vector<uint16_t> pdeps;
@@ -622,6 +640,7 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
         memset(lf_level, 0, sizeof(lf_level));
         memset(lf_mask, 0, sizeof(lf_mask));
         pj.clear();
+        int sb_lvl = 0;                 // levels: 1 + highest level of the other SBs read
         memset(lmap, -1, sizeof(lmap));
         memset(jmap, -1, sizeof(jmap));
         pdeps.clear();
@@ -737,6 +756,23 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
                         if (ux0 > 0 && (nd & 1))
                             for (int v = uy0; v < uy0 + n4; v++)
                                 if (v < unitsv) dep(v * 16 + ux0 - 1);
+                        if (levels) {       // reads of other SBs' units (frame unit coordinates)
+                            const int fx = sbx * units + ux0, fy = sby * unitsv + uy0;
+                            const int16_t *um = umap[p].data();
+                            auto xdep = [&](int ux, int uy) {
+                                if (ux < 0 || uy < 0 || ux >= uw[p]) return;
+                                const int16_t l = um[(size_t) uy * uw[p] + ux];
+                                if (l >= 0) sb_lvl = std::max(sb_lvl, l + 1);
+                            };
+                            if (uy0 == 0 && (nd & 6)) {
+                                const int u0 = (nd & 4) ? -1 : 0, u1 = (nd & 2) ? n4 + trx : 0;
+                                for (int u = u0; u < u1; u++) xdep(fx + u, fy - 1);
+                            } else if (ux0 == 0 && (nd & 4)) {
+                                xdep(fx - 1, fy - 1);
+                            }
+                            if (ux0 == 0 && (nd & 1))
+                                for (int v = 0; v < n4; v++) xdep(fx - 1, fy + v);
+                        }
                         q.nd = (uint32_t) pdeps.size() - q.d0;
                         lvl += 1;
                         for (int v = uy0; v < uy0 + n4 && v < unitsv; v++)
@@ -888,7 +924,17 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
             s.sbh.push_back(h);
             uint32_t sbi = (uint32_t) s.sbs.size();
             s.sbs.push_back(sr);
-            int d = (sbx - tile_sb0) + sby;
+            int d = levels ? sb_lvl : (sbx - tile_sb0) + sby;
+            if (levels)                                  // this SB's intra units carry its level
+                for (const PendingJob &q : pj) {
+                    const int p = PJ_PLANE(q.j), n4 = 1 << q.ts;
+                    const int units = (64 >> (p ? ss_h : 0)) >> 2, unitsv = (64 >> (p ? ss_v : 0)) >> 2;
+                    const int fx = sbx * units + PJ_X4(q.j), fy = sby * unitsv + PJ_Y4(q.j);
+                    for (int v = 0; v < n4; v++)
+                        for (int u = 0; u < n4; u++)
+                            if (PJ_X4(q.j) + u < units && PJ_Y4(q.j) + v < unitsv)
+                                umap[p][(size_t) (fy + v) * uw[p] + fx + u] = (int16_t) sb_lvl;
+                }
             if ((int) pred_steps.size() <= d) pred_steps.resize(d + 1);
             pred_steps[d].push_back(sbi);
         }
@@ -1105,6 +1151,15 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     for (int i = 0; i < n; i++) phase_n[grp[i] * (maxpos + 1) + pos[i]]++;
     std::vector<char> res_fused(NP);
     for (int ph = 0; ph < NP; ph++) res_fused[ph] = fuse && phase_n[ph] < RES_FUSE_MAX_FRAMES;
+    // level-scheduled phases (inter frames of k_lfr phases): MC, all residuals, the intra
+    // SBs by dependency level (k_pred), then the whole loop filter as one k_lfr launch
+    std::vector<char> lvl_ph(NP, 0);
+    if (lfr_any && c->level_sched) {
+        for (int ph = 0; ph < NP; ph++) lvl_ph[ph] = c->lf_rows > 1 || phase_n[ph] < LFR_MAX_FRAMES;
+        for (int i = 0; i < n; i++)
+            if (pkts[i].keyframe || pkts[i].intraonly) lvl_ph[grp[i] * (maxpos + 1) + pos[i]] = 0;
+        for (int ph = 0; ph < NP; ph++) if (lvl_ph[ph]) res_fused[ph] = false;
+    }
     // per frame: validate, frame descriptor, reference scaling (sequential, cheap)
     std::vector<FrameBuild> fbs(n);
     std::vector<size_t> coef_off(n + 1, 0);
@@ -1171,6 +1226,7 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
         fb.phase = grp[i] * (maxpos + 1) + pos[i];
         fb.tile_lo = tile_lo; fb.tile_hi = tile_hi;
         fb.by_diag = res_fused[fb.phase];
+        fb.levels = lvl_ph[fb.phase];
         s.frame_phase[i] = fb.phase;
         s.frame_log2[i] = f->log2_tile_cols;
         coef_off[i + 1] = coef_off[i] + (size_t) f->ncoefs * csz;
@@ -1324,7 +1380,7 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
                         recs.push_back(dep);
                         recs.push_back((uint32_t) nc);
                         recs.push_back((uint32_t) c0);
-                        recs.push_back(dep != ~0u ? (uint32_t) start(r - 1) : 0u);
+                        recs.push_back(dep != ~0u ? (uint32_t) std::max(0, start(r - 1) - 1) : 0u);
                         recs.insert(recs.end(), grid[f][r].begin() + c0, grid[f][r].end());
                     }
                 if (offs.empty()) return 0;
@@ -1344,7 +1400,7 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
                     }
                 return 0;
             };
-            if (!fuse) {
+            if (!fuse || lvl_ph[ph]) {
                 for (size_t d = 0; d < wls.size(); d++) add_list(K_PRED, wls[d], (int) d);
                 if (lfr) {
                     if (int e = add_lfr(0)) return e;

@@ -253,3 +253,43 @@ def test_loop_filter_schedules(v9, orc, monkeypatch, mode, bpp):
         _cmp(v9, dev.download(1), r1, w, h, "LFROW=%s inter" % mode)
     finally:
         dev.close()
+
+
+@pytest.mark.parametrize("levels,bpp,log2", [("1", 8, 0), ("0", 8, 0), ("1", 10, 1)])
+def test_inter_level_schedule(v9, orc, monkeypatch, levels, bpp, log2):
+    """Inter frames' intra SBs scheduled by dependency level (VP9HIP_LEVELS=1, default):
+    an SB runs once the intra SBs whose pixels its intra blocks read (left, top, top-left;
+    vp9recon.c:71-121) have run; inter pixels (MC + residuals) are final before the first
+    intra launch, and the loop filter is one k_lfr launch after them. A key + 4 P chain at a
+    size with 15 x 9 SBs (many intra blocks next to other SBs' intra blocks) and 2 chains."""
+    monkeypatch.setenv("VP9HIP_LEVELS", levels)
+    dev = v9.Device(0)
+    try:
+        w, h = 960, 544
+        frames, outs, refs = [], [], []
+        for c in range(2):
+            base = 5 * c
+            frames.append(v9.SynthFrame(v9.synth_params(w, h, bpp, seed=700 + 10 * c, log2_tile_cols=log2)))
+            outs.append(base)
+            refs.append(None)
+            for k in range(1, 5):
+                kw = {"compound": 1} if k == 3 else {}
+                frames.append(v9.SynthFrame(v9.synth_params(w, h, bpp, seed=701 + 10 * c + k, inter=1,
+                                                            log2_tile_cols=log2, **kw)))
+                outs.append(base + k)
+                refs.append((base + k - 1, base + k - 1, base))
+        order = [0, 5, 1, 6, 2, 7, 3, 8, 4, 9]
+        dev.configure(w, h, bpp, nbufs=10)
+        dev.stage_batch([frames[i] for i in order], [outs[i] for i in order], [refs[i] for i in order])
+        for _ in range(2):
+            dev.run_batch()
+            dev.sync()
+        dec = {}
+        for i in range(10):
+            out = v9.alloc_planes(w, h, bpp)
+            r = refs[i]
+            orc.decode_frame(frames[i].pkt, out, None if r is None else [dec[r[0]], dec[r[1]], dec[r[2]]])
+            dec[outs[i]] = out
+            _cmp(v9, dev.download(outs[i]), out, w, h, "LEVELS=%s chain frame %d" % (levels, i))
+    finally:
+        dev.close()
