@@ -1625,28 +1625,112 @@ DEV int mc_sample(const PIX *r, int pitch, int w, int h, int X, int Y, int mx, i
     return clipbd((s + 64) >> 7, bd);
 }
 
+// One MC unit (<= 64 x 64 pixels of one plane) per workgroup. Unscaled references: the
+// (h + 7) x (w + 7) reference window (edge-clamped, emulated_edge_mc) is staged in LDS once,
+// then the separable filter runs as a horizontal pass into a pixel-clipped LDS tmp and a
+// vertical pass (do_8tap_2d_c, vp9dsp_template.c:2076-2113; bilinear do_bilin_2d
+// 2150-2227). With an identity phase a pass is an exact copy, so the 2-D form also gives
+// the 1-D and copy cases of the unscaled selection (vp9dsp_template.c:2036-2059, 1971-2022).
+// Scaled references and small units keep the per-pixel sampler (no barriers; L1-served taps).
+#define MC_WP 72                      // window pitch (>= 64 + 7)
+#ifndef MC_LDS_MIN
+#define MC_LDS_MIN 1024               // units of at least this many pixels use the LDS passes
+#endif
 template <typename PIX>
 __global__ __launch_bounds__(256) void k_mc(const McUnit *__restrict__ units, int nunits,
                                             const FrameDesc *__restrict__ frames)
 {
+    __shared__ PIX win[71 * MC_WP];
+    __shared__ int16_t tmp[71 * 64];
     const McUnit u = units[blockIdx.x];
     const FrameDesc &fd = frames[u.frame];
     const int p = u.plane, c = p ? 1 : 0, bd = fd.bd;
     PIX *dst = (PIX *) fd.plane[p];
     const int pitch = fd.pitch[c];
-    for (int i = threadIdx.x; i < u.w * u.h; i += 256) {
-        int yy = i / u.w, xx = i - yy * u.w;
-        int out = 0;
-        for (int k = 0; k < u.nref; k++) {
-            const int rf = u.ref[k];
-            const McRef m = u.r[k];
-            const PIX *r = (const PIX *) fd.ref[rf][p];
-            const int px = m.mx + xx * m.dx, py = m.my + yy * m.dy;
-            const int v = mc_sample<PIX>(r, pitch, fd.refw[rf][c], fd.refh[rf][c], m.ix + (px >> 4), m.iy + (py >> 4),
-                                         px & 15, py & 15, u.filter, bd);
-            out = k ? (out + v + 1) >> 1 : v;
+    const int W = u.w, H = u.h, npx = W * H;
+    bool scaled = false;
+    for (int k = 0; k < u.nref; k++) scaled |= u.r[k].dx != 16 || u.r[k].dy != 16;
+    const int lw = 31 - __builtin_clz((unsigned) W);          // passes index pixels by shifts
+    // measured: the LDS passes win at 8 bits (C2 k_mc 12.0 -> 10.2 ms per 120 frames) and lose
+    // at 16 bits (C5 52.7 -> 79 ms: 19 KB of LDS per workgroup halves the loads in flight
+    // on 8K references that miss the caches)
+    if (sizeof(PIX) != 1 || scaled || npx < MC_LDS_MIN || (1 << lw) != W) {
+        for (int i = threadIdx.x; i < npx; i += 256) {
+            int yy = i / W, xx = i - yy * W;
+            int out = 0;
+            for (int k = 0; k < u.nref; k++) {
+                const int rf = u.ref[k];
+                const McRef m = u.r[k];
+                const PIX *r = (const PIX *) fd.ref[rf][p];
+                const int px = m.mx + xx * m.dx, py = m.my + yy * m.dy;
+                const int v = mc_sample<PIX>(r, pitch, fd.refw[rf][c], fd.refh[rf][c], m.ix + (px >> 4), m.iy + (py >> 4),
+                                             px & 15, py & 15, u.filter, bd);
+                out = k ? (out + v + 1) >> 1 : v;
+            }
+            dst[(size_t) (u.y + yy) * pitch + u.x + xx] = (PIX) out;
         }
-        dst[(size_t) (u.y + yy) * pitch + u.x + xx] = (PIX) out;
+        return;
+    }
+    const int WW = W + 7, WH = H + 7;
+    const bool bil = u.filter == 3;
+    int out[16];                                   // <= 64 x 64 / 256 pixels per thread
+    for (int k = 0; k < u.nref; k++) {
+        const int rf = u.ref[k];
+        const McRef m = u.r[k];
+        const PIX *r = (const PIX *) fd.ref[rf][p];
+        const int rw = fd.refw[rf][c], rh = fd.refh[rf][c];
+        const int mx = m.mx, my = m.my;
+        const int X0 = m.ix - 3, Y0 = m.iy - 3;   // window origin (integer position - 3)
+        if (k) __syncthreads();                    // the previous reference's passes are done
+        for (int i = threadIdx.x; i < WH * MC_WP; i += 256) {   // constant-divisor rows
+            const int wy = i / MC_WP, wx = i - wy * MC_WP;
+            if (wx < WW) win[i] = (PIX) mc_ref(r, pitch, rw, rh, X0 + wx, Y0 + wy);
+        }
+        __syncthreads();
+        // horizontal pass over the window rows the vertical pass reads (rows 3 .. 3 + H when
+        // the vertical phase is an identity; 8-tap reads rows y .. y + 7, bilinear y + 3, y + 4)
+        const int r0 = my ? (bil ? 3 : 0) : 3, r1 = my ? (bil ? H + 4 : H + 7) : H + 3;
+        const int16_t *fx = vp9t_subpel_filters[bil ? 0 : u.filter][mx];
+        for (int i = threadIdx.x; i < (r1 - r0) << lw; i += 256) {
+            const int ry = r0 + (i >> lw), x = i & (W - 1);
+            const PIX *w0 = win + ry * MC_WP + x;
+            int v;
+            if (!mx) v = w0[3];
+            else if (bil) v = w0[3] + ((mx * (w0[4] - w0[3]) + 8) >> 4);
+            else {
+                int s8 = 0;
+#pragma unroll
+                for (int t = 0; t < 8; t++) s8 += fx[t] * w0[t];
+                v = clipbd((s8 + 64) >> 7, bd);
+            }
+            tmp[ry * 64 + x] = (int16_t) v;
+        }
+        __syncthreads();
+        const int16_t *fy = vp9t_subpel_filters[bil ? 0 : u.filter][my];
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            const int i = threadIdx.x + 256 * q;
+            if (i >= npx) break;
+            const int yy = i >> lw, xx = i & (W - 1);
+            const int16_t *t0 = tmp + yy * 64 + xx;
+            int v;
+            if (!my) v = t0[3 * 64];
+            else if (bil) v = t0[3 * 64] + ((my * (t0[4 * 64] - t0[3 * 64]) + 8) >> 4);
+            else {
+                int s8 = 0;
+#pragma unroll
+                for (int t = 0; t < 8; t++) s8 += fy[t] * t0[t * 64];
+                v = clipbd((s8 + 64) >> 7, bd);
+            }
+            out[q] = k ? (out[q] + v + 1) >> 1 : v;
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        const int i = threadIdx.x + 256 * q;
+        if (i >= npx) break;
+        const int yy = i >> lw, xx = i & (W - 1);
+        dst[(size_t) (u.y + yy) * pitch + u.x + xx] = (PIX) out[q];
     }
 }
 
