@@ -115,6 +115,7 @@ struct Staged {
     // record counts of the arena (the host images above are not kept for these)
     uint32_t n_sbs = 0, n_pjobs = 0, n_passes = 0, n_wgs = 0, n_rjobs = 0, n_lfs = 0, n_mcs = 0;
     uint32_t n_ctr = 0;                 // k_lfr counter words (zero between launches)
+    std::vector<uint32_t> lfr_ctr;      // counter block offset of every k_lfr launch
     uint8_t *pinned = nullptr;          // pinned host image of the arena (one DMA per stage)
     size_t pinned_cap = 0;
     // device arena
@@ -1101,7 +1102,7 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     s.wgs.clear(); s.sbh.clear(); s.sbjobs.clear(); s.jdep0.clear(); s.jdeps.clear();
     s.rjobs.clear(); s.resid16 = 0;
     s.rbucket.clear();
-    s.lists.clear(); s.launches.clear(); s.coefs.clear(); s.n_ctr = 0;
+    s.lists.clear(); s.launches.clear(); s.coefs.clear(); s.n_ctr = 0; s.lfr_ctr.clear();
     s.frame_phase.assign(n, 0); s.frame_log2.assign(n, 0);
     s.tile_lo = tile_lo; s.tile_hi = tile_hi;
     for (int k = 0; k < K_N; k++) s.alg_bytes[k] = 0;
@@ -1389,6 +1390,7 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
                 for (uint32_t &o : offs) o += nt;
                 s.lists.insert(s.lists.end(), offs.begin(), offs.end());
                 s.lists.insert(s.lists.end(), recs.begin(), recs.end());
+                s.lfr_ctr.push_back(s.n_ctr);
                 s.n_ctr += 4 + nt;
                 s.launches.push_back(L);
                 for (int i : phase_frames[ph])
@@ -1807,6 +1809,15 @@ extern "C" int vp9hip_sync(vp9hip_ctx *c)
     if (!c) return VP9HIP_EINVAL;
     hipSetDevice(c->dev);
     HIPCHK(hipStreamSynchronize(c->st));
+    // k_lfr bounds its spins and counts the waits it gave up (timeout word of each
+    // launch's counter block): a nonzero count means the row hand-off broke, and the
+    // frames are not trusted
+    if (c->stg.ready && !c->stg.lfr_ctr.empty()) {
+        std::vector<uint32_t> ctr(c->stg.n_ctr);
+        HIPCHK(hipMemcpy(ctr.data(), c->stg.arena + c->stg.o_ctr, ctr.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        for (uint32_t o : c->stg.lfr_ctr)
+            if (ctr[o + 2]) return VP9HIP_EBUG;
+    }
     if (c->timing && c->timed_run && c->stg.ready) {
         for (int k = 0; k < K_N; k++) { c->kms[k] = 0; c->kcount[k] = 0; }
         for (size_t i = 0; i < c->stg.launches.size() && 2 * i + 1 < c->ev.size(); i++) {

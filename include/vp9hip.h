@@ -169,7 +169,8 @@ int  vp9hip_run_phase(vp9hip_ctx *ctx, int phase, int part);
  */
 int64_t vp9hip_stripe(vp9hip_ctx *ctx, int frame, int tile_lo, int tile_hi, void *dev, int to_frame);
 
-/* Wait for all queued work. */
+/* Wait for all queued work. VP9HIP_EBUG if a row-pipelined loop-filter launch (k_lfr)
+ * gave up a bounded wait on another workgroup's progress (frames not trusted). */
 int  vp9hip_sync(vp9hip_ctx *ctx);
 
 /* Copy device buffer `buf` into host planes (linesize in bytes). Synchronous. */
