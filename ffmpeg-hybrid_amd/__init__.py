@@ -735,7 +735,7 @@ def ivf_write(frames, width, height, time_base=(1, 30)):
 
 PLAN_STAT_NAMES = ("sbs", "passes", "pjobs", "rjobs", "jobs_4x4", "jobs_8x8", "jobs_16x16",
                    "jobs_32x32", "lane_use", "max_passes_sb", "lf_records", "mc_units", "pred_steps",
-                   "lf_steps", "levels", "pass_rows")
+                   "lf_steps", "levels", "pass_rows", "level_steps")
 
 
 def plan_stats(frame):

@@ -1983,5 +1983,15 @@ extern "C" int vp9hip_plan_stats(const vp9h_frame *f, double *out, int cap)
     out[12] = (double) ps.size();
     out[13] = (double) ls.size();
     for (auto &h : s.sbh) out[14] += h.nlev;                           // dependency levels (pass lower bound)
+    if (cap > 16) {                     // intra steps of the level schedule (inter frames)
+        Staged s2;
+        FrameBuild fb2 = fb;
+        fb2.levels = true;
+        s2.rbucket.resize(1);
+        std::vector<std::vector<uint32_t>> ps2, ls2;
+        r = build_frame(nullptr, s2, fb2, ps2, ls2);
+        if (r < 0) return r;
+        out[16] = (double) ps2.size();
+    }
     return 0;
 }

@@ -215,7 +215,8 @@ int  vp9hip_alg_bytes(vp9hip_ctx *ctx, double *bytes, int cap);
  * SBs with intra work, passes, intra jobs, residual jobs, intra jobs per tx size (4),
  * lane use, max passes per SB, LF records, MC units, intra / LF wavefront steps,
  * intra dependency levels (summed over SBs: the lower bound of the passes), pixel rows
- * the passes loop over (each pass: its largest job size). */
+ * the passes loop over (each pass: its largest job size). A 17th value (cap >= 17): intra
+ * steps under the dependency-level schedule of inter frames (= the diagonals otherwise). */
 int  vp9hip_plan_stats(const vp9h_frame *pkt, double *out, int cap);
 
 int  vp9hip_abi_version(void);

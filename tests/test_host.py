@@ -116,3 +116,17 @@ def test_planner_stats_c3_frame(v9):
     assert 0 < st["lane_use"] <= 1
     assert st["pred_steps"] == 15 + 34 - 1     # 4 tile columns of 15 SBs
     assert st["lf_steps"] == 60 + 2 * 33
+
+
+def test_planner_inter_level_schedule(v9):
+    """Inter frames (no GPU): intra SBs are scheduled by dependency level. An SB waits only
+    for the SBs whose intra pixels its intra blocks read, so a frame with ~10 % intra blocks
+    needs far fewer intra steps than the x_in_tile + y diagonals; a keyframe (every block
+    intra) keeps exactly the diagonals."""
+    key = v9.SynthFrame(v9.synth_params(1920, 1080, 8, seed=0x56503901))
+    st = v9.plan_stats(key)
+    assert st["level_steps"] == st["pred_steps"] == 30 + 17 - 1
+    inter = v9.SynthFrame(v9.synth_params(1920, 1080, 8, seed=0x56503911, inter=1))
+    st = v9.plan_stats(inter)
+    assert st["pred_steps"] <= 30 + 17 - 1        # diagonals holding an SB with intra blocks
+    assert 1 <= st["level_steps"] < st["pred_steps"] / 3
