@@ -1327,7 +1327,9 @@ __global__ __launch_bounds__(LfNT<G>::NT) void k_lf(const uint32_t *__restrict__
 //   filtering rewrites x = 64c + 57..63 of that row). progress[r] = p says the bottom
 //   rows of SBs 0..p-1 are final: row r publishes p = c right after SB c's column pass
 //   (SB c - 1's last columns are then final and stored), before its row pass, and p = ncols
-//   after its last SB; SB (r + 1, c) waits for progress[r] >= c + 1.
+//   after its last SB; SB (r + 1, c) waits for progress[r] >= c + 1 before its ROW pass
+//   (the column pass rewrites rows 0..63 only, so it runs ahead of the hand-off: the lag
+//   between rows is one SB's column + row pass instead of two column passes + a row pass).
 //   Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, Valid forms row 1): every
 //   byte of the bottom 8 rows is stored sc1 (write-through) and drained by every storing
 //   wave before the barrier and ONE lane's sc1 progress store; the consumer polls with sc1
@@ -1434,35 +1436,16 @@ __global__ __launch_bounds__(LfNT<G>::NT) void k_lfr(const uint32_t *__restrict_
                 }
             }
         }
-        if (lane == 0 && dep != ~0u) {
-            const uint32_t need = c + 1;
-            for (uint32_t n = 0; seen < need; n++) {
-                seen = __hip_atomic_load((gu32 *) &progress[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (seen >= need) break;
-                if (n > (1u << 22)) { atomicAdd(&ctr[2], 1u); seen = need; break; }
-                __builtin_amdgcn_s_sleep(1);
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        __syncthreads();
-        // top halo (y = -8..-1, x >= 0): rows row r - 1 handed off, sc1 loads only
-#pragma unroll
-        for (int u = 0; u < NU; u++) {
-            const int ci = lane + u * NT;
-            int p, r, k;
-            lf_chunk<PIX, G>(ci, p, r, k);
-            if (ci >= L::NCHUNK || r >= 8 || k == 0 || sby == 0) continue;
-            const PIX *g = lfr_addr<PIX, G>(P, sbx, sby, p, r, k);
-            const uint64_t lo = ld_sc1(g), hi = ld_sc1((const char *) g + 8);
-            v[u] = make_uint4((uint32_t) lo, (uint32_t) (lo >> 32), (uint32_t) hi, (uint32_t) (hi >> 32));
-        }
+        // interior (and left halo) into LDS, then the column pass: it rewrites rows 0..63 only,
+        // so it runs before the row above has handed over this SB's top halo
+        __syncthreads();                        // every lane has read the previous tile
         for (int i = lane; i < L::PROG / 4; i += NT) S.prog[i] = ((const uint32_t *) rec.prog)[i];
 #pragma unroll
         for (int u = 0; u < NU; u++) {
             const int ci = lane + u * NT;
             int p, r, k;
             lf_chunk<PIX, G>(ci, p, r, k);
-            if (ci < L::NCHUNK && (r >= 8 || k > 0)) {
+            if (ci < L::NCHUNK && r >= 8) {
                 PIX *t = p ? S.ct[p - 1] + r * FCP : S.lt + r * FLP;
                 Chunk16::to_lds(v[u], t + CPX * k);
             }
@@ -1491,6 +1474,34 @@ __global__ __launch_bounds__(LfNT<G>::NT) void k_lfr(const uint32_t *__restrict_
             __syncthreads();
             if (lane == 0) __hip_atomic_store((gu32 *) &progress[s_task], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        // the row pass needs the top halo: wait for the row above through SB c + 1's column pass
+        if (lane == 0 && dep != ~0u) {
+            const uint32_t need = c + 1;
+            for (uint32_t n = 0; seen < need; n++) {
+                seen = __hip_atomic_load((gu32 *) &progress[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (seen >= need) break;
+                if (n > (1u << 22)) { atomicAdd(&ctr[2], 1u); seen = need; break; }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        __syncthreads();
+        // top halo (y = -8..-1, x >= 0): rows row r - 1 handed off, sc1 loads only
+#pragma unroll
+        for (int u = 0; u < NU; u++) {
+            const int ci = lane + u * NT;
+            int p, r, k;
+            lf_chunk<PIX, G>(ci, p, r, k);
+            if (ci >= L::NCHUNK || r >= 8 || k == 0) continue;
+            if (sby > 0) {
+                const PIX *g = lfr_addr<PIX, G>(P, sbx, sby, p, r, k);
+                const uint64_t lo = ld_sc1(g), hi = ld_sc1((const char *) g + 8);
+                v[u] = make_uint4((uint32_t) lo, (uint32_t) (lo >> 32), (uint32_t) hi, (uint32_t) (hi >> 32));
+            }
+            PIX *t = p ? S.ct[p - 1] + r * FCP : S.lt + r * FLP;
+            Chunk16::to_lds(v[u], t + CPX * k);
+        }
+        __syncthreads();
         lf_passes<PIX, G, NT, 2>(S, lane, bd);
         // store rows [0, h) x cols [-XL, w) and rows [-8, 0) x cols [0, w), except the bytes
         // published above; the bottom rows sc1 (row r + 1 reads them)
