@@ -1386,6 +1386,23 @@ DEV void lfr_issue(Chunk16::T (&v)[NU], const LfrPlanes &P, int sbx, int sby, in
     }
 }
 
+// top halo (y = -8..-1, x >= 0) of SB (sbx, sby): rows row sby - 1 handed off, sc1 loads only
+template <typename PIX, class G, int NT, int NU>
+DEV void lfr_top(Chunk16::T (&v)[NU], const LfrPlanes &P, int sbx, int sby, int lane)
+{
+    typedef LfP<PIX, G> L;
+#pragma unroll
+    for (int u = 0; u < NU; u++) {
+        const int ci = lane + u * NT;
+        int p, r, k;
+        lf_chunk<PIX, G>(ci, p, r, k);
+        if (ci >= L::NCHUNK || r >= 8 || k == 0 || sby == 0) continue;
+        const PIX *g = lfr_addr<PIX, G>(P, sbx, sby, p, r, k);
+        const uint64_t lo = ld_sc1(g), hi = ld_sc1((const char *) g + 8);
+        v[u] = make_uint4((uint32_t) lo, (uint32_t) (lo >> 32), (uint32_t) hi, (uint32_t) (hi >> 32));
+    }
+}
+
 // PF: the next SB's interior loads are issued before this SB's filtering (in registers)
 template <typename PIX, class G, bool PF>
 __global__ __launch_bounds__(LfNT<G>::NT) void k_lfr(const uint32_t *__restrict__ tasks, const LFRec *__restrict__ recs,
@@ -1397,7 +1414,7 @@ __global__ __launch_bounds__(LfNT<G>::NT) void k_lfr(const uint32_t *__restrict_
     constexpr int FLP = L::YP, FCP = L::UVP, CW = G::CW, CPX = L::CPX;
     constexpr int NU = (L::NCHUNK + NT - 1) / NT;
     __shared__ LfLds<PIX, G> S;
-    __shared__ uint32_t s_task, s_last;
+    __shared__ uint32_t s_task, s_last, s_pre;
     const int lane = threadIdx.x;
     uint32_t *const progress = ctr + 4;
     // the row chain is the latency path of the phase: its waves issue first on their SIMDs
@@ -1450,7 +1467,17 @@ __global__ __launch_bounds__(LfNT<G>::NT) void k_lfr(const uint32_t *__restrict_
                 Chunk16::to_lds(v[u], t + CPX * k);
             }
         }
+        // usually the row above is already far enough: then the top halo's loads are issued
+        // here and run under the column pass instead of after it
+        if (lane == 0) {
+            if (dep != ~0u && seen < c + 1)
+                seen = __hip_atomic_load((gu32 *) &progress[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_pre = dep == ~0u || seen >= c + 1;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         __syncthreads();
+        const bool pre = s_pre;
+        if (pre) lfr_top<PIX, G, NT, NU>(v, P, sbx, sby, lane);
         // the next SB's interior loads run under this SB's filtering
         if (PF && c + 1 < ncols) lfr_issue<PIX, G, NT, NU>(v, P, sbx + 1, sby, lane, false);
         lf_passes<PIX, G, NT, 1>(S, lane, bd);
@@ -1475,7 +1502,7 @@ __global__ __launch_bounds__(LfNT<G>::NT) void k_lfr(const uint32_t *__restrict_
             if (lane == 0) __hip_atomic_store((gu32 *) &progress[s_task], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         // the row pass needs the top halo: wait for the row above through SB c + 1's column pass
-        if (lane == 0 && dep != ~0u) {
+        if (!pre && lane == 0 && dep != ~0u) {
             const uint32_t need = c + 1;
             for (uint32_t n = 0; seen < need; n++) {
                 seen = __hip_atomic_load((gu32 *) &progress[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1484,20 +1511,17 @@ __global__ __launch_bounds__(LfNT<G>::NT) void k_lfr(const uint32_t *__restrict_
                 __builtin_amdgcn_s_sleep(1);
             }
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        __syncthreads();
-        // top halo (y = -8..-1, x >= 0): rows row r - 1 handed off, sc1 loads only
+        if (!pre) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            __syncthreads();
+            lfr_top<PIX, G, NT, NU>(v, P, sbx, sby, lane);
+        }
 #pragma unroll
         for (int u = 0; u < NU; u++) {
             const int ci = lane + u * NT;
             int p, r, k;
             lf_chunk<PIX, G>(ci, p, r, k);
             if (ci >= L::NCHUNK || r >= 8 || k == 0) continue;
-            if (sby > 0) {
-                const PIX *g = lfr_addr<PIX, G>(P, sbx, sby, p, r, k);
-                const uint64_t lo = ld_sc1(g), hi = ld_sc1((const char *) g + 8);
-                v[u] = make_uint4((uint32_t) lo, (uint32_t) (lo >> 32), (uint32_t) hi, (uint32_t) (hi >> 32));
-            }
             PIX *t = p ? S.ct[p - 1] + r * FCP : S.lt + r * FLP;
             Chunk16::to_lds(v[u], t + CPX * k);
         }
