@@ -1331,8 +1331,9 @@ __global__ __launch_bounds__(LfNT<G>::NT) void k_lf(const uint32_t *__restrict__
 //   (the column pass rewrites rows 0..63 only, so it runs ahead of the hand-off: the lag
 //   between rows is one SB's column + row pass instead of two column passes + a row pass).
 //   Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, Valid forms row 1): every
-//   byte of the bottom 8 rows is stored sc1 (write-through) and drained by every storing
-//   wave before the barrier and ONE lane's sc1 progress store; the consumer polls with sc1
+//   byte of the bottom 8 rows is stored sc1 (write-through) by the workgroup's store wave
+//   (lanes NT.., the only wave that stores), which drains (s_waitcnt vmcnt(0)) before ONE
+//   of its lanes stores the progress word; the consumer polls with sc1
 //   loads and loads those rows only with sc1 loads. Every other load reads bytes written by
 //   earlier launches, or by this launch only after the load (row r + 1 rewrites row r's
 //   bottom rows once row r has published them).
@@ -1405,14 +1406,14 @@ DEV void lfr_top(Chunk16::T (&v)[NU], const LfrPlanes &P, int sbx, int sby, int 
 
 // PF: the next SB's interior loads are issued before this SB's filtering (in registers)
 template <typename PIX, class G, bool PF>
-__global__ __launch_bounds__(LfNT<G>::NT) void k_lfr(const uint32_t *__restrict__ tasks, const LFRec *__restrict__ recs,
+__global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfr(const uint32_t *__restrict__ tasks, const LFRec *__restrict__ recs,
                                                      const FrameDesc *__restrict__ frames, uint32_t *ctr, int ntasks)
 {
     constexpr int NT = LfNT<G>::NT;
     typedef LfP<PIX, G> L;
     typedef Chunk16::T CT;
     constexpr int FLP = L::YP, FCP = L::UVP, CW = G::CW, CPX = L::CPX;
-    constexpr int NU = (L::NCHUNK + NT - 1) / NT;
+    constexpr int NU = (L::NCHUNK + NT - 1) / NT, NUM = (L::NCHUNK + 63) / 64;
     __shared__ LfLds<PIX, G> S;
     __shared__ uint32_t s_task, s_last, s_pre;
     const int lane = threadIdx.x;
@@ -1434,60 +1435,71 @@ __global__ __launch_bounds__(LfNT<G>::NT) void k_lfr(const uint32_t *__restrict_
     CT v[NU];
 #pragma unroll
     for (int u = 0; u < NU; u++) v[u] = Chunk16::zero();
-    lfr_issue<PIX, G, NT, NU>(v, P, c0, sby, lane, c0 > 0);
+    // lanes NT.. form the store wave: it issues every global store of the task, so the
+    // filtering waves' load waits never queue behind stores (vmcnt retires in order)
+    const bool mover = lane >= NT;
+    const int ml = lane - NT;
+    if (!mover) lfr_issue<PIX, G, NT, NU>(v, P, c0, sby, lane, c0 > 0);
     for (uint32_t c = c0; c < ncols; c++) {
         const int sbx = (int) c;
         const LFRec &rec = recs[T[4 + c - c0]];
-        if (!PF && c > c0) lfr_issue<PIX, G, NT, NU>(v, P, sbx, sby, lane, false);
-        // left halo (x < 0): this workgroup's previous tile, read from LDS before the barrier
-        // below (SB c0's came from HBM with its interior)
-        if (c > c0) {
+        if (!mover) {
+            if (!PF && c > c0) lfr_issue<PIX, G, NT, NU>(v, P, sbx, sby, lane, false);
+            // left halo (x < 0): this workgroup's previous tile, read from LDS before the
+            // barrier below (SB c0's came from HBM with its interior)
+            if (c > c0) {
+#pragma unroll
+                for (int u = 0; u < NU; u++) {
+                    const int ci = lane + u * NT;
+                    int p, r, k;
+                    lf_chunk<PIX, G>(ci, p, r, k);
+                    if (ci < L::NCHUNK && r >= 8 && k == 0) {
+                        const PIX *t = p ? S.ct[p - 1] + r * FCP : S.lt + r * FLP;
+                        v[u] = Chunk16::from_lds(t + (p ? CW : 64));      // x = 64 - XL .. 63 (CW for chroma)
+                    }
+                }
+            }
+        }
+        __syncthreads();                        // every lane has read the previous tile
+        // interior (and left halo) into LDS, then the column pass: it rewrites rows 0..63 only,
+        // so it runs before the row above has handed over this SB's top halo. Usually the row
+        // above is already far enough: then the top halo's loads are issued before the column
+        // pass and run under it
+        if (!mover) {
+            for (int i = lane; i < L::PROG / 4; i += NT) S.prog[i] = ((const uint32_t *) rec.prog)[i];
 #pragma unroll
             for (int u = 0; u < NU; u++) {
                 const int ci = lane + u * NT;
                 int p, r, k;
                 lf_chunk<PIX, G>(ci, p, r, k);
-                if (ci < L::NCHUNK && r >= 8 && k == 0) {
-                    const PIX *t = p ? S.ct[p - 1] + r * FCP : S.lt + r * FLP;
-                    v[u] = Chunk16::from_lds(t + (p ? CW : 64));          // x = 64 - XL .. 63 (CW for chroma)
+                if (ci < L::NCHUNK && r >= 8) {
+                    PIX *t = p ? S.ct[p - 1] + r * FCP : S.lt + r * FLP;
+                    Chunk16::to_lds(v[u], t + CPX * k);
                 }
             }
-        }
-        // interior (and left halo) into LDS, then the column pass: it rewrites rows 0..63 only,
-        // so it runs before the row above has handed over this SB's top halo
-        __syncthreads();                        // every lane has read the previous tile
-        for (int i = lane; i < L::PROG / 4; i += NT) S.prog[i] = ((const uint32_t *) rec.prog)[i];
-#pragma unroll
-        for (int u = 0; u < NU; u++) {
-            const int ci = lane + u * NT;
-            int p, r, k;
-            lf_chunk<PIX, G>(ci, p, r, k);
-            if (ci < L::NCHUNK && r >= 8) {
-                PIX *t = p ? S.ct[p - 1] + r * FCP : S.lt + r * FLP;
-                Chunk16::to_lds(v[u], t + CPX * k);
+            if (lane == 0) {
+                if (dep != ~0u && seen < c + 1)
+                    seen = __hip_atomic_load((gu32 *) &progress[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                s_pre = dep == ~0u || seen >= c + 1;
             }
-        }
-        // usually the row above is already far enough: then the top halo's loads are issued
-        // here and run under the column pass instead of after it
-        if (lane == 0) {
-            if (dep != ~0u && seen < c + 1)
-                seen = __hip_atomic_load((gu32 *) &progress[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_pre = dep == ~0u || seen >= c + 1;
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         __syncthreads();
         const bool pre = s_pre;
-        if (pre) lfr_top<PIX, G, NT, NU>(v, P, sbx, sby, lane);
-        // the next SB's interior loads run under this SB's filtering
-        if (PF && c + 1 < ncols) lfr_issue<PIX, G, NT, NU>(v, P, sbx + 1, sby, lane, false);
-        lf_passes<PIX, G, NT, 1>(S, lane, bd);
+        if (!mover) {
+            if (pre) lfr_top<PIX, G, NT, NU>(v, P, sbx, sby, lane);
+            // the next SB's interior loads run under this SB's filtering
+            if (PF && c + 1 < ncols) lfr_issue<PIX, G, NT, NU>(v, P, sbx + 1, sby, lane, false);
+        }
+        lf_passes<PIX, G, NT, 1>(S, lane, bd);  // the store wave has no lines: barriers only
         // SB c - 1's bottom rows are final now (this SB's left-edge column filtering was the
-        // last to touch them): its last XL columns of them sc1, drained by every wave, then
-        // the progress word, ahead of this SB's row pass. Those bytes are not stored again.
-        if (sbx > 0) {
+        // last to touch them): the store wave writes its last XL columns of them sc1, drains
+        // and stores the progress word, while the filtering waves go on. Those bytes are not
+        // stored again.
+        if (mover && sbx > 0) {
 #pragma unroll
-            for (int u = 0; u < NU; u++) {
-                const int ci = lane + u * NT;
+            for (int u = 0; u < NUM; u++) {
+                const int ci = ml + u * 64;
                 int p, r, k;
                 lf_chunk<PIX, G>(ci, p, r, k);
                 if (ci >= L::NCHUNK || r < (p ? L::CR : 72) - 8 || k != 0) continue;
@@ -1498,64 +1510,68 @@ __global__ __launch_bounds__(LfNT<G>::NT) void k_lfr(const uint32_t *__restrict_
                 st_sc1((char *) g + 8, (uint64_t) w.z | (uint64_t) w.w << 32);
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (lane == 0) __hip_atomic_store((gu32 *) &progress[s_task], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (ml == 0) __hip_atomic_store((gu32 *) &progress[s_task], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        // the row pass needs the top halo: wait for the row above through SB c + 1's column pass
-        if (!pre && lane == 0 && dep != ~0u) {
-            const uint32_t need = c + 1;
-            for (uint32_t n = 0; seen < need; n++) {
-                seen = __hip_atomic_load((gu32 *) &progress[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (seen >= need) break;
-                if (n > (1u << 22)) { atomicAdd(&ctr[2], 1u); seen = need; break; }
-                __builtin_amdgcn_s_sleep(1);
-            }
-        }
+        // otherwise the row pass waits for the row above through SB c + 1's column pass
         if (!pre) {
+            if (lane == 0 && dep != ~0u) {
+                const uint32_t need = c + 1;
+                for (uint32_t n = 0; seen < need; n++) {
+                    seen = __hip_atomic_load((gu32 *) &progress[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (seen >= need) break;
+                    if (n > (1u << 22)) { atomicAdd(&ctr[2], 1u); seen = need; break; }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             __syncthreads();
-            lfr_top<PIX, G, NT, NU>(v, P, sbx, sby, lane);
+            if (!mover) lfr_top<PIX, G, NT, NU>(v, P, sbx, sby, lane);
         }
+        if (!mover) {
 #pragma unroll
-        for (int u = 0; u < NU; u++) {
-            const int ci = lane + u * NT;
-            int p, r, k;
-            lf_chunk<PIX, G>(ci, p, r, k);
-            if (ci >= L::NCHUNK || r >= 8 || k == 0) continue;
-            PIX *t = p ? S.ct[p - 1] + r * FCP : S.lt + r * FLP;
-            Chunk16::to_lds(v[u], t + CPX * k);
+            for (int u = 0; u < NU; u++) {
+                const int ci = lane + u * NT;
+                int p, r, k;
+                lf_chunk<PIX, G>(ci, p, r, k);
+                if (ci >= L::NCHUNK || r >= 8 || k == 0) continue;
+                PIX *t = p ? S.ct[p - 1] + r * FCP : S.lt + r * FLP;
+                Chunk16::to_lds(v[u], t + CPX * k);
+            }
         }
         __syncthreads();
         lf_passes<PIX, G, NT, 2>(S, lane, bd);
-        // store rows [0, h) x cols [-XL, w) and rows [-8, 0) x cols [0, w), except the bytes
-        // published above; the bottom rows sc1 (row r + 1 reads them)
+        // store wave: rows [0, h) x cols [-XL, w) and rows [-8, 0) x cols [0, w), except the
+        // bytes published above; the bottom rows sc1 (row r + 1 reads them). Its LDS reads
+        // finish before the next SB's first barrier.
+        if (mover) {
 #pragma unroll
-        for (int u = 0; u < NU; u++) {
-            const int ci = lane + u * NT;
-            int p, r, k;
-            lf_chunk<PIX, G>(ci, p, r, k);
-            if (ci >= L::NCHUNK || (k == 0 && (sbx == 0 || r < 8 || r >= (p ? L::CR : 72) - 8)) || (r < 8 && sby == 0))
-                continue;
-            if (r >= (p ? L::CR : 72) - 8) {
+            for (int u = 0; u < NUM; u++) {
+                const int ci = ml + u * 64;
+                int p, r, k;
+                lf_chunk<PIX, G>(ci, p, r, k);
+                if (ci >= L::NCHUNK || (k == 0 && (sbx == 0 || r < 8 || r >= (p ? L::CR : 72) - 8)) || (r < 8 && sby == 0))
+                    continue;
                 const PIX *t = p ? S.ct[p - 1] + r * FCP : S.lt + r * FLP;
-                PIX *g = lfr_addr<PIX, G>(P, sbx, sby, p, r, k);
                 const CT w = Chunk16::from_lds(t + CPX * k);
-                st_sc1(g, (uint64_t) w.x | (uint64_t) w.y << 32);
-                st_sc1((char *) g + 8, (uint64_t) w.z | (uint64_t) w.w << 32);
-                continue;
+                PIX *g = lfr_addr<PIX, G>(P, sbx, sby, p, r, k);
+                if (r >= (p ? L::CR : 72) - 8) {
+                    st_sc1(g, (uint64_t) w.x | (uint64_t) w.y << 32);
+                    st_sc1((char *) g + 8, (uint64_t) w.z | (uint64_t) w.w << 32);
+                } else {
+                    v4u x; x.x = w.x; x.y = w.y; x.z = w.z; x.w = w.w;
+                    *(gv4u *) g = x;
+                }
             }
-            const PIX *t = p ? S.ct[p - 1] + r * FCP : S.lt + r * FLP;
-            const CT w = Chunk16::from_lds(t + CPX * k);
-            v4u x; x.x = w.x; x.y = w.y; x.z = w.z; x.w = w.w;
-            *(gv4u *) lfr_addr<PIX, G>(P, sbx, sby, p, r, k) = x;
-        }
-        if (c + 1 == ncols) {                   // the row's last SB: its bottom rows are final
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (lane == 0) __hip_atomic_store((gu32 *) &progress[s_task], ncols, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (c + 1 == ncols) {               // the row's last SB: its bottom rows are final
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (ml == 0) __hip_atomic_store((gu32 *) &progress[s_task], ncols, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
         }
     }
-    // the last workgroup to finish resets the counters (every ticket is taken by then)
+    // the last workgroup to finish resets the counters (every ticket is taken by then);
+    // the store wave's last progress store has completed before this barrier
+    __syncthreads();
     if (lane == 0) s_last = atomicAdd(&ctr[1], 1u) == (uint32_t) ntasks - 1;
     __syncthreads();
     if (s_last) {
@@ -1811,8 +1827,8 @@ template <typename PIX, class G>
 static void launch_lfr_g(hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs, const FrameDesc *frames, uint32_t *ctr)
 {
     static const bool pf = getenv("VP9HIP_LFR_PF") && atoi(getenv("VP9HIP_LFR_PF"));
-    if (pf) hipLaunchKernelGGL((k_lfr<PIX, G, true>), dim3(ntasks), dim3(LfNT<G>::NT), 0, st, tasks, recs, frames, ctr, ntasks);
-    else    hipLaunchKernelGGL((k_lfr<PIX, G, false>), dim3(ntasks), dim3(LfNT<G>::NT), 0, st, tasks, recs, frames, ctr, ntasks);
+    if (pf) hipLaunchKernelGGL((k_lfr<PIX, G, true>), dim3(ntasks), dim3(LfNT<G>::NT + 64), 0, st, tasks, recs, frames, ctr, ntasks);
+    else    hipLaunchKernelGGL((k_lfr<PIX, G, false>), dim3(ntasks), dim3(LfNT<G>::NT + 64), 0, st, tasks, recs, frames, ctr, ntasks);
 }
 template <typename PIX>
 static void launch_lfr_p(int ss, hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs, const FrameDesc *frames,
