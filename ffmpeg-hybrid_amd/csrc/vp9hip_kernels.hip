@@ -1443,8 +1443,11 @@ __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfr(const uint32_t *__rest
     for (uint32_t c = c0; c < ncols; c++) {
         const int sbx = (int) c;
         const LFRec &rec = recs[T[4 + c - c0]];
+        static_assert(L::PROG / 4 <= NT, "one program word per filtering lane");
+        uint32_t pwv = 0;                       // this SB's program word, loaded with its interior
         if (!mover) {
             if (!PF && c > c0) lfr_issue<PIX, G, NT, NU>(v, P, sbx, sby, lane, false);
+            if (lane < L::PROG / 4) pwv = ((const uint32_t *) rec.prog)[lane];
             // left halo (x < 0): this workgroup's previous tile, read from LDS before the
             // barrier below (SB c0's came from HBM with its interior)
             if (c > c0) {
@@ -1466,7 +1469,7 @@ __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfr(const uint32_t *__rest
         // above is already far enough: then the top halo's loads are issued before the column
         // pass and run under it
         if (!mover) {
-            for (int i = lane; i < L::PROG / 4; i += NT) S.prog[i] = ((const uint32_t *) rec.prog)[i];
+            if (lane < L::PROG / 4) S.prog[lane] = pwv;
 #pragma unroll
             for (int u = 0; u < NU; u++) {
                 const int ci = lane + u * NT;
