@@ -55,6 +55,48 @@ def gop_refs(n, gop):
     return [None if i % gop == 0 else (i - 1, i - 1, i - i % gop) for i in range(n)]
 
 
+def make_frames(v, config, nframes=None, rank=0, chroma="420", **kw):
+    """The synthetic pass-1 packets of a BASELINE config exactly as the bench stages them:
+    (frames, refs, (W, H, BPP, log2 tile cols, gop)). refs[i] = (LAST, GOLDEN, ALTREF)
+    buffer ids or None (keyframes); frame i writes buffer i. Extra synth params in kw."""
+    import concurrent.futures    # the C generator releases the GIL: frames in parallel
+    cidx, W, H, BPP, log2, gop, nf = CONFIGS[config]
+    n = nf if nframes is None else nframes
+    refs = gop_refs(n, gop)
+    ssh, ssv = CHROMA[chroma]
+    with concurrent.futures.ThreadPoolExecutor(min(16, os.cpu_count() or 1)) as ex:
+        frames = list(ex.map(lambda i: v.SynthFrame(v.synth_params(
+            W, H, BPP, seed=frame_seed(rank, i, cidx), log2_tile_cols=log2,
+            inter=int(refs[i] is not None), ss_h=ssh, ss_v=ssv, **kw)), range(n)))
+    return frames, refs, (W, H, BPP, log2, gop)
+
+
+def oracle_frames(v, oracle, frames, refs, geom, chroma="420", count=None, keep=None):
+    """Decode frames 0..count-1 with the CPU oracle (test infrastructure) in decode order,
+    yielding (i, planes). Only frames later ones reference are kept in memory."""
+    W, H, BPP, _, gop = geom
+    ssh, ssv = CHROMA[chroma]
+    outs = {}
+    n = len(frames) if count is None else min(count, len(frames))
+    for i in range(n):
+        out = v.alloc_planes(W, H, BPP, ssh, ssv)
+        r = refs[i]
+        oracle.decode_frame(frames[i].pkt, out, None if r is None else [outs[r[0]], outs[r[1]], outs[r[2]]])
+        outs[i] = out
+        for k in [k for k in outs if k < i - gop]:     # keep only what later frames reference
+            del outs[k]
+        yield i, out
+
+
+def compare_frame(v, got, ref, geom, chroma="420"):
+    """Number of visible samples that differ between two frames' planes (0 = bit-exact)."""
+    import numpy as np
+    W, H = geom[0], geom[1]
+    ssh, ssv = CHROMA[chroma]
+    return sum(int(np.count_nonzero(a != b))
+               for a, b in zip(v.visible(got, W, H, ssh, ssv), v.visible(ref, W, H, ssh, ssv)))
+
+
 def reduce_elapsed(elapsed, dist):
     """Max over ranks of the timed region (the slowest rank defines the job time)."""
     if dist is None:
@@ -80,6 +122,7 @@ def main():
     ap.add_argument("--frames", type=int, default=None, help="frames per GPU (default: the config's)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--verify-all", action="store_true", help="compare every timed frame with the oracle")
     ap.add_argument("--timed-events", action="store_true",
                     help="per-launch HIP events inside the timed steps (no graph replay)")
     ap.add_argument("--chroma", choices=sorted(CHROMA), default="420",
@@ -103,14 +146,9 @@ def main():
     cidx, W, H, BPP, LOG2_TILE_COLS, gop, nf = CONFIGS[args.config]
     if args.frames is None:
         args.frames = nf
-    refs = gop_refs(args.frames, gop)
     t0 = time.time()
     ssh, ssv = CHROMA[args.chroma]
-    import concurrent.futures    # the C generator releases the GIL: frames in parallel
-    with concurrent.futures.ThreadPoolExecutor(min(16, os.cpu_count() or 1)) as ex:
-        frames = list(ex.map(lambda i: v.SynthFrame(v.synth_params(
-            W, H, BPP, seed=frame_seed(rank, i, cidx), log2_tile_cols=LOG2_TILE_COLS,
-            inter=int(refs[i] is not None), ss_h=ssh, ss_v=ssv)), range(args.frames)))
+    frames, refs, geom = make_frames(v, args.config, args.frames, rank, args.chroma)
     t_gen = time.time() - t0
 
     dev = v.Device(local_rank)
@@ -190,6 +228,14 @@ def main():
         "kernel_ms": {k: round(ksum[k][0] / args.steps, 3) for k in ksum},
     }
 
+    # bit-exactness of the timed frames: the CPU-baseline leg's oracle frames are compared
+    # with the device's (the first frames in decode order; all when the sample covers them)
+    cpu, verify = None, None
+    if rank == 0 and world == 1:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle  # checker + CPU baseline leg only: the scalar C restatement
+        cpu, verify = cpu_baseline(v, oracle, dev, frames, refs, geom, args)
+
     host = e2e = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sample = encode_sample(v, frames, gop, min(len(frames), max(gop, 16)))
@@ -207,27 +253,6 @@ def main():
         e2e["low_rate"] = e2e_rate(v, lsample, args, local_rank)
         e2e["low_rate"]["bytes_per_frame"] = int(sum(len(d) for g in lsample for d in g) / nlow)
         e2e["low_rate"]["host_parse"] = host_entropy_rate(v, lsample, gop, args)["fps_threads"]
-
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle  # CPU baseline leg only: the scalar C restatement, timed
-        outs = {}
-        n = 0
-        t0 = time.perf_counter()
-        while n < len(frames) and (time.perf_counter() - t0 < args.cpu_seconds or n < 2):
-            out = v.alloc_planes(W, H, BPP, ssh, ssv)
-            r = refs[n]
-            oracle.decode_frame(frames[n].pkt, out, None if r is None else [outs[r[0]], outs[r[1]], outs[r[2]]])
-            outs[n] = out
-            for k in [k for k in outs if k < n - gop]:     # keep only what later frames reference
-                del outs[k]
-            n += 1
-        dt = time.perf_counter() - t0
-        cpu = {"value": round(n / dt, 3), "unit": "frames/s", "cores": 1, "kind": "port",
-               "sample": "%d of the %d %s frames (in decode order), scalar C oracle, reconstruction + loop filter "
-                         "from the same pass-1 packets (host entropy decode excluded), 1 thread"
-                         % (n, len(frames), args.config)}
 
     out = {
         "metric": "decoded frames/sec (bit-exact) 4K VP9 Profile-0 @ 1/2/4/8 MI355X; % HBM roofline",
@@ -247,6 +272,8 @@ def main():
                    "host_gen_s": round(t_gen, 2), "host_stage_s": round(t_stage, 2)},
         "roofline": roofline,
         "cpu_baseline": cpu,
+        "verify": verify,
+        "verified_frames": verify["frames"] if verify else 0,
         "host_entropy": host,
         "e2e_decoder": e2e,
     }
@@ -256,6 +283,97 @@ def main():
         dev.close()
     if dist is not None:
         dist.destroy_process_group()
+    if verify and verify["mismatched"]:
+        sys.exit("bench: %d timed frames differ from the oracle: %s" % (len(verify["mismatched"]), verify["mismatched"]))
+
+
+def cpu_info():
+    """The host the CPU legs ran on: nproc, the CPU share used, the lscpu model name."""
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "threads_used": min(16, os.cpu_count() or 1), "model": model}
+
+
+def cpu_baseline(v, oracle, dev, frames, refs, geom, args):
+    """CPU baseline legs on this box's host cores, and the bit-exactness
+    check of the timed frames. Leg 1: the scalar C oracle on 1 thread over a bounded sample
+    in decode order; every frame it decodes is compared with the device's frame (downloads
+    and compares are outside the CPU timer). Leg 2: frame-parallel over the box's CPU share
+    (16 threads): independent keyframes (C3/C4) or independent GOP chains (C2/C5), one
+    oracle decode per thread (ctypes releases the GIL). Returns (cpu_baseline, verify)."""
+    import concurrent.futures
+    W, H, BPP, log2, gop = geom
+    bounded = not args.no_cpu_baseline
+    budget = args.cpu_seconds if bounded else 0.0
+    want = len(frames) if args.verify_all else (2 if not bounded else len(frames))
+    t_or, n, checked, bad = 0.0, 0, 0, []
+    gen = oracle_frames(v, oracle, frames, refs, geom, args.chroma)
+    while n < want:
+        t0 = time.perf_counter()
+        item = next(gen, None)
+        t_or += time.perf_counter() - t0
+        if item is None:
+            break
+        i, out = item
+        n += 1
+        d = compare_frame(v, dev.download(i), out, geom, args.chroma)
+        checked += 1
+        if d:
+            bad.append([i, d])
+        if not args.verify_all and n >= 2 and t_or >= budget:
+            break
+    verify = {"frames": checked, "of": len(frames), "mismatched": bad,
+              "what": "visible Y/U/V of frames 0..%d (decode order) after the timed steps vs the CPU oracle, "
+                      "sample-exact" % (checked - 1)}
+    if not bounded:
+        return None, verify
+    one = n / t_or
+    info = cpu_info()
+    thr = info["threads_used"]
+    # leg 2: frame-parallel (keyframes) / GOP-parallel (inter streams) over thr threads
+    if gop == 1:
+        units = [[i] for i in range(len(frames))]
+    else:
+        units = [list(range(g, min(len(frames), g + gop))) for g in range(0, len(frames), gop)]
+    per_unit = len(units[0]) / one
+    reps = max(1, int(budget / 2 * thr / max(per_unit * len(units), 1e-9)) + 1)
+    work = (units * reps)[:max(thr, int(budget / 2 * thr / per_unit) + 1)]
+    ssh, ssv = CHROMA[args.chroma]
+
+    def run_unit(idx):
+        outs = {}
+        for i in idx:
+            out = v.alloc_planes(W, H, BPP, ssh, ssv)
+            r = refs[i]
+            oracle.decode_frame(frames[i].pkt, out, None if r is None else [outs[r[0]], outs[r[1]], outs[r[2]]])
+            outs[i] = out
+            for k in [k for k in outs if k < i - 1 and k != idx[0]]:
+                del outs[k]
+        return len(idx)
+
+    with concurrent.futures.ThreadPoolExecutor(thr) as ex:
+        t0 = time.perf_counter()
+        done = sum(ex.map(run_unit, work))
+        par = done / (time.perf_counter() - t0)
+    legs = [
+        {"leg": "1 thread", "value": round(one, 3), "cores": 1,
+         "sample": "%d frames in decode order" % n},
+        {"leg": "%s-parallel" % ("frame" if gop == 1 else "GOP"), "value": round(par, 3), "cores": thr,
+         "sample": "%d %s on %d threads" % (len(work), "keyframes" if gop == 1 else "GOP chains", thr)},
+    ]
+    cpu = {"value": round(par, 3), "unit": "frames/s", "cores": thr, "kind": "port",
+           "sample": "%s %s frames, scalar C oracle (reconstruction + loop filter from the same pass-1 packets, "
+                     "host entropy decode excluded), %s-parallel over %d of the %s host threads"
+                     % (len(work) if gop == 1 else sum(len(u) for u in work), args.config,
+                        "frame" if gop == 1 else "GOP", thr, info["nproc"]),
+           "legs": legs, "host": info}
+    return cpu, verify
 
 
 def encode_sample(v, frames, gop, n):
