@@ -1,0 +1,836 @@
+// Device planner (gfx950): the per-frame work planning of the pixel path, from the pass-1
+// packets resident in HBM to the records the pixel kernels consume (vp9hip_work.h). It
+// replaces, on the GPU, the host planner of vp9hip_runtime.cpp and applies the same rules
+// (vp9hip_planlogic.h), so a batch needs nothing from the host between its packets and its
+// frames except the launch list, which depends on the record counts only.
+//
+//   k_pblk   one thread per block: the SB slot of each block, the slots' block ranges,
+//            decode-order validation, eob entries per block
+//   (scan)   eob entries -> each block's first eob
+//   k_psb    one wave per SB: per-tx eobs -> coefficient total, residual-job counts per
+//            (tcode, txtp), MC-unit count, the intra 4x4-unit map
+//   (scan)   coefficients (decode order) -> each SB's first coefficient; counts -> record offsets
+//   k_plan   one wave per SB: intra jobs with check_intra_mode resolved (vp9recon.c:37-221)
+//            and their producers, heights, list-scheduled passes (the host's merge_mixed,
+//            restated wave-parallel), residual jobs, MC units (vp9_mc_template.c:30-464),
+//            the LF program (vp9block.c:1142-1262, vp9lpf.c:31-230), the SB's intra step
+//   k_plevel one workgroup per level-scheduled inter frame: SB dependency levels along
+//            anti-diagonals
+//   k_pkeys  step-list offsets; the launch summary the host reads back
+//   k_plists the intra step lists
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <stdint.h>
+
+#include "vp9hip_plan.h"
+
+#define DEV __device__ __forceinline__
+
+namespace {
+
+DEV uint32_t wscan_incl(uint32_t v, int lane)
+{
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t t = __shfl_up(v, d);
+        if (lane >= d) v += t;
+    }
+    return v;
+}
+DEV uint32_t wsum(uint32_t v)
+{
+#pragma unroll
+    for (int d = 32; d; d >>= 1) v += __shfl_xor(v, d);
+    return v;
+}
+DEV uint32_t mbcnt(uint64_t m)
+{
+    return __builtin_amdgcn_mbcnt_hi((uint32_t) (m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) m, 0));
+}
+// Bounds guard of every planner write: false (and a status bit) when i >= cap.
+DEV bool inb(const PlanDev &D, uint32_t i, uint32_t cap, uint32_t bit)
+{
+    if (i < cap) return true;
+    atomicOr(&D.status[1], bit);
+    atomicOr(&D.status[0], PLS_BOUNDS);
+    return false;
+}
+DEV void wsync()
+{
+    __syncthreads();      // one-wave workgroups: orders the wave's LDS accesses
+}
+
+// A block as the planner uses it: fields out of range are clamped (the batch fails with
+// PLS_BLOCK / PLS_MODE from k_pblk / k_psb, and every later index stays in bounds).
+DEV vp9h_block load_block(const vp9h_block *g)
+{
+    vp9h_block b = *g;
+    if (b.bs >= VP9H_N_BS) b.bs = VP9H_BS_4x4;
+    if (b.tx > 3) b.tx = 0;
+    if (b.uvtx > 3) b.uvtx = 0;
+    return b;
+}
+DEV bool block_ok(const vp9h_block &b)
+{
+    return b.bs < VP9H_N_BS && b.tx <= 3 && b.uvtx <= 3;
+}
+
+// Per (block, plane) tx-block counts, packed all | eob << 10 | intra jobs << 20, and their
+// exclusive scan over the SB's blocks in decode order (pre[3 * nb] = totals).
+template <int SSH, int SSV>
+DEV uint32_t sb_prefix(const vp9h_block *blk, int nb, int cols, int rows, bool mine, uint32_t *pre, int lane)
+{
+    uint32_t v[3] = { 0, 0, 0 };
+    if (lane < nb) {
+        const vp9h_block &b = blk[lane];
+        for (int p = 0; p < 3; p++) {
+            const PlTxGrid g = pl_txgrid(b, p, cols, rows, SSH, SSV);
+            const uint32_t n = (uint32_t) (g.nx * g.ny);
+            v[p] = n | (b.skip ? 0u : n) << 10 | (b.intra && mine ? n : 0u) << 20;
+        }
+    }
+    const uint32_t sum = v[0] + v[1] + v[2];
+    const uint32_t incl = wscan_incl(sum, lane), excl = incl - sum;
+    if (lane < nb) {
+        pre[3 * lane] = excl;
+        pre[3 * lane + 1] = excl + v[0];
+        pre[3 * lane + 2] = excl + v[0] + v[1];
+    }
+    const uint32_t tot = __shfl(incl, 63);
+    if (lane == 0) pre[3 * nb] = tot;
+    wsync();
+    return tot;
+}
+
+// (block, plane) entry of tx t: the largest k with all-prefix(k) <= t
+DEV int sb_locate(const uint32_t *pre, int n3, uint32_t t)
+{
+    int lo = 0, hi = n3 - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if ((pre[mid] & 1023) <= t) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+struct Tx {
+    int b, p, k;            // block, plane, (block, plane) entry
+    int l, x, y;            // index in the plane's tx grid, position (4x4 units in the block)
+    PlTxGrid g;
+};
+template <int SSH, int SSV>
+DEV Tx sb_tx(const vp9h_block *blk, const uint32_t *pre, int nb, uint32_t t, int cols, int rows)
+{
+    Tx r;
+    r.k = sb_locate(pre, 3 * nb, t);
+    r.b = r.k / 3;
+    r.p = r.k - 3 * r.b;
+    r.l = (int) (t - (pre[r.k] & 1023));
+    r.g = pl_txgrid(blk[r.b], r.p, cols, rows, SSH, SSV);
+    const int nx = r.g.nx > 0 ? r.g.nx : 1;
+    r.x = (r.l % nx) << r.g.txs;
+    r.y = (r.l / nx) << r.g.txs;
+    return r;
+}
+
+// The eob of tx t (0 for skipped blocks), range-checked against the packet.
+DEV int tx_eob(const PlanDev &D, const vp9h_block &b, const Tx &tx, const uint32_t *pre, uint32_t b0, uint32_t &st)
+{
+    if (b.skip) return 0;
+    const uint32_t i = D.blk_eob0[b0 + tx.b] + ((pre[tx.k] & 1023) - (pre[3 * tx.b] & 1023)) + (uint32_t) tx.l;
+    if (i >= D.total_eobs) { st |= PLS_EOB; return 0; }
+    const int e = D.eobs[i];
+    if (e > (16 << (2 * tx.g.txs))) { st |= PLS_EOB; return 0; }
+    return e;
+}
+
+DEV int tx_mode(const vp9h_block &b, const Tx &tx, uint32_t &st)
+{
+    const int m = tx.p ? b.uvmode : b.mode[b.bs > VP9H_BS_8x8 && b.tx == 0 ? tx.y * 2 + tx.x : 0];
+    if (m > 9) { st |= PLS_MODE; return 0; }
+    return m;
+}
+
+DEV bool mc_refs_ok(const vp9h_block &b, const PlMcGeo &g)
+{
+    if (b.ref[0] > 2 || (b.comp && b.ref[1] > 2)) return false;
+    const int r1 = b.comp ? b.ref[1] : b.ref[0];
+    return g.scale[b.ref[0]][0] != 0xFFFF && g.scale[r1][0] != 0xFFFF;
+}
+
+DEV uint32_t cnt_idx(const PlanDev &D, const PlanFrame &F, uint32_t seg, uint32_t slot, int tc, int tp)
+{
+    return D.seg_pre4[seg] + (uint32_t) tc * F.s4 + (uint32_t) tp * D.seg_sz[seg] + D.slot_pos[slot];
+}
+
+struct SbGeo {
+    int sbx, sby, tile_sb0, mine;
+    uint32_t slot, seg, dord;
+};
+DEV SbGeo sb_geo(const PlanFrame &F, int s)
+{
+    SbGeo G;
+    G.sbx = s % F.sb_cols;
+    G.sby = s / F.sb_cols;
+    const int tile = pl_tile_of(G.sbx, F.sb_cols, F.log2_tc, &G.tile_sb0);
+    G.mine = tile >= F.tile_lo && tile < F.tile_hi;
+    G.slot = F.slot0 + (uint32_t) s;
+    G.seg = F.seg0 + (F.by_diag ? (uint32_t) ((G.sbx - G.tile_sb0) + G.sby) : 0u);
+    G.dord = F.slot0 + (uint32_t) pl_sb_dorder(G.sbx, G.sby, F.sb_cols);
+    return G;
+}
+
+// The SB's block range; 0 blocks if it has none (the batch is already marked invalid).
+DEV int sb_blocks(const PlanDev &D, uint32_t slot, uint32_t &b0, uint32_t &st)
+{
+    b0 = D.sb_first[slot];
+    const uint32_t b1 = D.sb_end[slot];
+    if (b0 == 0xffffffffu || b1 == 0xffffffffu || b1 <= b0 || b1 > D.total_blocks) { st |= PLS_ORDER; b0 = 0; return 0; }
+    if (b1 - b0 > 64) { st |= PLS_ORDER; return 64; }
+    return (int) (b1 - b0);
+}
+
+// ------------------------------------------------------------------ k_pblk
+__global__ __launch_bounds__(256) void k_pblk(PlanDev D)
+{
+    const PlanFrame &F = D.frames[blockIdx.y];
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= F.nblk) return;
+    const uint32_t gi = F.blk0 + i;
+    const int cols = F.mc.cols, rows = F.mc.rows;
+    auto sb_of = [&](const vp9h_block &b, int &dord) {
+        const int sbx = pl_min(b.col, cols - 1) >> 3, sby = pl_min(b.row, rows - 1) >> 3;
+        dord = pl_sb_dorder(sbx, sby, F.sb_cols);
+        return F.slot0 + (uint32_t) (sby * F.sb_cols + sbx);
+    };
+    const vp9h_block raw = D.blocks[gi];
+    uint32_t st = 0;
+    if (!block_ok(raw) || raw.row >= rows || raw.col >= cols) st |= PLS_BLOCK;
+    const vp9h_block b = load_block(&D.blocks[gi]);
+    int d, dp = -1, dn = -1;
+    const uint32_t slot = sb_of(b, d);
+    uint32_t sp = 0xffffffffu, sn = 0xffffffffu;
+    if (i > 0) sp = sb_of(load_block(&D.blocks[gi - 1]), dp);
+    if (i + 1 < F.nblk) sn = sb_of(load_block(&D.blocks[gi + 1]), dn);
+    if (!inb(D, slot, D.nslots, 1u)) return;
+    if (sp != slot) {
+        D.sb_first[slot] = gi;
+        if (i > 0 && dp >= d) st |= PLS_ORDER;       // SBs in decode order, each one contiguous
+    }
+    if (sn != slot) D.sb_end[slot] = gi + 1;
+    uint32_t n = 0;
+    if (!b.skip)
+        for (int p = 0; p < 3; p++) {
+            const PlTxGrid g = pl_txgrid(b, p, cols, rows, F.mc.ss_h, F.mc.ss_v);
+            n += (uint32_t) (g.nx * g.ny);
+        }
+    D.blk_neob[gi] = n;
+    if (st) atomicOr(D.status, st);
+}
+
+// ------------------------------------------------------------------ k_psb
+template <int SSH, int SSV>
+__global__ __launch_bounds__(64) void k_psb(PlanDev D)
+{
+    constexpr int CW = 16 >> SSH, CH = 16 >> SSV, JCAP = 256 + 2 * CW * CH;
+    __shared__ vp9h_block blk[64];
+    __shared__ uint32_t pre[3 * 64 + 1];
+    __shared__ uint32_t kc[24];
+    __shared__ uint32_t ib[24];
+    const PlanFrame &F = D.frames[blockIdx.y];
+    const int s = blockIdx.x, lane = threadIdx.x;
+    if (s >= F.sb_cols * F.sb_rows) return;
+    const SbGeo G = sb_geo(F, s);
+    const int cols = F.mc.cols, rows = F.mc.rows;
+    uint32_t st = 0, b0;
+    const int nb = sb_blocks(D, G.slot, b0, st);
+    if (lane < 24) { kc[lane] = 0; ib[lane] = 0; }
+    if (lane < nb) {
+        const vp9h_block b = load_block(&D.blocks[b0 + lane]);
+        blk[lane] = b;
+    }
+    wsync();
+    const uint32_t tot = sb_prefix<SSH, SSV>(blk, nb, cols, rows, G.mine, pre, lane);
+    const uint32_t T = pl_min((int) (tot & 1023), JCAP);
+    uint32_t ncoef = 0;
+    for (uint32_t t = lane; t < T; t += 64) {
+        const Tx tx = sb_tx<SSH, SSV>(blk, pre, nb, t, cols, rows);
+        const vp9h_block &b = blk[tx.b];
+        const int e = tx_eob(D, b, tx, pre, b0, st);
+        ncoef += (uint32_t) e;
+        int txtp = 0;
+        if (b.intra) {
+            const int mode = tx_mode(b, tx, st);
+            txtp = tx.p || tx.g.txs == 3 ? 0 : pl_intra_txfm_type(mode);
+        }
+        if (e && G.mine) atomicAdd(&kc[(F.lossless ? 4 : tx.g.txs) * 4 + txtp], 1u);
+        if (b.intra && G.mine) {            // the job's 4x4 units in the SB plane's unit map
+            const int sh = tx.p ? SSH : 0, sv = tx.p ? SSV : 0;
+            const int units = 16 >> sh, unitsv = 16 >> sv;
+            const int ux0 = ((tx.g.bx - G.sbx * (64 >> sh)) >> 2) + tx.x, uy0 = ((tx.g.by - G.sby * (64 >> sv)) >> 2) + tx.y;
+            for (int v = uy0; v < uy0 + tx.g.step && v < unitsv; v++) {
+                uint32_t m = 0;
+                for (int u = ux0; u < ux0 + tx.g.step && u < units; u++) m |= 1u << u;
+                atomicOr(&ib[tx.p * 8 + (v >> 1)], m << ((v & 1) * 16));
+            }
+        }
+    }
+    // MC units of the SB's inter blocks
+    uint32_t nmc = 0;
+    if (lane < nb && G.mine && !blk[lane].intra) {
+        if (mc_refs_ok(blk[lane], F.mc)) nmc = (uint32_t) pl_mc_block(blk[lane], F.mc, 0, [](const McUnit &) {});
+        else st |= PLS_REF;
+    }
+    nmc = wsum(nmc);
+    ncoef = wsum(ncoef);
+    wsync();
+    if (lane < 20) {
+        const uint32_t ci = cnt_idx(D, F, G.seg, G.slot, lane >> 2, lane & 3);
+        if (inb(D, ci, D.cap_cnt, 2u)) D.cnt[ci] = kc[lane];
+    }
+    if (lane == 20) {
+        const uint32_t ci = D.seg_pre1[G.seg] + D.slot_pos[G.slot];
+        if (inb(D, ci, D.cap_cntm, 2u)) D.cntm[ci] = nmc;
+    }
+    if (lane < 24 && inb(D, G.slot, D.nslots, 4u)) D.ibits[(size_t) G.slot * 24 + lane] = ib[lane];
+    if (lane == 0 && inb(D, G.dord, D.nslots, 8u)) D.sb_ncoef[G.dord] = ncoef;
+    if (st) atomicOr(D.status, st);
+}
+
+// ------------------------------------------------------------------ k_plan
+template <int JCAP> struct PlanLds {
+    vp9h_block blk[64];
+    uint32_t pre[3 * 64 + 1];
+    uint16_t et[JCAP];            // eob per tx (decode order)
+    uint16_t co[JCAP];            // SB-relative first coefficient per tx
+    uint32_t ja[JCAP];            // PJob word per intra job (decode order)
+    uint8_t  jx[JCAP];            // 4x4 top-right inside the block (trx)
+    uint16_t jmap[3][256];        // producing job of each 4x4 unit
+    uint16_t doff[JCAP + 1];      // producers of job j: dep[doff[j] .. doff[j + 1])
+    uint16_t dep[4 * JCAP];
+    uint32_t hgt[JCAP];           // longest path to a sink (list-scheduling priority)
+    uint16_t ord[JCAP];           // jobs by (height desc, index asc)
+    uint16_t sch[JCAP];           // pass of each job (0xffff: not yet)
+    uint32_t hs[64];              // height histogram -> list starts
+    uint32_t lfm[2][2][8];        // LF masks [cls][dir][row]: kinds 0..3 in bytes
+    uint8_t  lfl[64];             // LF level of each 8x8
+    uint32_t prog[LF_PROG_BYTES / 4];
+    uint16_t tk[16];              // jobs taken by the pass being built
+};
+
+// edges the job's (substituted) mode reads: 1 left, 2 top, 4 top-left, 8 top-right (pl_intra_job)
+DEV uint32_t needs_of(uint32_t a)
+{
+    const uint8_t needs[16] = { 2, 1, 2 | 8, 1 | 2 | 4, 1 | 2 | 4, 1 | 2 | 4, 2 | 8, 1, 1 | 2 | 4, 1 | 2, 1, 2, 0, 0, 0, 0 };
+    return needs[(a >> 8) & 15];
+}
+DEV uint32_t wor(uint32_t v)
+{
+#pragma unroll
+    for (int d = 32; d; d >>= 1) v |= __shfl_xor(v, d);
+    return v;
+}
+
+template <int SSH, int SSV>
+__global__ __launch_bounds__(64) void k_plan(PlanDev D)
+{
+    constexpr int CW = 16 >> SSH, CH = 16 >> SSV, JCAP = 256 + 2 * CW * CH;
+    __shared__ PlanLds<JCAP> S;
+    const PlanFrame &F = D.frames[blockIdx.y];
+    const int s = blockIdx.x, lane = threadIdx.x;
+    if (s >= F.sb_cols * F.sb_rows) return;
+    const SbGeo G = sb_geo(F, s);
+    const int cols = F.mc.cols, rows = F.mc.rows;
+    const uint32_t slot = G.slot;
+    uint32_t st = 0, b0;
+    const int nb = sb_blocks(D, slot, b0, st);
+    st = 0;                                   // reported by k_psb
+    if (lane < nb) S.blk[lane] = load_block(&D.blocks[b0 + lane]);
+    for (int i = lane; i < 3 * 256; i += 64) (&S.jmap[0][0])[i] = 0xffff;
+    if (lane < 32) (&S.lfm[0][0][0])[lane] = 0;
+    S.lfl[lane] = 0;
+    for (int i = lane; i < LF_PROG_BYTES / 4; i += 64) S.prog[i] = 0;
+    wsync();
+    const uint32_t tot = sb_prefix<SSH, SSV>(S.blk, nb, cols, rows, G.mine, S.pre, lane);
+    const int T = pl_min((int) (tot & 1023), JCAP), NJ = pl_min((int) (tot >> 20), JCAP);
+
+    // ---- eobs and SB-relative coefficient offsets (decode order)
+    for (int t = lane; t < T; t += 64) {
+        const Tx tx = sb_tx<SSH, SSV>(S.blk, S.pre, nb, (uint32_t) t, cols, rows);
+        S.et[t] = (uint16_t) tx_eob(D, S.blk[tx.b], tx, S.pre, b0, st);
+    }
+    wsync();
+    {
+        uint32_t carry = 0;
+        for (int c = 0; c < T; c += 64) {
+            const uint32_t v = c + lane < T ? S.et[c + lane] : 0u;
+            const uint32_t incl = wscan_incl(v, lane);
+            if (c + lane < T) S.co[c + lane] = (uint16_t) (carry + incl - v);
+            carry += __shfl(incl, 63);
+        }
+    }
+    // record bases of the SB: lanes 0..19 residual keys (tcode * 4 + txtp), lane 20 MC units
+    uint32_t rb = 0;
+    if (lane < 20) {
+        const uint32_t ci = cnt_idx(D, F, G.seg, slot, lane >> 2, lane & 3);
+        rb = inb(D, ci, D.cap_cnt, 16u) ? D.cnt0[ci] : 0u;
+    } else if (lane == 20) {
+        const uint32_t ci = D.seg_pre1[G.seg] + D.slot_pos[slot];
+        rb = inb(D, ci, D.cap_cntm, 16u) ? D.cntm0[ci] : 0u;
+    }
+    const uint32_t coef_sb = inb(D, G.dord, D.nslots, 32u) ? D.sb_coef0[G.dord] : 0u;
+    const uint32_t rbase = slot * D.rcap;
+    unsigned long long ibytes = 0, mbytes = 0;
+    wsync();
+
+    // ---- residual jobs (every coded tx block) and intra jobs with their unit map
+    const int tx0l = G.tile_sb0 * 64;
+    for (int c = 0; c < T; c += 64) {
+        const int t = c + lane;
+        int key = -1;
+        RJob r;
+        if (t < T) {
+            const Tx tx = sb_tx<SSH, SSV>(S.blk, S.pre, nb, (uint32_t) t, cols, rows);
+            const vp9h_block &b = S.blk[tx.b];
+            const int p = tx.p, sh = p ? SSH : 0, sv = p ? SSV : 0, txs = tx.g.txs;
+            const int e0 = S.et[t];
+            int mode = 0, txtp = 0;
+            if (b.intra) {
+                mode = tx_mode(b, tx, st);
+                txtp = p || txs == 3 ? 0 : pl_intra_txfm_type(mode);
+            }
+            const int tcode = F.lossless ? 4 : txs;
+            const int ux0 = ((tx.g.bx - G.sbx * (64 >> sh)) >> 2) + tx.x, uy0 = ((tx.g.by - G.sby * (64 >> sv)) >> 2) + tx.y;
+            const uint32_t roff = rbase + pl_resid_unit(p, ux0, uy0, SSH, SSV);
+            if (e0 && G.mine) {
+                uint32_t coef = coef_sb + S.co[t];
+                int e = e0;
+                if (coef + (uint32_t) e > D.total_coefs) { st |= PLS_COEF; e = 0; coef = 0; }
+                r.coef = coef;
+                r.eob = (uint16_t) e;
+                r.frame = (uint16_t) F.frame;
+                r.ptx = (uint8_t) (p | tcode << 2 | (b.intra ? 0 : 1) << 5 | txtp << 6);
+                r.nzc = D.nz[(((tcode * 4 + txtp) * 1025) + e) * 2];
+                r.nzr = D.nz[(((tcode * 4 + txtp) * 1025) + e) * 2 + 1];
+                r.pad = 0;
+                if (b.intra) r.dst = roff;
+                else {
+                    r.dst = (uint32_t) ((size_t) (tx.g.by + tx.y * 4) * F.pitch[p ? 1 : 0] + tx.g.bx + tx.x * 4);
+                    ibytes += (unsigned long long) (2 * (16 << (2 * txs)) * F.bypp);
+                }
+                key = tcode * 4 + txtp;
+            }
+            if (b.intra && G.mine) {
+                const int j = (int) (S.pre[tx.k] >> 20) + tx.l;
+                const int pw8 = p ? cols * 8 >> SSH : cols * 8, ph8 = p ? rows * 8 >> SSV : rows * 8;
+                const PlIntra pi = pl_intra_job(p, txs, mode, e0, tx.g.bx + tx.x * 4, tx.g.by + tx.y * 4, tx.x, tx.g.pw4,
+                                                p ? tx0l >> SSH : tx0l, pw8, ph8, ux0, uy0);
+                if (j < JCAP) {
+                    S.ja[j] = pi.a;
+                    S.jx[j] = (uint8_t) pi.trx;
+                    const int units = 16 >> sh, unitsv = 16 >> sv;
+                    for (int v = uy0; v < uy0 + tx.g.step && v < unitsv; v++)
+                        for (int u = ux0; u < ux0 + tx.g.step && u < units; u++) S.jmap[p][v * 16 + u] = (uint16_t) j;
+                }
+            }
+        }
+        // ranks within each key, in decode order: one ballot per distinct key of the chunk
+        uint64_t pend = __ballot(key >= 0);
+        uint32_t pos = 0;
+        while (pend) {
+            const int l0 = __builtin_ctzll(pend);
+            const int kk = __shfl(key, l0);
+            const uint64_t m = __ballot(key == kk);
+            const uint32_t base = __shfl(rb, kk);
+            if (key == kk) pos = base + mbcnt(m);
+            if (lane == kk) rb += (uint32_t) __popcll(m);
+            pend &= ~m;
+        }
+        if (key >= 0 && inb(D, pos, D.cap_rjobs, 64u)) D.rjobs[pos] = r;
+    }
+    wsync();
+
+    // ---- producers of every intra job (the pixels its substituted mode reads)
+    auto deps_of = [&](int j, auto fn) {
+        const uint32_t a = S.ja[j];
+        const int p = a & 3, ts = (a >> 2) & 3, ux0 = (a >> 12) & 15, uy0 = (a >> 16) & 15;
+        const int units = p ? CW : 16, unitsv = p ? CH : 16;
+        int last = -1, first = -1;
+        // producers of a run of units are consecutive; only the top-left unit's producer can
+        // recur in the left-column run
+        const int nd = (int) needs_of(a);
+        bool left_run = false;
+        pl_local_reads(ux0, uy0, 1 << ts, nd, S.jx[j], units, unitsv, [&](int unit) {
+            const int d = S.jmap[p][unit];
+            const bool is_left = (unit & 15) == ux0 - 1 && (unit >> 4) >= uy0;
+            if (is_left && !left_run) { left_run = true; last = -1; }
+            if (d == 0xffff || d >= j || d == last || (left_run && d == first)) { if (d != 0xffff && d < j) last = d; return; }
+            if (!left_run && first < 0) first = d;
+            last = d;
+            fn(d);
+        });
+    };
+    {
+        uint32_t carry = 0;
+        for (int c = 0; c < NJ; c += 64) {
+            const int j = c + lane;
+            uint32_t n = 0;
+            if (j < NJ) deps_of(j, [&](int) { n++; });
+            const uint32_t incl = wscan_incl(n, lane);
+            if (j < NJ) S.doff[j] = (uint16_t) (carry + incl - n);
+            carry += __shfl(incl, 63);
+        }
+        if (carry > 4 * JCAP) {             // more producers than valid tilings allow: no order
+            st |= PLS_SCHED;
+            for (int j = lane; j <= NJ; j += 64) S.doff[j] = 0;
+            carry = 0;
+        }
+        if (lane == 0) S.doff[NJ] = (uint16_t) carry;
+        wsync();
+        for (int j = lane; j < NJ; j += 64) {
+            int k = S.doff[j];
+            if (carry) deps_of(j, [&](int d) { S.dep[k++] = (uint16_t) d; });
+            S.hgt[j] = 1;
+            S.sch[j] = 0xffff;
+        }
+    }
+    wsync();
+    // ---- heights (longest path to a sink): relax until stable
+    for (int it = 0; it < JCAP + 1; it++) {
+        bool ch = false;
+        for (int c = ((NJ - 1) & ~63); c >= 0; c -= 64) {
+            const int j = c + lane;
+            if (j < NJ) {
+                const uint32_t h1 = S.hgt[j] + 1;
+                for (int k = S.doff[j]; k < S.doff[j + 1]; k++) {
+                    const int d = S.dep[k];
+                    if (S.hgt[d] < h1) { atomicMax(&S.hgt[d], h1); ch = true; }
+                }
+            }
+            wsync();
+        }
+        if (!__any(ch)) break;
+    }
+    // ---- priority order: height descending, then decode order
+    S.hs[lane] = 0;
+    wsync();
+    for (int j = lane; j < NJ; j += 64) atomicAdd(&S.hs[pl_min((int) S.hgt[j], 63)], 1u);
+    wsync();
+    {
+        const uint32_t v = S.hs[63 - lane];                // heights from the top
+        const uint32_t incl = wscan_incl(v, lane);
+        wsync();
+        S.hs[63 - lane] = incl - v;
+        wsync();
+        for (int c = 0; c < NJ; c += 64) {
+            const int j = c + lane;
+            const int h = j < NJ ? pl_min((int) S.hgt[j], 63) : -1;
+            uint64_t pend = __ballot(h >= 0);
+            while (pend) {
+                const int hh = __shfl(h, __builtin_ctzll(pend));
+                const uint64_t m = __ballot(h == hh);
+                const uint32_t base = S.hs[hh];
+                if (h == hh) S.ord[base + mbcnt(m)] = (uint16_t) j;
+                wsync();
+                if (lane == 0) S.hs[hh] = base + (uint32_t) __popcll(m);
+                wsync();
+                pend &= ~m;
+            }
+        }
+    }
+    wsync();
+    // ---- list scheduling (merge_mixed): each pass takes, in priority order, every ready job
+    // (all producers in earlier passes) that still fits in 64 lanes; lane groups by size
+    uint32_t *gpass = D.passes + (size_t) slot * JCAP;
+    PJob *gjob = D.pjobs + (size_t) slot * JCAP;
+    int done = 0, npass = 0, c0 = 0;
+    while (done < NJ) {
+        int budget = 64, ntake = 0;
+        for (int c = c0; c < NJ && budget >= 4; c += 64) {
+            const int pos = c + lane;
+            const int j = pos < NJ ? S.ord[pos] : 0;
+            bool cand = pos < NJ && S.sch[j] == 0xffff;
+            if (cand)
+                for (int k = S.doff[j]; k < S.doff[j + 1]; k++)
+                    if (S.sch[S.dep[k]] >= (uint16_t) npass) { cand = false; break; }
+            const int sz = 4 << ((S.ja[j] >> 2) & 3);
+            for (;;) {
+                const uint64_t m = __ballot(cand && sz <= budget);
+                if (!m) break;
+                const int i0 = __builtin_ctzll(m);
+                const int J = __shfl(j, i0);
+                budget -= __shfl(sz, i0);
+                if (lane == i0) { cand = false; S.sch[J] = (uint16_t) npass; }
+                if (lane == 0) S.tk[ntake] = (uint16_t) J;
+                ntake++;
+            }
+        }
+        wsync();
+        if (ntake == 0) { st |= PLS_SCHED; break; }
+        // emit: sizes 32, 16, 8, 4, take order within a size
+        const int J = lane < ntake ? S.tk[lane] : 0;
+        const int ts = lane < ntake ? (int) ((S.ja[J] >> 2) & 3) : -1;
+        uint32_t cnt[4], at = 0;
+        int mypos = 0;
+        for (int q = 3; q >= 0; q--) {
+            const uint64_t m = __ballot(ts == q);
+            cnt[q] = (uint32_t) __popcll(m);
+            if (ts == q) mypos = (int) (at + mbcnt(m));
+            at += cnt[q];
+        }
+        if (lane < ntake) {
+            const uint32_t a = S.ja[J];
+            PJob pj;
+            pj.a = a;
+            pj.roff = ((a >> 4) & 1) ? rbase + pl_resid_unit(a & 3, (a >> 12) & 15, (a >> 16) & 15, SSH, SSV) : 0u;
+            if (inb(D, (uint32_t) (done + mypos), JCAP, 128u)) gjob[done + mypos] = pj;
+        }
+        if (lane == 0 && inb(D, (uint32_t) npass, JCAP, 256u)) gpass[npass] = (uint32_t) done << 14 | cnt[0] << 9 | cnt[1] << 5 | cnt[2] << 2 | cnt[3];
+        done += ntake;
+        npass++;
+        // skip chunks of the priority order that are fully scheduled
+        while (c0 < NJ) {
+            const int pos = c0 + lane;
+            if (__any(pos < NJ && S.sch[S.ord[pos]] == 0xffff)) break;
+            c0 += 64;
+        }
+        wsync();
+    }
+    if (lane == 0) {
+        SBRec sr;
+        sr.frame = (uint32_t) F.frame; sr.sbx = (uint16_t) G.sbx; sr.sby = (uint16_t) G.sby;
+        sr.tile_x0 = (uint16_t) (G.tile_sb0 << 3);
+        sr.flags = F.intra ? 0 : 1;
+        D.sbs[slot] = sr;
+        WGRec w;
+        w.job0 = slot * JCAP; w.pass0 = slot * JCAP;
+        w.njobs = (uint16_t) done; w.npass = (uint16_t) npass;
+        w.sb[0] = slot;
+        D.wgs[slot] = w;
+    }
+
+    // ---- cross-SB reads of level-scheduled inter frames: left / top / top-left SBs whose
+    // intra units this SB's jobs read (the host's umap levels)
+    uint32_t dmask = 0;
+    if (F.levels && !F.intra)
+        for (int j = lane; j < NJ; j += 64) {
+            const uint32_t a = S.ja[j];
+            const int p = a & 3, ts = (a >> 2) & 3, ux0 = (a >> 12) & 15, uy0 = (a >> 16) & 15;
+            const int units = p ? CW : 16, unitsv = p ? CH : 16;
+            const int fx = G.sbx * units + ux0, fy = G.sby * unitsv + uy0;
+            pl_cross_reads(ux0, uy0, fx, fy, 1 << ts, (int) needs_of(a), S.jx[j], [&](int ux, int uy) {
+                if (ux < 0 || uy < 0 || ux >= F.sb_cols * units) return;
+                const int nx = ux / units, ny = uy / unitsv, u = ux - nx * units, v = uy - ny * unitsv;
+                const uint32_t ns = F.slot0 + (uint32_t) (ny * F.sb_cols + nx);
+                if (!((D.ibits[(size_t) ns * 24 + p * 8 + (v >> 1)] >> ((v & 1) * 16 + u)) & 1)) return;
+                dmask |= nx < G.sbx ? (ny < G.sby ? 8u : 2u) : 4u;      // TL, L, T
+            });
+        }
+    dmask = wor(dmask);
+
+    // ---- MC units (inter blocks in decode order)
+    {
+        const bool mc = lane < nb && G.mine && !S.blk[lane].intra && mc_refs_ok(S.blk[lane], F.mc);
+        const uint32_t n = mc ? (uint32_t) pl_mc_block(S.blk[lane], F.mc, 0, [](const McUnit &) {}) : 0u;
+        const uint32_t incl = wscan_incl(n, lane);
+        uint32_t o = __shfl(rb, 20) + incl - n;
+        if (mc)
+            pl_mc_block(S.blk[lane], F.mc, (uint32_t) F.frame, [&](const McUnit &m) {
+                if (inb(D, o, D.cap_mcs, 512u)) D.mcs[o] = m;
+                o++;
+                mbytes += (unsigned long long) m.w * m.h * F.bypp * (1 + m.nref);
+            });
+    }
+
+    // ---- loop-filter levels, masks and program (vp9block.c:1438-1452, vp9lpf.c:31-230)
+    if (F.filter_level) {
+        if (lane < nb) {
+            const vp9h_block &b = S.blk[lane];
+            if (const int lvl = pl_lf_level(b, F.lflvl, F.filter_level)) {
+                const int bw8 = pl_bwh(1, b.bs, 0), bh8 = pl_bwh(1, b.bs, 1), col7 = b.col & 7, row7 = b.row & 7;
+                for (int yy = 0; yy < bh8; yy++)
+                    for (int xx = 0; xx < bw8; xx++)
+                        if (row7 + yy < 8 && col7 + xx < 8) S.lfl[(row7 + yy) * 8 + col7 + xx] = (uint8_t) lvl;
+                pl_lf_block_masks(b, cols, rows, SSH, SSV, [&](int cls, int d, int y, int k, unsigned v) {
+                    if (y < 8) atomicOr(&S.lfm[cls][d][y], (v & 255u) << (8 * k));
+                });
+            }
+        }
+        wsync();
+        uint8_t *prog = (uint8_t *) S.prog;
+        for (int i = lane; i < pl_lf_items(SSH, SSV); i += 64)
+            pl_lf_item(i, SSH, SSV, G.sbx == 0, G.sby == 0, [&](int pos) { return (int) S.lfl[pos]; },
+                       [&](int cls, int d, int y, int k) { return (S.lfm[cls][d][y] >> (8 * k)) & 255u; },
+                       [&](int off, uint8_t v) { prog[off] = v; });
+        wsync();
+        uint32_t *g = (uint32_t *) &D.lfs[slot];
+        for (int i = lane; i < (int) (sizeof(LFRec) / 4); i += 64)
+            g[i] = i == 0 ? (uint32_t) F.frame : i == 1 ? ((uint32_t) G.sbx | (uint32_t) G.sby << 16) : S.prog[i - 2];
+    }
+
+    // ---- the SB's intra step (diagonal phases; level phases in k_plevel) and batch totals
+    if (lane == 0) {
+        const uint32_t has = done > 0;
+        D.sb_info[slot] = has | dmask;
+        if (has && !(F.levels && !F.intra)) {
+            const uint32_t key = F.key0 + (uint32_t) ((G.sbx - G.tile_sb0) + G.sby);
+            D.sb_key[slot] = key;
+            D.sb_kpos[slot] = inb(D, key, D.nkeys, 1024u) ? atomicAdd(&D.key_cnt[key], 1u) : 0u;
+        }
+    }
+    for (int d = 32; d; d >>= 1) {
+        ibytes += __shfl_xor(ibytes, d);
+        mbytes += __shfl_xor(mbytes, d);
+    }
+    if (lane == 0) {
+        if (!inb(D, (uint32_t) F.frame, D.nframes, 2048u)) return;
+        if (ibytes) atomicAdd(&D.fbytes[2 * F.frame], ibytes);
+        if (mbytes) atomicAdd(&D.fbytes[2 * F.frame + 1], mbytes);
+    }
+    st = wor(st);
+    if (lane == 0 && st) atomicOr(D.status, st);
+}
+
+// ------------------------------------------------------------------ k_plevel
+// Level schedule of one inter frame: an SB with intra jobs gets 1 + the highest level of
+// the left / top / top-left SBs whose intra pixels it reads (0 if none), computed along
+// anti-diagonals; its key is the phase's key0 + level.
+__global__ __launch_bounds__(256) void k_plevel(PlanDev D)
+{
+    const PlanFrame &F = D.frames[blockIdx.x];
+    if (!F.levels || F.intra) return;
+    const int W = F.sb_cols, H = F.sb_rows;
+    for (int d = 0; d < W + H - 1; d++) {
+        const int x0 = pl_max(0, d - (H - 1)), x1 = pl_min(d, W - 1);
+        for (int x = x0 + (int) threadIdx.x; x <= x1; x += 256) {
+            const int y = d - x;
+            const uint32_t slot = F.slot0 + (uint32_t) (y * W + x);
+            const uint32_t info = D.sb_info[slot];
+            if (!(info & 1)) continue;
+            // neighbours of earlier diagonals: agent-scope loads (not the CU's L1)
+            auto lv = [&](uint32_t n) {
+                return (int) (__hip_atomic_load(&D.sb_key[n], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - F.key0) + 1;
+            };
+            int lvl = 0;
+            if ((info & 2) && x > 0) lvl = pl_max(lvl, lv(slot - 1));
+            if ((info & 4) && y > 0) lvl = pl_max(lvl, lv(slot - W));
+            if ((info & 8) && x > 0 && y > 0) lvl = pl_max(lvl, lv(slot - W - 1));
+            const uint32_t key = F.key0 + (uint32_t) lvl;
+            if (!inb(D, key, D.nkeys, 4096u)) continue;
+            __hip_atomic_store(&D.sb_key[slot], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            D.sb_kpos[slot] = atomicAdd(&D.key_cnt[key], 1u);
+        }
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------ k_pkeys
+// One workgroup: exclusive scan of the step-key counts, and the launch summary:
+// out[0] status, out[1 .. 1 + ng) count-matrix offsets at the host's gather indices,
+// then nk + 1 key offsets, then 2 x nframes 64-bit byte totals.
+__global__ __launch_bounds__(1024) void k_pkeys(PlanDev D, int nk, const uint32_t *gidx, int ng, int nframes,
+                                                uint32_t *out)
+{
+    __shared__ uint32_t part[1024];
+    const int t = threadIdx.x;
+    const int per = (nk + 1023) / 1024, k0 = t * per, k1 = pl_min(nk, k0 + per);
+    uint32_t s = 0;
+    for (int k = k0; k < k1; k++) s += D.key_cnt[k];
+    part[t] = s;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+        const uint32_t v = t >= d ? part[t - d] : 0u;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint32_t run = part[t] - s;
+    uint32_t *ko = out + 1 + ng;
+    for (int k = k0; k < k1; k++) {
+        D.key_off[k] = run;
+        ko[k] = run;
+        run += D.key_cnt[k];
+    }
+    if (t == 1023) { D.key_off[nk] = part[1023]; ko[nk] = part[1023]; }
+    for (int i = t; i < ng; i += 1024)      // bit 31: an MC-count offset
+        out[1 + i] = (gidx[i] >> 31) ? D.cntm0[gidx[i] & 0x7fffffffu] : D.cnt0[gidx[i]];
+    uint32_t *fb = ko + nk + 1;
+    for (int i = t; i < 2 * nframes; i += 1024) {
+        fb[2 * i] = (uint32_t) D.fbytes[i];
+        fb[2 * i + 1] = (uint32_t) (D.fbytes[i] >> 32);
+    }
+    if (t == 0) { out[0] = D.status[0]; out[1 + ng + nk + 1 + 4 * nframes] = D.status[1]; }
+}
+
+// ------------------------------------------------------------------ k_plists
+__global__ __launch_bounds__(256) void k_plists(PlanDev D)
+{
+    const PlanFrame &F = D.frames[blockIdx.y];
+    const int s = blockIdx.x * 256 + threadIdx.x;
+    if (s >= F.sb_cols * F.sb_rows) return;
+    const uint32_t slot = F.slot0 + (uint32_t) s;
+    if (!(D.sb_info[slot] & 1)) return;
+    const uint32_t key = D.sb_key[slot];
+    if (!inb(D, key, D.nkeys, 8192u)) return;
+    const uint32_t i = D.key_off[key] + D.sb_kpos[slot];
+    if (inb(D, i, D.cap_dlists, 16384u)) D.dlists[i] = slot;
+}
+
+template <int SSH, int SSV>
+void launch_sb_kernels(hipStream_t st, const PlanDev &D, int max_sb, int nframes, bool second)
+{
+    if (second)
+        hipLaunchKernelGGL((k_plan<SSH, SSV>), dim3(max_sb, nframes), dim3(64), 0, st, D);
+    else
+        hipLaunchKernelGGL((k_psb<SSH, SSV>), dim3(max_sb, nframes), dim3(64), 0, st, D);
+}
+
+// ss: ss_h | ss_v << 1 (as the pixel kernels' launchers)
+void launch_sb(int ss, hipStream_t st, const PlanDev &D, int max_sb, int nframes, bool second)
+{
+    switch (ss) {
+    case 3: launch_sb_kernels<1, 1>(st, D, max_sb, nframes, second); break;
+    case 1: launch_sb_kernels<1, 0>(st, D, max_sb, nframes, second); break;
+    case 2: launch_sb_kernels<0, 1>(st, D, max_sb, nframes, second); break;
+    default: launch_sb_kernels<0, 0>(st, D, max_sb, nframes, second); break;
+    }
+}
+
+} // namespace
+
+extern "C" {
+// Temporary storage of the exclusive scans over up to n elements.
+size_t vp9hip_plan_scan_bytes(size_t n)
+{
+    size_t b = 0;
+    if (hipcub::DeviceScan::ExclusiveSum(nullptr, b, (const uint32_t *) nullptr, (uint32_t *) nullptr, (int) n) != hipSuccess) return 0;
+    return b;
+}
+
+// Enqueue the device planner of a staged batch on `st`. The caller has zeroed
+// status / key_cnt / fbytes and set sb_first / sb_end to 0xffffffff.
+// nb / nslots / ncnt: blocks, SB slots, count-matrix entries (each array + 1 zero entry).
+int vp9hip_plan_enqueue(hipStream_t st, const PlanDev *Dp, int ss, int nframes, int max_blk, int max_sb, uint32_t nb,
+                        uint32_t nslots, uint32_t ncnt, int nk, const uint32_t *gidx, int ng, uint32_t *summary,
+                        void *scan_tmp, size_t scan_bytes, int any_levels)
+{
+    const PlanDev &D = *Dp;
+    if (nframes <= 0) return 0;
+    hipLaunchKernelGGL(k_pblk, dim3((max_blk + 255) / 256, nframes), dim3(256), 0, st, D);
+    size_t tb = scan_bytes;
+    if (hipcub::DeviceScan::ExclusiveSum(scan_tmp, tb, D.blk_neob, D.blk_eob0, (int) nb + 1, st) != hipSuccess) return -1;
+    launch_sb(ss, st, D, max_sb, nframes, false);
+    tb = scan_bytes;
+    if (hipcub::DeviceScan::ExclusiveSum(scan_tmp, tb, D.sb_ncoef, D.sb_coef0, (int) nslots + 1, st) != hipSuccess) return -1;
+    tb = scan_bytes;
+    if (hipcub::DeviceScan::ExclusiveSum(scan_tmp, tb, D.cnt, D.cnt0, (int) ncnt + 1, st) != hipSuccess) return -1;
+    tb = scan_bytes;
+    if (hipcub::DeviceScan::ExclusiveSum(scan_tmp, tb, D.cntm, D.cntm0, (int) nslots + 1, st) != hipSuccess) return -1;
+    launch_sb(ss, st, D, max_sb, nframes, true);
+    if (any_levels) hipLaunchKernelGGL(k_plevel, dim3(nframes), dim3(256), 0, st, D);
+    hipLaunchKernelGGL(k_pkeys, dim3(1), dim3(1024), 0, st, D, nk, gidx, ng, nframes, summary);
+    hipLaunchKernelGGL(k_plists, dim3((max_sb + 255) / 256, nframes), dim3(256), 0, st, D);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+}

@@ -35,6 +35,8 @@
 #include "../../include/vp9hip.h"
 #include "vp9_tables.h"
 #include "vp9hip_work.h"
+#include "vp9hip_planlogic.h"
+#include "vp9hip_plan.h"
 
 extern "C" {
 int vp9hip_launch_resid(int hb, hipStream_t st, int tcode, int n, const RJob *jobs, const FrameDesc *frames,
@@ -45,6 +47,10 @@ int vp9hip_launch_pred(int fmt, hipStream_t st, int nwg, const uint32_t *list, c
 int vp9hip_launch_lf(int fmt, hipStream_t st, int nsb, const uint32_t *list, const LFRec *recs,
                      const FrameDesc *frames, int dbg);
 int vp9hip_launch_mc(int hb, hipStream_t st, int n, const McUnit *units, const FrameDesc *frames);
+size_t vp9hip_plan_scan_bytes(size_t n);
+int vp9hip_plan_enqueue(hipStream_t st, const PlanDev *D, int ss, int nframes, int max_blk, int max_sb, uint32_t nb,
+                        uint32_t nslots, uint32_t ncnt, int nk, const uint32_t *gidx, int ng, uint32_t *summary,
+                        void *scan_tmp, size_t scan_bytes, int any_levels);
 int vp9hip_launch_lfr(int fmt, hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs,
                       const FrameDesc *frames, uint32_t *ctr);
 int vp9hip_launch_plf(int fmt, hipStream_t st, const PlfLaunch *pl, const uint32_t *plist, const uint32_t *llist,
@@ -55,11 +61,10 @@ int vp9hip_launch_plf(int fmt, hipStream_t st, const PlfLaunch *pl, const uint32
 
 namespace {
 
-enum { K_MC, K_RESID, K_PRED, K_LF, K_PLF, K_LFR, K_N };
-const char *const kname[K_N] = { "k_mc", "k_resid", "k_pred", "k_lf", "k_plf", "k_lfr" };
+// K_PLAN: the device planner (k_pblk, scans, k_psb, k_plan, k_plevel, k_pkeys, k_plists) of a run
+enum { K_MC, K_RESID, K_PRED, K_LF, K_PLF, K_LFR, K_PLAN, K_N };
+const char *const kname[K_N] = { "k_mc", "k_resid", "k_pred", "k_lf", "k_plf", "k_lfr", "k_plan" };
 
-// ff_vp9_intra_txfm_type (vp9data.c:437-452)
-const uint8_t intra_txfm_type[14] = { 2, 1, 0, 0, 3, 2, 1, 2, 1, 3, 0, 0, 0, 0 };
 
 // step: wavefront diagonal of a K_PRED (x_in_tile + y) or K_LF (x + 2y) launch; K_PLF
 // (intra diagonal `step` + LF diagonal step - PLF_LAG in one launch): off / n the intra
@@ -127,6 +132,39 @@ struct Staged {
     size_t resid_cap = 0;               // bytes
     bool ready = false;
     hipGraphExec_t graph = nullptr;     // captured launch sequence of this batch (timing off)
+    std::vector<Launch> graph_launches; // the launch list the graph was captured from
+
+    // ---- device-planned batch (the default; VP9HIP_HOST_PLAN=1 plans on the host): stage
+    // uploads the packets and the batch geometry, every run plans on the device
+    bool dev = false, planned = false, fuse = false;
+    struct DevPhase {
+        std::vector<int> frames;
+        int group = 0, nseg = 1, nkey = 0, np = 0, nlf = 0;
+        bool fused = false, levels = false, lfr = false;
+        uint32_t key0 = 0;
+        std::vector<uint32_t> seg_sz;                         // SBs per residual segment
+        std::vector<std::pair<uint32_t, uint32_t>> lf;        // per LF diagonal: host list (offset, count)
+        std::vector<double> pred_bytes, lf_bytes;             // per intra diagonal (intra frames) / LF diagonal
+        uint32_t lfr_off = 0, lfr_n = 0;                      // k_lfr task table in the host lists
+        int lfr_ctr = 0;
+        double lfr_bytes = 0;
+        int g_res = 0, g_mc = 0;                              // summary gather slots
+    };
+    std::vector<DevPhase> dph;
+    std::vector<double> frame_res_bytes;                      // per frame: coefficient bytes
+    std::vector<int> frame_fused;                             // per frame: residuals inside k_plf
+    double alg_base[K_N] = {};                                // header-derived algorithmic bytes
+    uint32_t cap_mcs = 0;
+    uint32_t nslots = 0, nblk = 0, neob = 0, ncoef = 0, ncnt = 0, nkey = 0, host_lists = 0, n_gidx = 0;
+    int max_blk = 0, max_sb = 0, jcap = 0, rcap = 0, nframes = 0;
+    bool any_levels = false;
+    size_t o_pf = 0, o_blocks = 0, o_eobs = 0, o_slotpos = 0, o_segpre = 0, o_segsz = 0, o_segpre1 = 0, o_cntm = 0, o_cntm0 = 0, o_gidx = 0, o_bneob = 0,
+           o_beob0 = 0, o_sbfirst = 0, o_sbncoef = 0, o_sbcoef0 = 0, o_cnt = 0, o_cnt0 = 0, o_ibits = 0,
+           o_sbinfo = 0, o_sbkey = 0, o_sbkpos = 0, o_keycnt = 0, o_keyoff = 0, o_status = 0, o_fbytes = 0,
+           o_summary = 0, o_scan = 0, zero_bytes = 0;
+    size_t scan_bytes = 0, summary_words = 0;
+    uint32_t *summary_h = nullptr;                            // pinned readback of the summary
+    size_t summary_cap = 0;
 };
 
 } // namespace
@@ -152,6 +190,10 @@ struct vp9hip_ctx {
     std::vector<uint8_t *> bufs;
     std::vector<std::pair<int, int>> buf_wh;   // visible size of the frame each buffer holds
     uint32_t *ptab = nullptr;           // intra predictor formula table (device)
+    uint8_t *nz = nullptr;              // nonzero bounding boxes per (tcode, txtp, eob) (device, planner)
+    bool host_plan = false;             // VP9HIP_HOST_PLAN=1: plan batches on host threads (A/B, tests)
+    hipEvent_t pev[2] = {};             // device planner timing (timing runs)
+    bool plan_timed = false;
     int dbg = 0;                        // VP9HIP_DEBUG: ablation switches for profiling only
     bool use_graph = true;              // VP9HIP_GRAPH=0 disables graph replay
     Staged stg;
@@ -180,6 +222,7 @@ extern "C" int vp9hip_open(int device, vp9hip_ctx **out)
     if (const char *g = getenv("VP9HIP_PLF")) c->fuse_plf = atoi(g) != 0;
     if (const char *g = getenv("VP9HIP_LFROW")) c->lf_rows = atoi(g);
     if (const char *g = getenv("VP9HIP_LEVELS")) c->level_sched = atoi(g) != 0;
+    if (const char *g = getenv("VP9HIP_HOST_PLAN")) c->host_plan = atoi(g) != 0;
     bool ok = hipSetDevice(device) == hipSuccess && hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) == hipSuccess;
     for (int i = 0; ok && i < MAX_GROUPS; i++)
@@ -215,6 +258,9 @@ extern "C" void vp9hip_close(vp9hip_ctx *c)
     if (c->stg.pinned) hipHostFree(c->stg.pinned);
     if (c->stg.graph) hipGraphExecDestroy(c->stg.graph);
     if (c->ptab) hipFree(c->ptab);
+    if (c->nz) hipFree(c->nz);
+    if (c->stg.summary_h) hipHostFree(c->stg.summary_h);
+    for (auto e : c->pev) if (e) hipEventDestroy(e);
     for (auto e : c->ev) hipEventDestroy(e);
     hipStreamDestroy(c->st);
     for (int i = 0; i < MAX_GROUPS - 1; i++) {
@@ -308,6 +354,8 @@ static int upload_ptab(vp9hip_ctx *c)
     return hipMemcpy(c->ptab, t.data(), t.size() * 4, hipMemcpyHostToDevice) == hipSuccess ? 0 : VP9HIP_EEXTERNAL;
 }
 
+static int upload_nz(vp9hip_ctx *c);
+
 extern "C" int vp9hip_configure(vp9hip_ctx *c, int width, int height, int bpp, int ss_h, int ss_v, int nbufs)
 {
     if (!c || width <= 0 || height <= 0 || nbufs <= 0 || width > 16384 || height > 16384) return VP9HIP_EINVAL;
@@ -336,65 +384,10 @@ extern "C" int vp9hip_configure(vp9hip_ctx *c, int width, int height, int bpp, i
     }
     c->stg.ready = false;
     int r = upload_ptab(c);
+    if (!r) r = upload_nz(c);
     if (r) return r;
     return hipStreamSynchronize(c->st) == hipSuccess ? 0 : VP9HIP_EEXTERNAL;
 }
-
-// --------------------------------------------------------------------------
-// loop-filter masks: restates mask_edges (vp9block.c:1142-1262)
-static void lf_mask_edges(uint8_t (*mask)[8][4], int ss_h, int ss_v, int row7, int col7, int w, int h,
-                          int col_end, int row_end, int tx, int skip_inter)
-{
-    static const unsigned wide_col[2] = { 0x11, 0x01 }, wide_row[2] = { 0x03, 0x07 };
-    if (tx == 0 && (ss_v | ss_h)) {
-        if (h == ss_v) { if (row7 & 1) return; if (!row_end) h += 1; }
-        if (w == ss_h) { if (col7 & 1) return; if (!col_end) w += 1; }
-    }
-    const unsigned t = 1u << col7, m_col = (t << w) - t;
-    if (tx == 0 && !skip_inter) {
-        const unsigned m8 = m_col & wide_col[ss_h], m4 = m_col - m8;
-        for (int y = row7; y < h + row7; y++) {
-            const int id = 2 - !(y & wide_row[ss_v]);
-            mask[0][y][1] |= m8;
-            mask[0][y][2] |= m4;
-            mask[1][y][id] |= ((ss_h & ss_v) && (col_end & 1) && (y & 1)) ? (t << (w - 1)) - t : m_col;
-            if (!ss_h) mask[0][y][3] |= m_col;
-            if (!ss_v) mask[1][y][3] |= (ss_h && (col_end & 1)) ? (t << (w - 1)) - t : m_col;
-        }
-        return;
-    }
-    if (!skip_inter) {
-        static const unsigned masks[4] = { 0xff, 0x55, 0x11, 0x01 };
-        const int id = tx == 1;
-        int l2 = tx + ss_h - 1;
-        const unsigned m_row = m_col & masks[l2];
-        if (ss_h && tx > 1 && (w ^ (w - 1)) == 1) {
-            const unsigned m16 = ((t << (w - 1)) - t) & masks[l2], m8 = m_row - m16;
-            for (int y = row7; y < h + row7; y++) { mask[0][y][0] |= m16; mask[0][y][1] |= m8; }
-        } else {
-            for (int y = row7; y < h + row7; y++) mask[0][y][id] |= m_row;
-        }
-        l2 = tx + ss_v - 1;
-        const int step = 1 << l2;
-        int y;
-        if (ss_v && tx > 1 && (h ^ (h - 1)) == 1) {
-            for (y = row7; y < h + row7 - 1; y += step) mask[1][y][0] |= m_col;
-            if (y - row7 == h - 1) mask[1][y][1] |= m_col;
-        } else {
-            for (y = row7; y < h + row7; y += step) mask[1][y][id] |= m_col;
-        }
-    } else if (tx != 0) {
-        mask[1][row7][(tx == 1) || (h == ss_v)] |= m_col;
-        const int id = (tx == 1) || (w == ss_h);
-        for (int y = row7; y < h + row7; y++) mask[0][y][id] |= t;
-    } else {
-        const unsigned t8 = t & wide_col[ss_h], t4 = t - t8;
-        for (int y = row7; y < h + row7; y++) { mask[0][y][2] |= t4; mask[0][y][1] |= t8; }
-        mask[1][row7][2 - !(row7 & wide_row[ss_v])] |= m_col;
-    }
-}
-
-static inline int rdiv(int a, int b) { return (a >= 0 ? a + (b >> 1) : a - (b >> 1)) / b; }
 
 // Bounding box (columns, rows) of the coefficient positions scan[0 .. eob-1] for every
 // (tx, txtp, eob): the kernels transform only columns that can hold a nonzero value.
@@ -426,6 +419,14 @@ static void init_nz()
     done = true;
 }
 
+static int upload_nz(vp9hip_ctx *c)
+{
+    if (c->nz) return 0;
+    init_nz();
+    if (hipMalloc(&c->nz, sizeof(g_nz)) != hipSuccess) return VP9HIP_ENOMEM;
+    return hipMemcpy(c->nz, g_nz, sizeof(g_nz), hipMemcpyHostToDevice) == hipSuccess ? 0 : VP9HIP_EEXTERNAL;
+}
+
 // --------------------------------------------------------------------------
 // Per-frame work building
 namespace {
@@ -438,7 +439,7 @@ struct FrameBuild {
     int pitch[2];
     int phase;                   // (stream group, chain position) of this frame
     int tile_lo = 0, tile_hi = 64;   // tile columns to reconstruct (default: all)
-    int scale[3][2], step[3][2]; // reference scale factors (vp9.c:845-880), 0 = unscaled
+    PlMcGeo mc;                  // size, subsampling, reference scale factors (vp9.c:845-880), 0 = unscaled
     int refw[3][2], refh[3][2];  // visible reference plane sizes
     uint64_t coef_base;          // element offset of this frame's coefficients in the batch stream
     bool by_diag = false;        // residual buckets per intra diagonal of the SB (fused schedule)
@@ -450,138 +451,16 @@ struct PendingJob { PJob j; int level, ts; uint32_t d0, nd; };   // deps: pdeps[
 } // namespace
 
 #define SCALE_INVALID 0xFFFF
-static inline int scale_mv(int n, int scale) { return (int) (((int64_t) n * scale) >> 14); }
-static inline int clampi(int v, int lo, int hi) { return v < lo ? lo : v > hi ? hi : v; }
 
-// MC reference parameters of one luma unit at plane position (x, y): mc_luma_unscaled
-// (vp9recon.c:376-414) or the scaled branch of mc_luma_scaled (vp9recon.c:492-541).
-static McRef mc_luma_ref(const FrameBuild &fb, int rf, int x, int y, const int16_t *mv, int px, int py, int pw, int ph,
-                         int bw, int bh)
-{
-    McRef m;
-    if (!fb.scale[rf][0]) {
-        m.ix = x + (mv[0] >> 3); m.iy = y + (mv[1] >> 3);
-        m.mx = (uint8_t) ((mv[0] & 7) << 1); m.my = (uint8_t) ((mv[1] & 7) << 1);
-        m.dx = m.dy = 16;
-        return m;
-    }
-    const int mvx = clampi(mv[0], -(x + pw - px + 4) * 8, (fb.cols * 8 - x + px + 3) * 8);
-    const int mvy = clampi(mv[1], -(y + ph - py + 4) * 8, (fb.rows * 8 - y + py + 3) * 8);
-    const int mx = scale_mv(mvx * 2, fb.scale[rf][0]) + scale_mv(x * 16, fb.scale[rf][0]);
-    const int my = scale_mv(mvy * 2, fb.scale[rf][1]) + scale_mv(y * 16, fb.scale[rf][1]);
-    m.ix = mx >> 4; m.iy = my >> 4;
-    m.mx = (uint8_t) (mx & 15); m.my = (uint8_t) (my & 15);
-    m.dx = (uint8_t) fb.step[rf][0]; m.dy = (uint8_t) fb.step[rf][1];
-    (void) bw; (void) bh;
-    return m;
-}
-
-// Chroma: mc_chroma_unscaled (vp9recon.c:416-467; mv * 2 on a non-subsampled axis) or
-// mc_chroma_scaled with the libvpx rounding of webm issue 820 on subsampled axes
-// (vp9recon.c:543-628).
-static McRef mc_chroma_ref(const FrameBuild &fb, int rf, int x, int y, const int16_t *mv, int px, int py, int pw, int ph,
-                           int bw, int bh)
-{
-    McRef m;
-    const int ssh = fb.ss_h, ssv = fb.ss_v;
-    if (!fb.scale[rf][0]) {
-        const int mx = mv[0] * (1 << !ssh), my = mv[1] * (1 << !ssv);
-        m.ix = x + (mx >> 4); m.iy = y + (my >> 4);
-        m.mx = (uint8_t) (mx & 15); m.my = (uint8_t) (my & 15);
-        m.dx = m.dy = 16;
-        return m;
-    }
-    const int sx = fb.scale[rf][0], sy = fb.scale[rf][1];
-    int mx, my;
-    if (ssh) {
-        const int mvx = clampi(mv[0], -(x + pw - px + 4) * 16, (fb.cols * 4 - x + px + 3) * 16);
-        mx = scale_mv(mvx, sx) + (scale_mv(x * 16, sx) & ~15) + (scale_mv(x * 32, sx) & 15);
-    } else {
-        const int mvx = clampi(mv[0], -(x + pw - px + 4) * 8, (fb.cols * 8 - x + px + 3) * 8);
-        mx = scale_mv(mvx * 2, sx) + scale_mv(x * 16, sx);
-    }
-    if (ssv) {
-        const int mvy = clampi(mv[1], -(y + ph - py + 4) * 16, (fb.rows * 4 - y + py + 3) * 16);
-        my = scale_mv(mvy, sy) + (scale_mv(y * 16, sy) & ~15) + (scale_mv(y * 32, sy) & 15);
-    } else {
-        const int mvy = clampi(mv[1], -(y + ph - py + 4) * 8, (fb.rows * 8 - y + py + 3) * 8);
-        my = scale_mv(mvy * 2, sy) + scale_mv(y * 16, sy);
-    }
-    m.ix = mx >> 4; m.iy = my >> 4;
-    m.mx = (uint8_t) (mx & 15); m.my = (uint8_t) (my & 15);
-    m.dx = (uint8_t) fb.step[rf][0]; m.dy = (uint8_t) fb.step[rf][1];
-    (void) bw; (void) bh;
-    return m;
-}
-
-// Filter width code | level of one edge (LFRec.prog)
-static inline uint8_t lf_byte(int wd, int L)
-{
-    return wd ? (uint8_t) ((wd == 16 ? 3 : wd == 8 ? 2 : 1) << 6 | L) : 0;
-}
-
-// The LF program of one SB: which filter (width, level) every edge of every 8-line band
-// gets, exactly as filter_plane_cols / filter_plane_rows select it from the masks,
-// including the mix2 pairing of two 8-line halves (vp9lpf.c:31-181, loopfilter_sb
-// 183-230). Chroma uses mask[ss_h | ss_v] (vp9lpf.c:189) with the plane's subsampling.
-// col0 / row0: the SB is at the frame's left / top edge (no outer edge there).
+// Host LF program of one SB from its levels and masks (pl_lf_item per item).
 static void lf_program(const uint8_t *lvl, const uint8_t (*msk)[2][8][4], int ss_h, int ss_v, bool col0, bool row0,
                        uint8_t *prog)
 {
     memset(prog, 0, LF_PROG_BYTES);
-    for (int pl = 0; pl < 2; pl++) {
-        const int sh = pl ? ss_h : 0, sv = pl ? ss_v : 0;
-        const uint8_t (*m)[8][4] = msk[pl ? (ss_h | ss_v) : 0];
-        const int cbase = pl ? LFP_CC : LFP_YC, rbase = pl ? LFP_CR(ss_h, ss_v) : LFP_YR;
-        const int dy = 1 << sv, dh = 1 << sh;       // mask rows / columns per 8 pixel lines
-        // column edges (filter_plane_cols): band of pixel rows, edges left to right
-        for (int band = 0; band < (8 >> sv); band++) {
-            const int half = band & 1, y = (band >> 1) * 2 * dy;
-            const uint8_t *hm1 = m[0][y], *hm2 = m[0][y + dy];
-            const unsigned h1 = hm1[0] | hm1[1] | hm1[2], h2 = hm2[1] | hm2[2];
-            for (int k = 0; k < 8; k++) {
-                const unsigned x = 1u << k;
-                const int lc = sh ? k & ~1 : k;
-                int wd = 0, L = 0;
-                if (!col0 || k > 0) {
-                    if (!half) {
-                        if (h1 & x) { wd = (hm1[0] & x) ? 16 : (hm1[1] & x) ? 8 : 4; L = lvl[y * 8 + lc]; }
-                    } else if (h1 & x) {
-                        if (hm1[0] & x) { if (hm2[0] & x) { wd = 16; L = lvl[y * 8 + lc]; } }
-                        else if (h2 & x) { wd = (hm2[1] & x) ? 8 : 4; L = lvl[(y + dy) * 8 + lc]; }
-                    } else if (h2 & x) { wd = (hm2[1] & x) ? 8 : 4; L = lvl[(y + dy) * 8 + lc]; }
-                }
-                if (sh) { prog[cbase + band * 8 + k] = lf_byte(wd, L); continue; }
-                prog[cbase + band * 16 + k * 2] = lf_byte(wd, L);
-                const unsigned in = half ? hm2[3] : hm1[3];
-                if (in & x) prog[cbase + band * 16 + k * 2 + 1] = (uint8_t) (0x40 | lvl[(half ? y + dy : y) * 8 + k]);
-            }
-        }
-        // row edges (filter_plane_rows): band of pixel columns, edges top to bottom
-        for (int band = 0; band < (8 >> sh); band++) {
-            const int chunk = band >> 1, half = band & 1;
-            const unsigned x = 1u << (chunk * 2 * dh), x2 = x << dh;
-            const int lc1 = chunk * 2 * dh, lc2 = lc1 + dh;
-            for (int yy = 0; yy < 8; yy++) {
-                const uint8_t *vm_ = m[1][yy];
-                const unsigned vm = vm_[0] | vm_[1] | vm_[2], vm3 = vm_[3];
-                const int lr = sv ? yy & ~1 : yy;
-                int wd = 0, L = 0;
-                if (!row0 || yy) {
-                    if (!half) {
-                        if (vm & x) { wd = (vm_[0] & x) ? 16 : (vm_[1] & x) ? 8 : 4; L = lvl[lr * 8 + lc1]; }
-                    } else if (vm & x) {
-                        if (vm_[0] & x) { if (vm_[0] & x2) { wd = 16; L = lvl[lr * 8 + lc1]; } }
-                        else if (vm & x2) { wd = (vm_[1] & x2) ? 8 : 4; L = lvl[lr * 8 + lc2]; }
-                    } else if (vm & x2) { wd = (vm_[1] & x2) ? 8 : 4; L = lvl[lr * 8 + lc2]; }
-                }
-                if (sv) { prog[rbase + band * 8 + yy] = lf_byte(wd, L); continue; }
-                prog[rbase + band * 16 + yy * 2] = lf_byte(wd, L);
-                if (!half ? (vm3 & x) : (vm3 & x2))
-                    prog[rbase + band * 16 + yy * 2 + 1] = (uint8_t) (0x40 | lvl[yy * 8 + (half ? lc2 : lc1)]);
-            }
-        }
-    }
+    for (int i = 0; i < pl_lf_items(ss_h, ss_v); i++)
+        pl_lf_item(i, ss_h, ss_v, col0, row0, [&](int pos) { return (int) lvl[pos]; },
+                   [&](int cls, int d, int y, int k) { return (unsigned) msk[cls][d][y][k]; },
+                   [&](int off, uint8_t v) { prog[off] = v; });
 }
 
 // Build jobs/levels/LF/MC for one frame. Appends to stg. Returns 0 or error.
@@ -650,20 +529,17 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
             const vp9h_block *b = &f->blocks[bi];
             if ((b->col >> 3) != sbx || (b->row >> 3) != sby) break;
             if (b->bs >= VP9H_N_BS || b->tx > 3 || b->uvtx > 3) return VP9HIP_EINVALIDDATA;
-            const int bw8 = vp9t_bwh[1][b->bs][0], bh8 = vp9t_bwh[1][b->bs][1];
-            const int w4 = bw8 << 1, h4 = bh8 << 1;
-            int end_x = std::min(2 * (cols - b->col), w4), end_y = std::min(2 * (rows - b->row), h4);
+            const int bw8 = pl_bwh(1, b->bs, 0), bh8 = pl_bwh(1, b->bs, 1);
 
             for (int p = 0; p < 3; p++) {
                 const int sh = p ? ss_h : 0, sv = p ? ss_v : 0;
-                const int txs = p ? b->uvtx : b->tx, step = 1 << txs;
-                const int pw4 = w4 >> sh, ex = end_x >> sh, ey = end_y >> sv;
-                const int bx = (b->col * 8 >> sh), by = (b->row * 8 >> sv);     // plane pixel pos
+                const PlTxGrid g = pl_txgrid(*b, p, cols, rows, ss_h, ss_v);
+                const int txs = g.txs, step = g.step, bx = g.bx, by = g.by;
                 const int sbsz = 64 >> sh, sbszv = 64 >> sv;
                 const int ux_sb = (bx - sbx * sbsz) >> 2, uy_sb = (by - sby * sbszv) >> 2;
                 const int units = sbsz >> 2, unitsv = sbszv >> 2;   // 4x4 units of this plane's SB (16 luma)
-                for (int y = 0; y < ey; y += step)
-                    for (int x = 0; x < ex; x += step) {
+                for (int y = 0; y < g.ey; y += step)
+                    for (int x = 0; x < g.ex; x += step) {
                         int e = 0;
                         if (!b->skip) {
                             if (eob >= eob_end) return VP9HIP_EINVALIDDATA;
@@ -673,7 +549,7 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
                         if (b->intra) {
                             mode = p ? b->uvmode : b->mode[b->bs > VP9H_BS_8x8 && b->tx == 0 ? y * 2 + x : 0];
                             if (mode > 9) return VP9HIP_EINVALIDDATA;
-                            txtp = p || txs == 3 ? 0 : intra_txfm_type[mode];
+                            txtp = p || txs == 3 ? 0 : pl_intra_txfm_type(mode);
                         }
                         const int tcode = lossless ? 4 : txs;
                         if (e > (16 << (2 * txs))) return VP9HIP_EINVALIDDATA;
@@ -699,34 +575,15 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
                         }
                         coef += e;
                         if (!b->intra || !mine) continue;
-                        // intra: prediction job, levelled by the pixels its edges read; the
-                        // edge availability of check_intra_mode (vp9recon.c:37-221) is resolved here
+                        // intra: prediction job with check_intra_mode resolved (vp9recon.c:37-221),
+                        // ordered after the jobs that produce the pixels its mode reads
                         PendingJob q;
-                        {
-                            const int n = 4 << txs;
-                            const int gx = bx + x * 4, gy = by + y * 4;      // plane pixel position
-                            const int tx0 = p ? tile_x0 * 8 >> ss_h : tile_x0 * 8;
-                            const int have_top = gy > 0, have_left = gx > tx0, have_right = x < pw4 - 1;
-                            const int have_t = (p ? cols * 8 >> ss_h : cols * 8) - gx;
-                            const int have_l = (p ? rows * 8 >> ss_v : rows * 8) - gy;
-                            int m = mode;
-                            switch (m) {            // mode_conv[mode][have_left][have_top] (vp9recon.c:49-87)
-                            case 0: if (!have_top) m = 13; break;
-                            case 1: if (!have_left) m = 14; break;
-                            case 2: m = have_left ? (have_top ? 2 : 10) : (have_top ? 11 : 12); break;
-                            case 3: case 7: if (!have_top) m = 13; break;
-                            case 8: if (!have_left) m = 14; break;
-                            case 9: m = have_left ? (have_top ? 9 : 1) : (have_top ? 0 : 14); break;
-                            default: break;
-                            }
-                            static const uint8_t slot_of[15] = { 0, 1, 9, 2, 3, 4, 5, 6, 7, 8, 10, 11, 12, 13, 14 };
-                            const int ct = std::min(n, have_t) - 1, cl = std::min(n, have_l) - 1;
-                            const int trreal = txs == 0 && have_top && have_right && have_t >= 8;
-                            q.j.a = (uint32_t) p | (uint32_t) txs << 2 | (uint32_t) (e ? 1 : 0) << 4 | (uint32_t) trreal << 5 |
-                                    (uint32_t) have_top << 6 | (uint32_t) have_left << 7 | (uint32_t) slot_of[m] << 8 |
-                                    (uint32_t) ux0 << 12 | (uint32_t) uy0 << 16 | (uint32_t) ct << 20 | (uint32_t) cl << 25;
-                            q.j.roff = roff;
-                        }
+                        const PlIntra pi = pl_intra_job(p, txs, mode, e, bx + x * 4, by + y * 4, x, g.pw4,
+                                                        p ? tile_x0 * 8 >> ss_h : tile_x0 * 8,
+                                                        p ? cols * 8 >> ss_h : cols * 8, p ? rows * 8 >> ss_v : rows * 8,
+                                                        ux0, uy0);
+                        q.j.a = pi.a;
+                        q.j.roff = roff;
                         q.ts = txs;
                         // level = 1 + the levels of the tx blocks whose pixels this job's
                         // (substituted) mode reads: the edges[] needs of vp9recon.c:71-97.
@@ -736,43 +593,21 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
                         int8_t *lm = lmap[p];
                         int16_t *jm = jmap[p];
                         q.d0 = (uint32_t) pdeps.size();
-                        auto dep = [&](int unit) {
+                        pl_local_reads(ux0, uy0, n4, pi.nd, pi.trx, units, unitsv, [&](int unit) {
                             lvl = std::max<int>(lvl, lm[unit]);
                             const int j = jm[unit];
                             if (j < 0) return;
                             for (size_t k = q.d0; k < pdeps.size(); k++) if (pdeps[k] == j) return;
                             pdeps.push_back((uint16_t) j);
-                        };
-                        const int msub = (int) ((q.j.a >> 8) & 15);   // slot (slot_of) of the substituted mode
-                        static const uint8_t needs[15] = {            // by slot: 1 left, 2 top, 4 top-left, 8 top-right
-                            2, 1, 2 | 8, 1 | 2 | 4, 1 | 2 | 4, 1 | 2 | 4, 2 | 8, 1, 1 | 2 | 4,   // V H D45 D135 D117 D153 D63 D207 TM
-                            1 | 2, 1, 2, 0, 0, 0 };                                            // DC LEFT_DC TOP_DC DC_128/127/129
-                        const int nd = needs[msub];
-                        const int trx = (txs == 0 && (x < pw4 - 1) && (nd & 8)) ? 1 : 0;
-                        if (uy0 > 0) {
-                            const int u0 = (nd & 4) ? ux0 - 1 : ux0, u1 = (nd & 2) ? ux0 + n4 + trx : ux0;
-                            for (int u = u0; u < u1; u++)
-                                if (u >= 0 && u < units) dep((uy0 - 1) * 16 + u);
-                        }
-                        if (ux0 > 0 && (nd & 1))
-                            for (int v = uy0; v < uy0 + n4; v++)
-                                if (v < unitsv) dep(v * 16 + ux0 - 1);
+                        });
                         if (levels) {       // reads of other SBs' units (frame unit coordinates)
-                            const int fx = sbx * units + ux0, fy = sby * unitsv + uy0;
                             const int16_t *um = umap[p].data();
-                            auto xdep = [&](int ux, int uy) {
+                            pl_cross_reads(ux0, uy0, sbx * units + ux0, sby * unitsv + uy0, n4, pi.nd, pi.trx,
+                                           [&](int ux, int uy) {
                                 if (ux < 0 || uy < 0 || ux >= uw[p]) return;
                                 const int16_t l = um[(size_t) uy * uw[p] + ux];
                                 if (l >= 0) sb_lvl = std::max(sb_lvl, l + 1);
-                            };
-                            if (uy0 == 0 && (nd & 6)) {
-                                const int u0 = (nd & 4) ? -1 : 0, u1 = (nd & 2) ? n4 + trx : 0;
-                                for (int u = u0; u < u1; u++) xdep(fx + u, fy - 1);
-                            } else if (ux0 == 0 && (nd & 4)) {
-                                xdep(fx - 1, fy - 1);
-                            }
-                            if (ux0 == 0 && (nd & 1))
-                                for (int v = 0; v < n4; v++) xdep(fx - 1, fy + v);
+                            });
                         }
                         q.nd = (uint32_t) pdeps.size() - q.d0;
                         lvl += 1;
@@ -790,110 +625,17 @@ static int build_frame(vp9hip_ctx *c, Staged &s, FrameBuild &fb, std::vector<std
             if (!b->intra && mine) {
                 const int r0 = b->ref[0], r1 = b->comp ? b->ref[1] : r0;
                 if (b->ref[0] > 2 || (b->comp && b->ref[1] > 2)) return VP9HIP_EINVALIDDATA;
-                if (fb.scale[r0][0] == SCALE_INVALID || fb.scale[r1][0] == SCALE_INVALID) return VP9HIP_EINVALIDDATA;
-                // the SCALED template when any reference is scaled (vp9recon.c:670-680)
-                const bool scaled_tpl = fb.scale[r0][0] || (b->comp && fb.scale[r1][0]);
-                McUnit u;
-                memset(&u, 0, sizeof(u));
-                u.frame = fb.frame_idx;
-                u.filter = b->filter;
-                u.nref = b->comp ? 2 : 1;
-                u.ref[0] = b->ref[0];
-                u.ref[1] = b->ref[1];
-                // (x, y) plane position, (px, py, pw, ph) of mc_{luma,chroma}_dir
-                auto emit = [&](int plane, int x, int y, int w, int hh, const int16_t (*mv)[2], int px, int py, int pw,
-                                int ph) {
-                    McUnit m = u;
-                    m.plane = plane; m.x = x; m.y = y; m.w = w; m.h = hh;
-                    for (int k = 0; k < m.nref; k++) {
-                        const int rf = b->ref[k];
-                        m.r[k] = plane ? mc_chroma_ref(fb, rf, x, y, mv[k], px, py, pw, ph, w, hh)
-                                       : mc_luma_ref(fb, rf, x, y, mv[k], px, py, pw, ph, w, hh);
-                    }
-                    s.mcs.push_back(m);
-                };
-                auto chroma2 = [&](int x, int y, int w, int hh, const int16_t (*mv)[2], int px, int py, int pw, int ph) {
-                    emit(1, x, y, w, hh, mv, px, py, pw, ph);
-                    emit(2, x, y, w, hh, mv, px, py, pw, ph);
-                };
-                const int lx = b->col * 8, ly = b->row * 8, cx = b->col * (8 >> ss_h), cy = b->row * (8 >> ss_v);
-                int16_t uv[2][2];
-                // ROUNDED_DIV_MVx2 / x4 chroma MVs of sub-8x8 blocks (vp9_mc_template.c:24-28)
-                auto avg2 = [&](int i0, int i1) {
-                    for (int k = 0; k < 2; k++) for (int d = 0; d < 2; d++) uv[k][d] = (int16_t) rdiv(b->mv[i0][k][d] + b->mv[i1][k][d], 2);
-                    return uv;
-                };
-                auto avg4 = [&]() {
-                    for (int k = 0; k < 2; k++) for (int d = 0; d < 2; d++)
-                        uv[k][d] = (int16_t) rdiv(b->mv[0][k][d] + b->mv[1][k][d] + b->mv[2][k][d] + b->mv[3][k][d], 4);
-                    return uv;
-                };
-                static const int sub[4][2] = { { 0, 0 }, { 4, 0 }, { 0, 4 }, { 4, 4 } };
-                if (b->bs > VP9H_BS_8x8 && scaled_tpl) {
-                    // SCALED template (vp9_mc_template.c, SCALED == 1): four 4x4 luma blocks;
-                    // chroma 4x4 blocks with averaged MVs per subsampled axis
-                    for (int k = 0; k < 4; k++)
-                        emit(0, lx + sub[k][0], ly + sub[k][1], 4, 4, b->mv[k], sub[k][0], sub[k][1], 8, 8);
-                    if (ss_v && ss_h) chroma2(cx, cy, 4, 4, avg4(), 0, 0, 4, 4);
-                    else if (ss_v) {
-                        chroma2(cx, cy, 4, 4, avg2(0, 2), 0, 0, 8, 4);
-                        chroma2(cx + 4, cy, 4, 4, avg2(1, 3), 4, 0, 8, 4);
-                    } else if (ss_h) {
-                        chroma2(cx, cy, 4, 4, avg2(0, 1), 0, 0, 4, 8);
-                        chroma2(cx, cy + 4, 4, 4, avg2(1, 2), 0, 4, 4, 8);   // libvpx bug replica (296-305)
-                    } else {
-                        for (int k = 0; k < 4; k++)
-                            chroma2(cx + sub[k][0], cy + sub[k][1], 4, 4, b->mv[k], sub[k][0], sub[k][1], 8, 8);
-                    }
-                } else if (b->bs == VP9H_BS_8x4) {
-                    emit(0, lx, ly, 8, 4, b->mv[0], 0, 0, 0, 0);
-                    emit(0, lx, ly + 4, 8, 4, b->mv[2], 0, 0, 0, 0);
-                    if (ss_v) chroma2(cx, cy, 8 >> ss_h, 4, avg2(0, 2), 0, 0, 0, 0);
-                    else {
-                        chroma2(cx, cy, 8 >> ss_h, 4, b->mv[0], 0, 0, 0, 0);
-                        // libvpx uses the wrong block index for 4:4:4 (vp9_mc_template.c:107-114)
-                        chroma2(cx, cy + 4, 8 >> ss_h, 4, ss_h ? avg2(0, 2) : b->mv[2], 0, 0, 0, 0);
-                    }
-                } else if (b->bs == VP9H_BS_4x8) {
-                    emit(0, lx, ly, 4, 8, b->mv[0], 0, 0, 0, 0);
-                    emit(0, lx + 4, ly, 4, 8, b->mv[1], 0, 0, 0, 0);
-                    if (ss_h) chroma2(cx, cy, 4, 8 >> ss_v, avg2(0, 1), 0, 0, 0, 0);
-                    else {
-                        chroma2(cx, cy, 4, 8 >> ss_v, b->mv[0], 0, 0, 0, 0);
-                        chroma2(cx + 4, cy, 4, 8 >> ss_v, b->mv[1], 0, 0, 0, 0);
-                    }
-                } else if (b->bs > VP9H_BS_8x8) {
-                    for (int k = 0; k < 4; k++) emit(0, lx + sub[k][0], ly + sub[k][1], 4, 4, b->mv[k], 0, 0, 0, 0);
-                    if (ss_v && ss_h) chroma2(cx, cy, 4, 4, avg4(), 0, 0, 0, 0);
-                    else if (ss_v) {
-                        chroma2(cx, cy, 4, 4, avg2(0, 2), 0, 0, 0, 0);
-                        chroma2(cx + 4, cy, 4, 4, avg2(1, 3), 0, 0, 0, 0);
-                    } else if (ss_h) {
-                        chroma2(cx, cy, 4, 4, avg2(0, 1), 0, 0, 0, 0);
-                        chroma2(cx, cy + 4, 4, 4, avg2(1, 2), 0, 0, 0, 0);   // libvpx bug replica (296-305)
-                    } else {
-                        for (int k = 0; k < 4; k++) chroma2(cx + sub[k][0], cy + sub[k][1], 4, 4, b->mv[k], 0, 0, 0, 0);
-                    }
-                } else {
-                    const int bw = vp9t_bwh[0][b->bs][0] * 4, bh = vp9t_bwh[0][b->bs][1] * 4;
-                    const int uvbw = vp9t_bwh[ss_h][b->bs][0] * 4, uvbh = vp9t_bwh[ss_v][b->bs][1] * 4;
-                    emit(0, lx, ly, bw, bh, b->mv[0], 0, 0, bw, bh);
-                    chroma2(cx, cy, uvbw, uvbh, b->mv[0], 0, 0, uvbw, uvbh);
-                }
+                if (fb.mc.scale[r0][0] == SCALE_INVALID || fb.mc.scale[r1][0] == SCALE_INVALID) return VP9HIP_EINVALIDDATA;
+                pl_mc_block(*b, fb.mc, (uint32_t) fb.frame_idx, [&](const McUnit &m) { s.mcs.push_back(m); });
             }
 
             // LF level + masks (vp9block.c:1438-1452)
-            int lvl;
-            if (f->filter_level && b->seg_id < 8 &&
-                (lvl = f->lflvl[b->seg_id][b->intra ? 0 : b->ref[0] + 1][b->mode[3] != VP9H_ZEROMV]) > 0) {
-                const int x_end = std::min(cols - b->col, bw8), y_end = std::min(rows - b->row, bh8);
-                const int skip_inter = !b->intra && b->skip, col7 = b->col & 7, row7 = b->row & 7;
+            if (const int lvl = pl_lf_level(*b, f->lflvl, f->filter_level)) {
+                const int col7 = b->col & 7, row7 = b->row & 7;
                 for (int yy = 0; yy < bh8; yy++)
                     for (int xx = 0; xx < bw8; xx++) lf_level[(row7 + yy) * 8 + col7 + xx] = (uint8_t) lvl;
-                lf_mask_edges(lf_mask[0], 0, 0, row7, col7, x_end, y_end, 0, 0, b->tx, skip_inter);
-                lf_mask_edges(lf_mask[1], ss_h, ss_v, row7, col7, x_end, y_end,
-                              (cols & 1) && b->col + bw8 >= cols ? cols & 7 : 0,
-                              (rows & 1) && b->row + bh8 >= rows ? rows & 7 : 0, b->uvtx, skip_inter);
+                pl_lf_block_masks(*b, cols, rows, ss_h, ss_v,
+                                  [&](int cls, int d, int y, int k, unsigned v) { lf_mask[cls][d][y][k] |= (uint8_t) v; });
             }
         }
 
@@ -1077,6 +819,484 @@ static double sb_bytes(const vp9hip_ctx *c, const vp9h_frame &f, int sbx, int sb
     return (double) w * h * c->bypp * (1.0 + 2.0 / ((1 << c->ss_h) * (1 << c->ss_v)));
 }
 
+// ==========================================================================
+// Device-planned batches (the default). stage_dev: the batch geometry on the host (SB slots,
+// residual segments, intra-step keys, LF diagonal lists, k_lfr task tables: O(SBs), no
+// per-block work) and one upload of the packets; plan_dev (every run): the device planner
+// (vp9hip_plan.hip), a readback of its summary (record counts, status) and the launch list.
+struct DevIn {
+    const vp9h_frame *pkts;
+    int n, G, maxpos, NP, csz;
+    const std::vector<FrameBuild> *fbs;
+    const std::vector<char> *res_fused, *lvl_ph;
+    bool fuse, lfr_any;
+};
+
+static int stage_dev(vp9hip_ctx *c, const DevIn &in)
+{
+    Staged &s = c->stg;
+    const int n = in.n;
+    const std::vector<FrameBuild> &fbs = *in.fbs;
+    const vp9h_frame *pkts = in.pkts;
+    s.dev = true;
+    s.planned = false;
+    s.nframes = n;
+    s.jcap = s.rcap = pl_rcap(c->ss_h, c->ss_v);
+    s.fuse = in.fuse;
+    std::vector<uint32_t> slot0(n + 1, 0);
+    s.max_blk = 0; s.max_sb = 0;
+    for (int i = 0; i < n; i++) {
+        slot0[i + 1] = slot0[i] + (uint32_t) (fbs[i].sb_cols * fbs[i].sb_rows);
+        s.max_blk = std::max(s.max_blk, (int) pkts[i].nblocks);
+        s.max_sb = std::max(s.max_sb, fbs[i].sb_cols * fbs[i].sb_rows);
+    }
+    const uint32_t NS = slot0[n];
+    s.nslots = NS;
+    std::vector<uint32_t> slot_pos(NS, 0), seg_pre4, seg_sz, seg_pre1, gidx, hl;
+    s.dph.assign(in.NP, Staged::DevPhase());
+    for (int i = 0; i < n; i++) s.dph[fbs[i].phase].frames.push_back(i);
+    std::vector<PlanFrame> pf(n);
+    memset(pf.data(), 0, pf.size() * sizeof(PlanFrame));
+    uint32_t base = 0, segs = 0, keys = 0, sbs_before = 0;
+    s.n_ctr = 0;
+    s.lfr_ctr.clear();
+    for (int ph = 0; ph < in.NP; ph++) {
+        Staged::DevPhase &P = s.dph[ph];
+        if (P.frames.empty()) continue;
+        P.group = ph / (in.maxpos + 1);
+        P.fused = (*in.res_fused)[ph];
+        P.levels = (*in.lvl_ph)[ph];
+        P.lfr = in.lfr_any && (c->lf_rows > 1 || (int) P.frames.size() < LFR_MAX_FRAMES);
+        int nd = 0, nlfd = 0, nk = 0;
+        for (int i : P.frames) {
+            const FrameBuild &fb = fbs[i];
+            const int l2 = fb.f->log2_tile_cols;
+            int tw = 0;
+            for (int t = 0; t < (1 << l2); t++)
+                tw = std::max(tw, std::min(((t + 1) * fb.sb_cols) >> l2, fb.sb_cols) - std::min((t * fb.sb_cols) >> l2, fb.sb_cols));
+            nd = std::max(nd, tw + fb.sb_rows - 1);
+            nlfd = std::max(nlfd, fb.sb_cols + 2 * (fb.sb_rows - 1));
+            nk = std::max(nk, fb.sb_cols + fb.sb_rows - 1);
+        }
+        P.np = nd;
+        P.nseg = P.fused ? nd : 1;
+        P.seg_sz.assign(P.nseg, 0);
+        P.pred_bytes.assign(nd, 0.0);
+        P.nkey = nk;
+        P.key0 = keys;
+        keys += (uint32_t) nk;
+        // residual segments: the SBs' positions (frames in order, raster order)
+        for (int i : P.frames) {
+            const FrameBuild &fb = fbs[i];
+            const bool intra = fb.f->keyframe || fb.f->intraonly;
+            for (int y = 0; y < fb.sb_rows; y++)
+                for (int x = 0; x < fb.sb_cols; x++) {
+                    int ts0;
+                    pl_tile_of(x, fb.sb_cols, fb.f->log2_tile_cols, &ts0);
+                    const int d = (x - ts0) + y;
+                    slot_pos[slot0[i] + (uint32_t) (y * fb.sb_cols + x)] = P.seg_sz[P.fused ? d : 0]++;
+                    if (intra) P.pred_bytes[d] += sb_bytes(c, *fb.f, x, y);
+                }
+        }
+        uint32_t S = 0;
+        for (uint32_t z : P.seg_sz) S += z;
+        const uint32_t s4 = 4 * S;
+        P.g_res = (int) gidx.size();
+        uint32_t pre = 0;
+        for (int d = 0; d < P.nseg; d++) {
+            seg_pre4.push_back(base + 4 * pre);
+            seg_sz.push_back(P.seg_sz[d]);
+            seg_pre1.push_back(sbs_before + pre);
+            for (int tc = 0; tc < 5; tc++) {
+                gidx.push_back(base + 4 * pre + (uint32_t) tc * s4);
+                gidx.push_back(base + 4 * pre + (uint32_t) tc * s4 + 4 * P.seg_sz[d]);
+            }
+            pre += P.seg_sz[d];
+        }
+        P.g_mc = (int) gidx.size();                      // MC-count offsets (bit 31)
+        gidx.push_back(0x80000000u | sbs_before);
+        gidx.push_back(0x80000000u | (sbs_before + S));
+        for (int i : P.frames) { pf[i].seg0 = segs; pf[i].s4 = s4; pf[i].key0 = P.key0; }
+        segs += (uint32_t) P.nseg;
+        base += 20 * S;                                  // 5 transform codes x 4 transform types per SB
+        sbs_before += S;
+        // LF diagonals x + 2y: every SB of the phase's filtered frames
+        std::vector<std::vector<uint32_t>> lfd(nlfd);
+        P.lf_bytes.assign(nlfd, 0.0);
+        for (int i : P.frames) {
+            const FrameBuild &fb = fbs[i];
+            if (!fb.f->filter_level) continue;
+            for (int y = 0; y < fb.sb_rows; y++)
+                for (int x = 0; x < fb.sb_cols; x++) {
+                    lfd[x + 2 * y].push_back(slot0[i] + (uint32_t) (y * fb.sb_cols + x));
+                    P.lf_bytes[x + 2 * y] += 2.0 * sb_bytes(c, *fb.f, x, y);
+                }
+        }
+        P.lf.assign(nlfd, { 0, 0 });
+        for (int j = 0; j < nlfd; j++) {
+            P.lf[j] = { (uint32_t) hl.size(), (uint32_t) lfd[j].size() };
+            hl.insert(hl.end(), lfd[j].begin(), lfd[j].end());
+        }
+        // LF diagonals fused into the intra launches (the rest: k_lfr), as in stage()
+        const int nres = P.fused ? P.nseg : 0;
+        const int jlfr = std::max(0, std::max(P.np, nres - 1) - PLF_LAG);
+        P.nlf = P.lfr ? std::min(jlfr, nlfd) : nlfd;
+        if (P.lfr) {
+            const int j0 = (!in.fuse || P.levels) ? 0 : P.nlf;
+            // task table: one task per (frame, SB row), rows-major, each naming the task of
+            // the row above and its SBs' LF records (= slots) left to right
+            std::vector<std::vector<uint32_t>> tid;
+            std::vector<int> lff;
+            int maxr = 0;
+            for (int i : P.frames)
+                if (fbs[i].f->filter_level) { lff.push_back(i); maxr = std::max(maxr, fbs[i].sb_rows); }
+            tid.resize(lff.size());
+            std::vector<uint32_t> recs, offs;
+            auto start = [&](int r) { return std::max(0, j0 - 2 * r); };
+            for (int r = 0; r < maxr; r++)
+                for (size_t k = 0; k < lff.size(); k++) {
+                    const FrameBuild &fb = fbs[lff[k]];
+                    if (r >= fb.sb_rows) continue;
+                    const int nc = fb.sb_cols, c0 = start(r);
+                    if (c0 >= nc) { tid[k].push_back(~0u); continue; }
+                    tid[k].push_back((uint32_t) offs.size());
+                    offs.push_back((uint32_t) recs.size());
+                    const uint32_t dep = r ? tid[k][r - 1] : ~0u;
+                    recs.push_back(dep);
+                    recs.push_back((uint32_t) nc);
+                    recs.push_back((uint32_t) c0);
+                    recs.push_back(dep != ~0u ? (uint32_t) std::max(0, start(r - 1) - 1) : 0u);
+                    for (int x = c0; x < nc; x++) recs.push_back(slot0[lff[k]] + (uint32_t) (r * nc + x));
+                    for (int x = c0; x < nc; x++) P.lfr_bytes += 2.0 * sb_bytes(c, *fb.f, x, r);
+                }
+            if (!offs.empty()) {
+                const uint32_t nt = (uint32_t) offs.size();
+                for (uint32_t &o : offs) o += nt;
+                P.lfr_off = (uint32_t) hl.size();
+                P.lfr_n = nt;
+                hl.insert(hl.end(), offs.begin(), offs.end());
+                hl.insert(hl.end(), recs.begin(), recs.end());
+                P.lfr_ctr = (int) s.n_ctr;
+                s.lfr_ctr.push_back(s.n_ctr);
+                s.n_ctr += 4 + nt;
+            } else {
+                P.lfr = false;
+            }
+        }
+    }
+    s.nkey = keys;
+    s.host_lists = (uint32_t) hl.size();
+    s.n_gidx = (uint32_t) gidx.size();
+    // frame records of the planner
+    uint64_t nb = 0, ne = 0, nc = 0, nmc = 0;
+    s.any_levels = false;
+    s.frame_res_bytes.assign(n, 0.0);
+    s.frame_fused.assign(n, 0);
+    for (int i = 0; i < n; i++) {
+        const FrameBuild &fb = fbs[i];
+        const vp9h_frame *f = &pkts[i];
+        PlanFrame &F = pf[i];
+        F.blk0 = (uint32_t) nb; F.nblk = f->nblocks;
+        F.eob0 = (uint32_t) ne; F.neob = f->neobs;
+        F.coef0 = (uint32_t) nc; F.ncoef = (uint32_t) f->ncoefs;
+        F.slot0 = slot0[i];
+        F.frame = i;
+        F.sb_cols = fb.sb_cols; F.sb_rows = fb.sb_rows;
+        F.log2_tc = f->log2_tile_cols; F.log2_tr = f->log2_tile_rows;
+        F.tile_lo = fb.tile_lo; F.tile_hi = fb.tile_hi;
+        F.lossless = f->lossless; F.filter_level = f->filter_level;
+        F.intra = f->keyframe || f->intraonly;
+        F.by_diag = fb.by_diag;
+        F.levels = fb.levels && !F.intra;
+        F.bypp = c->bypp;
+        F.pitch[0] = fb.pitch[0]; F.pitch[1] = fb.pitch[1];
+        F.mc = fb.mc;
+        memcpy(F.lflvl, f->lflvl, sizeof(F.lflvl));
+        s.any_levels |= F.levels != 0;
+        nb += f->nblocks; ne += f->neobs; nc += f->ncoefs;
+        if (!F.intra) nmc += (uint64_t) 12 * f->nblocks;
+        s.frame_res_bytes[i] = (double) f->ncoefs * in.csz;
+        s.frame_fused[i] = fb.by_diag;
+    }
+    if (nb >= 0xffffffffull || ne >= 0xffffffffull || nc >= 0xffffffffull) return VP9HIP_ENOMEM;
+    s.nblk = (uint32_t) nb; s.neob = (uint32_t) ne; s.ncoef = (uint32_t) nc;
+    s.ncnt = 20 * NS;
+    for (int k = 0; k < K_N; k++) s.alg_base[k] = s.alg_bytes[k];
+    // arena: the uploaded part (one DMA from a pinned image), then the planner's buffers
+    auto al = [](size_t x) { return (x + 255) & ~(size_t) 255; };
+    size_t o = 0;
+    s.o_frames = o; o = al(o + n * sizeof(FrameDesc));
+    s.o_pf = o; o = al(o + n * sizeof(PlanFrame));
+    s.o_slotpos = o; o = al(o + (size_t) NS * 4);
+    s.o_segpre = o; o = al(o + seg_pre4.size() * 4);
+    s.o_segsz = o; o = al(o + seg_sz.size() * 4);
+    s.o_segpre1 = o; o = al(o + seg_pre1.size() * 4);
+    s.o_gidx = o; o = al(o + gidx.size() * 4);
+    s.o_lists = o; o = al(o + (hl.size() + NS) * 4);      // host lists, then the device step lists
+    s.o_ctr = o; o = al(o + (size_t) s.n_ctr * 4);
+    s.o_blocks = o; o = al(o + nb * sizeof(vp9h_block));
+    s.o_eobs = o; o = al(o + ne * 2);
+    s.o_coefs = o; o = al(o + nc * in.csz + 64);
+    const size_t up = o;
+    s.o_bneob = o; o = al(o + (nb + 1) * 4);
+    s.o_beob0 = o; o = al(o + (nb + 1) * 4);
+    s.o_sbfirst = o; o = al(o + (size_t) 2 * NS * 4);        // sb_first, then sb_end
+    s.o_sbncoef = o; o = al(o + ((size_t) NS + 1) * 4);
+    s.o_sbcoef0 = o; o = al(o + ((size_t) NS + 1) * 4);
+    s.o_cnt = o; o = al(o + ((size_t) s.ncnt + 1) * 4);
+    s.o_cnt0 = o; o = al(o + ((size_t) s.ncnt + 1) * 4);
+    s.o_cntm = o; o = al(o + ((size_t) NS + 1) * 4);
+    s.o_cntm0 = o; o = al(o + ((size_t) NS + 1) * 4);
+    s.o_ibits = o; o = al(o + (size_t) NS * 96);
+    s.o_sbinfo = o; o = al(o + (size_t) NS * 4);
+    s.o_sbkey = o; o = al(o + (size_t) NS * 4);
+    s.o_sbkpos = o; o = al(o + (size_t) NS * 4);
+    s.o_keyoff = o; o = al(o + ((size_t) keys + 1) * 4);
+    s.o_keycnt = o;                                           // zeroed every run: counts, status, byte totals
+    s.o_status = al(o + ((size_t) keys + 1) * 4);
+    s.o_fbytes = s.o_status + 256;
+    o = al(s.o_fbytes + (size_t) n * 16);
+    s.zero_bytes = o - s.o_keycnt;
+    s.summary_words = 1 + gidx.size() + keys + 1 + 4 * (size_t) n + 1;      // + status[1]
+    s.o_summary = o; o = al(o + s.summary_words * 4);
+    s.o_sbs = o; o = al(o + (size_t) NS * sizeof(SBRec));
+    s.o_wgs = o; o = al(o + (size_t) NS * sizeof(WGRec));
+    s.o_lfs = o; o = al(o + (size_t) NS * sizeof(LFRec));
+    s.o_pjobs = o; o = al(o + (size_t) NS * s.jcap * sizeof(PJob));
+    s.o_passes = o; o = al(o + (size_t) NS * s.jcap * 4);
+    s.o_rjobs = o; o = al(o + (ne + 1) * sizeof(RJob));
+    s.o_mcs = o; o = al(o + (nmc + 1) * sizeof(McUnit));
+    s.cap_mcs = (uint32_t) (nmc + 1);
+    s.scan_bytes = std::max<size_t>(vp9hip_plan_scan_bytes(std::max<uint64_t>(nb, s.ncnt) + 1), 256);
+    s.o_scan = o; o = al(o + s.scan_bytes);
+    if (o > s.arena_cap) {
+        if (s.arena) hipFree(s.arena);
+        s.arena = nullptr;
+        s.arena_cap = 0;
+        if (hipMalloc(&s.arena, o) != hipSuccess) return VP9HIP_ENOMEM;
+        s.arena_cap = o;
+    }
+    if (up > s.pinned_cap) {
+        if (s.pinned) hipHostFree(s.pinned);
+        s.pinned = nullptr;
+        s.pinned_cap = 0;
+        if (hipHostMalloc((void **) &s.pinned, up, hipHostMallocDefault) != hipSuccess) return VP9HIP_ENOMEM;
+        s.pinned_cap = up;
+    }
+    if (s.summary_words * 4 > s.summary_cap) {
+        if (s.summary_h) hipHostFree(s.summary_h);
+        s.summary_h = nullptr;
+        s.summary_cap = 0;
+        if (hipHostMalloc((void **) &s.summary_h, s.summary_words * 4, hipHostMallocDefault) != hipSuccess) return VP9HIP_ENOMEM;
+        s.summary_cap = s.summary_words * 4;
+    }
+    const size_t rbytes = ((size_t) NS + 1) * s.rcap * 32;
+    if (rbytes > s.resid_cap) {
+        if (s.resid) hipFree(s.resid);
+        s.resid = nullptr;
+        s.resid_cap = 0;
+        if (hipMalloc(&s.resid, rbytes) != hipSuccess) return VP9HIP_ENOMEM;
+        s.resid_cap = rbytes;
+    }
+    uint8_t *img = s.pinned;
+    memcpy(img + s.o_frames, s.frames.data(), n * sizeof(FrameDesc));
+    memcpy(img + s.o_pf, pf.data(), n * sizeof(PlanFrame));
+    memcpy(img + s.o_slotpos, slot_pos.data(), (size_t) NS * 4);
+    if (!seg_pre4.empty()) memcpy(img + s.o_segpre, seg_pre4.data(), seg_pre4.size() * 4);
+    if (!seg_sz.empty()) memcpy(img + s.o_segsz, seg_sz.data(), seg_sz.size() * 4);
+    if (!seg_pre1.empty()) memcpy(img + s.o_segpre1, seg_pre1.data(), seg_pre1.size() * 4);
+    if (!gidx.empty()) memcpy(img + s.o_gidx, gidx.data(), gidx.size() * 4);
+    if (!hl.empty()) memcpy(img + s.o_lists, hl.data(), hl.size() * 4);
+    memset(img + s.o_ctr, 0, (size_t) s.n_ctr * 4);
+    {   // packets: blocks, eobs, coefficients (frames copied in parallel)
+        std::atomic<int> next(0);
+        auto worker = [&]() {
+            for (int i; (i = next.fetch_add(1)) < n;) {
+                const vp9h_frame *f = &pkts[i];
+                const PlanFrame &F = pf[i];
+                if (f->nblocks) memcpy(img + s.o_blocks + (size_t) F.blk0 * sizeof(vp9h_block), f->blocks, (size_t) f->nblocks * sizeof(vp9h_block));
+                if (f->neobs) memcpy(img + s.o_eobs + (size_t) F.eob0 * 2, f->eobs, (size_t) f->neobs * 2);
+                if (f->ncoefs) memcpy(img + s.o_coefs + (size_t) F.coef0 * in.csz, f->coefs, (size_t) f->ncoefs * in.csz);
+            }
+        };
+        const int nt = std::min(n, host_threads());
+        std::vector<std::thread> pool;
+        for (int t = 1; t < nt; t++) pool.emplace_back(worker);
+        worker();
+        for (auto &t : pool) t.join();
+    }
+    HIPCHK(hipMemcpyAsync(s.arena, img, up, hipMemcpyHostToDevice, c->st));
+    // scan sentinels (never written by the planner)
+    HIPCHK(hipMemsetAsync(s.arena + s.o_bneob + nb * 4, 0, 4, c->st));
+    HIPCHK(hipMemsetAsync(s.arena + s.o_sbncoef + (size_t) NS * 4, 0, 4, c->st));
+    HIPCHK(hipMemsetAsync(s.arena + s.o_cnt + (size_t) s.ncnt * 4, 0, 4, c->st));
+    HIPCHK(hipMemsetAsync(s.arena + s.o_cntm + (size_t) NS * 4, 0, 4, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    s.ready = true;
+    return 0;
+}
+
+// Run the device planner of the staged batch and build its launch list from the summary.
+static int plan_dev(vp9hip_ctx *c)
+{
+    Staged &s = c->stg;
+    uint8_t *A = s.arena;
+    s.planned = false;
+    s.launches.clear();
+    HIPCHK(hipMemsetAsync(A + s.o_sbfirst, 0xff, (size_t) 2 * s.nslots * 4, c->st));
+    HIPCHK(hipMemsetAsync(A + s.o_keycnt, 0, s.zero_bytes, c->st));
+    PlanDev D;
+    D.frames = (const PlanFrame *) (A + s.o_pf);
+    D.blocks = (const vp9h_block *) (A + s.o_blocks);
+    D.eobs = (const uint16_t *) (A + s.o_eobs);
+    D.total_blocks = s.nblk;
+    D.total_eobs = s.neob;
+    D.total_coefs = s.ncoef;
+    D.slot_pos = (const uint32_t *) (A + s.o_slotpos);
+    D.seg_pre4 = (const uint32_t *) (A + s.o_segpre);
+    D.seg_sz = (const uint32_t *) (A + s.o_segsz);
+    D.seg_pre1 = (const uint32_t *) (A + s.o_segpre1);
+    D.blk_neob = (uint32_t *) (A + s.o_bneob);
+    D.blk_eob0 = (uint32_t *) (A + s.o_beob0);
+    D.sb_first = (uint32_t *) (A + s.o_sbfirst);
+    D.sb_end = D.sb_first + s.nslots;
+    D.sb_ncoef = (uint32_t *) (A + s.o_sbncoef);
+    D.sb_coef0 = (uint32_t *) (A + s.o_sbcoef0);
+    D.cnt = (uint32_t *) (A + s.o_cnt);
+    D.cnt0 = (uint32_t *) (A + s.o_cnt0);
+    D.cntm = (uint32_t *) (A + s.o_cntm);
+    D.cntm0 = (uint32_t *) (A + s.o_cntm0);
+    D.ibits = (uint32_t *) (A + s.o_ibits);
+    D.sb_info = (uint32_t *) (A + s.o_sbinfo);
+    D.sb_key = (uint32_t *) (A + s.o_sbkey);
+    D.sb_kpos = (uint32_t *) (A + s.o_sbkpos);
+    D.key_cnt = (uint32_t *) (A + s.o_keycnt);
+    D.key_off = (uint32_t *) (A + s.o_keyoff);
+    D.status = (uint32_t *) (A + s.o_status);
+    D.fbytes = (unsigned long long *) (A + s.o_fbytes);
+    D.sbs = (SBRec *) (A + s.o_sbs);
+    D.wgs = (WGRec *) (A + s.o_wgs);
+    D.pjobs = (PJob *) (A + s.o_pjobs);
+    D.passes = (uint32_t *) (A + s.o_passes);
+    D.lfs = (LFRec *) (A + s.o_lfs);
+    D.rjobs = (RJob *) (A + s.o_rjobs);
+    D.mcs = (McUnit *) (A + s.o_mcs);
+    D.dlists = (uint32_t *) (A + s.o_lists) + s.host_lists;
+    D.nz = c->nz;
+    D.jcap = (uint32_t) s.jcap;
+    D.rcap = (uint32_t) s.rcap;
+    D.nslots = s.nslots;
+    D.cap_cnt = s.ncnt + 1;
+    D.cap_cntm = s.nslots + 1;
+    D.cap_rjobs = s.neob + 1;
+    D.cap_mcs = s.cap_mcs;
+    D.cap_dlists = s.nslots;
+    D.nkeys = s.nkey;
+    D.nframes = (uint32_t) s.nframes;
+    if (c->timing) {
+        for (auto &e : c->pev)
+            if (!e) HIPCHK(hipEventCreate(&e));
+        HIPCHK(hipEventRecord(c->pev[0], c->st));
+    }
+    if (vp9hip_plan_enqueue(c->st, &D, c->ss_h | c->ss_v << 1, s.nframes, s.max_blk, s.max_sb, s.nblk, s.nslots,
+                            s.ncnt, (int) s.nkey, (const uint32_t *) (A + s.o_gidx), (int) s.n_gidx,
+                            (uint32_t *) (A + s.o_summary), A + s.o_scan, s.scan_bytes, s.any_levels))
+        return VP9HIP_EEXTERNAL;
+    if (c->timing) HIPCHK(hipEventRecord(c->pev[1], c->st));
+    c->plan_timed = c->timing;
+    HIPCHK(hipMemcpyAsync(s.summary_h, A + s.o_summary, s.summary_words * 4, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    const uint32_t *sm = s.summary_h;
+    if (sm[0]) {                                              // the packets are inconsistent (PLS_*)
+        fprintf(stderr, "vp9hip: batch rejected by the device planner (status 0x%x, bounds 0x%x)\n", sm[0],
+                sm[s.summary_words - 1]);
+        return VP9HIP_EINVALIDDATA;
+    }
+    const uint32_t *gv = sm + 1, *ko = sm + 1 + s.n_gidx, *fb32 = ko + s.nkey + 1;
+    auto fbytes = [&](int i, int k) {
+        return (double) ((uint64_t) fb32[2 * (2 * i + k)] | (uint64_t) fb32[2 * (2 * i + k) + 1] << 32);
+    };
+    for (int k = 0; k < K_N; k++) s.alg_bytes[k] = s.alg_base[k];
+    for (int i = 0; i < s.nframes; i++) {
+        s.alg_bytes[K_RESID] += fbytes(i, 0);
+        s.alg_bytes[K_MC] += fbytes(i, 1);
+        if (s.frame_fused[i]) {                               // residuals inside the k_plf launches
+            const double b = s.frame_res_bytes[i] + fbytes(i, 0);
+            s.alg_bytes[K_RESID] -= b;
+            s.alg_bytes[K_PLF] += b;
+        }
+    }
+    const uint32_t H = s.host_lists;
+    const int nph = (int) s.dph.size();
+    for (int g = 0; g < s.ngroups; g++)
+        for (int ph = 0; ph < nph; ph++) {
+            const Staged::DevPhase &P = s.dph[ph];
+            if (P.frames.empty() || P.group != g) continue;
+            auto push = [&](int kind, uint32_t off, uint32_t cnt, int arg, int part, int step) {
+                Launch L = { kind, off, cnt, arg, g, ph, part, step };
+                s.launches.push_back(L);
+            };
+            const uint32_t m0 = gv[P.g_mc], m1 = gv[P.g_mc + 1];
+            if (m1 > m0) push(K_MC, m0, m1 - m0, 0, PART_RECON, 0);
+            auto rr = [&](int d, int tc) {
+                const uint32_t a = gv[P.g_res + (d * 5 + tc) * 2], b = gv[P.g_res + (d * 5 + tc) * 2 + 1];
+                return std::make_pair(a, b - a);
+            };
+            if (!P.fused)
+                for (int tc = 0; tc < 5; tc++)
+                    if (rr(0, tc).second) push(K_RESID, rr(0, tc).first, rr(0, tc).second, tc, PART_RECON, 0);
+            auto step = [&](int d) {
+                const uint32_t k = P.key0 + (uint32_t) d;
+                return std::make_pair(H + ko[k], ko[k + 1] - ko[k]);
+            };
+            auto lfr = [&]() {
+                if (!P.lfr) return;
+                push(K_LFR, P.lfr_off, P.lfr_n, (int) P.lfr_ctr, PART_LF, 0);
+                s.alg_bytes[K_LF] -= P.lfr_bytes;
+                s.alg_bytes[K_LFR] += P.lfr_bytes;
+            };
+            if (!s.fuse || P.levels) {
+                for (int d = 0; d < P.nkey; d++)
+                    if (step(d).second) push(K_PRED, step(d).first, step(d).second, 0, PART_RECON, d);
+                if (P.lfr) lfr();
+                else
+                    for (size_t j = 0; j < P.lf.size(); j++)
+                        if (P.lf[j].second) push(K_LF, P.lf[j].first, P.lf[j].second, 0, PART_LF, (int) j);
+                continue;
+            }
+            // fused: launch t = intra diagonal t + LF diagonal t - PLF_LAG + residuals of t + 1
+            const int np = P.np, nres = P.fused ? P.nseg : 0, nlf = P.nlf;
+            const int nt = std::max(std::max(np, nlf ? nlf + PLF_LAG : 0), nres - 1);
+            for (int t = -1; t < nt; t++) {
+                const std::pair<uint32_t, uint32_t> pv = t >= 0 && t < np ? step(t) : std::make_pair(0u, 0u);
+                const int j = t - PLF_LAG;
+                const std::pair<uint32_t, uint32_t> lv = j >= 0 && j < nlf ? P.lf[j] : std::make_pair(0u, 0u);
+                bool res = false;
+                for (int k = 0; t + 1 < nres && k < 5; k++) res |= rr(t + 1, k).second > 0;
+                if (!pv.second && !res) {
+                    if (lv.second) push(K_LF, lv.first, lv.second, 0, PART_LF, j);
+                    continue;
+                }
+                Launch L = { K_PLF, pv.first, pv.second, 0, g, ph, PART_RECON, t };
+                L.off2 = lv.first;
+                L.n2 = lv.second;
+                if (pv.second && t < (int) P.pred_bytes.size()) {
+                    s.alg_bytes[K_PRED] -= P.pred_bytes[t];
+                    s.alg_bytes[K_PLF] += P.pred_bytes[t];
+                }
+                if (lv.second) {
+                    s.alg_bytes[K_LF] -= P.lf_bytes[j];
+                    s.alg_bytes[K_PLF] += P.lf_bytes[j];
+                }
+                for (int k = 0; res && k < 5; k++) { L.roff[k] = rr(t + 1, k).first; L.rn[k] = rr(t + 1, k).second; }
+                s.launches.push_back(L);
+            }
+            lfr();
+        }
+    s.planned = true;
+    return 0;
+}
+
 static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bufs, const int *ref_bufs /*n*3 or null*/,
                  int tile_lo = 0, int tile_hi = 64, int max_groups = 0, bool tiled = false)
 {
@@ -1201,8 +1421,8 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
         FrameBuild &fb = fbs[i];
         fb.f = f; fb.frame_idx = i;
         fb.cols = cols; fb.rows = rows; fb.sb_cols = fd.sb_cols; fb.sb_rows = fd.sb_rows;
-        memset(fb.scale, 0, sizeof(fb.scale));
-        memset(fb.step, 0, sizeof(fb.step));
+        memset(&fb.mc, 0, sizeof(fb.mc));
+        fb.mc.cols = cols; fb.mc.rows = rows; fb.mc.ss_h = c->ss_h; fb.mc.ss_v = c->ss_v;
         if (!intra) {
             // reference scale factors (vp9.c:845-880)
             int valid = 0;
@@ -1210,13 +1430,13 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
                 const int rw = f->ref_w[r], rh = f->ref_h[r], w = f->width, h = f->height;
                 if (rw == w && rh == h) { valid++; continue; }
                 if (w * 2 < rw || h * 2 < rh || w > 16 * rw || h > 16 * rh) {
-                    fb.scale[r][0] = fb.scale[r][1] = SCALE_INVALID;
+                    fb.mc.scale[r][0] = fb.mc.scale[r][1] = SCALE_INVALID;
                     continue;
                 }
-                fb.scale[r][0] = (rw << 14) / w;
-                fb.scale[r][1] = (rh << 14) / h;
-                fb.step[r][0] = 16 * fb.scale[r][0] >> 14;
-                fb.step[r][1] = 16 * fb.scale[r][1] >> 14;
+                fb.mc.scale[r][0] = (rw << 14) / w;
+                fb.mc.scale[r][1] = (rh << 14) / h;
+                fb.mc.step[r][0] = 16 * fb.mc.scale[r][0] >> 14;
+                fb.mc.step[r][1] = 16 * fb.mc.scale[r][1] >> 14;
                 valid++;
             }
             if (!valid) return VP9HIP_EINVALIDDATA;
@@ -1243,6 +1463,18 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     }
 
     STAGE_T(0);
+    s.dev = false;
+    if (!c->host_plan) {
+        DevIn in;
+        in.pkts = pkts; in.n = n; in.G = G; in.maxpos = maxpos; in.NP = NP; in.csz = csz;
+        in.fbs = &fbs; in.res_fused = &res_fused; in.lvl_ph = &lvl_ph;
+        in.fuse = fuse; in.lfr_any = lfr_any;
+        const int r = stage_dev(c, in);
+        if (r) return r;
+        STAGE_T(1);
+        if (stage_trace) fprintf(stderr, "vp9hip stage (device plan): %d frames: setup %.1f upload %.1f ms\n", n, st_ms[0], st_ms[1]);
+        return 0;
+    }
     // work planning of every frame (independent), on host threads: jobs, dependency
     // levels and pass packing, LF programs, MC units, coefficient copy
     std::vector<FramePlan> plans(n);
@@ -1585,6 +1817,19 @@ extern "C" int vp9hip_stage_batch_refs(vp9hip_ctx *c, const vp9h_frame *pkts, in
 
 static int enqueue_batch(vp9hip_ctx *c);
 
+static bool same_launches(const std::vector<Launch> &a, const std::vector<Launch> &b)
+{
+    if (a.size() != b.size()) return false;
+    for (size_t i = 0; i < a.size(); i++) {
+        const Launch &x = a[i], &y = b[i];
+        if (x.kind != y.kind || x.off != y.off || x.n != y.n || x.arg != y.arg || x.grp != y.grp || x.ph != y.ph ||
+            x.part != y.part || x.off2 != y.off2 || x.n2 != y.n2 || memcmp(x.roff, y.roff, sizeof(x.roff)) ||
+            memcmp(x.rn, y.rn, sizeof(x.rn)))
+            return false;
+    }
+    return true;
+}
+
 // Run the staged batch. Without per-launch timing the ~300 launches of a 4K batch are
 // captured once into a HIP graph (both frame-group streams) and replayed.
 extern "C" int vp9hip_run_batch(vp9hip_ctx *c)
@@ -1592,8 +1837,21 @@ extern "C" int vp9hip_run_batch(vp9hip_ctx *c)
     if (!c || !c->stg.ready) return VP9HIP_EINVAL;
     hipSetDevice(c->dev);
     Staged &s = c->stg;
+    if (s.dev) {                          // plan on the device from the resident packets
+        const int r = plan_dev(c);
+        if (r) return r;
+        static const bool plan_only = getenv("VP9HIP_PLAN_ONLY") && atoi(getenv("VP9HIP_PLAN_ONLY"));
+        if (plan_only) return 0;          // diagnostics: the planner alone
+    }
     if (c->timing || !c->use_graph) return enqueue_batch(c);
+    // the graph of the previous run is reused when the launch list is the same (same
+    // geometry and record counts); the records themselves were just rewritten in place
+    if (s.graph && !same_launches(s.graph_launches, s.launches)) {
+        hipGraphExecDestroy(s.graph);
+        s.graph = nullptr;
+    }
     if (!s.graph) {
+        s.graph_launches = s.launches;
         hipGraph_t g = nullptr;
         HIPCHK(hipStreamBeginCapture(c->st, hipStreamCaptureModeThreadLocal));
         int r = enqueue_batch(c);
@@ -1771,6 +2029,10 @@ extern "C" int vp9hip_run_phase(vp9hip_ctx *c, int phase, int part)
     if (!c || !c->stg.ready || phase < 0 || phase >= c->stg.nphases || (part != PART_RECON && part != PART_LF))
         return VP9HIP_EINVAL;
     hipSetDevice(c->dev);
+    if (c->stg.dev && !c->stg.planned) {
+        const int r = plan_dev(c);
+        if (r) return r;
+    }
     c->timed_run = false;
     for (const Launch &L : c->stg.launches)
         if (L.ph == phase && L.part == part && launch_one(c, L, c->st)) return VP9HIP_EEXTERNAL;
@@ -1826,6 +2088,11 @@ extern "C" int vp9hip_sync(vp9hip_ctx *c)
                 c->kms[c->stg.launches[i].kind] += ms;
                 c->kcount[c->stg.launches[i].kind]++;
             }
+        }
+        float ms = 0;
+        if (c->plan_timed && hipEventElapsedTime(&ms, c->pev[0], c->pev[1]) == hipSuccess) {
+            c->kms[K_PLAN] = ms;
+            c->kcount[K_PLAN] = 1;
         }
     }
     return 0;
@@ -1952,6 +2219,8 @@ extern "C" int vp9hip_plan_stats(const vp9h_frame *f, double *out, int cap)
     fb.pitch[0] = fb.sb_cols * 64; fb.pitch[1] = fb.sb_cols * 64 >> f->ss_h;
     fb.coef_base = 0;
     fb.phase = 0;
+    memset(&fb.mc, 0, sizeof(fb.mc));
+    fb.mc.cols = fb.cols; fb.mc.rows = fb.rows; fb.mc.ss_h = f->ss_h; fb.mc.ss_v = f->ss_v;
     s.rbucket.resize(1);
     std::vector<std::vector<uint32_t>> ps, ls;
     int r = build_frame(nullptr, s, fb, ps, ls);
