@@ -53,6 +53,10 @@ struct ParseJob {
 };
 struct Pending { vp9h_frame pkt; int out; int refs[3]; };   // refs: -1 for keyframes / intra-only
 struct Out { int buf; int64_t pts; bool submitted; };
+// Batches are numbered as launched; a frame's batch is the one that wrote its buffer
+// (buf_seq). A batch is checked (vp9hip_sync: the stream is drained and k_lfr's
+// hand-off timeout words are read) before the next one is staged, whose staging resets
+// them, or before one of its frames is handed out, whichever comes first.
 const int STALL = 1;                   // consume: no free device buffer until frames are released
 }
 
@@ -63,6 +67,9 @@ struct vp9hip_decoder {
     int cw = 0, ch = 0, cbpp = 0, css_h = 0, css_v = 0, nbufs = 0;
     int slot[8];
     std::vector<int> pins, busy, bw, bh;   // per device buffer
+    std::vector<uint64_t> buf_seq;         // per device buffer: the batch that wrote it
+    uint64_t launched = 0, checked = 0;    // batches launched / checked
+    std::vector<uint64_t> bad;             // batches whose check failed (VP9HIP_EBUG)
     std::vector<Pending> batch;
     std::deque<Out> outq;
     // parse pipeline
@@ -158,9 +165,29 @@ static void wait_all_parsed(vp9hip_decoder *d)
 
 // ---- device side ----
 // Stage + launch the pending frames as one batch.
+// Check the launched batches: 0, or the error of a failed check other than VP9HIP_EBUG
+// (an EBUG batch is remembered; its frames fail when they are received).
+static int check_batches(vp9hip_decoder *d)
+{
+    if (d->checked == d->launched) return 0;
+    const int r = vp9hip_sync(d->ctx);
+    if (r == VP9HIP_EBUG) d->bad.push_back(d->launched);
+    else if (r < 0) return r;
+    d->checked = d->launched;
+    return 0;
+}
+
+static bool batch_bad(const vp9hip_decoder *d, uint64_t seq)
+{
+    for (uint64_t b : d->bad) if (b == seq) return true;
+    return false;
+}
+
 static int submit(vp9hip_decoder *d)
 {
     if (d->batch.empty()) return 0;
+    int cr = check_batches(d);                // before the staging resets the batch's words
+    if (cr < 0) return cr;
     const int n = (int) d->batch.size();
     std::vector<vp9h_frame> pk(n);
     std::vector<int> outs(n), refs(3 * n);
@@ -171,6 +198,8 @@ static int submit(vp9hip_decoder *d)
     }
     int ret = vp9hip_stage_batch_refs(d->ctx, pk.data(), n, outs.data(), refs.data());
     if (ret >= 0) ret = vp9hip_run_batch(d->ctx);
+    d->launched++;
+    for (int i = 0; i < n; i++) d->buf_seq[outs[i]] = d->launched;
     for (auto &f : d->batch) {
         vp9h_frame_free(&f.pkt);
         d->busy[f.out]--;
@@ -196,6 +225,7 @@ static int configure(vp9hip_decoder *d, const vp9h_frame &f)
     d->cw = w; d->ch = h; d->cbpp = f.bpp; d->css_h = f.ss_h; d->css_v = f.ss_v;
     d->nbufs = nb;
     d->pins.assign(nb, 0); d->busy.assign(nb, 0); d->bw.assign(nb, 0); d->bh.assign(nb, 0);
+    d->buf_seq.assign(nb, 0);
     for (int s = 0; s < 8; s++) d->slot[s] = -1;
     return 0;
 }
@@ -380,7 +410,15 @@ extern "C" int vp9hip_decoder_receive_frame(vp9hip_decoder *d, vp9hip_decoded_fr
         return d->draining && d->inflight.empty() && d->batch.empty() ? VP9HIP_EOF : VP9HIP_EAGAIN;
     if (!d->outq.front().submitted) return VP9HIP_EAGAIN;
     const Out o = d->outq.front();
+    if (d->buf_seq[o.buf] > d->checked) {      // its batch may still run: drain and check it
+        r = check_batches(d);
+        if (r < 0) return r;
+    }
     d->outq.pop_front();
+    if (batch_bad(d, d->buf_seq[o.buf])) {     // the loop filter's row hand-off broke
+        d->pins[o.buf]--;
+        return VP9HIP_EBUG;
+    }
     memset(out, 0, sizeof(*out));
     out->buf = o.buf;
     out->width = d->bw[o.buf];

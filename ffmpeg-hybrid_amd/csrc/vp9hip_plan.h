@@ -83,6 +83,7 @@ typedef struct PlanDev {
     /* capacities: every planner write is checked against them; a violation sets a bit of
      * status[1] (and PLS_SCHED) instead of writing */
     uint32_t cap_cnt, cap_cntm, cap_rjobs, cap_mcs, cap_dlists, nkeys, nframes;
+    unsigned long long *prof;        /* diagnostics (VP9HIP_PLAN_PROF): k_plan cycles per phase, or null */
 } PlanDev;
 
 #endif

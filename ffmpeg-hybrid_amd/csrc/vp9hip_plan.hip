@@ -28,21 +28,25 @@
 
 namespace {
 
-DEV uint32_t wscan_incl(uint32_t v, int lane)
+// Wave-wide scans and reductions on DPP (row shifts within 16-lane rows, then the gfx9
+// row broadcasts of lanes 15 / 31): VALU-latency steps instead of ds_bpermute round trips.
+// Every value of a uniform lane index is read with readlane.
+enum { OP_ADD, OP_OR, OP_MAX };
+template <int OP> DEV uint32_t dpp_op(uint32_t a, uint32_t b) { return OP == OP_OR ? (a | b) : OP == OP_MAX ? (a > b ? a : b) : (a + b); }
+template <int OP> DEV uint32_t wscan_dpp(uint32_t v)
 {
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t t = __shfl_up(v, d);
-        if (lane >= d) v += t;
-    }
+    v = dpp_op<OP>(v, (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x111, 0xf, 0xf, true));   // row_shr:1
+    v = dpp_op<OP>(v, (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x112, 0xf, 0xf, true));   // row_shr:2
+    v = dpp_op<OP>(v, (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x114, 0xf, 0xf, true));   // row_shr:4
+    v = dpp_op<OP>(v, (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x118, 0xf, 0xf, true));   // row_shr:8
+    v = dpp_op<OP>(v, (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    v = dpp_op<OP>(v, (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x143, 0xc, 0xf, false));  // row_bcast:31
     return v;
 }
-DEV uint32_t wsum(uint32_t v)
-{
-#pragma unroll
-    for (int d = 32; d; d >>= 1) v += __shfl_xor(v, d);
-    return v;
-}
+DEV uint32_t wscan_incl(uint32_t v, int) { return wscan_dpp<OP_ADD>(v); }
+DEV uint32_t rdl(uint32_t v, int l) { return (uint32_t) __builtin_amdgcn_readlane((int) v, l); }
+DEV int rdl(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+DEV uint32_t wsum(uint32_t v) { return rdl(wscan_dpp<OP_ADD>(v), 63); }
 DEV uint32_t mbcnt(uint64_t m)
 {
     return __builtin_amdgcn_mbcnt_hi((uint32_t) (m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) m, 0));
@@ -55,9 +59,13 @@ DEV bool inb(const PlanDev &D, uint32_t i, uint32_t cap, uint32_t bit)
     atomicOr(&D.status[0], PLS_BOUNDS);
     return false;
 }
+// The planner's workgroups are one wave: the LDS unit executes a wave's DS instructions in
+// order, so a wave-scope fence (compiler ordering) replaces the workgroup barrier.
 DEV void wsync()
 {
-    __syncthreads();      // one-wave workgroups: orders the wave's LDS accesses
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // A block as the planner uses it: fields out of range are clamped (the batch fails with
@@ -96,7 +104,7 @@ DEV uint32_t sb_prefix(const vp9h_block *blk, int nb, int cols, int rows, bool m
         pre[3 * lane + 1] = excl + v[0];
         pre[3 * lane + 2] = excl + v[0] + v[1];
     }
-    const uint32_t tot = __shfl(incl, 63);
+    const uint32_t tot = rdl(incl, 63);
     if (lane == 0) pre[3 * nb] = tot;
     wsync();
     return tot;
@@ -120,10 +128,10 @@ struct Tx {
     PlTxGrid g;
 };
 template <int SSH, int SSV>
-DEV Tx sb_tx(const vp9h_block *blk, const uint32_t *pre, int nb, uint32_t t, int cols, int rows)
+DEV Tx sb_tx_at(const vp9h_block *blk, const uint32_t *pre, int k, uint32_t t, int cols, int rows)
 {
     Tx r;
-    r.k = sb_locate(pre, 3 * nb, t);
+    r.k = k;
     r.b = r.k / 3;
     r.p = r.k - 3 * r.b;
     r.l = (int) (t - (pre[r.k] & 1023));
@@ -132,6 +140,11 @@ DEV Tx sb_tx(const vp9h_block *blk, const uint32_t *pre, int nb, uint32_t t, int
     r.x = (r.l % nx) << r.g.txs;
     r.y = (r.l / nx) << r.g.txs;
     return r;
+}
+template <int SSH, int SSV>
+DEV Tx sb_tx(const vp9h_block *blk, const uint32_t *pre, int nb, uint32_t t, int cols, int rows)
+{
+    return sb_tx_at<SSH, SSV>(blk, pre, sb_locate(pre, 3 * nb, t), t, cols, rows);
 }
 
 // The eob of tx t (0 for skipped blocks), range-checked against the packet.
@@ -299,24 +312,35 @@ __global__ __launch_bounds__(64) void k_psb(PlanDev D)
 }
 
 // ------------------------------------------------------------------ k_plan
+// k_plan's LDS: the fields of consecutive phases share storage (lifetimes in brackets).
 template <int JCAP> struct PlanLds {
-    vp9h_block blk[64];
-    uint32_t pre[3 * 64 + 1];
-    uint16_t et[JCAP];            // eob per tx (decode order)
-    uint16_t co[JCAP];            // SB-relative first coefficient per tx
-    uint32_t ja[JCAP];            // PJob word per intra job (decode order)
-    uint8_t  jx[JCAP];            // 4x4 top-right inside the block (trx)
-    uint16_t jmap[3][256];        // producing job of each 4x4 unit
-    uint16_t doff[JCAP + 1];      // producers of job j: dep[doff[j] .. doff[j + 1])
-    uint16_t dep[4 * JCAP];
-    uint32_t hgt[JCAP];           // longest path to a sink (list-scheduling priority)
-    uint16_t ord[JCAP];           // jobs by (height desc, index asc)
-    uint16_t sch[JCAP];           // pass of each job (0xffff: not yet)
-    uint32_t hs[64];              // height histogram -> list starts
-    uint32_t lfm[2][2][8];        // LF masks [cls][dir][row]: kinds 0..3 in bytes
-    uint8_t  lfl[64];             // LF level of each 8x8
-    uint32_t prog[LF_PROG_BYTES / 4];
-    uint16_t tk[16];              // jobs taken by the pass being built
+    vp9h_block blk[64];           // [all]
+    uint32_t ja[JCAP];            // [jobs .. cross reads] PJob word per intra job (decode order)
+    uint8_t  jx[JCAP];            // [jobs .. cross reads] 4x4 top-right inside the block (trx)
+    uint16_t jmap[3][256];        // [jobs .. producers] producing job of each 4x4 unit
+    union {
+        struct {                  // [prefix .. jobs]
+            uint32_t pre[3 * 64 + 1];
+            uint16_t et[JCAP];    // eob per tx (decode order)
+            uint16_t co[JCAP];    // SB-relative first coefficient per tx
+            uint32_t ost[JCAP];   // (block, plane) entry starting at tx t, else 0
+            uint8_t  own[JCAP];   // (block, plane) entry of tx t (max-scan of ost)
+        } a;
+        struct {                  // [producers .. scheduling]
+            uint16_t doff[JCAP + 1];      // producers of job j: dep[doff[j] .. doff[j + 1])
+            uint16_t dep[4 * JCAP];
+            uint32_t hgt[JCAP];           // longest path to a sink (list-scheduling priority)
+            uint16_t ord[JCAP];           // jobs by (height desc, index asc)
+            uint16_t sch[JCAP];           // pass of each job (0xffff: not yet)
+            uint32_t hs[64];              // height histogram -> list starts
+            uint16_t tk[16];              // jobs taken by the pass being built
+        } b;
+        struct {                  // [loop filter]
+            uint32_t lfm[2][2][8];        // LF masks [cls][dir][row]: kinds 0..3 in bytes
+            uint8_t  lfl[64];             // LF level of each 8x8
+            uint32_t prog[LF_PROG_BYTES / 4];
+        } c;
+    } u;
 };
 
 // edges the job's (substituted) mode reads: 1 left, 2 top, 4 top-left, 8 top-right (pl_intra_job)
@@ -325,12 +349,11 @@ DEV uint32_t needs_of(uint32_t a)
     const uint8_t needs[16] = { 2, 1, 2 | 8, 1 | 2 | 4, 1 | 2 | 4, 1 | 2 | 4, 2 | 8, 1, 1 | 2 | 4, 1 | 2, 1, 2, 0, 0, 0, 0 };
     return needs[(a >> 8) & 15];
 }
-DEV uint32_t wor(uint32_t v)
-{
-#pragma unroll
-    for (int d = 32; d; d >>= 1) v |= __shfl_xor(v, d);
-    return v;
-}
+DEV uint32_t wor(uint32_t v) { return rdl(wscan_dpp<OP_OR>(v), 63); }
+
+// VP9HIP_PLAN_PROF: shader-clock cycles of each k_plan phase, summed over the SBs
+#define PPT(k) do { if (D.prof) { const unsigned long long t_ = clock64(); \
+        if (lane == 0) atomicAdd(&D.prof[k], t_ - pt0); pt0 = t_; } } while (0)
 
 template <int SSH, int SSV>
 __global__ __launch_bounds__(64) void k_plan(PlanDev D)
@@ -340,6 +363,7 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
     const PlanFrame &F = D.frames[blockIdx.y];
     const int s = blockIdx.x, lane = threadIdx.x;
     if (s >= F.sb_cols * F.sb_rows) return;
+    unsigned long long pt0 = D.prof ? clock64() : 0;
     const SbGeo G = sb_geo(F, s);
     const int cols = F.mc.cols, rows = F.mc.rows;
     const uint32_t slot = G.slot;
@@ -348,26 +372,45 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
     st = 0;                                   // reported by k_psb
     if (lane < nb) S.blk[lane] = load_block(&D.blocks[b0 + lane]);
     for (int i = lane; i < 3 * 256; i += 64) (&S.jmap[0][0])[i] = 0xffff;
-    if (lane < 32) (&S.lfm[0][0][0])[lane] = 0;
-    S.lfl[lane] = 0;
-    for (int i = lane; i < LF_PROG_BYTES / 4; i += 64) S.prog[i] = 0;
     wsync();
-    const uint32_t tot = sb_prefix<SSH, SSV>(S.blk, nb, cols, rows, G.mine, S.pre, lane);
+    const uint32_t tot = sb_prefix<SSH, SSV>(S.blk, nb, cols, rows, G.mine, S.u.a.pre, lane);
     const int T = pl_min((int) (tot & 1023), JCAP), NJ = pl_min((int) (tot >> 20), JCAP);
+    // the (block, plane) entry of every tx: each non-empty entry marks its first tx (ranges
+    // are disjoint), a max-scan fills the rest (= sb_locate's largest k with pre[k] <= t)
+    for (int t = lane; t < T; t += 64) S.u.a.ost[t] = 0;
+    wsync();
+    if (lane < nb)
+        for (int p = 0; p < 3; p++) {
+            const int k = 3 * lane + p;
+            const uint32_t a0 = S.u.a.pre[k] & 1023, a1 = S.u.a.pre[k + 1] & 1023;
+            if (a1 > a0 && a0 < (uint32_t) T) S.u.a.ost[a0] = (uint32_t) k;
+        }
+    wsync();
+    {
+        uint32_t carry = 0;
+        for (int c = 0; c < T; c += 64) {
+            const uint32_t v = c + lane < T ? S.u.a.ost[c + lane] : 0u;
+            const uint32_t incl = dpp_op<OP_MAX>(wscan_dpp<OP_MAX>(v), carry);
+            if (c + lane < T) S.u.a.own[c + lane] = (uint8_t) incl;
+            carry = rdl(incl, 63);
+        }
+    }
+    wsync();
+    PPT(0);
 
     // ---- eobs and SB-relative coefficient offsets (decode order)
     for (int t = lane; t < T; t += 64) {
-        const Tx tx = sb_tx<SSH, SSV>(S.blk, S.pre, nb, (uint32_t) t, cols, rows);
-        S.et[t] = (uint16_t) tx_eob(D, S.blk[tx.b], tx, S.pre, b0, st);
+        const Tx tx = sb_tx_at<SSH, SSV>(S.blk, S.u.a.pre, S.u.a.own[t], (uint32_t) t, cols, rows);
+        S.u.a.et[t] = (uint16_t) tx_eob(D, S.blk[tx.b], tx, S.u.a.pre, b0, st);
     }
     wsync();
     {
         uint32_t carry = 0;
         for (int c = 0; c < T; c += 64) {
-            const uint32_t v = c + lane < T ? S.et[c + lane] : 0u;
+            const uint32_t v = c + lane < T ? S.u.a.et[c + lane] : 0u;
             const uint32_t incl = wscan_incl(v, lane);
-            if (c + lane < T) S.co[c + lane] = (uint16_t) (carry + incl - v);
-            carry += __shfl(incl, 63);
+            if (c + lane < T) S.u.a.co[c + lane] = (uint16_t) (carry + incl - v);
+            carry += rdl(incl, 63);
         }
     }
     // record bases of the SB: lanes 0..19 residual keys (tcode * 4 + txtp), lane 20 MC units
@@ -383,6 +426,7 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
     const uint32_t rbase = slot * D.rcap;
     unsigned long long ibytes = 0, mbytes = 0;
     wsync();
+    PPT(1);
 
     // ---- residual jobs (every coded tx block) and intra jobs with their unit map
     const int tx0l = G.tile_sb0 * 64;
@@ -391,10 +435,10 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
         int key = -1;
         RJob r;
         if (t < T) {
-            const Tx tx = sb_tx<SSH, SSV>(S.blk, S.pre, nb, (uint32_t) t, cols, rows);
+            const Tx tx = sb_tx_at<SSH, SSV>(S.blk, S.u.a.pre, S.u.a.own[t], (uint32_t) t, cols, rows);
             const vp9h_block &b = S.blk[tx.b];
             const int p = tx.p, sh = p ? SSH : 0, sv = p ? SSV : 0, txs = tx.g.txs;
-            const int e0 = S.et[t];
+            const int e0 = S.u.a.et[t];
             int mode = 0, txtp = 0;
             if (b.intra) {
                 mode = tx_mode(b, tx, st);
@@ -404,7 +448,7 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
             const int ux0 = ((tx.g.bx - G.sbx * (64 >> sh)) >> 2) + tx.x, uy0 = ((tx.g.by - G.sby * (64 >> sv)) >> 2) + tx.y;
             const uint32_t roff = rbase + pl_resid_unit(p, ux0, uy0, SSH, SSV);
             if (e0 && G.mine) {
-                uint32_t coef = coef_sb + S.co[t];
+                uint32_t coef = coef_sb + S.u.a.co[t];
                 int e = e0;
                 if (coef + (uint32_t) e > D.total_coefs) { st |= PLS_COEF; e = 0; coef = 0; }
                 r.coef = coef;
@@ -422,7 +466,7 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
                 key = tcode * 4 + txtp;
             }
             if (b.intra && G.mine) {
-                const int j = (int) (S.pre[tx.k] >> 20) + tx.l;
+                const int j = (int) (S.u.a.pre[tx.k] >> 20) + tx.l;
                 const int pw8 = p ? cols * 8 >> SSH : cols * 8, ph8 = p ? rows * 8 >> SSV : rows * 8;
                 const PlIntra pi = pl_intra_job(p, txs, mode, e0, tx.g.bx + tx.x * 4, tx.g.by + tx.y * 4, tx.x, tx.g.pw4,
                                                 p ? tx0l >> SSH : tx0l, pw8, ph8, ux0, uy0);
@@ -440,9 +484,9 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
         uint32_t pos = 0;
         while (pend) {
             const int l0 = __builtin_ctzll(pend);
-            const int kk = __shfl(key, l0);
+            const int kk = rdl(key, l0);
             const uint64_t m = __ballot(key == kk);
-            const uint32_t base = __shfl(rb, kk);
+            const uint32_t base = rdl(rb, kk);
             if (key == kk) pos = base + mbcnt(m);
             if (lane == kk) rb += (uint32_t) __popcll(m);
             pend &= ~m;
@@ -450,6 +494,7 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
         if (key >= 0 && inb(D, pos, D.cap_rjobs, 64u)) D.rjobs[pos] = r;
     }
     wsync();
+    PPT(2);
 
     // ---- producers of every intra job (the pixels its substituted mode reads)
     auto deps_of = [&](int j, auto fn) {
@@ -478,68 +523,75 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
             uint32_t n = 0;
             if (j < NJ) deps_of(j, [&](int) { n++; });
             const uint32_t incl = wscan_incl(n, lane);
-            if (j < NJ) S.doff[j] = (uint16_t) (carry + incl - n);
-            carry += __shfl(incl, 63);
+            if (j < NJ) S.u.b.doff[j] = (uint16_t) (carry + incl - n);
+            carry += rdl(incl, 63);
         }
         if (carry > 4 * JCAP) {             // more producers than valid tilings allow: no order
             st |= PLS_SCHED;
-            for (int j = lane; j <= NJ; j += 64) S.doff[j] = 0;
+            for (int j = lane; j <= NJ; j += 64) S.u.b.doff[j] = 0;
             carry = 0;
         }
-        if (lane == 0) S.doff[NJ] = (uint16_t) carry;
+        if (lane == 0) S.u.b.doff[NJ] = (uint16_t) carry;
         wsync();
         for (int j = lane; j < NJ; j += 64) {
-            int k = S.doff[j];
-            if (carry) deps_of(j, [&](int d) { S.dep[k++] = (uint16_t) d; });
-            S.hgt[j] = 1;
-            S.sch[j] = 0xffff;
+            int k = S.u.b.doff[j];
+            if (carry) deps_of(j, [&](int d) { S.u.b.dep[k++] = (uint16_t) d; });
+            S.u.b.hgt[j] = 1;
+            S.u.b.sch[j] = 0xffff;
         }
     }
     wsync();
-    // ---- heights (longest path to a sink): relax until stable
-    for (int it = 0; it < JCAP + 1; it++) {
-        bool ch = false;
-        for (int c = ((NJ - 1) & ~63); c >= 0; c -= 64) {
-            const int j = c + lane;
+    PPT(3);
+    // ---- heights (longest path to a sink). Producers precede their consumers (d < j), so
+    // the chunks of 64 jobs are finished last to first: a chunk's consumers in later chunks
+    // are final, and the chunk relaxes until none of its own jobs rises (at most one round
+    // per job of a chain inside it); its last round pushes final heights to every producer
+    for (int c = ((NJ - 1) & ~63); c >= 0; c -= 64) {
+        const int j = c + lane;
+        const int k0 = j < NJ ? S.u.b.doff[j] : 0, k1 = j < NJ ? S.u.b.doff[j + 1] : 0;
+        for (int it = 0; it < 65; it++) {
+            bool ch = false;                  // a job of this chunk rose
             if (j < NJ) {
-                const uint32_t h1 = S.hgt[j] + 1;
-                for (int k = S.doff[j]; k < S.doff[j + 1]; k++) {
-                    const int d = S.dep[k];
-                    if (S.hgt[d] < h1) { atomicMax(&S.hgt[d], h1); ch = true; }
+                const uint32_t h1 = S.u.b.hgt[j] + 1;
+                for (int k = k0; k < k1; k++) {
+                    const int d = S.u.b.dep[k];
+                    if (S.u.b.hgt[d] < h1) { atomicMax(&S.u.b.hgt[d], h1); ch |= d >= c; }
                 }
             }
             wsync();
+            if (!__any(ch)) break;
         }
-        if (!__any(ch)) break;
     }
+    PPT(4);
     // ---- priority order: height descending, then decode order
-    S.hs[lane] = 0;
+    S.u.b.hs[lane] = 0;
     wsync();
-    for (int j = lane; j < NJ; j += 64) atomicAdd(&S.hs[pl_min((int) S.hgt[j], 63)], 1u);
+    for (int j = lane; j < NJ; j += 64) atomicAdd(&S.u.b.hs[pl_min((int) S.u.b.hgt[j], 63)], 1u);
     wsync();
     {
-        const uint32_t v = S.hs[63 - lane];                // heights from the top
+        const uint32_t v = S.u.b.hs[63 - lane];                // heights from the top
         const uint32_t incl = wscan_incl(v, lane);
         wsync();
-        S.hs[63 - lane] = incl - v;
+        S.u.b.hs[63 - lane] = incl - v;
         wsync();
         for (int c = 0; c < NJ; c += 64) {
             const int j = c + lane;
-            const int h = j < NJ ? pl_min((int) S.hgt[j], 63) : -1;
+            const int h = j < NJ ? pl_min((int) S.u.b.hgt[j], 63) : -1;
             uint64_t pend = __ballot(h >= 0);
             while (pend) {
-                const int hh = __shfl(h, __builtin_ctzll(pend));
+                const int hh = rdl(h, __builtin_ctzll(pend));
                 const uint64_t m = __ballot(h == hh);
-                const uint32_t base = S.hs[hh];
-                if (h == hh) S.ord[base + mbcnt(m)] = (uint16_t) j;
+                const uint32_t base = S.u.b.hs[hh];
+                if (h == hh) S.u.b.ord[base + mbcnt(m)] = (uint16_t) j;
                 wsync();
-                if (lane == 0) S.hs[hh] = base + (uint32_t) __popcll(m);
+                if (lane == 0) S.u.b.hs[hh] = base + (uint32_t) __popcll(m);
                 wsync();
                 pend &= ~m;
             }
         }
     }
     wsync();
+    PPT(5);
     // ---- list scheduling (merge_mixed): each pass takes, in priority order, every ready job
     // (all producers in earlier passes) that still fits in 64 lanes; lane groups by size
     uint32_t *gpass = D.passes + (size_t) slot * JCAP;
@@ -549,27 +601,27 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
         int budget = 64, ntake = 0;
         for (int c = c0; c < NJ && budget >= 4; c += 64) {
             const int pos = c + lane;
-            const int j = pos < NJ ? S.ord[pos] : 0;
-            bool cand = pos < NJ && S.sch[j] == 0xffff;
+            const int j = pos < NJ ? S.u.b.ord[pos] : 0;
+            bool cand = pos < NJ && S.u.b.sch[j] == 0xffff;
             if (cand)
-                for (int k = S.doff[j]; k < S.doff[j + 1]; k++)
-                    if (S.sch[S.dep[k]] >= (uint16_t) npass) { cand = false; break; }
+                for (int k = S.u.b.doff[j]; k < S.u.b.doff[j + 1]; k++)
+                    if (S.u.b.sch[S.u.b.dep[k]] >= (uint16_t) npass) { cand = false; break; }
             const int sz = 4 << ((S.ja[j] >> 2) & 3);
             for (;;) {
                 const uint64_t m = __ballot(cand && sz <= budget);
                 if (!m) break;
                 const int i0 = __builtin_ctzll(m);
-                const int J = __shfl(j, i0);
-                budget -= __shfl(sz, i0);
-                if (lane == i0) { cand = false; S.sch[J] = (uint16_t) npass; }
-                if (lane == 0) S.tk[ntake] = (uint16_t) J;
+                const int J = rdl(j, i0);
+                budget -= rdl(sz, i0);
+                if (lane == i0) { cand = false; S.u.b.sch[J] = (uint16_t) npass; }
+                if (lane == 0) S.u.b.tk[ntake] = (uint16_t) J;
                 ntake++;
             }
         }
         wsync();
         if (ntake == 0) { st |= PLS_SCHED; break; }
         // emit: sizes 32, 16, 8, 4, take order within a size
-        const int J = lane < ntake ? S.tk[lane] : 0;
+        const int J = lane < ntake ? S.u.b.tk[lane] : 0;
         const int ts = lane < ntake ? (int) ((S.ja[J] >> 2) & 3) : -1;
         uint32_t cnt[4], at = 0;
         int mypos = 0;
@@ -592,7 +644,7 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
         // skip chunks of the priority order that are fully scheduled
         while (c0 < NJ) {
             const int pos = c0 + lane;
-            if (__any(pos < NJ && S.sch[S.ord[pos]] == 0xffff)) break;
+            if (__any(pos < NJ && S.u.b.sch[S.u.b.ord[pos]] == 0xffff)) break;
             c0 += 64;
         }
         wsync();
@@ -609,6 +661,7 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
         w.sb[0] = slot;
         D.wgs[slot] = w;
     }
+    PPT(6);
 
     // ---- cross-SB reads of level-scheduled inter frames: left / top / top-left SBs whose
     // intra units this SB's jobs read (the host's umap levels)
@@ -628,13 +681,14 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
             });
         }
     dmask = wor(dmask);
+    PPT(7);
 
     // ---- MC units (inter blocks in decode order)
     {
         const bool mc = lane < nb && G.mine && !S.blk[lane].intra && mc_refs_ok(S.blk[lane], F.mc);
         const uint32_t n = mc ? (uint32_t) pl_mc_block(S.blk[lane], F.mc, 0, [](const McUnit &) {}) : 0u;
         const uint32_t incl = wscan_incl(n, lane);
-        uint32_t o = __shfl(rb, 20) + incl - n;
+        uint32_t o = rdl(rb, 20) + incl - n;
         if (mc)
             pl_mc_block(S.blk[lane], F.mc, (uint32_t) F.frame, [&](const McUnit &m) {
                 if (inb(D, o, D.cap_mcs, 512u)) D.mcs[o] = m;
@@ -642,32 +696,39 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
                 mbytes += (unsigned long long) m.w * m.h * F.bypp * (1 + m.nref);
             });
     }
+    PPT(8);
 
     // ---- loop-filter levels, masks and program (vp9block.c:1438-1452, vp9lpf.c:31-230)
     if (F.filter_level) {
+        wsync();                              // the scheduling fields are dead: LF fields reuse them
+        if (lane < 32) (&S.u.c.lfm[0][0][0])[lane] = 0;
+        S.u.c.lfl[lane] = 0;
+        for (int i = lane; i < LF_PROG_BYTES / 4; i += 64) S.u.c.prog[i] = 0;
+        wsync();
         if (lane < nb) {
             const vp9h_block &b = S.blk[lane];
             if (const int lvl = pl_lf_level(b, F.lflvl, F.filter_level)) {
                 const int bw8 = pl_bwh(1, b.bs, 0), bh8 = pl_bwh(1, b.bs, 1), col7 = b.col & 7, row7 = b.row & 7;
                 for (int yy = 0; yy < bh8; yy++)
                     for (int xx = 0; xx < bw8; xx++)
-                        if (row7 + yy < 8 && col7 + xx < 8) S.lfl[(row7 + yy) * 8 + col7 + xx] = (uint8_t) lvl;
+                        if (row7 + yy < 8 && col7 + xx < 8) S.u.c.lfl[(row7 + yy) * 8 + col7 + xx] = (uint8_t) lvl;
                 pl_lf_block_masks(b, cols, rows, SSH, SSV, [&](int cls, int d, int y, int k, unsigned v) {
-                    if (y < 8) atomicOr(&S.lfm[cls][d][y], (v & 255u) << (8 * k));
+                    if (y < 8) atomicOr(&S.u.c.lfm[cls][d][y], (v & 255u) << (8 * k));
                 });
             }
         }
         wsync();
-        uint8_t *prog = (uint8_t *) S.prog;
+        uint8_t *prog = (uint8_t *) S.u.c.prog;
         for (int i = lane; i < pl_lf_items(SSH, SSV); i += 64)
-            pl_lf_item(i, SSH, SSV, G.sbx == 0, G.sby == 0, [&](int pos) { return (int) S.lfl[pos]; },
-                       [&](int cls, int d, int y, int k) { return (S.lfm[cls][d][y] >> (8 * k)) & 255u; },
+            pl_lf_item(i, SSH, SSV, G.sbx == 0, G.sby == 0, [&](int pos) { return (int) S.u.c.lfl[pos]; },
+                       [&](int cls, int d, int y, int k) { return (S.u.c.lfm[cls][d][y] >> (8 * k)) & 255u; },
                        [&](int off, uint8_t v) { prog[off] = v; });
         wsync();
         uint32_t *g = (uint32_t *) &D.lfs[slot];
         for (int i = lane; i < (int) (sizeof(LFRec) / 4); i += 64)
-            g[i] = i == 0 ? (uint32_t) F.frame : i == 1 ? ((uint32_t) G.sbx | (uint32_t) G.sby << 16) : S.prog[i - 2];
+            g[i] = i == 0 ? (uint32_t) F.frame : i == 1 ? ((uint32_t) G.sbx | (uint32_t) G.sby << 16) : S.u.c.prog[i - 2];
     }
+    PPT(9);
 
     // ---- the SB's intra step (diagonal phases; level phases in k_plevel) and batch totals
     if (lane == 0) {
@@ -690,6 +751,7 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
     }
     st = wor(st);
     if (lane == 0 && st) atomicOr(D.status, st);
+    PPT(10);
 }
 
 // ------------------------------------------------------------------ k_plevel

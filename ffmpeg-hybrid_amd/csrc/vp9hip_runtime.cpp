@@ -193,6 +193,7 @@ struct vp9hip_ctx {
     uint8_t *nz = nullptr;              // nonzero bounding boxes per (tcode, txtp, eob) (device, planner)
     bool host_plan = false;             // VP9HIP_HOST_PLAN=1: plan batches on host threads (A/B, tests)
     hipEvent_t pev[2] = {};             // device planner timing (timing runs)
+    unsigned long long *plan_prof = nullptr;   // VP9HIP_PLAN_PROF: k_plan phase cycles (device)
     bool plan_timed = false;
     int dbg = 0;                        // VP9HIP_DEBUG: ablation switches for profiling only
     bool use_graph = true;              // VP9HIP_GRAPH=0 disables graph replay
@@ -259,6 +260,7 @@ extern "C" void vp9hip_close(vp9hip_ctx *c)
     if (c->stg.graph) hipGraphExecDestroy(c->stg.graph);
     if (c->ptab) hipFree(c->ptab);
     if (c->nz) hipFree(c->nz);
+    if (c->plan_prof) hipFree(c->plan_prof);
     if (c->stg.summary_h) hipHostFree(c->stg.summary_h);
     for (auto e : c->pev) if (e) hipEventDestroy(e);
     for (auto e : c->ev) hipEventDestroy(e);
@@ -832,6 +834,16 @@ struct DevIn {
     bool fuse, lfr_any;
 };
 
+// k_lfr counter blocks of a staged batch, zeroed; word 3 of each block is the spin bound of
+// a hand-off wait (VP9HIP_LFR_SPIN: a test hook that forces the timeout path; 0 = default)
+static void init_lfr_ctr(const Staged &s, uint32_t *ctr)
+{
+    memset(ctr, 0, (size_t) s.n_ctr * 4);
+    const char *e = getenv("VP9HIP_LFR_SPIN");
+    const uint32_t spin = e ? (uint32_t) strtoul(e, nullptr, 0) : 0u;
+    for (uint32_t o : s.lfr_ctr) ctr[o + 3] = spin;
+}
+
 static int stage_dev(vp9hip_ctx *c, const DevIn &in)
 {
     Staged &s = c->stg;
@@ -1107,7 +1119,7 @@ static int stage_dev(vp9hip_ctx *c, const DevIn &in)
     if (!seg_pre1.empty()) memcpy(img + s.o_segpre1, seg_pre1.data(), seg_pre1.size() * 4);
     if (!gidx.empty()) memcpy(img + s.o_gidx, gidx.data(), gidx.size() * 4);
     if (!hl.empty()) memcpy(img + s.o_lists, hl.data(), hl.size() * 4);
-    memset(img + s.o_ctr, 0, (size_t) s.n_ctr * 4);
+    init_lfr_ctr(s, (uint32_t *) (img + s.o_ctr));
     {   // packets: blocks, eobs, coefficients (frames copied in parallel)
         std::atomic<int> next(0);
         auto worker = [&]() {
@@ -1193,6 +1205,13 @@ static int plan_dev(vp9hip_ctx *c)
     D.cap_dlists = s.nslots;
     D.nkeys = s.nkey;
     D.nframes = (uint32_t) s.nframes;
+    static const bool pprof = getenv("VP9HIP_PLAN_PROF") && atoi(getenv("VP9HIP_PLAN_PROF"));
+    D.prof = nullptr;
+    if (pprof) {
+        if (!c->plan_prof && hipMalloc(&c->plan_prof, 16 * sizeof(unsigned long long)) != hipSuccess) return VP9HIP_ENOMEM;
+        HIPCHK(hipMemsetAsync(c->plan_prof, 0, 16 * sizeof(unsigned long long), c->st));
+        D.prof = c->plan_prof;
+    }
     if (c->timing) {
         for (auto &e : c->pev)
             if (!e) HIPCHK(hipEventCreate(&e));
@@ -1206,6 +1225,15 @@ static int plan_dev(vp9hip_ctx *c)
     c->plan_timed = c->timing;
     HIPCHK(hipMemcpyAsync(s.summary_h, A + s.o_summary, s.summary_words * 4, hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
+    if (pprof) {
+        unsigned long long pc[16];
+        HIPCHK(hipMemcpy(pc, c->plan_prof, sizeof(pc), hipMemcpyDeviceToHost));
+        double tot = 0;
+        for (int k = 0; k < 11; k++) tot += (double) pc[k];
+        fprintf(stderr, "vp9hip plan phases (%% of k_plan SB cycles, %.3g cycles/SB):", tot / std::max<uint32_t>(1, s.nslots));
+        for (int k = 0; k < 11; k++) fprintf(stderr, " %d:%.1f", k, 100.0 * (double) pc[k] / std::max(1.0, tot));
+        fprintf(stderr, "\n");
+    }
     const uint32_t *sm = s.summary_h;
     if (sm[0]) {                                              // the packets are inconsistent (PLS_*)
         fprintf(stderr, "vp9hip: batch rejected by the device planner (status 0x%x, bounds 0x%x)\n", sm[0],
@@ -1735,7 +1763,7 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     uint8_t *img = s.pinned;
     memcpy(img + s.o_frames, s.frames.data(), s.frames.size() * sizeof(FrameDesc));
     if (!s.lists.empty()) memcpy(img + s.o_lists, s.lists.data(), s.lists.size() * sizeof(uint32_t));
-    memset(img + s.o_ctr, 0, (size_t) s.n_ctr * sizeof(uint32_t));
+    init_lfr_ctr(s, (uint32_t *) (img + s.o_ctr));
     std::vector<double> inplace_bytes(n, 0.0);
     {
         std::atomic<int> next(0);
@@ -2252,6 +2280,21 @@ extern "C" int vp9hip_plan_stats(const vp9h_frame *f, double *out, int cap)
     out[12] = (double) ps.size();
     out[13] = (double) ls.size();
     for (auto &h : s.sbh) out[14] += h.nlev;                           // dependency levels (pass lower bound)
+    if (cap > 17) {                     // passes of ASAP-level packing (jobs of a level, sizes descending)
+        for (size_t sbi = 0; sbi < s.sbh.size(); sbi++) {
+            const Staged::SBHost &h = s.sbh[sbi];
+            const int N = (int) h.njobs;
+            const PJob *jobs = s.sbjobs.data() + h.job0;
+            const uint32_t *d0 = s.jdep0.data() + h.job0 + sbi;
+            std::vector<int> lv(N, 0), lanes;
+            for (int k = 0; k < N; k++) {
+                for (uint32_t e = d0[k]; e < d0[k + 1]; e++) lv[k] = std::max(lv[k], lv[s.jdeps[e]] + 1);
+                if ((int) lanes.size() <= lv[k]) lanes.resize(lv[k] + 1, 0);
+                lanes[lv[k]] += 4 << PJ_TS(jobs[k]);
+            }
+            for (int l : lanes) out[17] += (l + 63) / 64;
+        }
+    }
     if (cap > 16) {                     // intra steps of the level schedule (inter frames)
         Staged s2;
         FrameBuild fb2 = fb;

@@ -9,7 +9,7 @@ from collections import defaultdict
 
 
 def short(name):
-    for k in ("k_plf", "k_resid", "k_pred", "k_recon", "k_lfr", "k_lf", "k_mc"):
+    for k in ("k_plf", "k_resid", "k_pred", "k_recon", "k_lfr", "k_lf", "k_mc", "k_plan", "k_psb", "k_pblk"):
         if k in name:
             return k
     return name[:40]

@@ -1,0 +1,16 @@
+# GPU parity + planner phase profile + C3 bench with 1 / 2 / 3 batches in flight, C2 / C5
+set -e
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r02d_tests.log 2>&1 || { tail -40 gpurun_out/r02d_tests.log; exit 1; }
+tail -1 gpurun_out/r02d_tests.log
+VP9HIP_PLAN_PROF=1 timeout -k 10 300 python bench.py --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/r02d_pp.json 2> gpurun_out/r02d_pp.err
+tail -1 gpurun_out/r02d_pp.err
+line() { python -c "import json;d=json.loads(open('$1').read().strip().split(chr(10))[-1]);print('$2', d['value'], d['ms_per_step'], d['roofline']['kernel_ms'])"; }
+for i in 1 2 3; do
+  timeout -k 10 300 python bench.py --steps 6 --warmup 2 --no-cpu-baseline --inflight $i > gpurun_out/r02d_C3_$i.json 2> gpurun_out/r02d_C3_$i.err
+  line gpurun_out/r02d_C3_$i.json C3_inflight$i
+done
+for c in C2 C5; do
+  timeout -k 10 300 python bench.py --config $c --steps 4 --warmup 2 --no-cpu-baseline --inflight 2 > gpurun_out/r02d_$c.json 2> gpurun_out/r02d_$c.err
+  line gpurun_out/r02d_$c.json ${c}_inflight2
+done
