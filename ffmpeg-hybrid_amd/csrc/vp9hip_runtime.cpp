@@ -1245,6 +1245,8 @@ static int plan_dev(vp9hip_ctx *c)
         return (double) ((uint64_t) fb32[2 * (2 * i + k)] | (uint64_t) fb32[2 * (2 * i + k) + 1] << 32);
     };
     for (int k = 0; k < K_N; k++) s.alg_bytes[k] = s.alg_base[k];
+    // the planner's algorithmic bytes: the packet it plans from (blocks and eobs)
+    s.alg_bytes[K_PLAN] = (double) s.nblk * sizeof(vp9h_block) + (double) s.neob * 2;
     for (int i = 0; i < s.nframes; i++) {
         s.alg_bytes[K_RESID] += fbytes(i, 0);
         s.alg_bytes[K_MC] += fbytes(i, 1);
@@ -1949,11 +1951,17 @@ static int enqueue_batch(vp9hip_ctx *c)
         for (size_t i = old; i < c->ev.size(); i++) HIPCHK(hipEventCreate(&c->ev[i]));
     }
     const bool ovl = c->lf_overlap;
-    auto rstream = [&](int g) { return g ? c->xst[g - 1] : c->st; };
+    // timing runs put every launch on the main stream (serialised, as under a rocprofv3
+    // kernel trace), so each launch's event duration is its own, not one inflated by the
+    // other frame groups' launches (VP9HIP_TIMING_CONCURRENT=1: the groups' own streams)
+    static const bool tconc = getenv("VP9HIP_TIMING_CONCURRENT") && atoi(getenv("VP9HIP_TIMING_CONCURRENT"));
+    const bool serial = c->timing && !tconc && !ovl;
+    const int ngs = serial ? 1 : s.ngroups;
+    auto rstream = [&](int g) { return g && !serial ? c->xst[g - 1] : c->st; };
     // fork: every stream of the batch starts after what is queued on the main stream
-    if (s.ngroups > 1 || ovl) {
+    if (ngs > 1 || ovl) {
         HIPCHK(hipEventRecord(c->fork_ev, c->st));
-        for (int g = 1; g < s.ngroups; g++) HIPCHK(hipStreamWaitEvent(c->xst[g - 1], c->fork_ev, 0));
+        for (int g = 1; g < ngs; g++) HIPCHK(hipStreamWaitEvent(c->xst[g - 1], c->fork_ev, 0));
         if (ovl)
             for (int g = 0; g < s.ngroups; g++) HIPCHK(hipStreamWaitEvent(c->lst[g], c->fork_ev, 0));
     }
@@ -2005,7 +2013,7 @@ static int enqueue_batch(vp9hip_ctx *c)
         if (!lf && ovl && rec_ev[i] >= 0) HIPCHK(hipEventRecord(c->sev[rec_ev[i]], st));
     }
     // join: the main stream (downloads, sync, the next stage) waits for every stream
-    for (int g = 1; g < s.ngroups; g++) {
+    for (int g = 1; g < ngs; g++) {
         HIPCHK(hipEventRecord(c->join_ev[g - 1], c->xst[g - 1]));
         HIPCHK(hipStreamWaitEvent(c->st, c->join_ev[g - 1], 0));
     }

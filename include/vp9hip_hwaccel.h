@@ -1,0 +1,99 @@
+/*
+ * vp9hip_hwaccel.h — the FFHWAccel callbacks of a hybrid VP9 hwaccel over libvp9hip, and the
+ * HIP hwcontext pieces its frames need. Plain C ABI, no FFmpeg types: the FFmpeg-side file
+ * (libavcodec/vp9_hip.c) forwards each FFHWAccel / HWContextType callback
+ * to one of these functions in a few lines.
+ *
+ * Reference interfaces each entry point stands behind:
+ *   FFHWAccel (libavcodec/hwaccel_internal.h:34-166) as vp9_decode_frame calls it
+ *   (libavcodec/vp9.c:1694-1713: start_frame, decode_slice, end_frame once per frame, then
+ *   the reference slots are replaced by refreshrefmask, vp9.c:1705-1711);
+ *   show_existing_frame is answered by vp9.c itself from s->s.ref_frames (vp9.c:1636-1653);
+ *   FFHWAccel.frame_params (hwaccel_internal.h:146) fills an AVHWFramesContext;
+ *   HWContextType.frames_get_buffer / transfer_data_from (libavutil/hwcontext_internal.h:73-80)
+ *   for a device type next to AV_HWDEVICE_TYPE_CUDA (libavutil/hwcontext.h:26-44) whose frames
+ *   carry device pointers in data[] (as AV_PIX_FMT_CUDA frames do, pixfmt.h:260).
+ *
+ * The adapter owns the host entropy decoder state (vp9h_stream: probability contexts,
+ * segmentation, the previous frame's MVs), so decode_slice turns the frame's bytes into the
+ * pass-1 packet the device path reconstructs, and the reference slots (refidx /
+ * refreshrefmask, vp9shared.h:112,120) map to device frame buffers.
+ */
+#ifndef VP9HIP_HWACCEL_H
+#define VP9HIP_HWACCEL_H
+#include <stddef.h>
+#include <stdint.h>
+
+#include "vp9hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* The pixel format of a device frame's data (sw_format of the frames context):
+ * AV_PIX_FMT_YUV420P / YUV422P / YUV440P / YUV444P at 8 bits, the P10 / P12 forms above. */
+enum {
+    VP9HIP_SWFMT_YUV420P, VP9HIP_SWFMT_YUV422P, VP9HIP_SWFMT_YUV440P, VP9HIP_SWFMT_YUV444P,
+    VP9HIP_SWFMT_YUV420P10, VP9HIP_SWFMT_YUV422P10, VP9HIP_SWFMT_YUV440P10, VP9HIP_SWFMT_YUV444P10,
+    VP9HIP_SWFMT_YUV420P12, VP9HIP_SWFMT_YUV422P12, VP9HIP_SWFMT_YUV440P12, VP9HIP_SWFMT_YUV444P12,
+};
+
+/* FFHWAccel.frame_params: what the AVHWFramesContext of the stream's frames gets
+ * (format = the HIP hw pix_fmt, sw_format, width, height, initial_pool_size). */
+typedef struct vp9hip_frames_params {
+    int32_t sw_format;             /* VP9HIP_SWFMT_*                                         */
+    int32_t width, height;         /* coded size                                             */
+    int32_t initial_pool_size;     /* 8 reference slots + the frame being decoded + extra    */
+    int32_t bpp, ss_h, ss_v;
+} vp9hip_frames_params;
+int vp9hip_hwaccel_frame_params(int width, int height, int bpp, int ss_h, int ss_v, int extra,
+                                vp9hip_frames_params *out);
+
+/* A device frame (the AVFrame of a HIP frames context): data[] are device pointers with
+ * byte pitches, valid until vp9hip_hwframe_unref; consumers order their reads after
+ * `stream` (the hipStream_t the frame was produced on). */
+typedef struct vp9hip_hwframe {
+    void     *data[3];
+    ptrdiff_t linesize[3];
+    int32_t   width, height;
+    int32_t   sw_format;
+    int32_t   buf;                 /* pool buffer (the AVBufferRef of the frame)             */
+    int64_t   pts;
+    void     *stream;
+} vp9hip_hwframe;
+
+typedef struct vp9hip_hwaccel vp9hip_hwaccel;    /* hwaccel_priv_data (VP9HIPContext) */
+
+/* FFHWAccel.init: open the device, size its frame pool from frame_params. */
+int  vp9hip_hwaccel_init(int device, const vp9hip_frames_params *fp, vp9hip_hwaccel **out);
+/* FFHWAccel.uninit */
+int  vp9hip_hwaccel_uninit(vp9hip_hwaccel *h);
+/* FFHWAccel.start_frame(avctx, buf_ref, buf, size): the whole frame's bytes (one frame of
+ * a split superframe, not show_existing_frame). */
+int  vp9hip_hwaccel_start_frame(vp9hip_hwaccel *h, const uint8_t *buf, uint32_t size, int64_t pts);
+/* FFHWAccel.decode_slice(avctx, buf, size): the host entropy decode of the frame (all its
+ * tiles) into the pass-1 packet (vp9h_stream_decode). */
+int  vp9hip_hwaccel_decode_slice(vp9hip_hwaccel *h, const uint8_t *buf, uint32_t size);
+/* FFHWAccel.end_frame: reconstruct the frame on the device (its LAST / GOLDEN / ALTREF
+ * are the device buffers of slots refidx[]), replace the slots of refreshrefmask. When
+ * the frame is shown, *out (may be NULL) is the device frame, referenced until
+ * vp9hip_hwframe_unref; returns 1 if shown, 0 if hidden, or an error. */
+int  vp9hip_hwaccel_end_frame(vp9hip_hwaccel *h, vp9hip_hwframe *out);
+/* vp9.c:1636-1653 show_existing_frame: the frame of reference slot `slot`, referenced. */
+int  vp9hip_hwaccel_show_existing(vp9hip_hwaccel *h, int slot, int64_t pts, vp9hip_hwframe *out);
+/* FFHWAccel.flush: drop the reference slots (frames handed out stay valid). */
+void vp9hip_hwaccel_flush(vp9hip_hwaccel *h);
+/* The header fields the adapter mirrors from the parse (s->s.h.refidx / refreshrefmask,
+ * vp9shared.h:112,120) of the last decode_slice, for the decoder's own bookkeeping. */
+int  vp9hip_hwaccel_last_header(const vp9hip_hwaccel *h, vp9h_frame_info *info);
+
+/* HWContextType.transfer_data_from: device frame -> host planes (visible size). */
+int  vp9hip_hwframe_transfer(vp9hip_hwaccel *h, const vp9hip_hwframe *src, uint8_t *const dst[3],
+                             const ptrdiff_t dst_linesize[3]);
+/* av_frame_unref of a device frame: its pool buffer is free once no slot holds it. */
+int  vp9hip_hwframe_unref(vp9hip_hwaccel *h, vp9hip_hwframe *f);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -11,10 +11,11 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def test_library_exports_every_declared_symbol(v9):
-    hdr = open(os.path.join(ROOT, "include", "vp9hip.h")).read()
+@pytest.mark.parametrize("header", ["vp9hip.h", "vp9hip_hwaccel.h"])
+def test_library_exports_every_declared_symbol(v9, header):
+    hdr = open(os.path.join(ROOT, "include", header)).read()
     declared = sorted(set(re.findall(r"\b(vp9h(?:ip)?_\w+)\s*\(", hdr)))
-    assert declared, "no entry points found in include/vp9hip.h"
+    assert declared, "no entry points found in include/" + header
     L = v9.lib()
     for sym in declared:
         assert hasattr(L, sym), sym
