@@ -114,7 +114,7 @@ ABI_SYMBOLS = ["vp9hip_open", "vp9hip_close", "vp9hip_configure", "vp9hip_submit
                "vp9h_enc_defaults", "vp9h_superframe_split", "vp9h_frame_type",
                "vp9hip_synth_defaults", "vp9hip_synth_frame", "vp9hip_synth_free",
                "vp9h_ivf_probe", "vp9h_ivf_read_header", "vp9h_ivf_read_frame", "vp9h_ivf_write_header",
-               "vp9h_ivf_write_frame_header",
+               "vp9h_ivf_write_frame_header", "vp9h_webm_probe", "vp9h_webm_read_header", "vp9h_webm_read_frame",
                "vp9hip_decoder_defaults", "vp9hip_decoder_open", "vp9hip_decoder_close", "vp9hip_decoder_context",
                "vp9hip_decoder_send_packet", "vp9hip_decoder_receive_frame", "vp9hip_decoder_release",
                "vp9hip_decoder_flush"]
@@ -193,6 +193,12 @@ def lib():
                                         ctypes.c_uint32]
     L.vp9h_ivf_write_frame_header.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int64]
     L.vp9h_ivf_write_frame_header.restype = None
+    L.vp9h_webm_probe.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    L.vp9h_webm_read_header.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(WebmInfo),
+                                        ctypes.POINTER(WebmCursor)]
+    L.vp9h_webm_read_frame.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(WebmCursor),
+                                       ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint32),
+                                       ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int)]
     L.vp9hip_decoder_defaults.argtypes = [ctypes.POINTER(DecoderParams)]
     L.vp9hip_decoder_defaults.restype = None
     L.vp9hip_decoder_open.argtypes = [ctypes.POINTER(DecoderParams), ctypes.POINTER(vp)]
@@ -212,6 +218,19 @@ class IvfHeader(ctypes.Structure):
     _fields_ = [("fourcc", ctypes.c_char * 5), ("width", ctypes.c_int32), ("height", ctypes.c_int32),
                 ("time_base_den", ctypes.c_uint32), ("time_base_num", ctypes.c_uint32),
                 ("nb_frames", ctypes.c_uint32), ("header_size", ctypes.c_uint32)]
+
+
+class WebmInfo(ctypes.Structure):
+    _fields_ = [("doctype", ctypes.c_char * 16), ("codec_id", ctypes.c_char * 32), ("track", ctypes.c_uint64),
+                ("width", ctypes.c_int32), ("height", ctypes.c_int32), ("timecode_scale", ctypes.c_uint64)]
+
+
+class WebmCursor(ctypes.Structure):
+    _fields_ = [("pos", ctypes.c_uint64), ("seg_end", ctypes.c_uint64), ("cluster_end", ctypes.c_uint64),
+                ("track", ctypes.c_uint64), ("cluster_tc", ctypes.c_int64), ("block_pts", ctypes.c_int64),
+                ("block_duration", ctypes.c_int64), ("cluster_unknown", ctypes.c_int32), ("keyframe", ctypes.c_int32),
+                ("nlaces", ctypes.c_int32), ("lace_idx", ctypes.c_int32), ("lace_pos", ctypes.c_uint64),
+                ("lace_size", ctypes.c_uint32 * 256)]
 
 
 class DecoderParams(ctypes.Structure):
@@ -731,6 +750,116 @@ def ivf_write(frames, width, height, time_base=(1, 30)):
         lib().vp9h_ivf_write_frame_header(fh, len(data), pts)
         out += [fh.raw, bytes(data)]
     return b"".join(out)
+
+
+NOPTS = -(1 << 63)
+
+
+def webm_probe(data):
+    data = bytes(data)
+    return lib().vp9h_webm_probe(data, len(data))
+
+
+def webm_read(data):
+    """WebM / Matroska bytes -> (WebmInfo, [(pts, frame bytes, keyframe)]) of the first VP9
+    video track (vp9h_webm_read_header / _read_frame; pts in TimecodeScale units, NOPTS
+    for later laces of a block without a duration)."""
+    data = bytes(data)
+    info, cur = WebmInfo(), WebmCursor()
+    _check("vp9h_webm_read_header", lib().vp9h_webm_read_header(data, len(data), ctypes.byref(info), ctypes.byref(cur)))
+    frames = []
+    ptr, n, pts, key = ctypes.c_void_p(), ctypes.c_uint32(), ctypes.c_int64(), ctypes.c_int()
+    base = ctypes.cast(ctypes.c_char_p(data), ctypes.c_void_p).value
+    while True:
+        r = lib().vp9h_webm_read_frame(data, len(data), ctypes.byref(cur), ctypes.byref(ptr), ctypes.byref(n),
+                                       ctypes.byref(pts), ctypes.byref(key))
+        if r == EOF:
+            break
+        _check("vp9h_webm_read_frame", r)
+        off = ptr.value - base
+        frames.append((pts.value, data[off:off + n.value], key.value))
+    return info, frames
+
+
+# ---- a small WebM muxer (matroskaenc.c's element layout) for tests and tools: not the product
+def _ebml_id(i):
+    return i.to_bytes((i.bit_length() + 7) // 8, "big")
+
+
+def _ebml_size(n, width=None, unknown=False):
+    if unknown:
+        w = width or 8
+        return bytes([0xFF >> (w - 1) | (0x80 >> (w - 1))] + [0xFF] * (w - 1)) if w > 1 else b"\xff"
+    w = width or next(k for k in range(1, 9) if n < (1 << (7 * k)) - 1)
+    return (n | (1 << (7 * w))).to_bytes(w, "big")
+
+
+def _el(i, payload, unknown=False, width=None):
+    return _ebml_id(i) + _ebml_size(len(payload), width, unknown) + payload
+
+
+def _uint(i, v):
+    return _el(i, v.to_bytes(max(1, (v.bit_length() + 7) // 8), "big"))
+
+
+def webm_write(frames, width, height, timecode_scale=1000000, cluster_frames=8, lacing=None,
+               unknown_sizes=False, block_groups=False, other_track=False, voids=False):
+    """[(pts, bytes)] or [bytes] -> WebM bytes with one V_VP9 track (number 1). Options for
+    tests: lacing = "xiph" / "fixed" / "ebml" (frames laced in pairs), unknown-size Segment
+    and Clusters, BlockGroup + Block instead of SimpleBlock, an interleaved second track's
+    blocks, Void elements."""
+    fr = [f if isinstance(f, tuple) else (i, f) for i, f in enumerate(frames)]
+    hdr = _el(0x1A45DFA3, _uint(0x4286, 1) + _uint(0x42F7, 1) + _uint(0x42F2, 4) + _uint(0x42F3, 8) +
+              _el(0x4282, b"webm") + _uint(0x4287, 4) + _uint(0x4285, 2))
+    info = _el(0x1549A966, _uint(0x2AD7B1, timecode_scale) + _el(0x4D80, b"vp9hip"))
+    video = _el(0xE0, _uint(0xB0, width) + _uint(0xBA, height))
+    tracks = [_el(0xAE, _uint(0xD7, 1) + _uint(0x73C5, 1) + _uint(0x83, 1) + _el(0x86, b"V_VP9") + video)]
+    if other_track:
+        tracks.append(_el(0xAE, _uint(0xD7, 2) + _uint(0x73C5, 2) + _uint(0x83, 2) + _el(0x86, b"A_OPUS")))
+    body = [info, _el(0x1654AE6B, b"".join(tracks))]
+    if voids:
+        body.insert(1, _el(0xEC, b"\0" * 5))
+
+    def block(track, rel, flags, payloads, kind):
+        head = bytes([0x80 | track]) + (rel & 0xFFFF).to_bytes(2, "big")
+        if kind is None:
+            return head + bytes([flags]) + payloads[0]
+        n = len(payloads)
+        if kind == "xiph":
+            lace = bytes([n - 1]) + b"".join(b"\xff" * (len(p) // 255) + bytes([len(p) % 255]) for p in payloads[:-1])
+            return head + bytes([flags | 0x02]) + lace + b"".join(payloads)
+        if kind == "fixed":
+            return head + bytes([flags | 0x04]) + bytes([n - 1]) + b"".join(payloads)
+        sizes = _ebml_size(len(payloads[0]))                        # EBML lacing: size, then signed deltas
+        for a, b in zip(payloads, payloads[1:-1]):
+            d = len(b) - len(a)
+            w = next(k for k in range(1, 9) if abs(d) < (1 << (7 * k - 1)) - 1)
+            sizes += (d + (1 << (7 * w - 1)) - 1 | (1 << (7 * w))).to_bytes(w, "big")
+        return head + bytes([flags | 0x06]) + bytes([n - 1]) + sizes + b"".join(payloads)
+
+    for c0 in range(0, len(fr), cluster_frames):
+        grp = fr[c0:c0 + cluster_frames]
+        tc = grp[0][0]
+        parts = [_uint(0xE7, tc)]
+        k = 0
+        while k < len(grp):
+            n = 2 if lacing and k + 1 < len(grp) and (lacing != "fixed" or len(grp[k][1]) == len(grp[k + 1][1])) else 1
+            pays = [d for _, d in grp[k:k + n]]
+            rel = grp[k][0] - tc
+            if block_groups:
+                parts.append(_el(0xA0, _el(0xA1, block(1, rel, 0, pays, lacing if n > 1 else None)) +
+                                 (_uint(0x9B, n * (grp[1][0] - grp[0][0] if len(grp) > 1 else 1)) if n > 1 else b"")))
+            else:
+                parts.append(_el(0xA3, block(1, rel, 0x80 if k == 0 and c0 == 0 else 0, pays, lacing if n > 1 else None)))
+            if other_track:
+                parts.append(_el(0xA3, block(2, rel, 0x80, [b"\x01\x02\x03"], None)))
+            if voids and k == 0:
+                parts.append(_el(0xEC, b"\0\0"))
+            k += n
+        payload = b"".join(parts)
+        body.append(_el(0x1F43B675, payload, unknown=unknown_sizes))
+    body.append(_el(0x1C53BB6B, _el(0xBB, _uint(0xB3, 0))))        # a Cues element after the clusters
+    return hdr + _el(0x18538067, b"".join(body), unknown=unknown_sizes)
 
 
 PLAN_STAT_NAMES = ("sbs", "passes", "pjobs", "rjobs", "jobs_4x4", "jobs_8x8", "jobs_16x16",

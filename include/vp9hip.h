@@ -364,6 +364,36 @@ int  vp9h_ivf_write_header(uint8_t out[32], int width, int height, uint32_t time
                            uint32_t nb_frames);
 void vp9h_ivf_write_frame_header(uint8_t out[12], uint32_t frame_size, int64_t pts);
 
+/* ---- WebM / Matroska demux of a VP9 track (libavformat/matroskadec.c) -- */
+typedef struct vp9h_webm_info {
+    char     doctype[16];          /* "webm" / "matroska" (EBML DocType)                     */
+    char     codec_id[32];         /* "V_VP9"                                                */
+    uint64_t track;                /* TrackNumber of the first VP9 video track               */
+    int32_t  width, height;        /* PixelWidth / PixelHeight                               */
+    uint64_t timecode_scale;       /* ns per timecode unit (Info TimecodeScale, 1000000)     */
+} vp9h_webm_info;
+/* Reading position (opaque to callers beyond zero-initialisation by read_header). */
+typedef struct vp9h_webm_cursor {
+    uint64_t pos, seg_end, cluster_end, track;
+    int64_t  cluster_tc, block_pts, block_duration;
+    int32_t  cluster_unknown, keyframe;
+    int32_t  nlaces, lace_idx;
+    uint64_t lace_pos;
+    uint32_t lace_size[256];
+} vp9h_webm_cursor;
+/* matroska_probe (matroskadec.c:1614-1660): 100 for an EBML header with a matroska / webm
+ * DocType, 50 for another EBML document, else 0. */
+int  vp9h_webm_probe(const uint8_t *buf, size_t size);
+/* matroska_read_header (matroskadec.c:3303-3490): EBML header checks, Info, the first
+ * VP9 video track; *cur then points at the first Cluster. AVERROR_INVALIDDATA if there
+ * is no V_VP9 track or the header is malformed. */
+int  vp9h_webm_read_header(const uint8_t *buf, size_t size, vp9h_webm_info *info, vp9h_webm_cursor *cur);
+/* matroska_read_packet: the next frame (one lace of a SimpleBlock / Block of the track),
+ * pts in timecode units (INT64_MIN: none), keyframe flag (SimpleBlock; -1 unknown).
+ * Returns 0, VP9HIP_EOF at the end, or AVERROR_INVALIDDATA. */
+int  vp9h_webm_read_frame(const uint8_t *buf, size_t size, vp9h_webm_cursor *cur, const uint8_t **data,
+                          uint32_t *frame_size, int64_t *pts, int *keyframe);
+
 /* ---- bitstream decoder: avcodec_send_packet / avcodec_receive_frame for VP9 -------------
  * The decode loop of vp9_decode_frame (vp9.c:1558-1865) over the host parse (vp9h_stream)
  * and the device path (vp9hip_ctx): superframes split, show_existing_frame, hidden frames,
