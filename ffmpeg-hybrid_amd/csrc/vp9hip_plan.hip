@@ -78,6 +78,22 @@ DEV vp9h_block load_block(const vp9h_block *g)
     if (b.uvtx > 3) b.uvtx = 0;
     return b;
 }
+// The block fields k_plan's tx enumeration reads (16 bytes in LDS instead of 52).
+struct PBlk {
+    uint16_t row, col;
+    uint8_t bs, tx, uvtx, skip, intra, uvmode;
+    uint8_t mode[4];
+    uint8_t pad[2];
+};
+DEV PBlk pblk(const vp9h_block &b)
+{
+    PBlk r;
+    r.row = b.row; r.col = b.col; r.bs = b.bs; r.tx = b.tx; r.uvtx = b.uvtx; r.skip = b.skip; r.intra = b.intra;
+    r.uvmode = b.uvmode;
+    for (int i = 0; i < 4; i++) r.mode[i] = b.mode[i];
+    r.pad[0] = r.pad[1] = 0;
+    return r;
+}
 DEV bool block_ok(const vp9h_block &b)
 {
     return b.bs < VP9H_N_BS && b.tx <= 3 && b.uvtx <= 3;
@@ -85,12 +101,12 @@ DEV bool block_ok(const vp9h_block &b)
 
 // Per (block, plane) tx-block counts, packed all | eob << 10 | intra jobs << 20, and their
 // exclusive scan over the SB's blocks in decode order (pre[3 * nb] = totals).
-template <int SSH, int SSV>
-DEV uint32_t sb_prefix(const vp9h_block *blk, int nb, int cols, int rows, bool mine, uint32_t *pre, int lane)
+template <int SSH, int SSV, class B>
+DEV uint32_t sb_prefix(const B *blk, int nb, int cols, int rows, bool mine, uint32_t *pre, int lane)
 {
     uint32_t v[3] = { 0, 0, 0 };
     if (lane < nb) {
-        const vp9h_block &b = blk[lane];
+        const B &b = blk[lane];
         for (int p = 0; p < 3; p++) {
             const PlTxGrid g = pl_txgrid(b, p, cols, rows, SSH, SSV);
             const uint32_t n = (uint32_t) (g.nx * g.ny);
@@ -127,18 +143,24 @@ struct Tx {
     int l, x, y;            // index in the plane's tx grid, position (4x4 units in the block)
     PlTxGrid g;
 };
-template <int SSH, int SSV>
-DEV Tx sb_tx_at(const vp9h_block *blk, const uint32_t *pre, int k, uint32_t t, int cols, int rows)
+// q = l / n for l < 4096, 1 <= n <= 16: the multiply by ceil(2^16 / n) is exact there
+DEV int udiv16(int l, int n)
+{
+    return (int) (((uint32_t) l * ((65536u + (uint32_t) n - 1) / (uint32_t) n)) >> 16);
+}
+template <int SSH, int SSV, class B>
+DEV Tx sb_tx_at(const B *blk, const uint32_t *pre, int k, uint32_t t, int cols, int rows)
 {
     Tx r;
     r.k = k;
-    r.b = r.k / 3;
+    r.b = (k * 171) >> 9;                    // k / 3 for k < 192
     r.p = r.k - 3 * r.b;
     r.l = (int) (t - (pre[r.k] & 1023));
     r.g = pl_txgrid(blk[r.b], r.p, cols, rows, SSH, SSV);
     const int nx = r.g.nx > 0 ? r.g.nx : 1;
-    r.x = (r.l % nx) << r.g.txs;
-    r.y = (r.l / nx) << r.g.txs;
+    const int q = udiv16(r.l, nx);
+    r.x = (r.l - q * nx) << r.g.txs;
+    r.y = q << r.g.txs;
     return r;
 }
 template <int SSH, int SSV>
@@ -158,7 +180,7 @@ DEV int tx_eob(const PlanDev &D, const vp9h_block &b, const Tx &tx, const uint32
     return e;
 }
 
-DEV int tx_mode(const vp9h_block &b, const Tx &tx, uint32_t &st)
+template <class B> DEV int tx_mode(const B &b, const Tx &tx, uint32_t &st)
 {
     const int m = tx.p ? b.uvmode : b.mode[b.bs > VP9H_BS_8x8 && b.tx == 0 ? tx.y * 2 + tx.x : 0];
     if (m > 9) { st |= PLS_MODE; return 0; }
@@ -313,35 +335,34 @@ __global__ __launch_bounds__(64) void k_psb(PlanDev D)
 
 // ------------------------------------------------------------------ k_plan
 // k_plan's LDS: the fields of consecutive phases share storage (lifetimes in brackets).
+// b.hgt overlays a.jmap (read until the producers are listed, hgt is set after that);
+// b's other fields overlay a's tail, which is dead once the jobs are built.
 template <int JCAP> struct PlanLds {
-    vp9h_block blk[64];           // [all]
-    uint32_t ja[JCAP];            // [jobs .. cross reads] PJob word per intra job (decode order)
-    uint8_t  jx[JCAP];            // [jobs .. cross reads] 4x4 top-right inside the block (trx)
-    uint16_t jmap[3][256];        // [jobs .. producers] producing job of each 4x4 unit
+    PBlk blk[64];                 // [all]
+    uint32_t ja[JCAP];            // [jobs .. cross reads] PJob word per intra job (decode order),
+                                  // bit 30: the 4x4 top-right lies inside the block (trx)
     union {
-        struct {                  // [prefix .. jobs]
+        struct {                  // [prefix .. jobs], jmap [jobs .. producers]
+            uint16_t jmap[3][256];        // producing job of each 4x4 unit
             uint32_t pre[3 * 64 + 1];
-            uint16_t et[JCAP];    // eob per tx (decode order)
-            uint16_t co[JCAP];    // SB-relative first coefficient per tx
-            uint32_t ost[JCAP];   // (block, plane) entry starting at tx t, else 0
-            uint8_t  own[JCAP];   // (block, plane) entry of tx t (max-scan of ost)
+            uint16_t et[JCAP];            // eob per tx (decode order)
+            uint16_t co[JCAP];            // SB-relative first coefficient per tx; first the raw eobs
+            uint16_t ost[JCAP];           // (block, plane) entry starting at tx t, else 0
+            uint8_t  own[JCAP];           // (block, plane) entry of tx t (max-scan of ost)
+            uint32_t eb[64];              // first eob entry of each block
         } a;
         struct {                  // [producers .. scheduling]
+            uint32_t hgt[JCAP];           // longest path to a sink (list-scheduling priority)
             uint16_t doff[JCAP + 1];      // producers of job j: dep[doff[j] .. doff[j + 1])
             uint16_t dep[4 * JCAP];
-            uint32_t hgt[JCAP];           // longest path to a sink (list-scheduling priority)
             uint16_t ord[JCAP];           // jobs by (height desc, index asc)
             uint16_t sch[JCAP];           // pass of each job (0xffff: not yet)
             uint32_t hs[64];              // height histogram -> list starts
             uint16_t tk[16];              // jobs taken by the pass being built
         } b;
-        struct {                  // [loop filter]
-            uint32_t lfm[2][2][8];        // LF masks [cls][dir][row]: kinds 0..3 in bytes
-            uint8_t  lfl[64];             // LF level of each 8x8
-            uint32_t prog[LF_PROG_BYTES / 4];
-        } c;
     } u;
 };
+#define JA_TRX (1u << 30)
 
 // edges the job's (substituted) mode reads: 1 left, 2 top, 4 top-left, 8 top-right (pl_intra_job)
 DEV uint32_t needs_of(uint32_t a)
@@ -370,8 +391,8 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
     uint32_t st = 0, b0;
     const int nb = sb_blocks(D, slot, b0, st);
     st = 0;                                   // reported by k_psb
-    if (lane < nb) S.blk[lane] = load_block(&D.blocks[b0 + lane]);
-    for (int i = lane; i < 3 * 256; i += 64) (&S.jmap[0][0])[i] = 0xffff;
+    if (lane < nb) S.blk[lane] = pblk(load_block(&D.blocks[b0 + lane]));
+    for (int i = lane; i < 3 * 256; i += 64) (&S.u.a.jmap[0][0])[i] = 0xffff;
     wsync();
     const uint32_t tot = sb_prefix<SSH, SSV>(S.blk, nb, cols, rows, G.mine, S.u.a.pre, lane);
     const int T = pl_min((int) (tot & 1023), JCAP), NJ = pl_min((int) (tot >> 20), JCAP);
@@ -383,7 +404,7 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
         for (int p = 0; p < 3; p++) {
             const int k = 3 * lane + p;
             const uint32_t a0 = S.u.a.pre[k] & 1023, a1 = S.u.a.pre[k + 1] & 1023;
-            if (a1 > a0 && a0 < (uint32_t) T) S.u.a.ost[a0] = (uint32_t) k;
+            if (a1 > a0 && a0 < (uint32_t) T) S.u.a.ost[a0] = (uint16_t) k;
         }
     wsync();
     {
@@ -398,10 +419,30 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
     wsync();
     PPT(0);
 
-    // ---- eobs and SB-relative coefficient offsets (decode order)
-    for (int t = lane; t < T; t += 64) {
-        const Tx tx = sb_tx_at<SSH, SSV>(S.blk, S.u.a.pre, S.u.a.own[t], (uint32_t) t, cols, rows);
-        S.u.a.et[t] = (uint16_t) tx_eob(D, S.blk[tx.b], tx, S.u.a.pre, b0, st);
+    // ---- eobs and SB-relative coefficient offsets (decode order). The SB's eob entries are
+    // contiguous in the packet (its coded blocks' tx in decode order): one coalesced load
+    // into LDS, then each tx picks its entry (skipped blocks have none)
+    {
+        const uint32_t be = lane <= nb ? D.blk_eob0[b0 + (uint32_t) lane] : 0u;      // nb + 1 entries
+        if (lane < nb) S.u.a.eb[lane] = be;
+        const uint32_t E0 = rdl(be, 0), E1 = rdl(be, nb);
+        uint32_t E = E1 - E0;
+        if (E1 < E0 || E > (uint32_t) JCAP || E1 > D.total_eobs) { st |= PLS_EOB; E = 0; }
+        for (uint32_t i = (uint32_t) lane; i < E; i += 64) S.u.a.co[i] = D.eobs[E0 + i];
+        wsync();
+        for (int t = lane; t < T; t += 64) {
+            const int k = S.u.a.own[t], b = (k * 171) >> 9;
+            const PBlk &bk = S.blk[b];
+            int e = 0;
+            if (!bk.skip) {
+                const uint32_t i = S.u.a.eb[b] - E0 + (uint32_t) t - (S.u.a.pre[3 * b] & 1023);
+                const int txs = (k - 3 * b) ? bk.uvtx : bk.tx;
+                if (i < E) e = S.u.a.co[i];
+                else st |= PLS_EOB;
+                if (e > (16 << (2 * txs))) { st |= PLS_EOB; e = 0; }
+            }
+            S.u.a.et[t] = (uint16_t) e;
+        }
     }
     wsync();
     {
@@ -424,7 +465,7 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
     }
     const uint32_t coef_sb = inb(D, G.dord, D.nslots, 32u) ? D.sb_coef0[G.dord] : 0u;
     const uint32_t rbase = slot * D.rcap;
-    unsigned long long ibytes = 0, mbytes = 0;
+    unsigned long long ibytes = 0;
     wsync();
     PPT(1);
 
@@ -436,7 +477,7 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
         RJob r;
         if (t < T) {
             const Tx tx = sb_tx_at<SSH, SSV>(S.blk, S.u.a.pre, S.u.a.own[t], (uint32_t) t, cols, rows);
-            const vp9h_block &b = S.blk[tx.b];
+            const PBlk &b = S.blk[tx.b];
             const int p = tx.p, sh = p ? SSH : 0, sv = p ? SSV : 0, txs = tx.g.txs;
             const int e0 = S.u.a.et[t];
             int mode = 0, txtp = 0;
@@ -471,11 +512,10 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
                 const PlIntra pi = pl_intra_job(p, txs, mode, e0, tx.g.bx + tx.x * 4, tx.g.by + tx.y * 4, tx.x, tx.g.pw4,
                                                 p ? tx0l >> SSH : tx0l, pw8, ph8, ux0, uy0);
                 if (j < JCAP) {
-                    S.ja[j] = pi.a;
-                    S.jx[j] = (uint8_t) pi.trx;
+                    S.ja[j] = pi.a | (pi.trx ? JA_TRX : 0u);
                     const int units = 16 >> sh, unitsv = 16 >> sv;
                     for (int v = uy0; v < uy0 + tx.g.step && v < unitsv; v++)
-                        for (int u = ux0; u < ux0 + tx.g.step && u < units; u++) S.jmap[p][v * 16 + u] = (uint16_t) j;
+                        for (int u = ux0; u < ux0 + tx.g.step && u < units; u++) S.u.a.jmap[p][v * 16 + u] = (uint16_t) j;
                 }
             }
         }
@@ -506,8 +546,8 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
         // recur in the left-column run
         const int nd = (int) needs_of(a);
         bool left_run = false;
-        pl_local_reads(ux0, uy0, 1 << ts, nd, S.jx[j], units, unitsv, [&](int unit) {
-            const int d = S.jmap[p][unit];
+        pl_local_reads(ux0, uy0, 1 << ts, nd, (a & JA_TRX) ? 1 : 0, units, unitsv, [&](int unit) {
+            const int d = S.u.a.jmap[p][unit];
             const bool is_left = (unit & 15) == ux0 - 1 && (unit >> 4) >= uy0;
             if (is_left && !left_run) { left_run = true; last = -1; }
             if (d == 0xffff || d >= j || d == last || (left_run && d == first)) { if (d != 0xffff && d < j) last = d; return; }
@@ -536,9 +576,10 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
         for (int j = lane; j < NJ; j += 64) {
             int k = S.u.b.doff[j];
             if (carry) deps_of(j, [&](int d) { S.u.b.dep[k++] = (uint16_t) d; });
-            S.u.b.hgt[j] = 1;
             S.u.b.sch[j] = 0xffff;
         }
+        wsync();                              // jmap is dead: hgt overlays it
+        for (int j = lane; j < NJ; j += 64) S.u.b.hgt[j] = 1;
     }
     wsync();
     PPT(3);
@@ -634,7 +675,7 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
         if (lane < ntake) {
             const uint32_t a = S.ja[J];
             PJob pj;
-            pj.a = a;
+            pj.a = a & ~JA_TRX;
             pj.roff = ((a >> 4) & 1) ? rbase + pl_resid_unit(a & 3, (a >> 12) & 15, (a >> 16) & 15, SSH, SSV) : 0u;
             if (inb(D, (uint32_t) (done + mypos), JCAP, 128u)) gjob[done + mypos] = pj;
         }
@@ -672,7 +713,7 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
             const int p = a & 3, ts = (a >> 2) & 3, ux0 = (a >> 12) & 15, uy0 = (a >> 16) & 15;
             const int units = p ? CW : 16, unitsv = p ? CH : 16;
             const int fx = G.sbx * units + ux0, fy = G.sby * unitsv + uy0;
-            pl_cross_reads(ux0, uy0, fx, fy, 1 << ts, (int) needs_of(a), S.jx[j], [&](int ux, int uy) {
+            pl_cross_reads(ux0, uy0, fx, fy, 1 << ts, (int) needs_of(a), (a & JA_TRX) ? 1 : 0, [&](int ux, int uy) {
                 if (ux < 0 || uy < 0 || ux >= F.sb_cols * units) return;
                 const int nx = ux / units, ny = uy / unitsv, u = ux - nx * units, v = uy - ny * unitsv;
                 const uint32_t ns = F.slot0 + (uint32_t) (ny * F.sb_cols + nx);
@@ -683,52 +724,6 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
     dmask = wor(dmask);
     PPT(7);
 
-    // ---- MC units (inter blocks in decode order)
-    {
-        const bool mc = lane < nb && G.mine && !S.blk[lane].intra && mc_refs_ok(S.blk[lane], F.mc);
-        const uint32_t n = mc ? (uint32_t) pl_mc_block(S.blk[lane], F.mc, 0, [](const McUnit &) {}) : 0u;
-        const uint32_t incl = wscan_incl(n, lane);
-        uint32_t o = rdl(rb, 20) + incl - n;
-        if (mc)
-            pl_mc_block(S.blk[lane], F.mc, (uint32_t) F.frame, [&](const McUnit &m) {
-                if (inb(D, o, D.cap_mcs, 512u)) D.mcs[o] = m;
-                o++;
-                mbytes += (unsigned long long) m.w * m.h * F.bypp * (1 + m.nref);
-            });
-    }
-    PPT(8);
-
-    // ---- loop-filter levels, masks and program (vp9block.c:1438-1452, vp9lpf.c:31-230)
-    if (F.filter_level) {
-        wsync();                              // the scheduling fields are dead: LF fields reuse them
-        if (lane < 32) (&S.u.c.lfm[0][0][0])[lane] = 0;
-        S.u.c.lfl[lane] = 0;
-        for (int i = lane; i < LF_PROG_BYTES / 4; i += 64) S.u.c.prog[i] = 0;
-        wsync();
-        if (lane < nb) {
-            const vp9h_block &b = S.blk[lane];
-            if (const int lvl = pl_lf_level(b, F.lflvl, F.filter_level)) {
-                const int bw8 = pl_bwh(1, b.bs, 0), bh8 = pl_bwh(1, b.bs, 1), col7 = b.col & 7, row7 = b.row & 7;
-                for (int yy = 0; yy < bh8; yy++)
-                    for (int xx = 0; xx < bw8; xx++)
-                        if (row7 + yy < 8 && col7 + xx < 8) S.u.c.lfl[(row7 + yy) * 8 + col7 + xx] = (uint8_t) lvl;
-                pl_lf_block_masks(b, cols, rows, SSH, SSV, [&](int cls, int d, int y, int k, unsigned v) {
-                    if (y < 8) atomicOr(&S.u.c.lfm[cls][d][y], (v & 255u) << (8 * k));
-                });
-            }
-        }
-        wsync();
-        uint8_t *prog = (uint8_t *) S.u.c.prog;
-        for (int i = lane; i < pl_lf_items(SSH, SSV); i += 64)
-            pl_lf_item(i, SSH, SSV, G.sbx == 0, G.sby == 0, [&](int pos) { return (int) S.u.c.lfl[pos]; },
-                       [&](int cls, int d, int y, int k) { return (S.u.c.lfm[cls][d][y] >> (8 * k)) & 255u; },
-                       [&](int off, uint8_t v) { prog[off] = v; });
-        wsync();
-        uint32_t *g = (uint32_t *) &D.lfs[slot];
-        for (int i = lane; i < (int) (sizeof(LFRec) / 4); i += 64)
-            g[i] = i == 0 ? (uint32_t) F.frame : i == 1 ? ((uint32_t) G.sbx | (uint32_t) G.sby << 16) : S.u.c.prog[i - 2];
-    }
-    PPT(9);
 
     // ---- the SB's intra step (diagonal phases; level phases in k_plevel) and batch totals
     if (lane == 0) {
@@ -740,18 +735,93 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
             D.sb_kpos[slot] = inb(D, key, D.nkeys, 1024u) ? atomicAdd(&D.key_cnt[key], 1u) : 0u;
         }
     }
-    for (int d = 32; d; d >>= 1) {
-        ibytes += __shfl_xor(ibytes, d);
-        mbytes += __shfl_xor(mbytes, d);
-    }
+    for (int d = 32; d; d >>= 1) ibytes += __shfl_xor(ibytes, d);
     if (lane == 0) {
         if (!inb(D, (uint32_t) F.frame, D.nframes, 2048u)) return;
         if (ibytes) atomicAdd(&D.fbytes[2 * F.frame], ibytes);
-        if (mbytes) atomicAdd(&D.fbytes[2 * F.frame + 1], mbytes);
     }
     st = wor(st);
     if (lane == 0 && st) atomicOr(D.status, st);
     PPT(10);
+}
+
+// ------------------------------------------------------------------ k_plmc
+// MC units of the SB's inter blocks in decode order (vp9_mc_template.c:30-464), one wave per
+// SB of the batch's inter frames. A kernel of its own: the unit emission is large code that
+// keyframe batches never run, and it needs none of k_plan's LDS.
+template <int SSH, int SSV>
+__global__ __launch_bounds__(64) void k_plmc(PlanDev D)
+{
+    const PlanFrame &F = D.frames[blockIdx.y];
+    const int s = blockIdx.x, lane = threadIdx.x;
+    if (F.intra || s >= F.sb_cols * F.sb_rows) return;
+    const SbGeo G = sb_geo(F, s);
+    uint32_t st = 0, b0;
+    const int nb = sb_blocks(D, G.slot, b0, st);
+    const uint32_t ci = D.seg_pre1[G.seg] + D.slot_pos[G.slot];
+    const uint32_t base = inb(D, ci, D.cap_cntm, 16u) ? D.cntm0[ci] : 0u;
+    vp9h_block b;
+    bool mc = false;
+    if (lane < nb) {
+        b = load_block(&D.blocks[b0 + lane]);
+        mc = G.mine && !b.intra && mc_refs_ok(b, F.mc);
+    }
+    const uint32_t n = mc ? (uint32_t) pl_mc_block(b, F.mc, 0, [](const McUnit &) {}) : 0u;
+    const uint32_t incl = wscan_incl(n, lane);
+    uint32_t o = base + incl - n;
+    unsigned long long mbytes = 0;
+    if (mc)
+        pl_mc_block(b, F.mc, (uint32_t) F.frame, [&](const McUnit &m) {
+            if (inb(D, o, D.cap_mcs, 512u)) D.mcs[o] = m;
+            o++;
+            mbytes += (unsigned long long) m.w * m.h * F.bypp * (1 + m.nref);
+        });
+    for (int d = 32; d; d >>= 1) mbytes += __shfl_xor(mbytes, d);
+    if (lane == 0 && mbytes && inb(D, (uint32_t) F.frame, D.nframes, 2048u)) atomicAdd(&D.fbytes[2 * F.frame + 1], mbytes);
+}
+
+// ------------------------------------------------------------------ k_pllf
+// The SB's loop-filter levels, masks and program (vp9block.c:1438-1452 via mask_edges,
+// vp9lpf.c:31-230 via pl_lf_item): one wave per SB, 0.7 KB of LDS.
+template <int SSH, int SSV>
+__global__ __launch_bounds__(64) void k_pllf(PlanDev D)
+{
+    __shared__ uint32_t lfm[2][2][8];        // LF masks [cls][dir][row]: kinds 0..3 in bytes
+    __shared__ uint8_t lfl[64];              // LF level of each 8x8
+    __shared__ uint32_t prog[LF_PROG_BYTES / 4];
+    const PlanFrame &F = D.frames[blockIdx.y];
+    const int s = blockIdx.x, lane = threadIdx.x;
+    if (!F.filter_level || s >= F.sb_cols * F.sb_rows) return;
+    const SbGeo G = sb_geo(F, s);
+    const int cols = F.mc.cols, rows = F.mc.rows;
+    uint32_t st = 0, b0;
+    const int nb = sb_blocks(D, G.slot, b0, st);
+    if (lane < 32) (&lfm[0][0][0])[lane] = 0;
+    lfl[lane] = 0;
+    for (int i = lane; i < LF_PROG_BYTES / 4; i += 64) prog[i] = 0;
+    wsync();
+    if (lane < nb) {
+        const vp9h_block b = load_block(&D.blocks[b0 + lane]);
+        if (const int lvl = pl_lf_level(b, F.lflvl, F.filter_level)) {
+            const int bw8 = pl_bwh(1, b.bs, 0), bh8 = pl_bwh(1, b.bs, 1), col7 = b.col & 7, row7 = b.row & 7;
+            for (int yy = 0; yy < bh8; yy++)
+                for (int xx = 0; xx < bw8; xx++)
+                    if (row7 + yy < 8 && col7 + xx < 8) lfl[(row7 + yy) * 8 + col7 + xx] = (uint8_t) lvl;
+            pl_lf_block_masks(b, cols, rows, SSH, SSV, [&](int cls, int d, int y, int k, unsigned v) {
+                if (y < 8) atomicOr(&lfm[cls][d][y], (v & 255u) << (8 * k));
+            });
+        }
+    }
+    wsync();
+    uint8_t *pg = (uint8_t *) prog;
+    for (int i = lane; i < pl_lf_items(SSH, SSV); i += 64)
+        pl_lf_item(i, SSH, SSV, G.sbx == 0, G.sby == 0, [&](int pos) { return (int) lfl[pos]; },
+                   [&](int cls, int d, int y, int k) { return (lfm[cls][d][y] >> (8 * k)) & 255u; },
+                   [&](int off, uint8_t v) { pg[off] = v; });
+    wsync();
+    uint32_t *g = (uint32_t *) &D.lfs[G.slot];
+    for (int i = lane; i < (int) (sizeof(LFRec) / 4); i += 64)
+        g[i] = i == 0 ? (uint32_t) F.frame : i == 1 ? ((uint32_t) G.sbx | (uint32_t) G.sby << 16) : prog[i - 2];
 }
 
 // ------------------------------------------------------------------ k_plevel
@@ -839,23 +909,25 @@ __global__ __launch_bounds__(256) void k_plists(PlanDev D)
     if (inb(D, i, D.cap_dlists, 16384u)) D.dlists[i] = slot;
 }
 
+// stage 0: k_psb; 1: k_plan, then k_pllf (filtered frames) and k_plmc (inter frames)
 template <int SSH, int SSV>
-void launch_sb_kernels(hipStream_t st, const PlanDev &D, int max_sb, int nframes, bool second)
+void launch_sb_kernels(hipStream_t st, const PlanDev &D, int max_sb, int nframes, int stage, int flags)
 {
-    if (second)
-        hipLaunchKernelGGL((k_plan<SSH, SSV>), dim3(max_sb, nframes), dim3(64), 0, st, D);
-    else
-        hipLaunchKernelGGL((k_psb<SSH, SSV>), dim3(max_sb, nframes), dim3(64), 0, st, D);
+    const dim3 g(max_sb, nframes);
+    if (stage == 0) { hipLaunchKernelGGL((k_psb<SSH, SSV>), g, dim3(64), 0, st, D); return; }
+    hipLaunchKernelGGL((k_plan<SSH, SSV>), g, dim3(64), 0, st, D);
+    if (flags & 1) hipLaunchKernelGGL((k_pllf<SSH, SSV>), g, dim3(64), 0, st, D);
+    if (flags & 2) hipLaunchKernelGGL((k_plmc<SSH, SSV>), g, dim3(64), 0, st, D);
 }
 
 // ss: ss_h | ss_v << 1 (as the pixel kernels' launchers)
-void launch_sb(int ss, hipStream_t st, const PlanDev &D, int max_sb, int nframes, bool second)
+void launch_sb(int ss, hipStream_t st, const PlanDev &D, int max_sb, int nframes, int stage, int flags)
 {
     switch (ss) {
-    case 3: launch_sb_kernels<1, 1>(st, D, max_sb, nframes, second); break;
-    case 1: launch_sb_kernels<1, 0>(st, D, max_sb, nframes, second); break;
-    case 2: launch_sb_kernels<0, 1>(st, D, max_sb, nframes, second); break;
-    default: launch_sb_kernels<0, 0>(st, D, max_sb, nframes, second); break;
+    case 3: launch_sb_kernels<1, 1>(st, D, max_sb, nframes, stage, flags); break;
+    case 1: launch_sb_kernels<1, 0>(st, D, max_sb, nframes, stage, flags); break;
+    case 2: launch_sb_kernels<0, 1>(st, D, max_sb, nframes, stage, flags); break;
+    default: launch_sb_kernels<0, 0>(st, D, max_sb, nframes, stage, flags); break;
     }
 }
 
@@ -875,21 +947,21 @@ size_t vp9hip_plan_scan_bytes(size_t n)
 // nb / nslots / ncnt: blocks, SB slots, count-matrix entries (each array + 1 zero entry).
 int vp9hip_plan_enqueue(hipStream_t st, const PlanDev *Dp, int ss, int nframes, int max_blk, int max_sb, uint32_t nb,
                         uint32_t nslots, uint32_t ncnt, int nk, const uint32_t *gidx, int ng, uint32_t *summary,
-                        void *scan_tmp, size_t scan_bytes, int any_levels)
+                        void *scan_tmp, size_t scan_bytes, int any_levels, int flags)
 {
     const PlanDev &D = *Dp;
     if (nframes <= 0) return 0;
     hipLaunchKernelGGL(k_pblk, dim3((max_blk + 255) / 256, nframes), dim3(256), 0, st, D);
     size_t tb = scan_bytes;
     if (hipcub::DeviceScan::ExclusiveSum(scan_tmp, tb, D.blk_neob, D.blk_eob0, (int) nb + 1, st) != hipSuccess) return -1;
-    launch_sb(ss, st, D, max_sb, nframes, false);
+    launch_sb(ss, st, D, max_sb, nframes, 0, 0);
     tb = scan_bytes;
     if (hipcub::DeviceScan::ExclusiveSum(scan_tmp, tb, D.sb_ncoef, D.sb_coef0, (int) nslots + 1, st) != hipSuccess) return -1;
     tb = scan_bytes;
     if (hipcub::DeviceScan::ExclusiveSum(scan_tmp, tb, D.cnt, D.cnt0, (int) ncnt + 1, st) != hipSuccess) return -1;
     tb = scan_bytes;
     if (hipcub::DeviceScan::ExclusiveSum(scan_tmp, tb, D.cntm, D.cntm0, (int) nslots + 1, st) != hipSuccess) return -1;
-    launch_sb(ss, st, D, max_sb, nframes, true);
+    launch_sb(ss, st, D, max_sb, nframes, 1, flags);
     if (any_levels) hipLaunchKernelGGL(k_plevel, dim3(nframes), dim3(256), 0, st, D);
     hipLaunchKernelGGL(k_pkeys, dim3(1), dim3(1024), 0, st, D, nk, gidx, ng, nframes, summary);
     hipLaunchKernelGGL(k_plists, dim3((max_sb + 255) / 256, nframes), dim3(256), 0, st, D);

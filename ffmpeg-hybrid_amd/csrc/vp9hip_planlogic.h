@@ -72,7 +72,7 @@ struct PlTxGrid {
     int pw4;                /* block width in this plane (4x4 units) */
     int bx, by;             /* plane pixel position of the block */
 };
-PL_HD PlTxGrid pl_txgrid(const vp9h_block &b, int p, int cols, int rows, int ss_h, int ss_v)
+template <class B> PL_HD PlTxGrid pl_txgrid(const B &b, int p, int cols, int rows, int ss_h, int ss_v)
 {
     PlTxGrid g;
     const int w4 = pl_bwh(1, b.bs, 0) << 1, h4 = pl_bwh(1, b.bs, 1) << 1;

@@ -50,7 +50,7 @@ int vp9hip_launch_mc(int hb, hipStream_t st, int n, const McUnit *units, const F
 size_t vp9hip_plan_scan_bytes(size_t n);
 int vp9hip_plan_enqueue(hipStream_t st, const PlanDev *D, int ss, int nframes, int max_blk, int max_sb, uint32_t nb,
                         uint32_t nslots, uint32_t ncnt, int nk, const uint32_t *gidx, int ng, uint32_t *summary,
-                        void *scan_tmp, size_t scan_bytes, int any_levels);
+                        void *scan_tmp, size_t scan_bytes, int any_levels, int flags);
 int vp9hip_launch_lfr(int fmt, hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs,
                       const FrameDesc *frames, uint32_t *ctr);
 int vp9hip_launch_plf(int fmt, hipStream_t st, const PlfLaunch *pl, const uint32_t *plist, const uint32_t *llist,
@@ -158,6 +158,7 @@ struct Staged {
     uint32_t nslots = 0, nblk = 0, neob = 0, ncoef = 0, ncnt = 0, nkey = 0, host_lists = 0, n_gidx = 0;
     int max_blk = 0, max_sb = 0, jcap = 0, rcap = 0, nframes = 0;
     bool any_levels = false;
+    int plan_flags = 0;                 // device planner kernels: 1 any filtered frame, 2 any inter frame
     size_t o_pf = 0, o_blocks = 0, o_eobs = 0, o_slotpos = 0, o_segpre = 0, o_segsz = 0, o_segpre1 = 0, o_cntm = 0, o_cntm0 = 0, o_gidx = 0, o_bneob = 0,
            o_beob0 = 0, o_sbfirst = 0, o_sbncoef = 0, o_sbcoef0 = 0, o_cnt = 0, o_cnt0 = 0, o_ibits = 0,
            o_sbinfo = 0, o_sbkey = 0, o_sbkpos = 0, o_keycnt = 0, o_keyoff = 0, o_status = 0, o_fbytes = 0,
@@ -1002,6 +1003,7 @@ static int stage_dev(vp9hip_ctx *c, const DevIn &in)
     // frame records of the planner
     uint64_t nb = 0, ne = 0, nc = 0, nmc = 0;
     s.any_levels = false;
+    s.plan_flags = 0;
     s.frame_res_bytes.assign(n, 0.0);
     s.frame_fused.assign(n, 0);
     for (int i = 0; i < n; i++) {
@@ -1025,6 +1027,7 @@ static int stage_dev(vp9hip_ctx *c, const DevIn &in)
         F.mc = fb.mc;
         memcpy(F.lflvl, f->lflvl, sizeof(F.lflvl));
         s.any_levels |= F.levels != 0;
+        s.plan_flags |= (f->filter_level ? 1 : 0) | (F.intra ? 0 : 2);
         nb += f->nblocks; ne += f->neobs; nc += f->ncoefs;
         if (!F.intra) nmc += (uint64_t) 12 * f->nblocks;
         s.frame_res_bytes[i] = (double) f->ncoefs * in.csz;
@@ -1219,7 +1222,7 @@ static int plan_dev(vp9hip_ctx *c)
     }
     if (vp9hip_plan_enqueue(c->st, &D, c->ss_h | c->ss_v << 1, s.nframes, s.max_blk, s.max_sb, s.nblk, s.nslots,
                             s.ncnt, (int) s.nkey, (const uint32_t *) (A + s.o_gidx), (int) s.n_gidx,
-                            (uint32_t *) (A + s.o_summary), A + s.o_scan, s.scan_bytes, s.any_levels))
+                            (uint32_t *) (A + s.o_summary), A + s.o_scan, s.scan_bytes, s.any_levels, s.plan_flags))
         return VP9HIP_EEXTERNAL;
     if (c->timing) HIPCHK(hipEventRecord(c->pev[1], c->st));
     c->plan_timed = c->timing;
