@@ -127,9 +127,9 @@ def main():
                     help="per-launch HIP events inside the timed steps (no graph replay)")
     ap.add_argument("--chroma", choices=sorted(CHROMA), default="420",
                     help="chroma format (profiles 1/3: 422, 440, 444); the BASELINE configs are 4:2:0")
-    ap.add_argument("--inflight", type=int, default=1,
-                    help="batches in flight: contexts that alternate steps, so one batch's device "
-                         "planning overlaps the previous batch's pixel kernels")
+    ap.add_argument("--inflight", type=int, default=1, choices=[1, 2],
+                    help="batches in flight: the context's two batch slots hold the same workload and "
+                         "alternate steps, so one batch's device planning overlaps the other's pixel kernels")
     ap.add_argument("--shard", choices=["frames", "tiles"], default="frames",
                     help="frames: every rank decodes its own stream (weak scaling, default); tiles: all ranks "
                          "decode ONE stream, each its tile columns, pre-LF stripes all-gathered (strong scaling)")
@@ -155,19 +155,16 @@ def main():
     t_gen = time.time() - t0
 
     dev = v.Device(local_rank)
-    dev.configure(W, H, BPP, nbufs=args.frames, ss_h=ssh, ss_v=ssv)
+    dev.configure(W, H, BPP, nbufs=args.frames * args.inflight, ss_h=ssh, ss_v=ssv)
     t0 = time.time()
     dev.stage_batch(frames, list(range(args.frames)), None if gop == 1 else refs)
     t_stage = time.time() - t0
-    # further contexts holding the same batch (own arena, frame buffers and streams)
-    others = []
-    for _ in range(max(0, args.inflight - 1)):
-        d2 = v.Device(local_rank)
-        d2.configure(W, H, BPP, nbufs=args.frames, ss_h=ssh, ss_v=ssv)
-        d2.stage_batch(frames, list(range(args.frames)), None if gop == 1 else refs)
-        d2.set_timing(args.timed_events)
-        others.append(d2)
-    ring = [dev] + others
+    # slot 1: the same workload into the second half of the frame buffers
+    for k in range(1, args.inflight):
+        dev.set_slot(k)
+        dev.stage_batch(frames, [k * args.frames + i for i in range(args.frames)],
+                        None if gop == 1 else [None if r is None else tuple(k * args.frames + x for x in r) for r in refs])
+    dev.set_slot(0)
 
     def barrier():
         if dist is not None:
@@ -189,23 +186,21 @@ def main():
 
     # timed steps: the batch's launch sequence replayed as one HIP graph
     dev.set_timing(args.timed_events)
-    for k in range(args.warmup * len(ring)):
-        ring[k % len(ring)].run_batch()
-    for d in ring:
-        d.sync()
+    for k in range(args.warmup * args.inflight):
+        dev.set_slot(k % args.inflight)
+        dev.run_batch()
+    dev.sync()
     barrier()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        d = ring[k % len(ring)]
-        d.run_batch()              # device planning (waits for its summary), then the pixel kernels
-        if len(ring) == 1:
-            d.sync()
-    for d in ring:
-        d.sync()
+        dev.set_slot(k % args.inflight)
+        dev.run_batch()            # device planning (waits for its summary), then the pixel kernels
+        if args.inflight == 1:
+            dev.sync()
+    dev.sync()                     # every slot's work is on the main stream
     barrier()
     elapsed = time.perf_counter() - t0
-    for d in others:
-        d.close()
+    dev.set_slot(0)
 
     elapsed = reduce_elapsed(elapsed, dist)
 

@@ -367,8 +367,7 @@ template <int JCAP> struct PlanLds {
 // edges the job's (substituted) mode reads: 1 left, 2 top, 4 top-left, 8 top-right (pl_intra_job)
 DEV uint32_t needs_of(uint32_t a)
 {
-    const uint8_t needs[16] = { 2, 1, 2 | 8, 1 | 2 | 4, 1 | 2 | 4, 1 | 2 | 4, 2 | 8, 1, 1 | 2 | 4, 1 | 2, 1, 2, 0, 0, 0, 0 };
-    return needs[(a >> 8) & 15];
+    return (uint32_t) pl_field(0x21371a777a12ull, (int) ((a >> 8) & 15), 4);     /* pl_intra_job's needs by slot */
 }
 DEV uint32_t wor(uint32_t v) { return rdl(wscan_dpp<OP_OR>(v), 63); }
 

@@ -22,17 +22,18 @@
 
 #define PL_HD __host__ __device__ static inline
 
-/* ff_vp9_bwh_tab (vp9data.c:25-38): [0] 4x4 units, [1] 8x8 units; [ss] also indexes chroma */
+/* ff_vp9_bwh_tab (vp9data.c:25-38): [0] 4x4 units, [1] 8x8 units; [ss] also indexes chroma.
+ * Bit-packed log2 sizes (3 bits per block size), so device code computes them in registers
+ * instead of loading a table from memory. [1] = max([0] / 2, 1). */
 PL_HD int pl_bwh(int i, int bs, int d)
 {
-    const uint8_t t[2][13][2] = {
-        { { 16, 16 }, { 16, 8 }, { 8, 16 }, { 8, 8 }, { 8, 4 }, { 4, 8 }, { 4, 4 }, { 4, 2 }, { 2, 4 }, { 2, 2 },
-          { 2, 1 }, { 1, 2 }, { 1, 1 } },
-        { { 8, 8 }, { 8, 4 }, { 4, 8 }, { 4, 4 }, { 4, 2 }, { 2, 4 }, { 2, 2 }, { 2, 1 }, { 1, 2 }, { 1, 1 },
-          { 1, 1 }, { 1, 1 }, { 1, 1 } },
-    };
-    return t[i][bs][d];
+    const uint64_t lw = 0x494936e4ull, lh = 0x20a29a71cull;     /* log2 of [0][bs][0] / [0][bs][1] */
+    const int l = (int) (((d ? lh : lw) >> (3 * bs)) & 7) - i;
+    return 1 << (l > 0 ? l : 0);
 }
+
+/* entry i of a table of n-bit fields packed into a 64-bit constant */
+PL_HD int pl_field(uint64_t packed, int i, int bits) { return (int) ((packed >> (bits * i)) & ((1u << bits) - 1)); }
 
 PL_HD int pl_min(int a, int b) { return a < b ? a : b; }
 PL_HD int pl_max(int a, int b) { return a > b ? a : b; }
@@ -59,8 +60,7 @@ PL_HD int pl_sb_dorder(int sbx, int sby, int sb_cols) { return sby * sb_cols + s
 /* ff_vp9_intra_txfm_type (vp9data.c:437-452) */
 PL_HD int pl_intra_txfm_type(int mode)
 {
-    const uint8_t t[14] = { 2, 1, 0, 0, 3, 2, 1, 2, 1, 3, 0, 0, 0, 0 };
-    return t[mode];
+    return pl_field(0xd9b06ull, mode, 2);     /* { 2, 1, 0, 0, 3, 2, 1, 2, 1, 3, 0, 0, 0, 0 } */
 }
 
 /* The tx-block grid of one plane of a block (the end_x / end_y clipping of intra_recon /
@@ -110,17 +110,18 @@ PL_HD PlIntra pl_intra_job(int p, int txs, int mode, int e, int gx, int gy, int 
     case 9: m = have_left ? (have_top ? 9 : 1) : (have_top ? 0 : 14); break;
     default: break;
     }
-    const uint8_t slot_of[15] = { 0, 1, 9, 2, 3, 4, 5, 6, 7, 8, 10, 11, 12, 13, 14 };
-    const uint8_t needs[15] = {            /* by slot: V H D45 D135 D117 D153 D63 D207 TM DC LEFT_DC TOP_DC DC_128/127/129 */
-        2, 1, 2 | 8, 1 | 2 | 4, 1 | 2 | 4, 1 | 2 | 4, 2 | 8, 1, 1 | 2 | 4, 1 | 2, 1, 2, 0, 0, 0 };
-    const int slot = slot_of[m];
+    /* slot_of = { 0, 1, 9, 2, 3, 4, 5, 6, 7, 8, 10, 11, 12, 13, 14 }; needs by slot (V H D45 D135
+     * D117 D153 D63 D207 TM DC LEFT_DC TOP_DC DC_128/127/129) = { 2, 1, 2 | 8, 1 | 2 | 4, 1 | 2 | 4,
+     * 1 | 2 | 4, 2 | 8, 1, 1 | 2 | 4, 1 | 2, 1, 2, 0, 0, 0 }, both packed 4 bits per entry */
+    const uint64_t slot_of = 0xedcba8765432910ull, needs = 0x21371a777a12ull;
+    const int slot = pl_field(slot_of, m, 4);
     const int ct = pl_min(n, have_t) - 1, cl = pl_min(n, have_l) - 1;
     const int trreal = txs == 0 && have_top && have_right && have_t >= 8;
     PlIntra r;
     r.a = (uint32_t) p | (uint32_t) txs << 2 | (uint32_t) (e ? 1 : 0) << 4 | (uint32_t) trreal << 5 |
           (uint32_t) have_top << 6 | (uint32_t) have_left << 7 | (uint32_t) slot << 8 | (uint32_t) ux0 << 12 |
           (uint32_t) uy0 << 16 | (uint32_t) ct << 20 | (uint32_t) cl << 25;
-    r.nd = needs[slot];
+    r.nd = pl_field(needs, slot, 4);
     r.trx = (txs == 0 && (x < pw4 - 1) && (r.nd & 8)) ? 1 : 0;
     return r;
 }
@@ -182,12 +183,12 @@ PL_HD void pl_lf_mask_edges(OR or_, int ss_h, int ss_v, int row7, int col7, int 
         return;
     }
     if (!skip_inter) {
-        const unsigned masks[4] = { 0xff, 0x55, 0x11, 0x01 };
+        const uint32_t masks = 0x011155ffu;        /* { 0xff, 0x55, 0x11, 0x01 }, a byte each */
         const int id = tx == 1;
         int l2 = tx + ss_h - 1;
-        const unsigned m_row = m_col & masks[l2];
+        const unsigned m_row = m_col & ((masks >> (8 * l2)) & 255u);
         if (ss_h && tx > 1 && (w ^ (w - 1)) == 1) {
-            const unsigned m16 = ((t << (w - 1)) - t) & masks[l2], m8 = m_row - m16;
+            const unsigned m16 = ((t << (w - 1)) - t) & ((masks >> (8 * l2)) & 255u), m8 = m_row - m16;
             for (int y = row7; y < h + row7; y++) { or_(0, y, 0, m16); or_(0, y, 1, m8); }
         } else {
             for (int y = row7; y < h + row7; y++) or_(0, y, id, m_row);

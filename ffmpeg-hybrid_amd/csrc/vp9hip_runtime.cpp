@@ -166,6 +166,7 @@ struct Staged {
     size_t scan_bytes = 0, summary_words = 0;
     uint32_t *summary_h = nullptr;                            // pinned readback of the summary
     size_t summary_cap = 0;
+    hipEvent_t done_ev = nullptr;       // recorded on the main stream after this batch's last run
 };
 
 } // namespace
@@ -198,7 +199,11 @@ struct vp9hip_ctx {
     bool plan_timed = false;
     int dbg = 0;                        // VP9HIP_DEBUG: ablation switches for profiling only
     bool use_graph = true;              // VP9HIP_GRAPH=0 disables graph replay
-    Staged stg;
+    Staged stg;                         // the current batch slot
+    Staged alt;                         // the other slot (vp9hip_set_batch_slot swaps them)
+    int slot = 0;
+    hipStream_t pst = nullptr;          // device planner stream: a slot's planning overlaps the
+                                        // other slot's pixel kernels
     // timing of the last run
     bool timing = true;
     std::vector<hipEvent_t> ev;
@@ -225,15 +230,20 @@ extern "C" int vp9hip_open(int device, vp9hip_ctx **out)
     if (const char *g = getenv("VP9HIP_LFROW")) c->lf_rows = atoi(g);
     if (const char *g = getenv("VP9HIP_LEVELS")) c->level_sched = atoi(g) != 0;
     if (const char *g = getenv("VP9HIP_HOST_PLAN")) c->host_plan = atoi(g) != 0;
+    // streams in the order their work is busiest: the frame groups' streams, then the
+    // planner's, so that (with the default 4 hardware queues, GPU_MAX_HW_QUEUES) each lands
+    // on a queue of its own; the LF-overlap streams only when that mode is on
     bool ok = hipSetDevice(device) == hipSuccess && hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) == hipSuccess;
+    for (int i = 0; ok && i < c->max_groups - 1; i++)
+        ok = hipStreamCreateWithFlags(&c->xst[i], hipStreamNonBlocking) == hipSuccess;
+    ok = ok && hipStreamCreateWithFlags(&c->pst, hipStreamNonBlocking) == hipSuccess;
+    for (int i = 0; ok && i < MAX_GROUPS - 1; i++)
+        ok = hipEventCreateWithFlags(&c->join_ev[i], hipEventDisableTiming) == hipSuccess;
     for (int i = 0; ok && i < MAX_GROUPS; i++)
-        ok = hipStreamCreateWithFlags(&c->lst[i], hipStreamNonBlocking) == hipSuccess &&
+        ok = (!c->lf_overlap || hipStreamCreateWithFlags(&c->lst[i], hipStreamNonBlocking) == hipSuccess) &&
              hipEventCreateWithFlags(&c->lf_done[i], hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&c->join_ev[MAX_GROUPS + i], hipEventDisableTiming) == hipSuccess;
-    for (int i = 0; ok && i < MAX_GROUPS - 1; i++)
-        ok = hipStreamCreateWithFlags(&c->xst[i], hipStreamNonBlocking) == hipSuccess &&
-             hipEventCreateWithFlags(&c->join_ev[i], hipEventDisableTiming) == hipSuccess;
     if (!ok) {
         delete c;
         return VP9HIP_EEXTERNAL;
@@ -254,15 +264,20 @@ extern "C" void vp9hip_close(vp9hip_ctx *c)
     if (!c) return;
     hipSetDevice(c->dev);
     hipStreamSynchronize(c->st);
+    hipStreamSynchronize(c->pst);
     free_bufs(c);
-    if (c->stg.arena) hipFree(c->stg.arena);
-    if (c->stg.resid) hipFree(c->stg.resid);
-    if (c->stg.pinned) hipHostFree(c->stg.pinned);
-    if (c->stg.graph) hipGraphExecDestroy(c->stg.graph);
+    for (Staged *g : { &c->stg, &c->alt }) {
+        if (g->arena) hipFree(g->arena);
+        if (g->resid) hipFree(g->resid);
+        if (g->pinned) hipHostFree(g->pinned);
+        if (g->graph) hipGraphExecDestroy(g->graph);
+        if (g->summary_h) hipHostFree(g->summary_h);
+        if (g->done_ev) hipEventDestroy(g->done_ev);
+    }
     if (c->ptab) hipFree(c->ptab);
     if (c->nz) hipFree(c->nz);
     if (c->plan_prof) hipFree(c->plan_prof);
-    if (c->stg.summary_h) hipHostFree(c->stg.summary_h);
+    if (c->pst) hipStreamDestroy(c->pst);
     for (auto e : c->pev) if (e) hipEventDestroy(e);
     for (auto e : c->ev) hipEventDestroy(e);
     hipStreamDestroy(c->st);
@@ -1158,8 +1173,13 @@ static int plan_dev(vp9hip_ctx *c)
     uint8_t *A = s.arena;
     s.planned = false;
     s.launches.clear();
-    HIPCHK(hipMemsetAsync(A + s.o_sbfirst, 0xff, (size_t) 2 * s.nslots * 4, c->st));
-    HIPCHK(hipMemsetAsync(A + s.o_keycnt, 0, s.zero_bytes, c->st));
+    // the planner runs on its own stream, after this slot's previous run (its records are
+    // rewritten in place) and after whatever the main stream holds for it (the staging
+    // upload); the other slot's pixel kernels run meanwhile
+    const hipStream_t ps = c->pst;
+    if (s.done_ev) HIPCHK(hipStreamWaitEvent(ps, s.done_ev, 0));
+    HIPCHK(hipMemsetAsync(A + s.o_sbfirst, 0xff, (size_t) 2 * s.nslots * 4, ps));
+    HIPCHK(hipMemsetAsync(A + s.o_keycnt, 0, s.zero_bytes, ps));
     PlanDev D;
     D.frames = (const PlanFrame *) (A + s.o_pf);
     D.blocks = (const vp9h_block *) (A + s.o_blocks);
@@ -1212,22 +1232,22 @@ static int plan_dev(vp9hip_ctx *c)
     D.prof = nullptr;
     if (pprof) {
         if (!c->plan_prof && hipMalloc(&c->plan_prof, 16 * sizeof(unsigned long long)) != hipSuccess) return VP9HIP_ENOMEM;
-        HIPCHK(hipMemsetAsync(c->plan_prof, 0, 16 * sizeof(unsigned long long), c->st));
+        HIPCHK(hipMemsetAsync(c->plan_prof, 0, 16 * sizeof(unsigned long long), ps));
         D.prof = c->plan_prof;
     }
     if (c->timing) {
         for (auto &e : c->pev)
             if (!e) HIPCHK(hipEventCreate(&e));
-        HIPCHK(hipEventRecord(c->pev[0], c->st));
+        HIPCHK(hipEventRecord(c->pev[0], ps));
     }
-    if (vp9hip_plan_enqueue(c->st, &D, c->ss_h | c->ss_v << 1, s.nframes, s.max_blk, s.max_sb, s.nblk, s.nslots,
+    if (vp9hip_plan_enqueue(ps, &D, c->ss_h | c->ss_v << 1, s.nframes, s.max_blk, s.max_sb, s.nblk, s.nslots,
                             s.ncnt, (int) s.nkey, (const uint32_t *) (A + s.o_gidx), (int) s.n_gidx,
                             (uint32_t *) (A + s.o_summary), A + s.o_scan, s.scan_bytes, s.any_levels, s.plan_flags))
         return VP9HIP_EEXTERNAL;
-    if (c->timing) HIPCHK(hipEventRecord(c->pev[1], c->st));
+    if (c->timing) HIPCHK(hipEventRecord(c->pev[1], ps));
     c->plan_timed = c->timing;
-    HIPCHK(hipMemcpyAsync(s.summary_h, A + s.o_summary, s.summary_words * 4, hipMemcpyDeviceToHost, c->st));
-    HIPCHK(hipStreamSynchronize(c->st));
+    HIPCHK(hipMemcpyAsync(s.summary_h, A + s.o_summary, s.summary_words * 4, hipMemcpyDeviceToHost, ps));
+    HIPCHK(hipStreamSynchronize(ps));          // the pixel kernels, queued after this, read the plan
     if (pprof) {
         unsigned long long pc[16];
         HIPCHK(hipMemcpy(pc, c->plan_prof, sizeof(pc), hipMemcpyDeviceToHost));
@@ -1876,7 +1896,13 @@ extern "C" int vp9hip_run_batch(vp9hip_ctx *c)
         static const bool plan_only = getenv("VP9HIP_PLAN_ONLY") && atoi(getenv("VP9HIP_PLAN_ONLY"));
         if (plan_only) return 0;          // diagnostics: the planner alone
     }
-    if (c->timing || !c->use_graph) return enqueue_batch(c);
+    // this slot's last work on the main stream: its next planning waits for it
+    if (!s.done_ev) HIPCHK(hipEventCreateWithFlags(&s.done_ev, hipEventDisableTiming));
+    if (c->timing || !c->use_graph) {
+        const int r = enqueue_batch(c);
+        if (!r) HIPCHK(hipEventRecord(s.done_ev, c->st));
+        return r;
+    }
     // the graph of the previous run is reused when the launch list is the same (same
     // geometry and record counts); the records themselves were just rewritten in place
     if (s.graph && !same_launches(s.graph_launches, s.launches)) {
@@ -1895,6 +1921,7 @@ extern "C" int vp9hip_run_batch(vp9hip_ctx *c)
         if (e != hipSuccess) { s.graph = nullptr; return VP9HIP_EEXTERNAL; }
     }
     HIPCHK(hipGraphLaunch(s.graph, c->st));
+    HIPCHK(hipEventRecord(s.done_ev, c->st));
     return 0;
 }
 
@@ -2068,13 +2095,18 @@ extern "C" int vp9hip_run_phase(vp9hip_ctx *c, int phase, int part)
     if (!c || !c->stg.ready || phase < 0 || phase >= c->stg.nphases || (part != PART_RECON && part != PART_LF))
         return VP9HIP_EINVAL;
     hipSetDevice(c->dev);
-    if (c->stg.dev && !c->stg.planned) {
+    Staged &s = c->stg;
+    // a pass over the batch starts at phase 0's reconstruction: plan it again (decoding the
+    // batch includes planning it), after the previous pass's launches
+    if (s.dev && (!s.planned || (phase == 0 && part == PART_RECON))) {
         const int r = plan_dev(c);
         if (r) return r;
     }
     c->timed_run = false;
-    for (const Launch &L : c->stg.launches)
+    for (const Launch &L : s.launches)
         if (L.ph == phase && L.part == part && launch_one(c, L, c->st)) return VP9HIP_EEXTERNAL;
+    if (!s.done_ev) HIPCHK(hipEventCreateWithFlags(&s.done_ev, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(s.done_ev, c->st));
     return 0;
 }
 
@@ -2239,6 +2271,19 @@ extern "C" int vp9hip_set_graph(vp9hip_ctx *c, int on)
 }
 
 extern "C" int vp9hip_abi_version(void) { return VP9HIP_ABI_VERSION; }
+
+// Two batch slots per context: stage / run / sync / phase calls act on the current slot.
+// Each slot has its own arena, plan and graph; the frame buffers are the context's. A run of
+// one slot plans on the planner stream while the other slot's pixel kernels still run.
+extern "C" int vp9hip_set_batch_slot(vp9hip_ctx *c, int slot)
+{
+    if (!c || slot < 0 || slot > 1) return VP9HIP_EINVAL;
+    if (slot != c->slot) {
+        std::swap(c->stg, c->alt);
+        c->slot = slot;
+    }
+    return 0;
+}
 
 // Host-only planning statistics of one frame (no device needed): used by the CPU tests
 // and to size kernels. out[]: 0 SBs with intra work, 1 passes, 2 intra jobs, 3 residual

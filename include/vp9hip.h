@@ -169,6 +169,11 @@ int  vp9hip_run_phase(vp9hip_ctx *ctx, int phase, int part);
  */
 int64_t vp9hip_stripe(vp9hip_ctx *ctx, int frame, int tile_lo, int tile_hi, void *dev, int to_frame);
 
+/* Select batch slot 0 or 1 (default 0): stage_batch*, run_batch, sync, batch_phases,
+ * run_phase and stripe act on the current slot. Each slot holds its own staged batch
+ * (arena, plan, launch graph); the frame buffers are the context's. Alternating two staged
+ * batches lets one batch's device planning run while the other's pixel kernels do. */
+int  vp9hip_set_batch_slot(vp9hip_ctx *ctx, int slot);
 /* Wait for all queued work. VP9HIP_EBUG if a row-pipelined loop-filter launch (k_lfr)
  * gave up a bounded wait on another workgroup's progress (frames not trusted). */
 int  vp9hip_sync(vp9hip_ctx *ctx);
