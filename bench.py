@@ -323,9 +323,10 @@ def cpu_baseline(v, oracle, dev, frames, refs, geom, args):
     """CPU baseline legs on this box's host cores, and the bit-exactness
     check of the timed frames. Leg 1: the scalar C oracle on 1 thread over a bounded sample
     in decode order; every frame it decodes is compared with the device's frame (downloads
-    and compares are outside the CPU timer). Leg 2: frame-parallel over the box's CPU share
-    (16 threads): independent keyframes (C3/C4) or independent GOP chains (C2/C5), one
-    oracle decode per thread (ctypes releases the GIL). Returns (cpu_baseline, verify)."""
+    and compares are outside the CPU timer). Leg 2: tile-column threads per frame (the
+    reference's slice threading). Leg 3: frame-parallel over the box's CPU share (16
+    threads): independent keyframes (C3/C4) or independent GOP chains (C2/C5), one oracle
+    decode per thread (ctypes releases the GIL). Returns (cpu_baseline, verify)."""
     import concurrent.futures
     W, H, BPP, log2, gop = geom
     bounded = not args.no_cpu_baseline
@@ -355,7 +356,28 @@ def cpu_baseline(v, oracle, dev, frames, refs, geom, args):
     one = n / t_or
     info = cpu_info()
     thr = info["threads_used"]
-    # leg 2: frame-parallel (keyframes) / GOP-parallel (inter streams) over thr threads
+    # leg 2: the reference's slice threads: the tile columns of each SB row on their own
+    # threads, the loop filter of the previous row overlapped (vp9.c:1442-1551), frames one
+    # after another in decode order (vp9o_decode_frame_tiles, same output as leg 1)
+    tthr = min(1 << log2, thr)
+    t_tile, n_tile = 0.0, 0
+    outs = {}
+    ssh_, ssv_ = CHROMA[args.chroma]
+    for i in range(len(frames)):
+        out = v.alloc_planes(W, H, BPP, ssh_, ssv_)
+        r = refs[i]
+        t0 = time.perf_counter()
+        oracle.decode_frame(frames[i].pkt, out, None if r is None else [outs[r[0]], outs[r[1]], outs[r[2]]],
+                            tile_threads=tthr)
+        t_tile += time.perf_counter() - t0
+        n_tile += 1
+        outs[i] = out
+        for k in [k for k in outs if k < i - gop]:
+            del outs[k]
+        if n_tile >= 2 and t_tile >= budget / 3:
+            break
+    outs = None
+    # leg 3: frame-parallel (keyframes) / GOP-parallel (inter streams) over thr threads
     if gop == 1:
         units = [[i] for i in range(len(frames))]
     else:
@@ -383,6 +405,9 @@ def cpu_baseline(v, oracle, dev, frames, refs, geom, args):
     legs = [
         {"leg": "1 thread", "value": round(one, 3), "cores": 1,
          "sample": "%d frames in decode order" % n},
+        {"leg": "tile-column threads", "value": round(tiles, 3), "cores": tthr + 1,
+         "sample": "%d frames in decode order, %d tile-column threads + the loop filter on the calling thread"
+                   % (n_tile, tthr)},
         {"leg": "%s-parallel" % ("frame" if gop == 1 else "GOP"), "value": round(par, 3), "cores": thr,
          "sample": "%d %s on %d threads" % (len(work), "keyframes" if gop == 1 else "GOP chains", thr)},
     ]

@@ -453,8 +453,14 @@ template <int N> DEV void store_col(int16_t *dst, const int (&r)[N])
         for (int k = 0; k < N / 8; k++) ((uint4 *) dst)[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
 }
 
+// LDS row stride (coefficients) of an N x N block: padded so that the transposed store
+// (lane li writes row li) spreads over the banks: an odd number of dwords per row
+template <int N, typename COEF> struct RStride { static constexpr int S = N + (sizeof(COEF) == 2 ? 2 : 1); };
+// LDS coefficients of one residual wave: 64 / N blocks of N rows
+template <int N, typename COEF> struct RWave { static constexpr int E = (64 / N) * N * RStride<N, COEF>::S; };
+
 // One wave of residual work: jobs [wj * 64/N, (wj + 1) * 64/N) of `jobs`, n lanes per
-// job; cbw = the wave's LDS block (64 N coefficients).
+// job; cbw = the wave's LDS block (RWave<N, COEF>::E coefficients, rows padded to S).
 template <int N, int TCODE, typename PIX, class M, typename COEF>
 DEV void resid_wave(const RJob *__restrict__ jobs, int njobs, int wj, int lane, const FrameDesc *__restrict__ frames,
                     const COEF *__restrict__ coefs, int16_t *__restrict__ resid, COEF *cbw)
@@ -464,10 +470,11 @@ DEV void resid_wave(const RJob *__restrict__ jobs, int njobs, int wj, int lane, 
     constexpr int LG = N == 4 ? 2 : N == 8 ? 3 : N == 16 ? 4 : 5;
     constexpr int TS = LG - 2;
     constexpr int BITS = N == 32 ? 6 : TS + 4;
+    constexpr int S = RStride<N, COEF>::S;
     const int grp = lane >> LG, li = lane & (N - 1);
     const int j = wj * CAP + grp;
     const bool act = j < njobs;
-    COEF *cb = cbw + grp * N * N;
+    COEF *cb = cbw + grp * N * S;
 
     RJob r;
     if (act) r = jobs[j];
@@ -480,7 +487,7 @@ DEV void resid_wave(const RJob *__restrict__ jobs, int njobs, int wj, int lane, 
 
     // zero the nonzero bounding box, then scatter scan-order coefficients
     if (full)
-        for (int k = 0; k < nzr; k++) cb[k * N + li] = 0;
+        for (int k = 0; k < nzr; k++) cb[k * S + li] = 0;
     wave_sync();
     if (full) {
         const int16_t *scan = scan_for(TCODE, txtp);
@@ -490,7 +497,7 @@ DEV void resid_wave(const RJob *__restrict__ jobs, int njobs, int wj, int lane, 
 #pragma unroll
             for (int u = 0; u < 8; u++) {
                 const int k = k0 + li + u * N;
-                if (k < eob) { c[u] = src[k]; pos[u] = scan[k]; }
+                if (k < eob) { c[u] = src[k]; pos[u] = scan[k]; pos[u] += (pos[u] >> LG) * (S - N); }
             }
 #pragma unroll
             for (int u = 0; u < 8; u++)
@@ -503,11 +510,11 @@ DEV void resid_wave(const RJob *__restrict__ jobs, int njobs, int wj, int lane, 
     if (TCODE == 4) {
         // lossless WHT (vp9dsp_template.c:1719-1750); in-place transpose through LDS
         int32_t v[4];
-        if (full) for (int k = 0; k < 4; k++) v[k] = cb[k * 4 + li];
+        if (full) for (int k = 0; k < 4; k++) v[k] = cb[k * S + li];
         wave_sync();
-        if (full) { iwht4(v, 0); for (int k = 0; k < 4; k++) cb[li * 4 + k] = (COEF) v[k]; }
+        if (full) { iwht4(v, 0); for (int k = 0; k < 4; k++) cb[li * S + k] = (COEF) v[k]; }
         wave_sync();
-        if (full) { for (int k = 0; k < 4; k++) v[k] = cb[k * 4 + li]; iwht4(v, 1); }
+        if (full) { for (int k = 0; k < 4; k++) v[k] = cb[k * S + li]; iwht4(v, 1); }
 #pragma unroll
         for (int k = 0; k < N; k++) res[k] = full ? (int) (COEF) v[k & 3] : 0;
     } else {
@@ -515,18 +522,18 @@ DEV void resid_wave(const RJob *__restrict__ jobs, int njobs, int wj, int lane, 
         // column pass (type_a): lane c < nzc transforms column c into row c
         const bool colp = full && li < nzc;
 #pragma unroll
-        for (int k = 0; k < N; k++) v[k] = colp && k < nzr ? M::in(cb[k * N + li]) : (T) 0;
+        for (int k = 0; k < N; k++) v[k] = colp && k < nzr ? M::in(cb[k * S + li]) : (T) 0;
         wave_sync();
         if (colp) {
             tx1n<N, M>(v, txtp & 1);
 #pragma unroll
-            for (int k = 0; k < N; k++) cb[li * N + k] = (COEF) (int64_t) v[k];
+            for (int k = 0; k < N; k++) cb[li * S + k] = (COEF) (int64_t) v[k];
         }
         wave_sync();
         // row pass (type_b): lane i transforms column i of the transposed block
         if (full) {
 #pragma unroll
-            for (int k = 0; k < N; k++) v[k] = k < nzc ? M::in(cb[k * N + li]) : (T) 0;
+            for (int k = 0; k < N; k++) v[k] = k < nzc ? M::in(cb[k * S + li]) : (T) 0;
             tx1n<N, M>(v, txtp >> 1);
 #pragma unroll
             for (int k = 0; k < N; k++) {
@@ -565,7 +572,7 @@ __global__ __launch_bounds__(64 * RWAVES) void k_resid(const RJob *__restrict__ 
                                                        const FrameDesc *__restrict__ frames,
                                                        const COEF *__restrict__ coefs, int16_t *__restrict__ resid)
 {
-    __shared__ COEF cbs[RWAVES][64 * N];
+    __shared__ COEF cbs[RWAVES][RWave<N, COEF>::E];
     const int wave = threadIdx.x >> 6;
     resid_wave<N, TCODE, PIX, M, COEF>(jobs, njobs, blockIdx.x * RWAVES + wave, threadIdx.x & 63, frames, coefs, resid,
                                        cbs[wave]);
@@ -1616,7 +1623,7 @@ __global__ __launch_bounds__(LfNT<G>::NT) void k_plf(PlfLaunch a, const uint32_t
     typedef typename RT<PIX>::M M;
     typedef typename RT<PIX>::C COEF;
     constexpr int NW = LfNT<G>::NT / 64;
-    __shared__ union PlfLds { PredLds<PIX, G> p; LfLds<PIX, G> l; COEF r[NW][64 * 32]; } S;
+    __shared__ union PlfLds { PredLds<PIX, G> p; LfLds<PIX, G> l; COEF r[NW][RWave<32, COEF>::E]; } S;
     const int b = blockIdx.x;
     if (b < (int) a.npred) {
         if (threadIdx.x >= 64) return;

@@ -31,6 +31,8 @@ def lib():
             build()
         _L = ctypes.CDLL(LIB)
         _L.vp9o_decode_frame.argtypes = [ctypes.c_void_p, ctypes.POINTER(Planes), ctypes.POINTER(Planes)]
+        _L.vp9o_decode_frame_tiles.argtypes = [ctypes.c_void_p, ctypes.POINTER(Planes), ctypes.POINTER(Planes),
+                                               ctypes.c_int]
         _L.vp9o_itxfm_add.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_ssize_t, ctypes.c_void_p,
                                       ctypes.c_int, ctypes.c_int, ctypes.c_int]
         _L.vp9o_itxfm_add.restype = None
@@ -59,10 +61,12 @@ def _planes(arrs, w, h):
     return p
 
 
-def decode_frame(pkt, out_planes, ref_planes=None, ref_sizes=None):
+def decode_frame(pkt, out_planes, ref_planes=None, ref_sizes=None, tile_threads=0):
     """Reconstruct + loop-filter one pass-1 packet into out_planes (padded numpy planes).
 
-    ref_planes: list of 3 plane-lists (LAST, GOLDEN, ALTREF) for inter frames."""
+    ref_planes: list of 3 plane-lists (LAST, GOLDEN, ALTREF) for inter frames.
+    tile_threads > 0: the slice-threaded form (tile columns of an SB row on that many
+    threads, vp9o_decode_frame_tiles); same output."""
     cur = _planes(out_planes, pkt.width, pkt.height)
     refs = None
     if ref_planes is not None:
@@ -70,7 +74,10 @@ def decode_frame(pkt, out_planes, ref_planes=None, ref_sizes=None):
         for i in range(3):
             rw, rh = (ref_sizes[i] if ref_sizes else (pkt.width, pkt.height))
             refs[i] = _planes(ref_planes[i], rw, rh)
-    r = lib().vp9o_decode_frame(ctypes.addressof(pkt), ctypes.byref(cur), refs)
+    if tile_threads > 0:
+        r = lib().vp9o_decode_frame_tiles(ctypes.addressof(pkt), ctypes.byref(cur), refs, int(tile_threads))
+    else:
+        r = lib().vp9o_decode_frame(ctypes.addressof(pkt), ctypes.byref(cur), refs)
     if r < 0:
         raise RuntimeError("vp9o_decode_frame failed: %d" % r)
     return out_planes

@@ -959,14 +959,85 @@ static int n_txb(OCtx *c, const vp9h_block *b, int uv)
     return ((end_x + s - 1) / s) * ((end_y + s - 1) / s);
 }
 
-int vp9o_decode_frame(const vp9h_frame *f, vp9o_planes *cur, const vp9o_planes *refs)
+/* One coded block: reconstruction (intra_recon / inter_pred + inter_residual) and its LF
+ * level and masks (vp9block.c:1438-1452). eobp / coefp: the block's eob entries and
+ * coefficients; tile_col_start / end in c are those of the block's SB. */
+static int do_block(OCtx *c, const vp9h_block *b, const uint16_t *eobp, const uint8_t *coefp)
 {
-    OCtx *c = calloc(1, sizeof(*c));
-    const uint16_t *eobp = f->eobs;
-    const uint8_t *coefp = f->coefs;
-    int i, p, ret = 0, sharp = f->sharpness;
-    uint32_t bi;
-    if (!c) return VP9HIP_ENOMEM;
+    const vp9h_frame *f = c->f;
+    VP9Filter *lflvl = &c->lflvl[b->col >> 3];
+    int p, i, lvl, ret;
+    for (p = 0; p < 3; p++) {
+        c->n_eob[p] = b->skip ? 0 : n_txb(c, b, p > 0);
+        c->eob[p] = eobp;
+        eobp += c->n_eob[p];
+    }
+    for (p = 0; p < 3; p++) {
+        c->coef[p] = coefp;
+        for (i = 0; i < c->n_eob[p]; i++) coefp += c->eob[p][i] * (c->bypp == 1 ? 2 : 4);
+    }
+    if (b->intra) {
+        intra_recon(c, b);
+    } else {
+        if (!c->refs) return VP9HIP_EINVAL;
+        if ((ret = inter_pred(c, b)) < 0) return ret;
+        if (!b->skip) inter_residual(c, b);
+    }
+    /* LF level + masks, vp9block.c:1438-1452 */
+    if (f->filter_level &&
+        (lvl = f->lflvl[b->seg_id][b->intra ? 0 : b->ref[0] + 1][b->mode[3] != VP9H_ZEROMV]) > 0) {
+        int w4 = vp9t_bwh[1][b->bs][0], h4 = vp9t_bwh[1][b->bs][1];
+        int x_end = MIN(c->cols - b->col, w4), y_end = MIN(c->rows - b->row, h4);
+        int skip_inter = !b->intra && b->skip, col7 = b->col & 7, row7 = b->row & 7, yy, xx;
+        for (yy = 0; yy < h4; yy++)
+            for (xx = 0; xx < w4; xx++) lflvl->level[(row7 + yy) * 8 + col7 + xx] = lvl;
+        mask_edges(lflvl->mask[0], 0, 0, row7, col7, x_end, y_end, 0, 0, b->tx, skip_inter);
+        if (c->ss_h || c->ss_v)
+            mask_edges(lflvl->mask[1], c->ss_h, c->ss_v, row7, col7, x_end, y_end,
+                       c->cols & 1 && b->col + w4 >= c->cols ? c->cols & 7 : 0,
+                       c->rows & 1 && b->row + h4 >= c->rows ? c->rows & 7 : 0,
+                       b->uvtx, skip_inter);
+    }
+    return 0;
+}
+
+/* a new superblock: reset its masks (vp9.c:1381-1383); tile column bounds (vp9.c:1244-1250) */
+static void start_sb(OCtx *c, int sbc)
+{
+    const int log2 = c->f->log2_tile_cols;
+    memset(c->lflvl[sbc].mask, 0, sizeof(c->lflvl[sbc].mask));
+    for (int ti = 0; ti < (1 << log2); ti++) {
+        int s0 = MIN((ti * c->sb_cols) >> log2, c->sb_cols);
+        int s1 = MIN(((ti + 1) * c->sb_cols) >> log2, c->sb_cols);
+        if (sbc >= s0 && sbc < s1) { c->tile_col_start = s0 << 3; c->tile_col_end = s1 << 3; }
+    }
+}
+
+/* end of SB row sbr (all tile columns): the pre-LF copy of its last pixel row for the intra
+ * prediction of the next row (vp9.c:1404-1416) */
+static void save_ipd(OCtx *c, int sbr)
+{
+    int row = sbr << 3;
+    if (row + 8 < c->rows) {
+        memcpy(c->ipd[0], c->plane[0] + (row * 8 + 63) * c->ls[0], 8 * c->cols * c->bypp);
+        memcpy(c->ipd[1], c->plane[1] + ((row * 8 >> c->ss_v) + (64 >> c->ss_v) - 1) * c->ls[1],
+               8 * c->cols * c->bypp >> c->ss_h);
+        memcpy(c->ipd[2], c->plane[2] + ((row * 8 >> c->ss_v) + (64 >> c->ss_v) - 1) * c->ls[1],
+               8 * c->cols * c->bypp >> c->ss_h);
+    }
+}
+
+/* loopfilter_sb over SB row sbr (vp9.c:1417-1429) */
+static void lf_row(OCtx *c, int sbr)
+{
+    if (c->f->filter_level)
+        for (int col = 0; col < c->cols; col += 8)
+            loopfilter_sb(c, &c->lflvl[col >> 3], sbr << 3, col);
+}
+
+static int frame_init(OCtx *c, const vp9h_frame *f, vp9o_planes *cur, const vp9o_planes *refs)
+{
+    int i, p, sharp = f->sharpness;
     c->f = f;
     c->bd = f->bpp;
     c->bypp = f->bpp > 8 ? 2 : 1;
@@ -995,7 +1066,7 @@ int vp9o_decode_frame(const vp9h_frame *f, vp9o_planes *cur, const vp9o_planes *
             }
             valid++;
         }
-        if (!valid) { free(c); return VP9HIP_EINVALIDDATA; }
+        if (!valid) return VP9HIP_EINVALIDDATA;
     }
     for (p = 0; p < 3; p++) {
         c->plane[p] = cur->data[p];
@@ -1014,84 +1085,185 @@ int vp9o_decode_frame(const vp9h_frame *f, vp9o_planes *cur, const vp9o_planes *
     }
     c->lflvl = calloc(c->sb_cols, sizeof(VP9Filter));
     for (p = 0; p < 3; p++) c->ipd_base[p] = calloc(c->sb_cols * 64 * 2 + 64, 1);
-    if (!c->lflvl || !c->ipd_base[0] || !c->ipd_base[1] || !c->ipd_base[2]) { ret = VP9HIP_ENOMEM; goto end; }
+    if (!c->lflvl || !c->ipd_base[0] || !c->ipd_base[1] || !c->ipd_base[2]) return VP9HIP_ENOMEM;
     for (p = 0; p < 3; p++) c->ipd[p] = c->ipd_base[p] + 32;
+    return 0;
+}
 
+static void frame_free(OCtx *c)
+{
+    for (int p = 0; p < 3; p++) free(c->ipd_base[p]);
+    free(c->lflvl);
+    free(c);
+}
+
+int vp9o_decode_frame(const vp9h_frame *f, vp9o_planes *cur, const vp9o_planes *refs)
+{
+    OCtx *c = calloc(1, sizeof(*c));
+    const uint16_t *eobp = f->eobs;
+    const uint8_t *coefp = f->coefs;
+    int i, p, ret = 0;
+    uint32_t bi;
+    if (!c) return VP9HIP_ENOMEM;
+    if ((ret = frame_init(c, f, cur, refs)) < 0) goto end;
     {
         int prev_sb = -1;
         for (bi = 0; bi < f->nblocks; bi++) {
             const vp9h_block *b = &f->blocks[bi];
-            int sbr = b->row >> 3, sbc = b->col >> 3;
-            VP9Filter *lflvl = &c->lflvl[sbc];
-            int lvl, ti, log2 = f->log2_tile_cols;
-
+            int sbr = b->row >> 3, sbc = b->col >> 3, n = 0;
             if (sbr * c->sb_cols + sbc != prev_sb) {
-                /* new superblock: reset masks (vp9.c:1381-1383); tile col bounds (vp9.c:1244-1250) */
-                memset(lflvl->mask, 0, sizeof(lflvl->mask));
+                start_sb(c, sbc);
                 prev_sb = sbr * c->sb_cols + sbc;
-                for (ti = 0; ti < (1 << log2); ti++) {
-                    int s0 = MIN((ti * c->sb_cols) >> log2, c->sb_cols);
-                    int s1 = MIN(((ti + 1) * c->sb_cols) >> log2, c->sb_cols);
-                    if (sbc >= s0 && sbc < s1) { c->tile_col_start = s0 << 3; c->tile_col_end = s1 << 3; }
-                }
             }
-            /* gather this block's eobs + coefficient cursors */
-            for (p = 0; p < 3; p++) {
-                c->n_eob[p] = b->skip ? 0 : n_txb(c, b, p > 0);
-                c->eob[p] = eobp;
-                eobp += c->n_eob[p];
-            }
-            if ((uint64_t)(eobp - f->eobs) > f->neobs) { ret = VP9HIP_EINVALIDDATA; goto end; }
-            for (p = 0; p < 3; p++) {
-                c->coef[p] = coefp;
-                for (i = 0; i < c->n_eob[p]; i++) coefp += c->eob[p][i] * (c->bypp == 1 ? 2 : 4);
-            }
-
-            if (b->intra) {
-                intra_recon(c, b);
-            } else {
-                if (!refs) { ret = VP9HIP_EINVAL; goto end; }
-                if ((ret = inter_pred(c, b)) < 0) goto end;
-                if (!b->skip) inter_residual(c, b);
-            }
-
-            /* LF level + masks, vp9block.c:1438-1452 */
-            if (f->filter_level &&
-                (lvl = f->lflvl[b->seg_id][b->intra ? 0 : b->ref[0] + 1][b->mode[3] != VP9H_ZEROMV]) > 0) {
-                int w4 = vp9t_bwh[1][b->bs][0], h4 = vp9t_bwh[1][b->bs][1];
-                int x_end = MIN(c->cols - b->col, w4), y_end = MIN(c->rows - b->row, h4);
-                int skip_inter = !b->intra && b->skip, col7 = b->col & 7, row7 = b->row & 7, yy, xx;
-                for (yy = 0; yy < h4; yy++)
-                    for (xx = 0; xx < w4; xx++) lflvl->level[(row7 + yy) * 8 + col7 + xx] = lvl;
-                mask_edges(lflvl->mask[0], 0, 0, row7, col7, x_end, y_end, 0, 0, b->tx, skip_inter);
-                if (c->ss_h || c->ss_v)
-                    mask_edges(lflvl->mask[1], c->ss_h, c->ss_v, row7, col7, x_end, y_end,
-                               c->cols & 1 && b->col + w4 >= c->cols ? c->cols & 7 : 0,
-                               c->rows & 1 && b->row + h4 >= c->rows ? c->rows & 7 : 0,
-                               b->uvtx, skip_inter);
-            }
-
+            for (p = 0; p < 3; p++) n += b->skip ? 0 : n_txb(c, b, p > 0);
+            if ((uint64_t)(eobp + n - f->eobs) > f->neobs) { ret = VP9HIP_EINVALIDDATA; goto end; }
+            if ((ret = do_block(c, b, eobp, coefp)) < 0) goto end;
+            for (i = 0; i < n; i++) coefp += eobp[i] * (c->bypp == 1 ? 2 : 4);
+            eobp += n;
             /* end of an SB row (all tile columns): vp9.c:1404-1429 */
             if (bi + 1 == f->nblocks || (f->blocks[bi + 1].row >> 3) != sbr) {
-                int row = sbr << 3, col;
-                if (row + 8 < c->rows) {
-                    memcpy(c->ipd[0], c->plane[0] + (row * 8 + 63) * c->ls[0], 8 * c->cols * c->bypp);
-                    memcpy(c->ipd[1], c->plane[1] + ((row * 8 >> c->ss_v) + (64 >> c->ss_v) - 1) * c->ls[1],
-                           8 * c->cols * c->bypp >> c->ss_h);
-                    memcpy(c->ipd[2], c->plane[2] + ((row * 8 >> c->ss_v) + (64 >> c->ss_v) - 1) * c->ls[1],
-                           8 * c->cols * c->bypp >> c->ss_h);
-                }
-                if (f->filter_level)
-                    for (col = 0; col < c->cols; col += 8)
-                        loopfilter_sb(c, &c->lflvl[col >> 3], row, col);
+                save_ipd(c, sbr);
+                lf_row(c, sbr);
             }
         }
     }
     if ((uint64_t)(coefp - (const uint8_t *) f->coefs) != f->ncoefs * (c->bypp == 1 ? 2 : 4))
         ret = VP9HIP_EINVALIDDATA;
 end:
-    for (p = 0; p < 3; p++) free(c->ipd_base[p]);
-    free(c->lflvl);
-    free(c);
+    frame_free(c);
+    return ret;
+}
+
+/* ---- tile-column threads: the reference's slice-threaded decode (decode_tiles_mt, vp9.c:
+ * 1442-1520, and loopfilter_proc, 1522-1551), as the CPU baseline leg of BASELINE.md §3.
+ * Per SB row, the tile columns reconstruct on worker threads (each with its own context:
+ * edge buffers, cursors, tile bounds); the row's pre-LF copy is saved, and its loop filter
+ * runs on the calling thread while the workers reconstruct the next row (the LF of row r
+ * touches no pixel that the reconstruction of row r + 1 reads: intra reads row r through
+ * the saved copy, MC reads only references). Same output as vp9o_decode_frame. */
+#include <pthread.h>
+
+typedef struct TileJob {
+    OCtx *c;                      /* this worker's context (a copy of the frame's)           */
+    const vp9h_frame *f;
+    const uint32_t *blk0;         /* per block: first eob entry                              */
+    const uint64_t *coef0;        /* per block: first coefficient byte                        */
+    uint32_t b0, b1;              /* the tile column's blocks in this SB row                 */
+    int ret;
+} TileJob;
+
+static void *tile_worker(void *arg)
+{
+    TileJob *j = arg;
+    int prev = -1;
+    j->ret = 0;
+    for (uint32_t bi = j->b0; bi < j->b1 && j->ret >= 0; bi++) {
+        const vp9h_block *b = &j->f->blocks[bi];
+        if ((b->col >> 3) != prev) { start_sb(j->c, b->col >> 3); prev = b->col >> 3; }
+        j->ret = do_block(j->c, b, j->f->eobs + j->blk0[bi], (const uint8_t *) j->f->coefs + j->coef0[bi]);
+    }
+    return NULL;
+}
+
+int vp9o_decode_frame_tiles(const vp9h_frame *f, vp9o_planes *cur, const vp9o_planes *refs, int nthreads)
+{
+    OCtx *c = calloc(1, sizeof(*c));
+    const int ntile = 1 << f->log2_tile_cols;
+    int ret = 0, nt = nthreads < 1 ? 1 : nthreads > 64 ? 64 : nthreads;
+    uint32_t *blk0 = NULL;
+    uint64_t *coef0 = NULL;
+    OCtx **wc = NULL;
+    VP9Filter *lf_odd = NULL;
+    if (!c) return VP9HIP_ENOMEM;
+    if ((ret = frame_init(c, f, cur, refs)) < 0) goto end;
+    /* every block's eob and coefficient offsets (the entropy decoder's 2-pass buffers) */
+    blk0 = malloc(((size_t) f->nblocks + 1) * sizeof(*blk0));
+    coef0 = malloc(((size_t) f->nblocks + 1) * sizeof(*coef0));
+    wc = calloc((size_t) nt, sizeof(*wc));
+    if (!blk0 || !coef0 || !wc) { ret = VP9HIP_ENOMEM; goto end; }
+    {
+        uint64_t e = 0, cb = 0;
+        for (uint32_t bi = 0; bi < f->nblocks; bi++) {
+            const vp9h_block *b = &f->blocks[bi];
+            int n = 0;
+            for (int p = 0; p < 3; p++) n += b->skip ? 0 : n_txb(c, b, p > 0);
+            if (e + (uint64_t) n > f->neobs) { ret = VP9HIP_EINVALIDDATA; goto end; }
+            blk0[bi] = (uint32_t) e;
+            coef0[bi] = cb;
+            for (int i = 0; i < n; i++) cb += (uint64_t) f->eobs[e + i] * (c->bypp == 1 ? 2 : 4);
+            e += (uint64_t) n;
+        }
+        if (cb != f->ncoefs * (c->bypp == 1 ? 2 : 4)) { ret = VP9HIP_EINVALIDDATA; goto end; }
+    }
+    for (int t = 0; t < nt; t++) {
+        if (!(wc[t] = malloc(sizeof(OCtx)))) { ret = VP9HIP_ENOMEM; goto end; }
+        memcpy(wc[t], c, sizeof(OCtx));
+    }
+    /* LF levels / masks by row parity: row r + 1 fills its set while row r is filtered */
+    VP9Filter *lfb[2] = { c->lflvl, NULL };
+    if (!(lf_odd = calloc(c->sb_cols, sizeof(VP9Filter)))) { ret = VP9HIP_ENOMEM; goto end; }
+    lfb[1] = lf_odd;
+    {
+        uint32_t bi = 0;
+        int lf_pending = -1;
+        while (bi < f->nblocks && ret >= 0) {
+            const int sbr = f->blocks[bi].row >> 3;
+            uint32_t be = bi;
+            while (be < f->nblocks && (f->blocks[be].row >> 3) == sbr) be++;
+            /* the row's blocks by tile column (SB raster order within the row) */
+            TileJob jobs[64];
+            pthread_t th[64];
+            int nj = 0;
+            uint32_t k = bi;
+            for (int ti = 0; ti < ntile && k < be; ti++) {
+                const int s1 = MIN(((ti + 1) * c->sb_cols) >> f->log2_tile_cols, c->sb_cols);
+                uint32_t ke = k;
+                while (ke < be && (f->blocks[ke].col >> 3) < s1) ke++;
+                if (ke > k) {
+                    jobs[nj] = (TileJob) { NULL, f, blk0, coef0, k, ke, 0 };
+                    nj++;
+                }
+                k = ke;
+            }
+            /* up to nt workers, tile columns round-robin (the reference's one tile per thread) */
+            int nw = nj < nt ? nj : nt;
+            for (int w = 0; w < nt; w++) wc[w]->lflvl = lfb[sbr & 1];
+            for (int w = 0; w < nw; w++) {
+                TileJob *jj = &jobs[w];
+                jj->c = wc[w];
+                /* the other tile columns of this worker run after its first one */
+                if (pthread_create(&th[w], NULL, tile_worker, jj)) { ret = VP9HIP_ENOMEM; nw = w; break; }
+            }
+            if (lf_pending >= 0) {                              /* overlapped with this row's reconstruction */
+                c->lflvl = lfb[lf_pending & 1];
+                lf_row(c, lf_pending);
+            }
+            for (int w = 0; w < nw; w++) {
+                pthread_join(th[w], NULL);
+                if (jobs[w].ret < 0) ret = jobs[w].ret;
+            }
+            for (int w = nw; w < nj && ret >= 0; w++) {         /* tile columns beyond nt: on this thread */
+                jobs[w].c = wc[w % nt];
+                tile_worker(&jobs[w]);
+                if (jobs[w].ret < 0) ret = jobs[w].ret;
+            }
+            save_ipd(c, sbr);
+            lf_pending = sbr;
+            bi = be;
+        }
+        if (ret >= 0 && lf_pending >= 0) {
+            c->lflvl = lfb[lf_pending & 1];
+            lf_row(c, lf_pending);
+        }
+        c->lflvl = lfb[0];                                      /* frame_free's */
+    }
+end:
+    if (wc)
+        for (int t = 0; t < nt; t++) free(wc[t]);
+    free(wc);
+    free(blk0);
+    free(coef0);
+    free(lf_odd);
+    frame_free(c);
     return ret;
 }

@@ -31,6 +31,10 @@ typedef struct vp9o_planes {
 /* Reconstruct + loop-filter one frame. refs[i] = LAST/GOLDEN/ALTREF (may be NULL
  * for intra frames). Returns 0 or a negative error. */
 int vp9o_decode_frame(const vp9h_frame *f, vp9o_planes *cur, const vp9o_planes *refs);
+/* The same frame with the tile columns of each SB row on up to nthreads threads and the
+ * loop filter of the previous row overlapped (decode_tiles_mt + loopfilter_proc,
+ * vp9.c:1442-1551): the slice-threaded CPU baseline. Output identical. */
+int vp9o_decode_frame_tiles(const vp9h_frame *f, vp9o_planes *cur, const vp9o_planes *refs, int nthreads);
 
 /* DSP entry points for unit tests (stride in pixels). */
 void vp9o_itxfm_add(int bpp, void *dst, ptrdiff_t stride, void *coef, int eob, int tx, int txtp);

@@ -14,7 +14,7 @@ from collections import defaultdict
 
 
 def short(name):
-    for k in ("k_plf", "k_resid", "k_pred", "k_lfr", "k_lf", "k_mc"):
+    for k in ("k_plf", "k_resid", "k_pred", "k_lfr", "k_lf", "k_mc", "k_plan", "k_pllf", "k_psb"):
         if k in name:
             return k
     return None
