@@ -377,6 +377,7 @@ def cpu_baseline(v, oracle, dev, frames, refs, geom, args):
         if n_tile >= 2 and t_tile >= budget / 3:
             break
     outs = None
+    tiles = n_tile / t_tile
     # leg 3: frame-parallel (keyframes) / GOP-parallel (inter streams) over thr threads
     if gop == 1:
         units = [[i] for i in range(len(frames))]
