@@ -108,7 +108,7 @@ ABI_SYMBOLS = ["vp9hip_open", "vp9hip_close", "vp9hip_configure", "vp9hip_submit
                "vp9hip_upload_frame", "vp9hip_flush", "vp9hip_last_timing", "vp9hip_set_timing",
                "vp9hip_alg_bytes", "vp9hip_plan_stats", "vp9hip_abi_version", "vp9hip_set_graph",
                "vp9hip_stage_batch_tiles", "vp9hip_batch_phases", "vp9hip_phase_frames", "vp9hip_run_phase",
-               "vp9hip_stripe", "vp9hip_frame_device", "vp9hip_batch_groups", "vp9hip_set_batch_slot",
+               "vp9hip_stripe", "vp9hip_frame_device", "vp9hip_batch_groups", "vp9hip_set_batch_slot", "vp9hip_sync_slot", "vp9hip_slot_busy",
                "vp9h_decode_frame", "vp9h_encode_frame", "vp9h_frame_free", "vp9h_buffer_free",
                "vp9h_stream_open", "vp9h_stream_close", "vp9h_stream_decode", "vp9h_stream_encode",
                "vp9h_enc_defaults", "vp9h_superframe_split", "vp9h_frame_type",
@@ -142,6 +142,8 @@ def lib():
     L.vp9hip_batch_phases.argtypes = [vp]
     L.vp9hip_batch_groups.argtypes = [vp]
     L.vp9hip_set_batch_slot.argtypes = [vp, ctypes.c_int]
+    L.vp9hip_sync_slot.argtypes = [vp, ctypes.c_int]
+    L.vp9hip_slot_busy.argtypes = [vp, ctypes.c_int]
     L.vp9hip_phase_frames.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_int]
     L.vp9hip_run_phase.argtypes = [vp, ctypes.c_int, ctypes.c_int]
     L.vp9hip_stripe.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]

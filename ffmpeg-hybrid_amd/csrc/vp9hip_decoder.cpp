@@ -53,10 +53,12 @@ struct ParseJob {
 };
 struct Pending { vp9h_frame pkt; int out; int refs[3]; };   // refs: -1 for keyframes / intra-only
 struct Out { int buf; int64_t pts; bool submitted; };
-// Batches are numbered as launched; a frame's batch is the one that wrote its buffer
-// (buf_seq). A batch is checked (vp9hip_sync: the stream is drained and k_lfr's
-// hand-off timeout words are read) before the next one is staged, whose staging resets
-// them, or before one of its frames is handed out, whichever comes first.
+// Batches are numbered as launched (1, 2, ...) and alternate between the context's two
+// batch slots, so batch k + 1 is staged and planned while batch k's pixel kernels run. A
+// frame's batch is the one that wrote its buffer (buf_seq). A batch is checked
+// (vp9hip_sync_slot: its slot's work is drained and k_lfr's hand-off timeout words are
+// read) before its slot is staged again, which resets them, or before one of its frames
+// is handed out, whichever comes first.
 const int STALL = 1;                   // consume: no free device buffer until frames are released
 }
 
@@ -64,11 +66,14 @@ struct vp9hip_decoder {
     vp9hip_decoder_params p;
     vp9hip_ctx *ctx = nullptr;
     bool configured = false, draining = false;
+    bool stalled = false;                  // send_packet answered EAGAIN: receive must block
     int cw = 0, ch = 0, cbpp = 0, css_h = 0, css_v = 0, nbufs = 0;
     int slot[8];
     std::vector<int> pins, busy, bw, bh;   // per device buffer
     std::vector<uint64_t> buf_seq;         // per device buffer: the batch that wrote it
-    uint64_t launched = 0, checked = 0;    // batches launched / checked
+    uint64_t launched = 0;                 // batches launched; batch b ran in slot (b - 1) & 1
+    uint64_t slot_seq[2] = { 0, 0 };       // the batch last launched in each slot
+    bool slot_checked[2] = { true, true };
     std::vector<uint64_t> bad;             // batches whose check failed (VP9HIP_EBUG)
     std::vector<Pending> batch;
     std::deque<Out> outq;
@@ -165,15 +170,15 @@ static void wait_all_parsed(vp9hip_decoder *d)
 
 // ---- device side ----
 // Stage + launch the pending frames as one batch.
-// Check the launched batches: 0, or the error of a failed check other than VP9HIP_EBUG
-// (an EBUG batch is remembered; its frames fail when they are received).
-static int check_batches(vp9hip_decoder *d)
+// Check the batch last launched in slot s: 0, or the error of a failed check other than
+// VP9HIP_EBUG (an EBUG batch is remembered; its frames fail when they are received).
+static int check_slot(vp9hip_decoder *d, int s)
 {
-    if (d->checked == d->launched) return 0;
-    const int r = vp9hip_sync(d->ctx);
-    if (r == VP9HIP_EBUG) d->bad.push_back(d->launched);
+    if (d->slot_checked[s]) return 0;
+    const int r = vp9hip_sync_slot(d->ctx, s);
+    if (r == VP9HIP_EBUG) d->bad.push_back(d->slot_seq[s]);
     else if (r < 0) return r;
-    d->checked = d->launched;
+    d->slot_checked[s] = true;
     return 0;
 }
 
@@ -186,8 +191,10 @@ static bool batch_bad(const vp9hip_decoder *d, uint64_t seq)
 static int submit(vp9hip_decoder *d)
 {
     if (d->batch.empty()) return 0;
-    int cr = check_batches(d);                // before the staging resets the batch's words
+    const int slot = (int) (d->launched & 1);
+    int cr = check_slot(d, slot);             // before the staging resets that batch's words
     if (cr < 0) return cr;
+    if ((cr = vp9hip_set_batch_slot(d->ctx, slot)) < 0) return cr;
     const int n = (int) d->batch.size();
     std::vector<vp9h_frame> pk(n);
     std::vector<int> outs(n), refs(3 * n);
@@ -199,6 +206,8 @@ static int submit(vp9hip_decoder *d)
     int ret = vp9hip_stage_batch_refs(d->ctx, pk.data(), n, outs.data(), refs.data());
     if (ret >= 0) ret = vp9hip_run_batch(d->ctx);
     d->launched++;
+    d->slot_seq[slot] = d->launched;
+    d->slot_checked[slot] = ret < 0;
     for (int i = 0; i < n; i++) d->buf_seq[outs[i]] = d->launched;
     for (auto &f : d->batch) {
         vp9h_frame_free(&f.pkt);
@@ -320,7 +329,9 @@ extern "C" int vp9hip_decoder_open(const vp9hip_decoder_params *params, vp9hip_d
     if (d->p.max_batch > 256) d->p.max_batch = 256;
     if (d->p.parse_threads < 0) d->p.parse_threads = 0;
     if (d->p.parse_threads > 64) d->p.parse_threads = 64;
-    d->max_inflight = std::max(2 * d->p.parse_threads, d->p.max_batch) + 1;
+    // parse lookahead: enough frames that the pool keeps parsing while the caller's thread
+    // waits on the device (two batches in flight)
+    d->max_inflight = 4 * d->p.parse_threads + 2 * d->p.max_batch + 1;
     for (int s = 0; s < 8; s++) d->slot[s] = -1;
     int r = vp9hip_open(d->p.device, &d->ctx);
     if (r < 0) { vp9hip_decoder_close(d); return r; }
@@ -373,8 +384,9 @@ extern "C" int vp9hip_decoder_send_packet(vp9hip_decoder *d, const uint8_t *data
     if (d->inflight.size() + nf > (size_t) d->max_inflight) {
         int r = consume(d, true, d->max_inflight > nf ? d->max_inflight - nf : 0);
         if (r < 0) return r;
-        if (r == STALL) return VP9HIP_EAGAIN;
+        if (r == STALL) { d->stalled = true; return VP9HIP_EAGAIN; }
     }
+    d->stalled = false;
     for (int k = 0; k < nf; k++) {
         const int type = vp9h_frame_type(data + offs[k], sizes[k]);
         if (type < 0) return type;
@@ -410,9 +422,17 @@ extern "C" int vp9hip_decoder_receive_frame(vp9hip_decoder *d, vp9hip_decoded_fr
         return d->draining && d->inflight.empty() && d->batch.empty() ? VP9HIP_EOF : VP9HIP_EAGAIN;
     if (!d->outq.front().submitted) return VP9HIP_EAGAIN;
     const Out o = d->outq.front();
-    if (d->buf_seq[o.buf] > d->checked) {      // its batch may still run: drain and check it
-        r = check_batches(d);
-        if (r < 0) return r;
+    {                                          // its batch may still run: drain and check it
+        const uint64_t b = d->buf_seq[o.buf];
+        const int s = (int) ((b - 1) & 1);
+        if (b && d->slot_seq[s] == b && !d->slot_checked[s]) {
+            // the newest batch still running: EAGAIN (frame-threading delay), so the caller
+            // sends the next packets while it runs; an older batch, a drain or a stalled
+            // send_packet wait for it
+            if (!d->draining && !d->stalled && b == d->launched && vp9hip_slot_busy(d->ctx, s) == 1)
+                return VP9HIP_EAGAIN;
+            if ((r = check_slot(d, s)) < 0) return r;
+        }
     }
     d->outq.pop_front();
     if (batch_bad(d, d->buf_seq[o.buf])) {     // the loop filter's row hand-off broke
@@ -455,5 +475,6 @@ extern "C" int vp9hip_decoder_flush(vp9hip_decoder *d)
     d->outq.clear();
     for (int s = 0; s < 8; s++) d->slot[s] = -1;
     d->draining = false;
+    d->stalled = false;
     return d->ctx ? vp9hip_flush(d->ctx) : 0;
 }

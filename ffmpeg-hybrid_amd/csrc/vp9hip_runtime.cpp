@@ -1155,13 +1155,16 @@ static int stage_dev(vp9hip_ctx *c, const DevIn &in)
         worker();
         for (auto &t : pool) t.join();
     }
-    HIPCHK(hipMemcpyAsync(s.arena, img, up, hipMemcpyHostToDevice, c->st));
+    // the upload goes on the planner stream: the other batch slot's pixel kernels keep the
+    // main stream busy meanwhile
+    const hipStream_t us = c->pst;
+    HIPCHK(hipMemcpyAsync(s.arena, img, up, hipMemcpyHostToDevice, us));
     // scan sentinels (never written by the planner)
-    HIPCHK(hipMemsetAsync(s.arena + s.o_bneob + nb * 4, 0, 4, c->st));
-    HIPCHK(hipMemsetAsync(s.arena + s.o_sbncoef + (size_t) NS * 4, 0, 4, c->st));
-    HIPCHK(hipMemsetAsync(s.arena + s.o_cnt + (size_t) s.ncnt * 4, 0, 4, c->st));
-    HIPCHK(hipMemsetAsync(s.arena + s.o_cntm + (size_t) NS * 4, 0, 4, c->st));
-    HIPCHK(hipStreamSynchronize(c->st));
+    HIPCHK(hipMemsetAsync(s.arena + s.o_bneob + nb * 4, 0, 4, us));
+    HIPCHK(hipMemsetAsync(s.arena + s.o_sbncoef + (size_t) NS * 4, 0, 4, us));
+    HIPCHK(hipMemsetAsync(s.arena + s.o_cnt + (size_t) s.ncnt * 4, 0, 4, us));
+    HIPCHK(hipMemsetAsync(s.arena + s.o_cntm + (size_t) NS * 4, 0, 4, us));
+    HIPCHK(hipStreamSynchronize(us));
     s.ready = true;
     return 0;
 }
@@ -1169,6 +1172,8 @@ static int stage_dev(vp9hip_ctx *c, const DevIn &in)
 // Run the device planner of the staged batch and build its launch list from the summary.
 static int plan_dev(vp9hip_ctx *c)
 {
+    static const bool plan_trace = getenv("VP9HIP_STAGE_TRACE") && atoi(getenv("VP9HIP_STAGE_TRACE"));
+    const auto pt0 = std::chrono::steady_clock::now();
     Staged &s = c->stg;
     uint8_t *A = s.arena;
     s.planned = false;
@@ -1257,6 +1262,9 @@ static int plan_dev(vp9hip_ctx *c)
         for (int k = 0; k < 11; k++) fprintf(stderr, " %d:%.1f", k, 100.0 * (double) pc[k] / std::max(1.0, tot));
         fprintf(stderr, "\n");
     }
+    if (plan_trace)
+        fprintf(stderr, "vp9hip plan (device): %d frames: %.2f ms host wall\n", s.nframes,
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - pt0).count());
     const uint32_t *sm = s.summary_h;
     if (sm[0]) {                                              // the packets are inconsistent (PLS_*)
         fprintf(stderr, "vp9hip: batch rejected by the device planner (status 0x%x, bounds 0x%x)\n", sm[0],
@@ -1368,7 +1376,8 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     if (!c || !pkts || n <= 0 || !out_bufs) return VP9HIP_EINVAL;
     if (c->bufs.empty()) return VP9HIP_EINVAL;
     hipSetDevice(c->dev);
-    HIPCHK(hipStreamSynchronize(c->st));      // the previous batch may still read the arena
+    // this slot's previous batch may still read the arena (the other slot's work may go on)
+    if (c->stg.done_ev) HIPCHK(hipEventSynchronize(c->stg.done_ev));
     Staged &s = c->stg;
     if (s.graph) { hipGraphExecDestroy(s.graph); s.graph = nullptr; }
     s.frames.clear(); s.sbs.clear(); s.pjobs.clear(); s.passes.clear(); s.lfs.clear(); s.mcs.clear();
@@ -2137,20 +2146,44 @@ extern "C" int64_t vp9hip_stripe(vp9hip_ctx *c, int frame, int tile_lo, int tile
     return off;
 }
 
+// k_lfr bounds its spins and counts the waits it gave up (timeout word of each launch's
+// counter block): a nonzero count means the row hand-off broke, and the slot's frames are
+// not trusted. The slot's work must be complete.
+static int check_lfr(const Staged &g)
+{
+    if (!g.ready || g.lfr_ctr.empty()) return 0;
+    std::vector<uint32_t> ctr(g.n_ctr);
+    HIPCHK(hipMemcpy(ctr.data(), g.arena + g.o_ctr, ctr.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    for (uint32_t o : g.lfr_ctr)
+        if (ctr[o + 2]) return VP9HIP_EBUG;
+    return 0;
+}
+
+extern "C" int vp9hip_sync_slot(vp9hip_ctx *c, int slot)
+{
+    if (!c || slot < 0 || slot > 1) return VP9HIP_EINVAL;
+    hipSetDevice(c->dev);
+    const Staged &g = slot == c->slot ? c->stg : c->alt;
+    if (g.done_ev) HIPCHK(hipEventSynchronize(g.done_ev));
+    return check_lfr(g);
+}
+
+extern "C" int vp9hip_slot_busy(vp9hip_ctx *c, int slot)
+{
+    if (!c || slot < 0 || slot > 1) return VP9HIP_EINVAL;
+    hipSetDevice(c->dev);
+    const Staged &g = slot == c->slot ? c->stg : c->alt;
+    if (!g.done_ev) return 0;
+    const hipError_t e = hipEventQuery(g.done_ev);
+    return e == hipErrorNotReady ? 1 : e == hipSuccess ? 0 : VP9HIP_EEXTERNAL;
+}
+
 extern "C" int vp9hip_sync(vp9hip_ctx *c)
 {
     if (!c) return VP9HIP_EINVAL;
     hipSetDevice(c->dev);
     HIPCHK(hipStreamSynchronize(c->st));
-    // k_lfr bounds its spins and counts the waits it gave up (timeout word of each
-    // launch's counter block): a nonzero count means the row hand-off broke, and the
-    // frames are not trusted
-    if (c->stg.ready && !c->stg.lfr_ctr.empty()) {
-        std::vector<uint32_t> ctr(c->stg.n_ctr);
-        HIPCHK(hipMemcpy(ctr.data(), c->stg.arena + c->stg.o_ctr, ctr.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
-        for (uint32_t o : c->stg.lfr_ctr)
-            if (ctr[o + 2]) return VP9HIP_EBUG;
-    }
+    if (const int r = check_lfr(c->stg)) return r;
     if (c->timing && c->timed_run && c->stg.ready) {
         for (int k = 0; k < K_N; k++) { c->kms[k] = 0; c->kcount[k] = 0; }
         for (size_t i = 0; i < c->stg.launches.size() && 2 * i + 1 < c->ev.size(); i++) {

@@ -174,6 +174,11 @@ int64_t vp9hip_stripe(vp9hip_ctx *ctx, int frame, int tile_lo, int tile_hi, void
  * (arena, plan, launch graph); the frame buffers are the context's. Alternating two staged
  * batches lets one batch's device planning run while the other's pixel kernels do. */
 int  vp9hip_set_batch_slot(vp9hip_ctx *ctx, int slot);
+/* Wait for the last run of batch slot `slot` only (the other slot's work may continue)
+ * and check it as vp9hip_sync does (VP9HIP_EBUG: a loop-filter hand-off timed out). */
+int  vp9hip_sync_slot(vp9hip_ctx *ctx, int slot);
+/* 1 while the last run of batch slot `slot` is still executing, 0 once it is done. */
+int  vp9hip_slot_busy(vp9hip_ctx *ctx, int slot);
 /* Wait for all queued work. VP9HIP_EBUG if a row-pipelined loop-filter launch (k_lfr)
  * gave up a bounded wait on another workgroup's progress (frames not trusted). */
 int  vp9hip_sync(vp9hip_ctx *ctx);

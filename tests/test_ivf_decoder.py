@@ -157,7 +157,7 @@ def test_decoder_formats(v9, orc, bpp, ssh, ssv):
 def test_decoder_eagain_flush_and_restart(v9, orc):
     """send_packet's EAGAIN when no buffer is free (frames held by the caller), receive's
     EAGAIN inside the decoder delay, flush (seek) then a new keyframe."""
-    fr = _frames(v9, 136, 72, 30)
+    fr = _frames(v9, 136, 72, 60)          # more than the parse lookahead + the buffer pool
     enc = v9.Stream()
     long_gop = [enc.encode(fr[0])[0]] + [enc.encode(f, ref_slot=(1 if i else 0, 0, 0), refresh_mask=2)[0]
                                          for i, f in enumerate(fr[1:])]
