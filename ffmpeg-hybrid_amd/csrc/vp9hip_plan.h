@@ -77,6 +77,8 @@ typedef struct PlanDev {
     /* products */
     SBRec *sbs; WGRec *wgs; PJob *pjobs; uint32_t *passes; LFRec *lfs; RJob *rjobs; McUnit *mcs;
     uint32_t *dlists;                /* intra step lists (device part of the lists array)    */
+    uint32_t *jobw;                  /* per slot: jcap intra job words (k_pjob -> k_plan)     */
+    uint32_t *sb_nj;                 /* per slot: intra jobs                                 */
     const uint8_t *nz;               /* [5][4][1025][2] nonzero bounding boxes                */
     uint32_t jcap, rcap;             /* jobs / residual units per SB slot                    */
     uint32_t nslots;

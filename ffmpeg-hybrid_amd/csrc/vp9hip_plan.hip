@@ -10,10 +10,12 @@
 //   k_psb    one wave per SB: per-tx eobs -> coefficient total, residual-job counts per
 //            (tcode, txtp), MC-unit count, the intra 4x4-unit map
 //   (scan)   coefficients (decode order) -> each SB's first coefficient; counts -> record offsets
-//   k_plan   one wave per SB: intra jobs with check_intra_mode resolved (vp9recon.c:37-221)
-//            and their producers, heights, list-scheduled passes (the host's merge_mixed,
-//            restated wave-parallel), residual jobs, MC units (vp9_mc_template.c:30-464),
-//            the LF program (vp9block.c:1142-1262, vp9lpf.c:31-230), the SB's intra step
+//   k_pjob   one wave per SB: the tx blocks in decode order, eobs, coefficient offsets,
+//            residual jobs, intra job words with check_intra_mode resolved (vp9recon.c:37-221)
+//   k_plan   one wave per SB: the intra jobs' producers, heights, list-scheduled passes (the
+//            host's merge_mixed, restated wave-parallel), the SB's intra step
+//   k_pllf   one wave per SB: the LF program (vp9block.c:1142-1262, vp9lpf.c:31-230)
+//   k_plmc   one wave per SB of inter frames: MC units (vp9_mc_template.c:30-464)
 //   k_plevel one workgroup per level-scheduled inter frame: SB dependency levels along
 //            anti-diagonals
 //   k_pkeys  step-list offsets; the launch summary the host reads back
@@ -334,24 +336,24 @@ __global__ __launch_bounds__(64) void k_psb(PlanDev D)
 }
 
 // ------------------------------------------------------------------ k_plan
-// k_plan's LDS: the fields of consecutive phases share storage (lifetimes in brackets).
-// b.hgt overlays a.jmap (read until the producers are listed, hgt is set after that);
-// b's other fields overlay a's tail, which is dead once the jobs are built.
+// k_pjob's LDS: the SB's blocks and its tx enumeration.
+template <int JCAP> struct PJobLds {
+    PBlk blk[64];
+    uint32_t pre[3 * 64 + 1];
+    uint16_t et[JCAP];            // eob per tx (decode order)
+    uint16_t co[JCAP];            // SB-relative first coefficient per tx; first the raw eobs
+    uint16_t ost[JCAP];           // (block, plane) entry starting at tx t, else 0
+    uint8_t  own[JCAP];           // (block, plane) entry of tx t (max-scan of ost)
+    uint32_t eb[64];              // first eob entry of each block
+};
+// k_plan's LDS: hgt overlays the unit map (read until the producers are listed, hgt is set
+// after that); the other scheduling fields follow it.
 template <int JCAP> struct PlanLds {
-    PBlk blk[64];                 // [all]
-    uint32_t ja[JCAP];            // [jobs .. cross reads] PJob word per intra job (decode order),
-                                  // bit 30: the 4x4 top-right lies inside the block (trx)
+    uint32_t ja[JCAP];            // PJob word per intra job (decode order), bit 30: the 4x4
+                                  // top-right lies inside the block (trx)
     union {
-        struct {                  // [prefix .. jobs], jmap [jobs .. producers]
-            uint16_t jmap[3][256];        // producing job of each 4x4 unit
-            uint32_t pre[3 * 64 + 1];
-            uint16_t et[JCAP];            // eob per tx (decode order)
-            uint16_t co[JCAP];            // SB-relative first coefficient per tx; first the raw eobs
-            uint16_t ost[JCAP];           // (block, plane) entry starting at tx t, else 0
-            uint8_t  own[JCAP];           // (block, plane) entry of tx t (max-scan of ost)
-            uint32_t eb[64];              // first eob entry of each block
-        } a;
-        struct {                  // [producers .. scheduling]
+        uint16_t jmap[3][256];    // producing job of each 4x4 unit
+        struct {
             uint32_t hgt[JCAP];           // longest path to a sink (list-scheduling priority)
             uint16_t doff[JCAP + 1];      // producers of job j: dep[doff[j] .. doff[j + 1])
             uint16_t dep[4 * JCAP];
@@ -375,11 +377,16 @@ DEV uint32_t wor(uint32_t v) { return rdl(wscan_dpp<OP_OR>(v), 63); }
 #define PPT(k) do { if (D.prof) { const unsigned long long t_ = clock64(); \
         if (lane == 0) atomicAdd(&D.prof[k], t_ - pt0); pt0 = t_; } } while (0)
 
+// One wave per SB: the SB's tx blocks in decode order (the (block, plane) entry of each
+// by a max-scan), their eobs and coefficient offsets, the residual jobs (every coded tx,
+// bucketed by transform), and the intra jobs' words with check_intra_mode resolved, for
+// k_plan. Small LDS (4.8 KB at 4:2:0): a kernel of its own so this per-tx work runs at full
+// occupancy instead of with k_plan's scheduling state.
 template <int SSH, int SSV>
-__global__ __launch_bounds__(64) void k_plan(PlanDev D)
+__global__ __launch_bounds__(64) void k_pjob(PlanDev D)
 {
     constexpr int CW = 16 >> SSH, CH = 16 >> SSV, JCAP = 256 + 2 * CW * CH;
-    __shared__ PlanLds<JCAP> S;
+    __shared__ PJobLds<JCAP> S;
     const PlanFrame &F = D.frames[blockIdx.y];
     const int s = blockIdx.x, lane = threadIdx.x;
     if (s >= F.sb_cols * F.sb_rows) return;
@@ -391,27 +398,26 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
     const int nb = sb_blocks(D, slot, b0, st);
     st = 0;                                   // reported by k_psb
     if (lane < nb) S.blk[lane] = pblk(load_block(&D.blocks[b0 + lane]));
-    for (int i = lane; i < 3 * 256; i += 64) (&S.u.a.jmap[0][0])[i] = 0xffff;
     wsync();
-    const uint32_t tot = sb_prefix<SSH, SSV>(S.blk, nb, cols, rows, G.mine, S.u.a.pre, lane);
+    const uint32_t tot = sb_prefix<SSH, SSV>(S.blk, nb, cols, rows, G.mine, S.pre, lane);
     const int T = pl_min((int) (tot & 1023), JCAP), NJ = pl_min((int) (tot >> 20), JCAP);
     // the (block, plane) entry of every tx: each non-empty entry marks its first tx (ranges
     // are disjoint), a max-scan fills the rest (= sb_locate's largest k with pre[k] <= t)
-    for (int t = lane; t < T; t += 64) S.u.a.ost[t] = 0;
+    for (int t = lane; t < T; t += 64) S.ost[t] = 0;
     wsync();
     if (lane < nb)
         for (int p = 0; p < 3; p++) {
             const int k = 3 * lane + p;
-            const uint32_t a0 = S.u.a.pre[k] & 1023, a1 = S.u.a.pre[k + 1] & 1023;
-            if (a1 > a0 && a0 < (uint32_t) T) S.u.a.ost[a0] = (uint16_t) k;
+            const uint32_t a0 = S.pre[k] & 1023, a1 = S.pre[k + 1] & 1023;
+            if (a1 > a0 && a0 < (uint32_t) T) S.ost[a0] = (uint16_t) k;
         }
     wsync();
     {
         uint32_t carry = 0;
         for (int c = 0; c < T; c += 64) {
-            const uint32_t v = c + lane < T ? S.u.a.ost[c + lane] : 0u;
+            const uint32_t v = c + lane < T ? S.ost[c + lane] : 0u;
             const uint32_t incl = dpp_op<OP_MAX>(wscan_dpp<OP_MAX>(v), carry);
-            if (c + lane < T) S.u.a.own[c + lane] = (uint8_t) incl;
+            if (c + lane < T) S.own[c + lane] = (uint8_t) incl;
             carry = rdl(incl, 63);
         }
     }
@@ -423,33 +429,33 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
     // into LDS, then each tx picks its entry (skipped blocks have none)
     {
         const uint32_t be = lane <= nb ? D.blk_eob0[b0 + (uint32_t) lane] : 0u;      // nb + 1 entries
-        if (lane < nb) S.u.a.eb[lane] = be;
+        if (lane < nb) S.eb[lane] = be;
         const uint32_t E0 = rdl(be, 0), E1 = rdl(be, nb);
         uint32_t E = E1 - E0;
         if (E1 < E0 || E > (uint32_t) JCAP || E1 > D.total_eobs) { st |= PLS_EOB; E = 0; }
-        for (uint32_t i = (uint32_t) lane; i < E; i += 64) S.u.a.co[i] = D.eobs[E0 + i];
+        for (uint32_t i = (uint32_t) lane; i < E; i += 64) S.co[i] = D.eobs[E0 + i];
         wsync();
         for (int t = lane; t < T; t += 64) {
-            const int k = S.u.a.own[t], b = (k * 171) >> 9;
+            const int k = S.own[t], b = (k * 171) >> 9;
             const PBlk &bk = S.blk[b];
             int e = 0;
             if (!bk.skip) {
-                const uint32_t i = S.u.a.eb[b] - E0 + (uint32_t) t - (S.u.a.pre[3 * b] & 1023);
+                const uint32_t i = S.eb[b] - E0 + (uint32_t) t - (S.pre[3 * b] & 1023);
                 const int txs = (k - 3 * b) ? bk.uvtx : bk.tx;
-                if (i < E) e = S.u.a.co[i];
+                if (i < E) e = S.co[i];
                 else st |= PLS_EOB;
                 if (e > (16 << (2 * txs))) { st |= PLS_EOB; e = 0; }
             }
-            S.u.a.et[t] = (uint16_t) e;
+            S.et[t] = (uint16_t) e;
         }
     }
     wsync();
     {
         uint32_t carry = 0;
         for (int c = 0; c < T; c += 64) {
-            const uint32_t v = c + lane < T ? S.u.a.et[c + lane] : 0u;
+            const uint32_t v = c + lane < T ? S.et[c + lane] : 0u;
             const uint32_t incl = wscan_incl(v, lane);
-            if (c + lane < T) S.u.a.co[c + lane] = (uint16_t) (carry + incl - v);
+            if (c + lane < T) S.co[c + lane] = (uint16_t) (carry + incl - v);
             carry += rdl(incl, 63);
         }
     }
@@ -475,10 +481,10 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
         int key = -1;
         RJob r;
         if (t < T) {
-            const Tx tx = sb_tx_at<SSH, SSV>(S.blk, S.u.a.pre, S.u.a.own[t], (uint32_t) t, cols, rows);
+            const Tx tx = sb_tx_at<SSH, SSV>(S.blk, S.pre, S.own[t], (uint32_t) t, cols, rows);
             const PBlk &b = S.blk[tx.b];
             const int p = tx.p, sh = p ? SSH : 0, sv = p ? SSV : 0, txs = tx.g.txs;
-            const int e0 = S.u.a.et[t];
+            const int e0 = S.et[t];
             int mode = 0, txtp = 0;
             if (b.intra) {
                 mode = tx_mode(b, tx, st);
@@ -488,7 +494,7 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
             const int ux0 = ((tx.g.bx - G.sbx * (64 >> sh)) >> 2) + tx.x, uy0 = ((tx.g.by - G.sby * (64 >> sv)) >> 2) + tx.y;
             const uint32_t roff = rbase + pl_resid_unit(p, ux0, uy0, SSH, SSV);
             if (e0 && G.mine) {
-                uint32_t coef = coef_sb + S.u.a.co[t];
+                uint32_t coef = coef_sb + S.co[t];
                 int e = e0;
                 if (coef + (uint32_t) e > D.total_coefs) { st |= PLS_COEF; e = 0; coef = 0; }
                 r.coef = coef;
@@ -506,16 +512,11 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
                 key = tcode * 4 + txtp;
             }
             if (b.intra && G.mine) {
-                const int j = (int) (S.u.a.pre[tx.k] >> 20) + tx.l;
+                const int j = (int) (S.pre[tx.k] >> 20) + tx.l;
                 const int pw8 = p ? cols * 8 >> SSH : cols * 8, ph8 = p ? rows * 8 >> SSV : rows * 8;
                 const PlIntra pi = pl_intra_job(p, txs, mode, e0, tx.g.bx + tx.x * 4, tx.g.by + tx.y * 4, tx.x, tx.g.pw4,
                                                 p ? tx0l >> SSH : tx0l, pw8, ph8, ux0, uy0);
-                if (j < JCAP) {
-                    S.ja[j] = pi.a | (pi.trx ? JA_TRX : 0u);
-                    const int units = 16 >> sh, unitsv = 16 >> sv;
-                    for (int v = uy0; v < uy0 + tx.g.step && v < unitsv; v++)
-                        for (int u = ux0; u < ux0 + tx.g.step && u < units; u++) S.u.a.jmap[p][v * 16 + u] = (uint16_t) j;
-                }
+                if (j < JCAP) D.jobw[(size_t) slot * JCAP + (uint32_t) j] = pi.a | (pi.trx ? JA_TRX : 0u);
             }
         }
         // ranks within each key, in decode order: one ballot per distinct key of the chunk
@@ -532,8 +533,44 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
         }
         if (key >= 0 && inb(D, pos, D.cap_rjobs, 64u)) D.rjobs[pos] = r;
     }
-    wsync();
+    for (int d = 32; d; d >>= 1) ibytes += __shfl_xor(ibytes, d);
+    if (lane == 0) {
+        D.sb_nj[slot] = (uint32_t) (G.mine ? NJ : 0);
+        if (ibytes && inb(D, (uint32_t) F.frame, D.nframes, 2048u)) atomicAdd(&D.fbytes[2 * F.frame], ibytes);
+    }
+    st = wor(st);
+    if (lane == 0 && st) atomicOr(D.status, st);
     PPT(2);
+}
+
+// One wave per SB: producers of every intra job, heights, priority order, list-scheduled
+// passes (the host's merge_mixed), the PJob / pass records, the SB's records, its level
+// dependencies and intra step. Jobs come from k_pjob (D.jobw); the unit map is rebuilt.
+template <int SSH, int SSV>
+__global__ __launch_bounds__(64) void k_plan(PlanDev D)
+{
+    constexpr int CW = 16 >> SSH, CH = 16 >> SSV, JCAP = 256 + 2 * CW * CH;
+    __shared__ PlanLds<JCAP> S;
+    const PlanFrame &F = D.frames[blockIdx.y];
+    const int s = blockIdx.x, lane = threadIdx.x;
+    if (s >= F.sb_cols * F.sb_rows) return;
+    unsigned long long pt0 = D.prof ? clock64() : 0;
+    const SbGeo G = sb_geo(F, s);
+    const uint32_t slot = G.slot;
+    const uint32_t rbase = slot * D.rcap;
+    uint32_t st = 0;
+    const int NJ = pl_min((int) D.sb_nj[slot], JCAP);
+    for (int i = lane; i < 3 * 256; i += 64) (&S.u.jmap[0][0])[i] = 0xffff;
+    for (int j = lane; j < NJ; j += 64) S.ja[j] = D.jobw[(size_t) slot * JCAP + (uint32_t) j];
+    wsync();
+    for (int j = lane; j < NJ; j += 64) {                  // the unit map: each job's 4x4 units
+        const uint32_t a = S.ja[j];
+        const int p = a & 3, step = 1 << ((a >> 2) & 3), ux0 = (a >> 12) & 15, uy0 = (a >> 16) & 15;
+        const int units = p ? CW : 16, unitsv = p ? CH : 16;
+        for (int v = uy0; v < uy0 + step && v < unitsv; v++)
+            for (int u = ux0; u < ux0 + step && u < units; u++) S.u.jmap[p][v * 16 + u] = (uint16_t) j;
+    }
+    wsync();
 
     // ---- producers of every intra job (the pixels its substituted mode reads)
     auto deps_of = [&](int j, auto fn) {
@@ -546,7 +583,7 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
         const int nd = (int) needs_of(a);
         bool left_run = false;
         pl_local_reads(ux0, uy0, 1 << ts, nd, (a & JA_TRX) ? 1 : 0, units, unitsv, [&](int unit) {
-            const int d = S.u.a.jmap[p][unit];
+            const int d = S.u.jmap[p][unit];
             const bool is_left = (unit & 15) == ux0 - 1 && (unit >> 4) >= uy0;
             if (is_left && !left_run) { left_run = true; last = -1; }
             if (d == 0xffff || d >= j || d == last || (left_run && d == first)) { if (d != 0xffff && d < j) last = d; return; }
@@ -734,11 +771,6 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
             D.sb_kpos[slot] = inb(D, key, D.nkeys, 1024u) ? atomicAdd(&D.key_cnt[key], 1u) : 0u;
         }
     }
-    for (int d = 32; d; d >>= 1) ibytes += __shfl_xor(ibytes, d);
-    if (lane == 0) {
-        if (!inb(D, (uint32_t) F.frame, D.nframes, 2048u)) return;
-        if (ibytes) atomicAdd(&D.fbytes[2 * F.frame], ibytes);
-    }
     st = wor(st);
     if (lane == 0 && st) atomicOr(D.status, st);
     PPT(10);
@@ -908,12 +940,13 @@ __global__ __launch_bounds__(256) void k_plists(PlanDev D)
     if (inb(D, i, D.cap_dlists, 16384u)) D.dlists[i] = slot;
 }
 
-// stage 0: k_psb; 1: k_plan, then k_pllf (filtered frames) and k_plmc (inter frames)
+// stage 0: k_psb; 1: k_pjob, k_plan, then k_pllf (filtered frames) and k_plmc (inter frames)
 template <int SSH, int SSV>
 void launch_sb_kernels(hipStream_t st, const PlanDev &D, int max_sb, int nframes, int stage, int flags)
 {
     const dim3 g(max_sb, nframes);
     if (stage == 0) { hipLaunchKernelGGL((k_psb<SSH, SSV>), g, dim3(64), 0, st, D); return; }
+    hipLaunchKernelGGL((k_pjob<SSH, SSV>), g, dim3(64), 0, st, D);
     hipLaunchKernelGGL((k_plan<SSH, SSV>), g, dim3(64), 0, st, D);
     if (flags & 1) hipLaunchKernelGGL((k_pllf<SSH, SSV>), g, dim3(64), 0, st, D);
     if (flags & 2) hipLaunchKernelGGL((k_plmc<SSH, SSV>), g, dim3(64), 0, st, D);

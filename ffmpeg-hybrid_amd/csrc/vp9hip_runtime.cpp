@@ -162,7 +162,7 @@ struct Staged {
     size_t o_pf = 0, o_blocks = 0, o_eobs = 0, o_slotpos = 0, o_segpre = 0, o_segsz = 0, o_segpre1 = 0, o_cntm = 0, o_cntm0 = 0, o_gidx = 0, o_bneob = 0,
            o_beob0 = 0, o_sbfirst = 0, o_sbncoef = 0, o_sbcoef0 = 0, o_cnt = 0, o_cnt0 = 0, o_ibits = 0,
            o_sbinfo = 0, o_sbkey = 0, o_sbkpos = 0, o_keycnt = 0, o_keyoff = 0, o_status = 0, o_fbytes = 0,
-           o_summary = 0, o_scan = 0, zero_bytes = 0;
+           o_summary = 0, o_scan = 0, zero_bytes = 0, o_jobw = 0, o_sbnj = 0;
     size_t scan_bytes = 0, summary_words = 0;
     uint32_t *summary_h = nullptr;                            // pinned readback of the summary
     size_t summary_cap = 0;
@@ -1094,6 +1094,8 @@ static int stage_dev(vp9hip_ctx *c, const DevIn &in)
     s.o_lfs = o; o = al(o + (size_t) NS * sizeof(LFRec));
     s.o_pjobs = o; o = al(o + (size_t) NS * s.jcap * sizeof(PJob));
     s.o_passes = o; o = al(o + (size_t) NS * s.jcap * 4);
+    s.o_jobw = o; o = al(o + (size_t) NS * s.jcap * 4);
+    s.o_sbnj = o; o = al(o + (size_t) NS * 4);
     s.o_rjobs = o; o = al(o + (ne + 1) * sizeof(RJob));
     s.o_mcs = o; o = al(o + (nmc + 1) * sizeof(McUnit));
     s.cap_mcs = (uint32_t) (nmc + 1);
@@ -1222,6 +1224,8 @@ static int plan_dev(vp9hip_ctx *c)
     D.rjobs = (RJob *) (A + s.o_rjobs);
     D.mcs = (McUnit *) (A + s.o_mcs);
     D.dlists = (uint32_t *) (A + s.o_lists) + s.host_lists;
+    D.jobw = (uint32_t *) (A + s.o_jobw);
+    D.sb_nj = (uint32_t *) (A + s.o_sbnj);
     D.nz = c->nz;
     D.jcap = (uint32_t) s.jcap;
     D.rcap = (uint32_t) s.rcap;
