@@ -86,6 +86,7 @@ typedef struct PlanDev {
      * status[1] (and PLS_SCHED) instead of writing */
     uint32_t cap_cnt, cap_cntm, cap_rjobs, cap_mcs, cap_dlists, nkeys, nframes;
     unsigned long long *prof;        /* diagnostics (VP9HIP_PLAN_PROF): k_plan cycles per phase, or null */
+    int dbg;                         /* diagnostics (VP9HIP_PLAN_DBG): ablation switches, timing only */
 } PlanDev;
 
 #endif

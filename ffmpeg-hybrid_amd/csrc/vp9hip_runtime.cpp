@@ -1238,6 +1238,8 @@ static int plan_dev(vp9hip_ctx *c)
     D.nkeys = s.nkey;
     D.nframes = (uint32_t) s.nframes;
     static const bool pprof = getenv("VP9HIP_PLAN_PROF") && atoi(getenv("VP9HIP_PLAN_PROF"));
+    static const int pdbg = getenv("VP9HIP_PLAN_DBG") ? atoi(getenv("VP9HIP_PLAN_DBG")) : 0;
+    D.dbg = pdbg;
     D.prof = nullptr;
     if (pprof) {
         if (!c->plan_prof && hipMalloc(&c->plan_prof, 16 * sizeof(unsigned long long)) != hipSuccess) return VP9HIP_ENOMEM;
