@@ -674,6 +674,7 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
     uint32_t *gpass = D.passes + (size_t) slot * JCAP;
     PJob *gjob = D.pjobs + (size_t) slot * JCAP;
     int done = 0, npass = 0, c0 = 0;
+    if (D.dbg & 2) done = NJ;                 // ablation (timing only): no pass building
     while (done < NJ) {
         int budget = 64, ntake = 0;
         for (int c = c0; c < NJ && budget >= 4; c += 64) {
