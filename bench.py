@@ -229,6 +229,26 @@ def main():
         per = json.load(open(tf))["per_launch"].get(dom)
         if per:
             traffic, traffic_src = round(per["traffic_bytes"]), "profiles/%s/traffic.json" % TRAFFIC_PROFILE
+    # instruction issue of the same kernel from the committed SQ pass (profiles/<P>/pmc_summary.txt):
+    # VALU wave-instructions per launch / its mean duration there, vs the VALU issue peak
+    # (256 CUs x 4 SIMDs x 16 lanes: one wave64 instruction per 4 cycles per SIMD at 2.4 GHz)
+    issue = None
+    pf = os.path.join(ROOT, "profiles", TRAFFIC_PROFILE, "pmc_summary.txt")
+    if os.path.exists(pf) and args.config == "C3" and args.chroma == "420":
+        cur, vals = None, {}
+        for line in open(pf):
+            if not line.startswith(" "):
+                cur = line.strip()
+            elif cur == dom:
+                f = line.split()
+                vals[f[0]] = float(f[2].split("=")[1])
+        if "SQ_INSTS_VALU" in vals and vals.get("duration_us"):
+            peak = 256 * 4 * 2.4e9 / 4
+            rate = vals["SQ_INSTS_VALU"] / (vals["duration_us"] * 1e-6)
+            issue = {"valu_instr_per_launch": vals["SQ_INSTS_VALU"], "salu_instr_per_launch": vals.get("SQ_INSTS_SALU"),
+                     "duration_us": vals["duration_us"], "valu_frac": round(rate / peak, 4),
+                     "wait_frac": round(vals["SQ_WAIT_ANY"] / vals["SQ_WAVE_CYCLES"], 4) if vals.get("SQ_WAVE_CYCLES") else None,
+                     "source": "profiles/%s/pmc_summary.txt" % TRAFFIC_PROFILE}
     roofline = {
         "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": traffic_src,
@@ -245,6 +265,7 @@ def main():
                             "with the %d frame groups on concurrent streams" % streams,
         "kernel_ms": {k: round(ksum[k][0] / args.steps, 3) for k in ksum},
         "kernel_launches": {k: int(ksum[k][1] / args.steps) for k in ksum},
+        "issue": issue,
     }
 
     # bit-exactness of the timed frames: the CPU-baseline leg's oracle frames are compared
