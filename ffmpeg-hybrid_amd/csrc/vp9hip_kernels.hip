@@ -1208,24 +1208,22 @@ DEV uint32_t lf_eih(int L, int sharp, int bd)
 // The filter passes of one SB over its LDS tile: all column edges of every plane (lanes =
 // pixel rows), then all row edges (lanes = pixel columns). Ends with a barrier.
 template <typename PIX, class G, int NT, int PASSES = 3>
-DEV void lf_passes(LfLds<PIX, G> &S, int lane, int bd)
+DEV void lf_passes_v(PIX *lt, PIX (*ct)[LfP<PIX, G>::CR * LfP<PIX, G>::UVP], const uint32_t *prog, const uint32_t *lut,
+                     int lane, int bd)
 {
 #define LF_SYNC() do { if (NT == 64) wave_sync(); else __syncthreads(); } while (0)
     typedef LfP<PIX, G> L;
     constexpr int FLP = L::YP, FCP = L::UVP, CW = G::CW, CH = G::CH;
     constexpr int XL = L::XL, XO = L::XO;
-    PIX *lt = S.lt;
-    PIX (*ct)[L::CR * FCP] = S.ct;
-    const uint32_t *lut = S.lut;
     // ---- column edges (filter_plane_cols, vp9lpf.c:31-104): one lane per pixel row ----
     if (PASSES & 1) {
     for (int tid = lane; tid < 64 + 2 * CH; tid += NT) {
         if (tid < 64) {
-            lf_line_row_wide<PIX>((uint32_t *) (lt + (tid + 8) * FLP + XO), S.prog + (LFP_YC + (tid >> 3) * 16) / 4, lut, bd);
+            lf_line_row_wide<PIX>((uint32_t *) (lt + (tid + 8) * FLP + XO), prog + (LFP_YC + (tid >> 3) * 16) / 4, lut, bd);
         } else {
             const int p = 1 + (tid - 64 >= CH), r = tid - 64 - (p - 1) * CH;
             uint32_t *rowp = (uint32_t *) (ct[p - 1] + (r + 8) * FCP + XO);
-            const uint32_t *pw = S.prog + (LFP_CC + (r >> 3) * LFP_CSTRIDE(G::SH)) / 4;
+            const uint32_t *pw = prog + (LFP_CC + (r >> 3) * LFP_CSTRIDE(G::SH)) / 4;
             if (G::SH) lf_line_row_narrow<PIX>(rowp, pw, lut, bd);
             else lf_line_row_wide<PIX>(rowp, pw, lut, bd);
         }
@@ -1236,11 +1234,11 @@ DEV void lf_passes(LfLds<PIX, G> &S, int lane, int bd)
     if (PASSES & 2) {
     for (int tid = lane; tid < 64 + 2 * CW; tid += NT) {
         if (tid < 64) {
-            lf_line_col_wide<PIX, FLP>(lt + XL + tid, S.prog + (LFP_YR + (tid >> 3) * 16) / 4, lut, bd);
+            lf_line_col_wide<PIX, FLP>(lt + XL + tid, prog + (LFP_YR + (tid >> 3) * 16) / 4, lut, bd);
         } else {
             const int p = 1 + (tid - 64 >= CW), c = tid - 64 - (p - 1) * CW;
             PIX *colp = ct[p - 1] + XL + c;
-            const uint32_t *pw = S.prog + (LFP_CR(G::SH, G::SV) + (c >> 3) * LFP_CSTRIDE(G::SV)) / 4;
+            const uint32_t *pw = prog + (LFP_CR(G::SH, G::SV) + (c >> 3) * LFP_CSTRIDE(G::SV)) / 4;
             if (G::SV) lf_line_col_narrow<PIX, FCP>(colp, pw, lut, bd);
             else lf_line_col_wide<PIX, FCP>(colp, pw, lut, bd);
         }
@@ -1248,6 +1246,12 @@ DEV void lf_passes(LfLds<PIX, G> &S, int lane, int bd)
     LF_SYNC();
     }
 #undef LF_SYNC
+}
+
+template <typename PIX, class G, int NT, int PASSES = 3>
+DEV void lf_passes(LfLds<PIX, G> &S, int lane, int bd)
+{
+    lf_passes_v<PIX, G, NT, PASSES>(S.lt, S.ct, S.prog, S.lut, lane, bd);
 }
 
 template <typename PIX, class G, int NT>
@@ -1411,6 +1415,16 @@ DEV void lfr_top(Chunk16::T (&v)[NU], const LfrPlanes &P, int sbx, int sby, int 
     }
 }
 
+// LFR_PROF builds (profiling only, tools/lfr_prof.sh): lane 0 of each k_lfr workgroup sums
+// the shader-clock cycles of its SB-step phases into lfr_prof[] (vp9hip_lfr_prof_read)
+#ifndef LFR_PROF
+#define LFR_PROF 0
+#endif
+__device__ unsigned long long lfr_prof[16];
+#define LFR_T(i)                                                                                  \
+    do {                                                                                          \
+        if (LFR_PROF) { const uint64_t tn = clock64(); pacc[i] += tn - tp; tp = tn; }             \
+    } while (0)
 // PF: the next SB's interior loads are issued before this SB's filtering (in registers)
 template <typename PIX, class G, bool PF>
 __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfr(const uint32_t *__restrict__ tasks, const LFRec *__restrict__ recs,
@@ -1427,6 +1441,8 @@ __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfr(const uint32_t *__rest
     uint32_t *const progress = ctr + 4;
     // the row chain is the latency path of the phase: its waves issue first on their SIMDs
     __builtin_amdgcn_s_setprio(3);
+    uint64_t pacc[14] = {0}, tp = LFR_PROF ? clock64() : 0;
+    const uint64_t tk0 = tp;
     if (lane == 0) s_task = atomicAdd(&ctr[0], 1u);
     __syncthreads();
     const uint32_t *T = tasks + tasks[s_task];
@@ -1450,6 +1466,7 @@ __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfr(const uint32_t *__rest
     const bool mover = lane >= NT;
     const int ml = lane - NT;
     if (!mover) lfr_issue<PIX, G, NT, NU>(v, P, c0, sby, lane, c0 > 0);
+    LFR_T(7);
     for (uint32_t c = c0; c < ncols; c++) {
         const int sbx = (int) c;
         const LFRec &rec = recs[T[4 + c - c0]];
@@ -1457,6 +1474,7 @@ __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfr(const uint32_t *__rest
         uint32_t pwv = 0;                       // this SB's program word, loaded with its interior
         if (!mover) {
             if (!PF && c > c0) lfr_issue<PIX, G, NT, NU>(v, P, sbx, sby, lane, false);
+            LFR_T(8);
             if (lane < L::PROG / 4) pwv = ((const uint32_t *) rec.prog)[lane];
             // left halo (x < 0): this workgroup's previous tile, read from LDS before the
             // barrier below (SB c0's came from HBM with its interior)
@@ -1472,8 +1490,10 @@ __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfr(const uint32_t *__rest
                     }
                 }
             }
+            LFR_T(9);
         }
         __syncthreads();                        // every lane has read the previous tile
+        LFR_T(0);
         // interior (and left halo) into LDS, then the column pass: it rewrites rows 0..63 only,
         // so it runs before the row above has handed over this SB's top halo. Usually the row
         // above is already far enough: then the top halo's loads are issued before the column
@@ -1506,12 +1526,14 @@ __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfr(const uint32_t *__rest
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         __syncthreads();
         const bool pre = s_pre;
+        LFR_T(1);
         if (!mover) {
             if (pre) lfr_top<PIX, G, NT, NU>(v, P, sbx, sby, lane);
             // the next SB's interior loads run under this SB's filtering
             if (PF && c + 1 < ncols) lfr_issue<PIX, G, NT, NU>(v, P, sbx + 1, sby, lane, false);
         }
         lf_passes<PIX, G, NT, 1>(S, lane, bd);  // the store wave has no lines: barriers only
+        LFR_T(2);
         // SB c - 1's bottom rows are final now (this SB's left-edge column filtering was the
         // last to touch them): the store wave writes its last XL columns of them sc1, drains
         // and stores the progress word, while the filtering waves go on. Those bytes are not
@@ -1543,8 +1565,10 @@ __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfr(const uint32_t *__rest
                     __builtin_amdgcn_s_sleep(1);
                 }
             }
+            if (c == c0) LFR_T(12); else LFR_T(10);
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");      // see the fence above
             __syncthreads();
+            LFR_T(11);
             if (!mover) lfr_top<PIX, G, NT, NU>(v, P, sbx, sby, lane);
         }
         if (!mover) {
@@ -1559,7 +1583,11 @@ __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfr(const uint32_t *__rest
             }
         }
         __syncthreads();
+        LFR_T(3);
         lf_passes<PIX, G, NT, 2>(S, lane, bd);
+        LFR_T(4);
+        if (LFR_PROF && !pre) pacc[5]++;
+        if (LFR_PROF) pacc[6]++;
         // store wave: rows [0, h) x cols [-XL, w) and rows [-8, 0) x cols [0, w), except the
         // bytes published above; the bottom rows sc1 (row r + 1 reads them). Its LDS reads
         // finish before the next SB's first barrier.
@@ -1589,8 +1617,277 @@ __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfr(const uint32_t *__rest
             }
         }
     }
+    if (LFR_PROF && lane == 0) {
+        pacc[7] = clock64() - tk0;
+        for (int i = 0; i < 14; i++) atomicAdd(&lfr_prof[i], pacc[i]);
+        atomicAdd(&lfr_prof[14], 1ull);
+    }
     // the last workgroup to finish resets the counters (every ticket is taken by then);
     // the store wave's last progress store has completed before this barrier
+    __syncthreads();
+    if (lane == 0) s_last = atomicAdd(&ctr[1], 1u) == (uint32_t) ntasks - 1;
+    __syncthreads();
+    if (s_last) {
+        for (int i = lane; i < ntasks; i += NT) progress[i] = 0;
+        if (lane == 0) { ctr[0] = 0; ctr[1] = 0; }
+    }
+}
+
+// k_lfrd: k_lfr with two LDS tiles (SB c in tile (c - c0) & 1). The store wave writes SB
+// c - 1's tile to HBM while the filtering waves run SB c's column pass, instead of between
+// SB c - 1's row pass and SB c's first barrier (where every lane of the workgroup waited
+// for its ~17 serialised LDS-read + store rounds); SB c + 1's interior loads and program
+// words are issued during SB c (after its top halo is in LDS, so waiting for the halo never
+// waits for them), and SB c's left halo is copied LDS to LDS from tile c - 1's last
+// chunk column. The last chunk column of tile c - 1 (rows >= 8) is not stored from tile
+// c - 1: tile c's left halo holds the same pixels after SB c's column pass (the final
+// ones) and is stored from there (bottom rows at the hand-off, the rest with tile c).
+// Hand-off, task table, spin bound and counter reset as k_lfr.
+template <typename PIX, class G> struct LfrLds {
+    typedef LfP<PIX, G> L;
+    PIX lt[2][72 * L::YP];
+    PIX ct[2][2][L::CR * L::UVP];
+    uint32_t prog[2][L::PROG / 4];
+    uint32_t lut[64];
+};
+
+// store wave: SB (sbx, sby)'s tile from LDS, except the bytes other steps store (the left
+// halo's bottom rows, published at the hand-off; its top-left corner, never modified;
+// unless `last`, the last chunk column's rows >= 8, stored from the next tile's left halo)
+template <typename PIX, class G>
+DEV void lfrd_store(const LfrLds<PIX, G> &S, int tb, const LfrPlanes &P, int sbx, int sby, int ml, bool last)
+{
+    typedef LfP<PIX, G> L;
+    typedef Chunk16::T CT;
+    constexpr int FLP = L::YP, FCP = L::UVP, NUM = (L::NCHUNK + 63) / 64;
+#pragma unroll
+    for (int u = 0; u < NUM; u++) {
+        const int ci = ml + u * 64;
+        int p, r, k;
+        lf_chunk<PIX, G>(ci, p, r, k);
+        const int rows = p ? L::CR : 72, kl = (p ? L::CK : L::YK) - 1;
+        if (ci >= L::NCHUNK || (k == 0 && (sbx == 0 || r < 8 || r >= rows - 8)) || (r < 8 && sby == 0) ||
+            (!last && k == kl && r >= 8))
+            continue;
+        const PIX *t = p ? S.ct[tb][p - 1] + r * FCP : S.lt[tb] + r * FLP;
+        const CT w = Chunk16::from_lds(t + L::CPX * k);
+        PIX *g = lfr_addr<PIX, G>(P, sbx, sby, p, r, k);
+        if (r >= rows - 8) {
+            st_sc1(g, (uint64_t) w.x | (uint64_t) w.y << 32);
+            st_sc1((char *) g + 8, (uint64_t) w.z | (uint64_t) w.w << 32);
+        } else {
+            v4u x; x.x = w.x; x.y = w.y; x.z = w.z; x.w = w.w;
+            *(gv4u *) g = x;
+        }
+    }
+}
+
+// k_lfrd's chunk sets: the top halo (tile rows 0..7 of every plane) and the rest (rows
+// 8..), each enumerated on its own so their registers never alias (a load into a register
+// another outstanding load also writes would wait for it)
+template <typename PIX, class G> DEV void lfrd_chunk(int ci, bool top, int &p, int &r, int &k)
+{
+    typedef LfP<PIX, G> L;
+    const int ry = top ? 8 : 64, rc = top ? 8 : G::CH, r0 = top ? 0 : 8;
+    if (ci < ry * L::YK) { p = 0; r = ci / L::YK; k = ci - r * L::YK; }
+    else { const int c = ci - ry * L::YK; p = 1 + (c >= rc * L::CK); const int cc = c - (p - 1) * rc * L::CK; r = cc / L::CK; k = cc - r * L::CK; }
+    r += r0;
+}
+template <typename PIX, class G> struct LfrdN {
+    typedef LfP<PIX, G> L;
+    static constexpr int NTOP = 8 * (L::YK + 2 * L::CK), NINT = L::NCHUNK - NTOP;
+    static constexpr int NUT = (NTOP + LfNT<G>::NT - 1) / LfNT<G>::NT, NUI = (NINT + LfNT<G>::NT - 1) / LfNT<G>::NT;
+};
+// interior loads of SB (sbx, sby) (left halo from HBM only when `halo`)
+template <typename PIX, class G, int NUI>
+DEV void lfrd_issue(Chunk16::T (&v)[NUI], const LfrPlanes &P, int sbx, int sby, int lane, bool halo)
+{
+    typedef LfrdN<PIX, G> N;
+    static_assert(NUI == N::NUI, "interior chunk registers");
+#pragma unroll
+    for (int u = 0; u < NUI; u++) {
+        const int ci = lane + u * LfNT<G>::NT;
+        int p, r, k;
+        lfrd_chunk<PIX, G>(ci, false, p, r, k);
+        if (ci < N::NINT && (k > 0 || halo)) {
+            const v4u x = *(const gv4u *) lfr_addr<PIX, G>(P, sbx, sby, p, r, k);
+            v[u] = make_uint4(x.x, x.y, x.z, x.w);
+        }
+    }
+}
+// top halo (rows handed off by the row above, sc1 loads)
+template <typename PIX, class G, int NUT>
+DEV void lfrd_top(Chunk16::T (&v)[NUT], const LfrPlanes &P, int sbx, int sby, int lane)
+{
+    typedef LfrdN<PIX, G> N;
+    static_assert(NUT == N::NUT, "top-halo chunk registers");
+#pragma unroll
+    for (int u = 0; u < NUT; u++) {
+        const int ci = lane + u * LfNT<G>::NT;
+        int p, r, k;
+        lfrd_chunk<PIX, G>(ci, true, p, r, k);
+        if (ci >= N::NTOP || k == 0 || sby == 0) continue;
+        const PIX *g = lfr_addr<PIX, G>(P, sbx, sby, p, r, k);
+        const uint64_t lo = ld_sc1(g), hi = ld_sc1((const char *) g + 8);
+        v[u] = make_uint4((uint32_t) lo, (uint32_t) (lo >> 32), (uint32_t) hi, (uint32_t) (hi >> 32));
+    }
+}
+
+template <typename PIX, class G>
+__global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfrd(const uint32_t *__restrict__ tasks, const LFRec *__restrict__ recs,
+                                                      const FrameDesc *__restrict__ frames, uint32_t *ctr, int ntasks)
+{
+    constexpr int NT = LfNT<G>::NT;
+    typedef LfP<PIX, G> L;
+    typedef Chunk16::T CT;
+    constexpr int FLP = L::YP, FCP = L::UVP, CW = G::CW, CPX = L::CPX;
+    typedef LfrdN<PIX, G> N;
+    constexpr int NUM = (L::NCHUNK + 63) / 64;
+    __shared__ LfrLds<PIX, G> S;
+    __shared__ uint32_t s_task, s_last, s_pre;
+    const int lane = threadIdx.x;
+    uint32_t *const progress = ctr + 4;
+    __builtin_amdgcn_s_setprio(3);
+    uint64_t pacc[14] = {0}, tp = LFR_PROF ? clock64() : 0;
+    const uint64_t tk0 = tp;
+    if (lane == 0) s_task = atomicAdd(&ctr[0], 1u);
+    __syncthreads();
+    const uint32_t *T = tasks + tasks[s_task];
+    const uint32_t dep = T[0], ncols = T[1], c0 = T[2];
+    uint32_t seen = T[3];
+    const uint32_t spin = ctr[3] ? ctr[3] : (1u << 22);
+    const LFRec &rec0 = recs[T[4]];
+    const FrameDesc &fd = frames[rec0.frame];
+    const int bd = fd.bd, sby = rec0.sby;
+    LfrPlanes P;
+    P.b0 = fd.plane[0]; P.d1 = fd.plane[1] - P.b0; P.d2 = fd.plane[2] - P.b0;
+    P.pit0 = fd.pitch[0]; P.pit1 = fd.pitch[1];
+    for (int i = lane; i < 64; i += NT) S.lut[i] = lf_eih(i, fd.sharp, bd);
+    static_assert(L::PROG / 4 <= NT, "one program word per filtering lane");
+    CT vi[N::NUI], vt[N::NUT];
+#pragma unroll
+    for (int u = 0; u < N::NUI; u++) vi[u] = Chunk16::zero();
+#pragma unroll
+    for (int u = 0; u < N::NUT; u++) vt[u] = Chunk16::zero();
+    const bool mover = lane >= NT;
+    const int ml = lane - NT;
+    uint32_t pwv = 0;                           // the next SB's program word
+    if (!mover) {
+        lfrd_issue<PIX, G>(vi, P, c0, sby, lane, c0 > 0);
+        if (lane < L::PROG / 4) pwv = ((const uint32_t *) rec0.prog)[lane];
+    }
+    LFR_T(7);
+    for (uint32_t c = c0; c < ncols; c++) {
+        const int sbx = (int) c, tb = (int) ((c - c0) & 1);
+        PIX *lt = S.lt[tb];
+        PIX (*ct)[L::CR * FCP] = S.ct[tb];
+        // interior (loaded during the previous SB) and left halo into this SB's tile
+        if (!mover) {
+            if (lane < L::PROG / 4) S.prog[tb][lane] = pwv;
+#pragma unroll
+            for (int u = 0; u < N::NUI; u++) {
+                const int ci = lane + u * NT;
+                int p, r, k;
+                lfrd_chunk<PIX, G>(ci, false, p, r, k);
+                if (ci < N::NINT) {
+                    PIX *t = (p ? ct[p - 1] + r * FCP : lt + r * FLP) + CPX * k;
+                    if (k == 0 && c > c0) {
+                        const PIX *src = (p ? S.ct[tb ^ 1][p - 1] + r * FCP : S.lt[tb ^ 1] + r * FLP) + (p ? CW : 64);
+                        Chunk16::to_lds(Chunk16::from_lds(src), t);
+                    } else {
+                        Chunk16::to_lds(vi[u], t);
+                    }
+                }
+            }
+            if (lane == 0) {
+                if (dep != ~0u && seen < c + 1)
+                    seen = __hip_atomic_load((gu32 *) &progress[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                s_pre = dep == ~0u || seen >= c + 1;
+            }
+        }
+        LFR_T(8);
+        // k_lfr's hand-off ordering; wavefront-scope fence: see k_lfr
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        __syncthreads();
+        LFR_T(0);
+        const bool pre = s_pre;
+        if (!mover) {
+            if (pre) lfrd_top<PIX, G>(vt, P, sbx, sby, lane);
+        } else if (c > c0) {
+            lfrd_store<PIX, G>(S, tb ^ 1, P, sbx - 1, sby, ml, false);     // SB c - 1, under the column pass
+        }
+        LFR_T(9);
+        lf_passes_v<PIX, G, NT, 1>(lt, ct, S.prog[tb], S.lut, lane, bd);
+        LFR_T(2);
+        // SB c - 1's last columns are final: publish its bottom rows (k_lfr's hand-off)
+        if (mover && sbx > 0) {
+#pragma unroll
+            for (int u = 0; u < NUM; u++) {
+                const int ci = ml + u * 64;
+                int p, r, k;
+                lf_chunk<PIX, G>(ci, p, r, k);
+                if (ci >= L::NCHUNK || r < (p ? L::CR : 72) - 8 || k != 0) continue;
+                const PIX *t = p ? ct[p - 1] + r * FCP : lt + r * FLP;
+                PIX *g = lfr_addr<PIX, G>(P, sbx, sby, p, r, k);
+                const CT w = Chunk16::from_lds(t);
+                st_sc1(g, (uint64_t) w.x | (uint64_t) w.y << 32);
+                st_sc1((char *) g + 8, (uint64_t) w.z | (uint64_t) w.w << 32);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (ml == 0) __hip_atomic_store((gu32 *) &progress[s_task], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (!pre) {
+            if (lane == 0 && dep != ~0u) {
+                const uint32_t need = c + 1;
+                for (uint32_t n = 0; seen < need; n++) {
+                    seen = __hip_atomic_load((gu32 *) &progress[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (seen >= need) break;
+                    if (n > spin) { atomicAdd(&ctr[2], 1u); seen = need; break; }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+            if (c == c0) LFR_T(12); else LFR_T(10);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            __syncthreads();
+            LFR_T(11);
+            if (!mover) lfrd_top<PIX, G>(vt, P, sbx, sby, lane);
+        }
+        if (!mover) {
+#pragma unroll
+            for (int u = 0; u < N::NUT; u++) {
+                const int ci = lane + u * NT;
+                int p, r, k;
+                lfrd_chunk<PIX, G>(ci, true, p, r, k);
+                if (ci >= N::NTOP || k == 0) continue;
+                PIX *t = p ? ct[p - 1] + r * FCP : lt + r * FLP;
+                Chunk16::to_lds(vt[u], t + CPX * k);
+            }
+            // the next SB's interior and program word, in flight under the row pass (issued
+            // after the top halo's LDS writes: their waits never cover these loads)
+            if (c + 1 < ncols) {
+                lfrd_issue<PIX, G>(vi, P, sbx + 1, sby, lane, false);
+                if (lane < L::PROG / 4) pwv = ((const uint32_t *) recs[T[4 + c + 1 - c0]].prog)[lane];
+            }
+        }
+        __syncthreads();
+        LFR_T(3);
+        lf_passes_v<PIX, G, NT, 2>(lt, ct, S.prog[tb], S.lut, lane, bd);
+        LFR_T(4);
+        if (LFR_PROF && !pre) pacc[5]++;
+        if (LFR_PROF) pacc[6]++;
+    }
+    // the row's last SB: its whole tile, then its bottom rows are final
+    if (mover) {
+        lfrd_store<PIX, G>(S, (int) ((ncols - 1 - c0) & 1), P, (int) ncols - 1, sby, ml, true);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (ml == 0) __hip_atomic_store((gu32 *) &progress[s_task], ncols, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    if (LFR_PROF && lane == 0) {
+        pacc[7] = clock64() - tk0;
+        for (int i = 0; i < 14; i++) atomicAdd(&lfr_prof[i], pacc[i]);
+        atomicAdd(&lfr_prof[14], 1ull);
+    }
     __syncthreads();
     if (lane == 0) s_last = atomicAdd(&ctr[1], 1u) == (uint32_t) ntasks - 1;
     __syncthreads();
@@ -1846,8 +2143,9 @@ static void launch_lf_g(hipStream_t st, int nsb, const uint32_t *list, const LFR
 template <typename PIX, class G>
 static void launch_lfr_g(hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs, const FrameDesc *frames, uint32_t *ctr)
 {
-    static const bool pf = getenv("VP9HIP_LFR_PF") && atoi(getenv("VP9HIP_LFR_PF"));
-    if (pf) hipLaunchKernelGGL((k_lfr<PIX, G, true>), dim3(ntasks), dim3(LfNT<G>::NT + 64), 0, st, tasks, recs, frames, ctr, ntasks);
+    // VP9HIP_LFR_DB=0: the single-tile k_lfr (A/B switch)
+    static const bool db = !getenv("VP9HIP_LFR_DB") || atoi(getenv("VP9HIP_LFR_DB"));
+    if (db) hipLaunchKernelGGL((k_lfrd<PIX, G>), dim3(ntasks), dim3(LfNT<G>::NT + 64), 0, st, tasks, recs, frames, ctr, ntasks);
     else    hipLaunchKernelGGL((k_lfr<PIX, G, false>), dim3(ntasks), dim3(LfNT<G>::NT + 64), 0, st, tasks, recs, frames, ctr, ntasks);
 }
 template <typename PIX>
@@ -1899,6 +2197,13 @@ static void launch_plf_p(int ss, hipStream_t st, const PlfLaunch &pl, const uint
     }
 }
 extern "C" {
+// LFR_PROF builds: read and clear the k_lfr phase sums (profiling only, not in the ABI)
+int vp9hip_lfr_prof_read(unsigned long long *out)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lfr_prof), 16 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    static const unsigned long long z[16] = {0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(lfr_prof), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
 int vp9hip_launch_resid(int hb, hipStream_t st, int tcode, int n, const RJob *jobs, const FrameDesc *frames,
                         const void *coefs, int16_t *resid)
 {
