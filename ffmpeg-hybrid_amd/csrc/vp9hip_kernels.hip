@@ -1150,6 +1150,52 @@ DEV void lf_line_row_narrow(uint32_t *rowp, const uint32_t *pw, const uint32_t *
     LF_EDGE_NARROW(4) LF_EDGE_NARROW(5) LF_EDGE_NARROW(6) LF_EDGE_NARROW(7)
     lf_pack<PIX>(rowp, px, 0, 40 / PPW, 0);
 }
+// k_lfrd's column pass in two parts around a barrier: part 1 filters a row's first edge
+// (x = 0, the only one that reaches x < 0: later edges modify x >= 1) and writes
+// x = -8..-1 back, so the previous SB's last columns are final in LDS after it; part 2
+// runs the row's other edges on the same registers.
+template <typename PIX>
+DEV void lf_row_wide_1(uint32_t *rowp, const uint32_t *pw, const uint32_t *lut, int bd, int (&px)[40])
+{
+    constexpr int PPW = 4 / sizeof(PIX);
+    lf_unpack<PIX>(rowp, px, 0, 40 / PPW, 0);
+    const uint32_t m = pw[0] & 255;
+    if (m >> 6) lf_reg<8>(px, m >> 6, lut[m & 63], bd);
+    lf_pack<PIX>(rowp, px, 0, 8 / PPW, 0);
+}
+template <typename PIX>
+DEV void lf_row_wide_2(uint32_t *rowp, const uint32_t *pw, const uint32_t *lut, int bd, int (&px)[40])
+{
+    constexpr int PPW = 4 / sizeof(PIX);
+    const uint32_t pw0 = pw[0], pw1 = pw[1], pw2 = pw[2], pw3 = pw[3];
+    const uint32_t in0 = (pw0 >> 8) & 255;
+    if (in0) lf_reg<12>(px, 1, lut[in0 & 63], bd);
+    LF_EDGE_WIDE(1, 0) LF_EDGE_WIDE(2, 0) LF_EDGE_WIDE(3, 0)
+    lf_pack<PIX>(rowp, px, 8 / PPW, 32 / PPW, 8);
+#pragma unroll
+    for (int i = 0; i < 8; i++) px[i] = px[32 + i];
+    lf_unpack<PIX>(rowp, px, 40 / PPW, 72 / PPW, 8);
+    LF_EDGE_WIDE(4, 32) LF_EDGE_WIDE(5, 32) LF_EDGE_WIDE(6, 32) LF_EDGE_WIDE(7, 32)
+    lf_pack<PIX>(rowp, px, 32 / PPW, 72 / PPW, 0);
+}
+template <typename PIX>
+DEV void lf_row_narrow_1(uint32_t *rowp, const uint32_t *pw, const uint32_t *lut, int bd, int (&px)[40])
+{
+    constexpr int PPW = 4 / sizeof(PIX);
+    lf_unpack<PIX>(rowp, px, 0, 40 / PPW, 0);
+    const uint32_t m = pw[0] & 255;
+    if (m >> 6) lf_reg<8>(px, m >> 6, lut[m & 63], bd);
+    lf_pack<PIX>(rowp, px, 0, 8 / PPW, 0);
+}
+template <typename PIX>
+DEV void lf_row_narrow_2(uint32_t *rowp, const uint32_t *pw, const uint32_t *lut, int bd, int (&px)[40])
+{
+    constexpr int PPW = 4 / sizeof(PIX);
+    const uint32_t pc0 = pw[0], pc1 = pw[1];
+    LF_EDGE_NARROW(1) LF_EDGE_NARROW(2) LF_EDGE_NARROW(3)
+    LF_EDGE_NARROW(4) LF_EDGE_NARROW(5) LF_EDGE_NARROW(6) LF_EDGE_NARROW(7)
+    lf_pack<PIX>(rowp, px, 8 / PPW, 40 / PPW, 8);
+}
 // row edges of one pixel column (tile pitch P)
 template <typename PIX, int P>
 DEV void lf_line_col_wide(PIX *colp, const uint32_t *pw, const uint32_t *lut, int bd)
@@ -1643,6 +1689,17 @@ __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfr(const uint32_t *__rest
 // c - 1: tile c's left halo holds the same pixels after SB c's column pass (the final
 // ones) and is stored from there (bottom rows at the hand-off, the rest with tile c).
 // Hand-off, task table, spin bound and counter reset as k_lfr.
+template <typename PIX, class G> DEV void lfrd_chunk_rows(int ci, int ry0, int nry, int rc0, int nrc, int &p, int &r, int &k)
+{
+    typedef LfP<PIX, G> L;
+    if (ci < nry * L::YK) { p = 0; r = ci / L::YK; k = ci - r * L::YK; r += ry0; }
+    else { const int c = ci - nry * L::YK; p = 1 + (c >= nrc * L::CK); const int cc = c - (p - 1) * nrc * L::CK; r = cc / L::CK; k = cc - r * L::CK; r += rc0; }
+}
+template <typename PIX, class G> DEV void lfrd_chunk(int ci, bool top, int &p, int &r, int &k)
+{
+    if (top) lfrd_chunk_rows<PIX, G>(ci, 0, 8, 0, 8, p, r, k);
+    else lfrd_chunk_rows<PIX, G>(ci, 8, 64, 8, G::CH, p, r, k);
+}
 template <typename PIX, class G> struct LfrLds {
     typedef LfP<PIX, G> L;
     PIX lt[2][72 * L::YP];
@@ -1653,46 +1710,44 @@ template <typename PIX, class G> struct LfrLds {
 
 // store wave: SB (sbx, sby)'s tile from LDS, except the bytes other steps store (the left
 // halo's bottom rows, published at the hand-off; its top-left corner, never modified;
-// unless `last`, the last chunk column's rows >= 8, stored from the next tile's left halo)
+// unless `last`, the last chunk column's rows >= 8, stored from the next tile's left halo).
+// part 0: the bottom 8 rows only (sc1: the row below reads them), 1: the other rows, 2: all.
 template <typename PIX, class G>
-DEV void lfrd_store(const LfrLds<PIX, G> &S, int tb, const LfrPlanes &P, int sbx, int sby, int ml, bool last)
+DEV void lfrd_store(const LfrLds<PIX, G> &S, int tb, const LfrPlanes &P, int sbx, int sby, int ml, bool last, int part)
 {
     typedef LfP<PIX, G> L;
     typedef Chunk16::T CT;
-    constexpr int FLP = L::YP, FCP = L::UVP, NUM = (L::NCHUNK + 63) / 64;
+    constexpr int FLP = L::YP, FCP = L::UVP;
+    // part 0 enumerates the bottom rows (luma 64..71, chroma CR - 8..), part 1 the others,
+    // part 2 both in turn
 #pragma unroll
-    for (int u = 0; u < NUM; u++) {
-        const int ci = ml + u * 64;
-        int p, r, k;
-        lf_chunk<PIX, G>(ci, p, r, k);
-        const int rows = p ? L::CR : 72, kl = (p ? L::CK : L::YK) - 1;
-        if (ci >= L::NCHUNK || (k == 0 && (sbx == 0 || r < 8 || r >= rows - 8)) || (r < 8 && sby == 0) ||
-            (!last && k == kl && r >= 8))
-            continue;
-        const PIX *t = p ? S.ct[tb][p - 1] + r * FCP : S.lt[tb] + r * FLP;
-        const CT w = Chunk16::from_lds(t + L::CPX * k);
-        PIX *g = lfr_addr<PIX, G>(P, sbx, sby, p, r, k);
-        if (r >= rows - 8) {
-            st_sc1(g, (uint64_t) w.x | (uint64_t) w.y << 32);
-            st_sc1((char *) g + 8, (uint64_t) w.z | (uint64_t) w.w << 32);
-        } else {
-            v4u x; x.x = w.x; x.y = w.y; x.z = w.z; x.w = w.w;
-            *(gv4u *) g = x;
+    for (int q = 0; q < 2; q++) {
+        if ((part == 0 && q == 1) || (part == 1 && q == 0)) continue;
+        const int ry0 = q ? 0 : 64, nry = q ? 64 : 8, rc0 = q ? 0 : L::CR - 8, nrc = q ? L::CR - 8 : 8;
+        const int n = nry * L::YK + 2 * nrc * L::CK;
+        const int nu = q ? (64 * L::YK + 2 * (L::CR - 8) * L::CK + 63) / 64 : (8 * (L::YK + 2 * L::CK) + 63) / 64;
+#pragma unroll 4
+        for (int u = 0; u < nu; u++) {
+            const int ci = ml + u * 64;
+            if (ci >= n) break;
+            int p, r, k;
+            lfrd_chunk_rows<PIX, G>(ci, ry0, nry, rc0, nrc, p, r, k);
+            const int kl = (p ? L::CK : L::YK) - 1;
+            if ((k == 0 && (sbx == 0 || r < 8 || !q)) || (r < 8 && sby == 0) || (!last && k == kl && r >= 8)) continue;
+            const PIX *t = p ? S.ct[tb][p - 1] + r * FCP : S.lt[tb] + r * FLP;
+            const CT w = Chunk16::from_lds(t + L::CPX * k);
+            PIX *g = lfr_addr<PIX, G>(P, sbx, sby, p, r, k);
+            if (!q) {
+                st_sc1(g, (uint64_t) w.x | (uint64_t) w.y << 32);
+                st_sc1((char *) g + 8, (uint64_t) w.z | (uint64_t) w.w << 32);
+            } else {
+                v4u x; x.x = w.x; x.y = w.y; x.z = w.z; x.w = w.w;
+                *(gv4u *) g = x;
+            }
         }
     }
 }
 
-// k_lfrd's chunk sets: the top halo (tile rows 0..7 of every plane) and the rest (rows
-// 8..), each enumerated on its own so their registers never alias (a load into a register
-// another outstanding load also writes would wait for it)
-template <typename PIX, class G> DEV void lfrd_chunk(int ci, bool top, int &p, int &r, int &k)
-{
-    typedef LfP<PIX, G> L;
-    const int ry = top ? 8 : 64, rc = top ? 8 : G::CH, r0 = top ? 0 : 8;
-    if (ci < ry * L::YK) { p = 0; r = ci / L::YK; k = ci - r * L::YK; }
-    else { const int c = ci - ry * L::YK; p = 1 + (c >= rc * L::CK); const int cc = c - (p - 1) * rc * L::CK; r = cc / L::CK; k = cc - r * L::CK; }
-    r += r0;
-}
 template <typename PIX, class G> struct LfrdN {
     typedef LfP<PIX, G> L;
     static constexpr int NTOP = 8 * (L::YK + 2 * L::CK), NINT = L::NCHUNK - NTOP;
@@ -1783,6 +1838,12 @@ __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfrd(const uint32_t *__res
         PIX (*ct)[L::CR * FCP] = S.ct[tb];
         // interior (loaded during the previous SB) and left halo into this SB's tile
         if (!mover) {
+            // the progress probe first: its round trip runs under the tile writes
+            if (lane == 0) {
+                if (dep != ~0u && seen < c + 1)
+                    seen = __hip_atomic_load((gu32 *) &progress[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                s_pre = dep == ~0u || seen >= c + 1;
+            }
             if (lane < L::PROG / 4) S.prog[tb][lane] = pwv;
 #pragma unroll
             for (int u = 0; u < N::NUI; u++) {
@@ -1799,11 +1860,6 @@ __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfrd(const uint32_t *__res
                     }
                 }
             }
-            if (lane == 0) {
-                if (dep != ~0u && seen < c + 1)
-                    seen = __hip_atomic_load((gu32 *) &progress[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                s_pre = dep == ~0u || seen >= c + 1;
-            }
         }
         LFR_T(8);
         // k_lfr's hand-off ordering; wavefront-scope fence: see k_lfr
@@ -1814,21 +1870,37 @@ __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfrd(const uint32_t *__res
         if (!mover) {
             if (pre) lfrd_top<PIX, G>(vt, P, sbx, sby, lane);
         } else if (c > c0) {
-            lfrd_store<PIX, G>(S, tb ^ 1, P, sbx - 1, sby, ml, false);     // SB c - 1, under the column pass
+            lfrd_store<PIX, G>(S, tb ^ 1, P, sbx - 1, sby, ml, false, 0);  // SB c - 1's bottom rows first
         }
         LFR_T(9);
-        lf_passes_v<PIX, G, NT, 1>(lt, ct, S.prog[tb], S.lut, lane, bd);
-        LFR_T(2);
-        // SB c - 1's last columns are final: publish its bottom rows (k_lfr's hand-off)
+        // column pass part 1: every row's edge x = 0 (one row per lane)
+        static_assert(64 + 2 * G::CH <= NT, "one column-pass row per filtering lane");
+        int lpx[40];
+        const bool cl = !mover && lane < 64 + 2 * G::CH, cwide = lane < 64 || !G::SH;
+        uint32_t *rowp = nullptr;
+        const uint32_t *pwl = nullptr;
+        if (cl) {
+            if (lane < 64) {
+                rowp = (uint32_t *) (lt + (lane + 8) * FLP + L::XO);
+                pwl = S.prog[tb] + (LFP_YC + (lane >> 3) * 16) / 4;
+            } else {
+                const int p = 1 + (lane - 64 >= G::CH), r = lane - 64 - (p - 1) * G::CH;
+                rowp = (uint32_t *) (ct[p - 1] + (r + 8) * FCP + L::XO);
+                pwl = S.prog[tb] + (LFP_CC + (r >> 3) * LFP_CSTRIDE(G::SH)) / 4;
+            }
+            if (cwide) lf_row_wide_1<PIX>(rowp, pwl, S.lut, bd, lpx);
+            else lf_row_narrow_1<PIX>(rowp, pwl, S.lut, bd, lpx);
+        }
+        __syncthreads();
+        LFR_T(13);
+        // SB c - 1's last columns are final: publish its bottom rows (k_lfr's hand-off) while
+        // the filtering waves run the rest of the column pass
         if (mover && sbx > 0) {
-#pragma unroll
-            for (int u = 0; u < NUM; u++) {
-                const int ci = ml + u * 64;
-                int p, r, k;
-                lf_chunk<PIX, G>(ci, p, r, k);
-                if (ci >= L::NCHUNK || r < (p ? L::CR : 72) - 8 || k != 0) continue;
+            // the left halo's bottom 8 rows of each plane: one chunk per lane 0..23
+            if (ml < 24) {
+                const int p = ml >> 3, r = (p ? L::CR : 72) - 8 + (ml & 7);
                 const PIX *t = p ? ct[p - 1] + r * FCP : lt + r * FLP;
-                PIX *g = lfr_addr<PIX, G>(P, sbx, sby, p, r, k);
+                PIX *g = lfr_addr<PIX, G>(P, sbx, sby, p, r, 0);
                 const CT w = Chunk16::from_lds(t);
                 st_sc1(g, (uint64_t) w.x | (uint64_t) w.y << 32);
                 st_sc1((char *) g + 8, (uint64_t) w.z | (uint64_t) w.w << 32);
@@ -1836,6 +1908,14 @@ __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfrd(const uint32_t *__res
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (ml == 0) __hip_atomic_store((gu32 *) &progress[s_task], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        if (mover && c > c0) lfrd_store<PIX, G>(S, tb ^ 1, P, sbx - 1, sby, ml, false, 1);   // the rest of SB c - 1
+        // column pass part 2
+        if (cl) {
+            if (cwide) lf_row_wide_2<PIX>(rowp, pwl, S.lut, bd, lpx);
+            else lf_row_narrow_2<PIX>(rowp, pwl, S.lut, bd, lpx);
+        }
+        __syncthreads();
+        LFR_T(2);
         if (!pre) {
             if (lane == 0 && dep != ~0u) {
                 const uint32_t need = c + 1;
@@ -1878,7 +1958,7 @@ __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfrd(const uint32_t *__res
     }
     // the row's last SB: its whole tile, then its bottom rows are final
     if (mover) {
-        lfrd_store<PIX, G>(S, (int) ((ncols - 1 - c0) & 1), P, (int) ncols - 1, sby, ml, true);
+        lfrd_store<PIX, G>(S, (int) ((ncols - 1 - c0) & 1), P, (int) ncols - 1, sby, ml, true, 2);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (ml == 0) __hip_atomic_store((gu32 *) &progress[s_task], ncols, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

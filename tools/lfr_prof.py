@@ -14,7 +14,8 @@ assert L.vp9hip_lfr_prof_read(out) == 0
 v = list(out)
 nsb, nwg = max(v[6], 1), max(v[14], 1)
 names = {8: "interior + left halo into the tile, progress probe", 0: "barrier A",
-         9: "top-halo loads issued (store wave: previous tile stored)", 2: "column pass (+ barrier)",
+         9: "top-halo loads issued (store wave: previous tile stored)", 13: "column pass part 1 (edge x = 0) + barrier",
+         2: "column pass part 2 (+ barrier)",
          12: "blocking wait for the row above, first SB (pipeline fill)",
          10: "blocking wait for the row above, later SBs", 11: "barrier after the wait",
          3: "top halo into the tile, next interior issued, barrier", 4: "row pass (+ barrier)"}

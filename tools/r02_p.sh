@@ -15,5 +15,5 @@ line gpurun_out/r02p_C3.json C3
 cp ffmpeg-hybrid_amd/prof/libvp9hip.so ffmpeg-hybrid_amd/libvp9hip.so
 for c in C5 C2; do
   timeout -k 10 300 python tools/lfr_prof.py --config $c --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/lfrprof2_$c.json 2> gpurun_out/lfrprof2_$c.err
-  echo $c; tail -14 gpurun_out/lfrprof2_$c.err
+  echo $c; tail -15 gpurun_out/lfrprof2_$c.err
 done
