@@ -1712,39 +1712,44 @@ template <typename PIX, class G> struct LfrLds {
 // halo's bottom rows, published at the hand-off; its top-left corner, never modified;
 // unless `last`, the last chunk column's rows >= 8, stored from the next tile's left halo).
 // part 0: the bottom 8 rows only (sc1: the row below reads them), 1: the other rows, 2: all.
+// one plane's tile rows [ra, rb) (NK chunks per row, tile pitch TP), chunk-parallel over
+// the 64 store lanes; g0 = the plane at the tile's origin (x = -XL, y = -8)
+template <typename PIX, int NK, int TP>
+DEV void lfrd_store_rows(const PIX *tile, PIX *g0, int pitch, int ra, int rb, int ml, int sbx, int sby, bool last, bool bot)
+{
+    typedef Chunk16::T CT;
+    constexpr int CPX = 16 / sizeof(PIX);
+    const int n = (rb - ra) * NK;
+    for (int ci = ml; ci < n; ci += 64) {
+        const int rr = ci / NK, k = ci - rr * NK, r = ra + rr;
+        if ((k == 0 && (sbx == 0 || r < 8 || bot)) || (r < 8 && sby == 0) || (!last && k == NK - 1 && r >= 8)) continue;
+        const CT w = Chunk16::from_lds(tile + r * TP + CPX * k);
+        PIX *g = g0 + (ptrdiff_t) r * pitch + CPX * k;
+        if (bot) {
+            st_sc1(g, (uint64_t) w.x | (uint64_t) w.y << 32);
+            st_sc1((char *) g + 8, (uint64_t) w.z | (uint64_t) w.w << 32);
+        } else {
+            v4u x; x.x = w.x; x.y = w.y; x.z = w.z; x.w = w.w;
+            *(gv4u *) g = x;
+        }
+    }
+}
 template <typename PIX, class G>
 DEV void lfrd_store(const LfrLds<PIX, G> &S, int tb, const LfrPlanes &P, int sbx, int sby, int ml, bool last, int part)
 {
     typedef LfP<PIX, G> L;
-    typedef Chunk16::T CT;
-    constexpr int FLP = L::YP, FCP = L::UVP;
-    // part 0 enumerates the bottom rows (luma 64..71, chroma CR - 8..), part 1 the others,
-    // part 2 both in turn
+    // part 0: the bottom 8 rows of each plane (sc1: the row below reads them), 1: the other
+    // rows, 2: both
+    PIX *g0 = lfr_addr<PIX, G>(P, sbx, sby, 0, 0, 0), *g1 = lfr_addr<PIX, G>(P, sbx, sby, 1, 0, 0),
+        *g2 = lfr_addr<PIX, G>(P, sbx, sby, 2, 0, 0);
 #pragma unroll
     for (int q = 0; q < 2; q++) {
         if ((part == 0 && q == 1) || (part == 1 && q == 0)) continue;
-        const int ry0 = q ? 0 : 64, nry = q ? 64 : 8, rc0 = q ? 0 : L::CR - 8, nrc = q ? L::CR - 8 : 8;
-        const int n = nry * L::YK + 2 * nrc * L::CK;
-        const int nu = q ? (64 * L::YK + 2 * (L::CR - 8) * L::CK + 63) / 64 : (8 * (L::YK + 2 * L::CK) + 63) / 64;
-#pragma unroll 4
-        for (int u = 0; u < nu; u++) {
-            const int ci = ml + u * 64;
-            if (ci >= n) break;
-            int p, r, k;
-            lfrd_chunk_rows<PIX, G>(ci, ry0, nry, rc0, nrc, p, r, k);
-            const int kl = (p ? L::CK : L::YK) - 1;
-            if ((k == 0 && (sbx == 0 || r < 8 || !q)) || (r < 8 && sby == 0) || (!last && k == kl && r >= 8)) continue;
-            const PIX *t = p ? S.ct[tb][p - 1] + r * FCP : S.lt[tb] + r * FLP;
-            const CT w = Chunk16::from_lds(t + L::CPX * k);
-            PIX *g = lfr_addr<PIX, G>(P, sbx, sby, p, r, k);
-            if (!q) {
-                st_sc1(g, (uint64_t) w.x | (uint64_t) w.y << 32);
-                st_sc1((char *) g + 8, (uint64_t) w.z | (uint64_t) w.w << 32);
-            } else {
-                v4u x; x.x = w.x; x.y = w.y; x.z = w.z; x.w = w.w;
-                *(gv4u *) g = x;
-            }
-        }
+        const bool bot = !q;
+        const int ya = bot ? 64 : 0, yb = bot ? 72 : 64, ca = bot ? L::CR - 8 : 0, cb = bot ? L::CR : L::CR - 8;
+        lfrd_store_rows<PIX, L::YK, L::YP>(S.lt[tb], g0, P.pit0, ya, yb, ml, sbx, sby, last, bot);
+        lfrd_store_rows<PIX, L::CK, L::UVP>(S.ct[tb][0], g1, P.pit1, ca, cb, ml, sbx, sby, last, bot);
+        lfrd_store_rows<PIX, L::CK, L::UVP>(S.ct[tb][1], g2, P.pit1, ca, cb, ml, sbx, sby, last, bot);
     }
 }
 
