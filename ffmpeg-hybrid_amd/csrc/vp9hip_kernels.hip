@@ -2089,10 +2089,11 @@ DEV int mc_sample(const PIX *r, int pitch, int w, int h, int X, int Y, int mx, i
 #ifndef MC_LDS_MIN
 #define MC_LDS_MIN 1024               // units of at least this many pixels use the LDS passes
 #endif
-template <typename PIX>
-__global__ __launch_bounds__(256) void k_mc(const McUnit *__restrict__ units, int nunits,
+template <typename PIX, int NTH>
+__global__ __launch_bounds__(NTH) void k_mc(const McUnit *__restrict__ units, int nunits,
                                             const FrameDesc *__restrict__ frames)
 {
+    static_assert(NTH == 256 || (NTH == 64 && sizeof(PIX) == 2), "the LDS passes assume 256 threads");
     __shared__ PIX win[71 * MC_WP];
     __shared__ int16_t tmp[71 * 64];
     const McUnit u = units[blockIdx.x];
@@ -2108,7 +2109,7 @@ __global__ __launch_bounds__(256) void k_mc(const McUnit *__restrict__ units, in
     // at 16 bits (C5 52.7 -> 79 ms: 19 KB of LDS per workgroup halves the loads in flight
     // on 8K references that miss the caches)
     if (sizeof(PIX) != 1 || scaled || npx < MC_LDS_MIN || (1 << lw) != W) {
-        for (int i = threadIdx.x; i < npx; i += 256) {
+        for (int i = threadIdx.x; i < npx; i += NTH) {
             int yy = i / W, xx = i - yy * W;
             int out = 0;
             for (int k = 0; k < u.nref; k++) {
@@ -2342,8 +2343,12 @@ int vp9hip_launch_plf(int fmt, hipStream_t st, const PlfLaunch *pl, const uint32
 int vp9hip_launch_mc(int hb, hipStream_t st, int n, const McUnit *units, const FrameDesc *frames)
 {
     if (n <= 0) return 0;
-    if (hb) hipLaunchKernelGGL(k_mc<uint16_t>, dim3(n), dim3(256), 0, st, units, n, frames);
-    else    hipLaunchKernelGGL(k_mc<uint8_t>, dim3(n), dim3(256), 0, st, units, n, frames);
+    // high bit depth: one wave per unit (the per-pixel sampler keeps every lane of a small
+    // unit busy; VP9HIP_MC64=0: 256 threads, as 8-bit, whose LDS passes need them)
+    static const bool mc64 = !getenv("VP9HIP_MC64") || atoi(getenv("VP9HIP_MC64"));
+    if (hb && mc64) hipLaunchKernelGGL((k_mc<uint16_t, 64>), dim3(n), dim3(64), 0, st, units, n, frames);
+    else if (hb)    hipLaunchKernelGGL((k_mc<uint16_t, 256>), dim3(n), dim3(256), 0, st, units, n, frames);
+    else            hipLaunchKernelGGL((k_mc<uint8_t, 256>), dim3(n), dim3(256), 0, st, units, n, frames);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 }
