@@ -685,15 +685,22 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
                 for (int k = S.u.b.doff[j]; k < S.u.b.doff[j + 1]; k++)
                     if (S.u.b.sch[S.u.b.dep[k]] >= (uint16_t) npass) { cand = false; break; }
             const int sz = 4 << ((S.ja[j] >> 2) & 3);
-            for (;;) {
-                const uint64_t m = __ballot(cand && sz <= budget);
+            // takes in priority order by lane-size prefix sums: round 1 takes the longest
+            // prefix of the chunk's ready jobs that fits, later rounds refill the remaining
+            // lanes from the jobs skipped (any packing that respects the producers is exact;
+            // only the pass count depends on it)
+            for (int round = 0; round < 3 && budget >= 4; round++) {
+                const uint32_t incl = wscan_incl(cand ? (uint32_t) sz : 0u, lane);
+                const bool take = cand && incl <= (uint32_t) budget;
+                const uint64_t m = __ballot(take);
                 if (!m) break;
-                const int i0 = __builtin_ctzll(m);
-                const int J = rdl(j, i0);
-                budget -= rdl(sz, i0);
-                if (lane == i0) { cand = false; S.u.b.sch[J] = (uint16_t) npass; }
-                if (lane == 0) S.u.b.tk[ntake] = (uint16_t) J;
-                ntake++;
+                if (take) {
+                    cand = false;
+                    S.u.b.sch[j] = (uint16_t) npass;
+                    S.u.b.tk[ntake + (int) mbcnt(m)] = (uint16_t) j;
+                }
+                ntake += __popcll(m);
+                budget -= (int) rdl(incl, 63 - __builtin_clzll(m));
             }
         }
         wsync();
