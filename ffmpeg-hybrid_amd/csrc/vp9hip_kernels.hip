@@ -2078,6 +2078,50 @@ DEV int mc_sample(const PIX *r, int pitch, int w, int h, int X, int Y, int mx, i
     return clipbd((s + 64) >> 7, bd);
 }
 
+// Unscaled MC of 4 vertically adjacent pixels (rows Y .. Y + 3 of column X) from one
+// reference, as mc_sample's unscaled cases: each horizontally filtered reference row is
+// computed once for the 4 outputs (11 rows for the 8-tap 2-D case: 88 taps instead of 256).
+template <typename PIX>
+DEV int mc_hrow(const PIX *r, int pitch, int w, int h, int X, int Y, int mx, bool bil, const int16_t *fx, int bd)
+{
+    if (!mx) return mc_ref(r, pitch, w, h, X, Y);
+    if (bil) {
+        const int a0 = mc_ref(r, pitch, w, h, X, Y), a1 = mc_ref(r, pitch, w, h, X + 1, Y);
+        return a0 + ((mx * (a1 - a0) + 8) >> 4);
+    }
+    int s = 0;
+#pragma unroll
+    for (int t = 0; t < 8; t++) s += fx[t] * mc_ref(r, pitch, w, h, X - 3 + t, Y);
+    return clipbd((s + 64) >> 7, bd);
+}
+template <typename PIX>
+DEV void mc_quad(const PIX *r, int pitch, int w, int h, int X, int Y, int mx, int my, int filter, int bd, int (&o)[4])
+{
+    const bool bil = filter == 3;
+    const int16_t *fx = vp9t_subpel_filters[bil ? 0 : filter][mx], *fy = vp9t_subpel_filters[bil ? 0 : filter][my];
+    if (!my) {
+#pragma unroll
+        for (int t = 0; t < 4; t++) o[t] = mc_hrow<PIX>(r, pitch, w, h, X, Y + t, mx, bil, fx, bd);
+    } else if (bil) {
+        int hr[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++) hr[k] = mc_hrow<PIX>(r, pitch, w, h, X, Y + k, mx, true, fx, bd);
+#pragma unroll
+        for (int t = 0; t < 4; t++) o[t] = hr[t] + ((my * (hr[t + 1] - hr[t]) + 8) >> 4);
+    } else {
+        int hr[11];
+#pragma unroll
+        for (int k = 0; k < 11; k++) hr[k] = mc_hrow<PIX>(r, pitch, w, h, X, Y - 3 + k, mx, false, fx, bd);
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            int s = 0;
+#pragma unroll
+            for (int k = 0; k < 8; k++) s += fy[k] * hr[t + k];
+            o[t] = clipbd((s + 64) >> 7, bd);
+        }
+    }
+}
+
 // One MC unit (<= 64 x 64 pixels of one plane) per workgroup. Unscaled references: the
 // (h + 7) x (w + 7) reference window (edge-clamped, emulated_edge_mc) is staged in LDS once,
 // then the separable filter runs as a horizontal pass into a pixel-clipped LDS tmp and a
@@ -2108,6 +2152,27 @@ __global__ __launch_bounds__(NTH) void k_mc(const McUnit *__restrict__ units, in
     // measured: the LDS passes win at 8 bits (C2 k_mc 12.0 -> 10.2 ms per 120 frames) and lose
     // at 16 bits (C5 52.7 -> 79 ms: 19 KB of LDS per workgroup halves the loads in flight
     // on 8K references that miss the caches)
+    // high bit depth, unscaled: 4 rows per lane (C5 k_mc 39.1 -> 27.9 ms per step; for the
+    // small 8-bit units it measured slower than the per-pixel sampler, C2 7.9 -> 8.2 ms)
+    if (sizeof(PIX) != 1 && !scaled && !(H & 3)) {
+        const int nq = npx >> 2;
+        for (int i = threadIdx.x; i < nq; i += NTH) {
+            const int yq = i / W, xx = i - yq * W, yy = yq * 4;
+            int out[4];
+            for (int k = 0; k < u.nref; k++) {
+                const int rf = u.ref[k];
+                const McRef m = u.r[k];
+                int v[4];
+                mc_quad<PIX>((const PIX *) fd.ref[rf][p], pitch, fd.refw[rf][c], fd.refh[rf][c], m.ix + xx, m.iy + yy,
+                             m.mx, m.my, u.filter, bd, v);
+#pragma unroll
+                for (int t = 0; t < 4; t++) out[t] = k ? (out[t] + v[t] + 1) >> 1 : v[t];
+            }
+#pragma unroll
+            for (int t = 0; t < 4; t++) dst[(size_t) (u.y + yy + t) * pitch + u.x + xx] = (PIX) out[t];
+        }
+        return;
+    }
     if (sizeof(PIX) != 1 || scaled || npx < MC_LDS_MIN || (1 << lw) != W) {
         for (int i = threadIdx.x; i < npx; i += NTH) {
             int yy = i / W, xx = i - yy * W;
