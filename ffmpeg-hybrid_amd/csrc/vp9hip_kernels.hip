@@ -2078,9 +2078,10 @@ DEV int mc_sample(const PIX *r, int pitch, int w, int h, int X, int Y, int mx, i
     return clipbd((s + 64) >> 7, bd);
 }
 
-// Unscaled MC of 4 vertically adjacent pixels (rows Y .. Y + 3 of column X) from one
+// Unscaled MC of R vertically adjacent pixels (rows Y .. Y + R - 1 of column X) from one
 // reference, as mc_sample's unscaled cases: each horizontally filtered reference row is
-// computed once for the 4 outputs (11 rows for the 8-tap 2-D case: 88 taps instead of 256).
+// computed once for the R outputs (R + 7 rows for the 8-tap 2-D case: 88 taps instead of
+// 256 for R = 4, 120 instead of 512 for R = 8).
 template <typename PIX>
 DEV int mc_hrow(const PIX *r, int pitch, int w, int h, int X, int Y, int mx, bool bil, const int16_t *fx, int bd)
 {
@@ -2094,31 +2095,52 @@ DEV int mc_hrow(const PIX *r, int pitch, int w, int h, int X, int Y, int mx, boo
     for (int t = 0; t < 8; t++) s += fx[t] * mc_ref(r, pitch, w, h, X - 3 + t, Y);
     return clipbd((s + 64) >> 7, bd);
 }
-template <typename PIX>
-DEV void mc_quad(const PIX *r, int pitch, int w, int h, int X, int Y, int mx, int my, int filter, int bd, int (&o)[4])
+template <typename PIX, int R>
+DEV void mc_rows(const PIX *r, int pitch, int w, int h, int X, int Y, int mx, int my, int filter, int bd, int (&o)[R])
 {
     const bool bil = filter == 3;
     const int16_t *fx = vp9t_subpel_filters[bil ? 0 : filter][mx], *fy = vp9t_subpel_filters[bil ? 0 : filter][my];
     if (!my) {
 #pragma unroll
-        for (int t = 0; t < 4; t++) o[t] = mc_hrow<PIX>(r, pitch, w, h, X, Y + t, mx, bil, fx, bd);
+        for (int t = 0; t < R; t++) o[t] = mc_hrow<PIX>(r, pitch, w, h, X, Y + t, mx, bil, fx, bd);
     } else if (bil) {
-        int hr[5];
+        int hr[R + 1];
 #pragma unroll
-        for (int k = 0; k < 5; k++) hr[k] = mc_hrow<PIX>(r, pitch, w, h, X, Y + k, mx, true, fx, bd);
+        for (int k = 0; k < R + 1; k++) hr[k] = mc_hrow<PIX>(r, pitch, w, h, X, Y + k, mx, true, fx, bd);
 #pragma unroll
-        for (int t = 0; t < 4; t++) o[t] = hr[t] + ((my * (hr[t + 1] - hr[t]) + 8) >> 4);
+        for (int t = 0; t < R; t++) o[t] = hr[t] + ((my * (hr[t + 1] - hr[t]) + 8) >> 4);
     } else {
-        int hr[11];
+        int hr[R + 7];
 #pragma unroll
-        for (int k = 0; k < 11; k++) hr[k] = mc_hrow<PIX>(r, pitch, w, h, X, Y - 3 + k, mx, false, fx, bd);
+        for (int k = 0; k < R + 7; k++) hr[k] = mc_hrow<PIX>(r, pitch, w, h, X, Y - 3 + k, mx, false, fx, bd);
 #pragma unroll
-        for (int t = 0; t < 4; t++) {
+        for (int t = 0; t < R; t++) {
             int s = 0;
 #pragma unroll
             for (int k = 0; k < 8; k++) s += fy[k] * hr[t + k];
             o[t] = clipbd((s + 64) >> 7, bd);
         }
+    }
+}
+// R rows per lane over a unit (H % R == 0), compound averaged
+template <typename PIX, int R>
+DEV void mc_unit_rows(const McUnit &u, const FrameDesc &fd, PIX *dst, int pitch, int c, int bd, int nth)
+{
+    const int W = u.w, nq = W * u.h / R, p = u.plane;
+    for (int i = threadIdx.x; i < nq; i += nth) {
+        const int yq = i / W, xx = i - yq * W, yy = yq * R;
+        int out[R];
+        for (int k = 0; k < u.nref; k++) {
+            const int rf = u.ref[k];
+            const McRef m = u.r[k];
+            int v[R];
+            mc_rows<PIX, R>((const PIX *) fd.ref[rf][p], pitch, fd.refw[rf][c], fd.refh[rf][c], m.ix + xx, m.iy + yy,
+                            m.mx, m.my, u.filter, bd, v);
+#pragma unroll
+            for (int t = 0; t < R; t++) out[t] = k ? (out[t] + v[t] + 1) >> 1 : v[t];
+        }
+#pragma unroll
+        for (int t = 0; t < R; t++) dst[(size_t) (u.y + yy + t) * pitch + u.x + xx] = (PIX) out[t];
     }
 }
 
@@ -2130,6 +2152,9 @@ DEV void mc_quad(const PIX *r, int pitch, int w, int h, int X, int Y, int mx, in
 // the 1-D and copy cases of the unscaled selection (vp9dsp_template.c:2036-2059, 1971-2022).
 // Scaled references and small units keep the per-pixel sampler (no barriers; L1-served taps).
 #define MC_WP 72                      // window pitch (>= 64 + 7)
+#ifndef MC_ROWS8
+#define MC_ROWS8 1                    // high bit depth: 8 rows per lane where the unit height allows
+#endif
 #ifndef MC_LDS_MIN
 #define MC_LDS_MIN 1024               // units of at least this many pixels use the LDS passes
 #endif
@@ -2155,22 +2180,11 @@ __global__ __launch_bounds__(NTH) void k_mc(const McUnit *__restrict__ units, in
     // high bit depth, unscaled: 4 rows per lane (C5 k_mc 39.1 -> 27.9 ms per step; for the
     // small 8-bit units it measured slower than the per-pixel sampler, C2 7.9 -> 8.2 ms)
     if (sizeof(PIX) != 1 && !scaled && !(H & 3)) {
-        const int nq = npx >> 2;
-        for (int i = threadIdx.x; i < nq; i += NTH) {
-            const int yq = i / W, xx = i - yq * W, yy = yq * 4;
-            int out[4];
-            for (int k = 0; k < u.nref; k++) {
-                const int rf = u.ref[k];
-                const McRef m = u.r[k];
-                int v[4];
-                mc_quad<PIX>((const PIX *) fd.ref[rf][p], pitch, fd.refw[rf][c], fd.refh[rf][c], m.ix + xx, m.iy + yy,
-                             m.mx, m.my, u.filter, bd, v);
-#pragma unroll
-                for (int t = 0; t < 4; t++) out[t] = k ? (out[t] + v[t] + 1) >> 1 : v[t];
-            }
-#pragma unroll
-            for (int t = 0; t < 4; t++) dst[(size_t) (u.y + yy + t) * pitch + u.x + xx] = (PIX) out[t];
-        }
+#if MC_ROWS8
+        if (!(H & 7)) mc_unit_rows<PIX, 8>(u, fd, dst, pitch, c, bd, NTH);
+        else
+#endif
+        mc_unit_rows<PIX, 4>(u, fd, dst, pitch, c, bd, NTH);
         return;
     }
     if (sizeof(PIX) != 1 || scaled || npx < MC_LDS_MIN || (1 << lw) != W) {
