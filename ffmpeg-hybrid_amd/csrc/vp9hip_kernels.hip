@@ -1065,23 +1065,18 @@ DEV void lf_reg(int (&px)[NPX], int code, uint32_t eih, int bd)
         px[C + 2] = (p0 + q0 + q1 + 2 * q2 + q3 + q3 + q3 + 4) >> 3;
         return;
     }
+    // 4-wide, both hev forms in one branch-free sequence (lanes of a wave differ in hev):
+    // with hev the p1 - q1 term enters f and p1 / q1 stay, without it f = 3 (q0 - p0) and
+    // p1 / q1 move by (f1 + 1) >> 1 (vp9dsp_template.c:1858-1885)
     const int mx = (1 << (bd - 1)) - 1, mn = -(1 << (bd - 1));
     const bool hev = (ap1p0 > H) | (aq1q0 > H);
-    if (hev) {
-        int f = p1 - q1; f = f < mn ? mn : f > mx ? mx : f;
-        f = 3 * (q0 - p0) + f; f = f < mn ? mn : f > mx ? mx : f;
-        const int f1 = (f + 4 < mx ? f + 4 : mx) >> 3, f2 = (f + 3 < mx ? f + 3 : mx) >> 3;
-        px[C - 1] = clipbd(p0 + f2, bd);
-        px[C] = clipbd(q0 - f1, bd);
-    } else {
-        int f = 3 * (q0 - p0); f = f < mn ? mn : f > mx ? mx : f;
-        const int f1 = (f + 4 < mx ? f + 4 : mx) >> 3, f2 = (f + 3 < mx ? f + 3 : mx) >> 3;
-        px[C - 1] = clipbd(p0 + f2, bd);
-        px[C] = clipbd(q0 - f1, bd);
-        f = (f1 + 1) >> 1;
-        px[C - 2] = clipbd(p1 + f, bd);
-        px[C + 1] = clipbd(q1 - f, bd);
-    }
+    int f = hev ? min(max(p1 - q1, mn), mx) : 0;
+    f = min(max(3 * (q0 - p0) + f, mn), mx);
+    const int f1 = min(f + 4, mx) >> 3, f2 = min(f + 3, mx) >> 3, f3 = (f1 + 1) >> 1;
+    px[C - 1] = clipbd(p0 + f2, bd);
+    px[C] = clipbd(q0 - f1, bd);
+    px[C - 2] = hev ? p1 : clipbd(p1 + f3, bd);
+    px[C + 1] = hev ? q1 : clipbd(q1 - f3, bd);
 }
 
 template <typename PIX, int N> DEV void lf_unpack(const uint32_t *w, int (&px)[N], int i0, int i1, int o)
