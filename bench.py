@@ -158,7 +158,7 @@ def main():
     frames, refs, geom = make_frames(v, args.config, args.frames, rank, args.chroma)
     t_gen = time.time() - t0
 
-    dev = v.Device(local_rank)
+    dev = v.Device(_device_of(local_rank))
     dev.configure(W, H, BPP, nbufs=args.frames * args.inflight, ss_h=ssh, ss_v=ssv)
     t0 = time.time()
     dev.stage_batch(frames, list(range(args.frames)), None if gop == 1 else refs)
@@ -525,6 +525,14 @@ def e2e_rate(v, gops, args, device):
     return {"fps": round(n / dt, 2), "frames": n, "parse_threads": threads, "max_batch": 16,
             "sample": "the %d-frame %s sample stream sent %d times through vp9hip_decoder "
                       "(send_packet / receive_frame, device frames)" % (len(pkts), args.config, reps)}
+
+
+def _device_of(local_rank):
+    """One rank per GPU; ranks beyond the visible GPUs share them round-robin (a multi-rank
+    rehearsal on a 1-GPU box). Counting devices does not initialise the GPU."""
+    import torch
+    n = torch.cuda.device_count()
+    return local_rank % n if n > 0 else local_rank
 
 
 def bench_tiles(args, v, dist, world, rank, local_rank):
