@@ -578,6 +578,37 @@ __global__ __launch_bounds__(64 * RWAVES) void k_resid(const RJob *__restrict__ 
                                        cbs[wave]);
 }
 
+// Every transform size of a phase in ONE launch (narrow, level-scheduled phases: the chain
+// positions of inter streams, whose launches are latency-bound): waves [w0[t], w0[t + 1])
+// run tx code t's jobs, each wave with an LDS block sized for the largest transform. The
+// five per-size launches ran one after another on the phase's stream.
+struct ResidMulti { uint32_t off[5], n[5], w0[6]; };
+template <typename PIX, class M, typename COEF>
+__global__ __launch_bounds__(64 * RWAVES) void k_resid_multi(ResidMulti a, const RJob *__restrict__ jobs,
+                                                             const FrameDesc *__restrict__ frames,
+                                                             const COEF *__restrict__ coefs, int16_t *__restrict__ resid)
+{
+    constexpr int E = RWave<32, COEF>::E > RWave<16, COEF>::E ? RWave<32, COEF>::E : RWave<16, COEF>::E;
+    static_assert(E >= RWave<8, COEF>::E && E >= RWave<4, COEF>::E, "LDS block of the largest transform");
+    __shared__ COEF cbs[RWAVES][E];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t gw = blockIdx.x * RWAVES + wave;
+    if (gw >= a.w0[5]) return;
+    int t = 0;
+#pragma unroll
+    for (int k = 1; k < 5; k++) t += gw >= a.w0[k];
+    const int wj = (int) (gw - a.w0[t]);
+    const RJob *j = jobs + a.off[t];
+    const int n = (int) a.n[t];
+    switch (t) {
+    case 0: resid_wave<4, 0, PIX, M, COEF>(j, n, wj, lane, frames, coefs, resid, cbs[wave]); break;
+    case 1: resid_wave<8, 1, PIX, M, COEF>(j, n, wj, lane, frames, coefs, resid, cbs[wave]); break;
+    case 2: resid_wave<16, 2, PIX, M, COEF>(j, n, wj, lane, frames, coefs, resid, cbs[wave]); break;
+    case 3: resid_wave<32, 3, PIX, M, COEF>(j, n, wj, lane, frames, coefs, resid, cbs[wave]); break;
+    default: resid_wave<4, 4, PIX, M, COEF>(j, n, wj, lane, frames, coefs, resid, cbs[wave]); break;
+    }
+}
+
 // ------------------------------------------------------------- k_pred
 // One wavefront predicts one 64x64 superblock (luma + 4:2:0 chroma) in LDS. The host
 // packs the SB's intra tx blocks into passes of independent jobs of one size (same
@@ -2376,6 +2407,27 @@ int vp9hip_launch_resid(int hb, hipStream_t st, int tcode, int n, const RJob *jo
     case 4: launch_resid_n<4, 4>(hb, st, n, jobs, frames, coefs, resid); break;
     default: return -1;
     }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int vp9hip_launch_resid_multi(int hb, hipStream_t st, const uint32_t *off, const uint32_t *n, const RJob *jobs,
+                              const FrameDesc *frames, const void *coefs, int16_t *resid)
+{
+    static const int tn[5] = { 4, 8, 16, 32, 4 };
+    ResidMulti a;
+    a.w0[0] = 0;
+    for (int t = 0; t < 5; t++) {
+        a.off[t] = off[t]; a.n[t] = n[t];
+        const uint32_t per = 64 / tn[t];
+        a.w0[t + 1] = a.w0[t] + (n[t] + per - 1) / per;
+    }
+    if (!a.w0[5]) return 0;
+    const int nb = (int) ((a.w0[5] + RWAVES - 1) / RWAVES);
+    if (hb)
+        hipLaunchKernelGGL((k_resid_multi<uint16_t, M64, int32_t>), dim3(nb), dim3(64 * RWAVES), 0, st, a, jobs, frames,
+                           (const int32_t *) coefs, resid);
+    else
+        hipLaunchKernelGGL((k_resid_multi<uint8_t, M32, int16_t>), dim3(nb), dim3(64 * RWAVES), 0, st, a, jobs, frames,
+                           (const int16_t *) coefs, resid);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 // fmt: bit 0 high bit depth, bit 1 ss_h, bit 2 ss_v

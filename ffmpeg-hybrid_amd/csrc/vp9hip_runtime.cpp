@@ -39,6 +39,8 @@
 #include "vp9hip_plan.h"
 
 extern "C" {
+int vp9hip_launch_resid_multi(int hb, hipStream_t st, const uint32_t *off, const uint32_t *n, const RJob *jobs,
+                              const FrameDesc *frames, const void *coefs, int16_t *resid);
 int vp9hip_launch_resid(int hb, hipStream_t st, int tcode, int n, const RJob *jobs, const FrameDesc *frames,
                         const void *coefs, int16_t *resid);
 int vp9hip_launch_pred(int fmt, hipStream_t st, int nwg, const uint32_t *list, const WGRec *wgs, const SBRec *sbs,
@@ -1309,7 +1311,14 @@ static int plan_dev(vp9hip_ctx *c)
                 const uint32_t a = gv[P.g_res + (d * 5 + tc) * 2], b = gv[P.g_res + (d * 5 + tc) * 2 + 1];
                 return std::make_pair(a, b - a);
             };
-            if (!P.fused)
+            // level-scheduled (inter chain) phases: every tx size in one launch (arg 5, the
+            // ranges in roff / rn); VP9HIP_RESID_MULTI=0 keeps one launch per size
+            static const bool rmulti = !getenv("VP9HIP_RESID_MULTI") || atoi(getenv("VP9HIP_RESID_MULTI"));
+            if (!P.fused && P.levels && rmulti) {
+                Launch L = { K_RESID, 0, 0, 5, g, ph, PART_RECON, 0 };
+                for (int tc = 0; tc < 5; tc++) { L.roff[tc] = rr(0, tc).first; L.rn[tc] = rr(0, tc).second; L.n += L.rn[tc]; }
+                if (L.n) s.launches.push_back(L);
+            } else if (!P.fused)
                 for (int tc = 0; tc < 5; tc++)
                     if (rr(0, tc).second) push(K_RESID, rr(0, tc).first, rr(0, tc).second, tc, PART_RECON, 0);
             auto step = [&](int d) {
@@ -1949,6 +1958,9 @@ static int launch_one(vp9hip_ctx *c, const Launch &L, hipStream_t st)
     case K_MC:
         return vp9hip_launch_mc(c->hb, st, (int) L.n, (const McUnit *) (s.arena + s.o_mcs) + L.off, fr);
     case K_RESID:
+        if (L.arg == 5)
+            return vp9hip_launch_resid_multi(c->hb, st, L.roff, L.rn, (const RJob *) (s.arena + s.o_rjobs), fr,
+                                             s.arena + s.o_coefs, s.resid);
         return vp9hip_launch_resid(c->hb, st, L.arg, (int) L.n, (const RJob *) (s.arena + s.o_rjobs) + L.off, fr,
                                    s.arena + s.o_coefs, s.resid);
     case K_PRED:
