@@ -1868,13 +1868,14 @@ __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfrd(const uint32_t *__res
         PIX *lt = S.lt[tb];
         PIX (*ct)[L::CR * FCP] = S.ct[tb];
         // interior (loaded during the previous SB) and left halo into this SB's tile
+        // the progress probe on the store wave (idle here): its round trip runs under the
+        // filtering waves' tile writes
+        if (lane == NT) {
+            if (dep != ~0u && seen < c + 1)
+                seen = __hip_atomic_load((gu32 *) &progress[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_pre = dep == ~0u || seen >= c + 1;
+        }
         if (!mover) {
-            // the progress probe first: its round trip runs under the tile writes
-            if (lane == 0) {
-                if (dep != ~0u && seen < c + 1)
-                    seen = __hip_atomic_load((gu32 *) &progress[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                s_pre = dep == ~0u || seen >= c + 1;
-            }
             if (lane < L::PROG / 4) S.prog[tb][lane] = pwv;
 #pragma unroll
             for (int u = 0; u < N::NUI; u++) {
@@ -1948,7 +1949,7 @@ __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfrd(const uint32_t *__res
         __syncthreads();
         LFR_T(2);
         if (!pre) {
-            if (lane == 0 && dep != ~0u) {
+            if (lane == NT && dep != ~0u) {
                 const uint32_t need = c + 1;
                 for (uint32_t n = 0; seen < need; n++) {
                     seen = __hip_atomic_load((gu32 *) &progress[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

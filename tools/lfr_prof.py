@@ -17,7 +17,7 @@ names = {8: "interior + left halo into the tile, progress probe", 0: "barrier A"
          9: "top-halo loads issued (store wave: previous tile stored)", 13: "column pass part 1 (edge x = 0) + barrier",
          2: "column pass part 2 (+ barrier)",
          12: "blocking wait for the row above, first SB (pipeline fill)",
-         10: "blocking wait for the row above, later SBs", 11: "barrier after the wait",
+         10: "blocking wait for the row above, later SBs", 11: "barrier after the wait (the store wave's spin: the blocking wait)",
          3: "top halo into the tile, next interior issued, barrier", 4: "row pass (+ barrier)"}
 print("workgroups", v[14], "SB steps", v[6], "blocking waits", v[5], file=sys.stderr)
 for i, n in names.items():
