@@ -41,7 +41,7 @@ W, H, BPP, LOG2_TILE_COLS = 3840, 2160, 8, 2
 CONFIG_INDEX = 2               # C3
 CHROMA = {"420": (1, 1), "422": (1, 0), "440": (0, 1), "444": (0, 0)}   # (ss_h, ss_v)
 SEED0 = 0x56503900 + CONFIG_INDEX
-TRAFFIC_PROFILE = "r02h"       # rocprofv3 PMC pass of C3 (tools/profile.sh)
+TRAFFIC_PROFILE = "r02i"       # rocprofv3 PMC pass of C3 (tools/profile.sh)
 
 
 def frame_seed(rank, i, config_index=CONFIG_INDEX):
