@@ -2336,7 +2336,8 @@ template <typename PIX, class G>
 static void launch_lfr_g(hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs, const FrameDesc *frames, uint32_t *ctr)
 {
     // VP9HIP_LFR_DB=0: the single-tile k_lfr (A/B switch)
-    static const bool db = !getenv("VP9HIP_LFR_DB") || atoi(getenv("VP9HIP_LFR_DB"));
+    const char *e = getenv("VP9HIP_LFR_DB");          // read per launch (tests switch it)
+    const bool db = !e || atoi(e);
     if (db) hipLaunchKernelGGL((k_lfrd<PIX, G>), dim3(ntasks), dim3(LfNT<G>::NT + 64), 0, st, tasks, recs, frames, ctr, ntasks);
     else    hipLaunchKernelGGL((k_lfr<PIX, G, false>), dim3(ntasks), dim3(LfNT<G>::NT + 64), 0, st, tasks, recs, frames, ctr, ntasks);
 }
@@ -2472,7 +2473,8 @@ int vp9hip_launch_mc(int hb, hipStream_t st, int n, const McUnit *units, const F
     if (n <= 0) return 0;
     // high bit depth: one wave per unit (the per-pixel sampler keeps every lane of a small
     // unit busy; VP9HIP_MC64=0: 256 threads, as 8-bit, whose LDS passes need them)
-    static const bool mc64 = !getenv("VP9HIP_MC64") || atoi(getenv("VP9HIP_MC64"));
+    const char *e = getenv("VP9HIP_MC64");
+    const bool mc64 = !e || atoi(e);
     if (hb && mc64) hipLaunchKernelGGL((k_mc<uint16_t, 64>), dim3(n), dim3(64), 0, st, units, n, frames);
     else if (hb)    hipLaunchKernelGGL((k_mc<uint16_t, 256>), dim3(n), dim3(256), 0, st, units, n, frames);
     else            hipLaunchKernelGGL((k_mc<uint8_t, 256>), dim3(n), dim3(256), 0, st, units, n, frames);

@@ -1313,7 +1313,8 @@ static int plan_dev(vp9hip_ctx *c)
             };
             // level-scheduled (inter chain) phases: every tx size in one launch (arg 5, the
             // ranges in roff / rn); VP9HIP_RESID_MULTI=0 keeps one launch per size
-            static const bool rmulti = !getenv("VP9HIP_RESID_MULTI") || atoi(getenv("VP9HIP_RESID_MULTI"));
+            const char *rme = getenv("VP9HIP_RESID_MULTI");
+            const bool rmulti = !rme || atoi(rme);
             if (!P.fused && P.levels && rmulti) {
                 Launch L = { K_RESID, 0, 0, 5, g, ph, PART_RECON, 0 };
                 for (int tc = 0; tc < 5; tc++) { L.roff[tc] = rr(0, tc).first; L.rn[tc] = rr(0, tc).second; L.n += L.rn[tc]; }
