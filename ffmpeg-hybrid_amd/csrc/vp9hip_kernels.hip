@@ -935,6 +935,13 @@ DEV void load_ltab(uint32_t *ltab, const uint32_t *__restrict__ ptab, int lane)
         if (lane + 64 * u < 800) ltab[lane + 64 * u] = t[u];
 }
 
+// PRED_PROF builds (profiling only, tools/pred_prof.py): lane 0 of each intra workgroup
+// sums shader-clock cycles: [0] tile loads, [1] all passes, [2] interior stores, [3] passes,
+// [4] workgroups, [5 + i] cycles and [9 + i] count of passes with MAXN = 4 << i
+#ifndef PRED_PROF
+#define PRED_PROF 0
+#endif
+__device__ unsigned long long pred_prof[16];
 // Intra prediction of one workgroup record (the ltab copy must be loaded).
 template <typename PIX, class G>
 DEV void pred_wg(const WGRec *wgp, const SBRec *__restrict__ sbs, const PJob *__restrict__ jobs,
@@ -953,6 +960,7 @@ DEV void pred_wg(const WGRec *wgp, const SBRec *__restrict__ sbs, const PJob *__
     const PJob *lj = jobs + wjob0;         // job records: read a pass ahead (L1/L2)
     const uint32_t *lp = passes + wpass0;  // pass words: wave-uniform scalar loads
     const int bd = frames[sbs[wgp->sb[0]].frame].bd;
+    uint64_t pp0 = PRED_PROF ? clock64() : 0, pp[13] = {0};
 
     // ---- prologue: job list, pass words, SB neighbourhoods (pre-LF pixels) ----
 #pragma unroll 1
@@ -964,6 +972,7 @@ DEV void pred_wg(const WGRec *wgp, const SBRec *__restrict__ sbs, const PJob *__
         }
     }
     wave_sync();
+    if (PRED_PROF) { const uint64_t t = clock64(); pp[0] += t - pp0; pp0 = t; }
 
     // passes: residual sets A / B alternate (loop unrolled by two), job records J run a
     // pass ahead of them; pass words are wave-uniform scalar loads (index clamped)
@@ -979,14 +988,27 @@ DEV void pred_wg(const WGRec *wgp, const SBRec *__restrict__ sbs, const PJob *__
             const uint32_t w0 = LPW(pi), w1 = LPW(pi + 1);
             load_resid(J, resid, B);
             load_job(LPW(pi + 2), lane, lj, J);
+            uint64_t tq = PRED_PROF ? clock64() : 0;
             run_pass<PIX, G>(w0, lane, tile, eb, bd, A, ltab, resid, ptab, dbg);
+            if (PRED_PROF) {
+                const uint64_t t = clock64();
+                const int b = PASS_MAXN(w0) == 4 ? 0 : PASS_MAXN(w0) == 8 ? 1 : PASS_MAXN(w0) == 16 ? 2 : 3;
+                pp[5 + b] += t - tq; pp[9 + b]++; tq = t;
+            }
             if (pi + 1 >= npass) break;
             load_resid(J, resid, A);
             load_job(LPW(pi + 3), lane, lj, J);
+            if (PRED_PROF) tq = clock64();
             run_pass<PIX, G>(w1, lane, tile, eb, bd, B, ltab, resid, ptab, dbg);
+            if (PRED_PROF) {
+                const uint64_t t = clock64();
+                const int b = PASS_MAXN(w1) == 4 ? 0 : PASS_MAXN(w1) == 8 ? 1 : PASS_MAXN(w1) == 16 ? 2 : 3;
+                pp[5 + b] += t - tq; pp[9 + b]++;
+            }
         }
     }
 #undef LPW
+    if (PRED_PROF) { const uint64_t t = clock64(); pp[1] += t - pp0; pp0 = t; pp[3] = (uint64_t) npass; }
 
     // ---- store the SB interiors ----
     if (!(dbg & 2))
@@ -996,6 +1018,11 @@ DEV void pred_wg(const WGRec *wgp, const SBRec *__restrict__ sbs, const PJob *__
         if (sbi == 0xffffffffu) continue;
         const SBRec sb = sbs[sbi];
         sb_interior<PIX, G, true>(frames[sb.frame], sb.sbx, sb.sby, lane, tile + k * G::TILE);
+    }
+    if (PRED_PROF && lane == 0) {
+        pp[2] += clock64() - pp0;
+        pp[4] = 1;
+        for (int i = 0; i < 13; i++) atomicAdd(&pred_prof[i], pp[i]);
     }
 }
 
@@ -2390,6 +2417,13 @@ static void launch_plf_p(int ss, hipStream_t st, const PlfLaunch &pl, const uint
     }
 }
 extern "C" {
+// PRED_PROF builds: read and clear the intra workgroup phase sums (profiling only)
+int vp9hip_pred_prof_read(unsigned long long *out)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(pred_prof), 16 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    static const unsigned long long z[16] = {0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(pred_prof), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
 // LFR_PROF builds: read and clear the k_lfr phase sums (profiling only, not in the ABI)
 int vp9hip_lfr_prof_read(unsigned long long *out)
 {
