@@ -12,8 +12,11 @@ One process per GPU. Each rank:
 - per phase (the frames of one chain position), exchanges the pre-LF stripes of those
   frames with one all-gather, then runs the loop filter over whole frames.
 Every rank ends a phase holding the full post-LF frames that later phases reference.
-The collective is RCCL (`nccl` backend) on device buffers. The `gloo` backend (the CPU
-tests, several ranks sharing one GPU) stages the same bytes through host tensors.
+The collective is RCCL (`nccl` backend) on device buffers, stream-ordered: the packs,
+the all-gather and the unpacks all follow the context's HIP stream (the one
+vp9hip_frame_device returns), so a phase never waits on the host. The `gloo` backend
+(the CPU tests, several ranks sharing one GPU) stages the same bytes through host
+tensors, which needs a host sync per phase.
 
 Per phase, rank r ships the stripes of its tile columns: about P/N bytes (P = frame
 bytes, N = ranks). It receives P(N-1)/N, padded to the largest stripe.
@@ -54,6 +57,15 @@ class TileShard:
         m = max((p[2] for p in self.plan), default=0) if world > 1 else 0
         self.send = torch.empty(max(m, 1), dtype=torch.uint8, device=self.device)
         self.recv = torch.empty(max(m, 1) * world, dtype=torch.uint8, device=self.device)
+        self._ext = None
+
+    def _stream(self):
+        """The context's HIP stream as a torch stream: every launch of run_phase and every
+        vp9hip_stripe copy is enqueued on it."""
+        if self._ext is None:
+            st = self.dev.frame_device(0)[3]
+            self._ext = torch.cuda.ExternalStream(st, device=self.device)
+        return self._ext
 
     def bytes_per_phase(self):
         """(bytes sent, bytes received) by this rank per phase, padded as exchanged."""
@@ -65,10 +77,12 @@ class TileShard:
         if self.world == 1:
             return
         if not self.host_staged:
-            dist.all_gather_into_tensor(self.recv[:m * self.world], self.send[:m], group=self.group)
-            if self.device.type == "cuda":
-                torch.cuda.synchronize(self.device)
+            # RCCL's stream waits for the context stream (the packs), and the context
+            # stream waits for RCCL's (the unpacks that follow): no host round trip
+            with torch.cuda.stream(self._stream()):
+                dist.all_gather_into_tensor(self.recv[:m * self.world], self.send[:m], group=self.group)
             return
+        self.dev.sync()                         # packed stripes complete before the host copy
         parts = [torch.empty(m, dtype=torch.uint8) for _ in range(self.world)]
         dist.all_gather(parts, self.send[:m].cpu(), group=self.group)
         self.recv[:m * self.world].copy_(torch.cat(parts))
@@ -85,7 +99,6 @@ class TileShard:
                 if n:
                     dev.stripe(i, self.lo, self.hi, self.send.data_ptr() + off, to_frame=False)
                 off += n
-            dev.sync()                          # packed stripes complete before the collective
             self._all_gather(m)
             base = self.recv.data_ptr()
             for q, (lo, hi) in enumerate(self.ranges):
