@@ -116,6 +116,65 @@ def test_exchange_completes_every_frame(world, w, h, log2):
         assert all(m > 0 for m, _ in bpp)
 
 
+def test_nccl_exchange_is_stream_ordered(monkeypatch):
+    """The RCCL branch, host logic only (no GPU here): the all-gather is issued under the
+    context's stream (vp9hip_frame_device's handle as an ExternalStream) and the host never
+    syncs the context inside a pass; the exchanged stripes still complete every frame."""
+    import contextlib
+    ts = _ts()
+    w, h, log2, world, rank = 1000, 200, 2, 2, 0
+    phases = [[0, 1], [2], [3, 4]]
+    ranges = ts.tile_ranges(1 << log2, world)
+
+    class Dev(FakeDev):
+        syncs = 0
+
+        def sync(self):
+            Dev.syncs += 1
+
+        def frame_device(self, buf):
+            return None, None, (w, h), 0xC0FFEE
+
+    dev = Dev(w, h, log2, phases, *ranges[rank])
+    peer = FakeDev(w, h, log2, phases, *ranges[1 - rank])
+    for ph in range(len(phases)):
+        peer.run_phase(ph, FakeDev.PART_RECON)
+    state = {"stream": None, "ph": None, "issued": []}
+
+    class Ext:
+        def __init__(self, handle, device=None):
+            self.handle = handle
+
+    @contextlib.contextmanager
+    def under(s):
+        state["stream"] = s
+        try:
+            yield
+        finally:
+            state["stream"] = None
+
+    def gather(out, inp, group=None):
+        s = state["stream"]
+        state["issued"].append(s.handle if s is not None else None)
+        m = inp.numel()
+        out[rank * m:(rank + 1) * m].copy_(inp)
+        off = (1 - rank) * m
+        for i in phases[state["ph"]]:
+            off += peer.stripe(i, *ranges[1 - rank], out.data_ptr() + off)
+
+    monkeypatch.setattr(ts.dist, "get_backend", lambda group=None: "nccl")
+    monkeypatch.setattr(ts.dist, "all_gather_into_tensor", gather)
+    monkeypatch.setattr(ts.torch.cuda, "ExternalStream", Ext)
+    monkeypatch.setattr(ts.torch.cuda, "stream", under)
+    sh = ts.TileShard(dev, 1 << log2, rank, world)
+    for ph in range(len(phases)):
+        state["ph"] = ph
+        sh.run_phase(ph)
+    assert Dev.syncs == 0
+    assert state["issued"] == [0xC0FFEE] * len(phases)
+    assert len(dev.checked) == 5 * 3 and all(dev.checked), dev.checked
+
+
 def test_tile_ranges():
     ts = _ts()
     assert ts.tile_ranges(8, 2) == [(0, 4), (4, 8)]
