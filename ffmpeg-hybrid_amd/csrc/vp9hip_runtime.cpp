@@ -181,7 +181,7 @@ struct vp9hip_ctx {
     hipEvent_t fork_ev = nullptr, join_ev[2 * MAX_GROUPS] = {};
     hipEvent_t lf_done[MAX_GROUPS] = {};
     std::vector<hipEvent_t> sev;            // recon -> LF step events (lf_overlap)
-    int max_groups = 3;                 // VP9HIP_STREAMS overrides (1..8); 3 measured best at C3, with even chain splits
+    int max_groups = 2;                 // VP9HIP_STREAMS overrides (1..8); 2 measured best with the device planner and two batch slots (r02k: C3 +3.7 %, C4 +2.7 %, C2 +1.1 % over 3)
     bool lf_overlap = false;            // VP9HIP_LF_OVERLAP=1: LF on a second stream per group (measured slower)
     bool fuse_plf = true;               // VP9HIP_PLF=0: no fused intra + LF launches
     bool level_sched = true;            // VP9HIP_LEVELS=0: inter frames' intra SBs by diagonal

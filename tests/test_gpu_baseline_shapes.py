@@ -9,8 +9,9 @@ vp9dsp_template.c / vp9recon.c / vp9lpf.c / vp9_mc_template.c), sample-exact.
 
 Frame counts are cut down from the bench's 120 / 60 so the oracle finishes in seconds, but
 every schedule the bench's full batch uses is exercised:
-  - C3 / C4: 3 frame groups of >= 8 keyframes each, i.e. wide phases (k_resid launches,
-    fused k_plf intra + LF diagonals, 4 tile columns) on 3 concurrent HIP streams;
+  - C3 / C4: 2 frame groups (the default) of >= 8 keyframes each, i.e. wide phases (k_resid
+    launches, fused k_plf intra + LF diagonals, 4 tile columns) on 2 concurrent HIP streams;
+    C3 also with VP9HIP_STREAMS=3 (3 groups, the round-1 default);
   - C2: GOP chains of key + P frames, i.e. narrow phases (the inter level schedule of k_pred,
     k_mc, the row-pipelined k_lfr over 17 SB rows), 2 chains on 2 streams;
   - C5: 8K 10-bit, 8 tile columns, key + 2 P (k_lfr over 68 SB rows x 120 SB columns).
@@ -27,11 +28,13 @@ import bench  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 SHAPES = [
-    # (config, frames): GOP lengths are the config's (C2 / C5: 32; the cut keeps key + P chains)
-    ("C3", 27),
-    ("C4", 24),
-    ("C2", 6),
-    ("C5", 3),
+    # (config, frames, VP9HIP_STREAMS or None, frame groups expected): GOP lengths are the
+    # config's (C2 / C5: 32; the cut keeps key + P chains)
+    ("C3", 28, None, 2),                 # chains split evenly over the groups (stage: nroots % G)
+    ("C3", 27, "3", 3),
+    ("C4", 24, None, 2),
+    ("C2", 6, None, 2),
+    ("C5", 3, None, 1),
 ]
 
 
@@ -45,8 +48,12 @@ def _two_chains(frames, refs, geom, n_per_chain):
     return fr, rf
 
 
-@pytest.mark.parametrize("config,n", SHAPES)
-def test_baseline_shape_parity(v9, orc, config, n):
+@pytest.mark.parametrize("config,n,streams,groups", SHAPES)
+def test_baseline_shape_parity(v9, orc, monkeypatch, config, n, streams, groups):
+    if streams is None:
+        monkeypatch.delenv("VP9HIP_STREAMS", raising=False)
+    else:
+        monkeypatch.setenv("VP9HIP_STREAMS", streams)   # read when the context opens
     if config == "C2":
         frames, refs, geom = bench.make_frames(v9, config, 32 + n // 2)
         frames, refs = _two_chains(frames, refs, geom, n // 2)
@@ -62,7 +69,7 @@ def test_baseline_shape_parity(v9, orc, config, n):
         for _ in range(2):
             dev.run_batch()
             dev.sync()
-        assert dev.groups() == (2 if config == "C2" else 1 if config == "C5" else 3)
+        assert dev.groups() == groups
         # C2: decode order of the two chains is chain-major in `frames`
         bad = []
         for i, ref in bench.oracle_frames(v9, orc, frames, refs, (W, H, BPP, log2, len(frames)
