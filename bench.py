@@ -130,8 +130,9 @@ def main():
     ap.add_argument("--inflight", type=int, default=None, choices=[1, 2],
                     help="batches in flight: the context's two batch slots hold the same workload and "
                          "alternate steps, so one batch's device planning overlaps the other's pixel kernels "
-                         "(as the decoder loop runs). Default 2 for keyframe configs (C3/C4: measured +3%%), "
-                         "1 for GOP chains (C5: -6%%)")
+                         "(as the decoder loop runs). Default 2 for keyframe configs (C3/C4: measured +3%%) and "
+                         "for GOP chains up to 1080p (C2: +1.9%%, profiles/r02k), 1 for larger GOP-chain "
+                         "frames (C5 8K: -6%%)")
     ap.add_argument("--shard", choices=["frames", "tiles"], default="frames",
                     help="frames: every rank decodes its own stream (weak scaling, default); tiles: all ranks "
                          "decode ONE stream, each its tile columns, pre-LF stripes all-gathered (strong scaling)")
@@ -152,7 +153,7 @@ def main():
     if args.frames is None:
         args.frames = nf
     if args.inflight is None:
-        args.inflight = 2 if gop == 1 else 1
+        args.inflight = 2 if gop == 1 or W * H <= 1920 * 1088 else 1
     t0 = time.time()
     ssh, ssv = CHROMA[args.chroma]
     frames, refs, geom = make_frames(v, args.config, args.frames, rank, args.chroma)
