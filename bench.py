@@ -41,7 +41,8 @@ W, H, BPP, LOG2_TILE_COLS = 3840, 2160, 8, 2
 CONFIG_INDEX = 2               # C3
 CHROMA = {"420": (1, 1), "422": (1, 0), "440": (0, 1), "444": (0, 0)}   # (ss_h, ss_v)
 SEED0 = 0x56503900 + CONFIG_INDEX
-TRAFFIC_PROFILE = "r02i"       # rocprofv3 PMC pass of C3 (tools/profile.sh)
+TRAFFIC_PROFILE = "r03a"       # rocprofv3 PMC passes of the default C3 bench (tools/profile.sh)
+POISON = 0xA5                  # fill byte of the frame buffers before the timed steps
 
 
 def frame_seed(rank, i, config_index=CONFIG_INDEX):
@@ -122,7 +123,12 @@ def main():
     ap.add_argument("--frames", type=int, default=None, help="frames per GPU (default: the config's)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--verify-all", action="store_true", help="compare every timed frame with the oracle")
+    ap.add_argument("--verify-all", action="store_true",
+                    help="compare every timed frame with the oracle (the default at 1 GPU; kept for old scripts)")
+    ap.add_argument("--verify-frames", type=int, default=None,
+                    help="at 1 GPU: compare only the first N frames (decode order) of each slot with the oracle")
+    ap.add_argument("--verify-frames-per-rank", type=int, default=2,
+                    help="at N > 1 GPUs: the frames per slot every rank compares with the oracle")
     ap.add_argument("--timed-events", action="store_true",
                     help="per-launch HIP events inside the timed steps (no graph replay)")
     ap.add_argument("--chroma", choices=sorted(CHROMA), default="420",
@@ -195,6 +201,10 @@ def main():
         dev.set_slot(k % args.inflight)
         dev.run_batch()
     dev.sync()
+    # poison every frame buffer of both slots: the frames verified below can only have been
+    # written by the timed steps (a replay that did nothing would leave the poison byte)
+    dev.fill(0, args.frames * args.inflight, POISON)
+    dev.sync()
     barrier()
     t0 = time.perf_counter()
     for k in range(args.steps):
@@ -202,10 +212,11 @@ def main():
         dev.run_batch()            # device planning (waits for its summary), then the pixel kernels
         if args.inflight == 1:
             dev.sync()
-    dev.sync()                     # every slot's work is on the main stream
+    dev.sync()                     # every slot's work is on the main stream; checks both slots
     barrier()
     elapsed = time.perf_counter() - t0
     dev.set_slot(0)
+    slots_run = min(args.inflight, args.steps)   # slots the timed steps wrote
 
     elapsed = reduce_elapsed(elapsed, dist)
 
@@ -230,16 +241,28 @@ def main():
     # rocprofv3 PMC pass (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; tools/traffic.py)
     traffic, traffic_src = None, None
     tf = os.path.join(ROOT, "profiles", TRAFFIC_PROFILE, "traffic.json")
+    shape_ok, shape_note = False, None
     if os.path.exists(tf) and args.config == "C3" and args.chroma == "420":
-        per = json.load(open(tf))["per_launch"].get(dom)
-        if per:
+        tj = json.load(open(tf))
+        # the profile must have been taken at this run's launch shape: same frames per launch
+        # (frame groups / streams, frames per batch) and the same launches of the kernel per step
+        run_shape = {"launches_per_step": int(round(launches_per_step)), "streams_per_gpu": streams,
+                     "frames_per_gpu": args.frames}
+        prof_shape = tj.get("shape", {}).get(dom)
+        shape_ok = prof_shape == run_shape
+        if not shape_ok:
+            shape_note = "refused: profiles/%s launch shape %s != this run's %s" % (TRAFFIC_PROFILE, prof_shape, run_shape)
+        per = tj["per_launch"].get(dom)
+        if per and shape_ok:
             traffic, traffic_src = round(per["traffic_bytes"]), "profiles/%s/traffic.json" % TRAFFIC_PROFILE
+        elif shape_note:
+            traffic_src = shape_note
     # instruction issue of the same kernel from the committed SQ pass (profiles/<P>/pmc_summary.txt):
     # VALU wave-instructions per launch / its mean duration there, vs the VALU issue peak
     # (256 CUs x 4 SIMDs x 16 lanes: one wave64 instruction per 4 cycles per SIMD at 2.4 GHz)
     issue = None
     pf = os.path.join(ROOT, "profiles", TRAFFIC_PROFILE, "pmc_summary.txt")
-    if os.path.exists(pf) and args.config == "C3" and args.chroma == "420":
+    if os.path.exists(pf) and shape_ok:
         cur, vals = None, {}
         for line in open(pf):
             if not line.startswith(" "):
@@ -273,13 +296,35 @@ def main():
         "issue": issue,
     }
 
-    # bit-exactness of the timed frames: the CPU-baseline leg's oracle frames are compared
-    # with the device's (the first frames in decode order; all when the sample covers them)
+    # bit-exactness of the timed frames: the oracle's frames are compared with the device's,
+    # in every batch slot the timed steps wrote (the buffers were poisoned before them)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # checker + CPU baseline leg only: the scalar C restatement
     cpu, verify = None, None
-    if rank == 0 and world == 1:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle  # checker + CPU baseline leg only: the scalar C restatement
-        cpu, verify = cpu_baseline(v, oracle, dev, frames, refs, geom, args)
+    if world == 1:
+        cpu, verify = cpu_baseline(v, oracle, dev, frames, refs, geom, args, slots_run)
+    else:
+        # every rank checks a sample of its own frames (the first frames of each slot in
+        # decode order); rank 0 reports all ranks' results
+        verify = verify_frames(v, oracle, dev, frames, refs, geom, args, slots_run,
+                               range(min(args.verify_frames_per_rank, len(frames))), threads=1)
+        verify["rank"] = rank
+    rank_info = {"rank": rank, "local_rank": local_rank, "device": _device_of(local_rank),
+                 "host": os.uname().nodename}
+    rank_info.update(_device_ids(v, rank_info["device"]))
+    ranks = [rank_info]
+    if dist is not None:
+        got = [None] * world
+        dist.all_gather_object(got, (rank_info, verify))
+        ranks = [g[0] for g in got]
+        per = [g[1] for g in got]
+        verify = {"frames": sum(p["frames"] for p in per), "of": len(frames) * slots_run * world,
+                  "mismatched": [[p["rank"]] + m for p in per for m in p["mismatched"]],
+                  "what": "per rank: visible Y/U/V of its first %d frames (decode order) in each of its %d batch "
+                          "slot(s), written by the timed steps after a poison fill, vs the CPU oracle"
+                          % (min(args.verify_frames_per_rank, len(frames)), slots_run),
+                  "per_rank": [{"rank": p["rank"], "frames": p["frames"], "mismatched": len(p["mismatched"])}
+                               for p in per]}
 
     host = e2e = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -314,6 +359,7 @@ def main():
                    "parallelism": "frame-sharded x%d (independent %s, no collective)"
                                   % (world, "keyframes" if gop == 1 else "GOPs"),
                    "streams_per_gpu": streams, "batches_in_flight": args.inflight,
+                   "ranks": ranks,
                    "host_gen_s": round(t_gen, 2), "host_stage_s": round(t_stage, 2)},
         "roofline": roofline,
         "cpu_baseline": cpu,
@@ -332,6 +378,84 @@ def main():
         sys.exit("bench: %d timed frames differ from the oracle: %s" % (len(verify["mismatched"]), verify["mismatched"]))
 
 
+def _compare_slots(v, dev, i, out, geom, args, slots_run, lock=None):
+    """Compare frame i's oracle planes with the device frame in every slot the timed steps
+    wrote (slot k holds frame i in buffer k * frames + i); returns the mismatches."""
+    bad = []
+    for k in range(slots_run):
+        b = k * args.frames + i
+        if lock is not None:
+            with lock:
+                got = dev.download(b)
+        else:
+            got = dev.download(b)
+        d = compare_frame(v, got, out, geom, args.chroma)
+        if d:
+            bad.append([i, k, d])
+    return bad
+
+
+def verify_frames(v, oracle, dev, frames, refs, geom, args, slots_run, idx, threads=None):
+    """Verify frames `idx` (decode-order indices) of every written slot against the oracle,
+    on a thread pool: keyframes independently, inter frames by GOP chain from its keyframe
+    (ctypes releases the GIL in the oracle; device downloads are serialised)."""
+    import concurrent.futures
+    import threading
+    idx = sorted(set(idx))
+    gop = geom[4]
+    if not idx:
+        return {"frames": 0, "mismatched": []}
+    lock = threading.Lock()
+    W, H, BPP = geom[0], geom[1], geom[2]
+    ssh, ssv = CHROMA[args.chroma]
+
+    def unit(chain):
+        outs, bad, n = {}, [], 0
+        for i in range(chain[0], chain[-1] + 1):
+            out = v.alloc_planes(W, H, BPP, ssh, ssv)
+            r = refs[i]
+            oracle.decode_frame(frames[i].pkt, out, None if r is None else [outs[r[0]], outs[r[1]], outs[r[2]]])
+            outs[i] = out
+            for k in [k for k in outs if k < i - 1 and k != chain[0] - chain[0] % gop]:
+                del outs[k]
+            if i in want:
+                bad += _compare_slots(v, dev, i, out, geom, args, slots_run, lock)
+                n += slots_run
+        return n, bad
+
+    want = set(idx)
+    if gop == 1:
+        chains = [[i] for i in idx]
+    else:
+        chains = {}
+        for i in idx:
+            g0 = i - i % gop
+            chains.setdefault(g0, [g0, i])[1] = i
+        chains = list(chains.values())
+    nthr = threads or min(16, os.cpu_count() or 1)
+    with concurrent.futures.ThreadPoolExecutor(nthr) as ex:
+        res = list(ex.map(unit, chains))
+    return {"frames": sum(r[0] for r in res), "mismatched": [m for r in res for m in r[1]]}
+
+
+def _device_ids(v, ordinal):
+    """PCI identity of a rank's GPU (so a multi-GPU line shows each rank on its own card)."""
+    try:
+        bus, name = v.device_info(ordinal)
+        return {"pci_bus_id": bus, "gpu_name": name}
+    except Exception as e:                      # no GPU (CPU rehearsal)
+        return {"pci_bus_id": None, "error": str(e)}
+
+
+def _cpu_quota():
+    """CPUs the cgroup grants this process (cpu.max quota / period), or None if unlimited."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_info():
     """The host the CPU legs ran on: nproc, the CPU share used, the lscpu model name."""
     model = None
@@ -342,25 +466,33 @@ def cpu_info():
                 break
     except OSError:
         pass
-    return {"nproc": os.cpu_count(), "threads_used": min(16, os.cpu_count() or 1), "model": model}
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
+    return {"nproc": os.cpu_count(), "threads_used": min(16, os.cpu_count() or 1), "model": model,
+            "affinity": affinity, "cpu_quota": _cpu_quota()}
 
 
-def cpu_baseline(v, oracle, dev, frames, refs, geom, args):
+def cpu_baseline(v, oracle, dev, frames, refs, geom, args, slots_run):
     """CPU baseline legs on this box's host cores, and the bit-exactness
     check of the timed frames. Leg 1: the scalar C oracle on 1 thread over a bounded sample
-    in decode order; every frame it decodes is compared with the device's frame (downloads
-    and compares are outside the CPU timer). Leg 2: tile-column threads per frame (the
-    reference's slice threading). Leg 3: frame-parallel over the box's CPU share (16
-    threads): independent keyframes (C3/C4) or independent GOP chains (C2/C5), one oracle
-    decode per thread (ctypes releases the GIL). Returns (cpu_baseline, verify)."""
+    in decode order; every frame it decodes is compared with the device's frame in each
+    batch slot the timed steps wrote (downloads and compares are outside the CPU timer).
+    The frames leg 1 did not reach are then verified with the oracle on a thread pool.
+    Leg 2: tile-column threads per frame (the reference's slice threading). Leg 3:
+    frame-parallel over the box's CPU share (16 threads): independent keyframes (C3/C4) or
+    independent GOP chains (C2/C5), one oracle decode per thread (ctypes releases the GIL).
+    Leg 4: the same over every host thread nproc reports. Returns (cpu_baseline, verify)."""
     import concurrent.futures
     W, H, BPP, log2, gop = geom
+    nf = len(frames)
     bounded = not args.no_cpu_baseline
     budget = args.cpu_seconds if bounded else 0.0
-    want = len(frames) if args.verify_all else (2 if not bounded else len(frames))
-    t_or, n, checked, bad = 0.0, 0, 0, []
+    want = nf if args.verify_frames is None else min(nf, args.verify_frames)
+    t_or, n, bad = 0.0, 0, []
     gen = oracle_frames(v, oracle, frames, refs, geom, args.chroma)
-    while n < want:
+    while n < nf:
         t0 = time.perf_counter()
         item = next(gen, None)
         t_or += time.perf_counter() - t0
@@ -368,15 +500,19 @@ def cpu_baseline(v, oracle, dev, frames, refs, geom, args):
             break
         i, out = item
         n += 1
-        d = compare_frame(v, dev.download(i), out, geom, args.chroma)
-        checked += 1
-        if d:
-            bad.append([i, d])
-        if not args.verify_all and n >= 2 and t_or >= budget:
+        if i < want:
+            bad += _compare_slots(v, dev, i, out, geom, args, slots_run)
+        if n >= 2 and t_or >= budget:
             break
-    verify = {"frames": checked, "of": len(frames), "mismatched": bad,
-              "what": "visible Y/U/V of frames 0..%d (decode order) after the timed steps vs the CPU oracle, "
-                      "sample-exact" % (checked - 1)}
+    gen = None
+    rest = verify_frames(v, oracle, dev, frames, refs, geom, args, slots_run, range(n, want))
+    bad += rest["mismatched"]
+    checked = min(n, want) * slots_run + rest["frames"]
+    verify = {"frames": checked, "of": nf * slots_run, "mismatched": bad, "slots": slots_run,
+              "poisoned": True,
+              "what": "visible Y/U/V of frames 0..%d (decode order) of each of the %d batch slot(s) the timed "
+                      "steps wrote (every frame buffer filled with 0x%02X before them) vs the CPU oracle, "
+                      "sample-exact" % (want - 1, slots_run, POISON)}
     if not bounded:
         return None, verify
     one = n / t_or
@@ -429,6 +565,21 @@ def cpu_baseline(v, oracle, dev, frames, refs, geom, args):
         t0 = time.perf_counter()
         done = sum(ex.map(run_unit, work))
         par = done / (time.perf_counter() - t0)
+    # leg 4: the same pool over every host thread the box reports (nproc); the cgroup's CPU
+    # quota, when there is one, bounds what these threads get
+    nall = os.cpu_count() or 1
+    eff = min(x for x in (nall, info["cpu_quota"], info["affinity"]) if x)   # CPUs the threads can get
+    par_all, all_note = None, None
+    work_all = (units * max(1, -(-nall // len(units))))[:nall]       # one unit per thread
+    est = len(work_all) * per_unit / eff
+    if nall > thr and est > 2 * budget:
+        all_note = "skipped: %d %s on %d threads would take ~%.0f s on %.4g CPUs" % (
+            len(work_all), "keyframes" if gop == 1 else "GOP chains", nall, est, eff)
+    elif nall > thr:
+        with concurrent.futures.ThreadPoolExecutor(nall) as ex:
+            t0 = time.perf_counter()
+            done = sum(ex.map(run_unit, work_all))
+            par_all = done / (time.perf_counter() - t0)
     legs = [
         {"leg": "1 thread", "value": round(one, 3), "cores": 1,
          "sample": "%d frames in decode order" % n},
@@ -438,9 +589,16 @@ def cpu_baseline(v, oracle, dev, frames, refs, geom, args):
         {"leg": "%s-parallel" % ("frame" if gop == 1 else "GOP"), "value": round(par, 3), "cores": thr,
          "sample": "%d %s on %d threads" % (len(work), "keyframes" if gop == 1 else "GOP chains", thr)},
     ]
+    if par_all is not None or all_note:
+        legs.append({"leg": "%s-parallel, all host threads" % ("frame" if gop == 1 else "GOP"),
+                     "value": None if par_all is None else round(par_all, 3), "cores": nall,
+                     "sample": all_note or "%d %s on %d threads (nproc); cgroup CPU quota %s, affinity %s CPUs"
+                               % (len(work_all), "keyframes" if gop == 1 else "GOP chains", nall, info["cpu_quota"],
+                                  info["affinity"])})
     cpu = {"value": round(par, 3), "unit": "frames/s", "cores": thr, "kind": "port",
-           "sample": "%s %s frames, scalar C oracle (reconstruction + loop filter from the same pass-1 packets, "
-                     "host entropy decode excluded), %s-parallel over %d of the %s host threads"
+           "sample": "%s %s frames, scalar C oracle (the build's restatement, without the reference's SIMD; "
+                     "reconstruction + loop filter from the same pass-1 packets, host entropy decode excluded), "
+                     "%s-parallel over %d of the %s host threads"
                      % (len(work) if gop == 1 else sum(len(u) for u in work), args.config,
                         "frame" if gop == 1 else "GOP", thr, info["nproc"]),
            "legs": legs, "host": info}

@@ -109,6 +109,7 @@ ABI_SYMBOLS = ["vp9hip_open", "vp9hip_close", "vp9hip_configure", "vp9hip_submit
                "vp9hip_alg_bytes", "vp9hip_plan_stats", "vp9hip_abi_version", "vp9hip_set_graph",
                "vp9hip_stage_batch_tiles", "vp9hip_batch_phases", "vp9hip_phase_frames", "vp9hip_run_phase",
                "vp9hip_stripe", "vp9hip_frame_device", "vp9hip_batch_groups", "vp9hip_set_batch_slot", "vp9hip_sync_slot", "vp9hip_slot_busy",
+               "vp9hip_fill_buffers", "vp9hip_device_info",
                "vp9h_decode_frame", "vp9h_encode_frame", "vp9h_frame_free", "vp9h_buffer_free",
                "vp9h_stream_open", "vp9h_stream_close", "vp9h_stream_decode", "vp9h_stream_encode",
                "vp9h_enc_defaults", "vp9h_superframe_split", "vp9h_frame_type",
@@ -151,6 +152,8 @@ def lib():
     L.vp9hip_frame_device.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_ssize_t),
                                        ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                                        ctypes.POINTER(ctypes.c_void_p)]
+    L.vp9hip_device_info.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+    L.vp9hip_fill_buffers.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int]
     L.vp9hip_run_batch.argtypes = [vp]
     L.vp9hip_sync.argtypes = [vp]
     L.vp9hip_download_frame.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
@@ -420,6 +423,13 @@ def decode_frame(data):
     return DecodedFrame(data)
 
 
+def device_info(device):
+    """(PCI bus id, name) of HIP device `device` (vp9hip_device_info)."""
+    bus, name = ctypes.create_string_buffer(64), ctypes.create_string_buffer(256)
+    _check("vp9hip_device_info", lib().vp9hip_device_info(device, bus, 64, name, 256))
+    return bus.value.decode(), name.value.decode()
+
+
 class Device:
     """A vp9hip context on one GPU (vp9hip_open / vp9hip_configure)."""
 
@@ -507,6 +517,14 @@ class Device:
 
     def sync(self):
         _check("vp9hip_sync", lib().vp9hip_sync(self._c))
+
+    def sync_slot(self, slot):
+        """Wait for batch slot `slot`'s last run and check its loop-filter hand-offs."""
+        _check("vp9hip_sync_slot", lib().vp9hip_sync_slot(self._c, int(slot)))
+
+    def fill(self, buf0, count, value):
+        """Fill device buffers [buf0, buf0 + count) with byte `value` (async, context stream)."""
+        _check("vp9hip_fill_buffers", "vp9hip_device_info", lib().vp9hip_fill_buffers(self._c, int(buf0), int(count), int(value)))
 
     def set_timing(self, on):
         _check("vp9hip_set_timing", lib().vp9hip_set_timing(self._c, int(bool(on))))

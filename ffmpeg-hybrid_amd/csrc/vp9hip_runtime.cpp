@@ -261,6 +261,20 @@ static void free_bufs(vp9hip_ctx *c)
     c->buf_wh.clear();
 }
 
+// Forget the staged batches of both slots (their FrameDescs, graphs and launch lists name
+// frame buffers): a later run_batch of either slot needs a new stage. The caller has
+// synchronised the main and planner streams.
+static void drop_slots(vp9hip_ctx *c)
+{
+    for (Staged *g : { &c->stg, &c->alt }) {
+        g->ready = false;
+        g->planned = false;
+        if (g->graph) hipGraphExecDestroy(g->graph);
+        g->graph = nullptr;
+        g->graph_launches.clear();
+    }
+}
+
 extern "C" void vp9hip_close(vp9hip_ctx *c)
 {
     if (!c) return;
@@ -383,6 +397,8 @@ extern "C" int vp9hip_configure(vp9hip_ctx *c, int width, int height, int bpp, i
     if (ss_h < 0 || ss_h > 1 || ss_v < 0 || ss_v > 1) return VP9HIP_EINVAL;   // 4:2:0 / 4:2:2 / 4:4:0 / 4:4:4
     hipSetDevice(c->dev);
     hipStreamSynchronize(c->st);
+    hipStreamSynchronize(c->pst);
+    drop_slots(c);                      // both slots' records point at the buffers freed here
     free_bufs(c);
     c->w = width; c->h = height; c->bpp = bpp; c->ss_h = ss_h; c->ss_v = ss_v;
     c->hb = bpp > 8; c->bypp = c->hb ? 2 : 1;
@@ -402,7 +418,6 @@ extern "C" int vp9hip_configure(vp9hip_ctx *c, int width, int height, int bpp, i
         c->bufs.push_back(b);
         c->buf_wh.push_back({ width, height });
     }
-    c->stg.ready = false;
     int r = upload_ptab(c);
     if (!r) r = upload_nz(c);
     if (r) return r;
@@ -2202,7 +2217,9 @@ extern "C" int vp9hip_sync(vp9hip_ctx *c)
     if (!c) return VP9HIP_EINVAL;
     hipSetDevice(c->dev);
     HIPCHK(hipStreamSynchronize(c->st));
+    // every slot's pixel work is on the main stream: both slots' hand-off counters are final
     if (const int r = check_lfr(c->stg)) return r;
+    if (const int r = check_lfr(c->alt)) return r;
     if (c->timing && c->timed_run && c->stg.ready) {
         for (int k = 0; k < K_N; k++) { c->kms[k] = 0; c->kcount[k] = 0; }
         for (size_t i = 0; i < c->stg.launches.size() && 2 * i + 1 < c->ev.size(); i++) {
@@ -2283,7 +2300,16 @@ extern "C" int vp9hip_flush(vp9hip_ctx *c)
     if (!c) return VP9HIP_EINVAL;
     hipSetDevice(c->dev);
     HIPCHK(hipStreamSynchronize(c->st));
-    c->stg.ready = false;
+    HIPCHK(hipStreamSynchronize(c->pst));
+    drop_slots(c);
+    return 0;
+}
+
+extern "C" int vp9hip_fill_buffers(vp9hip_ctx *c, int buf0, int count, int value)
+{
+    if (!c || buf0 < 0 || count < 0 || buf0 + count > (int) c->bufs.size()) return VP9HIP_EINVAL;
+    hipSetDevice(c->dev);
+    for (int i = buf0; i < buf0 + count; i++) HIPCHK(hipMemsetAsync(c->bufs[i], value & 255, c->buf_bytes, c->st));
     return 0;
 }
 
@@ -2323,6 +2349,19 @@ extern "C" int vp9hip_set_graph(vp9hip_ctx *c, int on)
 }
 
 extern "C" int vp9hip_abi_version(void) { return VP9HIP_ABI_VERSION; }
+
+extern "C" int vp9hip_device_info(int device, char *pci_bus_id, int len, char *name, int name_len)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return VP9HIP_ENOSYS;
+    if (pci_bus_id && len > 0) HIPCHK(hipDeviceGetPCIBusId(pci_bus_id, len, device));
+    if (name && name_len > 0) {
+        hipDeviceProp_t p;
+        HIPCHK(hipGetDeviceProperties(&p, device));
+        snprintf(name, (size_t) name_len, "%s (%s)", p.name, p.gcnArchName);
+    }
+    return 0;
+}
 
 // Two batch slots per context: stage / run / sync / phase calls act on the current slot.
 // Each slot has its own arena, plan and graph; the frame buffers are the context's. A run of

@@ -179,8 +179,9 @@ int  vp9hip_set_batch_slot(vp9hip_ctx *ctx, int slot);
 int  vp9hip_sync_slot(vp9hip_ctx *ctx, int slot);
 /* 1 while the last run of batch slot `slot` is still executing, 0 once it is done. */
 int  vp9hip_slot_busy(vp9hip_ctx *ctx, int slot);
-/* Wait for all queued work. VP9HIP_EBUG if a row-pipelined loop-filter launch (k_lfr)
- * gave up a bounded wait on another workgroup's progress (frames not trusted). */
+/* Wait for all queued work of both batch slots. VP9HIP_EBUG if a row-pipelined
+ * loop-filter launch (k_lfr) of either slot gave up a bounded wait on another workgroup's
+ * progress (frames not trusted). */
 int  vp9hip_sync(vp9hip_ctx *ctx);
 
 /* Copy device buffer `buf` into host planes (linesize in bytes). Synchronous. */
@@ -201,8 +202,12 @@ int  vp9hip_frame_device(vp9hip_ctx *ctx, int buf, void *planes[3], ptrdiff_t li
 int  vp9hip_upload_frame(vp9hip_ctx *ctx, int buf, const uint8_t *const planes[3],
                          const ptrdiff_t linesize[3]);
 
-/* Drop queued work and staged batches (FFHWAccel.flush). */
+/* Drop queued work and the staged batches of both slots (FFHWAccel.flush). */
 int  vp9hip_flush(vp9hip_ctx *ctx);
+/* Fill device buffers [buf0, buf0 + count) with the byte `value`, asynchronously on the
+ * context's stream (the bench poisons its frame buffers before the timed steps, so the
+ * frames it verifies afterwards were written by those steps). No reference counterpart. */
+int  vp9hip_fill_buffers(vp9hip_ctx *ctx, int buf0, int count, int value);
 
 /*
  * Per-kernel timing of the last run (HIP events on the execution stream):
@@ -230,6 +235,9 @@ int  vp9hip_alg_bytes(vp9hip_ctx *ctx, double *bytes, int cap);
 int  vp9hip_plan_stats(const vp9h_frame *pkt, double *out, int cap);
 
 int  vp9hip_abi_version(void);
+/* PCI bus id ("0000:75:00.0") and name of HIP device `device` (so a multi-GPU run can show
+ * each rank on its own card). VP9HIP_ENOSYS if there is no such device. */
+int  vp9hip_device_info(int device, char *pci_bus_id, int len, char *name, int name_len);
 
 /* ---- synthetic pass-1 generator (test / bench input) -------------------- */
 /*

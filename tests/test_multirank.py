@@ -60,3 +60,31 @@ def test_single_rank_aggregate_is_identity():
     assert b.reduce_elapsed(3.0, None) == 3.0
     fps, ms = b.aggregate(120, 4, 1, 2.0)
     assert fps == pytest.approx(240.0) and ms == pytest.approx(500.0)
+
+
+@pytest.mark.gpu
+def test_two_rank_bench_verifies_every_rank():
+    """bench.py at world 2 as the driver launches it (torch.distributed.run, one process per
+    rank; both ranks share the box's one GPU here): every rank decodes its own frames after a
+    poison fill and compares a sample of them with the oracle; rank 0 reports each rank's
+    result and device."""
+    import json
+    import subprocess
+    import sys
+    port = 29700 + os.getpid() % 200
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--frames", "8", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith('{"metric"')]
+    assert len(line) == 1
+    d = json.loads(line[0])
+    assert d["n_gpus"] == 2
+    v = d["verify"]
+    assert v["mismatched"] == []
+    assert [p["rank"] for p in v["per_rank"]] == [0, 1]
+    assert all(p["frames"] == 2 * 2 for p in v["per_rank"])          # 2 frames x 2 batch slots per rank
+    assert d["verified_frames"] == 8
+    assert [x["rank"] for x in d["config"]["ranks"]] == [0, 1]
+    assert all(x["pci_bus_id"] for x in d["config"]["ranks"])

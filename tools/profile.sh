@@ -17,3 +17,7 @@ run sq --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST
 run lds --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM SQ_WAIT_INST_LDS SQ_BUSY_CYCLES
 run fetch --pmc FETCH_SIZE
 run write --pmc WRITE_SIZE
+python3 "$ROOT/tools/traffic.py" "$OUT" "$OUT/traffic.json" > /dev/null
+python3 "$ROOT/tools/pmc_summary.py" "$OUT" > "$OUT/pmc_summary.txt"
+echo "[profile] summaries written"
+

@@ -33,9 +33,25 @@ def main(d, out=None):
         wr = sum(c["WRITE_SIZE"]) / max(1, len(c["WRITE_SIZE"]))
         res[k] = {"fetch_bytes": fe, "fetch_corrected": 2 * fe, "write_bytes": wr,
                   "traffic_bytes": 2 * fe + wr, "launches": len(c["FETCH_SIZE"])}
-    print(json.dumps(res, indent=1))
+    # the launch shape the counters were taken at (bench.py refuses a profile whose shape
+    # differs from its own run): the bench line the profiled runs printed
+    shape, bench = {}, None
+    for f in sorted(glob.glob(os.path.join(d, "*.log"))):
+        for line in open(f, errors="replace"):
+            if line.startswith('{"metric"'):
+                bench = json.loads(line)
+        if bench:
+            break
+    if bench:
+        kl = bench["roofline"]["kernel_launches"]
+        for k in res:
+            if k in kl:
+                shape[k] = {"launches_per_step": kl[k], "streams_per_gpu": bench["config"]["streams_per_gpu"],
+                            "frames_per_gpu": bench["config"]["frames_per_gpu"]}
+    print(json.dumps({"per_launch": res, "shape": shape}, indent=1))
     if out:
-        json.dump({"source": d, "per_launch": res}, open(out, "w"), indent=1)
+        json.dump({"source": d, "per_launch": res, "shape": shape,
+                   "bench_workload": bench["config"]["workload"] if bench else None}, open(out, "w"), indent=1)
 
 
 if __name__ == "__main__":
