@@ -633,8 +633,8 @@ def host_entropy_rate(v, gops, gop, args):
     import concurrent.futures
     n = sum(len(g) for g in gops)
 
-    def decode_gop(datas):
-        dec = v.Stream()
+    def decode_gop(datas, tile_threads=1):
+        dec = v.Stream(threads=tile_threads)
         for d in datas:
             dec.decode(d)
         return len(datas)
@@ -650,7 +650,20 @@ def host_entropy_rate(v, gops, gop, args):
     with concurrent.futures.ThreadPoolExecutor(threads) as ex:
         t0 = time.perf_counter()
         many = sum(ex.map(decode_gop, gops * reps)) / (time.perf_counter() - t0)
+    # one stream at a time, its frames' tile columns on threads (decode_tiles_mt,
+    # vp9.c:1441-1520): the rate of a single GOP chain, which GOP-parallel parsing cannot raise
+    ntc = 1 << CONFIGS[args.config][4]
+    tiles = None
+    if ntc > 1:
+        tt = min(threads, ntc)
+        t0 = time.perf_counter()
+        done = k = 0
+        while time.perf_counter() - t0 < args.cpu_seconds / 4 or k < len(gops):
+            done += decode_gop(gops[k % len(gops)], tt)
+            k += 1
+        tiles = {"fps": round(done / (time.perf_counter() - t0), 2), "tile_threads": tt}
     return {"fps_1_thread": round(one, 2), "fps_threads": round(many, 2), "threads": threads,
+            "tile_threaded": tiles,
             "bytes_per_frame": int(sum(len(d) for g in gops for d in g) / n),
             "sample": "%d synthetic %s frames as a VP9 stream (%s), parsed to pass-1 packets"
                       % (n, args.config, "keyframes" if gop == 1 else "GOPs of %d" % gop)}

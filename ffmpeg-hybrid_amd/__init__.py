@@ -111,7 +111,7 @@ ABI_SYMBOLS = ["vp9hip_open", "vp9hip_close", "vp9hip_configure", "vp9hip_submit
                "vp9hip_stripe", "vp9hip_frame_device", "vp9hip_batch_groups", "vp9hip_set_batch_slot", "vp9hip_sync_slot", "vp9hip_slot_busy",
                "vp9hip_fill_buffers", "vp9hip_device_info",
                "vp9h_decode_frame", "vp9h_encode_frame", "vp9h_frame_free", "vp9h_buffer_free",
-               "vp9h_stream_open", "vp9h_stream_close", "vp9h_stream_decode", "vp9h_stream_encode",
+               "vp9h_stream_open", "vp9h_stream_close", "vp9h_stream_set_threads", "vp9h_stream_decode", "vp9h_stream_encode",
                "vp9h_enc_defaults", "vp9h_superframe_split", "vp9h_frame_type",
                "vp9hip_synth_defaults", "vp9hip_synth_frame", "vp9hip_synth_free",
                "vp9h_ivf_probe", "vp9h_ivf_read_header", "vp9h_ivf_read_frame", "vp9h_ivf_write_header",
@@ -178,6 +178,7 @@ def lib():
     L.vp9h_buffer_free.argtypes = [ctypes.c_void_p]
     L.vp9h_buffer_free.restype = None
     L.vp9h_stream_open.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+    L.vp9h_stream_set_threads.argtypes = [ctypes.c_void_p, ctypes.c_int]
     L.vp9h_stream_close.argtypes = [ctypes.c_void_p]
     L.vp9h_stream_close.restype = None
     L.vp9h_stream_decode.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(FramePacket),
@@ -346,9 +347,15 @@ def enc_params(**kw):
 class Stream:
     """A stream's host parse state (vp9h_stream): decode or encode frames in order."""
 
-    def __init__(self):
+    def __init__(self, threads=1):
         self._s = ctypes.c_void_p()
         _check("vp9h_stream_open", lib().vp9h_stream_open(ctypes.byref(self._s)))
+        if threads != 1:
+            self.set_threads(threads)
+
+    def set_threads(self, n):
+        """Tile-column threads of decode (vp9h_stream_set_threads)."""
+        _check("vp9h_stream_set_threads", lib().vp9h_stream_set_threads(self._s, int(n)))
 
     def close(self):
         if self._s:

@@ -27,6 +27,7 @@
  * Scope: profiles 0-3 (4:2:0 / 4:2:2 / 4:4:0 / 4:4:4, 8/10/12-bit; RGB parses as 4:4:4).
  * The encoder never sends loop-filter delta updates or segmentation.
  */
+#include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -350,6 +351,7 @@ typedef struct Hdr {
 } Hdr;
 
 struct vp9h_stream {
+    int tile_threads;                    /* decode: tile columns walked concurrently (1: serial) */
     Hdr h;
     SavedCtx ctx[4];
     struct { int valid, w, h, bpp, ss_h, ss_v; } slot[8];
@@ -371,6 +373,7 @@ int vp9h_stream_open(vp9h_stream **out)
     if (!s) return VP9HIP_ENOMEM;
     for (int i = 0; i < 4; i++) ctx_reset(&s->ctx[i]);
     s->h.sharpness = -1;
+    s->tile_threads = 1;
     *out = s;
     return 0;
 }
@@ -1950,11 +1953,30 @@ static void free_ctx(Walk *w)
     free(w->a_segpred); free(w->a_intra); free(w->a_comp); free(w->a_ref); free(w->a_filter); free(w->a_mv);
 }
 
+/* One SB row of one tile: the left contexts restart (vp9.c:1358-1366), then its SBs. */
+static int walk_tile_row(Walk *w, BC *coder, int row, int c0, int c1)
+{
+    const int intra_frame = w->h->keyframe || w->h->intraonly;
+    w->tile_col_start = c0;
+    memset(w->l_part, 0, sizeof(w->l_part)); memset(w->l_skip, 0, sizeof(w->l_skip));
+    if (intra_frame) memset(w->l_mode, 2, sizeof(w->l_mode));
+    else memset(w->l_mode, VP9H_NEARESTMV, 8);
+    memset(w->l_ynnz, 0, sizeof(w->l_ynnz)); memset(w->l_unnz, 0, sizeof(w->l_unnz));
+    memset(w->l_vnnz, 0, sizeof(w->l_vnnz)); memset(w->l_segpred, 0, sizeof(w->l_segpred));
+    w->c = coder;
+    for (int col = c0; col < c1; col += 8) {
+        /* a tile whose data ran out is invalid (vp9.c:1383-1385) */
+        if (!w->c->enc && bd_overrun(&w->c->d) > 10) { w->err = 1; return -1; }
+        walk_sb(w, row, col, 0);
+        if (w->err) return -1;
+    }
+    return 0;
+}
+
 /* Walk every tile (vp9.c:1325-1395): per tile row, SB rows, tile columns, SBs. */
 static int walk_tiles(Walk *w, BC *coders)
 {
     const int ntc = 1 << w->h->log2_tile_cols, ntr = 1 << w->h->log2_tile_rows;
-    const int intra_frame = w->h->keyframe || w->h->intraonly;
     for (int tr = 0; tr < ntr; tr++) {
         int r0, r1;
         tile_offsets(tr, w->h->log2_tile_rows, w->sb_rows, &r0, &r1);
@@ -1962,21 +1984,124 @@ static int walk_tiles(Walk *w, BC *coders)
             for (int tc = 0; tc < ntc; tc++) {
                 int c0, c1;
                 tile_offsets(tc, w->h->log2_tile_cols, w->sb_cols, &c0, &c1);
-                w->tile_col_start = c0;
-                memset(w->l_part, 0, sizeof(w->l_part)); memset(w->l_skip, 0, sizeof(w->l_skip));
-                if (intra_frame) memset(w->l_mode, 2, sizeof(w->l_mode));
-                else memset(w->l_mode, VP9H_NEARESTMV, 8);
-                memset(w->l_ynnz, 0, sizeof(w->l_ynnz)); memset(w->l_unnz, 0, sizeof(w->l_unnz));
-                memset(w->l_vnnz, 0, sizeof(w->l_vnnz)); memset(w->l_segpred, 0, sizeof(w->l_segpred));
-                w->c = &coders[tr * ntc + tc];
-                for (int col = c0; col < c1; col += 8) {
-                    /* a tile whose data ran out is invalid (vp9.c:1383-1385) */
-                    if (!w->c->enc && bd_overrun(&w->c->d) > 10) { w->err = 1; return -1; }
-                    walk_sb(w, row, col, 0);
-                    if (w->err) return -1;
-                }
+                if (walk_tile_row(w, &coders[tr * ntc + tc], row, c0, c1) < 0) return -1;
             }
     }
+    return 0;
+}
+
+/* ---- tile-column threads (decode_tiles_mt, vp9.c:1441-1520; launched at 1777-1806) ----
+ * A tile column decodes independently of the others: its blocks read above / left
+ * contexts and MV candidates of its own columns only (have_left and the candidate checks
+ * stop at tile_col_start, vp9mvs.c / vp9block.c), and its bool coders are its own. Each
+ * column walks all tile rows on a copy of the frame's walk state with its own left
+ * contexts, coder, symbol counts and output arrays; the above contexts and the frame's MV /
+ * segmentation arrays are shared, written at the column's own positions only. The packet
+ * keeps the serial walk's order: per SB row, the tile columns' segments left to right. */
+typedef struct TileCol {
+    Walk w;
+    BC *coders;
+    int tc, ntc, ntr;
+    size_t *seg;                         /* per SB row of the frame: (nb, ne, nc) at its end */
+    int ret;
+} TileCol;
+
+static void *tile_col_run(void *arg)
+{
+    TileCol *t = arg;
+    Walk *w = &t->w;
+    int c0, c1;
+    tile_offsets(t->tc, w->h->log2_tile_cols, w->sb_cols, &c0, &c1);
+    for (int tr = 0; tr < t->ntr && !t->ret; tr++) {
+        int r0, r1;
+        tile_offsets(tr, w->h->log2_tile_rows, w->sb_rows, &r0, &r1);
+        for (int row = r0; row < r1; row += 8) {
+            if (walk_tile_row(w, &t->coders[tr * t->ntc + t->tc], row, c0, c1) < 0) { t->ret = -1; break; }
+            size_t *e = t->seg + 3 * (row >> 3);
+            e[0] = w->nb; e[1] = w->ne; e[2] = w->nc;
+        }
+    }
+    return NULL;
+}
+
+typedef struct TileWorker { TileCol *cols; int first, step, n; } TileWorker;
+static void *tile_worker_run(void *arg)
+{
+    TileWorker *k = arg;
+    for (int i = k->first; i < k->n; i += k->step) tile_col_run(&k->cols[i]);
+    return NULL;
+}
+
+static int walk_tiles_mt(Walk *w, BC *coders, int nthreads)
+{
+    const int ntc = 1 << w->h->log2_tile_cols, ntr = 1 << w->h->log2_tile_rows, nsr = w->sb_rows;
+    TileCol *cols = calloc((size_t) ntc, sizeof(TileCol));
+    size_t *segs = calloc((size_t) ntc * nsr * 3, sizeof(size_t));
+    pthread_t th[64];
+    TileWorker wk[64];
+    int r = cols && segs ? 0 : -1, started = 0;
+    nthreads = MIN(MIN(nthreads, ntc), 64);
+    for (int tc = 0; tc < ntc && !r; tc++) {
+        TileCol *t = &cols[tc];
+        t->w = *w;                       /* shared: header, probabilities, above contexts, side buffers */
+        memset(&t->w.cnt, 0, sizeof(t->w.cnt));
+        t->w.blocks = NULL; t->w.nb = t->w.cb = 0;
+        t->w.eobs = NULL; t->w.ne = t->w.ce = 0;
+        t->w.coefs = NULL; t->w.nc = t->w.cc = 0;
+        t->w.err = 0;
+        t->coders = coders; t->tc = tc; t->ntc = ntc; t->ntr = ntr;
+        t->seg = segs + (size_t) tc * nsr * 3;
+    }
+    for (int k = 1; k < nthreads && !r; k++) {
+        wk[k] = (TileWorker) { cols, k, nthreads, ntc };
+        if (pthread_create(&th[k], NULL, tile_worker_run, &wk[k])) break;
+        started = k;
+    }
+    if (!r)                              /* this thread's share, and that of any thread that did not start */
+        for (int k = 0; k < nthreads; k++)
+            if (k == 0 || k > started) {
+                wk[k] = (TileWorker) { cols, k, nthreads, ntc };
+                tile_worker_run(&wk[k]);
+            }
+    for (int k = 1; k <= started; k++) pthread_join(th[k], NULL);
+    for (int tc = 0; tc < ntc && !r; tc++)
+        if (cols[tc].ret || cols[tc].w.err) { r = -1; w->err = cols[tc].w.err ? cols[tc].w.err : 1; }
+    if (!r) {                            /* concatenate in the serial order: SB rows, then tile columns */
+        size_t nb = 0, ne = 0, nc = 0;
+        for (int tc = 0; tc < ntc; tc++) { nb += cols[tc].w.nb; ne += cols[tc].w.ne; nc += cols[tc].w.nc; }
+        w->blocks = grow(w->blocks, &w->cb, w->nb + nb, sizeof(vp9h_block), &w->err);
+        w->eobs = grow(w->eobs, &w->ce, w->ne + ne, sizeof(uint16_t), &w->err);
+        w->coefs = grow(w->coefs, &w->cc, w->nc + nc, 1, &w->err);
+        if (w->err) r = -1;
+        for (int sr = 0; sr < nsr && !r; sr++)
+            for (int tc = 0; tc < ntc; tc++) {
+                const Walk *t = &cols[tc].w;
+                const size_t *e = cols[tc].seg + 3 * sr, *p = sr ? e - 3 : NULL;
+                const size_t b0 = p ? p[0] : 0, e0 = p ? p[1] : 0, k0 = p ? p[2] : 0;
+                memcpy(w->blocks + w->nb, t->blocks + b0, (e[0] - b0) * sizeof(vp9h_block));
+                memcpy(w->eobs + w->ne, t->eobs + e0, (e[1] - e0) * sizeof(uint16_t));
+                memcpy(w->coefs + w->nc, t->coefs + k0, e[2] - k0);
+                w->nb += e[0] - b0; w->ne += e[1] - e0; w->nc += e[2] - k0;
+            }
+        /* the columns' symbol counts (backward adaptation reads their sum, vp9prob.c) */
+        unsigned *dst = (unsigned *) &w->cnt;
+        for (int tc = 0; tc < ntc && !r; tc++) {
+            const unsigned *src = (const unsigned *) &cols[tc].w.cnt;
+            for (size_t i = 0; i < sizeof(Counts) / sizeof(unsigned); i++) dst[i] += src[i];
+        }
+    }
+    for (int tc = 0; cols && tc < ntc; tc++) {
+        free(cols[tc].w.blocks); free(cols[tc].w.eobs); free(cols[tc].w.coefs);
+    }
+    free(cols);
+    free(segs);
+    return r;
+}
+
+int vp9h_stream_set_threads(vp9h_stream *s, int n)
+{
+    if (!s || n < 1 || n > 64) return VP9HIP_EINVAL;
+    s->tile_threads = n;
     return 0;
 }
 
@@ -2141,7 +2266,8 @@ int vp9h_stream_decode(vp9h_stream *st, const uint8_t *data, size_t size, vp9h_f
         p += n;
     }
     if (!r) save_forward_ctx(w);
-    if (!r && walk_tiles(w, coders) < 0) r = w->err ? VP9HIP_EINVALIDDATA : VP9HIP_ENOMEM;
+    if (!r && (st->tile_threads > 1 && ntc > 1 ? walk_tiles_mt(w, coders, st->tile_threads) : walk_tiles(w, coders)) < 0)
+        r = w->err ? VP9HIP_EINVALIDDATA : VP9HIP_ENOMEM;
     free(coders);
     if (!r) {
         end_frame(w);

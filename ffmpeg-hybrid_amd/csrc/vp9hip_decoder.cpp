@@ -23,6 +23,7 @@
 //   3. receive_frame hands out frames whose batch has been launched, in output order.
 // Like libavcodec's frame threading this adds decoder delay (up to max_batch frames plus
 // the frames in parse); flushing (send_packet with data = NULL) drains it.
+#include <algorithm>
 #include <condition_variable>
 #include <cstring>
 #include <deque>
@@ -85,6 +86,7 @@ struct vp9hip_decoder {
     std::deque<std::shared_ptr<Chain>> runq;
     std::vector<std::thread> workers;
     bool stop = false;
+    int active = 0;                                   // chains being parsed by a worker
     int max_inflight = 0;
 };
 
@@ -108,6 +110,10 @@ static void parse_one(ParseJob *j)
     j->ret = vp9h_stream_decode(j->chain->st, j->data.data(), j->data.size(), &j->pkt, &j->info);
 }
 
+// A worker parses one chain's frames in order. The pool's threads are shared out over
+// the chains that have work: a chain parsing alone (one GOP, or the last of a drain)
+// walks its frames' tile columns on the idle threads' share (vp9h_stream_set_threads,
+// decode_tiles_mt), frame-parallel keyframe streams keep one thread per frame.
 static void worker_main(vp9hip_decoder *d)
 {
     std::unique_lock<std::mutex> lk(d->mu);
@@ -116,15 +122,19 @@ static void worker_main(vp9hip_decoder *d)
         if (d->stop) return;
         std::shared_ptr<Chain> c = d->runq.front();
         d->runq.pop_front();
+        d->active++;
         while (!c->q.empty()) {                       // the chain's frames, in order
             ParseJob *j = c->q.front();
             c->q.pop_front();
+            const int share = (int) d->workers.size() / std::max<int>(1, d->active + (int) d->runq.size());
             lk.unlock();
+            vp9h_stream_set_threads(c->st, std::max(1, std::min(share, 16)));
             parse_one(j);
             lk.lock();
             j->done = true;
             d->cv_done.notify_all();
         }
+        d->active--;
         c->scheduled = false;
     }
 }

@@ -298,6 +298,11 @@ typedef struct vp9h_stream vp9h_stream;
 int  vp9h_stream_open(vp9h_stream **out);
 void vp9h_stream_close(vp9h_stream *s);
 
+/* Tile-column threads of vp9h_stream_decode (default 1): the tile columns of a frame are
+ * entropy-decoded concurrently, as decode_tiles_mt does with slice threads
+ * (vp9.c:1441-1520, launched at 1777-1806). The packet is the serial walk's, byte for byte. */
+int  vp9h_stream_set_threads(vp9h_stream *s, int n);
+
 /* What the frame header decided beyond the packet (reference slot bookkeeping for the
  * device buffers, vp9.c:1686-1691, 1845-1849). */
 typedef struct vp9h_frame_info {

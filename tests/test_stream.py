@@ -314,3 +314,44 @@ def test_inter_bitstream_to_gpu_matches_oracle(v9, orc, gpu, ssh, ssv):
         got = gpu.download(i)
         for a, b in zip(v9.visible(got, w, h, ssh, ssv), v9.visible(oracle[i], w, h, ssh, ssv)):
             assert np.array_equal(a, b), "frame %d" % i
+
+
+TILE_STREAMS = [
+    ("keyframes_8_cols", dict(w=2048, h=200, n=2, log2_tile_cols=3), None, 0),
+    ("inter_4_cols", dict(w=1024, h=136, n=4, log2_tile_cols=2, compound=1), None, 0),
+    ("adaptation_4_cols", dict(w=1024, h=200, n=4, log2_tile_cols=2, compound=1),
+     lambda i: {"refresh_ctx": 1, "parallel": 0, "ctx_id": i % 4, "prob_updates": 3 + i}, 0),
+    ("tile_rows", dict(w=1024, h=520, n=3, log2_tile_cols=2), lambda i: {"refresh_ctx": 1, "parallel": 0}, 1),
+]
+
+
+@pytest.mark.parametrize("name,shape,per_frame,log2_rows", TILE_STREAMS, ids=[s[0] for s in TILE_STREAMS])
+@pytest.mark.parametrize("threads", [2, 3, 8])
+def test_tile_threaded_parse_equals_serial(v9, name, shape, per_frame, log2_rows, threads):
+    """vp9h_stream_set_threads (decode_tiles_mt, vp9.c:1441-1520): the tile columns parsed on
+    `threads` threads give the serial walk's packet, field by field, including the symbol
+    counts that backward adaptation sums over the columns (the next frame parses with the
+    adapted probabilities) and tile rows (each column walks every tile row)."""
+    shape = dict(shape)
+    frames = _frames(v9, shape.pop("w"), shape.pop("h"), shape.pop("n"), **shape)
+    for f in frames:
+        f.pkt.log2_tile_rows = log2_rows
+    datas, coded = encode_stream(v9, frames, per_frame)
+    serial = v9.Stream()
+    par = v9.Stream(threads=threads)
+    for d, c in zip(datas, coded):
+        (p0, i0), (p1, i1) = serial.decode(d), par.decode(d)
+        same_packet(p0.pkt, c.pkt)
+        same_packet(p1.pkt, p0.pkt)
+        assert p1.pkt.log2_tile_rows == c.pkt.log2_tile_rows and (c.pkt.log2_tile_rows > 0) == (log2_rows > 0)
+
+
+def test_tile_threaded_parse_rejects_truncated_tiles(v9):
+    """A truncated tile fails the threaded parse with AVERROR_INVALIDDATA, as the serial one."""
+    frames = _frames(v9, 1024, 136, 1, log2_tile_cols=2)
+    datas, _ = encode_stream(v9, frames)
+    d = datas[0][: len(datas[0]) * 3 // 4]
+    for threads in (1, 4):
+        with pytest.raises(v9.Vp9HipError) as e:
+            v9.Stream(threads=threads).decode(d)
+        assert e.value.code == v9.EINVALIDDATA
