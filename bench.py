@@ -343,6 +343,13 @@ def main():
         e2e["low_rate"] = e2e_rate(v, lsample, args, local_rank)
         e2e["low_rate"]["bytes_per_frame"] = int(sum(len(d) for g in lsample for d in g) / nlow)
         e2e["low_rate"]["host_parse"] = host_entropy_rate(v, lsample, gop, args)["fps_threads"]
+        # the FFHWAccel surface avcodec_receive_frame() reaches (tests/c/hwaccel_harness plays
+        # vp9.c around it) on the same realistic-density stream, and on a C2 one
+        hw = {args.config: hwaccel_rate(v, lsample, W, H, BPP, args)}
+        if args.config != "C2" and args.chroma == "420":
+            c2f, c2refs, c2geom = make_frames(v, "C2", 32, rank, p_zero_eob=0.9, p_skip=0.7)
+            hw["C2"] = hwaccel_rate(v, encode_sample(v, c2f, 32, 32), 1920, 1080, 8, args)
+        e2e["hwaccel_path"] = hw
 
     out = {
         "metric": "decoded frames/sec (bit-exact) 4K VP9 Profile-0 @ 1/2/4/8 MI355X; % HBM roofline",
@@ -667,6 +674,42 @@ def host_entropy_rate(v, gops, gop, args):
             "bytes_per_frame": int(sum(len(d) for g in gops for d in g) / n),
             "sample": "%d synthetic %s frames as a VP9 stream (%s), parsed to pass-1 packets"
                       % (n, args.config, "keyframes" if gop == 1 else "GOPs of %d" % gop)}
+
+
+def hwaccel_rate(v, gops, W, H, BPP, args):
+    """Frames/s through the FFHWAccel adapter (include/vp9hip_hwaccel.h) driven in vp9.c's
+    call order by tests/c/hwaccel_harness: the sample stream written as IVF, decoded
+    `passes` times (a flush between passes), frames read 16 behind the decoder (FFmpeg's
+    frame-threading delay) by a device consumer (vp9hip_hwframe_sync) and by a download
+    consumer (transfer_data_from: a D2H copy per frame). Host parse on the adapter's pool."""
+    import subprocess
+    import tempfile
+    harness = os.path.join(ROOT, "tests", "c", "hwaccel_harness")
+    if not os.access(harness, os.X_OK):
+        return {"error": "tests/c/hwaccel_harness not built"}
+    pkts = [d for g in gops for d in g]
+    ssh, ssv = CHROMA[args.chroma]
+    out = {"frames_per_pass": len(pkts), "bytes_per_frame": int(sum(map(len, pkts)) / len(pkts)), "lag": 16,
+           "async_depth": 16}
+    with tempfile.TemporaryDirectory() as td:
+        ivf = os.path.join(td, "s.ivf")
+        with open(ivf, "wb") as f:
+            f.write(v.ivf_write(pkts, W, H))
+        for mode in ("device", "download"):
+            passes = 1
+            while True:
+                r = subprocess.run([harness, ivf, "-", str(BPP), str(ssh), str(ssv), str(passes), "16", mode, "16"],
+                                   capture_output=True, text=True, timeout=300)
+                f = r.stdout.split()
+                if r.returncode or len(f) < 4:
+                    out[mode] = {"error": r.stderr.strip()[-300:]}
+                    break
+                n, sec = int(f[1]), float(f[3])
+                if sec >= args.cpu_seconds / 4 or passes >= 64:
+                    out[mode] = {"fps": round(n / sec, 2), "frames": n, "passes": passes}
+                    break
+                passes = min(64, max(passes * 2, int(passes * args.cpu_seconds / 4 / max(sec, 1e-3)) + 1))
+    return out
 
 
 def e2e_rate(v, gops, args, device):

@@ -112,7 +112,8 @@ ABI_SYMBOLS = ["vp9hip_open", "vp9hip_close", "vp9hip_configure", "vp9hip_submit
                "vp9hip_fill_buffers", "vp9hip_device_info",
                "vp9h_decode_frame", "vp9h_encode_frame", "vp9h_frame_free", "vp9h_buffer_free",
                "vp9h_stream_open", "vp9h_stream_close", "vp9h_stream_set_threads", "vp9h_stream_decode", "vp9h_stream_encode",
-               "vp9h_enc_defaults", "vp9h_superframe_split", "vp9h_frame_type",
+               "vp9h_enc_defaults", "vp9h_superframe_split", "vp9h_frame_type", "vp9h_frame_peek",
+               "vp9hip_slot_stream_wait",
                "vp9hip_synth_defaults", "vp9hip_synth_frame", "vp9hip_synth_free",
                "vp9h_ivf_probe", "vp9h_ivf_read_header", "vp9h_ivf_read_frame", "vp9h_ivf_write_header",
                "vp9h_ivf_write_frame_header", "vp9h_webm_probe", "vp9h_webm_read_header", "vp9h_webm_read_frame",
@@ -191,6 +192,8 @@ def lib():
     L.vp9h_superframe_split.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t),
                                         ctypes.POINTER(ctypes.c_size_t), ctypes.c_int]
     L.vp9h_frame_type.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    L.vp9h_frame_peek.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(FrameInfo)]
+    L.vp9hip_slot_stream_wait.argtypes = [vp, ctypes.c_int, ctypes.c_void_p]
     L.vp9h_ivf_probe.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
     L.vp9h_ivf_read_header.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(IvfHeader)]
     L.vp9h_ivf_read_frame.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t),
@@ -735,6 +738,15 @@ class Decoder:
             if got is None:
                 break
             yield got
+
+
+def frame_peek(data):
+    """(type, FrameInfo) from the start of the uncompressed header (vp9h_frame_peek): type 0
+    keyframe, 1 inter, 2 show_existing_frame, 3 intra-only; slot bookkeeping without state."""
+    data = bytes(data)
+    info = FrameInfo()
+    t = _check("vp9h_frame_peek", lib().vp9h_frame_peek(data, len(data), ctypes.byref(info)))
+    return t, info
 
 
 def vp9h_type(data):

@@ -2516,6 +2516,55 @@ int vp9h_frame_type(const uint8_t *data, size_t size)
     return (b >> --pos & 1) ? 1 : 0;                                 /* frame_type: 0 = key */
 }
 
+/* The reference bookkeeping of a frame from its uncompressed header alone (the start of
+ * decode_frame_header, vp9.c:519-611): show_existing_frame / its slot, show_frame,
+ * error_res, and refresh_frame_flags with the LAST / GOLDEN / ALTREF slots (refidx) of an
+ * inter frame. Everything read here precedes the first field that needs stream state, so
+ * it takes no vp9h_stream: what vp9.c knows before ff_thread_finish_setup. */
+int vp9h_frame_peek(const uint8_t *data, size_t size, vp9h_frame_info *info)
+{
+    if (!data || size < 1 || !info) return VP9HIP_EINVAL;
+    memset(info, 0, sizeof(*info));
+    Bits b;
+    memset(&b, 0, sizeof(b));
+    b.in = data; b.in_bits = size * 8;
+    Hdr h;
+    memset(&h, 0, sizeof(h));
+    if (bits_rw(&b, 2, 0) != 2) return VP9HIP_EINVALIDDATA;             /* frame marker */
+    int prof = bits_rw(&b, 1, 0);
+    prof |= bits_rw(&b, 1, 0) << 1;
+    if (prof == 3 && bits_rw(&b, 1, 0)) return VP9HIP_EINVALIDDATA;    /* reserved bit */
+    if (bits_rw(&b, 1, 0)) {                                            /* show_existing_frame */
+        info->show_existing_frame = 1;
+        info->show_slot = bits_rw(&b, 3, 0);
+        info->show_frame = 1;
+        return b.err ? VP9HIP_EINVALIDDATA : 2;
+    }
+    const int key = !bits_rw(&b, 1, 0);
+    info->show_frame = bits_rw(&b, 1, 0);
+    info->error_res = bits_rw(&b, 1, 0);
+    int type = key ? 0 : 1;
+    if (key) {
+        info->refresh_mask = 0xff;
+    } else {
+        const int intraonly = info->show_frame ? 0 : bits_rw(&b, 1, 0);
+        if (!info->error_res) bits_rw(&b, 2, 0);                        /* reset_frame_context */
+        if (intraonly) {
+            if (bits_rw(&b, 24, 0) != 0x498342) return VP9HIP_EINVALIDDATA;
+            if (prof >= 1 && walk_color(&b, &h, prof) < 0) return VP9HIP_EINVALIDDATA;
+            info->refresh_mask = bits_rw(&b, 8, 0);
+            type = 3;
+        } else {
+            info->refresh_mask = bits_rw(&b, 8, 0);
+            for (int i = 0; i < 3; i++) {
+                info->ref_slot[i] = bits_rw(&b, 3, 0);
+                info->sign_bias[i] = bits_rw(&b, 1, 0) && !info->error_res;
+            }
+        }
+    }
+    return b.err ? VP9HIP_EINVALIDDATA : type;
+}
+
 int vp9h_superframe_split(const uint8_t *data, size_t size, size_t *offsets, size_t *sizes, int cap)
 {
     if (!data || size < 1) return VP9HIP_EINVAL;

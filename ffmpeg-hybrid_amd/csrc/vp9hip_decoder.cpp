@@ -33,25 +33,13 @@
 #include <vector>
 
 #include "../../include/vp9hip.h"
+#include "vp9hip_parse.h"
+
+using vp9hip::Chain;
+using vp9hip::ParseJob;
+using vp9hip::ParsePool;
 
 namespace {
-struct ParseJob;
-struct Chain {                         // one parse state: its frames parse in order
-    vp9h_stream *st = nullptr;
-    std::deque<ParseJob *> q;          // queued, not started
-    bool scheduled = false;            // on the run queue or being run by a worker
-    ~Chain() { if (st) vp9h_stream_close(st); }
-};
-struct ParseJob {
-    std::vector<uint8_t> data;
-    int64_t pts = 0;
-    std::shared_ptr<Chain> chain;
-    vp9h_frame pkt;
-    vp9h_frame_info info;
-    int ret = 0;
-    bool done = false;
-    ParseJob() { memset(&pkt, 0, sizeof(pkt)); memset(&info, 0, sizeof(info)); }
-};
 struct Pending { vp9h_frame pkt; int out; int refs[3]; };   // refs: -1 for keyframes / intra-only
 struct Out { int buf; int64_t pts; bool submitted; };
 // Batches are numbered as launched (1, 2, ...) and alternate between the context's two
@@ -81,12 +69,7 @@ struct vp9hip_decoder {
     // parse pipeline
     std::deque<std::unique_ptr<ParseJob>> inflight;   // decode order
     std::shared_ptr<Chain> chain;                     // the chain of the next non-key frame
-    std::mutex mu;
-    std::condition_variable cv_work, cv_done;
-    std::deque<std::shared_ptr<Chain>> runq;
-    std::vector<std::thread> workers;
-    bool stop = false;
-    int active = 0;                                   // chains being parsed by a worker
+    std::unique_ptr<ParsePool> pool;
     int max_inflight = 0;
 };
 
@@ -104,78 +87,24 @@ static int alloc_buffer(vp9hip_decoder *d)
     return -1;
 }
 
-// ---- parse workers ----
-static void parse_one(ParseJob *j)
-{
-    j->ret = vp9h_stream_decode(j->chain->st, j->data.data(), j->data.size(), &j->pkt, &j->info);
-}
-
-// A worker parses one chain's frames in order. The pool's threads are shared out over
-// the chains that have work: a chain parsing alone (one GOP, or the last of a drain)
-// walks its frames' tile columns on the idle threads' share (vp9h_stream_set_threads,
-// decode_tiles_mt), frame-parallel keyframe streams keep one thread per frame.
-static void worker_main(vp9hip_decoder *d)
-{
-    std::unique_lock<std::mutex> lk(d->mu);
-    for (;;) {
-        d->cv_work.wait(lk, [&] { return d->stop || !d->runq.empty(); });
-        if (d->stop) return;
-        std::shared_ptr<Chain> c = d->runq.front();
-        d->runq.pop_front();
-        d->active++;
-        while (!c->q.empty()) {                       // the chain's frames, in order
-            ParseJob *j = c->q.front();
-            c->q.pop_front();
-            const int share = (int) d->workers.size() / std::max<int>(1, d->active + (int) d->runq.size());
-            lk.unlock();
-            vp9h_stream_set_threads(c->st, std::max(1, std::min(share, 16)));
-            parse_one(j);
-            lk.lock();
-            j->done = true;
-            d->cv_done.notify_all();
-        }
-        d->active--;
-        c->scheduled = false;
-    }
-}
-
+// ---- parse (vp9hip_parse.h) ----
 static void enqueue_parse(vp9hip_decoder *d, std::unique_ptr<ParseJob> j)
 {
     ParseJob *raw = j.get();
-    if (d->workers.empty()) {                         // no pool: parse now, in order
-        parse_one(raw);
-        raw->done = true;
-        d->inflight.push_back(std::move(j));
-        return;
-    }
-    std::lock_guard<std::mutex> lk(d->mu);
     d->inflight.push_back(std::move(j));
-    Chain *c = raw->chain.get();
-    c->q.push_back(raw);
-    if (!c->scheduled) {
-        c->scheduled = true;
-        d->runq.push_back(raw->chain);
-        d->cv_work.notify_one();
-    }
+    d->pool->enqueue(raw);
 }
 
 static bool front_done(vp9hip_decoder *d, bool block)
 {
     if (d->inflight.empty()) return false;
-    if (d->workers.empty()) return true;
-    std::unique_lock<std::mutex> lk(d->mu);
-    if (block) d->cv_done.wait(lk, [&] { return d->inflight.front()->done; });
-    return d->inflight.front()->done;
+    if (block) d->pool->wait(d->inflight.front().get());
+    return d->pool->done(d->inflight.front().get());
 }
 
 static void wait_all_parsed(vp9hip_decoder *d)
 {
-    if (d->workers.empty()) return;
-    std::unique_lock<std::mutex> lk(d->mu);
-    d->cv_done.wait(lk, [&] {
-        for (auto &j : d->inflight) if (!j->done) return false;
-        return true;
-    });
+    for (auto &j : d->inflight) d->pool->wait(j.get());
 }
 
 // ---- device side ----
@@ -313,7 +242,6 @@ static int consume(vp9hip_decoder *d, bool block, size_t keep = 0)
     while (d->inflight.size() > keep && front_done(d, block)) {
         int r = consume_one(d, *d->inflight.front());
         if (r == STALL) return STALL;
-        vp9h_frame_free(&d->inflight.front()->pkt);
         d->inflight.pop_front();
         if (r < 0) return r;
     }
@@ -347,7 +275,7 @@ extern "C" int vp9hip_decoder_open(const vp9hip_decoder_params *params, vp9hip_d
     if (r < 0) { vp9hip_decoder_close(d); return r; }
     vp9hip_set_timing(d->ctx, 0);             // every batch runs once: plain launches, no events
     vp9hip_set_graph(d->ctx, 0);
-    for (int t = 0; t < d->p.parse_threads; t++) d->workers.emplace_back(worker_main, d);
+    d->pool.reset(new ParsePool(d->p.parse_threads));
     *out = d;
     return 0;
 }
@@ -355,20 +283,14 @@ extern "C" int vp9hip_decoder_open(const vp9hip_decoder_params *params, vp9hip_d
 static void drop_inflight(vp9hip_decoder *d)
 {
     wait_all_parsed(d);
-    for (auto &j : d->inflight) vp9h_frame_free(&j->pkt);
     d->inflight.clear();
 }
 
 extern "C" void vp9hip_decoder_close(vp9hip_decoder *d)
 {
     if (!d) return;
-    drop_inflight(d);
-    {
-        std::lock_guard<std::mutex> lk(d->mu);
-        d->stop = true;
-    }
-    d->cv_work.notify_all();
-    for (auto &t : d->workers) t.join();
+    if (d->pool) drop_inflight(d);
+    d->pool.reset();
     for (auto &f : d->batch) vp9h_frame_free(&f.pkt);
     d->chain.reset();
     if (d->ctx) vp9hip_close(d->ctx);
@@ -404,9 +326,9 @@ extern "C" int vp9hip_decoder_send_packet(vp9hip_decoder *d, const uint8_t *data
         j->data.assign(data + offs[k], data + offs[k] + sizes[k]);
         j->pts = pts;
         if (type == 0 || !d->chain) {          // a keyframe parses on a fresh stream
-            std::shared_ptr<Chain> c = std::make_shared<Chain>();
-            int r = vp9h_stream_open(&c->st);
-            if (r < 0) return r;
+            int r = 0;
+            std::shared_ptr<Chain> c = ParsePool::new_chain(&r);
+            if (!c) return r;
             d->chain = c;
         }
         j->chain = d->chain;

@@ -1,0 +1,406 @@
+// The FFHWAccel adapter of the hybrid VP9 decoder over libvp9hip (include/vp9hip_hwaccel.h).
+//
+// One context per stream, as avctx->internal->hwaccel_priv_data: the device context, the
+// host parse pool, the frames in flight, and the device frame pool with the reference
+// slots. The call order is the reference's (vp9.c:1694-1713): start_frame, decode_slice,
+// end_frame per coded frame; show_existing_frame never reaches the hwaccel
+// (vp9.c:1636-1653) and is answered from the slots.
+//
+// Asynchronous, as an HWACCEL_CAP_ASYNC_SAFE hwaccel is (hwaccel_internal.h:31-32, the cap
+// vulkan_vp9.c:369 sets; frame threading gates on it at pthread_frame.c:687): nothing
+// waits on the GPU or on the entropy decode inside the per-frame calls.
+//   - decode_slice reads the slot bookkeeping from the start of the uncompressed header
+//     (vp9h_frame_peek, what vp9.c knows before ff_thread_finish_setup) and queues the
+//     entropy decode on the parse pool (vp9hip_parse.h): keyframes start new chains, so
+//     they parse in parallel; a lone chain's tile columns parse on the idle threads.
+//   - end_frame maps refidx to device buffers, replaces the slots of refreshrefmask and
+//     appends the frame to the batch being filled; every `async_depth` frames the batch is
+//     staged into the context's free batch slot and launched (vp9hip_stage_batch_refs /
+//     run_batch: dependent frames chained, independent chains concurrent).
+//   - A frame handed out is a device frame whose pixels are complete once
+//     vp9hip_hwframe_sync (host) or vp9hip_hwframe_ready (a consumer's HIP stream) says so;
+//     both launch the batch holding it if it is still being filled. transfer syncs.
+// Errors of asynchronous work surface on the call that waits for it: a batch whose
+// row-pipelined loop filter gave up a hand-off (k_lfr timeout words, read by
+// vp9hip_sync_slot) fails its frames with VP9HIP_EBUG; a frame whose entropy decode fails
+// fails with that error, and so do the frames launched with it.
+//
+// Pool: a buffer is free when no reference slot holds it, no frame reference (the
+// AVBufferRef of an AVFrame, vp9hip_hwframe_unref) holds it, it is not the frame being
+// decoded, and it is not in the batch being filled.
+#include <algorithm>
+#include <cstdlib>
+#include <thread>
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "../../include/vp9hip_hwaccel.h"
+#include "vp9hip_parse.h"
+
+using vp9hip::Chain;
+using vp9hip::ParseJob;
+using vp9hip::ParsePool;
+
+namespace {
+struct Pend { std::unique_ptr<ParseJob> job; int out; int refs[3]; };
+}
+
+struct vp9hip_hwaccel {
+    vp9hip_ctx *gpu = nullptr;
+    vp9hip_frames_params fp;
+    std::unique_ptr<ParsePool> pool;
+    std::shared_ptr<Chain> chain;           // the parse chain of the next non-key frame
+    int slot[8];                            // device buffer of each reference slot (s->s.ref_frames)
+    std::vector<int> refs;                  // per pool buffer: frame references handed out
+    std::vector<int> pend;                  // per pool buffer: in the batch being filled
+    std::vector<int> inref;                 // per pool buffer: read by frames of that batch
+    std::vector<uint64_t> buf_seq;          // per pool buffer: the batch that last wrote it
+    std::vector<int> buf_err;               // per pool buffer: error of the frame it holds
+    int cur = -1;                           // buffer of the frame being decoded
+    int64_t pts = 0;
+    std::unique_ptr<ParseJob> job;          // decode_slice -> end_frame
+    int intra = 0;
+    vp9h_frame_info info;                   // the peeked header of the current frame
+    std::vector<Pend> batch;                // the batch being filled
+    uint64_t launched = 0;                  // batches launched; batch b ran in slot (b - 1) & 1
+    uint64_t slot_seq[2] = { 0, 0 };
+    bool slot_checked[2] = { true, true };
+    std::vector<uint64_t> bad;              // launched batches that failed their check
+};
+
+static int swfmt(int bpp, int ss_h, int ss_v)
+{
+    const int chroma = ss_h && ss_v ? 0 : ss_h ? 1 : ss_v ? 2 : 3;
+    return (bpp == 8 ? 0 : bpp == 10 ? 4 : 8) + chroma;
+}
+
+extern "C" int vp9hip_hwaccel_frame_params(int width, int height, int bpp, int ss_h, int ss_v, int extra,
+                                           vp9hip_frames_params *out)
+{
+    if (!out || width <= 0 || height <= 0 || (bpp != 8 && bpp != 10 && bpp != 12) || ss_h < 0 || ss_h > 1 ||
+        ss_v < 0 || ss_v > 1 || extra < 0)
+        return VP9HIP_EINVAL;
+    memset(out, 0, sizeof(*out));
+    out->sw_format = swfmt(bpp, ss_h, ss_v);
+    out->width = width;
+    out->height = height;
+    out->async_depth = VP9HIP_HWACCEL_ASYNC_DEPTH;
+    // 8 reference slots, the frame being decoded, the frames of the batch being filled
+    // (each also handed out until the consumer has waited for it) and the caller's extra
+    out->initial_pool_size = 8 + 1 + out->async_depth + extra;
+    out->bpp = bpp;
+    out->ss_h = ss_h;
+    out->ss_v = ss_v;
+    out->parse_threads = (int) std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    return 0;
+}
+
+extern "C" int vp9hip_hwaccel_uninit(vp9hip_hwaccel *h);
+
+extern "C" int vp9hip_hwaccel_init(int device, const vp9hip_frames_params *fp, vp9hip_hwaccel **out)
+{
+    if (!fp || !out || fp->initial_pool_size < 9 || fp->async_depth < 1 || fp->async_depth > 256 ||
+        fp->parse_threads < 0 || fp->parse_threads > 64)
+        return VP9HIP_EINVAL;
+    *out = nullptr;
+    vp9hip_hwaccel *h = new (std::nothrow) vp9hip_hwaccel();
+    if (!h) return VP9HIP_ENOMEM;
+    h->fp = *fp;
+    for (int i = 0; i < 8; i++) h->slot[i] = -1;
+    const size_t n = (size_t) fp->initial_pool_size;
+    h->refs.assign(n, 0);
+    h->pend.assign(n, 0);
+    h->inref.assign(n, 0);
+    h->buf_seq.assign(n, 0);
+    h->buf_err.assign(n, 0);
+    int r = vp9hip_open(device, &h->gpu);
+    if (!r) r = vp9hip_configure(h->gpu, fp->width, fp->height, fp->bpp, fp->ss_h, fp->ss_v, fp->initial_pool_size);
+    if (r < 0) {
+        vp9hip_hwaccel_uninit(h);
+        return r;
+    }
+    vp9hip_set_timing(h->gpu, 0);              // every batch runs once: plain launches, no events
+    vp9hip_set_graph(h->gpu, 0);
+    h->pool.reset(new ParsePool(fp->parse_threads));
+    *out = h;
+    return 0;
+}
+
+// Check the batch last launched in slot s (waits for it): an EBUG batch is remembered and
+// its frames fail when they are waited for.
+static int check_slot(vp9hip_hwaccel *h, int s)
+{
+    if (h->slot_checked[s]) return 0;
+    const int r = vp9hip_sync_slot(h->gpu, s);
+    if (r == VP9HIP_EBUG) h->bad.push_back(h->slot_seq[s]);
+    else if (r < 0) return r;
+    h->slot_checked[s] = true;
+    return 0;
+}
+
+static bool batch_bad(const vp9hip_hwaccel *h, uint64_t seq)
+{
+    for (uint64_t b : h->bad) if (b == seq) return true;
+    return false;
+}
+
+// Stage + launch the batch being filled in the next batch slot. Its packets are parsed
+// by now or soon: wait for them (in decode order).
+static int submit(vp9hip_hwaccel *h)
+{
+    if (h->batch.empty()) return 0;
+    const int n = (int) h->batch.size();
+    int err = 0;
+    for (auto &p : h->batch) {
+        h->pool->wait(p.job.get());
+        const vp9h_frame &f = p.job->pkt;
+        int e = p.job->ret;
+        if (!e && (f.width > h->fp.width || f.height > h->fp.height || f.bpp != h->fp.bpp ||
+                   f.ss_h != h->fp.ss_h || f.ss_v != h->fp.ss_v))
+            e = VP9HIP_ENOSYS;               // a new format: get_format re-inits the hwaccel
+        if (e && !err) err = e;
+    }
+    int ret = err;
+    const int slot = (int) (h->launched & 1);
+    if (!ret) ret = check_slot(h, slot);     // before the staging resets that batch's words
+    if (!ret) ret = vp9hip_set_batch_slot(h->gpu, slot);
+    if (!ret) {
+        std::vector<vp9h_frame> pk(n);
+        std::vector<int> outs(n), refs(3 * n);
+        for (int i = 0; i < n; i++) {
+            pk[i] = h->batch[i].job->pkt;
+            outs[i] = h->batch[i].out;
+            for (int r = 0; r < 3; r++) refs[3 * i + r] = h->batch[i].refs[r] >= 0 ? h->batch[i].refs[r] : 0;
+        }
+        ret = vp9hip_stage_batch_refs(h->gpu, pk.data(), n, outs.data(), refs.data());   // copies the packets
+        if (ret >= 0) ret = vp9hip_run_batch(h->gpu);
+        if (ret >= 0) {
+            h->launched++;
+            h->slot_seq[slot] = h->launched;
+            h->slot_checked[slot] = false;
+        }
+    }
+    for (auto &p : h->batch) {
+        h->pend[p.out] = 0;
+        for (int r = 0; r < 3; r++)
+            if (p.refs[r] >= 0) h->inref[p.refs[r]]--;
+        h->buf_seq[p.out] = ret < 0 ? 0 : h->launched;
+        h->buf_err[p.out] = ret < 0 ? ret : 0;
+    }
+    h->batch.clear();                        // the jobs free their packets
+    return ret < 0 ? ret : 0;
+}
+
+static bool buf_busy(const vp9hip_hwaccel *h, int b)
+{
+    // a buffer a batched frame reads is not rewritten by a later frame of the same batch
+    if (h->refs[b] || h->pend[b] || h->inref[b] || b == h->cur) return true;
+    for (int s = 0; s < 8; s++)
+        if (h->slot[s] == b) return true;
+    return false;
+}
+
+static int find_free(const vp9hip_hwaccel *h)
+{
+    for (int b = 0; b < h->fp.initial_pool_size; b++)
+        if (!buf_busy(h, b)) return b;
+    return -1;
+}
+
+extern "C" int vp9hip_hwaccel_start_frame(vp9hip_hwaccel *h, const uint8_t *buf, uint32_t size, int64_t pts)
+{
+    if (!h || (!buf && size)) return VP9HIP_EINVAL;
+    h->job.reset();                          // a frame that never reached end_frame
+    h->cur = -1;
+    int b = find_free(h);
+    if (b < 0 && !h->batch.empty()) {        // unreferenced hidden frames free up once launched
+        const int r = submit(h);
+        if (r < 0) return r;
+        b = find_free(h);
+    }
+    if (b < 0) return VP9HIP_EAGAIN;         // every buffer held: the caller must unref frames
+    h->cur = b;
+    h->pts = pts;
+    return 0;
+}
+
+extern "C" int vp9hip_hwaccel_decode_slice(vp9hip_hwaccel *h, const uint8_t *buf, uint32_t size)
+{
+    if (!h || !buf || !size || h->cur < 0) return VP9HIP_EINVAL;
+    vp9h_frame_info info;
+    const int type = vp9h_frame_peek(buf, size, &info);
+    if (type < 0) return type;
+    if (type == 2) return VP9HIP_EINVALIDDATA;           // show_existing_frame: vp9.c answers it itself
+    std::unique_ptr<ParseJob> j(new (std::nothrow) ParseJob());
+    if (!j) return VP9HIP_ENOMEM;
+    if (type == 0) {                                     // a keyframe parses on a fresh stream
+        int r = 0;
+        h->chain = ParsePool::new_chain(&r);
+        if (!h->chain) return r;
+    } else if (!h->chain) {
+        return VP9HIP_EINVALIDDATA;                      // no keyframe yet since init / flush
+    }
+    j->data.assign(buf, buf + size);
+    j->pts = h->pts;
+    j->chain = h->chain;
+    h->pool->enqueue(j.get());
+    h->job = std::move(j);
+    h->info = info;
+    h->intra = type == 0 || type == 3;
+    return 0;
+}
+
+static void fill_frame(vp9hip_hwaccel *h, int b, int64_t pts, vp9hip_hwframe *out)
+{
+    memset(out, 0, sizeof(*out));
+    int w = 0, ht = 0;
+    vp9hip_frame_device(h->gpu, b, out->data, out->linesize, &w, &ht, &out->stream);
+    out->width = w;
+    out->height = ht;
+    out->sw_format = h->fp.sw_format;
+    out->buf = b;
+    out->pts = pts;
+    h->refs[b]++;
+}
+
+extern "C" int vp9hip_hwaccel_end_frame(vp9hip_hwaccel *h, vp9hip_hwframe *out)
+{
+    if (!h || h->cur < 0 || !h->job) return VP9HIP_EINVAL;
+    Pend p;
+    p.out = h->cur;
+    for (int i = 0; i < 3; i++) {            // s->s.h.refidx -> the slots' device buffers
+        p.refs[i] = h->intra ? -1 : h->slot[h->info.ref_slot[i] & 7];
+        if (!h->intra && p.refs[i] < 0) { h->job.reset(); h->cur = -1; return VP9HIP_EINVALIDDATA; }
+    }
+    p.job = std::move(h->job);
+    for (int i = 0; i < 8; i++)              // vp9.c:1705-1711: slots of refreshrefmask
+        if (h->info.refresh_mask & (1 << i)) h->slot[i] = h->cur;
+    h->pend[p.out] = 1;
+    for (int i = 0; i < 3; i++)
+        if (p.refs[i] >= 0) h->inref[p.refs[i]]++;
+    h->buf_err[p.out] = 0;
+    h->batch.push_back(std::move(p));
+    if (out) fill_frame(h, h->cur, h->pts, out);          // shown or hidden: vp9.c's AVFrame of the frame
+    const int shown = h->info.show_frame != 0;
+    h->cur = -1;
+    if ((int) h->batch.size() >= h->fp.async_depth) {
+        const int r = submit(h);
+        if (r < 0) return r;
+    }
+    return shown;
+}
+
+extern "C" int vp9hip_hwaccel_show_existing(vp9hip_hwaccel *h, int slot, int64_t pts, vp9hip_hwframe *out)
+{
+    if (!h || !out || slot < 0 || slot > 7) return VP9HIP_EINVAL;
+    if (h->slot[slot] < 0) return VP9HIP_EINVALIDDATA;   // "Requested reference ... not available"
+    fill_frame(h, h->slot[slot], pts, out);
+    return 0;
+}
+
+// Launch the frame's batch if it is still being filled; 0 or the frame's error.
+static int launch_for(vp9hip_hwaccel *h, int b)
+{
+    if (h->pend[b]) {
+        const int r = submit(h);
+        if (r < 0) return r;
+    }
+    return h->buf_err[b];
+}
+
+extern "C" int vp9hip_hwframe_sync(vp9hip_hwaccel *h, const vp9hip_hwframe *f)
+{
+    if (!h || !f || f->buf < 0 || f->buf >= h->fp.initial_pool_size || !h->refs[f->buf]) return VP9HIP_EINVAL;
+    int r = launch_for(h, f->buf);
+    if (r < 0) return r;
+    const uint64_t b = h->buf_seq[f->buf];
+    if (!b) return 0;                                    // written before any batch (never decoded)
+    const int s = (int) ((b - 1) & 1);
+    if (h->slot_seq[s] == b && (r = check_slot(h, s)) < 0) return r;
+    // an older batch of the slot was drained and checked before its slot was reused
+    return batch_bad(h, b) ? VP9HIP_EBUG : 0;
+}
+
+extern "C" int vp9hip_hwframe_ready(vp9hip_hwaccel *h, const vp9hip_hwframe *f, void *stream)
+{
+    if (!h || !f || f->buf < 0 || f->buf >= h->fp.initial_pool_size || !h->refs[f->buf]) return VP9HIP_EINVAL;
+    int r = launch_for(h, f->buf);
+    if (r < 0) return r;
+    const uint64_t b = h->buf_seq[f->buf];
+    if (batch_bad(h, b)) return VP9HIP_EBUG;
+    if (!b) return 0;
+    const int s = (int) ((b - 1) & 1);
+    // the slot's last run is this batch or a later one (which follows it on the context's
+    // stream): ordering the consumer's stream after it orders it after the frame
+    return vp9hip_slot_stream_wait(h->gpu, s, stream);
+}
+
+extern "C" int vp9hip_hwaccel_uninit(vp9hip_hwaccel *h)
+{
+    if (!h) return 0;
+    h->job.reset();
+    if (h->gpu) {
+        submit(h);                           // frames handed out may still be read by the caller
+        vp9hip_sync(h->gpu);
+    }
+    h->batch.clear();
+    h->pool.reset();
+    h->chain.reset();
+    if (h->gpu) vp9hip_close(h->gpu);
+    delete h;
+    return 0;
+}
+
+extern "C" void vp9hip_hwaccel_flush(vp9hip_hwaccel *h)
+{
+    if (!h) return;
+    h->job.reset();
+    h->cur = -1;
+    // frames already handed out stay valid: their batch runs, then the slots are dropped
+    if (submit(h) >= 0) {
+        for (int s = 0; s < 2; s++) check_slot(h, s);
+    }
+    for (auto &p : h->batch) {              // a failed launch leaves them here
+        h->pend[p.out] = 0;
+        for (int r = 0; r < 3; r++)
+            if (p.refs[r] >= 0) h->inref[p.refs[r]]--;
+    }
+    h->batch.clear();
+    for (int i = 0; i < 8; i++) h->slot[i] = -1;
+    h->chain.reset();                        // the next frame must be a keyframe
+    vp9hip_sync(h->gpu);
+}
+
+extern "C" int vp9hip_hwaccel_last_header(const vp9hip_hwaccel *h, vp9h_frame_info *info)
+{
+    if (!h || !info) return VP9HIP_EINVAL;
+    *info = h->info;
+    return 0;
+}
+
+extern "C" int vp9hip_hwframe_transfer(vp9hip_hwaccel *h, const vp9hip_hwframe *src, uint8_t *const dst[3],
+                                       const ptrdiff_t dst_linesize[3])
+{
+    const int r = vp9hip_hwframe_sync(h, src);
+    if (r < 0) return r;
+    return vp9hip_download_frame(h->gpu, src->buf, dst, dst_linesize);
+}
+
+extern "C" int vp9hip_hwframe_unref(vp9hip_hwaccel *h, vp9hip_hwframe *f)
+{
+    if (!h || !f || f->buf < 0 || f->buf >= h->fp.initial_pool_size || h->refs[f->buf] <= 0) return VP9HIP_EINVAL;
+    h->refs[f->buf]--;
+    memset(f, 0, sizeof(*f));
+    f->buf = -1;
+    return 0;
+}
+
+extern "C" int vp9hip_hwframe_ref(vp9hip_hwaccel *h, const vp9hip_hwframe *src, vp9hip_hwframe *dst)
+{
+    if (!h || !src || !dst || src->buf < 0 || src->buf >= h->fp.initial_pool_size || h->refs[src->buf] <= 0)
+        return VP9HIP_EINVAL;
+    *dst = *src;
+    h->refs[src->buf]++;
+    return 0;
+}

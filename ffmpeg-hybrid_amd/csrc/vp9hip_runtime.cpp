@@ -2202,6 +2202,15 @@ extern "C" int vp9hip_sync_slot(vp9hip_ctx *c, int slot)
     return check_lfr(g);
 }
 
+extern "C" int vp9hip_slot_stream_wait(vp9hip_ctx *c, int slot, void *stream)
+{
+    if (!c || slot < 0 || slot > 1) return VP9HIP_EINVAL;
+    hipSetDevice(c->dev);
+    const Staged &g = slot == c->slot ? c->stg : c->alt;
+    if (g.done_ev) HIPCHK(hipStreamWaitEvent((hipStream_t) stream, g.done_ev, 0));
+    return 0;
+}
+
 extern "C" int vp9hip_slot_busy(vp9hip_ctx *c, int slot)
 {
     if (!c || slot < 0 || slot > 1) return VP9HIP_EINVAL;

@@ -177,6 +177,10 @@ int  vp9hip_set_batch_slot(vp9hip_ctx *ctx, int slot);
 /* Wait for the last run of batch slot `slot` only (the other slot's work may continue)
  * and check it as vp9hip_sync does (VP9HIP_EBUG: a loop-filter hand-off timed out). */
 int  vp9hip_sync_slot(vp9hip_ctx *ctx, int slot);
+/* Make HIP stream `stream` (a hipStream_t; NULL: the null stream) wait for the last run of
+ * batch slot `slot`, without a host wait: work enqueued on it afterwards sees that run's
+ * frames. The loop-filter hand-off check needs a host wait (vp9hip_sync_slot). */
+int  vp9hip_slot_stream_wait(vp9hip_ctx *ctx, int slot, void *stream);
 /* 1 while the last run of batch slot `slot` is still executing, 0 once it is done. */
 int  vp9hip_slot_busy(vp9hip_ctx *ctx, int slot);
 /* Wait for all queued work of both batch slots. VP9HIP_EBUG if a row-pipelined
@@ -360,6 +364,13 @@ int  vp9h_stream_encode(vp9h_stream *s, const vp9h_frame *pkt, const vp9h_enc_pa
 /* The frame type from the first header bits: 0 keyframe (its parse needs no earlier
  * frame), 1 other frame, 2 show_existing_frame, or AVERROR_INVALIDDATA. */
 int  vp9h_frame_type(const uint8_t *data, size_t size);
+
+/* The slot bookkeeping of a frame from the start of its uncompressed header, without
+ * stream state (vp9.c:519-611, what vp9.c knows before ff_thread_finish_setup):
+ * show_existing_frame + show_slot, show_frame, error_res, refresh_mask, and ref_slot /
+ * sign_bias of inter frames; the other fields are zero. Returns 0 keyframe, 1 inter frame,
+ * 2 show_existing_frame, 3 intra-only frame, or AVERROR_INVALIDDATA. */
+int  vp9h_frame_peek(const uint8_t *data, size_t size, vp9h_frame_info *info);
 
 /* Split a superframe into its frames (vp9_superframe_split_bsf,
  * bsf/vp9_superframe_split.c:40-95): up to cap (offset, size) pairs; returns the frame

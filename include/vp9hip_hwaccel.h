@@ -40,11 +40,17 @@ enum {
 
 /* FFHWAccel.frame_params: what the AVHWFramesContext of the stream's frames gets
  * (format = the HIP hw pix_fmt, sw_format, width, height, initial_pool_size). */
+#define VP9HIP_HWACCEL_ASYNC_DEPTH 16
 typedef struct vp9hip_frames_params {
     int32_t sw_format;             /* VP9HIP_SWFMT_*                                         */
     int32_t width, height;         /* coded size                                             */
-    int32_t initial_pool_size;     /* 8 reference slots + the frame being decoded + extra    */
+    int32_t initial_pool_size;     /* 8 reference slots + the frame being decoded +          */
+                                   /* async_depth + extra                                    */
     int32_t bpp, ss_h, ss_v;
+    /* set by frame_params, adjustable before init (the FFmpeg glue maps its options here): */
+    int32_t async_depth;           /* frames per device launch (VP9HIP_HWACCEL_ASYNC_DEPTH);  */
+                                   /* 1 = each frame launched by its end_frame               */
+    int32_t parse_threads;         /* host entropy-decode threads (0: in decode_slice)       */
 } vp9hip_frames_params;
 int vp9hip_hwaccel_frame_params(int width, int height, int bpp, int ss_h, int ss_v, int extra,
                                 vp9hip_frames_params *out);
@@ -71,26 +77,44 @@ int  vp9hip_hwaccel_uninit(vp9hip_hwaccel *h);
 /* FFHWAccel.start_frame(avctx, buf_ref, buf, size): the whole frame's bytes (one frame of
  * a split superframe, not show_existing_frame). */
 int  vp9hip_hwaccel_start_frame(vp9hip_hwaccel *h, const uint8_t *buf, uint32_t size, int64_t pts);
-/* FFHWAccel.decode_slice(avctx, buf, size): the host entropy decode of the frame (all its
- * tiles) into the pass-1 packet (vp9h_stream_decode). */
+/* FFHWAccel.decode_slice(avctx, buf, size): the header's slot bookkeeping (vp9h_frame_peek)
+ * now; the host entropy decode of the frame (all its tiles) into the pass-1 packet
+ * (vp9h_stream_decode) queued on the parse threads. */
 int  vp9hip_hwaccel_decode_slice(vp9hip_hwaccel *h, const uint8_t *buf, uint32_t size);
-/* FFHWAccel.end_frame: reconstruct the frame on the device (its LAST / GOLDEN / ALTREF
- * are the device buffers of slots refidx[]), replace the slots of refreshrefmask. When
- * the frame is shown, *out (may be NULL) is the device frame, referenced until
- * vp9hip_hwframe_unref; returns 1 if shown, 0 if hidden, or an error. */
+/* FFHWAccel.end_frame: queue the frame's reconstruction on the device (its LAST / GOLDEN /
+ * ALTREF are the device buffers of slots refidx[]) and replace the slots of
+ * refreshrefmask. Asynchronous (HWACCEL_CAP_ASYNC_SAFE): frames are launched in batches
+ * of async_depth, and nothing here waits for the GPU. *out (may be NULL) is the frame,
+ * shown or hidden: the device frame behind vp9.c's AVFrame of this VP9Frame, referenced
+ * until vp9hip_hwframe_unref (the AVBufferRef's free callback). Its pixels are complete
+ * after vp9hip_hwframe_sync / vp9hip_hwframe_ready. Returns 1 if shown, 0 if hidden, or an
+ * error (also one of an earlier frame's batch launched by this call). */
 int  vp9hip_hwaccel_end_frame(vp9hip_hwaccel *h, vp9hip_hwframe *out);
 /* vp9.c:1636-1653 show_existing_frame: the frame of reference slot `slot`, referenced. */
 int  vp9hip_hwaccel_show_existing(vp9hip_hwaccel *h, int slot, int64_t pts, vp9hip_hwframe *out);
-/* FFHWAccel.flush: drop the reference slots (frames handed out stay valid). */
+/* FFHWAccel.flush: launch what is queued (frames handed out stay valid), drop the
+ * reference slots; the next frame must be a keyframe. */
 void vp9hip_hwaccel_flush(vp9hip_hwaccel *h);
-/* The header fields the adapter mirrors from the parse (s->s.h.refidx / refreshrefmask,
- * vp9shared.h:112,120) of the last decode_slice, for the decoder's own bookkeeping. */
+/* The header fields the adapter read in the last decode_slice (vp9h_frame_peek:
+ * s->s.h.refidx / refreshrefmask / show_frame, vp9shared.h:112,120). */
 int  vp9hip_hwaccel_last_header(const vp9hip_hwaccel *h, vp9h_frame_info *info);
 
-/* HWContextType.transfer_data_from: device frame -> host planes (visible size). */
+/* Host wait for a frame's pixels (launching its batch if it is still being filled), with
+ * its batch's checks: VP9HIP_EBUG if the loop filter's row hand-off gave up, or the error
+ * of the frame's entropy decode. The hwcontext's frame sync. */
+int  vp9hip_hwframe_sync(vp9hip_hwaccel *h, const vp9hip_hwframe *f);
+/* Order HIP stream `stream` (a hipStream_t) after a frame's pixels without a host wait
+ * (launching its batch if needed): a GPU consumer's wait. The batch's hand-off check runs
+ * at the next host wait on it. */
+int  vp9hip_hwframe_ready(vp9hip_hwaccel *h, const vp9hip_hwframe *f, void *stream);
+/* HWContextType.transfer_data_from: device frame -> host planes (visible size); syncs. */
 int  vp9hip_hwframe_transfer(vp9hip_hwaccel *h, const vp9hip_hwframe *src, uint8_t *const dst[3],
                              const ptrdiff_t dst_linesize[3]);
-/* av_frame_unref of a device frame: its pool buffer is free once no slot holds it. */
+/* av_frame_ref of a device frame (av_buffer_ref of its AVBufferRef): *dst is another
+ * reference to src's pool buffer. */
+int  vp9hip_hwframe_ref(vp9hip_hwaccel *h, const vp9hip_hwframe *src, vp9hip_hwframe *dst);
+/* av_frame_unref of a device frame: its pool buffer is free once no reference and no slot
+ * holds it. */
 int  vp9hip_hwframe_unref(vp9hip_hwaccel *h, vp9hip_hwframe *f);
 
 #ifdef __cplusplus

@@ -1,21 +1,34 @@
 /*
- * FFHWAccel call-order harness for libvp9hip (tests/test_hwaccel_harness.py runs it on the GPU).
+ * FFHWAccel call-order harness for libvp9hip (tests/test_hwaccel_harness.py runs it on the GPU;
+ * bench.py times it as the `hwaccel_path` field).
  *
  * Plays the part of libavcodec's VP9 decoder around the hwaccel, in the reference order:
  *   get_format -> FFHWAccel.frame_params + init           (decode.c:1153-1200, hwaccel_internal.h:146)
  *   per packet: the superframe split BSF                  (vp9.c:1977, vp9_superframe_split.c:40-95)
  *   per frame: show_existing_frame answered from the slots (vp9.c:1636-1653)
  *              else start_frame, decode_slice, end_frame  (vp9.c:1694-1713)
- *   shown frames: av_hwframe_transfer_data + av_frame_unref (hwcontext_internal.h:79)
+ *   output frames: av_hwframe_transfer_data + av_frame_unref (hwcontext_internal.h:79)
  *   avcodec_flush_buffers -> FFHWAccel.flush, then the stream again from its first packet
  *   avcodec_free_context -> FFHWAccel.uninit
- * Output: the visible planes of every output frame, in output order, appended to OUT.
+ * Frame ownership follows FFmpeg's: every decoded frame (shown or hidden) is an AVFrame whose
+ * buffer reference comes from end_frame; vp9.c keeps it as s->s.frames[CUR_FRAME] until the
+ * next frame and as a reference in s->s.ref_frames[] for each slot of its refresh mask
+ * (vp9.c:1686-1691, 1845-1849); an output frame is one more reference (av_frame_ref), which
+ * the consumer drops after reading it. Every drop is vp9hip_hwframe_unref (the
+ * AVBufferRef's free callback).
  *
- * usage: hwaccel_harness IN.ivf OUT.yuv BPP SS_H SS_V [PASSES]
+ * The consumer reads output frames LAG frames behind the decoder (FFmpeg's frame-threading
+ * delay; 0 = each frame as soon as end_frame returns it). MODE: "download" transfers each
+ * output frame to host planes (appended to OUT unless OUT is "-"); "device" only waits for
+ * its pixels on the GPU (vp9hip_hwframe_sync), as a consumer of device frames does.
+ * Prints "frames N seconds S" (wall time of the decode loop, init / uninit excluded).
+ *
+ * usage: hwaccel_harness IN.ivf OUT.yuv|- BPP SS_H SS_V [PASSES [LAG [MODE [ASYNC_DEPTH]]]]
  */
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "../../include/vp9hip_hwaccel.h"
 
@@ -42,30 +55,74 @@ static int show_existing_slot(const uint8_t *d, size_t n)
     return s;
 }
 
-static int emit(vp9hip_hwaccel *h, vp9hip_hwframe *f, int bpp, int ssh, int ssv, FILE *out)
+typedef struct Consumer {
+    vp9hip_hwaccel *h;
+    int bpp, ssh, ssv, download, lag;
+    FILE *out;
+    vp9hip_hwframe q[512];             /* output frames not read yet (av_frame_ref'd) */
+    int head, n;
+    int frames_out;
+} Consumer;
+
+static int consume_one(Consumer *c)
 {
-    const int by = bpp > 8 ? 2 : 1, w = f->width, ht = f->height;
-    const int cw = (w + ssh) >> ssh, chh = (ht + ssv) >> ssv;
-    uint8_t *pl[3];
-    ptrdiff_t ls[3] = { (ptrdiff_t) w * by, (ptrdiff_t) cw * by, (ptrdiff_t) cw * by };
-    pl[0] = malloc((size_t) ls[0] * ht);
-    pl[1] = malloc((size_t) ls[1] * chh);
-    pl[2] = malloc((size_t) ls[2] * chh);
-    int r = vp9hip_hwframe_transfer(h, f, pl, ls);                 /* transfer_data_from */
-    if (r >= 0) {
-        fwrite(pl[0], 1, (size_t) ls[0] * ht, out);
-        fwrite(pl[1], 1, (size_t) ls[1] * chh, out);
-        fwrite(pl[2], 1, (size_t) ls[2] * chh, out);
-        r = vp9hip_hwframe_unref(h, f);                              /* av_frame_unref */
+    vp9hip_hwframe *f = &c->q[c->head];
+    int r;
+    if (c->download) {
+        const int by = c->bpp > 8 ? 2 : 1, w = f->width, ht = f->height;
+        const int cw = (w + c->ssh) >> c->ssh, chh = (ht + c->ssv) >> c->ssv;
+        uint8_t *pl[3];
+        ptrdiff_t ls[3] = { (ptrdiff_t) w * by, (ptrdiff_t) cw * by, (ptrdiff_t) cw * by };
+        pl[0] = malloc((size_t) ls[0] * ht);
+        pl[1] = malloc((size_t) ls[1] * chh);
+        pl[2] = malloc((size_t) ls[2] * chh);
+        r = vp9hip_hwframe_transfer(c->h, f, pl, ls);               /* transfer_data_from */
+        if (r >= 0 && c->out) {
+            fwrite(pl[0], 1, (size_t) ls[0] * ht, c->out);
+            fwrite(pl[1], 1, (size_t) ls[1] * chh, c->out);
+            fwrite(pl[2], 1, (size_t) ls[2] * chh, c->out);
+        }
+        free(pl[0]); free(pl[1]); free(pl[2]);
+    } else {
+        r = vp9hip_hwframe_sync(c->h, f);                            /* the frame's pixels are final */
     }
-    free(pl[0]); free(pl[1]); free(pl[2]);
+    const int u = vp9hip_hwframe_unref(c->h, f);                     /* av_frame_unref */
+    c->head = (c->head + 1) % 512;
+    c->n--;
+    c->frames_out++;
+    return r < 0 ? r : u;
+}
+
+/* av_frame_ref of an output frame into the consumer's queue; reads the frames more than
+ * LAG behind */
+static int output(Consumer *c, const vp9hip_hwframe *f)
+{
+    if (c->n == 512) return -1;
+    vp9hip_hwframe *d = &c->q[(c->head + c->n) % 512];
+    int r = vp9hip_hwframe_ref(c->h, f, d);
+    if (r < 0) return r;
+    c->n++;
+    while (c->n > c->lag && r >= 0) r = consume_one(c);
+    return r;
+}
+
+static int drain(Consumer *c)
+{
+    int r = 0;
+    while (c->n && r >= 0) r = consume_one(c);
     return r;
 }
 
 int main(int argc, char **argv)
 {
-    if (argc < 6) { fprintf(stderr, "usage: %s IN.ivf OUT.yuv BPP SS_H SS_V [PASSES]\n", argv[0]); return 2; }
+    if (argc < 6) {
+        fprintf(stderr, "usage: %s IN.ivf OUT.yuv|- BPP SS_H SS_V [PASSES [LAG [MODE [ASYNC_DEPTH]]]]\n", argv[0]);
+        return 2;
+    }
     const int bpp = atoi(argv[3]), ssh = atoi(argv[4]), ssv = atoi(argv[5]), passes = argc > 6 ? atoi(argv[6]) : 2;
+    const int lag = argc > 7 ? atoi(argv[7]) : 0;
+    const int download = argc > 8 ? strcmp(argv[8], "device") != 0 : 1;
+    const int depth = argc > 9 ? atoi(argv[9]) : 0;
     FILE *fi = fopen(argv[1], "rb");
     if (!fi) { perror(argv[1]); return 2; }
     fseek(fi, 0, SEEK_END);
@@ -74,23 +131,41 @@ int main(int argc, char **argv)
     uint8_t *buf = malloc((size_t) n);
     if (fread(buf, 1, (size_t) n, fi) != (size_t) n) { fclose(fi); return 2; }
     fclose(fi);
-    FILE *out = fopen(argv[2], "wb");
-    if (!out) { perror(argv[2]); return 2; }
+    FILE *out = NULL;
+    if (strcmp(argv[2], "-") && !(out = fopen(argv[2], "wb"))) { perror(argv[2]); return 2; }
 
     vp9h_ivf_header ih;
     int r = vp9h_ivf_read_header(buf, (size_t) n, &ih);
     if (r < 0) { fprintf(stderr, "ivf header: %d\n", r); return 1; }
-    /* get_format: frame_params then init */
+    /* get_format: frame_params (+ the options the glue maps onto it) then init */
     vp9hip_frames_params fp;
     vp9hip_hwaccel *h = NULL;
-    if ((r = vp9hip_hwaccel_frame_params(ih.width, ih.height, bpp, ssh, ssv, 2, &fp)) < 0 ||
-        (r = vp9hip_hwaccel_init(0, &fp, &h)) < 0) {
+    if ((r = vp9hip_hwaccel_frame_params(ih.width, ih.height, bpp, ssh, ssv, 2 + lag, &fp)) < 0) {
+        fprintf(stderr, "frame_params: %d\n", r);
+        return 1;
+    }
+    if (depth > 0) {
+        fp.initial_pool_size += depth - fp.async_depth;
+        fp.async_depth = depth;
+    }
+    if ((r = vp9hip_hwaccel_init(0, &fp, &h)) < 0) {
         fprintf(stderr, "init: %d\n", r);
         return 1;
     }
-    int frames_out = 0;
+    static Consumer c;
+    c.h = h; c.bpp = bpp; c.ssh = ssh; c.ssv = ssv; c.download = download; c.lag = lag; c.out = out;
+    vp9hip_hwframe slots[8], cur;                  /* s->s.ref_frames[], s->s.frames[CUR_FRAME] */
+    int have_slot[8] = { 0 }, have_cur = 0;
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
     for (int pass = 0; pass < passes && r >= 0; pass++) {
-        if (pass) vp9hip_hwaccel_flush(h);                         /* avcodec_flush_buffers */
+        if (pass) {                                                 /* avcodec_flush_buffers */
+            if ((r = drain(&c)) < 0) break;
+            vp9hip_hwaccel_flush(h);
+            for (int s = 0; s < 8; s++)
+                if (have_slot[s]) { vp9hip_hwframe_unref(h, &slots[s]); have_slot[s] = 0; }
+            if (have_cur) { vp9hip_hwframe_unref(h, &cur); have_cur = 0; }
+        }
         size_t pos = ih.header_size;
         const uint8_t *pkt;
         uint32_t psz;
@@ -102,24 +177,43 @@ int main(int argc, char **argv)
             if (nf < 0) { r = nf; break; }
             for (int k = 0; k < nf && r >= 0; k++) {
                 const uint8_t *d = pkt + offs[k];
-                vp9hip_hwframe f;
                 const int ex = show_existing_slot(d, sizes[k]);
                 if (ex >= 0) {
+                    vp9hip_hwframe f;
                     r = vp9hip_hwaccel_show_existing(h, ex, pts, &f);
-                    if (r >= 0) { r = emit(h, &f, bpp, ssh, ssv, out); frames_out++; }
+                    if (r >= 0) {
+                        r = output(&c, &f);
+                        vp9hip_hwframe_unref(h, &f);
+                    }
                     continue;
                 }
+                if (have_cur) { vp9hip_hwframe_unref(h, &cur); have_cur = 0; }   /* vp9_frame_unref(CUR_FRAME) */
                 if ((r = vp9hip_hwaccel_start_frame(h, d, (uint32_t) sizes[k], pts)) < 0) break;
                 if ((r = vp9hip_hwaccel_decode_slice(h, d, (uint32_t) sizes[k])) < 0) break;
-                if ((r = vp9hip_hwaccel_end_frame(h, &f)) < 0) break;
-                if (r == 1) { r = emit(h, &f, bpp, ssh, ssv, out); frames_out++; }
+                if ((r = vp9hip_hwaccel_end_frame(h, &cur)) < 0) break;
+                have_cur = 1;
+                const int shown = r;
+                vp9h_frame_info info;
+                vp9hip_hwaccel_last_header(h, &info);
+                for (int s = 0; s < 8 && r >= 0; s++)                 /* s->s.ref_frames[] by refreshrefmask */
+                    if (info.refresh_mask & (1 << s)) {
+                        if (have_slot[s]) vp9hip_hwframe_unref(h, &slots[s]);
+                        r = vp9hip_hwframe_ref(h, &cur, &slots[s]);
+                        have_slot[s] = r >= 0;
+                    }
+                if (r >= 0 && shown) r = output(&c, &cur);
             }
         }
     }
+    if (r >= 0) r = drain(&c);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    for (int s = 0; s < 8; s++)
+        if (have_slot[s]) vp9hip_hwframe_unref(h, &slots[s]);
+    if (have_cur) vp9hip_hwframe_unref(h, &cur);
     vp9hip_hwaccel_uninit(h);
-    fclose(out);
+    if (out) fclose(out);
     free(buf);
-    if (r < 0) { fprintf(stderr, "decode: %d after %d frames\n", r, frames_out); return 1; }
-    printf("frames %d\n", frames_out);
+    if (r < 0) { fprintf(stderr, "decode: %d after %d frames\n", r, c.frames_out); return 1; }
+    printf("frames %d seconds %.6f\n", c.frames_out, (double) (t1.tv_sec - t0.tv_sec) + 1e-9 * (double) (t1.tv_nsec - t0.tv_nsec));
     return 0;
 }

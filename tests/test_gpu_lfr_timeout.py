@@ -62,3 +62,14 @@ def test_default_bound_decodes_bit_exact(v9, orc):
     got = [pl for pl, _ in dec.decode(pkts)]
     dec.close()
     _same(got, _oracle_outputs(v9, orc, pkts), "default spin bound")
+
+
+def test_hwaccel_fails_frames_of_a_timed_out_batch(v9, tmp_path, tiny_spin):
+    """The FFHWAccel path checks the same hand-off words before a frame is read
+    (vp9hip_hwframe_sync / transfer): the harness's decode fails with VP9HIP_EBUG."""
+    from test_hwaccel_harness import run_harness
+    ivf = tmp_path / "t.ivf"
+    ivf.write_bytes(v9.ivf_write(_gop(v9), 1920, 1080))
+    for mode in ("download", "device"):
+        rc, _, _, err = run_harness(ivf, "-", 8, 1, 1, 1, 0, mode, 4, env=dict(os.environ))
+        assert rc == 1 and ("decode: %d" % v9.EBUG) in err, (mode, err)

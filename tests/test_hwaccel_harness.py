@@ -30,15 +30,19 @@ def test_harness_is_built_against_the_library():
     assert "libvp9hip.so" in ldd and "not found" not in ldd.split("libvp9hip.so")[1].split("\n")[0]
 
 
+class _FP(__import__("ctypes").Structure):
+    _fields_ = [(n, __import__("ctypes").c_int32) for n in ("sw_format", "width", "height", "initial_pool_size", "bpp",
+                                                            "ss_h", "ss_v", "async_depth", "parse_threads")]
+
+
 def test_frame_params(v9):
     import ctypes
-
-    class FP(ctypes.Structure):
-        _fields_ = [(n, ctypes.c_int32) for n in ("sw_format", "width", "height", "initial_pool_size", "bpp", "ss_h", "ss_v")]
     L = v9.lib()
-    fp = FP()
+    fp = _FP()
     assert L.vp9hip_hwaccel_frame_params(1920, 1080, 10, 1, 1, 3, ctypes.byref(fp)) == 0
-    assert (fp.sw_format, fp.width, fp.height, fp.initial_pool_size) == (4, 1920, 1080, 12)   # YUV420P10
+    # 8 slots + the frame being decoded + the batch being filled (async depth 16) + 3 extra
+    assert (fp.sw_format, fp.width, fp.height, fp.async_depth) == (4, 1920, 1080, 16)   # YUV420P10
+    assert fp.initial_pool_size == 8 + 1 + 16 + 3 and fp.parse_threads >= 1
     assert L.vp9hip_hwaccel_frame_params(64, 64, 8, 0, 0, 0, ctypes.byref(fp)) == 0 and fp.sw_format == 3
     assert L.vp9hip_hwaccel_frame_params(64, 64, 9, 1, 1, 0, ctypes.byref(fp)) == v9.EINVAL
 
@@ -56,20 +60,64 @@ def _read_frames(path, w, h, bpp, ssh, ssv):
     return out
 
 
+def run_harness(ivf, out, bpp, ssh, ssv, passes=2, lag=0, mode="download", depth=0, env=None, timeout=120):
+    """The harness binary; returns (returncode, frames, seconds, stderr)."""
+    r = subprocess.run([HARNESS, str(ivf), str(out), str(bpp), str(ssh), str(ssv), str(passes), str(lag), mode,
+                        str(depth)], capture_output=True, text=True, timeout=timeout, env=env)
+    f = r.stdout.split()
+    if r.returncode or len(f) < 4:
+        return r.returncode, None, None, r.stderr
+    return 0, int(f[1]), float(f[3]), r.stderr
+
+
+# async depth (frames per launch) x consumer lag: 16 / 0 reads each frame at once (every
+# read launches the partial batch holding it); lag 8 / depth 4 keeps batches full; depth 1
+# launches every frame from its end_frame; hidden frames ride with the next batch
 @pytest.mark.gpu
-@pytest.mark.parametrize("w,h,bpp,ssh,ssv", [(200, 130, 8, 1, 1), (176, 144, 10, 1, 1), (136, 72, 8, 0, 0)])
-def test_hwaccel_call_order_matches_oracle(v9, orc, tmp_path, w, h, bpp, ssh, ssv):
+@pytest.mark.parametrize("w,h,bpp,ssh,ssv,lag,depth", [(200, 130, 8, 1, 1, 0, 0), (176, 144, 10, 1, 1, 0, 0),
+                                                     (136, 72, 8, 0, 0, 0, 0), (200, 130, 8, 1, 1, 8, 4),
+                                                     (200, 130, 8, 1, 1, 3, 1), (176, 144, 10, 1, 1, 20, 0)])
+def test_hwaccel_call_order_matches_oracle(v9, orc, tmp_path, w, h, bpp, ssh, ssv, lag, depth):
     pkts = _stream(v9, w, h, bpp, ssh, ssv)
     ivf = tmp_path / "s.ivf"
     ivf.write_bytes(v9.ivf_write(pkts, w, h))
     out = tmp_path / "out.yuv"
-    r = subprocess.run([HARNESS, str(ivf), str(out), str(bpp), str(ssh), str(ssv), "2"], capture_output=True,
-                       text=True, timeout=120)
-    assert r.returncode == 0, r.stderr
+    rc, nout, _, err = run_harness(ivf, out, bpp, ssh, ssv, 2, lag, "download", depth)
+    assert rc == 0, err
     ref = _oracle_outputs(v9, orc, pkts)
     got = _read_frames(str(out), w, h, bpp, ssh, ssv)
-    assert r.stdout.strip() == "frames %d" % (2 * len(ref))
+    assert nout == 2 * len(ref)
     assert len(got) == 2 * len(ref)
     for i, (g, o) in enumerate(zip(got, ref + ref)):                # flush, then the same stream again
+        for p in range(3):
+            assert np.array_equal(g[p], o[p]), "frame %d plane %d" % (i, p)
+
+
+@pytest.mark.gpu
+def test_hwaccel_device_consumer_and_many_gops(v9, orc, tmp_path):
+    """A device-frame consumer (vp9hip_hwframe_sync, no download) over several GOPs and a
+    run of keyframes with full batches: the frames the harness then downloads are still
+    the oracle's (first pass device consumer, second pass download)."""
+    from test_stream import _frames
+    pkts = []
+    for g in range(3):
+        fr = _frames(v9, 176, 144, 5, seed=900 + 10 * g, compound=1)
+        enc = v9.Stream()
+        pkts.append(enc.encode(fr[0])[0])
+        for i, f in enumerate(fr[1:]):
+            pkts.append(enc.encode(f, ref_slot=(i % 8, 0, i % 8), refresh_mask=1 << ((i + 1) % 8))[0])
+    for k in range(6):
+        pkts.append(v9.Stream().encode(v9.SynthFrame(v9.synth_params(176, 144, 8, seed=990 + k)))[0])
+    ivf = tmp_path / "g.ivf"
+    ivf.write_bytes(v9.ivf_write(pkts, 176, 144))
+    rc, nout, _, err = run_harness(ivf, "-", 8, 1, 1, 1, 16, "device", 8)
+    assert rc == 0 and nout == len(pkts), err
+    out = tmp_path / "g.yuv"
+    rc, nout, _, err = run_harness(ivf, out, 8, 1, 1, 1, 16, "download", 8)
+    assert rc == 0, err
+    ref = _oracle_outputs(v9, orc, pkts)
+    got = _read_frames(str(out), 176, 144, 8, 1, 1)
+    assert len(got) == len(ref)
+    for i, (g, o) in enumerate(zip(got, ref)):
         for p in range(3):
             assert np.array_equal(g[p], o[p]), "frame %d plane %d" % (i, p)

@@ -355,3 +355,39 @@ def test_tile_threaded_parse_rejects_truncated_tiles(v9):
         with pytest.raises(v9.Vp9HipError) as e:
             v9.Stream(threads=threads).decode(d)
         assert e.value.code == v9.EINVALIDDATA
+
+
+def test_header_peek_matches_the_parse(v9):
+    """vp9h_frame_peek (no stream state) reads the same slot bookkeeping as the full parse:
+    show_existing_frame / slot, show_frame, error_res, refresh mask, LAST / GOLDEN / ALTREF
+    slots and sign bias; keyframes, inter, hidden, intra-only and show-existing headers."""
+    import ctypes
+    from test_ivf_decoder import _stream
+    L = v9.lib()
+    L.vp9h_frame_peek.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(v9.FrameInfo)]
+    streams = [_stream(v9),
+               encode_stream(v9, _frames(v9, 200, 130, 4), lambda i: {"error_res": int(i == 2)})[0]]
+    enc = v9.Stream()
+    key = enc.encode(_frames(v9, 176, 144, 1)[0])[0]
+    intra = v9.SynthFrame(v9.synth_params(176, 144, 8, seed=77))
+    intra.pkt.keyframe, intra.pkt.intraonly = 0, 1
+    streams.append([key, enc.encode(intra, show_frame=0, refresh_mask=0x24)[0]])
+    types = set()
+    for pkts in streams:
+        st = v9.Stream()
+        for data in pkts:
+            for fr in v9.superframe_split(data):
+                peek = v9.FrameInfo()
+                t = L.vp9h_frame_peek(fr, len(fr), ctypes.byref(peek))
+                assert t >= 0
+                types.add(t)
+                _, info = st.decode(fr)
+                assert (t == 2) == bool(info.show_existing_frame)
+                for k in ("show_existing_frame", "show_frame", "refresh_mask", "error_res"):
+                    assert getattr(peek, k) == getattr(info, k), k
+                if info.show_existing_frame:
+                    assert peek.show_slot == info.show_slot
+                elif t == 1:
+                    assert list(peek.ref_slot) == list(info.ref_slot)
+                    assert list(peek.sign_bias) == list(info.sign_bias)
+    assert types == {0, 1, 2, 3}
