@@ -534,7 +534,7 @@ class Device:
 
     def fill(self, buf0, count, value):
         """Fill device buffers [buf0, buf0 + count) with byte `value` (async, context stream)."""
-        _check("vp9hip_fill_buffers", "vp9hip_device_info", lib().vp9hip_fill_buffers(self._c, int(buf0), int(count), int(value)))
+        _check("vp9hip_fill_buffers", lib().vp9hip_fill_buffers(self._c, int(buf0), int(count), int(value)))
 
     def set_timing(self, on):
         _check("vp9hip_set_timing", lib().vp9hip_set_timing(self._c, int(bool(on))))

@@ -20,6 +20,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #define VP9T_STORAGE static __constant__ const
 #include "vp9_tables.h"
 #include "vp9hip_work.h"
@@ -576,6 +578,23 @@ __global__ __launch_bounds__(64 * RWAVES) void k_resid(const RJob *__restrict__ 
     const int wave = threadIdx.x >> 6;
     resid_wave<N, TCODE, PIX, M, COEF>(jobs, njobs, blockIdx.x * RWAVES + wave, threadIdx.x & 63, frames, coefs, resid,
                                        cbs[wave]);
+}
+
+// k_resid of a launch list fixed at staging (runtime "static plan"): the job range comes
+// from the planner's summary in HBM (rng = {first, end}), the grid from an upper bound
+// (capped); waves stride over the range.
+template <int N, int TCODE, typename PIX, class M, typename COEF>
+__global__ __launch_bounds__(64 * RWAVES) void k_resid_dev(const RJob *__restrict__ jobs, const uint32_t *__restrict__ rng,
+                                                           const FrameDesc *__restrict__ frames,
+                                                           const COEF *__restrict__ coefs, int16_t *__restrict__ resid)
+{
+    __shared__ COEF cbs[RWAVES][RWave<N, COEF>::E];
+    constexpr int CAP = 64 / N;
+    const uint32_t j0 = __builtin_amdgcn_readfirstlane(rng[0]), j1 = __builtin_amdgcn_readfirstlane(rng[1]);
+    const int njobs = j1 > j0 ? (int) (j1 - j0) : 0;
+    const int wave = threadIdx.x >> 6;
+    for (int wj = (int) blockIdx.x * RWAVES + wave; wj * CAP < njobs; wj += (int) gridDim.x * RWAVES)
+        resid_wave<N, TCODE, PIX, M, COEF>(jobs + j0, njobs, wj, threadIdx.x & 63, frames, coefs, resid, cbs[wave]);
 }
 
 // Every transform size of a phase in ONE launch (narrow, level-scheduled phases: the chain
@@ -2335,6 +2354,20 @@ static void launch_resid_n(int hb, hipStream_t st, int n, const RJob *jobs, cons
         hipLaunchKernelGGL((k_resid<N, TC, uint8_t, M32, int16_t>), dim3(nb), dim3(64 * RWAVES), 0, st,
                            jobs, n, frames, (const int16_t *) coefs, resid);
 }
+#define RESID_DEV_MAX_WG 8192           // grid cap of k_resid_dev (32 waves per CU)
+template <int N, int TC>
+static void launch_resid_dev_n(int hb, hipStream_t st, int ub, const RJob *jobs, const uint32_t *rng,
+                               const FrameDesc *frames, const void *coefs, int16_t *resid)
+{
+    const int per = RWAVES * (64 / N);
+    const int nb = std::min((ub + per - 1) / per, RESID_DEV_MAX_WG);
+    if (hb)
+        hipLaunchKernelGGL((k_resid_dev<N, TC, uint16_t, M64, int32_t>), dim3(nb), dim3(64 * RWAVES), 0, st,
+                           jobs, rng, frames, (const int32_t *) coefs, resid);
+    else
+        hipLaunchKernelGGL((k_resid_dev<N, TC, uint8_t, M32, int16_t>), dim3(nb), dim3(64 * RWAVES), 0, st,
+                           jobs, rng, frames, (const int16_t *) coefs, resid);
+}
 template <typename PIX, class G>
 static void launch_pred_g(hipStream_t st, int nwg, size_t pad, const uint32_t *list, const WGRec *wgs, const SBRec *sbs,
                           const PJob *jobs, const uint32_t *passes, const FrameDesc *frames, const int16_t *resid,
@@ -2441,6 +2474,20 @@ int vp9hip_launch_resid(int hb, hipStream_t st, int tcode, int n, const RJob *jo
     case 2: launch_resid_n<16, 2>(hb, st, n, jobs, frames, coefs, resid); break;
     case 3: launch_resid_n<32, 3>(hb, st, n, jobs, frames, coefs, resid); break;
     case 4: launch_resid_n<4, 4>(hb, st, n, jobs, frames, coefs, resid); break;
+    default: return -1;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int vp9hip_launch_resid_dev(int hb, hipStream_t st, int tcode, int ub, const RJob *jobs, const uint32_t *rng,
+                            const FrameDesc *frames, const void *coefs, int16_t *resid)
+{
+    if (ub <= 0) return 0;
+    switch (tcode) {
+    case 0: launch_resid_dev_n<4, 0>(hb, st, ub, jobs, rng, frames, coefs, resid); break;
+    case 1: launch_resid_dev_n<8, 1>(hb, st, ub, jobs, rng, frames, coefs, resid); break;
+    case 2: launch_resid_dev_n<16, 2>(hb, st, ub, jobs, rng, frames, coefs, resid); break;
+    case 3: launch_resid_dev_n<32, 3>(hb, st, ub, jobs, rng, frames, coefs, resid); break;
+    case 4: launch_resid_dev_n<4, 4>(hb, st, ub, jobs, rng, frames, coefs, resid); break;
     default: return -1;
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -948,6 +948,27 @@ __global__ __launch_bounds__(256) void k_plists(PlanDev D)
     if (inb(D, i, D.cap_dlists, 16384u)) D.dlists[i] = slot;
 }
 
+// ------------------------------------------------------------------ k_pguard
+// Batches whose launch list is fixed at staging (keyframe batches, runtime "static plan"):
+// their pixel kernels run after the planner without a host check of its status, so a
+// rejected batch (status[0] != 0: the packets are inconsistent) is neutralised here: no
+// intra passes (WGRec), no residual jobs (the summary's ranges); the status is re-copied
+// into the summary (k_plists' bound checks come after k_pkeys), which the host reads when
+// it next waits for the batch (vp9hip_sync / sync_slot: AVERROR_INVALIDDATA).
+__global__ __launch_bounds__(256) void k_pguard(PlanDev D, uint32_t *summary, int ng)
+{
+    const uint32_t st = __builtin_amdgcn_readfirstlane(D.status[0]);
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) summary[0] = st;
+    if (!st) return;
+    const PlanFrame &F = D.frames[blockIdx.y];
+    const int s = blockIdx.x * 256 + threadIdx.x;
+    if (blockIdx.y == 0)
+        for (int i = s; i < ng; i += (int) gridDim.x * 256) summary[1 + i] = 0;
+    if (s >= F.sb_cols * F.sb_rows) return;
+    const uint32_t slot = F.slot0 + (uint32_t) s;
+    if (slot < D.nslots) { D.wgs[slot].njobs = 0; D.wgs[slot].npass = 0; }
+}
+
 // stage 0: k_psb; 1: k_pjob, k_plan, then k_pllf (filtered frames) and k_plmc (inter frames)
 template <int SSH, int SSV>
 void launch_sb_kernels(hipStream_t st, const PlanDev &D, int max_sb, int nframes, int stage, int flags)
@@ -987,7 +1008,7 @@ size_t vp9hip_plan_scan_bytes(size_t n)
 // nb / nslots / ncnt: blocks, SB slots, count-matrix entries (each array + 1 zero entry).
 int vp9hip_plan_enqueue(hipStream_t st, const PlanDev *Dp, int ss, int nframes, int max_blk, int max_sb, uint32_t nb,
                         uint32_t nslots, uint32_t ncnt, int nk, const uint32_t *gidx, int ng, uint32_t *summary,
-                        void *scan_tmp, size_t scan_bytes, int any_levels, int flags)
+                        void *scan_tmp, size_t scan_bytes, int any_levels, int flags, int guard)
 {
     const PlanDev &D = *Dp;
     if (nframes <= 0) return 0;
@@ -1005,6 +1026,7 @@ int vp9hip_plan_enqueue(hipStream_t st, const PlanDev *Dp, int ss, int nframes, 
     if (any_levels) hipLaunchKernelGGL(k_plevel, dim3(nframes), dim3(256), 0, st, D);
     hipLaunchKernelGGL(k_pkeys, dim3(1), dim3(1024), 0, st, D, nk, gidx, ng, nframes, summary);
     hipLaunchKernelGGL(k_plists, dim3((max_sb + 255) / 256, nframes), dim3(256), 0, st, D);
+    if (guard) hipLaunchKernelGGL(k_pguard, dim3((max_sb + 255) / 256, nframes), dim3(256), 0, st, D, summary, ng);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 }

@@ -43,6 +43,8 @@ int vp9hip_launch_resid_multi(int hb, hipStream_t st, const uint32_t *off, const
                               const FrameDesc *frames, const void *coefs, int16_t *resid);
 int vp9hip_launch_resid(int hb, hipStream_t st, int tcode, int n, const RJob *jobs, const FrameDesc *frames,
                         const void *coefs, int16_t *resid);
+int vp9hip_launch_resid_dev(int hb, hipStream_t st, int tcode, int ub, const RJob *jobs, const uint32_t *rng,
+                            const FrameDesc *frames, const void *coefs, int16_t *resid);
 int vp9hip_launch_pred(int fmt, hipStream_t st, int nwg, const uint32_t *list, const WGRec *wgs, const SBRec *sbs,
                        const PJob *jobs, const uint32_t *passes, const FrameDesc *frames, const int16_t *resid,
                        const uint32_t *ptab, int dbg);
@@ -52,7 +54,7 @@ int vp9hip_launch_mc(int hb, hipStream_t st, int n, const McUnit *units, const F
 size_t vp9hip_plan_scan_bytes(size_t n);
 int vp9hip_plan_enqueue(hipStream_t st, const PlanDev *D, int ss, int nframes, int max_blk, int max_sb, uint32_t nb,
                         uint32_t nslots, uint32_t ncnt, int nk, const uint32_t *gidx, int ng, uint32_t *summary,
-                        void *scan_tmp, size_t scan_bytes, int any_levels, int flags);
+                        void *scan_tmp, size_t scan_bytes, int any_levels, int flags, int guard);
 int vp9hip_launch_lfr(int fmt, hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs,
                       const FrameDesc *frames, uint32_t *ctr);
 int vp9hip_launch_plf(int fmt, hipStream_t st, const PlfLaunch *pl, const uint32_t *plist, const uint32_t *llist,
@@ -75,6 +77,7 @@ const char *const kname[K_N] = { "k_mc", "k_resid", "k_pred", "k_lf", "k_plf", "
 struct Launch { int kind; uint32_t off; uint32_t n; int arg; int grp; int ph; int part; int step;
                 uint32_t off2 = 0, n2 = 0;
                 uint32_t roff[5] = { 0, 0, 0, 0, 0 }, rn[5] = { 0, 0, 0, 0, 0 };   // K_PLF residual jobs by tx code
+                int devr = 0;   // K_RESID of a static plan: off = the summary index of its job range, n = a bound
 };
 #define PLF_LAG 3   // see the schedule in stage()
 // Residuals run inside the fused launches (one intra diagonal ahead) for phases of fewer
@@ -169,6 +172,17 @@ struct Staged {
     uint32_t *summary_h = nullptr;                            // pinned readback of the summary
     size_t summary_cap = 0;
     hipEvent_t done_ev = nullptr;       // recorded on the main stream after this batch's last run
+    // ---- static plan (keyframe batches): the launch list is built at staging from the batch
+    // geometry (every SB of an intra frame has intra work, so the step lists' sizes and
+    // offsets are known); only the residual job ranges come from the planner, read by the
+    // kernels from the summary in HBM. A run enqueues the planner and, ordered after it by
+    // an event, the pixel launches: no host wait. The summary is read (status, the key
+    // offsets checked against the staged ones, byte totals) when the host next waits.
+    bool stat = false;
+    hipEvent_t plan_ev = nullptr;
+    bool summary_pending = false;
+    std::vector<uint32_t> exp_ko;       // key offsets the launch list was built with
+    double alg_stat[K_N] = {};          // algorithmic bytes after the launch-list moves
 };
 
 } // namespace
@@ -272,6 +286,7 @@ static void drop_slots(vp9hip_ctx *c)
         if (g->graph) hipGraphExecDestroy(g->graph);
         g->graph = nullptr;
         g->graph_launches.clear();
+        g->summary_pending = false;
     }
 }
 
@@ -289,6 +304,7 @@ extern "C" void vp9hip_close(vp9hip_ctx *c)
         if (g->graph) hipGraphExecDestroy(g->graph);
         if (g->summary_h) hipHostFree(g->summary_h);
         if (g->done_ev) hipEventDestroy(g->done_ev);
+        if (g->plan_ev) hipEventDestroy(g->plan_ev);
     }
     if (c->ptab) hipFree(c->ptab);
     if (c->nz) hipFree(c->nz);
@@ -877,6 +893,88 @@ static void init_lfr_ctr(const Staged &s, uint32_t *ctr)
     for (uint32_t o : s.lfr_ctr) ctr[o + 3] = spin;
 }
 
+// Keyframe batches (every phase wide, not fused, no k_lfr, intra frames only): the launch
+// list plan_dev would build, from the geometry. Intra frames have intra work in every SB
+// (PLS_ORDER rejects an SB without blocks), so step key k holds every SB of its phase's
+// frames on intra diagonal k - key0, and the step lists' offsets are the prefix sums of
+// those counts (k_pkeys). Residual launches take their job ranges from the summary.
+static void build_static_plan(vp9hip_ctx *c, const DevIn &in, const std::vector<uint32_t> &slot0)
+{
+    Staged &s = c->stg;
+    const char *e = getenv("VP9HIP_STATIC");           // read per stage (tests switch it)
+    const bool off = e && !atoi(e);
+    s.stat = false;
+    s.launches.clear();
+    s.exp_ko.clear();
+    if (off || !in.fuse) return;
+    const std::vector<FrameBuild> &fbs = *in.fbs;
+    for (const Staged::DevPhase &P : s.dph) {
+        if (P.frames.empty()) continue;
+        if (P.fused || P.levels || P.lfr) return;
+        for (int i : P.frames)
+            if (!(in.pkts[i].keyframe || in.pkts[i].intraonly)) return;
+    }
+    std::vector<uint32_t> kc(s.nkey, 0);
+    for (const Staged::DevPhase &P : s.dph)
+        for (int i : P.frames) {
+            const FrameBuild &fb = fbs[i];
+            for (int y = 0; y < fb.sb_rows; y++)
+                for (int x = 0; x < fb.sb_cols; x++) {
+                    int ts0;
+                    pl_tile_of(x, fb.sb_cols, fb.f->log2_tile_cols, &ts0);
+                    const uint32_t k = P.key0 + (uint32_t) ((x - ts0) + y);
+                    if (k < s.nkey) kc[k]++;
+                }
+        }
+    s.exp_ko.assign(s.nkey + 1, 0);
+    for (uint32_t k = 0; k < s.nkey; k++) s.exp_ko[k + 1] = s.exp_ko[k] + kc[k];
+    for (int k = 0; k < K_N; k++) s.alg_stat[k] = s.alg_base[k];
+    const uint32_t H = s.host_lists;
+    const int nph = (int) s.dph.size();
+    for (int g = 0; g < s.ngroups; g++)
+        for (int ph = 0; ph < nph; ph++) {
+            const Staged::DevPhase &P = s.dph[ph];
+            if (P.frames.empty() || P.group != g) continue;
+            uint32_t ub = 0;
+            bool lossy = false, lossless = false;
+            for (int i : P.frames) {
+                ub += in.pkts[i].neobs;
+                (in.pkts[i].lossless ? lossless : lossy) = true;
+            }
+            for (int tc = 0; tc < 5; tc++) {
+                if (tc < 4 ? !lossy : !lossless) continue;
+                Launch L = { K_RESID, (uint32_t) (P.g_res + tc * 2), ub, tc, g, ph, PART_RECON, 0 };
+                L.devr = 1;
+                s.launches.push_back(L);
+            }
+            const int np = P.np, nlf = P.nlf;
+            const int nt = std::max(np, nlf ? nlf + PLF_LAG : 0);
+            for (int t = 0; t < nt; t++) {
+                const uint32_t k = P.key0 + (uint32_t) t;
+                const uint32_t pn = t < np && k < s.nkey ? kc[k] : 0u;
+                const int j = t - PLF_LAG;
+                const std::pair<uint32_t, uint32_t> lv = j >= 0 && j < nlf ? P.lf[j] : std::make_pair(0u, 0u);
+                if (!pn) {
+                    if (lv.second) s.launches.push_back(Launch{ K_LF, lv.first, lv.second, 0, g, ph, PART_LF, j });
+                    continue;
+                }
+                Launch L = { K_PLF, H + s.exp_ko[k], pn, 0, g, ph, PART_RECON, t };
+                L.off2 = lv.first;
+                L.n2 = lv.second;
+                if (t < (int) P.pred_bytes.size()) {
+                    s.alg_stat[K_PRED] -= P.pred_bytes[t];
+                    s.alg_stat[K_PLF] += P.pred_bytes[t];
+                }
+                if (lv.second) {
+                    s.alg_stat[K_LF] -= P.lf_bytes[j];
+                    s.alg_stat[K_PLF] += P.lf_bytes[j];
+                }
+                s.launches.push_back(L);
+            }
+        }
+    s.stat = true;
+}
+
 static int stage_dev(vp9hip_ctx *c, const DevIn &in)
 {
     Staged &s = c->stg;
@@ -1069,6 +1167,7 @@ static int stage_dev(vp9hip_ctx *c, const DevIn &in)
     s.nblk = (uint32_t) nb; s.neob = (uint32_t) ne; s.ncoef = (uint32_t) nc;
     s.ncnt = 20 * NS;
     for (int k = 0; k < K_N; k++) s.alg_base[k] = s.alg_bytes[k];
+    build_static_plan(c, in, slot0);
     // arena: the uploaded part (one DMA from a pinned image), then the planner's buffers
     auto al = [](size_t x) { return (x + 255) & ~(size_t) 255; };
     size_t o = 0;
@@ -1188,6 +1287,36 @@ static int stage_dev(vp9hip_ctx *c, const DevIn &in)
     return 0;
 }
 
+// A static-plan batch's summary, once its run is complete (the caller waited for it):
+// planner status (AVERROR_INVALIDDATA: the batch was neutralised by k_pguard), the step-list
+// offsets checked against the ones the launch list was built with (VP9HIP_EBUG: they
+// differ), and the algorithmic byte totals.
+static int finish_summary(vp9hip_ctx *c, Staged &s)
+{
+    if (!s.stat || !s.summary_pending) return 0;
+    s.summary_pending = false;
+    HIPCHK(hipMemcpy(s.summary_h, s.arena + s.o_summary, s.summary_words * 4, hipMemcpyDeviceToHost));
+    const uint32_t *sm = s.summary_h;
+    if (sm[0]) {
+        fprintf(stderr, "vp9hip: batch rejected by the device planner (status 0x%x, bounds 0x%x)\n", sm[0],
+                sm[s.summary_words - 1]);
+        return VP9HIP_EINVALIDDATA;
+    }
+    const uint32_t *ko = sm + 1 + s.n_gidx, *fb32 = ko + s.nkey + 1;
+    for (uint32_t k = 0; k <= s.nkey; k++)
+        if (ko[k] != s.exp_ko[k]) {
+            fprintf(stderr, "vp9hip: static plan: step offset %u is %u on the device, %u staged\n", k, ko[k], s.exp_ko[k]);
+            return VP9HIP_EBUG;
+        }
+    for (int k = 0; k < K_N; k++) s.alg_bytes[k] = s.alg_stat[k];
+    s.alg_bytes[K_PLAN] = (double) s.nblk * sizeof(vp9h_block) + (double) s.neob * 2;
+    for (int i = 0; i < s.nframes; i++) {
+        s.alg_bytes[K_RESID] += (double) ((uint64_t) fb32[4 * i] | (uint64_t) fb32[4 * i + 1] << 32);
+        s.alg_bytes[K_MC] += (double) ((uint64_t) fb32[4 * i + 2] | (uint64_t) fb32[4 * i + 3] << 32);
+    }
+    return 0;
+}
+
 // Run the device planner of the staged batch and build its launch list from the summary.
 static int plan_dev(vp9hip_ctx *c)
 {
@@ -1196,7 +1325,7 @@ static int plan_dev(vp9hip_ctx *c)
     Staged &s = c->stg;
     uint8_t *A = s.arena;
     s.planned = false;
-    s.launches.clear();
+    if (!s.stat) s.launches.clear();
     // the planner runs on its own stream, after this slot's previous run (its records are
     // rewritten in place) and after whatever the main stream holds for it (the staging
     // upload); the other slot's pixel kernels run meanwhile
@@ -1270,10 +1399,18 @@ static int plan_dev(vp9hip_ctx *c)
     }
     if (vp9hip_plan_enqueue(ps, &D, c->ss_h | c->ss_v << 1, s.nframes, s.max_blk, s.max_sb, s.nblk, s.nslots,
                             s.ncnt, (int) s.nkey, (const uint32_t *) (A + s.o_gidx), (int) s.n_gidx,
-                            (uint32_t *) (A + s.o_summary), A + s.o_scan, s.scan_bytes, s.any_levels, s.plan_flags))
+                            (uint32_t *) (A + s.o_summary), A + s.o_scan, s.scan_bytes, s.any_levels, s.plan_flags,
+                            s.stat ? 1 : 0))
         return VP9HIP_EEXTERNAL;
     if (c->timing) HIPCHK(hipEventRecord(c->pev[1], ps));
     c->plan_timed = c->timing;
+    if (s.stat) {                  // launch list fixed at staging: the pixel launches wait on the device
+        if (!s.plan_ev) HIPCHK(hipEventCreateWithFlags(&s.plan_ev, hipEventDisableTiming));
+        HIPCHK(hipEventRecord(s.plan_ev, ps));
+        s.summary_pending = true;
+        s.planned = true;
+        return 0;
+    }
     HIPCHK(hipMemcpyAsync(s.summary_h, A + s.o_summary, s.summary_words * 4, hipMemcpyDeviceToHost, ps));
     HIPCHK(hipStreamSynchronize(ps));          // the pixel kernels, queued after this, read the plan
     if (pprof) {
@@ -1418,6 +1555,8 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     s.lists.clear(); s.launches.clear(); s.coefs.clear(); s.n_ctr = 0; s.lfr_ctr.clear();
     s.frame_phase.assign(n, 0); s.frame_log2.assign(n, 0);
     s.tile_lo = tile_lo; s.tile_hi = tile_hi;
+    s.stat = false;
+    s.summary_pending = false;
     for (int k = 0; k < K_N; k++) s.alg_bytes[k] = 0;
     s.ready = false;
 
@@ -1916,7 +2055,7 @@ static bool same_launches(const std::vector<Launch> &a, const std::vector<Launch
     for (size_t i = 0; i < a.size(); i++) {
         const Launch &x = a[i], &y = b[i];
         if (x.kind != y.kind || x.off != y.off || x.n != y.n || x.arg != y.arg || x.grp != y.grp || x.ph != y.ph ||
-            x.part != y.part || x.off2 != y.off2 || x.n2 != y.n2 || memcmp(x.roff, y.roff, sizeof(x.roff)) ||
+            x.part != y.part || x.off2 != y.off2 || x.n2 != y.n2 || x.devr != y.devr || memcmp(x.roff, y.roff, sizeof(x.roff)) ||
             memcmp(x.rn, y.rn, sizeof(x.rn)))
             return false;
     }
@@ -1936,6 +2075,7 @@ extern "C" int vp9hip_run_batch(vp9hip_ctx *c)
         static const bool plan_only = getenv("VP9HIP_PLAN_ONLY") && atoi(getenv("VP9HIP_PLAN_ONLY"));
         if (plan_only) return 0;          // diagnostics: the planner alone
     }
+    if (s.dev && s.stat) HIPCHK(hipStreamWaitEvent(c->st, s.plan_ev, 0));
     // this slot's last work on the main stream: its next planning waits for it
     if (!s.done_ev) HIPCHK(hipEventCreateWithFlags(&s.done_ev, hipEventDisableTiming));
     if (c->timing || !c->use_graph) {
@@ -1974,6 +2114,10 @@ static int launch_one(vp9hip_ctx *c, const Launch &L, hipStream_t st)
     case K_MC:
         return vp9hip_launch_mc(c->hb, st, (int) L.n, (const McUnit *) (s.arena + s.o_mcs) + L.off, fr);
     case K_RESID:
+        if (L.devr)
+            return vp9hip_launch_resid_dev(c->hb, st, L.arg, (int) L.n, (const RJob *) (s.arena + s.o_rjobs),
+                                           (const uint32_t *) (s.arena + s.o_summary) + 1 + L.off, fr,
+                                           s.arena + s.o_coefs, s.resid);
         if (L.arg == 5)
             return vp9hip_launch_resid_multi(c->hb, st, L.roff, L.rn, (const RJob *) (s.arena + s.o_rjobs), fr,
                                              s.arena + s.o_coefs, s.resid);
@@ -2197,8 +2341,9 @@ extern "C" int vp9hip_sync_slot(vp9hip_ctx *c, int slot)
 {
     if (!c || slot < 0 || slot > 1) return VP9HIP_EINVAL;
     hipSetDevice(c->dev);
-    const Staged &g = slot == c->slot ? c->stg : c->alt;
+    Staged &g = slot == c->slot ? c->stg : c->alt;
     if (g.done_ev) HIPCHK(hipEventSynchronize(g.done_ev));
+    if (const int r = finish_summary(c, g)) return r;
     return check_lfr(g);
 }
 
@@ -2227,6 +2372,8 @@ extern "C" int vp9hip_sync(vp9hip_ctx *c)
     hipSetDevice(c->dev);
     HIPCHK(hipStreamSynchronize(c->st));
     // every slot's pixel work is on the main stream: both slots' hand-off counters are final
+    for (Staged *g : { &c->stg, &c->alt })
+        if (const int r = finish_summary(c, *g)) return r;
     if (const int r = check_lfr(c->stg)) return r;
     if (const int r = check_lfr(c->alt)) return r;
     if (c->timing && c->timed_run && c->stg.ready) {
@@ -2338,6 +2485,11 @@ extern "C" int vp9hip_last_timing(vp9hip_ctx *c, const char **names, double *ms,
 extern "C" int vp9hip_alg_bytes(vp9hip_ctx *c, double *bytes, int cap)
 {
     if (!c) return VP9HIP_EINVAL;
+    if (c->stg.summary_pending) {            // a static plan's totals: after its run
+        hipSetDevice(c->dev);
+        HIPCHK(hipStreamSynchronize(c->st));
+        if (const int r = finish_summary(c, c->stg)) return r;
+    }
     int n = 0;
     for (int k = 0; k < K_N && n < cap; k++, n++) bytes[n] = c->stg.alg_bytes[k];
     return n;

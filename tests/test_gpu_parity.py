@@ -116,6 +116,56 @@ def test_wide_batch_separate_residual_launches(v9, orc, gpu):
         _cmp(v9, gpu.download(i), ref, w, h, "wide batch frame %d" % i)
 
 
+@pytest.mark.parametrize("static", [1, 0])
+def test_static_plan_keyframe_batch(v9, orc, gpu, monkeypatch, static):
+    """Keyframe batches of wide phases run a launch list fixed at staging (runtime "static
+    plan": no host wait between the device planner and the pixel launches; residual job
+    ranges read from the planner's summary in HBM). Same pixels as the summary-read path
+    (VP9HIP_STATIC=0), over 3 runs of the staged batch, mixed tile columns, lossless and
+    lossy frames in one phase, and 10-bit."""
+    monkeypatch.setenv("VP9HIP_STATIC", str(static))
+    for bpp in (8, 10):
+        w, h, n = 520, 136, 18
+        frames = [v9.SynthFrame(v9.synth_params(w, h, bpp, seed=500 + i, log2_tile_cols=i % 2,
+                                                **({"lossless": 1, "q_idx": 0} if i % 5 == 3 else {})))
+                  for i in range(n)]
+        gpu.configure(w, h, bpp, nbufs=n)
+        gpu.stage_batch(frames, list(range(n)))
+        for _ in range(3):
+            gpu.run_batch()
+        gpu.sync()
+        assert sum(gpu.alg_bytes().values()) > 0
+        for i in range(n):
+            ref = v9.alloc_planes(w, h, bpp)
+            orc.decode_frame(frames[i].pkt, ref)
+            _cmp(v9, gpu.download(i), ref, w, h, "static=%d %d-bit batch frame %d" % (static, bpp, i))
+
+
+def test_static_plan_rejects_inconsistent_packets(v9, orc, gpu):
+    """A packet the device planner rejects (an intra mode > 9) in a static-plan batch: the
+    planner neutralises the batch on the device (k_pguard) and the next wait reports
+    AVERROR_INVALIDDATA; the context then decodes a clean batch bit-exact."""
+    w, h, n = 352, 288, 16
+    frames = [v9.SynthFrame(v9.synth_params(w, h, 8, seed=700 + i)) for i in range(n)]
+    gpu.configure(w, h, 8, nbufs=n)
+    b = frames[5].pkt.blocks[3]
+    saved = b.mode[0]
+    b.mode[0] = 20
+    gpu.stage_batch(frames, list(range(n)))
+    gpu.run_batch()
+    with pytest.raises(v9.Vp9HipError) as e:
+        gpu.sync()
+    assert e.value.code == v9.EINVALIDDATA
+    b.mode[0] = saved
+    gpu.stage_batch(frames, list(range(n)))
+    gpu.run_batch()
+    gpu.sync()
+    for i in (0, 5, 15):
+        ref = v9.alloc_planes(w, h, 8)
+        orc.decode_frame(frames[i].pkt, ref)
+        _cmp(v9, gpu.download(i), ref, w, h, "clean batch frame %d" % i)
+
+
 def test_decoder_api_sequence(v9, orc):
     """send_packet / receive_frame over a key + 3 inter frames."""
     w, h = 160, 96
