@@ -21,6 +21,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #define VP9T_STORAGE static __constant__ const
 #include "vp9_tables.h"
@@ -581,8 +582,10 @@ __global__ __launch_bounds__(64 * RWAVES) void k_resid(const RJob *__restrict__ 
 }
 
 // k_resid of a launch list fixed at staging (runtime "static plan"): the job range comes
-// from the planner's summary in HBM (rng = {first, end}), the grid from an upper bound
-// (capped); waves stride over the range.
+// from the planner's summary in HBM (rng = {first, end}); the grid is sized from a staged
+// bound on the range (every tx block of the coded blocks), so one wave per 64 / N jobs as
+// in k_resid, the waves past the range returning at once (a strided loop here costs 15-20
+// VGPRs and measurably slower launches beside the other frame group's).
 template <int N, int TCODE, typename PIX, class M, typename COEF>
 __global__ __launch_bounds__(64 * RWAVES) void k_resid_dev(const RJob *__restrict__ jobs, const uint32_t *__restrict__ rng,
                                                            const FrameDesc *__restrict__ frames,
@@ -592,9 +595,9 @@ __global__ __launch_bounds__(64 * RWAVES) void k_resid_dev(const RJob *__restric
     constexpr int CAP = 64 / N;
     const uint32_t j0 = __builtin_amdgcn_readfirstlane(rng[0]), j1 = __builtin_amdgcn_readfirstlane(rng[1]);
     const int njobs = j1 > j0 ? (int) (j1 - j0) : 0;
-    const int wave = threadIdx.x >> 6;
-    for (int wj = (int) blockIdx.x * RWAVES + wave; wj * CAP < njobs; wj += (int) gridDim.x * RWAVES)
-        resid_wave<N, TCODE, PIX, M, COEF>(jobs + j0, njobs, wj, threadIdx.x & 63, frames, coefs, resid, cbs[wave]);
+    const int wave = threadIdx.x >> 6, wj = (int) blockIdx.x * RWAVES + wave;
+    if (wj * CAP >= njobs) return;
+    resid_wave<N, TCODE, PIX, M, COEF>(jobs + j0, njobs, wj, threadIdx.x & 63, frames, coefs, resid, cbs[wave]);
 }
 
 // Every transform size of a phase in ONE launch (narrow, level-scheduled phases: the chain
@@ -2354,13 +2357,12 @@ static void launch_resid_n(int hb, hipStream_t st, int n, const RJob *jobs, cons
         hipLaunchKernelGGL((k_resid<N, TC, uint8_t, M32, int16_t>), dim3(nb), dim3(64 * RWAVES), 0, st,
                            jobs, n, frames, (const int16_t *) coefs, resid);
 }
-#define RESID_DEV_MAX_WG 8192           // grid cap of k_resid_dev (32 waves per CU)
 template <int N, int TC>
 static void launch_resid_dev_n(int hb, hipStream_t st, int ub, const RJob *jobs, const uint32_t *rng,
                                const FrameDesc *frames, const void *coefs, int16_t *resid)
 {
     const int per = RWAVES * (64 / N);
-    const int nb = std::min((ub + per - 1) / per, RESID_DEV_MAX_WG);
+    const int nb = (ub + per - 1) / per;
     if (hb)
         hipLaunchKernelGGL((k_resid_dev<N, TC, uint16_t, M64, int32_t>), dim3(nb), dim3(64 * RWAVES), 0, st,
                            jobs, rng, frames, (const int32_t *) coefs, resid);

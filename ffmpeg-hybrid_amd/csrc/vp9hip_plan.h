@@ -87,6 +87,8 @@ typedef struct PlanDev {
     uint32_t cap_cnt, cap_cntm, cap_rjobs, cap_mcs, cap_dlists, nkeys, nframes;
     unsigned long long *prof;        /* diagnostics (VP9HIP_PLAN_PROF): k_plan cycles per phase, or null */
     int dbg;                         /* diagnostics (VP9HIP_PLAN_DBG): ablation switches, timing only */
+    int static_lists;                /* the intra step lists were staged by the host (static plan):  */
+                                     /* no step keys; an intra-frame SB without intra jobs fails    */
 } PlanDev;
 
 #endif

@@ -355,7 +355,7 @@ template <int JCAP> struct PlanLds {
         uint16_t jmap[3][256];    // producing job of each 4x4 unit
         struct {
             uint32_t hgt[JCAP];           // longest path to a sink (list-scheduling priority)
-            uint16_t doff[JCAP + 1];      // producers of job j: dep[doff[j] .. doff[j + 1])
+            uint16_t doff[JCAP + 1];      // producers of job j: dep[2 (doff & 2047) ..] (count doff >> 11)
             uint16_t dep[4 * JCAP];
             uint16_t ord[JCAP];           // jobs by (height desc, index asc)
             uint16_t sch[JCAP];           // pass of each job (0xffff: not yet)
@@ -593,26 +593,24 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
         });
     };
     {
+        // one enumeration: job j's list starts at the prefix sum of the per-size bounds (an
+        // n-unit job reads at most 2n + 2 units: its left column, and the top row with the
+        // top-left and top-right units; 4 * JCAP for a tiling of 4x4 jobs): every bound is
+        // even, so doff[j] holds the start / 2 in bits 0-10 and the length in bits 11-15
         uint32_t carry = 0;
         for (int c = 0; c < NJ; c += 64) {
             const int j = c + lane;
-            uint32_t n = 0;
-            if (j < NJ) deps_of(j, [&](int) { n++; });
-            const uint32_t incl = wscan_incl(n, lane);
-            if (j < NJ) S.u.b.doff[j] = (uint16_t) (carry + incl - n);
+            const uint32_t cap = j < NJ ? 2u * (1u << ((S.ja[j] >> 2) & 3)) + 2u : 0u;
+            const uint32_t incl = wscan_incl(cap, lane);
+            const uint32_t off = carry + incl - cap;
+            if (j < NJ) {
+                uint32_t k = off;
+                if (off + cap <= 4u * JCAP) deps_of(j, [&](int d) { if (k < off + cap) S.u.b.dep[k++] = (uint16_t) d; });
+                else st |= PLS_SCHED;
+                S.u.b.doff[j] = (uint16_t) (off >> 1 | (k - off) << 11);
+                S.u.b.sch[j] = 0xffff;
+            }
             carry += rdl(incl, 63);
-        }
-        if (carry > 4 * JCAP) {             // more producers than valid tilings allow: no order
-            st |= PLS_SCHED;
-            for (int j = lane; j <= NJ; j += 64) S.u.b.doff[j] = 0;
-            carry = 0;
-        }
-        if (lane == 0) S.u.b.doff[NJ] = (uint16_t) carry;
-        wsync();
-        for (int j = lane; j < NJ; j += 64) {
-            int k = S.u.b.doff[j];
-            if (carry) deps_of(j, [&](int d) { S.u.b.dep[k++] = (uint16_t) d; });
-            S.u.b.sch[j] = 0xffff;
         }
         wsync();                              // jmap is dead: hgt overlays it
         for (int j = lane; j < NJ; j += 64) S.u.b.hgt[j] = 1;
@@ -625,7 +623,8 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
     // per job of a chain inside it); its last round pushes final heights to every producer
     for (int c = ((NJ - 1) & ~63); c >= 0; c -= 64) {
         const int j = c + lane;
-        const int k0 = j < NJ ? S.u.b.doff[j] : 0, k1 = j < NJ ? S.u.b.doff[j + 1] : 0;
+        const uint32_t dw = j < NJ ? S.u.b.doff[j] : 0u;
+        const int k0 = (int) (dw & 2047) << 1, k1 = k0 + (int) (dw >> 11);
         for (int it = 0; it < 65; it++) {
             bool ch = false;                  // a job of this chunk rose
             if (j < NJ) {
@@ -681,9 +680,11 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
             const int pos = c + lane;
             const int j = pos < NJ ? S.u.b.ord[pos] : 0;
             bool cand = pos < NJ && S.u.b.sch[j] == 0xffff;
-            if (cand)
-                for (int k = S.u.b.doff[j]; k < S.u.b.doff[j + 1]; k++)
+            if (cand) {
+                const uint32_t dw = S.u.b.doff[j];
+                for (int k = (int) (dw & 2047) << 1, k1 = k + (int) (dw >> 11); k < k1; k++)
                     if (S.u.b.sch[S.u.b.dep[k]] >= (uint16_t) npass) { cand = false; break; }
+            }
             const int sz = 4 << ((S.ja[j] >> 2) & 3);
             // takes in priority order by lane-size prefix sums: round 1 takes the longest
             // prefix of the chunk's ready jobs that fits, later rounds refill the remaining
@@ -773,7 +774,9 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
     if (lane == 0) {
         const uint32_t has = done > 0;
         D.sb_info[slot] = has | dmask;
-        if (has && !(F.levels && !F.intra)) {
+        if (D.static_lists) {
+            if (!has && G.mine) st |= PLS_SCHED;          // the staged step list holds every SB
+        } else if (has && !(F.levels && !F.intra)) {
             const uint32_t key = F.key0 + (uint32_t) ((G.sbx - G.tile_sb0) + G.sby);
             D.sb_key[slot] = key;
             D.sb_kpos[slot] = inb(D, key, D.nkeys, 1024u) ? atomicAdd(&D.key_cnt[key], 1u) : 0u;
@@ -1025,7 +1028,7 @@ int vp9hip_plan_enqueue(hipStream_t st, const PlanDev *Dp, int ss, int nframes, 
     launch_sb(ss, st, D, max_sb, nframes, 1, flags);
     if (any_levels) hipLaunchKernelGGL(k_plevel, dim3(nframes), dim3(256), 0, st, D);
     hipLaunchKernelGGL(k_pkeys, dim3(1), dim3(1024), 0, st, D, nk, gidx, ng, nframes, summary);
-    hipLaunchKernelGGL(k_plists, dim3((max_sb + 255) / 256, nframes), dim3(256), 0, st, D);
+    if (!D.static_lists) hipLaunchKernelGGL(k_plists, dim3((max_sb + 255) / 256, nframes), dim3(256), 0, st, D);
     if (guard) hipLaunchKernelGGL(k_pguard, dim3((max_sb + 255) / 256, nframes), dim3(256), 0, st, D, summary, ng);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -182,6 +182,7 @@ struct Staged {
     hipEvent_t plan_ev = nullptr;
     bool summary_pending = false;
     std::vector<uint32_t> exp_ko;       // key offsets the launch list was built with
+    std::vector<uint32_t> stat_lists;   // the intra step lists (uploaded with the batch)
     double alg_stat[K_N] = {};          // algorithmic bytes after the launch-list moves
 };
 
@@ -249,11 +250,18 @@ extern "C" int vp9hip_open(int device, vp9hip_ctx **out)
     // streams in the order their work is busiest: the frame groups' streams, then the
     // planner's, so that (with the default 4 hardware queues, GPU_MAX_HW_QUEUES) each lands
     // on a queue of its own; the LF-overlap streams only when that mode is on
-    bool ok = hipSetDevice(device) == hipSuccess && hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) == hipSuccess &&
+    // VP9HIP_PRIO (A/B): 1 the planner stream at the lowest priority, 2 the pixel streams at
+    // the highest (hipDeviceGetStreamPriorityRange), 0 all default
+    int prio_lo = 0, prio_hi = 0, prio = 0;
+    if (const char *g = getenv("VP9HIP_PRIO")) prio = atoi(g);
+    hipSetDevice(device);
+    if (prio) hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+    const int pix_prio = prio == 2 ? prio_hi : 0, plan_prio = prio == 1 ? prio_lo : 0;
+    bool ok = hipStreamCreateWithPriority(&c->st, hipStreamNonBlocking, pix_prio) == hipSuccess &&
               hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) == hipSuccess;
     for (int i = 0; ok && i < c->max_groups - 1; i++)
-        ok = hipStreamCreateWithFlags(&c->xst[i], hipStreamNonBlocking) == hipSuccess;
-    ok = ok && hipStreamCreateWithFlags(&c->pst, hipStreamNonBlocking) == hipSuccess;
+        ok = hipStreamCreateWithPriority(&c->xst[i], hipStreamNonBlocking, pix_prio) == hipSuccess;
+    ok = ok && hipStreamCreateWithPriority(&c->pst, hipStreamNonBlocking, plan_prio) == hipSuccess;
     for (int i = 0; ok && i < MAX_GROUPS - 1; i++)
         ok = hipEventCreateWithFlags(&c->join_ev[i], hipEventDisableTiming) == hipSuccess;
     for (int i = 0; ok && i < MAX_GROUPS; i++)
@@ -928,6 +936,21 @@ static void build_static_plan(vp9hip_ctx *c, const DevIn &in, const std::vector<
         }
     s.exp_ko.assign(s.nkey + 1, 0);
     for (uint32_t k = 0; k < s.nkey; k++) s.exp_ko[k + 1] = s.exp_ko[k] + kc[k];
+    // the step lists themselves (k_plists' output): key k's SBs, frames in phase order,
+    // raster order inside a frame
+    s.stat_lists.assign(s.exp_ko[s.nkey], 0);
+    std::vector<uint32_t> fill(s.exp_ko.begin(), s.exp_ko.end() - 1);
+    for (const Staged::DevPhase &P : s.dph)
+        for (int i : P.frames) {
+            const FrameBuild &fb = fbs[i];
+            for (int y = 0; y < fb.sb_rows; y++)
+                for (int x = 0; x < fb.sb_cols; x++) {
+                    int ts0;
+                    pl_tile_of(x, fb.sb_cols, fb.f->log2_tile_cols, &ts0);
+                    const uint32_t k = P.key0 + (uint32_t) ((x - ts0) + y);
+                    if (k < s.nkey) s.stat_lists[fill[k]++] = slot0[i] + (uint32_t) (y * fb.sb_cols + x);
+                }
+        }
     for (int k = 0; k < K_N; k++) s.alg_stat[k] = s.alg_base[k];
     const uint32_t H = s.host_lists;
     const int nph = (int) s.dph.size();
@@ -935,15 +958,25 @@ static void build_static_plan(vp9hip_ctx *c, const DevIn &in, const std::vector<
         for (int ph = 0; ph < nph; ph++) {
             const Staged::DevPhase &P = s.dph[ph];
             if (P.frames.empty() || P.group != g) continue;
-            uint32_t ub = 0;
-            bool lossy = false, lossless = false;
+            // per transform code, the tx blocks of the phase's coded blocks: a bound of its
+            // residual jobs (those with eob > 0) that sizes the launch as the summary's count would
+            uint64_t ub[5] = { 0, 0, 0, 0, 0 };
             for (int i : P.frames) {
-                ub += in.pkts[i].neobs;
-                (in.pkts[i].lossless ? lossless : lossy) = true;
+                const vp9h_frame &f = in.pkts[i];
+                const FrameBuild &fb = fbs[i];
+                for (uint32_t k = 0; k < f.nblocks; k++) {
+                    const vp9h_block &b = f.blocks[k];
+                    if (b.skip || b.bs >= VP9H_N_BS || b.tx > 3 || b.uvtx > 3) continue;
+                    for (int p = 0; p < 3; p++) {
+                        const PlTxGrid gr = pl_txgrid(b, p, fb.cols, fb.rows, c->ss_h, c->ss_v);
+                        ub[f.lossless ? 4 : gr.txs] += (uint64_t) (gr.nx * gr.ny);
+                    }
+                }
             }
             for (int tc = 0; tc < 5; tc++) {
-                if (tc < 4 ? !lossy : !lossless) continue;
-                Launch L = { K_RESID, (uint32_t) (P.g_res + tc * 2), ub, tc, g, ph, PART_RECON, 0 };
+                if (!ub[tc]) continue;
+                Launch L = { K_RESID, (uint32_t) (P.g_res + tc * 2), (uint32_t) std::min<uint64_t>(ub[tc], 0xffffffffu), tc,
+                             g, ph, PART_RECON, 0 };
                 L.devr = 1;
                 s.launches.push_back(L);
             }
@@ -1255,6 +1288,10 @@ static int stage_dev(vp9hip_ctx *c, const DevIn &in)
     if (!seg_pre1.empty()) memcpy(img + s.o_segpre1, seg_pre1.data(), seg_pre1.size() * 4);
     if (!gidx.empty()) memcpy(img + s.o_gidx, gidx.data(), gidx.size() * 4);
     if (!hl.empty()) memcpy(img + s.o_lists, hl.data(), hl.size() * 4);
+    if (s.stat && !s.stat_lists.empty()) {
+        if (s.stat_lists.size() > NS) return VP9HIP_EBUG;
+        memcpy(img + s.o_lists + hl.size() * 4, s.stat_lists.data(), s.stat_lists.size() * 4);
+    }
     init_lfr_ctr(s, (uint32_t *) (img + s.o_ctr));
     {   // packets: blocks, eobs, coefficients (frames copied in parallel)
         std::atomic<int> next(0);
@@ -1303,11 +1340,6 @@ static int finish_summary(vp9hip_ctx *c, Staged &s)
         return VP9HIP_EINVALIDDATA;
     }
     const uint32_t *ko = sm + 1 + s.n_gidx, *fb32 = ko + s.nkey + 1;
-    for (uint32_t k = 0; k <= s.nkey; k++)
-        if (ko[k] != s.exp_ko[k]) {
-            fprintf(stderr, "vp9hip: static plan: step offset %u is %u on the device, %u staged\n", k, ko[k], s.exp_ko[k]);
-            return VP9HIP_EBUG;
-        }
     for (int k = 0; k < K_N; k++) s.alg_bytes[k] = s.alg_stat[k];
     s.alg_bytes[K_PLAN] = (double) s.nblk * sizeof(vp9h_block) + (double) s.neob * 2;
     for (int i = 0; i < s.nframes; i++) {
@@ -1386,6 +1418,7 @@ static int plan_dev(vp9hip_ctx *c)
     static const bool pprof = getenv("VP9HIP_PLAN_PROF") && atoi(getenv("VP9HIP_PLAN_PROF"));
     static const int pdbg = getenv("VP9HIP_PLAN_DBG") ? atoi(getenv("VP9HIP_PLAN_DBG")) : 0;
     D.dbg = pdbg;
+    D.static_lists = s.stat ? 1 : 0;
     D.prof = nullptr;
     if (pprof) {
         if (!c->plan_prof && hipMalloc(&c->plan_prof, 16 * sizeof(unsigned long long)) != hipSuccess) return VP9HIP_ENOMEM;
@@ -1400,13 +1433,18 @@ static int plan_dev(vp9hip_ctx *c)
     if (vp9hip_plan_enqueue(ps, &D, c->ss_h | c->ss_v << 1, s.nframes, s.max_blk, s.max_sb, s.nblk, s.nslots,
                             s.ncnt, (int) s.nkey, (const uint32_t *) (A + s.o_gidx), (int) s.n_gidx,
                             (uint32_t *) (A + s.o_summary), A + s.o_scan, s.scan_bytes, s.any_levels, s.plan_flags,
-                            s.stat ? 1 : 0))
+                            s.stat && !(getenv("VP9HIP_PGUARD") && !atoi(getenv("VP9HIP_PGUARD"))) ? 1 : 0))
         return VP9HIP_EEXTERNAL;
     if (c->timing) HIPCHK(hipEventRecord(c->pev[1], ps));
     c->plan_timed = c->timing;
     if (s.stat) {                  // launch list fixed at staging: the pixel launches wait on the device
         if (!s.plan_ev) HIPCHK(hipEventCreateWithFlags(&s.plan_ev, hipEventDisableTiming));
         HIPCHK(hipEventRecord(s.plan_ev, ps));
+        static const bool ssync = getenv("VP9HIP_STATIC_SYNC") && atoi(getenv("VP9HIP_STATIC_SYNC"));
+        if (ssync) {                           // A/B diagnostics only: the summary-read path's host pacing
+            HIPCHK(hipMemcpyAsync(s.summary_h, A + s.o_summary, s.summary_words * 4, hipMemcpyDeviceToHost, ps));
+            HIPCHK(hipStreamSynchronize(ps));
+        }
         s.summary_pending = true;
         s.planned = true;
         return 0;
@@ -1471,9 +1509,14 @@ static int plan_dev(vp9hip_ctx *c)
                 Launch L = { K_RESID, 0, 0, 5, g, ph, PART_RECON, 0 };
                 for (int tc = 0; tc < 5; tc++) { L.roff[tc] = rr(0, tc).first; L.rn[tc] = rr(0, tc).second; L.n += L.rn[tc]; }
                 if (L.n) s.launches.push_back(L);
-            } else if (!P.fused)
+            } else if (!P.fused) {
+                static const bool rdev = getenv("VP9HIP_RESID_DEV") && atoi(getenv("VP9HIP_RESID_DEV"));   // A/B only
                 for (int tc = 0; tc < 5; tc++)
-                    if (rr(0, tc).second) push(K_RESID, rr(0, tc).first, rr(0, tc).second, tc, PART_RECON, 0);
+                    if (rr(0, tc).second) {
+                        push(K_RESID, rdev ? (uint32_t) (P.g_res + tc * 2) : rr(0, tc).first, rr(0, tc).second, tc, PART_RECON, 0);
+                        s.launches.back().devr = rdev;
+                    }
+            }
             auto step = [&](int d) {
                 const uint32_t k = P.key0 + (uint32_t) d;
                 return std::make_pair(H + ko[k], ko[k + 1] - ko[k]);
@@ -2075,7 +2118,11 @@ extern "C" int vp9hip_run_batch(vp9hip_ctx *c)
         static const bool plan_only = getenv("VP9HIP_PLAN_ONLY") && atoi(getenv("VP9HIP_PLAN_ONLY"));
         if (plan_only) return 0;          // diagnostics: the planner alone
     }
-    if (s.dev && s.stat) HIPCHK(hipStreamWaitEvent(c->st, s.plan_ev, 0));
+    if (s.dev && s.stat) {
+        static const bool hw = getenv("VP9HIP_STATIC_HOSTWAIT") && atoi(getenv("VP9HIP_STATIC_HOSTWAIT"));
+        if (hw) HIPCHK(hipEventSynchronize(s.plan_ev));          // A/B diagnostics only
+        else HIPCHK(hipStreamWaitEvent(c->st, s.plan_ev, 0));
+    }
     // this slot's last work on the main stream: its next planning waits for it
     if (!s.done_ev) HIPCHK(hipEventCreateWithFlags(&s.done_ev, hipEventDisableTiming));
     if (c->timing || !c->use_graph) {
@@ -2601,6 +2648,31 @@ extern "C" int vp9hip_plan_stats(const vp9h_frame *f, double *out, int cap)
                 lanes[lv[k]] += 4 << PJ_TS(jobs[k]);
             }
             for (int l : lanes) out[17] += (l + 63) / 64;
+        }
+    }
+    if (cap > 18) {                     // passes of first-fit packing in decode order: each job
+                                        // into the first pass after its producers' with room
+        for (size_t sbi = 0; sbi < s.sbh.size(); sbi++) {
+            const Staged::SBHost &h = s.sbh[sbi];
+            const int N = (int) h.njobs;
+            const PJob *jobs = s.sbjobs.data() + h.job0;
+            const uint32_t *d0 = s.jdep0.data() + h.job0 + sbi;
+            std::vector<int> ps(N, 0), room, hg(N, 1), order(N);
+            for (int k = N - 1; k >= 0; k--)                      // heights (producers precede consumers)
+                for (uint32_t q = d0[k]; q < d0[k + 1]; q++) hg[s.jdeps[q]] = std::max(hg[s.jdeps[q]], hg[k] + 1);
+            for (int k = 0; k < N; k++) order[k] = k;
+            if (cap > 19) std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return hg[a] > hg[b]; });
+            for (int kk = 0; kk < N; kk++) {
+                const int k = order[kk];
+                int e = 0;
+                for (uint32_t q = d0[k]; q < d0[k + 1]; q++) e = std::max(e, ps[s.jdeps[q]] + 1);
+                const int sz = 4 << PJ_TS(jobs[k]);
+                while ((int) room.size() <= e) room.push_back(64);
+                while (room[e] < sz) { e++; if ((int) room.size() <= e) room.push_back(64); }
+                room[e] -= sz;
+                ps[k] = e;
+            }
+            out[cap > 19 ? 19 : 18] += (double) room.size();
         }
     }
     if (cap > 16) {                     // intra steps of the level schedule (inter frames)
