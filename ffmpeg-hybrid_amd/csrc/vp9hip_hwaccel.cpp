@@ -14,9 +14,11 @@
 //     entropy decode on the parse pool (vp9hip_parse.h): keyframes start new chains, so
 //     they parse in parallel; a lone chain's tile columns parse on the idle threads.
 //   - end_frame maps refidx to device buffers, replaces the slots of refreshrefmask and
-//     appends the frame to the batch being filled; every `async_depth` frames the batch is
-//     staged into the context's free batch slot and launched (vp9hip_stage_batch_refs /
-//     run_batch: dependent frames chained, independent chains concurrent).
+//     appends the frame to the batch being filled. A batch of `async_depth` frames is staged
+//     into the context's free batch slot and launched (vp9hip_stage_batch_refs / run_batch:
+//     dependent frames chained, independent chains concurrent) once its parses are done,
+//     checked at each later end_frame, so the pool parses the next batch meanwhile; with
+//     more than two filled batches waiting the oldest launches anyway.
 //   - A frame handed out is a device frame whose pixels are complete once
 //     vp9hip_hwframe_sync (host) or vp9hip_hwframe_ready (a consumer's HIP stream) says so;
 //     both launch the batch holding it if it is still being filled. transfer syncs.
@@ -32,6 +34,7 @@
 #include <cstdlib>
 #include <thread>
 #include <cstring>
+#include <deque>
 #include <memory>
 #include <vector>
 
@@ -63,6 +66,7 @@ struct vp9hip_hwaccel {
     int intra = 0;
     vp9h_frame_info info;                   // the peeked header of the current frame
     std::vector<Pend> batch;                // the batch being filled
+    std::deque<std::vector<Pend>> full;     // filled batches waiting for their parses (decode order)
     uint64_t launched = 0;                  // batches launched; batch b ran in slot (b - 1) & 1
     uint64_t slot_seq[2] = { 0, 0 };
     bool slot_checked[2] = { true, true };
@@ -145,14 +149,14 @@ static bool batch_bad(const vp9hip_hwaccel *h, uint64_t seq)
     return false;
 }
 
-// Stage + launch the batch being filled in the next batch slot. Its packets are parsed
-// by now or soon: wait for them (in decode order).
-static int submit(vp9hip_hwaccel *h)
+// Stage + launch one batch in the next batch slot. Its packets are parsed by now or soon:
+// wait for them (in decode order).
+static int submit_list(vp9hip_hwaccel *h, std::vector<Pend> &batch)
 {
-    if (h->batch.empty()) return 0;
-    const int n = (int) h->batch.size();
+    if (batch.empty()) return 0;
+    const int n = (int) batch.size();
     int err = 0;
-    for (auto &p : h->batch) {
+    for (auto &p : batch) {
         h->pool->wait(p.job.get());
         const vp9h_frame &f = p.job->pkt;
         int e = p.job->ret;
@@ -169,9 +173,9 @@ static int submit(vp9hip_hwaccel *h)
         std::vector<vp9h_frame> pk(n);
         std::vector<int> outs(n), refs(3 * n);
         for (int i = 0; i < n; i++) {
-            pk[i] = h->batch[i].job->pkt;
-            outs[i] = h->batch[i].out;
-            for (int r = 0; r < 3; r++) refs[3 * i + r] = h->batch[i].refs[r] >= 0 ? h->batch[i].refs[r] : 0;
+            pk[i] = batch[i].job->pkt;
+            outs[i] = batch[i].out;
+            for (int r = 0; r < 3; r++) refs[3 * i + r] = batch[i].refs[r] >= 0 ? batch[i].refs[r] : 0;
         }
         ret = vp9hip_stage_batch_refs(h->gpu, pk.data(), n, outs.data(), refs.data());   // copies the packets
         if (ret >= 0) ret = vp9hip_run_batch(h->gpu);
@@ -181,15 +185,53 @@ static int submit(vp9hip_hwaccel *h)
             h->slot_checked[slot] = false;
         }
     }
-    for (auto &p : h->batch) {
+    for (auto &p : batch) {
         h->pend[p.out] = 0;
         for (int r = 0; r < 3; r++)
             if (p.refs[r] >= 0) h->inref[p.refs[r]]--;
         h->buf_seq[p.out] = ret < 0 ? 0 : h->launched;
         h->buf_err[p.out] = ret < 0 ? ret : 0;
     }
-    h->batch.clear();                        // the jobs free their packets
+    batch.clear();                           // the jobs free their packets
     return ret < 0 ? ret : 0;
+}
+
+// Launch every queued batch in decode order (the filled ones, then, with partial, the one
+// being filled); the first error, after all were handled.
+static int submit(vp9hip_hwaccel *h, bool partial = true)
+{
+    int err = 0;
+    while (!h->full.empty()) {
+        const int r = submit_list(h, h->full.front());
+        h->full.pop_front();
+        if (r < 0 && !err) err = r;
+    }
+    if (partial) {
+        const int r = submit_list(h, h->batch);
+        if (r < 0 && !err) err = r;
+    }
+    return err;
+}
+
+// The filled batches whose parses are done launch now, without waiting; more than two
+// filled batches waiting launch the oldest anyway (bounds the frames in flight). The parse
+// pool meanwhile works on the frames the caller keeps handing over.
+static int pump(vp9hip_hwaccel *h)
+{
+    int err = 0;
+    while (!h->full.empty()) {
+        bool ready = h->full.size() > 2;
+        if (!ready) {
+            ready = true;
+            for (auto &p : h->full.front())
+                if (!h->pool->done(p.job.get())) { ready = false; break; }
+        }
+        if (!ready) break;
+        const int r = submit_list(h, h->full.front());
+        h->full.pop_front();
+        if (r < 0 && !err) err = r;
+    }
+    return err;
 }
 
 static bool buf_busy(const vp9hip_hwaccel *h, int b)
@@ -214,7 +256,7 @@ extern "C" int vp9hip_hwaccel_start_frame(vp9hip_hwaccel *h, const uint8_t *buf,
     h->job.reset();                          // a frame that never reached end_frame
     h->cur = -1;
     int b = find_free(h);
-    if (b < 0 && !h->batch.empty()) {        // unreferenced hidden frames free up once launched
+    if (b < 0 && (!h->batch.empty() || !h->full.empty())) {   // unreferenced hidden frames free up once launched
         const int r = submit(h);
         if (r < 0) return r;
         b = find_free(h);
@@ -285,9 +327,11 @@ extern "C" int vp9hip_hwaccel_end_frame(vp9hip_hwaccel *h, vp9hip_hwframe *out)
     const int shown = h->info.show_frame != 0;
     h->cur = -1;
     if ((int) h->batch.size() >= h->fp.async_depth) {
-        const int r = submit(h);
-        if (r < 0) return r;
+        h->full.push_back(std::move(h->batch));
+        h->batch.clear();
     }
+    const int r = pump(h);
+    if (r < 0) return r;
     return shown;
 }
 
@@ -345,6 +389,7 @@ extern "C" int vp9hip_hwaccel_uninit(vp9hip_hwaccel *h)
         vp9hip_sync(h->gpu);
     }
     h->batch.clear();
+    h->full.clear();
     h->pool.reset();
     h->chain.reset();
     if (h->gpu) vp9hip_close(h->gpu);
@@ -361,12 +406,8 @@ extern "C" void vp9hip_hwaccel_flush(vp9hip_hwaccel *h)
     if (submit(h) >= 0) {
         for (int s = 0; s < 2; s++) check_slot(h, s);
     }
-    for (auto &p : h->batch) {              // a failed launch leaves them here
-        h->pend[p.out] = 0;
-        for (int r = 0; r < 3; r++)
-            if (p.refs[r] >= 0) h->inref[p.refs[r]]--;
-    }
     h->batch.clear();
+    h->full.clear();
     for (int i = 0; i < 8; i++) h->slot[i] = -1;
     h->chain.reset();                        // the next frame must be a keyframe
     vp9hip_sync(h->gpu);

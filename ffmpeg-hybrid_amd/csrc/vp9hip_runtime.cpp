@@ -183,6 +183,8 @@ struct Staged {
     bool summary_pending = false;
     std::vector<uint32_t> exp_ko;       // key offsets the launch list was built with
     std::vector<uint32_t> stat_lists;   // the intra step lists (uploaded with the batch)
+    std::vector<int> wr, rd;            // frame buffers the batch writes / reads (sorted)
+    bool dep_other = false;             // it touches a buffer of the other slot's batch
     double alg_stat[K_N] = {};          // algorithmic bytes after the launch-list moves
 };
 
@@ -220,7 +222,14 @@ struct vp9hip_ctx {
     Staged alt;                         // the other slot (vp9hip_set_batch_slot swaps them)
     int slot = 0;
     hipStream_t pst = nullptr;          // device planner stream: a slot's planning overlaps the
-                                        // other slot's pixel kernels
+                                        // other slot's pixel kernels (VP9HIP_SLOT_STREAMS=0 only)
+    // Per-slot streams (default): each batch slot has its own main and group streams, swapped
+    // into st / xst with the slot, and plans on its main stream ahead of its pixel work. Two
+    // staged batches that share no frame buffer then run concurrently (the second batch's
+    // intra wavefront under the first one's loop-filter tail); a batch that reads or writes a
+    // buffer of the other slot's batch waits for it (dep_other, found at staging).
+    bool slot_streams = true;
+    hipStream_t st_o = nullptr, xst_o[MAX_GROUPS - 1] = {};
     // timing of the last run
     bool timing = true;
     std::vector<hipEvent_t> ev;
@@ -231,6 +240,17 @@ struct vp9hip_ctx {
 
 #define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
     fprintf(stderr, "vp9hip: %s failed: %s\n", #x, hipGetErrorString(e_)); return VP9HIP_EEXTERNAL; } } while (0)
+
+// The planner's stream: the slot's main stream with per-slot streams, else its own.
+static hipStream_t plan_stream(const vp9hip_ctx *c) { return c->slot_streams ? c->st : c->pst; }
+// Wait for everything either slot queued.
+static hipError_t sync_all(vp9hip_ctx *c)
+{
+    hipError_t e = hipStreamSynchronize(c->st);
+    if (e == hipSuccess && c->st_o) e = hipStreamSynchronize(c->st_o);
+    if (e == hipSuccess && c->pst) e = hipStreamSynchronize(c->pst);
+    return e;
+}
 
 extern "C" int vp9hip_open(int device, vp9hip_ctx **out)
 {
@@ -247,21 +267,33 @@ extern "C" int vp9hip_open(int device, vp9hip_ctx **out)
     if (const char *g = getenv("VP9HIP_LFROW")) c->lf_rows = atoi(g);
     if (const char *g = getenv("VP9HIP_LEVELS")) c->level_sched = atoi(g) != 0;
     if (const char *g = getenv("VP9HIP_HOST_PLAN")) c->host_plan = atoi(g) != 0;
+    if (const char *g = getenv("VP9HIP_SLOT_STREAMS")) c->slot_streams = atoi(g) != 0;
     // streams in the order their work is busiest: the frame groups' streams, then the
     // planner's, so that (with the default 4 hardware queues, GPU_MAX_HW_QUEUES) each lands
     // on a queue of its own; the LF-overlap streams only when that mode is on
-    // VP9HIP_PRIO (A/B): 1 the planner stream at the lowest priority, 2 the pixel streams at
-    // the highest (hipDeviceGetStreamPriorityRange), 0 all default
-    int prio_lo = 0, prio_hi = 0, prio = 0;
+    // Stream priorities (hipDeviceGetStreamPriorityRange): with per-slot streams every
+    // stream of the context is created at the highest priority (measured at C3: 9,320 vs
+    // 8,530 frames/s at default priority, r03f/ab5); with one planner stream the pixel
+    // streams at the highest priority starve the planner (6,520), so all stay default.
+    // VP9HIP_PRIO overrides (A/B): 0 all default, 1 the planner stream lowest, 2 the pixel
+    // streams highest, 3 every stream lowest.
+    int prio_lo = 0, prio_hi = 0, prio = c->slot_streams ? 2 : 0;
     if (const char *g = getenv("VP9HIP_PRIO")) prio = atoi(g);
     hipSetDevice(device);
     if (prio) hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-    const int pix_prio = prio == 2 ? prio_hi : 0, plan_prio = prio == 1 ? prio_lo : 0;
+    const int pix_prio = prio == 2 ? prio_hi : prio == 3 ? prio_lo : 0;
+    const int plan_prio = prio == 1 || prio == 3 ? prio_lo : 0;
     bool ok = hipStreamCreateWithPriority(&c->st, hipStreamNonBlocking, pix_prio) == hipSuccess &&
               hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) == hipSuccess;
     for (int i = 0; ok && i < c->max_groups - 1; i++)
         ok = hipStreamCreateWithPriority(&c->xst[i], hipStreamNonBlocking, pix_prio) == hipSuccess;
-    ok = ok && hipStreamCreateWithPriority(&c->pst, hipStreamNonBlocking, plan_prio) == hipSuccess;
+    if (c->slot_streams) {             // the other slot's set: with 2 groups, 4 streams = the 4 hardware queues
+        ok = ok && hipStreamCreateWithPriority(&c->st_o, hipStreamNonBlocking, pix_prio) == hipSuccess;
+        for (int i = 0; ok && i < c->max_groups - 1; i++)
+            ok = hipStreamCreateWithPriority(&c->xst_o[i], hipStreamNonBlocking, pix_prio) == hipSuccess;
+    } else {
+        ok = ok && hipStreamCreateWithPriority(&c->pst, hipStreamNonBlocking, plan_prio) == hipSuccess;
+    }
     for (int i = 0; ok && i < MAX_GROUPS - 1; i++)
         ok = hipEventCreateWithFlags(&c->join_ev[i], hipEventDisableTiming) == hipSuccess;
     for (int i = 0; ok && i < MAX_GROUPS; i++)
@@ -302,8 +334,7 @@ extern "C" void vp9hip_close(vp9hip_ctx *c)
 {
     if (!c) return;
     hipSetDevice(c->dev);
-    hipStreamSynchronize(c->st);
-    hipStreamSynchronize(c->pst);
+    sync_all(c);
     free_bufs(c);
     for (Staged *g : { &c->stg, &c->alt }) {
         if (g->arena) hipFree(g->arena);
@@ -321,8 +352,10 @@ extern "C" void vp9hip_close(vp9hip_ctx *c)
     for (auto e : c->pev) if (e) hipEventDestroy(e);
     for (auto e : c->ev) hipEventDestroy(e);
     hipStreamDestroy(c->st);
+    if (c->st_o) hipStreamDestroy(c->st_o);
     for (int i = 0; i < MAX_GROUPS - 1; i++) {
         if (c->xst[i]) hipStreamDestroy(c->xst[i]);
+        if (c->xst_o[i]) hipStreamDestroy(c->xst_o[i]);
         if (c->join_ev[i]) hipEventDestroy(c->join_ev[i]);
     }
     for (int i = 0; i < MAX_GROUPS; i++) {
@@ -420,8 +453,7 @@ extern "C" int vp9hip_configure(vp9hip_ctx *c, int width, int height, int bpp, i
     if (bpp != 8 && bpp != 10 && bpp != 12) return VP9HIP_EINVAL;
     if (ss_h < 0 || ss_h > 1 || ss_v < 0 || ss_v > 1) return VP9HIP_EINVAL;   // 4:2:0 / 4:2:2 / 4:4:0 / 4:4:4
     hipSetDevice(c->dev);
-    hipStreamSynchronize(c->st);
-    hipStreamSynchronize(c->pst);
+    sync_all(c);
     drop_slots(c);                      // both slots' records point at the buffers freed here
     free_bufs(c);
     c->w = width; c->h = height; c->bpp = bpp; c->ss_h = ss_h; c->ss_v = ss_v;
@@ -1312,7 +1344,7 @@ static int stage_dev(vp9hip_ctx *c, const DevIn &in)
     }
     // the upload goes on the planner stream: the other batch slot's pixel kernels keep the
     // main stream busy meanwhile
-    const hipStream_t us = c->pst;
+    const hipStream_t us = plan_stream(c);
     HIPCHK(hipMemcpyAsync(s.arena, img, up, hipMemcpyHostToDevice, us));
     // scan sentinels (never written by the planner)
     HIPCHK(hipMemsetAsync(s.arena + s.o_bneob + nb * 4, 0, 4, us));
@@ -1361,7 +1393,7 @@ static int plan_dev(vp9hip_ctx *c)
     // the planner runs on its own stream, after this slot's previous run (its records are
     // rewritten in place) and after whatever the main stream holds for it (the staging
     // upload); the other slot's pixel kernels run meanwhile
-    const hipStream_t ps = c->pst;
+    const hipStream_t ps = plan_stream(c);
     if (s.done_ev) HIPCHK(hipStreamWaitEvent(ps, s.done_ev, 0));
     HIPCHK(hipMemsetAsync(A + s.o_sbfirst, 0xff, (size_t) 2 * s.nslots * 4, ps));
     HIPCHK(hipMemsetAsync(A + s.o_keycnt, 0, s.zero_bytes, ps));
@@ -1738,6 +1770,24 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     }
 
     STAGE_T(0);
+    // the buffers this batch writes and reads, and whether the other slot's batch touches them
+    s.wr.assign(out_bufs, out_bufs + n);
+    s.rd.clear();
+    for (int i = 0; i < n && ref_bufs; i++)
+        if (!(pkts[i].keyframe || pkts[i].intraonly))
+            for (int r = 0; r < 3; r++) s.rd.push_back(ref_bufs[i * 3 + r]);
+    for (auto *v : { &s.wr, &s.rd }) { std::sort(v->begin(), v->end()); v->erase(std::unique(v->begin(), v->end()), v->end()); }
+    {
+        auto meet = [](const std::vector<int> &a, const std::vector<int> &b) {
+            for (size_t i = 0, j = 0; i < a.size() && j < b.size();) {
+                if (a[i] == b[j]) return true;
+                if (a[i] < b[j]) i++; else j++;
+            }
+            return false;
+        };
+        const Staged &o = c->alt;
+        s.dep_other = o.ready && (meet(s.wr, o.wr) || meet(s.wr, o.rd) || meet(s.rd, o.wr));
+    }
     s.dev = false;
     if (!c->host_plan) {
         DevIn in;
@@ -2118,11 +2168,13 @@ extern "C" int vp9hip_run_batch(vp9hip_ctx *c)
         static const bool plan_only = getenv("VP9HIP_PLAN_ONLY") && atoi(getenv("VP9HIP_PLAN_ONLY"));
         if (plan_only) return 0;          // diagnostics: the planner alone
     }
-    if (s.dev && s.stat) {
+    if (s.dev && s.stat && plan_stream(c) != c->st) {
         static const bool hw = getenv("VP9HIP_STATIC_HOSTWAIT") && atoi(getenv("VP9HIP_STATIC_HOSTWAIT"));
         if (hw) HIPCHK(hipEventSynchronize(s.plan_ev));          // A/B diagnostics only
         else HIPCHK(hipStreamWaitEvent(c->st, s.plan_ev, 0));
     }
+    // a batch touching the other slot's buffers follows that slot's last run
+    if (c->slot_streams && s.dep_other && c->alt.done_ev) HIPCHK(hipStreamWaitEvent(c->st, c->alt.done_ev, 0));
     // this slot's last work on the main stream: its next planning waits for it
     if (!s.done_ev) HIPCHK(hipEventCreateWithFlags(&s.done_ev, hipEventDisableTiming));
     if (c->timing || !c->use_graph) {
@@ -2417,8 +2469,8 @@ extern "C" int vp9hip_sync(vp9hip_ctx *c)
 {
     if (!c) return VP9HIP_EINVAL;
     hipSetDevice(c->dev);
-    HIPCHK(hipStreamSynchronize(c->st));
-    // every slot's pixel work is on the main stream: both slots' hand-off counters are final
+    HIPCHK(sync_all(c));
+    // both slots' work is complete: their hand-off counters and summaries are final
     for (Staged *g : { &c->stg, &c->alt })
         if (const int r = finish_summary(c, *g)) return r;
     if (const int r = check_lfr(c->stg)) return r;
@@ -2452,7 +2504,7 @@ extern "C" int vp9hip_download_frame(vp9hip_ctx *c, int buf, uint8_t *const plan
 {
     if (!c || buf < 0 || buf >= (int) c->bufs.size() || !planes) return VP9HIP_EINVAL;
     hipSetDevice(c->dev);
-    HIPCHK(hipStreamSynchronize(c->st));
+    HIPCHK(sync_all(c));                 // either slot may have written the buffer
     for (int p = 0; p < 3; p++) {
         const int bw = c->buf_wh[buf].first, bh = c->buf_wh[buf].second;
         int pw = p ? (bw + c->ss_h) >> c->ss_h : bw, ph = p ? (bh + c->ss_v) >> c->ss_v : bh;
@@ -2468,6 +2520,7 @@ extern "C" int vp9hip_upload_frame(vp9hip_ctx *c, int buf, const uint8_t *const 
 {
     if (!c || buf < 0 || buf >= (int) c->bufs.size() || !planes) return VP9HIP_EINVAL;
     hipSetDevice(c->dev);
+    HIPCHK(sync_all(c));
     for (int p = 0; p < 3; p++) {
         const int bw = c->buf_wh[buf].first, bh = c->buf_wh[buf].second;
         int pw = p ? (bw + c->ss_h) >> c->ss_h : bw, ph = p ? (bh + c->ss_v) >> c->ss_v : bh;
@@ -2502,8 +2555,7 @@ extern "C" int vp9hip_flush(vp9hip_ctx *c)
 {
     if (!c) return VP9HIP_EINVAL;
     hipSetDevice(c->dev);
-    HIPCHK(hipStreamSynchronize(c->st));
-    HIPCHK(hipStreamSynchronize(c->pst));
+    HIPCHK(sync_all(c));
     drop_slots(c);
     return 0;
 }
@@ -2512,6 +2564,7 @@ extern "C" int vp9hip_fill_buffers(vp9hip_ctx *c, int buf0, int count, int value
 {
     if (!c || buf0 < 0 || count < 0 || buf0 + count > (int) c->bufs.size()) return VP9HIP_EINVAL;
     hipSetDevice(c->dev);
+    HIPCHK(sync_all(c));                 // neither slot's work may still read the buffers
     for (int i = buf0; i < buf0 + count; i++) HIPCHK(hipMemsetAsync(c->bufs[i], value & 255, c->buf_bytes, c->st));
     return 0;
 }
@@ -2534,7 +2587,7 @@ extern "C" int vp9hip_alg_bytes(vp9hip_ctx *c, double *bytes, int cap)
     if (!c) return VP9HIP_EINVAL;
     if (c->stg.summary_pending) {            // a static plan's totals: after its run
         hipSetDevice(c->dev);
-        HIPCHK(hipStreamSynchronize(c->st));
+        HIPCHK(sync_all(c));
         if (const int r = finish_summary(c, c->stg)) return r;
     }
     int n = 0;
@@ -2579,6 +2632,10 @@ extern "C" int vp9hip_set_batch_slot(vp9hip_ctx *c, int slot)
     if (!c || slot < 0 || slot > 1) return VP9HIP_EINVAL;
     if (slot != c->slot) {
         std::swap(c->stg, c->alt);
+        if (c->slot_streams) {
+            std::swap(c->st, c->st_o);
+            for (int i = 0; i < MAX_GROUPS - 1; i++) std::swap(c->xst[i], c->xst_o[i]);
+        }
         c->slot = slot;
     }
     return 0;

@@ -169,10 +169,12 @@ int  vp9hip_run_phase(vp9hip_ctx *ctx, int phase, int part);
  */
 int64_t vp9hip_stripe(vp9hip_ctx *ctx, int frame, int tile_lo, int tile_hi, void *dev, int to_frame);
 
-/* Select batch slot 0 or 1 (default 0): stage_batch*, run_batch, sync, batch_phases,
- * run_phase and stripe act on the current slot. Each slot holds its own staged batch
- * (arena, plan, launch graph); the frame buffers are the context's. Alternating two staged
- * batches lets one batch's device planning run while the other's pixel kernels do. */
+/* Select batch slot 0 or 1 (default 0): stage_batch*, run_batch, batch_phases, run_phase
+ * and stripe act on the current slot. Each slot holds its own staged batch (arena, plan,
+ * launch graph) and runs on HIP streams of its own; the frame buffers are the context's.
+ * Two staged batches that share no frame buffer run concurrently (one batch's device
+ * planning and intra wavefront under the other's loop filter); a batch that reads or
+ * writes a buffer of the other slot's batch follows that slot's last run. */
 int  vp9hip_set_batch_slot(vp9hip_ctx *ctx, int slot);
 /* Wait for the last run of batch slot `slot` only (the other slot's work may continue)
  * and check it as vp9hip_sync does (VP9HIP_EBUG: a loop-filter hand-off timed out). */
@@ -195,9 +197,10 @@ int  vp9hip_download_frame(vp9hip_ctx *ctx, int buf, uint8_t *const planes[3],
  * Zero-copy export of device buffer `buf` (replaces the D2H of vp9hip_download_frame for
  * consumers on the GPU; the hwcontext frame export of SURVEY 8f rank 2,
  * hwaccel_internal.h:146, libavutil/hwcontext.h:26-44): device pointers and byte
- * pitches of the three planes, the visible size, and the context's hipStream_t, which
- * orders every write of the buffer. Work enqueued on that stream, or after
- * vp9hip_sync, sees the finished frame. Pointers stay valid until vp9hip_configure /
+ * pitches of the three planes, the visible size, and the current batch slot's main
+ * hipStream_t. Each batch slot runs on streams of its own, so a consumer orders its reads
+ * after the slot that wrote the frame (vp9hip_slot_stream_wait), or reads after
+ * vp9hip_sync / vp9hip_sync_slot. Pointers stay valid until vp9hip_configure /
  * vp9hip_close.
  */
 int  vp9hip_frame_device(vp9hip_ctx *ctx, int buf, void *planes[3], ptrdiff_t linesize[3],

@@ -56,8 +56,9 @@ int vp9hip_hwaccel_frame_params(int width, int height, int bpp, int ss_h, int ss
                                 vp9hip_frames_params *out);
 
 /* A device frame (the AVFrame of a HIP frames context): data[] are device pointers with
- * byte pitches, valid until vp9hip_hwframe_unref; consumers order their reads after
- * `stream` (the hipStream_t the frame was produced on). */
+ * byte pitches, valid until vp9hip_hwframe_unref; consumers order their reads after the
+ * frame's batch with vp9hip_hwframe_ready (GPU) or vp9hip_hwframe_sync (host). `stream` is
+ * the context's stream at hand-out, informational. */
 typedef struct vp9hip_hwframe {
     void     *data[3];
     ptrdiff_t linesize[3];

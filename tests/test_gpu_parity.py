@@ -141,6 +141,54 @@ def test_static_plan_keyframe_batch(v9, orc, gpu, monkeypatch, static):
             _cmp(v9, gpu.download(i), ref, w, h, "static=%d %d-bit batch frame %d" % (static, bpp, i))
 
 
+@pytest.mark.parametrize("slot_streams", [1, 0])
+def test_two_slots_cross_batch_dependency(v9, orc, monkeypatch, slot_streams):
+    """The two batch slots run on streams of their own (VP9HIP_SLOT_STREAMS=1): a batch that
+    references the other slot's frames waits for that slot's run on the device (dep_other),
+    one that shares no buffer with it runs concurrently. Slot 1's P frames continue slot 0's
+    GOP, run back to back without a host wait; then slot 0 again, overwriting buffers slot 1
+    read (write-after-read across slots)."""
+    monkeypatch.setenv("VP9HIP_SLOT_STREAMS", str(slot_streams))
+    w, h = 352, 288
+    key = v9.SynthFrame(v9.synth_params(w, h, 8, seed=900))
+    ps = [v9.SynthFrame(v9.synth_params(w, h, 8, seed=901 + i, inter=1, compound=i % 2)) for i in range(5)]
+    key2 = v9.SynthFrame(v9.synth_params(w, h, 8, seed=910))
+    dev = v9.Device(0)
+    try:
+        dev.configure(w, h, 8, nbufs=8)
+        dev.set_slot(0)
+        dev.stage_batch([key, ps[0], ps[1]], [0, 1, 2], [None, (0, 0, 0), (1, 1, 0)])
+        dev.set_slot(1)
+        dev.stage_batch([ps[2], ps[3], key2], [3, 4, 5], [(2, 2, 0), (3, 3, 0), None])
+        dev.set_slot(0)
+        dev.run_batch()
+        dev.set_slot(1)
+        dev.run_batch()
+        dev.sync()
+        ref = {}
+        seq = [(key, 0, None), (ps[0], 1, (0, 0, 0)), (ps[1], 2, (1, 1, 0)), (ps[2], 3, (2, 2, 0)),
+               (ps[3], 4, (3, 3, 0)), (key2, 5, None)]
+        for f, b, r in seq:
+            out = v9.alloc_planes(w, h, 8)
+            orc.decode_frame(f.pkt, out, None if r is None else [ref[r[0]], ref[r[1]], ref[r[2]]])
+            ref[b] = out
+            _cmp(v9, dev.download(b), out, w, h, "slot streams %d buffer %d" % (slot_streams, b))
+        # slot 0 again, into buffers 3 / 4 that slot 1 read and wrote, from buffer 5 (slot 1's)
+        dev.set_slot(0)
+        dev.stage_batch([ps[4], key], [3, 4], [(5, 5, 5), None])
+        dev.set_slot(1)
+        dev.run_batch()          # slot 1's batch again (reads 2, 3; writes 3, 4, 5) ...
+        dev.set_slot(0)
+        dev.run_batch()          # ... then slot 0's, which must wait for it
+        dev.sync()
+        out = v9.alloc_planes(w, h, 8)
+        orc.decode_frame(ps[4].pkt, out, [ref[5], ref[5], ref[5]])
+        _cmp(v9, dev.download(3), out, w, h, "slot streams %d rewrite" % slot_streams)
+        _cmp(v9, dev.download(4), ref[0], w, h, "slot streams %d key rewrite" % slot_streams)
+    finally:
+        dev.close()
+
+
 def test_static_plan_rejects_inconsistent_packets(v9, orc, gpu):
     """A packet the device planner rejects (an intra mode > 9) in a static-plan batch: the
     planner neutralises the batch on the device (k_pguard) and the next wait reports
