@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """GPU timeline of the last N graph-replayed steps in a rocprofv3 kernel trace: busy
 fraction (union of kernel intervals), mean kernel concurrency, per-kernel busy time.
-Usage: timeline.py gpurun_out/trace_TAG [steps]"""
+Usage: timeline.py gpurun_out/trace_TAG [steps]
+With steps = 0: the kernels after bench.py's poison fill (the last fill-buffer kernel),
+i.e. exactly the timed steps."""
 import csv, glob, os, sys
 from collections import defaultdict
 
@@ -18,7 +20,13 @@ for e in ev[1:]:
     else:
         cur.append(e)
 groups.append(cur)
-sel = [x for g in groups[-steps:] for x in g]
+if steps == 0:
+    fills = [x[0] for x in ev if "fill" in x[2].lower()]
+    sel = [x for x in ev if x[0] > fills[-1] and "fill" not in x[2].lower()]
+    groups = [sel]
+    steps = 1
+else:
+    sel = [x for g in groups[-steps:] for x in g]
 t0, t1 = min(x[0] for x in sel), max(x[1] for x in sel)
 # union + concurrency
 pts = sorted([(s, 1) for s, e, n in sel] + [(e, -1) for s, e, n in sel])
@@ -33,6 +41,6 @@ for s, e, n in sel:
     k = n.split("<")[0].split("(")[0].replace("void ", "")
     per[k] += e - s
 span = t1 - t0
-print("steps %d span %.3f ms busy %.1f%% mean concurrency %.2f" % (len(groups[-steps:]), span / 1e6 / len(groups[-steps:]) if False else span / 1e6, 100.0 * busy / span, conc_area / max(busy, 1)))
+print("groups %d span %.3f ms busy %.1f%% mean concurrency %.2f" % (len(groups[-steps:]), span / 1e6, 100.0 * busy / span, conc_area / max(busy, 1)))
 for k, v in sorted(per.items(), key=lambda x: -x[1]):
-    print("  %-10s %.3f ms per step (sum of launch durations)" % (k, v / 1e6 / steps))
+    print("  %-10s %.3f ms (sum of launch durations over the span / %d)" % (k, v / 1e6 / steps, steps))
