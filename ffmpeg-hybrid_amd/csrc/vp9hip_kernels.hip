@@ -1868,9 +1868,33 @@ DEV void lfrd_top(Chunk16::T (&v)[NUT], const LfrPlanes &P, int sbx, int sby, in
     }
 }
 
+// Frame pipelining inside one k_lfrd launch (chain positions of inter streams): tickets
+// ntasks .. ntasks + nmc - 1 are the next position's MC units (one unit per workgroup, in
+// the planner's raster SB order). A unit reads reference rows that this launch may still be
+// filtering; it waits for the row tasks that finish those rows (the reference's
+// ff_progress_frame_await, vp9recon.c:392-395, reported per SB row at vp9.c:1434). Tickets
+// are taken in workgroup start order and every row task's ticket is below every MC
+// ticket, so a unit waits only on row tasks held by running workgroups. Defined with k_mc.
+template <typename PIX, class G>
+DEV void lfmc_ticket(const McUnit &u, const FrameDesc *__restrict__ frames, const uint32_t *__restrict__ mw,
+                     const uint32_t *rdone, uint32_t *ctr, uint32_t spin, int nth);
+// the last workgroup of a k_lfrd launch (row tasks and MC tickets) zeroes its counters,
+// row progress and row-done words for the next launch (graph replay)
+DEV void lfrd_retire(uint32_t *ctr, int ntasks, int nmc, int lane, int nth, uint32_t *s_last)
+{
+    __syncthreads();
+    if (lane == 0) *s_last = atomicAdd(&ctr[1], 1u) == (uint32_t) (ntasks + nmc) - 1;
+    __syncthreads();
+    if (*s_last) {
+        for (int i = lane; i < 2 * ntasks; i += nth) ctr[4 + i] = 0;
+        if (lane == 0) { ctr[0] = 0; ctr[1] = 0; }
+    }
+}
+
 template <typename PIX, class G>
 __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfrd(const uint32_t *__restrict__ tasks, const LFRec *__restrict__ recs,
-                                                      const FrameDesc *__restrict__ frames, uint32_t *ctr, int ntasks)
+                                                      const FrameDesc *__restrict__ frames, uint32_t *ctr, int ntasks,
+                                                      const McUnit *__restrict__ mcu, int nmc, const uint32_t *__restrict__ mw)
 {
     constexpr int NT = LfNT<G>::NT;
     typedef LfP<PIX, G> L;
@@ -1887,10 +1911,18 @@ __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfrd(const uint32_t *__res
     const uint64_t tk0 = tp;
     if (lane == 0) s_task = atomicAdd(&ctr[0], 1u);
     __syncthreads();
+    // spin bound of a wait (ctr[3], 0 = 2^22 polls; a small bound is a test hook)
+    const uint32_t spin = ctr[3] ? ctr[3] : (1u << 22);
+    uint32_t *const rdone = progress + ntasks;      // per row task: 1 once its rows are released
+    if (s_task >= (uint32_t) ntasks) {              // an MC unit of the next chain position
+        __builtin_amdgcn_s_setprio(0);
+        lfmc_ticket<PIX, G>(mcu[s_task - ntasks], frames, mw, rdone, ctr, spin, NT + 64);
+        lfrd_retire(ctr, ntasks, nmc, lane, NT + 64, &s_last);
+        return;
+    }
     const uint32_t *T = tasks + tasks[s_task];
     const uint32_t dep = T[0], ncols = T[1], c0 = T[2];
     uint32_t seen = T[3];
-    const uint32_t spin = ctr[3] ? ctr[3] : (1u << 22);
     const LFRec &rec0 = recs[T[4]];
     const FrameDesc &fd = frames[rec0.frame];
     const int bd = fd.bd, sby = rec0.sby;
@@ -2043,19 +2075,23 @@ __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfrd(const uint32_t *__res
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (ml == 0) __hip_atomic_store((gu32 *) &progress[s_task], ncols, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (nmc) {
+            // MC tickets of this launch read the row: the store wave (the only storing wave)
+            // releases its plain stores at agent scope, then sets the row-done word
+            // (MI355X_MICROARCH.md, inter-workgroup visibility, Valid forms: producer); after
+            // the hand-off word above, so the row below never waits for the write-back
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (ml == 0) __hip_atomic_store((gu32 *) &rdone[s_task], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
     }
     if (LFR_PROF && lane == 0) {
         pacc[7] = clock64() - tk0;
         for (int i = 0; i < 14; i++) atomicAdd(&lfr_prof[i], pacc[i]);
         atomicAdd(&lfr_prof[14], 1ull);
     }
-    __syncthreads();
-    if (lane == 0) s_last = atomicAdd(&ctr[1], 1u) == (uint32_t) ntasks - 1;
-    __syncthreads();
-    if (s_last) {
-        for (int i = lane; i < ntasks; i += NT) progress[i] = 0;
-        if (lane == 0) { ctr[0] = 0; ctr[1] = 0; }
-    }
+    lfrd_retire(ctr, ntasks, nmc, lane, NT + 64, &s_last);
 }
 
 // Residual arithmetic types per pixel type: 8-bit int16 coefficients / 32-bit math,
@@ -2220,6 +2256,85 @@ DEV void mc_unit_rows(const McUnit &u, const FrameDesc &fd, PIX *dst, int pitch,
     }
 }
 
+// one output pixel per thread (any reference scaling), compound averaged
+template <typename PIX>
+DEV void mc_unit_pixels(const McUnit &u, const FrameDesc &fd, PIX *dst, int pitch, int c, int bd, int nth)
+{
+    const int W = u.w, npx = W * u.h, p = u.plane;
+    for (int i = threadIdx.x; i < npx; i += nth) {
+        int yy = i / W, xx = i - yy * W;
+        int out = 0;
+        for (int k = 0; k < u.nref; k++) {
+            const int rf = u.ref[k];
+            const McRef m = u.r[k];
+            const PIX *r = (const PIX *) fd.ref[rf][p];
+            const int px = m.mx + xx * m.dx, py = m.my + yy * m.dy;
+            const int v = mc_sample<PIX>(r, pitch, fd.refw[rf][c], fd.refh[rf][c], m.ix + (px >> 4), m.iy + (py >> 4),
+                                         px & 15, py & 15, u.filter, bd);
+            out = k ? (out + v + 1) >> 1 : v;
+        }
+        dst[(size_t) (u.y + yy) * pitch + u.x + xx] = (PIX) out;
+    }
+}
+
+// An MC ticket of k_lfrd (see there). Wait table mw: {F, then per frame the launch filters:
+// batch frame index, SB rows, row task of each SB row (~0u: filtered by an earlier launch)}.
+// Pixel row y of a reference plane is final once the row task of SB row y / SBH is done and,
+// for its last 8 rows (rewritten by the next SB row's top-edge filtering), the next one's.
+// A unit waits for rows ymin - 1 .. ymax + 1 of what its taps read (a 128-byte line may
+// straddle two pixel rows when the pitch is not a multiple of 128 bytes); scaled
+// references wait for the whole frame. Lane 0 polls (relaxed agent loads), then one agent
+// acquire and a barrier before any load (Valid forms: consumer).
+template <typename PIX, class G>
+DEV void lfmc_ticket(const McUnit &u, const FrameDesc *__restrict__ frames, const uint32_t *__restrict__ mw,
+                     const uint32_t *rdone, uint32_t *ctr, uint32_t spin, int nth)
+{
+    const FrameDesc &fd = frames[u.frame];
+    const int p = u.plane, c = p ? 1 : 0, bd = fd.bd;
+    if (threadIdx.x == 0) {
+        bool waited = false;
+        const uint32_t nf = mw[0];
+        for (int k = 0; k < u.nref; k++) {
+            const int rf = u.ref[k];
+            const McRef m = u.r[k];
+            const int sbh = p ? G::CH : 64, refh = fd.refh[rf][c];
+            const bool scaled = m.dx != 16 || m.dy != 16;
+            int y0 = scaled ? 0 : m.iy - 4, y1 = scaled ? refh - 1 : m.iy + (int) u.h + 5;
+            y0 = y0 < 0 ? 0 : y0 >= refh ? refh - 1 : y0;
+            y1 = y1 < 0 ? 0 : y1 >= refh ? refh - 1 : y1;
+            for (uint32_t f = 0, o = 1; f < nf; f++, o += 2 + mw[o + 1]) {
+                if (frames[mw[o]].plane[p] != fd.ref[rf][p]) continue;
+                const int nrows = (int) mw[o + 1];
+                int r0 = y0 / sbh, r1 = y1 / sbh;
+                if (y1 % sbh >= sbh - 8) r1++;
+                if (r1 > nrows - 1) r1 = nrows - 1;
+                for (int r = r0; r <= r1; r++) {
+                    const uint32_t t = mw[o + 2 + r];
+                    if (t == ~0u) continue;
+                    waited = true;
+                    for (uint32_t n = 0; !__hip_atomic_load((const gu32 *) &rdone[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); n++) {
+                        if (n > spin) { atomicAdd(&ctr[2], 1u); break; }
+                        __builtin_amdgcn_s_sleep(2);
+                    }
+                }
+            }
+        }
+        if (waited) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    PIX *dst = (PIX *) fd.plane[p];
+    const int pitch = fd.pitch[c];
+    bool scaled = false;
+    for (int k = 0; k < u.nref; k++) scaled |= u.r[k].dx != 16 || u.r[k].dy != 16;
+    if (sizeof(PIX) != 1 && !scaled && !(u.h & 3)) {
+        if (!(u.h & 7)) mc_unit_rows<PIX, 8>(u, fd, dst, pitch, c, bd, nth);
+        else mc_unit_rows<PIX, 4>(u, fd, dst, pitch, c, bd, nth);
+        return;
+    }
+    mc_unit_pixels<PIX>(u, fd, dst, pitch, c, bd, nth);
+}
+
 // One MC unit (<= 64 x 64 pixels of one plane) per workgroup. Unscaled references: the
 // (h + 7) x (w + 7) reference window (edge-clamped, emulated_edge_mc) is staged in LDS once,
 // then the separable filter runs as a horizontal pass into a pixel-clipped LDS tmp and a
@@ -2264,20 +2379,7 @@ __global__ __launch_bounds__(NTH) void k_mc(const McUnit *__restrict__ units, in
         return;
     }
     if (sizeof(PIX) != 1 || scaled || npx < MC_LDS_MIN || (1 << lw) != W) {
-        for (int i = threadIdx.x; i < npx; i += NTH) {
-            int yy = i / W, xx = i - yy * W;
-            int out = 0;
-            for (int k = 0; k < u.nref; k++) {
-                const int rf = u.ref[k];
-                const McRef m = u.r[k];
-                const PIX *r = (const PIX *) fd.ref[rf][p];
-                const int px = m.mx + xx * m.dx, py = m.my + yy * m.dy;
-                const int v = mc_sample<PIX>(r, pitch, fd.refw[rf][c], fd.refh[rf][c], m.ix + (px >> 4), m.iy + (py >> 4),
-                                             px & 15, py & 15, u.filter, bd);
-                out = k ? (out + v + 1) >> 1 : v;
-            }
-            dst[(size_t) (u.y + yy) * pitch + u.x + xx] = (PIX) out;
-        }
+        mc_unit_pixels<PIX>(u, fd, dst, pitch, c, bd, NTH);
         return;
     }
     const int WW = W + 7, WH = H + 7;
@@ -2395,23 +2497,29 @@ static void launch_lf_g(hipStream_t st, int nsb, const uint32_t *list, const LFR
     hipLaunchKernelGGL((k_lf<PIX, G>), dim3(nsb), dim3(LfNT<G>::NT), 0, st, list, recs, frames, dbg);
 }
 template <typename PIX, class G>
-static void launch_lfr_g(hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs, const FrameDesc *frames, uint32_t *ctr)
+static void launch_lfr_g(hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs, const FrameDesc *frames, uint32_t *ctr,
+                         const McUnit *mcu, int nmc, const uint32_t *mw)
 {
-    // VP9HIP_LFR_DB=0: the single-tile k_lfr (A/B switch)
+    // VP9HIP_LFR_DB=0: the single-tile k_lfr (A/B switch), MC units after it
     const char *e = getenv("VP9HIP_LFR_DB");          // read per launch (tests switch it)
     const bool db = !e || atoi(e);
-    if (db) hipLaunchKernelGGL((k_lfrd<PIX, G>), dim3(ntasks), dim3(LfNT<G>::NT + 64), 0, st, tasks, recs, frames, ctr, ntasks);
-    else    hipLaunchKernelGGL((k_lfr<PIX, G, false>), dim3(ntasks), dim3(LfNT<G>::NT + 64), 0, st, tasks, recs, frames, ctr, ntasks);
+    if (db) {
+        hipLaunchKernelGGL((k_lfrd<PIX, G>), dim3(ntasks + nmc), dim3(LfNT<G>::NT + 64), 0, st, tasks, recs, frames, ctr, ntasks,
+                           mcu, nmc, mw);
+        return;
+    }
+    hipLaunchKernelGGL((k_lfr<PIX, G, false>), dim3(ntasks), dim3(LfNT<G>::NT + 64), 0, st, tasks, recs, frames, ctr, ntasks);
+    if (nmc) hipLaunchKernelGGL((k_mc<PIX, 256>), dim3(nmc), dim3(256), 0, st, mcu, nmc, frames);
 }
 template <typename PIX>
 static void launch_lfr_p(int ss, hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs, const FrameDesc *frames,
-                         uint32_t *ctr)
+                         uint32_t *ctr, const McUnit *mcu, int nmc, const uint32_t *mw)
 {
     switch (ss) {
-    case 3: launch_lfr_g<PIX, Geo<1, 1>>(st, ntasks, tasks, recs, frames, ctr); break;
-    case 1: launch_lfr_g<PIX, Geo<1, 0>>(st, ntasks, tasks, recs, frames, ctr); break;
-    case 2: launch_lfr_g<PIX, Geo<0, 1>>(st, ntasks, tasks, recs, frames, ctr); break;
-    default: launch_lfr_g<PIX, Geo<0, 0>>(st, ntasks, tasks, recs, frames, ctr); break;
+    case 3: launch_lfr_g<PIX, Geo<1, 1>>(st, ntasks, tasks, recs, frames, ctr, mcu, nmc, mw); break;
+    case 1: launch_lfr_g<PIX, Geo<1, 0>>(st, ntasks, tasks, recs, frames, ctr, mcu, nmc, mw); break;
+    case 2: launch_lfr_g<PIX, Geo<0, 1>>(st, ntasks, tasks, recs, frames, ctr, mcu, nmc, mw); break;
+    default: launch_lfr_g<PIX, Geo<0, 0>>(st, ntasks, tasks, recs, frames, ctr, mcu, nmc, mw); break;
     }
 }
 template <typename PIX>
@@ -2535,11 +2643,12 @@ int vp9hip_launch_lf(int fmt, hipStream_t st, int nsb, const uint32_t *list, con
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int vp9hip_launch_lfr(int fmt, hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs,
-                      const FrameDesc *frames, uint32_t *ctr)
+                      const FrameDesc *frames, uint32_t *ctr, const McUnit *mcu, int nmc, const uint32_t *mw)
 {
-    if (ntasks <= 0) return 0;
-    if (fmt & 1) launch_lfr_p<uint16_t>(fmt >> 1, st, ntasks, tasks, recs, frames, ctr);
-    else         launch_lfr_p<uint8_t>(fmt >> 1, st, ntasks, tasks, recs, frames, ctr);
+    if (ntasks <= 0) return nmc > 0 ? -1 : 0;
+    if (nmc < 0 || (nmc && (!mcu || !mw))) return -1;
+    if (fmt & 1) launch_lfr_p<uint16_t>(fmt >> 1, st, ntasks, tasks, recs, frames, ctr, mcu, nmc, mw);
+    else         launch_lfr_p<uint8_t>(fmt >> 1, st, ntasks, tasks, recs, frames, ctr, mcu, nmc, mw);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int vp9hip_launch_plf(int fmt, hipStream_t st, const PlfLaunch *pl, const uint32_t *plist, const uint32_t *llist,

@@ -56,7 +56,7 @@ int vp9hip_plan_enqueue(hipStream_t st, const PlanDev *D, int ss, int nframes, i
                         uint32_t nslots, uint32_t ncnt, int nk, const uint32_t *gidx, int ng, uint32_t *summary,
                         void *scan_tmp, size_t scan_bytes, int any_levels, int flags, int guard);
 int vp9hip_launch_lfr(int fmt, hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs,
-                      const FrameDesc *frames, uint32_t *ctr);
+                      const FrameDesc *frames, uint32_t *ctr, const McUnit *mcu, int nmc, const uint32_t *mw);
 int vp9hip_launch_plf(int fmt, hipStream_t st, const PlfLaunch *pl, const uint32_t *plist, const uint32_t *llist,
                       const WGRec *wgs, const SBRec *sbs, const PJob *jobs, const uint32_t *passes, const LFRec *recs,
                       const RJob *rjobs, const FrameDesc *frames, const void *coefs, int16_t *resid, const uint32_t *ptab,
@@ -73,7 +73,9 @@ const char *const kname[K_N] = { "k_mc", "k_resid", "k_pred", "k_lf", "k_plf", "
 // step: wavefront diagonal of a K_PRED (x_in_tile + y) or K_LF (x + 2y) launch; K_PLF
 // (intra diagonal `step` + LF diagonal step - PLF_LAG in one launch): off / n the intra
 // workgroups, off2 / n2 the LF SBs; K_LFR (row-pipelined loop filter of a phase): off / n
-// its task table, arg its counter block (uint32 index into the arena's counter words)
+// its task table, arg its counter block (uint32 index into the arena's counter words),
+// off2 / n2 the next chain position's MC units run as extra tickets of the launch (0: none)
+// and roff[0] their wait table (host lists)
 struct Launch { int kind; uint32_t off; uint32_t n; int arg; int grp; int ph; int part; int step;
                 uint32_t off2 = 0, n2 = 0;
                 uint32_t roff[5] = { 0, 0, 0, 0, 0 }, rn[5] = { 0, 0, 0, 0, 0 };   // K_PLF residual jobs by tx code
@@ -151,6 +153,7 @@ struct Staged {
         std::vector<std::pair<uint32_t, uint32_t>> lf;        // per LF diagonal: host list (offset, count)
         std::vector<double> pred_bytes, lf_bytes;             // per intra diagonal (intra frames) / LF diagonal
         uint32_t lfr_off = 0, lfr_n = 0;                      // k_lfr task table in the host lists
+        uint32_t lfw_off = 0;                                 // its wait table (k_lfrd MC tickets)
         int lfr_ctr = 0;
         double lfr_bytes = 0;
         int g_res = 0, g_mc = 0;                              // summary gather slots
@@ -1184,9 +1187,18 @@ static int stage_dev(vp9hip_ctx *c, const DevIn &in)
                 P.lfr_n = nt;
                 hl.insert(hl.end(), offs.begin(), offs.end());
                 hl.insert(hl.end(), recs.begin(), recs.end());
+                // wait table of the next position's MC tickets (lfmc_ticket): per filtered
+                // frame its index, SB rows and the row task of each SB row
+                P.lfw_off = (uint32_t) hl.size();
+                hl.push_back((uint32_t) lff.size());
+                for (size_t k = 0; k < lff.size(); k++) {
+                    hl.push_back((uint32_t) lff[k]);
+                    hl.push_back((uint32_t) tid[k].size());
+                    hl.insert(hl.end(), tid[k].begin(), tid[k].end());
+                }
                 P.lfr_ctr = (int) s.n_ctr;
                 s.lfr_ctr.push_back(s.n_ctr);
-                s.n_ctr += 4 + nt;
+                s.n_ctr += 4 + 2 * nt;     // ticket, done, timeouts, spin; progress and row-done per task
             } else {
                 P.lfr = false;
             }
@@ -1519,6 +1531,15 @@ static int plan_dev(vp9hip_ctx *c)
     }
     const uint32_t H = s.host_lists;
     const int nph = (int) s.dph.size();
+    // frame pipelining (VP9HIP_LFMC=1; off by default): a phase's k_lfr launch also runs the MC
+    // units of the group's next phase as extra tickets, each waiting for the reference rows it
+    // reads. Bit-exact, but measured 6.7x slower at C5 (113 vs 760 fps) and 4.7x at C2
+    // (profiles/r03h): a k_lfr row finishes only in the last ~28 % of the launch (each row is
+    // a 120-SB chain), so the MC workgroups sit on their CU slots polling for most of it and
+    // starve the other chains' and the other slot's kernels, which fill the chip otherwise
+    const char *lfe = getenv("VP9HIP_LFMC");                 // read per build (tests switch it)
+    const bool lfmc = lfe && atoi(lfe);
+    std::vector<char> mc_in_lfr(nph, 0);
     for (int g = 0; g < s.ngroups; g++)
         for (int ph = 0; ph < nph; ph++) {
             const Staged::DevPhase &P = s.dph[ph];
@@ -1528,7 +1549,7 @@ static int plan_dev(vp9hip_ctx *c)
                 s.launches.push_back(L);
             };
             const uint32_t m0 = gv[P.g_mc], m1 = gv[P.g_mc + 1];
-            if (m1 > m0) push(K_MC, m0, m1 - m0, 0, PART_RECON, 0);
+            if (m1 > m0 && !mc_in_lfr[ph]) push(K_MC, m0, m1 - m0, 0, PART_RECON, 0);
             auto rr = [&](int d, int tc) {
                 const uint32_t a = gv[P.g_res + (d * 5 + tc) * 2], b = gv[P.g_res + (d * 5 + tc) * 2 + 1];
                 return std::make_pair(a, b - a);
@@ -1558,6 +1579,19 @@ static int plan_dev(vp9hip_ctx *c)
                 push(K_LFR, P.lfr_off, P.lfr_n, (int) P.lfr_ctr, PART_LF, 0);
                 s.alg_bytes[K_LF] -= P.lfr_bytes;
                 s.alg_bytes[K_LFR] += P.lfr_bytes;
+                int nx = ph + 1;                                  // the group's next phase
+                while (nx < nph && (s.dph[nx].frames.empty() || s.dph[nx].group != g)) nx++;
+                if (!lfmc || nx >= nph) return;
+                const Staged::DevPhase &Q = s.dph[nx];
+                const uint32_t q0 = gv[Q.g_mc], q1 = gv[Q.g_mc + 1];
+                if (q1 <= q0) return;
+                Launch &L = s.launches.back();
+                L.off2 = q0; L.n2 = q1 - q0; L.roff[0] = P.lfw_off;
+                mc_in_lfr[nx] = 1;
+                for (int i : Q.frames) {
+                    s.alg_bytes[K_MC] -= fbytes(i, 1);
+                    s.alg_bytes[K_LFR] += fbytes(i, 1);
+                }
             };
             if (!s.fuse || P.levels) {
                 for (int d = 0; d < P.nkey; d++)
@@ -1948,7 +1982,7 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
                 s.lists.insert(s.lists.end(), offs.begin(), offs.end());
                 s.lists.insert(s.lists.end(), recs.begin(), recs.end());
                 s.lfr_ctr.push_back(s.n_ctr);
-                s.n_ctr += 4 + nt;
+                s.n_ctr += 4 + 2 * nt;     // ticket, done, timeouts, spin; progress and row-done per task
                 s.launches.push_back(L);
                 for (int i : phase_frames[ph])
                     for (size_t k = 0; k < plans[i].s.lfs.size(); k++) {
@@ -2228,7 +2262,8 @@ static int launch_one(vp9hip_ctx *c, const Launch &L, hipStream_t st)
                                   (const uint32_t *) (s.arena + s.o_passes), fr, s.resid, c->ptab, c->dbg);
     case K_LFR:
         return vp9hip_launch_lfr(c->hb | c->ss_h << 1 | c->ss_v << 2, st, (int) L.n, lists + L.off,
-                                 (const LFRec *) (s.arena + s.o_lfs), fr, (uint32_t *) (s.arena + s.o_ctr) + L.arg);
+                                 (const LFRec *) (s.arena + s.o_lfs), fr, (uint32_t *) (s.arena + s.o_ctr) + L.arg,
+                                 (const McUnit *) (s.arena + s.o_mcs) + L.off2, (int) L.n2, L.n2 ? lists + L.roff[0] : nullptr);
     case K_LF:
         return vp9hip_launch_lf(c->hb | c->ss_h << 1 | c->ss_v << 2, st, (int) L.n, lists + L.off, (const LFRec *) (s.arena + s.o_lfs), fr, c->dbg >> 16);
     case K_PLF: {

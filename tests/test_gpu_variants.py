@@ -1,6 +1,8 @@
 """The A/B switches of the inter-frame kernels stay bit-exact: the single-tile row LF
-(VP9HIP_LFR_DB=0 instead of k_lfrd), 256-thread high-bit-depth MC (VP9HIP_MC64=0) and one
-residual launch per transform size (VP9HIP_RESID_MULTI=0). Each is switched off (read
+(VP9HIP_LFR_DB=0 instead of k_lfrd), 256-thread high-bit-depth MC (VP9HIP_MC64=0), one
+residual launch per transform size (VP9HIP_RESID_MULTI=0), and frame pipelining
+(VP9HIP_LFMC=1: the next chain position's MC units as waiting tickets of k_lfrd, alone and
+with the single-tile k_lfr, where they run as a k_mc launch after it). Each is switched (read
 per launch / per staging) on a key + P chain of the C2 (1080p 8-bit) or C5 (8K 10-bit)
 shape, decoded through the bench's batch path and compared with the CPU oracle."""
 import os
@@ -15,31 +17,36 @@ import bench  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 CASES = [
-    ("VP9HIP_LFR_DB", "C2", 4),
-    ("VP9HIP_LFR_DB", "C5", 2),
-    ("VP9HIP_MC64", "C5", 2),
-    ("VP9HIP_RESID_MULTI", "C2", 4),
-    ("VP9HIP_RESID_MULTI", "C5", 2),
+    ({"VP9HIP_LFR_DB": "0"}, "C2", 4),
+    ({"VP9HIP_LFR_DB": "0"}, "C5", 2),
+    ({"VP9HIP_MC64": "0"}, "C5", 2),
+    ({"VP9HIP_RESID_MULTI": "0"}, "C2", 4),
+    ({"VP9HIP_RESID_MULTI": "0"}, "C5", 2),
+    ({"VP9HIP_LFMC": "1"}, "C2", 6),
+    ({"VP9HIP_LFMC": "1"}, "C5", 3),
+    ({"VP9HIP_LFMC": "1", "VP9HIP_LFR_DB": "0"}, "C2", 4),
 ]
 
 
-@pytest.mark.parametrize("var,config,n", CASES)
-def test_switch_off_matches_oracle(v9, orc, var, config, n):
+@pytest.mark.parametrize("env,config,n", CASES)
+def test_switch_matches_oracle(v9, orc, env, config, n):
     frames, refs, geom = bench.make_frames(v9, config, n)
     W, H, BPP, log2, gop = geom
-    os.environ[var] = "0"
+    os.environ.update(env)
     dev = v9.Device(0)
     try:
         dev.configure(W, H, BPP, nbufs=len(frames))
         dev.stage_batch(frames, list(range(len(frames))), refs)
-        dev.run_batch()
+        for _ in range(2):                       # the second run replays the captured graph
+            dev.run_batch()
         dev.sync()
         bad = []
         for i, ref in bench.oracle_frames(v9, orc, frames, refs, (W, H, BPP, log2, gop)):
             d = bench.compare_frame(v9, dev.download(i), ref, geom)
             if d:
                 bad.append((i, d))
-        assert not bad, "%s=0 %s: frames differing from the oracle: %s" % (var, config, bad)
+        assert not bad, "%s %s: frames differing from the oracle: %s" % (env, config, bad)
     finally:
         dev.close()
-        del os.environ[var]
+        for k in env:
+            del os.environ[k]
