@@ -264,7 +264,7 @@ def main():
         for line in open(pf):
             if not line.startswith(" "):
                 cur = line.strip()
-            elif cur == dom:
+            elif cur in (dom, dom + "d"):          # k_lfr: the k_lfrd kernel
                 f = line.split()
                 vals[f[0]] = float(f[2].split("=")[1])
         if "SQ_INSTS_VALU" in vals and vals.get("duration_us"):

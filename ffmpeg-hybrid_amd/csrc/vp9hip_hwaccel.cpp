@@ -31,6 +31,8 @@
 // AVBufferRef of an AVFrame, vp9hip_hwframe_unref) holds it, it is not the frame being
 // decoded, and it is not in the batch being filled.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <thread>
 #include <cstring>
@@ -47,6 +49,26 @@ using vp9hip::ParsePool;
 
 namespace {
 struct Pend { std::unique_ptr<ParseJob> job; int out; int refs[3]; };
+
+// VP9HIP_HWACCEL_TRACE=1: host wall time of the adapter's steps, printed at uninit
+enum { T_SLICE, T_END, T_PARSE_WAIT, T_CHECK, T_STAGE, T_RUN, T_SYNC_WAIT, T_N };
+const char *const tname[T_N] = { "decode_slice", "end_frame (excl. launches)", "submit: wait for parses",
+                                  "submit: check the slot's previous batch", "submit: stage", "submit: run_batch",
+                                  "hwframe_sync: wait for the frame's batch" };
+struct Trace {
+    bool on = false;
+    double ms[T_N] = {};
+    long batches = 0, frames = 0;
+    std::chrono::steady_clock::time_point t0;
+    void start() { if (on) t0 = std::chrono::steady_clock::now(); }
+    void stop(int k)
+    {
+        if (!on) return;
+        const auto t = std::chrono::steady_clock::now();
+        ms[k] += std::chrono::duration<double, std::milli>(t - t0).count();
+        t0 = t;
+    }
+};
 }
 
 struct vp9hip_hwaccel {
@@ -71,6 +93,7 @@ struct vp9hip_hwaccel {
     uint64_t slot_seq[2] = { 0, 0 };
     bool slot_checked[2] = { true, true };
     std::vector<uint64_t> bad;              // launched batches that failed their check
+    Trace tr;
 };
 
 static int swfmt(int bpp, int ss_h, int ss_v)
@@ -126,6 +149,7 @@ extern "C" int vp9hip_hwaccel_init(int device, const vp9hip_frames_params *fp, v
     }
     vp9hip_set_timing(h->gpu, 0);              // every batch runs once: plain launches, no events
     vp9hip_set_graph(h->gpu, 0);
+    h->tr.on = getenv("VP9HIP_HWACCEL_TRACE") && atoi(getenv("VP9HIP_HWACCEL_TRACE"));
     h->pool.reset(new ParsePool(fp->parse_threads));
     *out = h;
     return 0;
@@ -156,6 +180,8 @@ static int submit_list(vp9hip_hwaccel *h, std::vector<Pend> &batch)
     if (batch.empty()) return 0;
     const int n = (int) batch.size();
     int err = 0;
+    Trace &tr = h->tr;
+    tr.start();
     for (auto &p : batch) {
         h->pool->wait(p.job.get());
         const vp9h_frame &f = p.job->pkt;
@@ -167,7 +193,9 @@ static int submit_list(vp9hip_hwaccel *h, std::vector<Pend> &batch)
     }
     int ret = err;
     const int slot = (int) (h->launched & 1);
+    tr.stop(T_PARSE_WAIT);
     if (!ret) ret = check_slot(h, slot);     // before the staging resets that batch's words
+    tr.stop(T_CHECK);
     if (!ret) ret = vp9hip_set_batch_slot(h->gpu, slot);
     if (!ret) {
         std::vector<vp9h_frame> pk(n);
@@ -178,7 +206,11 @@ static int submit_list(vp9hip_hwaccel *h, std::vector<Pend> &batch)
             for (int r = 0; r < 3; r++) refs[3 * i + r] = batch[i].refs[r] >= 0 ? batch[i].refs[r] : 0;
         }
         ret = vp9hip_stage_batch_refs(h->gpu, pk.data(), n, outs.data(), refs.data());   // copies the packets
+        tr.stop(T_STAGE);
         if (ret >= 0) ret = vp9hip_run_batch(h->gpu);
+        tr.stop(T_RUN);
+        tr.batches++;
+        tr.frames += n;
         if (ret >= 0) {
             h->launched++;
             h->slot_seq[slot] = h->launched;
@@ -270,6 +302,7 @@ extern "C" int vp9hip_hwaccel_start_frame(vp9hip_hwaccel *h, const uint8_t *buf,
 extern "C" int vp9hip_hwaccel_decode_slice(vp9hip_hwaccel *h, const uint8_t *buf, uint32_t size)
 {
     if (!h || !buf || !size || h->cur < 0) return VP9HIP_EINVAL;
+    h->tr.start();
     vp9h_frame_info info;
     const int type = vp9h_frame_peek(buf, size, &info);
     if (type < 0) return type;
@@ -290,6 +323,7 @@ extern "C" int vp9hip_hwaccel_decode_slice(vp9hip_hwaccel *h, const uint8_t *buf
     h->job = std::move(j);
     h->info = info;
     h->intra = type == 0 || type == 3;
+    h->tr.stop(T_SLICE);
     return 0;
 }
 
@@ -309,6 +343,7 @@ static void fill_frame(vp9hip_hwaccel *h, int b, int64_t pts, vp9hip_hwframe *ou
 extern "C" int vp9hip_hwaccel_end_frame(vp9hip_hwaccel *h, vp9hip_hwframe *out)
 {
     if (!h || h->cur < 0 || !h->job) return VP9HIP_EINVAL;
+    h->tr.start();
     Pend p;
     p.out = h->cur;
     for (int i = 0; i < 3; i++) {            // s->s.h.refidx -> the slots' device buffers
@@ -330,6 +365,7 @@ extern "C" int vp9hip_hwaccel_end_frame(vp9hip_hwaccel *h, vp9hip_hwframe *out)
         h->full.push_back(std::move(h->batch));
         h->batch.clear();
     }
+    h->tr.stop(T_END);
     const int r = pump(h);
     if (r < 0) return r;
     return shown;
@@ -361,7 +397,9 @@ extern "C" int vp9hip_hwframe_sync(vp9hip_hwaccel *h, const vp9hip_hwframe *f)
     const uint64_t b = h->buf_seq[f->buf];
     if (!b) return 0;                                    // written before any batch (never decoded)
     const int s = (int) ((b - 1) & 1);
+    h->tr.start();
     if (h->slot_seq[s] == b && (r = check_slot(h, s)) < 0) return r;
+    h->tr.stop(T_SYNC_WAIT);
     // an older batch of the slot was drained and checked before its slot was reused
     return batch_bad(h, b) ? VP9HIP_EBUG : 0;
 }
@@ -383,6 +421,11 @@ extern "C" int vp9hip_hwframe_ready(vp9hip_hwaccel *h, const vp9hip_hwframe *f, 
 extern "C" int vp9hip_hwaccel_uninit(vp9hip_hwaccel *h)
 {
     if (!h) return 0;
+    if (h->tr.on) {
+        fprintf(stderr, "vp9hip hwaccel trace: %ld batches, %ld frames; host ms:", h->tr.batches, h->tr.frames);
+        for (int k = 0; k < T_N; k++) fprintf(stderr, " [%s] %.1f", tname[k], h->tr.ms[k]);
+        fprintf(stderr, "\n");
+    }
     h->job.reset();
     if (h->gpu) {
         submit(h);                           // frames handed out may still be read by the caller

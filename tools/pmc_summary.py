@@ -9,10 +9,13 @@ from collections import defaultdict
 
 
 def short(name):
-    for k in ("k_plf", "k_resid", "k_pred", "k_recon", "k_lfr", "k_lf", "k_mc", "k_plan", "k_psb", "k_pblk"):
-        if k in name:
-            return k
-    return name[:40]
+    """The kernel's identifier ("void k_plan<1, 1>(PlanDev)" -> "k_plan")."""
+    n = name.strip()
+    if n.startswith("void "):
+        n = n[5:]
+    for sep in "<(":
+        n = n.split(sep)[0]
+    return n.strip() or name[:40]
 
 
 def main(d):
