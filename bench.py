@@ -688,7 +688,9 @@ def hwaccel_rate(v, gops, W, H, BPP, args):
     pkts = [d for g in gops for d in g]
     ssh, ssv = CHROMA[args.chroma]
     nbytes = sum(map(len, pkts))
-    out = {"sample_frames": len(pkts), "bytes_per_frame": int(nbytes / len(pkts)), "lag": 16, "async_depth": 16}
+    # lag 16 (a 16-thread frame delay); async depth = frame_params' default for it (the power
+    # of two <= extra / 2 with extra = 2 + lag: 8)
+    out = {"sample_frames": len(pkts), "bytes_per_frame": int(nbytes / len(pkts)), "lag": 16, "async_depth": 8}
     with tempfile.TemporaryDirectory() as td:
         ivf = os.path.join(td, "s.ivf")
         for mode in ("device", "download"):
@@ -696,7 +698,7 @@ def hwaccel_rate(v, gops, W, H, BPP, args):
             while True:
                 with open(ivf, "wb") as f:
                     f.write(v.ivf_write(pkts * reps, W, H))
-                r = subprocess.run([harness, ivf, "-", str(BPP), str(ssh), str(ssv), "1", "16", mode, "16"],
+                r = subprocess.run([harness, ivf, "-", str(BPP), str(ssh), str(ssv), "1", "16", mode, "0"],
                                    capture_output=True, text=True, timeout=300)
                 f = r.stdout.split()
                 if r.returncode or len(f) < 4:

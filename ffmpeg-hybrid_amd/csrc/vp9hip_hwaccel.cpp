@@ -93,6 +93,7 @@ struct vp9hip_hwaccel {
     uint64_t slot_seq[2] = { 0, 0 };
     bool slot_checked[2] = { true, true };
     std::vector<uint64_t> bad;              // launched batches that failed their check
+    size_t max_full = 1;                    // filled batches that may wait for their parses
     Trace tr;
 };
 
@@ -112,10 +113,15 @@ extern "C" int vp9hip_hwaccel_frame_params(int width, int height, int bpp, int s
     out->sw_format = swfmt(bpp, ss_h, ss_v);
     out->width = width;
     out->height = height;
-    out->async_depth = VP9HIP_HWACCEL_ASYNC_DEPTH;
-    // 8 reference slots, the frame being decoded, the frames of the batch being filled
-    // (each also handed out until the consumer has waited for it) and the caller's extra
-    out->initial_pool_size = 8 + 1 + out->async_depth + extra;
+    // batches of half the consumer's frame delay, rounded down to a power of two
+    // (include/vp9hip_hwaccel.h)
+    int d = 1;
+    while (2 * d <= extra / 2 && 2 * d <= VP9HIP_HWACCEL_ASYNC_DEPTH) d *= 2;
+    out->async_depth = d;
+    // 8 reference slots, the frame being decoded, the frames of the batch being filled and
+    // of the filled batches waiting for their parses (each also handed out until the
+    // consumer has waited for it) and the caller's extra
+    out->initial_pool_size = 8 + 1 + (1 + VP9HIP_HWACCEL_AHEAD) * out->async_depth + extra;
     out->bpp = bpp;
     out->ss_h = ss_h;
     out->ss_v = ss_v;
@@ -150,6 +156,8 @@ extern "C" int vp9hip_hwaccel_init(int device, const vp9hip_frames_params *fp, v
     vp9hip_set_timing(h->gpu, 0);              // every batch runs once: plain launches, no events
     vp9hip_set_graph(h->gpu, 0);
     h->tr.on = getenv("VP9HIP_HWACCEL_TRACE") && atoi(getenv("VP9HIP_HWACCEL_TRACE"));
+    // the look-ahead the pool affords beyond the batch being filled
+    h->max_full = (size_t) std::max(1, (fp->initial_pool_size - 9) / fp->async_depth - 1);
     h->pool.reset(new ParsePool(fp->parse_threads));
     *out = h;
     return 0;
@@ -245,14 +253,14 @@ static int submit(vp9hip_hwaccel *h, bool partial = true)
     return err;
 }
 
-// The filled batches whose parses are done launch now, without waiting; more than two
-// filled batches waiting launch the oldest anyway (bounds the frames in flight). The parse
-// pool meanwhile works on the frames the caller keeps handing over.
+// The filled batches whose parses are done launch now, without waiting; more than
+// max_full filled batches waiting launch the oldest anyway (bounds the frames in flight).
+// The parse pool meanwhile works on the frames the caller keeps handing over.
 static int pump(vp9hip_hwaccel *h)
 {
     int err = 0;
     while (!h->full.empty()) {
-        bool ready = h->full.size() > 2;
+        bool ready = h->full.size() > h->max_full;
         if (!ready) {
             ready = true;
             for (auto &p : h->full.front())
@@ -287,12 +295,21 @@ extern "C" int vp9hip_hwaccel_start_frame(vp9hip_hwaccel *h, const uint8_t *buf,
     if (!h || (!buf && size)) return VP9HIP_EINVAL;
     h->job.reset();                          // a frame that never reached end_frame
     h->cur = -1;
-    int b = find_free(h);
-    if (b < 0 && (!h->batch.empty() || !h->full.empty())) {   // unreferenced hidden frames free up once launched
-        const int r = submit(h);
-        if (r < 0) return r;
+    // a full pool: launch the oldest filled batches first (waiting for their parses), then
+    // the one being filled; their unreferenced hidden frames free up once launched
+    int b = find_free(h), err = 0;
+    while (b < 0 && !h->full.empty()) {
+        const int r = submit_list(h, h->full.front());
+        h->full.pop_front();
+        if (r < 0 && !err) err = r;
         b = find_free(h);
     }
+    if (b < 0 && !h->batch.empty()) {
+        const int r = submit_list(h, h->batch);
+        if (r < 0 && !err) err = r;
+        b = find_free(h);
+    }
+    if (err < 0) return err;
     if (b < 0) return VP9HIP_EAGAIN;         // every buffer held: the caller must unref frames
     h->cur = b;
     h->pts = pts;
@@ -379,13 +396,22 @@ extern "C" int vp9hip_hwaccel_show_existing(vp9hip_hwaccel *h, int slot, int64_t
     return 0;
 }
 
-// Launch the frame's batch if it is still being filled; 0 or the frame's error.
+// Launch the frame's batch if it has not been launched yet (and the filled batches before
+// it; the batch being filled only when the frame is in it, so batches stay whole); 0 or
+// the frame's error.
 static int launch_for(vp9hip_hwaccel *h, int b)
 {
-    if (h->pend[b]) {
-        const int r = submit(h);
-        if (r < 0) return r;
+    int err = 0;
+    while (h->pend[b] && !h->full.empty()) {
+        const int r = submit_list(h, h->full.front());
+        h->full.pop_front();
+        if (r < 0 && !err) err = r;
     }
+    if (h->pend[b]) {
+        const int r = submit_list(h, h->batch);
+        if (r < 0 && !err) err = r;
+    }
+    if (err < 0) return err;
     return h->buf_err[b];
 }
 

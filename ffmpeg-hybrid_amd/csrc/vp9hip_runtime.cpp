@@ -175,6 +175,8 @@ struct Staged {
     uint32_t *summary_h = nullptr;                            // pinned readback of the summary
     size_t summary_cap = 0;
     hipEvent_t done_ev = nullptr;       // recorded on the main stream after this batch's last run
+    hipEvent_t up_ev = nullptr;         // recorded after the staging upload: the pinned image is
+                                        // rewritten by the next staging only once it completed
     // ---- static plan (keyframe batches): the launch list is built at staging from the batch
     // geometry (every SB of an intra frame has intra work, so the step lists' sizes and
     // offsets are known); only the residual job ranges come from the planner, read by the
@@ -346,6 +348,7 @@ extern "C" void vp9hip_close(vp9hip_ctx *c)
         if (g->graph) hipGraphExecDestroy(g->graph);
         if (g->summary_h) hipHostFree(g->summary_h);
         if (g->done_ev) hipEventDestroy(g->done_ev);
+        if (g->up_ev) hipEventDestroy(g->up_ev);
         if (g->plan_ev) hipEventDestroy(g->plan_ev);
     }
     if (c->ptab) hipFree(c->ptab);
@@ -1363,7 +1366,10 @@ static int stage_dev(vp9hip_ctx *c, const DevIn &in)
     HIPCHK(hipMemsetAsync(s.arena + s.o_sbncoef + (size_t) NS * 4, 0, 4, us));
     HIPCHK(hipMemsetAsync(s.arena + s.o_cnt + (size_t) s.ncnt * 4, 0, 4, us));
     HIPCHK(hipMemsetAsync(s.arena + s.o_cntm + (size_t) NS * 4, 0, 4, us));
-    HIPCHK(hipStreamSynchronize(us));
+    // no host wait: the planner and the pixel launches follow on this stream (or after it),
+    // and the next staging of this slot waits for the event before rewriting the image
+    if (!s.up_ev) HIPCHK(hipEventCreateWithFlags(&s.up_ev, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(s.up_ev, us));
     s.ready = true;
     return 0;
 }
@@ -1655,6 +1661,7 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     hipSetDevice(c->dev);
     // this slot's previous batch may still read the arena (the other slot's work may go on)
     if (c->stg.done_ev) HIPCHK(hipEventSynchronize(c->stg.done_ev));
+    if (c->stg.up_ev) HIPCHK(hipEventSynchronize(c->stg.up_ev));
     Staged &s = c->stg;
     if (s.graph) { hipGraphExecDestroy(s.graph); s.graph = nullptr; }
     s.frames.clear(); s.sbs.clear(); s.pjobs.clear(); s.passes.clear(); s.lfs.clear(); s.mcs.clear();

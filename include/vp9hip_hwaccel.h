@@ -40,15 +40,24 @@ enum {
 
 /* FFHWAccel.frame_params: what the AVHWFramesContext of the stream's frames gets
  * (format = the HIP hw pix_fmt, sw_format, width, height, initial_pool_size). */
+/* async_depth = the largest power of two <= extra / 2 (the consumer's frame delay: FFmpeg
+ * passes its frame threads and extra_hw_frames as `extra`), at most
+ * VP9HIP_HWACCEL_ASYNC_DEPTH: a consumer that reads a frame `extra` frames after the decoder
+ * finds its batch launched and parsed. Measured C3 (realistic density, lag 16, extra 18):
+ * depth 8 1,210 fps, 4 1,100, 9 830, 16 910 (profiles/r03i). */
 #define VP9HIP_HWACCEL_ASYNC_DEPTH 16
+/* Filled batches that may wait for their entropy decode before the oldest is launched
+ * anyway: the parse look-ahead is (1 + VP9HIP_HWACCEL_AHEAD) x async_depth frames, so that
+ * several GOP chains (whose frames parse one after another) parse at once. */
+#define VP9HIP_HWACCEL_AHEAD 4
 typedef struct vp9hip_frames_params {
     int32_t sw_format;             /* VP9HIP_SWFMT_*                                         */
     int32_t width, height;         /* coded size                                             */
     int32_t initial_pool_size;     /* 8 reference slots + the frame being decoded +          */
-                                   /* async_depth + extra                                    */
+                                   /* (1 + VP9HIP_HWACCEL_AHEAD) x async_depth + extra       */
     int32_t bpp, ss_h, ss_v;
     /* set by frame_params, adjustable before init (the FFmpeg glue maps its options here): */
-    int32_t async_depth;           /* frames per device launch (VP9HIP_HWACCEL_ASYNC_DEPTH);  */
+    int32_t async_depth;           /* frames per device launch (see above);                  */
                                    /* 1 = each frame launched by its end_frame               */
     int32_t parse_threads;         /* host entropy-decode threads (0: in decode_slice)       */
 } vp9hip_frames_params;

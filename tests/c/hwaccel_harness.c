@@ -145,7 +145,7 @@ int main(int argc, char **argv)
         return 1;
     }
     if (depth > 0) {
-        fp.initial_pool_size += depth - fp.async_depth;
+        fp.initial_pool_size += (1 + VP9HIP_HWACCEL_AHEAD) * (depth - fp.async_depth);
         fp.async_depth = depth;
     }
     if ((r = vp9hip_hwaccel_init(0, &fp, &h)) < 0) {

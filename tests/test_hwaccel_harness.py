@@ -39,10 +39,14 @@ def test_frame_params(v9):
     import ctypes
     L = v9.lib()
     fp = _FP()
-    assert L.vp9hip_hwaccel_frame_params(1920, 1080, 10, 1, 1, 3, ctypes.byref(fp)) == 0
-    # 8 slots + the frame being decoded + the batch being filled (async depth 16) + 3 extra
-    assert (fp.sw_format, fp.width, fp.height, fp.async_depth) == (4, 1920, 1080, 16)   # YUV420P10
-    assert fp.initial_pool_size == 8 + 1 + 16 + 3 and fp.parse_threads >= 1
+    assert L.vp9hip_hwaccel_frame_params(1920, 1080, 10, 1, 1, 18, ctypes.byref(fp)) == 0
+    # async depth = the power of two <= half the caller's extra (its frame delay); 8 slots +
+    # the frame being decoded + the batch being filled and VP9HIP_HWACCEL_AHEAD (4) filled
+    # ones + 18 extra
+    assert (fp.sw_format, fp.width, fp.height, fp.async_depth) == (4, 1920, 1080, 8)   # YUV420P10
+    assert fp.initial_pool_size == 8 + 1 + (1 + 4) * 8 + 18 and fp.parse_threads >= 1
+    assert L.vp9hip_hwaccel_frame_params(1920, 1080, 8, 1, 1, 1, ctypes.byref(fp)) == 0 and fp.async_depth == 1
+    assert L.vp9hip_hwaccel_frame_params(1920, 1080, 8, 1, 1, 64, ctypes.byref(fp)) == 0 and fp.async_depth == 16
     assert L.vp9hip_hwaccel_frame_params(64, 64, 8, 0, 0, 0, ctypes.byref(fp)) == 0 and fp.sw_format == 3
     assert L.vp9hip_hwaccel_frame_params(64, 64, 9, 1, 1, 0, ctypes.byref(fp)) == v9.EINVAL
 
@@ -72,10 +76,11 @@ def run_harness(ivf, out, bpp, ssh, ssv, passes=2, lag=0, mode="download", depth
 
 # async depth (frames per launch) x consumer lag: 16 / 0 reads each frame at once (every
 # read launches the partial batch holding it); lag 8 / depth 4 keeps batches full; depth 1
-# launches every frame from its end_frame; hidden frames ride with the next batch
+# launches every frame from its end_frame; depth 0 takes frame_params' default (half the
+# extra frames, a power of two: 1 at lag 0, 8 at lag 20); hidden frames ride with the next batch
 @pytest.mark.gpu
-@pytest.mark.parametrize("w,h,bpp,ssh,ssv,lag,depth", [(200, 130, 8, 1, 1, 0, 0), (176, 144, 10, 1, 1, 0, 0),
-                                                     (136, 72, 8, 0, 0, 0, 0), (200, 130, 8, 1, 1, 8, 4),
+@pytest.mark.parametrize("w,h,bpp,ssh,ssv,lag,depth", [(200, 130, 8, 1, 1, 0, 16), (176, 144, 10, 1, 1, 0, 0),
+                                                     (136, 72, 8, 0, 0, 0, 16), (200, 130, 8, 1, 1, 8, 4),
                                                      (200, 130, 8, 1, 1, 3, 1), (176, 144, 10, 1, 1, 20, 0)])
 def test_hwaccel_call_order_matches_oracle(v9, orc, tmp_path, w, h, bpp, ssh, ssv, lag, depth):
     pkts = _stream(v9, w, h, bpp, ssh, ssv)

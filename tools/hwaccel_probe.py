@@ -2,7 +2,7 @@
 """FFHWAccel adapter probe (GPU box): the bench's realistic-density C3 (or --config) sample
 stream, repeated, through tests/c/hwaccel_harness with VP9HIP_HWACCEL_TRACE=1 (host time per
 adapter step on stderr). Usage: hwaccel_probe.py [--config C3] [--reps 20] [--mode device]
-[--lag 16] [--depth 16] [extra env NAME=VALUE ...]"""
+[--lag 16] [--depth 0] [extra env NAME=VALUE ...]"""
 import argparse, os, subprocess, sys, tempfile
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -14,7 +14,7 @@ ap.add_argument("--config", default="C3")
 ap.add_argument("--reps", type=int, default=20)
 ap.add_argument("--mode", default="device")
 ap.add_argument("--lag", type=int, default=16)
-ap.add_argument("--depth", type=int, default=16)
+ap.add_argument("--depth", type=int, default=0)          # 0: frame_params' default
 ap.add_argument("env", nargs="*")
 a = ap.parse_args()
 v = importlib.import_module("ffmpeg-hybrid_amd")
