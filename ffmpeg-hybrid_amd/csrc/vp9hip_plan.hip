@@ -359,6 +359,7 @@ template <int JCAP> struct PlanLds {
             uint16_t dep[4 * JCAP];
             uint16_t ord[JCAP];           // jobs by (height desc, index asc)
             uint16_t sch[JCAP];           // pass of each job (0xffff: not yet)
+            uint8_t  dpos[JCAP];          // producers of job j before dep[.. + dpos] are scheduled
             uint32_t hs[64];              // height histogram -> list starts
             uint16_t tk[16];              // jobs taken by the pass being built
         } b;
@@ -609,6 +610,7 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
                 else st |= PLS_SCHED;
                 S.u.b.doff[j] = (uint16_t) (off >> 1 | (k - off) << 11);
                 S.u.b.sch[j] = 0xffff;
+                S.u.b.dpos[j] = 0;
             }
             carry += rdl(incl, 63);
         }
@@ -681,9 +683,14 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
             const int j = pos < NJ ? S.u.b.ord[pos] : 0;
             bool cand = pos < NJ && S.u.b.sch[j] == 0xffff;
             if (cand) {
+                // producers scheduled in earlier passes stay so: resume after the ones already
+                // seen (each producer passes this check once; a blocked job costs one test per pass)
                 const uint32_t dw = S.u.b.doff[j];
-                for (int k = (int) (dw & 2047) << 1, k1 = k + (int) (dw >> 11); k < k1; k++)
-                    if (S.u.b.sch[S.u.b.dep[k]] >= (uint16_t) npass) { cand = false; break; }
+                const int k0 = (int) (dw & 2047) << 1, k1 = k0 + (int) (dw >> 11);
+                int k = k0 + S.u.b.dpos[j];
+                while (k < k1 && S.u.b.sch[S.u.b.dep[k]] < (uint16_t) npass) k++;
+                S.u.b.dpos[j] = (uint8_t) (k - k0);
+                cand = k == k1;
             }
             const int sz = 4 << ((S.ja[j] >> 2) & 3);
             // takes in priority order by lane-size prefix sums: round 1 takes the longest

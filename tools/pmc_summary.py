@@ -13,6 +13,7 @@ def short(name):
     n = name.strip()
     if n.startswith("void "):
         n = n[5:]
+    n = n.replace("(anonymous namespace)::", "")
     for sep in "<(":
         n = n.split(sep)[0]
     return n.strip() or name[:40]

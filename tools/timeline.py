@@ -38,7 +38,7 @@ for t, dlt in pts:
     c += dlt; last = t
 per = defaultdict(int)
 for s, e, n in sel:
-    k = n.split("<")[0].split("(")[0].replace("void ", "")
+    k = n.replace("(anonymous namespace)::", "").split("<")[0].split("(")[0].replace("void ", "")
     per[k] += e - s
 span = t1 - t0
 print("groups %d span %.3f ms busy %.1f%% mean concurrency %.2f" % (len(groups[-steps:]), span / 1e6, 100.0 * busy / span, conc_area / max(busy, 1)))
