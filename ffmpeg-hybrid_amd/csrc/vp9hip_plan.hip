@@ -359,7 +359,6 @@ template <int JCAP> struct PlanLds {
             uint16_t dep[4 * JCAP];
             uint16_t ord[JCAP];           // jobs by (height desc, index asc)
             uint16_t sch[JCAP];           // pass of each job (0xffff: not yet)
-            uint8_t  dpos[JCAP];          // producers of job j before dep[.. + dpos] are scheduled
             uint32_t hs[64];              // height histogram -> list starts
             uint16_t tk[16];              // jobs taken by the pass being built
         } b;
@@ -610,7 +609,6 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
                 else st |= PLS_SCHED;
                 S.u.b.doff[j] = (uint16_t) (off >> 1 | (k - off) << 11);
                 S.u.b.sch[j] = 0xffff;
-                S.u.b.dpos[j] = 0;
             }
             carry += rdl(incl, 63);
         }
@@ -674,36 +672,58 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
     // (all producers in earlier passes) that still fits in 64 lanes; lane groups by size
     uint32_t *gpass = D.passes + (size_t) slot * JCAP;
     PJob *gjob = D.pjobs + (size_t) slot * JCAP;
-    int done = 0, npass = 0, c0 = 0;
+    int done = 0, npass = 0;
+    // Each lane holds, per chunk c of the priority order, position c * 64 + lane: its job, size,
+    // and the range of its producer list still to see (k: the first producer not known to be
+    // scheduled in an earlier pass; producers scheduled in earlier passes stay so), and bit c
+    // of `pend` while it is unscheduled. A pass then reads LDS only for the sch[] word of each
+    // waiting job's current producer.
+    constexpr int NCH = JCAP / 64;
+    uint32_t jreg[NCH], kreg[NCH], k1reg[NCH], szreg[NCH];
+    uint32_t pend = 0;
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+        const int pos = c * 64 + lane;
+        jreg[c] = kreg[c] = k1reg[c] = 0;
+        szreg[c] = 0;
+        if (pos < NJ) {
+            const uint32_t j = S.u.b.ord[pos], dw = S.u.b.doff[j];
+            jreg[c] = j;
+            kreg[c] = (dw & 2047) << 1;
+            k1reg[c] = kreg[c] + (dw >> 11);
+            szreg[c] = 4u << ((S.ja[j] >> 2) & 3);
+            pend |= 1u << c;
+        }
+    }
     if (D.dbg & 2) done = NJ;                 // ablation (timing only): no pass building
     while (done < NJ) {
         int budget = 64, ntake = 0;
-        for (int c = c0; c < NJ && budget >= 4; c += 64) {
-            const int pos = c + lane;
-            const int j = pos < NJ ? S.u.b.ord[pos] : 0;
-            bool cand = pos < NJ && S.u.b.sch[j] == 0xffff;
+#pragma unroll
+        for (int c = 0; c < NCH; c++) {
+            if (budget < 4) break;
+            bool cand = (pend >> c) & 1u;
+            if (!__any(cand)) continue;           // every job of this chunk is scheduled
             if (cand) {
-                // producers scheduled in earlier passes stay so: resume after the ones already
-                // seen (each producer passes this check once; a blocked job costs one test per pass)
-                const uint32_t dw = S.u.b.doff[j];
-                const int k0 = (int) (dw & 2047) << 1, k1 = k0 + (int) (dw >> 11);
-                int k = k0 + S.u.b.dpos[j];
+                uint32_t k = kreg[c];
+                const uint32_t k1 = k1reg[c];
                 while (k < k1 && S.u.b.sch[S.u.b.dep[k]] < (uint16_t) npass) k++;
-                S.u.b.dpos[j] = (uint8_t) (k - k0);
+                kreg[c] = k;
                 cand = k == k1;
             }
-            const int sz = 4 << ((S.ja[j] >> 2) & 3);
+            if (!__any(cand)) continue;           // nothing ready in this chunk
+            const uint32_t j = jreg[c], sz = szreg[c];
             // takes in priority order by lane-size prefix sums: round 1 takes the longest
             // prefix of the chunk's ready jobs that fits, later rounds refill the remaining
             // lanes from the jobs skipped (any packing that respects the producers is exact;
             // only the pass count depends on it)
             for (int round = 0; round < 3 && budget >= 4; round++) {
-                const uint32_t incl = wscan_incl(cand ? (uint32_t) sz : 0u, lane);
+                const uint32_t incl = wscan_incl(cand ? sz : 0u, lane);
                 const bool take = cand && incl <= (uint32_t) budget;
                 const uint64_t m = __ballot(take);
                 if (!m) break;
                 if (take) {
                     cand = false;
+                    pend &= ~(1u << c);
                     S.u.b.sch[j] = (uint16_t) npass;
                     S.u.b.tk[ntake + (int) mbcnt(m)] = (uint16_t) j;
                 }
@@ -734,12 +754,6 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
         if (lane == 0 && inb(D, (uint32_t) npass, JCAP, 256u)) gpass[npass] = (uint32_t) done << 14 | cnt[0] << 9 | cnt[1] << 5 | cnt[2] << 2 | cnt[3];
         done += ntake;
         npass++;
-        // skip chunks of the priority order that are fully scheduled
-        while (c0 < NJ) {
-            const int pos = c0 + lane;
-            if (__any(pos < NJ && S.u.b.sch[S.u.b.ord[pos]] == 0xffff)) break;
-            c0 += 64;
-        }
         wsync();
     }
     if (lane == 0) {
