@@ -12,6 +12,7 @@ raises :class:`Vp9HipUnavailable`.
 """
 import ctypes
 import os
+import sys
 
 import numpy as np
 
@@ -100,6 +101,11 @@ class EncParams(ctypes.Structure):
 
 
 _lib_handle = None
+# torch's ROCm wheel ships its own libamdhip64 under the same soname as /opt/rocm's, which
+# libvp9hip.so links: whichever process loads first serves both. torch's device init fails
+# ("No HIP GPUs are available") on the newer /opt/rocm runtime, so torch interop
+# (frame_tensors) needs torch imported before this library is loaded.
+_torch_first = False
 
 # Exported symbols of include/vp9hip.h (checked by the CPU test suite).
 ABI_SYMBOLS = ["vp9hip_open", "vp9hip_close", "vp9hip_configure", "vp9hip_submit_frame",
@@ -129,6 +135,8 @@ def lib():
         return _lib_handle
     if not os.path.exists(LIB_PATH):
         raise Vp9HipUnavailable("libvp9hip.so not built: run __graft_entry__.build() (%s)" % LIB_PATH)
+    global _torch_first
+    _torch_first = "torch" in sys.modules
     L = ctypes.CDLL(LIB_PATH)
     vp = ctypes.c_void_p
     L.vp9hip_open.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
@@ -577,7 +585,11 @@ class Device:
     def frame_tensors(self, buf, device=None):
         """Zero-copy torch views (uint8 / int16 storage of the u16 samples) of buffer
         `buf`'s visible planes, via __cuda_array_interface__. Call sync() first (or order
-        consumers after the context's stream)."""
+        consumers after the context's stream). Needs torch imported before the library was
+        loaded (see _torch_first)."""
+        if not _torch_first:
+            raise Vp9HipUnavailable("frame_tensors: import torch before ffmpeg-hybrid_amd loads libvp9hip.so "
+                                    "(both use libamdhip64; torch's device init needs its own runtime loaded first)")
         import torch
         ptrs, ls, (w, h), _ = self.frame_device(buf)
         bpp = 1 if self.bpp == 8 else 2

@@ -9,6 +9,11 @@ independently of intra parity.
 import numpy as np
 import pytest
 
+try:     # torch first: the zero-copy test shares its HIP runtime with libvp9hip.so (see _torch_first)
+    import torch  # noqa: F401
+except ImportError:
+    pass
+
 pytestmark = pytest.mark.gpu
 
 # (w, h, bpp, extra synth params) — odd sizes exercise the frame-edge rules
