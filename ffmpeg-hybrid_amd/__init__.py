@@ -499,10 +499,11 @@ class Device:
         _check("vp9hip_stage_batch_refs", lib().vp9hip_stage_batch_refs(self._c, arr, len(frames), ob, rb))
 
     PART_RECON, PART_LF = 0, 1
+    MAX_SLOTS = 4                  # VP9HIP_MAX_SLOTS (include/vp9hip.h)
 
     def set_slot(self, slot):
-        """Select batch slot 0 / 1 (vp9hip_set_batch_slot): two staged batches, run alternately,
-        overlap one batch's device planning with the other's pixel kernels."""
+        """Select batch slot 0 .. MAX_SLOTS - 1 (vp9hip_set_batch_slot): staged batches run in
+        turn overlap one batch's device planning and pixel chains with the others'."""
         _check("vp9hip_set_batch_slot", lib().vp9hip_set_batch_slot(self._c, int(slot)))
 
     def phases(self):

@@ -93,6 +93,7 @@ struct Launch { int kind; uint32_t off; uint32_t n; int arg; int grp; int ph; in
 #define LFR_MAX_FRAMES 8
 enum { PART_RECON, PART_LF };           // a phase's reconstruction launches, then its loop filter
 #define MAX_GROUPS 8                    // independent frame groups = concurrent launch chains
+#define MAX_SLOTS VP9HIP_MAX_SLOTS      // batch slots per context (include/vp9hip.h)
 #define LF_LAG 2                        // LF diagonal j needs intra diagonals <= j + LF_LAG (see enqueue_batch)
 
 struct Staged {
@@ -189,7 +190,7 @@ struct Staged {
     std::vector<uint32_t> exp_ko;       // key offsets the launch list was built with
     std::vector<uint32_t> stat_lists;   // the intra step lists (uploaded with the batch)
     std::vector<int> wr, rd;            // frame buffers the batch writes / reads (sorted)
-    bool dep_other = false;             // it touches a buffer of the other slot's batch
+    uint32_t dep_mask = 0;              // bit k: it touches a buffer of slot k's batch
     double alg_stat[K_N] = {};          // algorithmic bytes after the launch-list moves
 };
 
@@ -224,7 +225,8 @@ struct vp9hip_ctx {
     int dbg = 0;                        // VP9HIP_DEBUG: ablation switches for profiling only
     bool use_graph = true;              // VP9HIP_GRAPH=0 disables graph replay
     Staged stg;                         // the current batch slot
-    Staged alt;                         // the other slot (vp9hip_set_batch_slot swaps them)
+    Staged sl[MAX_SLOTS];               // the other slots (sl[slot] is a moved-out placeholder;
+                                        // vp9hip_set_batch_slot swaps a slot in and out)
     int slot = 0;
     hipStream_t pst = nullptr;          // device planner stream: a slot's planning overlaps the
                                         // other slot's pixel kernels (VP9HIP_SLOT_STREAMS=0 only)
@@ -232,9 +234,11 @@ struct vp9hip_ctx {
     // into st / xst with the slot, and plans on its main stream ahead of its pixel work. Two
     // staged batches that share no frame buffer then run concurrently (the second batch's
     // intra wavefront under the first one's loop-filter tail); a batch that reads or writes a
-    // buffer of the other slot's batch waits for it (dep_other, found at staging).
+    // buffer of another slot's batch waits for it (dep_mask, found at staging). Slots 0 and 1
+    // get their streams at open, slots 2.. at their first use.
     bool slot_streams = true;
-    hipStream_t st_o = nullptr, xst_o[MAX_GROUPS - 1] = {};
+    int pix_prio = 0;
+    hipStream_t sst[MAX_SLOTS] = {}, sxst[MAX_SLOTS][MAX_GROUPS - 1] = {};   // per slot: main, groups
     // timing of the last run
     bool timing = true;
     std::vector<hipEvent_t> ev;
@@ -248,13 +252,25 @@ struct vp9hip_ctx {
 
 // The planner's stream: the slot's main stream with per-slot streams, else its own.
 static hipStream_t plan_stream(const vp9hip_ctx *c) { return c->slot_streams ? c->st : c->pst; }
-// Wait for everything either slot queued.
+// Slot k's staged batch (the current one lives in c->stg).
+static Staged &slot_ref(vp9hip_ctx *c, int k) { return k == c->slot ? c->stg : c->sl[k]; }
+// Wait for everything any slot queued.
 static hipError_t sync_all(vp9hip_ctx *c)
 {
     hipError_t e = hipStreamSynchronize(c->st);
-    if (e == hipSuccess && c->st_o) e = hipStreamSynchronize(c->st_o);
+    for (int k = 0; k < MAX_SLOTS && e == hipSuccess; k++)
+        if (c->sst[k] && c->sst[k] != c->st) e = hipStreamSynchronize(c->sst[k]);
     if (e == hipSuccess && c->pst) e = hipStreamSynchronize(c->pst);
     return e;
+}
+// The streams of slot k (per-slot streams): created at the context's stream priority.
+static bool slot_streams_make(vp9hip_ctx *c, int k)
+{
+    if (c->sst[k]) return true;
+    bool ok = hipStreamCreateWithPriority(&c->sst[k], hipStreamNonBlocking, c->pix_prio) == hipSuccess;
+    for (int i = 0; ok && i < c->max_groups - 1; i++)
+        ok = hipStreamCreateWithPriority(&c->sxst[k][i], hipStreamNonBlocking, c->pix_prio) == hipSuccess;
+    return ok;
 }
 
 extern "C" int vp9hip_open(int device, vp9hip_ctx **out)
@@ -287,15 +303,16 @@ extern "C" int vp9hip_open(int device, vp9hip_ctx **out)
     hipSetDevice(device);
     if (prio) hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
     const int pix_prio = prio == 2 ? prio_hi : prio == 3 ? prio_lo : 0;
+    c->pix_prio = pix_prio;
     const int plan_prio = prio == 1 || prio == 3 ? prio_lo : 0;
     bool ok = hipStreamCreateWithPriority(&c->st, hipStreamNonBlocking, pix_prio) == hipSuccess &&
               hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) == hipSuccess;
     for (int i = 0; ok && i < c->max_groups - 1; i++)
         ok = hipStreamCreateWithPriority(&c->xst[i], hipStreamNonBlocking, pix_prio) == hipSuccess;
-    if (c->slot_streams) {             // the other slot's set: with 2 groups, 4 streams = the 4 hardware queues
-        ok = ok && hipStreamCreateWithPriority(&c->st_o, hipStreamNonBlocking, pix_prio) == hipSuccess;
-        for (int i = 0; ok && i < c->max_groups - 1; i++)
-            ok = hipStreamCreateWithPriority(&c->xst_o[i], hipStreamNonBlocking, pix_prio) == hipSuccess;
+    if (c->slot_streams) {             // slot 1's set: with 2 groups, 4 streams = the 4 hardware queues
+        c->sst[0] = c->st;
+        for (int i = 0; i < MAX_GROUPS - 1; i++) c->sxst[0][i] = c->xst[i];
+        ok = ok && slot_streams_make(c, 1);
     } else {
         ok = ok && hipStreamCreateWithPriority(&c->pst, hipStreamNonBlocking, plan_prio) == hipSuccess;
     }
@@ -320,12 +337,13 @@ static void free_bufs(vp9hip_ctx *c)
     c->buf_wh.clear();
 }
 
-// Forget the staged batches of both slots (their FrameDescs, graphs and launch lists name
-// frame buffers): a later run_batch of either slot needs a new stage. The caller has
+// Forget the staged batches of every slot (their FrameDescs, graphs and launch lists name
+// frame buffers): a later run_batch of any slot needs a new stage. The caller has
 // synchronised the main and planner streams.
 static void drop_slots(vp9hip_ctx *c)
 {
-    for (Staged *g : { &c->stg, &c->alt }) {
+    for (int k = 0; k < MAX_SLOTS; k++) {
+        Staged *g = &slot_ref(c, k);
         g->ready = false;
         g->planned = false;
         if (g->graph) hipGraphExecDestroy(g->graph);
@@ -341,7 +359,8 @@ extern "C" void vp9hip_close(vp9hip_ctx *c)
     hipSetDevice(c->dev);
     sync_all(c);
     free_bufs(c);
-    for (Staged *g : { &c->stg, &c->alt }) {
+    for (int k = 0; k < MAX_SLOTS; k++) {
+        Staged *g = &slot_ref(c, k);
         if (g->arena) hipFree(g->arena);
         if (g->resid) hipFree(g->resid);
         if (g->pinned) hipHostFree(g->pinned);
@@ -357,13 +376,19 @@ extern "C" void vp9hip_close(vp9hip_ctx *c)
     if (c->pst) hipStreamDestroy(c->pst);
     for (auto e : c->pev) if (e) hipEventDestroy(e);
     for (auto e : c->ev) hipEventDestroy(e);
-    hipStreamDestroy(c->st);
-    if (c->st_o) hipStreamDestroy(c->st_o);
-    for (int i = 0; i < MAX_GROUPS - 1; i++) {
-        if (c->xst[i]) hipStreamDestroy(c->xst[i]);
-        if (c->xst_o[i]) hipStreamDestroy(c->xst_o[i]);
-        if (c->join_ev[i]) hipEventDestroy(c->join_ev[i]);
+    if (c->slot_streams) {             // every slot's streams (c->st / xst are one slot's)
+        for (int k = 0; k < MAX_SLOTS; k++) {
+            if (c->sst[k]) hipStreamDestroy(c->sst[k]);
+            for (int i = 0; i < MAX_GROUPS - 1; i++)
+                if (c->sxst[k][i]) hipStreamDestroy(c->sxst[k][i]);
+        }
+    } else {
+        hipStreamDestroy(c->st);
+        for (int i = 0; i < MAX_GROUPS - 1; i++)
+            if (c->xst[i]) hipStreamDestroy(c->xst[i]);
     }
+    for (int i = 0; i < MAX_GROUPS - 1; i++)
+        if (c->join_ev[i]) hipEventDestroy(c->join_ev[i]);
     for (int i = 0; i < MAX_GROUPS; i++) {
         if (c->lst[i]) hipStreamDestroy(c->lst[i]);
         if (c->lf_done[i]) hipEventDestroy(c->lf_done[i]);
@@ -460,7 +485,7 @@ extern "C" int vp9hip_configure(vp9hip_ctx *c, int width, int height, int bpp, i
     if (ss_h < 0 || ss_h > 1 || ss_v < 0 || ss_v > 1) return VP9HIP_EINVAL;   // 4:2:0 / 4:2:2 / 4:4:0 / 4:4:4
     hipSetDevice(c->dev);
     sync_all(c);
-    drop_slots(c);                      // both slots' records point at the buffers freed here
+    drop_slots(c);                      // every slot's records point at the buffers freed here
     free_bufs(c);
     c->w = width; c->h = height; c->bpp = bpp; c->ss_h = ss_h; c->ss_v = ss_v;
     c->hb = bpp > 8; c->bypp = c->hb ? 2 : 1;
@@ -1811,7 +1836,7 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     }
 
     STAGE_T(0);
-    // the buffers this batch writes and reads, and whether the other slot's batch touches them
+    // the buffers this batch writes and reads, and which other slots' batches touch them
     s.wr.assign(out_bufs, out_bufs + n);
     s.rd.clear();
     for (int i = 0; i < n && ref_bufs; i++)
@@ -1826,8 +1851,12 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
             }
             return false;
         };
-        const Staged &o = c->alt;
-        s.dep_other = o.ready && (meet(s.wr, o.wr) || meet(s.wr, o.rd) || meet(s.rd, o.wr));
+        s.dep_mask = 0;
+        for (int k = 0; k < MAX_SLOTS; k++) {
+            if (k == c->slot) continue;
+            const Staged &o = c->sl[k];
+            if (o.ready && (meet(s.wr, o.wr) || meet(s.wr, o.rd) || meet(s.rd, o.wr))) s.dep_mask |= 1u << k;
+        }
     }
     s.dev = false;
     if (!c->host_plan) {
@@ -2214,8 +2243,9 @@ extern "C" int vp9hip_run_batch(vp9hip_ctx *c)
         if (hw) HIPCHK(hipEventSynchronize(s.plan_ev));          // A/B diagnostics only
         else HIPCHK(hipStreamWaitEvent(c->st, s.plan_ev, 0));
     }
-    // a batch touching the other slot's buffers follows that slot's last run
-    if (c->slot_streams && s.dep_other && c->alt.done_ev) HIPCHK(hipStreamWaitEvent(c->st, c->alt.done_ev, 0));
+    // a batch touching another slot's buffers follows that slot's last run
+    for (int k = 0; c->slot_streams && k < MAX_SLOTS; k++)
+        if (((s.dep_mask >> k) & 1) && c->sl[k].done_ev) HIPCHK(hipStreamWaitEvent(c->st, c->sl[k].done_ev, 0));
     // this slot's last work on the main stream: its next planning waits for it
     if (!s.done_ev) HIPCHK(hipEventCreateWithFlags(&s.done_ev, hipEventDisableTiming));
     if (c->timing || !c->use_graph) {
@@ -2480,9 +2510,9 @@ static int check_lfr(const Staged &g)
 
 extern "C" int vp9hip_sync_slot(vp9hip_ctx *c, int slot)
 {
-    if (!c || slot < 0 || slot > 1) return VP9HIP_EINVAL;
+    if (!c || slot < 0 || slot >= MAX_SLOTS) return VP9HIP_EINVAL;
     hipSetDevice(c->dev);
-    Staged &g = slot == c->slot ? c->stg : c->alt;
+    Staged &g = slot_ref(c, slot);
     if (g.done_ev) HIPCHK(hipEventSynchronize(g.done_ev));
     if (const int r = finish_summary(c, g)) return r;
     return check_lfr(g);
@@ -2490,18 +2520,18 @@ extern "C" int vp9hip_sync_slot(vp9hip_ctx *c, int slot)
 
 extern "C" int vp9hip_slot_stream_wait(vp9hip_ctx *c, int slot, void *stream)
 {
-    if (!c || slot < 0 || slot > 1) return VP9HIP_EINVAL;
+    if (!c || slot < 0 || slot >= MAX_SLOTS) return VP9HIP_EINVAL;
     hipSetDevice(c->dev);
-    const Staged &g = slot == c->slot ? c->stg : c->alt;
+    const Staged &g = slot_ref(c, slot);
     if (g.done_ev) HIPCHK(hipStreamWaitEvent((hipStream_t) stream, g.done_ev, 0));
     return 0;
 }
 
 extern "C" int vp9hip_slot_busy(vp9hip_ctx *c, int slot)
 {
-    if (!c || slot < 0 || slot > 1) return VP9HIP_EINVAL;
+    if (!c || slot < 0 || slot >= MAX_SLOTS) return VP9HIP_EINVAL;
     hipSetDevice(c->dev);
-    const Staged &g = slot == c->slot ? c->stg : c->alt;
+    const Staged &g = slot_ref(c, slot);
     if (!g.done_ev) return 0;
     const hipError_t e = hipEventQuery(g.done_ev);
     return e == hipErrorNotReady ? 1 : e == hipSuccess ? 0 : VP9HIP_EEXTERNAL;
@@ -2512,11 +2542,11 @@ extern "C" int vp9hip_sync(vp9hip_ctx *c)
     if (!c) return VP9HIP_EINVAL;
     hipSetDevice(c->dev);
     HIPCHK(sync_all(c));
-    // both slots' work is complete: their hand-off counters and summaries are final
-    for (Staged *g : { &c->stg, &c->alt })
-        if (const int r = finish_summary(c, *g)) return r;
-    if (const int r = check_lfr(c->stg)) return r;
-    if (const int r = check_lfr(c->alt)) return r;
+    // every slot's work is complete: their hand-off counters and summaries are final
+    for (int k = 0; k < MAX_SLOTS; k++)
+        if (const int r = finish_summary(c, slot_ref(c, k))) return r;
+    for (int k = 0; k < MAX_SLOTS; k++)
+        if (const int r = check_lfr(slot_ref(c, k))) return r;
     if (c->timing && c->timed_run && c->stg.ready) {
         for (int k = 0; k < K_N; k++) { c->kms[k] = 0; c->kcount[k] = 0; }
         for (size_t i = 0; i < c->stg.launches.size() && 2 * i + 1 < c->ev.size(); i++) {
@@ -2666,17 +2696,23 @@ extern "C" int vp9hip_device_info(int device, char *pci_bus_id, int len, char *n
     return 0;
 }
 
-// Two batch slots per context: stage / run / sync / phase calls act on the current slot.
-// Each slot has its own arena, plan and graph; the frame buffers are the context's. A run of
-// one slot plans on the planner stream while the other slot's pixel kernels still run.
+// VP9HIP_MAX_SLOTS batch slots per context: stage / run / sync / phase calls act on the
+// current slot. Each slot has its own arena, plan, graph and (per-slot streams) streams; the
+// frame buffers are the context's. A run of one slot plans while other slots' pixel kernels
+// still run.
 extern "C" int vp9hip_set_batch_slot(vp9hip_ctx *c, int slot)
 {
-    if (!c || slot < 0 || slot > 1) return VP9HIP_EINVAL;
+    if (!c || slot < 0 || slot >= MAX_SLOTS) return VP9HIP_EINVAL;
     if (slot != c->slot) {
-        std::swap(c->stg, c->alt);
         if (c->slot_streams) {
-            std::swap(c->st, c->st_o);
-            for (int i = 0; i < MAX_GROUPS - 1; i++) std::swap(c->xst[i], c->xst_o[i]);
+            hipSetDevice(c->dev);
+            if (!slot_streams_make(c, slot)) return VP9HIP_EEXTERNAL;
+        }
+        std::swap(c->stg, c->sl[c->slot]);   // the current batch back into its storage
+        std::swap(c->stg, c->sl[slot]);      // and the other one in
+        if (c->slot_streams) {
+            c->st = c->sst[slot];
+            for (int i = 0; i < MAX_GROUPS - 1; i++) c->xst[i] = c->sxst[slot][i];
         }
         c->slot = slot;
     }
@@ -2687,6 +2723,48 @@ extern "C" int vp9hip_set_batch_slot(vp9hip_ctx *c, int slot)
 // and to size kernels. out[]: 0 SBs with intra work, 1 passes, 2 intra jobs, 3 residual
 // jobs, 4..7 intra jobs per tx size, 8 lane use (job lanes / 64 per pass), 9 max passes
 // in one SB, 10 LF records, 11 MC units, 12 intra wavefront steps, 13 LF wavefront steps.
+// Diagnostics (tools/wave_tail.py): per SB of one packet, in raster order, the pixel rows its
+// intra passes loop over (sum of each pass's largest job size), as staged for the device.
+extern "C" int vp9hip_plan_sb_costs(const vp9h_frame *f, double *out, int cap)
+{
+    if (!f || !out) return VP9HIP_EINVAL;
+    if (f->ss_h > 1 || f->ss_v > 1) return VP9HIP_EINVAL;
+    init_nz();
+    Staged s;
+    FrameBuild fb;
+    fb.f = f; fb.frame_idx = 0;
+    fb.cols = (f->width + 7) >> 3; fb.rows = (f->height + 7) >> 3;
+    fb.sb_cols = (f->width + 63) >> 6; fb.sb_rows = (f->height + 63) >> 6;
+    fb.ss_h = f->ss_h; fb.ss_v = f->ss_v; fb.coef_size = f->bpp > 8 ? 4 : 2;
+    fb.pitch[0] = fb.sb_cols * 64; fb.pitch[1] = fb.sb_cols * 64 >> f->ss_h;
+    fb.coef_base = 0;
+    fb.phase = 0;
+    memset(&fb.mc, 0, sizeof(fb.mc));
+    fb.mc.cols = fb.cols; fb.mc.rows = fb.rows; fb.mc.ss_h = f->ss_h; fb.mc.ss_v = f->ss_v;
+    s.rbucket.resize(1);
+    std::vector<std::vector<uint32_t>> ps, ls;
+    int r = build_frame(nullptr, s, fb, ps, ls);
+    if (r < 0) return r;
+    const int n = fb.sb_cols * fb.sb_rows;
+    if (cap < n) return VP9HIP_EINVAL;
+    for (int i = 0; i < n; i++) out[i] = 0;
+    for (auto &v : ps)
+        for (uint32_t sbi : v) {
+            r = merge_mixed(s, sbi);
+            if (r) return r;
+        }
+    for (const WGRec &wg : s.wgs) {
+        const SBRec &sb = s.sbs[wg.sb[0]];
+        double rows = 0;
+        for (uint32_t k = 0; k < wg.npass; k++) {
+            const uint32_t w = s.passes[wg.pass0 + k];
+            rows += (w & 3) ? 32 : ((w >> 2) & 7) ? 16 : ((w >> 5) & 15) ? 8 : 4;
+        }
+        out[sb.sby * fb.sb_cols + sb.sbx] = rows;
+    }
+    return n;
+}
+
 extern "C" int vp9hip_plan_stats(const vp9h_frame *f, double *out, int cap)
 {
     if (!f || !out || cap < 16) return VP9HIP_EINVAL;

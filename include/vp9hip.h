@@ -169,14 +169,17 @@ int  vp9hip_run_phase(vp9hip_ctx *ctx, int phase, int part);
  */
 int64_t vp9hip_stripe(vp9hip_ctx *ctx, int frame, int tile_lo, int tile_hi, void *dev, int to_frame);
 
-/* Select batch slot 0 or 1 (default 0): stage_batch*, run_batch, batch_phases, run_phase
- * and stripe act on the current slot. Each slot holds its own staged batch (arena, plan,
- * launch graph) and runs on HIP streams of its own; the frame buffers are the context's.
- * Two staged batches that share no frame buffer run concurrently (one batch's device
- * planning and intra wavefront under the other's loop filter); a batch that reads or
- * writes a buffer of the other slot's batch follows that slot's last run. */
+/* Batch slots per context. */
+#define VP9HIP_MAX_SLOTS 4
+/* Select batch slot 0 .. VP9HIP_MAX_SLOTS - 1 (default 0): stage_batch*, run_batch,
+ * batch_phases, run_phase and stripe act on the current slot. Each slot holds its own
+ * staged batch (arena, plan, launch graph) and runs on HIP streams of its own (slots 2..
+ * create theirs at first selection); the frame buffers are the context's. Staged batches
+ * that share no frame buffer run concurrently (one batch's device planning and intra
+ * wavefront under another's loop filter); a batch that reads or writes a buffer of
+ * another slot's batch follows that slot's last run. */
 int  vp9hip_set_batch_slot(vp9hip_ctx *ctx, int slot);
-/* Wait for the last run of batch slot `slot` only (the other slot's work may continue)
+/* Wait for the last run of batch slot `slot` only (other slots' work may continue)
  * and check it as vp9hip_sync does (VP9HIP_EBUG: a loop-filter hand-off timed out). */
 int  vp9hip_sync_slot(vp9hip_ctx *ctx, int slot);
 /* Make HIP stream `stream` (a hipStream_t; NULL: the null stream) wait for the last run of
@@ -185,8 +188,8 @@ int  vp9hip_sync_slot(vp9hip_ctx *ctx, int slot);
 int  vp9hip_slot_stream_wait(vp9hip_ctx *ctx, int slot, void *stream);
 /* 1 while the last run of batch slot `slot` is still executing, 0 once it is done. */
 int  vp9hip_slot_busy(vp9hip_ctx *ctx, int slot);
-/* Wait for all queued work of both batch slots. VP9HIP_EBUG if a row-pipelined
- * loop-filter launch (k_lfr) of either slot gave up a bounded wait on another workgroup's
+/* Wait for all queued work of every batch slot. VP9HIP_EBUG if a row-pipelined
+ * loop-filter launch (k_lfr) of any slot gave up a bounded wait on another workgroup's
  * progress (frames not trusted). */
 int  vp9hip_sync(vp9hip_ctx *ctx);
 
@@ -209,7 +212,7 @@ int  vp9hip_frame_device(vp9hip_ctx *ctx, int buf, void *planes[3], ptrdiff_t li
 int  vp9hip_upload_frame(vp9hip_ctx *ctx, int buf, const uint8_t *const planes[3],
                          const ptrdiff_t linesize[3]);
 
-/* Drop queued work and the staged batches of both slots (FFHWAccel.flush). */
+/* Drop queued work and the staged batches of every slot (FFHWAccel.flush). */
 int  vp9hip_flush(vp9hip_ctx *ctx);
 /* Fill device buffers [buf0, buf0 + count) with the byte `value`, asynchronously on the
  * context's stream (the bench poisons its frame buffers before the timed steps, so the
@@ -240,6 +243,10 @@ int  vp9hip_alg_bytes(vp9hip_ctx *ctx, double *bytes, int cap);
  * the passes loop over (each pass: its largest job size). A 17th value (cap >= 17): intra
  * steps under the dependency-level schedule of inter frames (= the diagonals otherwise). */
 int  vp9hip_plan_stats(const vp9h_frame *pkt, double *out, int cap);
+/* Diagnostics: per SB of one packet (raster order) the pixel rows its intra passes loop
+ * over, as staged for the device (the wavefront-tail estimate of tools/wave_tail.py).
+ * Returns the SB count, or a negative AVERROR. */
+int  vp9hip_plan_sb_costs(const vp9h_frame *pkt, double *out, int cap);
 
 int  vp9hip_abi_version(void);
 /* PCI bus id ("0000:75:00.0") and name of HIP device `device` (so a multi-GPU run can show

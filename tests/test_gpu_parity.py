@@ -194,6 +194,58 @@ def test_two_slots_cross_batch_dependency(v9, orc, monkeypatch, slot_streams):
         dev.close()
 
 
+@pytest.mark.parametrize("slot_streams", [1, 0])
+def test_four_slots_chain_across_slots(v9, orc, monkeypatch, slot_streams):
+    """VP9HIP_MAX_SLOTS batch slots: one GOP continued from slot to slot (each slot's batch
+    reads the previous slot's last frame: dep_mask), plus an independent keyframe batch in
+    every slot; all four run back to back without a host wait, then slot 3 wraps around
+    onto slot 0's buffers (write-after-read across slots)."""
+    monkeypatch.setenv("VP9HIP_SLOT_STREAMS", str(slot_streams))
+    assert v9.Device.MAX_SLOTS == 4
+    w, h = 352, 288
+    key = v9.SynthFrame(v9.synth_params(w, h, 8, seed=930))
+    ps = [v9.SynthFrame(v9.synth_params(w, h, 8, seed=931 + i, inter=1, compound=i % 2)) for i in range(8)]
+    keys = [v9.SynthFrame(v9.synth_params(w, h, 8, seed=950 + i)) for i in range(4)]
+    dev = v9.Device(0)
+    try:
+        dev.configure(w, h, 8, nbufs=12)
+        # slot k: P frames into buffers 3k, 3k + 1 (chained from buffer 3k - 2), keyframe into 3k + 2
+        seq = []
+        for k in range(4):
+            dev.set_slot(k)
+            prev = 3 * k - 2 if k else None
+            fr = ([key] if k == 0 else [ps[2 * k - 1]]) + [ps[2 * k], keys[k]]
+            refs = [None if k == 0 else (prev, prev, prev), (3 * k, 3 * k, 3 * k), None]
+            dev.stage_batch(fr, [3 * k, 3 * k + 1, 3 * k + 2], refs)
+            seq += list(zip(fr, [3 * k, 3 * k + 1, 3 * k + 2], refs))
+        for k in range(4):
+            dev.set_slot(k)
+            dev.run_batch()
+        dev.sync()
+        ref = {}
+        for f, b, r in seq:
+            out = v9.alloc_planes(w, h, 8)
+            orc.decode_frame(f.pkt, out, None if r is None else [ref[r[0]], ref[r[1]], ref[r[2]]])
+            ref[b] = out
+            _cmp(v9, dev.download(b), out, w, h, "4 slots, slot streams %d, buffer %d" % (slot_streams, b))
+        # slot 3 again (reads 7, writes 9..11), then slot 0 re-staged into buffers 0..2 from 11
+        dev.set_slot(0)
+        dev.stage_batch([ps[7], keys[0]], [0, 1], [(11, 11, 11), None])
+        dev.set_slot(3)
+        dev.run_batch()
+        dev.set_slot(0)
+        dev.run_batch()
+        dev.sync()
+        out = v9.alloc_planes(w, h, 8)
+        orc.decode_frame(ps[7].pkt, out, [ref[11], ref[11], ref[11]])
+        _cmp(v9, dev.download(0), out, w, h, "4 slots, slot streams %d, wrap-around" % slot_streams)
+        _cmp(v9, dev.download(1), ref[2], w, h, "4 slots, slot streams %d, key rewrite" % slot_streams)
+        with pytest.raises(v9.Vp9HipError):
+            dev.set_slot(4)
+    finally:
+        dev.close()
+
+
 def test_static_plan_rejects_inconsistent_packets(v9, orc, gpu):
     """A packet the device planner rejects (an intra mode > 9) in a static-plan batch: the
     planner neutralises the batch on the device (k_pguard) and the next wait reports
