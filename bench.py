@@ -134,7 +134,7 @@ def main():
     ap.add_argument("--chroma", choices=sorted(CHROMA), default="420",
                     help="chroma format (profiles 1/3: 422, 440, 444); the BASELINE configs are 4:2:0")
     ap.add_argument("--inflight", type=int, default=2, choices=[1, 2, 3, 4],
-                    help="batches in flight: the context's two batch slots hold the same workload and "
+                    help="batches in flight: that many of the context's batch slots (VP9HIP_MAX_SLOTS) hold the same workload and "
                          "alternate steps; each slot runs on HIP streams of its own, so the two batches run "
                          "concurrently (as the decoder loop and the FFHWAccel adapter run them). Measured "
                          "with per-slot streams (profiles/r03g): C2 7,778 vs 4,485 fps at 1, C5 761 vs 593")
