@@ -348,7 +348,7 @@ template <int JCAP> struct PJobLds {
 };
 // k_plan's LDS: hgt overlays the unit map (read until the producers are listed, hgt is set
 // after that); the other scheduling fields follow it.
-template <int JCAP> struct PlanLds {
+template <int JCAP> struct alignas(16) PlanLds {   // 16: jmap rows are stored 16 bytes at a time
     uint32_t ja[JCAP];            // PJob word per intra job (decode order), bit 30: the 4x4
                                   // top-right lies inside the block (trx)
     union {
@@ -567,30 +567,64 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
         const uint32_t a = S.ja[j];
         const int p = a & 3, step = 1 << ((a >> 2) & 3), ux0 = (a >> 12) & 15, uy0 = (a >> 16) & 15;
         const int units = p ? CW : 16, unitsv = p ? CH : 16;
-        for (int v = uy0; v < uy0 + step && v < unitsv; v++)
-            for (int u = ux0; u < ux0 + step && u < units; u++) S.u.jmap[p][v * 16 + u] = (uint16_t) j;
+        if (ux0 + step <= units) {
+            // a job is an aligned square inside its plane's 16-unit rows, so each of its unit
+            // rows is one aligned 2 / 4 / 8 / 16-byte store: a 32x32 job paints 8 rows, not 64
+            // units (the loop's trip count is the largest job's of the chunk)
+            const uint32_t w = (uint32_t) j | (uint32_t) j << 16;
+            uint16_t *row = &S.u.jmap[p][uy0 * 16 + ux0];
+            for (int v = 0; v < step && uy0 + v < unitsv; v++, row += 16) {
+                if (step == 1) *row = (uint16_t) j;
+                else if (step == 2) *(uint32_t *) row = w;
+                else if (step == 4) *(uint2 *) row = make_uint2(w, w);
+                else *(uint4 *) row = make_uint4(w, w, w, w);
+            }
+        } else {
+            for (int v = uy0; v < uy0 + step && v < unitsv; v++)
+                for (int u = ux0; u < ux0 + step && u < units; u++) S.u.jmap[p][v * 16 + u] = (uint16_t) j;
+        }
     }
     wsync();
 
     // ---- producers of every intra job (the pixels its substituted mode reads)
+    // The units job j reads are pl_local_reads' runs: the top row (uy0 - 1, from ux0 - 1 with
+    // the top-left unit to ux0 + n + trx) and the left column (ux0 - 1, rows uy0 .. uy0 + n - 1).
+    // Jobs are aligned squares, so a run's units of one producer are consecutive: the walk
+    // jumps from a producer's unit past that producer's extent (one step per distinct
+    // producer instead of one per unit). Only the top-left unit's producer can recur in the
+    // left run. Units no intra job covers (0xffff) are stepped over one by one.
     auto deps_of = [&](int j, auto fn) {
         const uint32_t a = S.ja[j];
         const int p = a & 3, ts = (a >> 2) & 3, ux0 = (a >> 12) & 15, uy0 = (a >> 16) & 15;
-        const int units = p ? CW : 16, unitsv = p ? CH : 16;
-        int last = -1, first = -1;
-        // producers of a run of units are consecutive; only the top-left unit's producer can
-        // recur in the left-column run
-        const int nd = (int) needs_of(a);
-        bool left_run = false;
-        pl_local_reads(ux0, uy0, 1 << ts, nd, (a & JA_TRX) ? 1 : 0, units, unitsv, [&](int unit) {
-            const int d = S.u.jmap[p][unit];
-            const bool is_left = (unit & 15) == ux0 - 1 && (unit >> 4) >= uy0;
-            if (is_left && !left_run) { left_run = true; last = -1; }
-            if (d == 0xffff || d >= j || d == last || (left_run && d == first)) { if (d != 0xffff && d < j) last = d; return; }
-            if (!left_run && first < 0) first = d;
-            last = d;
-            fn(d);
-        });
+        const int units = p ? CW : 16, unitsv = p ? CH : 16, n4 = 1 << ts;
+        const int nd = (int) needs_of(a), trx = (a & JA_TRX) ? 1 : 0;
+        int tl = -1;                                       // producer of the top-left unit
+        if (uy0 > 0) {
+            const int u1 = pl_min((nd & 2) ? ux0 + n4 + trx : ux0, units);
+            int u = (nd & 4) ? ux0 - 1 : ux0;
+            if (u < 0) u = 0;
+            const uint16_t *row = S.u.jmap[p] + (uy0 - 1) * 16;
+            while (u < u1) {
+                const int d = row[u];
+                if (d == 0xffff) { u++; continue; }
+                const uint32_t ad = S.ja[d];
+                if (u == ux0 - 1) tl = d;
+                if (d < j) fn(d);
+                u = pl_max((int) ((ad >> 12) & 15) + (1 << ((ad >> 2) & 3)), u + 1);
+            }
+        }
+        if (ux0 > 0 && (nd & 1)) {
+            const int v1 = pl_min(uy0 + n4, unitsv);
+            int v = uy0;
+            const uint16_t *col = S.u.jmap[p] + ux0 - 1;
+            while (v < v1) {
+                const int d = col[v * 16];
+                if (d == 0xffff) { v++; continue; }
+                const uint32_t ad = S.ja[d];
+                if (d < j && d != tl) fn(d);
+                v = pl_max((int) ((ad >> 16) & 15) + (1 << ((ad >> 2) & 3)), v + 1);
+            }
+        }
     };
     {
         // one enumeration: job j's list starts at the prefix sum of the per-size bounds (an
