@@ -751,6 +751,7 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
             // lanes from the jobs skipped (any packing that respects the producers is exact;
             // only the pass count depends on it)
             for (int round = 0; round < 3 && budget >= 4; round++) {
+                if (round && !__any(cand)) break;     // round 1 took every ready job
                 const uint32_t incl = wscan_incl(cand ? sz : 0u, lane);
                 const bool take = cand && incl <= (uint32_t) budget;
                 const uint64_t m = __ballot(take);

@@ -1,9 +1,13 @@
-# Default bench (as the driver runs it) + the other BASELINE.md configs, 1 GPU.
-set -e
-mkdir -p gpurun_out
-timeout -k 10 400 python bench.py > gpurun_out/rb_default.json 2> gpurun_out/rb_default.err
-tail -1 gpurun_out/rb_default.json
+#!/bin/bash
+# End-of-round bench lines on 1 GPU: the default bench (as the driver runs it, every CPU / e2e /
+# hwaccel leg), then the other BASELINE.md configs. usage: tools/round_bench.sh TAG
+# (CFGS: configs after the default, default "C2 C4 C5")
+set -o pipefail
+O=gpurun_out/${1:-rb}; mkdir -p $O
+timeout -k 10 500 python bench.py > $O/bench_default_C3.json 2> $O/bench_default_C3.err || { tail -5 $O/bench_default_C3.err; exit 1; }
+echo "C3 $(python -c "import json;d=json.loads(open('$O/bench_default_C3.json').read().strip().split(chr(10))[-1]);print(d['value'], d['ms_per_step'], d['verified_frames'], d['roofline']['frac'])")"
 for c in ${CFGS:-C2 C4 C5}; do
-  timeout -k 10 400 python bench.py --config $c --steps 3 --warmup 1 --cpu-seconds 5 > gpurun_out/rb_$c.json 2> gpurun_out/rb_$c.err
-  echo "$c $(python -c "import json;d=json.loads(open('gpurun_out/rb_$c.json').read().strip().split(chr(10))[-1]);print(d['value'], d['ms_per_step'], d['roofline']['kernel_ms'], d['cpu_baseline']['value'] if d['cpu_baseline'] else None)")"
+  st=20; [ $c = C5 ] && st=6
+  timeout -k 10 600 python bench.py --config $c --steps $st --warmup 2 > $O/bench_$c.json 2> $O/bench_$c.err || { tail -5 $O/bench_$c.err; exit 1; }
+  echo "$c $(python -c "import json;d=json.loads(open('$O/bench_$c.json').read().strip().split(chr(10))[-1]);print(d['value'], d['ms_per_step'], d['verified_frames'], d['roofline']['frac'])")"
 done
