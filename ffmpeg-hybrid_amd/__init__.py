@@ -112,7 +112,7 @@ ABI_SYMBOLS = ["vp9hip_open", "vp9hip_close", "vp9hip_configure", "vp9hip_submit
                "vp9hip_stage_batch", "vp9hip_stage_batch_refs", "vp9hip_run_batch", "vp9hip_sync",
                "vp9hip_download_frame",
                "vp9hip_upload_frame", "vp9hip_flush", "vp9hip_last_timing", "vp9hip_set_timing",
-               "vp9hip_alg_bytes", "vp9hip_plan_stats", "vp9hip_abi_version", "vp9hip_set_graph",
+               "vp9hip_alg_bytes", "vp9hip_plan_stats", "vp9hip_plan_sb_costs", "vp9hip_abi_version", "vp9hip_set_graph",
                "vp9hip_stage_batch_tiles", "vp9hip_batch_phases", "vp9hip_phase_frames", "vp9hip_run_phase",
                "vp9hip_stripe", "vp9hip_frame_device", "vp9hip_batch_groups", "vp9hip_set_batch_slot", "vp9hip_sync_slot", "vp9hip_slot_busy",
                "vp9hip_fill_buffers", "vp9hip_device_info",
@@ -923,6 +923,15 @@ def webm_write(frames, width, height, timecode_scale=1000000, cluster_frames=8, 
 PLAN_STAT_NAMES = ("sbs", "passes", "pjobs", "rjobs", "jobs_4x4", "jobs_8x8", "jobs_16x16",
                    "jobs_32x32", "lane_use", "max_passes_sb", "lf_records", "mc_units", "pred_steps",
                    "lf_steps", "levels", "pass_rows", "level_steps", "asap_passes", "firstfit_passes", "firstfit_height_passes")
+
+
+def plan_sb_costs(frame):
+    """Per SB of one packet (raster order) the pixel rows its intra passes loop over, as staged
+    for the device (vp9hip_plan_sb_costs; host only, tools/wave_tail.py)."""
+    n = ((frame.pkt.width + 63) >> 6) * ((frame.pkt.height + 63) >> 6)
+    out = (ctypes.c_double * n)()
+    got = _check("vp9hip_plan_sb_costs", lib().vp9hip_plan_sb_costs(ctypes.byref(frame.pkt), out, n))
+    return np.array(out[:got])
 
 
 def plan_stats(frame):

@@ -119,6 +119,16 @@ def test_planner_stats_c3_frame(v9):
     assert st["lf_steps"] == 60 + 2 * 33
 
 
+def test_plan_sb_costs_sum_to_pass_rows(v9):
+    """vp9hip_plan_sb_costs (the wavefront-tail diagnostic): per-SB pass rows of a 4K
+    keyframe, every SB has intra work, and they sum to plan_stats' pass rows."""
+    f = v9.SynthFrame(v9.synth_params(3840, 2160, 8, seed=0x56503902, log2_tile_cols=2))
+    c = v9.plan_sb_costs(f)
+    assert c.shape == (60 * 34,)
+    assert (c >= 4).all()
+    assert c.sum() == v9.plan_stats(f)["pass_rows"]
+
+
 def test_planner_inter_level_schedule(v9):
     """Inter frames (no GPU): intra SBs are scheduled by dependency level. An SB waits only
     for the SBs whose intra pixels its intra blocks read, so a frame with ~10 % intra blocks

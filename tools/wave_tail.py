@@ -7,7 +7,6 @@ plus a fixed per-SB overhead C0 (tile loads + interior stores). For one frame gr
 - dataflow bound: each SB waits only for its left and top neighbours, so the group takes
   the longest path through any frame's tile DAG.
 usage: python tools/wave_tail.py [frames] [C0]"""
-import ctypes
 import importlib
 import os
 import sys
@@ -25,16 +24,13 @@ frames, _, _ = bench.make_frames(v, "C3", nf, 0, "420")
 W, H, tiles = 3840, 2160, 4
 sbc, sbr = 60, 34
 bounds = [(t * sbc // tiles, (t + 1) * sbc // tiles) for t in range(tiles)]   # SB columns per tile (approx.)
-out = (ctypes.c_double * (sbc * sbr))()
 ndiag = max(hi - lo for lo, hi in bounds) + sbr - 1
 dmax = np.zeros(ndiag)
 crit = 0.0
 tot = 0.0
 allc = []
 for f in frames:
-    n = v.lib().vp9hip_plan_sb_costs(ctypes.byref(f.pkt), out, sbc * sbr)
-    assert n == sbc * sbr, n
-    c = np.array(out[:n]).reshape(sbr, sbc) + c0
+    c = v.plan_sb_costs(f).reshape(sbr, sbc) + c0
     allc.append(c)
     tot += c.sum()
     for lo, hi in bounds:
