@@ -270,6 +270,12 @@ static bool slot_streams_make(vp9hip_ctx *c, int k)
     bool ok = hipStreamCreateWithPriority(&c->sst[k], hipStreamNonBlocking, c->pix_prio) == hipSuccess;
     for (int i = 0; ok && i < c->max_groups - 1; i++)
         ok = hipStreamCreateWithPriority(&c->sxst[k][i], hipStreamNonBlocking, c->pix_prio) == hipSuccess;
+    if (!ok) {                          // all or nothing: a later selection retries
+        for (int i = 0; i < MAX_GROUPS - 1; i++)
+            if (c->sxst[k][i]) { hipStreamDestroy(c->sxst[k][i]); c->sxst[k][i] = nullptr; }
+        if (c->sst[k]) hipStreamDestroy(c->sst[k]);
+        c->sst[k] = nullptr;
+    }
     return ok;
 }
 
