@@ -806,7 +806,13 @@ DEV void load_sb_tile(const FrameDesc &fd, int sbx, int sby, bool interior, int 
         if (cx - 1 + ci >= 0) v2 = gc[(size_t) (cy - 1) * pc + cx - 1 + ci];
         if (lane < 2) v5 = gv[(size_t) (cy - 1) * pc + cx + 30 + lane];
     }
-    if (left) {
+    if (left && fd.edge) {
+        // the left SB's right column as its intra workgroup saved it (FrameDesc.edge):
+        // two 64-pixel runs instead of 128 one-pixel frame rows
+        const PIX *e = (const PIX *) fd.edge + (size_t) (sby * fd.sb_cols + sbx - 1) * EDGE_PIX;
+        v1 = e[lane];
+        v3 = e[64 + lane];
+    } else if (left) {
         v1 = gy[(size_t) (ly + lane) * py + lx - 1];
         v3 = (lane < 32 ? gu : gv)[(size_t) (cy + (lane & 31)) * pc + cx - 1];
     }
@@ -1039,7 +1045,18 @@ DEV void pred_wg(const WGRec *wgp, const SBRec *__restrict__ sbs, const PJob *__
         const uint32_t sbi = __builtin_amdgcn_readfirstlane(wgp->sb[k]);
         if (sbi == 0xffffffffu) continue;
         const SBRec sb = sbs[sbi];
-        sb_interior<PIX, G, true>(frames[sb.frame], sb.sbx, sb.sby, lane, tile + k * G::TILE);
+        const FrameDesc &fd = frames[sb.frame];
+        sb_interior<PIX, G, true>(fd, sb.sbx, sb.sby, lane, tile + k * G::TILE);
+        if (fd.edge) {                 // the right column of each plane, for the SB to the right
+            PIX *e = (PIX *) fd.edge + (size_t) (sb.sby * fd.sb_cols + sb.sbx) * EDGE_PIX;
+            const PIX *t = tile + k * G::TILE;
+#pragma unroll
+            for (int i = lane; i < 64 + 2 * G::CH; i += 64) {
+                const int p = i < 64 ? 0 : i < 64 + G::CH ? 1 : 2, r = p == 0 ? i : p == 1 ? i - 64 : i - 64 - G::CH;
+                e[i] = t[(p == 0 ? 0 : p == 1 ? LT_SIZE : LT_SIZE + G::CT) + (r + 1) * (p ? G::CP : LP) + PX0 +
+                         (p ? G::CW : 64) - 1];
+            }
+        }
     }
     if (PRED_PROF && lane == 0) {
         pp[2] += clock64() - pp0;

@@ -138,6 +138,8 @@ struct Staged {
            o_coefs = 0, o_ctr = 0;
     int16_t *resid = nullptr;           // intra residual scratch (column-major n x n blocks)
     size_t resid_cap = 0;               // bytes
+    uint8_t *edge = nullptr;            // intra frames' SB right columns (FrameDesc.edge)
+    size_t edge_cap = 0;                // bytes
     bool ready = false;
     hipGraphExec_t graph = nullptr;     // captured launch sequence of this batch (timing off)
     std::vector<Launch> graph_launches; // the launch list the graph was captured from
@@ -369,6 +371,7 @@ extern "C" void vp9hip_close(vp9hip_ctx *c)
         Staged *g = &slot_ref(c, k);
         if (g->arena) hipFree(g->arena);
         if (g->resid) hipFree(g->resid);
+        if (g->edge) hipFree(g->edge);
         if (g->pinned) hipHostFree(g->pinned);
         if (g->graph) hipGraphExecDestroy(g->graph);
         if (g->summary_h) hipHostFree(g->summary_h);
@@ -1764,6 +1767,7 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     std::vector<FrameBuild> fbs(n);
     std::vector<size_t> coef_off(n + 1, 0);
     uint64_t coef_base = 0;
+    uint64_t edge_sbs = 0;                  // SBs of the batch's intra frames (FrameDesc.edge)
     for (int i = 0; i < n; i++) {
         const vp9h_frame *f = &pkts[i];
         // frames up to the configured size share the buffers (reference scaling, vp9.c:845-880)
@@ -1794,6 +1798,10 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
                 fd.refw[r][0] = f->ref_w[r]; fd.refh[r][0] = f->ref_h[r];
                 fd.refw[r][1] = (f->ref_w[r] + c->ss_h) >> c->ss_h; fd.refh[r][1] = (f->ref_h[r] + c->ss_v) >> c->ss_v;
             }
+        }
+        if (intra) {                    // FrameDesc.edge: an SB index for now, a pointer below
+            fd.edge = edge_sbs + 1;
+            edge_sbs += (uint64_t) fd.sb_cols * fd.sb_rows;
         }
         s.frames.push_back(fd);
         c->buf_wh[out_bufs[i]] = { f->width, f->height };
@@ -1839,6 +1847,22 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
         s.alg_bytes[K_RESID] += (double) f->ncoefs * csz;
         if (intra) s.alg_bytes[K_PRED] += pix_bytes;
         if (f->filter_level) s.alg_bytes[K_LF] += 2.0 * pix_bytes;
+    }
+    // the intra frames' SB right columns: written by each SB's intra workgroup, read by the
+    // SB to its right in place of a column of one-pixel frame rows (128 scattered lines)
+    {
+        const size_t eb = (size_t) edge_sbs * EDGE_PIX * c->bypp + 256;
+        const char *ee = getenv("VP9HIP_EDGE");      // read per staging (tests switch it)
+        const bool edge_off = ee && !atoi(ee);
+        if (edge_sbs && !edge_off && eb > s.edge_cap) {
+            if (s.edge) hipFree(s.edge);
+            s.edge = nullptr;
+            s.edge_cap = 0;
+            if (hipMalloc(&s.edge, eb) != hipSuccess) return VP9HIP_ENOMEM;
+            s.edge_cap = eb;
+        }
+        for (FrameDesc &fd : s.frames)
+            fd.edge = fd.edge && !edge_off ? (uint64_t) (s.edge + (size_t) (fd.edge - 1) * EDGE_PIX * c->bypp) : 0;
     }
 
     STAGE_T(0);

@@ -23,7 +23,12 @@ typedef struct FrameDesc {
     int32_t  sb_cols, sb_rows;
     int32_t  bd;              /* bit depth                                            */
     int32_t  sharp;           /* LF sharpness                                         */
+    uint64_t edge;            /* intra frames: per SB (raster) its pre-LF right column,
+                                 EDGE_PIX pixels (luma 64, then the chroma planes' rows),
+                                 written by its intra workgroup, read by the SB to its
+                                 right instead of 128 one-pixel frame rows; 0: none     */
 } FrameDesc;
+#define EDGE_PIX 192          /* pixels per SB in FrameDesc.edge (64 + 2 x 64 at 4:4:4) */
 
 /* Residual job (k_resid): one tx block with coefficients, 16 bytes. The residual
  * (out + (1 << (bits - 1))) >> bits of itxfm_add (vp9dsp_template.c:1139-1180) depends

@@ -2,7 +2,9 @@
 (VP9HIP_LFR_DB=0 instead of k_lfrd), 256-thread high-bit-depth MC (VP9HIP_MC64=0), one
 residual launch per transform size (VP9HIP_RESID_MULTI=0), and frame pipelining
 (VP9HIP_LFMC=1: the next chain position's MC units as waiting tickets of k_lfrd, alone and
-with the single-tile k_lfr, where they run as a k_mc launch after it). Each is switched (read
+with the single-tile k_lfr, where they run as a k_mc launch after it), and intra SBs reading
+their left neighbour's column from the frame rows instead of the saved SB edges
+(VP9HIP_EDGE=0, also on the C3 keyframe shape). Each is switched (read
 per launch / per staging) on a key + P chain of the C2 (1080p 8-bit) or C5 (8K 10-bit)
 shape, decoded through the bench's batch path and compared with the CPU oracle."""
 import os
@@ -25,6 +27,8 @@ CASES = [
     ({"VP9HIP_LFMC": "1"}, "C2", 6),
     ({"VP9HIP_LFMC": "1"}, "C5", 3),
     ({"VP9HIP_LFMC": "1", "VP9HIP_LFR_DB": "0"}, "C2", 4),
+    ({"VP9HIP_EDGE": "0"}, "C3", 3),
+    ({"VP9HIP_EDGE": "0"}, "C2", 3),
 ]
 
 
