@@ -255,8 +255,9 @@ def main():
         elif shape_note:
             traffic_src = shape_note
     # instruction issue of the same kernel from the committed SQ pass (profiles/<P>/pmc_summary.txt):
-    # VALU wave-instructions per launch / its mean duration there, vs the VALU issue peak
-    # (256 CUs x 4 SIMDs x 16 lanes: one wave64 instruction per 4 cycles per SIMD at 2.4 GHz)
+    # VALU wave-instructions per launch / its mean duration there, vs the VALU issue peak:
+    # 256 CUs x 4 SIMD-32s, each issuing one wave64 VALU instruction per 2 cycles at 2.4 GHz
+    # (MI355X_MICROARCH.md, Wave scheduling; = the 157.3 TF FP32 vector peak / 128 FLOP)
     issue = None
     pf = os.path.join(ROOT, "profiles", TRAFFIC_PROFILE, "pmc_summary.txt")
     if os.path.exists(pf) and shape_ok:
@@ -268,7 +269,7 @@ def main():
                 f = line.split()
                 vals[f[0]] = float(f[2].split("=")[1])
         if "SQ_INSTS_VALU" in vals and vals.get("duration_us"):
-            peak = 256 * 4 * 2.4e9 / 4
+            peak = 256 * 4 * 2.4e9 / 2
             rate = vals["SQ_INSTS_VALU"] / (vals["duration_us"] * 1e-6)
             issue = {"valu_instr_per_launch": vals["SQ_INSTS_VALU"], "salu_instr_per_launch": vals.get("SQ_INSTS_SALU"),
                      "duration_us": vals["duration_us"], "valu_frac": round(rate / peak, 4),

@@ -27,6 +27,20 @@
 #include "vp9_tables.h"
 #include "vp9hip_work.h"
 
+// The Makefile compiles this file once per KPART (0..5), each object holding a subset of
+// the launchers below and so of the kernel instantiations (parallel builds); without KPART
+// (profiling builds) one object holds everything.
+#ifdef KPART
+#define KP(n) (KPART == (n))
+#else
+#define KP(n) 1
+#endif
+#if !defined(KPART) || KPART == 0
+#define KP_DEV __device__
+#else
+#define KP_DEV static __device__
+#endif
+
 #define DEV __device__ __forceinline__
 
 // ------------------------------------------------------------------ helpers
@@ -969,7 +983,7 @@ DEV void load_ltab(uint32_t *ltab, const uint32_t *__restrict__ ptab, int lane)
 #ifndef PRED_PROF
 #define PRED_PROF 0
 #endif
-__device__ unsigned long long pred_prof[16];
+KP_DEV unsigned long long pred_prof[16];
 // Intra prediction of one workgroup record (the ltab copy must be loaded).
 template <typename PIX, class G>
 DEV void pred_wg(const WGRec *wgp, const SBRec *__restrict__ sbs, const PJob *__restrict__ jobs,
@@ -1558,7 +1572,7 @@ DEV void lfr_top(Chunk16::T (&v)[NU], const LfrPlanes &P, int sbx, int sby, int 
 #ifndef LFR_PROF
 #define LFR_PROF 0
 #endif
-__device__ unsigned long long lfr_prof[16];
+KP_DEV unsigned long long lfr_prof[16];
 #define LFR_T(i)                                                                                  \
     do {                                                                                          \
         if (LFR_PROF) { const uint64_t tn = clock64(); pacc[i] += tn - tp; tp = tn; }             \
@@ -2577,6 +2591,7 @@ static void launch_plf_p(int ss, hipStream_t st, const PlfLaunch &pl, const uint
     }
 }
 extern "C" {
+#if KP(0)
 // PRED_PROF builds: read and clear the intra workgroup phase sums (profiling only)
 int vp9hip_pred_prof_read(unsigned long long *out)
 {
@@ -2640,6 +2655,8 @@ int vp9hip_launch_resid_multi(int hb, hipStream_t st, const uint32_t *off, const
                            (const int16_t *) coefs, resid);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+#endif
+#if KP(1)
 // fmt: bit 0 high bit depth, bit 1 ss_h, bit 2 ss_v
 int vp9hip_launch_pred(int fmt, hipStream_t st, int nwg, const uint32_t *list, const WGRec *wgs, const SBRec *sbs,
                        const PJob *jobs, const uint32_t *passes, const FrameDesc *frames, const int16_t *resid,
@@ -2659,34 +2676,78 @@ int vp9hip_launch_lf(int fmt, hipStream_t st, int nsb, const uint32_t *list, con
     else         launch_lf_p<uint8_t>(fmt >> 1, st, nsb, list, recs, frames, dbg);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+#endif
+int vp9hip_launch_lfr_8(int ss, hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs, const FrameDesc *frames,
+                        uint32_t *ctr, const McUnit *mcu, int nmc, const uint32_t *mw);
+#if KP(2)
+int vp9hip_launch_lfr_8(int ss, hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs, const FrameDesc *frames,
+                        uint32_t *ctr, const McUnit *mcu, int nmc, const uint32_t *mw)
+{
+    launch_lfr_p<uint8_t>(ss, st, ntasks, tasks, recs, frames, ctr, mcu, nmc, mw);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+#endif
+int vp9hip_launch_lfr_16(int ss, hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs, const FrameDesc *frames,
+                        uint32_t *ctr, const McUnit *mcu, int nmc, const uint32_t *mw);
+#if KP(3)
+int vp9hip_launch_lfr_16(int ss, hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs, const FrameDesc *frames,
+                        uint32_t *ctr, const McUnit *mcu, int nmc, const uint32_t *mw)
+{
+    launch_lfr_p<uint16_t>(ss, st, ntasks, tasks, recs, frames, ctr, mcu, nmc, mw);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+#endif
+int vp9hip_launch_plf_8(int ss, hipStream_t st, const PlfLaunch *pl, const uint32_t *plist, const uint32_t *llist, const WGRec *wgs,
+                        const SBRec *sbs, const PJob *jobs, const uint32_t *passes, const LFRec *recs, const RJob *rjobs,
+                        const FrameDesc *frames, const void *coefs, int16_t *resid, const uint32_t *ptab, int dbg);
+#if KP(4)
+int vp9hip_launch_plf_8(int ss, hipStream_t st, const PlfLaunch *pl, const uint32_t *plist, const uint32_t *llist, const WGRec *wgs,
+                        const SBRec *sbs, const PJob *jobs, const uint32_t *passes, const LFRec *recs, const RJob *rjobs,
+                        const FrameDesc *frames, const void *coefs, int16_t *resid, const uint32_t *ptab, int dbg)
+{
+    launch_plf_p<uint8_t>(ss, st, *pl, plist, llist, wgs, sbs, jobs, passes, recs, rjobs, frames, coefs, resid, ptab, dbg);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+#endif
+int vp9hip_launch_plf_16(int ss, hipStream_t st, const PlfLaunch *pl, const uint32_t *plist, const uint32_t *llist, const WGRec *wgs,
+                        const SBRec *sbs, const PJob *jobs, const uint32_t *passes, const LFRec *recs, const RJob *rjobs,
+                        const FrameDesc *frames, const void *coefs, int16_t *resid, const uint32_t *ptab, int dbg);
+#if KP(5)
+int vp9hip_launch_plf_16(int ss, hipStream_t st, const PlfLaunch *pl, const uint32_t *plist, const uint32_t *llist, const WGRec *wgs,
+                        const SBRec *sbs, const PJob *jobs, const uint32_t *passes, const LFRec *recs, const RJob *rjobs,
+                        const FrameDesc *frames, const void *coefs, int16_t *resid, const uint32_t *ptab, int dbg)
+{
+    launch_plf_p<uint16_t>(ss, st, *pl, plist, llist, wgs, sbs, jobs, passes, recs, rjobs, frames, coefs, resid, ptab, dbg);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+#endif
+#if KP(0)
 int vp9hip_launch_lfr(int fmt, hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs,
                       const FrameDesc *frames, uint32_t *ctr, const McUnit *mcu, int nmc, const uint32_t *mw)
 {
     if (ntasks <= 0) return nmc > 0 ? -1 : 0;
     if (nmc < 0 || (nmc && (!mcu || !mw))) return -1;
-    if (fmt & 1) launch_lfr_p<uint16_t>(fmt >> 1, st, ntasks, tasks, recs, frames, ctr, mcu, nmc, mw);
-    else         launch_lfr_p<uint8_t>(fmt >> 1, st, ntasks, tasks, recs, frames, ctr, mcu, nmc, mw);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    return (fmt & 1 ? vp9hip_launch_lfr_16 : vp9hip_launch_lfr_8)(fmt >> 1, st, ntasks, tasks, recs, frames, ctr, mcu, nmc, mw);
 }
 int vp9hip_launch_plf(int fmt, hipStream_t st, const PlfLaunch *pl, const uint32_t *plist, const uint32_t *llist,
                       const WGRec *wgs, const SBRec *sbs, const PJob *jobs, const uint32_t *passes, const LFRec *recs,
                       const RJob *rjobs, const FrameDesc *frames, const void *coefs, int16_t *resid, const uint32_t *ptab,
                       int dbg)
 {
-    if (fmt & 1) launch_plf_p<uint16_t>(fmt >> 1, st, *pl, plist, llist, wgs, sbs, jobs, passes, recs, rjobs, frames, coefs, resid, ptab, dbg);
-    else         launch_plf_p<uint8_t>(fmt >> 1, st, *pl, plist, llist, wgs, sbs, jobs, passes, recs, rjobs, frames, coefs, resid, ptab, dbg);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    return (fmt & 1 ? vp9hip_launch_plf_16 : vp9hip_launch_plf_8)(fmt >> 1, st, pl, plist, llist, wgs, sbs, jobs, passes,
+                                                                  recs, rjobs, frames, coefs, resid, ptab, dbg);
 }
 int vp9hip_launch_mc(int hb, hipStream_t st, int n, const McUnit *units, const FrameDesc *frames)
 {
     if (n <= 0) return 0;
     // high bit depth: one wave per unit (the per-pixel sampler keeps every lane of a small
     // unit busy; VP9HIP_MC64=0: 256 threads, as 8-bit, whose LDS passes need them)
-    const char *e = getenv("VP9HIP_MC64");
+    const char *e = getenv("VP9HIP_MC64");              // read per launch (tests switch it)
     const bool mc64 = !e || atoi(e);
     if (hb && mc64) hipLaunchKernelGGL((k_mc<uint16_t, 64>), dim3(n), dim3(64), 0, st, units, n, frames);
     else if (hb)    hipLaunchKernelGGL((k_mc<uint16_t, 256>), dim3(n), dim3(256), 0, st, units, n, frames);
     else            hipLaunchKernelGGL((k_mc<uint8_t, 256>), dim3(n), dim3(256), 0, st, units, n, frames);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+#endif
 }
