@@ -28,6 +28,7 @@
 #include <cstring>
 #include <deque>
 #include <memory>
+#include <utility>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -63,7 +64,7 @@ struct vp9hip_decoder {
     uint64_t launched = 0;                 // batches launched; batch b ran in slot (b - 1) & 1
     uint64_t slot_seq[2] = { 0, 0 };       // the batch last launched in each slot
     bool slot_checked[2] = { true, true };
-    std::vector<uint64_t> bad;             // batches whose check failed (VP9HIP_EBUG)
+    std::vector<std::pair<uint64_t, int>> bad;   // batches whose check failed, + error
     std::vector<Pending> batch;
     std::deque<Out> outq;
     // parse pipeline
@@ -115,16 +116,19 @@ static int check_slot(vp9hip_decoder *d, int s)
 {
     if (d->slot_checked[s]) return 0;
     const int r = vp9hip_sync_slot(d->ctx, s);
-    if (r == VP9HIP_EBUG) d->bad.push_back(d->slot_seq[s]);
+    // a batch that failed on the device (loop-filter hand-off: VP9HIP_EBUG; planner
+    // rejection: AVERROR_INVALIDDATA) fails its own frames only
+    if (r == VP9HIP_EBUG || r == VP9HIP_EINVALIDDATA) d->bad.push_back(std::make_pair(d->slot_seq[s], r));
     else if (r < 0) return r;
     d->slot_checked[s] = true;
     return 0;
 }
 
-static bool batch_bad(const vp9hip_decoder *d, uint64_t seq)
+// 0, or the error of a launched batch that failed its check
+static int batch_bad(const vp9hip_decoder *d, uint64_t seq)
 {
-    for (uint64_t b : d->bad) if (b == seq) return true;
-    return false;
+    for (const auto &b : d->bad) if (b.first == seq) return b.second;
+    return 0;
 }
 
 static int submit(vp9hip_decoder *d)
@@ -367,9 +371,9 @@ extern "C" int vp9hip_decoder_receive_frame(vp9hip_decoder *d, vp9hip_decoded_fr
         }
     }
     d->outq.pop_front();
-    if (batch_bad(d, d->buf_seq[o.buf])) {     // the loop filter's row hand-off broke
+    if (const int e = batch_bad(d, d->buf_seq[o.buf])) {   // the batch failed on the device
         d->pins[o.buf]--;
-        return VP9HIP_EBUG;
+        return e;
     }
     memset(out, 0, sizeof(*out));
     out->buf = o.buf;

@@ -38,6 +38,8 @@
 #include <cstring>
 #include <deque>
 #include <memory>
+#include <mutex>
+#include <utility>
 #include <vector>
 
 #include "../../include/vp9hip_hwaccel.h"
@@ -77,7 +79,10 @@ struct vp9hip_hwaccel {
     std::unique_ptr<ParsePool> pool;
     std::shared_ptr<Chain> chain;           // the parse chain of the next non-key frame
     int slot[8];                            // device buffer of each reference slot (s->s.ref_frames)
-    std::vector<int> refs;                  // per pool buffer: frame references handed out
+    std::vector<int> refs;                  // per pool buffer: frame references handed out (under rmu:
+                                            // vp9hip_hwframe_ref / unref may come from any thread,
+                                            // as av_frame_unref of an output frame does)
+    mutable std::mutex rmu;
     std::vector<int> pend;                  // per pool buffer: in the batch being filled
     std::vector<int> inref;                 // per pool buffer: read by frames of that batch
     std::vector<uint64_t> buf_seq;          // per pool buffer: the batch that last wrote it
@@ -92,7 +97,7 @@ struct vp9hip_hwaccel {
     uint64_t launched = 0;                  // batches launched; batch b ran in slot (b - 1) & 1
     uint64_t slot_seq[2] = { 0, 0 };
     bool slot_checked[2] = { true, true };
-    std::vector<uint64_t> bad;              // launched batches that failed their check
+    std::vector<std::pair<uint64_t, int>> bad;   // launched batches that failed their check, + error
     size_t max_full = 1;                    // filled batches that may wait for their parses
     Trace tr;
 };
@@ -107,8 +112,11 @@ extern "C" int vp9hip_hwaccel_frame_params(int width, int height, int bpp, int s
                                            vp9hip_frames_params *out)
 {
     if (!out || width <= 0 || height <= 0 || (bpp != 8 && bpp != 10 && bpp != 12) || ss_h < 0 || ss_h > 1 ||
-        ss_v < 0 || ss_v > 1 || extra < 0)
+        ss_v < 0 || ss_v > 1)
         return VP9HIP_EINVAL;
+    // FFmpeg's extra_hw_frames defaults to -1 (options_table.h:397; decode.c:1135 adds it
+    // only when > 0): a negative count asks for no extra frames
+    if (extra < 0) extra = 0;
     memset(out, 0, sizeof(*out));
     out->sw_format = swfmt(bpp, ss_h, ss_v);
     out->width = width;
@@ -169,16 +177,19 @@ static int check_slot(vp9hip_hwaccel *h, int s)
 {
     if (h->slot_checked[s]) return 0;
     const int r = vp9hip_sync_slot(h->gpu, s);
-    if (r == VP9HIP_EBUG) h->bad.push_back(h->slot_seq[s]);
+    // a batch that failed on the device (loop-filter hand-off: VP9HIP_EBUG; planner
+    // rejection: AVERROR_INVALIDDATA) fails its own frames only
+    if (r == VP9HIP_EBUG || r == VP9HIP_EINVALIDDATA) h->bad.push_back(std::make_pair(h->slot_seq[s], r));
     else if (r < 0) return r;
     h->slot_checked[s] = true;
     return 0;
 }
 
-static bool batch_bad(const vp9hip_hwaccel *h, uint64_t seq)
+// 0, or the error of a launched batch that failed its check
+static int batch_bad(const vp9hip_hwaccel *h, uint64_t seq)
 {
-    for (uint64_t b : h->bad) if (b == seq) return true;
-    return false;
+    for (const auto &b : h->bad) if (b.first == seq) return b.second;
+    return 0;
 }
 
 // Stage + launch one batch in the next batch slot. Its packets are parsed by now or soon:
@@ -274,10 +285,16 @@ static int pump(vp9hip_hwaccel *h)
     return err;
 }
 
+static int nrefs(const vp9hip_hwaccel *h, int b)
+{
+    std::lock_guard<std::mutex> g(h->rmu);
+    return h->refs[b];
+}
+
 static bool buf_busy(const vp9hip_hwaccel *h, int b)
 {
     // a buffer a batched frame reads is not rewritten by a later frame of the same batch
-    if (h->refs[b] || h->pend[b] || h->inref[b] || b == h->cur) return true;
+    if (nrefs(h, b) || h->pend[b] || h->inref[b] || b == h->cur) return true;
     for (int s = 0; s < 8; s++)
         if (h->slot[s] == b) return true;
     return false;
@@ -354,6 +371,7 @@ static void fill_frame(vp9hip_hwaccel *h, int b, int64_t pts, vp9hip_hwframe *ou
     out->sw_format = h->fp.sw_format;
     out->buf = b;
     out->pts = pts;
+    std::lock_guard<std::mutex> g(h->rmu);
     h->refs[b]++;
 }
 
@@ -417,7 +435,7 @@ static int launch_for(vp9hip_hwaccel *h, int b)
 
 extern "C" int vp9hip_hwframe_sync(vp9hip_hwaccel *h, const vp9hip_hwframe *f)
 {
-    if (!h || !f || f->buf < 0 || f->buf >= h->fp.initial_pool_size || !h->refs[f->buf]) return VP9HIP_EINVAL;
+    if (!h || !f || f->buf < 0 || f->buf >= h->fp.initial_pool_size || !nrefs(h, f->buf)) return VP9HIP_EINVAL;
     int r = launch_for(h, f->buf);
     if (r < 0) return r;
     const uint64_t b = h->buf_seq[f->buf];
@@ -427,16 +445,16 @@ extern "C" int vp9hip_hwframe_sync(vp9hip_hwaccel *h, const vp9hip_hwframe *f)
     if (h->slot_seq[s] == b && (r = check_slot(h, s)) < 0) return r;
     h->tr.stop(T_SYNC_WAIT);
     // an older batch of the slot was drained and checked before its slot was reused
-    return batch_bad(h, b) ? VP9HIP_EBUG : 0;
+    return batch_bad(h, b);
 }
 
 extern "C" int vp9hip_hwframe_ready(vp9hip_hwaccel *h, const vp9hip_hwframe *f, void *stream)
 {
-    if (!h || !f || f->buf < 0 || f->buf >= h->fp.initial_pool_size || !h->refs[f->buf]) return VP9HIP_EINVAL;
+    if (!h || !f || f->buf < 0 || f->buf >= h->fp.initial_pool_size || !nrefs(h, f->buf)) return VP9HIP_EINVAL;
     int r = launch_for(h, f->buf);
     if (r < 0) return r;
     const uint64_t b = h->buf_seq[f->buf];
-    if (batch_bad(h, b)) return VP9HIP_EBUG;
+    if ((r = batch_bad(h, b)) < 0) return r;
     if (!b) return 0;
     const int s = (int) ((b - 1) & 1);
     // the slot's last run is this batch or a later one (which follows it on the context's
@@ -499,8 +517,12 @@ extern "C" int vp9hip_hwframe_transfer(vp9hip_hwaccel *h, const vp9hip_hwframe *
 
 extern "C" int vp9hip_hwframe_unref(vp9hip_hwaccel *h, vp9hip_hwframe *f)
 {
-    if (!h || !f || f->buf < 0 || f->buf >= h->fp.initial_pool_size || h->refs[f->buf] <= 0) return VP9HIP_EINVAL;
-    h->refs[f->buf]--;
+    if (!h || !f || f->buf < 0 || f->buf >= h->fp.initial_pool_size) return VP9HIP_EINVAL;
+    {
+        std::lock_guard<std::mutex> g(h->rmu);
+        if (h->refs[f->buf] <= 0) return VP9HIP_EINVAL;
+        h->refs[f->buf]--;
+    }
     memset(f, 0, sizeof(*f));
     f->buf = -1;
     return 0;
@@ -508,8 +530,9 @@ extern "C" int vp9hip_hwframe_unref(vp9hip_hwaccel *h, vp9hip_hwframe *f)
 
 extern "C" int vp9hip_hwframe_ref(vp9hip_hwaccel *h, const vp9hip_hwframe *src, vp9hip_hwframe *dst)
 {
-    if (!h || !src || !dst || src->buf < 0 || src->buf >= h->fp.initial_pool_size || h->refs[src->buf] <= 0)
-        return VP9HIP_EINVAL;
+    if (!h || !src || !dst || src->buf < 0 || src->buf >= h->fp.initial_pool_size) return VP9HIP_EINVAL;
+    std::lock_guard<std::mutex> g(h->rmu);
+    if (h->refs[src->buf] <= 0) return VP9HIP_EINVAL;
     *dst = *src;
     h->refs[src->buf]++;
     return 0;

@@ -189,6 +189,8 @@ struct Staged {
     bool stat = false;
     hipEvent_t plan_ev = nullptr;
     bool summary_pending = false;
+    int status = 0;                     // sticky until the slot is restaged: the planner rejected
+                                        // the batch (AVERROR_INVALIDDATA; k_pguard neutralised it)
     std::vector<uint32_t> exp_ko;       // key offsets the launch list was built with
     std::vector<uint32_t> stat_lists;   // the intra step lists (uploaded with the batch)
     std::vector<int> wr, rd;            // frame buffers the batch writes / reads (sorted)
@@ -230,6 +232,7 @@ struct vp9hip_ctx {
     Staged sl[MAX_SLOTS];               // the other slots (sl[slot] is a moved-out placeholder;
                                         // vp9hip_set_batch_slot swaps a slot in and out)
     int slot = 0;
+    int nstat_staged = 0;               // static-plan batches staged (VP9HIP_TEST_REJECT)
     hipStream_t pst = nullptr;          // device planner stream: a slot's planning overlaps the
                                         // other slot's pixel kernels (VP9HIP_SLOT_STREAMS=0 only)
     // Per-slot streams (default): each batch slot has its own main and group streams, swapped
@@ -241,6 +244,13 @@ struct vp9hip_ctx {
     bool slot_streams = true;
     int pix_prio = 0;
     hipStream_t sst[MAX_SLOTS] = {}, sxst[MAX_SLOTS][MAX_GROUPS - 1] = {};   // per slot: main, groups
+    // downloads (vp9hip_download_frame): a stream of their own (the slot streams may hold
+    // newer batches) and a pinned staging ring of DL_RING chunks, host copies overlapped
+    // with the next chunk's D2H
+    hipStream_t dst_dl = nullptr;
+    uint8_t *dl_pin = nullptr;
+    hipEvent_t dl_ev[4] = {};
+    hipEvent_t fill_ev = nullptr;       // after vp9hip_fill_buffers' memsets
     // timing of the last run
     bool timing = true;
     std::vector<hipEvent_t> ev;
@@ -381,6 +391,10 @@ extern "C" void vp9hip_close(vp9hip_ctx *c)
     }
     if (c->ptab) hipFree(c->ptab);
     if (c->nz) hipFree(c->nz);
+    if (c->dl_pin) hipHostFree(c->dl_pin);
+    if (c->dst_dl) hipStreamDestroy(c->dst_dl);
+    for (auto e : c->dl_ev) if (e) hipEventDestroy(e);
+    if (c->fill_ev) hipEventDestroy(c->fill_ev);
     if (c->plan_prof) hipFree(c->plan_prof);
     if (c->pst) hipStreamDestroy(c->pst);
     for (auto e : c->pev) if (e) hipEventDestroy(e);
@@ -1391,6 +1405,12 @@ static int stage_dev(vp9hip_ctx *c, const DevIn &in)
         worker();
         for (auto &t : pool) t.join();
     }
+    if (s.stat) {   // test hook (VP9HIP_TEST_REJECT=k): the k-th static-plan batch of the context
+        // gets an intra mode the device planner rejects in its first frame's first block, so
+        // the adapters' handling of a rejected batch can be tested from real bitstreams
+        const char *e = getenv("VP9HIP_TEST_REJECT");
+        if (++c->nstat_staged == (e ? atoi(e) : 0) && nb) ((vp9h_block *) (img + s.o_blocks))->mode[0] = 20;
+    }
     // the upload goes on the planner stream: the other batch slot's pixel kernels keep the
     // main stream busy meanwhile
     const hipStream_t us = plan_stream(c);
@@ -1409,19 +1429,22 @@ static int stage_dev(vp9hip_ctx *c, const DevIn &in)
 }
 
 // A static-plan batch's summary, once its run is complete (the caller waited for it):
-// planner status (AVERROR_INVALIDDATA: the batch was neutralised by k_pguard), the step-list
-// offsets checked against the ones the launch list was built with (VP9HIP_EBUG: they
-// differ), and the algorithmic byte totals.
+// planner status (AVERROR_INVALIDDATA: the batch was neutralised by k_pguard; kept in
+// s.status and returned by every later check until the slot is restaged) and the
+// algorithmic byte totals. Consistency of the step lists with the staged launch list rests
+// on k_plan's PLS_SCHED check (with static lists k_plan does not count keys, so the summary's
+// key offsets are only used to locate the byte totals).
 static int finish_summary(vp9hip_ctx *c, Staged &s)
 {
-    if (!s.stat || !s.summary_pending) return 0;
+    if (!s.stat || !s.summary_pending) return s.status;
     s.summary_pending = false;
     HIPCHK(hipMemcpy(s.summary_h, s.arena + s.o_summary, s.summary_words * 4, hipMemcpyDeviceToHost));
     const uint32_t *sm = s.summary_h;
     if (sm[0]) {
         fprintf(stderr, "vp9hip: batch rejected by the device planner (status 0x%x, bounds 0x%x)\n", sm[0],
                 sm[s.summary_words - 1]);
-        return VP9HIP_EINVALIDDATA;
+        s.status = VP9HIP_EINVALIDDATA;
+        return s.status;
     }
     const uint32_t *ko = sm + 1 + s.n_gidx, *fb32 = ko + s.nkey + 1;
     for (int k = 0; k < K_N; k++) s.alg_bytes[k] = s.alg_stat[k];
@@ -1707,6 +1730,7 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     s.tile_lo = tile_lo; s.tile_hi = tile_hi;
     s.stat = false;
     s.summary_pending = false;
+    s.status = 0;
     for (int k = 0; k < K_N; k++) s.alg_bytes[k] = 0;
     s.ready = false;
 
@@ -2572,11 +2596,15 @@ extern "C" int vp9hip_sync(vp9hip_ctx *c)
     if (!c) return VP9HIP_EINVAL;
     hipSetDevice(c->dev);
     HIPCHK(sync_all(c));
-    // every slot's work is complete: their hand-off counters and summaries are final
-    for (int k = 0; k < MAX_SLOTS; k++)
-        if (const int r = finish_summary(c, slot_ref(c, k))) return r;
-    for (int k = 0; k < MAX_SLOTS; k++)
-        if (const int r = check_lfr(slot_ref(c, k))) return r;
+    // every slot's work is complete: their hand-off counters and summaries are final; every
+    // slot is checked (each summary read once), the first error returned
+    int err = 0;
+    for (int k = 0; k < MAX_SLOTS; k++) {
+        int r = finish_summary(c, slot_ref(c, k));
+        if (!r) r = check_lfr(slot_ref(c, k));
+        if (r && !err) err = r;
+    }
+    if (err) return err;
     if (c->timing && c->timed_run && c->stg.ready) {
         for (int k = 0; k < K_N; k++) { c->kms[k] = 0; c->kcount[k] = 0; }
         for (size_t i = 0; i < c->stg.launches.size() && 2 * i + 1 < c->ev.size(); i++) {
@@ -2602,19 +2630,66 @@ extern "C" int vp9hip_submit_frame(vp9hip_ctx *c, const vp9h_frame *pkt, int out
     return vp9hip_run_batch(c);
 }
 
+// Wait for the batches that write buffer `buf`: the slots whose staged batch has it in its
+// write set (a slot's older batches were complete when it was restaged: stage() waits for
+// them), not the whole context, whose streams may already hold newer batches.
+static int wait_writers(vp9hip_ctx *c, int buf)
+{
+    for (int k = 0; k < MAX_SLOTS; k++) {
+        const Staged &g = slot_ref(c, k);
+        if (g.done_ev && std::binary_search(g.wr.begin(), g.wr.end(), buf))
+            HIPCHK(hipEventSynchronize(g.done_ev));
+    }
+    return 0;
+}
+
+#define DL_CHUNK ((size_t) 8 << 20)     // bytes per staging chunk
+#define DL_RING 4
+
 extern "C" int vp9hip_download_frame(vp9hip_ctx *c, int buf, uint8_t *const planes[3], const ptrdiff_t linesize[3])
 {
     if (!c || buf < 0 || buf >= (int) c->bufs.size() || !planes) return VP9HIP_EINVAL;
     hipSetDevice(c->dev);
-    HIPCHK(sync_all(c));                 // either slot may have written the buffer
+    if (const int r = wait_writers(c, buf)) return r;
+    if (!c->dst_dl) HIPCHK(hipStreamCreateWithFlags(&c->dst_dl, hipStreamNonBlocking));
+    if (!c->dl_pin) HIPCHK(hipHostMalloc((void **) &c->dl_pin, DL_CHUNK * DL_RING, hipHostMallocDefault));
+    for (auto &e : c->dl_ev)
+        if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    // chunks of whole rows: D2H into ring slot k, then (once the slot after it is queued)
+    // the host copy of slot k into the caller's planes
+    struct Piece { int p, y0, ny; };
+    std::vector<Piece> pieces;
+    const int bw = c->buf_wh[buf].first, bh = c->buf_wh[buf].second;
     for (int p = 0; p < 3; p++) {
-        const int bw = c->buf_wh[buf].first, bh = c->buf_wh[buf].second;
-        int pw = p ? (bw + c->ss_h) >> c->ss_h : bw, ph = p ? (bh + c->ss_v) >> c->ss_v : bh;
-        HIPCHK(hipMemcpy2DAsync(planes[p], linesize[p], c->bufs[buf] + c->plane_off[p],
-                                (size_t) c->pitch[p ? 1 : 0] * c->bypp, (size_t) pw * c->bypp, ph,
-                                hipMemcpyDeviceToHost, c->st));
+        const int pw = p ? (bw + c->ss_h) >> c->ss_h : bw, ph = p ? (bh + c->ss_v) >> c->ss_v : bh;
+        const size_t row = (size_t) pw * c->bypp;
+        const int per = (int) std::max<size_t>(1, DL_CHUNK / row);
+        for (int y = 0; y < ph; y += per) pieces.push_back({ p, y, std::min(per, ph - y) });
     }
-    HIPCHK(hipStreamSynchronize(c->st));
+    auto row_bytes = [&](int p) { return (size_t) (p ? (bw + c->ss_h) >> c->ss_h : bw) * c->bypp; };
+    auto issue = [&](size_t i) -> int {
+        const Piece &q = pieces[i];
+        const size_t row = row_bytes(q.p), pitch = (size_t) c->pitch[q.p ? 1 : 0] * c->bypp;
+        HIPCHK(hipMemcpy2DAsync(c->dl_pin + (i % DL_RING) * DL_CHUNK, row,
+                                c->bufs[buf] + c->plane_off[q.p] + (size_t) q.y0 * pitch, pitch, row, q.ny,
+                                hipMemcpyDeviceToHost, c->dst_dl));
+        HIPCHK(hipEventRecord(c->dl_ev[i % DL_RING], c->dst_dl));
+        return 0;
+    };
+    for (size_t i = 0; i < pieces.size() && i < DL_RING; i++)
+        if (const int r = issue(i)) return r;
+    for (size_t i = 0; i < pieces.size(); i++) {
+        const Piece &q = pieces[i];
+        HIPCHK(hipEventSynchronize(c->dl_ev[i % DL_RING]));
+        const size_t row = row_bytes(q.p);
+        const uint8_t *src = c->dl_pin + (i % DL_RING) * DL_CHUNK;
+        uint8_t *dst = planes[q.p] + (ptrdiff_t) q.y0 * linesize[q.p];
+        if ((size_t) linesize[q.p] == row) memcpy(dst, src, row * q.ny);
+        else
+            for (int y = 0; y < q.ny; y++) memcpy(dst + (ptrdiff_t) y * linesize[q.p], src + (size_t) y * row, row);
+        if (i + DL_RING < pieces.size())
+            if (const int r = issue(i + DL_RING)) return r;
+    }
     return 0;
 }
 
@@ -2668,6 +2743,12 @@ extern "C" int vp9hip_fill_buffers(vp9hip_ctx *c, int buf0, int count, int value
     hipSetDevice(c->dev);
     HIPCHK(sync_all(c));                 // neither slot's work may still read the buffers
     for (int i = buf0; i < buf0 + count; i++) HIPCHK(hipMemsetAsync(c->bufs[i], value & 255, c->buf_bytes, c->st));
+    // every slot's later work (whichever stream it runs on) follows the fill
+    if (!c->fill_ev) HIPCHK(hipEventCreateWithFlags(&c->fill_ev, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(c->fill_ev, c->st));
+    for (int k = 0; k < MAX_SLOTS; k++)
+        if (c->sst[k] && c->sst[k] != c->st) HIPCHK(hipStreamWaitEvent(c->sst[k], c->fill_ev, 0));
+    if (c->pst) HIPCHK(hipStreamWaitEvent(c->pst, c->fill_ev, 0));
     return 0;
 }
 

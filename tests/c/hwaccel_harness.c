@@ -23,7 +23,11 @@
  * its pixels on the GPU (vp9hip_hwframe_sync), as a consumer of device frames does.
  * Prints "frames N seconds S" (wall time of the decode loop, init / uninit excluded).
  *
- * usage: hwaccel_harness IN.ivf OUT.yuv|- BPP SS_H SS_V [PASSES [LAG [MODE [ASYNC_DEPTH]]]]
+ * EXTRA (default 2 + LAG) is the frame count the FFmpeg glue hands frame_params
+ * (integration/vp9_hip.c: max(0, extra_hw_frames) + frame threads); -1 plays a glue that passes
+ * FFmpeg's default extra_hw_frames (-1, options_table.h:397) through unclamped.
+ *
+ * usage: hwaccel_harness IN.ivf OUT.yuv|- BPP SS_H SS_V [PASSES [LAG [MODE [ASYNC_DEPTH [EXTRA]]]]]
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -116,13 +120,14 @@ static int drain(Consumer *c)
 int main(int argc, char **argv)
 {
     if (argc < 6) {
-        fprintf(stderr, "usage: %s IN.ivf OUT.yuv|- BPP SS_H SS_V [PASSES [LAG [MODE [ASYNC_DEPTH]]]]\n", argv[0]);
+        fprintf(stderr, "usage: %s IN.ivf OUT.yuv|- BPP SS_H SS_V [PASSES [LAG [MODE [ASYNC_DEPTH [EXTRA]]]]]\n", argv[0]);
         return 2;
     }
     const int bpp = atoi(argv[3]), ssh = atoi(argv[4]), ssv = atoi(argv[5]), passes = argc > 6 ? atoi(argv[6]) : 2;
     const int lag = argc > 7 ? atoi(argv[7]) : 0;
     const int download = argc > 8 ? strcmp(argv[8], "device") != 0 : 1;
     const int depth = argc > 9 ? atoi(argv[9]) : 0;
+    const int extra = argc > 10 ? atoi(argv[10]) : 2 + lag;
     FILE *fi = fopen(argv[1], "rb");
     if (!fi) { perror(argv[1]); return 2; }
     fseek(fi, 0, SEEK_END);
@@ -140,7 +145,7 @@ int main(int argc, char **argv)
     /* get_format: frame_params (+ the options the glue maps onto it) then init */
     vp9hip_frames_params fp;
     vp9hip_hwaccel *h = NULL;
-    if ((r = vp9hip_hwaccel_frame_params(ih.width, ih.height, bpp, ssh, ssv, 2 + lag, &fp)) < 0) {
+    if ((r = vp9hip_hwaccel_frame_params(ih.width, ih.height, bpp, ssh, ssv, extra, &fp)) < 0) {
         fprintf(stderr, "frame_params: %d\n", r);
         return 1;
     }

@@ -49,6 +49,10 @@ def test_frame_params(v9):
     assert L.vp9hip_hwaccel_frame_params(1920, 1080, 8, 1, 1, 64, ctypes.byref(fp)) == 0 and fp.async_depth == 16
     assert L.vp9hip_hwaccel_frame_params(64, 64, 8, 0, 0, 0, ctypes.byref(fp)) == 0 and fp.sw_format == 3
     assert L.vp9hip_hwaccel_frame_params(64, 64, 9, 1, 1, 0, ctypes.byref(fp)) == v9.EINVAL
+    # FFmpeg's default extra_hw_frames is -1 (options_table.h:397; decode.c:1135 adds it only
+    # when > 0): a glue that passes it through unclamped gets the no-extra parameters
+    assert L.vp9hip_hwaccel_frame_params(1920, 1080, 8, 1, 1, -1, ctypes.byref(fp)) == 0
+    assert fp.async_depth == 1 and fp.initial_pool_size == 8 + 1 + (1 + 4) * 1
 
 
 def _read_frames(path, w, h, bpp, ssh, ssv):
@@ -64,10 +68,13 @@ def _read_frames(path, w, h, bpp, ssh, ssv):
     return out
 
 
-def run_harness(ivf, out, bpp, ssh, ssv, passes=2, lag=0, mode="download", depth=0, env=None, timeout=120):
-    """The harness binary; returns (returncode, frames, seconds, stderr)."""
-    r = subprocess.run([HARNESS, str(ivf), str(out), str(bpp), str(ssh), str(ssv), str(passes), str(lag), mode,
-                        str(depth)], capture_output=True, text=True, timeout=timeout, env=env)
+def run_harness(ivf, out, bpp, ssh, ssv, passes=2, lag=0, mode="download", depth=0, env=None, timeout=120, extra=None):
+    """The harness binary; returns (returncode, frames, seconds, stderr). extra: the frame
+    count handed to frame_params (default 2 + lag)."""
+    args = [HARNESS, str(ivf), str(out), str(bpp), str(ssh), str(ssv), str(passes), str(lag), mode, str(depth)]
+    if extra is not None:
+        args.append(str(extra))
+    r = subprocess.run(args, capture_output=True, text=True, timeout=timeout, env=env)
     f = r.stdout.split()
     if r.returncode or len(f) < 4:
         return r.returncode, None, None, r.stderr
@@ -96,6 +103,27 @@ def test_hwaccel_call_order_matches_oracle(v9, orc, tmp_path, w, h, bpp, ssh, ss
     for i, (g, o) in enumerate(zip(got, ref + ref)):                # flush, then the same stream again
         for p in range(3):
             assert np.array_equal(g[p], o[p]), "frame %d plane %d" % (i, p)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["download", "device"])
+def test_hwaccel_default_extra_hw_frames(v9, orc, tmp_path, mode):
+    """frame_params with FFmpeg's default extra_hw_frames (-1) as `extra`, consumer reading
+    each frame at once: init succeeds and the decode equals the oracle's."""
+    w, h = 200, 130
+    pkts = _stream(v9, w, h)
+    ivf = tmp_path / "s.ivf"
+    ivf.write_bytes(v9.ivf_write(pkts, w, h))
+    out = tmp_path / "out.yuv"
+    rc, nout, _, err = run_harness(ivf, out if mode == "download" else "-", 8, 1, 1, 2, 0, mode, 0, extra=-1)
+    assert rc == 0, err
+    ref = _oracle_outputs(v9, orc, pkts)
+    assert nout == 2 * len(ref)
+    if mode == "download":
+        got = _read_frames(str(out), w, h, 8, 1, 1)
+        for i, (g, o) in enumerate(zip(got, ref + ref)):
+            for p in range(3):
+                assert np.array_equal(g[p], o[p]), "frame %d plane %d" % (i, p)
 
 
 @pytest.mark.gpu
