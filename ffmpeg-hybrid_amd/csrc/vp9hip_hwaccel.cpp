@@ -79,10 +79,11 @@ struct vp9hip_hwaccel {
     std::unique_ptr<ParsePool> pool;
     std::shared_ptr<Chain> chain;           // the parse chain of the next non-key frame
     int slot[8];                            // device buffer of each reference slot (s->s.ref_frames)
-    std::vector<int> refs;                  // per pool buffer: frame references handed out (under rmu:
-                                            // vp9hip_hwframe_ref / unref may come from any thread,
-                                            // as av_frame_unref of an output frame does)
-    mutable std::mutex rmu;
+    std::vector<int> refs;                  // per pool buffer: frame references handed out
+    // Every entry point holds mu: FFmpeg calls the per-frame callbacks from its decoding
+    // thread(s) while the user's thread transfers and unrefs output frames
+    // (av_hwframe_transfer_data, av_frame_unref run the hwcontext / buffer callbacks there).
+    mutable std::mutex mu;
     std::vector<int> pend;                  // per pool buffer: in the batch being filled
     std::vector<int> inref;                 // per pool buffer: read by frames of that batch
     std::vector<uint64_t> buf_seq;          // per pool buffer: the batch that last wrote it
@@ -285,11 +286,7 @@ static int pump(vp9hip_hwaccel *h)
     return err;
 }
 
-static int nrefs(const vp9hip_hwaccel *h, int b)
-{
-    std::lock_guard<std::mutex> g(h->rmu);
-    return h->refs[b];
-}
+static int nrefs(const vp9hip_hwaccel *h, int b) { return h->refs[b]; }
 
 static bool buf_busy(const vp9hip_hwaccel *h, int b)
 {
@@ -310,6 +307,7 @@ static int find_free(const vp9hip_hwaccel *h)
 extern "C" int vp9hip_hwaccel_start_frame(vp9hip_hwaccel *h, const uint8_t *buf, uint32_t size, int64_t pts)
 {
     if (!h || (!buf && size)) return VP9HIP_EINVAL;
+    std::lock_guard<std::mutex> g(h->mu);
     h->job.reset();                          // a frame that never reached end_frame
     h->cur = -1;
     // a full pool: launch the oldest filled batches first (waiting for their parses), then
@@ -335,7 +333,9 @@ extern "C" int vp9hip_hwaccel_start_frame(vp9hip_hwaccel *h, const uint8_t *buf,
 
 extern "C" int vp9hip_hwaccel_decode_slice(vp9hip_hwaccel *h, const uint8_t *buf, uint32_t size)
 {
-    if (!h || !buf || !size || h->cur < 0) return VP9HIP_EINVAL;
+    if (!h || !buf || !size) return VP9HIP_EINVAL;
+    std::lock_guard<std::mutex> g(h->mu);
+    if (h->cur < 0) return VP9HIP_EINVAL;
     h->tr.start();
     vp9h_frame_info info;
     const int type = vp9h_frame_peek(buf, size, &info);
@@ -371,13 +371,14 @@ static void fill_frame(vp9hip_hwaccel *h, int b, int64_t pts, vp9hip_hwframe *ou
     out->sw_format = h->fp.sw_format;
     out->buf = b;
     out->pts = pts;
-    std::lock_guard<std::mutex> g(h->rmu);
     h->refs[b]++;
 }
 
 extern "C" int vp9hip_hwaccel_end_frame(vp9hip_hwaccel *h, vp9hip_hwframe *out)
 {
-    if (!h || h->cur < 0 || !h->job) return VP9HIP_EINVAL;
+    if (!h) return VP9HIP_EINVAL;
+    std::lock_guard<std::mutex> g(h->mu);
+    if (h->cur < 0 || !h->job) return VP9HIP_EINVAL;
     h->tr.start();
     Pend p;
     p.out = h->cur;
@@ -409,6 +410,7 @@ extern "C" int vp9hip_hwaccel_end_frame(vp9hip_hwaccel *h, vp9hip_hwframe *out)
 extern "C" int vp9hip_hwaccel_show_existing(vp9hip_hwaccel *h, int slot, int64_t pts, vp9hip_hwframe *out)
 {
     if (!h || !out || slot < 0 || slot > 7) return VP9HIP_EINVAL;
+    std::lock_guard<std::mutex> g(h->mu);
     if (h->slot[slot] < 0) return VP9HIP_EINVALIDDATA;   // "Requested reference ... not available"
     fill_frame(h, h->slot[slot], pts, out);
     return 0;
@@ -433,9 +435,9 @@ static int launch_for(vp9hip_hwaccel *h, int b)
     return h->buf_err[b];
 }
 
-extern "C" int vp9hip_hwframe_sync(vp9hip_hwaccel *h, const vp9hip_hwframe *f)
+static int hwframe_sync_l(vp9hip_hwaccel *h, const vp9hip_hwframe *f)
 {
-    if (!h || !f || f->buf < 0 || f->buf >= h->fp.initial_pool_size || !nrefs(h, f->buf)) return VP9HIP_EINVAL;
+    if (f->buf < 0 || f->buf >= h->fp.initial_pool_size || !nrefs(h, f->buf)) return VP9HIP_EINVAL;
     int r = launch_for(h, f->buf);
     if (r < 0) return r;
     const uint64_t b = h->buf_seq[f->buf];
@@ -448,9 +450,18 @@ extern "C" int vp9hip_hwframe_sync(vp9hip_hwaccel *h, const vp9hip_hwframe *f)
     return batch_bad(h, b);
 }
 
+extern "C" int vp9hip_hwframe_sync(vp9hip_hwaccel *h, const vp9hip_hwframe *f)
+{
+    if (!h || !f) return VP9HIP_EINVAL;
+    std::lock_guard<std::mutex> g(h->mu);
+    return hwframe_sync_l(h, f);
+}
+
 extern "C" int vp9hip_hwframe_ready(vp9hip_hwaccel *h, const vp9hip_hwframe *f, void *stream)
 {
-    if (!h || !f || f->buf < 0 || f->buf >= h->fp.initial_pool_size || !nrefs(h, f->buf)) return VP9HIP_EINVAL;
+    if (!h || !f) return VP9HIP_EINVAL;
+    std::lock_guard<std::mutex> g(h->mu);
+    if (f->buf < 0 || f->buf >= h->fp.initial_pool_size || !nrefs(h, f->buf)) return VP9HIP_EINVAL;
     int r = launch_for(h, f->buf);
     if (r < 0) return r;
     const uint64_t b = h->buf_seq[f->buf];
@@ -470,10 +481,13 @@ extern "C" int vp9hip_hwaccel_uninit(vp9hip_hwaccel *h)
         for (int k = 0; k < T_N; k++) fprintf(stderr, " [%s] %.1f", tname[k], h->tr.ms[k]);
         fprintf(stderr, "\n");
     }
-    h->job.reset();
-    if (h->gpu) {
-        submit(h);                           // frames handed out may still be read by the caller
-        vp9hip_sync(h->gpu);
+    {
+        std::lock_guard<std::mutex> g(h->mu);
+        h->job.reset();
+        if (h->gpu) {
+            submit(h);                       // frames handed out may still be read by the caller
+            vp9hip_sync(h->gpu);
+        }
     }
     h->batch.clear();
     h->full.clear();
@@ -487,6 +501,7 @@ extern "C" int vp9hip_hwaccel_uninit(vp9hip_hwaccel *h)
 extern "C" void vp9hip_hwaccel_flush(vp9hip_hwaccel *h)
 {
     if (!h) return;
+    std::lock_guard<std::mutex> g(h->mu);
     h->job.reset();
     h->cur = -1;
     // frames already handed out stay valid: their batch runs, then the slots are dropped
@@ -503,6 +518,7 @@ extern "C" void vp9hip_hwaccel_flush(vp9hip_hwaccel *h)
 extern "C" int vp9hip_hwaccel_last_header(const vp9hip_hwaccel *h, vp9h_frame_info *info)
 {
     if (!h || !info) return VP9HIP_EINVAL;
+    std::lock_guard<std::mutex> g(h->mu);
     *info = h->info;
     return 0;
 }
@@ -510,17 +526,19 @@ extern "C" int vp9hip_hwaccel_last_header(const vp9hip_hwaccel *h, vp9h_frame_in
 extern "C" int vp9hip_hwframe_transfer(vp9hip_hwaccel *h, const vp9hip_hwframe *src, uint8_t *const dst[3],
                                        const ptrdiff_t dst_linesize[3])
 {
-    const int r = vp9hip_hwframe_sync(h, src);
+    if (!h || !src || !dst || !dst_linesize) return VP9HIP_EINVAL;
+    std::lock_guard<std::mutex> g(h->mu);
+    const int r = hwframe_sync_l(h, src);
     if (r < 0) return r;
     return vp9hip_download_frame(h->gpu, src->buf, dst, dst_linesize);
 }
 
 extern "C" int vp9hip_hwframe_unref(vp9hip_hwaccel *h, vp9hip_hwframe *f)
 {
-    if (!h || !f || f->buf < 0 || f->buf >= h->fp.initial_pool_size) return VP9HIP_EINVAL;
+    if (!h || !f) return VP9HIP_EINVAL;
     {
-        std::lock_guard<std::mutex> g(h->rmu);
-        if (h->refs[f->buf] <= 0) return VP9HIP_EINVAL;
+        std::lock_guard<std::mutex> g(h->mu);
+        if (f->buf < 0 || f->buf >= h->fp.initial_pool_size || h->refs[f->buf] <= 0) return VP9HIP_EINVAL;
         h->refs[f->buf]--;
     }
     memset(f, 0, sizeof(*f));
@@ -530,9 +548,9 @@ extern "C" int vp9hip_hwframe_unref(vp9hip_hwaccel *h, vp9hip_hwframe *f)
 
 extern "C" int vp9hip_hwframe_ref(vp9hip_hwaccel *h, const vp9hip_hwframe *src, vp9hip_hwframe *dst)
 {
-    if (!h || !src || !dst || src->buf < 0 || src->buf >= h->fp.initial_pool_size) return VP9HIP_EINVAL;
-    std::lock_guard<std::mutex> g(h->rmu);
-    if (h->refs[src->buf] <= 0) return VP9HIP_EINVAL;
+    if (!h || !src || !dst) return VP9HIP_EINVAL;
+    std::lock_guard<std::mutex> g(h->mu);
+    if (src->buf < 0 || src->buf >= h->fp.initial_pool_size || h->refs[src->buf] <= 0) return VP9HIP_EINVAL;
     *dst = *src;
     h->refs[src->buf]++;
     return 0;

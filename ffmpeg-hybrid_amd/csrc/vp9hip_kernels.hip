@@ -1124,70 +1124,103 @@ template <typename PIX, class G> DEV void lf_chunk(int ci, int &p, int &r, int &
 DEV int ad16(int a, int b) { return (int) __builtin_amdgcn_sad_u16((uint32_t) a, (uint32_t) b, 0u); }
 DEV int max3i(int a, int b, int c) { return max(max(a, b), c); }
 
+
 // loop_filter (vp9dsp_template.c:1780-1889) on a line held in registers: q0 = px[C],
 // compile-time positions, so a row's chain of edges (vp9lpf.c:31-104 order) runs
 // without LDS round trips.
 // `code` = filter width (1: 4, 2: 8, 3: 16), `eih` = the E | I << 12 | H << 22 word of
 // the edge's level (lf_lut).
+// Instruction economy (a line's chain of edges is the loop filter's critical path):
+// - decisions branch-free: |a - b| is one v_sad_u16 (pixels < 2^12), reductions by max3,
+//   one compare per condition;
+// - the 4-wide results are computed by every filtered lane, both hev forms in one
+//   sequence (lanes differ in hev), clamps as v_med3_i32 / min + max;
+// - a wave none of whose lanes is flat (the common case) writes them in place and is done;
+//   otherwise the 8- and 16-wide outputs are running sums (each output = the previous sum
+//   + two entering - two leaving taps: the reference's sums term for term, exact) and every
+//   position takes its lane's result by a select, so no branch leaves copies of the line's
+//   registers at its join.
 template <int C, int NPX>
 DEV void lf_reg(int (&px)[NPX], int code, uint32_t eih, int bd)
 {
     const int E = eih & 4095, I = (eih >> 12) & 1023, H = eih >> 22;
-    const int F = 1 << (bd - 8);
-    const int wd = 4 << (code - 1);
+    const int F = 1 << (bd - 8), pmax = (1 << bd) - 1, smx = (1 << (bd - 1)) - 1, smn = -smx - 1;
     const int p3 = px[C - 4], p2 = px[C - 3], p1 = px[C - 2], p0 = px[C - 1];
     const int q0 = px[C], q1 = px[C + 1], q2 = px[C + 2], q3 = px[C + 3];
-    // decisions branch-free: |a - b| is one v_sad_u16 (pixels < 2^12), reductions by max3,
-    // one compare per condition (the reference's && chains compile to a branch per term)
     const int ap1p0 = ad16(p1, p0), aq1q0 = ad16(q1, q0);
     const int mi = max3i(max3i(ad16(p3, p2), ad16(p2, p1), ap1p0), max3i(aq1q0, ad16(q2, q1), ad16(q3, q2)), 0);
     const bool fm = (mi <= I) & (ad16(p0, q0) * 2 + (ad16(p1, q1) >> 1) <= E);
     if (!fm) return;
-    const bool flat8in = (wd >= 8) &
-                         (max3i(max3i(ad16(p3, p0), ad16(p2, p0), ap1p0), max3i(aq1q0, ad16(q2, q0), ad16(q3, q0)), 0) <= F);
-    if (C >= 8 && C + 7 < NPX && wd >= 16 && flat8in) {
+    const bool f8 = (code >= 2) &
+                    (max3i(max3i(ad16(p3, p0), ad16(p2, p0), ap1p0), max3i(aq1q0, ad16(q2, q0), ad16(q3, q0)), 0) <= F);
+    // 4-wide (vp9dsp_template.c:1865-1885): with hev the p1 - q1 term enters f and p1 / q1
+    // stay, without it f = 3 (q0 - p0) and p1 / q1 move by (f1 + 1) >> 1
+    const bool hev = max(ap1p0, aq1q0) > H;
+    const int fh = min(max(p1 - q1, smn), smx);
+    int f = __mul24(q0 - p0, 3) + (hev ? fh : 0);        // v_mad_i32_i24 (|q0 - p0| < 2^12)
+    f = min(max(f, smn), smx);
+    const int f1 = min(f + 4, smx) >> 3, f2 = min(f + 3, smx) >> 3, f3 = (f1 + 1) >> 1;
+    // v_med3_i32 clamps, evaluated for every lane (the asm is not speculated into a branch)
+    const int a_p0 = med3_0(p0 + f2, pmax), a_q0 = med3_0(q0 - f1, pmax);
+    const int t_p1 = med3_0(p1 + f3, pmax), t_q1 = med3_0(q1 - f3, pmax);
+    const int a_p1 = hev ? p1 : t_p1, a_q1 = hev ? q1 : t_q1;
+    if (!__builtin_amdgcn_ballot_w64(f8)) {              // wave-uniform: no lane is flat
+        px[C - 2] = a_p1;
+        px[C - 1] = a_p0;
+        px[C] = a_q0;
+        px[C + 1] = a_q1;
+        return;
+    }
+    // 7-tap (vp9dsp_template.c:1859-1864) as a running sum, + 4 rounding
+    int b[6];
+    {
+        int sm = (int) __umul24((uint32_t) p3, 3u) + 4 + (p2 + p2 + p1) + (p0 + q0);
+        b[0] = sm >> 3;
+        sm = sm + (p1 - p3) + (q1 - p2);
+        b[1] = sm >> 3;
+        sm = sm + (p0 - p3) + (q2 - p1);
+        b[2] = sm >> 3;
+        sm = sm + (q0 - p3) + (q3 - p0);
+        b[3] = sm >> 3;
+        sm = sm + (q1 - p2) + (q3 - q0);
+        b[4] = sm >> 3;
+        sm = sm + (q2 - p1) + (q3 - q1);
+        b[5] = sm >> 3;
+    }
+    // positions p2 .. q2: the lane's 8- or 4-wide result (selects: no join copies)
+    px[C - 3] = f8 ? b[0] : p2;
+    px[C - 2] = f8 ? b[1] : a_p1;
+    px[C - 1] = f8 ? b[2] : a_p0;
+    px[C] = f8 ? b[3] : a_q0;
+    px[C + 1] = f8 ? b[4] : a_q1;
+    px[C + 2] = f8 ? b[5] : q2;
+    if (C >= 8 && C + 7 < NPX) {
         const int p7 = px[C - 8 >= 0 ? C - 8 : 0], p6 = px[C - 7 >= 0 ? C - 7 : 0], p5 = px[C - 6 >= 0 ? C - 6 : 0],
                   p4 = px[C - 5 >= 0 ? C - 5 : 0];
         const int q4 = px[C + 4 < NPX ? C + 4 : NPX - 1], q5 = px[C + 5 < NPX ? C + 5 : NPX - 1],
                   q6 = px[C + 6 < NPX ? C + 6 : NPX - 1], q7 = px[C + 7 < NPX ? C + 7 : NPX - 1];
-        const bool flat8out = max3i(max3i(ad16(p7, p0), ad16(p6, p0), ad16(p5, p0)),
-                                    max3i(ad16(p4, p0), ad16(q4, q0), ad16(q5, q0)),
-                                    max3i(ad16(q6, q0), ad16(q7, q0), 0)) <= F;
-        if (flat8out) {
-            // 15-tap (vp9dsp_template.c:1836-1857): running window sum with edge replication
+        const bool f16 = f8 & (code == 3) &
+                         (max3i(max3i(ad16(p7, p0), ad16(p6, p0), ad16(p5, p0)), max3i(ad16(p4, p0), ad16(q4, q0), ad16(q5, q0)),
+                                max3i(ad16(q6, q0), ad16(q7, q0), 0)) <= F);
+        if (__builtin_amdgcn_ballot_w64(f16)) {
+            // 15-tap (vp9dsp_template.c:1836-1857): the window sum of output k (+ the rounding
+            // 8) slides by v[k + 8] - v[k - 7] + v[k + 1] - v[k], ends replicated; inputs
+            // are the values before this edge (p7 .. q7 and p3 .. q3 above)
             const int v[16] = { p7, p6, p5, p4, p3, p2, p1, p0, q0, q1, q2, q3, q4, q5, q6, q7 };
-            int sum = p7 * 7 + p6 * 2 + p5 + p4 + p3 + p2 + p1 + p0 + q0;
+            int o[14];
+            int sum = (int) __umul24((uint32_t) p7, 7u) + 8 + (p6 + p6 + p5) + (p4 + p3 + p2) + (p1 + p0 + q0);
+            o[0] = sum >> 4;
 #pragma unroll
-            for (int k = 1; k < 15; k++) {
-                const int o = (sum + 8) >> 4;
+            for (int k = 1; k < 14; k++) {
                 const int lo = k - 7 < 0 ? 0 : k - 7, hi = k + 8 > 15 ? 15 : k + 8;
-                sum += v[hi] - v[lo] + v[k + 1] - v[k];
-                px[(C + k - 8) >= 0 && (C + k - 8) < NPX ? C + k - 8 : 0] = o;
+                sum = sum + (v[hi] - v[lo]) + (v[k + 1] - v[k]);
+                o[k] = sum >> 4;
             }
-            return;
+#pragma unroll
+            for (int k = 0; k < 14; k++)
+                px[C - 7 + k] = f16 ? o[k] : px[C - 7 + k];
         }
     }
-    if (wd >= 8 && flat8in) {
-        px[C - 3] = (p3 + p3 + p3 + 2 * p2 + p1 + p0 + q0 + 4) >> 3;
-        px[C - 2] = (p3 + p3 + p2 + 2 * p1 + p0 + q0 + q1 + 4) >> 3;
-        px[C - 1] = (p3 + p2 + p1 + 2 * p0 + q0 + q1 + q2 + 4) >> 3;
-        px[C] = (p2 + p1 + p0 + 2 * q0 + q1 + q2 + q3 + 4) >> 3;
-        px[C + 1] = (p1 + p0 + q0 + 2 * q1 + q2 + q3 + q3 + 4) >> 3;
-        px[C + 2] = (p0 + q0 + q1 + 2 * q2 + q3 + q3 + q3 + 4) >> 3;
-        return;
-    }
-    // 4-wide, both hev forms in one branch-free sequence (lanes of a wave differ in hev):
-    // with hev the p1 - q1 term enters f and p1 / q1 stay, without it f = 3 (q0 - p0) and
-    // p1 / q1 move by (f1 + 1) >> 1 (vp9dsp_template.c:1858-1885)
-    const int mx = (1 << (bd - 1)) - 1, mn = -(1 << (bd - 1));
-    const bool hev = (ap1p0 > H) | (aq1q0 > H);
-    int f = hev ? min(max(p1 - q1, mn), mx) : 0;
-    f = min(max(3 * (q0 - p0) + f, mn), mx);
-    const int f1 = min(f + 4, mx) >> 3, f2 = min(f + 3, mx) >> 3, f3 = (f1 + 1) >> 1;
-    px[C - 1] = clipbd(p0 + f2, bd);
-    px[C] = clipbd(q0 - f1, bd);
-    px[C - 2] = hev ? p1 : clipbd(p1 + f3, bd);
-    px[C + 1] = hev ? q1 : clipbd(q1 - f3, bd);
 }
 
 template <typename PIX, int N> DEV void lf_unpack(const uint32_t *w, int (&px)[N], int i0, int i1, int o)
@@ -2265,7 +2298,75 @@ DEV void mc_rows(const PIX *r, int pitch, int w, int h, int X, int Y, int mx, in
         }
     }
 }
-// R rows per lane over a unit (H % R == 0), compound averaged
+// mc_rows for a reference window that lies inside the visible reference (no emulated edge):
+// taps read directly from one row pointer (the 8 taps of a row merge into one 16-byte
+// load), the filter taps held in registers, the phase cases split outside the row loops
+// (mx, my and the filter are the unit's: wave-uniform)
+template <typename PIX, int R>
+DEV void mc_rows_direct(const PIX *r, int pitch, int X, int Y, int mx, int my, int filter, int bd, int (&o)[R])
+{
+    typedef __attribute__((address_space(1))) const PIX gpix;
+    const int pmax = (1 << bd) - 1;
+    gpix *b = (gpix *) r + (ptrdiff_t) (Y - 3) * pitch + (X - 3);
+    mx = __builtin_amdgcn_readfirstlane(mx);
+    my = __builtin_amdgcn_readfirstlane(my);
+    filter = __builtin_amdgcn_readfirstlane(filter);
+    if (filter == 3) {                                    // bilinear (vp9dsp_template.c:2150-2227)
+        int hr[R + 1];
+#pragma unroll
+        for (int k = 0; k < R + 1; k++) {
+            gpix *q = b + (ptrdiff_t) (3 + k) * pitch;
+            hr[k] = q[3] + ((mx * (q[4] - q[3]) + 8) >> 4);
+        }
+#pragma unroll
+        for (int t = 0; t < R; t++) o[t] = hr[t] + ((my * (hr[t + 1] - hr[t]) + 8) >> 4);
+        return;
+    }
+    int fx[8], fy[8];
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+        fx[t] = vp9t_subpel_filters[filter][mx][t];
+        fy[t] = vp9t_subpel_filters[filter][my][t];
+    }
+    auto hrow = [&](int k) -> int {                       // window row k, 8-tap, pixel-clipped
+        gpix *q = b + (ptrdiff_t) k * pitch;
+        int sh = 0;
+#pragma unroll
+        for (int t = 0; t < 8; t++) sh += fx[t] * q[t];
+        return med3_0((sh + 64) >> 7, pmax);
+    };
+    // one basic block per case, so every row's load is in flight before the first use
+    if (!my) {                                            // 1-D horizontal, or a copy
+        if (mx) {
+#pragma unroll
+            for (int t = 0; t < R; t++) o[t] = hrow(3 + t);
+        } else {
+#pragma unroll
+            for (int t = 0; t < R; t++) o[t] = b[(ptrdiff_t) (3 + t) * pitch + 3];
+        }
+        return;
+    }
+    int hr[R + 7];                                        // 1-D vertical, or 2-D
+    if (mx) {
+#pragma unroll
+        for (int k = 0; k < R + 7; k++) hr[k] = hrow(k);
+    } else {
+#pragma unroll
+        for (int k = 0; k < R + 7; k++) hr[k] = b[(ptrdiff_t) k * pitch + 3];
+    }
+#pragma unroll
+    for (int t = 0; t < R; t++) {
+        int sv = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) sv += fy[k] * hr[t + k];
+        o[t] = med3_0((sv + 64) >> 7, pmax);
+    }
+}
+
+// R rows per lane over a unit (H % R == 0), compound averaged. A reference whose 8-tap
+// window [ix - 3, ix + w + 4] x [iy - 3, iy + h + 4] lies inside its visible area (nearly
+// every unit of a large frame) takes the direct taps; the rest clamp every tap
+// (emulated_edge_mc, videodsp_template.c:27-105).
 template <typename PIX, int R>
 DEV void mc_unit_rows(const McUnit &u, const FrameDesc &fd, PIX *dst, int pitch, int c, int bd, int nth)
 {
@@ -2276,9 +2377,13 @@ DEV void mc_unit_rows(const McUnit &u, const FrameDesc &fd, PIX *dst, int pitch,
         for (int k = 0; k < u.nref; k++) {
             const int rf = u.ref[k];
             const McRef m = u.r[k];
+            const int rw = fd.refw[rf][c], rh = fd.refh[rf][c];
             int v[R];
-            mc_rows<PIX, R>((const PIX *) fd.ref[rf][p], pitch, fd.refw[rf][c], fd.refh[rf][c], m.ix + xx, m.iy + yy,
-                            m.mx, m.my, u.filter, bd, v);
+            if (m.ix >= 3 && m.iy >= 3 && m.ix + W + 4 < rw && m.iy + (int) u.h + 4 < rh)
+                mc_rows_direct<PIX, R>((const PIX *) fd.ref[rf][p], pitch, m.ix + xx, m.iy + yy, m.mx, m.my, u.filter, bd, v);
+            else
+                mc_rows<PIX, R>((const PIX *) fd.ref[rf][p], pitch, rw, rh, m.ix + xx, m.iy + yy, m.mx, m.my, u.filter,
+                                bd, v);
 #pragma unroll
             for (int t = 0; t < R; t++) out[t] = k ? (out[t] + v[t] + 1) >> 1 : v[t];
         }

@@ -20,7 +20,10 @@
  * The consumer reads output frames LAG frames behind the decoder (FFmpeg's frame-threading
  * delay; 0 = each frame as soon as end_frame returns it). MODE: "download" transfers each
  * output frame to host planes (appended to OUT unless OUT is "-"); "device" only waits for
- * its pixels on the GPU (vp9hip_hwframe_sync), as a consumer of device frames does.
+ * its pixels on the GPU (vp9hip_hwframe_sync), as a consumer of device frames does;
+ * "thread" downloads on a consumer thread of its own, as a user thread of FFmpeg does while
+ * the decoder keeps calling the hwaccel (at most max(LAG, 1) frames queued to it; a full pool
+ * makes start_frame answer EAGAIN until the consumer releases frames).
  * Prints "frames N seconds S" (wall time of the decode loop, init / uninit excluded).
  *
  * EXTRA (default 2 + LAG) is the frame count the FFmpeg glue hands frame_params
@@ -29,10 +32,12 @@
  *
  * usage: hwaccel_harness IN.ivf OUT.yuv|- BPP SS_H SS_V [PASSES [LAG [MODE [ASYNC_DEPTH [EXTRA]]]]]
  */
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <unistd.h>
 
 #include "../../include/vp9hip_hwaccel.h"
 
@@ -66,11 +71,16 @@ typedef struct Consumer {
     vp9hip_hwframe q[512];             /* output frames not read yet (av_frame_ref'd) */
     int head, n;
     int frames_out;
+    /* MODE "thread": the queue is shared with the consumer thread */
+    int threaded, busy, stop, err;
+    pthread_t th;
+    pthread_mutex_t mu;
+    pthread_cond_t cv;
 } Consumer;
 
 static int consume_one(Consumer *c)
 {
-    vp9hip_hwframe *f = &c->q[c->head];
+    vp9hip_hwframe *f = &c->q[c->head];      /* MODE thread: only the consumer moves head */
     int r;
     if (c->download) {
         const int by = c->bpp > 8 ? 2 : 1, w = f->width, ht = f->height;
@@ -91,16 +101,49 @@ static int consume_one(Consumer *c)
         r = vp9hip_hwframe_sync(c->h, f);                            /* the frame's pixels are final */
     }
     const int u = vp9hip_hwframe_unref(c->h, f);                     /* av_frame_unref */
+    if (c->threaded) pthread_mutex_lock(&c->mu);
     c->head = (c->head + 1) % 512;
     c->n--;
     c->frames_out++;
+    if (c->threaded) pthread_mutex_unlock(&c->mu);
     return r < 0 ? r : u;
+}
+
+/* the consumer thread: reads queued frames in order until stopped with an empty queue */
+static void *consumer_main(void *arg)
+{
+    Consumer *c = arg;
+    pthread_mutex_lock(&c->mu);
+    for (;;) {
+        while (!c->n && !c->stop) pthread_cond_wait(&c->cv, &c->mu);
+        if (!c->n) break;
+        c->busy = 1;
+        pthread_mutex_unlock(&c->mu);
+        const int r = consume_one(c);  /* the queue head is the consumer's: n > 0 */
+        pthread_mutex_lock(&c->mu);
+        c->busy = 0;
+        if (r < 0 && !c->err) c->err = r;
+        pthread_cond_broadcast(&c->cv);
+    }
+    pthread_mutex_unlock(&c->mu);
+    return NULL;
 }
 
 /* av_frame_ref of an output frame into the consumer's queue; reads the frames more than
  * LAG behind */
 static int output(Consumer *c, const vp9hip_hwframe *f)
 {
+    if (c->threaded) {
+        const int cap = c->lag > 0 ? c->lag : 1;
+        int r = 0;
+        pthread_mutex_lock(&c->mu);
+        while (c->n >= cap && !c->err) pthread_cond_wait(&c->cv, &c->mu);
+        if (c->err) r = c->err;
+        else if ((r = vp9hip_hwframe_ref(c->h, f, &c->q[(c->head + c->n) % 512])) >= 0) c->n++;
+        pthread_cond_broadcast(&c->cv);
+        pthread_mutex_unlock(&c->mu);
+        return r;
+    }
     if (c->n == 512) return -1;
     vp9hip_hwframe *d = &c->q[(c->head + c->n) % 512];
     int r = vp9hip_hwframe_ref(c->h, f, d);
@@ -112,6 +155,13 @@ static int output(Consumer *c, const vp9hip_hwframe *f)
 
 static int drain(Consumer *c)
 {
+    if (c->threaded) {                 /* wait until the consumer thread has read everything */
+        pthread_mutex_lock(&c->mu);
+        while ((c->n || c->busy) && !c->err) pthread_cond_wait(&c->cv, &c->mu);
+        const int r = c->err;
+        pthread_mutex_unlock(&c->mu);
+        return r;
+    }
     int r = 0;
     while (c->n && r >= 0) r = consume_one(c);
     return r;
@@ -126,6 +176,7 @@ int main(int argc, char **argv)
     const int bpp = atoi(argv[3]), ssh = atoi(argv[4]), ssv = atoi(argv[5]), passes = argc > 6 ? atoi(argv[6]) : 2;
     const int lag = argc > 7 ? atoi(argv[7]) : 0;
     const int download = argc > 8 ? strcmp(argv[8], "device") != 0 : 1;
+    const int threaded = argc > 8 && !strcmp(argv[8], "thread");
     const int depth = argc > 9 ? atoi(argv[9]) : 0;
     const int extra = argc > 10 ? atoi(argv[10]) : 2 + lag;
     FILE *fi = fopen(argv[1], "rb");
@@ -159,6 +210,12 @@ int main(int argc, char **argv)
     }
     static Consumer c;
     c.h = h; c.bpp = bpp; c.ssh = ssh; c.ssv = ssv; c.download = download; c.lag = lag; c.out = out;
+    c.threaded = threaded;
+    if (threaded) {
+        pthread_mutex_init(&c.mu, NULL);
+        pthread_cond_init(&c.cv, NULL);
+        pthread_create(&c.th, NULL, consumer_main, &c);
+    }
     vp9hip_hwframe slots[8], cur;                  /* s->s.ref_frames[], s->s.frames[CUR_FRAME] */
     int have_slot[8] = { 0 }, have_cur = 0;
     struct timespec t0, t1;
@@ -193,7 +250,11 @@ int main(int argc, char **argv)
                     continue;
                 }
                 if (have_cur) { vp9hip_hwframe_unref(h, &cur); have_cur = 0; }   /* vp9_frame_unref(CUR_FRAME) */
-                if ((r = vp9hip_hwaccel_start_frame(h, d, (uint32_t) sizes[k], pts)) < 0) break;
+                /* a full pool (the consumer thread still holds frames): wait for releases */
+                for (int tries = 0; (r = vp9hip_hwaccel_start_frame(h, d, (uint32_t) sizes[k], pts)) == VP9HIP_EAGAIN &&
+                                    threaded && tries < 200000; tries++)
+                    usleep(50);
+                if (r < 0) break;
                 if ((r = vp9hip_hwaccel_decode_slice(h, d, (uint32_t) sizes[k])) < 0) break;
                 if ((r = vp9hip_hwaccel_end_frame(h, &cur)) < 0) break;
                 have_cur = 1;
@@ -212,6 +273,14 @@ int main(int argc, char **argv)
     }
     if (r >= 0) r = drain(&c);
     clock_gettime(CLOCK_MONOTONIC, &t1);
+    if (threaded) {
+        pthread_mutex_lock(&c.mu);
+        c.stop = 1;
+        pthread_cond_broadcast(&c.cv);
+        pthread_mutex_unlock(&c.mu);
+        pthread_join(c.th, NULL);
+        if (r >= 0 && c.err < 0) r = c.err;
+    }
     for (int s = 0; s < 8; s++)
         if (have_slot[s]) vp9hip_hwframe_unref(h, &slots[s]);
     if (have_cur) vp9hip_hwframe_unref(h, &cur);

@@ -96,9 +96,11 @@ def test_sync_reports_rejection_until_restaged(v9, orc, reject_second):
 
 def test_hwaccel_fails_the_rejected_batch(v9, tmp_path, reject_second):
     """The FFHWAccel path: the harness's wait on a frame of the rejected batch fails with
-    AVERROR_INVALIDDATA (its first batch, 16 frames, decoded and was read before)."""
+    AVERROR_INVALIDDATA after the first batch's 16 frames were read."""
     from test_hwaccel_harness import run_harness
     ivf = tmp_path / "k.ivf"
     ivf.write_bytes(v9.ivf_write(_keyframes(v9, 352, 288, 48), 352, 288))
-    rc, _, _, err = run_harness(ivf, "-", 8, 1, 1, 1, 0, "download", 16, env=dict(os.environ))
-    assert rc == 1 and ("decode: %d" % v9.EINVALIDDATA) in err, err
+    # the consumer reads 32 frames behind: batches of 16 fill up (static plans)
+    rc, _, _, err = run_harness(ivf, "-", 8, 1, 1, 1, 32, "download", 16, env=dict(os.environ))
+    # the harness counts the failed read too: 16 good frames + the first of the rejected batch
+    assert rc == 1 and ("decode: %d after 17 frames" % v9.EINVALIDDATA) in err, err
