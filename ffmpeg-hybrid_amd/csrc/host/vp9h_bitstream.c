@@ -298,12 +298,21 @@ static inline uint32_t mv_bits(Mv m) { return (uint16_t) m.x | (uint32_t) (uint1
 typedef struct MvPair { Mv mv[2]; int8_t ref[2]; } MvPair;
 
 /* a frame's side buffers (VP9Frame.extradata: segmentation map + MV pairs), shared by
- * reference between CUR_FRAME / REF_FRAME_MVPAIR / REF_FRAME_SEGMAP (vp9.c:110-165) */
+ * reference between CUR_FRAME / REF_FRAME_MVPAIR / REF_FRAME_SEGMAP (vp9.c:110-165).
+ * Row progress, as the reference's frame threads report it (ff_thread_report_progress,
+ * vp9.c:1434; awaited at vp9mvs.c:177-178 and vp9block.c:116-117): rows_done[r] counts the
+ * tile columns that have walked SB row r; the row is final at ntc. A frame whose walk
+ * failed marks its side failed, so a frame reading it does not wait forever. */
 typedef struct Side {
-    int refs;
+    int refs;                            /* atomic: frames of a pipelined parse share sides */
     int w, h, sb_cols, sb_rows;
     uint8_t *seg;
     MvPair *mv;
+    int ntc;                             /* tile columns of the frame that writes it */
+    int *rows_done;
+    int failed;
+    pthread_mutex_t mu;
+    pthread_cond_t cv;
 } Side;
 
 static Side *side_new(int w, int h)
@@ -315,15 +324,52 @@ static Side *side_new(int w, int h)
     const size_t n = (size_t) s->sb_cols * s->sb_rows * 64;
     s->seg = calloc(n, 1);
     s->mv = calloc(n, sizeof(MvPair));
-    if (!s->seg || !s->mv) { free(s->seg); free(s->mv); free(s); return NULL; }
+    s->rows_done = calloc((size_t) s->sb_rows, sizeof(int));
+    s->ntc = 1;
+    if (!s->seg || !s->mv || !s->rows_done) { free(s->seg); free(s->mv); free(s->rows_done); free(s); return NULL; }
+    pthread_mutex_init(&s->mu, NULL);
+    pthread_cond_init(&s->cv, NULL);
     return s;
 }
-static Side *side_ref(Side *s) { if (s) s->refs++; return s; }
+static Side *side_ref(Side *s) { if (s) __atomic_add_fetch(&s->refs, 1, __ATOMIC_RELAXED); return s; }
 static void side_unref(Side **p)
 {
     Side *s = *p;
     *p = NULL;
-    if (s && !--s->refs) { free(s->seg); free(s->mv); free(s); }
+    if (s && !__atomic_sub_fetch(&s->refs, 1, __ATOMIC_ACQ_REL)) {
+        pthread_mutex_destroy(&s->mu);
+        pthread_cond_destroy(&s->cv);
+        free(s->seg); free(s->mv); free(s->rows_done); free(s);
+    }
+}
+/* one tile column has walked SB row r (its MV pairs and segment ids are written) */
+static void side_publish(Side *s, int r)
+{
+    if (__atomic_add_fetch(&s->rows_done[r], 1, __ATOMIC_ACQ_REL) >= s->ntc) {
+        pthread_mutex_lock(&s->mu);
+        pthread_cond_broadcast(&s->cv);
+        pthread_mutex_unlock(&s->mu);
+    }
+}
+static void side_fail(Side *s)
+{
+    if (!s) return;
+    pthread_mutex_lock(&s->mu);
+    __atomic_store_n(&s->failed, 1, __ATOMIC_RELEASE);
+    pthread_cond_broadcast(&s->cv);
+    pthread_mutex_unlock(&s->mu);
+}
+/* wait until SB row r is final; -1 if its frame failed */
+static int side_wait(Side *s, int r)
+{
+    if (r >= s->sb_rows) r = s->sb_rows - 1;
+    if (__atomic_load_n(&s->rows_done[r], __ATOMIC_ACQUIRE) >= s->ntc) return 0;
+    pthread_mutex_lock(&s->mu);
+    while (__atomic_load_n(&s->rows_done[r], __ATOMIC_ACQUIRE) < s->ntc && !__atomic_load_n(&s->failed, __ATOMIC_ACQUIRE))
+        pthread_cond_wait(&s->cv, &s->mu);
+    const int ok = __atomic_load_n(&s->rows_done[r], __ATOMIC_ACQUIRE) >= s->ntc;
+    pthread_mutex_unlock(&s->mu);
+    return ok ? 0 : -1;
 }
 
 enum { P_SINGLE = 0, P_COMP = 1, P_SWITCH = 2 };     /* comppredmode */
@@ -413,6 +459,8 @@ typedef struct Walk {
     uint64_t rng;
     int prob_updates, keep_modes;
     int last_keyframe, last_invisible;   /* the previous frame's header flags */
+    Hdr hs;                              /* pipelined parse: the header as of this frame */
+    int32_t ref_w[3], ref_h[3];          /* reference sizes at this frame's header */
     /* output packet (decoded, or as coded by the encoder) */
     vp9h_block *blocks; size_t nb, cb;
     uint16_t *eobs; size_t ne, ce;
@@ -1838,7 +1886,7 @@ static void adapt_probs(Walk *w)
     SavedCtx *sc = &w->st->ctx[h->ctxid];
     PC *p = &sc->p;
     const Counts *ct = &w->cnt;
-    const int uf = (h->keyframe || h->intraonly || !w->st->last_keyframe) ? 112 : 128;
+    const int uf = (h->keyframe || h->intraonly || !w->last_keyframe) ? 112 : 128;
     for (int i = 0; i < 4; i++)
         for (int j = 0; j < 2; j++)
             for (int k = 0; k < 2; k++)
@@ -1953,10 +2001,16 @@ static void free_ctx(Walk *w)
     free(w->a_segpred); free(w->a_intra); free(w->a_comp); free(w->a_ref); free(w->a_filter); free(w->a_mv);
 }
 
-/* One SB row of one tile: the left contexts restart (vp9.c:1358-1366), then its SBs. */
+/* One SB row of one tile: the left contexts restart (vp9.c:1358-1366), then its SBs. The
+ * previous frame's MV pairs and the reference segmentation map of this SB row must be final
+ * first (a pipelined parse may still be writing them); this row's are published after. */
 static int walk_tile_row(Walk *w, BC *coder, int row, int c0, int c1)
 {
     const int intra_frame = w->h->keyframe || w->h->intraonly;
+    if ((w->mvref && side_wait(w->mvref, row >> 3)) || (w->segref && w->segref != w->mvref && side_wait(w->segref, row >> 3))) {
+        w->err = 1;
+        return -1;
+    }
     w->tile_col_start = c0;
     memset(w->l_part, 0, sizeof(w->l_part)); memset(w->l_skip, 0, sizeof(w->l_skip));
     if (intra_frame) memset(w->l_mode, 2, sizeof(w->l_mode));
@@ -1970,6 +2024,7 @@ static int walk_tile_row(Walk *w, BC *coder, int row, int c0, int c1)
         walk_sb(w, row, col, 0);
         if (w->err) return -1;
     }
+    side_publish(w->side, row >> 3);
     return 0;
 }
 
@@ -2118,9 +2173,38 @@ static int begin_frame(Walk *w, int retain_segmap)
     w->mvref = inter_src ? side_ref(st->cur) : NULL;
     w->side = side_new(h->w, h->h);
     if (!w->side) return -1;
+    w->side->ntc = 1 << h->log2_tile_cols;
     if (!w->mvref || w->mvref->w != h->w || w->mvref->h != h->h) side_unref(&st->segref);
     w->segref = st->segref;
     return 0;
+}
+
+/* the reference sizes the packet reports (before this frame refreshes any slot) */
+static void capture_refs(Walk *w)
+{
+    const Hdr *h = w->h;
+    for (int i = 0; i < 3; i++) {
+        const int s = h->keyframe || h->intraonly ? -1 : h->refidx[i];
+        w->ref_w[i] = s >= 0 ? w->st->slot[s].w : h->w;
+        w->ref_h[i] = s >= 0 ? w->st->slot[s].h : h->h;
+    }
+}
+
+/* the slots and CUR_FRAME after a frame (vp9.c:1845-1849): what the next frame's header
+ * reads; with a pipelined parse, right after this frame's headers (its side buffers are
+ * then written while the next frame's walk reads them, row by row) */
+static void end_frame_header(Walk *w, int keep_side)
+{
+    vp9h_stream *st = w->st;
+    const Hdr *h = w->h;
+    for (int i = 0; i < 8; i++)
+        if (h->refreshmask & (1 << i)) {
+            st->slot[i].valid = 1; st->slot[i].w = h->w; st->slot[i].h = h->h; st->slot[i].bpp = h->bpp;
+            st->slot[i].ss_h = h->ss_h; st->slot[i].ss_v = h->ss_v;
+        }
+    side_unref(&st->cur);
+    st->cur = keep_side ? side_ref(w->side) : w->side;
+    if (!keep_side) w->side = NULL;
 }
 
 /* the state after a frame (vp9.c:1738-1751, 1821-1823, 1845-1849) */
@@ -2187,9 +2271,8 @@ static void fill_packet(Walk *w, vp9h_frame *out)
     out->log2_tile_cols = (uint8_t) h->log2_tile_cols; out->log2_tile_rows = (uint8_t) h->log2_tile_rows;
     memcpy(out->lflvl, h->lflvl, sizeof(out->lflvl));
     for (int i = 0; i < 3; i++) {
-        const int s = h->keyframe || h->intraonly ? -1 : h->refidx[i];
-        out->ref_w[i] = s >= 0 ? w->st->slot[s].w : h->w;
-        out->ref_h[i] = s >= 0 ? w->st->slot[s].h : h->h;
+        out->ref_w[i] = w->ref_w[i];
+        out->ref_h[i] = w->ref_h[i];
     }
     out->nblocks = (uint32_t) w->nb; out->neobs = (uint32_t) w->ne;
     out->ncoefs = w->nc / (h->bpp > 8 ? 4 : 2);
@@ -2206,10 +2289,32 @@ static void walk_free(Walk *w)
 }
 
 /* ------------------------------------------------------------------ API: decode */
-int vp9h_stream_decode(vp9h_stream *st, const uint8_t *data, size_t size, vp9h_frame *out, vp9h_frame_info *info)
+/* A frame between its headers and its tiles. */
+struct vp9h_pending {
+    Walk *w;
+    BC *coders;
+    int serial;                          /* the next frame's headers read this frame's adapted probabilities */
+    int done;                            /* the tiles' walk completed (else the side is failed) */
+};
+
+static void pending_free(vp9h_pending *p)
 {
-    if (!st || !data || !out || size < 1) return VP9HIP_EINVAL;
-    memset(out, 0, sizeof(*out));
+    if (!p) return;
+    if (p->w) {
+        if (!p->done) side_fail(p->w->side);
+        walk_free(p->w);
+        free(p->w);
+    }
+    free(p->coders);
+    free(p);
+}
+
+/* The uncompressed and compressed headers and the tile layout of one frame (vp9.c:519-1110,
+ * 1247-1262): 0 with *pend set, or 0 with *pend NULL for show_existing_frame (info says
+ * which slot), or an error. data must outlive the tiles' walk. */
+static int decode_headers(vp9h_stream *st, const uint8_t *data, size_t size, vp9h_frame_info *info, vp9h_pending **pend)
+{
+    *pend = NULL;
     Walk *w = calloc(1, sizeof(Walk));
     if (!w) return VP9HIP_ENOMEM;
     w->st = st;
@@ -2248,37 +2353,103 @@ int vp9h_stream_decode(vp9h_stream *st, const uint8_t *data, size_t size, vp9h_f
     bd_init(&ch.d, data + hbytes, csize);
     w->c = &ch;
     if (walk_compressed(w) < 0) { free(w); return VP9HIP_EINVALIDDATA; }
+    capture_refs(w);
     /* tiles */
     const int ntc = 1 << h->log2_tile_cols, ntr = 1 << h->log2_tile_rows, nt = ntc * ntr;
+    vp9h_pending *p = calloc(1, sizeof(*p));
     BC *coders = calloc((size_t) nt, sizeof(BC));
-    if (!coders || alloc_ctx(w) < 0 || begin_frame(w, retain) < 0) r = VP9HIP_ENOMEM;
-    const uint8_t *p = data + hbytes + csize, *end = data + size;
+    if (p) { p->w = w; p->coders = coders; }
+    if (!p || !coders || alloc_ctx(w) < 0 || begin_frame(w, retain) < 0) r = VP9HIP_ENOMEM;
+    const uint8_t *q = data + hbytes + csize, *end = data + size;
     for (int i = 0; i < nt && !r; i++) {
-        size_t n = (size_t) (end - p);
+        size_t n = (size_t) (end - q);
         if (i + 1 < nt) {
-            if (end - p < 4) { r = VP9HIP_EINVALIDDATA; break; }
-            n = (size_t) p[0] << 24 | (size_t) p[1] << 16 | (size_t) p[2] << 8 | p[3];
-            p += 4;
-            if (n > (size_t) (end - p)) { r = VP9HIP_EINVALIDDATA; break; }
+            if (end - q < 4) { r = VP9HIP_EINVALIDDATA; break; }
+            n = (size_t) q[0] << 24 | (size_t) q[1] << 16 | (size_t) q[2] << 8 | q[3];
+            q += 4;
+            if (n > (size_t) (end - q)) { r = VP9HIP_EINVALIDDATA; break; }
         }
-        bd_init(&coders[i].d, p, n);
+        bd_init(&coders[i].d, q, n);
         if (bc_bool(&coders[i], 128, 0)) r = VP9HIP_EINVALIDDATA;   /* marker bit */
-        p += n;
+        q += n;
     }
     if (!r) save_forward_ctx(w);
-    if (!r && (st->tile_threads > 1 && ntc > 1 ? walk_tiles_mt(w, coders, st->tile_threads) : walk_tiles(w, coders)) < 0)
-        r = w->err ? VP9HIP_EINVALIDDATA : VP9HIP_ENOMEM;
-    free(coders);
-    if (!r) {
-        end_frame(w);
-        fill_packet(w, out);
-        fill_info(w, info);
-        if (info) { info->header_size = (uint32_t) hbytes; info->compressed_header_size = (uint32_t) csize; }
+    if (r) {
+        if (p) pending_free(p);
+        else { free(coders); walk_free(w); free(w); }
+        return r;
     }
-    walk_free(w);
-    free(w);
+    fill_info(w, info);
+    if (info) { info->header_size = (uint32_t) hbytes; info->compressed_header_size = (uint32_t) csize; }
+    p->serial = h->refreshctx && !h->parallel;
+    *pend = p;
+    return 0;
+}
+
+/* The tiles of a frame whose headers were read (vp9.c:1325-1395 / 1441-1520): 0 or an error. */
+static int decode_tiles(vp9h_pending *p, int threads)
+{
+    Walk *w = p->w;
+    const int ntc = 1 << w->h->log2_tile_cols;
+    if ((threads > 1 && ntc > 1 ? walk_tiles_mt(w, p->coders, threads) : walk_tiles(w, p->coders)) < 0) {
+        side_fail(w->side);
+        return w->err ? VP9HIP_EINVALIDDATA : VP9HIP_ENOMEM;
+    }
+    return 0;
+}
+
+int vp9h_stream_decode(vp9h_stream *st, const uint8_t *data, size_t size, vp9h_frame *out, vp9h_frame_info *info)
+{
+    if (!st || !data || !out || size < 1) return VP9HIP_EINVAL;
+    memset(out, 0, sizeof(*out));
+    vp9h_pending *p = NULL;
+    int r = decode_headers(st, data, size, info, &p);
+    if (r < 0 || !p) return r;
+    r = decode_tiles(p, st->tile_threads);
+    if (!r) {
+        end_frame(p->w);
+        fill_packet(p->w, out);
+        p->done = 1;
+    }
+    pending_free(p);
     return r;
 }
+
+int vp9h_stream_decode_begin(vp9h_stream *st, const uint8_t *data, size_t size, vp9h_pending **pend,
+                             vp9h_frame_info *info, int *serial)
+{
+    if (!st || !data || !pend || size < 1) return VP9HIP_EINVAL;
+    *pend = NULL;
+    if (serial) *serial = 0;
+    vp9h_pending *p = NULL;
+    const int r = decode_headers(st, data, size, info, &p);
+    if (r < 0 || !p) return r;
+    /* the stream moves on to the next frame's headers: this frame keeps its header as of
+     * now, and its side buffers become CUR_FRAME (written row by row by its tiles' walk) */
+    p->w->hs = st->h;
+    p->w->h = &p->w->hs;
+    end_frame_header(p->w, 1);
+    if (serial) *serial = p->serial;
+    *pend = p;
+    return 0;
+}
+
+int vp9h_stream_decode_finish(vp9h_pending *p, int threads, vp9h_frame *out)
+{
+    if (!p || !out || threads < 1 || threads > 64) { pending_free(p); return VP9HIP_EINVAL; }
+    memset(out, 0, sizeof(*out));
+    int r = decode_tiles(p, threads);
+    if (!r) {
+        Walk *w = p->w;
+        if (p->serial) adapt_probs(w);   /* vp9.c:1821-1823; the next frame's headers wait for it */
+        fill_packet(w, out);
+        p->done = 1;
+    }
+    pending_free(p);
+    return r;
+}
+
+void vp9h_pending_free(vp9h_pending *p) { pending_free(p); }
 
 /* ------------------------------------------------------------------ API: encode */
 void vp9h_enc_defaults(vp9h_enc_params *p)
@@ -2445,6 +2616,7 @@ int vp9h_stream_encode(vp9h_stream *st, const vp9h_frame *pkt, const vp9h_enc_pa
     }
     if (!r) r = write_frame(w, &b, szpos, &ch, coders, nt, out, out_size);
     if (!r) {
+        capture_refs(w);
         end_frame(w);
         if (coded) fill_packet(w, coded);
     }

@@ -288,6 +288,13 @@ static int pump(vp9hip_hwaccel *h)
 
 static int nrefs(const vp9hip_hwaccel *h, int b) { return h->refs[b]; }
 
+// drop the frame decode_slice queued for parsing (the pool may be working on it)
+static void drop_job(vp9hip_hwaccel *h)
+{
+    if (h->job) h->pool->wait(h->job.get());
+    h->job.reset();
+}
+
 static bool buf_busy(const vp9hip_hwaccel *h, int b)
 {
     // a buffer a batched frame reads is not rewritten by a later frame of the same batch
@@ -308,7 +315,7 @@ extern "C" int vp9hip_hwaccel_start_frame(vp9hip_hwaccel *h, const uint8_t *buf,
 {
     if (!h || (!buf && size)) return VP9HIP_EINVAL;
     std::lock_guard<std::mutex> g(h->mu);
-    h->job.reset();                          // a frame that never reached end_frame
+    drop_job(h);                             // a frame that never reached end_frame
     h->cur = -1;
     // a full pool: launch the oldest filled batches first (waiting for their parses), then
     // the one being filled; their unreferenced hidden frames free up once launched
@@ -384,7 +391,7 @@ extern "C" int vp9hip_hwaccel_end_frame(vp9hip_hwaccel *h, vp9hip_hwframe *out)
     p.out = h->cur;
     for (int i = 0; i < 3; i++) {            // s->s.h.refidx -> the slots' device buffers
         p.refs[i] = h->intra ? -1 : h->slot[h->info.ref_slot[i] & 7];
-        if (!h->intra && p.refs[i] < 0) { h->job.reset(); h->cur = -1; return VP9HIP_EINVALIDDATA; }
+        if (!h->intra && p.refs[i] < 0) { drop_job(h); h->cur = -1; return VP9HIP_EINVALIDDATA; }
     }
     p.job = std::move(h->job);
     for (int i = 0; i < 8; i++)              // vp9.c:1705-1711: slots of refreshrefmask
@@ -483,7 +490,7 @@ extern "C" int vp9hip_hwaccel_uninit(vp9hip_hwaccel *h)
     }
     {
         std::lock_guard<std::mutex> g(h->mu);
-        h->job.reset();
+        if (h->pool) drop_job(h);
         if (h->gpu) {
             submit(h);                       // frames handed out may still be read by the caller
             vp9hip_sync(h->gpu);
@@ -502,7 +509,7 @@ extern "C" void vp9hip_hwaccel_flush(vp9hip_hwaccel *h)
 {
     if (!h) return;
     std::lock_guard<std::mutex> g(h->mu);
-    h->job.reset();
+    drop_job(h);
     h->cur = -1;
     // frames already handed out stay valid: their batch runs, then the slots are dropped
     if (submit(h) >= 0) {

@@ -1250,24 +1250,63 @@ template <typename PIX, int N> DEV void lf_pack(uint32_t *w, const int (&px)[N],
 // (an edge touches 8 pixels either side: x = -8..31 for edges 0-3, then x = 24..63 for
 // edges 4-7, x = 24..31 carried over). "narrow": a subsampled 32-pixel chroma dimension,
 // x = -8..31, 8 edges 4 apart.
+// PF (k_lfrd: one wave per SIMD, nothing hides an LDS read's latency): the E | I | H words
+// of a line's edges are read from the LDS table before its first edge (lf_eih_wide /
+// _narrow: every load in flight at once), so no edge waits on an LDS read. Without PF (the
+// diagonal kernels, several waves per SIMD) each edge reads its word: fewer live registers.
+template <bool PF, int N> struct LfEv {
+    uint32_t v[PF ? N : 1];
+    const uint32_t *lut;
+    DEV uint32_t operator()(int i, uint32_t lvl) const
+    {
+        if constexpr (PF) return v[i];
+        else return lut[lvl & 63];
+    }
+};
 #define LF_EDGE_WIDE(k, C0)                                                                              \
     {                                                                                                    \
         const uint32_t ww = (k) < 2 ? pw0 : (k) < 4 ? pw1 : (k) < 6 ? pw2 : pw3;                         \
         const uint32_t m = (ww >> (16 * ((k) & 1))) & 255, in = (ww >> (16 * ((k) & 1) + 8)) & 255;      \
-        if (m >> 6) lf_reg<8 * (k) + 8 - (C0)>(px, m >> 6, lut[m & 63], bd);                             \
-        if (in) lf_reg<8 * (k) + 12 - (C0)>(px, 1, lut[in & 63], bd);                                    \
+        if (m >> 6) lf_reg<8 * (k) + 8 - (C0)>(px, m >> 6, ev(2 * (k), m), bd);                          \
+        if (in) lf_reg<8 * (k) + 12 - (C0)>(px, 1, ev(2 * (k) + 1, in), bd);                             \
     }
 #define LF_EDGE_NARROW(k)                                                                                \
     {                                                                                                    \
         const uint32_t m = (((k) < 4 ? pc0 : pc1) >> (8 * ((k) & 3))) & 255;                             \
-        if (m >> 6) lf_reg<4 * (k) + 8>(px, m >> 6, lut[m & 63], bd);                                    \
+        if (m >> 6) lf_reg<4 * (k) + 8>(px, m >> 6, ev(k, m), bd);                                       \
     }
+// the 16 edge words of a 64-pixel line (8 edges + their inner 4-wide edges), program words pw0..3
+template <bool PF>
+DEV void lf_eih_wide(LfEv<PF, 16> &ev, uint32_t pw0, uint32_t pw1, uint32_t pw2, uint32_t pw3, const uint32_t *lut)
+{
+    ev.lut = lut;
+    if constexpr (PF) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint32_t ww = k < 2 ? pw0 : k < 4 ? pw1 : k < 6 ? pw2 : pw3;
+            ev.v[2 * k] = lut[(ww >> (16 * (k & 1))) & 63];
+            ev.v[2 * k + 1] = lut[(ww >> (16 * (k & 1) + 8)) & 63];
+        }
+    }
+}
+// the 8 edge words of a subsampled 32-pixel chroma line
+template <bool PF, int N>
+DEV void lf_eih_narrow(LfEv<PF, N> &ev, uint32_t pc0, uint32_t pc1, const uint32_t *lut)
+{
+    ev.lut = lut;
+    if constexpr (PF) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) ev.v[k] = lut[((k < 4 ? pc0 : pc1) >> (8 * (k & 3))) & 63];
+    }
+}
 // column edges of one pixel row (packed dwords in LDS)
-template <typename PIX>
+template <typename PIX, bool PF = false>
 DEV void lf_line_row_wide(uint32_t *rowp, const uint32_t *pw, const uint32_t *lut, int bd)
 {
     constexpr int PPW = 4 / sizeof(PIX);
     const uint32_t pw0 = pw[0], pw1 = pw[1], pw2 = pw[2], pw3 = pw[3];
+    LfEv<PF, 16> ev;
+    lf_eih_wide<PF>(ev, pw0, pw1, pw2, pw3, lut);
     int px[40];
     lf_unpack<PIX>(rowp, px, 0, 40 / PPW, 0);
     LF_EDGE_WIDE(0, 0) LF_EDGE_WIDE(1, 0) LF_EDGE_WIDE(2, 0) LF_EDGE_WIDE(3, 0)
@@ -1278,13 +1317,15 @@ DEV void lf_line_row_wide(uint32_t *rowp, const uint32_t *pw, const uint32_t *lu
     LF_EDGE_WIDE(4, 32) LF_EDGE_WIDE(5, 32) LF_EDGE_WIDE(6, 32) LF_EDGE_WIDE(7, 32)
     lf_pack<PIX>(rowp, px, 32 / PPW, 72 / PPW, 0);
 }
-template <typename PIX>
+template <typename PIX, bool PF = false>
 DEV void lf_line_row_narrow(uint32_t *rowp, const uint32_t *pw, const uint32_t *lut, int bd)
 {
     constexpr int PPW = 4 / sizeof(PIX);
+    const uint32_t pc0 = pw[0], pc1 = pw[1];
+    LfEv<PF, 8> ev;
+    lf_eih_narrow<PF>(ev, pc0, pc1, lut);
     int px[40];
     lf_unpack<PIX>(rowp, px, 0, 40 / PPW, 0);
-    const uint32_t pc0 = pw[0], pc1 = pw[1];
     LF_EDGE_NARROW(0) LF_EDGE_NARROW(1) LF_EDGE_NARROW(2) LF_EDGE_NARROW(3)
     LF_EDGE_NARROW(4) LF_EDGE_NARROW(5) LF_EDGE_NARROW(6) LF_EDGE_NARROW(7)
     lf_pack<PIX>(rowp, px, 0, 40 / PPW, 0);
@@ -1292,23 +1333,24 @@ DEV void lf_line_row_narrow(uint32_t *rowp, const uint32_t *pw, const uint32_t *
 // k_lfrd's column pass in two parts around a barrier: part 1 filters a row's first edge
 // (x = 0, the only one that reaches x < 0: later edges modify x >= 1) and writes
 // x = -8..-1 back, so the previous SB's last columns are final in LDS after it; part 2
-// runs the row's other edges on the same registers.
+// runs the row's other edges on the same registers (and edge words: ev, read in part 1).
 template <typename PIX>
-DEV void lf_row_wide_1(uint32_t *rowp, const uint32_t *pw, const uint32_t *lut, int bd, int (&px)[40])
+DEV void lf_row_wide_1(uint32_t *rowp, const uint32_t *pw, const uint32_t *lut, int bd, int (&px)[40], LfEv<true, 16> &ev)
 {
     constexpr int PPW = 4 / sizeof(PIX);
+    lf_eih_wide<true>(ev, pw[0], pw[1], pw[2], pw[3], lut);
     lf_unpack<PIX>(rowp, px, 0, 40 / PPW, 0);
     const uint32_t m = pw[0] & 255;
-    if (m >> 6) lf_reg<8>(px, m >> 6, lut[m & 63], bd);
+    if (m >> 6) lf_reg<8>(px, m >> 6, ev(0, m), bd);
     lf_pack<PIX>(rowp, px, 0, 8 / PPW, 0);
 }
 template <typename PIX>
-DEV void lf_row_wide_2(uint32_t *rowp, const uint32_t *pw, const uint32_t *lut, int bd, int (&px)[40])
+DEV void lf_row_wide_2(uint32_t *rowp, const uint32_t *pw, const uint32_t *lut, int bd, int (&px)[40], const LfEv<true, 16> &ev)
 {
     constexpr int PPW = 4 / sizeof(PIX);
     const uint32_t pw0 = pw[0], pw1 = pw[1], pw2 = pw[2], pw3 = pw[3];
     const uint32_t in0 = (pw0 >> 8) & 255;
-    if (in0) lf_reg<12>(px, 1, lut[in0 & 63], bd);
+    if (in0) lf_reg<12>(px, 1, ev(1, in0), bd);
     LF_EDGE_WIDE(1, 0) LF_EDGE_WIDE(2, 0) LF_EDGE_WIDE(3, 0)
     lf_pack<PIX>(rowp, px, 8 / PPW, 32 / PPW, 8);
 #pragma unroll
@@ -1318,16 +1360,17 @@ DEV void lf_row_wide_2(uint32_t *rowp, const uint32_t *pw, const uint32_t *lut, 
     lf_pack<PIX>(rowp, px, 32 / PPW, 72 / PPW, 0);
 }
 template <typename PIX>
-DEV void lf_row_narrow_1(uint32_t *rowp, const uint32_t *pw, const uint32_t *lut, int bd, int (&px)[40])
+DEV void lf_row_narrow_1(uint32_t *rowp, const uint32_t *pw, const uint32_t *lut, int bd, int (&px)[40], LfEv<true, 16> &ev)
 {
     constexpr int PPW = 4 / sizeof(PIX);
+    lf_eih_narrow<true, 16>(ev, pw[0], pw[1], lut);
     lf_unpack<PIX>(rowp, px, 0, 40 / PPW, 0);
     const uint32_t m = pw[0] & 255;
-    if (m >> 6) lf_reg<8>(px, m >> 6, lut[m & 63], bd);
+    if (m >> 6) lf_reg<8>(px, m >> 6, ev(0, m), bd);
     lf_pack<PIX>(rowp, px, 0, 8 / PPW, 0);
 }
 template <typename PIX>
-DEV void lf_row_narrow_2(uint32_t *rowp, const uint32_t *pw, const uint32_t *lut, int bd, int (&px)[40])
+DEV void lf_row_narrow_2(uint32_t *rowp, const uint32_t *pw, const uint32_t *lut, int bd, int (&px)[40], const LfEv<true, 16> &ev)
 {
     constexpr int PPW = 4 / sizeof(PIX);
     const uint32_t pc0 = pw[0], pc1 = pw[1];
@@ -1336,13 +1379,15 @@ DEV void lf_row_narrow_2(uint32_t *rowp, const uint32_t *pw, const uint32_t *lut
     lf_pack<PIX>(rowp, px, 8 / PPW, 40 / PPW, 8);
 }
 // row edges of one pixel column (tile pitch P)
-template <typename PIX, int P>
+template <typename PIX, int P, bool PF = false>
 DEV void lf_line_col_wide(PIX *colp, const uint32_t *pw, const uint32_t *lut, int bd)
 {
+    const uint32_t pw0 = pw[0], pw1 = pw[1], pw2 = pw[2], pw3 = pw[3];
+    LfEv<PF, 16> ev;
+    lf_eih_wide<PF>(ev, pw0, pw1, pw2, pw3, lut);
     int px[40];                    // rows -8..31, then 24..63 (as the column pass)
 #pragma unroll
     for (int i = 0; i < 40; i++) px[i] = colp[i * P];
-    const uint32_t pw0 = pw[0], pw1 = pw[1], pw2 = pw[2], pw3 = pw[3];
     LF_EDGE_WIDE(0, 0) LF_EDGE_WIDE(1, 0) LF_EDGE_WIDE(2, 0) LF_EDGE_WIDE(3, 0)
 #pragma unroll
     for (int i = 1; i < 32; i++) colp[i * P] = (PIX) px[i];
@@ -1354,13 +1399,15 @@ DEV void lf_line_col_wide(PIX *colp, const uint32_t *pw, const uint32_t *lut, in
 #pragma unroll
     for (int i = 0; i < 40; i++) colp[(32 + i) * P] = (PIX) px[i];
 }
-template <typename PIX, int P>
+template <typename PIX, int P, bool PF = false>
 DEV void lf_line_col_narrow(PIX *colp, const uint32_t *pw, const uint32_t *lut, int bd)
 {
+    const uint32_t pc0 = pw[0], pc1 = pw[1];
+    LfEv<PF, 8> ev;
+    lf_eih_narrow<PF>(ev, pc0, pc1, lut);
     int px[40];
 #pragma unroll
     for (int i = 0; i < 40; i++) px[i] = colp[i * P];
-    const uint32_t pc0 = pw[0], pc1 = pw[1];
     LF_EDGE_NARROW(0) LF_EDGE_NARROW(1) LF_EDGE_NARROW(2) LF_EDGE_NARROW(3)
     LF_EDGE_NARROW(4) LF_EDGE_NARROW(5) LF_EDGE_NARROW(6) LF_EDGE_NARROW(7)
 #pragma unroll
@@ -1392,7 +1439,7 @@ DEV uint32_t lf_eih(int L, int sharp, int bd)
 
 // The filter passes of one SB over its LDS tile: all column edges of every plane (lanes =
 // pixel rows), then all row edges (lanes = pixel columns). Ends with a barrier.
-template <typename PIX, class G, int NT, int PASSES = 3>
+template <typename PIX, class G, int NT, int PASSES = 3, bool PF = false>
 DEV void lf_passes_v(PIX *lt, PIX (*ct)[LfP<PIX, G>::CR * LfP<PIX, G>::UVP], const uint32_t *prog, const uint32_t *lut,
                      int lane, int bd)
 {
@@ -1404,13 +1451,13 @@ DEV void lf_passes_v(PIX *lt, PIX (*ct)[LfP<PIX, G>::CR * LfP<PIX, G>::UVP], con
     if (PASSES & 1) {
     for (int tid = lane; tid < 64 + 2 * CH; tid += NT) {
         if (tid < 64) {
-            lf_line_row_wide<PIX>((uint32_t *) (lt + (tid + 8) * FLP + XO), prog + (LFP_YC + (tid >> 3) * 16) / 4, lut, bd);
+            lf_line_row_wide<PIX, PF>((uint32_t *) (lt + (tid + 8) * FLP + XO), prog + (LFP_YC + (tid >> 3) * 16) / 4, lut, bd);
         } else {
             const int p = 1 + (tid - 64 >= CH), r = tid - 64 - (p - 1) * CH;
             uint32_t *rowp = (uint32_t *) (ct[p - 1] + (r + 8) * FCP + XO);
             const uint32_t *pw = prog + (LFP_CC + (r >> 3) * LFP_CSTRIDE(G::SH)) / 4;
-            if (G::SH) lf_line_row_narrow<PIX>(rowp, pw, lut, bd);
-            else lf_line_row_wide<PIX>(rowp, pw, lut, bd);
+            if (G::SH) lf_line_row_narrow<PIX, PF>(rowp, pw, lut, bd);
+            else lf_line_row_wide<PIX, PF>(rowp, pw, lut, bd);
         }
     }
     LF_SYNC();
@@ -1419,13 +1466,13 @@ DEV void lf_passes_v(PIX *lt, PIX (*ct)[LfP<PIX, G>::CR * LfP<PIX, G>::UVP], con
     if (PASSES & 2) {
     for (int tid = lane; tid < 64 + 2 * CW; tid += NT) {
         if (tid < 64) {
-            lf_line_col_wide<PIX, FLP>(lt + XL + tid, prog + (LFP_YR + (tid >> 3) * 16) / 4, lut, bd);
+            lf_line_col_wide<PIX, FLP, PF>(lt + XL + tid, prog + (LFP_YR + (tid >> 3) * 16) / 4, lut, bd);
         } else {
             const int p = 1 + (tid - 64 >= CW), c = tid - 64 - (p - 1) * CW;
             PIX *colp = ct[p - 1] + XL + c;
             const uint32_t *pw = prog + (LFP_CR(G::SH, G::SV) + (c >> 3) * LFP_CSTRIDE(G::SV)) / 4;
-            if (G::SV) lf_line_col_narrow<PIX, FCP>(colp, pw, lut, bd);
-            else lf_line_col_wide<PIX, FCP>(colp, pw, lut, bd);
+            if (G::SV) lf_line_col_narrow<PIX, FCP, PF>(colp, pw, lut, bd);
+            else lf_line_col_wide<PIX, FCP, PF>(colp, pw, lut, bd);
         }
     }
     LF_SYNC();
@@ -2053,6 +2100,7 @@ __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfrd(const uint32_t *__res
         // column pass part 1: every row's edge x = 0 (one row per lane)
         static_assert(64 + 2 * G::CH <= NT, "one column-pass row per filtering lane");
         int lpx[40];
+        LfEv<true, 16> lev;
         const bool cl = !mover && lane < 64 + 2 * G::CH, cwide = lane < 64 || !G::SH;
         uint32_t *rowp = nullptr;
         const uint32_t *pwl = nullptr;
@@ -2065,8 +2113,8 @@ __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfrd(const uint32_t *__res
                 rowp = (uint32_t *) (ct[p - 1] + (r + 8) * FCP + L::XO);
                 pwl = S.prog[tb] + (LFP_CC + (r >> 3) * LFP_CSTRIDE(G::SH)) / 4;
             }
-            if (cwide) lf_row_wide_1<PIX>(rowp, pwl, S.lut, bd, lpx);
-            else lf_row_narrow_1<PIX>(rowp, pwl, S.lut, bd, lpx);
+            if (cwide) lf_row_wide_1<PIX>(rowp, pwl, S.lut, bd, lpx, lev);
+            else lf_row_narrow_1<PIX>(rowp, pwl, S.lut, bd, lpx, lev);
         }
         __syncthreads();
         LFR_T(13);
@@ -2088,8 +2136,8 @@ __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfrd(const uint32_t *__res
         if (mover && c > c0) lfrd_store<PIX, G>(S, tb ^ 1, P, sbx - 1, sby, ml, false, 1);   // the rest of SB c - 1
         // column pass part 2
         if (cl) {
-            if (cwide) lf_row_wide_2<PIX>(rowp, pwl, S.lut, bd, lpx);
-            else lf_row_narrow_2<PIX>(rowp, pwl, S.lut, bd, lpx);
+            if (cwide) lf_row_wide_2<PIX>(rowp, pwl, S.lut, bd, lpx, lev);
+            else lf_row_narrow_2<PIX>(rowp, pwl, S.lut, bd, lpx, lev);
         }
         __syncthreads();
         LFR_T(2);
@@ -2128,7 +2176,7 @@ __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfrd(const uint32_t *__res
         }
         __syncthreads();
         LFR_T(3);
-        lf_passes_v<PIX, G, NT, 2>(lt, ct, S.prog[tb], S.lut, lane, bd);
+        lf_passes_v<PIX, G, NT, 2, true>(lt, ct, S.prog[tb], S.lut, lane, bd);
         LFR_T(4);
         if (LFR_PROF && !pre) pacc[5]++;
         if (LFR_PROF) pacc[6]++;

@@ -336,6 +336,28 @@ typedef struct vp9h_frame_info {
 int  vp9h_stream_decode(vp9h_stream *s, const uint8_t *data, size_t size, vp9h_frame *out,
                         vp9h_frame_info *info);
 
+/*
+ * The same parse in two steps, so consecutive frames of one stream overlap as the
+ * reference's frame threads do (ff_thread_finish_setup once the headers are parsed,
+ * vp9.c:1752-1754; the next frame then waits per SB row for this frame's MV pairs and
+ * segmentation map, vp9mvs.c:177-178, vp9block.c:116-117):
+ *   vp9h_stream_decode_begin parses the headers and advances the stream: the next frame's
+ *   begin may follow at once unless *serial is set (refresh_frame_context without
+ *   frame_parallel_decoding_mode: the next headers read the probabilities this frame's tiles
+ *   adapt, so its finish must complete first). *pending is NULL for show_existing_frame
+ *   (info says which slot). data must stay valid until finish.
+ *   vp9h_stream_decode_finish walks the tiles on `threads` tile-column threads, waiting for
+ *   the rows of the earlier frames' side buffers it reads, and frees the pending frame. The
+ *   finishes of one stream may run concurrently on different threads if each frame's finish
+ *   starts after the previous frame's finish has started.
+ * The packets equal vp9h_stream_decode's byte for byte (tests/c/host_san.cpp). A frame
+ * whose tiles fail makes the later frames that read its side buffers fail too. */
+typedef struct vp9h_pending vp9h_pending;
+int  vp9h_stream_decode_begin(vp9h_stream *s, const uint8_t *data, size_t size, vp9h_pending **pending,
+                              vp9h_frame_info *info, int *serial);
+int  vp9h_stream_decode_finish(vp9h_pending *pending, int threads, vp9h_frame *out);
+void vp9h_pending_free(vp9h_pending *pending);     /* a begun frame that will not be finished */
+
 /* Encoder choices for one frame (vp9h_enc_defaults: the SURVEY 8(d) stream settings). */
 typedef struct vp9h_enc_params {
     int32_t base_q_idx;

@@ -8,8 +8,10 @@
 //
 // 1. streams (key + inter frames, 1-8 tile columns, backward adaptation on and off, 8/10-bit,
 //    4:2:0 / 4:4:4) encoded by vp9h_stream_encode and parsed back: serially, with 2 / 3 / 8
-//    tile-column threads (vp9h_stream_set_threads) and through the parse pool
-//    (csrc/vp9hip_parse.h, 4 workers, several chains at once): every packet equal byte for byte;
+//    tile-column threads (vp9h_stream_set_threads), frame-pipelined (vp9h_stream_decode_begin /
+//    _finish: every frame's tiles on a thread of its own, started in order, waiting per SB row
+//    for the previous frame's side buffers) and through the parse pool (csrc/vp9hip_parse.h,
+//    4 workers, several chains at once, pipelined the same way): every packet equal byte for byte;
 // 2. the same streams with bit flips and truncations: every frame parses or fails with an
 //    error, nothing else;
 // 3. each FILE demuxed (vp9h_ivf_* / vp9h_webm_*) and parsed, then N_MUTATIONS mutated copies
@@ -18,6 +20,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <thread>
 #include <vector>
 
 #include "../../ffmpeg-hybrid_amd/csrc/vp9hip_parse.h"
@@ -108,6 +111,34 @@ static int parse_stream(const std::vector<Bytes> &s, int threads, std::vector<vp
     return err;
 }
 
+// frame-pipelined parse: each frame's headers on this thread in order, its tiles on a thread
+// of its own (tthreads tile-column threads each); a frame whose tiles adapt the next
+// headers' probabilities is finished before the next begin
+static int parse_pipelined(const std::vector<Bytes> &s, int tthreads, std::vector<vp9h_frame> *out)
+{
+    vp9h_stream *st = nullptr;
+    int r = vp9h_stream_open(&st);
+    if (r < 0) return r;
+    out->assign(s.size(), vp9h_frame());
+    for (auto &f : *out) memset(&f, 0, sizeof(f));
+    std::vector<int> rets(s.size(), 0);
+    std::vector<std::thread> th;
+    for (size_t i = 0; i < s.size(); i++) {
+        vp9h_pending *p = nullptr;
+        vp9h_frame_info info;
+        int serial = 0;
+        r = vp9h_stream_decode_begin(st, s[i].data(), s[i].size(), &p, &info, &serial);
+        if (r < 0 || !p) { rets[i] = r; continue; }
+        if (serial) rets[i] = vp9h_stream_decode_finish(p, tthreads, &(*out)[i]);
+        else th.emplace_back([p, tthreads, out, &rets, i] { rets[i] = vp9h_stream_decode_finish(p, tthreads, &(*out)[i]); });
+    }
+    for (auto &t : th) t.join();
+    vp9h_stream_close(st);
+    int err = 0;
+    for (int e : rets) if (e < 0 && !err) err = e;
+    return err;
+}
+
 static void free_all(std::vector<vp9h_frame> &v)
 {
     for (auto &f : v) vp9h_frame_free(&f);
@@ -134,6 +165,14 @@ static void check_streams(int nmut)
                 CHECK(same_packet(ser[i], thr[i]), "%dx%d tiles %d frame %zu: %d threads != serial", c.w, c.h,
                       1 << c.log2tc, i, t);
             free_all(thr);
+        }
+        for (int t : { 1, 3 }) {
+            std::vector<vp9h_frame> pip;
+            CHECK(parse_pipelined(s, t, &pip) == 0, "pipelined parse (%d tile threads)", t);
+            for (size_t i = 0; i < ser.size() && i < pip.size(); i++)
+                CHECK(same_packet(ser[i], pip[i]), "%dx%d adapt %d frame %zu: pipelined (%d) != serial", c.w, c.h, c.adapt,
+                      i, t);
+            free_all(pip);
         }
         free_all(ser);
         streams.push_back(std::move(s));

@@ -3,7 +3,9 @@
 `make -C ffmpeg-hybrid_amd/csrc sanitize` builds, from the library's own host sources and
 without HIP:
 - tests/c/host_san.cpp: streams encoded and parsed back serially, on 2 / 3 / 8 tile-column
-  threads and through the parse pool (every packet equal byte for byte), corrupted and
+  threads, frame-pipelined (headers in order, each frame's tiles on a thread of its own,
+  waiting per SB row for the previous frame's MVs; probability adaptation off and on,
+  use_last_frame_mvs set) and through the parse pool (every packet equal byte for byte), corrupted and
   truncated streams, IVF / WebM files demuxed, parsed and mutated;
 - the call-order harness (tests/c/hwaccel_harness.c) over csrc/vp9hip_hwaccel.cpp with
   tests/c/fake_device.cpp in place of the device (the oracle reconstructs on a worker thread,
