@@ -891,7 +891,7 @@ DEV void pred_pass(uint32_t w, int lane, PIX *tile, uint16_t *eb, int bd, const 
     const int lv = hleft ? l_px : base + 1;
     const int tl = (hleft & htop) ? tl_px : base + (htop ? 1 : -1);
     const int tr = htop ? tr_px : base - 1;
-    uint16_t *e = eb + 2 * m.gstart + 8 * m.jidx;
+    uint16_t *e = eb + 2 * m.gstart + 10 * m.jidx;  // 2n + 10 entries per job: n + 5 dwords, odd
     if (act && !(dbg & 16)) {
         e[li] = (uint16_t) lv;
         e[n + 1 + li] = (uint16_t) tv;
@@ -957,7 +957,8 @@ DEV void run_pass(uint32_t w, int lane, PIX *tile, uint16_t *eb, int bd, const P
 // LDS of one k_pred workgroup (one wavefront).
 template <typename PIX, class G> struct PredLds {
     PIX tile[PRED_K * G::TILE];
-    uint16_t eb[256];                 // per job 2n+8 edge pixels
+    uint16_t eb[288];                 // per job 2n+8 edge pixels at a pitch of 2n+10 (an odd dword
+                                      // count: the jobs' arrays start in different banks)
 #if PRED_LTAB_LDS
     uint32_t ltab[10 * 80];           // formula words of 4x4 and 8x8, all slots
 #endif
@@ -2629,6 +2630,210 @@ __global__ __launch_bounds__(NTH) void k_mc(const McUnit *__restrict__ units, in
     }
 }
 
+// --------------------------------------------------------------- k_mcp
+// Packed MC: the units of a workgroup as one flat list of lane tasks, R = 8 (R = 4 for
+// units 4 rows tall) vertically adjacent output pixels of one column per task, so a 4x4
+// chroma unit takes 4 lanes instead of a wave and every wave is full (k_mc gives each unit
+// a workgroup of its own: at C5 an 8K frame is ~243k units of ~26 tasks). The taps are the
+// task's unit's, per lane, and one separable 8-tap form gives every unscaled case exactly:
+// an identity phase is the tap 128 (an exact copy), so the copy and 1-D paths of
+// vp9dsp_template.c:1971-2059 equal the pixel-clipped 2-D form (2076-2113) with one
+// identity pass; the bilinear filter (2150-2227) is the 8-tap (0, 0, 0, 8(16 - m), 8m, 0,
+// 0, 0): a + ((m(b - a) + 8) >> 4) = ((16 - m)a + mb + 8) >> 4, scaled by 8, and its
+// values lie between a and b (the clip is an identity). Scaled references keep the
+// per-pixel sampler, one pixel per task.
+#define MCP_U 64                                  // units per workgroup
+struct McL {                                      // a unit as its tasks read it (LDS)
+    uint64_t ref[2], dst;
+    int32_t ix[2], iy[2];
+    int32_t pitch;
+    uint16_t x, y, rw[2], rh[2];
+    uint8_t lw, h, mx[2], my[2], filter, nref, direct, bd, cat, pad[3];
+};
+struct McpLds {
+    alignas(16) int16_t taps[64][8];              // [filter * 16 + phase], bilinear = filter 3
+    McL u[MCP_U];
+    uint32_t off[3][MCP_U + 1];                   // exclusive task offsets per category
+};
+
+// the last unit k < n with off[k] <= g (units without tasks of this category share the
+// next one's offset and are stepped over)
+DEV int mcp_find(const uint32_t *off, int n, uint32_t g)
+{
+    int k = 0;
+#pragma unroll
+    for (int st = MCP_U / 2; st; st >>= 1)
+        if (k + st < n && off[k + st] <= g) k += st;
+    return k;
+}
+
+template <typename PIX, int R, bool V>
+DEV void mcp_rows(const McL &u, const int16_t (*taps)[8], int xx, int yy)
+{
+    const int pmax = (1 << u.bd) - 1, pitch = u.pitch;
+    int out[R];
+    for (int k = 0; k < u.nref; k++) {
+        const uint4 hw = *(const uint4 *) taps[u.filter * 16 + u.mx[k]];
+        const uint4 vw = *(const uint4 *) taps[u.filter * 16 + u.my[k]];
+        const int fx[8] = { (int16_t) hw.x, (int) hw.x >> 16, (int16_t) hw.y, (int) hw.y >> 16,
+                            (int16_t) hw.z, (int) hw.z >> 16, (int16_t) hw.w, (int) hw.w >> 16 };
+        const int fy[8] = { (int16_t) vw.x, (int) vw.x >> 16, (int16_t) vw.y, (int) vw.y >> 16,
+                            (int16_t) vw.z, (int) vw.z >> 16, (int16_t) vw.w, (int) vw.w >> 16 };
+        constexpr int NR = V ? R + 7 : R, R0 = V ? 0 : 3;     // window rows the vertical pass reads
+        int hr[NR];
+        const int X = u.ix[k] + xx - 3, Y = u.iy[k] + yy - 3 + R0;
+        const PIX *rp = (const PIX *) u.ref[k];
+        if ((u.direct >> k) & 1) {                            // window inside the reference
+            typedef __attribute__((address_space(1))) const PIX gpix;
+            gpix *b = (gpix *) rp + (ptrdiff_t) Y * pitch + X;
+#pragma unroll
+            for (int j = 0; j < NR; j++) {
+                gpix *q = b + (ptrdiff_t) j * pitch;
+                int sh = 0;
+#pragma unroll
+                for (int t = 0; t < 8; t++) sh += fx[t] * (int) q[t];
+                hr[j] = med3_0((sh + 64) >> 7, pmax);
+            }
+        } else {                                              // emulated edge: every tap clamped
+            const int rw = u.rw[k], rh = u.rh[k];
+#pragma unroll
+            for (int j = 0; j < NR; j++) {
+                const int yc = Y + j < 0 ? 0 : Y + j >= rh ? rh - 1 : Y + j;
+                const PIX *q = rp + (size_t) yc * pitch;
+                int sh = 0;
+#pragma unroll
+                for (int t = 0; t < 8; t++) {
+                    const int xc = X + t < 0 ? 0 : X + t >= rw ? rw - 1 : X + t;
+                    sh += fx[t] * (int) q[xc];
+                }
+                hr[j] = med3_0((sh + 64) >> 7, pmax);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < R; t++) {
+            int v = hr[t];
+            if (V) {
+                int sv = 0;
+#pragma unroll
+                for (int q = 0; q < 8; q++) sv += fy[q] * hr[t + q];
+                v = med3_0((sv + 64) >> 7, pmax);
+            }
+            out[t] = k ? (out[t] + v + 1) >> 1 : v;
+        }
+    }
+    PIX *d = (PIX *) u.dst + (size_t) (u.y + yy) * pitch + u.x + xx;
+#pragma unroll
+    for (int t = 0; t < R; t++) d[(size_t) t * pitch] = (PIX) out[t];
+}
+
+template <typename PIX>
+__global__ __launch_bounds__(256) void k_mcp(const McUnit *__restrict__ units, int nunits,
+                                             const FrameDesc *__restrict__ frames)
+{
+    __shared__ McpLds S;
+    const int tid = threadIdx.x;
+    const int u0 = blockIdx.x * MCP_U, nu = nunits - u0 < MCP_U ? nunits - u0 : MCP_U;
+    {
+        // filter rows: 3 x 16 8-tap phases, then the bilinear ones as 8-taps
+        const int r = tid >> 2, q = (tid & 3) * 2;
+        int16_t a, b;
+        if (r < 48) { a = vp9t_subpel_filters[r >> 4][r & 15][q]; b = vp9t_subpel_filters[r >> 4][r & 15][q + 1]; }
+        else {
+            const int m = r & 15;
+            a = (int16_t) (q == 2 ? 0 : q == 4 ? 8 * m : 0);
+            b = (int16_t) (q == 2 ? 8 * (16 - m) : 0);
+        }
+        S.taps[r][q] = a;
+        S.taps[r][q + 1] = b;
+    }
+    uint32_t cnt[3] = { 0, 0, 0 };
+    if (tid < nu) {
+        const McUnit m = units[u0 + tid];
+        const FrameDesc &fd = frames[m.frame];
+        const int p = m.plane, c = p ? 1 : 0;
+        McL L;
+        L.dst = fd.plane[p];
+        L.pitch = fd.pitch[c];
+        L.x = m.x; L.y = m.y;
+        L.lw = (uint8_t) (31 - __builtin_clz((unsigned) m.w));
+        L.h = m.h;
+        L.filter = m.filter > 3 ? 3 : m.filter;
+        L.nref = m.nref;
+        L.bd = (uint8_t) fd.bd;
+        L.direct = 0;
+        bool scaled = false;
+        for (int k = 0; k < 2; k++) {
+            const int rf = m.ref[k] > 2 ? 0 : m.ref[k];
+            const McRef r = m.r[k];
+            L.ref[k] = fd.ref[rf][p];
+            L.ix[k] = r.ix; L.iy[k] = r.iy;
+            L.mx[k] = r.mx & 15; L.my[k] = r.my & 15;
+            L.rw[k] = (uint16_t) fd.refw[rf][c]; L.rh[k] = (uint16_t) fd.refh[rf][c];
+            if (k < m.nref) {
+                scaled |= r.dx != 16 || r.dy != 16;
+                if (r.ix >= 3 && r.iy >= 3 && r.ix + (int) m.w + 4 < fd.refw[rf][c] && r.iy + (int) m.h + 4 < fd.refh[rf][c])
+                    L.direct |= (uint8_t) (1 << k);
+            }
+        }
+        L.cat = scaled ? 2 : (m.h & 7) ? 1 : 0;
+        cnt[L.cat] = scaled ? (uint32_t) m.w * m.h : (uint32_t) m.w * m.h >> (L.cat ? 2 : 3);
+        S.u[tid] = L;
+    }
+    if (tid < 64) {
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            uint32_t v = cnt[c];
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t o = __shfl_up(v, d);
+                if (tid >= d) v += o;
+            }
+            S.off[c][tid + 1] = v;
+            if (tid == 0) S.off[c][0] = 0;
+        }
+    }
+    __syncthreads();
+    // R = 8 tasks, then R = 4; the vertical pass only where a lane of the wave needs it
+    for (int c = 0; c < 2; c++) {
+        const uint32_t T = S.off[c][nu];
+        for (uint32_t g = tid; g < T; g += 256) {
+            const int k = mcp_find(S.off[c], nu, g);
+            const McL &u = S.u[k];
+            const uint32_t ti = g - S.off[c][k];
+            const int xx = (int) (ti & ((1u << u.lw) - 1));
+            const int yy = (int) (ti >> u.lw) << (c ? 2 : 3);
+            const bool v = u.my[0] | (u.nref > 1 ? u.my[1] : 0);
+            if (c == 0) {
+                if (__any(v)) mcp_rows<PIX, 8, true>(u, S.taps, xx, yy);
+                else mcp_rows<PIX, 8, false>(u, S.taps, xx, yy);
+            } else {
+                if (__any(v)) mcp_rows<PIX, 4, true>(u, S.taps, xx, yy);
+                else mcp_rows<PIX, 4, false>(u, S.taps, xx, yy);
+            }
+        }
+    }
+    // scaled references: one pixel per task (mc_unit_pixels)
+    const uint32_t T2 = S.off[2][nu];
+    for (uint32_t g = tid; g < T2; g += 256) {
+        const int k = mcp_find(S.off[2], nu, g);
+        const McUnit m = units[u0 + k];
+        const FrameDesc &fd = frames[m.frame];
+        const int p = m.plane, c = p ? 1 : 0, W = m.w;
+        const uint32_t ti = g - S.off[2][k];
+        const int yy = (int) ti / W, xx = (int) ti - yy * W;
+        int out = 0;
+        for (int r = 0; r < m.nref; r++) {
+            const int rf = m.ref[r];
+            const McRef q = m.r[r];
+            const int px = q.mx + xx * q.dx, py = q.my + yy * q.dy;
+            const int v = mc_sample<PIX>((const PIX *) fd.ref[rf][p], fd.pitch[c], fd.refw[rf][c], fd.refh[rf][c],
+                                         q.ix + (px >> 4), q.iy + (py >> 4), px & 15, py & 15, m.filter, fd.bd);
+            out = r ? (out + v + 1) >> 1 : v;
+        }
+        ((PIX *) fd.plane[p])[(size_t) (m.y + yy) * fd.pitch[c] + m.x + xx] = (PIX) out;
+    }
+}
+
 // ------------------------------------------------------------ launchers
 template <int N, int TC>
 static void launch_resid_n(int hb, hipStream_t st, int n, const RJob *jobs, const FrameDesc *frames,
@@ -2897,6 +3102,15 @@ int vp9hip_launch_mc(int hb, hipStream_t st, int n, const McUnit *units, const F
     // unit busy; VP9HIP_MC64=0: 256 threads, as 8-bit, whose LDS passes need them)
     const char *e = getenv("VP9HIP_MC64");              // read per launch (tests switch it)
     const bool mc64 = !e || atoi(e);
+    // VP9HIP_MCP (default 1): the packed kernel for high bit depth; 2 also for 8-bit
+    const char *pe = getenv("VP9HIP_MCP");
+    const int mcp = pe ? atoi(pe) : 1;
+    if (mcp >= (hb ? 1 : 2)) {
+        const int nb = (n + MCP_U - 1) / MCP_U;
+        if (hb) hipLaunchKernelGGL((k_mcp<uint16_t>), dim3(nb), dim3(256), 0, st, units, n, frames);
+        else    hipLaunchKernelGGL((k_mcp<uint8_t>), dim3(nb), dim3(256), 0, st, units, n, frames);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     if (hb && mc64) hipLaunchKernelGGL((k_mc<uint16_t, 64>), dim3(n), dim3(64), 0, st, units, n, frames);
     else if (hb)    hipLaunchKernelGGL((k_mc<uint16_t, 256>), dim3(n), dim3(256), 0, st, units, n, frames);
     else            hipLaunchKernelGGL((k_mc<uint8_t, 256>), dim3(n), dim3(256), 0, st, units, n, frames);

@@ -267,14 +267,18 @@ __global__ __launch_bounds__(256) void k_pblk(PlanDev D)
 }
 
 // ------------------------------------------------------------------ k_psb
+// Residual-job counts: lane k holds key k's count, one ballot per distinct key of a chunk.
+// Intra unit map: each lane ORs into a column of its own (IBP row pitch 65 dwords: lane l
+// of word w at bank (w + l) mod 64, and the final column reduction, lane w reading word w's
+// 64 entries in step, is conflict-free too) -- no same-address LDS atomics.
+#define IBP 65
 template <int SSH, int SSV>
 __global__ __launch_bounds__(64) void k_psb(PlanDev D)
 {
     constexpr int CW = 16 >> SSH, CH = 16 >> SSV, JCAP = 256 + 2 * CW * CH;
     __shared__ vp9h_block blk[64];
     __shared__ uint32_t pre[3 * 64 + 1];
-    __shared__ uint32_t kc[24];
-    __shared__ uint32_t ib[24];
+    __shared__ uint32_t ibp[24 * IBP];
     const PlanFrame &F = D.frames[blockIdx.y];
     const int s = blockIdx.x, lane = threadIdx.x;
     if (s >= F.sb_cols * F.sb_rows) return;
@@ -282,7 +286,8 @@ __global__ __launch_bounds__(64) void k_psb(PlanDev D)
     const int cols = F.mc.cols, rows = F.mc.rows;
     uint32_t st = 0, b0;
     const int nb = sb_blocks(D, G.slot, b0, st);
-    if (lane < 24) { kc[lane] = 0; ib[lane] = 0; }
+#pragma unroll
+    for (int w = 0; w < 24; w++) ibp[w * IBP + lane] = 0;
     if (lane < nb) {
         const vp9h_block b = load_block(&D.blocks[b0 + lane]);
         blk[lane] = b;
@@ -290,27 +295,37 @@ __global__ __launch_bounds__(64) void k_psb(PlanDev D)
     wsync();
     const uint32_t tot = sb_prefix<SSH, SSV>(blk, nb, cols, rows, G.mine, pre, lane);
     const uint32_t T = pl_min((int) (tot & 1023), JCAP);
-    uint32_t ncoef = 0;
-    for (uint32_t t = lane; t < T; t += 64) {
-        const Tx tx = sb_tx<SSH, SSV>(blk, pre, nb, t, cols, rows);
-        const vp9h_block &b = blk[tx.b];
-        const int e = tx_eob(D, b, tx, pre, b0, st);
-        ncoef += (uint32_t) e;
-        int txtp = 0;
-        if (b.intra) {
-            const int mode = tx_mode(b, tx, st);
-            txtp = tx.p || tx.g.txs == 3 ? 0 : pl_intra_txfm_type(mode);
-        }
-        if (e && G.mine) atomicAdd(&kc[(F.lossless ? 4 : tx.g.txs) * 4 + txtp], 1u);
-        if (b.intra && G.mine) {            // the job's 4x4 units in the SB plane's unit map
-            const int sh = tx.p ? SSH : 0, sv = tx.p ? SSV : 0;
-            const int units = 16 >> sh, unitsv = 16 >> sv;
-            const int ux0 = ((tx.g.bx - G.sbx * (64 >> sh)) >> 2) + tx.x, uy0 = ((tx.g.by - G.sby * (64 >> sv)) >> 2) + tx.y;
-            for (int v = uy0; v < uy0 + tx.g.step && v < unitsv; v++) {
+    uint32_t ncoef = 0, kcnt = 0;
+    for (uint32_t t0 = 0; t0 < T; t0 += 64) {
+        const uint32_t t = t0 + (uint32_t) lane;
+        int key = -1;
+        if (t < T) {
+            const Tx tx = sb_tx<SSH, SSV>(blk, pre, nb, t, cols, rows);
+            const vp9h_block &b = blk[tx.b];
+            const int e = tx_eob(D, b, tx, pre, b0, st);
+            ncoef += (uint32_t) e;
+            int txtp = 0;
+            if (b.intra) {
+                const int mode = tx_mode(b, tx, st);
+                txtp = tx.p || tx.g.txs == 3 ? 0 : pl_intra_txfm_type(mode);
+            }
+            if (e && G.mine) key = (F.lossless ? 4 : tx.g.txs) * 4 + txtp;
+            if (b.intra && G.mine) {            // the job's 4x4 units in the SB plane's unit map
+                const int sh = tx.p ? SSH : 0, sv = tx.p ? SSV : 0;
+                const int units = 16 >> sh, unitsv = 16 >> sv;
+                const int ux0 = ((tx.g.bx - G.sbx * (64 >> sh)) >> 2) + tx.x, uy0 = ((tx.g.by - G.sby * (64 >> sv)) >> 2) + tx.y;
                 uint32_t m = 0;
                 for (int u = ux0; u < ux0 + tx.g.step && u < units; u++) m |= 1u << u;
-                atomicOr(&ib[tx.p * 8 + (v >> 1)], m << ((v & 1) * 16));
+                for (int v = uy0; v < uy0 + tx.g.step && v < unitsv; v++)
+                    atomicOr(&ibp[(tx.p * 8 + (v >> 1)) * IBP + lane], m << ((v & 1) * 16));
             }
+        }
+        uint64_t pend = __ballot(key >= 0);
+        while (pend) {
+            const int kk = rdl(key, __builtin_ctzll(pend));
+            const uint64_t m = __ballot(key == kk);
+            if (lane == kk) kcnt += (uint32_t) __popcll(m);
+            pend &= ~m;
         }
     }
     // MC units of the SB's inter blocks
@@ -322,15 +337,19 @@ __global__ __launch_bounds__(64) void k_psb(PlanDev D)
     nmc = wsum(nmc);
     ncoef = wsum(ncoef);
     wsync();
+    uint32_t ib = 0;
+    if (lane < 24)
+#pragma unroll 16
+        for (int j = 0; j < 64; j++) ib |= ibp[lane * IBP + j];
     if (lane < 20) {
         const uint32_t ci = cnt_idx(D, F, G.seg, G.slot, lane >> 2, lane & 3);
-        if (inb(D, ci, D.cap_cnt, 2u)) D.cnt[ci] = kc[lane];
+        if (inb(D, ci, D.cap_cnt, 2u)) D.cnt[ci] = kcnt;
     }
     if (lane == 20) {
         const uint32_t ci = D.seg_pre1[G.seg] + D.slot_pos[G.slot];
         if (inb(D, ci, D.cap_cntm, 2u)) D.cntm[ci] = nmc;
     }
-    if (lane < 24 && inb(D, G.slot, D.nslots, 4u)) D.ibits[(size_t) G.slot * 24 + lane] = ib[lane];
+    if (lane < 24 && inb(D, G.slot, D.nslots, 4u)) D.ibits[(size_t) G.slot * 24 + lane] = ib;
     if (lane == 0 && inb(D, G.dord, D.nslots, 8u)) D.sb_ncoef[G.dord] = ncoef;
     if (st) atomicOr(D.status, st);
 }

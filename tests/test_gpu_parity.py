@@ -69,8 +69,12 @@ INTER = [
 ]
 
 
+@pytest.mark.parametrize("mcp", ["1", "2", "0"])
 @pytest.mark.parametrize("w,h,bpp,kw", INTER)
-def test_inter_parity(v9, orc, gpu, w, h, bpp, kw):
+def test_inter_parity(v9, orc, gpu, monkeypatch, w, h, bpp, kw, mcp):
+    """VP9HIP_MCP: 1 (default) the packed MC kernel k_mcp for high bit depth, 2 for every
+    bit depth, 0 one workgroup per unit (k_mc)."""
+    monkeypatch.setenv("VP9HIP_MCP", mcp)
     key_kw = {k: x for k, x in kw.items() if k in ("log2_tile_cols",)}
     key = v9.SynthFrame(v9.synth_params(w, h, bpp, seed=11, **key_kw))
     ref0 = v9.alloc_planes(w, h, bpp)
@@ -327,10 +331,13 @@ SCALED = [
 ]
 
 
+@pytest.mark.parametrize("mcp", ["1", "2"])
 @pytest.mark.parametrize("rs,fs,bpp,kw", SCALED)
-def test_scaled_reference_parity(v9, orc, gpu, rs, fs, bpp, kw):
+def test_scaled_reference_parity(v9, orc, gpu, monkeypatch, rs, fs, bpp, kw, mcp):
     """Reference scaling (vp9recon.c:492-628, vp9.c:845-880): a keyframe at one size,
-    an inter frame at another size predicting from it."""
+    an inter frame at another size predicting from it (VP9HIP_MCP=2: k_mcp's per-pixel
+    tasks at 8 bits too)."""
+    monkeypatch.setenv("VP9HIP_MCP", mcp)
     (rw, rh), (w, h) = rs, fs
     key = v9.SynthFrame(v9.synth_params(rw, rh, bpp, seed=900))
     gpu.configure(max(rw, w), max(rh, h), bpp, nbufs=2)
