@@ -2695,11 +2695,12 @@ DEV void mcp_rows(const McL &u, const int16_t (*taps)[8], int xx, int yy)
                 hr[j] = med3_0((sh + 64) >> 7, pmax);
             }
         } else {                                              // emulated edge: every tap clamped
+            typedef __attribute__((address_space(1))) const PIX gpix;
             const int rw = u.rw[k], rh = u.rh[k];
 #pragma unroll
             for (int j = 0; j < NR; j++) {
                 const int yc = Y + j < 0 ? 0 : Y + j >= rh ? rh - 1 : Y + j;
-                const PIX *q = rp + (size_t) yc * pitch;
+                gpix *q = (gpix *) rp + (size_t) yc * pitch;
                 int sh = 0;
 #pragma unroll
                 for (int t = 0; t < 8; t++) {
@@ -2721,7 +2722,8 @@ DEV void mcp_rows(const McL &u, const int16_t (*taps)[8], int xx, int yy)
             out[t] = k ? (out[t] + v + 1) >> 1 : v;
         }
     }
-    PIX *d = (PIX *) u.dst + (size_t) (u.y + yy) * pitch + u.x + xx;
+    typedef __attribute__((address_space(1))) PIX gpo;
+    gpo *d = (gpo *) u.dst + (size_t) (u.y + yy) * pitch + u.x + xx;
 #pragma unroll
     for (int t = 0; t < R; t++) d[(size_t) t * pitch] = (PIX) out[t];
 }
@@ -3102,9 +3104,13 @@ int vp9hip_launch_mc(int hb, hipStream_t st, int n, const McUnit *units, const F
     // unit busy; VP9HIP_MC64=0: 256 threads, as 8-bit, whose LDS passes need them)
     const char *e = getenv("VP9HIP_MC64");              // read per launch (tests switch it)
     const bool mc64 = !e || atoi(e);
-    // VP9HIP_MCP (default 1): the packed kernel for high bit depth; 2 also for 8-bit
+    // VP9HIP_MCP: 2 (default) the packed kernel k_mcp at every bit depth, 1 for high bit
+    // depth only, 0 one workgroup per unit (k_mc). Measured (profiles/r04i, event-timed
+    // launches): C5 8K 10-bit 320 -> 219 us per frame, C2 1080p 8-bit 128 -> 61 us. An
+    // occupancy target of 6 waves / SIMD (78 VGPRs instead of 113) measured slower (325 us
+    // at C5): the rows of a task are all in flight at once only with the larger budget.
     const char *pe = getenv("VP9HIP_MCP");
-    const int mcp = pe ? atoi(pe) : 1;
+    const int mcp = pe ? atoi(pe) : 2;
     if (mcp >= (hb ? 1 : 2)) {
         const int nb = (n + MCP_U - 1) / MCP_U;
         if (hb) hipLaunchKernelGGL((k_mcp<uint16_t>), dim3(nb), dim3(256), 0, st, units, n, frames);

@@ -72,8 +72,8 @@ INTER = [
 @pytest.mark.parametrize("mcp", ["1", "2", "0"])
 @pytest.mark.parametrize("w,h,bpp,kw", INTER)
 def test_inter_parity(v9, orc, gpu, monkeypatch, w, h, bpp, kw, mcp):
-    """VP9HIP_MCP: 1 (default) the packed MC kernel k_mcp for high bit depth, 2 for every
-    bit depth, 0 one workgroup per unit (k_mc)."""
+    """VP9HIP_MCP: 2 (default) the packed MC kernel k_mcp at every bit depth, 1 for high
+    bit depth only, 0 one workgroup per unit (k_mc)."""
     monkeypatch.setenv("VP9HIP_MCP", mcp)
     key_kw = {k: x for k, x in kw.items() if k in ("log2_tile_cols",)}
     key = v9.SynthFrame(v9.synth_params(w, h, bpp, seed=11, **key_kw))
@@ -331,12 +331,12 @@ SCALED = [
 ]
 
 
-@pytest.mark.parametrize("mcp", ["1", "2"])
+@pytest.mark.parametrize("mcp", ["0", "2"])
 @pytest.mark.parametrize("rs,fs,bpp,kw", SCALED)
 def test_scaled_reference_parity(v9, orc, gpu, monkeypatch, rs, fs, bpp, kw, mcp):
     """Reference scaling (vp9recon.c:492-628, vp9.c:845-880): a keyframe at one size,
-    an inter frame at another size predicting from it (VP9HIP_MCP=2: k_mcp's per-pixel
-    tasks at 8 bits too)."""
+    an inter frame at another size predicting from it (k_mcp's per-pixel tasks, and
+    VP9HIP_MCP=0: k_mc)."""
     monkeypatch.setenv("VP9HIP_MCP", mcp)
     (rw, rh), (w, h) = rs, fs
     key = v9.SynthFrame(v9.synth_params(rw, rh, bpp, seed=900))

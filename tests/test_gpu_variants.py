@@ -1,6 +1,7 @@
 """The A/B switches of the inter-frame kernels stay bit-exact: the single-tile row LF
 (VP9HIP_LFR_DB=0 instead of k_lfrd), one workgroup per MC unit instead of the packed
-k_mcp (VP9HIP_MCP=0; 256 threads with VP9HIP_MC64=0), k_mcp for 8-bit (VP9HIP_MCP=2), one
+k_mcp (VP9HIP_MCP=0; 256 threads with VP9HIP_MC64=0; VP9HIP_MCP=1: k_mcp at high bit
+depth only), one
 residual launch per transform size (VP9HIP_RESID_MULTI=0), and frame pipelining
 (VP9HIP_LFMC=1: the next chain position's MC units as waiting tickets of k_lfrd, alone and
 with the single-tile k_lfr, where they run as a k_mc launch after it), and intra SBs reading
@@ -24,7 +25,8 @@ CASES = [
     ({"VP9HIP_LFR_DB": "0"}, "C5", 2),
     ({"VP9HIP_MC64": "0", "VP9HIP_MCP": "0"}, "C5", 2),
     ({"VP9HIP_MCP": "0"}, "C5", 2),
-    ({"VP9HIP_MCP": "2"}, "C2", 4),
+    ({"VP9HIP_MCP": "0"}, "C2", 4),
+    ({"VP9HIP_MCP": "1"}, "C2", 4),
     ({"VP9HIP_RESID_MULTI": "0"}, "C2", 4),
     ({"VP9HIP_RESID_MULTI": "0"}, "C5", 2),
     ({"VP9HIP_LFMC": "1"}, "C2", 6),
