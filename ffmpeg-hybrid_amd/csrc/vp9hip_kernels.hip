@@ -2207,6 +2207,313 @@ __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfrd(const uint32_t *__res
     lfrd_retire(ctr, ntasks, nmc, lane, NT + 64, &s_last);
 }
 
+// k_lfro: k_lfrd with SB c's luma row pass overlapped with SB c + 1's luma column pass
+// (4:2:0). Within one SB row the SBs are serial (vp9lpf.c:183-230 order: SB c + 1's first
+// column edge reads SB c's right columns after SB c's row edges), but the dependency is per
+// pixel row: the column pass of pixel rows 0..31 of SB c + 1 needs SB c's row pass only
+// through its row edges y = 32 / 36 (later row edges read rows >= 32), rows 32..63 all of
+// it; SB c + 1's row edges y <= 28 read rows <= 35 only after the column pass of rows
+// 0..31... (and its edges y >= 32 the rest). So the luma column pass runs as two waves of 32
+// rows each (H0: rows 0..31, H1: rows 32..63) and the row pass as one wave (R), each
+// starting as soon as the pixel rows it reads are final: the luma chain per SB is about
+// half a row pass + a column pass instead of a column pass + a row pass. Chroma (both
+// planes, both passes: half the luma edges) runs on one wave of its own (C), a loader wave
+// (L) stages interiors, program words and top halos, the store wave (S) writes the tiles
+// and publishes the row hand-off as k_lfrd does. The waves order through monotonic
+// per-workgroup counters in LDS (a wave's DS operations execute in order, so a counter
+// written after a tile write and read before the tile read orders them; the fences are
+// compiler-only, wavefront scope). Every wait is bounded: one that gives up is counted in
+// ctr[2] like a hand-off timeout (the batch fails with VP9HIP_EBUG), never hangs.
+#define LFRO_NTH 384                              // R, H0, H1, C, L, S
+struct LfroSync { uint32_t ld_int, ld_top, ra, rb, h0x, h1x, h0, h1, cx, c, st, abort, pad[4]; };
+DEV void lfro_pub(uint32_t *f, uint32_t v)
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// (after a wait gives up, `abort` makes every later wait of the workgroup return at once:
+// the task drains in one bounded wait instead of one per SB and counter)
+DEV void lfro_wait(uint32_t *f, uint32_t need, uint32_t *ctr, uint32_t *abort)
+{
+    for (uint32_t n = 0; __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need; n++) {
+        if (n > (1u << 20) || __hip_atomic_load(abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+            if ((threadIdx.x & 63) == 0 && !__hip_atomic_exchange(abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+                atomicAdd(&ctr[2], 1u);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// the store wave's tile parts: 0 the left chunk column's bottom 8 rows (SB sbx - 1's last
+// columns, final after this SB's first column edges; sc1), 1 the other bottom rows (sc1;
+// the last chunk column only for the row's last SB: otherwise the next tile's part 0),
+// 2 everything else (the top halo's corner chunk is never modified)
+template <typename PIX, class G>
+DEV void lfro_store(const LfrLds<PIX, G> &S, int tb, const LfrPlanes &P, int sbx, int sby, int ml, bool last, int part)
+{
+    typedef LfP<PIX, G> L;
+    typedef Chunk16::T CT;
+    for (int ci = ml; ci < L::NCHUNK; ci += 64) {
+        int p, r, k;
+        lf_chunk<PIX, G>(ci, p, r, k);
+        const int nk = p ? L::CK : L::YK, nr = p ? L::CR : 72;
+        const bool bot = r >= nr - 8;
+        bool st;
+        if (part == 0) st = bot && k == 0 && sbx > 0;
+        else if (part == 1) st = bot && k > 0 && (k < nk - 1 || last);
+        else st = !bot && (r >= 8 ? (k > 0 || sbx > 0) && (k < nk - 1 || last) : k > 0 && sby > 0);
+        if (!st) continue;
+        const PIX *t = (p ? S.ct[tb][p - 1] + r * L::UVP : S.lt[tb] + r * L::YP) + L::CPX * k;
+        const CT w = Chunk16::from_lds(t);
+        PIX *g = lfr_addr<PIX, G>(P, sbx, sby, p, r, k);
+        if (part < 2) {
+            st_sc1(g, (uint64_t) w.x | (uint64_t) w.y << 32);
+            st_sc1((char *) g + 8, (uint64_t) w.z | (uint64_t) w.w << 32);
+        } else {
+            v4u x; x.x = w.x; x.y = w.y; x.z = w.z; x.w = w.w;
+            *(gv4u *) g = x;
+        }
+    }
+}
+#define LFRO_EDGE_WIDE(k, C0)                                                                            \
+    {                                                                                                    \
+        const uint32_t ww = (k) < 2 ? pw0 : (k) < 4 ? pw1 : (k) < 6 ? pw2 : pw3;                         \
+        const uint32_t m = (ww >> (16 * ((k) & 1))) & 255, in = (ww >> (16 * ((k) & 1) + 8)) & 255;      \
+        if (m >> 6) lf_reg<8 * (k) + 8 - (C0)>(px, m >> 6, ev(2 * (k), m), bd);                          \
+        if (in) lf_reg<8 * (k) + 12 - (C0)>(px, 1, ev(2 * (k) + 1, in), bd);                             \
+    }
+template <typename PIX, class G>
+__global__ __launch_bounds__(LFRO_NTH) void k_lfro(const uint32_t *__restrict__ tasks, const LFRec *__restrict__ recs,
+                                                   const FrameDesc *__restrict__ frames, uint32_t *ctr, int ntasks)
+{
+    static_assert(G::SH == 1 && G::SV == 1, "4:2:0: one chroma wave holds both planes' 32 lines");
+    typedef LfP<PIX, G> L;
+    typedef Chunk16::T CT;
+    typedef LfrdN<PIX, G> N;
+    constexpr int FLP = L::YP, FCP = L::UVP, CW = G::CW, CH = G::CH;
+    constexpr int NUI = (N::NINT + 63) / 64, NUT = (N::NTOP + 63) / 64, NPW = (L::PROG / 4 + 63) / 64;
+    __shared__ LfrLds<PIX, G> S;
+    __shared__ LfroSync F;
+    __shared__ uint32_t s_task, s_last;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    uint32_t *const progress = ctr + 4;
+    __builtin_amdgcn_s_setprio(3);
+    if (tid == 0) s_task = atomicAdd(&ctr[0], 1u);
+    if (tid < 16) (&F.ld_int)[tid] = 0;
+    __syncthreads();
+    const uint32_t spin = ctr[3] ? ctr[3] : (1u << 22);
+    const uint32_t *T = tasks + tasks[s_task];
+    const uint32_t dep = T[0], ncols = T[1], c0 = T[2];
+    const LFRec &rec0 = recs[T[4]];
+    const FrameDesc &fd = frames[rec0.frame];
+    const int bd = fd.bd, sby = rec0.sby;
+    LfrPlanes P;
+    P.b0 = fd.plane[0]; P.d1 = fd.plane[1] - P.b0; P.d2 = fd.plane[2] - P.b0;
+    P.pit0 = fd.pitch[0]; P.pit1 = fd.pitch[1];
+    for (int i = tid; i < 64; i += LFRO_NTH) S.lut[i] = lf_eih(i, fd.sharp, bd);
+    __syncthreads();
+    const int n = (int) (ncols - c0);
+    if (w == 0) {
+        // ---- R: luma row edges, one lane per pixel column (lf_line_col_wide split at its
+        // halves, each waiting for the column pass of the rows it loads)
+        for (int i = 0; i < n; i++) {
+            const int tb = i & 1;
+            PIX *colp = S.lt[tb] + L::XL + lane;
+            lfro_wait(&F.ld_top, (uint32_t) i + 1, ctr, &F.abort);
+            lfro_wait(&F.h0, (uint32_t) i + 1, ctr, &F.abort);
+            const uint32_t *pw = S.prog[tb] + (LFP_YR + (lane >> 3) * 16) / 4;
+            const uint32_t pw0 = pw[0], pw1 = pw[1], pw2 = pw[2], pw3 = pw[3];
+            LfEv<true, 16> ev;
+            lf_eih_wide<true>(ev, pw0, pw1, pw2, pw3, S.lut);
+            int px[40];
+#pragma unroll
+            for (int r = 0; r < 40; r++) px[r] = colp[r * FLP];
+            LFRO_EDGE_WIDE(0, 0) LFRO_EDGE_WIDE(1, 0) LFRO_EDGE_WIDE(2, 0) LFRO_EDGE_WIDE(3, 0)
+#pragma unroll
+            for (int r = 1; r < 32; r++) colp[r * FLP] = (PIX) px[r];
+#pragma unroll
+            for (int r = 0; r < 8; r++) px[r] = px[32 + r];
+            lfro_wait(&F.h1, (uint32_t) i + 1, ctr, &F.abort);
+#pragma unroll
+            for (int r = 8; r < 40; r++) px[r] = colp[(32 + r) * FLP];
+            LFRO_EDGE_WIDE(4, 32)
+            // pixel rows 24..31 are final (later row edges read rows >= 32): SB c + 1's
+            // column pass of rows 0..31 may start
+#pragma unroll
+            for (int r = 0; r < 8; r++) colp[(32 + r) * FLP] = (PIX) px[r];
+            lfro_pub(&F.ra, (uint32_t) i + 1);
+            LFRO_EDGE_WIDE(5, 32) LFRO_EDGE_WIDE(6, 32) LFRO_EDGE_WIDE(7, 32)
+#pragma unroll
+            for (int r = 8; r < 40; r++) colp[(32 + r) * FLP] = (PIX) px[r];
+            lfro_pub(&F.rb, (uint32_t) i + 1);
+        }
+    } else if (w <= 2) {
+        // ---- H0 / H1: luma column edges of pixel rows 0..31 / 32..63, one lane per row
+        const int h = w - 1;
+        if (lane < 32) {
+            const int row = h * 32 + lane;
+            for (int i = 0; i < n; i++) {
+                const int tb = i & 1;
+                lfro_wait(&F.ld_int, (uint32_t) i + 1, ctr, &F.abort);
+                if (i > 0) lfro_wait(h ? &F.rb : &F.ra, (uint32_t) i, ctr, &F.abort);
+                PIX *trow = S.lt[tb] + (row + 8) * FLP;
+                // left halo: SB c - 1's last chunk, final for these rows now
+                if (i > 0) Chunk16::to_lds(Chunk16::from_lds(S.lt[tb ^ 1] + (row + 8) * FLP + 64), trow);
+                uint32_t *rowp = (uint32_t *) (trow + L::XO);
+                const uint32_t *pwl = S.prog[tb] + (LFP_YC + (row >> 3) * 16) / 4;
+                int lpx[40];
+                LfEv<true, 16> lev;
+                lf_row_wide_1<PIX>(rowp, pwl, S.lut, bd, lpx, lev);
+                lfro_pub(h ? &F.h1x : &F.h0x, (uint32_t) i + 1);
+                lf_row_wide_2<PIX>(rowp, pwl, S.lut, bd, lpx, lev);
+                lfro_pub(h ? &F.h1 : &F.h0, (uint32_t) i + 1);
+            }
+        }
+    } else if (w == 3) {
+        // ---- C: chroma, both planes: column edges (lane = row), then row edges (lane = column)
+        const int p = 1 + (lane >= CH), r = lane & (CH - 1);
+        for (int i = 0; i < n; i++) {
+            const int tb = i & 1;
+            lfro_wait(&F.ld_int, (uint32_t) i + 1, ctr, &F.abort);
+            PIX *trow = S.ct[tb][p - 1] + (r + 8) * FCP;
+            if (i > 0) Chunk16::to_lds(Chunk16::from_lds(S.ct[tb ^ 1][p - 1] + (r + 8) * FCP + CW), trow);
+            uint32_t *rowp = (uint32_t *) (trow + L::XO);
+            const uint32_t *pwc = S.prog[tb] + (LFP_CC + (r >> 3) * LFP_CSTRIDE(1)) / 4;
+            int lpx[40];
+            LfEv<true, 16> lev;
+            lf_row_narrow_1<PIX>(rowp, pwc, S.lut, bd, lpx, lev);
+            lfro_pub(&F.cx, (uint32_t) i + 1);
+            lf_row_narrow_2<PIX>(rowp, pwc, S.lut, bd, lpx, lev);
+            wave_sync();
+            lfro_wait(&F.ld_top, (uint32_t) i + 1, ctr, &F.abort);
+            PIX *colp = S.ct[tb][p - 1] + L::XL + r;
+            const uint32_t *pwr = S.prog[tb] + (LFP_CR(1, 1) + (r >> 3) * LFP_CSTRIDE(1)) / 4;
+            lf_line_col_narrow<PIX, FCP, true>(colp, pwr, S.lut, bd);
+            lfro_pub(&F.c, (uint32_t) i + 1);
+        }
+    } else if (w == 4) {
+        // ---- L: interiors (+ program words) one SB ahead, top halos after the row above
+        CT vi[NUI], vt[NUT];
+        uint32_t pwv[NPW];
+        auto issue = [&](int c, bool halo) {
+#pragma unroll
+            for (int u = 0; u < NUI; u++) {
+                const int ci = lane + 64 * u;
+                int pp, rr, kk;
+                lfrd_chunk<PIX, G>(ci, false, pp, rr, kk);
+                if (ci < N::NINT && (kk > 0 || halo)) {
+                    const v4u x = *(const gv4u *) lfr_addr<PIX, G>(P, c, sby, pp, rr, kk);
+                    vi[u] = make_uint4(x.x, x.y, x.z, x.w);
+                }
+            }
+            const LFRec &rc = recs[T[4 + c - c0]];
+#pragma unroll
+            for (int q = 0; q < NPW; q++)
+                if (lane + 64 * q < L::PROG / 4) pwv[q] = ((const uint32_t *) rc.prog)[lane + 64 * q];
+        };
+        auto stage = [&](int tb, bool halo) {
+#pragma unroll
+            for (int u = 0; u < NUI; u++) {
+                const int ci = lane + 64 * u;
+                int pp, rr, kk;
+                lfrd_chunk<PIX, G>(ci, false, pp, rr, kk);
+                if (ci < N::NINT && (kk > 0 || halo))
+                    Chunk16::to_lds(vi[u], (pp ? S.ct[tb][pp - 1] + rr * FCP : S.lt[tb] + rr * FLP) + L::CPX * kk);
+            }
+#pragma unroll
+            for (int q = 0; q < NPW; q++)
+                if (lane + 64 * q < L::PROG / 4) S.prog[tb][lane + 64 * q] = pwv[q];
+        };
+        issue((int) c0, c0 > 0);
+        stage(0, c0 > 0);
+        lfro_pub(&F.ld_int, 1u);
+        uint32_t seen = T[3];
+        for (int i = 0; i < n; i++) {
+            const uint32_t c = c0 + (uint32_t) i;
+            const int tb = i & 1;
+            if (i + 1 < n) issue((int) c + 1, false);
+            // the row above hands over SB c's top halo once its progress reaches c + 1
+            // (k_lfr's hand-off: sc1 stores drained before the progress word; sc1 loads here)
+            if (dep != ~0u && seen < c + 1) {
+                for (uint32_t k = 0;; k++) {
+                    seen = __builtin_amdgcn_readfirstlane(
+                        __hip_atomic_load((gu32 *) &progress[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                    if (seen >= c + 1) break;
+                    if (k > spin) {
+                        if (lane == 0) atomicAdd(&ctr[2], 1u);
+                        seen = c + 1;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+            if (sby > 0) {
+#pragma unroll
+                for (int u = 0; u < NUT; u++) {
+                    const int ci = lane + 64 * u;
+                    int pp, rr, kk;
+                    lfrd_chunk<PIX, G>(ci, true, pp, rr, kk);
+                    if (ci >= N::NTOP || kk == 0) continue;
+                    const PIX *g = lfr_addr<PIX, G>(P, (int) c, sby, pp, rr, kk);
+                    const uint64_t lo = ld_sc1(g), hi = ld_sc1((const char *) g + 8);
+                    vt[u] = make_uint4((uint32_t) lo, (uint32_t) (lo >> 32), (uint32_t) hi, (uint32_t) (hi >> 32));
+                }
+#pragma unroll
+                for (int u = 0; u < NUT; u++) {
+                    const int ci = lane + 64 * u;
+                    int pp, rr, kk;
+                    lfrd_chunk<PIX, G>(ci, true, pp, rr, kk);
+                    if (ci >= N::NTOP || kk == 0) continue;
+                    Chunk16::to_lds(vt[u], (pp ? S.ct[tb][pp - 1] + rr * FCP : S.lt[tb] + rr * FLP) + L::CPX * kk);
+                }
+            }
+            lfro_pub(&F.ld_top, (uint32_t) i + 1);
+            if (i + 1 < n) {
+                // tile tb ^ 1 is free once the store wave is done with SB c - 1 and SB c's
+                // waves have copied their left halos out of it
+                lfro_wait(&F.st, (uint32_t) i, ctr, &F.abort);
+                lfro_wait(&F.h0x, (uint32_t) i + 1, ctr, &F.abort);
+                lfro_wait(&F.h1x, (uint32_t) i + 1, ctr, &F.abort);
+                lfro_wait(&F.cx, (uint32_t) i + 1, ctr, &F.abort);
+                stage(tb ^ 1, false);
+                lfro_pub(&F.ld_int, (uint32_t) i + 2);
+            }
+        }
+    } else {
+        // ---- S: tiles to HBM, the row hand-off (progress word of this task)
+        for (int i = 0; i < n; i++) {
+            const int c = (int) c0 + i, tb = i & 1;
+            const bool last = i == n - 1;
+            if (c > 0) {
+                // SB c - 1's last columns (this tile's left halo) are final after this SB's
+                // first column edges: its bottom rows are then complete
+                lfro_wait(&F.h1x, (uint32_t) i + 1, ctr, &F.abort);
+                lfro_wait(&F.cx, (uint32_t) i + 1, ctr, &F.abort);
+                lfro_store<PIX, G>(S, tb, P, c, sby, lane, false, 0);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (lane == 0) __hip_atomic_store((gu32 *) &progress[s_task], (uint32_t) c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            lfro_wait(&F.rb, (uint32_t) i + 1, ctr, &F.abort);
+            lfro_wait(&F.c, (uint32_t) i + 1, ctr, &F.abort);
+            lfro_wait(&F.h0x, (uint32_t) i + 1, ctr, &F.abort);
+            lfro_store<PIX, G>(S, tb, P, c, sby, lane, last, 1);
+            if (last) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (lane == 0) __hip_atomic_store((gu32 *) &progress[s_task], ncols, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            lfro_store<PIX, G>(S, tb, P, c, sby, lane, last, 2);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            lfro_pub(&F.st, (uint32_t) i + 1);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    lfrd_retire(ctr, ntasks, 0, tid, LFRO_NTH, &s_last);
+}
+#undef LFRO_EDGE_WIDE
+
 // Residual arithmetic types per pixel type: 8-bit int16 coefficients / 32-bit math,
 // high bit depth int32 coefficients / 64-bit math (vp9dsp_template.c dctcoef / dctint)
 template <typename PIX> struct RT;
@@ -2895,6 +3202,14 @@ static void launch_lfr_g(hipStream_t st, int ntasks, const uint32_t *tasks, cons
     const char *e = getenv("VP9HIP_LFR_DB");          // read per launch (tests switch it)
     const bool db = !e || atoi(e);
     if (db) {
+        if constexpr (G::SH == 1 && G::SV == 1) {
+            // VP9HIP_LFRO=0: k_lfrd instead of the band-overlapped k_lfro (4:2:0, no MC tickets)
+            const char *o = getenv("VP9HIP_LFRO");
+            if (!nmc && (!o || atoi(o))) {
+                hipLaunchKernelGGL((k_lfro<PIX, G>), dim3(ntasks), dim3(LFRO_NTH), 0, st, tasks, recs, frames, ctr, ntasks);
+                return;
+            }
+        }
         hipLaunchKernelGGL((k_lfrd<PIX, G>), dim3(ntasks + nmc), dim3(LfNT<G>::NT + 64), 0, st, tasks, recs, frames, ctr, ntasks,
                            mcu, nmc, mw);
         return;
