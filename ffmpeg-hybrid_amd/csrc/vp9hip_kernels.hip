@@ -3203,9 +3203,9 @@ static void launch_lfr_g(hipStream_t st, int ntasks, const uint32_t *tasks, cons
     const bool db = !e || atoi(e);
     if (db) {
         if constexpr (G::SH == 1 && G::SV == 1) {
-            // VP9HIP_LFRO=0: k_lfrd instead of the band-overlapped k_lfro (4:2:0, no MC tickets)
+            // VP9HIP_LFRO=1: the band-overlapped k_lfro instead of k_lfrd (4:2:0, no MC tickets)
             const char *o = getenv("VP9HIP_LFRO");
-            if (!nmc && (!o || atoi(o))) {
+            if (!nmc && o && atoi(o)) {
                 hipLaunchKernelGGL((k_lfro<PIX, G>), dim3(ntasks), dim3(LFRO_NTH), 0, st, tasks, recs, frames, ctr, ntasks);
                 return;
             }
