@@ -2233,8 +2233,9 @@ DEV void lfro_pub(uint32_t *f, uint32_t v)
 }
 // (after a wait gives up, `abort` makes every later wait of the workgroup return at once:
 // the task drains in one bounded wait instead of one per SB and counter)
-DEV void lfro_wait(uint32_t *f, uint32_t need, uint32_t *ctr, uint32_t *abort)
+DEV void lfro_wait(uint32_t *f, uint32_t need, uint32_t *ctr, uint32_t *abort, uint64_t &wc)
 {
+    const uint64_t t0 = LFR_PROF ? clock64() : 0;
     for (uint32_t n = 0; __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need; n++) {
         if (n > (1u << 20) || __hip_atomic_load(abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
             if ((threadIdx.x & 63) == 0 && !__hip_atomic_exchange(abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
@@ -2244,6 +2245,7 @@ DEV void lfro_wait(uint32_t *f, uint32_t need, uint32_t *ctr, uint32_t *abort)
         __builtin_amdgcn_s_sleep(1);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (LFR_PROF) wc += clock64() - t0;
 }
 // the store wave's tile parts: 0 the left chunk column's bottom 8 rows (SB sbx - 1's last
 // columns, final after this SB's first column edges; sc1), 1 the other bottom rows (sc1;
@@ -2300,6 +2302,10 @@ __global__ __launch_bounds__(LFRO_NTH) void k_lfro(const uint32_t *__restrict__ 
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     uint32_t *const progress = ctr + 4;
     __builtin_amdgcn_s_setprio(3);
+    // LFR_PROF builds: per wave role, cycles waiting on the workgroup's counters (lfr_prof[w])
+    // and lifetime (lfr_prof[6 + w]); the loader's waits for the row above: lfr_prof[12]
+    uint64_t wc = 0, wrow = 0;
+    const uint64_t tk0 = LFR_PROF ? clock64() : 0;
     if (tid == 0) s_task = atomicAdd(&ctr[0], 1u);
     if (tid < 16) (&F.ld_int)[tid] = 0;
     __syncthreads();
@@ -2321,8 +2327,8 @@ __global__ __launch_bounds__(LFRO_NTH) void k_lfro(const uint32_t *__restrict__ 
         for (int i = 0; i < n; i++) {
             const int tb = i & 1;
             PIX *colp = S.lt[tb] + L::XL + lane;
-            lfro_wait(&F.ld_top, (uint32_t) i + 1, ctr, &F.abort);
-            lfro_wait(&F.h0, (uint32_t) i + 1, ctr, &F.abort);
+            lfro_wait(&F.ld_top, (uint32_t) i + 1, ctr, &F.abort, wc);
+            lfro_wait(&F.h0, (uint32_t) i + 1, ctr, &F.abort, wc);
             const uint32_t *pw = S.prog[tb] + (LFP_YR + (lane >> 3) * 16) / 4;
             const uint32_t pw0 = pw[0], pw1 = pw[1], pw2 = pw[2], pw3 = pw[3];
             LfEv<true, 16> ev;
@@ -2335,7 +2341,7 @@ __global__ __launch_bounds__(LFRO_NTH) void k_lfro(const uint32_t *__restrict__ 
             for (int r = 1; r < 32; r++) colp[r * FLP] = (PIX) px[r];
 #pragma unroll
             for (int r = 0; r < 8; r++) px[r] = px[32 + r];
-            lfro_wait(&F.h1, (uint32_t) i + 1, ctr, &F.abort);
+            lfro_wait(&F.h1, (uint32_t) i + 1, ctr, &F.abort, wc);
 #pragma unroll
             for (int r = 8; r < 40; r++) px[r] = colp[(32 + r) * FLP];
             LFRO_EDGE_WIDE(4, 32)
@@ -2356,8 +2362,8 @@ __global__ __launch_bounds__(LFRO_NTH) void k_lfro(const uint32_t *__restrict__ 
             const int row = h * 32 + lane;
             for (int i = 0; i < n; i++) {
                 const int tb = i & 1;
-                lfro_wait(&F.ld_int, (uint32_t) i + 1, ctr, &F.abort);
-                if (i > 0) lfro_wait(h ? &F.rb : &F.ra, (uint32_t) i, ctr, &F.abort);
+                lfro_wait(&F.ld_int, (uint32_t) i + 1, ctr, &F.abort, wc);
+                if (i > 0) lfro_wait(h ? &F.rb : &F.ra, (uint32_t) i, ctr, &F.abort, wc);
                 PIX *trow = S.lt[tb] + (row + 8) * FLP;
                 // left halo: SB c - 1's last chunk, final for these rows now
                 if (i > 0) Chunk16::to_lds(Chunk16::from_lds(S.lt[tb ^ 1] + (row + 8) * FLP + 64), trow);
@@ -2376,7 +2382,7 @@ __global__ __launch_bounds__(LFRO_NTH) void k_lfro(const uint32_t *__restrict__ 
         const int p = 1 + (lane >= CH), r = lane & (CH - 1);
         for (int i = 0; i < n; i++) {
             const int tb = i & 1;
-            lfro_wait(&F.ld_int, (uint32_t) i + 1, ctr, &F.abort);
+            lfro_wait(&F.ld_int, (uint32_t) i + 1, ctr, &F.abort, wc);
             PIX *trow = S.ct[tb][p - 1] + (r + 8) * FCP;
             if (i > 0) Chunk16::to_lds(Chunk16::from_lds(S.ct[tb ^ 1][p - 1] + (r + 8) * FCP + CW), trow);
             uint32_t *rowp = (uint32_t *) (trow + L::XO);
@@ -2387,7 +2393,7 @@ __global__ __launch_bounds__(LFRO_NTH) void k_lfro(const uint32_t *__restrict__ 
             lfro_pub(&F.cx, (uint32_t) i + 1);
             lf_row_narrow_2<PIX>(rowp, pwc, S.lut, bd, lpx, lev);
             wave_sync();
-            lfro_wait(&F.ld_top, (uint32_t) i + 1, ctr, &F.abort);
+            lfro_wait(&F.ld_top, (uint32_t) i + 1, ctr, &F.abort, wc);
             PIX *colp = S.ct[tb][p - 1] + L::XL + r;
             const uint32_t *pwr = S.prog[tb] + (LFP_CR(1, 1) + (r >> 3) * LFP_CSTRIDE(1)) / 4;
             lf_line_col_narrow<PIX, FCP, true>(colp, pwr, S.lut, bd);
@@ -2437,6 +2443,7 @@ __global__ __launch_bounds__(LFRO_NTH) void k_lfro(const uint32_t *__restrict__ 
             // the row above hands over SB c's top halo once its progress reaches c + 1
             // (k_lfr's hand-off: sc1 stores drained before the progress word; sc1 loads here)
             if (dep != ~0u && seen < c + 1) {
+                const uint64_t tw0 = LFR_PROF ? clock64() : 0;
                 for (uint32_t k = 0;; k++) {
                     seen = __builtin_amdgcn_readfirstlane(
                         __hip_atomic_load((gu32 *) &progress[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -2449,6 +2456,7 @@ __global__ __launch_bounds__(LFRO_NTH) void k_lfro(const uint32_t *__restrict__ 
                     __builtin_amdgcn_s_sleep(1);
                 }
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if (LFR_PROF) wrow += clock64() - tw0;
             }
             if (sby > 0) {
 #pragma unroll
@@ -2474,10 +2482,10 @@ __global__ __launch_bounds__(LFRO_NTH) void k_lfro(const uint32_t *__restrict__ 
             if (i + 1 < n) {
                 // tile tb ^ 1 is free once the store wave is done with SB c - 1 and SB c's
                 // waves have copied their left halos out of it
-                lfro_wait(&F.st, (uint32_t) i, ctr, &F.abort);
-                lfro_wait(&F.h0x, (uint32_t) i + 1, ctr, &F.abort);
-                lfro_wait(&F.h1x, (uint32_t) i + 1, ctr, &F.abort);
-                lfro_wait(&F.cx, (uint32_t) i + 1, ctr, &F.abort);
+                lfro_wait(&F.st, (uint32_t) i, ctr, &F.abort, wc);
+                lfro_wait(&F.h0x, (uint32_t) i + 1, ctr, &F.abort, wc);
+                lfro_wait(&F.h1x, (uint32_t) i + 1, ctr, &F.abort, wc);
+                lfro_wait(&F.cx, (uint32_t) i + 1, ctr, &F.abort, wc);
                 stage(tb ^ 1, false);
                 lfro_pub(&F.ld_int, (uint32_t) i + 2);
             }
@@ -2490,15 +2498,15 @@ __global__ __launch_bounds__(LFRO_NTH) void k_lfro(const uint32_t *__restrict__ 
             if (c > 0) {
                 // SB c - 1's last columns (this tile's left halo) are final after this SB's
                 // first column edges: its bottom rows are then complete
-                lfro_wait(&F.h1x, (uint32_t) i + 1, ctr, &F.abort);
-                lfro_wait(&F.cx, (uint32_t) i + 1, ctr, &F.abort);
+                lfro_wait(&F.h1x, (uint32_t) i + 1, ctr, &F.abort, wc);
+                lfro_wait(&F.cx, (uint32_t) i + 1, ctr, &F.abort, wc);
                 lfro_store<PIX, G>(S, tb, P, c, sby, lane, false, 0);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 if (lane == 0) __hip_atomic_store((gu32 *) &progress[s_task], (uint32_t) c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            lfro_wait(&F.rb, (uint32_t) i + 1, ctr, &F.abort);
-            lfro_wait(&F.c, (uint32_t) i + 1, ctr, &F.abort);
-            lfro_wait(&F.h0x, (uint32_t) i + 1, ctr, &F.abort);
+            lfro_wait(&F.rb, (uint32_t) i + 1, ctr, &F.abort, wc);
+            lfro_wait(&F.c, (uint32_t) i + 1, ctr, &F.abort, wc);
+            lfro_wait(&F.h0x, (uint32_t) i + 1, ctr, &F.abort, wc);
             lfro_store<PIX, G>(S, tb, P, c, sby, lane, last, 1);
             if (last) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2509,6 +2517,12 @@ __global__ __launch_bounds__(LFRO_NTH) void k_lfro(const uint32_t *__restrict__ 
             lfro_pub(&F.st, (uint32_t) i + 1);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    if (LFR_PROF && lane == 0) {
+        atomicAdd(&lfr_prof[w], wc);
+        atomicAdd(&lfr_prof[6 + w], clock64() - tk0);
+        if (w == 4) { atomicAdd(&lfr_prof[12], wrow); atomicAdd(&lfr_prof[13], (unsigned long long) n); }
+        if (w == 0) atomicAdd(&lfr_prof[14], 1ull);
     }
     lfrd_retire(ctr, ntasks, 0, tid, LFRO_NTH, &s_last);
 }
@@ -2974,6 +2988,81 @@ DEV int mcp_find(const uint32_t *off, int n, uint32_t g)
     return k;
 }
 
+// a unit as its tasks read it; cat 0: unscaled, height a multiple of 8; 1: unscaled, 4
+// rows; 2: a scaled reference. direct (per reference): the filter window of every pixel
+// lies inside the visible reference (no clamping)
+DEV void mcp_unit(const McUnit &m, const FrameDesc *__restrict__ frames, McL &L)
+{
+    const FrameDesc &fd = frames[m.frame];
+    const int p = m.plane, c = p ? 1 : 0;
+    L.dst = fd.plane[p];
+    L.pitch = fd.pitch[c];
+    L.x = m.x; L.y = m.y;
+    L.lw = (uint8_t) (31 - __builtin_clz((unsigned) m.w));
+    L.h = m.h;
+    L.filter = m.filter > 3 ? 3 : m.filter;
+    L.nref = m.nref;
+    L.bd = (uint8_t) fd.bd;
+    L.direct = 0;
+    bool scaled = false;
+    for (int k = 0; k < 2; k++) {
+        const int rf = m.ref[k] > 2 ? 0 : m.ref[k];
+        const McRef r = m.r[k];
+        L.ref[k] = fd.ref[rf][p];
+        L.ix[k] = r.ix; L.iy[k] = r.iy;
+        L.mx[k] = r.mx & 15; L.my[k] = r.my & 15;
+        L.rw[k] = (uint16_t) fd.refw[rf][c]; L.rh[k] = (uint16_t) fd.refh[rf][c];
+        if (k < m.nref) {
+            scaled |= r.dx != 16 || r.dy != 16;
+            if (r.ix >= 3 && r.iy >= 3 && r.ix + (int) m.w + 4 < fd.refw[rf][c] && r.iy + (int) m.h + 4 < fd.refh[rf][c])
+                L.direct |= (uint8_t) (1 << k);
+        }
+    }
+    L.cat = scaled ? 2 : (m.h & 7) ? 1 : 0;
+}
+// exclusive task offsets per category over the workgroup's units (wave 0)
+DEV void mcp_offsets(uint32_t (*off)[MCP_U + 1], const uint32_t (&cnt)[3], int tid)
+{
+    if (tid < 64) {
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            uint32_t v = cnt[c];
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t o = __shfl_up(v, d);
+                if (tid >= d) v += o;
+            }
+            off[c][tid + 1] = v;
+            if (tid == 0) off[c][0] = 0;
+        }
+    }
+}
+// scaled references: one pixel per task (mc_unit_pixels)
+template <typename PIX>
+DEV void mcp_scaled(const McUnit *__restrict__ units, const uint32_t *off, int nu, const FrameDesc *__restrict__ frames, int tid,
+                    int g0 = 0, int gs = 256)
+{
+    const uint32_t T2 = off[nu];
+    for (uint32_t g = tid + g0; g < T2; g += gs) {
+        const int k = mcp_find(off, nu, g);
+        const McUnit m = units[k];
+        const FrameDesc &fd = frames[m.frame];
+        const int p = m.plane, c = p ? 1 : 0, W = m.w;
+        const uint32_t ti = g - off[k];
+        const int yy = (int) ti / W, xx = (int) ti - yy * W;
+        int out = 0;
+        for (int r = 0; r < m.nref; r++) {
+            const int rf = m.ref[r];
+            const McRef q = m.r[r];
+            const int px = q.mx + xx * q.dx, py = q.my + yy * q.dy;
+            const int v = mc_sample<PIX>((const PIX *) fd.ref[rf][p], fd.pitch[c], fd.refw[rf][c], fd.refh[rf][c],
+                                         q.ix + (px >> 4), q.iy + (py >> 4), px & 15, py & 15, m.filter, fd.bd);
+            out = r ? (out + v + 1) >> 1 : v;
+        }
+        ((PIX *) fd.plane[p])[(size_t) (m.y + yy) * fd.pitch[c] + m.x + xx] = (PIX) out;
+    }
+}
+
 template <typename PIX, int R, bool V>
 DEV void mcp_rows(const McL &u, const int16_t (*taps)[8], int xx, int yy)
 {
@@ -3057,50 +3146,13 @@ __global__ __launch_bounds__(256) void k_mcp(const McUnit *__restrict__ units, i
     }
     uint32_t cnt[3] = { 0, 0, 0 };
     if (tid < nu) {
-        const McUnit m = units[u0 + tid];
-        const FrameDesc &fd = frames[m.frame];
-        const int p = m.plane, c = p ? 1 : 0;
         McL L;
-        L.dst = fd.plane[p];
-        L.pitch = fd.pitch[c];
-        L.x = m.x; L.y = m.y;
-        L.lw = (uint8_t) (31 - __builtin_clz((unsigned) m.w));
-        L.h = m.h;
-        L.filter = m.filter > 3 ? 3 : m.filter;
-        L.nref = m.nref;
-        L.bd = (uint8_t) fd.bd;
-        L.direct = 0;
-        bool scaled = false;
-        for (int k = 0; k < 2; k++) {
-            const int rf = m.ref[k] > 2 ? 0 : m.ref[k];
-            const McRef r = m.r[k];
-            L.ref[k] = fd.ref[rf][p];
-            L.ix[k] = r.ix; L.iy[k] = r.iy;
-            L.mx[k] = r.mx & 15; L.my[k] = r.my & 15;
-            L.rw[k] = (uint16_t) fd.refw[rf][c]; L.rh[k] = (uint16_t) fd.refh[rf][c];
-            if (k < m.nref) {
-                scaled |= r.dx != 16 || r.dy != 16;
-                if (r.ix >= 3 && r.iy >= 3 && r.ix + (int) m.w + 4 < fd.refw[rf][c] && r.iy + (int) m.h + 4 < fd.refh[rf][c])
-                    L.direct |= (uint8_t) (1 << k);
-            }
-        }
-        L.cat = scaled ? 2 : (m.h & 7) ? 1 : 0;
-        cnt[L.cat] = scaled ? (uint32_t) m.w * m.h : (uint32_t) m.w * m.h >> (L.cat ? 2 : 3);
+        const McUnit m = units[u0 + tid];
+        mcp_unit(m, frames, L);
+        cnt[L.cat] = L.cat == 2 ? (uint32_t) m.w * m.h : (uint32_t) m.w * m.h >> (L.cat ? 2 : 3);
         S.u[tid] = L;
     }
-    if (tid < 64) {
-#pragma unroll
-        for (int c = 0; c < 3; c++) {
-            uint32_t v = cnt[c];
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const uint32_t o = __shfl_up(v, d);
-                if (tid >= d) v += o;
-            }
-            S.off[c][tid + 1] = v;
-            if (tid == 0) S.off[c][0] = 0;
-        }
-    }
+    mcp_offsets(S.off, cnt, tid);
     __syncthreads();
     // R = 8 tasks, then R = 4; the vertical pass only where a lane of the wave needs it
     for (int c = 0; c < 2; c++) {
@@ -3121,26 +3173,269 @@ __global__ __launch_bounds__(256) void k_mcp(const McUnit *__restrict__ units, i
             }
         }
     }
-    // scaled references: one pixel per task (mc_unit_pixels)
-    const uint32_t T2 = S.off[2][nu];
-    for (uint32_t g = tid; g < T2; g += 256) {
-        const int k = mcp_find(S.off[2], nu, g);
-        const McUnit m = units[u0 + k];
-        const FrameDesc &fd = frames[m.frame];
-        const int p = m.plane, c = p ? 1 : 0, W = m.w;
-        const uint32_t ti = g - S.off[2][k];
-        const int yy = (int) ti / W, xx = (int) ti - yy * W;
-        int out = 0;
-        for (int r = 0; r < m.nref; r++) {
-            const int rf = m.ref[r];
-            const McRef q = m.r[r];
-            const int px = q.mx + xx * q.dx, py = q.my + yy * q.dy;
-            const int v = mc_sample<PIX>((const PIX *) fd.ref[rf][p], fd.pitch[c], fd.refw[rf][c], fd.refh[rf][c],
-                                         q.ix + (px >> 4), q.iy + (py >> 4), px & 15, py & 15, m.filter, fd.bd);
-            out = r ? (out + v + 1) >> 1 : v;
+    mcp_scaled<PIX>(units + u0, S.off[2], nu, frames, tid);
+}
+
+// --------------------------------------------------------------- k_mcq
+// k_mcp with 4-column lane tasks: a lane filters 4 adjacent output columns x R rows (R = 8;
+// 4 for units 4 rows tall) from ONE load per window row (12 pixels, x - 3 .. x + 8: 8-bit
+// a 12-byte load, 16-bit 24 bytes), where k_mcp's one-column tasks load 8 pixels per row
+// and output pixel (4x the load instructions, 2.7x the bytes through the L1). The
+// horizontal 8-tap sums are packed dot products: 8-bit v_dot4_i32_i8 on the pixels biased
+// by -128 (every VP9 8-tap and the bilinear-as-8-tap sum to 128, so + 128 * 128 restores
+// the bias; an identity phase, tap 128, does not fit an int8 and selects the pixel), 16-bit
+// v_dot2_i32_i16 on the pixel pairs (odd columns from byte-aligned pairs). The vertical pass
+// accumulates each horizontally filtered row into the <= 8 outputs whose taps cover it.
+// Arithmetic exactly vp9dsp_template.c:2076-2113 (the pixel-clipped 2-D form, equal to the
+// 1-D / copy forms through identity phases, see k_mcp); compound averages
+// (a + b + 1) >> 1 per packed pixel as (a | b) - ((a ^ b) >> 1).
+struct McqLds {
+    alignas(16) int16_t taps[64][8];              // [filter * 16 + phase], bilinear = filter 3 (k_mcp's)
+    uint32_t tap8[64][2];                         // the same taps as int8 quads (identity phases: 0)
+    alignas(16) uint32_t tapp[64][12];            // vertical tap pairs (f[q], f[q + 1]), q = -1..7 (f[-1] = f[8] = 0)
+    McL u[MCP_U];
+    uint32_t off[3][MCP_U + 1];
+};
+typedef struct __attribute__((packed, aligned(1))) { uint32_t d[3]; } McqW8;   // 12 window bytes
+typedef struct __attribute__((packed, aligned(2))) { uint32_t d[6]; } McqW16;  // 12 window pixels
+typedef short mcq_s2 __attribute__((ext_vector_type(2)));
+
+template <typename PIX> struct McqW { static constexpr int N = sizeof(PIX) == 1 ? 3 : 6; };
+
+// one window row: direct (inside the visible reference) or with every pixel clamped
+template <typename PIX>
+DEV void mcq_load(const PIX *rp, const PIX *wrow, int pitch, int X, int Y, bool direct, int rw, int rh,
+                  uint32_t (&d)[McqW<PIX>::N])
+{
+    if (direct) {                                      // wrow: the window row's first pixel
+        if constexpr (sizeof(PIX) == 1) {
+            const __attribute__((address_space(1))) McqW8 *q = (const __attribute__((address_space(1))) McqW8 *) wrow;
+            d[0] = q->d[0]; d[1] = q->d[1]; d[2] = q->d[2];
+        } else {
+            const __attribute__((address_space(1))) McqW16 *q = (const __attribute__((address_space(1))) McqW16 *) wrow;
+#pragma unroll
+            for (int i = 0; i < 6; i++) d[i] = q->d[i];
         }
-        ((PIX *) fd.plane[p])[(size_t) (m.y + yy) * fd.pitch[c] + m.x + xx] = (PIX) out;
+        return;
     }
+    const int yc = Y < 0 ? 0 : Y >= rh ? rh - 1 : Y;
+    const PIX *row = rp + (size_t) yc * pitch;
+    constexpr int PPW = 4 / sizeof(PIX);
+#pragma unroll
+    for (int i = 0; i < McqW<PIX>::N; i++) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int b = 0; b < PPW; b++) {
+            const int x = X + i * PPW + b, xc = x < 0 ? 0 : x >= rw ? rw - 1 : x;
+            w |= (uint32_t) row[xc] << (8 * sizeof(PIX) * b);
+        }
+        d[i] = w;
+    }
+}
+
+// the 4 horizontal 8-tap outputs of one window row (clipped pixels)
+template <typename PIX>
+DEV void mcq_h(const uint32_t (&d)[McqW<PIX>::N], const uint32_t (&th)[4], bool ident, int pmax, int (&h)[4])
+{
+    if constexpr (sizeof(PIX) == 1) {
+        const uint32_t e0 = d[0] ^ 0x80808080u, e1 = d[1] ^ 0x80808080u, e2 = d[2] ^ 0x80808080u;
+#pragma unroll
+        for (int o = 0; o < 4; o++) {
+            const uint32_t lo = o ? __builtin_amdgcn_alignbyte(e1, e0, o) : e0;
+            const uint32_t hi = o ? __builtin_amdgcn_alignbyte(e2, e1, o) : e1;
+            const int s = __builtin_amdgcn_sdot4((int) lo, (int) th[0],
+                                                 __builtin_amdgcn_sdot4((int) hi, (int) th[1], 16384 + 64, false), false);
+            h[o] = ident ? (int) ((lo >> 24) ^ 0x80u) : med3_0(s >> 7, 255);
+        }
+    } else {
+        uint32_t sh[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++) sh[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], 2);
+#pragma unroll
+        for (int o = 0; o < 4; o++) {
+            int s = 64;
+#pragma unroll
+            for (int q = 3; q >= 0; q--) {
+                const uint32_t w = (o & 1) ? sh[(o >> 1) + q] : d[(o >> 1) + q];
+                s = __builtin_amdgcn_sdot2(__builtin_bit_cast(mcq_s2, w), __builtin_bit_cast(mcq_s2, th[q]), s, false);
+            }
+            h[o] = med3_0(s >> 7, pmax);
+        }
+    }
+}
+
+template <typename PIX, int R, bool V, bool DIRECT>
+DEV void mcq_rows(const McL &u, const McqLds &S, int xx, int yy)
+{
+    constexpr int NW = sizeof(PIX) == 1 ? 1 : 2;          // output dwords per row
+    constexpr int NR = V ? R + 7 : R, R0 = V ? 0 : 3;      // window rows the vertical pass reads
+    const int pmax = (1 << u.bd) - 1, pitch = u.pitch;
+    uint32_t outp[R][NW];
+    for (int k = 0; k < u.nref; k++) {
+        const int fh = u.filter * 16 + u.mx[k], fv = u.filter * 16 + u.my[k];
+        uint32_t th[4];
+        if constexpr (sizeof(PIX) == 1) {
+            th[0] = S.tap8[fh][0]; th[1] = S.tap8[fh][1]; th[2] = th[3] = 0;
+        } else {
+            const uint4 hw = *(const uint4 *) S.taps[fh];
+            th[0] = hw.x; th[1] = hw.y; th[2] = hw.z; th[3] = hw.w;
+        }
+        uint32_t fp[9];                                    // fp[q + 1] = (f[q], f[q + 1])
+        if (V) {
+            const uint4 v0 = *(const uint4 *) &S.tapp[fv][0], v1 = *(const uint4 *) &S.tapp[fv][4];
+            fp[0] = v0.x; fp[1] = v0.y; fp[2] = v0.z; fp[3] = v0.w;
+            fp[4] = v1.x; fp[5] = v1.y; fp[6] = v1.z; fp[7] = v1.w; fp[8] = S.tapp[fv][8];
+        }
+        const bool ident = u.mx[k] == 0;
+        const int X = u.ix[k] + xx - 3, Y = u.iy[k] + yy - 3 + R0;
+        const PIX *rp = (const PIX *) u.ref[k];
+        const int rw = u.rw[k], rh = u.rh[k];
+        const PIX *wrow = DIRECT ? rp + (ptrdiff_t) Y * pitch + X : rp;
+        int acc[R][4];
+#pragma unroll
+        for (int t = 0; t < R; t++)
+#pragma unroll
+            for (int o = 0; o < 4; o++) acc[t][o] = 64;
+        // window rows in pairs (2 jp, 2 jp + 1): the vertical pass as one v_dot2 per output
+        // and pair, the rows' filtered pixels packed (h[2 jp], h[2 jp + 1]) per column
+#pragma unroll
+        for (int jp = 0; jp < (NR + 1) / 2; jp++) {
+            int h[2][4];
+#pragma unroll
+            for (int e = 0; e < 2; e++) {
+                const int j = 2 * jp + e;
+                if (j >= NR) {
+#pragma unroll
+                    for (int o = 0; o < 4; o++) h[e][o] = 0;
+                    continue;
+                }
+                uint32_t d[McqW<PIX>::N];
+                mcq_load<PIX>(rp, wrow, pitch, X, Y + j, DIRECT, rw, rh, d);
+                if (DIRECT) wrow += pitch;
+                mcq_h<PIX>(d, th, ident, pmax, h[e]);
+            }
+            if (V) {
+                uint32_t pk[4];
+#pragma unroll
+                for (int o = 0; o < 4; o++) pk[o] = (uint32_t) h[0][o] | (uint32_t) h[1][o] << 16;
+                const int j = 2 * jp;
+#pragma unroll
+                for (int t = (j > 7 ? j - 7 : 0); t <= (j + 1 < R - 1 ? j + 1 : R - 1); t++)
+#pragma unroll
+                    for (int o = 0; o < 4; o++)
+                        acc[t][o] = __builtin_amdgcn_sdot2(__builtin_bit_cast(mcq_s2, pk[o]), __builtin_bit_cast(mcq_s2, fp[j - t + 1]),
+                                                           acc[t][o], false);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 2; e++)
+                    if (2 * jp + e < NR)
+#pragma unroll
+                        for (int o = 0; o < 4; o++) acc[2 * jp + e][o] = h[e][o];
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < R; t++) {
+            int v[4];
+#pragma unroll
+            for (int o = 0; o < 4; o++) v[o] = V ? med3_0(acc[t][o] >> 7, pmax) : acc[t][o];
+            uint32_t w[NW];
+            if constexpr (sizeof(PIX) == 1) w[0] = (uint32_t) v[0] | (uint32_t) v[1] << 8 | (uint32_t) v[2] << 16 | (uint32_t) v[3] << 24;
+            else { w[0] = (uint32_t) v[0] | (uint32_t) v[1] << 16; w[1] = (uint32_t) v[2] | (uint32_t) v[3] << 16; }
+            constexpr uint32_t HM = sizeof(PIX) == 1 ? 0x7f7f7f7fu : 0x7fff7fffu;
+#pragma unroll
+            for (int i = 0; i < NW; i++) outp[t][i] = k ? (outp[t][i] | w[i]) - (((outp[t][i] ^ w[i]) >> 1) & HM) : w[i];
+        }
+    }
+    typedef __attribute__((address_space(1))) PIX gpo;
+    gpo *dst = (gpo *) u.dst + (size_t) (u.y + yy) * pitch + u.x + xx;
+#pragma unroll
+    for (int t = 0; t < R; t++) {
+        if constexpr (sizeof(PIX) == 1) *(__attribute__((address_space(1))) uint32_t *) (dst + (size_t) t * pitch) = outp[t][0];
+        else {
+            typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+            v2u w2; w2.x = outp[t][0]; w2.y = outp[t][1];
+            *(__attribute__((address_space(1))) v2u *) (dst + (size_t) t * pitch) = w2;
+        }
+    }
+}
+
+template <typename PIX, int R>
+DEV void mcq_task(const McL &u, const McqLds &S, int xx, int yy)
+{
+    const bool v = u.my[0] | (u.nref > 1 ? u.my[1] : 0);
+    const bool dir = (u.direct & ((1 << u.nref) - 1)) == ((1 << u.nref) - 1);
+    if (__all(dir)) {
+        if (__any(v)) mcq_rows<PIX, R, true, true>(u, S, xx, yy);
+        else mcq_rows<PIX, R, false, true>(u, S, xx, yy);
+    } else {
+        if (__any(v)) mcq_rows<PIX, R, true, false>(u, S, xx, yy);
+        else mcq_rows<PIX, R, false, false>(u, S, xx, yy);
+    }
+}
+
+template <typename PIX>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_mcq(const McUnit *__restrict__ units, int nunits,
+                                             const FrameDesc *__restrict__ frames)
+{
+    __shared__ McqLds S;
+    const int tid = threadIdx.x;
+    const int u0 = blockIdx.x * MCP_U, nu = nunits - u0 < MCP_U ? nunits - u0 : MCP_U;
+    {
+        // filter rows: 3 x 16 8-tap phases, then the bilinear ones as 8-taps; int8 quads of
+        // the non-identity phases (every tap of phases 1-15 lies in [-128, 127])
+        const int r = tid >> 2, q = (tid & 3) * 2;
+        int16_t a, b;
+        if (r < 48) { a = vp9t_subpel_filters[r >> 4][r & 15][q]; b = vp9t_subpel_filters[r >> 4][r & 15][q + 1]; }
+        else {
+            const int m = r & 15;
+            a = (int16_t) (q == 2 ? 0 : q == 4 ? 8 * m : 0);
+            b = (int16_t) (q == 2 ? 8 * (16 - m) : 0);
+        }
+        S.taps[r][q] = a;
+        S.taps[r][q + 1] = b;
+        S.tapp[r][q + 1] = (uint32_t) (uint16_t) a | (uint32_t) (uint16_t) b << 16;   // (f[q], f[q + 1])
+        // tap8 dword (q >> 2): bytes q & 3, (q & 3) + 1 of it from this thread's pair
+        const uint32_t pr = (r & 15) ? ((uint32_t) (uint8_t) a | (uint32_t) (uint8_t) b << 8) << (8 * (q & 3)) : 0u;
+        const uint32_t other = __shfl_xor(pr, 1);
+        if (!(tid & 1)) S.tap8[r][q >> 2] = pr | other;
+    }
+    __syncthreads();
+    {
+        // the odd-q pairs (f[q], f[q + 1]), q = -1, 1, 3, 5, 7, from the int16 rows
+        const int r = tid >> 2;
+        for (int q = 2 * (tid & 3) - 1; q < 8; q += 8) {
+            const int lo = q < 0 ? 0 : S.taps[r][q], hi = q + 1 > 7 ? 0 : S.taps[r][q + 1];
+            S.tapp[r][q + 1] = (uint32_t) (uint16_t) lo | (uint32_t) (uint16_t) hi << 16;
+        }
+    }
+    uint32_t cnt[3] = { 0, 0, 0 };
+    if (tid < nu) {
+        McL L;
+        const McUnit m = units[u0 + tid];
+        mcp_unit(m, frames, L);
+        // 4 x 8 (4 x 4) pixels per task
+        cnt[L.cat] = L.cat == 2 ? (uint32_t) m.w * m.h : (uint32_t) m.w * m.h >> (L.cat ? 4 : 5);
+        S.u[tid] = L;
+    }
+    mcp_offsets(S.off, cnt, tid);
+    __syncthreads();
+    // blockIdx.y: one of gridDim.y slices of the tasks (a workgroup of 64 large units is
+    // otherwise the launch's tail: units per workgroup are counted, not their pixels)
+    const int g0 = (int) blockIdx.y * 256, gs = 256 * (int) gridDim.y;
+    for (int c = 0; c < 2; c++) {
+        const uint32_t T = S.off[c][nu];
+        for (uint32_t g = tid + g0; g < T; g += gs) {
+            const int k = mcp_find(S.off[c], nu, g);
+            const McL &u = S.u[k];
+            const uint32_t ti = g - S.off[c][k];
+            const int lq = u.lw - 2;                      // 4-column groups per row: w / 4
+            const int xx = (int) (ti & ((1u << lq) - 1)) * 4;
+            const int yy = (int) (ti >> lq) << (c ? 2 : 3);
+            if (c == 0) mcq_task<PIX, 8>(u, S, xx, yy);
+            else mcq_task<PIX, 4>(u, S, xx, yy);
+        }
+    }
+    mcp_scaled<PIX>(units + u0, S.off[2], nu, frames, tid, g0, gs);
 }
 
 // ------------------------------------------------------------ launchers
@@ -3424,8 +3719,18 @@ int vp9hip_launch_mc(int hb, hipStream_t st, int n, const McUnit *units, const F
     // launches): C5 8K 10-bit 320 -> 219 us per frame, C2 1080p 8-bit 128 -> 61 us. An
     // occupancy target of 6 waves / SIMD (78 VGPRs instead of 113) measured slower (325 us
     // at C5): the rows of a task are all in flight at once only with the larger budget.
+    // VP9HIP_MCP=3 (default): k_mcq, 4-column tasks with packed dot products
     const char *pe = getenv("VP9HIP_MCP");
-    const int mcp = pe ? atoi(pe) : 2;
+    const int mcp = pe ? atoi(pe) : 3;
+    if (mcp >= 3) {
+        const int nb = (n + MCP_U - 1) / MCP_U;
+        // task slices per unit group: ~4k workgroups at least, 2 to 8 slices
+        const char *se = getenv("VP9HIP_MCQ_SLICES");
+        const int ns = se ? std::max(1, std::min(16, atoi(se))) : std::max(2, std::min(8, 4096 / nb));
+        if (hb) hipLaunchKernelGGL((k_mcq<uint16_t>), dim3(nb, ns), dim3(256), 0, st, units, n, frames);
+        else    hipLaunchKernelGGL((k_mcq<uint8_t>), dim3(nb, ns), dim3(256), 0, st, units, n, frames);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     if (mcp >= (hb ? 1 : 2)) {
         const int nb = (n + MCP_U - 1) / MCP_U;
         if (hb) hipLaunchKernelGGL((k_mcp<uint16_t>), dim3(nb), dim3(256), 0, st, units, n, frames);

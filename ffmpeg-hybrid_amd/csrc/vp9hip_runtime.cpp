@@ -1446,6 +1446,17 @@ static int finish_summary(vp9hip_ctx *c, Staged &s)
         s.status = VP9HIP_EINVALIDDATA;
         return s.status;
     }
+    // each static k_resid_dev grid was sized from a staged bound on its job range: a range
+    // beyond it would have dropped residual jobs silently
+    for (const Launch &L : s.launches)
+        if (L.kind == K_RESID && L.devr) {
+            const uint32_t *rng = sm + 1 + L.off;
+            if (rng[1] > rng[0] && rng[1] - rng[0] > L.n) {
+                fprintf(stderr, "vp9hip: residual job range %u exceeds its staged bound %u\n", rng[1] - rng[0], (unsigned) L.n);
+                s.status = VP9HIP_EBUG;
+                return s.status;
+            }
+        }
     const uint32_t *ko = sm + 1 + s.n_gidx, *fb32 = ko + s.nkey + 1;
     for (int k = 0; k < K_N; k++) s.alg_bytes[k] = s.alg_stat[k];
     s.alg_bytes[K_PLAN] = (double) s.nblk * sizeof(vp9h_block) + (double) s.neob * 2;
@@ -1877,7 +1888,9 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     {
         const size_t eb = (size_t) edge_sbs * EDGE_PIX * c->bypp + 256;
         const char *ee = getenv("VP9HIP_EDGE");      // read per staging (tests switch it)
-        const bool edge_off = ee && !atoi(ee);
+        // only the 4:2:0 tile loader reads the edge columns (the other chroma formats load
+        // their left column from frame rows): no buffer written and never read for those
+        const bool edge_off = (ee && !atoi(ee)) || !(c->ss_h && c->ss_v);
         if (edge_sbs && !edge_off && eb > s.edge_cap) {
             if (s.edge) hipFree(s.edge);
             s.edge = nullptr;

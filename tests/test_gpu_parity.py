@@ -65,15 +65,17 @@ INTER = [
     (352, 288, 8, {"bilinear": 1}),
     (66, 66, 8, {"compound": 1, "p_zero_eob": 0.4}),
     (352, 288, 10, {"compound": 1}),
+    (200, 130, 12, {"compound": 1}),
     (512, 256, 8, {"log2_tile_cols": 1, "coef_stress": 1}),
 ]
 
 
-@pytest.mark.parametrize("mcp", ["1", "2", "0"])
+@pytest.mark.parametrize("mcp", ["3", "2", "1", "0"])
 @pytest.mark.parametrize("w,h,bpp,kw", INTER)
 def test_inter_parity(v9, orc, gpu, monkeypatch, w, h, bpp, kw, mcp):
-    """VP9HIP_MCP: 2 (default) the packed MC kernel k_mcp at every bit depth, 1 for high
-    bit depth only, 0 one workgroup per unit (k_mc)."""
+    """VP9HIP_MCP: 3 (default) k_mcq (4-column tasks, packed dot products), 2 the packed
+    one-column kernel k_mcp at every bit depth, 1 k_mcp for high bit depth only, 0 one
+    workgroup per unit (k_mc)."""
     monkeypatch.setenv("VP9HIP_MCP", mcp)
     key_kw = {k: x for k, x in kw.items() if k in ("log2_tile_cols",)}
     key = v9.SynthFrame(v9.synth_params(w, h, bpp, seed=11, **key_kw))
@@ -331,7 +333,7 @@ SCALED = [
 ]
 
 
-@pytest.mark.parametrize("mcp", ["0", "2"])
+@pytest.mark.parametrize("mcp", ["0", "2", "3"])
 @pytest.mark.parametrize("rs,fs,bpp,kw", SCALED)
 def test_scaled_reference_parity(v9, orc, gpu, monkeypatch, rs, fs, bpp, kw, mcp):
     """Reference scaling (vp9recon.c:492-628, vp9.c:845-880): a keyframe at one size,
