@@ -2224,8 +2224,8 @@ __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfrd(const uint32_t *__res
 // written after a tile write and read before the tile read orders them; the fences are
 // compiler-only, wavefront scope). Every wait is bounded: one that gives up is counted in
 // ctr[2] like a hand-off timeout (the batch fails with VP9HIP_EBUG), never hangs.
-#define LFRO_NTH 384                              // R, H0, H1, C, L, S
-struct LfroSync { uint32_t ld_int, ld_top, ra, rb, h0x, h1x, h0, h1, cx, c, st, abort, pad[4]; };
+#define LFRO_NTH 512                              // R, H0, H1, C, L1, L2, S1, S2
+struct LfroSync { uint32_t ld_int, ld_top, ra, rb, h0x, h1x, h0, h1, cx, c, st1, st2, abort, pad[3]; };
 DEV void lfro_pub(uint32_t *f, uint32_t v)
 {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -2248,35 +2248,27 @@ DEV void lfro_wait(uint32_t *f, uint32_t need, uint32_t *ctr, uint32_t *abort, u
     if (LFR_PROF) wc += clock64() - t0;
 }
 // the store wave's tile parts: 0 the left chunk column's bottom 8 rows (SB sbx - 1's last
-// columns, final after this SB's first column edges; sc1), 1 the other bottom rows (sc1;
-// the last chunk column only for the row's last SB: otherwise the next tile's part 0),
-// 2 everything else (the top halo's corner chunk is never modified)
+// columns, final after this SB's first column edges; sc1; one chunk per lane 0..23),
+// 1 the other bottom rows (sc1; the last chunk column only for the row's last SB:
+// otherwise the next tile's part 0) = lfrd_store part 0, 2 everything else (the top
+// halo's corner chunk is never modified) = lfrd_store part 1: compile-time row walks
 template <typename PIX, class G>
 DEV void lfro_store(const LfrLds<PIX, G> &S, int tb, const LfrPlanes &P, int sbx, int sby, int ml, bool last, int part)
 {
     typedef LfP<PIX, G> L;
     typedef Chunk16::T CT;
-    for (int ci = ml; ci < L::NCHUNK; ci += 64) {
-        int p, r, k;
-        lf_chunk<PIX, G>(ci, p, r, k);
-        const int nk = p ? L::CK : L::YK, nr = p ? L::CR : 72;
-        const bool bot = r >= nr - 8;
-        bool st;
-        if (part == 0) st = bot && k == 0 && sbx > 0;
-        else if (part == 1) st = bot && k > 0 && (k < nk - 1 || last);
-        else st = !bot && (r >= 8 ? (k > 0 || sbx > 0) && (k < nk - 1 || last) : k > 0 && sby > 0);
-        if (!st) continue;
-        const PIX *t = (p ? S.ct[tb][p - 1] + r * L::UVP : S.lt[tb] + r * L::YP) + L::CPX * k;
-        const CT w = Chunk16::from_lds(t);
-        PIX *g = lfr_addr<PIX, G>(P, sbx, sby, p, r, k);
-        if (part < 2) {
+    if (part == 0) {
+        if (sbx > 0 && ml < 24) {
+            const int p = ml >> 3, r = (p ? L::CR : 72) - 8 + (ml & 7);
+            const PIX *t = p ? S.ct[tb][p - 1] + r * L::UVP : S.lt[tb] + r * L::YP;
+            PIX *g = lfr_addr<PIX, G>(P, sbx, sby, p, r, 0);
+            const CT w = Chunk16::from_lds(t);
             st_sc1(g, (uint64_t) w.x | (uint64_t) w.y << 32);
             st_sc1((char *) g + 8, (uint64_t) w.z | (uint64_t) w.w << 32);
-        } else {
-            v4u x; x.x = w.x; x.y = w.y; x.z = w.z; x.w = w.w;
-            *(gv4u *) g = x;
         }
+        return;
     }
+    lfrd_store<PIX, G>(S, tb, P, sbx, sby, ml, last, part - 1);
 }
 #define LFRO_EDGE_WIDE(k, C0)                                                                            \
     {                                                                                                    \
@@ -2302,8 +2294,8 @@ __global__ __launch_bounds__(LFRO_NTH) void k_lfro(const uint32_t *__restrict__ 
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     uint32_t *const progress = ctr + 4;
     __builtin_amdgcn_s_setprio(3);
-    // LFR_PROF builds: per wave role, cycles waiting on the workgroup's counters (lfr_prof[w])
-    // and lifetime (lfr_prof[6 + w]); the loader's waits for the row above: lfr_prof[12]
+    // LFR_PROF builds: per wave role, cycles waiting on the workgroup's counters (lfr_prof[w]);
+    // R's lifetime [8], L2's waits for the row above [9], SB steps [10], workgroups [11]
     uint64_t wc = 0, wrow = 0;
     const uint64_t tk0 = LFR_PROF ? clock64() : 0;
     if (tid == 0) s_task = atomicAdd(&ctr[0], 1u);
@@ -2400,8 +2392,10 @@ __global__ __launch_bounds__(LFRO_NTH) void k_lfro(const uint32_t *__restrict__ 
             lfro_pub(&F.c, (uint32_t) i + 1);
         }
     } else if (w == 4) {
-        // ---- L: interiors (+ program words) one SB ahead, top halos after the row above
-        CT vi[NUI], vt[NUT];
+        // ---- L1: interiors and program words, one SB ahead: SB i's are staged into tile
+        // i & 1 once SB i - 2 is stored (S1, S2) and SB i - 1's waves have copied their left
+        // halos out of that tile; SB i + 1's loads are issued right after
+        CT vi[NUI];
         uint32_t pwv[NPW];
         auto issue = [&](int c, bool halo) {
 #pragma unroll
@@ -2419,7 +2413,19 @@ __global__ __launch_bounds__(LFRO_NTH) void k_lfro(const uint32_t *__restrict__ 
             for (int q = 0; q < NPW; q++)
                 if (lane + 64 * q < L::PROG / 4) pwv[q] = ((const uint32_t *) rc.prog)[lane + 64 * q];
         };
-        auto stage = [&](int tb, bool halo) {
+        issue((int) c0, c0 > 0);
+        for (int i = 0; i < n; i++) {
+            const int tb = i & 1;
+            const bool halo = i == 0 && c0 > 0;
+            if (i >= 2) {
+                lfro_wait(&F.st1, (uint32_t) i - 1, ctr, &F.abort, wc);
+                lfro_wait(&F.st2, (uint32_t) i - 1, ctr, &F.abort, wc);
+            }
+            if (i >= 1) {
+                lfro_wait(&F.h0x, (uint32_t) i, ctr, &F.abort, wc);
+                lfro_wait(&F.h1x, (uint32_t) i, ctr, &F.abort, wc);
+                lfro_wait(&F.cx, (uint32_t) i, ctr, &F.abort, wc);
+            }
 #pragma unroll
             for (int u = 0; u < NUI; u++) {
                 const int ci = lane + 64 * u;
@@ -2431,34 +2437,35 @@ __global__ __launch_bounds__(LFRO_NTH) void k_lfro(const uint32_t *__restrict__ 
 #pragma unroll
             for (int q = 0; q < NPW; q++)
                 if (lane + 64 * q < L::PROG / 4) S.prog[tb][lane + 64 * q] = pwv[q];
-        };
-        issue((int) c0, c0 > 0);
-        stage(0, c0 > 0);
-        lfro_pub(&F.ld_int, 1u);
+            lfro_pub(&F.ld_int, (uint32_t) i + 1);
+            if (i + 1 < n) issue((int) (c0 + i) + 1, false);
+        }
+    } else if (w == 5) {
+        // ---- L2: top halos, handed over by the row above (its progress reaches c + 1; k_lfr's
+        // hand-off: sc1 stores drained before the progress word, sc1 loads here), into tile
+        // i & 1 once SB i - 2 is stored
+        CT vt[NUT];
         uint32_t seen = T[3];
         for (int i = 0; i < n; i++) {
             const uint32_t c = c0 + (uint32_t) i;
             const int tb = i & 1;
-            if (i + 1 < n) issue((int) c + 1, false);
-            // the row above hands over SB c's top halo once its progress reaches c + 1
-            // (k_lfr's hand-off: sc1 stores drained before the progress word; sc1 loads here)
-            if (dep != ~0u && seen < c + 1) {
-                const uint64_t tw0 = LFR_PROF ? clock64() : 0;
-                for (uint32_t k = 0;; k++) {
-                    seen = __builtin_amdgcn_readfirstlane(
-                        __hip_atomic_load((gu32 *) &progress[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                    if (seen >= c + 1) break;
-                    if (k > spin) {
-                        if (lane == 0) atomicAdd(&ctr[2], 1u);
-                        seen = c + 1;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                }
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                if (LFR_PROF) wrow += clock64() - tw0;
-            }
             if (sby > 0) {
+                if (dep != ~0u && seen < c + 1) {
+                    const uint64_t tw0 = LFR_PROF ? clock64() : 0;
+                    for (uint32_t k = 0;; k++) {
+                        seen = __builtin_amdgcn_readfirstlane(
+                            __hip_atomic_load((gu32 *) &progress[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                        if (seen >= c + 1) break;
+                        if (k > spin) {
+                            if (lane == 0) atomicAdd(&ctr[2], 1u);
+                            seen = c + 1;
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    if (LFR_PROF) wrow += clock64() - tw0;
+                }
 #pragma unroll
                 for (int u = 0; u < NUT; u++) {
                     const int ci = lane + 64 * u;
@@ -2468,6 +2475,10 @@ __global__ __launch_bounds__(LFRO_NTH) void k_lfro(const uint32_t *__restrict__ 
                     const PIX *g = lfr_addr<PIX, G>(P, (int) c, sby, pp, rr, kk);
                     const uint64_t lo = ld_sc1(g), hi = ld_sc1((const char *) g + 8);
                     vt[u] = make_uint4((uint32_t) lo, (uint32_t) (lo >> 32), (uint32_t) hi, (uint32_t) (hi >> 32));
+                }
+                if (i >= 2) {
+                    lfro_wait(&F.st1, (uint32_t) i - 1, ctr, &F.abort, wc);
+                    lfro_wait(&F.st2, (uint32_t) i - 1, ctr, &F.abort, wc);
                 }
 #pragma unroll
                 for (int u = 0; u < NUT; u++) {
@@ -2479,19 +2490,9 @@ __global__ __launch_bounds__(LFRO_NTH) void k_lfro(const uint32_t *__restrict__ 
                 }
             }
             lfro_pub(&F.ld_top, (uint32_t) i + 1);
-            if (i + 1 < n) {
-                // tile tb ^ 1 is free once the store wave is done with SB c - 1 and SB c's
-                // waves have copied their left halos out of it
-                lfro_wait(&F.st, (uint32_t) i, ctr, &F.abort, wc);
-                lfro_wait(&F.h0x, (uint32_t) i + 1, ctr, &F.abort, wc);
-                lfro_wait(&F.h1x, (uint32_t) i + 1, ctr, &F.abort, wc);
-                lfro_wait(&F.cx, (uint32_t) i + 1, ctr, &F.abort, wc);
-                stage(tb ^ 1, false);
-                lfro_pub(&F.ld_int, (uint32_t) i + 2);
-            }
         }
-    } else {
-        // ---- S: tiles to HBM, the row hand-off (progress word of this task)
+    } else if (w == 6) {
+        // ---- S1: the bottom rows (sc1) and the row hand-off (progress word of this task)
         for (int i = 0; i < n; i++) {
             const int c = (int) c0 + i, tb = i & 1;
             const bool last = i == n - 1;
@@ -2506,23 +2507,32 @@ __global__ __launch_bounds__(LFRO_NTH) void k_lfro(const uint32_t *__restrict__ 
             }
             lfro_wait(&F.rb, (uint32_t) i + 1, ctr, &F.abort, wc);
             lfro_wait(&F.c, (uint32_t) i + 1, ctr, &F.abort, wc);
-            lfro_wait(&F.h0x, (uint32_t) i + 1, ctr, &F.abort, wc);
             lfro_store<PIX, G>(S, tb, P, c, sby, lane, last, 1);
             if (last) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 if (lane == 0) __hip_atomic_store((gu32 *) &progress[s_task], ncols, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            lfro_store<PIX, G>(S, tb, P, c, sby, lane, last, 2);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            lfro_pub(&F.st, (uint32_t) i + 1);
+            lfro_pub(&F.st1, (uint32_t) i + 1);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+        // ---- S2: the tile's other rows
+        for (int i = 0; i < n; i++) {
+            const int c = (int) c0 + i, tb = i & 1;
+            lfro_wait(&F.rb, (uint32_t) i + 1, ctr, &F.abort, wc);
+            lfro_wait(&F.c, (uint32_t) i + 1, ctr, &F.abort, wc);
+            lfro_wait(&F.h0x, (uint32_t) i + 1, ctr, &F.abort, wc);
+            lfro_store<PIX, G>(S, tb, P, c, sby, lane, i == n - 1, 2);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            lfro_pub(&F.st2, (uint32_t) i + 1);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     if (LFR_PROF && lane == 0) {
         atomicAdd(&lfr_prof[w], wc);
-        atomicAdd(&lfr_prof[6 + w], clock64() - tk0);
-        if (w == 4) { atomicAdd(&lfr_prof[12], wrow); atomicAdd(&lfr_prof[13], (unsigned long long) n); }
-        if (w == 0) atomicAdd(&lfr_prof[14], 1ull);
+        if (w == 0) { atomicAdd(&lfr_prof[8], clock64() - tk0); atomicAdd(&lfr_prof[10], (unsigned long long) n); atomicAdd(&lfr_prof[11], 1ull); }
+        if (w == 5) atomicAdd(&lfr_prof[9], wrow);
     }
     lfrd_retire(ctr, ntasks, 0, tid, LFRO_NTH, &s_last);
 }
@@ -3498,9 +3508,10 @@ static void launch_lfr_g(hipStream_t st, int ntasks, const uint32_t *tasks, cons
     const bool db = !e || atoi(e);
     if (db) {
         if constexpr (G::SH == 1 && G::SV == 1) {
-            // VP9HIP_LFRO=1: the band-overlapped k_lfro instead of k_lfrd (4:2:0, no MC tickets)
+            // the band-overlapped k_lfro (default; 4:2:0, no MC tickets), VP9HIP_LFRO=0: k_lfrd.
+            // Measured (profiles/r04l): C5 k_lfr 1,403 -> 1,021 us per 8K frame, C2 300 -> 238 us
             const char *o = getenv("VP9HIP_LFRO");
-            if (!nmc && o && atoi(o)) {
+            if (!nmc && (!o || atoi(o))) {
                 hipLaunchKernelGGL((k_lfro<PIX, G>), dim3(ntasks), dim3(LFRO_NTH), 0, st, tasks, recs, frames, ctr, ntasks);
                 return;
             }

@@ -1,5 +1,5 @@
-"""The A/B switches of the inter-frame kernels stay bit-exact: the band-overlapped
-k_lfro instead of k_lfrd (VP9HIP_LFRO=1), the single-tile row LF (VP9HIP_LFR_DB=0), one workgroup per MC unit instead of the packed
+"""The A/B switches of the inter-frame kernels stay bit-exact: k_lfrd instead of the
+band-overlapped k_lfro (VP9HIP_LFRO=0), the single-tile row LF (VP9HIP_LFR_DB=0), one workgroup per MC unit instead of the packed
 k_mcq (VP9HIP_MCP=0; the one-column k_mcp with VP9HIP_MCP=2; k_mcq's task slices per unit group, VP9HIP_MCQ_SLICES; 256 threads with VP9HIP_MC64=0; VP9HIP_MCP=1: k_mcp at high bit
 depth only), one
 residual launch per transform size (VP9HIP_RESID_MULTI=0), and frame pipelining
@@ -21,8 +21,8 @@ import bench  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 CASES = [
-    ({"VP9HIP_LFRO": "1"}, "C2", 4),
-    ({"VP9HIP_LFRO": "1"}, "C5", 2),
+    ({"VP9HIP_LFRO": "0"}, "C2", 4),
+    ({"VP9HIP_LFRO": "0"}, "C5", 2),
     ({"VP9HIP_LFR_DB": "0"}, "C2", 4),
     ({"VP9HIP_LFR_DB": "0"}, "C5", 2),
     ({"VP9HIP_MC64": "0", "VP9HIP_MCP": "0"}, "C5", 2),
