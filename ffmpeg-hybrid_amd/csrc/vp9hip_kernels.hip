@@ -501,6 +501,23 @@ DEV void resid_wave(const RJob *__restrict__ jobs, int njobs, int wj, int lane, 
     const COEF *src = coefs + r.coef;
     const bool dconly = TCODE != 4 && act && eob == 1 && txtp == 0;
     const bool full = act && !dconly;
+    // in place (inter residuals, N <= 16): the destination column's prediction pixels are
+    // loaded here, under the coefficient loads and the transform, not after it (one global
+    // round trip less on the wave's chain; 32-point columns keep the late load: registers)
+    constexpr bool PRE = N <= 16;
+    int pq[PRE ? N : 1];
+    PIX *q = nullptr;
+    size_t qp = 0;
+    if (act && RJ_INPLACE(r)) {
+        const FrameDesc &fd = frames[r.frame];
+        const int p = RJ_PLANE(r);
+        q = (PIX *) fd.plane[p] + r.dst + li;
+        qp = (size_t) fd.pitch[p ? 1 : 0];
+        if (PRE) {
+#pragma unroll
+            for (int k = 0; k < (PRE ? N : 1); k++) pq[k] = q[k * qp];
+        }
+    }
 
     // zero the nonzero bounding box, then scatter scan-order coefficients
     if (full)
@@ -571,12 +588,12 @@ DEV void resid_wave(const RJob *__restrict__ jobs, int njobs, int wj, int lane, 
     }
     if (!act) return;
     if (RJ_INPLACE(r)) {
-        const FrameDesc &fd = frames[r.frame];
-        const int p = RJ_PLANE(r);
-        PIX *q = (PIX *) fd.plane[p] + r.dst + li;
-        const int pitch = fd.pitch[p ? 1 : 0], bd = fd.bd;
+        const int bd = frames[r.frame].bd;
 #pragma unroll
-        for (int k = 0; k < N; k++) q[(size_t) k * pitch] = (PIX) clipbd(q[(size_t) k * pitch] + res[k], bd);
+        for (int k = 0; k < N; k++) {
+            const int pv = PRE ? pq[PRE ? k : 0] : (int) q[k * qp];
+            q[k * qp] = (PIX) clipbd(pv + res[k], bd);
+        }
     } else {
 #pragma unroll
         for (int k = 0; k < N; k++) res[k] = res[k] < -32768 ? -32768 : res[k] > 32767 ? 32767 : res[k];
@@ -1654,6 +1671,13 @@ DEV void lfr_top(Chunk16::T (&v)[NU], const LfrPlanes &P, int sbx, int sby, int 
 #define LFR_PROF 0
 #endif
 KP_DEV unsigned long long lfr_prof[16];
+// LFR_PROF builds: one k_lfro workgroup's event timeline (lfro_tl[event][sb - TL_SB0],
+// shader clock), the first workgroup of row task TL_TASK to claim it (lfro_tl_claim)
+#define TL_SB0 40
+#define TL_NSB 8
+#define TL_TASK 30
+KP_DEV unsigned long long lfro_tl[24][TL_NSB];
+KP_DEV unsigned int lfro_tl_claim;
 #define LFR_T(i)                                                                                  \
     do {                                                                                          \
         if (LFR_PROF) { const uint64_t tn = clock64(); pacc[i] += tn - tp; tp = tn; }             \
@@ -1887,11 +1911,11 @@ template <typename PIX, class G> DEV void lfrd_chunk(int ci, bool top, int &p, i
     if (top) lfrd_chunk_rows<PIX, G>(ci, 0, 8, 0, 8, p, r, k);
     else lfrd_chunk_rows<PIX, G>(ci, 8, 64, 8, G::CH, p, r, k);
 }
-template <typename PIX, class G> struct LfrLds {
+template <typename PIX, class G, int NTB = 2> struct LfrLds {
     typedef LfP<PIX, G> L;
-    PIX lt[2][72 * L::YP];
-    PIX ct[2][2][L::CR * L::UVP];
-    uint32_t prog[2][L::PROG / 4];
+    PIX lt[NTB][72 * L::YP];
+    PIX ct[NTB][2][L::CR * L::UVP];
+    uint32_t prog[NTB][L::PROG / 4];
     uint32_t lut[64];
 };
 
@@ -1921,8 +1945,8 @@ DEV void lfrd_store_rows(const PIX *tile, PIX *g0, int pitch, int ra, int rb, in
         }
     }
 }
-template <typename PIX, class G>
-DEV void lfrd_store(const LfrLds<PIX, G> &S, int tb, const LfrPlanes &P, int sbx, int sby, int ml, bool last, int part)
+template <typename PIX, class G, class LDS>
+DEV void lfrd_store(const LDS &S, int tb, const LfrPlanes &P, int sbx, int sby, int ml, bool last, int part)
 {
     typedef LfP<PIX, G> L;
     // part 0: the bottom 8 rows of each plane (sc1: the row below reads them), 1: the other
@@ -2225,6 +2249,10 @@ __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfrd(const uint32_t *__res
 // compiler-only, wavefront scope). Every wait is bounded: one that gives up is counted in
 // ctr[2] like a hand-off timeout (the batch fails with VP9HIP_EBUG), never hangs.
 #define LFRO_NTH 512                              // R, H0, H1, C, L1, L2, S1, S2
+#define LFRO_NTB 3                                // LDS tiles: SB i + 3 reuses SB i's
+#ifndef LFRO_ROLES
+#define LFRO_ROLES 0x76543210u                    // roles of waves 7..0, one nibble each
+#endif
 struct LfroSync { uint32_t ld_int, ld_top, ra, rb, h0x, h1x, h0, h1, cx, c, st1, st2, abort, pad[3]; };
 DEV void lfro_pub(uint32_t *f, uint32_t v)
 {
@@ -2252,8 +2280,8 @@ DEV void lfro_wait(uint32_t *f, uint32_t need, uint32_t *ctr, uint32_t *abort, u
 // 1 the other bottom rows (sc1; the last chunk column only for the row's last SB:
 // otherwise the next tile's part 0) = lfrd_store part 0, 2 everything else (the top
 // halo's corner chunk is never modified) = lfrd_store part 1: compile-time row walks
-template <typename PIX, class G>
-DEV void lfro_store(const LfrLds<PIX, G> &S, int tb, const LfrPlanes &P, int sbx, int sby, int ml, bool last, int part)
+template <typename PIX, class G, class LDS>
+DEV void lfro_store(const LDS &S, int tb, const LfrPlanes &P, int sbx, int sby, int ml, bool last, int part)
 {
     typedef LfP<PIX, G> L;
     typedef Chunk16::T CT;
@@ -2278,7 +2306,7 @@ DEV void lfro_store(const LfrLds<PIX, G> &S, int tb, const LfrPlanes &P, int sbx
         if (in) lf_reg<8 * (k) + 12 - (C0)>(px, 1, ev(2 * (k) + 1, in), bd);                             \
     }
 template <typename PIX, class G>
-__global__ __launch_bounds__(LFRO_NTH) void k_lfro(const uint32_t *__restrict__ tasks, const LFRec *__restrict__ recs,
+__global__ __launch_bounds__(LFRO_NTH) __attribute__((amdgpu_waves_per_eu(4))) void k_lfro(const uint32_t *__restrict__ tasks, const LFRec *__restrict__ recs,
                                                    const FrameDesc *__restrict__ frames, uint32_t *ctr, int ntasks)
 {
     static_assert(G::SH == 1 && G::SV == 1, "4:2:0: one chroma wave holds both planes' 32 lines");
@@ -2287,20 +2315,32 @@ __global__ __launch_bounds__(LFRO_NTH) void k_lfro(const uint32_t *__restrict__ 
     typedef LfrdN<PIX, G> N;
     constexpr int FLP = L::YP, FCP = L::UVP, CW = G::CW, CH = G::CH;
     constexpr int NUI = (N::NINT + 63) / 64, NUT = (N::NTOP + 63) / 64, NPW = (L::PROG / 4 + 63) / 64;
-    __shared__ LfrLds<PIX, G> S;
+    __shared__ LfrLds<PIX, G, LFRO_NTB> S;
     __shared__ LfroSync F;
     __shared__ uint32_t s_task, s_last;
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // wave -> role (R 0, H0 1, H1 2, C 3, L1 4, L2 5, S1 6, S2 7), one nibble per wave; wave
+    // w runs on SIMD w % 4 (-DLFRO_ROLES=...: another permutation, for A/B builds; pairing
+    // each filtering wave with the lightest helper measured equal, profiles/r04l)
+    const int role = (int) ((LFRO_ROLES >> (4 * w)) & 15);
     uint32_t *const progress = ctr + 4;
     __builtin_amdgcn_s_setprio(3);
     // LFR_PROF builds: per wave role, cycles waiting on the workgroup's counters (lfr_prof[w]);
-    // R's lifetime [8], L2's waits for the row above [9], SB steps [10], workgroups [11]
-    uint64_t wc = 0, wrow = 0;
+    // R's lifetime [8], L2's waits for the row above [9], SB steps [10], workgroups [11],
+    // R's steady-state span (SBs n/4 .. 3n/4) [12] over [13] SBs, L2's first-SB wait [14],
+    // R's waits for the top halo [15]
+    uint64_t wc = 0, wrow = 0, wfill = 0, wtop = 0, tq1 = 0, tspan = 0, nspan = 0;
     const uint64_t tk0 = LFR_PROF ? clock64() : 0;
-    if (tid == 0) s_task = atomicAdd(&ctr[0], 1u);
+    __shared__ uint32_t s_tl;
+    if (tid == 0) {
+        s_task = atomicAdd(&ctr[0], 1u);
+        s_tl = LFR_PROF && s_task == TL_TASK && atomicCAS(&lfro_tl_claim, 0u, 1u) == 0u;
+    }
     if (tid < 16) (&F.ld_int)[tid] = 0;
     __syncthreads();
+    const bool tl = LFR_PROF && s_tl;
+#define TLE(e, i) do { if (tl && lane == 0 && (i) >= TL_SB0 && (i) < TL_SB0 + TL_NSB) lfro_tl[e][(i) - TL_SB0] = clock64(); } while (0)
     const uint32_t spin = ctr[3] ? ctr[3] : (1u << 22);
     const uint32_t *T = tasks + tasks[s_task];
     const uint32_t dep = T[0], ncols = T[1], c0 = T[2];
@@ -2313,14 +2353,18 @@ __global__ __launch_bounds__(LFRO_NTH) void k_lfro(const uint32_t *__restrict__ 
     for (int i = tid; i < 64; i += LFRO_NTH) S.lut[i] = lf_eih(i, fd.sharp, bd);
     __syncthreads();
     const int n = (int) (ncols - c0);
-    if (w == 0) {
+    if (role == 0) {
         // ---- R: luma row edges, one lane per pixel column (lf_line_col_wide split at its
         // halves, each waiting for the column pass of the rows it loads)
         for (int i = 0; i < n; i++) {
-            const int tb = i & 1;
+            const int tb = i % LFRO_NTB, tp = tb ? tb - 1 : LFRO_NTB - 1;
             PIX *colp = S.lt[tb] + L::XL + lane;
+            const uint64_t wt0 = wc;
             lfro_wait(&F.ld_top, (uint32_t) i + 1, ctr, &F.abort, wc);
+            if (LFR_PROF) wtop += wc - wt0;
+            TLE(0, i);
             lfro_wait(&F.h0, (uint32_t) i + 1, ctr, &F.abort, wc);
+            TLE(1, i);
             const uint32_t *pw = S.prog[tb] + (LFP_YR + (lane >> 3) * 16) / 4;
             const uint32_t pw0 = pw[0], pw1 = pw[1], pw2 = pw[2], pw3 = pw[3];
             LfEv<true, 16> ev;
@@ -2333,7 +2377,9 @@ __global__ __launch_bounds__(LFRO_NTH) void k_lfro(const uint32_t *__restrict__ 
             for (int r = 1; r < 32; r++) colp[r * FLP] = (PIX) px[r];
 #pragma unroll
             for (int r = 0; r < 8; r++) px[r] = px[32 + r];
+            TLE(2, i);
             lfro_wait(&F.h1, (uint32_t) i + 1, ctr, &F.abort, wc);
+            TLE(3, i);
 #pragma unroll
             for (int r = 8; r < 40; r++) px[r] = colp[(32 + r) * FLP];
             LFRO_EDGE_WIDE(4, 32)
@@ -2346,19 +2392,23 @@ __global__ __launch_bounds__(LFRO_NTH) void k_lfro(const uint32_t *__restrict__ 
 #pragma unroll
             for (int r = 8; r < 40; r++) colp[(32 + r) * FLP] = (PIX) px[r];
             lfro_pub(&F.rb, (uint32_t) i + 1);
+            TLE(4, i);
+            if (LFR_PROF && i == n / 4) tq1 = clock64();
+            if (LFR_PROF && i == (3 * n) / 4 && i > n / 4) { tspan = clock64() - tq1; nspan = (uint64_t) (i - n / 4); }
         }
-    } else if (w <= 2) {
+    } else if (role <= 2) {
         // ---- H0 / H1: luma column edges of pixel rows 0..31 / 32..63, one lane per row
-        const int h = w - 1;
+        const int h = role - 1;
         if (lane < 32) {
             const int row = h * 32 + lane;
             for (int i = 0; i < n; i++) {
-                const int tb = i & 1;
+                const int tb = i % LFRO_NTB, tp = tb ? tb - 1 : LFRO_NTB - 1;
                 lfro_wait(&F.ld_int, (uint32_t) i + 1, ctr, &F.abort, wc);
                 if (i > 0) lfro_wait(h ? &F.rb : &F.ra, (uint32_t) i, ctr, &F.abort, wc);
+                TLE(5 + 2 * h, i);
                 PIX *trow = S.lt[tb] + (row + 8) * FLP;
                 // left halo: SB c - 1's last chunk, final for these rows now
-                if (i > 0) Chunk16::to_lds(Chunk16::from_lds(S.lt[tb ^ 1] + (row + 8) * FLP + 64), trow);
+                if (i > 0) Chunk16::to_lds(Chunk16::from_lds(S.lt[tp] + (row + 8) * FLP + 64), trow);
                 uint32_t *rowp = (uint32_t *) (trow + L::XO);
                 const uint32_t *pwl = S.prog[tb] + (LFP_YC + (row >> 3) * 16) / 4;
                 int lpx[40];
@@ -2367,16 +2417,18 @@ __global__ __launch_bounds__(LFRO_NTH) void k_lfro(const uint32_t *__restrict__ 
                 lfro_pub(h ? &F.h1x : &F.h0x, (uint32_t) i + 1);
                 lf_row_wide_2<PIX>(rowp, pwl, S.lut, bd, lpx, lev);
                 lfro_pub(h ? &F.h1 : &F.h0, (uint32_t) i + 1);
+                TLE(6 + 2 * h, i);
             }
         }
-    } else if (w == 3) {
+    } else if (role == 3) {
         // ---- C: chroma, both planes: column edges (lane = row), then row edges (lane = column)
         const int p = 1 + (lane >= CH), r = lane & (CH - 1);
         for (int i = 0; i < n; i++) {
-            const int tb = i & 1;
+            const int tb = i % LFRO_NTB, tp = tb ? tb - 1 : LFRO_NTB - 1;
             lfro_wait(&F.ld_int, (uint32_t) i + 1, ctr, &F.abort, wc);
+            TLE(9, i);
             PIX *trow = S.ct[tb][p - 1] + (r + 8) * FCP;
-            if (i > 0) Chunk16::to_lds(Chunk16::from_lds(S.ct[tb ^ 1][p - 1] + (r + 8) * FCP + CW), trow);
+            if (i > 0) Chunk16::to_lds(Chunk16::from_lds(S.ct[tp][p - 1] + (r + 8) * FCP + CW), trow);
             uint32_t *rowp = (uint32_t *) (trow + L::XO);
             const uint32_t *pwc = S.prog[tb] + (LFP_CC + (r >> 3) * LFP_CSTRIDE(1)) / 4;
             int lpx[40];
@@ -2385,16 +2437,19 @@ __global__ __launch_bounds__(LFRO_NTH) void k_lfro(const uint32_t *__restrict__ 
             lfro_pub(&F.cx, (uint32_t) i + 1);
             lf_row_narrow_2<PIX>(rowp, pwc, S.lut, bd, lpx, lev);
             wave_sync();
+            TLE(10, i);
             lfro_wait(&F.ld_top, (uint32_t) i + 1, ctr, &F.abort, wc);
+            TLE(11, i);
             PIX *colp = S.ct[tb][p - 1] + L::XL + r;
             const uint32_t *pwr = S.prog[tb] + (LFP_CR(1, 1) + (r >> 3) * LFP_CSTRIDE(1)) / 4;
             lf_line_col_narrow<PIX, FCP, true>(colp, pwr, S.lut, bd);
             lfro_pub(&F.c, (uint32_t) i + 1);
+            TLE(12, i);
         }
-    } else if (w == 4) {
+    } else if (role == 4) {
         // ---- L1: interiors and program words, one SB ahead: SB i's are staged into tile
-        // i & 1 once SB i - 2 is stored (S1, S2) and SB i - 1's waves have copied their left
-        // halos out of that tile; SB i + 1's loads are issued right after
+        // i % LFRO_NTB once SB i - LFRO_NTB is stored (S1, S2) and SB i - LFRO_NTB + 1's waves
+        // have copied their left halos out of that tile; SB i + 1's loads are issued right after
         CT vi[NUI];
         uint32_t pwv[NPW];
         auto issue = [&](int c, bool halo) {
@@ -2415,17 +2470,18 @@ __global__ __launch_bounds__(LFRO_NTH) void k_lfro(const uint32_t *__restrict__ 
         };
         issue((int) c0, c0 > 0);
         for (int i = 0; i < n; i++) {
-            const int tb = i & 1;
+            const int tb = i % LFRO_NTB, tp = tb ? tb - 1 : LFRO_NTB - 1;
             const bool halo = i == 0 && c0 > 0;
-            if (i >= 2) {
-                lfro_wait(&F.st1, (uint32_t) i - 1, ctr, &F.abort, wc);
-                lfro_wait(&F.st2, (uint32_t) i - 1, ctr, &F.abort, wc);
+            if (i >= LFRO_NTB) {
+                lfro_wait(&F.st1, (uint32_t) (i - LFRO_NTB + 1), ctr, &F.abort, wc);
+                lfro_wait(&F.st2, (uint32_t) (i - LFRO_NTB + 1), ctr, &F.abort, wc);
             }
-            if (i >= 1) {
-                lfro_wait(&F.h0x, (uint32_t) i, ctr, &F.abort, wc);
-                lfro_wait(&F.h1x, (uint32_t) i, ctr, &F.abort, wc);
-                lfro_wait(&F.cx, (uint32_t) i, ctr, &F.abort, wc);
+            if (i >= LFRO_NTB - 1) {
+                lfro_wait(&F.h0x, (uint32_t) (i - LFRO_NTB + 2), ctr, &F.abort, wc);
+                lfro_wait(&F.h1x, (uint32_t) (i - LFRO_NTB + 2), ctr, &F.abort, wc);
+                lfro_wait(&F.cx, (uint32_t) (i - LFRO_NTB + 2), ctr, &F.abort, wc);
             }
+            TLE(13, i);
 #pragma unroll
             for (int u = 0; u < NUI; u++) {
                 const int ci = lane + 64 * u;
@@ -2438,17 +2494,18 @@ __global__ __launch_bounds__(LFRO_NTH) void k_lfro(const uint32_t *__restrict__ 
             for (int q = 0; q < NPW; q++)
                 if (lane + 64 * q < L::PROG / 4) S.prog[tb][lane + 64 * q] = pwv[q];
             lfro_pub(&F.ld_int, (uint32_t) i + 1);
+            TLE(14, i);
             if (i + 1 < n) issue((int) (c0 + i) + 1, false);
         }
-    } else if (w == 5) {
+    } else if (role == 5) {
         // ---- L2: top halos, handed over by the row above (its progress reaches c + 1; k_lfr's
         // hand-off: sc1 stores drained before the progress word, sc1 loads here), into tile
-        // i & 1 once SB i - 2 is stored
+        // i % LFRO_NTB once SB i - LFRO_NTB is stored
         CT vt[NUT];
         uint32_t seen = T[3];
         for (int i = 0; i < n; i++) {
             const uint32_t c = c0 + (uint32_t) i;
-            const int tb = i & 1;
+            const int tb = i % LFRO_NTB, tp = tb ? tb - 1 : LFRO_NTB - 1;
             if (sby > 0) {
                 if (dep != ~0u && seen < c + 1) {
                     const uint64_t tw0 = LFR_PROF ? clock64() : 0;
@@ -2464,8 +2521,9 @@ __global__ __launch_bounds__(LFRO_NTH) void k_lfro(const uint32_t *__restrict__ 
                         __builtin_amdgcn_s_sleep(1);
                     }
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    if (LFR_PROF) wrow += clock64() - tw0;
+                    if (LFR_PROF) { wrow += clock64() - tw0; if (i == 0) wfill += clock64() - tw0; }
                 }
+                TLE(15, i);
 #pragma unroll
                 for (int u = 0; u < NUT; u++) {
                     const int ci = lane + 64 * u;
@@ -2476,9 +2534,9 @@ __global__ __launch_bounds__(LFRO_NTH) void k_lfro(const uint32_t *__restrict__ 
                     const uint64_t lo = ld_sc1(g), hi = ld_sc1((const char *) g + 8);
                     vt[u] = make_uint4((uint32_t) lo, (uint32_t) (lo >> 32), (uint32_t) hi, (uint32_t) (hi >> 32));
                 }
-                if (i >= 2) {
-                    lfro_wait(&F.st1, (uint32_t) i - 1, ctr, &F.abort, wc);
-                    lfro_wait(&F.st2, (uint32_t) i - 1, ctr, &F.abort, wc);
+                if (i >= LFRO_NTB) {
+                    lfro_wait(&F.st1, (uint32_t) (i - LFRO_NTB + 1), ctr, &F.abort, wc);
+                    lfro_wait(&F.st2, (uint32_t) (i - LFRO_NTB + 1), ctr, &F.abort, wc);
                 }
 #pragma unroll
                 for (int u = 0; u < NUT; u++) {
@@ -2490,20 +2548,23 @@ __global__ __launch_bounds__(LFRO_NTH) void k_lfro(const uint32_t *__restrict__ 
                 }
             }
             lfro_pub(&F.ld_top, (uint32_t) i + 1);
+            TLE(16, i);
         }
-    } else if (w == 6) {
+    } else if (role == 6) {
         // ---- S1: the bottom rows (sc1) and the row hand-off (progress word of this task)
         for (int i = 0; i < n; i++) {
-            const int c = (int) c0 + i, tb = i & 1;
+            const int c = (int) c0 + i, tb = i % LFRO_NTB;
             const bool last = i == n - 1;
             if (c > 0) {
                 // SB c - 1's last columns (this tile's left halo) are final after this SB's
                 // first column edges: its bottom rows are then complete
                 lfro_wait(&F.h1x, (uint32_t) i + 1, ctr, &F.abort, wc);
                 lfro_wait(&F.cx, (uint32_t) i + 1, ctr, &F.abort, wc);
+                TLE(17, i);
                 lfro_store<PIX, G>(S, tb, P, c, sby, lane, false, 0);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 if (lane == 0) __hip_atomic_store((gu32 *) &progress[s_task], (uint32_t) c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                TLE(18, i);
             }
             lfro_wait(&F.rb, (uint32_t) i + 1, ctr, &F.abort, wc);
             lfro_wait(&F.c, (uint32_t) i + 1, ctr, &F.abort, wc);
@@ -2519,22 +2580,28 @@ __global__ __launch_bounds__(LFRO_NTH) void k_lfro(const uint32_t *__restrict__ 
     } else {
         // ---- S2: the tile's other rows
         for (int i = 0; i < n; i++) {
-            const int c = (int) c0 + i, tb = i & 1;
+            const int c = (int) c0 + i, tb = i % LFRO_NTB;
             lfro_wait(&F.rb, (uint32_t) i + 1, ctr, &F.abort, wc);
             lfro_wait(&F.c, (uint32_t) i + 1, ctr, &F.abort, wc);
             lfro_wait(&F.h0x, (uint32_t) i + 1, ctr, &F.abort, wc);
+            TLE(19, i);
             lfro_store<PIX, G>(S, tb, P, c, sby, lane, i == n - 1, 2);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             lfro_pub(&F.st2, (uint32_t) i + 1);
+            TLE(20, i);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     if (LFR_PROF && lane == 0) {
-        atomicAdd(&lfr_prof[w], wc);
-        if (w == 0) { atomicAdd(&lfr_prof[8], clock64() - tk0); atomicAdd(&lfr_prof[10], (unsigned long long) n); atomicAdd(&lfr_prof[11], 1ull); }
-        if (w == 5) atomicAdd(&lfr_prof[9], wrow);
+        atomicAdd(&lfr_prof[role], wc);
+        if (role == 0) {
+            atomicAdd(&lfr_prof[8], clock64() - tk0); atomicAdd(&lfr_prof[10], (unsigned long long) n); atomicAdd(&lfr_prof[11], 1ull);
+            atomicAdd(&lfr_prof[12], tspan); atomicAdd(&lfr_prof[13], nspan); atomicAdd(&lfr_prof[15], wtop);
+        }
+        if (role == 5) { atomicAdd(&lfr_prof[9], wrow); atomicAdd(&lfr_prof[14], wfill); }
     }
     lfrd_retire(ctr, ntasks, 0, tid, LFRO_NTH, &s_last);
+#undef TLE
 }
 #undef LFRO_EDGE_WIDE
 
@@ -3581,6 +3648,11 @@ int vp9hip_pred_prof_read(unsigned long long *out)
     return hipMemcpyToSymbol(HIP_SYMBOL(pred_prof), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 // LFR_PROF builds: read and clear the k_lfr phase sums (profiling only, not in the ABI)
+// LFR_PROF builds: the k_lfro event timeline (24 x 8 shader-clock values; profiling only)
+int vp9hip_lfro_tl_read(unsigned long long *out)
+{
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(lfro_tl), sizeof(lfro_tl)) == hipSuccess ? 0 : -1;
+}
 int vp9hip_lfr_prof_read(unsigned long long *out)
 {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lfr_prof), 16 * sizeof(unsigned long long)) != hipSuccess) return -1;
