@@ -20,7 +20,10 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <functional>
+#include <memory>
+#include <mutex>
 #include <thread>
 #include <array>
 #include <cstdio>
@@ -200,6 +203,78 @@ struct Staged {
 
 } // namespace
 
+// Host copies of a download (pinned staging chunk -> the caller's planes) split over a few
+// worker threads plus the caller: one thread's memcpy (~8-10 GB/s) was the download path's
+// bound at 8K (99.5 MB per 10-bit frame). Rows of a part are copied one by one when the
+// strides differ.
+struct CopyPool {
+    struct Part { uint8_t *dst; ptrdiff_t dstride; const uint8_t *src; size_t sstride, row; int rows; };
+    std::vector<std::thread> th;
+    std::mutex m;
+    std::condition_variable cv, done_cv;
+    std::vector<Part> parts;
+    size_t next = 0, pending = 0;
+    bool quit = false;
+    static void copy(const Part &q)
+    {
+        if ((size_t) q.dstride == q.row && q.sstride == q.row) { memcpy(q.dst, q.src, q.row * (size_t) q.rows); return; }
+        for (int y = 0; y < q.rows; y++) memcpy(q.dst + (ptrdiff_t) y * q.dstride, q.src + (size_t) y * q.sstride, q.row);
+    }
+    bool take(Part &q)
+    {
+        std::lock_guard<std::mutex> l(m);
+        if (next >= parts.size()) return false;
+        q = parts[next++];
+        return true;
+    }
+    void finish()
+    {
+        std::lock_guard<std::mutex> l(m);
+        if (--pending == 0) done_cv.notify_all();
+    }
+    explicit CopyPool(int n)
+    {
+        for (int i = 0; i < n; i++)
+            th.emplace_back([this] {
+                for (;;) {
+                    Part q;
+                    {
+                        std::unique_lock<std::mutex> l(m);
+                        cv.wait(l, [&] { return quit || next < parts.size(); });
+                        if (quit) return;
+                        q = parts[next++];
+                    }
+                    copy(q);
+                    finish();
+                }
+            });
+    }
+    ~CopyPool()
+    {
+        { std::lock_guard<std::mutex> l(m); quit = true; }
+        cv.notify_all();
+        for (auto &t : th) t.join();
+    }
+    // copy `rows` rows split into parts of the pool's size, the caller taking parts too
+    void run(uint8_t *dst, ptrdiff_t dstride, const uint8_t *src, size_t sstride, size_t row, int rows)
+    {
+        const int np = (int) th.size() + 1, per = (rows + np - 1) / np;
+        {
+            std::lock_guard<std::mutex> l(m);
+            parts.clear();
+            for (int y = 0; y < rows; y += per)
+                parts.push_back({ dst + (ptrdiff_t) y * dstride, dstride, src + (size_t) y * sstride, sstride, row, std::min(per, rows - y) });
+            next = 0;
+            pending = parts.size();
+        }
+        cv.notify_all();
+        Part q;
+        while (take(q)) { copy(q); finish(); }
+        std::unique_lock<std::mutex> l(m);
+        done_cv.wait(l, [&] { return pending == 0; });
+    }
+};
+
 struct vp9hip_ctx {
     int dev = 0;
     hipStream_t st = nullptr;           // main stream: uploads, downloads, group 0
@@ -250,6 +325,7 @@ struct vp9hip_ctx {
     hipStream_t dst_dl = nullptr;
     uint8_t *dl_pin = nullptr;
     hipEvent_t dl_ev[4] = {};
+    std::unique_ptr<CopyPool> dl_pool;  // host copies out of the ring (created at the first download)
     hipEvent_t fill_ev = nullptr;       // after vp9hip_fill_buffers' memsets
     // timing of the last run
     bool timing = true;
@@ -2668,6 +2744,10 @@ extern "C" int vp9hip_download_frame(vp9hip_ctx *c, int buf, uint8_t *const plan
     if (!c->dl_pin) HIPCHK(hipHostMalloc((void **) &c->dl_pin, DL_CHUNK * DL_RING, hipHostMallocDefault));
     for (auto &e : c->dl_ev)
         if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    if (!c->dl_pool) {
+        const char *e = getenv("VP9HIP_DL_THREADS");   // copy threads besides the caller (default 3)
+        c->dl_pool.reset(new CopyPool(e ? std::max(0, std::min(15, atoi(e))) : 3));
+    }
     // chunks of whole rows: D2H into ring slot k, then (once the slot after it is queued)
     // the host copy of slot k into the caller's planes
     struct Piece { int p, y0, ny; };
@@ -2683,9 +2763,12 @@ extern "C" int vp9hip_download_frame(vp9hip_ctx *c, int buf, uint8_t *const plan
     auto issue = [&](size_t i) -> int {
         const Piece &q = pieces[i];
         const size_t row = row_bytes(q.p), pitch = (size_t) c->pitch[q.p ? 1 : 0] * c->bypp;
-        HIPCHK(hipMemcpy2DAsync(c->dl_pin + (i % DL_RING) * DL_CHUNK, row,
-                                c->bufs[buf] + c->plane_off[q.p] + (size_t) q.y0 * pitch, pitch, row, q.ny,
-                                hipMemcpyDeviceToHost, c->dst_dl));
+        const uint8_t *src = c->bufs[buf] + c->plane_off[q.p] + (size_t) q.y0 * pitch;
+        if (pitch == row)   // unpadded rows (widths of 64-multiples): one linear copy
+            HIPCHK(hipMemcpyAsync(c->dl_pin + (i % DL_RING) * DL_CHUNK, src, row * q.ny, hipMemcpyDeviceToHost, c->dst_dl));
+        else
+            HIPCHK(hipMemcpy2DAsync(c->dl_pin + (i % DL_RING) * DL_CHUNK, row, src, pitch, row, q.ny,
+                                    hipMemcpyDeviceToHost, c->dst_dl));
         HIPCHK(hipEventRecord(c->dl_ev[i % DL_RING], c->dst_dl));
         return 0;
     };
@@ -2697,9 +2780,7 @@ extern "C" int vp9hip_download_frame(vp9hip_ctx *c, int buf, uint8_t *const plan
         const size_t row = row_bytes(q.p);
         const uint8_t *src = c->dl_pin + (i % DL_RING) * DL_CHUNK;
         uint8_t *dst = planes[q.p] + (ptrdiff_t) q.y0 * linesize[q.p];
-        if ((size_t) linesize[q.p] == row) memcpy(dst, src, row * q.ny);
-        else
-            for (int y = 0; y < q.ny; y++) memcpy(dst + (ptrdiff_t) y * linesize[q.p], src + (size_t) y * row, row);
+        c->dl_pool->run(dst, linesize[q.p], src, row, row, q.ny);
         if (i + DL_RING < pieces.size())
             if (const int r = issue(i + DL_RING)) return r;
     }
