@@ -81,7 +81,9 @@ static void run_worker(vp9hip_ctx *c)
             planes_of(c, o, &cur, std::make_pair((int) f.width, (int) f.height));
             const bool intra = f.keyframe || f.intraonly;
             for (int r = 0; r < 3; r++) planes_of(c, b.refs[3 * i + r], &refs[r], b.refwh[3 * i + r]);
-            e = vp9o_decode_frame(&f, &cur, intra ? nullptr : refs);
+            // FAKE_NO_RECON=1: no reconstruction (host-side timing of the adapter only)
+            static const bool norecon = getenv("FAKE_NO_RECON") && atoi(getenv("FAKE_NO_RECON"));
+            if (!norecon) e = vp9o_decode_frame(&f, &cur, intra ? nullptr : refs);
         }
         lk.lock();
         if (e && !c->err) c->err = e;

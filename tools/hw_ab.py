@@ -20,10 +20,20 @@ with tempfile.TemporaryDirectory() as td:
     ivf = os.path.join(td, "s.ivf")
     with open(ivf, "wb") as f:
         f.write(v.ivf_write(pkts * reps, W, H))
+    head = os.path.join(ROOT, "tests", "c", "hwaccel_harness")
+    variants = [("B(head)", head, dict(os.environ)), ("A(ab_r03)", os.path.join(ab, "hwaccel_harness"), dict(os.environ, LD_LIBRARY_PATH=ab))]
+    for kv in os.environ.get("HW_AB_ENVS", "").split():      # extra head variants: NAME=VALUE
+        k, val = kv.split("=", 1)
+        variants.append(("B(%s)" % kv, head, dict(os.environ, **{k: val})))
+    for xl in os.environ.get("HW_AB_X", "").split():          # harness:libdir pairs, relative to the repo
+        x, l = xl.split(":", 1)
+        variants.append(("X(%s)" % xl, os.path.join(ROOT, x), dict(os.environ, LD_LIBRARY_PATH=os.path.join(ROOT, l))))
     for r in range(rounds):
-        for tag, exe, env in (("B(head)", os.path.join(ROOT, "tests", "c", "hwaccel_harness"), dict(os.environ)),
-                              ("A(ab_r03)", os.path.join(ab, "hwaccel_harness"), dict(os.environ, LD_LIBRARY_PATH=ab))):
+        for tag, exe, env in variants:
             p = subprocess.run([exe, ivf, "-", str(BPP), "1", "1", "1", "16", "device", "0"], capture_output=True, text=True,
                                timeout=300, env=env)
             f = p.stdout.split()
             print(cfg, tag, "fps %.1f" % (int(f[1]) / float(f[3])) if len(f) >= 4 else p.stderr[-300:], flush=True)
+            for line in p.stderr.splitlines():
+                if "hwaccel trace" in line:
+                    print("   ", line, flush=True)
