@@ -2175,7 +2175,9 @@ static int begin_frame(Walk *w, int retain_segmap)
     if (!w->side) return -1;
     w->side->ntc = 1 << h->log2_tile_cols;
     if (!w->mvref || w->mvref->w != h->w || w->mvref->h != h->h) side_unref(&st->segref);
-    w->segref = st->segref;
+    /* a counted reference: with a pipelined parse the next frame's begin_frame may drop the
+     * stream's reference while this frame's tiles still wait on and read the map */
+    w->segref = side_ref(st->segref);
     return 0;
 }
 
@@ -2286,6 +2288,7 @@ static void walk_free(Walk *w)
     free(w->blocks); free(w->eobs); free(w->coefs);
     side_unref(&w->side);
     side_unref(&w->mvref);
+    side_unref(&w->segref);
 }
 
 /* ------------------------------------------------------------------ API: decode */

@@ -172,7 +172,7 @@ DEV Tx sb_tx(const vp9h_block *blk, const uint32_t *pre, int nb, uint32_t t, int
 }
 
 // The eob of tx t (0 for skipped blocks), range-checked against the packet.
-DEV int tx_eob(const PlanDev &D, const vp9h_block &b, const Tx &tx, const uint32_t *pre, uint32_t b0, uint32_t &st)
+template <class B> DEV int tx_eob(const PlanDev &D, const B &b, const Tx &tx, const uint32_t *pre, uint32_t b0, uint32_t &st)
 {
     if (b.skip) return 0;
     const uint32_t i = D.blk_eob0[b0 + tx.b] + ((pre[tx.k] & 1023) - (pre[3 * tx.b] & 1023)) + (uint32_t) tx.l;
@@ -268,17 +268,19 @@ __global__ __launch_bounds__(256) void k_pblk(PlanDev D)
 
 // ------------------------------------------------------------------ k_psb
 // Residual-job counts: lane k holds key k's count, one ballot per distinct key of a chunk.
-// Intra unit map: each lane ORs into a column of its own (IBP row pitch 65 dwords: lane l
-// of word w at bank (w + l) mod 64, and the final column reduction, lane w reading word w's
-// 64 entries in step, is conflict-free too) -- no same-address LDS atomics.
-#define IBP 65
+// Intra unit map: ORed into IBC copies of the 24 map words (copy = lane & 3), so at most a
+// quarter of a chunk's lanes share an address. Round 4's per-lane map columns (6.2 KB of
+// LDS) removed the conflicts but cut occupancy from 32 to 15 waves per CU and made the
+// kernel 1.58x slower; the blocks are held as 16-byte PBlk for the same reason (LDS 2.2 KB
+// per workgroup: the 32-waves/CU cap binds, not LDS).
+#define IBC 4
 template <int SSH, int SSV>
 __global__ __launch_bounds__(64) void k_psb(PlanDev D)
 {
     constexpr int CW = 16 >> SSH, CH = 16 >> SSV, JCAP = 256 + 2 * CW * CH;
-    __shared__ vp9h_block blk[64];
+    __shared__ PBlk blk[64];
     __shared__ uint32_t pre[3 * 64 + 1];
-    __shared__ uint32_t ibp[24 * IBP];
+    __shared__ uint32_t ibw[24 * IBC];
     const PlanFrame &F = D.frames[blockIdx.y];
     const int s = blockIdx.x, lane = threadIdx.x;
     if (s >= F.sb_cols * F.sb_rows) return;
@@ -286,11 +288,11 @@ __global__ __launch_bounds__(64) void k_psb(PlanDev D)
     const int cols = F.mc.cols, rows = F.mc.rows;
     uint32_t st = 0, b0;
     const int nb = sb_blocks(D, G.slot, b0, st);
-#pragma unroll
-    for (int w = 0; w < 24; w++) ibp[w * IBP + lane] = 0;
+    if (lane < 24 * IBC / 2) { ibw[2 * lane] = 0; ibw[2 * lane + 1] = 0; }
+    vp9h_block own;
     if (lane < nb) {
-        const vp9h_block b = load_block(&D.blocks[b0 + lane]);
-        blk[lane] = b;
+        own = load_block(&D.blocks[b0 + lane]);
+        blk[lane] = pblk(own);
     }
     wsync();
     const uint32_t tot = sb_prefix<SSH, SSV>(blk, nb, cols, rows, G.mine, pre, lane);
@@ -300,8 +302,8 @@ __global__ __launch_bounds__(64) void k_psb(PlanDev D)
         const uint32_t t = t0 + (uint32_t) lane;
         int key = -1;
         if (t < T) {
-            const Tx tx = sb_tx<SSH, SSV>(blk, pre, nb, t, cols, rows);
-            const vp9h_block &b = blk[tx.b];
+            const Tx tx = sb_tx_at<SSH, SSV>(blk, pre, sb_locate(pre, 3 * nb, t), t, cols, rows);
+            const PBlk &b = blk[tx.b];
             const int e = tx_eob(D, b, tx, pre, b0, st);
             ncoef += (uint32_t) e;
             int txtp = 0;
@@ -317,7 +319,7 @@ __global__ __launch_bounds__(64) void k_psb(PlanDev D)
                 uint32_t m = 0;
                 for (int u = ux0; u < ux0 + tx.g.step && u < units; u++) m |= 1u << u;
                 for (int v = uy0; v < uy0 + tx.g.step && v < unitsv; v++)
-                    atomicOr(&ibp[(tx.p * 8 + (v >> 1)) * IBP + lane], m << ((v & 1) * 16));
+                    atomicOr(&ibw[(tx.p * 8 + (v >> 1)) * IBC + (lane & (IBC - 1))], m << ((v & 1) * 16));
             }
         }
         uint64_t pend = __ballot(key >= 0);
@@ -330,8 +332,8 @@ __global__ __launch_bounds__(64) void k_psb(PlanDev D)
     }
     // MC units of the SB's inter blocks
     uint32_t nmc = 0;
-    if (lane < nb && G.mine && !blk[lane].intra) {
-        if (mc_refs_ok(blk[lane], F.mc)) nmc = (uint32_t) pl_mc_block(blk[lane], F.mc, 0, [](const McUnit &) {});
+    if (lane < nb && G.mine && !own.intra) {
+        if (mc_refs_ok(own, F.mc)) nmc = (uint32_t) pl_mc_block(own, F.mc, 0, [](const McUnit &) {});
         else st |= PLS_REF;
     }
     nmc = wsum(nmc);
@@ -339,8 +341,8 @@ __global__ __launch_bounds__(64) void k_psb(PlanDev D)
     wsync();
     uint32_t ib = 0;
     if (lane < 24)
-#pragma unroll 16
-        for (int j = 0; j < 64; j++) ib |= ibp[lane * IBP + j];
+#pragma unroll
+        for (int j = 0; j < IBC; j++) ib |= ibw[lane * IBC + j];
     if (lane < 20) {
         const uint32_t ci = cnt_idx(D, F, G.seg, G.slot, lane >> 2, lane & 3);
         if (inb(D, ci, D.cap_cnt, 2u)) D.cnt[ci] = kcnt;
