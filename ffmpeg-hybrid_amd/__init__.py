@@ -115,7 +115,7 @@ ABI_SYMBOLS = ["vp9hip_open", "vp9hip_close", "vp9hip_configure", "vp9hip_submit
                "vp9hip_alg_bytes", "vp9hip_plan_stats", "vp9hip_plan_sb_costs", "vp9hip_abi_version", "vp9hip_set_graph",
                "vp9hip_stage_batch_tiles", "vp9hip_batch_phases", "vp9hip_phase_frames", "vp9hip_run_phase",
                "vp9hip_stripe", "vp9hip_frame_device", "vp9hip_batch_groups", "vp9hip_set_batch_slot", "vp9hip_sync_slot", "vp9hip_slot_busy",
-               "vp9hip_fill_buffers", "vp9hip_device_info",
+               "vp9hip_fill_buffers", "vp9hip_device_info", "vp9hip_test_hooks",
                "vp9h_decode_frame", "vp9h_encode_frame", "vp9h_frame_free", "vp9h_buffer_free",
                "vp9h_stream_open", "vp9h_stream_close", "vp9h_stream_set_threads", "vp9h_stream_decode", "vp9h_stream_encode",
                "vp9h_enc_defaults", "vp9h_superframe_split", "vp9h_frame_type", "vp9h_frame_peek",
@@ -163,6 +163,8 @@ def lib():
                                        ctypes.POINTER(ctypes.c_void_p)]
     L.vp9hip_device_info.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
     L.vp9hip_fill_buffers.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    L.vp9hip_test_hooks.argtypes = [ctypes.c_int, ctypes.c_uint32]
+    L.vp9hip_test_hooks.restype = None
     L.vp9hip_run_batch.argtypes = [vp]
     L.vp9hip_sync.argtypes = [vp]
     L.vp9hip_download_frame.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
@@ -439,6 +441,13 @@ def visible(planes, width, height, ss_h=1, ss_v=1):
 def decode_frame(data):
     """Host entropy decode of one VP9 frame -> DecodedFrame (pass-1 packet)."""
     return DecodedFrame(data)
+
+
+def test_hooks(reject_batch=0, lfr_spin=0):
+    """Test hooks copied by every context opened afterwards (vp9hip_test_hooks): the
+    reject_batch-th static-plan batch gets an intra mode the planner rejects; lfr_spin bounds
+    the row loop filter's hand-off waits (0, 0: off)."""
+    lib().vp9hip_test_hooks(int(reject_batch), int(lfr_spin))
 
 
 def device_info(device):

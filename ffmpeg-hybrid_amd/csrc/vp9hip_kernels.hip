@@ -1,18 +1,17 @@
-// gfx950 (MI355X) kernels of the VP9 hybrid decoder pixel path.
+// gfx950 (MI355X) kernels of the VP9 hybrid decoder pixel path (DESIGN.md §3, §5).
 //
-//   k_recon  — one workgroup (4 waves) per 64x64 superblock: intra prediction +
-//              inverse transform + residual add for every tx block of the SB, in
-//              host-computed dependency levels, entirely in LDS; superblocks are
-//              launched along an SB wavefront (left/top/top-left dependencies only,
-//              tile columns independent: vp9recon.c:45-47).
-//   k_lf     — one workgroup per SB: the in-loop deblocking filter of
-//              ff_vp9_loopfilter_sb (vp9lpf.c:183-230) on a 72x72 LDS tile, one lane
-//              per pixel row (column edges) then one lane per pixel column (row
-//              edges); SBs launched along the t = x + 2y wavefront that reproduces the
-//              reference's raster order.
-//   k_mc     — sub-pel motion compensation, unscaled and scaled references
-//              (vp9dsp_template.c:1969-2569), edge clamping (videodsp_template.c:27-105),
-//              one thread per pixel.
+//   k_resid / k_resid_dev / k_resid_multi — inverse DCT / ADST / WHT of every coded tx block
+//              (vp9dsp_template.c:1155-1754): one lane per column, 64 / N jobs per wave,
+//              LDS transpose; intra residuals to int16 scratch, inter ones added in place.
+//   k_pred   — intra prediction passes of an SB (vp9recon.c:235-364, the 15 predictors of
+//              vp9dsp_template.c:28-1106 as a per-pixel formula table) + residual add.
+//   k_lf     — the deblocking filter of one SB (ff_vp9_loopfilter_sb, vp9lpf.c:183-230) on
+//              an LDS tile, SBs launched along the t = x + 2y wavefront (raster order).
+//   k_plf    — fused keyframe launches: intra diagonal t and LF diagonal t - 3.
+//   k_lfrd / k_lfro — the row-pipelined loop filter of narrow phases: one workgroup per SB
+//              row, hand-offs between rows through sc1 stores and progress words.
+//   k_mcq    — sub-pel motion compensation, unscaled and scaled references, compound
+//              (vp9dsp_template.c:1969-2569), edge clamping (videodsp_template.c:27-105).
 //
 // Arithmetic restates vp9dsp_template.c bit-exactly: 8-bit transforms run in
 // wrapping 32-bit arithmetic with int16 intermediates (dctint int / dctcoef int16,
@@ -478,7 +477,11 @@ template <int N, typename COEF> struct RWave { static constexpr int E = (64 / N)
 
 // One wave of residual work: jobs [wj * 64/N, (wj + 1) * 64/N) of `jobs`, n lanes per
 // job; cbw = the wave's LDS block (RWave<N, COEF>::E coefficients, rows padded to S).
-template <int N, int TCODE, typename PIX, class M, typename COEF>
+// PREQ: in-place jobs load their prediction pixels before the transform (the inter
+// launches); the keyframe launches (k_resid_dev) write scratch and keep their registers:
+// they run beside the other slot's k_plf chains, whose co-resident waves the extra
+// registers cost (r04's PREQ everywhere: C3 10,245 -> 9,863 fps on one box, profiles/r05b).
+template <int N, int TCODE, typename PIX, class M, typename COEF, bool PREQ = true>
 DEV void resid_wave(const RJob *__restrict__ jobs, int njobs, int wj, int lane, const FrameDesc *__restrict__ frames,
                     const COEF *__restrict__ coefs, int16_t *__restrict__ resid, COEF *cbw)
 {
@@ -504,7 +507,7 @@ DEV void resid_wave(const RJob *__restrict__ jobs, int njobs, int wj, int lane, 
     // in place (inter residuals, N <= 16): the destination column's prediction pixels are
     // loaded here, under the coefficient loads and the transform, not after it (one global
     // round trip less on the wave's chain; 32-point columns keep the late load: registers)
-    constexpr bool PRE = N <= 16;
+    constexpr bool PRE = PREQ && N <= 16;
     int pq[PRE ? N : 1];
     PIX *q = nullptr;
     size_t qp = 0;
@@ -628,7 +631,7 @@ __global__ __launch_bounds__(64 * RWAVES) void k_resid_dev(const RJob *__restric
     const int njobs = j1 > j0 ? (int) (j1 - j0) : 0;
     const int wave = threadIdx.x >> 6, wj = (int) blockIdx.x * RWAVES + wave;
     if (wj * CAP >= njobs) return;
-    resid_wave<N, TCODE, PIX, M, COEF>(jobs + j0, njobs, wj, threadIdx.x & 63, frames, coefs, resid, cbs[wave]);
+    resid_wave<N, TCODE, PIX, M, COEF, false>(jobs + j0, njobs, wj, threadIdx.x & 63, frames, coefs, resid, cbs[wave]);
 }
 
 // Every transform size of a phase in ONE launch (narrow, level-scheduled phases: the chain
@@ -1577,7 +1580,7 @@ __global__ __launch_bounds__(LfNT<G>::NT) void k_lf(const uint32_t *__restrict__
     lf_sb<PIX, G, LfNT<G>::NT>(recs[list[blockIdx.x]], frames, S, threadIdx.x, dbg);
 }
 
-// ------------------------------------------------------------- k_lfr
+// ------------------------------------------------------------- k_lfrd / k_lfro
 // Row-pipelined loop filter: one workgroup filters one SB row of one frame, SB by SB left to
 // right (the raster SB order of ff_vp9_loopfilter_sb's callers, vp9.c:1522-1551 /
 // vp9lpf.c:183-230), instead of one launch per x + 2y wavefront diagonal.
@@ -1615,7 +1618,7 @@ typedef __attribute__((address_space(1))) uint32_t gu32;
 DEV uint64_t ld_sc1(const void *p) { return __hip_atomic_load((gu64 *) p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 DEV void st_sc1(void *p, uint64_t v) { __hip_atomic_store((gu64 *) p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
-// k_lfr pieces: chunk (p, r, k) of SB (sbx, sby) in its plane. Plane bases are offsets from
+// row-LF pieces: chunk (p, r, k) of SB (sbx, sby) in its plane. Plane bases are offsets from
 // plane 0 chosen by selects (an indexed array of pointers would live in scratch).
 struct LfrPlanes {
     uint64_t b0, d1, d2;
@@ -1630,42 +1633,7 @@ template <typename PIX, class G> DEV PIX *lfr_addr(const LfrPlanes &P, int sbx, 
     const uint64_t a = P.b0 + (p == 1 ? P.d1 : 0) + (p == 2 ? P.d2 : 0);
     return (PIX *) a + (ptrdiff_t) gy * (p ? P.pit1 : P.pit0) + gx;
 }
-// issue the plain loads of SB (sbx, sby)'s interior chunks (and its left halo from HBM when
-// `halo`), all in flight before any use
-template <typename PIX, class G, int NT, int NU>
-DEV void lfr_issue(Chunk16::T (&v)[NU], const LfrPlanes &P, int sbx, int sby, int lane, bool halo)
-{
-    typedef LfP<PIX, G> L;
-#pragma unroll
-    for (int u = 0; u < NU; u++) {
-        const int ci = lane + u * NT;
-        int p, r, k;
-        lf_chunk<PIX, G>(ci, p, r, k);
-        if (ci < L::NCHUNK && r >= 8 && (k > 0 || halo)) {
-            const v4u x = *(const gv4u *) lfr_addr<PIX, G>(P, sbx, sby, p, r, k);
-            v[u] = make_uint4(x.x, x.y, x.z, x.w);
-        }
-    }
-}
-
-// top halo (y = -8..-1, x >= 0) of SB (sbx, sby): rows row sby - 1 handed off, sc1 loads only
-template <typename PIX, class G, int NT, int NU>
-DEV void lfr_top(Chunk16::T (&v)[NU], const LfrPlanes &P, int sbx, int sby, int lane)
-{
-    typedef LfP<PIX, G> L;
-#pragma unroll
-    for (int u = 0; u < NU; u++) {
-        const int ci = lane + u * NT;
-        int p, r, k;
-        lf_chunk<PIX, G>(ci, p, r, k);
-        if (ci >= L::NCHUNK || r >= 8 || k == 0 || sby == 0) continue;
-        const PIX *g = lfr_addr<PIX, G>(P, sbx, sby, p, r, k);
-        const uint64_t lo = ld_sc1(g), hi = ld_sc1((const char *) g + 8);
-        v[u] = make_uint4((uint32_t) lo, (uint32_t) (lo >> 32), (uint32_t) hi, (uint32_t) (hi >> 32));
-    }
-}
-
-// LFR_PROF builds (profiling only, tools/lfr_prof.sh): lane 0 of each k_lfr workgroup sums
+// LFR_PROF builds (profiling only, tools/lfr_prof.sh): lane 0 of each row-LF workgroup sums
 // the shader-clock cycles of its SB-step phases into lfr_prof[] (vp9hip_lfr_prof_read)
 #ifndef LFR_PROF
 #define LFR_PROF 0
@@ -1682,215 +1650,7 @@ KP_DEV unsigned int lfro_tl_claim;
     do {                                                                                          \
         if (LFR_PROF) { const uint64_t tn = clock64(); pacc[i] += tn - tp; tp = tn; }             \
     } while (0)
-// PF: the next SB's interior loads are issued before this SB's filtering (in registers)
-template <typename PIX, class G, bool PF>
-__global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfr(const uint32_t *__restrict__ tasks, const LFRec *__restrict__ recs,
-                                                     const FrameDesc *__restrict__ frames, uint32_t *ctr, int ntasks)
-{
-    constexpr int NT = LfNT<G>::NT;
-    typedef LfP<PIX, G> L;
-    typedef Chunk16::T CT;
-    constexpr int FLP = L::YP, FCP = L::UVP, CW = G::CW, CPX = L::CPX;
-    constexpr int NU = (L::NCHUNK + NT - 1) / NT, NUM = (L::NCHUNK + 63) / 64;
-    __shared__ LfLds<PIX, G> S;
-    __shared__ uint32_t s_task, s_last, s_pre;
-    const int lane = threadIdx.x;
-    uint32_t *const progress = ctr + 4;
-    // the row chain is the latency path of the phase: its waves issue first on their SIMDs
-    __builtin_amdgcn_s_setprio(3);
-    uint64_t pacc[14] = {0}, tp = LFR_PROF ? clock64() : 0;
-    const uint64_t tk0 = tp;
-    if (lane == 0) s_task = atomicAdd(&ctr[0], 1u);
-    __syncthreads();
-    const uint32_t *T = tasks + tasks[s_task];
-    const uint32_t dep = T[0], ncols = T[1], c0 = T[2];
-    uint32_t seen = T[3];                                  // lane 0: dep's columns known done
-    // spin bound of a hand-off wait (ctr[3], 0 = 2^22 polls; a small bound is a test hook
-    // that forces the timeout path); a wait that gives up is counted in ctr[2]
-    const uint32_t spin = ctr[3] ? ctr[3] : (1u << 22);
-    const LFRec &rec0 = recs[T[4]];
-    const FrameDesc &fd = frames[rec0.frame];
-    const int bd = fd.bd, sby = rec0.sby;
-    LfrPlanes P;
-    P.b0 = fd.plane[0]; P.d1 = fd.plane[1] - P.b0; P.d2 = fd.plane[2] - P.b0;
-    P.pit0 = fd.pitch[0]; P.pit1 = fd.pitch[1];
-    for (int i = lane; i < 64; i += NT) S.lut[i] = lf_eih(i, fd.sharp, bd);
-    CT v[NU];
-#pragma unroll
-    for (int u = 0; u < NU; u++) v[u] = Chunk16::zero();
-    // lanes NT.. form the store wave: it issues every global store of the task, so the
-    // filtering waves' load waits never queue behind stores (vmcnt retires in order)
-    const bool mover = lane >= NT;
-    const int ml = lane - NT;
-    if (!mover) lfr_issue<PIX, G, NT, NU>(v, P, c0, sby, lane, c0 > 0);
-    LFR_T(7);
-    for (uint32_t c = c0; c < ncols; c++) {
-        const int sbx = (int) c;
-        const LFRec &rec = recs[T[4 + c - c0]];
-        static_assert(L::PROG / 4 <= NT, "one program word per filtering lane");
-        uint32_t pwv = 0;                       // this SB's program word, loaded with its interior
-        if (!mover) {
-            if (!PF && c > c0) lfr_issue<PIX, G, NT, NU>(v, P, sbx, sby, lane, false);
-            LFR_T(8);
-            if (lane < L::PROG / 4) pwv = ((const uint32_t *) rec.prog)[lane];
-            // left halo (x < 0): this workgroup's previous tile, read from LDS before the
-            // barrier below (SB c0's came from HBM with its interior)
-            if (c > c0) {
-#pragma unroll
-                for (int u = 0; u < NU; u++) {
-                    const int ci = lane + u * NT;
-                    int p, r, k;
-                    lf_chunk<PIX, G>(ci, p, r, k);
-                    if (ci < L::NCHUNK && r >= 8 && k == 0) {
-                        const PIX *t = p ? S.ct[p - 1] + r * FCP : S.lt + r * FLP;
-                        v[u] = Chunk16::from_lds(t + (p ? CW : 64));      // x = 64 - XL .. 63 (CW for chroma)
-                    }
-                }
-            }
-            LFR_T(9);
-        }
-        __syncthreads();                        // every lane has read the previous tile
-        LFR_T(0);
-        // interior (and left halo) into LDS, then the column pass: it rewrites rows 0..63 only,
-        // so it runs before the row above has handed over this SB's top halo. Usually the row
-        // above is already far enough: then the top halo's loads are issued before the column
-        // pass and run under it
-        if (!mover) {
-            if (lane < L::PROG / 4) S.prog[lane] = pwv;
-#pragma unroll
-            for (int u = 0; u < NU; u++) {
-                const int ci = lane + u * NT;
-                int p, r, k;
-                lf_chunk<PIX, G>(ci, p, r, k);
-                if (ci < L::NCHUNK && r >= 8) {
-                    PIX *t = p ? S.ct[p - 1] + r * FCP : S.lt + r * FLP;
-                    Chunk16::to_lds(v[u], t + CPX * k);
-                }
-            }
-            if (lane == 0) {
-                if (dep != ~0u && seen < c + 1)
-                    seen = __hip_atomic_load((gu32 *) &progress[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                s_pre = dep == ~0u || seen >= c + 1;
-            }
-        }
-        // The hand-off's ordering is the hardware's, not the memory model's: the producer's
-        // sc1 (write-through) stores drain (vmcnt(0)) before its progress store, and every
-        // consumer load of the handed-off rows is an sc1 load issued after lane 0 saw the
-        // progress word (MI355X_MICROARCH.md, inter-workgroup visibility, Valid forms row 1).
-        // This fence is deliberately wavefront-scope: it only keeps the compiler from moving
-        // those loads above the poll; an agent-scope acquire would add a cache invalidate
-        // per SB step for bytes that are never read through the cache.
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        __syncthreads();
-        const bool pre = s_pre;
-        LFR_T(1);
-        if (!mover) {
-            if (pre) lfr_top<PIX, G, NT, NU>(v, P, sbx, sby, lane);
-            // the next SB's interior loads run under this SB's filtering
-            if (PF && c + 1 < ncols) lfr_issue<PIX, G, NT, NU>(v, P, sbx + 1, sby, lane, false);
-        }
-        lf_passes<PIX, G, NT, 1>(S, lane, bd);  // the store wave has no lines: barriers only
-        LFR_T(2);
-        // SB c - 1's bottom rows are final now (this SB's left-edge column filtering was the
-        // last to touch them): the store wave writes its last XL columns of them sc1, drains
-        // and stores the progress word, while the filtering waves go on. Those bytes are not
-        // stored again.
-        if (mover && sbx > 0) {
-#pragma unroll
-            for (int u = 0; u < NUM; u++) {
-                const int ci = ml + u * 64;
-                int p, r, k;
-                lf_chunk<PIX, G>(ci, p, r, k);
-                if (ci >= L::NCHUNK || r < (p ? L::CR : 72) - 8 || k != 0) continue;
-                const PIX *t = p ? S.ct[p - 1] + r * FCP : S.lt + r * FLP;
-                PIX *g = lfr_addr<PIX, G>(P, sbx, sby, p, r, k);
-                const CT w = Chunk16::from_lds(t);
-                st_sc1(g, (uint64_t) w.x | (uint64_t) w.y << 32);
-                st_sc1((char *) g + 8, (uint64_t) w.z | (uint64_t) w.w << 32);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (ml == 0) __hip_atomic_store((gu32 *) &progress[s_task], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        // otherwise the row pass waits for the row above through SB c + 1's column pass
-        if (!pre) {
-            if (lane == 0 && dep != ~0u) {
-                const uint32_t need = c + 1;
-                for (uint32_t n = 0; seen < need; n++) {
-                    seen = __hip_atomic_load((gu32 *) &progress[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (seen >= need) break;
-                    if (n > spin) { atomicAdd(&ctr[2], 1u); seen = need; break; }
-                    __builtin_amdgcn_s_sleep(1);
-                }
-            }
-            if (c == c0) LFR_T(12); else LFR_T(10);
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");      // see the fence above
-            __syncthreads();
-            LFR_T(11);
-            if (!mover) lfr_top<PIX, G, NT, NU>(v, P, sbx, sby, lane);
-        }
-        if (!mover) {
-#pragma unroll
-            for (int u = 0; u < NU; u++) {
-                const int ci = lane + u * NT;
-                int p, r, k;
-                lf_chunk<PIX, G>(ci, p, r, k);
-                if (ci >= L::NCHUNK || r >= 8 || k == 0) continue;
-                PIX *t = p ? S.ct[p - 1] + r * FCP : S.lt + r * FLP;
-                Chunk16::to_lds(v[u], t + CPX * k);
-            }
-        }
-        __syncthreads();
-        LFR_T(3);
-        lf_passes<PIX, G, NT, 2>(S, lane, bd);
-        LFR_T(4);
-        if (LFR_PROF && !pre) pacc[5]++;
-        if (LFR_PROF) pacc[6]++;
-        // store wave: rows [0, h) x cols [-XL, w) and rows [-8, 0) x cols [0, w), except the
-        // bytes published above; the bottom rows sc1 (row r + 1 reads them). Its LDS reads
-        // finish before the next SB's first barrier.
-        if (mover) {
-#pragma unroll
-            for (int u = 0; u < NUM; u++) {
-                const int ci = ml + u * 64;
-                int p, r, k;
-                lf_chunk<PIX, G>(ci, p, r, k);
-                if (ci >= L::NCHUNK || (k == 0 && (sbx == 0 || r < 8 || r >= (p ? L::CR : 72) - 8)) || (r < 8 && sby == 0))
-                    continue;
-                const PIX *t = p ? S.ct[p - 1] + r * FCP : S.lt + r * FLP;
-                const CT w = Chunk16::from_lds(t + CPX * k);
-                PIX *g = lfr_addr<PIX, G>(P, sbx, sby, p, r, k);
-                if (r >= (p ? L::CR : 72) - 8) {
-                    st_sc1(g, (uint64_t) w.x | (uint64_t) w.y << 32);
-                    st_sc1((char *) g + 8, (uint64_t) w.z | (uint64_t) w.w << 32);
-                } else {
-                    v4u x; x.x = w.x; x.y = w.y; x.z = w.z; x.w = w.w;
-                    *(gv4u *) g = x;
-                }
-            }
-            if (c + 1 == ncols) {               // the row's last SB: its bottom rows are final
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if (ml == 0) __hip_atomic_store((gu32 *) &progress[s_task], ncols, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-        }
-    }
-    if (LFR_PROF && lane == 0) {
-        pacc[7] = clock64() - tk0;
-        for (int i = 0; i < 14; i++) atomicAdd(&lfr_prof[i], pacc[i]);
-        atomicAdd(&lfr_prof[14], 1ull);
-    }
-    // the last workgroup to finish resets the counters (every ticket is taken by then);
-    // the store wave's last progress store has completed before this barrier
-    __syncthreads();
-    if (lane == 0) s_last = atomicAdd(&ctr[1], 1u) == (uint32_t) ntasks - 1;
-    __syncthreads();
-    if (s_last) {
-        for (int i = lane; i < ntasks; i += NT) progress[i] = 0;
-        if (lane == 0) { ctr[0] = 0; ctr[1] = 0; }
-    }
-}
-
-// k_lfrd: k_lfr with two LDS tiles (SB c in tile (c - c0) & 1). The store wave writes SB
+// k_lfrd: the row-pipelined loop filter with two LDS tiles (SB c in tile (c - c0) & 1). The store wave writes SB
 // c - 1's tile to HBM while the filtering waves run SB c's column pass, instead of between
 // SB c - 1's row pass and SB c's first barrier (where every lane of the workgroup waited
 // for its ~17 serialised LDS-read + store rounds); SB c + 1's interior loads and program
@@ -1899,7 +1659,7 @@ __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfr(const uint32_t *__rest
 // chunk column. The last chunk column of tile c - 1 (rows >= 8) is not stored from tile
 // c - 1: tile c's left halo holds the same pixels after SB c's column pass (the final
 // ones) and is stored from there (bottom rows at the hand-off, the rest with tile c).
-// Hand-off, task table, spin bound and counter reset as k_lfr.
+// Hand-off, task table, spin bound and counter reset as described at the top of this section.
 template <typename PIX, class G> DEV void lfrd_chunk_rows(int ci, int ry0, int nry, int rc0, int nrc, int &p, int &r, int &k)
 {
     typedef LfP<PIX, G> L;
@@ -2004,33 +1764,22 @@ DEV void lfrd_top(Chunk16::T (&v)[NUT], const LfrPlanes &P, int sbx, int sby, in
     }
 }
 
-// Frame pipelining inside one k_lfrd launch (chain positions of inter streams): tickets
-// ntasks .. ntasks + nmc - 1 are the next position's MC units (one unit per workgroup, in
-// the planner's raster SB order). A unit reads reference rows that this launch may still be
-// filtering; it waits for the row tasks that finish those rows (the reference's
-// ff_progress_frame_await, vp9recon.c:392-395, reported per SB row at vp9.c:1434). Tickets
-// are taken in workgroup start order and every row task's ticket is below every MC
-// ticket, so a unit waits only on row tasks held by running workgroups. Defined with k_mc.
-template <typename PIX, class G>
-DEV void lfmc_ticket(const McUnit &u, const FrameDesc *__restrict__ frames, const uint32_t *__restrict__ mw,
-                     const uint32_t *rdone, uint32_t *ctr, uint32_t spin, int nth);
-// the last workgroup of a k_lfrd launch (row tasks and MC tickets) zeroes its counters,
-// row progress and row-done words for the next launch (graph replay)
-DEV void lfrd_retire(uint32_t *ctr, int ntasks, int nmc, int lane, int nth, uint32_t *s_last)
+// the last workgroup of a row-LF launch zeroes its counters and row progress words for the
+// next launch (graph replay)
+DEV void lfrd_retire(uint32_t *ctr, int ntasks, int lane, int nth, uint32_t *s_last)
 {
     __syncthreads();
-    if (lane == 0) *s_last = atomicAdd(&ctr[1], 1u) == (uint32_t) (ntasks + nmc) - 1;
+    if (lane == 0) *s_last = atomicAdd(&ctr[1], 1u) == (uint32_t) ntasks - 1;
     __syncthreads();
     if (*s_last) {
-        for (int i = lane; i < 2 * ntasks; i += nth) ctr[4 + i] = 0;
+        for (int i = lane; i < ntasks; i += nth) ctr[4 + i] = 0;
         if (lane == 0) { ctr[0] = 0; ctr[1] = 0; }
     }
 }
 
 template <typename PIX, class G>
 __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfrd(const uint32_t *__restrict__ tasks, const LFRec *__restrict__ recs,
-                                                      const FrameDesc *__restrict__ frames, uint32_t *ctr, int ntasks,
-                                                      const McUnit *__restrict__ mcu, int nmc, const uint32_t *__restrict__ mw)
+                                                      const FrameDesc *__restrict__ frames, uint32_t *ctr, int ntasks)
 {
     constexpr int NT = LfNT<G>::NT;
     typedef LfP<PIX, G> L;
@@ -2049,13 +1798,6 @@ __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfrd(const uint32_t *__res
     __syncthreads();
     // spin bound of a wait (ctr[3], 0 = 2^22 polls; a small bound is a test hook)
     const uint32_t spin = ctr[3] ? ctr[3] : (1u << 22);
-    uint32_t *const rdone = progress + ntasks;      // per row task: 1 once its rows are released
-    if (s_task >= (uint32_t) ntasks) {              // an MC unit of the next chain position
-        __builtin_amdgcn_s_setprio(0);
-        lfmc_ticket<PIX, G>(mcu[s_task - ntasks], frames, mw, rdone, ctr, spin, NT + 64);
-        lfrd_retire(ctr, ntasks, nmc, lane, NT + 64, &s_last);
-        return;
-    }
     const uint32_t *T = tasks + tasks[s_task];
     const uint32_t dep = T[0], ncols = T[1], c0 = T[2];
     uint32_t seen = T[3];
@@ -2111,7 +1853,7 @@ __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfrd(const uint32_t *__res
             }
         }
         LFR_T(8);
-        // k_lfr's hand-off ordering; wavefront-scope fence: see k_lfr
+        // the hand-off ordering above; wavefront-scope fence
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         __syncthreads();
         LFR_T(0);
@@ -2143,7 +1885,7 @@ __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfrd(const uint32_t *__res
         }
         __syncthreads();
         LFR_T(13);
-        // SB c - 1's last columns are final: publish its bottom rows (k_lfr's hand-off) while
+        // SB c - 1's last columns are final: publish its bottom rows (the hand-off above) while
         // the filtering waves run the rest of the column pass
         if (mover && sbx > 0) {
             // the left halo's bottom 8 rows of each plane: one chunk per lane 0..23
@@ -2212,23 +1954,13 @@ __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfrd(const uint32_t *__res
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (ml == 0) __hip_atomic_store((gu32 *) &progress[s_task], ncols, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (nmc) {
-            // MC tickets of this launch read the row: the store wave (the only storing wave)
-            // releases its plain stores at agent scope, then sets the row-done word
-            // (MI355X_MICROARCH.md, inter-workgroup visibility, Valid forms: producer); after
-            // the hand-off word above, so the row below never waits for the write-back
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (ml == 0) __hip_atomic_store((gu32 *) &rdone[s_task], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
     }
     if (LFR_PROF && lane == 0) {
         pacc[7] = clock64() - tk0;
         for (int i = 0; i < 14; i++) atomicAdd(&lfr_prof[i], pacc[i]);
         atomicAdd(&lfr_prof[14], 1ull);
     }
-    lfrd_retire(ctr, ntasks, nmc, lane, NT + 64, &s_last);
+    lfrd_retire(ctr, ntasks, lane, NT + 64, &s_last);
 }
 
 // k_lfro: k_lfrd with SB c's luma row pass overlapped with SB c + 1's luma column pass
@@ -2498,7 +2230,7 @@ __global__ __launch_bounds__(LFRO_NTH) __attribute__((amdgpu_waves_per_eu(4))) v
             if (i + 1 < n) issue((int) (c0 + i) + 1, false);
         }
     } else if (role == 5) {
-        // ---- L2: top halos, handed over by the row above (its progress reaches c + 1; k_lfr's
+        // ---- L2: top halos, handed over by the row above (its progress reaches c + 1; the row LF's
         // hand-off: sc1 stores drained before the progress word, sc1 loads here), into tile
         // i % LFRO_NTB once SB i - LFRO_NTB is stored
         CT vt[NUT];
@@ -2600,7 +2332,7 @@ __global__ __launch_bounds__(LFRO_NTH) __attribute__((amdgpu_waves_per_eu(4))) v
         }
         if (role == 5) { atomicAdd(&lfr_prof[9], wrow); atomicAdd(&lfr_prof[14], wfill); }
     }
-    lfrd_retire(ctr, ntasks, 0, tid, LFRO_NTH, &s_last);
+    lfrd_retire(ctr, ntasks, tid, LFRO_NTH, &s_last);
 #undef TLE
 }
 #undef LFRO_EDGE_WIDE
@@ -2660,7 +2392,7 @@ __global__ __launch_bounds__(LfNT<G>::NT) void k_plf(PlfLaunch a, const uint32_t
 #undef RES_CASE
 }
 
-// --------------------------------------------------------------- k_mc
+// --------------------------------------------------------------- MC (k_mcq)
 template <typename PIX>
 DEV int mc_ref(const PIX *r, int pitch, int w, int h, int x, int y)
 {
@@ -2701,345 +2433,15 @@ DEV int mc_sample(const PIX *r, int pitch, int w, int h, int X, int Y, int mx, i
     return clipbd((s + 64) >> 7, bd);
 }
 
-// Unscaled MC of R vertically adjacent pixels (rows Y .. Y + R - 1 of column X) from one
-// reference, as mc_sample's unscaled cases: each horizontally filtered reference row is
-// computed once for the R outputs (R + 7 rows for the 8-tap 2-D case: 88 taps instead of
-// 256 for R = 4, 120 instead of 512 for R = 8).
-template <typename PIX>
-DEV int mc_hrow(const PIX *r, int pitch, int w, int h, int X, int Y, int mx, bool bil, const int16_t *fx, int bd)
-{
-    if (!mx) return mc_ref(r, pitch, w, h, X, Y);
-    if (bil) {
-        const int a0 = mc_ref(r, pitch, w, h, X, Y), a1 = mc_ref(r, pitch, w, h, X + 1, Y);
-        return a0 + ((mx * (a1 - a0) + 8) >> 4);
-    }
-    int s = 0;
-#pragma unroll
-    for (int t = 0; t < 8; t++) s += fx[t] * mc_ref(r, pitch, w, h, X - 3 + t, Y);
-    return clipbd((s + 64) >> 7, bd);
-}
-template <typename PIX, int R>
-DEV void mc_rows(const PIX *r, int pitch, int w, int h, int X, int Y, int mx, int my, int filter, int bd, int (&o)[R])
-{
-    const bool bil = filter == 3;
-    const int16_t *fx = vp9t_subpel_filters[bil ? 0 : filter][mx], *fy = vp9t_subpel_filters[bil ? 0 : filter][my];
-    if (!my) {
-#pragma unroll
-        for (int t = 0; t < R; t++) o[t] = mc_hrow<PIX>(r, pitch, w, h, X, Y + t, mx, bil, fx, bd);
-    } else if (bil) {
-        int hr[R + 1];
-#pragma unroll
-        for (int k = 0; k < R + 1; k++) hr[k] = mc_hrow<PIX>(r, pitch, w, h, X, Y + k, mx, true, fx, bd);
-#pragma unroll
-        for (int t = 0; t < R; t++) o[t] = hr[t] + ((my * (hr[t + 1] - hr[t]) + 8) >> 4);
-    } else {
-        int hr[R + 7];
-#pragma unroll
-        for (int k = 0; k < R + 7; k++) hr[k] = mc_hrow<PIX>(r, pitch, w, h, X, Y - 3 + k, mx, false, fx, bd);
-#pragma unroll
-        for (int t = 0; t < R; t++) {
-            int s = 0;
-#pragma unroll
-            for (int k = 0; k < 8; k++) s += fy[k] * hr[t + k];
-            o[t] = clipbd((s + 64) >> 7, bd);
-        }
-    }
-}
-// mc_rows for a reference window that lies inside the visible reference (no emulated edge):
-// taps read directly from one row pointer (the 8 taps of a row merge into one 16-byte
-// load), the filter taps held in registers, the phase cases split outside the row loops
-// (mx, my and the filter are the unit's: wave-uniform)
-template <typename PIX, int R>
-DEV void mc_rows_direct(const PIX *r, int pitch, int X, int Y, int mx, int my, int filter, int bd, int (&o)[R])
-{
-    typedef __attribute__((address_space(1))) const PIX gpix;
-    const int pmax = (1 << bd) - 1;
-    gpix *b = (gpix *) r + (ptrdiff_t) (Y - 3) * pitch + (X - 3);
-    mx = __builtin_amdgcn_readfirstlane(mx);
-    my = __builtin_amdgcn_readfirstlane(my);
-    filter = __builtin_amdgcn_readfirstlane(filter);
-    if (filter == 3) {                                    // bilinear (vp9dsp_template.c:2150-2227)
-        int hr[R + 1];
-#pragma unroll
-        for (int k = 0; k < R + 1; k++) {
-            gpix *q = b + (ptrdiff_t) (3 + k) * pitch;
-            hr[k] = q[3] + ((mx * (q[4] - q[3]) + 8) >> 4);
-        }
-#pragma unroll
-        for (int t = 0; t < R; t++) o[t] = hr[t] + ((my * (hr[t + 1] - hr[t]) + 8) >> 4);
-        return;
-    }
-    int fx[8], fy[8];
-#pragma unroll
-    for (int t = 0; t < 8; t++) {
-        fx[t] = vp9t_subpel_filters[filter][mx][t];
-        fy[t] = vp9t_subpel_filters[filter][my][t];
-    }
-    auto hrow = [&](int k) -> int {                       // window row k, 8-tap, pixel-clipped
-        gpix *q = b + (ptrdiff_t) k * pitch;
-        int sh = 0;
-#pragma unroll
-        for (int t = 0; t < 8; t++) sh += fx[t] * q[t];
-        return med3_0((sh + 64) >> 7, pmax);
-    };
-    // one basic block per case, so every row's load is in flight before the first use
-    if (!my) {                                            // 1-D horizontal, or a copy
-        if (mx) {
-#pragma unroll
-            for (int t = 0; t < R; t++) o[t] = hrow(3 + t);
-        } else {
-#pragma unroll
-            for (int t = 0; t < R; t++) o[t] = b[(ptrdiff_t) (3 + t) * pitch + 3];
-        }
-        return;
-    }
-    int hr[R + 7];                                        // 1-D vertical, or 2-D
-    if (mx) {
-#pragma unroll
-        for (int k = 0; k < R + 7; k++) hr[k] = hrow(k);
-    } else {
-#pragma unroll
-        for (int k = 0; k < R + 7; k++) hr[k] = b[(ptrdiff_t) k * pitch + 3];
-    }
-#pragma unroll
-    for (int t = 0; t < R; t++) {
-        int sv = 0;
-#pragma unroll
-        for (int k = 0; k < 8; k++) sv += fy[k] * hr[t + k];
-        o[t] = med3_0((sv + 64) >> 7, pmax);
-    }
-}
-
-// R rows per lane over a unit (H % R == 0), compound averaged. A reference whose 8-tap
-// window [ix - 3, ix + w + 4] x [iy - 3, iy + h + 4] lies inside its visible area (nearly
-// every unit of a large frame) takes the direct taps; the rest clamp every tap
-// (emulated_edge_mc, videodsp_template.c:27-105).
-template <typename PIX, int R>
-DEV void mc_unit_rows(const McUnit &u, const FrameDesc &fd, PIX *dst, int pitch, int c, int bd, int nth)
-{
-    const int W = u.w, nq = W * u.h / R, p = u.plane;
-    for (int i = threadIdx.x; i < nq; i += nth) {
-        const int yq = i / W, xx = i - yq * W, yy = yq * R;
-        int out[R];
-        for (int k = 0; k < u.nref; k++) {
-            const int rf = u.ref[k];
-            const McRef m = u.r[k];
-            const int rw = fd.refw[rf][c], rh = fd.refh[rf][c];
-            int v[R];
-            if (m.ix >= 3 && m.iy >= 3 && m.ix + W + 4 < rw && m.iy + (int) u.h + 4 < rh)
-                mc_rows_direct<PIX, R>((const PIX *) fd.ref[rf][p], pitch, m.ix + xx, m.iy + yy, m.mx, m.my, u.filter, bd, v);
-            else
-                mc_rows<PIX, R>((const PIX *) fd.ref[rf][p], pitch, rw, rh, m.ix + xx, m.iy + yy, m.mx, m.my, u.filter,
-                                bd, v);
-#pragma unroll
-            for (int t = 0; t < R; t++) out[t] = k ? (out[t] + v[t] + 1) >> 1 : v[t];
-        }
-#pragma unroll
-        for (int t = 0; t < R; t++) dst[(size_t) (u.y + yy + t) * pitch + u.x + xx] = (PIX) out[t];
-    }
-}
-
-// one output pixel per thread (any reference scaling), compound averaged
-template <typename PIX>
-DEV void mc_unit_pixels(const McUnit &u, const FrameDesc &fd, PIX *dst, int pitch, int c, int bd, int nth)
-{
-    const int W = u.w, npx = W * u.h, p = u.plane;
-    for (int i = threadIdx.x; i < npx; i += nth) {
-        int yy = i / W, xx = i - yy * W;
-        int out = 0;
-        for (int k = 0; k < u.nref; k++) {
-            const int rf = u.ref[k];
-            const McRef m = u.r[k];
-            const PIX *r = (const PIX *) fd.ref[rf][p];
-            const int px = m.mx + xx * m.dx, py = m.my + yy * m.dy;
-            const int v = mc_sample<PIX>(r, pitch, fd.refw[rf][c], fd.refh[rf][c], m.ix + (px >> 4), m.iy + (py >> 4),
-                                         px & 15, py & 15, u.filter, bd);
-            out = k ? (out + v + 1) >> 1 : v;
-        }
-        dst[(size_t) (u.y + yy) * pitch + u.x + xx] = (PIX) out;
-    }
-}
-
-// An MC ticket of k_lfrd (see there). Wait table mw: {F, then per frame the launch filters:
-// batch frame index, SB rows, row task of each SB row (~0u: filtered by an earlier launch)}.
-// Pixel row y of a reference plane is final once the row task of SB row y / SBH is done and,
-// for its last 8 rows (rewritten by the next SB row's top-edge filtering), the next one's.
-// A unit waits for rows ymin - 1 .. ymax + 1 of what its taps read (a 128-byte line may
-// straddle two pixel rows when the pitch is not a multiple of 128 bytes); scaled
-// references wait for the whole frame. Lane 0 polls (relaxed agent loads), then one agent
-// acquire and a barrier before any load (Valid forms: consumer).
-template <typename PIX, class G>
-DEV void lfmc_ticket(const McUnit &u, const FrameDesc *__restrict__ frames, const uint32_t *__restrict__ mw,
-                     const uint32_t *rdone, uint32_t *ctr, uint32_t spin, int nth)
-{
-    const FrameDesc &fd = frames[u.frame];
-    const int p = u.plane, c = p ? 1 : 0, bd = fd.bd;
-    if (threadIdx.x == 0) {
-        bool waited = false;
-        const uint32_t nf = mw[0];
-        for (int k = 0; k < u.nref; k++) {
-            const int rf = u.ref[k];
-            const McRef m = u.r[k];
-            const int sbh = p ? G::CH : 64, refh = fd.refh[rf][c];
-            const bool scaled = m.dx != 16 || m.dy != 16;
-            int y0 = scaled ? 0 : m.iy - 4, y1 = scaled ? refh - 1 : m.iy + (int) u.h + 5;
-            y0 = y0 < 0 ? 0 : y0 >= refh ? refh - 1 : y0;
-            y1 = y1 < 0 ? 0 : y1 >= refh ? refh - 1 : y1;
-            for (uint32_t f = 0, o = 1; f < nf; f++, o += 2 + mw[o + 1]) {
-                if (frames[mw[o]].plane[p] != fd.ref[rf][p]) continue;
-                const int nrows = (int) mw[o + 1];
-                int r0 = y0 / sbh, r1 = y1 / sbh;
-                if (y1 % sbh >= sbh - 8) r1++;
-                if (r1 > nrows - 1) r1 = nrows - 1;
-                for (int r = r0; r <= r1; r++) {
-                    const uint32_t t = mw[o + 2 + r];
-                    if (t == ~0u) continue;
-                    waited = true;
-                    for (uint32_t n = 0; !__hip_atomic_load((const gu32 *) &rdone[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); n++) {
-                        if (n > spin) { atomicAdd(&ctr[2], 1u); break; }
-                        __builtin_amdgcn_s_sleep(2);
-                    }
-                }
-            }
-        }
-        if (waited) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    PIX *dst = (PIX *) fd.plane[p];
-    const int pitch = fd.pitch[c];
-    bool scaled = false;
-    for (int k = 0; k < u.nref; k++) scaled |= u.r[k].dx != 16 || u.r[k].dy != 16;
-    if (sizeof(PIX) != 1 && !scaled && !(u.h & 3)) {
-        if (!(u.h & 7)) mc_unit_rows<PIX, 8>(u, fd, dst, pitch, c, bd, nth);
-        else mc_unit_rows<PIX, 4>(u, fd, dst, pitch, c, bd, nth);
-        return;
-    }
-    mc_unit_pixels<PIX>(u, fd, dst, pitch, c, bd, nth);
-}
-
-// One MC unit (<= 64 x 64 pixels of one plane) per workgroup. Unscaled references: the
-// (h + 7) x (w + 7) reference window (edge-clamped, emulated_edge_mc) is staged in LDS once,
-// then the separable filter runs as a horizontal pass into a pixel-clipped LDS tmp and a
-// vertical pass (do_8tap_2d_c, vp9dsp_template.c:2076-2113; bilinear do_bilin_2d
-// 2150-2227). With an identity phase a pass is an exact copy, so the 2-D form also gives
-// the 1-D and copy cases of the unscaled selection (vp9dsp_template.c:2036-2059, 1971-2022).
-// Scaled references and small units keep the per-pixel sampler (no barriers; L1-served taps).
-#define MC_WP 72                      // window pitch (>= 64 + 7)
-#ifndef MC_ROWS8
-#define MC_ROWS8 1                    // high bit depth: 8 rows per lane where the unit height allows
-#endif
-#ifndef MC_LDS_MIN
-#define MC_LDS_MIN 1024               // units of at least this many pixels use the LDS passes
-#endif
-template <typename PIX, int NTH>
-__global__ __launch_bounds__(NTH) void k_mc(const McUnit *__restrict__ units, int nunits,
-                                            const FrameDesc *__restrict__ frames)
-{
-    static_assert(NTH == 256 || (NTH == 64 && sizeof(PIX) == 2), "the LDS passes assume 256 threads");
-    __shared__ PIX win[71 * MC_WP];
-    __shared__ int16_t tmp[71 * 64];
-    const McUnit u = units[blockIdx.x];
-    const FrameDesc &fd = frames[u.frame];
-    const int p = u.plane, c = p ? 1 : 0, bd = fd.bd;
-    PIX *dst = (PIX *) fd.plane[p];
-    const int pitch = fd.pitch[c];
-    const int W = u.w, H = u.h, npx = W * H;
-    bool scaled = false;
-    for (int k = 0; k < u.nref; k++) scaled |= u.r[k].dx != 16 || u.r[k].dy != 16;
-    const int lw = 31 - __builtin_clz((unsigned) W);          // passes index pixels by shifts
-    // measured: the LDS passes win at 8 bits (C2 k_mc 12.0 -> 10.2 ms per 120 frames) and lose
-    // at 16 bits (C5 52.7 -> 79 ms: 19 KB of LDS per workgroup halves the loads in flight
-    // on 8K references that miss the caches)
-    // high bit depth, unscaled: 4 rows per lane (C5 k_mc 39.1 -> 27.9 ms per step; for the
-    // small 8-bit units it measured slower than the per-pixel sampler, C2 7.9 -> 8.2 ms)
-    if (sizeof(PIX) != 1 && !scaled && !(H & 3)) {
-#if MC_ROWS8
-        if (!(H & 7)) mc_unit_rows<PIX, 8>(u, fd, dst, pitch, c, bd, NTH);
-        else
-#endif
-        mc_unit_rows<PIX, 4>(u, fd, dst, pitch, c, bd, NTH);
-        return;
-    }
-    if (sizeof(PIX) != 1 || scaled || npx < MC_LDS_MIN || (1 << lw) != W) {
-        mc_unit_pixels<PIX>(u, fd, dst, pitch, c, bd, NTH);
-        return;
-    }
-    const int WW = W + 7, WH = H + 7;
-    const bool bil = u.filter == 3;
-    int out[16];                                   // <= 64 x 64 / 256 pixels per thread
-    for (int k = 0; k < u.nref; k++) {
-        const int rf = u.ref[k];
-        const McRef m = u.r[k];
-        const PIX *r = (const PIX *) fd.ref[rf][p];
-        const int rw = fd.refw[rf][c], rh = fd.refh[rf][c];
-        const int mx = m.mx, my = m.my;
-        const int X0 = m.ix - 3, Y0 = m.iy - 3;   // window origin (integer position - 3)
-        if (k) __syncthreads();                    // the previous reference's passes are done
-        for (int i = threadIdx.x; i < WH * MC_WP; i += 256) {   // constant-divisor rows
-            const int wy = i / MC_WP, wx = i - wy * MC_WP;
-            if (wx < WW) win[i] = (PIX) mc_ref(r, pitch, rw, rh, X0 + wx, Y0 + wy);
-        }
-        __syncthreads();
-        // horizontal pass over the window rows the vertical pass reads (rows 3 .. 3 + H when
-        // the vertical phase is an identity; 8-tap reads rows y .. y + 7, bilinear y + 3, y + 4)
-        const int r0 = my ? (bil ? 3 : 0) : 3, r1 = my ? (bil ? H + 4 : H + 7) : H + 3;
-        const int16_t *fx = vp9t_subpel_filters[bil ? 0 : u.filter][mx];
-        for (int i = threadIdx.x; i < (r1 - r0) << lw; i += 256) {
-            const int ry = r0 + (i >> lw), x = i & (W - 1);
-            const PIX *w0 = win + ry * MC_WP + x;
-            int v;
-            if (!mx) v = w0[3];
-            else if (bil) v = w0[3] + ((mx * (w0[4] - w0[3]) + 8) >> 4);
-            else {
-                int s8 = 0;
-#pragma unroll
-                for (int t = 0; t < 8; t++) s8 += fx[t] * w0[t];
-                v = clipbd((s8 + 64) >> 7, bd);
-            }
-            tmp[ry * 64 + x] = (int16_t) v;
-        }
-        __syncthreads();
-        const int16_t *fy = vp9t_subpel_filters[bil ? 0 : u.filter][my];
-#pragma unroll
-        for (int q = 0; q < 16; q++) {
-            const int i = threadIdx.x + 256 * q;
-            if (i >= npx) break;
-            const int yy = i >> lw, xx = i & (W - 1);
-            const int16_t *t0 = tmp + yy * 64 + xx;
-            int v;
-            if (!my) v = t0[3 * 64];
-            else if (bil) v = t0[3 * 64] + ((my * (t0[4 * 64] - t0[3 * 64]) + 8) >> 4);
-            else {
-                int s8 = 0;
-#pragma unroll
-                for (int t = 0; t < 8; t++) s8 += fy[t] * t0[t * 64];
-                v = clipbd((s8 + 64) >> 7, bd);
-            }
-            out[q] = k ? (out[q] + v + 1) >> 1 : v;
-        }
-    }
-#pragma unroll
-    for (int q = 0; q < 16; q++) {
-        const int i = threadIdx.x + 256 * q;
-        if (i >= npx) break;
-        const int yy = i >> lw, xx = i & (W - 1);
-        dst[(size_t) (u.y + yy) * pitch + u.x + xx] = (PIX) out[q];
-    }
-}
-
-// --------------------------------------------------------------- k_mcp
-// Packed MC: the units of a workgroup as one flat list of lane tasks, R = 8 (R = 4 for
-// units 4 rows tall) vertically adjacent output pixels of one column per task, so a 4x4
-// chroma unit takes 4 lanes instead of a wave and every wave is full (k_mc gives each unit
-// a workgroup of its own: at C5 an 8K frame is ~243k units of ~26 tasks). The taps are the
-// task's unit's, per lane, and one separable 8-tap form gives every unscaled case exactly:
-// an identity phase is the tap 128 (an exact copy), so the copy and 1-D paths of
+// MC unit packing: the units of a workgroup as one flat list of lane tasks (so a 4x4 chroma
+// unit takes a few lanes instead of a wave and every wave is full; at C5 an 8K frame is
+// ~243k units). One separable 8-tap form gives every unscaled case exactly: an identity
+// phase is the tap 128 (an exact copy), so the copy and 1-D paths of
 // vp9dsp_template.c:1971-2059 equal the pixel-clipped 2-D form (2076-2113) with one
 // identity pass; the bilinear filter (2150-2227) is the 8-tap (0, 0, 0, 8(16 - m), 8m, 0,
 // 0, 0): a + ((m(b - a) + 8) >> 4) = ((16 - m)a + mb + 8) >> 4, scaled by 8, and its
 // values lie between a and b (the clip is an identity). Scaled references keep the
-// per-pixel sampler, one pixel per task.
+// per-pixel sampler (mc_sample), one pixel per task.
 #define MCP_U 64                                  // units per workgroup
 struct McL {                                      // a unit as its tasks read it (LDS)
     uint64_t ref[2], dst;
@@ -3047,11 +2449,6 @@ struct McL {                                      // a unit as its tasks read it
     int32_t pitch;
     uint16_t x, y, rw[2], rh[2];
     uint8_t lw, h, mx[2], my[2], filter, nref, direct, bd, cat, pad[3];
-};
-struct McpLds {
-    alignas(16) int16_t taps[64][8];              // [filter * 16 + phase], bilinear = filter 3
-    McL u[MCP_U];
-    uint32_t off[3][MCP_U + 1];                   // exclusive task offsets per category
 };
 
 // the last unit k < n with off[k] <= g (units without tasks of this category share the
@@ -3140,134 +2537,21 @@ DEV void mcp_scaled(const McUnit *__restrict__ units, const uint32_t *off, int n
     }
 }
 
-template <typename PIX, int R, bool V>
-DEV void mcp_rows(const McL &u, const int16_t (*taps)[8], int xx, int yy)
-{
-    const int pmax = (1 << u.bd) - 1, pitch = u.pitch;
-    int out[R];
-    for (int k = 0; k < u.nref; k++) {
-        const uint4 hw = *(const uint4 *) taps[u.filter * 16 + u.mx[k]];
-        const uint4 vw = *(const uint4 *) taps[u.filter * 16 + u.my[k]];
-        const int fx[8] = { (int16_t) hw.x, (int) hw.x >> 16, (int16_t) hw.y, (int) hw.y >> 16,
-                            (int16_t) hw.z, (int) hw.z >> 16, (int16_t) hw.w, (int) hw.w >> 16 };
-        const int fy[8] = { (int16_t) vw.x, (int) vw.x >> 16, (int16_t) vw.y, (int) vw.y >> 16,
-                            (int16_t) vw.z, (int) vw.z >> 16, (int16_t) vw.w, (int) vw.w >> 16 };
-        constexpr int NR = V ? R + 7 : R, R0 = V ? 0 : 3;     // window rows the vertical pass reads
-        int hr[NR];
-        const int X = u.ix[k] + xx - 3, Y = u.iy[k] + yy - 3 + R0;
-        const PIX *rp = (const PIX *) u.ref[k];
-        if ((u.direct >> k) & 1) {                            // window inside the reference
-            typedef __attribute__((address_space(1))) const PIX gpix;
-            gpix *b = (gpix *) rp + (ptrdiff_t) Y * pitch + X;
-#pragma unroll
-            for (int j = 0; j < NR; j++) {
-                gpix *q = b + (ptrdiff_t) j * pitch;
-                int sh = 0;
-#pragma unroll
-                for (int t = 0; t < 8; t++) sh += fx[t] * (int) q[t];
-                hr[j] = med3_0((sh + 64) >> 7, pmax);
-            }
-        } else {                                              // emulated edge: every tap clamped
-            typedef __attribute__((address_space(1))) const PIX gpix;
-            const int rw = u.rw[k], rh = u.rh[k];
-#pragma unroll
-            for (int j = 0; j < NR; j++) {
-                const int yc = Y + j < 0 ? 0 : Y + j >= rh ? rh - 1 : Y + j;
-                gpix *q = (gpix *) rp + (size_t) yc * pitch;
-                int sh = 0;
-#pragma unroll
-                for (int t = 0; t < 8; t++) {
-                    const int xc = X + t < 0 ? 0 : X + t >= rw ? rw - 1 : X + t;
-                    sh += fx[t] * (int) q[xc];
-                }
-                hr[j] = med3_0((sh + 64) >> 7, pmax);
-            }
-        }
-#pragma unroll
-        for (int t = 0; t < R; t++) {
-            int v = hr[t];
-            if (V) {
-                int sv = 0;
-#pragma unroll
-                for (int q = 0; q < 8; q++) sv += fy[q] * hr[t + q];
-                v = med3_0((sv + 64) >> 7, pmax);
-            }
-            out[t] = k ? (out[t] + v + 1) >> 1 : v;
-        }
-    }
-    typedef __attribute__((address_space(1))) PIX gpo;
-    gpo *d = (gpo *) u.dst + (size_t) (u.y + yy) * pitch + u.x + xx;
-#pragma unroll
-    for (int t = 0; t < R; t++) d[(size_t) t * pitch] = (PIX) out[t];
-}
-
-template <typename PIX>
-__global__ __launch_bounds__(256) void k_mcp(const McUnit *__restrict__ units, int nunits,
-                                             const FrameDesc *__restrict__ frames)
-{
-    __shared__ McpLds S;
-    const int tid = threadIdx.x;
-    const int u0 = blockIdx.x * MCP_U, nu = nunits - u0 < MCP_U ? nunits - u0 : MCP_U;
-    {
-        // filter rows: 3 x 16 8-tap phases, then the bilinear ones as 8-taps
-        const int r = tid >> 2, q = (tid & 3) * 2;
-        int16_t a, b;
-        if (r < 48) { a = vp9t_subpel_filters[r >> 4][r & 15][q]; b = vp9t_subpel_filters[r >> 4][r & 15][q + 1]; }
-        else {
-            const int m = r & 15;
-            a = (int16_t) (q == 2 ? 0 : q == 4 ? 8 * m : 0);
-            b = (int16_t) (q == 2 ? 8 * (16 - m) : 0);
-        }
-        S.taps[r][q] = a;
-        S.taps[r][q + 1] = b;
-    }
-    uint32_t cnt[3] = { 0, 0, 0 };
-    if (tid < nu) {
-        McL L;
-        const McUnit m = units[u0 + tid];
-        mcp_unit(m, frames, L);
-        cnt[L.cat] = L.cat == 2 ? (uint32_t) m.w * m.h : (uint32_t) m.w * m.h >> (L.cat ? 2 : 3);
-        S.u[tid] = L;
-    }
-    mcp_offsets(S.off, cnt, tid);
-    __syncthreads();
-    // R = 8 tasks, then R = 4; the vertical pass only where a lane of the wave needs it
-    for (int c = 0; c < 2; c++) {
-        const uint32_t T = S.off[c][nu];
-        for (uint32_t g = tid; g < T; g += 256) {
-            const int k = mcp_find(S.off[c], nu, g);
-            const McL &u = S.u[k];
-            const uint32_t ti = g - S.off[c][k];
-            const int xx = (int) (ti & ((1u << u.lw) - 1));
-            const int yy = (int) (ti >> u.lw) << (c ? 2 : 3);
-            const bool v = u.my[0] | (u.nref > 1 ? u.my[1] : 0);
-            if (c == 0) {
-                if (__any(v)) mcp_rows<PIX, 8, true>(u, S.taps, xx, yy);
-                else mcp_rows<PIX, 8, false>(u, S.taps, xx, yy);
-            } else {
-                if (__any(v)) mcp_rows<PIX, 4, true>(u, S.taps, xx, yy);
-                else mcp_rows<PIX, 4, false>(u, S.taps, xx, yy);
-            }
-        }
-    }
-    mcp_scaled<PIX>(units + u0, S.off[2], nu, frames, tid);
-}
-
 // --------------------------------------------------------------- k_mcq
-// k_mcp with 4-column lane tasks: a lane filters 4 adjacent output columns x R rows (R = 8;
-// 4 for units 4 rows tall) from ONE load per window row (12 pixels, x - 3 .. x + 8: 8-bit
-// a 12-byte load, 16-bit 24 bytes), where k_mcp's one-column tasks load 8 pixels per row
-// and output pixel (4x the load instructions, 2.7x the bytes through the L1). The
+// 4-column lane tasks: a lane filters 4 adjacent output columns x R rows (R = 8; 4 for
+// units 4 rows tall) from ONE load per window row (12 pixels, x - 3 .. x + 8: 8-bit a
+// 12-byte load, 16-bit 24 bytes), where round 4's one-column tasks (k_mcp) loaded 8 pixels
+// per row and output pixel (4x the load instructions, 2.7x the bytes through the L1). The
 // horizontal 8-tap sums are packed dot products: 8-bit v_dot4_i32_i8 on the pixels biased
 // by -128 (every VP9 8-tap and the bilinear-as-8-tap sum to 128, so + 128 * 128 restores
 // the bias; an identity phase, tap 128, does not fit an int8 and selects the pixel), 16-bit
 // v_dot2_i32_i16 on the pixel pairs (odd columns from byte-aligned pairs). The vertical pass
 // accumulates each horizontally filtered row into the <= 8 outputs whose taps cover it.
 // Arithmetic exactly vp9dsp_template.c:2076-2113 (the pixel-clipped 2-D form, equal to the
-// 1-D / copy forms through identity phases, see k_mcp); compound averages
+// 1-D / copy forms through identity phases, see above); compound averages
 // (a + b + 1) >> 1 per packed pixel as (a | b) - ((a ^ b) >> 1).
 struct McqLds {
-    alignas(16) int16_t taps[64][8];              // [filter * 16 + phase], bilinear = filter 3 (k_mcp's)
+    alignas(16) int16_t taps[64][8];              // [filter * 16 + phase], bilinear = filter 3
     uint32_t tap8[64][2];                         // the same taps as int8 quads (identity phases: 0)
     alignas(16) uint32_t tapp[64][12];            // vertical tap pairs (f[q], f[q + 1]), q = -1..7 (f[-1] = f[8] = 0)
     McL u[MCP_U];
@@ -3568,37 +2852,27 @@ static void launch_lf_g(hipStream_t st, int nsb, const uint32_t *list, const LFR
 }
 template <typename PIX, class G>
 static void launch_lfr_g(hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs, const FrameDesc *frames, uint32_t *ctr,
-                         const McUnit *mcu, int nmc, const uint32_t *mw)
+                         const KCfg &k)
 {
-    // VP9HIP_LFR_DB=0: the single-tile k_lfr (A/B switch), MC units after it
-    const char *e = getenv("VP9HIP_LFR_DB");          // read per launch (tests switch it)
-    const bool db = !e || atoi(e);
-    if (db) {
-        if constexpr (G::SH == 1 && G::SV == 1) {
-            // the band-overlapped k_lfro (default; 4:2:0, no MC tickets), VP9HIP_LFRO=0: k_lfrd.
-            // Measured (profiles/r04l): C5 k_lfr 1,403 -> 1,021 us per 8K frame, C2 300 -> 238 us
-            const char *o = getenv("VP9HIP_LFRO");
-            if (!nmc && (!o || atoi(o))) {
-                hipLaunchKernelGGL((k_lfro<PIX, G>), dim3(ntasks), dim3(LFRO_NTH), 0, st, tasks, recs, frames, ctr, ntasks);
-                return;
-            }
+    if constexpr (G::SH == 1 && G::SV == 1) {
+        // the band-overlapped k_lfro (4:2:0 default; KCfg::lfro = 0: k_lfrd). Measured
+        // (profiles/r04l): C5 k_lfr 1,403 -> 1,021 us per 8K frame, C2 300 -> 238 us
+        if (k.lfro) {
+            hipLaunchKernelGGL((k_lfro<PIX, G>), dim3(ntasks), dim3(LFRO_NTH), 0, st, tasks, recs, frames, ctr, ntasks);
+            return;
         }
-        hipLaunchKernelGGL((k_lfrd<PIX, G>), dim3(ntasks + nmc), dim3(LfNT<G>::NT + 64), 0, st, tasks, recs, frames, ctr, ntasks,
-                           mcu, nmc, mw);
-        return;
     }
-    hipLaunchKernelGGL((k_lfr<PIX, G, false>), dim3(ntasks), dim3(LfNT<G>::NT + 64), 0, st, tasks, recs, frames, ctr, ntasks);
-    if (nmc) hipLaunchKernelGGL((k_mc<PIX, 256>), dim3(nmc), dim3(256), 0, st, mcu, nmc, frames);
+    hipLaunchKernelGGL((k_lfrd<PIX, G>), dim3(ntasks), dim3(LfNT<G>::NT + 64), 0, st, tasks, recs, frames, ctr, ntasks);
 }
 template <typename PIX>
 static void launch_lfr_p(int ss, hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs, const FrameDesc *frames,
-                         uint32_t *ctr, const McUnit *mcu, int nmc, const uint32_t *mw)
+                         uint32_t *ctr, const KCfg &k)
 {
     switch (ss) {
-    case 3: launch_lfr_g<PIX, Geo<1, 1>>(st, ntasks, tasks, recs, frames, ctr, mcu, nmc, mw); break;
-    case 1: launch_lfr_g<PIX, Geo<1, 0>>(st, ntasks, tasks, recs, frames, ctr, mcu, nmc, mw); break;
-    case 2: launch_lfr_g<PIX, Geo<0, 1>>(st, ntasks, tasks, recs, frames, ctr, mcu, nmc, mw); break;
-    default: launch_lfr_g<PIX, Geo<0, 0>>(st, ntasks, tasks, recs, frames, ctr, mcu, nmc, mw); break;
+    case 3: launch_lfr_g<PIX, Geo<1, 1>>(st, ntasks, tasks, recs, frames, ctr, k); break;
+    case 1: launch_lfr_g<PIX, Geo<1, 0>>(st, ntasks, tasks, recs, frames, ctr, k); break;
+    case 2: launch_lfr_g<PIX, Geo<0, 1>>(st, ntasks, tasks, recs, frames, ctr, k); break;
+    default: launch_lfr_g<PIX, Geo<0, 0>>(st, ntasks, tasks, recs, frames, ctr, k); break;
     }
 }
 template <typename PIX>
@@ -3647,7 +2921,7 @@ int vp9hip_pred_prof_read(unsigned long long *out)
     static const unsigned long long z[16] = {0};
     return hipMemcpyToSymbol(HIP_SYMBOL(pred_prof), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
-// LFR_PROF builds: read and clear the k_lfr phase sums (profiling only, not in the ABI)
+// LFR_PROF builds: read and clear the row-LF phase sums (profiling only, not in the ABI)
 // LFR_PROF builds: the k_lfro event timeline (24 x 8 shader-clock values; profiling only)
 int vp9hip_lfro_tl_read(unsigned long long *out)
 {
@@ -3731,22 +3005,22 @@ int vp9hip_launch_lf(int fmt, hipStream_t st, int nsb, const uint32_t *list, con
 }
 #endif
 int vp9hip_launch_lfr_8(int ss, hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs, const FrameDesc *frames,
-                        uint32_t *ctr, const McUnit *mcu, int nmc, const uint32_t *mw);
+                        uint32_t *ctr, const KCfg &k);
 #if KP(2)
 int vp9hip_launch_lfr_8(int ss, hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs, const FrameDesc *frames,
-                        uint32_t *ctr, const McUnit *mcu, int nmc, const uint32_t *mw)
+                        uint32_t *ctr, const KCfg &k)
 {
-    launch_lfr_p<uint8_t>(ss, st, ntasks, tasks, recs, frames, ctr, mcu, nmc, mw);
+    launch_lfr_p<uint8_t>(ss, st, ntasks, tasks, recs, frames, ctr, k);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 #endif
 int vp9hip_launch_lfr_16(int ss, hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs, const FrameDesc *frames,
-                        uint32_t *ctr, const McUnit *mcu, int nmc, const uint32_t *mw);
+                        uint32_t *ctr, const KCfg &k);
 #if KP(3)
 int vp9hip_launch_lfr_16(int ss, hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs, const FrameDesc *frames,
-                        uint32_t *ctr, const McUnit *mcu, int nmc, const uint32_t *mw)
+                        uint32_t *ctr, const KCfg &k)
 {
-    launch_lfr_p<uint16_t>(ss, st, ntasks, tasks, recs, frames, ctr, mcu, nmc, mw);
+    launch_lfr_p<uint16_t>(ss, st, ntasks, tasks, recs, frames, ctr, k);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 #endif
@@ -3776,11 +3050,10 @@ int vp9hip_launch_plf_16(int ss, hipStream_t st, const PlfLaunch *pl, const uint
 #endif
 #if KP(0)
 int vp9hip_launch_lfr(int fmt, hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs,
-                      const FrameDesc *frames, uint32_t *ctr, const McUnit *mcu, int nmc, const uint32_t *mw)
+                      const FrameDesc *frames, uint32_t *ctr, const KCfg *k)
 {
-    if (ntasks <= 0) return nmc > 0 ? -1 : 0;
-    if (nmc < 0 || (nmc && (!mcu || !mw))) return -1;
-    return (fmt & 1 ? vp9hip_launch_lfr_16 : vp9hip_launch_lfr_8)(fmt >> 1, st, ntasks, tasks, recs, frames, ctr, mcu, nmc, mw);
+    if (ntasks <= 0) return 0;
+    return (fmt & 1 ? vp9hip_launch_lfr_16 : vp9hip_launch_lfr_8)(fmt >> 1, st, ntasks, tasks, recs, frames, ctr, *k);
 }
 int vp9hip_launch_plf(int fmt, hipStream_t st, const PlfLaunch *pl, const uint32_t *plist, const uint32_t *llist,
                       const WGRec *wgs, const SBRec *sbs, const PJob *jobs, const uint32_t *passes, const LFRec *recs,
@@ -3790,39 +3063,15 @@ int vp9hip_launch_plf(int fmt, hipStream_t st, const PlfLaunch *pl, const uint32
     return (fmt & 1 ? vp9hip_launch_plf_16 : vp9hip_launch_plf_8)(fmt >> 1, st, pl, plist, llist, wgs, sbs, jobs, passes,
                                                                   recs, rjobs, frames, coefs, resid, ptab, dbg);
 }
-int vp9hip_launch_mc(int hb, hipStream_t st, int n, const McUnit *units, const FrameDesc *frames)
+int vp9hip_launch_mc(int hb, hipStream_t st, int n, const McUnit *units, const FrameDesc *frames, const KCfg *k)
 {
     if (n <= 0) return 0;
-    // high bit depth: one wave per unit (the per-pixel sampler keeps every lane of a small
-    // unit busy; VP9HIP_MC64=0: 256 threads, as 8-bit, whose LDS passes need them)
-    const char *e = getenv("VP9HIP_MC64");              // read per launch (tests switch it)
-    const bool mc64 = !e || atoi(e);
-    // VP9HIP_MCP: 2 (default) the packed kernel k_mcp at every bit depth, 1 for high bit
-    // depth only, 0 one workgroup per unit (k_mc). Measured (profiles/r04i, event-timed
-    // launches): C5 8K 10-bit 320 -> 219 us per frame, C2 1080p 8-bit 128 -> 61 us. An
-    // occupancy target of 6 waves / SIMD (78 VGPRs instead of 113) measured slower (325 us
-    // at C5): the rows of a task are all in flight at once only with the larger budget.
-    // VP9HIP_MCP=3 (default): k_mcq, 4-column tasks with packed dot products
-    const char *pe = getenv("VP9HIP_MCP");
-    const int mcp = pe ? atoi(pe) : 3;
-    if (mcp >= 3) {
-        const int nb = (n + MCP_U - 1) / MCP_U;
-        // task slices per unit group: ~4k workgroups at least, 2 to 8 slices
-        const char *se = getenv("VP9HIP_MCQ_SLICES");
-        const int ns = se ? std::max(1, std::min(16, atoi(se))) : std::max(2, std::min(8, 4096 / nb));
-        if (hb) hipLaunchKernelGGL((k_mcq<uint16_t>), dim3(nb, ns), dim3(256), 0, st, units, n, frames);
-        else    hipLaunchKernelGGL((k_mcq<uint8_t>), dim3(nb, ns), dim3(256), 0, st, units, n, frames);
-        return hipGetLastError() == hipSuccess ? 0 : -1;
-    }
-    if (mcp >= (hb ? 1 : 2)) {
-        const int nb = (n + MCP_U - 1) / MCP_U;
-        if (hb) hipLaunchKernelGGL((k_mcp<uint16_t>), dim3(nb), dim3(256), 0, st, units, n, frames);
-        else    hipLaunchKernelGGL((k_mcp<uint8_t>), dim3(nb), dim3(256), 0, st, units, n, frames);
-        return hipGetLastError() == hipSuccess ? 0 : -1;
-    }
-    if (hb && mc64) hipLaunchKernelGGL((k_mc<uint16_t, 64>), dim3(n), dim3(64), 0, st, units, n, frames);
-    else if (hb)    hipLaunchKernelGGL((k_mc<uint16_t, 256>), dim3(n), dim3(256), 0, st, units, n, frames);
-    else            hipLaunchKernelGGL((k_mc<uint8_t, 256>), dim3(n), dim3(256), 0, st, units, n, frames);
+    // k_mcq: 64 units per workgroup, each unit group's tasks split into slices (grid y):
+    // ~4k workgroups at least, 2 to 8 slices (KCfg::mcq_slices overrides; profiles/r04k)
+    const int nb = (n + MCP_U - 1) / MCP_U;
+    const int ns = k->mcq_slices > 0 ? std::min(16, k->mcq_slices) : std::max(2, std::min(8, 4096 / nb));
+    if (hb) hipLaunchKernelGGL((k_mcq<uint16_t>), dim3(nb, ns), dim3(256), 0, st, units, n, frames);
+    else    hipLaunchKernelGGL((k_mcq<uint8_t>), dim3(nb, ns), dim3(256), 0, st, units, n, frames);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 #endif

@@ -53,13 +53,13 @@ int vp9hip_launch_pred(int fmt, hipStream_t st, int nwg, const uint32_t *list, c
                        const uint32_t *ptab, int dbg);
 int vp9hip_launch_lf(int fmt, hipStream_t st, int nsb, const uint32_t *list, const LFRec *recs,
                      const FrameDesc *frames, int dbg);
-int vp9hip_launch_mc(int hb, hipStream_t st, int n, const McUnit *units, const FrameDesc *frames);
+int vp9hip_launch_mc(int hb, hipStream_t st, int n, const McUnit *units, const FrameDesc *frames, const KCfg *k);
 size_t vp9hip_plan_scan_bytes(size_t n);
 int vp9hip_plan_enqueue(hipStream_t st, const PlanDev *D, int ss, int nframes, int max_blk, int max_sb, uint32_t nb,
                         uint32_t nslots, uint32_t ncnt, int nk, const uint32_t *gidx, int ng, uint32_t *summary,
                         void *scan_tmp, size_t scan_bytes, int any_levels, int flags, int guard);
 int vp9hip_launch_lfr(int fmt, hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs,
-                      const FrameDesc *frames, uint32_t *ctr, const McUnit *mcu, int nmc, const uint32_t *mw);
+                      const FrameDesc *frames, uint32_t *ctr, const KCfg *k);
 int vp9hip_launch_plf(int fmt, hipStream_t st, const PlfLaunch *pl, const uint32_t *plist, const uint32_t *llist,
                       const WGRec *wgs, const SBRec *sbs, const PJob *jobs, const uint32_t *passes, const LFRec *recs,
                       const RJob *rjobs, const FrameDesc *frames, const void *coefs, int16_t *resid, const uint32_t *ptab,
@@ -76,9 +76,7 @@ const char *const kname[K_N] = { "k_mc", "k_resid", "k_pred", "k_lf", "k_plf", "
 // step: wavefront diagonal of a K_PRED (x_in_tile + y) or K_LF (x + 2y) launch; K_PLF
 // (intra diagonal `step` + LF diagonal step - PLF_LAG in one launch): off / n the intra
 // workgroups, off2 / n2 the LF SBs; K_LFR (row-pipelined loop filter of a phase): off / n
-// its task table, arg its counter block (uint32 index into the arena's counter words),
-// off2 / n2 the next chain position's MC units run as extra tickets of the launch (0: none)
-// and roff[0] their wait table (host lists)
+// its task table, arg its counter block (uint32 index into the arena's counter words)
 struct Launch { int kind; uint32_t off; uint32_t n; int arg; int grp; int ph; int part; int step;
                 uint32_t off2 = 0, n2 = 0;
                 uint32_t roff[5] = { 0, 0, 0, 0, 0 }, rn[5] = { 0, 0, 0, 0, 0 };   // K_PLF residual jobs by tx code
@@ -97,7 +95,6 @@ struct Launch { int kind; uint32_t off; uint32_t n; int arg; int grp; int ph; in
 enum { PART_RECON, PART_LF };           // a phase's reconstruction launches, then its loop filter
 #define MAX_GROUPS 8                    // independent frame groups = concurrent launch chains
 #define MAX_SLOTS VP9HIP_MAX_SLOTS      // batch slots per context (include/vp9hip.h)
-#define LF_LAG 2                        // LF diagonal j needs intra diagonals <= j + LF_LAG (see enqueue_batch)
 
 struct Staged {
     // host images (kept for rebuilds / inspection)
@@ -159,7 +156,6 @@ struct Staged {
         std::vector<std::pair<uint32_t, uint32_t>> lf;        // per LF diagonal: host list (offset, count)
         std::vector<double> pred_bytes, lf_bytes;             // per intra diagonal (intra frames) / LF diagonal
         uint32_t lfr_off = 0, lfr_n = 0;                      // k_lfr task table in the host lists
-        uint32_t lfw_off = 0;                                 // its wait table (k_lfrd MC tickets)
         int lfr_ctr = 0;
         double lfr_bytes = 0;
         int g_res = 0, g_mc = 0;                              // summary gather slots
@@ -279,12 +275,8 @@ struct vp9hip_ctx {
     int dev = 0;
     hipStream_t st = nullptr;           // main stream: uploads, downloads, group 0
     hipStream_t xst[MAX_GROUPS - 1] = {};   // groups 1.. of a batch (joined back into st)
-    hipStream_t lst[MAX_GROUPS] = {};       // per group: its loop-filter launches (lf_overlap)
-    hipEvent_t fork_ev = nullptr, join_ev[2 * MAX_GROUPS] = {};
-    hipEvent_t lf_done[MAX_GROUPS] = {};
-    std::vector<hipEvent_t> sev;            // recon -> LF step events (lf_overlap)
+    hipEvent_t fork_ev = nullptr, join_ev[MAX_GROUPS] = {};
     int max_groups = 2;                 // VP9HIP_STREAMS overrides (1..8); 2 measured best with the device planner and two batch slots (r02k: C3 +3.7 %, C4 +2.7 %, C2 +1.1 % over 3)
-    bool lf_overlap = false;            // VP9HIP_LF_OVERLAP=1: LF on a second stream per group (measured slower)
     bool fuse_plf = true;               // VP9HIP_PLF=0: no fused intra + LF launches
     bool level_sched = true;            // VP9HIP_LEVELS=0: inter frames' intra SBs by diagonal
     int lf_rows = 1;                    // VP9HIP_LFROW: 0 LF as diagonal launches only, 1 k_lfr for
@@ -303,6 +295,20 @@ struct vp9hip_ctx {
     bool plan_timed = false;
     int dbg = 0;                        // VP9HIP_DEBUG: ablation switches for profiling only
     bool use_graph = true;              // VP9HIP_GRAPH=0 disables graph replay
+    // the other VP9HIP_* switches, read once by vp9hip_open (read_config): the staging and
+    // launch paths never read the environment
+    KCfg kcfg = { 1, 0 };               // kernel selections (VP9HIP_LFRO, VP9HIP_MCQ_SLICES)
+    int host_threads = 16;              // VP9HIP_HOST_THREADS: host planning / staging threads
+    uint32_t lfr_spin = 0;              // row-LF hand-off spin bound, 0 = 2^22 polls (test hook)
+    int test_reject = 0;                // the k-th static-plan batch staged is made invalid (test hook)
+    bool static_plan = true;            // VP9HIP_STATIC=0: keyframe batches planned like the others
+    bool edge = true;                   // VP9HIP_EDGE=0: no SB edge columns (4:2:0 tile loader)
+    bool resid_multi = true;            // VP9HIP_RESID_MULTI=0: one residual launch per tx size
+    bool stage_trace = false;           // VP9HIP_STAGE_TRACE=1: host time of staging / planning
+    bool plan_prof_on = false;          // VP9HIP_PLAN_PROF=1: k_plan phase cycles
+    int plan_dbg = 0;                   // VP9HIP_PLAN_DBG: planner ablations (timing only)
+    bool plan_only = false;             // VP9HIP_PLAN_ONLY=1: run the planner alone (diagnostics)
+    int dl_threads = 3;                 // VP9HIP_DL_THREADS: download copy threads besides the caller
     Staged stg;                         // the current batch slot
     Staged sl[MAX_SLOTS];               // the other slots (sl[slot] is a moved-out placeholder;
                                         // vp9hip_set_batch_slot swaps a slot in and out)
@@ -367,6 +373,45 @@ static bool slot_streams_make(vp9hip_ctx *c, int k)
     return ok;
 }
 
+// Test hooks (vp9hip_test_hooks): process-wide values a context copies when it opens.
+static std::atomic<int> g_test_reject{0};
+static std::atomic<uint32_t> g_test_lfr_spin{0};
+
+extern "C" void vp9hip_test_hooks(int reject_batch, uint32_t lfr_spin)
+{
+    g_test_reject = reject_batch;
+    g_test_lfr_spin = lfr_spin;
+}
+
+// Every VP9HIP_* switch of a context, read here once: A/B and diagnostic switches of the
+// pixel path (DESIGN.md §5 names the measurements each default rests on).
+static void read_config(vp9hip_ctx *c)
+{
+    auto num = [](const char *name, int def) { const char *e = getenv(name); return e ? atoi(e) : def; };
+    c->dbg = num("VP9HIP_DEBUG", 0);
+    c->use_graph = num("VP9HIP_GRAPH", 1) != 0;
+    c->max_groups = std::max(1, std::min(MAX_GROUPS, num("VP9HIP_STREAMS", c->max_groups)));
+    c->fuse_plf = num("VP9HIP_PLF", 1) != 0;
+    c->lf_rows = num("VP9HIP_LFROW", c->lf_rows);
+    c->level_sched = num("VP9HIP_LEVELS", 1) != 0;
+    c->host_plan = num("VP9HIP_HOST_PLAN", 0) != 0;
+    c->slot_streams = num("VP9HIP_SLOT_STREAMS", 1) != 0;
+    c->kcfg.lfro = num("VP9HIP_LFRO", 1) != 0;
+    c->kcfg.mcq_slices = std::max(0, std::min(16, num("VP9HIP_MCQ_SLICES", 0)));
+    c->host_threads = std::max(1, std::min(64, num("VP9HIP_HOST_THREADS",
+                                                   (int) std::min(16u, std::max(1u, std::thread::hardware_concurrency())))));
+    c->static_plan = num("VP9HIP_STATIC", 1) != 0;
+    c->edge = num("VP9HIP_EDGE", 1) != 0;
+    c->resid_multi = num("VP9HIP_RESID_MULTI", 1) != 0;
+    c->stage_trace = num("VP9HIP_STAGE_TRACE", 0) != 0;
+    c->plan_prof_on = num("VP9HIP_PLAN_PROF", 0) != 0;
+    c->plan_dbg = num("VP9HIP_PLAN_DBG", 0);
+    c->plan_only = num("VP9HIP_PLAN_ONLY", 0) != 0;
+    c->dl_threads = std::max(0, std::min(15, num("VP9HIP_DL_THREADS", 3)));
+    c->test_reject = g_test_reject;
+    c->lfr_spin = g_test_lfr_spin;
+}
+
 extern "C" int vp9hip_open(int device, vp9hip_ctx **out)
 {
     if (!out) return VP9HIP_EINVAL;
@@ -374,26 +419,16 @@ extern "C" int vp9hip_open(int device, vp9hip_ctx **out)
     if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return VP9HIP_ENOSYS;
     vp9hip_ctx *c = new vp9hip_ctx;
     c->dev = device;
-    if (const char *d = getenv("VP9HIP_DEBUG")) c->dbg = atoi(d);
-    if (const char *g = getenv("VP9HIP_GRAPH")) c->use_graph = atoi(g) != 0;
-    if (const char *g = getenv("VP9HIP_STREAMS")) c->max_groups = std::max(1, std::min(MAX_GROUPS, atoi(g)));
-    if (const char *g = getenv("VP9HIP_LF_OVERLAP")) c->lf_overlap = atoi(g) != 0;
-    if (const char *g = getenv("VP9HIP_PLF")) c->fuse_plf = atoi(g) != 0;
-    if (const char *g = getenv("VP9HIP_LFROW")) c->lf_rows = atoi(g);
-    if (const char *g = getenv("VP9HIP_LEVELS")) c->level_sched = atoi(g) != 0;
-    if (const char *g = getenv("VP9HIP_HOST_PLAN")) c->host_plan = atoi(g) != 0;
-    if (const char *g = getenv("VP9HIP_SLOT_STREAMS")) c->slot_streams = atoi(g) != 0;
+    read_config(c);
     // streams in the order their work is busiest: the frame groups' streams, then the
     // planner's, so that (with the default 4 hardware queues, GPU_MAX_HW_QUEUES) each lands
-    // on a queue of its own; the LF-overlap streams only when that mode is on
+    // on a queue of its own
     // Stream priorities (hipDeviceGetStreamPriorityRange): with per-slot streams every
     // stream of the context is created at the highest priority (measured at C3: 9,320 vs
     // 8,530 frames/s at default priority, r03f/ab5); with one planner stream the pixel
     // streams at the highest priority starve the planner (6,520), so all stay default.
-    // VP9HIP_PRIO overrides (A/B): 0 all default, 1 the planner stream lowest, 2 the pixel
-    // streams highest, 3 every stream lowest.
-    int prio_lo = 0, prio_hi = 0, prio = c->slot_streams ? 2 : 0;
-    if (const char *g = getenv("VP9HIP_PRIO")) prio = atoi(g);
+    int prio_lo = 0, prio_hi = 0;
+    const int prio = c->slot_streams ? 2 : 0;   // 2: the pixel streams highest
     hipSetDevice(device);
     if (prio) hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
     const int pix_prio = prio == 2 ? prio_hi : prio == 3 ? prio_lo : 0;
@@ -412,10 +447,6 @@ extern "C" int vp9hip_open(int device, vp9hip_ctx **out)
     }
     for (int i = 0; ok && i < MAX_GROUPS - 1; i++)
         ok = hipEventCreateWithFlags(&c->join_ev[i], hipEventDisableTiming) == hipSuccess;
-    for (int i = 0; ok && i < MAX_GROUPS; i++)
-        ok = (!c->lf_overlap || hipStreamCreateWithFlags(&c->lst[i], hipStreamNonBlocking) == hipSuccess) &&
-             hipEventCreateWithFlags(&c->lf_done[i], hipEventDisableTiming) == hipSuccess &&
-             hipEventCreateWithFlags(&c->join_ev[MAX_GROUPS + i], hipEventDisableTiming) == hipSuccess;
     if (!ok) {
         delete c;
         return VP9HIP_EEXTERNAL;
@@ -488,12 +519,6 @@ extern "C" void vp9hip_close(vp9hip_ctx *c)
     }
     for (int i = 0; i < MAX_GROUPS - 1; i++)
         if (c->join_ev[i]) hipEventDestroy(c->join_ev[i]);
-    for (int i = 0; i < MAX_GROUPS; i++) {
-        if (c->lst[i]) hipStreamDestroy(c->lst[i]);
-        if (c->lf_done[i]) hipEventDestroy(c->lf_done[i]);
-        if (c->join_ev[MAX_GROUPS + i]) hipEventDestroy(c->join_ev[MAX_GROUPS + i]);
-    }
-    for (auto e : c->sev) hipEventDestroy(e);
     if (c->fork_ev) hipEventDestroy(c->fork_ev);
     delete c;
 }
@@ -1019,19 +1044,6 @@ static int plan_frame(FrameBuild fb, FramePlan &fp)
     return 0;
 }
 
-// Host threads for batch planning: VP9HIP_HOST_THREADS, default min(16, hardware threads)
-// (16 = the CPU share of one GPU on the MI355X boxes).
-static int host_threads()
-{
-    static int n = 0;
-    if (!n) {
-        const char *e = getenv("VP9HIP_HOST_THREADS");
-        n = e ? atoi(e) : (int) std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
-        n = std::max(1, std::min(64, n));
-    }
-    return n;
-}
-
 // Pixel bytes of SB (sbx, sby) of frame f (all planes, visible area): its share of the
 // frame's algorithmic bytes P.
 static double sb_bytes(const vp9hip_ctx *c, const vp9h_frame &f, int sbx, int sby)
@@ -1053,14 +1065,12 @@ struct DevIn {
     bool fuse, lfr_any;
 };
 
-// k_lfr counter blocks of a staged batch, zeroed; word 3 of each block is the spin bound of
-// a hand-off wait (VP9HIP_LFR_SPIN: a test hook that forces the timeout path; 0 = default)
-static void init_lfr_ctr(const Staged &s, uint32_t *ctr)
+// row-LF counter blocks of a staged batch, zeroed; word 3 of each block is the spin bound of
+// a hand-off wait (0 = default; vp9hip_test_hooks sets a small one to force the timeout path)
+static void init_lfr_ctr(const vp9hip_ctx *c, const Staged &s, uint32_t *ctr)
 {
     memset(ctr, 0, (size_t) s.n_ctr * 4);
-    const char *e = getenv("VP9HIP_LFR_SPIN");
-    const uint32_t spin = e ? (uint32_t) strtoul(e, nullptr, 0) : 0u;
-    for (uint32_t o : s.lfr_ctr) ctr[o + 3] = spin;
+    for (uint32_t o : s.lfr_ctr) ctr[o + 3] = c->lfr_spin;
 }
 
 // Keyframe batches (every phase wide, not fused, no k_lfr, intra frames only): the launch
@@ -1071,8 +1081,7 @@ static void init_lfr_ctr(const Staged &s, uint32_t *ctr)
 static void build_static_plan(vp9hip_ctx *c, const DevIn &in, const std::vector<uint32_t> &slot0)
 {
     Staged &s = c->stg;
-    const char *e = getenv("VP9HIP_STATIC");           // read per stage (tests switch it)
-    const bool off = e && !atoi(e);
+    const bool off = !c->static_plan;
     s.stat = false;
     s.launches.clear();
     s.exp_ko.clear();
@@ -1314,18 +1323,9 @@ static int stage_dev(vp9hip_ctx *c, const DevIn &in)
                 P.lfr_n = nt;
                 hl.insert(hl.end(), offs.begin(), offs.end());
                 hl.insert(hl.end(), recs.begin(), recs.end());
-                // wait table of the next position's MC tickets (lfmc_ticket): per filtered
-                // frame its index, SB rows and the row task of each SB row
-                P.lfw_off = (uint32_t) hl.size();
-                hl.push_back((uint32_t) lff.size());
-                for (size_t k = 0; k < lff.size(); k++) {
-                    hl.push_back((uint32_t) lff[k]);
-                    hl.push_back((uint32_t) tid[k].size());
-                    hl.insert(hl.end(), tid[k].begin(), tid[k].end());
-                }
                 P.lfr_ctr = (int) s.n_ctr;
                 s.lfr_ctr.push_back(s.n_ctr);
-                s.n_ctr += 4 + 2 * nt;     // ticket, done, timeouts, spin; progress and row-done per task
+                s.n_ctr += 4 + nt;         // ticket, done, timeouts, spin; progress per task
             } else {
                 P.lfr = false;
             }
@@ -1463,7 +1463,7 @@ static int stage_dev(vp9hip_ctx *c, const DevIn &in)
         if (s.stat_lists.size() > NS) return VP9HIP_EBUG;
         memcpy(img + s.o_lists + hl.size() * 4, s.stat_lists.data(), s.stat_lists.size() * 4);
     }
-    init_lfr_ctr(s, (uint32_t *) (img + s.o_ctr));
+    init_lfr_ctr(c, s, (uint32_t *) (img + s.o_ctr));
     {   // packets: blocks, eobs, coefficients (frames copied in parallel)
         std::atomic<int> next(0);
         auto worker = [&]() {
@@ -1475,17 +1475,17 @@ static int stage_dev(vp9hip_ctx *c, const DevIn &in)
                 if (f->ncoefs) memcpy(img + s.o_coefs + (size_t) F.coef0 * in.csz, f->coefs, (size_t) f->ncoefs * in.csz);
             }
         };
-        const int nt = std::min(n, host_threads());
+        const int nt = std::min(n, c->host_threads);
         std::vector<std::thread> pool;
         for (int t = 1; t < nt; t++) pool.emplace_back(worker);
         worker();
         for (auto &t : pool) t.join();
     }
-    if (s.stat) {   // test hook (VP9HIP_TEST_REJECT=k): the k-th static-plan batch of the context
-        // gets an intra mode the device planner rejects in its first frame's first block, so
-        // the adapters' handling of a rejected batch can be tested from real bitstreams
-        const char *e = getenv("VP9HIP_TEST_REJECT");
-        if (++c->nstat_staged == (e ? atoi(e) : 0) && nb) ((vp9h_block *) (img + s.o_blocks))->mode[0] = 20;
+    if (s.stat && c->test_reject) {   // test hook (vp9hip_test_hooks): the k-th static-plan batch
+        // of the context gets an intra mode the device planner rejects in its first frame's
+        // first block, so the adapters' handling of a rejected batch can be tested from real
+        // bitstreams
+        if (++c->nstat_staged == c->test_reject && nb) ((vp9h_block *) (img + s.o_blocks))->mode[0] = 20;
     }
     // the upload goes on the planner stream: the other batch slot's pixel kernels keep the
     // main stream busy meanwhile
@@ -1546,7 +1546,7 @@ static int finish_summary(vp9hip_ctx *c, Staged &s)
 // Run the device planner of the staged batch and build its launch list from the summary.
 static int plan_dev(vp9hip_ctx *c)
 {
-    static const bool plan_trace = getenv("VP9HIP_STAGE_TRACE") && atoi(getenv("VP9HIP_STAGE_TRACE"));
+    const bool plan_trace = c->stage_trace;
     const auto pt0 = std::chrono::steady_clock::now();
     Staged &s = c->stg;
     uint8_t *A = s.arena;
@@ -1609,9 +1609,8 @@ static int plan_dev(vp9hip_ctx *c)
     D.cap_dlists = s.nslots;
     D.nkeys = s.nkey;
     D.nframes = (uint32_t) s.nframes;
-    static const bool pprof = getenv("VP9HIP_PLAN_PROF") && atoi(getenv("VP9HIP_PLAN_PROF"));
-    static const int pdbg = getenv("VP9HIP_PLAN_DBG") ? atoi(getenv("VP9HIP_PLAN_DBG")) : 0;
-    D.dbg = pdbg;
+    const bool pprof = c->plan_prof_on;
+    D.dbg = c->plan_dbg;
     D.static_lists = s.stat ? 1 : 0;
     D.prof = nullptr;
     if (pprof) {
@@ -1627,18 +1626,13 @@ static int plan_dev(vp9hip_ctx *c)
     if (vp9hip_plan_enqueue(ps, &D, c->ss_h | c->ss_v << 1, s.nframes, s.max_blk, s.max_sb, s.nblk, s.nslots,
                             s.ncnt, (int) s.nkey, (const uint32_t *) (A + s.o_gidx), (int) s.n_gidx,
                             (uint32_t *) (A + s.o_summary), A + s.o_scan, s.scan_bytes, s.any_levels, s.plan_flags,
-                            s.stat && !(getenv("VP9HIP_PGUARD") && !atoi(getenv("VP9HIP_PGUARD"))) ? 1 : 0))
+                            s.stat ? 1 : 0))
         return VP9HIP_EEXTERNAL;
     if (c->timing) HIPCHK(hipEventRecord(c->pev[1], ps));
     c->plan_timed = c->timing;
     if (s.stat) {                  // launch list fixed at staging: the pixel launches wait on the device
         if (!s.plan_ev) HIPCHK(hipEventCreateWithFlags(&s.plan_ev, hipEventDisableTiming));
         HIPCHK(hipEventRecord(s.plan_ev, ps));
-        static const bool ssync = getenv("VP9HIP_STATIC_SYNC") && atoi(getenv("VP9HIP_STATIC_SYNC"));
-        if (ssync) {                           // A/B diagnostics only: the summary-read path's host pacing
-            HIPCHK(hipMemcpyAsync(s.summary_h, A + s.o_summary, s.summary_words * 4, hipMemcpyDeviceToHost, ps));
-            HIPCHK(hipStreamSynchronize(ps));
-        }
         s.summary_pending = true;
         s.planned = true;
         return 0;
@@ -1681,15 +1675,6 @@ static int plan_dev(vp9hip_ctx *c)
     }
     const uint32_t H = s.host_lists;
     const int nph = (int) s.dph.size();
-    // frame pipelining (VP9HIP_LFMC=1; off by default): a phase's k_lfr launch also runs the MC
-    // units of the group's next phase as extra tickets, each waiting for the reference rows it
-    // reads. Bit-exact, but measured 6.7x slower at C5 (113 vs 760 fps) and 4.7x at C2
-    // (profiles/r03h): a k_lfr row finishes only in the last ~28 % of the launch (each row is
-    // a 120-SB chain), so the MC workgroups sit on their CU slots polling for most of it and
-    // starve the other chains' and the other slot's kernels, which fill the chip otherwise
-    const char *lfe = getenv("VP9HIP_LFMC");                 // read per build (tests switch it)
-    const bool lfmc = lfe && atoi(lfe);
-    std::vector<char> mc_in_lfr(nph, 0);
     for (int g = 0; g < s.ngroups; g++)
         for (int ph = 0; ph < nph; ph++) {
             const Staged::DevPhase &P = s.dph[ph];
@@ -1699,26 +1684,21 @@ static int plan_dev(vp9hip_ctx *c)
                 s.launches.push_back(L);
             };
             const uint32_t m0 = gv[P.g_mc], m1 = gv[P.g_mc + 1];
-            if (m1 > m0 && !mc_in_lfr[ph]) push(K_MC, m0, m1 - m0, 0, PART_RECON, 0);
+            if (m1 > m0) push(K_MC, m0, m1 - m0, 0, PART_RECON, 0);
             auto rr = [&](int d, int tc) {
                 const uint32_t a = gv[P.g_res + (d * 5 + tc) * 2], b = gv[P.g_res + (d * 5 + tc) * 2 + 1];
                 return std::make_pair(a, b - a);
             };
             // level-scheduled (inter chain) phases: every tx size in one launch (arg 5, the
             // ranges in roff / rn); VP9HIP_RESID_MULTI=0 keeps one launch per size
-            const char *rme = getenv("VP9HIP_RESID_MULTI");
-            const bool rmulti = !rme || atoi(rme);
+            const bool rmulti = c->resid_multi;
             if (!P.fused && P.levels && rmulti) {
                 Launch L = { K_RESID, 0, 0, 5, g, ph, PART_RECON, 0 };
                 for (int tc = 0; tc < 5; tc++) { L.roff[tc] = rr(0, tc).first; L.rn[tc] = rr(0, tc).second; L.n += L.rn[tc]; }
                 if (L.n) s.launches.push_back(L);
             } else if (!P.fused) {
-                static const bool rdev = getenv("VP9HIP_RESID_DEV") && atoi(getenv("VP9HIP_RESID_DEV"));   // A/B only
                 for (int tc = 0; tc < 5; tc++)
-                    if (rr(0, tc).second) {
-                        push(K_RESID, rdev ? (uint32_t) (P.g_res + tc * 2) : rr(0, tc).first, rr(0, tc).second, tc, PART_RECON, 0);
-                        s.launches.back().devr = rdev;
-                    }
+                    if (rr(0, tc).second) push(K_RESID, rr(0, tc).first, rr(0, tc).second, tc, PART_RECON, 0);
             }
             auto step = [&](int d) {
                 const uint32_t k = P.key0 + (uint32_t) d;
@@ -1729,19 +1709,6 @@ static int plan_dev(vp9hip_ctx *c)
                 push(K_LFR, P.lfr_off, P.lfr_n, (int) P.lfr_ctr, PART_LF, 0);
                 s.alg_bytes[K_LF] -= P.lfr_bytes;
                 s.alg_bytes[K_LFR] += P.lfr_bytes;
-                int nx = ph + 1;                                  // the group's next phase
-                while (nx < nph && (s.dph[nx].frames.empty() || s.dph[nx].group != g)) nx++;
-                if (!lfmc || nx >= nph) return;
-                const Staged::DevPhase &Q = s.dph[nx];
-                const uint32_t q0 = gv[Q.g_mc], q1 = gv[Q.g_mc + 1];
-                if (q1 <= q0) return;
-                Launch &L = s.launches.back();
-                L.off2 = q0; L.n2 = q1 - q0; L.roff[0] = P.lfw_off;
-                mc_in_lfr[nx] = 1;
-                for (int i : Q.frames) {
-                    s.alg_bytes[K_MC] -= fbytes(i, 1);
-                    s.alg_bytes[K_LFR] += fbytes(i, 1);
-                }
             };
             if (!s.fuse || P.levels) {
                 for (int d = 0; d < P.nkey; d++)
@@ -1795,7 +1762,7 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     // reconstruction) instead of x + 2y diagonal launches
     const bool lfr_any = c->lf_rows > 0 && !tiled;
     // VP9HIP_STAGE_TRACE=1: host time of the staging steps on stderr
-    static const bool stage_trace = getenv("VP9HIP_STAGE_TRACE") && atoi(getenv("VP9HIP_STAGE_TRACE"));
+    const bool stage_trace = c->stage_trace;
     double st_ms[6] = { 0, 0, 0, 0, 0, 0 };
     auto st_t0 = std::chrono::steady_clock::now();
 #define STAGE_T(k) do { auto t_ = std::chrono::steady_clock::now(); \
@@ -1963,10 +1930,9 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     // SB to its right in place of a column of one-pixel frame rows (128 scattered lines)
     {
         const size_t eb = (size_t) edge_sbs * EDGE_PIX * c->bypp + 256;
-        const char *ee = getenv("VP9HIP_EDGE");      // read per staging (tests switch it)
         // only the 4:2:0 tile loader reads the edge columns (the other chroma formats load
         // their left column from frame rows): no buffer written and never read for those
-        const bool edge_off = (ee && !atoi(ee)) || !(c->ss_h && c->ss_v);
+        const bool edge_off = !c->edge || !(c->ss_h && c->ss_v);
         if (edge_sbs && !edge_off && eb > s.edge_cap) {
             if (s.edge) hipFree(s.edge);
             s.edge = nullptr;
@@ -2023,7 +1989,7 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
                 plans[i].err = plan_frame(fbs[i], plans[i]);
             }
         };
-        const int nt = std::min(n, host_threads());
+        const int nt = std::min(n, c->host_threads);
         std::vector<std::thread> pool;
         for (int t = 1; t < nt; t++) pool.emplace_back(worker);
         worker();
@@ -2273,7 +2239,7 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     uint8_t *img = s.pinned;
     memcpy(img + s.o_frames, s.frames.data(), s.frames.size() * sizeof(FrameDesc));
     if (!s.lists.empty()) memcpy(img + s.o_lists, s.lists.data(), s.lists.size() * sizeof(uint32_t));
-    init_lfr_ctr(s, (uint32_t *) (img + s.o_ctr));
+    init_lfr_ctr(c, s, (uint32_t *) (img + s.o_ctr));
     std::vector<double> inplace_bytes(n, 0.0);
     {
         std::atomic<int> next(0);
@@ -2318,7 +2284,7 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
                 plans[i] = FramePlan();                  // release the frame's host images
             }
         };
-        const int nt = std::min(n, host_threads());
+        const int nt = std::min(n, c->host_threads);
         std::vector<std::thread> pool;
         for (int t = 1; t < nt; t++) pool.emplace_back(worker);
         worker();
@@ -2378,13 +2344,10 @@ extern "C" int vp9hip_run_batch(vp9hip_ctx *c)
     if (s.dev) {                          // plan on the device from the resident packets
         const int r = plan_dev(c);
         if (r) return r;
-        static const bool plan_only = getenv("VP9HIP_PLAN_ONLY") && atoi(getenv("VP9HIP_PLAN_ONLY"));
-        if (plan_only) return 0;          // diagnostics: the planner alone
+        if (c->plan_only) return 0;       // diagnostics: the planner alone
     }
     if (s.dev && s.stat && plan_stream(c) != c->st) {
-        static const bool hw = getenv("VP9HIP_STATIC_HOSTWAIT") && atoi(getenv("VP9HIP_STATIC_HOSTWAIT"));
-        if (hw) HIPCHK(hipEventSynchronize(s.plan_ev));          // A/B diagnostics only
-        else HIPCHK(hipStreamWaitEvent(c->st, s.plan_ev, 0));
+        HIPCHK(hipStreamWaitEvent(c->st, s.plan_ev, 0));
     }
     // a batch touching another slot's buffers follows that slot's last run
     for (int k = 0; c->slot_streams && k < MAX_SLOTS; k++)
@@ -2425,7 +2388,7 @@ static int launch_one(vp9hip_ctx *c, const Launch &L, hipStream_t st)
     const uint32_t *lists = (const uint32_t *) (s.arena + s.o_lists);
     switch (L.kind) {
     case K_MC:
-        return vp9hip_launch_mc(c->hb, st, (int) L.n, (const McUnit *) (s.arena + s.o_mcs) + L.off, fr);
+        return vp9hip_launch_mc(c->hb, st, (int) L.n, (const McUnit *) (s.arena + s.o_mcs) + L.off, fr, &c->kcfg);
     case K_RESID:
         if (L.devr)
             return vp9hip_launch_resid_dev(c->hb, st, L.arg, (int) L.n, (const RJob *) (s.arena + s.o_rjobs),
@@ -2443,7 +2406,7 @@ static int launch_one(vp9hip_ctx *c, const Launch &L, hipStream_t st)
     case K_LFR:
         return vp9hip_launch_lfr(c->hb | c->ss_h << 1 | c->ss_v << 2, st, (int) L.n, lists + L.off,
                                  (const LFRec *) (s.arena + s.o_lfs), fr, (uint32_t *) (s.arena + s.o_ctr) + L.arg,
-                                 (const McUnit *) (s.arena + s.o_mcs) + L.off2, (int) L.n2, L.n2 ? lists + L.roff[0] : nullptr);
+                                 &c->kcfg);
     case K_LF:
         return vp9hip_launch_lf(c->hb | c->ss_h << 1 | c->ss_v << 2, st, (int) L.n, lists + L.off, (const LFRec *) (s.arena + s.o_lfs), fr, c->dbg >> 16);
     case K_PLF: {
@@ -2461,16 +2424,9 @@ static int launch_one(vp9hip_ctx *c, const Launch &L, hipStream_t st)
 }
 
 // Enqueue the staged launches: group g runs on its own stream (group 0 on the main
-// stream), forked from and joined back into the main stream.
-// lf_overlap: a group's loop filter runs on a second stream of its own, overlapping the
-// intra wavefront of the same phase. LF of SB (x, y) rewrites pre-LF pixels that intra
-// prediction reads: the last row / column of SB (x, y) and of its left / upper neighbours
-// (SB (x, y)'s left and top edges). Their readers are the intra blocks of SBs (x - 1 .. x + 1,
-// y .. y + 1), on intra diagonals <= x_in_tile + y + 2 <= (x + 2y) + LF_LAG. So LF diagonal j
-// (x + 2y = j) starts after intra diagonal j + LF_LAG (and after MC / residuals); the LF
-// stream is in order (the x + 2y wavefront), and the next phase's reconstruction (whose MC
-// reads post-LF references) waits for the phase's last LF launch. This is the ordering
-// the reference gets from its intra_pred_data backup of the pre-LF SB row (vp9.c:1404-1416).
+// stream), forked from and joined back into the main stream. (Round 1 also ran a group's
+// loop filter on a second stream, LF diagonal j after intra diagonal j + LF_LAG through
+// cross-stream events: 8,131 vs 11,800 fps at C3, removed; k_plf fuses the two instead.)
 static int enqueue_batch(vp9hip_ctx *c)
 {
     Staged &s = c->stg;
@@ -2481,78 +2437,29 @@ static int enqueue_batch(vp9hip_ctx *c)
         c->ev.resize(2 * nl);
         for (size_t i = old; i < c->ev.size(); i++) HIPCHK(hipEventCreate(&c->ev[i]));
     }
-    const bool ovl = c->lf_overlap;
     // timing runs put every launch on the main stream (serialised, as under a rocprofv3
     // kernel trace), so each launch's event duration is its own, not one inflated by the
-    // other frame groups' launches (VP9HIP_TIMING_CONCURRENT=1: the groups' own streams)
-    static const bool tconc = getenv("VP9HIP_TIMING_CONCURRENT") && atoi(getenv("VP9HIP_TIMING_CONCURRENT"));
-    const bool serial = c->timing && !tconc && !ovl;
+    // other frame groups' launches
+    const bool serial = c->timing;
     const int ngs = serial ? 1 : s.ngroups;
     auto rstream = [&](int g) { return g && !serial ? c->xst[g - 1] : c->st; };
     // fork: every stream of the batch starts after what is queued on the main stream
-    if (ngs > 1 || ovl) {
+    if (ngs > 1) {
         HIPCHK(hipEventRecord(c->fork_ev, c->st));
         for (int g = 1; g < ngs; g++) HIPCHK(hipStreamWaitEvent(c->xst[g - 1], c->fork_ev, 0));
-        if (ovl)
-            for (int g = 0; g < s.ngroups; g++) HIPCHK(hipStreamWaitEvent(c->lst[g], c->fork_ev, 0));
     }
-    // recon -> LF dependencies: for each LF launch, the recon launch (same group and phase)
-    // it must follow; events are recorded after those recon launches only
-    std::vector<int> lf_dep(nl, -1), rec_ev(nl, -1);
-    int nev = 0;
-    if (ovl) {
-        for (size_t i = 0; i < nl; i++) {
-            const Launch &L = s.launches[i];
-            if (L.kind != K_LF) continue;
-            int dep = -1;
-            for (size_t k = 0; k < nl; k++) {           // launches of the phase precede its LF
-                const Launch &R = s.launches[k];
-                if (R.ph != L.ph || R.kind == K_LF) continue;
-                if (R.kind != K_PRED || R.step <= L.step + LF_LAG) dep = (int) k;
-            }
-            lf_dep[i] = dep;
-            if (dep >= 0 && rec_ev[dep] < 0) rec_ev[dep] = nev++;
-        }
-        while ((int) c->sev.size() < nev) {
-            hipEvent_t e;
-            HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            c->sev.push_back(e);
-        }
-    }
-    std::vector<int> waited(s.ngroups, -1), last_lf_ph(s.ngroups, -1), rec_ph(s.ngroups, -1);
     for (size_t i = 0; i < nl; i++) {
         const Launch &L = s.launches[i];
-        const bool lf = ovl && L.kind == K_LF;
-        hipStream_t st = lf ? c->lst[L.grp] : rstream(L.grp);
-        if (lf) {
-            if (lf_dep[i] >= 0 && lf_dep[i] != waited[L.grp]) {
-                HIPCHK(hipStreamWaitEvent(st, c->sev[rec_ev[lf_dep[i]]], 0));
-                waited[L.grp] = lf_dep[i];
-            }
-            last_lf_ph[L.grp] = L.ph;
-        } else if (ovl && rec_ph[L.grp] != L.ph) {
-            // a new phase's reconstruction follows the previous phase's loop filter
-            rec_ph[L.grp] = L.ph;
-            if (last_lf_ph[L.grp] >= 0) {
-                HIPCHK(hipEventRecord(c->lf_done[L.grp], c->lst[L.grp]));
-                HIPCHK(hipStreamWaitEvent(st, c->lf_done[L.grp], 0));
-            }
-        }
+        hipStream_t st = rstream(L.grp);
         if (c->timing) HIPCHK(hipEventRecord(c->ev[2 * i], st));
         if (launch_one(c, L, st)) return VP9HIP_EEXTERNAL;
         if (c->timing) HIPCHK(hipEventRecord(c->ev[2 * i + 1], st));
-        if (!lf && ovl && rec_ev[i] >= 0) HIPCHK(hipEventRecord(c->sev[rec_ev[i]], st));
     }
     // join: the main stream (downloads, sync, the next stage) waits for every stream
     for (int g = 1; g < ngs; g++) {
         HIPCHK(hipEventRecord(c->join_ev[g - 1], c->xst[g - 1]));
         HIPCHK(hipStreamWaitEvent(c->st, c->join_ev[g - 1], 0));
     }
-    if (ovl)
-        for (int g = 0; g < s.ngroups; g++) {
-            HIPCHK(hipEventRecord(c->join_ev[MAX_GROUPS + g], c->lst[g]));
-            HIPCHK(hipStreamWaitEvent(c->st, c->join_ev[MAX_GROUPS + g], 0));
-        }
     return 0;
 }
 
@@ -2741,13 +2648,13 @@ extern "C" int vp9hip_download_frame(vp9hip_ctx *c, int buf, uint8_t *const plan
     hipSetDevice(c->dev);
     if (const int r = wait_writers(c, buf)) return r;
     if (!c->dst_dl) HIPCHK(hipStreamCreateWithFlags(&c->dst_dl, hipStreamNonBlocking));
+    // a buffer no staged batch writes may still be under vp9hip_fill_buffers' memset (on the
+    // main stream): the copies follow it
+    if (c->fill_ev) HIPCHK(hipStreamWaitEvent(c->dst_dl, c->fill_ev, 0));
     if (!c->dl_pin) HIPCHK(hipHostMalloc((void **) &c->dl_pin, DL_CHUNK * DL_RING, hipHostMallocDefault));
     for (auto &e : c->dl_ev)
         if (!e) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    if (!c->dl_pool) {
-        const char *e = getenv("VP9HIP_DL_THREADS");   // copy threads besides the caller (default 3)
-        c->dl_pool.reset(new CopyPool(e ? std::max(0, std::min(15, atoi(e))) : 3));
-    }
+    if (!c->dl_pool) c->dl_pool.reset(new CopyPool(c->dl_threads));
     // chunks of whole rows: D2H into ring slot k, then (once the slot after it is queued)
     // the host copy of slot k into the caller's planes
     struct Piece { int p, y0, ny; };

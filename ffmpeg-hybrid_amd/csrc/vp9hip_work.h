@@ -166,4 +166,11 @@ typedef struct McUnit {
     McRef    r[2];
 } McUnit;
 
+/* Kernel selections a context fixes when it opens (vp9hip_open reads the VP9HIP_* switches
+ * once; no launcher reads the environment). */
+typedef struct KCfg {
+    int lfro;                 /* 4:2:0 row LF: 1 k_lfro (default), 0 k_lfrd (VP9HIP_LFRO=0)     */
+    int mcq_slices;           /* k_mcq task slices per unit group; 0: from the grid size         */
+} KCfg;
+
 #endif

@@ -103,9 +103,16 @@ typedef struct vp9h_frame {
 /* ---- device context ---------------------------------------------------- */
 typedef struct vp9hip_ctx vp9hip_ctx;
 
-/* Open a context on HIP device `device`. Returns 0 or a negative error. */
+/* Open a context on HIP device `device`. Returns 0 or a negative error. The context reads
+ * its VP9HIP_* environment switches (kernel A/B selections and diagnostics)
+ * here, once; nothing later reads the environment. */
 int  vp9hip_open(int device, vp9hip_ctx **out);
 void vp9hip_close(vp9hip_ctx *ctx);
+/* Test hooks, copied by every context opened afterwards (0, 0 = off, the default):
+ * reject_batch = k makes the k-th static-plan batch the context stages carry an intra mode
+ * the device planner rejects; lfr_spin = n bounds the row loop filter's hand-off waits to
+ * n polls (forcing its timeout path). No reference counterpart; never called in production. */
+void vp9hip_test_hooks(int reject_batch, uint32_t lfr_spin);
 
 /* Allocate `nbufs` device frame buffers of w x h (padded to 64 internally). */
 int  vp9hip_configure(vp9hip_ctx *ctx, int width, int height, int bpp, int ss_h, int ss_v,
@@ -189,7 +196,7 @@ int  vp9hip_slot_stream_wait(vp9hip_ctx *ctx, int slot, void *stream);
 /* 1 while the last run of batch slot `slot` is still executing, 0 once it is done. */
 int  vp9hip_slot_busy(vp9hip_ctx *ctx, int slot);
 /* Wait for all queued work of every batch slot. VP9HIP_EBUG if a row-pipelined
- * loop-filter launch (k_lfr) of any slot gave up a bounded wait on another workgroup's
+ * loop-filter launch (k_lfrd / k_lfro) of any slot gave up a bounded wait on another workgroup's
  * progress (frames not trusted). */
 int  vp9hip_sync(vp9hip_ctx *ctx);
 

@@ -170,7 +170,7 @@ static int drain(Consumer *c)
 int main(int argc, char **argv)
 {
     if (argc < 6) {
-        fprintf(stderr, "usage: %s IN.ivf OUT.yuv|- BPP SS_H SS_V [PASSES [LAG [MODE [ASYNC_DEPTH [EXTRA]]]]]\n", argv[0]);
+        fprintf(stderr, "usage: %s IN.ivf OUT.yuv|- BPP SS_H SS_V [PASSES [LAG [MODE [ASYNC_DEPTH [EXTRA [REJECT,SPIN]]]]]]\n", argv[0]);
         return 2;
     }
     const int bpp = atoi(argv[3]), ssh = atoi(argv[4]), ssv = atoi(argv[5]), passes = argc > 6 ? atoi(argv[6]) : 2;
@@ -179,6 +179,11 @@ int main(int argc, char **argv)
     const int threaded = argc > 8 && !strcmp(argv[8], "thread");
     const int depth = argc > 9 ? atoi(argv[9]) : 0;
     const int extra = argc > 10 ? atoi(argv[10]) : 2 + lag;
+    if (argc > 11) {                     /* test hooks: reject the k-th static batch, row-LF spin bound */
+        char *e = NULL;
+        const int reject = (int) strtol(argv[11], &e, 0);
+        vp9hip_test_hooks(reject, e && *e == ',' ? (uint32_t) strtoul(e + 1, NULL, 0) : 0u);
+    }
     FILE *fi = fopen(argv[1], "rb");
     if (!fi) { perror(argv[1]); return 2; }
     fseek(fi, 0, SEEK_END);

@@ -2,14 +2,12 @@
 
 k_lfr bounds each wait for the SB row above (ctr[3] polls, 2^22 by default) and counts the
 waits it gave up in its counter block (ctr[2]); such a frame was filtered with a stale top
-halo. VP9HIP_LFR_SPIN (read at every stage) sets the bound, here to 1 poll, so the waits
+halo. vp9hip_test_hooks(0, n) sets the bound for contexts opened afterwards, here to 1 poll, so the waits
 of the first SBs of each row give up. The batch API must then fail vp9hip_sync with
 VP9HIP_EBUG, and the decoder must fail the frames of that batch instead of handing them
 out (the advisor's silent-corruption path: staging the next batch used to zero the words).
 With the default bound the same stream decodes bit-exact.
 """
-import os
-
 import pytest
 
 from test_ivf_decoder import _oracle_outputs, _same
@@ -26,10 +24,10 @@ def _gop(v9, n=4):
 
 
 @pytest.fixture
-def tiny_spin():
-    os.environ["VP9HIP_LFR_SPIN"] = "1"
+def tiny_spin(v9):
+    v9.test_hooks(lfr_spin=1)
     yield
-    del os.environ["VP9HIP_LFR_SPIN"]
+    v9.test_hooks()
 
 
 def test_decoder_fails_frames_of_a_timed_out_batch(v9, tiny_spin):
@@ -64,12 +62,12 @@ def test_default_bound_decodes_bit_exact(v9, orc):
     _same(got, _oracle_outputs(v9, orc, pkts), "default spin bound")
 
 
-def test_hwaccel_fails_frames_of_a_timed_out_batch(v9, tmp_path, tiny_spin):
+def test_hwaccel_fails_frames_of_a_timed_out_batch(v9, tmp_path):
     """The FFHWAccel path checks the same hand-off words before a frame is read
     (vp9hip_hwframe_sync / transfer): the harness's decode fails with VP9HIP_EBUG."""
     from test_hwaccel_harness import run_harness
     ivf = tmp_path / "t.ivf"
     ivf.write_bytes(v9.ivf_write(_gop(v9), 1920, 1080))
     for mode in ("download", "device"):
-        rc, _, _, err = run_harness(ivf, "-", 8, 1, 1, 1, 0, mode, 4, env=dict(os.environ))
+        rc, _, _, err = run_harness(ivf, "-", 8, 1, 1, 1, 0, mode, 4, hooks=(0, 1))
         assert rc == 1 and ("decode: %d" % v9.EBUG) in err, (mode, err)

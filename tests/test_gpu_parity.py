@@ -70,13 +70,10 @@ INTER = [
 ]
 
 
-@pytest.mark.parametrize("mcp", ["3", "2", "1", "0"])
 @pytest.mark.parametrize("w,h,bpp,kw", INTER)
-def test_inter_parity(v9, orc, gpu, monkeypatch, w, h, bpp, kw, mcp):
-    """VP9HIP_MCP: 3 (default) k_mcq (4-column tasks, packed dot products), 2 the packed
-    one-column kernel k_mcp at every bit depth, 1 k_mcp for high bit depth only, 0 one
-    workgroup per unit (k_mc)."""
-    monkeypatch.setenv("VP9HIP_MCP", mcp)
+def test_inter_parity(v9, orc, gpu, w, h, bpp, kw):
+    """Inter frames through k_mcq (4-column tasks, packed dot products) and the in-place
+    residuals, every MC variant of the INTER cases."""
     key_kw = {k: x for k, x in kw.items() if k in ("log2_tile_cols",)}
     key = v9.SynthFrame(v9.synth_params(w, h, bpp, seed=11, **key_kw))
     ref0 = v9.alloc_planes(w, h, bpp)
@@ -128,13 +125,14 @@ def test_wide_batch_separate_residual_launches(v9, orc, gpu):
 
 
 @pytest.mark.parametrize("static", [1, 0])
-def test_static_plan_keyframe_batch(v9, orc, gpu, monkeypatch, static):
+def test_static_plan_keyframe_batch(v9, orc, monkeypatch, static):
     """Keyframe batches of wide phases run a launch list fixed at staging (runtime "static
     plan": no host wait between the device planner and the pixel launches; residual job
     ranges read from the planner's summary in HBM). Same pixels as the summary-read path
     (VP9HIP_STATIC=0), over 3 runs of the staged batch, mixed tile columns, lossless and
     lossy frames in one phase, and 10-bit."""
-    monkeypatch.setenv("VP9HIP_STATIC", str(static))
+    monkeypatch.setenv("VP9HIP_STATIC", str(static))      # read when the context opens
+    gpu = v9.Device(0)
     for bpp in (8, 10):
         w, h, n = 520, 136, 18
         frames = [v9.SynthFrame(v9.synth_params(w, h, bpp, seed=500 + i, log2_tile_cols=i % 2,
@@ -150,6 +148,7 @@ def test_static_plan_keyframe_batch(v9, orc, gpu, monkeypatch, static):
             ref = v9.alloc_planes(w, h, bpp)
             orc.decode_frame(frames[i].pkt, ref)
             _cmp(v9, gpu.download(i), ref, w, h, "static=%d %d-bit batch frame %d" % (static, bpp, i))
+    gpu.close()
 
 
 @pytest.mark.parametrize("slot_streams", [1, 0])
@@ -333,13 +332,10 @@ SCALED = [
 ]
 
 
-@pytest.mark.parametrize("mcp", ["0", "2", "3"])
 @pytest.mark.parametrize("rs,fs,bpp,kw", SCALED)
-def test_scaled_reference_parity(v9, orc, gpu, monkeypatch, rs, fs, bpp, kw, mcp):
+def test_scaled_reference_parity(v9, orc, gpu, rs, fs, bpp, kw):
     """Reference scaling (vp9recon.c:492-628, vp9.c:845-880): a keyframe at one size,
-    an inter frame at another size predicting from it (k_mcp's per-pixel tasks, and
-    VP9HIP_MCP=0: k_mc)."""
-    monkeypatch.setenv("VP9HIP_MCP", mcp)
+    an inter frame at another size predicting from it (k_mcq's per-pixel scaled tasks)."""
     (rw, rh), (w, h) = rs, fs
     key = v9.SynthFrame(v9.synth_params(rw, rh, bpp, seed=900))
     gpu.configure(max(rw, w), max(rh, h), bpp, nbufs=2)

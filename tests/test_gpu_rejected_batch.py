@@ -7,11 +7,10 @@ that slot reports it, and the adapters remember the batch and fail its frames, n
 batch's (the advisor's round-3 finding: the rejection used to be reported once and then
 charged to whichever batch came next, or lost).
 
-VP9HIP_TEST_REJECT=k makes the k-th static-plan batch a context stages carry an intra mode
-the planner rejects (a test hook in stage_dev); the bitstreams themselves are valid.
+vp9hip_test_hooks(k, 0) makes the k-th static-plan batch a context stages carry an intra mode
+the planner rejects (a test hook in stage_dev, copied by contexts opened afterwards); the
+bitstreams themselves are valid.
 """
-import os
-
 import numpy as np
 import pytest
 
@@ -26,10 +25,10 @@ def _keyframes(v9, w, h, n, seed=900):
 
 
 @pytest.fixture
-def reject_second():
-    os.environ["VP9HIP_TEST_REJECT"] = "2"
+def reject_second(v9):
+    v9.test_hooks(reject_batch=2)
     yield
-    del os.environ["VP9HIP_TEST_REJECT"]
+    v9.test_hooks()
 
 
 def test_decoder_fails_only_the_rejected_batch(v9, orc, reject_second):
@@ -94,13 +93,13 @@ def test_sync_reports_rejection_until_restaged(v9, orc, reject_second):
         dev.close()
 
 
-def test_hwaccel_fails_the_rejected_batch(v9, tmp_path, reject_second):
+def test_hwaccel_fails_the_rejected_batch(v9, tmp_path):
     """The FFHWAccel path: the harness's wait on a frame of the rejected batch fails with
     AVERROR_INVALIDDATA after the first batch's 16 frames were read."""
     from test_hwaccel_harness import run_harness
     ivf = tmp_path / "k.ivf"
     ivf.write_bytes(v9.ivf_write(_keyframes(v9, 352, 288, 48), 352, 288))
     # the consumer reads 32 frames behind: batches of 16 fill up (static plans)
-    rc, _, _, err = run_harness(ivf, "-", 8, 1, 1, 1, 32, "download", 16, env=dict(os.environ))
+    rc, _, _, err = run_harness(ivf, "-", 8, 1, 1, 1, 32, "download", 16, hooks=(2, 0))
     # the harness counts the failed read too: 16 good frames + the first of the rejected batch
     assert rc == 1 and ("decode: %d after 17 frames" % v9.EINVALIDDATA) in err, err

@@ -68,12 +68,16 @@ def _read_frames(path, w, h, bpp, ssh, ssv):
     return out
 
 
-def run_harness(ivf, out, bpp, ssh, ssv, passes=2, lag=0, mode="download", depth=0, env=None, timeout=120, extra=None):
+def run_harness(ivf, out, bpp, ssh, ssv, passes=2, lag=0, mode="download", depth=0, env=None, timeout=120, extra=None,
+                hooks=None):
     """The harness binary; returns (returncode, frames, seconds, stderr). extra: the frame
-    count handed to frame_params (default 2 + lag)."""
+    count handed to frame_params (default 2 + lag); hooks: (reject_batch, lfr_spin), the
+    vp9hip_test_hooks values the harness sets before it opens the decoder."""
     args = [HARNESS, str(ivf), str(out), str(bpp), str(ssh), str(ssv), str(passes), str(lag), mode, str(depth)]
-    if extra is not None:
-        args.append(str(extra))
+    if extra is not None or hooks is not None:
+        args.append(str(extra if extra is not None else 2 + lag))
+    if hooks is not None:
+        args.append("%d,%d" % hooks)
     r = subprocess.run(args, capture_output=True, text=True, timeout=timeout, env=env)
     f = r.stdout.split()
     if r.returncode or len(f) < 4:
