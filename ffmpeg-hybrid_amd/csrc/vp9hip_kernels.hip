@@ -885,6 +885,8 @@ DEV void pred_pass(uint32_t w, int lane, PIX *tile, uint16_t *eb, int bd, const 
     // one chunk ahead, so at most two chunks are live
     constexpr int F0 = MAXN < 8 ? MAXN : 8;
     uint32_t f[F0];
+    // (a per-lane choice in mixed passes, so a flat pointer there; reading every job of a
+    // 16 / 32 pass from the global table instead measured slower: C3 k_plf 7.28 -> 7.36 ms)
     const uint32_t *ftab = PRED_LTAB_LDS && (ts <= 1 || MAXN <= 8) ? ltab + slot * 80 + toff + li
                                                                    : ptab + slot * PTAB_SLOT + toff + li;
 #pragma unroll
@@ -974,14 +976,28 @@ DEV void run_pass(uint32_t w, int lane, PIX *tile, uint16_t *eb, int bd, const P
     wave_sync();
 }
 
+// The intra wave's job records and pass words, copied to LDS in the prologue (k_pred, 4:2:0):
+// a pass then finds its job records by an LDS read instead of a global load whose address
+// waited on another global load (the pass word), so only the residual loads are global in
+// the pass chain. JL = the planner's job cap per SB (4x4 units of all planes, vp9hip_plan.hip
+// JCAP). Measured (profiles/r05d): C2 11,808 -> 12,018 fps; in k_plf the extra 4.6 KB of LDS
+// (10.8 -> 15.2 KB per workgroup of the fused launch) cost more than it saved (C3 10,219 ->
+// 9,797 fps, k_plf 7.27 -> 7.69 ms per step), so k_plf keeps the global lists.
+template <class G, bool LISTS> struct PredLists {
+    static constexpr bool ON = LISTS && G::SH == 1 && G::SV == 1;
+    static constexpr int JL = 256 + 2 * (16 >> G::SH) * (16 >> G::SV);
+    static constexpr int N = ON ? JL : 1;
+};
 // LDS of one k_pred workgroup (one wavefront).
-template <typename PIX, class G> struct PredLds {
+template <typename PIX, class G, bool LISTS> struct PredLds {
     PIX tile[PRED_K * G::TILE];
     uint16_t eb[288];                 // per job 2n+8 edge pixels at a pitch of 2n+10 (an odd dword
                                       // count: the jobs' arrays start in different banks)
 #if PRED_LTAB_LDS
     uint32_t ltab[10 * 80];           // formula words of 4x4 and 8x8, all slots
 #endif
+    PJob jl[PredLists<G, LISTS>::N];  // job records (pass order)
+    uint32_t pw[PredLists<G, LISTS>::N];   // pass words
 };
 
 template <typename PIX>
@@ -1000,16 +1016,17 @@ DEV void load_ltab(uint32_t *ltab, const uint32_t *__restrict__ ptab, int lane)
 
 // PRED_PROF builds (profiling only, tools/pred_prof.py): lane 0 of each intra workgroup
 // sums shader-clock cycles: [0] tile loads, [1] all passes, [2] interior stores, [3] passes,
-// [4] workgroups, [5 + i] cycles and [9 + i] count of passes with MAXN = 4 << i
+// [4] workgroups, [5 + i] cycles and [9 + i] count of passes with MAXN = 4 << i; k_plf's LF
+// workgroups: [13] cycles, [14] count; [15] the slowest intra workgroup's cycles
 #ifndef PRED_PROF
 #define PRED_PROF 0
 #endif
 KP_DEV unsigned long long pred_prof[16];
 // Intra prediction of one workgroup record (the ltab copy must be loaded).
-template <typename PIX, class G>
+template <typename PIX, class G, bool LISTS>
 DEV void pred_wg(const WGRec *wgp, const SBRec *__restrict__ sbs, const PJob *__restrict__ jobs,
                  const uint32_t *__restrict__ passes, const FrameDesc *__restrict__ frames,
-                 const int16_t *__restrict__ resid, const uint32_t *__restrict__ ptab, PredLds<PIX, G> &S, int lane,
+                 const int16_t *__restrict__ resid, const uint32_t *__restrict__ ptab, PredLds<PIX, G, LISTS> &S, int lane,
                  int dbg)
 {
     PIX *tile = S.tile;
@@ -1019,13 +1036,27 @@ DEV void pred_wg(const WGRec *wgp, const SBRec *__restrict__ sbs, const PJob *__
 #else
     const uint32_t *ltab = nullptr;
 #endif
-    const uint32_t wjob0 = wgp->job0, wpass0 = wgp->pass0, wnjobs = wgp->njobs, wnpass = wgp->npass;
-    const PJob *lj = jobs + wjob0;         // job records: read a pass ahead (L1/L2)
-    const uint32_t *lp = passes + wpass0;  // pass words: wave-uniform scalar loads
+    typedef PredLists<G, LISTS> PL;
+    const uint32_t wjob0 = wgp->job0, wpass0 = wgp->pass0;
+    const uint32_t wnjobs = PL::ON ? min((uint32_t) wgp->njobs, (uint32_t) PL::JL) : wgp->njobs;
+    const uint32_t wnpass = PL::ON ? min((uint32_t) wgp->npass, wnjobs) : wgp->npass;
+    const PJob *gj = jobs + wjob0;         // job records (global)
+    const uint32_t *gp = passes + wpass0;  // pass words (global)
     const int bd = frames[sbs[wgp->sb[0]].frame].bd;
     uint64_t pp0 = PRED_PROF ? clock64() : 0, pp[13] = {0};
 
     // ---- prologue: job list, pass words, SB neighbourhoods (pre-LF pixels) ----
+    constexpr int LU = PL::ON ? (PL::JL + 63) / 64 : 1;
+    PJob lv[LU];
+    uint32_t pv[LU];
+    if (PL::ON) {                          // issued first: they land under the tile loads
+#pragma unroll
+        for (int u = 0; u < LU; u++) {
+            const uint32_t i = (uint32_t) (lane + 64 * u);
+            if (i < wnjobs) lv[u] = gj[i];
+            if (i < wnpass) pv[u] = gp[i];
+        }
+    }
 #pragma unroll 1
     for (int k = 0; k < PRED_K; k++) {
         const uint32_t sbi = __builtin_amdgcn_readfirstlane(wgp->sb[k]);
@@ -1034,6 +1065,16 @@ DEV void pred_wg(const WGRec *wgp, const SBRec *__restrict__ sbs, const PJob *__
             if (!(dbg & 4)) load_sb_tile<PIX, G>(frames[sb.frame], sb.sbx, sb.sby, sb.flags & 1, lane, tile + k * G::TILE);
         }
     }
+    if (PL::ON) {
+#pragma unroll
+        for (int u = 0; u < LU; u++) {
+            const uint32_t i = (uint32_t) (lane + 64 * u);
+            if (i < wnjobs) S.jl[i] = lv[u];
+            if (i < wnpass) S.pw[i] = pv[u];
+        }
+    }
+    const PJob *lj = PL::ON ? S.jl : gj;   // job records: read a pass ahead
+    const uint32_t *lp = PL::ON ? S.pw : gp;   // pass words: wave-uniform
     wave_sync();
     if (PRED_PROF) { const uint64_t t = clock64(); pp[0] += t - pp0; pp0 = t; }
 
@@ -1097,6 +1138,7 @@ DEV void pred_wg(const WGRec *wgp, const SBRec *__restrict__ sbs, const PJob *__
         pp[2] += clock64() - pp0;
         pp[4] = 1;
         for (int i = 0; i < 13; i++) atomicAdd(&pred_prof[i], pp[i]);
+        atomicMax(&pred_prof[15], pp[0] + pp[1] + pp[2]);    // the slowest intra workgroup
     }
 }
 
@@ -1106,11 +1148,11 @@ __global__ __launch_bounds__(64) void k_pred(const uint32_t *__restrict__ list, 
                                              const uint32_t *__restrict__ passes, const FrameDesc *__restrict__ frames,
                                              const int16_t *__restrict__ resid, const uint32_t *__restrict__ ptab, int dbg)
 {
-    __shared__ PredLds<PIX, G> S;
+    __shared__ PredLds<PIX, G, true> S;
 #if PRED_LTAB_LDS
     load_ltab<PIX>(S.ltab, ptab, threadIdx.x);
 #endif
-    pred_wg<PIX, G>(wgs + list[blockIdx.x], sbs, jobs, passes, frames, resid, ptab, S, threadIdx.x, dbg);
+    pred_wg<PIX, G, true>(wgs + list[blockIdx.x], sbs, jobs, passes, frames, resid, ptab, S, threadIdx.x, dbg);
 }
 
 // LF tile geometry. A tile row starts XL pixels left of the SB (16 at 8-bit, 8 at 16-bit,
@@ -2360,18 +2402,20 @@ __global__ __launch_bounds__(LfNT<G>::NT) void k_plf(PlfLaunch a, const uint32_t
     typedef typename RT<PIX>::M M;
     typedef typename RT<PIX>::C COEF;
     constexpr int NW = LfNT<G>::NT / 64;
-    __shared__ union PlfLds { PredLds<PIX, G> p; LfLds<PIX, G> l; COEF r[NW][RWave<32, COEF>::E]; } S;
+    __shared__ union PlfLds { PredLds<PIX, G, false> p; LfLds<PIX, G> l; COEF r[NW][RWave<32, COEF>::E]; } S;
     const int b = blockIdx.x;
     if (b < (int) a.npred) {
         if (threadIdx.x >= 64) return;
 #if PRED_LTAB_LDS
         load_ltab<PIX>(S.p.ltab, ptab, threadIdx.x);
 #endif
-        pred_wg<PIX, G>(wgs + plist[b], sbs, jobs, passes, frames, resid, ptab, S.p, threadIdx.x, dbg);
+        pred_wg<PIX, G, false>(wgs + plist[b], sbs, jobs, passes, frames, resid, ptab, S.p, threadIdx.x, dbg);
         return;
     }
     if (b < (int) (a.npred + a.nlf)) {
+        const uint64_t t0 = PRED_PROF ? clock64() : 0;
         lf_sb<PIX, G, LfNT<G>::NT>(recs[llist[b - a.npred]], frames, S.l, threadIdx.x, dbg >> 16);
+        if (PRED_PROF && threadIdx.x == 0) { atomicAdd(&pred_prof[13], clock64() - t0); atomicAdd(&pred_prof[14], 1ull); }
         return;
     }
     // residual workgroups: transform code k owns ceil(rn[k] / (NW * 64 / n)) of them

@@ -20,3 +20,6 @@ for b in range(4):
     c = max(v[9 + b], 1)
     print("  pass MAXN %-2d        %8.0f cycles / pass  (%.2f passes / workgroup)" % (4 << b, v[5 + b] / c, v[9 + b] / nwg),
           file=sys.stderr)
+c = max(v[14], 1)
+print("  k_plf LF workgroup   %8.0f cycles / SB  (%d SBs)" % (v[13] / c, v[14]), file=sys.stderr)
+print("  slowest intra wg     %8.0f cycles" % v[15], file=sys.stderr)
