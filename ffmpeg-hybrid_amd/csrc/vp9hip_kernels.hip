@@ -861,12 +861,15 @@ DEV void load_sb_tile(const FrameDesc &fd, int sbx, int sby, bool interior, int 
     if (interior) sb_interior<PIX, G, false>(fd, sbx, sby, lane, tile);
 }
 
-// One pass of N x N jobs: lane li of group grp predicts column li of its job.
 // One mixed pass: lane li of an n x n job predicts pixel column li (rows 0..n-1); the
 // row loop runs to the pass's largest n (MAXN, unrolled), rows >= n are masked.
-template <int MAXN, typename PIX, class G>
+// pf() issues the next passes' global prefetches: after this pass's own global loads, so
+// that waiting for those (vmcnt counts in issue order) never waits for the prefetches.
+typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+typedef __attribute__((address_space(1))) const uint32_t glb_u32;
+template <int MAXN, typename PIX, class G, class PF>
 DEV void pred_pass(uint32_t w, int lane, PIX *tile, uint16_t *eb, int bd, const PSet &ps, const uint32_t *ltab,
-                   const int16_t *__restrict__ resid, const uint32_t *__restrict__ ptab, int dbg)
+                   const int16_t *__restrict__ resid, const uint32_t *__restrict__ ptab, int dbg, PF &&pf)
 {
     const LaneMap m = lane_map(w, lane);
     PJob jb;
@@ -885,20 +888,23 @@ DEV void pred_pass(uint32_t w, int lane, PIX *tile, uint16_t *eb, int bd, const 
     // one chunk ahead, so at most two chunks are live
     constexpr int F0 = MAXN < 8 ? MAXN : 8;
     uint32_t f[F0];
-    // (a per-lane choice in mixed passes, so a flat pointer there; reading every job of a
-    // 16 / 32 pass from the global table instead measured slower: C3 k_plf 7.28 -> 7.36 ms)
-    const uint32_t *ftab = PRED_LTAB_LDS && (ts <= 1 || MAXN <= 8) ? ltab + slot * 80 + toff + li
-                                                                   : ptab + slot * PTAB_SLOT + toff + li;
+    // passes of 4x4 / 8x8 jobs read the LDS copy, passes with a 16 / 32 job the global table
+    // for every job (explicit address spaces: a per-lane choice between the two was a flat
+    // pointer, and a flat load's wait covers every outstanding load, the prefetches included)
+    lds_u32 *ftl = (lds_u32 *) (ltab + slot * 80 + toff + li);
+    glb_u32 *ftg = (glb_u32 *) (ptab + slot * PTAB_SLOT + toff + li);
+    auto fword = [&](int row) -> uint32_t { return PRED_LTAB_LDS && MAXN <= 8 ? ftl[row * n] : ftg[row * n]; };
 #pragma unroll
-    for (int y = 0; y < F0; y++) f[y] = ftab[(y < n ? y : 0) * n];
+    for (int y = 0; y < F0; y++) f[y] = fword(y < n ? y : 0);
     const uint32_t *rr = (const uint32_t *) (resid + (PJ_RES(jb) && ts >= 2 ? (size_t) jb.roff * 16 + li * n : 0));
     uint32_t fa[8], ra[4], fb[8], rb[4];
     if (MAXN > 8) {
 #pragma unroll
-        for (int y = 0; y < 8; y++) fa[y] = ftab[(8 + y < n ? 8 + y : 0) * n];
+        for (int y = 0; y < 8; y++) fa[y] = fword(8 + y < n ? 8 + y : 0);
 #pragma unroll
         for (int k = 0; k < 4; k++) ra[k] = rr[4 + k < n / 2 ? 4 + k : 0];
     }
+    pf();
 
     // edges (fills: vp9recon.c:103-210): every load hits a valid tile address, the
     // host-resolved availability selects between pixel and fill value (no branches)
@@ -944,7 +950,7 @@ DEV void pred_pass(uint32_t w, int lane, PIX *tile, uint16_t *eb, int bd, const 
             if (MAXN > 8 && (y & 7) == 0 && y >= 8 && y + 8 < MAXN) {   // prefetch the chunk after this one
                 uint32_t *fn = ((y >> 3) & 1) ? fb : fa, *rn = ((y >> 3) & 1) ? rb : ra;
 #pragma unroll
-                for (int k = 0; k < 8; k++) fn[k] = ftab[(y + 8 + k < n ? y + 8 + k : 0) * n];
+                for (int k = 0; k < 8; k++) fn[k] = fword(y + 8 + k < n ? y + 8 + k : 0);
 #pragma unroll
                 for (int k = 0; k < 4; k++) rn[k] = rr[(y + 8) / 2 + k < n / 2 ? (y + 8) / 2 + k : 0];
             }
@@ -963,15 +969,15 @@ DEV void pred_pass(uint32_t w, int lane, PIX *tile, uint16_t *eb, int bd, const 
     }
 }
 
-template <typename PIX, class G>
+template <typename PIX, class G, class PF>
 DEV void run_pass(uint32_t w, int lane, PIX *tile, uint16_t *eb, int bd, const PSet &ps, const uint32_t *ltab,
-                  const int16_t *__restrict__ resid, const uint32_t *__restrict__ ptab, int dbg)
+                  const int16_t *__restrict__ resid, const uint32_t *__restrict__ ptab, int dbg, PF &&pf)
 {
     switch (PASS_MAXN(w)) {
-    case 4: pred_pass<4, PIX, G>(w, lane, tile, eb, bd, ps, ltab, resid, ptab, dbg); break;
-    case 8: pred_pass<8, PIX, G>(w, lane, tile, eb, bd, ps, ltab, resid, ptab, dbg); break;
-    case 16: pred_pass<16, PIX, G>(w, lane, tile, eb, bd, ps, ltab, resid, ptab, dbg); break;
-    default: pred_pass<32, PIX, G>(w, lane, tile, eb, bd, ps, ltab, resid, ptab, dbg); break;
+    case 4: pred_pass<4, PIX, G>(w, lane, tile, eb, bd, ps, ltab, resid, ptab, dbg, pf); break;
+    case 8: pred_pass<8, PIX, G>(w, lane, tile, eb, bd, ps, ltab, resid, ptab, dbg, pf); break;
+    case 16: pred_pass<16, PIX, G>(w, lane, tile, eb, bd, ps, ltab, resid, ptab, dbg, pf); break;
+    default: pred_pass<32, PIX, G>(w, lane, tile, eb, bd, ps, ltab, resid, ptab, dbg, pf); break;
     }
     wave_sync();
 }
@@ -1089,21 +1095,23 @@ DEV void pred_wg(const WGRec *wgp, const SBRec *__restrict__ sbs, const PJob *__
         load_resid(J, resid, A);
         load_job(LPW(1), lane, lj, J);
         for (int pi = 0; pi < npass; pi += 2) {
-            const uint32_t w0 = LPW(pi), w1 = LPW(pi + 1);
-            load_resid(J, resid, B);
-            load_job(LPW(pi + 2), lane, lj, J);
+            const uint32_t w0 = LPW(pi), w1 = LPW(pi + 1), w2 = LPW(pi + 2), w3 = LPW(pi + 3);
             uint64_t tq = PRED_PROF ? clock64() : 0;
-            run_pass<PIX, G>(w0, lane, tile, eb, bd, A, ltab, resid, ptab, dbg);
+            run_pass<PIX, G>(w0, lane, tile, eb, bd, A, ltab, resid, ptab, dbg, [&] {
+                load_resid(J, resid, B);
+                load_job(w2, lane, lj, J);
+            });
             if (PRED_PROF) {
                 const uint64_t t = clock64();
                 const int b = PASS_MAXN(w0) == 4 ? 0 : PASS_MAXN(w0) == 8 ? 1 : PASS_MAXN(w0) == 16 ? 2 : 3;
                 pp[5 + b] += t - tq; pp[9 + b]++; tq = t;
             }
             if (pi + 1 >= npass) break;
-            load_resid(J, resid, A);
-            load_job(LPW(pi + 3), lane, lj, J);
             if (PRED_PROF) tq = clock64();
-            run_pass<PIX, G>(w1, lane, tile, eb, bd, B, ltab, resid, ptab, dbg);
+            run_pass<PIX, G>(w1, lane, tile, eb, bd, B, ltab, resid, ptab, dbg, [&] {
+                load_resid(J, resid, A);
+                load_job(w3, lane, lj, J);
+            });
             if (PRED_PROF) {
                 const uint64_t t = clock64();
                 const int b = PASS_MAXN(w1) == 4 ? 0 : PASS_MAXN(w1) == 8 ? 1 : PASS_MAXN(w1) == 16 ? 2 : 3;
@@ -2385,6 +2393,15 @@ template <typename PIX> struct RT;
 template <> struct RT<uint8_t> { typedef M32 M; typedef int16_t C; };
 template <> struct RT<uint16_t> { typedef M64 M; typedef int32_t C; };
 
+// PRED_PROF builds: a workgroup timeline of k_plf launches of one shape: per workgroup its
+// start / end on the device real-time clock (s_memrealtime, 100 MHz) | kind << 62 (0 intra,
+// 1 LF, 2 residual), for the launches whose npred equals that of the first launch seen with
+// npred >= PLF_TL_MIN (tools/pred_prof.py --timeline)
+#define PLF_TL_N 65536
+#define PLF_TL_MIN 2000
+KP_DEV unsigned long long plf_tl[PLF_TL_N][2];
+KP_DEV unsigned int plf_tl_n, plf_tl_key;
+
 // Fused wavefront launch (runtime schedule, stage()): launch t holds intra diagonal t, LF
 // diagonal t - 3 (disjoint pixels) and the residuals of intra diagonal t + 1.
 // Workgroups [0, npred) predict one SB each with wave 0 (the other waves exit), the next
@@ -2404,18 +2421,33 @@ __global__ __launch_bounds__(LfNT<G>::NT) void k_plf(PlfLaunch a, const uint32_t
     constexpr int NW = LfNT<G>::NT / 64;
     __shared__ union PlfLds { PredLds<PIX, G, false> p; LfLds<PIX, G> l; COEF r[NW][RWave<32, COEF>::E]; } S;
     const int b = blockIdx.x;
+    bool tl_rec = false;
+    uint64_t tl_t0 = 0;
+    if (PRED_PROF && threadIdx.x == 0 && a.npred >= PLF_TL_MIN) {
+        const uint32_t k = atomicCAS(&plf_tl_key, 0u, a.npred);
+        tl_rec = k == 0 || k == a.npred;
+        tl_t0 = __builtin_amdgcn_s_memrealtime();
+    }
+    auto tl_end = [&](uint64_t kind) {
+        if (PRED_PROF && tl_rec) {
+            const uint32_t i = atomicAdd(&plf_tl_n, 1u);
+            if (i < PLF_TL_N) { plf_tl[i][0] = tl_t0 | kind << 62; plf_tl[i][1] = __builtin_amdgcn_s_memrealtime(); }
+        }
+    };
     if (b < (int) a.npred) {
         if (threadIdx.x >= 64) return;
 #if PRED_LTAB_LDS
         load_ltab<PIX>(S.p.ltab, ptab, threadIdx.x);
 #endif
         pred_wg<PIX, G, false>(wgs + plist[b], sbs, jobs, passes, frames, resid, ptab, S.p, threadIdx.x, dbg);
+        tl_end(0);
         return;
     }
     if (b < (int) (a.npred + a.nlf)) {
         const uint64_t t0 = PRED_PROF ? clock64() : 0;
         lf_sb<PIX, G, LfNT<G>::NT>(recs[llist[b - a.npred]], frames, S.l, threadIdx.x, dbg >> 16);
         if (PRED_PROF && threadIdx.x == 0) { atomicAdd(&pred_prof[13], clock64() - t0); atomicAdd(&pred_prof[14], 1ull); }
+        tl_end(1);
         return;
     }
     // residual workgroups: transform code k owns ceil(rn[k] / (NW * 64 / n)) of them
@@ -2428,6 +2460,7 @@ __global__ __launch_bounds__(LfNT<G>::NT) void k_plf(PlfLaunch a, const uint32_t
         if (rb < nwg) {                                                                                     \
             resid_wave<N, TC, PIX, M, COEF>(rjobs + a.roff[K], a.rn[K], rb * NW + wave, lane, frames, cf,    \
                                             resid, S.r[wave]);                                              \
+            tl_end(2);                                                                                      \
             return;                                                                                         \
         }                                                                                                   \
         rb -= nwg;                                                                                          \
@@ -2964,6 +2997,17 @@ int vp9hip_pred_prof_read(unsigned long long *out)
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(pred_prof), 16 * sizeof(unsigned long long)) != hipSuccess) return -1;
     static const unsigned long long z[16] = {0};
     return hipMemcpyToSymbol(HIP_SYMBOL(pred_prof), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+// PRED_PROF builds: the k_plf workgroup timeline (n = entries, then 2 words each; profiling
+// only, not in the ABI), cleared after the read
+int vp9hip_plf_tl_read(unsigned long long *out, int cap, int *n)
+{
+    unsigned int k = 0;
+    if (hipMemcpyFromSymbol(&k, HIP_SYMBOL(plf_tl_n), 4) != hipSuccess) return -1;
+    *n = (int) std::min<unsigned int>(k, PLF_TL_N);
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(plf_tl), (size_t) std::min(*n, cap) * 16) != hipSuccess) return -1;
+    const unsigned int z = 0;
+    return hipMemcpyToSymbol(HIP_SYMBOL(plf_tl_n), &z, 4) == hipSuccess && hipMemcpyToSymbol(HIP_SYMBOL(plf_tl_key), &z, 4) == hipSuccess ? 0 : -1;
 }
 // LFR_PROF builds: read and clear the row-LF phase sums (profiling only, not in the ABI)
 // LFR_PROF builds: the k_lfro event timeline (24 x 8 shader-clock values; profiling only)
