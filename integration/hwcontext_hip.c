@@ -17,8 +17,11 @@
  * Modelled on the shape of hwcontext_cuda.c (a pitched device pool, 2-D copies on the device
  * context's stream); HIP is linked directly (libamdhip64), there is no dynamic loader.
  *
- * Not compiled in this repository (it needs an FFmpeg tree; INTEGRATION.md lists the
+ * Not built into a library here (it needs an FFmpeg tree; INTEGRATION.md lists the
  * registration lines: hwcontext.c tables, pixfmt.h / pixdesc.c entries, Makefile).
+ * tests/test_glue_typecheck.py type-checks it (gcc -fsyntax-only -Wall -Werror) against the
+ * FFmpeg 8.0 declarations it binds, restated in tests/glue/ffmpeg_decls.h and pinned line by
+ * line to the reference headers.
  */
 #include <stdlib.h>
 #include <string.h>

@@ -22,7 +22,10 @@
  * HWACCEL_HIP(vp9)), AV_PIX_FMT_HIP in update_size's offer list (vp9.c:168-266), and
  * libavcodec/Makefile: OBJS-$(CONFIG_VP9_HIP_HWACCEL) += vp9_hip.o, -lvp9hip.
  *
- * Not compiled in this repository (it needs an FFmpeg tree).
+ * Not built into a library here (it needs an FFmpeg tree).
+ * tests/test_glue_typecheck.py type-checks it (gcc -fsyntax-only -Wall -Werror) against the
+ * FFmpeg 8.0 declarations it binds, restated in tests/glue/ffmpeg_decls.h and pinned line by
+ * line to the reference headers.
  */
 #include "libavutil/hwcontext.h"
 #include "libavutil/hwcontext_hip.h"

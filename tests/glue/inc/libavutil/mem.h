@@ -1,0 +1,2 @@
+/* TEST INFRASTRUCTURE: shim for libavutil/mem.h (tests/glue/ffmpeg_decls.h restates what the glue binds) */
+#include "ffmpeg_decls.h"
