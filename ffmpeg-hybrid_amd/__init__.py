@@ -67,6 +67,27 @@ class FramePacket(ctypes.Structure):
                 ("coefs", ctypes.c_void_p)]
 
 
+class SegParams(ctypes.Structure):
+    """vp9h_seg_params: segmentation and LF deltas in effect for a frame."""
+    _fields_ = [("enabled", ctypes.c_int32), ("update_map", ctypes.c_int32), ("temporal", ctypes.c_int32),
+                ("update_data", ctypes.c_int32), ("abs_delta", ctypes.c_int32), ("q_en", ctypes.c_int32),
+                ("lf_en", ctypes.c_int32), ("q", ctypes.c_int32 * 8), ("lf", ctypes.c_int32 * 8),
+                ("nseg", ctypes.c_int32), ("lf_delta_update", ctypes.c_int32), ("lf_ref", ctypes.c_int32 * 4),
+                ("lf_mode", ctypes.c_int32 * 2)]
+
+
+def seg_params(**kw):
+    """A SegParams from keyword fields (lists for q / lf / lf_ref / lf_mode)."""
+    p = SegParams()
+    for k, v in kw.items():
+        if not hasattr(p, k):
+            raise KeyError(k)
+        if k in ("q", "lf", "lf_ref", "lf_mode"):
+            v = (ctypes.c_int32 * {"q": 8, "lf": 8, "lf_ref": 4, "lf_mode": 2}[k])(*v)
+        setattr(p, k, v)
+    return p
+
+
 class SynthParams(ctypes.Structure):
     """vp9h_synth_params."""
     _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32), ("bpp", ctypes.c_int32),
@@ -75,7 +96,7 @@ class SynthParams(ctypes.Structure):
                 ("lossless", ctypes.c_int32), ("filter_level", ctypes.c_int32),
                 ("sharpness", ctypes.c_int32), ("bilinear", ctypes.c_int32),
                 ("coef_stress", ctypes.c_int32), ("p_zero_eob", ctypes.c_float),
-                ("p_skip", ctypes.c_float), ("seed", ctypes.c_uint64)]
+                ("p_skip", ctypes.c_float), ("seed", ctypes.c_uint64), ("seg", SegParams)]
 
 
 class FrameInfo(ctypes.Structure):
@@ -97,7 +118,7 @@ class EncParams(ctypes.Structure):
                 ("sign_bias", ctypes.c_int32 * 3), ("refresh_ctx", ctypes.c_int32), ("parallel", ctypes.c_int32),
                 ("ctx_id", ctypes.c_int32), ("reset_ctx", ctypes.c_int32), ("allow_hp", ctypes.c_int32),
                 ("interp", ctypes.c_int32), ("comp_mode", ctypes.c_int32), ("tx_mode", ctypes.c_int32),
-                ("prob_updates", ctypes.c_int32), ("keep_modes", ctypes.c_int32)]
+                ("prob_updates", ctypes.c_int32), ("keep_modes", ctypes.c_int32), ("seg", SegParams)]
 
 
 _lib_handle = None
@@ -277,6 +298,8 @@ def synth_params(width, height, bpp=8, **kw):
     for k, v in kw.items():
         if not hasattr(p, k):
             raise KeyError(k)
+        if k == "seg" and isinstance(v, dict):
+            v = seg_params(**v)
         setattr(p, k, v)
     return p
 
@@ -353,6 +376,8 @@ def enc_params(**kw):
             raise KeyError(k)
         if k in ("ref_slot", "sign_bias"):
             v = (ctypes.c_int32 * 3)(*v)
+        if k == "seg" and isinstance(v, dict):
+            v = seg_params(**v)
         setattr(p, k, v)
     return p
 

@@ -458,6 +458,7 @@ typedef struct Walk {
     uint32_t bi, ei;  uint64_t ci;
     uint64_t rng;
     int prob_updates, keep_modes;
+    const vp9h_seg_params *eseg;         /* segment features / LF deltas to write */
     int last_keyframe, last_invisible;   /* the previous frame's header flags */
     Hdr hs;                              /* pipelined parse: the header as of this frame */
     int32_t ref_w[3], ref_h[3];          /* reference sizes at this frame's header */
@@ -1698,9 +1699,14 @@ static long walk_uncompressed(Walk *w, Bits *b, int *existing)
     h->filter_level = bits_rw(b, 6, h->filter_level);
     h->sharpness = bits_rw(b, 3, h->sharpness);
     if ((h->lf_delta_enabled = bits_rw(b, 1, h->lf_delta_enabled))) {
-        if (bits_rw(b, 1, 0)) {                                  /* delta update (encoder: none) */
-            for (int i = 0; i < 4; i++) if (bits_rw(b, 1, 0)) h->lf_ref[i] = bits_sinv(b, 6, 0);
-            for (int i = 0; i < 2; i++) if (bits_rw(b, 1, 0)) h->lf_mode[i] = bits_sinv(b, 6, 0);
+        /* delta update (vp9.c:692-702); the encoder codes the values in effect that differ */
+        const vp9h_seg_params *e = b->enc ? w->eseg : NULL;
+        const int upd = e && e->lf_delta_update;
+        if (bits_rw(b, 1, upd)) {
+            for (int i = 0; i < 4; i++)
+                if (bits_rw(b, 1, upd && e->lf_ref[i] != h->lf_ref[i])) h->lf_ref[i] = bits_sinv(b, 6, upd ? e->lf_ref[i] : 0);
+            for (int i = 0; i < 2; i++)
+                if (bits_rw(b, 1, upd && e->lf_mode[i] != h->lf_mode[i])) h->lf_mode[i] = bits_sinv(b, 6, upd ? e->lf_mode[i] : 0);
         }
     }
     h->qidx = bits_rw(b, 8, h->qidx);
@@ -1717,6 +1723,15 @@ static long walk_uncompressed(Walk *w, Bits *b, int *existing)
                     h->seg_pred[i] = (uint8_t) (bits_rw(b, 1, h->seg_pred[i] != 255) ? bits_rw(b, 8, h->seg_pred[i]) : 255);
         }
         if ((h->seg_update_data = bits_rw(b, 1, h->seg_update_data))) {
+            if (b->enc && w->eseg)                               /* the features to write */
+                for (int i = 0; i < 8; i++) {
+                    SegFeat *f = &h->seg[i];
+                    memset(f, 0, sizeof(*f));
+                    f->q_en = (w->eseg->q_en >> i) & 1;
+                    f->q = f->q_en ? w->eseg->q[i] : 0;
+                    f->lf_en = (w->eseg->lf_en >> i) & 1;
+                    f->lf = f->lf_en ? w->eseg->lf[i] : 0;
+                }
             h->seg_abs = bits_rw(b, 1, h->seg_abs);
             for (int i = 0; i < 8; i++) {
                 SegFeat *f = &h->seg[i];
@@ -2544,7 +2559,14 @@ int vp9h_stream_encode(vp9h_stream *st, const vp9h_frame *pkt, const vp9h_enc_pa
     h->filter_level = pkt->filter_level; h->sharpness = pkt->sharpness;
     h->qidx = pkt->lossless ? 0 : ep->base_q_idx;
     h->ydc = h->uvdc = h->uvac = 0;
-    h->seg_enabled = 0;
+    /* segmentation (vp9.c:707-765): the map's tree / prediction probabilities are coded as 128 */
+    h->seg_enabled = !!ep->seg.enabled;
+    h->seg_update_map = h->seg_enabled && (ep->seg.update_map || h->keyframe || h->intraonly);
+    h->seg_temporal = h->seg_update_map && ep->seg.temporal && inter;
+    h->seg_update_data = h->seg_enabled && ep->seg.update_data;
+    h->seg_abs = !!ep->seg.abs_delta;
+    for (int i = 0; i < 7; i++) h->seg_prob[i] = 128;
+    for (int i = 0; i < 3; i++) h->seg_pred[i] = 128;
     h->log2_tile_cols = pkt->log2_tile_cols; h->log2_tile_rows = pkt->log2_tile_rows;
     h->txmode = pkt->lossless ? 0 : ep->tx_mode >= 0 ? ep->tx_mode : TX_SEL;
     if (inter) {
@@ -2576,6 +2598,7 @@ int vp9h_stream_encode(vp9h_stream *st, const vp9h_frame *pkt, const vp9h_enc_pa
     if (!w) return VP9HIP_ENOMEM;
     w->st = st; w->h = h; w->in = pkt;
     w->prob_updates = ep->prob_updates;
+    w->eseg = &ep->seg;
     w->keep_modes = ep->keep_modes;
     w->rng = (uint64_t) ep->prob_updates * 0x2545F4914F6CDD1Dull;
     w->last_keyframe = last_keyframe;

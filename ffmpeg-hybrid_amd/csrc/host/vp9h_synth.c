@@ -8,7 +8,9 @@
  * (vp9.c:1325-1395); transform-size limits follow decode_mode (vp9block.c:88-91,
  * 171-215, 1291-1292); dequantization follows decode_coeffs_b_generic
  * (vp9block.c:905-917) with the qlookup tables (vp9.c:745-766); LF levels follow
- * vp9.c:767-791 with libvpx's default ref/mode deltas (vp9.c:659-668).
+ * vp9.c:767-791 with libvpx's default ref/mode deltas (vp9.c:659-668) or the given ones;
+ * with segmentation (p->seg) the blocks draw segment ids, each segment with its alternate q
+ * (the coefficients are multiples of that segment's step) and LF level.
  */
 #include <stdlib.h>
 #include <string.h>
@@ -33,7 +35,8 @@ typedef struct Gen {
     const vp9h_synth_params *p;
     Rng rng;
     int cols, rows, sb_cols, sb_rows;
-    int qmul[2][2];              /* [y/uv][dc/ac] */
+    int qmul[8][2][2];           /* [segment][y/uv][dc/ac] */
+    int seg;                     /* the segment of the block being generated */
     /* growable outputs */
     vp9h_block *blocks; size_t nb, cb;
     uint16_t *eobs; size_t ne, ce;
@@ -84,7 +87,7 @@ static void gen_txb(Gen *g, int tx, int uv)
             v = (i + 1 < eob && rng_f(&g->rng) < 0.3) ? 0 : coef_mag(g);
         }
         if (rng_u64(&g->rng) & 1) v = -v;
-        int q = g->qmul[uv][i > 0];
+        int q = g->qmul[g->seg][uv][i > 0];
         int32_t stored;
         if (tx == 3)
             stored = (int32_t) ((int) ((unsigned) v * (unsigned) q) / 2);   /* vp9block.c:915 */
@@ -111,6 +114,8 @@ static void gen_block(Gen *g, int row, int col, int bl, int bp)
 
     memset(&b, 0, sizeof(b));
     b.row = row; b.col = col; b.bs = bs;
+    if (p->seg.enabled && p->seg.nseg > 1) b.seg_id = (uint8_t) rng_int(&g->rng, MIN(8, p->seg.nseg));
+    g->seg = b.seg_id;
     b.intra = !p->inter || rng_f(&g->rng) < 0.1;
     b.skip = rng_f(&g->rng) < p->p_skip;
     b.tx = p->lossless ? 0 : rng_int(&g->rng, max_tx_for_bs[bs] + 1);
@@ -247,12 +252,15 @@ int vp9hip_synth_frame(vp9h_frame *out, const vp9h_synth_params *p)
     g.rows = (p->height + 7) >> 3;
     g.sb_cols = (p->width + 63) >> 6;
     g.sb_rows = (p->height + 63) >> 6;
-    {
+    /* per-segment dequantization (vp9.c:745-766): the alternate-q feature of segment s */
+    for (s = 0; s < 8; s++) {
         int q = p->lossless ? 0 : p->q_idx;
-        g.qmul[0][0] = vp9t_dc_q[bidx][q];
-        g.qmul[0][1] = vp9t_ac_q[bidx][q];
-        g.qmul[1][0] = vp9t_dc_q[bidx][q];
-        g.qmul[1][1] = vp9t_ac_q[bidx][q];
+        if (p->seg.enabled && ((p->seg.q_en >> s) & 1)) q = p->seg.abs_delta ? p->seg.q[s] : q + p->seg.q[s];
+        q = q < 0 ? 0 : q > 255 ? 255 : q;
+        g.qmul[s][0][0] = vp9t_dc_q[bidx][q];
+        g.qmul[s][0][1] = vp9t_ac_q[bidx][q];
+        g.qmul[s][1][0] = vp9t_dc_q[bidx][q];
+        g.qmul[s][1][1] = vp9t_ac_q[bidx][q];
     }
     /* legal tile-column range (vp9.c:800-810) */
     {
@@ -284,14 +292,21 @@ int vp9hip_synth_frame(vp9h_frame *out, const vp9h_synth_params *p)
     out->filter_level = p->lossless ? 0 : p->filter_level;
     out->sharpness = p->sharpness;
     out->log2_tile_cols = p->log2_tile_cols;
-    /* lflvl with lf_delta enabled at the defaults ref {1,0,-1,-1}, mode {0,0} */
+    /* lflvl (vp9.c:767-791): the segment's alternate LF level, then the ref / mode deltas
+     * in effect (libvpx's defaults ref {1,0,-1,-1}, mode {0,0} unless given) */
     {
-        static const int ref_delta[4] = { 1, 0, -1, -1 };
-        int lvl = out->filter_level, sh = lvl >= 32;
+        static const int ref_def[4] = { 1, 0, -1, -1 }, mode_def[2] = { 0, 0 };
+        const int *ref_delta = p->seg.lf_delta_update ? p->seg.lf_ref : ref_def;
+        const int *mode_delta = p->seg.lf_delta_update ? p->seg.lf_mode : mode_def;
+        const int sh = out->filter_level >= 32;
         for (s = 0; s < 8; s++) {
+            int lvl = out->filter_level;
+            if (p->seg.enabled && ((p->seg.lf_en >> s) & 1)) lvl = p->seg.abs_delta ? p->seg.lf[s] : lvl + p->seg.lf[s];
+            lvl = clip_u6(lvl);
             out->lflvl[s][0][0] = out->lflvl[s][0][1] = clip_u6(lvl + ref_delta[0] * (1 << sh));
             for (i = 1; i < 4; i++)
-                out->lflvl[s][i][0] = out->lflvl[s][i][1] = clip_u6(lvl + ref_delta[i] * (1 << sh));
+                for (int m = 0; m < 2; m++)
+                    out->lflvl[s][i][m] = clip_u6(lvl + (ref_delta[i] + mode_delta[m]) * (1 << sh));
         }
     }
     for (i = 0; i < 3; i++) { out->ref_w[i] = p->width; out->ref_h[i] = p->height; }

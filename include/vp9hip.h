@@ -270,6 +270,25 @@ int  vp9hip_device_info(int device, char *pci_bus_id, int len, char *name, int n
  * defaults. inter != 0: LAST-ref inter frame (50 % NEWMV, MVs uniform in +-64 px,
  * 10 % intra blocks). The packet owns heap arrays; release with vp9hip_synth_free.
  */
+/* Segmentation and loop-filter deltas of a frame (vp9.c:692-765, vp9block.c:101-141): what
+ * vp9h_stream_encode writes into the frame header, and what vp9hip_synth_frame assumes for
+ * the packet's segment ids, per-segment dequantization and LF levels. Values are the ones in
+ * effect for the frame (the encoder codes the LF deltas that differ from the stream's, and
+ * the segment features when update_data). All zero: no segmentation, libvpx's default LF
+ * deltas (ref 1, 0, -1, -1; mode 0, 0) unchanged. */
+typedef struct vp9h_seg_params {
+    int32_t enabled;               /* segmentation_enabled                                  */
+    int32_t update_map;            /* code the blocks' segment ids (else the map is kept)   */
+    int32_t temporal;              /* inter frames: ids predicted from the previous map     */
+    int32_t update_data;           /* code the per-segment features                         */
+    int32_t abs_delta;             /* feature values absolute (else deltas to the frame's)  */
+    int32_t q_en, lf_en;           /* bit s: segment s has the alternate q / LF feature     */
+    int32_t q[8], lf[8];
+    int32_t nseg;                  /* synth: segment ids drawn from 0 .. nseg - 1           */
+    int32_t lf_delta_update;       /* lf_ref / lf_mode below are in effect (else defaults)  */
+    int32_t lf_ref[4], lf_mode[2];
+} vp9h_seg_params;
+
 typedef struct vp9h_synth_params {
     int32_t  width, height;
     int32_t  bpp;              /* 8 / 10 / 12                                   */
@@ -286,6 +305,7 @@ typedef struct vp9h_synth_params {
     float    p_zero_eob;       /* chance that a tx block codes eob 0            */
     float    p_skip;           /* default 0.2                                   */
     uint64_t seed;
+    vp9h_seg_params seg;       /* segmentation / LF deltas (default: none)      */
 } vp9h_synth_params;
 
 /* Fill p with the §8(d) defaults for a w x h bpp stream. */
@@ -382,6 +402,7 @@ typedef struct vp9h_enc_params {
     int32_t prob_updates;          /* 0: none; else the seed of random forward updates      */
     int32_t keep_modes;            /* 1: code the packet's inter modes, taking the MVs they  */
                                    /*    predict (NEAREST / NEAR / ZERO); 0: keep the MVs    */
+    vp9h_seg_params seg;           /* segmentation / LF deltas to code (default: none)      */
 } vp9h_enc_params;
 void vp9h_enc_defaults(vp9h_enc_params *p);
 

@@ -78,6 +78,59 @@ static std::vector<Bytes> make_stream(const Cfg &c, uint64_t seed)
     return out;
 }
 
+// segmentation stream (the advisor's round-4 use-after-free): key with a coded map, an inter
+// frame with its own map, two keeping it, then a hidden intra-only frame (its headers drop
+// the kept map while the previous frame's tiles may still walk, frame-pipelined), an inter
+// frame on it, an error-resilient frame, one updating the map. Without the counted segref
+// reference ASan reports the use-after-free here (3 of 3 runs).
+static std::vector<Bytes> make_seg_stream(int w, int h, int log2tc, uint64_t seed)
+{
+    std::vector<Bytes> out;
+    vp9h_stream *enc = nullptr;
+    if (vp9h_stream_open(&enc) < 0) return out;
+    vp9h_seg_params sg;
+    memset(&sg, 0, sizeof(sg));
+    sg.enabled = 1; sg.update_map = 1; sg.update_data = 1; sg.nseg = 4;
+    sg.q_en = 0x6; sg.q[1] = 8; sg.q[2] = -12;
+    sg.lf_en = 0xb; sg.lf[0] = 3; sg.lf[2] = -5; sg.lf[3] = 10;
+    sg.lf_delta_update = 1; sg.lf_ref[0] = 2; sg.lf_ref[2] = -2; sg.lf_ref[3] = -1; sg.lf_mode[0] = 1; sg.lf_mode[1] = -1;
+    struct F { int inter, intraonly, update_map, temporal, q_en, errres, refresh, ref; };
+    // (a frame keeps the map only after a frame that did not update it: frame 3 reads frame
+    // 1's map through its own reference while frame 4's headers drop the stream's)
+    static const F fs[] = { { 0, 0, 1, 0, 0x6, 0, 0xff, 0 }, { 1, 0, 1, 1, 0x6, 0, 2, 0 }, { 1, 0, 0, 0, 0, 0, 4, 1 },
+                            { 1, 0, 0, 0, 0, 0, 8, 2 }, { 0, 1, 1, 0, 0x6, 0, 16, 0 }, { 1, 0, 0, 0, 0, 0, 32, 4 },
+                            { 1, 0, 1, 0, 0x6, 1, 64, 5 }, { 1, 0, 1, 1, 0x6, 0, 128, 6 } };
+    for (size_t i = 0; i < sizeof(fs) / sizeof(fs[0]); i++) {
+        vp9h_synth_params sp;
+        vp9hip_synth_defaults(&sp, w, h, 8);
+        sp.log2_tile_cols = log2tc;
+        sp.inter = fs[i].inter;
+        sp.seed = seed + i;
+        sp.seg = sg;
+        sp.seg.update_map = fs[i].update_map; sp.seg.temporal = fs[i].temporal; sp.seg.q_en = fs[i].q_en;
+        vp9h_frame f;
+        memset(&f, 0, sizeof(f));
+        if (vp9hip_synth_frame(&f, &sp) < 0) break;
+        if (fs[i].intraonly) { f.keyframe = 0; f.intraonly = 1; }
+        vp9h_enc_params ep;
+        vp9h_enc_defaults(&ep);
+        ep.seg = sp.seg;
+        ep.refresh_mask = fs[i].refresh;
+        ep.error_res = fs[i].errres;
+        if (fs[i].intraonly) ep.show_frame = 0;
+        for (int k = 0; k < 3; k++) ep.ref_slot[k] = fs[i].ref;
+        uint8_t *buf = nullptr;
+        size_t sz = 0;
+        const int r = vp9h_stream_encode(enc, &f, &ep, &buf, &sz, nullptr);
+        vp9hip_synth_free(&f);
+        if (r < 0) { fprintf(stderr, "seg stream frame %zu: encode %d\n", i, r); break; }
+        out.push_back(Bytes(buf, buf + sz));
+        vp9h_buffer_free(buf);
+    }
+    vp9h_stream_close(enc);
+    return out;
+}
+
 static bool same_packet(const vp9h_frame &a, const vp9h_frame &b)
 {
     if (a.width != b.width || a.height != b.height || a.bpp != b.bpp || a.nblocks != b.nblocks || a.neobs != b.neobs ||
@@ -174,6 +227,23 @@ static void check_streams(int nmut)
                       i, t);
             free_all(pip);
         }
+        free_all(ser);
+        streams.push_back(std::move(s));
+    }
+    // segmentation streams: a kept map read by a frame whose successor's headers drop it
+    for (int tc = 0; tc < 2; tc++) {
+        std::vector<Bytes> s = make_seg_stream(tc ? 704 : 352, 288, tc, 5000u + (uint64_t) tc * 17u);
+        CHECK(s.size() == 8, "seg stream: %zu of 8 frames", s.size());
+        std::vector<vp9h_frame> ser;
+        CHECK(parse_stream(s, 1, &ser) == 0, "seg stream serial parse");
+        for (int rep = 0; rep < 8; rep++)
+            for (int t : { 1, 2 }) {
+                std::vector<vp9h_frame> pip;
+                CHECK(parse_pipelined(s, t, &pip) == 0, "seg stream pipelined parse (%d)", t);
+                for (size_t i = 0; i < ser.size() && i < pip.size(); i++)
+                    CHECK(same_packet(ser[i], pip[i]), "seg stream frame %zu: pipelined (%d) != serial", i, t);
+                free_all(pip);
+            }
         free_all(ser);
         streams.push_back(std::move(s));
     }

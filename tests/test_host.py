@@ -28,7 +28,10 @@ def test_library_exports_every_declared_symbol(v9, header):
 def test_struct_layouts_match_header(v9):
     # vp9h_block is 52 bytes (include/vp9hip.h); the Python mirror must agree
     assert ctypes.sizeof(v9.Block) == 52
-    assert ctypes.sizeof(v9.SynthParams) == 72
+    assert ctypes.sizeof(v9.SegParams) == 124             # 31 int32
+    assert ctypes.sizeof(v9.SynthParams) == 200           # 72 + vp9h_seg_params + padding to the uint64 alignment
+    assert ctypes.sizeof(v9.EncParams) == 88 + 124          # 22 int32 + vp9h_seg_params
+    assert v9.SynthParams.seg.offset == 72 and v9.EncParams.seg.offset == 88
 
 
 def test_no_device_is_an_error_not_a_fallback(v9):
