@@ -1087,15 +1087,23 @@ DEV void pred_wg(const WGRec *wgp, const SBRec *__restrict__ sbs, const PJob *__
     // passes: residual sets A / B alternate (loop unrolled by two), job records J run a
     // pass ahead of them; pass words are wave-uniform scalar loads (index clamped)
     const int npass = (dbg & 1) ? 0 : wnpass;
-#define LPW(k) __builtin_amdgcn_readfirstlane(lp[(k) < npass ? (k) : npass - 1])
+    // pass words: wave-uniform; from the global list through the constant address space, so
+    // they are scalar loads (a vector load of a uniform address was waited on at once)
+    typedef __attribute__((address_space(4))) const uint32_t cst_u32;
+    const cst_u32 *lpc = (const cst_u32 *) gp;
+#define LPW(k) (PL::ON ? __builtin_amdgcn_readfirstlane(lp[(k) < npass ? (k) : npass - 1]) \
+                       : lpc[(k) < npass ? (k) : npass - 1])
     if (npass) {
         PSet A, B;
         JSet J;
-        load_job(LPW(0), lane, lj, J);
+        // pass words one iteration ahead: this iteration's pair was read by the previous
+        // one, the next pair (needed by this iteration's prefetches only) is read here
+        uint32_t w0 = LPW(0), w1 = LPW(1);
+        load_job(w0, lane, lj, J);
         load_resid(J, resid, A);
-        load_job(LPW(1), lane, lj, J);
+        load_job(w1, lane, lj, J);
         for (int pi = 0; pi < npass; pi += 2) {
-            const uint32_t w0 = LPW(pi), w1 = LPW(pi + 1), w2 = LPW(pi + 2), w3 = LPW(pi + 3);
+            const uint32_t w2 = LPW(pi + 2), w3 = LPW(pi + 3);
             uint64_t tq = PRED_PROF ? clock64() : 0;
             run_pass<PIX, G>(w0, lane, tile, eb, bd, A, ltab, resid, ptab, dbg, [&] {
                 load_resid(J, resid, B);
@@ -1117,6 +1125,8 @@ DEV void pred_wg(const WGRec *wgp, const SBRec *__restrict__ sbs, const PJob *__
                 const int b = PASS_MAXN(w1) == 4 ? 0 : PASS_MAXN(w1) == 8 ? 1 : PASS_MAXN(w1) == 16 ? 2 : 3;
                 pp[5 + b] += t - tq; pp[9 + b]++;
             }
+            w0 = w2;
+            w1 = w3;
         }
     }
 #undef LPW
