@@ -41,7 +41,7 @@ W, H, BPP, LOG2_TILE_COLS = 3840, 2160, 8, 2
 CONFIG_INDEX = 2               # C3
 CHROMA = {"420": (1, 1), "422": (1, 0), "440": (0, 1), "444": (0, 0)}   # (ss_h, ss_v)
 SEED0 = 0x56503900 + CONFIG_INDEX
-TRAFFIC_PROFILE = "r04t"       # rocprofv3 PMC passes of the default C3 bench (tools/profile.sh)
+TRAFFIC_PROFILE = "r05h/C3"      # rocprofv3 PMC passes of the default C3 bench (tools/profile.sh)
 POISON = 0xA5                  # fill byte of the frame buffers before the timed steps
 
 
