@@ -719,7 +719,7 @@ DEV LaneMap lane_map(uint32_t w, int lane)
 // (global, L1/L2) are read two passes ahead, the residual rows (whose address needs the
 // job record) one pass ahead; every load is unconditional (clamped pass index), so no
 // control-flow join forces an early s_waitcnt.
-struct PSet { uint32_t ja, jr; uint4 r0; int c0, c1, c2, c3; };
+struct PSet { uint32_t ja, jr; uint4 r0; };
 struct JSet { uint32_t ja, jr, lt; };     // job record + (li | ts << 8) of the lane
 DEV uint32_t pr_word(const PSet &s, int k)
 {
@@ -735,76 +735,12 @@ DEV void load_job(uint32_t w, int lane, const PJob *__restrict__ lj, JSet &j)
     j.lt = (uint32_t) m.li | (uint32_t) m.ts << 8;
 }
 
-// 4x4 inverse scans (raster position -> scan index, one nibble per position) of txtp 0 / 3
-// (default), 1 (col) and 2 (row): the inverses of vp9t_scan_*_4x4 (vp9data.c:600-640)
-#define ISCAN4_DEF 0xfec8db95a7326410ull
-#define ISCAN4_COL 0xfecbda9786534210ull
-#define ISCAN4_ROW 0xfd95eb63c841a720ull
-typedef __attribute__((address_space(1))) const int16_t glb_i16;
-KP_DEV int16_t r4_zero[4];            // the coefficient a lane past the eob reads
-
-// (8-bit) a PJ_R4 job's lane li < 4 also loads its input column: the coefficients of raster
-// positions 4k + li, k = 0..3 (scan index >= eob: zero); unconditional loads, as above
-template <typename PIX>
-DEV void load_resid(const JSet &j, const int16_t *__restrict__ resid, const int16_t *__restrict__ coefs, PSet &ps)
+DEV void load_resid(const JSet &j, const int16_t *__restrict__ resid, PSet &ps)
 {
     ps.ja = j.ja;
     ps.jr = j.jr;
     const uint32_t li = j.lt & 255, ts = j.lt >> 8;
-    const bool res = (j.ja >> 4) & 1, r4 = sizeof(PIX) == 1 && res && (j.jr & PJ_R4);
-    ps.r0 = *(const uint4 *) (resid + (res && !r4 ? (size_t) j.jr * 16 + (li << (ts + 2)) : 0));
-    ps.c0 = ps.c1 = ps.c2 = ps.c3 = 0;
-    if (sizeof(PIX) == 1 && r4) {          // passes without PJ_R4 lanes skip this
-        const uint32_t tp = PJ_R4_TXTP(j.jr), last = PJ_R4_LAST(j.jr), q4 = 4 * (li & 3);
-        const uint64_t isc = tp == 1 ? ISCAN4_COL : tp == 2 ? ISCAN4_ROW : ISCAN4_DEF;
-        const uint32_t lo = (uint32_t) isc >> q4, hi = (uint32_t) (isc >> 32) >> q4;
-        glb_i16 *cb = (glb_i16 *) coefs + PJ_R4_COEF(j.jr), *z = (glb_i16 *) r4_zero;
-        auto ld = [&](uint32_t i) -> int { return *(i <= last ? cb + i : z); };
-        ps.c0 = ld(lo & 15); ps.c1 = ld((lo >> 16) & 15); ps.c2 = ld(hi & 15); ps.c3 = ld((hi >> 16) & 15);
-    }
-}
-
-// DPP quad permutations (quad_perm controls): [1,0,3,2], [2,3,0,1], [0,0,0,0]
-template <int CTRL> DEV int qperm(int v) { return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, false); }
-
-// The residual column li of a PJ_R4 job (8-bit), on the job's 4 lanes (an aligned quad) in
-// registers: column pass on this lane's input column (-> intermediate row li, int16 as the
-// reference's tmp[]), 4x4 transpose across the quad (two DPP butterfly stages), row pass,
-// (x + 8) >> 4 (vp9dsp_template.c:1155-1180 itxfm_wrapper, 1202-1232 idct4 / iadst4); the
-// DC-only shortcut of DCT_DCT at eob 1 (vp9dsp_template.c:1165-1178). Every lane of the wave
-// runs it (DPP reads the neighbours); the caller keeps the R4 lanes' results.
-DEV void resid4_col(const PSet &ps, int li, int (&rs)[4])
-{
-    const uint32_t tp = PJ_R4_TXTP(ps.jr);
-    uint32_t a[4] = { (uint32_t) ps.c0, (uint32_t) ps.c1, (uint32_t) ps.c2, (uint32_t) ps.c3 };
-    uint32_t b[4] = { a[0], a[1], a[2], a[3] };
-    idct4<M32>(a);
-    iadst4<M32>(b);
-    int t[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) t[k] = (int16_t) ((tp & 1) ? b[k] : a[k]);
-    const bool o1 = li & 1, o2 = li & 2;
-#define QSWAP(CTRL, O, I, J)                                       \
-    {                                                              \
-        const int r = qperm<CTRL>(O ? t[I] : t[J]);                \
-        if (O) t[I] = r; else t[J] = r;                            \
-    }
-    QSWAP(0xB1, o1, 0, 1) QSWAP(0xB1, o1, 2, 3) QSWAP(0x4E, o2, 0, 2) QSWAP(0x4E, o2, 1, 3)
-#undef QSWAP
-#pragma unroll
-    for (int k = 0; k < 4; k++) a[k] = b[k] = (uint32_t) t[k];
-    idct4<M32>(a);
-    iadst4<M32>(b);
-    const int dc = qperm<0x00>(ps.c0);
-    const uint32_t t1 = M32::r14((uint32_t) dc * 11585u);
-    const int32_t tdc = (int32_t) M32::r14(t1 * 11585u);
-    const int add = (int32_t) ((uint32_t) tdc + 8u) >> 4;
-    const bool dco = tp == 0 && PJ_R4_LAST(ps.jr) == 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int32_t ov = (int16_t) ((tp >> 1) ? b[k] : a[k]);
-        rs[k] = dco ? add : (int32_t) ((uint32_t) ov + 8u) >> 4;
-    }
+    ps.r0 = *(const uint4 *) (resid + (((j.ja >> 4) & 1) ? (size_t) j.jr * 16 + (li << (ts + 2)) : 0));
 }
 
 // Load the pixels above / left of an SB (and, for inter frames, its interior: the
@@ -969,20 +905,6 @@ DEV void pred_pass(uint32_t w, int lane, PIX *tile, uint16_t *eb, int bd, const 
         for (int k = 0; k < 4; k++) ra[k] = rr[4 + k < n / 2 ? 4 + k : 0];
     }
     pf();
-    // residual rows 0-3: from the scratch, or (PJ_R4 jobs) transformed here
-    // (passes of 4x4 jobs only: no branch, so the transform interleaves with the edge reads)
-    uint32_t rq0 = ps.r0.x, rq1 = ps.r0.y;
-    if (sizeof(PIX) == 1 && (MAXN == 4 || ((w >> 9) & 31))) {
-        const bool r4 = act && ts == 0 && PJ_RES(jb) && (jb.roff & PJ_R4);
-        if (MAXN == 4 || __any(r4)) {
-            int rs[4];
-            resid4_col(ps, li & 3, rs);
-            if (r4) {
-                rq0 = ((uint32_t) rs[0] & 0xffff) | (uint32_t) rs[1] << 16;
-                rq1 = ((uint32_t) rs[2] & 0xffff) | (uint32_t) rs[3] << 16;
-            }
-        }
-    }
 
     // edges (fills: vp9recon.c:103-210): every load hits a valid tile address, the
     // host-resolved availability selects between pixel and fill value (no branches)
@@ -1039,8 +961,7 @@ DEV void pred_pass(uint32_t w, int lane, PIX *tile, uint16_t *eb, int bd, const 
             const int wb = (fw >> 24) & 3, s = (fw >> 28) & 3, rnd = fw >> 30;
             const int wc = __builtin_amdgcn_sbfe((int) fw, 26, 2);
             int v = med3_0(((a + rnd) + wb * b + wc * c) >> s, mx);
-            const uint32_t rw = y < 2 ? rq0 : y < 4 ? rq1 : y < 8 ? pr_word(ps, y >> 1)
-                              : ((y >> 3) & 1) ? ra[(y >> 1) & 3] : rb[(y >> 1) & 3];
+            const uint32_t rw = y < 8 ? pr_word(ps, y >> 1) : ((y >> 3) & 1) ? ra[(y >> 1) & 3] : rb[(y >> 1) & 3];
             const int r = (int) (int16_t) (rw >> ((y & 1) * 16));
             v = med3_0(v + (hr ? r : 0), mx);
             o[y * tpch + li] = (PIX) v;
@@ -1111,8 +1032,8 @@ KP_DEV unsigned long long pred_prof[16];
 template <typename PIX, class G, bool LISTS>
 DEV void pred_wg(const WGRec *wgp, const SBRec *__restrict__ sbs, const PJob *__restrict__ jobs,
                  const uint32_t *__restrict__ passes, const FrameDesc *__restrict__ frames,
-                 const int16_t *__restrict__ resid, const int16_t *__restrict__ coefs, const uint32_t *__restrict__ ptab,
-                 PredLds<PIX, G, LISTS> &S, int lane, int dbg)
+                 const int16_t *__restrict__ resid, const uint32_t *__restrict__ ptab, PredLds<PIX, G, LISTS> &S, int lane,
+                 int dbg)
 {
     PIX *tile = S.tile;
     uint16_t *eb = S.eb;
@@ -1128,8 +1049,6 @@ DEV void pred_wg(const WGRec *wgp, const SBRec *__restrict__ sbs, const PJob *__
     const PJob *gj = jobs + wjob0;         // job records (global)
     const uint32_t *gp = passes + wpass0;  // pass words (global)
     const int bd = frames[sbs[wgp->sb[0]].frame].bd;
-    static_assert(PRED_K == 1, "PJ_R4 offsets are relative to the workgroup's one SB");
-    const int16_t *cf = coefs + (sizeof(PIX) == 1 ? sbs[wgp->sb[0]].coef0 : 0u);
     uint64_t pp0 = PRED_PROF ? clock64() : 0, pp[13] = {0};
 
     // ---- prologue: job list, pass words, SB neighbourhoods (pre-LF pixels) ----
@@ -1181,13 +1100,13 @@ DEV void pred_wg(const WGRec *wgp, const SBRec *__restrict__ sbs, const PJob *__
         // one, the next pair (needed by this iteration's prefetches only) is read here
         uint32_t w0 = LPW(0), w1 = LPW(1);
         load_job(w0, lane, lj, J);
-        load_resid<PIX>(J, resid, cf, A);
+        load_resid(J, resid, A);
         load_job(w1, lane, lj, J);
         for (int pi = 0; pi < npass; pi += 2) {
             const uint32_t w2 = LPW(pi + 2), w3 = LPW(pi + 3);
             uint64_t tq = PRED_PROF ? clock64() : 0;
             run_pass<PIX, G>(w0, lane, tile, eb, bd, A, ltab, resid, ptab, dbg, [&] {
-                load_resid<PIX>(J, resid, cf, B);
+                load_resid(J, resid, B);
                 load_job(w2, lane, lj, J);
             });
             if (PRED_PROF) {
@@ -1198,7 +1117,7 @@ DEV void pred_wg(const WGRec *wgp, const SBRec *__restrict__ sbs, const PJob *__
             if (pi + 1 >= npass) break;
             if (PRED_PROF) tq = clock64();
             run_pass<PIX, G>(w1, lane, tile, eb, bd, B, ltab, resid, ptab, dbg, [&] {
-                load_resid<PIX>(J, resid, cf, A);
+                load_resid(J, resid, A);
                 load_job(w3, lane, lj, J);
             });
             if (PRED_PROF) {
@@ -1245,14 +1164,13 @@ template <typename PIX, class G>
 __global__ __launch_bounds__(64) void k_pred(const uint32_t *__restrict__ list, const WGRec *__restrict__ wgs,
                                              const SBRec *__restrict__ sbs, const PJob *__restrict__ jobs,
                                              const uint32_t *__restrict__ passes, const FrameDesc *__restrict__ frames,
-                                             const int16_t *__restrict__ resid, const int16_t *__restrict__ coefs,
-                                             const uint32_t *__restrict__ ptab, int dbg)
+                                             const int16_t *__restrict__ resid, const uint32_t *__restrict__ ptab, int dbg)
 {
     __shared__ PredLds<PIX, G, true> S;
 #if PRED_LTAB_LDS
     load_ltab<PIX>(S.ltab, ptab, threadIdx.x);
 #endif
-    pred_wg<PIX, G, true>(wgs + list[blockIdx.x], sbs, jobs, passes, frames, resid, coefs, ptab, S, threadIdx.x, dbg);
+    pred_wg<PIX, G, true>(wgs + list[blockIdx.x], sbs, jobs, passes, frames, resid, ptab, S, threadIdx.x, dbg);
 }
 
 // LF tile geometry. A tile row starts XL pixels left of the SB (16 at 8-bit, 8 at 16-bit,
@@ -2531,8 +2449,7 @@ __global__ __launch_bounds__(LfNT<G>::NT) void k_plf(PlfLaunch a, const uint32_t
 #if PRED_LTAB_LDS
         load_ltab<PIX>(S.p.ltab, ptab, threadIdx.x);
 #endif
-        pred_wg<PIX, G, false>(wgs + plist[b], sbs, jobs, passes, frames, resid, (const int16_t *) coefs, ptab, S.p,
-                                threadIdx.x, dbg);
+        pred_wg<PIX, G, false>(wgs + plist[b], sbs, jobs, passes, frames, resid, ptab, S.p, threadIdx.x, dbg);
         tl_end(0);
         return;
     }
@@ -2999,21 +2916,20 @@ static void launch_resid_dev_n(int hb, hipStream_t st, int ub, const RJob *jobs,
 template <typename PIX, class G>
 static void launch_pred_g(hipStream_t st, int nwg, size_t pad, const uint32_t *list, const WGRec *wgs, const SBRec *sbs,
                           const PJob *jobs, const uint32_t *passes, const FrameDesc *frames, const int16_t *resid,
-                          const int16_t *coefs, const uint32_t *ptab, int dbg)
+                          const uint32_t *ptab, int dbg)
 {
-    hipLaunchKernelGGL((k_pred<PIX, G>), dim3(nwg), dim3(64), pad, st, list, wgs, sbs, jobs, passes, frames, resid, coefs,
-                       ptab, dbg);
+    hipLaunchKernelGGL((k_pred<PIX, G>), dim3(nwg), dim3(64), pad, st, list, wgs, sbs, jobs, passes, frames, resid, ptab, dbg);
 }
 template <typename PIX>
 static void launch_pred_p(int ss, hipStream_t st, int nwg, size_t pad, const uint32_t *list, const WGRec *wgs,
                           const SBRec *sbs, const PJob *jobs, const uint32_t *passes, const FrameDesc *frames,
-                          const int16_t *resid, const int16_t *coefs, const uint32_t *ptab, int dbg)
+                          const int16_t *resid, const uint32_t *ptab, int dbg)
 {
     switch (ss) {
-    case 3: launch_pred_g<PIX, Geo<1, 1>>(st, nwg, pad, list, wgs, sbs, jobs, passes, frames, resid, coefs, ptab, dbg); break;
-    case 1: launch_pred_g<PIX, Geo<1, 0>>(st, nwg, pad, list, wgs, sbs, jobs, passes, frames, resid, coefs, ptab, dbg); break;
-    case 2: launch_pred_g<PIX, Geo<0, 1>>(st, nwg, pad, list, wgs, sbs, jobs, passes, frames, resid, coefs, ptab, dbg); break;
-    default: launch_pred_g<PIX, Geo<0, 0>>(st, nwg, pad, list, wgs, sbs, jobs, passes, frames, resid, coefs, ptab, dbg); break;
+    case 3: launch_pred_g<PIX, Geo<1, 1>>(st, nwg, pad, list, wgs, sbs, jobs, passes, frames, resid, ptab, dbg); break;
+    case 1: launch_pred_g<PIX, Geo<1, 0>>(st, nwg, pad, list, wgs, sbs, jobs, passes, frames, resid, ptab, dbg); break;
+    case 2: launch_pred_g<PIX, Geo<0, 1>>(st, nwg, pad, list, wgs, sbs, jobs, passes, frames, resid, ptab, dbg); break;
+    default: launch_pred_g<PIX, Geo<0, 0>>(st, nwg, pad, list, wgs, sbs, jobs, passes, frames, resid, ptab, dbg); break;
     }
 }
 template <typename PIX, class G>
@@ -3169,14 +3085,12 @@ int vp9hip_launch_resid_multi(int hb, hipStream_t st, const uint32_t *off, const
 // fmt: bit 0 high bit depth, bit 1 ss_h, bit 2 ss_v
 int vp9hip_launch_pred(int fmt, hipStream_t st, int nwg, const uint32_t *list, const WGRec *wgs, const SBRec *sbs,
                        const PJob *jobs, const uint32_t *passes, const FrameDesc *frames, const int16_t *resid,
-                       const void *coefs, const uint32_t *ptab, int dbg)
+                       const uint32_t *ptab, int dbg)
 {
     if (nwg <= 0) return 0;
     const size_t pad = (size_t) ((dbg >> 8) & 255) * 1024;     // profiling: occupancy sweep via LDS padding
-    if (fmt & 1) launch_pred_p<uint16_t>(fmt >> 1, st, nwg, pad, list, wgs, sbs, jobs, passes, frames, resid,
-                                           (const int16_t *) coefs, ptab, dbg);
-    else         launch_pred_p<uint8_t>(fmt >> 1, st, nwg, pad, list, wgs, sbs, jobs, passes, frames, resid,
-                                           (const int16_t *) coefs, ptab, dbg);
+    if (fmt & 1) launch_pred_p<uint16_t>(fmt >> 1, st, nwg, pad, list, wgs, sbs, jobs, passes, frames, resid, ptab, dbg);
+    else         launch_pred_p<uint8_t>(fmt >> 1, st, nwg, pad, list, wgs, sbs, jobs, passes, frames, resid, ptab, dbg);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int vp9hip_launch_lf(int fmt, hipStream_t st, int nsb, const uint32_t *list, const LFRec *recs,

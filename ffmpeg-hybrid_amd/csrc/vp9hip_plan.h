@@ -78,9 +78,6 @@ typedef struct PlanDev {
     SBRec *sbs; WGRec *wgs; PJob *pjobs; uint32_t *passes; LFRec *lfs; RJob *rjobs; McUnit *mcs;
     uint32_t *dlists;                /* intra step lists (device part of the lists array)    */
     uint32_t *jobw;                  /* per slot: jcap intra job words (k_pjob -> k_plan)     */
-    uint32_t *jobr;                  /* per slot: jcap PJ_R4 residual words of 4x4 jobs (same) */
-    int r4;                          /* 8-bit intra 4x4 residuals inside the intra pass (PJ_R4):  */
-                                     /* host-set per batch (VP9HIP_R4, coefficients < 2^25)        */
     uint32_t *sb_nj;                 /* per slot: intra jobs                                 */
     const uint8_t *nz;               /* [5][4][1025][2] nonzero bounding boxes                */
     uint32_t jcap, rcap;             /* jobs / residual units per SB slot                    */

@@ -196,13 +196,6 @@ DEV bool mc_refs_ok(const vp9h_block &b, const PlMcGeo &g)
     return g.scale[b.ref[0]][0] != 0xFFFF && g.scale[r1][0] != 0xFFFF;
 }
 
-// A tx block whose residual the intra pass computes from its coefficients (PJ_R4): 8-bit
-// intra 4x4, not lossless. It gets no residual job (k_psb's counts and k_pjob's records agree).
-DEV bool r4_tx(const PlanDev &D, const PlanFrame &F, bool intra, int txs)
-{
-    return D.r4 && intra && txs == 0 && F.bypp == 1 && !F.lossless;
-}
-
 DEV uint32_t cnt_idx(const PlanDev &D, const PlanFrame &F, uint32_t seg, uint32_t slot, int tc, int tp)
 {
     return D.seg_pre4[seg] + (uint32_t) tc * F.s4 + (uint32_t) tp * D.seg_sz[seg] + D.slot_pos[slot];
@@ -318,7 +311,7 @@ __global__ __launch_bounds__(64) void k_psb(PlanDev D)
                 const int mode = tx_mode(b, tx, st);
                 txtp = tx.p || tx.g.txs == 3 ? 0 : pl_intra_txfm_type(mode);
             }
-            if (e && G.mine && !r4_tx(D, F, b.intra, tx.g.txs)) key = (F.lossless ? 4 : tx.g.txs) * 4 + txtp;
+            if (e && G.mine) key = (F.lossless ? 4 : tx.g.txs) * 4 + txtp;
             if (b.intra && G.mine) {            // the job's 4x4 units in the SB plane's unit map
                 const int sh = tx.p ? SSH : 0, sv = tx.p ? SSV : 0;
                 const int units = 16 >> sh, unitsv = 16 >> sv;
@@ -521,14 +514,7 @@ __global__ __launch_bounds__(64) void k_pjob(PlanDev D)
             const int tcode = F.lossless ? 4 : txs;
             const int ux0 = ((tx.g.bx - G.sbx * (64 >> sh)) >> 2) + tx.x, uy0 = ((tx.g.by - G.sby * (64 >> sv)) >> 2) + tx.y;
             const uint32_t roff = rbase + pl_resid_unit(p, ux0, uy0, SSH, SSV);
-            const bool r4 = r4_tx(D, F, b.intra, txs);
-            uint32_t r4w = 0;
-            if (e0 && G.mine && r4) {
-                uint32_t coef = coef_sb + S.co[t];
-                if (coef + (uint32_t) e0 > D.total_coefs) { st |= PLS_COEF; coef = coef_sb; }
-                r4w = PJ_R4 | (uint32_t) txtp << 29 | (uint32_t) (e0 - 1) << 25 | (coef - coef_sb);
-            }
-            if (e0 && G.mine && !r4) {
+            if (e0 && G.mine) {
                 uint32_t coef = coef_sb + S.co[t];
                 int e = e0;
                 if (coef + (uint32_t) e > D.total_coefs) { st |= PLS_COEF; e = 0; coef = 0; }
@@ -552,7 +538,6 @@ __global__ __launch_bounds__(64) void k_pjob(PlanDev D)
                 const PlIntra pi = pl_intra_job(p, txs, mode, e0, tx.g.bx + tx.x * 4, tx.g.by + tx.y * 4, tx.x, tx.g.pw4,
                                                 p ? tx0l >> SSH : tx0l, pw8, ph8, ux0, uy0);
                 if (j < JCAP) D.jobw[(size_t) slot * JCAP + (uint32_t) j] = pi.a | (pi.trx ? JA_TRX : 0u);
-                if (r4w && j < JCAP) D.jobr[(size_t) slot * JCAP + (uint32_t) j] = r4w;
             }
         }
         // ranks within each key, in decode order: one ballot per distinct key of the chunk
@@ -819,9 +804,7 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
             const uint32_t a = S.ja[J];
             PJob pj;
             pj.a = a & ~JA_TRX;
-            pj.roff = !((a >> 4) & 1) ? 0u
-                    : r4_tx(D, F, true, (a >> 2) & 3) ? D.jobr[(size_t) slot * JCAP + (uint32_t) J]
-                    : rbase + pl_resid_unit(a & 3, (a >> 12) & 15, (a >> 16) & 15, SSH, SSV);
+            pj.roff = ((a >> 4) & 1) ? rbase + pl_resid_unit(a & 3, (a >> 12) & 15, (a >> 16) & 15, SSH, SSV) : 0u;
             if (inb(D, (uint32_t) (done + mypos), JCAP, 128u)) gjob[done + mypos] = pj;
         }
         if (lane == 0 && inb(D, (uint32_t) npass, JCAP, 256u)) gpass[npass] = (uint32_t) done << 14 | cnt[0] << 9 | cnt[1] << 5 | cnt[2] << 2 | cnt[3];
@@ -834,7 +817,6 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
         sr.frame = (uint32_t) F.frame; sr.sbx = (uint16_t) G.sbx; sr.sby = (uint16_t) G.sby;
         sr.tile_x0 = (uint16_t) (G.tile_sb0 << 3);
         sr.flags = F.intra ? 0 : 1;
-        sr.coef0 = inb(D, G.dord, D.nslots, 32u) ? D.sb_coef0[G.dord] : 0u;
         D.sbs[slot] = sr;
         WGRec w;
         w.job0 = slot * JCAP; w.pass0 = slot * JCAP;

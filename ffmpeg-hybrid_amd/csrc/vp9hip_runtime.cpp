@@ -50,7 +50,7 @@ int vp9hip_launch_resid_dev(int hb, hipStream_t st, int tcode, int ub, const RJo
                             const FrameDesc *frames, const void *coefs, int16_t *resid);
 int vp9hip_launch_pred(int fmt, hipStream_t st, int nwg, const uint32_t *list, const WGRec *wgs, const SBRec *sbs,
                        const PJob *jobs, const uint32_t *passes, const FrameDesc *frames, const int16_t *resid,
-                       const void *coefs, const uint32_t *ptab, int dbg);
+                       const uint32_t *ptab, int dbg);
 int vp9hip_launch_lf(int fmt, hipStream_t st, int nsb, const uint32_t *list, const LFRec *recs,
                      const FrameDesc *frames, int dbg);
 int vp9hip_launch_mc(int hb, hipStream_t st, int n, const McUnit *units, const FrameDesc *frames, const KCfg *k);
@@ -172,7 +172,7 @@ struct Staged {
     size_t o_pf = 0, o_blocks = 0, o_eobs = 0, o_slotpos = 0, o_segpre = 0, o_segsz = 0, o_segpre1 = 0, o_cntm = 0, o_cntm0 = 0, o_gidx = 0, o_bneob = 0,
            o_beob0 = 0, o_sbfirst = 0, o_sbncoef = 0, o_sbcoef0 = 0, o_cnt = 0, o_cnt0 = 0, o_ibits = 0,
            o_sbinfo = 0, o_sbkey = 0, o_sbkpos = 0, o_keycnt = 0, o_keyoff = 0, o_status = 0, o_fbytes = 0,
-           o_summary = 0, o_scan = 0, zero_bytes = 0, o_jobw = 0, o_jobr = 0, o_sbnj = 0;
+           o_summary = 0, o_scan = 0, zero_bytes = 0, o_jobw = 0, o_sbnj = 0;
     size_t scan_bytes = 0, summary_words = 0;
     uint32_t *summary_h = nullptr;                            // pinned readback of the summary
     size_t summary_cap = 0;
@@ -304,7 +304,6 @@ struct vp9hip_ctx {
     bool static_plan = true;            // VP9HIP_STATIC=0: keyframe batches planned like the others
     bool edge = true;                   // VP9HIP_EDGE=0: no SB edge columns (4:2:0 tile loader)
     bool resid_multi = true;            // VP9HIP_RESID_MULTI=0: one residual launch per tx size
-    bool r4 = true;                     // VP9HIP_R4=0: 8-bit intra 4x4 residuals through k_resid's scratch
     bool stage_trace = false;           // VP9HIP_STAGE_TRACE=1: host time of staging / planning
     bool plan_prof_on = false;          // VP9HIP_PLAN_PROF=1: k_plan phase cycles
     int plan_dbg = 0;                   // VP9HIP_PLAN_DBG: planner ablations (timing only)
@@ -404,7 +403,6 @@ static void read_config(vp9hip_ctx *c)
     c->static_plan = num("VP9HIP_STATIC", 1) != 0;
     c->edge = num("VP9HIP_EDGE", 1) != 0;
     c->resid_multi = num("VP9HIP_RESID_MULTI", 1) != 0;
-    c->r4 = num("VP9HIP_R4", 1) != 0;
     c->stage_trace = num("VP9HIP_STAGE_TRACE", 0) != 0;
     c->plan_prof_on = num("VP9HIP_PLAN_PROF", 0) != 0;
     c->plan_dbg = num("VP9HIP_PLAN_DBG", 0);
@@ -1417,7 +1415,6 @@ static int stage_dev(vp9hip_ctx *c, const DevIn &in)
     s.o_pjobs = o; o = al(o + (size_t) NS * s.jcap * sizeof(PJob));
     s.o_passes = o; o = al(o + (size_t) NS * s.jcap * 4);
     s.o_jobw = o; o = al(o + (size_t) NS * s.jcap * 4);
-    s.o_jobr = o; o = al(o + (size_t) NS * s.jcap * 4);
     s.o_sbnj = o; o = al(o + (size_t) NS * 4);
     s.o_rjobs = o; o = al(o + (ne + 1) * sizeof(RJob));
     s.o_mcs = o; o = al(o + (nmc + 1) * sizeof(McUnit));
@@ -1600,8 +1597,6 @@ static int plan_dev(vp9hip_ctx *c)
     D.mcs = (McUnit *) (A + s.o_mcs);
     D.dlists = (uint32_t *) (A + s.o_lists) + s.host_lists;
     D.jobw = (uint32_t *) (A + s.o_jobw);
-    D.jobr = (uint32_t *) (A + s.o_jobr);
-    D.r4 = c->r4;
     D.sb_nj = (uint32_t *) (A + s.o_sbnj);
     D.nz = c->nz;
     D.jcap = (uint32_t) s.jcap;
@@ -2407,8 +2402,7 @@ static int launch_one(vp9hip_ctx *c, const Launch &L, hipStream_t st)
     case K_PRED:
         return vp9hip_launch_pred(c->hb | c->ss_h << 1 | c->ss_v << 2, st, (int) L.n, lists + L.off, (const WGRec *) (s.arena + s.o_wgs),
                                   (const SBRec *) (s.arena + s.o_sbs), (const PJob *) (s.arena + s.o_pjobs),
-                                  (const uint32_t *) (s.arena + s.o_passes), fr, s.resid, s.arena + s.o_coefs, c->ptab,
-                                  c->dbg);
+                                  (const uint32_t *) (s.arena + s.o_passes), fr, s.resid, c->ptab, c->dbg);
     case K_LFR:
         return vp9hip_launch_lfr(c->hb | c->ss_h << 1 | c->ss_v << 2, st, (int) L.n, lists + L.off,
                                  (const LFRec *) (s.arena + s.o_lfs), fr, (uint32_t *) (s.arena + s.o_ctr) + L.arg,

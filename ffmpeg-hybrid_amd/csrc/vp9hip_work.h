@@ -75,13 +75,6 @@ typedef struct PJob {
 #define PJ_Y4(j) (((j).a >> 16) & 15)
 #define PJ_CT(j) (((j).a >> 20) & 31)
 #define PJ_CL(j) (((j).a >> 25) & 31)
-/* 8-bit intra 4x4 jobs with coefficients (device planner, PlanDev.r4): no k_resid job and no
- * scratch; roff = PJ_R4 | txtp << 29 | (eob - 1) << 25 | coefficient offset (25 bits), and
- * the intra pass transforms the 16 coefficients itself (vp9dsp_template.c:1155-1232). */
-#define PJ_R4 (1u << 31)         /* (offset: relative to SBRec.coef0) */
-#define PJ_R4_COEF(r) ((r) & 0x1ffffffu)
-#define PJ_R4_LAST(r) (((r) >> 25) & 15)
-#define PJ_R4_TXTP(r) (((r) >> 29) & 3)
 
 /* Intra predictor formula table: for (table slot 0..9, ts, y, x) one word
  *   i0 | i1 << 7 | i2 << 14 | wb << 21 | wc << 23 (2-bit signed: 1 = +1, 3 = -1) | s << 25 | dc << 27
@@ -96,8 +89,6 @@ typedef struct SBRec {
     uint16_t sbx, sby;
     uint16_t tile_x0;         /* tile column start, 8x8 units (vp9.c:1244-1250)         */
     uint16_t flags;           /* bit0: load SB interior first (inter frame)             */
-    uint32_t coef0;           /* the SB's first coefficient in the batch (PJ_R4 offsets are
-                                 relative to it; 0 where no job is PJ_R4)                  */
 } SBRec;
 
 /* One k_pred workgroup: up to PRED_K superblocks of the same wavefront step (any frames)
