@@ -678,6 +678,10 @@ __global__ __launch_bounds__(64 * RWAVES) void k_resid_multi(ResidMulti a, const
 #ifndef PRED_LTAB_LDS
 #define PRED_LTAB_LDS 1       // 4x4 / 8x8 formula words: LDS copy (1) or the global table via L1 (0)
 #endif
+#ifndef PRED_ABL
+#define PRED_ABL 0            // timing-only ablations of a pass (build flag, tools/ablate.sh): 8 no
+                              // predictor rows, 16 no edge writes (frames are then wrong)
+#endif
 #define LP 68            // luma tile pitch (17 dwords at 8-bit: column reads are bank-conflict free)
 #define PX0 4            // tile column of pixel x = 0 (x = -1 at column 3)
 #define LT_SIZE (65 * LP)
@@ -861,6 +865,35 @@ DEV void load_sb_tile(const FrameDesc &fd, int sbx, int sby, bool interior, int 
     if (interior) sb_interior<PIX, G, false>(fd, sbx, sby, lane, tile);
 }
 
+// one predictor pixel from its formula word and the three edge values it names
+DEV int pix_formula_apply(uint32_t fw, int a, int b, int c, int mx)
+{
+    const int wb = (fw >> 24) & 3, s = (fw >> 28) & 3, rnd = fw >> 30;
+    const int wc = __builtin_amdgcn_sbfe((int) fw, 26, 2);
+    return med3_0(((a + rnd) + wb * b + wc * c) >> s, mx);
+}
+
+// The rows of a pass of 4x4 / 8x8 jobs. The edge array and the tile are disjoint LDS
+// (restrict): the compiler issues the edge reads of every row before the first tile store,
+// one LDS round trip for the column; inline in pred_pass each row's reads waited for the
+// previous row's store (C2 k_plf 4.10 -> 3.99 ms, C3 6.62 -> 6.50 ms per step, profiles/r05l).
+template <int N, typename PIX>
+DEV void pass_rows(const char *__restrict__ e8, PIX *__restrict__ o, int tpch, int li, int n, int mx, int hr,
+                   const uint32_t (&f)[N], const PSet &ps)
+{
+#pragma unroll
+    for (int y = 0; y < N; y++) {
+        if (N > 4 && y >= n) continue;
+        const uint32_t fw = f[y];
+        const int a = *(const uint16_t *) (e8 + (fw & 255)), b = *(const uint16_t *) (e8 + ((fw >> 8) & 255)),
+                  c = *(const uint16_t *) (e8 + ((fw >> 16) & 255));
+        int v = pix_formula_apply(fw, a, b, c, mx);
+        const int r = (int) (int16_t) (pr_word(ps, y >> 1) >> ((y & 1) * 16));
+        v = med3_0(v + (hr ? r : 0), mx);
+        o[y * tpch + li] = (PIX) v;
+    }
+}
+
 // One mixed pass: lane li of an n x n job predicts pixel column li (rows 0..n-1); the
 // row loop runs to the pass's largest n (MAXN, unrolled), rows >= n are masked.
 // pf() issues the next passes' global prefetches: after this pass's own global loads, so
@@ -882,7 +915,7 @@ DEV void pred_pass(uint32_t w, int lane, PIX *tile, uint16_t *eb, int bd, const 
     PIX *o = tile + PJ_SLOT(jb) * G::TILE + (p == 0 ? 0 : p == 1 ? LT_SIZE : LT_SIZE + G::CT) +
              (PJ_Y4(jb) * 4 + 1) * tpch + PJ_X4(jb) * 4 + PX0;
     const int ms = PJ_MSLOT(jb), slot = ms < 9 ? ms : 9;
-    const int toff = ts == 0 ? 0 : ts == 1 ? 16 : ts == 2 ? 80 : 336;
+    const int toff = ts == 3 ? 336 : (int) __builtin_amdgcn_ubfe(16u << 10 | 80u << 20, 10 * ts, 10);
     // formula words of this column: rows of 4x4 / 8x8 from the LDS copy, larger from L1/L2.
     // Rows 0-7 here; rows >= 8 of 16x16 / 32x32 (formula + residual words) per 8-row chunk,
     // one chunk ahead, so at most two chunks are live
@@ -920,7 +953,7 @@ DEV void pred_pass(uint32_t w, int lane, PIX *tile, uint16_t *eb, int bd, const 
     const int tl = (hleft & htop) ? tl_px : base + (htop ? 1 : -1);
     const int tr = htop ? tr_px : base - 1;
     uint16_t *e = eb + 2 * m.gstart + 10 * m.jidx;  // 2n + 10 entries per job: n + 5 dwords, odd
-    if (act && !(dbg & 16)) {
+    if (act && !(PRED_ABL & 16)) {
         e[li] = (uint16_t) lv;
         e[n + 1 + li] = (uint16_t) tv;
         if (ts == 0) e[n + 5 + li] = (uint16_t) tr;
@@ -939,11 +972,15 @@ DEV void pred_pass(uint32_t w, int lane, PIX *tile, uint16_t *eb, int bd, const 
         const int d9 = (sl + st + n) >> (ts + 3), d10 = (sl + (n >> 1)) >> (ts + 2), d11 = (st + (n >> 1)) >> (ts + 2);
         dc = ms == 9 ? d9 : ms == 10 ? d10 : ms == 11 ? d11 : dc;
     }
-    if (act && ms >= 9 && li == 0 && !(dbg & 16)) e[2 * n + 7] = (uint16_t) dc;
+    if (act && ms >= 9 && li == 0 && !(PRED_ABL & 16)) e[2 * n + 7] = (uint16_t) dc;
     wave_sync();
-    if (act && !(dbg & 8)) {
+    if (act && !(PRED_ABL & 8)) {
         const int mx = (1 << bd) - 1;
         const int hr = PJ_RES(jb);
+        if constexpr (MAXN <= 8) {
+            pass_rows<MAXN, PIX>((const char *) e, o, tpch, li, n, mx, hr, f, ps);
+            return;
+        }
         const char *e8 = (const char *) e;
 #pragma unroll
         for (int y = 0; y < MAXN; y++) {
@@ -954,13 +991,11 @@ DEV void pred_pass(uint32_t w, int lane, PIX *tile, uint16_t *eb, int bd, const 
 #pragma unroll
                 for (int k = 0; k < 4; k++) rn[k] = rr[(y + 8) / 2 + k < n / 2 ? (y + 8) / 2 + k : 0];
             }
-            if (MAXN > 4 && y >= n) continue;
+            if (y >= n) continue;
             const uint32_t fw = y < 8 ? f[y < F0 ? y : 0] : ((y >> 3) & 1) ? fa[y & 7] : fb[y & 7];
             const int a = *(const uint16_t *) (e8 + (fw & 255)), b = *(const uint16_t *) (e8 + ((fw >> 8) & 255)),
                       c = *(const uint16_t *) (e8 + ((fw >> 16) & 255));
-            const int wb = (fw >> 24) & 3, s = (fw >> 28) & 3, rnd = fw >> 30;
-            const int wc = __builtin_amdgcn_sbfe((int) fw, 26, 2);
-            int v = med3_0(((a + rnd) + wb * b + wc * c) >> s, mx);
+            int v = pix_formula_apply(fw, a, b, c, mx);
             const uint32_t rw = y < 8 ? pr_word(ps, y >> 1) : ((y >> 3) & 1) ? ra[(y >> 1) & 3] : rb[(y >> 1) & 3];
             const int r = (int) (int16_t) (rw >> ((y & 1) * 16));
             v = med3_0(v + (hr ? r : 0), mx);
