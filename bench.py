@@ -284,7 +284,8 @@ def main():
         # whole device: algorithmic bytes of a step / step wall time (all kernels, all chains)
         "gpu_wall_frac": round(frame_bytes * args.frames / (ms_per_step / 1000.0) / 1e9 / HBM_PEAK_GBS, 5),
         # algorithmic bytes of a step / the sum of its serialised kernel durations (planner included)
-        "all_kernels_frac": round(frame_bytes * args.frames / (kernel_ms_step / 1000.0) / 1e9 / HBM_PEAK_GBS, 5),
+        "all_kernels_frac": round(frame_bytes * args.frames / (kernel_ms_step / 1000.0) / 1e9 / HBM_PEAK_GBS, 5)
+        if kernel_ms_step > 0 else None,
         "launch_time_note": "HIP-event launch durations with every launch of the batch on one stream "
                             "(serialised, as under a rocprofv3 kernel trace), in separate steps of the same "
                             "batch with launches enqueued individually; the timed steps replay a HIP graph "

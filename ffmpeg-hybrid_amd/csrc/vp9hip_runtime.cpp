@@ -308,6 +308,8 @@ struct vp9hip_ctx {
     bool plan_prof_on = false;          // VP9HIP_PLAN_PROF=1: k_plan phase cycles
     int plan_dbg = 0;                   // VP9HIP_PLAN_DBG: planner ablations (timing only)
     bool plan_only = false;             // VP9HIP_PLAN_ONLY=1: run the planner alone (diagnostics)
+    bool plan_reuse = false;            // VP9HIP_PLAN_REUSE=1: a static-plan batch's reruns skip the planner
+                                        // (its records are unchanged): the pixel launches alone (diagnostics)
     int dl_threads = 3;                 // VP9HIP_DL_THREADS: download copy threads besides the caller
     Staged stg;                         // the current batch slot
     Staged sl[MAX_SLOTS];               // the other slots (sl[slot] is a moved-out placeholder;
@@ -407,6 +409,7 @@ static void read_config(vp9hip_ctx *c)
     c->plan_prof_on = num("VP9HIP_PLAN_PROF", 0) != 0;
     c->plan_dbg = num("VP9HIP_PLAN_DBG", 0);
     c->plan_only = num("VP9HIP_PLAN_ONLY", 0) != 0;
+    c->plan_reuse = num("VP9HIP_PLAN_REUSE", 0) != 0;
     c->dl_threads = std::max(0, std::min(15, num("VP9HIP_DL_THREADS", 3)));
     c->test_reject = g_test_reject;
     c->lfr_spin = g_test_lfr_spin;
@@ -2341,7 +2344,7 @@ extern "C" int vp9hip_run_batch(vp9hip_ctx *c)
     if (!c || !c->stg.ready) return VP9HIP_EINVAL;
     hipSetDevice(c->dev);
     Staged &s = c->stg;
-    if (s.dev) {                          // plan on the device from the resident packets
+    if (s.dev && !(c->plan_reuse && s.stat && s.planned)) {   // plan on the device from the resident packets
         const int r = plan_dev(c);
         if (r) return r;
         if (c->plan_only) return 0;       // diagnostics: the planner alone
