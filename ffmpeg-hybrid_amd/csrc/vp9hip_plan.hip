@@ -367,24 +367,30 @@ template <int JCAP> struct PJobLds {
     uint8_t  own[JCAP];           // (block, plane) entry of tx t (max-scan of ost)
     uint32_t eb[64];              // first eob entry of each block
 };
-// k_plan's LDS: hgt overlays the unit map (read until the producers are listed, hgt is set
-// after that); the other scheduling fields follow it.
+// k_plan's LDS: the unit map, then the heights, then the priority order with the pass of
+// each job share one region, each dead before the next is written (7.2 KB at 4:2:0; with ord
+// and sch after the heights 8.75 KB: 17 instead of 21 workgroups per CU)
 template <int JCAP> struct alignas(16) PlanLds {   // 16: jmap rows are stored 16 bytes at a time
     uint32_t ja[JCAP];            // PJob word per intra job (decode order), bit 30: the 4x4
                                   // top-right lies inside the block (trx)
     union {
         uint16_t jmap[3][256];    // producing job of each 4x4 unit
         struct {
-            uint32_t hgt[JCAP];           // longest path to a sink (list-scheduling priority)
+            union {
+                uint32_t hgt[JCAP];           // longest path to a sink (list-scheduling priority)
+                struct {
+                    uint16_t ord[JCAP];       // jobs by (height desc, index asc)
+                    uint16_t sch[JCAP];       // pass of each job (0xffff: not yet)
+                } os;
+            } h;
             uint16_t doff[JCAP + 1];      // producers of job j: dep[2 (doff & 2047) ..] (count doff >> 11)
             uint16_t dep[4 * JCAP];
-            uint16_t ord[JCAP];           // jobs by (height desc, index asc)
-            uint16_t sch[JCAP];           // pass of each job (0xffff: not yet)
             uint32_t hs[64];              // height histogram -> list starts
             uint16_t tk[16];              // jobs taken by the pass being built
         } b;
     } u;
 };
+static_assert(sizeof(uint16_t[3][256]) <= sizeof(uint32_t[256 + 2 * 64]), "the unit map fits the heights' region");
 #define JA_TRX (1u << 30)
 
 // edges the job's (substituted) mode reads: 1 left, 2 top, 4 top-left, 8 top-right (pl_intra_job)
@@ -663,12 +669,11 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
                 if (off + cap <= 4u * JCAP) deps_of(j, [&](int d) { if (k < off + cap) S.u.b.dep[k++] = (uint16_t) d; });
                 else st |= PLS_SCHED;
                 S.u.b.doff[j] = (uint16_t) (off >> 1 | (k - off) << 11);
-                S.u.b.sch[j] = 0xffff;
             }
             carry += rdl(incl, 63);
         }
         wsync();                              // jmap is dead: hgt overlays it
-        for (int j = lane; j < NJ; j += 64) S.u.b.hgt[j] = 1;
+        for (int j = lane; j < NJ; j += 64) S.u.b.h.hgt[j] = 1;
     }
     wsync();
     PPT(3);
@@ -683,10 +688,10 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
         for (int it = 0; it < 65; it++) {
             bool ch = false;                  // a job of this chunk rose
             if (j < NJ) {
-                const uint32_t h1 = S.u.b.hgt[j] + 1;
+                const uint32_t h1 = S.u.b.h.hgt[j] + 1;
                 for (int k = k0; k < k1; k++) {
                     const int d = S.u.b.dep[k];
-                    if (S.u.b.hgt[d] < h1) { atomicMax(&S.u.b.hgt[d], h1); ch |= d >= c; }
+                    if (S.u.b.h.hgt[d] < h1) { atomicMax(&S.u.b.h.hgt[d], h1); ch |= d >= c; }
                 }
             }
             wsync();
@@ -694,10 +699,20 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
         }
     }
     PPT(4);
-    // ---- priority order: height descending, then decode order
+    // ---- priority order: height descending, then decode order. The heights go to registers
+    // first: the order and the pass words overlay them
+    constexpr int NCH = JCAP / 64;
+    int hreg[NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+        const int j = c * 64 + lane;
+        hreg[c] = j < NJ ? pl_min((int) S.u.b.h.hgt[j], 63) : -1;
+    }
     S.u.b.hs[lane] = 0;
     wsync();
-    for (int j = lane; j < NJ; j += 64) atomicAdd(&S.u.b.hs[pl_min((int) S.u.b.hgt[j], 63)], 1u);
+#pragma unroll
+    for (int c = 0; c < NCH; c++)
+        if (hreg[c] >= 0) atomicAdd(&S.u.b.hs[hreg[c]], 1u);
     wsync();
     {
         const uint32_t v = S.u.b.hs[63 - lane];                // heights from the top
@@ -705,15 +720,17 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
         wsync();
         S.u.b.hs[63 - lane] = incl - v;
         wsync();
-        for (int c = 0; c < NJ; c += 64) {
-            const int j = c + lane;
-            const int h = j < NJ ? pl_min((int) S.u.b.hgt[j], 63) : -1;
+#pragma unroll
+        for (int c = 0; c < NCH; c++) {
+            if (c * 64 >= NJ) break;
+            const int j = c * 64 + lane;
+            const int h = hreg[c];
             uint64_t pend = __ballot(h >= 0);
             while (pend) {
                 const int hh = rdl(h, __builtin_ctzll(pend));
                 const uint64_t m = __ballot(h == hh);
                 const uint32_t base = S.u.b.hs[hh];
-                if (h == hh) S.u.b.ord[base + mbcnt(m)] = (uint16_t) j;
+                if (h == hh) S.u.b.h.os.ord[base + mbcnt(m)] = (uint16_t) j;
                 wsync();
                 if (lane == 0) S.u.b.hs[hh] = base + (uint32_t) __popcll(m);
                 wsync();
@@ -721,6 +738,8 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
             }
         }
     }
+    wsync();
+    for (int j = lane; j < NJ; j += 64) S.u.b.h.os.sch[j] = 0xffff;
     wsync();
     PPT(5);
     // ---- list scheduling (merge_mixed): each pass takes, in priority order, every ready job
@@ -733,7 +752,6 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
     // scheduled in an earlier pass; producers scheduled in earlier passes stay so), and bit c
     // of `pend` while it is unscheduled. A pass then reads LDS only for the sch[] word of each
     // waiting job's current producer.
-    constexpr int NCH = JCAP / 64;
     uint32_t jreg[NCH], kreg[NCH], k1reg[NCH], szreg[NCH];
     uint32_t pend = 0;
 #pragma unroll
@@ -742,7 +760,7 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
         jreg[c] = kreg[c] = k1reg[c] = 0;
         szreg[c] = 0;
         if (pos < NJ) {
-            const uint32_t j = S.u.b.ord[pos], dw = S.u.b.doff[j];
+            const uint32_t j = S.u.b.h.os.ord[pos], dw = S.u.b.doff[j];
             jreg[c] = j;
             kreg[c] = (dw & 2047) << 1;
             k1reg[c] = kreg[c] + (dw >> 11);
@@ -761,7 +779,7 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
             if (cand) {
                 uint32_t k = kreg[c];
                 const uint32_t k1 = k1reg[c];
-                while (k < k1 && S.u.b.sch[S.u.b.dep[k]] < (uint16_t) npass) k++;
+                while (k < k1 && S.u.b.h.os.sch[S.u.b.dep[k]] < (uint16_t) npass) k++;
                 kreg[c] = k;
                 cand = k == k1;
             }
@@ -780,7 +798,7 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
                 if (take) {
                     cand = false;
                     pend &= ~(1u << c);
-                    S.u.b.sch[j] = (uint16_t) npass;
+                    S.u.b.h.os.sch[j] = (uint16_t) npass;
                     S.u.b.tk[ntake + (int) mbcnt(m)] = (uint16_t) j;
                 }
                 ntake += __popcll(m);
