@@ -13,6 +13,6 @@ for r in $(seq 1 $R); do
     t=${spec%%@*}; ev=""; [ "$t" != "$spec" ] && ev=${spec#*@}
     tag=$(basename $(cd $t && pwd))${ev:+_$ev}_$r
     (cd $t && env $ev timeout -k 10 300 python bench.py --steps ${STEPS:-20} --warmup 5 --no-cpu-baseline --verify-frames 4 ${BARGS:-}) > $O/$tag.json 2> $O/$tag.err || { echo "$tag failed"; tail -5 $O/$tag.err; exit 1; }
-    python3 -c "import json;d=json.loads(open('$O/$tag.json').read().strip().split(chr(10))[-1]);km=d['roofline'].get('kernel_ms',{});print('$tag', d['value'], d['ms_per_step'], d['verify']['frames'], len(d['verify']['mismatched']), 'k_lf', km.get('k_lf'), 'k_plf', km.get('k_plf'), 'plan', km.get('k_plan'))"
+    python3 -c "import json;d=json.loads(open('$O/$tag.json').read().strip().split(chr(10))[-1]);km=d['roofline'].get('kernel_ms',{});print('$tag', d['value'], d['ms_per_step'], d['verify']['frames'], len(d['verify']['mismatched']), 'k_lf', km.get('k_lf'), 'k_plf', km.get('k_plf'), 'plan', km.get('k_plan'), 'k_mc', km.get('k_mc'), 'k_lfr', km.get('k_lfr'))"
   done
 done
