@@ -956,7 +956,8 @@ def webm_write(frames, width, height, timecode_scale=1000000, cluster_frames=8, 
 
 PLAN_STAT_NAMES = ("sbs", "passes", "pjobs", "rjobs", "jobs_4x4", "jobs_8x8", "jobs_16x16",
                    "jobs_32x32", "lane_use", "max_passes_sb", "lf_records", "mc_units", "pred_steps",
-                   "lf_steps", "levels", "pass_rows", "level_steps", "asap_passes", "firstfit_passes", "firstfit_height_passes")
+                   "lf_steps", "levels", "pass_rows", "level_steps", "asap_passes", "firstfit_passes", "firstfit_height_passes",
+                   "mc_out_bytes", "mc_alg_bytes", "mc_line_bytes")
 
 
 def plan_sb_costs(frame):

@@ -2977,5 +2977,26 @@ extern "C" int vp9hip_plan_stats(const vp9h_frame *f, double *out, int cap)
         if (r < 0) return r;
         out[16] = (double) ps2.size();
     }
+    if (cap > 22) {                     // MC bytes of the frame's units: [20] predicted pixels,
+                                        // [21] x (1 + references) (the roofline's algorithmic
+                                        // bytes), [22] the 128-byte lines k_mcq's window rows
+                                        // touch (columns x - 3 .. x + w + 4, rows y - 3 .. y + h + 3
+                                        // when the vertical phase is fractional), each unit alone
+        const int bypp = f->bpp > 8 ? 2 : 1;
+        for (const McUnit &m : s.mcs) {
+            const double ob = (double) m.w * m.h * bypp;
+            out[20] += ob;
+            out[21] += ob * (1 + m.nref);
+            const int pw = m.plane ? ((f->width + f->ss_h) >> f->ss_h) : f->width;
+            for (int k = 0; k < m.nref && k < 2; k++) {
+                const McRef &r = m.r[k];
+                const int rows = r.my || r.dy != 16 ? m.h + 7 : m.h;
+                const int x0 = std::max(0, std::min(pw - 1, r.ix - 3));
+                const int x1 = std::max(x0 + 1, std::min(pw, r.ix + m.w + 5));
+                const int lines = (x1 * bypp - 1) / 128 - (x0 * bypp) / 128 + 1;
+                out[22] += (double) rows * lines * 128;
+            }
+        }
+    }
     return 0;
 }

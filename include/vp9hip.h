@@ -248,7 +248,9 @@ int  vp9hip_alg_bytes(vp9hip_ctx *ctx, double *bytes, int cap);
  * lane use, max passes per SB, LF records, MC units, intra / LF wavefront steps,
  * intra dependency levels (summed over SBs: the lower bound of the passes), pixel rows
  * the passes loop over (each pass: its largest job size). A 17th value (cap >= 17): intra
- * steps under the dependency-level schedule of inter frames (= the diagonals otherwise). */
+ * steps under the dependency-level schedule of inter frames (= the diagonals otherwise);
+ * 18-20: pass-packing estimates; 21-23 (cap >= 23): MC predicted-pixel bytes, those x (1 +
+ * references), and the 128-byte lines the MC window rows touch, each unit counted alone. */
 int  vp9hip_plan_stats(const vp9h_frame *pkt, double *out, int cap);
 /* Diagnostics: per SB of one packet (raster order) the pixel rows its intra passes loop
  * over, as staged for the device (the wavefront-tail estimate of tools/wave_tail.py).
