@@ -202,6 +202,35 @@ static int bc_tree(BC *c, const int8_t (*t)[2], const uint8_t *probs, int sym)
     return -i;
 }
 
+/* small context fills (SET_CTXS, vp9block.c:718-745, and the SPLAT / segment-map fills):
+ * sizes 1, 2, 4, 8, 16 as one or two stores, as the reference's setctx_2d / AV_WN64A splats do;
+ * a libc memset call per fill cost ~30 % of the single-thread parse (tools/parse_bench.c) */
+typedef uint16_t __attribute__((may_alias, aligned(1))) u16_ua;
+typedef uint32_t __attribute__((may_alias, aligned(1))) u32_ua;
+typedef uint64_t __attribute__((may_alias, aligned(1))) u64_ua;
+static inline __attribute__((always_inline)) void fill_ctx(uint8_t *p, int v, int n)
+{
+    const uint64_t x = 0x0101010101010101ull * (uint8_t) v;
+    switch (n) {
+    case 1: p[0] = (uint8_t) v; return;
+    case 2: *(u16_ua *) p = (uint16_t) x; return;
+    case 4: *(u32_ua *) p = (uint32_t) x; return;
+    case 8: *(u64_ua *) p = x; return;
+    default: memset(p, v, (size_t) n);
+    }
+}
+/* the same for the non-zero contexts, whose fills reach 16 bytes */
+static inline __attribute__((always_inline)) void fill_ctx16(uint8_t *p, int v, int n)
+{
+    if (n == 16) {
+        const uint64_t x = 0x0101010101010101ull * (uint8_t) v;
+        ((u64_ua *) p)[0] = x;
+        ((u64_ua *) p)[1] = x;
+    } else {
+        fill_ctx(p, v, n);
+    }
+}
+
 /* VP9 trees (spec constants): partition NONE/H/V/SPLIT; intra modes V=0 H=1 DC=2 D45=3
  * D135=4 D117=5 D153=6 D63=7 D207=8 TM=9; segment ids 0..7 */
 static const int8_t partition_tree[3][2] = { { -0, 1 }, { -1, 2 }, { -2, -3 } };
@@ -1072,17 +1101,17 @@ static void walk_seg_id(Walk *w, vp9h_block *b, const vp9h_block *t, int row, in
         if (!h->seg_update_map ||
             (h->seg_temporal && bc_bool(c, h->seg_pred[w->a_segpred[col] + w->l_segpred[row7]], t->seg_id == pred))) {
             b->seg_id = (uint8_t) pred;
-            memset(w->a_segpred + col, 1, w4);
-            memset(w->l_segpred + row7, 1, h4);
+            fill_ctx(w->a_segpred + col, 1, w4);
+            fill_ctx(w->l_segpred + row7, 1, h4);
         } else {
             b->seg_id = (uint8_t) bc_tree(c, segment_tree, h->seg_prob, t->seg_id);
-            memset(w->a_segpred + col, 0, w4);
-            memset(w->l_segpred + row7, 0, h4);
+            fill_ctx(w->a_segpred + col, 0, w4);
+            fill_ctx(w->l_segpred + row7, 0, h4);
         }
     }
     if (h->seg_enabled && (h->seg_update_map || h->keyframe || h->intraonly)) {
         const int bw4 = vp9t_bwh[1][b->bs][0], bh4 = vp9t_bwh[1][b->bs][1];
-        for (int y = 0; y < bh4; y++) memset(w->side->seg + (row + y) * 8 * w->sb_cols + col, b->seg_id, bw4);
+        for (int y = 0; y < bh4; y++) fill_ctx(w->side->seg + (row + y) * 8 * w->sb_cols + col, b->seg_id, bw4);
     }
 }
 
@@ -1326,8 +1355,8 @@ static void walk_block(Walk *w, int row, int col, int bl, int bp)
         } else {
             b.mode[0] = (uint8_t) bc_tree(c, intramode_tree, vp9t_kf_ymode_probs[*a][*l], t->mode[0]);
             b.mode[3] = b.mode[2] = b.mode[1] = b.mode[0];
-            memset(a, b.mode[0], vp9t_bwh[0][bs][0]);
-            memset(l, b.mode[0], vp9t_bwh[0][bs][1]);
+            fill_ctx(a, b.mode[0], vp9t_bwh[0][bs][0]);
+            fill_ctx(l, b.mode[0], vp9t_bwh[0][bs][1]);
         }
         b.uvmode = (uint8_t) bc_tree(c, intramode_tree, vp9t_kf_uvmode_probs[b.mode[3]], t->uvmode);
     } else if (b.intra) {
@@ -1425,17 +1454,17 @@ static void walk_block(Walk *w, int row, int col, int bl, int bp)
     b.uvtx = (uint8_t) (b.tx - ((h->ss_h && bw4 * 2 == (1 << b.tx)) || (h->ss_v && bh4 * 2 == (1 << b.tx))));
 
     /* contexts (SET_CTXS, vp9block.c:718-745) */
-    memset(w->a_skip + col, b.skip, bw4); memset(w->l_skip + row7, b.skip, bh4);
-    memset(w->a_tx + col, b.tx, bw4); memset(w->l_tx + row7, b.tx, bh4);
-    memset(w->a_part + col, above_ctx_of[bs], bw4); memset(w->l_part + row7, left_ctx_of[bs], bh4);
+    fill_ctx(w->a_skip + col, b.skip, bw4); fill_ctx(w->l_skip + row7, b.skip, bh4);
+    fill_ctx(w->a_tx + col, b.tx, bw4); fill_ctx(w->l_tx + row7, b.tx, bh4);
+    fill_ctx(w->a_part + col, above_ctx_of[bs], bw4); fill_ctx(w->l_part + row7, left_ctx_of[bs], bh4);
     if (!intra_frame) {
-        memset(w->a_intra + col, b.intra, bw4); memset(w->l_intra + row7, b.intra, bh4);
-        memset(w->a_comp + col, b.comp, bw4); memset(w->l_comp + row7, b.comp, bh4);
-        memset(w->a_mode + col, b.mode[3], bw4); memset(w->l_mode + row7, b.mode[3], bh4);
+        fill_ctx(w->a_intra + col, b.intra, bw4); fill_ctx(w->l_intra + row7, b.intra, bh4);
+        fill_ctx(w->a_comp + col, b.comp, bw4); fill_ctx(w->l_comp + row7, b.comp, bh4);
+        fill_ctx(w->a_mode + col, b.mode[3], bw4); fill_ctx(w->l_mode + row7, b.mode[3], bh4);
         if (!b.intra) {
-            memset(w->a_ref + col, vref, bw4); memset(w->l_ref + row7, vref, bh4);
+            fill_ctx(w->a_ref + col, vref, bw4); fill_ctx(w->l_ref + row7, vref, bh4);
             if (h->filtermode == FILTER_SWITCHABLE) {
-                memset(w->a_filter + col, filter_id, bw4); memset(w->l_filter + row7, filter_id, bh4);
+                fill_ctx(w->a_filter + col, filter_id, bw4); fill_ctx(w->l_filter + row7, filter_id, bh4);
             }
         }
         /* MV contexts for the sub-8x8 candidates (vp9block.c:747-770) */
@@ -1472,16 +1501,16 @@ static void walk_block(Walk *w, int row, int col, int bl, int bp)
         if (!walk_coeffs(w, &b, row, col) && !w->err && bs <= VP9H_BS_8x8 && !b.intra) {
             /* an inter block <= 8x8 without coefficients becomes skip (vp9block.c:1310-1314) */
             b.skip = 1;
-            memset(w->a_skip + col, 1, bw4);
-            memset(w->l_skip + row7, 1, bh4);
+            fill_ctx(w->a_skip + col, 1, bw4);
+            fill_ctx(w->l_skip + row7, 1, bh4);
             w->ne = ne0; w->nc = nc0;
         }
     } else {
         /* SPLAT_ZERO_YUV (vp9block.c:1313-1345): the whole block, unclipped */
-        memset(w->a_ynnz + col * 2, 0, 2 * bw4); memset(w->l_ynnz + row7 * 2, 0, 2 * bh4);
+        fill_ctx16(w->a_ynnz + col * 2, 0, 2 * bw4); fill_ctx16(w->l_ynnz + row7 * 2, 0, 2 * bh4);
         const int ux = h->ss_h ? bw4 : 2 * bw4, uy = h->ss_v ? bh4 : 2 * bh4;
-        memset(w->a_unnz + (col << !h->ss_h), 0, ux); memset(w->a_vnnz + (col << !h->ss_h), 0, ux);
-        memset(w->l_unnz + (row7 << !h->ss_v), 0, uy); memset(w->l_vnnz + (row7 << !h->ss_v), 0, uy);
+        fill_ctx16(w->a_unnz + (col << !h->ss_h), 0, ux); fill_ctx16(w->a_vnnz + (col << !h->ss_h), 0, ux);
+        fill_ctx16(w->l_unnz + (row7 << !h->ss_v), 0, uy); fill_ctx16(w->l_vnnz + (row7 << !h->ss_v), 0, uy);
     }
     if (w->err) return;
     w->blocks = grow(w->blocks, &w->cb, w->nb + 1, sizeof(vp9h_block), &w->err);
@@ -2006,8 +2035,8 @@ static int alloc_ctx(Walk *w)
     if (!w->a_part || !w->a_skip || !w->a_tx || !w->a_mode || !w->a_ynnz || !w->a_unnz || !w->a_vnnz ||
         !w->a_segpred || !w->a_intra || !w->a_comp || !w->a_ref || !w->a_filter || !w->a_mv)
         return -1;
-    if (w->h->keyframe || w->h->intraonly) memset(w->a_mode, 2 /* DC_PRED */, 2 * n);
-    else memset(w->a_mode, VP9H_NEARESTMV, n);
+    if (w->h->keyframe || w->h->intraonly) fill_ctx(w->a_mode, 2 /* DC_PRED */, 2 * n);
+    else fill_ctx(w->a_mode, VP9H_NEARESTMV, n);
     return 0;
 }
 static void free_ctx(Walk *w)
@@ -2027,11 +2056,11 @@ static int walk_tile_row(Walk *w, BC *coder, int row, int c0, int c1)
         return -1;
     }
     w->tile_col_start = c0;
-    memset(w->l_part, 0, sizeof(w->l_part)); memset(w->l_skip, 0, sizeof(w->l_skip));
-    if (intra_frame) memset(w->l_mode, 2, sizeof(w->l_mode));
-    else memset(w->l_mode, VP9H_NEARESTMV, 8);
-    memset(w->l_ynnz, 0, sizeof(w->l_ynnz)); memset(w->l_unnz, 0, sizeof(w->l_unnz));
-    memset(w->l_vnnz, 0, sizeof(w->l_vnnz)); memset(w->l_segpred, 0, sizeof(w->l_segpred));
+    fill_ctx(w->l_part, 0, sizeof(w->l_part)); fill_ctx(w->l_skip, 0, sizeof(w->l_skip));
+    if (intra_frame) fill_ctx(w->l_mode, 2, sizeof(w->l_mode));
+    else fill_ctx(w->l_mode, VP9H_NEARESTMV, 8);
+    fill_ctx16(w->l_ynnz, 0, sizeof(w->l_ynnz)); fill_ctx16(w->l_unnz, 0, sizeof(w->l_unnz));
+    fill_ctx16(w->l_vnnz, 0, sizeof(w->l_vnnz)); fill_ctx(w->l_segpred, 0, sizeof(w->l_segpred));
     w->c = coder;
     for (int col = c0; col < c1; col += 8) {
         /* a tile whose data ran out is invalid (vp9.c:1383-1385) */
