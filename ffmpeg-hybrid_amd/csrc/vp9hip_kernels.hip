@@ -809,7 +809,26 @@ DEV void sb_interior(const FrameDesc &fd, int sbx, int sby, int lane, PIX *tile)
     }
 }
 
-template <typename PIX, class G>
+// Pixel loads / stores of the intra hand-off inside one k_predd launch: sc1 (agent scope), so
+// a workgroup on another XCD reads what the producer wrote through, without an L2 write-back
+// or invalidate (the k_lfro row hand-off's protocol). SC = false: plain.
+typedef __attribute__((address_space(1))) uint8_t gpx8;
+typedef __attribute__((address_space(1))) uint16_t gpx16;
+template <bool SC, typename PIX> DEV PIX ld_px(const PIX *p)
+{
+    if constexpr (!SC) return *p;
+    else if constexpr (sizeof(PIX) == 1) return __hip_atomic_load((gpx8 *) p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return __hip_atomic_load((gpx16 *) p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <bool SC, typename PIX> DEV void st_px(PIX *p, PIX v)
+{
+    if constexpr (!SC) *p = v;
+    else if constexpr (sizeof(PIX) == 1) __hip_atomic_store((gpx8 *) p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else __hip_atomic_store((gpx16 *) p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// SC: the halo (the row above, the left column) with sc1 loads (k_predd; 4:2:0)
+template <typename PIX, class G, bool SC = false>
 DEV void load_sb_tile(const FrameDesc &fd, int sbx, int sby, bool interior, int lane, PIX *tile)
 {
     if (G::SH != 1 || G::SV != 1) {
@@ -839,20 +858,20 @@ DEV void load_sb_tile(const FrameDesc &fd, int sbx, int sby, bool interior, int 
     const PIX *gc = lane < 33 ? gu : gv;
     const int ci = lane < 33 ? lane : lane - 33;
     if (top) {
-        if (lx - 1 + lane >= 0) v0 = gy[(size_t) (ly - 1) * py + lx - 1 + lane];
-        if (lane == 0) v4 = gy[(size_t) (ly - 1) * py + lx + 63];
-        if (cx - 1 + ci >= 0) v2 = gc[(size_t) (cy - 1) * pc + cx - 1 + ci];
-        if (lane < 2) v5 = gv[(size_t) (cy - 1) * pc + cx + 30 + lane];
+        if (lx - 1 + lane >= 0) v0 = ld_px<SC>(gy + (size_t) (ly - 1) * py + lx - 1 + lane);
+        if (lane == 0) v4 = ld_px<SC>(gy + (size_t) (ly - 1) * py + lx + 63);
+        if (cx - 1 + ci >= 0) v2 = ld_px<SC>(gc + (size_t) (cy - 1) * pc + cx - 1 + ci);
+        if (lane < 2) v5 = ld_px<SC>(gv + (size_t) (cy - 1) * pc + cx + 30 + lane);
     }
     if (left && fd.edge) {
         // the left SB's right column as its intra workgroup saved it (FrameDesc.edge):
         // two 64-pixel runs instead of 128 one-pixel frame rows
         const PIX *e = (const PIX *) fd.edge + (size_t) (sby * fd.sb_cols + sbx - 1) * EDGE_PIX;
-        v1 = e[lane];
-        v3 = e[64 + lane];
+        v1 = ld_px<SC>(e + lane);
+        v3 = ld_px<SC>(e + 64 + lane);
     } else if (left) {
-        v1 = gy[(size_t) (ly + lane) * py + lx - 1];
-        v3 = (lane < 32 ? gu : gv)[(size_t) (cy + (lane & 31)) * pc + cx - 1];
+        v1 = ld_px<SC>(gy + (size_t) (ly + lane) * py + lx - 1);
+        v3 = ld_px<SC>((lane < 32 ? gu : gv) + (size_t) (cy + (lane & 31)) * pc + cx - 1);
     }
     PIX *tu = tile + LT_SIZE, *tv = tile + LT_SIZE + CT_SIZE;
     if (top) {
@@ -1063,8 +1082,10 @@ DEV void load_ltab(uint32_t *ltab, const uint32_t *__restrict__ ptab, int lane)
 #define PRED_PROF 0
 #endif
 KP_DEV unsigned long long pred_prof[16];
-// Intra prediction of one workgroup record (the ltab copy must be loaded).
-template <typename PIX, class G, bool LISTS>
+// Intra prediction of one workgroup record (the ltab copy must be loaded). HO (k_predd,
+// 4:2:0): the halo loads and the SB's own right column / bottom row (what the SBs to the
+// right and below read) go through sc1 as well.
+template <typename PIX, class G, bool LISTS, bool HO = false>
 DEV void pred_wg(const WGRec *wgp, const SBRec *__restrict__ sbs, const PJob *__restrict__ jobs,
                  const uint32_t *__restrict__ passes, const FrameDesc *__restrict__ frames,
                  const int16_t *__restrict__ resid, const uint32_t *__restrict__ ptab, PredLds<PIX, G, LISTS> &S, int lane,
@@ -1103,7 +1124,7 @@ DEV void pred_wg(const WGRec *wgp, const SBRec *__restrict__ sbs, const PJob *__
         const uint32_t sbi = __builtin_amdgcn_readfirstlane(wgp->sb[k]);
         if (sbi != 0xffffffffu) {
             const SBRec sb = sbs[sbi];
-            if (!(dbg & 4)) load_sb_tile<PIX, G>(frames[sb.frame], sb.sbx, sb.sby, sb.flags & 1, lane, tile + k * G::TILE);
+            if (!(dbg & 4)) load_sb_tile<PIX, G, HO>(frames[sb.frame], sb.sbx, sb.sby, sb.flags & 1, lane, tile + k * G::TILE);
         }
     }
     if (PL::ON) {
@@ -1176,14 +1197,27 @@ DEV void pred_wg(const WGRec *wgp, const SBRec *__restrict__ sbs, const PJob *__
         const SBRec sb = sbs[sbi];
         const FrameDesc &fd = frames[sb.frame];
         sb_interior<PIX, G, true>(fd, sb.sbx, sb.sby, lane, tile + k * G::TILE);
+        if constexpr (HO) {            // right column and bottom row again, written through
+            static_assert(G::SH == 1 && G::SV == 1, "k_predd: 4:2:0");
+            const PIX *t = tile + k * G::TILE;
+            PIX *gy = (PIX *) fd.plane[0];
+            const int p = 1 + (lane >> 5), x = lane & 31;
+            PIX *gc = (PIX *) fd.plane[p];
+            const PIX *tc = t + (p == 1 ? LT_SIZE : LT_SIZE + G::CT);
+            const size_t ly = (size_t) sb.sby * 64, cy = (size_t) sb.sby * 32;
+            st_px<true>(gy + (ly + 63) * fd.pitch[0] + sb.sbx * 64 + lane, t[64 * LP + PX0 + lane]);
+            st_px<true>(gy + (ly + lane) * fd.pitch[0] + sb.sbx * 64 + 63, t[(lane + 1) * LP + PX0 + 63]);
+            st_px<true>(gc + (cy + 31) * fd.pitch[1] + sb.sbx * 32 + x, tc[32 * G::CP + PX0 + x]);
+            st_px<true>(gc + (cy + x) * fd.pitch[1] + sb.sbx * 32 + 31, tc[(x + 1) * G::CP + PX0 + 31]);
+        }
         if (fd.edge) {                 // the right column of each plane, for the SB to the right
             PIX *e = (PIX *) fd.edge + (size_t) (sb.sby * fd.sb_cols + sb.sbx) * EDGE_PIX;
             const PIX *t = tile + k * G::TILE;
 #pragma unroll
             for (int i = lane; i < 64 + 2 * G::CH; i += 64) {
                 const int p = i < 64 ? 0 : i < 64 + G::CH ? 1 : 2, r = p == 0 ? i : p == 1 ? i - 64 : i - 64 - G::CH;
-                e[i] = t[(p == 0 ? 0 : p == 1 ? LT_SIZE : LT_SIZE + G::CT) + (r + 1) * (p ? G::CP : LP) + PX0 +
-                         (p ? G::CW : 64) - 1];
+                st_px<HO>(e + i, t[(p == 0 ? 0 : p == 1 ? LT_SIZE : LT_SIZE + G::CT) + (r + 1) * (p ? G::CP : LP) + PX0 +
+                                   (p ? G::CW : 64) - 1]);
             }
         }
     }
@@ -1712,6 +1746,73 @@ typedef __attribute__((address_space(1))) uint64_t gu64;
 typedef __attribute__((address_space(1))) uint32_t gu32;
 DEV uint64_t ld_sc1(const void *p) { return __hip_atomic_load((gu64 *) p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 DEV void st_sc1(void *p, uint64_t v) { __hip_atomic_store((gu64 *) p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+// ------------------------------------------------------------- k_predd
+// The intra SBs of a level-scheduled phase (inter frames: their intra blocks read the
+// reconstructed pixels of the left / top / top-left SBs, the planner's dependency mask) in ONE
+// launch instead of one k_pred launch per dependency level (C5: ~5 per frame). The list is
+// the phase's level lists back to back (level order). Workgroups take list entries from a
+// ticket counter (ctr[0]) and take the next one when done, so an SB waits only on SBs of lower
+// levels held by running workgroups: no assumption about dispatch order. The grid is capped
+// (a waiting workgroup holds its CU slot: uncapped, C5's thousands of waiting SBs crowded the
+// other chain's kernels). An SB polls its producers' done flags (slot-indexed, sc1), then runs
+// pred_wg with sc1 halo loads; the producer wrote its right column and bottom row through
+// with sc1 stores and drained them (s_waitcnt vmcnt(0)) before its flag: the k_lfro row
+// hand-off's protocol. Waits are bounded (ctr[2] counts the ones given up: the batch fails
+// with VP9HIP_EBUG, like a k_lfr timeout); the last workgroup zeroes the flags and counters
+// for the next launch (graph replay). ctr: {ticket, finished workgroups, timeouts, spin bound}.
+template <typename PIX, class G>
+__global__ __launch_bounds__(64) void k_predd(const uint32_t *__restrict__ list, int n, const uint32_t *__restrict__ sbinfo,
+                                              const WGRec *__restrict__ wgs, const SBRec *__restrict__ sbs,
+                                              const PJob *__restrict__ jobs, const uint32_t *__restrict__ passes,
+                                              const FrameDesc *__restrict__ frames, const int16_t *__restrict__ resid,
+                                              const uint32_t *__restrict__ ptab, uint32_t *ctr, uint32_t *done, int dbg)
+{
+    static_assert(G::SH == 1 && G::SV == 1, "k_predd: 4:2:0");
+    __shared__ PredLds<PIX, G, true> S;
+    __shared__ uint32_t s_task, s_last;
+    const int lane = threadIdx.x;
+#if PRED_LTAB_LDS
+    load_ltab<PIX>(S.ltab, ptab, lane);
+#endif
+    const uint32_t spin = ctr[3] ? ctr[3] : (1u << 22);
+    for (;;) {
+        if (lane == 0) s_task = atomicAdd(&ctr[0], 1u);
+        wave_sync();
+        const uint32_t task = __builtin_amdgcn_readfirstlane(s_task);
+        if (task >= (uint32_t) n) break;
+        const uint32_t slot = __builtin_amdgcn_readfirstlane(list[task]);
+        const WGRec *wg = wgs + slot;
+        const uint32_t info = sbinfo[slot];
+        const SBRec sb = sbs[wg->sb[0]];
+        const uint32_t W = (uint32_t) frames[sb.frame].sb_cols;
+        // lanes 0 / 1 / 2: the left / top / top-left producer
+        uint32_t dep = ~0u;
+        if (lane == 0 && (info & 2) && sb.sbx > 0) dep = slot - 1;
+        if (lane == 1 && (info & 4) && sb.sby > 0) dep = slot - W;
+        if (lane == 2 && (info & 8) && sb.sbx > 0 && sb.sby > 0) dep = slot - W - 1;
+        for (uint32_t t = 0;; t++) {
+            const bool ok = dep == ~0u || __hip_atomic_load((gu32 *) &done[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+            if (__all(ok)) break;
+            if (t > spin) {
+                if (lane == 0) atomicAdd(&ctr[2], 1u);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        pred_wg<PIX, G, true, true>(wg, sbs, jobs, passes, frames, resid, ptab, S, lane, dbg);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_store((gu32 *) &done[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        wave_sync();                   // pred_wg's LDS reads before the next SB's tile writes
+    }
+    if (lane == 0) s_last = atomicAdd(&ctr[1], 1u) == gridDim.x - 1;
+    wave_sync();
+    if (__builtin_amdgcn_readfirstlane(s_last)) {
+        for (int i = lane; i < n; i += 64) done[list[i]] = 0;
+        if (lane == 0) { ctr[0] = 0; ctr[1] = 0; }
+    }
+}
 
 // row-LF pieces: chunk (p, r, k) of SB (sbx, sby) in its plane. Plane bases are offsets from
 // plane 0 chosen by selects (an indexed array of pointers would live in scratch).
@@ -2967,6 +3068,14 @@ static void launch_pred_p(int ss, hipStream_t st, int nwg, size_t pad, const uin
     default: launch_pred_g<PIX, Geo<0, 0>>(st, nwg, pad, list, wgs, sbs, jobs, passes, frames, resid, ptab, dbg); break;
     }
 }
+template <typename PIX>
+static void launch_predd_p(hipStream_t st, int n, int wgcap, const uint32_t *list, const uint32_t *sbinfo, const WGRec *wgs,
+                           const SBRec *sbs, const PJob *jobs, const uint32_t *passes, const FrameDesc *frames,
+                           const int16_t *resid, const uint32_t *ptab, uint32_t *ctr, uint32_t *done, int dbg)
+{
+    hipLaunchKernelGGL((k_predd<PIX, Geo<1, 1>>), dim3(std::min(n, wgcap)), dim3(64), 0, st, list, n, sbinfo, wgs, sbs, jobs,
+                       passes, frames, resid, ptab, ctr, done, dbg);
+}
 template <typename PIX, class G>
 static void launch_lf_g(hipStream_t st, int nsb, const uint32_t *list, const LFRec *recs, const FrameDesc *frames, int dbg)
 {
@@ -3126,6 +3235,17 @@ int vp9hip_launch_pred(int fmt, hipStream_t st, int nwg, const uint32_t *list, c
     const size_t pad = (size_t) ((dbg >> 8) & 255) * 1024;     // profiling: occupancy sweep via LDS padding
     if (fmt & 1) launch_pred_p<uint16_t>(fmt >> 1, st, nwg, pad, list, wgs, sbs, jobs, passes, frames, resid, ptab, dbg);
     else         launch_pred_p<uint8_t>(fmt >> 1, st, nwg, pad, list, wgs, sbs, jobs, passes, frames, resid, ptab, dbg);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+// k_predd (4:2:0 only: fmt bits 1..2 must be 3): n = the list length, wgcap the grid's cap
+int vp9hip_launch_predd(int fmt, hipStream_t st, int n, int wgcap, const uint32_t *list, const uint32_t *sbinfo, const WGRec *wgs,
+                        const SBRec *sbs, const PJob *jobs, const uint32_t *passes, const FrameDesc *frames,
+                        const int16_t *resid, const uint32_t *ptab, uint32_t *ctr, uint32_t *done, int dbg)
+{
+    if (n <= 0) return 0;
+    if ((fmt >> 1) != 3 || wgcap <= 0) return -1;
+    if (fmt & 1) launch_predd_p<uint16_t>(st, n, wgcap, list, sbinfo, wgs, sbs, jobs, passes, frames, resid, ptab, ctr, done, dbg);
+    else         launch_predd_p<uint8_t>(st, n, wgcap, list, sbinfo, wgs, sbs, jobs, passes, frames, resid, ptab, ctr, done, dbg);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int vp9hip_launch_lf(int fmt, hipStream_t st, int nsb, const uint32_t *list, const LFRec *recs,

@@ -53,6 +53,9 @@ int vp9hip_launch_pred(int fmt, hipStream_t st, int nwg, const uint32_t *list, c
                        const uint32_t *ptab, int dbg);
 int vp9hip_launch_lf(int fmt, hipStream_t st, int nsb, const uint32_t *list, const LFRec *recs,
                      const FrameDesc *frames, int dbg);
+int vp9hip_launch_predd(int fmt, hipStream_t st, int n, int wgcap, const uint32_t *list, const uint32_t *sbinfo, const WGRec *wgs,
+                        const SBRec *sbs, const PJob *jobs, const uint32_t *passes, const FrameDesc *frames,
+                        const int16_t *resid, const uint32_t *ptab, uint32_t *ctr, uint32_t *done, int dbg);
 int vp9hip_launch_mc(int hb, hipStream_t st, int n, const McUnit *units, const FrameDesc *frames, const KCfg *k);
 size_t vp9hip_plan_scan_bytes(size_t n);
 int vp9hip_plan_enqueue(hipStream_t st, const PlanDev *D, int ss, int nframes, int max_blk, int max_sb, uint32_t nb,
@@ -81,6 +84,7 @@ struct Launch { int kind; uint32_t off; uint32_t n; int arg; int grp; int ph; in
                 uint32_t off2 = 0, n2 = 0;
                 uint32_t roff[5] = { 0, 0, 0, 0, 0 }, rn[5] = { 0, 0, 0, 0, 0 };   // K_PLF residual jobs by tx code
                 int devr = 0;   // K_RESID of a static plan: off = the summary index of its job range, n = a bound
+                int flow = -1;  // K_PRED of a level phase as one k_predd launch: its counter block
 };
 #define PLF_LAG 3   // see the schedule in stage()
 // Residuals run inside the fused launches (one intra diagonal ahead) for phases of fewer
@@ -128,7 +132,8 @@ struct Staged {
     // record counts of the arena (the host images above are not kept for these)
     uint32_t n_sbs = 0, n_pjobs = 0, n_passes = 0, n_wgs = 0, n_rjobs = 0, n_lfs = 0, n_mcs = 0;
     uint32_t n_ctr = 0;                 // k_lfr counter words (zero between launches)
-    std::vector<uint32_t> lfr_ctr;      // counter block offset of every k_lfr launch
+    std::vector<uint32_t> lfr_ctr;      // counter block offset of every k_lfr / k_predd launch
+    uint32_t pdone = 0;                 // k_predd: slot-indexed intra done flags (counter words)
     uint8_t *pinned = nullptr;          // pinned host image of the arena (one DMA per stage)
     size_t pinned_cap = 0;
     // device arena
@@ -157,6 +162,7 @@ struct Staged {
         std::vector<double> pred_bytes, lf_bytes;             // per intra diagonal (intra frames) / LF diagonal
         uint32_t lfr_off = 0, lfr_n = 0;                      // k_lfr task table in the host lists
         int lfr_ctr = 0;
+        int pred_ctr = -1;                                    // k_predd counter block (level phases)
         double lfr_bytes = 0;
         int g_res = 0, g_mc = 0;                              // summary gather slots
     };
@@ -310,6 +316,11 @@ struct vp9hip_ctx {
     bool plan_only = false;             // VP9HIP_PLAN_ONLY=1: run the planner alone (diagnostics)
     bool plan_reuse = false;            // VP9HIP_PLAN_REUSE=1: a static-plan batch's reruns skip the planner
                                         // (its records are unchanged): the pixel launches alone (diagnostics)
+    bool pred_df = true;                // VP9HIP_PRED_DF=0: a level phase's intra SBs as one k_pred launch per level
+    int pred_df_wgs = 1024;             // VP9HIP_PRED_DF_WGS: k_predd grid cap (workgroups)
+    int pred_df_max = 1024;             // VP9HIP_PRED_DF_MAX: phases of more intra SBs keep level launches
+    bool pred_merge = false;            // VP9HIP_PRED_MERGE=1: a level phase's k_pred launches as one, the
+                                        // levels' order ignored (timing bound only: wrong pixels)
     int dl_threads = 3;                 // VP9HIP_DL_THREADS: download copy threads besides the caller
     Staged stg;                         // the current batch slot
     Staged sl[MAX_SLOTS];               // the other slots (sl[slot] is a moved-out placeholder;
@@ -410,6 +421,10 @@ static void read_config(vp9hip_ctx *c)
     c->plan_dbg = num("VP9HIP_PLAN_DBG", 0);
     c->plan_only = num("VP9HIP_PLAN_ONLY", 0) != 0;
     c->plan_reuse = num("VP9HIP_PLAN_REUSE", 0) != 0;
+    c->pred_merge = num("VP9HIP_PRED_MERGE", 0) != 0;
+    c->pred_df = num("VP9HIP_PRED_DF", 1) != 0;
+    c->pred_df_wgs = std::max(1, num("VP9HIP_PRED_DF_WGS", 1024));
+    c->pred_df_max = std::max(0, num("VP9HIP_PRED_DF_MAX", 1024));
     c->dl_threads = std::max(0, std::min(15, num("VP9HIP_DL_THREADS", 3)));
     c->test_reject = g_test_reject;
     c->lfr_spin = g_test_lfr_spin;
@@ -1217,6 +1232,11 @@ static int stage_dev(vp9hip_ctx *c, const DevIn &in)
         P.fused = (*in.res_fused)[ph];
         P.levels = (*in.lvl_ph)[ph];
         P.lfr = in.lfr_any && (c->lf_rows > 1 || (int) P.frames.size() < LFR_MAX_FRAMES);
+        if (P.levels && c->pred_df && c->ss_h && c->ss_v) {  // the phase's intra levels as one k_predd
+            P.pred_ctr = (int) s.n_ctr;
+            s.lfr_ctr.push_back(s.n_ctr);
+            s.n_ctr += 4;              // ticket, finished, timeouts, spin
+        }
         int nd = 0, nlfd = 0, nk = 0;
         for (int i : P.frames) {
             const FrameBuild &fb = fbs[i];
@@ -1334,6 +1354,9 @@ static int stage_dev(vp9hip_ctx *c, const DevIn &in)
             }
         }
     }
+    s.pdone = 0;
+    for (const Staged::DevPhase &P : s.dph)
+        if (P.pred_ctr >= 0) { s.pdone = s.n_ctr; s.n_ctr += NS; break; }
     s.nkey = keys;
     s.host_lists = (uint32_t) hl.size();
     s.n_gidx = (uint32_t) gidx.size();
@@ -1714,6 +1737,18 @@ static int plan_dev(vp9hip_ctx *c)
                 s.alg_bytes[K_LFR] += P.lfr_bytes;
             };
             if (!s.fuse || P.levels) {
+                // the level lists are back to back in level order: one k_predd launch when the
+                // phase has few intra SBs (its level launches are latency-bound); wide phases
+                // keep the level launches, which run every SB of a level at once (C5: its 8K
+                // frames' levels were faster than k_predd's capped grid, profiles/r05u)
+                // (VP9HIP_PRED_MERGE: one k_pred launch, timing bound only)
+                const uint32_t a = P.nkey ? step(0).first : 0, b = P.nkey ? step(P.nkey - 1).first + step(P.nkey - 1).second : 0;
+                if ((c->pred_merge || (P.pred_ctr >= 0 && b - a <= (uint32_t) c->pred_df_max)) && P.levels && P.nkey) {
+                    if (b > a) {
+                        push(K_PRED, a, b - a, 0, PART_RECON, 0);
+                        if (!c->pred_merge) s.launches.back().flow = P.pred_ctr;
+                    }
+                } else
                 for (int d = 0; d < P.nkey; d++)
                     if (step(d).second) push(K_PRED, step(d).first, step(d).second, 0, PART_RECON, d);
                 if (P.lfr) lfr();
@@ -2403,6 +2438,13 @@ static int launch_one(vp9hip_ctx *c, const Launch &L, hipStream_t st)
         return vp9hip_launch_resid(c->hb, st, L.arg, (int) L.n, (const RJob *) (s.arena + s.o_rjobs) + L.off, fr,
                                    s.arena + s.o_coefs, s.resid);
     case K_PRED:
+        if (L.flow >= 0)
+            return vp9hip_launch_predd(c->hb | c->ss_h << 1 | c->ss_v << 2, st, (int) L.n, c->pred_df_wgs, lists + L.off,
+                                       (const uint32_t *) (s.arena + s.o_sbinfo), (const WGRec *) (s.arena + s.o_wgs),
+                                       (const SBRec *) (s.arena + s.o_sbs), (const PJob *) (s.arena + s.o_pjobs),
+                                       (const uint32_t *) (s.arena + s.o_passes), fr, s.resid, c->ptab,
+                                       (uint32_t *) (s.arena + s.o_ctr) + L.flow, (uint32_t *) (s.arena + s.o_ctr) + s.pdone,
+                                       c->dbg);
         return vp9hip_launch_pred(c->hb | c->ss_h << 1 | c->ss_v << 2, st, (int) L.n, lists + L.off, (const WGRec *) (s.arena + s.o_wgs),
                                   (const SBRec *) (s.arena + s.o_sbs), (const PJob *) (s.arena + s.o_pjobs),
                                   (const uint32_t *) (s.arena + s.o_passes), fr, s.resid, c->ptab, c->dbg);

@@ -415,14 +415,18 @@ def test_loop_filter_schedules(v9, orc, monkeypatch, mode, bpp):
         dev.close()
 
 
-@pytest.mark.parametrize("levels,bpp,log2", [("1", 8, 0), ("0", 8, 0), ("1", 10, 1)])
-def test_inter_level_schedule(v9, orc, monkeypatch, levels, bpp, log2):
+@pytest.mark.parametrize("levels,bpp,log2,df", [("1", 8, 0, "1"), ("1", 8, 0, "0"), ("0", 8, 0, "1"),
+                                                 ("1", 10, 1, "1"), ("1", 10, 1, "0")])
+def test_inter_level_schedule(v9, orc, monkeypatch, levels, bpp, log2, df):
     """Inter frames' intra SBs scheduled by dependency level (VP9HIP_LEVELS=1, default):
     an SB runs once the intra SBs whose pixels its intra blocks read (left, top, top-left;
     vp9recon.c:71-121) have run; inter pixels (MC + residuals) are final before the first
     intra launch, and the loop filter is one k_lfr launch after them. A key + 4 P chain at a
-    size with 15 x 9 SBs (many intra blocks next to other SBs' intra blocks) and 2 chains."""
+    size with 15 x 9 SBs (many intra blocks next to other SBs' intra blocks) and 2 chains.
+    VP9HIP_PRED_DF=1 (default): a phase's levels in one k_predd launch (per-SB done flags),
+    0: one k_pred launch per level. Three runs: the graph replays reuse k_predd's counters."""
     monkeypatch.setenv("VP9HIP_LEVELS", levels)
+    monkeypatch.setenv("VP9HIP_PRED_DF", df)
     dev = v9.Device(0)
     try:
         w, h = 960, 544
@@ -441,7 +445,7 @@ def test_inter_level_schedule(v9, orc, monkeypatch, levels, bpp, log2):
         order = [0, 5, 1, 6, 2, 7, 3, 8, 4, 9]
         dev.configure(w, h, bpp, nbufs=10)
         dev.stage_batch([frames[i] for i in order], [outs[i] for i in order], [refs[i] for i in order])
-        for _ in range(2):
+        for _ in range(3):
             dev.run_batch()
             dev.sync()
         dec = {}
