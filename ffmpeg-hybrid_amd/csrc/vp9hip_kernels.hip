@@ -770,7 +770,10 @@ struct Chunk16 {
 // The SB interior (all planes) between HBM and the LDS tile in 16-byte chunks (16 px at
 // 8-bit, 8 at 16-bit): STORE = false loads (inter frames: MC prediction + inter residuals),
 // true stores the reconstructed SB. All loads of a lane are issued before its LDS writes.
-template <typename PIX, class G, bool STORE>
+typedef __attribute__((address_space(1))) uint64_t gpx64;
+// SC (stores only): written through with sc1 (intra workers inside k_lfro: its loader on
+// another XCD reads them in the same launch)
+template <typename PIX, class G, bool STORE, bool SC = false>
 DEV void sb_interior(const FrameDesc &fd, int sbx, int sby, int lane, PIX *tile)
 {
     constexpr int CPX = 16 / sizeof(PIX);
@@ -794,8 +797,15 @@ DEV void sb_interior(const FrameDesc &fd, int sbx, int sby, int lane, PIX *tile)
             if (c >= NT) break;
             PIX *g, *t;
             where(c, g, t);
-            if (STORE) *(uint4 *) g = Chunk16::from_lds(t);
-            else v[u] = *(const uint4 *) g;
+            if (STORE && SC) {
+                const uint4 w = Chunk16::from_lds(t);
+                __hip_atomic_store((gpx64 *) g, (uint64_t) w.x | (uint64_t) w.y << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store((gpx64 *) g + 1, (uint64_t) w.z | (uint64_t) w.w << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else if (STORE) {
+                *(uint4 *) g = Chunk16::from_lds(t);
+            } else {
+                v[u] = *(const uint4 *) g;
+            }
         }
         if (STORE) continue;
 #pragma unroll
@@ -1082,10 +1092,11 @@ DEV void load_ltab(uint32_t *ltab, const uint32_t *__restrict__ ptab, int lane)
 #define PRED_PROF 0
 #endif
 KP_DEV unsigned long long pred_prof[16];
-// Intra prediction of one workgroup record (the ltab copy must be loaded). HO (k_predd,
-// 4:2:0): the halo loads and the SB's own right column / bottom row (what the SBs to the
-// right and below read) go through sc1 as well.
-template <typename PIX, class G, bool LISTS, bool HO = false>
+// Intra prediction of one workgroup record (the ltab copy must be loaded). HO (4:2:0): the
+// halo loads are sc1, and 1 (k_predd): the SB's own right column / bottom row (what the SBs to
+// the right and below read) are written through again; 2 (intra workers inside k_lfro): its
+// whole interior is written through.
+template <typename PIX, class G, bool LISTS, int HO = 0>
 DEV void pred_wg(const WGRec *wgp, const SBRec *__restrict__ sbs, const PJob *__restrict__ jobs,
                  const uint32_t *__restrict__ passes, const FrameDesc *__restrict__ frames,
                  const int16_t *__restrict__ resid, const uint32_t *__restrict__ ptab, PredLds<PIX, G, LISTS> &S, int lane,
@@ -1124,7 +1135,7 @@ DEV void pred_wg(const WGRec *wgp, const SBRec *__restrict__ sbs, const PJob *__
         const uint32_t sbi = __builtin_amdgcn_readfirstlane(wgp->sb[k]);
         if (sbi != 0xffffffffu) {
             const SBRec sb = sbs[sbi];
-            if (!(dbg & 4)) load_sb_tile<PIX, G, HO>(frames[sb.frame], sb.sbx, sb.sby, sb.flags & 1, lane, tile + k * G::TILE);
+            if (!(dbg & 4)) load_sb_tile<PIX, G, HO != 0>(frames[sb.frame], sb.sbx, sb.sby, sb.flags & 1, lane, tile + k * G::TILE);
         }
     }
     if (PL::ON) {
@@ -1196,8 +1207,8 @@ DEV void pred_wg(const WGRec *wgp, const SBRec *__restrict__ sbs, const PJob *__
         if (sbi == 0xffffffffu) continue;
         const SBRec sb = sbs[sbi];
         const FrameDesc &fd = frames[sb.frame];
-        sb_interior<PIX, G, true>(fd, sb.sbx, sb.sby, lane, tile + k * G::TILE);
-        if constexpr (HO) {            // right column and bottom row again, written through
+        sb_interior<PIX, G, true, HO == 2>(fd, sb.sbx, sb.sby, lane, tile + k * G::TILE);
+        if constexpr (HO == 1) {       // right column and bottom row again, written through
             static_assert(G::SH == 1 && G::SV == 1, "k_predd: 4:2:0");
             const PIX *t = tile + k * G::TILE;
             PIX *gy = (PIX *) fd.plane[0];
@@ -1216,7 +1227,7 @@ DEV void pred_wg(const WGRec *wgp, const SBRec *__restrict__ sbs, const PJob *__
 #pragma unroll
             for (int i = lane; i < 64 + 2 * G::CH; i += 64) {
                 const int p = i < 64 ? 0 : i < 64 + G::CH ? 1 : 2, r = p == 0 ? i : p == 1 ? i - 64 : i - 64 - G::CH;
-                st_px<HO>(e + i, t[(p == 0 ? 0 : p == 1 ? LT_SIZE : LT_SIZE + G::CT) + (r + 1) * (p ? G::CP : LP) + PX0 +
+                st_px<HO != 0>(e + i, t[(p == 0 ? 0 : p == 1 ? LT_SIZE : LT_SIZE + G::CT) + (r + 1) * (p ? G::CP : LP) + PX0 +
                                    (p ? G::CW : 64) - 1]);
             }
         }
@@ -1801,7 +1812,7 @@ __global__ __launch_bounds__(64) void k_predd(const uint32_t *__restrict__ list,
             __builtin_amdgcn_s_sleep(2);
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        pred_wg<PIX, G, true, true>(wg, sbs, jobs, passes, frames, resid, ptab, S, lane, dbg);
+        pred_wg<PIX, G, true, 1>(wg, sbs, jobs, passes, frames, resid, ptab, S, lane, dbg);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0) __hip_atomic_store((gu32 *) &done[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         wave_sync();                   // pred_wg's LDS reads before the next SB's tile writes
@@ -2176,6 +2187,52 @@ __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfrd(const uint32_t *__res
 // written after a tile write and read before the tile read orders them; the fences are
 // compiler-only, wavefront scope). Every wait is bounded: one that gives up is counted in
 // ctr[2] like a hand-off timeout (the batch fails with VP9HIP_EBUG), never hangs.
+// One intra worker wave inside a k_lfro launch (LfrIntra): k_predd's ticket loop, whole
+// interiors written through (the LF loader reads them with sc1 loads in the same launch).
+// The last wave zeroes the tickets; the LF's last workgroup zeroes the done flags (it waited
+// for every one of them).
+template <typename PIX, class G>
+DEV void lfri_worker(const LfrIntra &li, const FrameDesc *__restrict__ frames, PredLds<PIX, G, true> &S, int lane)
+{
+#if PRED_LTAB_LDS
+    load_ltab<PIX>(S.ltab, li.ptab, lane);
+#endif
+    const uint32_t spin = li.pctr[3] ? li.pctr[3] : (1u << 22);
+    for (;;) {
+        uint32_t task = 0;
+        if (lane == 0) task = atomicAdd(&li.pctr[0], 1u);
+        task = __builtin_amdgcn_readfirstlane(task);
+        if (task >= (uint32_t) li.n) break;
+        const uint32_t slot = __builtin_amdgcn_readfirstlane(li.list[task]);
+        const WGRec *wg = li.wgs + slot;
+        const uint32_t info = li.sbinfo[slot];
+        const SBRec sb = li.sbs[wg->sb[0]];
+        const uint32_t W = (uint32_t) frames[sb.frame].sb_cols;
+        uint32_t dep = ~0u;
+        if (lane == 0 && (info & 2) && sb.sbx > 0) dep = slot - 1;
+        if (lane == 1 && (info & 4) && sb.sby > 0) dep = slot - W;
+        if (lane == 2 && (info & 8) && sb.sbx > 0 && sb.sby > 0) dep = slot - W - 1;
+        for (uint32_t t = 0;; t++) {
+            const bool ok = dep == ~0u || __hip_atomic_load((gu32 *) &li.done[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+            if (__all(ok)) break;
+            if (t > spin) {
+                if (lane == 0) atomicAdd(&li.pctr[2], 1u);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        pred_wg<PIX, G, true, 2>(wg, li.sbs, li.jobs, li.passes, frames, li.resid, li.ptab, S, lane, li.dbg);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_store((gu32 *) &li.done[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        wave_sync();
+    }
+    if (lane == 0 && atomicAdd(&li.pctr[1], 1u) == (uint32_t) (li.nblk * LFRI_WAVES) - 1) {
+        li.pctr[0] = 0;
+        li.pctr[1] = 0;
+    }
+}
+
 #define LFRO_NTH 512                              // R, H0, H1, C, L1, L2, S1, S2
 #define LFRO_NTB 3                                // LDS tiles: SB i + 3 reuses SB i's
 #ifndef LFRO_ROLES
@@ -2233,9 +2290,12 @@ DEV void lfro_store(const LDS &S, int tb, const LfrPlanes &P, int sbx, int sby, 
         if (m >> 6) lf_reg<8 * (k) + 8 - (C0)>(px, m >> 6, ev(2 * (k), m), bd);                          \
         if (in) lf_reg<8 * (k) + 12 - (C0)>(px, 1, ev(2 * (k) + 1, in), bd);                             \
     }
-template <typename PIX, class G>
+// FI: intra worker workgroups in front of the LF tasks (LfrIntra; a separate instantiation,
+// so the plain kernel keeps its registers and LDS)
+template <typename PIX, class G, bool FI>
 __global__ __launch_bounds__(LFRO_NTH) __attribute__((amdgpu_waves_per_eu(4))) void k_lfro(const uint32_t *__restrict__ tasks, const LFRec *__restrict__ recs,
-                                                   const FrameDesc *__restrict__ frames, uint32_t *ctr, int ntasks)
+                                                   const FrameDesc *__restrict__ frames, uint32_t *ctr, int ntasks,
+                                                   LfrIntra li)
 {
     static_assert(G::SH == 1 && G::SV == 1, "4:2:0: one chroma wave holds both planes' 32 lines");
     typedef LfP<PIX, G> L;
@@ -2243,11 +2303,22 @@ __global__ __launch_bounds__(LFRO_NTH) __attribute__((amdgpu_waves_per_eu(4))) v
     typedef LfrdN<PIX, G> N;
     constexpr int FLP = L::YP, FCP = L::UVP, CW = G::CW, CH = G::CH;
     constexpr int NUI = (N::NINT + 63) / 64, NUT = (N::NTOP + 63) / 64, NPW = (L::PROG / 4 + 63) / 64;
-    __shared__ LfrLds<PIX, G, LFRO_NTB> S;
-    __shared__ LfroSync F;
+    // the LF tiles, or (intra worker workgroups) LFRI_WAVES intra tiles
+    __shared__ union {
+        struct { LfrLds<PIX, G, LFRO_NTB> S; LfroSync F; } lf;
+        PredLds<PIX, G, true> pr[FI ? LFRI_WAVES : 1];
+    } U;
+    LfrLds<PIX, G, LFRO_NTB> &S = U.lf.S;
+    LfroSync &F = U.lf.F;
     __shared__ uint32_t s_task, s_last;
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    if constexpr (FI) {
+        if ((int) blockIdx.x < li.nblk) {         // an intra worker workgroup
+            if (w < LFRI_WAVES) lfri_worker<PIX, G>(li, frames, U.pr[w], lane);
+            return;
+        }
+    }
     // wave -> role (R 0, H0 1, H1 2, C 3, L1 4, L2 5, S1 6, S2 7), one nibble per wave; wave
     // w runs on SIMD w % 4 (-DLFRO_ROLES=...: another permutation, for A/B builds; pairing
     // each filtering wave with the lightest helper measured equal, profiles/r04l)
@@ -2380,15 +2451,42 @@ __global__ __launch_bounds__(LFRO_NTH) __attribute__((amdgpu_waves_per_eu(4))) v
         // have copied their left halos out of that tile; SB i + 1's loads are issued right after
         CT vi[NUI];
         uint32_t pwv[NPW];
+        constexpr bool intra = FI;
         auto issue = [&](int c, bool halo) {
+            if constexpr (intra) {
+                // intra workers in this launch: SB (r, c)'s own intra and its pre-LF readers'
+                // (LfrIntra), then sc1 loads of what they wrote through
+                const int dx = lane == 1 ? 1 : lane >= 2 ? lane - 3 : 0, dy = lane >= 2 ? 1 : 0;
+                uint32_t s = ~0u;
+                if (lane < 5 && c + dx >= 0 && c + dx < fd.sb_cols && sby + dy < fd.sb_rows) {
+                    s = T[4 + c - c0] + (uint32_t) (dy * fd.sb_cols + dx);
+                    if (!(li.sbinfo[s] & 1)) s = ~0u;
+                }
+                for (uint32_t t = 0;; t++) {
+                    const bool ok = s == ~0u || __hip_atomic_load((gu32 *) &li.done[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+                    if (__all(ok)) break;
+                    if (t > spin) {
+                        if (lane == 0) atomicAdd(&ctr[2], 1u);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
 #pragma unroll
             for (int u = 0; u < NUI; u++) {
                 const int ci = lane + 64 * u;
                 int pp, rr, kk;
                 lfrd_chunk<PIX, G>(ci, false, pp, rr, kk);
                 if (ci < N::NINT && (kk > 0 || halo)) {
-                    const v4u x = *(const gv4u *) lfr_addr<PIX, G>(P, c, sby, pp, rr, kk);
-                    vi[u] = make_uint4(x.x, x.y, x.z, x.w);
+                    const PIX *g = lfr_addr<PIX, G>(P, c, sby, pp, rr, kk);
+                    if constexpr (intra) {
+                        const uint64_t lo = ld_sc1(g), hi = ld_sc1((const char *) g + 8);
+                        vi[u] = make_uint4((uint32_t) lo, (uint32_t) (lo >> 32), (uint32_t) hi, (uint32_t) (hi >> 32));
+                    } else {
+                        const v4u x = *(const gv4u *) g;
+                        vi[u] = make_uint4(x.x, x.y, x.z, x.w);
+                    }
                 }
             }
             const LFRec &rc = recs[T[4 + c - c0]];
@@ -2529,6 +2627,8 @@ __global__ __launch_bounds__(LFRO_NTH) __attribute__((amdgpu_waves_per_eu(4))) v
         if (role == 5) { atomicAdd(&lfr_prof[9], wrow); atomicAdd(&lfr_prof[14], wfill); }
     }
     lfrd_retire(ctr, ntasks, tid, LFRO_NTH, &s_last);
+    if (FI && s_last)
+        for (int i = tid; i < li.n; i += LFRO_NTH) li.done[li.list[i]] = 0;
 #undef TLE
 }
 #undef LFRO_EDGE_WIDE
@@ -3083,13 +3183,18 @@ static void launch_lf_g(hipStream_t st, int nsb, const uint32_t *list, const LFR
 }
 template <typename PIX, class G>
 static void launch_lfr_g(hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs, const FrameDesc *frames, uint32_t *ctr,
-                         const KCfg &k)
+                         const KCfg &k, const LfrIntra &li)
 {
     if constexpr (G::SH == 1 && G::SV == 1) {
         // the band-overlapped k_lfro (4:2:0 default; KCfg::lfro = 0: k_lfrd). Measured
         // (profiles/r04l): C5 k_lfr 1,403 -> 1,021 us per 8K frame, C2 300 -> 238 us
         if (k.lfro) {
-            hipLaunchKernelGGL((k_lfro<PIX, G>), dim3(ntasks), dim3(LFRO_NTH), 0, st, tasks, recs, frames, ctr, ntasks);
+            if (li.nblk)
+                hipLaunchKernelGGL((k_lfro<PIX, G, true>), dim3(li.nblk + ntasks), dim3(LFRO_NTH), 0, st, tasks, recs, frames,
+                                   ctr, ntasks, li);
+            else
+                hipLaunchKernelGGL((k_lfro<PIX, G, false>), dim3(ntasks), dim3(LFRO_NTH), 0, st, tasks, recs, frames, ctr,
+                                   ntasks, li);
             return;
         }
     }
@@ -3097,13 +3202,13 @@ static void launch_lfr_g(hipStream_t st, int ntasks, const uint32_t *tasks, cons
 }
 template <typename PIX>
 static void launch_lfr_p(int ss, hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs, const FrameDesc *frames,
-                         uint32_t *ctr, const KCfg &k)
+                         uint32_t *ctr, const KCfg &k, const LfrIntra &li)
 {
     switch (ss) {
-    case 3: launch_lfr_g<PIX, Geo<1, 1>>(st, ntasks, tasks, recs, frames, ctr, k); break;
-    case 1: launch_lfr_g<PIX, Geo<1, 0>>(st, ntasks, tasks, recs, frames, ctr, k); break;
-    case 2: launch_lfr_g<PIX, Geo<0, 1>>(st, ntasks, tasks, recs, frames, ctr, k); break;
-    default: launch_lfr_g<PIX, Geo<0, 0>>(st, ntasks, tasks, recs, frames, ctr, k); break;
+    case 3: launch_lfr_g<PIX, Geo<1, 1>>(st, ntasks, tasks, recs, frames, ctr, k, li); break;
+    case 1: launch_lfr_g<PIX, Geo<1, 0>>(st, ntasks, tasks, recs, frames, ctr, k, li); break;
+    case 2: launch_lfr_g<PIX, Geo<0, 1>>(st, ntasks, tasks, recs, frames, ctr, k, li); break;
+    default: launch_lfr_g<PIX, Geo<0, 0>>(st, ntasks, tasks, recs, frames, ctr, k, li); break;
     }
 }
 template <typename PIX>
@@ -3258,22 +3363,22 @@ int vp9hip_launch_lf(int fmt, hipStream_t st, int nsb, const uint32_t *list, con
 }
 #endif
 int vp9hip_launch_lfr_8(int ss, hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs, const FrameDesc *frames,
-                        uint32_t *ctr, const KCfg &k);
+                        uint32_t *ctr, const KCfg &k, const LfrIntra &li);
 #if KP(2)
 int vp9hip_launch_lfr_8(int ss, hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs, const FrameDesc *frames,
-                        uint32_t *ctr, const KCfg &k)
+                        uint32_t *ctr, const KCfg &k, const LfrIntra &li)
 {
-    launch_lfr_p<uint8_t>(ss, st, ntasks, tasks, recs, frames, ctr, k);
+    launch_lfr_p<uint8_t>(ss, st, ntasks, tasks, recs, frames, ctr, k, li);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 #endif
 int vp9hip_launch_lfr_16(int ss, hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs, const FrameDesc *frames,
-                        uint32_t *ctr, const KCfg &k);
+                        uint32_t *ctr, const KCfg &k, const LfrIntra &li);
 #if KP(3)
 int vp9hip_launch_lfr_16(int ss, hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs, const FrameDesc *frames,
-                        uint32_t *ctr, const KCfg &k)
+                        uint32_t *ctr, const KCfg &k, const LfrIntra &li)
 {
-    launch_lfr_p<uint16_t>(ss, st, ntasks, tasks, recs, frames, ctr, k);
+    launch_lfr_p<uint16_t>(ss, st, ntasks, tasks, recs, frames, ctr, k, li);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 #endif
@@ -3302,11 +3407,15 @@ int vp9hip_launch_plf_16(int ss, hipStream_t st, const PlfLaunch *pl, const uint
 }
 #endif
 #if KP(0)
+// li: intra workers inside the launch (null or nblk = 0: none; k_lfro, 4:2:0 only)
 int vp9hip_launch_lfr(int fmt, hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs,
-                      const FrameDesc *frames, uint32_t *ctr, const KCfg *k)
+                      const FrameDesc *frames, uint32_t *ctr, const KCfg *k, const LfrIntra *li)
 {
     if (ntasks <= 0) return 0;
-    return (fmt & 1 ? vp9hip_launch_lfr_16 : vp9hip_launch_lfr_8)(fmt >> 1, st, ntasks, tasks, recs, frames, ctr, *k);
+    const LfrIntra none = {};
+    if (li && li->nblk && (!k->lfro || (fmt >> 1) != 3 || li->n <= 0)) return -1;
+    return (fmt & 1 ? vp9hip_launch_lfr_16 : vp9hip_launch_lfr_8)(fmt >> 1, st, ntasks, tasks, recs, frames, ctr, *k,
+                                                                  li && li->nblk ? *li : none);
 }
 int vp9hip_launch_plf(int fmt, hipStream_t st, const PlfLaunch *pl, const uint32_t *plist, const uint32_t *llist,
                       const WGRec *wgs, const SBRec *sbs, const PJob *jobs, const uint32_t *passes, const LFRec *recs,

@@ -62,7 +62,7 @@ int vp9hip_plan_enqueue(hipStream_t st, const PlanDev *D, int ss, int nframes, i
                         uint32_t nslots, uint32_t ncnt, int nk, const uint32_t *gidx, int ng, uint32_t *summary,
                         void *scan_tmp, size_t scan_bytes, int any_levels, int flags, int guard);
 int vp9hip_launch_lfr(int fmt, hipStream_t st, int ntasks, const uint32_t *tasks, const LFRec *recs,
-                      const FrameDesc *frames, uint32_t *ctr, const KCfg *k);
+                      const FrameDesc *frames, uint32_t *ctr, const KCfg *k, const LfrIntra *li);
 int vp9hip_launch_plf(int fmt, hipStream_t st, const PlfLaunch *pl, const uint32_t *plist, const uint32_t *llist,
                       const WGRec *wgs, const SBRec *sbs, const PJob *jobs, const uint32_t *passes, const LFRec *recs,
                       const RJob *rjobs, const FrameDesc *frames, const void *coefs, int16_t *resid, const uint32_t *ptab,
@@ -84,7 +84,8 @@ struct Launch { int kind; uint32_t off; uint32_t n; int arg; int grp; int ph; in
                 uint32_t off2 = 0, n2 = 0;
                 uint32_t roff[5] = { 0, 0, 0, 0, 0 }, rn[5] = { 0, 0, 0, 0, 0 };   // K_PLF residual jobs by tx code
                 int devr = 0;   // K_RESID of a static plan: off = the summary index of its job range, n = a bound
-                int flow = -1;  // K_PRED of a level phase as one k_predd launch: its counter block
+                int flow = -1;  // K_PRED of a level phase as one k_predd launch: its counter block;
+                                // K_LFR with the phase's intra SBs inside (off2 / n2 their list)
 };
 #define PLF_LAG 3   // see the schedule in stage()
 // Residuals run inside the fused launches (one intra diagonal ahead) for phases of fewer
@@ -163,6 +164,7 @@ struct Staged {
         uint32_t lfr_off = 0, lfr_n = 0;                      // k_lfr task table in the host lists
         int lfr_ctr = 0;
         int pred_ctr = -1;                                    // k_predd counter block (level phases)
+        bool all_lf = false;                                  // every frame of the phase is loop-filtered
         double lfr_bytes = 0;
         int g_res = 0, g_mc = 0;                              // summary gather slots
     };
@@ -319,6 +321,8 @@ struct vp9hip_ctx {
     bool pred_df = true;                // VP9HIP_PRED_DF=0: a level phase's intra SBs as one k_pred launch per level
     int pred_df_wgs = 1024;             // VP9HIP_PRED_DF_WGS: k_predd grid cap (workgroups)
     int pred_df_max = 1024;             // VP9HIP_PRED_DF_MAX: phases of more intra SBs keep level launches
+    bool pred_lf_fuse = true;           // VP9HIP_PRED_LF_FUSE=0: a phase's k_predd work as its own launch, not
+                                        // as intra workers inside the phase's k_lfro launch
     bool pred_merge = false;            // VP9HIP_PRED_MERGE=1: a level phase's k_pred launches as one, the
                                         // levels' order ignored (timing bound only: wrong pixels)
     int dl_threads = 3;                 // VP9HIP_DL_THREADS: download copy threads besides the caller
@@ -423,6 +427,7 @@ static void read_config(vp9hip_ctx *c)
     c->plan_reuse = num("VP9HIP_PLAN_REUSE", 0) != 0;
     c->pred_merge = num("VP9HIP_PRED_MERGE", 0) != 0;
     c->pred_df = num("VP9HIP_PRED_DF", 1) != 0;
+    c->pred_lf_fuse = num("VP9HIP_PRED_LF_FUSE", 1) != 0;
     c->pred_df_wgs = std::max(1, num("VP9HIP_PRED_DF_WGS", 1024));
     c->pred_df_max = std::max(0, num("VP9HIP_PRED_DF_MAX", 1024));
     c->dl_threads = std::max(0, std::min(15, num("VP9HIP_DL_THREADS", 3)));
@@ -1232,6 +1237,8 @@ static int stage_dev(vp9hip_ctx *c, const DevIn &in)
         P.fused = (*in.res_fused)[ph];
         P.levels = (*in.lvl_ph)[ph];
         P.lfr = in.lfr_any && (c->lf_rows > 1 || (int) P.frames.size() < LFR_MAX_FRAMES);
+        P.all_lf = true;
+        for (int i : P.frames) P.all_lf &= fbs[i].f->filter_level != 0;
         if (P.levels && c->pred_df && c->ss_h && c->ss_v) {  // the phase's intra levels as one k_predd
             P.pred_ctr = (int) s.n_ctr;
             s.lfr_ctr.push_back(s.n_ctr);
@@ -1730,9 +1737,15 @@ static int plan_dev(vp9hip_ctx *c)
                 const uint32_t k = P.key0 + (uint32_t) d;
                 return std::make_pair(H + ko[k], ko[k + 1] - ko[k]);
             };
+            uint32_t in_off = 0, in_n = 0;          // intra SBs inside the k_lfro launch
             auto lfr = [&]() {
                 if (!P.lfr) return;
                 push(K_LFR, P.lfr_off, P.lfr_n, (int) P.lfr_ctr, PART_LF, 0);
+                if (in_n) {
+                    s.launches.back().off2 = in_off;
+                    s.launches.back().n2 = in_n;
+                    s.launches.back().flow = P.pred_ctr;
+                }
                 s.alg_bytes[K_LF] -= P.lfr_bytes;
                 s.alg_bytes[K_LFR] += P.lfr_bytes;
             };
@@ -1744,7 +1757,12 @@ static int plan_dev(vp9hip_ctx *c)
                 // (VP9HIP_PRED_MERGE: one k_pred launch, timing bound only)
                 const uint32_t a = P.nkey ? step(0).first : 0, b = P.nkey ? step(P.nkey - 1).first + step(P.nkey - 1).second : 0;
                 if ((c->pred_merge || (P.pred_ctr >= 0 && b - a <= (uint32_t) c->pred_df_max)) && P.levels && P.nkey) {
-                    if (b > a) {
+                    if (b > a && !c->pred_merge && c->pred_lf_fuse && P.lfr && P.all_lf && c->kcfg.lfro) {
+                        // inside the phase's k_lfro launch (VP9HIP_PRED_LF_FUSE): the LF of an
+                        // SB starts once it and the SBs reading its pre-LF pixels are predicted
+                        in_off = a;
+                        in_n = b - a;
+                    } else if (b > a) {
                         push(K_PRED, a, b - a, 0, PART_RECON, 0);
                         if (!c->pred_merge) s.launches.back().flow = P.pred_ctr;
                     }
@@ -2365,7 +2383,8 @@ static bool same_launches(const std::vector<Launch> &a, const std::vector<Launch
     for (size_t i = 0; i < a.size(); i++) {
         const Launch &x = a[i], &y = b[i];
         if (x.kind != y.kind || x.off != y.off || x.n != y.n || x.arg != y.arg || x.grp != y.grp || x.ph != y.ph ||
-            x.part != y.part || x.off2 != y.off2 || x.n2 != y.n2 || x.devr != y.devr || memcmp(x.roff, y.roff, sizeof(x.roff)) ||
+            x.part != y.part || x.off2 != y.off2 || x.n2 != y.n2 || x.devr != y.devr || x.flow != y.flow ||
+            memcmp(x.roff, y.roff, sizeof(x.roff)) ||
             memcmp(x.rn, y.rn, sizeof(x.rn)))
             return false;
     }
@@ -2449,9 +2468,28 @@ static int launch_one(vp9hip_ctx *c, const Launch &L, hipStream_t st)
                                   (const SBRec *) (s.arena + s.o_sbs), (const PJob *) (s.arena + s.o_pjobs),
                                   (const uint32_t *) (s.arena + s.o_passes), fr, s.resid, c->ptab, c->dbg);
     case K_LFR:
+    {
+        LfrIntra li = {};
+        if (L.n2) {                    // the phase's intra SBs inside the launch
+            li.list = lists + L.off2;
+            li.sbinfo = (const uint32_t *) (s.arena + s.o_sbinfo);
+            li.wgs = (const WGRec *) (s.arena + s.o_wgs);
+            li.sbs = (const SBRec *) (s.arena + s.o_sbs);
+            li.jobs = (const PJob *) (s.arena + s.o_pjobs);
+            li.passes = (const uint32_t *) (s.arena + s.o_passes);
+            li.resid = s.resid;
+            li.ptab = c->ptab;
+            li.pctr = (uint32_t *) (s.arena + s.o_ctr) + L.flow;
+            li.done = (uint32_t *) (s.arena + s.o_ctr) + s.pdone;
+            li.n = (int) L.n2;
+            li.nblk = (int) std::min<uint32_t>((L.n2 + LFRI_WAVES - 1) / LFRI_WAVES,
+                                               (uint32_t) std::max(1, c->pred_df_wgs / LFRI_WAVES));
+            li.dbg = c->dbg;
+        }
         return vp9hip_launch_lfr(c->hb | c->ss_h << 1 | c->ss_v << 2, st, (int) L.n, lists + L.off,
                                  (const LFRec *) (s.arena + s.o_lfs), fr, (uint32_t *) (s.arena + s.o_ctr) + L.arg,
-                                 &c->kcfg);
+                                 &c->kcfg, &li);
+    }
     case K_LF:
         return vp9hip_launch_lf(c->hb | c->ss_h << 1 | c->ss_v << 2, st, (int) L.n, lists + L.off, (const LFRec *) (s.arena + s.o_lfs), fr, c->dbg >> 16);
     case K_PLF: {

@@ -173,4 +173,25 @@ typedef struct KCfg {
     int mcq_slices;           /* k_mcq task slices per unit group; 0: from the grid size         */
 } KCfg;
 
+/* A level phase's intra SBs inside its k_lfro launch (VP9HIP_PRED_LF_FUSE): the first nblk
+ * workgroups are intra workers (LFRI_WAVES waves each, every wave k_predd's loop over the
+ * list's tickets), the rest the row-LF tasks. The LF loader waits, before it loads SB (r, c),
+ * for the done flags of (r, c) (its pixels) and of (r, c + 1), (r + 1, c - 1 .. c + 1) (they
+ * read its pre-LF pixels), and loads the interior with sc1 loads (the workers write whole
+ * interiors through). nblk = 0: none. */
+typedef struct LfrIntra {
+    const uint32_t *list;     /* the phase's level lists back to back: slots                     */
+    const uint32_t *sbinfo;   /* per slot: bit 0 has intra jobs, bits 1-3 the producer mask      */
+    const WGRec *wgs;
+    const SBRec *sbs;
+    const PJob *jobs;
+    const uint32_t *passes;
+    const int16_t *resid;
+    const uint32_t *ptab;
+    uint32_t *pctr;           /* {ticket, finished waves, timeouts, spin}                        */
+    uint32_t *done;           /* slot-indexed done flags                                        */
+    int n, nblk, dbg;
+} LfrIntra;
+#define LFRI_WAVES 4
+
 #endif

@@ -415,18 +415,23 @@ def test_loop_filter_schedules(v9, orc, monkeypatch, mode, bpp):
         dev.close()
 
 
-@pytest.mark.parametrize("levels,bpp,log2,df", [("1", 8, 0, "1"), ("1", 8, 0, "0"), ("0", 8, 0, "1"),
-                                                 ("1", 10, 1, "1"), ("1", 10, 1, "0")])
-def test_inter_level_schedule(v9, orc, monkeypatch, levels, bpp, log2, df):
+@pytest.mark.parametrize("levels,bpp,log2,df,fuse", [("1", 8, 0, "1", "0"), ("1", 8, 0, "0", "0"),
+                                                      ("0", 8, 0, "1", "0"), ("1", 10, 1, "1", "0"),
+                                                      ("1", 10, 1, "0", "0"), ("1", 8, 0, "1", "1"),
+                                                      ("1", 10, 1, "1", "1")])
+def test_inter_level_schedule(v9, orc, monkeypatch, levels, bpp, log2, df, fuse):
     """Inter frames' intra SBs scheduled by dependency level (VP9HIP_LEVELS=1, default):
     an SB runs once the intra SBs whose pixels its intra blocks read (left, top, top-left;
     vp9recon.c:71-121) have run; inter pixels (MC + residuals) are final before the first
     intra launch, and the loop filter is one k_lfr launch after them. A key + 4 P chain at a
     size with 15 x 9 SBs (many intra blocks next to other SBs' intra blocks) and 2 chains.
     VP9HIP_PRED_DF=1 (default): a phase's levels in one k_predd launch (per-SB done flags),
-    0: one k_pred launch per level. Three runs: the graph replays reuse k_predd's counters."""
+    0: one k_pred launch per level; VP9HIP_PRED_LF_FUSE=1: the k_predd work as intra worker
+    workgroups inside the phase's k_lfro launch, whose loader waits per SB for their flags.
+    Three runs: the graph replays reuse the counters and flags."""
     monkeypatch.setenv("VP9HIP_LEVELS", levels)
     monkeypatch.setenv("VP9HIP_PRED_DF", df)
+    monkeypatch.setenv("VP9HIP_PRED_LF_FUSE", fuse)
     dev = v9.Device(0)
     try:
         w, h = 960, 544

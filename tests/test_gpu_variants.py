@@ -4,7 +4,8 @@ launch per transform size (VP9HIP_RESID_MULTI=0), and intra SBs reading their le
 neighbour's column from the frame rows instead of the saved SB edges (VP9HIP_EDGE=0, also on
 the C3 keyframe shape); inter frames' intra levels as one k_pred launch per level instead of
 k_predd (VP9HIP_PRED_DF=0), k_predd on the 8K phases too (VP9HIP_PRED_DF_MAX) and with a
-3-workgroup grid that loops over every ticket (VP9HIP_PRED_DF_WGS=3). Each is switched (read when the context opens) on a key + P chain of
+3-workgroup grid that loops over every ticket (VP9HIP_PRED_DF_WGS=3), and the k_predd work
+inside the k_lfro launch (VP9HIP_PRED_LF_FUSE=1; with DF_WGS=4: one intra worker workgroup). Each is switched (read when the context opens) on a key + P chain of
 the C2 (1080p 8-bit) or C5 (8K 10-bit) shape, decoded through the bench's batch path and
 compared with the CPU oracle. (The losing alternates of rounds 1-4 -- the single-tile row LF,
 k_mc / k_mcp, MC tickets inside k_lfrd -- were removed in round 5; DESIGN.md §5 keeps
@@ -32,6 +33,9 @@ CASES = [
     ({"VP9HIP_PRED_DF": "0"}, "C2", 4),
     ({"VP9HIP_PRED_DF_MAX": "100000"}, "C5", 2),
     ({"VP9HIP_PRED_DF_WGS": "3"}, "C2", 4),
+    ({"VP9HIP_PRED_LF_FUSE": "1"}, "C2", 4),
+    ({"VP9HIP_PRED_LF_FUSE": "1", "VP9HIP_PRED_DF_MAX": "100000"}, "C5", 2),
+    ({"VP9HIP_PRED_LF_FUSE": "1", "VP9HIP_PRED_DF_WGS": "4"}, "C2", 4),
 ]
 
 
