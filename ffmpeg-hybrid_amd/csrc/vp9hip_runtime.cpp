@@ -323,8 +323,6 @@ struct vp9hip_ctx {
     int pred_df_max = 1024;             // VP9HIP_PRED_DF_MAX: phases of more intra SBs keep level launches
     bool pred_lf_fuse = true;           // VP9HIP_PRED_LF_FUSE=0: a phase's k_predd work as its own launch, not
                                         // as intra workers inside the phase's k_lfro launch
-    bool pred_merge = false;            // VP9HIP_PRED_MERGE=1: a level phase's k_pred launches as one, the
-                                        // levels' order ignored (timing bound only: wrong pixels)
     int dl_threads = 3;                 // VP9HIP_DL_THREADS: download copy threads besides the caller
     Staged stg;                         // the current batch slot
     Staged sl[MAX_SLOTS];               // the other slots (sl[slot] is a moved-out placeholder;
@@ -425,7 +423,6 @@ static void read_config(vp9hip_ctx *c)
     c->plan_dbg = num("VP9HIP_PLAN_DBG", 0);
     c->plan_only = num("VP9HIP_PLAN_ONLY", 0) != 0;
     c->plan_reuse = num("VP9HIP_PLAN_REUSE", 0) != 0;
-    c->pred_merge = num("VP9HIP_PRED_MERGE", 0) != 0;
     c->pred_df = num("VP9HIP_PRED_DF", 1) != 0;
     c->pred_lf_fuse = num("VP9HIP_PRED_LF_FUSE", 1) != 0;
     c->pred_df_wgs = std::max(1, num("VP9HIP_PRED_DF_WGS", 1024));
@@ -1754,17 +1751,16 @@ static int plan_dev(vp9hip_ctx *c)
                 // phase has few intra SBs (its level launches are latency-bound); wide phases
                 // keep the level launches, which run every SB of a level at once (C5: its 8K
                 // frames' levels were faster than k_predd's capped grid, profiles/r05u)
-                // (VP9HIP_PRED_MERGE: one k_pred launch, timing bound only)
                 const uint32_t a = P.nkey ? step(0).first : 0, b = P.nkey ? step(P.nkey - 1).first + step(P.nkey - 1).second : 0;
-                if ((c->pred_merge || (P.pred_ctr >= 0 && b - a <= (uint32_t) c->pred_df_max)) && P.levels && P.nkey) {
-                    if (b > a && !c->pred_merge && c->pred_lf_fuse && P.lfr && P.all_lf && c->kcfg.lfro) {
+                if (P.pred_ctr >= 0 && b - a <= (uint32_t) c->pred_df_max && P.levels && P.nkey) {
+                    if (b > a && c->pred_lf_fuse && P.lfr && P.all_lf && c->kcfg.lfro) {
                         // inside the phase's k_lfro launch (VP9HIP_PRED_LF_FUSE): the LF of an
                         // SB starts once it and the SBs reading its pre-LF pixels are predicted
                         in_off = a;
                         in_n = b - a;
                     } else if (b > a) {
                         push(K_PRED, a, b - a, 0, PART_RECON, 0);
-                        if (!c->pred_merge) s.launches.back().flow = P.pred_ctr;
+                        s.launches.back().flow = P.pred_ctr;
                     }
                 } else
                 for (int d = 0; d < P.nkey; d++)
