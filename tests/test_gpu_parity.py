@@ -415,11 +415,11 @@ def test_loop_filter_schedules(v9, orc, monkeypatch, mode, bpp):
         dev.close()
 
 
-@pytest.mark.parametrize("levels,bpp,log2,df,fuse", [("1", 8, 0, "1", "0"), ("1", 8, 0, "0", "0"),
-                                                      ("0", 8, 0, "1", "0"), ("1", 10, 1, "1", "0"),
-                                                      ("1", 10, 1, "0", "0"), ("1", 8, 0, "1", "1"),
-                                                      ("1", 10, 1, "1", "1")])
-def test_inter_level_schedule(v9, orc, monkeypatch, levels, bpp, log2, df, fuse):
+@pytest.mark.parametrize("levels,bpp,log2,df,fuse,nolf", [("1", 8, 0, "1", "0", 0), ("1", 8, 0, "0", "0", 0),
+                                                           ("0", 8, 0, "1", "0", 0), ("1", 10, 1, "1", "0", 0),
+                                                           ("1", 10, 1, "0", "0", 0), ("1", 8, 0, "1", "1", 0),
+                                                           ("1", 10, 1, "1", "1", 0), ("1", 8, 0, "1", "1", 1)])
+def test_inter_level_schedule(v9, orc, monkeypatch, levels, bpp, log2, df, fuse, nolf):
     """Inter frames' intra SBs scheduled by dependency level (VP9HIP_LEVELS=1, default):
     an SB runs once the intra SBs whose pixels its intra blocks read (left, top, top-left;
     vp9recon.c:71-121) have run; inter pixels (MC + residuals) are final before the first
@@ -428,7 +428,8 @@ def test_inter_level_schedule(v9, orc, monkeypatch, levels, bpp, log2, df, fuse)
     VP9HIP_PRED_DF=1 (default): a phase's levels in one k_predd launch (per-SB done flags),
     0: one k_pred launch per level; VP9HIP_PRED_LF_FUSE=1: the k_predd work as intra worker
     workgroups inside the phase's k_lfro launch, whose loader waits per SB for their flags.
-    Three runs: the graph replays reuse the counters and flags."""
+    Three runs: the graph replays reuse the counters and flags. nolf: chain 0's third frame
+    is not loop-filtered (its phase takes the k_predd launch, the others the fused one)."""
     monkeypatch.setenv("VP9HIP_LEVELS", levels)
     monkeypatch.setenv("VP9HIP_PRED_DF", df)
     monkeypatch.setenv("VP9HIP_PRED_LF_FUSE", fuse)
@@ -443,6 +444,8 @@ def test_inter_level_schedule(v9, orc, monkeypatch, levels, bpp, log2, df, fuse)
             refs.append(None)
             for k in range(1, 5):
                 kw = {"compound": 1} if k == 3 else {}
+                if nolf and c == 0 and k == 2:
+                    kw["filter_level"] = 0
                 frames.append(v9.SynthFrame(v9.synth_params(w, h, bpp, seed=701 + 10 * c + k, inter=1,
                                                             log2_tile_cols=log2, **kw)))
                 outs.append(base + k)
