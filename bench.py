@@ -37,6 +37,10 @@ CONFIGS = {
     "C4": (3, 3840, 2160, 10, 2, 1, 120),
     "C5": (4, 7680, 4320, 10, 3, 32, 60),
 }
+# GOP-chain shapes whose step is chain latency: more batches in flight (the default line's
+# depth), each on one stream, so the 4 slots map onto the 4 hardware queues (profiles/r05z)
+INFLIGHT = {"C2": 4}
+
 W, H, BPP, LOG2_TILE_COLS = 3840, 2160, 8, 2
 CONFIG_INDEX = 2               # C3
 CHROMA = {"420": (1, 1), "422": (1, 0), "440": (0, 1), "444": (0, 0)}   # (ss_h, ss_v)
@@ -133,11 +137,14 @@ def main():
                     help="per-launch HIP events inside the timed steps (no graph replay)")
     ap.add_argument("--chroma", choices=sorted(CHROMA), default="420",
                     help="chroma format (profiles 1/3: 422, 440, 444); the BASELINE configs are 4:2:0")
-    ap.add_argument("--inflight", type=int, default=2, choices=[1, 2, 3, 4],
+    ap.add_argument("--inflight", type=int, default=None, choices=[1, 2, 3, 4],
                     help="batches in flight: that many of the context's batch slots (VP9HIP_MAX_SLOTS) hold the same workload and "
-                         "alternate steps; each slot runs on HIP streams of its own, so the two batches run "
+                         "alternate steps; each slot runs on HIP streams of its own, so the batches run "
                          "concurrently (as the decoder loop and the FFHWAccel adapter run them). Measured "
-                         "with per-slot streams (profiles/r03g): C2 7,778 vs 4,485 fps at 1, C5 761 vs 593")
+                         "with per-slot streams (profiles/r03g): C2 7,778 vs 4,485 fps at 1, C5 761 vs 593. "
+                         "Default: 4 for C2 (one stream per slot: the 4 slots on the 4 hardware queues; "
+                         "profiles/r05z: 17,598-17,786 vs 13,752-13,815 fps at 2), 2 otherwise (C3 loses "
+                         "at 3-4, C5 within 3 %%)")
     ap.add_argument("--shard", choices=["frames", "tiles"], default="frames",
                     help="frames: every rank decodes its own stream (weak scaling, default); tiles: all ranks "
                          "decode ONE stream, each its tile columns, pre-LF stripes all-gathered (strong scaling)")
@@ -151,6 +158,8 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("gloo")
 
+    if args.inflight is None:
+        args.inflight = INFLIGHT.get(args.config, 2)
     v = importlib.import_module("ffmpeg-hybrid_amd")
     if args.shard == "tiles":
         return bench_tiles(args, v, dist, world, rank, local_rank)
@@ -162,7 +171,16 @@ def main():
     frames, refs, geom = make_frames(v, args.config, args.frames, rank, args.chroma)
     t_gen = time.time() - t0
 
-    dev = v.Device(_device_of(local_rank))
+    # at the INFLIGHT depth: one frame-group stream per slot (VP9HIP_STREAMS, read when the
+    # context opens; an explicit setting wins), for this context only
+    one_stream = INFLIGHT.get(args.config) == args.inflight and "VP9HIP_STREAMS" not in os.environ
+    if one_stream:
+        os.environ["VP9HIP_STREAMS"] = "1"
+    try:
+        dev = v.Device(_device_of(local_rank))
+    finally:
+        if one_stream:
+            del os.environ["VP9HIP_STREAMS"]
     dev.configure(W, H, BPP, nbufs=args.frames * args.inflight, ss_h=ssh, ss_v=ssv)
     t0 = time.time()
     dev.stage_batch(frames, list(range(args.frames)), None if gop == 1 else refs)
