@@ -38,9 +38,8 @@ CONFIGS = {
     "C5": (4, 7680, 4320, 10, 3, 32, 60),
 }
 # Batches in flight of the default lines, each slot on ONE frame-group stream so the slots'
-# streams fit the 4 hardware queues (profiles/r05z): C2 (GOP-chain latency) 4, C3 / C4 3;
-# C5 2 slots of 2 streams
-INFLIGHT = {"C2": 4, "C3": 3, "C4": 3}
+# streams fit the 4 hardware queues (profiles/r05z): C2 (GOP-chain latency) 4, the others 3
+INFLIGHT = {"C2": 4, "C3": 3, "C4": 3, "C5": 3}
 
 W, H, BPP, LOG2_TILE_COLS = 3840, 2160, 8, 2
 CONFIG_INDEX = 2               # C3
@@ -143,9 +142,9 @@ def main():
                          "alternate steps; each slot runs on HIP streams of its own, so the batches run "
                          "concurrently (as the decoder loop and the FFHWAccel adapter run them). Measured "
                          "with per-slot streams (profiles/r03g): C2 7,778 vs 4,485 fps at 1, C5 761 vs 593. "
-                         "Default: 4 for C2, 3 for C3 / C4, each slot on one stream (the slots on the 4 "
+                         "Default: 4 for C2, 3 for C3 / C4 / C5, each slot on one stream (the slots on the 4 "
                          "hardware queues; profiles/r05z: C2 17,598-17,786 vs 13,752-13,815 fps at 2, C3 "
-                         "11,205 vs 10,821, C4 8,554 vs 8,380), 2 for C5 (within 3 %%)")
+                         "11,205 vs 10,821, C4 8,554 vs 8,380, C5 1,316-1,329 vs 1,286-1,304)")
     ap.add_argument("--shard", choices=["frames", "tiles"], default="frames",
                     help="frames: every rank decodes its own stream (weak scaling, default); tiles: all ranks "
                          "decode ONE stream, each its tile columns, pre-LF stripes all-gathered (strong scaling)")
