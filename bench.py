@@ -37,15 +37,20 @@ CONFIGS = {
     "C4": (3, 3840, 2160, 10, 2, 1, 120),
     "C5": (4, 7680, 4320, 10, 3, 32, 60),
 }
-# Batches in flight of the default lines, each slot on ONE frame-group stream so the slots'
-# streams fit the 4 hardware queues (profiles/r05z): C2 (GOP-chain latency) 4, the others 3
+# Batches in flight of the default lines, each slot on ONE frame-group stream (the library
+# default, VP9HIP_STREAMS = 1) so the slots' streams fit the 4 hardware queues
+# (profiles/r05z): C3 / C4 / C5 at 3 = VP9HIP_PIPELINE_SLOTS, the depth the decoder and the
+# FFHWAccel adapter run; C2 (GOP-chain latency) at 4 = VP9HIP_MAX_SLOTS
 INFLIGHT = {"C2": 4, "C3": 3, "C4": 3, "C5": 3}
 
 W, H, BPP, LOG2_TILE_COLS = 3840, 2160, 8, 2
 CONFIG_INDEX = 2               # C3
 CHROMA = {"420": (1, 1), "422": (1, 0), "440": (0, 1), "444": (0, 0)}   # (ss_h, ss_v)
 SEED0 = 0x56503900 + CONFIG_INDEX
-TRAFFIC_PROFILE = "r05zz/C3"     # rocprofv3 PMC passes of the default C3 bench (tools/profile.sh)
+# rocprofv3 passes of the default C3 bench's serialised timing steps (tools/profile.sh with
+# --serial-only): the kernel trace the roofline's launch duration is checked against, and
+# the PMC passes its traffic / issue fields come from
+TRAFFIC_PROFILE = "r06a/C3"
 POISON = 0xA5                  # fill byte of the frame buffers before the timed steps
 
 
@@ -102,6 +107,27 @@ def compare_frame(v, got, ref, geom, chroma="420"):
                for a, b in zip(v.visible(got, W, H, ssh, ssv), v.visible(ref, W, H, ssh, ssv)))
 
 
+def stage_slots(dev, frames, refs, gop, inflight):
+    """The bench's staging: the same workload into `inflight` batch slots, slot k writing
+    buffers k * n .. k * n + n - 1 (its references shifted alike); slot 0 selected after."""
+    n = len(frames)
+    for k in range(inflight):
+        dev.set_slot(k)
+        dev.stage_batch(frames, [k * n + i for i in range(n)],
+                        None if gop == 1 else [None if r is None else tuple(k * n + x for x in r) for r in refs])
+    dev.set_slot(0)
+
+
+def run_slots(dev, steps, inflight, start=0):
+    """The timed loop: steps run_batch calls rotating over the slots (each replays its HIP
+    graph: device planning, then the pixel kernels), with no host wait between them."""
+    for k in range(start, start + steps):
+        dev.set_slot(k % inflight)
+        dev.run_batch()
+        if inflight == 1:
+            dev.sync()
+
+
 def reduce_elapsed(elapsed, dist):
     """Max over ranks of the timed region (the slowest rank defines the job time)."""
     if dist is None:
@@ -133,6 +159,9 @@ def main():
                     help="at 1 GPU: compare only the first N frames (decode order) of each slot with the oracle")
     ap.add_argument("--verify-frames-per-rank", type=int, default=2,
                     help="at N > 1 GPUs: the frames per slot every rank compares with the oracle")
+    ap.add_argument("--serial-only", action="store_true",
+                    help="profiling runs (tools/profile.sh): only the serialised timing steps the roofline's "
+                         "launch durations come from (every launch of the batch on one stream), then a summary line")
     ap.add_argument("--timed-events", action="store_true",
                     help="per-launch HIP events inside the timed steps (no graph replay)")
     ap.add_argument("--chroma", choices=sorted(CHROMA), default="420",
@@ -171,26 +200,12 @@ def main():
     frames, refs, geom = make_frames(v, args.config, args.frames, rank, args.chroma)
     t_gen = time.time() - t0
 
-    # at the INFLIGHT depth: one frame-group stream per slot (VP9HIP_STREAMS, read when the
-    # context opens; an explicit setting wins), for this context only
-    one_stream = INFLIGHT.get(args.config) == args.inflight and "VP9HIP_STREAMS" not in os.environ
-    if one_stream:
-        os.environ["VP9HIP_STREAMS"] = "1"
-    try:
-        dev = v.Device(_device_of(local_rank))
-    finally:
-        if one_stream:
-            del os.environ["VP9HIP_STREAMS"]
+    # the library's defaults: one frame-group stream per batch slot (VP9HIP_STREAMS unset)
+    dev = v.Device(_device_of(local_rank))
     dev.configure(W, H, BPP, nbufs=args.frames * args.inflight, ss_h=ssh, ss_v=ssv)
     t0 = time.time()
-    dev.stage_batch(frames, list(range(args.frames)), None if gop == 1 else refs)
-    t_stage = time.time() - t0
-    # slot 1: the same workload into the second half of the frame buffers
-    for k in range(1, args.inflight):
-        dev.set_slot(k)
-        dev.stage_batch(frames, [k * args.frames + i for i in range(args.frames)],
-                        None if gop == 1 else [None if r is None else tuple(k * args.frames + x for x in r) for r in refs])
-    dev.set_slot(0)
+    stage_slots(dev, frames, refs, gop, args.inflight)
+    t_stage = (time.time() - t0) / args.inflight
 
     def barrier():
         if dist is not None:
@@ -210,11 +225,19 @@ def main():
             a[0] += ms
             a[1] += n
 
+    if args.serial_only:
+        kl = {k: int(ksum[k][1] / args.steps) for k in ksum}
+        print(json.dumps({"metric": "serial timing steps only (profiling run)", "serial_only": True,
+                          "config": {"workload": args.config, "frames_per_gpu": args.frames,
+                                     "streams_per_gpu": dev.groups(), "batches_in_flight": 1},
+                          "roofline": {"kernel_ms": {k: round(ksum[k][0] / args.steps, 3) for k in ksum},
+                                       "kernel_launches": kl}}), flush=True)
+        dev.close()
+        return
+
     # timed steps: the batch's launch sequence replayed as one HIP graph
     dev.set_timing(args.timed_events)
-    for k in range(args.warmup * args.inflight):
-        dev.set_slot(k % args.inflight)
-        dev.run_batch()
+    run_slots(dev, args.warmup * args.inflight, args.inflight)
     dev.sync()
     # poison every frame buffer of both slots: the frames verified below can only have been
     # written by the timed steps (a replay that did nothing would leave the poison byte)
@@ -222,12 +245,8 @@ def main():
     dev.sync()
     barrier()
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        dev.set_slot(k % args.inflight)
-        dev.run_batch()            # device planning (waits for its summary), then the pixel kernels
-        if args.inflight == 1:
-            dev.sync()
-    dev.sync()                     # every slot's work is on the main stream; checks both slots
+    run_slots(dev, args.steps, args.inflight)
+    dev.sync()                     # every slot's work; checks every slot
     barrier()
     elapsed = time.perf_counter() - t0
     dev.set_slot(0)
@@ -272,6 +291,20 @@ def main():
             traffic, traffic_src = round(per["traffic_bytes"]), "profiles/%s/traffic.json" % TRAFFIC_PROFILE
         elif shape_note:
             traffic_src = shape_note
+    # the same launches' durations under the committed rocprofv3 kernel trace of those
+    # serialised steps (profiles/<P>/kernel_stats.csv): the profile figure `frac` must agree with
+    trace = None
+    kf = os.path.join(ROOT, "profiles", TRAFFIC_PROFILE, "kernel_stats.csv")
+    if os.path.exists(kf) and shape_ok:
+        import csv
+        for r in csv.DictReader(open(kf)):
+            if r["Name"].split("(")[0].split("<")[0].split()[-1] == dom:
+                t_us = float(r["AverageNs"]) / 1000.0
+                t_frac = bytes_per_launch / (t_us * 1e-6) / 1e9 / HBM_PEAK_GBS
+                trace = {"avg_launch_us": round(t_us, 2), "calls": int(r["Calls"]), "frac": round(t_frac, 5),
+                         "frac_ratio": round(achieved / HBM_PEAK_GBS / t_frac, 4) if t_frac else None,
+                         "source": "profiles/%s/kernel_stats.csv" % TRAFFIC_PROFILE}
+                break
     # instruction issue of the same kernel from the committed SQ pass (profiles/<P>/pmc_summary.txt):
     # VALU wave-instructions per launch / its mean duration there, vs the VALU issue peak:
     # 256 CUs x 4 SIMD-32s, each issuing one wave64 VALU instruction per 2 cycles at 2.4 GHz
@@ -304,10 +337,14 @@ def main():
         # algorithmic bytes of a step / the sum of its serialised kernel durations (planner included)
         "all_kernels_frac": round(frame_bytes * args.frames / (kernel_ms_step / 1000.0) / 1e9 / HBM_PEAK_GBS, 5)
         if kernel_ms_step > 0 else None,
-        "launch_time_note": "HIP-event launch durations with every launch of the batch on one stream "
-                            "(serialised, as under a rocprofv3 kernel trace), in separate steps of the same "
-                            "batch with launches enqueued individually; the timed steps replay a HIP graph "
-                            "with the %d frame groups on concurrent streams" % streams,
+        "launch_time_note": "avg_launch_us: HIP-event durations of the kernel's launches in separate steps of "
+                            "slot 0's batch with every launch on one stream, enqueued one by one (each launch "
+                            "alone on the GPU); trace: the same serialised steps under rocprofv3 --kernel-trace "
+                            "(bench.py --serial-only, tools/profile.sh). The timed steps replay HIP graphs of "
+                            "%d batch slots concurrently (%d frame-group stream(s) each), where launches of "
+                            "different slots overlap and a trace's durations include the overlap"
+                            % (args.inflight, streams),
+        "trace": trace,
         "kernel_ms": {k: round(ksum[k][0] / args.steps, 3) for k in ksum},
         "kernel_launches": {k: int(ksum[k][1] / args.steps) for k in ksum},
         "issue": issue,
@@ -318,8 +355,13 @@ def main():
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # checker + CPU baseline leg only: the scalar C restatement
     cpu, verify = None, None
+    sample = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # the first frames as a VP9 stream: the CPU baseline's whole-stream legs and the host
+        # entropy / decoder / adapter legs below
+        sample = encode_sample(v, frames, gop, min(len(frames), max(gop, 16)))
     if world == 1:
-        cpu, verify = cpu_baseline(v, oracle, dev, frames, refs, geom, args, slots_run)
+        cpu, verify = cpu_baseline(v, oracle, dev, frames, refs, geom, args, slots_run, sample)
     else:
         # every rank checks a sample of its own frames (the first frames of each slot in
         # decode order); rank 0 reports all ranks' results
@@ -345,7 +387,6 @@ def main():
 
     host = e2e = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        sample = encode_sample(v, frames, gop, min(len(frames), max(gop, 16)))
         host = host_entropy_rate(v, sample, gop, args)
         dev.close()                                     # free the batch's HBM before the decoder runs
         dev = None
@@ -498,9 +539,36 @@ def cpu_info():
             "affinity": affinity, "cpu_quota": _cpu_quota()}
 
 
-def cpu_baseline(v, oracle, dev, frames, refs, geom, args, slots_run):
+def stream_cpu(v, oracle, datas, geom, chroma):
+    """The whole CPU decode of one stream (entropy + reconstruction + loop
+    filter): the host parse (vp9h_stream, the restatement of vp9.c / vp9block.c) into pass-1
+    packets, the oracle's reconstruction and loop filter, reference slots by refresh mask
+    (vp9.c:1686-1691). Returns the frames decoded."""
+    W, H, BPP = geom[:3]
+    ssh, ssv = CHROMA[chroma]
+    st, slots, n = v.Stream(), [None] * 8, 0
+    for d in datas:
+        p, info = st.decode(d)
+        if p is None:
+            continue
+        pk = p.pkt
+        out = v.alloc_planes(W, H, BPP, ssh, ssv)
+        intra = pk.keyframe or pk.intraonly
+        oracle.decode_frame(pk, out, None if intra else [slots[s] for s in info.ref_slot])
+        for s in range(8):
+            if info.refresh_mask & (1 << s):
+                slots[s] = out
+        n += 1
+    return n
+
+
+def cpu_baseline(v, oracle, dev, frames, refs, geom, args, slots_run, sample=None):
     """CPU baseline legs on this box's host cores, and the bit-exactness
-    check of the timed frames. Leg 1: the scalar C oracle on 1 thread over a bounded sample
+    check of the timed frames. `value`: the whole stream (host entropy decode + oracle
+    reconstruction + loop filter, stream_cpu) over the encoded sample, independent
+    keyframes (C3 / C4) or GOP chains (C2 / C5) on the box's 16-thread share; the same on 1
+    thread beside it. Reconstruction-only legs from the pass-1 packets: leg 1 the scalar C
+    oracle on 1 thread over a bounded sample
     in decode order; every frame it decodes is compared with the device's frame in each
     batch slot the timed steps wrote (downloads and compares are outside the CPU timer).
     The frames leg 1 did not reach are then verified with the oracle on a thread pool.
@@ -619,6 +687,8 @@ def cpu_baseline(v, oracle, dev, frames, refs, geom, args, slots_run):
                      "sample": all_note or "%d %s on %d threads (nproc); cgroup CPU quota %s, affinity %s CPUs"
                                % (len(work_all), "keyframes" if gop == 1 else "GOP chains", nall, info["cpu_quota"],
                                   info["affinity"])})
+    for lg in legs:
+        lg["leg"] = "reconstruction + LF, " + lg["leg"]
     cpu = {"value": round(par, 3), "unit": "frames/s", "cores": thr, "kind": "port",
            "sample": "%s %s frames, scalar C oracle (the build's restatement, without the reference's SIMD; "
                      "reconstruction + loop filter from the same pass-1 packets, host entropy decode excluded), "
@@ -626,6 +696,31 @@ def cpu_baseline(v, oracle, dev, frames, refs, geom, args, slots_run):
                      % (len(work) if gop == 1 else sum(len(u) for u in work), args.config,
                         "frame" if gop == 1 else "GOP", thr, info["nproc"]),
            "legs": legs, "host": info}
+    if sample:
+        # the whole stream as BASELINE.md §3 states it: the encoded sample parsed and
+        # reconstructed, 1 thread, then units (keyframes / GOPs) over the 16-thread share
+        t0, n1, k = time.perf_counter(), 0, 0
+        while k < len(sample) or time.perf_counter() - t0 < budget / 4:
+            n1 += stream_cpu(v, oracle, sample[k % len(sample)], geom, args.chroma)
+            k += 1
+        one_ws = n1 / (time.perf_counter() - t0)
+        per = sum(len(g) for g in sample) / len(sample) / one_ws          # seconds per unit, 1 thread
+        nunits = max(thr, int(budget / 3 * thr / per) + 1)
+        with concurrent.futures.ThreadPoolExecutor(thr) as ex:
+            t0 = time.perf_counter()
+            done = sum(ex.map(lambda g: stream_cpu(v, oracle, g, geom, args.chroma),
+                              [sample[i % len(sample)] for i in range(nunits)]))
+            par_ws = done / (time.perf_counter() - t0)
+        unit = "keyframes" if gop == 1 else "GOP chains"
+        legs.insert(0, {"leg": "whole stream (entropy + reconstruction + LF), 1 thread", "value": round(one_ws, 3),
+                        "cores": 1, "sample": "%d frames of the %d-frame sample stream" % (n1, sum(map(len, sample)))})
+        legs.insert(1, {"leg": "whole stream, %s-parallel" % ("frame" if gop == 1 else "GOP"), "value": round(par_ws, 3),
+                        "cores": thr, "sample": "%d %s of the sample stream on %d threads" % (nunits, unit, thr)})
+        cpu.update({"value": round(par_ws, 3),
+                    "sample": "%d %s frames as VP9 bitstreams (%s of the timed workload, encoded by vp9h_stream): host "
+                              "entropy decode (vp9h_stream) + scalar C oracle reconstruction + loop filter (the build's "
+                              "restatement, without the reference's SIMD), %s-parallel over %d of the %s host threads"
+                              % (done, args.config, unit, "frame" if gop == 1 else "GOP", thr, info["nproc"])})
     return cpu, verify
 
 

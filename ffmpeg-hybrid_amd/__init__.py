@@ -128,6 +128,8 @@ _lib_handle = None
 # (frame_tensors) needs torch imported before this library is loaded.
 _torch_first = False
 
+ABI_VERSION = 2                # VP9HIP_ABI_VERSION of include/vp9hip.h these bindings mirror
+PIPELINE_SLOTS = 3             # VP9HIP_PIPELINE_SLOTS: batch slots the decoder / adapter rotate
 # Exported symbols of include/vp9hip.h (checked by the CPU test suite).
 ABI_SYMBOLS = ["vp9hip_open", "vp9hip_close", "vp9hip_configure", "vp9hip_submit_frame",
                "vp9hip_stage_batch", "vp9hip_stage_batch_refs", "vp9hip_run_batch", "vp9hip_sync",
@@ -136,7 +138,7 @@ ABI_SYMBOLS = ["vp9hip_open", "vp9hip_close", "vp9hip_configure", "vp9hip_submit
                "vp9hip_alg_bytes", "vp9hip_plan_stats", "vp9hip_plan_sb_costs", "vp9hip_abi_version", "vp9hip_set_graph",
                "vp9hip_stage_batch_tiles", "vp9hip_batch_phases", "vp9hip_phase_frames", "vp9hip_run_phase",
                "vp9hip_stripe", "vp9hip_frame_device", "vp9hip_batch_groups", "vp9hip_set_batch_slot", "vp9hip_sync_slot", "vp9hip_slot_busy",
-               "vp9hip_fill_buffers", "vp9hip_device_info", "vp9hip_test_hooks",
+               "vp9hip_fill_buffers", "vp9hip_device_info", "vp9hip_test_hooks", "vp9hip_batch_frame_status",
                "vp9h_decode_frame", "vp9h_encode_frame", "vp9h_frame_free", "vp9h_buffer_free",
                "vp9h_stream_open", "vp9h_stream_close", "vp9h_stream_set_threads", "vp9h_stream_decode", "vp9h_stream_encode",
                "vp9h_enc_defaults", "vp9h_superframe_split", "vp9h_frame_type", "vp9h_frame_peek",
@@ -159,6 +161,11 @@ def lib():
     global _torch_first
     _torch_first = "torch" in sys.modules
     L = ctypes.CDLL(LIB_PATH)
+    # the struct mirrors below are the header's of this ABI version (vp9h_synth_params and
+    # vp9h_enc_params grew in version 2): a library built from another header is refused
+    if L.vp9hip_abi_version() != ABI_VERSION:
+        raise Vp9HipUnavailable("libvp9hip.so ABI version %d, these bindings need %d: rebuild it (%s)"
+                                % (L.vp9hip_abi_version(), ABI_VERSION, LIB_PATH))
     vp = ctypes.c_void_p
     L.vp9hip_open.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
     L.vp9hip_close.argtypes = [vp]
@@ -174,6 +181,7 @@ def lib():
     L.vp9hip_batch_groups.argtypes = [vp]
     L.vp9hip_set_batch_slot.argtypes = [vp, ctypes.c_int]
     L.vp9hip_sync_slot.argtypes = [vp, ctypes.c_int]
+    L.vp9hip_batch_frame_status.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_int]
     L.vp9hip_slot_busy.argtypes = [vp, ctypes.c_int]
     L.vp9hip_phase_frames.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_int]
     L.vp9hip_run_phase.argtypes = [vp, ctypes.c_int, ctypes.c_int]
@@ -468,11 +476,12 @@ def decode_frame(data):
     return DecodedFrame(data)
 
 
-def test_hooks(reject_batch=0, lfr_spin=0):
-    """Test hooks copied by every context opened afterwards (vp9hip_test_hooks): the
-    reject_batch-th static-plan batch gets an intra mode the planner rejects; lfr_spin bounds
-    the row loop filter's hand-off waits (0, 0: off)."""
-    lib().vp9hip_test_hooks(int(reject_batch), int(lfr_spin))
+def test_hooks(reject_batch=0, lfr_spin=0, reject_frame=0):
+    """Test hooks copied by every context opened afterwards (vp9hip_test_hooks): frame
+    reject_frame of the reject_batch-th batch a context stages starts with an intra block
+    whose mode the planner rejects; lfr_spin bounds the row loop filter's hand-off waits
+    (0, 0: off)."""
+    lib().vp9hip_test_hooks(int(reject_batch) | int(reject_frame) << 16 if reject_batch else 0, int(lfr_spin))
 
 
 def device_info(device):
@@ -574,6 +583,15 @@ class Device:
     def sync_slot(self, slot):
         """Wait for batch slot `slot`'s last run and check its loop-filter hand-offs."""
         _check("vp9hip_sync_slot", lib().vp9hip_sync_slot(self._c, int(slot)))
+
+    def frame_status(self, slot):
+        """Per-frame outcome of the slot's last stage / run after it reported
+        AVERROR_INVALIDDATA (vp9hip_batch_frame_status): 0 reconstructed, EINVALIDDATA
+        rejected, EAGAIN valid but not run."""
+        n = _check("vp9hip_batch_frame_status", lib().vp9hip_batch_frame_status(self._c, int(slot), None, 0))
+        a = (ctypes.c_int * max(n, 1))()
+        _check("vp9hip_batch_frame_status", lib().vp9hip_batch_frame_status(self._c, int(slot), a, n))
+        return list(a[:n])
 
     def fill(self, buf0, count, value):
         """Fill device buffers [buf0, buf0 + count) with byte `value` (async, context stream)."""

@@ -23,6 +23,10 @@
 //   3. receive_frame hands out frames whose batch has been launched, in output order.
 // Like libavcodec's frame threading this adds decoder delay (up to max_batch frames plus
 // the frames in parse); flushing (send_packet with data = NULL) drains it.
+// Errors are per frame (vp9hip_pipeline.h): a packet whose parse fails is reported by the
+// send_packet / receive_frame call that consumes it and updates no reference slot (vp9.c
+// fails that decode, :1827-1832, and refreshes no slot); a frame the device rejects, or
+// one predicted from a failed frame, fails when it is received.
 #include <algorithm>
 #include <condition_variable>
 #include <cstring>
@@ -35,20 +39,22 @@
 
 #include "../../include/vp9hip.h"
 #include "vp9hip_parse.h"
+#include "vp9hip_pipeline.h"
 
 using vp9hip::Chain;
+using vp9hip::LFrame;
 using vp9hip::ParseJob;
 using vp9hip::ParsePool;
 
 namespace {
-struct Pending { vp9h_frame pkt; int out; int refs[3]; };   // refs: -1 for keyframes / intra-only
-struct Out { int buf; int64_t pts; bool submitted; };
-// Batches are numbered as launched (1, 2, ...) and alternate between the context's two
-// batch slots, so batch k + 1 is staged and planned while batch k's pixel kernels run. A
-// frame's batch is the one that wrote its buffer (buf_seq). A batch is checked
-// (vp9hip_sync_slot: its slot's work is drained and k_lfr's hand-off timeout words are
-// read) before its slot is staged again, which resets them, or before one of its frames
-// is handed out, whichever comes first.
+struct Pending { vp9h_frame pkt; LFrame f; };   // f.refs: -1 for keyframes / intra-only
+struct Out { int buf; int64_t pts; bool submitted; uint64_t id; };
+// Batches are numbered as launched (1, 2, ...) and rotate over VP9HIP_PIPELINE_SLOTS batch
+// slots (vp9hip::Ledger), so batches k + 1 and k + 2 are staged and planned while batch k's
+// pixel kernels run. A frame's batch is the one that wrote its buffer (Ledger::seq_of). A
+// batch is checked (vp9hip_sync_slot: its slot's work is drained, the planner's verdicts and
+// k_lfr's hand-off timeout words are read) before its slot is staged again, which resets
+// them, or before one of its frames is handed out, whichever comes first.
 const int STALL = 1;                   // consume: no free device buffer until frames are released
 }
 
@@ -60,11 +66,7 @@ struct vp9hip_decoder {
     int cw = 0, ch = 0, cbpp = 0, css_h = 0, css_v = 0, nbufs = 0;
     int slot[8];
     std::vector<int> pins, busy, bw, bh;   // per device buffer
-    std::vector<uint64_t> buf_seq;         // per device buffer: the batch that wrote it
-    uint64_t launched = 0;                 // batches launched; batch b ran in slot (b - 1) & 1
-    uint64_t slot_seq[2] = { 0, 0 };       // the batch last launched in each slot
-    bool slot_checked[2] = { true, true };
-    std::vector<std::pair<uint64_t, int>> bad;   // batches whose check failed, + error
+    vp9hip::Ledger led;                    // batches in flight, per-frame outcomes
     std::vector<Pending> batch;
     std::deque<Out> outq;
     // parse pipeline
@@ -109,54 +111,24 @@ static void wait_all_parsed(vp9hip_decoder *d)
 }
 
 // ---- device side ----
-// Stage + launch the pending frames as one batch.
-// Check the batch last launched in slot s: 0, or the error of a failed check other than
-// VP9HIP_EBUG (an EBUG batch is remembered; its frames fail when they are received).
-static int check_slot(vp9hip_decoder *d, int s)
-{
-    if (d->slot_checked[s]) return 0;
-    const int r = vp9hip_sync_slot(d->ctx, s);
-    // a batch that failed on the device (loop-filter hand-off: VP9HIP_EBUG; planner
-    // rejection: AVERROR_INVALIDDATA) fails its own frames only
-    if (r == VP9HIP_EBUG || r == VP9HIP_EINVALIDDATA) d->bad.push_back(std::make_pair(d->slot_seq[s], r));
-    else if (r < 0) return r;
-    d->slot_checked[s] = true;
-    return 0;
-}
-
-// 0, or the error of a launched batch that failed its check
-static int batch_bad(const vp9hip_decoder *d, uint64_t seq)
-{
-    for (const auto &b : d->bad) if (b.first == seq) return b.second;
-    return 0;
-}
-
+// Stage + launch the pending frames as one batch in the next pipeline slot (frames the
+// device rejects fail alone, Ledger::launch). 0, or a failure of the device context.
 static int submit(vp9hip_decoder *d)
 {
     if (d->batch.empty()) return 0;
-    const int slot = (int) (d->launched & 1);
-    int cr = check_slot(d, slot);             // before the staging resets that batch's words
-    if (cr < 0) return cr;
-    if ((cr = vp9hip_set_batch_slot(d->ctx, slot)) < 0) return cr;
     const int n = (int) d->batch.size();
-    std::vector<vp9h_frame> pk(n);
-    std::vector<int> outs(n), refs(3 * n);
+    std::vector<const vp9h_frame *> pk(n);
+    std::vector<LFrame> fr(n);
     for (int i = 0; i < n; i++) {
-        pk[i] = d->batch[i].pkt;
-        outs[i] = d->batch[i].out;
-        for (int r = 0; r < 3; r++) refs[3 * i + r] = d->batch[i].refs[r] >= 0 ? d->batch[i].refs[r] : 0;
+        pk[i] = &d->batch[i].pkt;
+        fr[i] = d->batch[i].f;
     }
-    int ret = vp9hip_stage_batch_refs(d->ctx, pk.data(), n, outs.data(), refs.data());
-    if (ret >= 0) ret = vp9hip_run_batch(d->ctx);
-    d->launched++;
-    d->slot_seq[slot] = d->launched;
-    d->slot_checked[slot] = ret < 0;
-    for (int i = 0; i < n; i++) d->buf_seq[outs[i]] = d->launched;
-    for (auto &f : d->batch) {
-        vp9h_frame_free(&f.pkt);
-        d->busy[f.out]--;
+    const int ret = d->led.launch(d->ctx, pk, fr);
+    for (auto &p : d->batch) {
+        vp9h_frame_free(&p.pkt);
+        d->busy[p.f.out]--;
         for (int r = 0; r < 3; r++)
-            if (f.refs[r] >= 0) d->busy[f.refs[r]]--;
+            if (p.f.refs[r] >= 0) d->busy[p.f.refs[r]]--;
     }
     d->batch.clear();
     for (auto &o : d->outq) o.submitted = true;
@@ -168,16 +140,16 @@ static int configure(vp9hip_decoder *d, const vp9h_frame &f)
     const int w = d->p.max_width > 0 ? d->p.max_width : f.width;
     const int h = d->p.max_height > 0 ? d->p.max_height : f.height;
     if (f.width > w || f.height > h) return VP9HIP_ENOSYS;
-    // 8 reference slots, the batch being filled, the launched batch's frames still to be
-    // received, and the frames the caller holds
-    const int nb = 8 + 2 * d->p.max_batch + (d->p.extra_bufs > 0 ? d->p.extra_bufs : 4);
+    // 8 reference slots, the batch being filled, the launched batches' frames still to be
+    // received (VP9HIP_PIPELINE_SLOTS in flight), and the frames the caller holds
+    const int nb = 8 + (VP9HIP_PIPELINE_SLOTS + 1) * d->p.max_batch + (d->p.extra_bufs > 0 ? d->p.extra_bufs : 4);
     int r = vp9hip_configure(d->ctx, w, h, f.bpp, f.ss_h, f.ss_v, nb);
     if (r < 0) return r;
     d->configured = true;
     d->cw = w; d->ch = h; d->cbpp = f.bpp; d->css_h = f.ss_h; d->css_v = f.ss_v;
     d->nbufs = nb;
     d->pins.assign(nb, 0); d->busy.assign(nb, 0); d->bw.assign(nb, 0); d->bh.assign(nb, 0);
-    d->buf_seq.assign(nb, 0);
+    d->led.reset_buffers(nb);
     for (int s = 0; s < 8; s++) d->slot[s] = -1;
     return 0;
 }
@@ -193,7 +165,7 @@ static int consume_one(vp9hip_decoder *d, ParseJob &j)
         const int b = d->configured ? d->slot[info.show_slot & 7] : -1;
         if (b < 0) return VP9HIP_EINVALIDDATA;
         d->pins[b]++;
-        d->outq.push_back({ b, j.pts, d->batch.empty() });
+        d->outq.push_back({ b, j.pts, d->batch.empty(), d->led.holder(b) });
         return 0;
     }
     const bool intra = f.keyframe || f.intraonly;
@@ -216,24 +188,25 @@ static int consume_one(vp9hip_decoder *d, ParseJob &j)
         out = alloc_buffer(d);
         if (out < 0) return STALL;
     }
+    int refs[3];
+    for (int i = 0; i < 3; i++) {
+        refs[i] = intra ? -1 : d->slot[info.ref_slot[i] & 7];
+        if (!intra && refs[i] < 0) return VP9HIP_EINVALIDDATA;
+    }
     Pending q;
     q.pkt = f;
-    q.out = out;
-    for (int i = 0; i < 3; i++) {
-        q.refs[i] = intra ? -1 : d->slot[info.ref_slot[i] & 7];
-        if (!intra && q.refs[i] < 0) return VP9HIP_EINVALIDDATA;
-    }
+    q.f = d->led.frame(out, refs);
     memset(&f, 0, sizeof(f));            // the batch owns the packet now
-    d->busy[q.out]++;
+    d->busy[out]++;
     for (int i = 0; i < 3; i++)
-        if (q.refs[i] >= 0) d->busy[q.refs[i]]++;
-    d->bw[q.out] = q.pkt.width; d->bh[q.out] = q.pkt.height;
+        if (refs[i] >= 0) d->busy[refs[i]]++;
+    d->bw[out] = q.pkt.width; d->bh[out] = q.pkt.height;
     for (int s = 0; s < 8; s++)
-        if (info.refresh_mask & (1 << s)) d->slot[s] = q.out;
+        if (info.refresh_mask & (1 << s)) d->slot[s] = out;
     d->batch.push_back(q);
     if (info.show_frame) {
-        d->pins[q.out]++;
-        d->outq.push_back({ q.out, j.pts, false });
+        d->pins[out]++;
+        d->outq.push_back({ out, j.pts, false, q.f.id });
     }
     if ((int) d->batch.size() >= d->p.max_batch) return submit(d);
     return 0;
@@ -272,8 +245,8 @@ extern "C" int vp9hip_decoder_open(const vp9hip_decoder_params *params, vp9hip_d
     if (d->p.parse_threads < 0) d->p.parse_threads = 0;
     if (d->p.parse_threads > 64) d->p.parse_threads = 64;
     // parse lookahead: enough frames that the pool keeps parsing while the caller's thread
-    // waits on the device (two batches in flight)
-    d->max_inflight = 4 * d->p.parse_threads + 2 * d->p.max_batch + 1;
+    // waits on the device (the batches in flight)
+    d->max_inflight = 4 * d->p.parse_threads + VP9HIP_PIPELINE_SLOTS * d->p.max_batch + 1;
     for (int s = 0; s < 8; s++) d->slot[s] = -1;
     int r = vp9hip_open(d->p.device, &d->ctx);
     if (r < 0) { vp9hip_decoder_close(d); return r; }
@@ -316,28 +289,31 @@ extern "C" int vp9hip_decoder_send_packet(vp9hip_decoder *d, const uint8_t *data
     const int nf = vp9h_superframe_split(data, size, offs, sizes, 8);
     if (nf < 0) return nf;
     // bound the frames in flight: consume parsed ones first; a stall (no free device
-    // buffer) asks the caller to receive frames (avcodec_send_packet's EAGAIN)
+    // buffer) asks the caller to receive frames (avcodec_send_packet's EAGAIN). An earlier
+    // frame's error found here is returned after this packet is queued: the packet is taken
+    int err = 0;
     if (d->inflight.size() + nf > (size_t) d->max_inflight) {
         int r = consume(d, true, d->max_inflight > nf ? d->max_inflight - nf : 0);
-        if (r < 0) return r;
         if (r == STALL) { d->stalled = true; return VP9HIP_EAGAIN; }
+        if (r < 0) err = r;
     }
     d->stalled = false;
     for (int k = 0; k < nf; k++) {
         const int type = vp9h_frame_type(data + offs[k], sizes[k]);
-        if (type < 0) return type;
+        if (type < 0) return err < 0 ? err : type;
         std::unique_ptr<ParseJob> j(new ParseJob());
         j->data.assign(data + offs[k], data + offs[k] + sizes[k]);
         j->pts = pts;
         if (type == 0 || !d->chain) {          // a keyframe parses on a fresh stream
             int r = 0;
             std::shared_ptr<Chain> c = ParsePool::new_chain(&r);
-            if (!c) return r;
+            if (!c) return err < 0 ? err : r;
             d->chain = c;
         }
         j->chain = d->chain;
         enqueue_parse(d, std::move(j));
     }
+    if (err < 0) return err;
     int r = consume(d, false);
     return r < 0 ? r : 0;
 }
@@ -358,20 +334,20 @@ extern "C" int vp9hip_decoder_receive_frame(vp9hip_decoder *d, vp9hip_decoded_fr
         return d->draining && d->inflight.empty() && d->batch.empty() ? VP9HIP_EOF : VP9HIP_EAGAIN;
     if (!d->outq.front().submitted) return VP9HIP_EAGAIN;
     const Out o = d->outq.front();
-    {                                          // its batch may still run: drain and check it
-        const uint64_t b = d->buf_seq[o.buf];
-        const int s = (int) ((b - 1) & 1);
-        if (b && d->slot_seq[s] == b && !d->slot_checked[s]) {
+    if (!d->led.error(o.id)) {                 // its batch may still run: drain and check it
+        const uint64_t b = d->led.seq_of(o.buf);
+        const int s = d->led.unchecked(b);
+        if (s >= 0) {
             // the newest batch still running: EAGAIN (frame-threading delay), so the caller
             // sends the next packets while it runs; an older batch, a drain or a stalled
-            // send_packet wait for it
-            if (!d->draining && !d->stalled && b == d->launched && vp9hip_slot_busy(d->ctx, s) == 1)
+            // send_packet wait for it (and for the batches before it: checks run in order)
+            if (!d->draining && !d->stalled && b == d->led.last() && vp9hip_slot_busy(d->ctx, s) == 1)
                 return VP9HIP_EAGAIN;
-            if ((r = check_slot(d, s)) < 0) return r;
+            if ((r = d->led.check_through(d->ctx, b)) < 0) return r;
         }
     }
     d->outq.pop_front();
-    if (const int e = batch_bad(d, d->buf_seq[o.buf])) {   // the batch failed on the device
+    if (const int e = d->led.error(o.id)) {    // rejected on the device, or read a failed frame
         d->pins[o.buf]--;
         return e;
     }
@@ -400,11 +376,11 @@ extern "C" int vp9hip_decoder_flush(vp9hip_decoder *d)
     if (!d) return VP9HIP_EINVAL;
     drop_inflight(d);
     d->chain.reset();
-    for (auto &f : d->batch) {
-        vp9h_frame_free(&f.pkt);
-        d->busy[f.out]--;
+    for (auto &p : d->batch) {
+        vp9h_frame_free(&p.pkt);
+        d->busy[p.f.out]--;
         for (int r = 0; r < 3; r++)
-            if (f.refs[r] >= 0) d->busy[f.refs[r]]--;
+            if (p.f.refs[r] >= 0) d->busy[p.f.refs[r]]--;
     }
     d->batch.clear();
     for (auto &o : d->outq) d->pins[o.buf]--;
@@ -412,5 +388,6 @@ extern "C" int vp9hip_decoder_flush(vp9hip_decoder *d)
     for (int s = 0; s < 8; s++) d->slot[s] = -1;
     d->draining = false;
     d->stalled = false;
+    d->led.reset();                            // vp9hip_flush drops the batches in flight
     return d->ctx ? vp9hip_flush(d->ctx) : 0;
 }

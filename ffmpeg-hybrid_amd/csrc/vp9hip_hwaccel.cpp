@@ -15,17 +15,22 @@
 //     they parse in parallel; a lone chain's tile columns parse on the idle threads.
 //   - end_frame maps refidx to device buffers, replaces the slots of refreshrefmask and
 //     appends the frame to the batch being filled. A batch of `async_depth` frames is staged
-//     into the context's free batch slot and launched (vp9hip_stage_batch_refs / run_batch:
-//     dependent frames chained, independent chains concurrent) once its parses are done,
-//     checked at each later end_frame, so the pool parses the next batch meanwhile; with
-//     more than two filled batches waiting the oldest launches anyway.
+//     into the next of VP9HIP_PIPELINE_SLOTS batch slots and launched
+//     (vp9hip_stage_batch_refs / run_batch: dependent frames chained, independent chains
+//     concurrent) once its parses are done, checked at each later end_frame, so the pool
+//     parses the next batches meanwhile; with more than max_full filled batches waiting the
+//     oldest launches anyway.
 //   - A frame handed out is a device frame whose pixels are complete once
 //     vp9hip_hwframe_sync (host) or vp9hip_hwframe_ready (a consumer's HIP stream) says so;
 //     both launch the batch holding it if it is still being filled. transfer syncs.
-// Errors of asynchronous work surface on the call that waits for it: a batch whose
-// row-pipelined loop filter gave up a hand-off (k_lfr timeout words, read by
-// vp9hip_sync_slot) fails its frames with VP9HIP_EBUG; a frame whose entropy decode fails
-// fails with that error, and so do the frames launched with it.
+// Errors of asynchronous work surface on the call that waits for the frame, and they are
+// the frame's own (vp9hip_pipeline.h), as vp9.c fails only the corrupt frame's decode
+// (:1827-1832): a frame whose entropy decode fails fails with that error, a frame the device
+// planner rejects with AVERROR_INVALIDDATA, and so does every frame predicted from a failed
+// one (its slots were mapped to the failed frame's buffer at end_frame, before the outcome
+// was known); the other frames of the same batch decode. A batch whose row-pipelined loop
+// filter gave up a hand-off (k_lfr timeout words, read by vp9hip_sync_slot) fails its frames
+// with VP9HIP_EBUG.
 //
 // Pool: a buffer is free when no reference slot holds it, no frame reference (the
 // AVBufferRef of an AVFrame, vp9hip_hwframe_unref) holds it, it is not the frame being
@@ -44,18 +49,20 @@
 
 #include "../../include/vp9hip_hwaccel.h"
 #include "vp9hip_parse.h"
+#include "vp9hip_pipeline.h"
 
 using vp9hip::Chain;
+using vp9hip::LFrame;
 using vp9hip::ParseJob;
 using vp9hip::ParsePool;
 
 namespace {
-struct Pend { std::unique_ptr<ParseJob> job; int out; int refs[3]; };
+struct Pend { std::unique_ptr<ParseJob> job; LFrame f; };
 
 // VP9HIP_HWACCEL_TRACE=1: host wall time of the adapter's steps, printed at uninit
-enum { T_SLICE, T_END, T_PARSE_WAIT, T_CHECK, T_STAGE, T_RUN, T_SYNC_WAIT, T_N };
+enum { T_SLICE, T_END, T_PARSE_WAIT, T_RUN, T_SYNC_WAIT, T_N };
 const char *const tname[T_N] = { "decode_slice", "end_frame (excl. launches)", "submit: wait for parses",
-                                  "submit: check the slot's previous batch", "submit: stage", "submit: run_batch",
+                                  "submit: check the slot's previous batch, stage, run_batch",
                                   "hwframe_sync: wait for the frame's batch" };
 struct Trace {
     bool on = false;
@@ -86,8 +93,7 @@ struct vp9hip_hwaccel {
     mutable std::mutex mu;
     std::vector<int> pend;                  // per pool buffer: in the batch being filled
     std::vector<int> inref;                 // per pool buffer: read by frames of that batch
-    std::vector<uint64_t> buf_seq;          // per pool buffer: the batch that last wrote it
-    std::vector<int> buf_err;               // per pool buffer: error of the frame it holds
+    vp9hip::Ledger led;                     // batches in flight, per-frame outcomes
     int cur = -1;                           // buffer of the frame being decoded
     int64_t pts = 0;
     std::unique_ptr<ParseJob> job;          // decode_slice -> end_frame
@@ -95,10 +101,6 @@ struct vp9hip_hwaccel {
     vp9h_frame_info info;                   // the peeked header of the current frame
     std::vector<Pend> batch;                // the batch being filled
     std::deque<std::vector<Pend>> full;     // filled batches waiting for their parses (decode order)
-    uint64_t launched = 0;                  // batches launched; batch b ran in slot (b - 1) & 1
-    uint64_t slot_seq[2] = { 0, 0 };
-    bool slot_checked[2] = { true, true };
-    std::vector<std::pair<uint64_t, int>> bad;   // launched batches that failed their check, + error
     size_t max_full = 1;                    // filled batches that may wait for their parses
     Trace tr;
 };
@@ -154,8 +156,7 @@ extern "C" int vp9hip_hwaccel_init(int device, const vp9hip_frames_params *fp, v
     h->refs.assign(n, 0);
     h->pend.assign(n, 0);
     h->inref.assign(n, 0);
-    h->buf_seq.assign(n, 0);
-    h->buf_err.assign(n, 0);
+    h->led.reset_buffers((int) n);
     int r = vp9hip_open(device, &h->gpu);
     if (!r) r = vp9hip_configure(h->gpu, fp->width, fp->height, fp->bpp, fp->ss_h, fp->ss_v, fp->initial_pool_size);
     if (r < 0) {
@@ -172,77 +173,39 @@ extern "C" int vp9hip_hwaccel_init(int device, const vp9hip_frames_params *fp, v
     return 0;
 }
 
-// Check the batch last launched in slot s (waits for it): an EBUG batch is remembered and
-// its frames fail when they are waited for.
-static int check_slot(vp9hip_hwaccel *h, int s)
-{
-    if (h->slot_checked[s]) return 0;
-    const int r = vp9hip_sync_slot(h->gpu, s);
-    // a batch that failed on the device (loop-filter hand-off: VP9HIP_EBUG; planner
-    // rejection: AVERROR_INVALIDDATA) fails its own frames only
-    if (r == VP9HIP_EBUG || r == VP9HIP_EINVALIDDATA) h->bad.push_back(std::make_pair(h->slot_seq[s], r));
-    else if (r < 0) return r;
-    h->slot_checked[s] = true;
-    return 0;
-}
-
-// 0, or the error of a launched batch that failed its check
-static int batch_bad(const vp9hip_hwaccel *h, uint64_t seq)
-{
-    for (const auto &b : h->bad) if (b.first == seq) return b.second;
-    return 0;
-}
-
-// Stage + launch one batch in the next batch slot. Its packets are parsed by now or soon:
-// wait for them (in decode order).
+// Stage + launch one batch in the next pipeline slot. Its packets are parsed by now or
+// soon: wait for them (in decode order). A frame whose parse failed fails alone (with the
+// frames that read it); the others launch (Ledger::launch). 0, or a failure of the device
+// context.
 static int submit_list(vp9hip_hwaccel *h, std::vector<Pend> &batch)
 {
     if (batch.empty()) return 0;
     const int n = (int) batch.size();
-    int err = 0;
     Trace &tr = h->tr;
     tr.start();
-    for (auto &p : batch) {
+    std::vector<const vp9h_frame *> pk(n, nullptr);
+    std::vector<LFrame> fr(n);
+    for (int i = 0; i < n; i++) {
+        Pend &p = batch[i];
         h->pool->wait(p.job.get());
         const vp9h_frame &f = p.job->pkt;
         int e = p.job->ret;
         if (!e && (f.width > h->fp.width || f.height > h->fp.height || f.bpp != h->fp.bpp ||
                    f.ss_h != h->fp.ss_h || f.ss_v != h->fp.ss_v))
             e = VP9HIP_ENOSYS;               // a new format: get_format re-inits the hwaccel
-        if (e && !err) err = e;
+        fr[i] = p.f;
+        if (e) h->led.fail(p.f, e);
+        else pk[i] = &f;
     }
-    int ret = err;
-    const int slot = (int) (h->launched & 1);
     tr.stop(T_PARSE_WAIT);
-    if (!ret) ret = check_slot(h, slot);     // before the staging resets that batch's words
-    tr.stop(T_CHECK);
-    if (!ret) ret = vp9hip_set_batch_slot(h->gpu, slot);
-    if (!ret) {
-        std::vector<vp9h_frame> pk(n);
-        std::vector<int> outs(n), refs(3 * n);
-        for (int i = 0; i < n; i++) {
-            pk[i] = batch[i].job->pkt;
-            outs[i] = batch[i].out;
-            for (int r = 0; r < 3; r++) refs[3 * i + r] = batch[i].refs[r] >= 0 ? batch[i].refs[r] : 0;
-        }
-        ret = vp9hip_stage_batch_refs(h->gpu, pk.data(), n, outs.data(), refs.data());   // copies the packets
-        tr.stop(T_STAGE);
-        if (ret >= 0) ret = vp9hip_run_batch(h->gpu);
-        tr.stop(T_RUN);
-        tr.batches++;
-        tr.frames += n;
-        if (ret >= 0) {
-            h->launched++;
-            h->slot_seq[slot] = h->launched;
-            h->slot_checked[slot] = false;
-        }
-    }
+    const int ret = h->led.launch(h->gpu, pk, fr);   // checks the slot's last batch, stages, runs
+    tr.stop(T_RUN);
+    tr.batches++;
+    tr.frames += n;
     for (auto &p : batch) {
-        h->pend[p.out] = 0;
+        h->pend[p.f.out] = 0;
         for (int r = 0; r < 3; r++)
-            if (p.refs[r] >= 0) h->inref[p.refs[r]]--;
-        h->buf_seq[p.out] = ret < 0 ? 0 : h->launched;
-        h->buf_err[p.out] = ret < 0 ? ret : 0;
+            if (p.f.refs[r] >= 0) h->inref[p.f.refs[r]]--;
     }
     batch.clear();                           // the jobs free their packets
     return ret < 0 ? ret : 0;
@@ -387,19 +350,19 @@ extern "C" int vp9hip_hwaccel_end_frame(vp9hip_hwaccel *h, vp9hip_hwframe *out)
     std::lock_guard<std::mutex> g(h->mu);
     if (h->cur < 0 || !h->job) return VP9HIP_EINVAL;
     h->tr.start();
-    Pend p;
-    p.out = h->cur;
+    int refs[3];
     for (int i = 0; i < 3; i++) {            // s->s.h.refidx -> the slots' device buffers
-        p.refs[i] = h->intra ? -1 : h->slot[h->info.ref_slot[i] & 7];
-        if (!h->intra && p.refs[i] < 0) { drop_job(h); h->cur = -1; return VP9HIP_EINVALIDDATA; }
+        refs[i] = h->intra ? -1 : h->slot[h->info.ref_slot[i] & 7];
+        if (!h->intra && refs[i] < 0) { drop_job(h); h->cur = -1; return VP9HIP_EINVALIDDATA; }
     }
+    Pend p;
+    p.f = h->led.frame(h->cur, refs);
     p.job = std::move(h->job);
     for (int i = 0; i < 8; i++)              // vp9.c:1705-1711: slots of refreshrefmask
         if (h->info.refresh_mask & (1 << i)) h->slot[i] = h->cur;
-    h->pend[p.out] = 1;
+    h->pend[p.f.out] = 1;
     for (int i = 0; i < 3; i++)
-        if (p.refs[i] >= 0) h->inref[p.refs[i]]++;
-    h->buf_err[p.out] = 0;
+        if (refs[i] >= 0) h->inref[refs[i]]++;
     h->batch.push_back(std::move(p));
     if (out) fill_frame(h, h->cur, h->pts, out);          // shown or hidden: vp9.c's AVFrame of the frame
     const int shown = h->info.show_frame != 0;
@@ -425,7 +388,7 @@ extern "C" int vp9hip_hwaccel_show_existing(vp9hip_hwaccel *h, int slot, int64_t
 
 // Launch the frame's batch if it has not been launched yet (and the filled batches before
 // it; the batch being filled only when the frame is in it, so batches stay whole); 0 or
-// the frame's error.
+// the frame's error known so far.
 static int launch_for(vp9hip_hwaccel *h, int b)
 {
     int err = 0;
@@ -439,7 +402,7 @@ static int launch_for(vp9hip_hwaccel *h, int b)
         if (r < 0 && !err) err = r;
     }
     if (err < 0) return err;
-    return h->buf_err[b];
+    return h->led.error(h->led.holder(b));
 }
 
 static int hwframe_sync_l(vp9hip_hwaccel *h, const vp9hip_hwframe *f)
@@ -447,14 +410,14 @@ static int hwframe_sync_l(vp9hip_hwaccel *h, const vp9hip_hwframe *f)
     if (f->buf < 0 || f->buf >= h->fp.initial_pool_size || !nrefs(h, f->buf)) return VP9HIP_EINVAL;
     int r = launch_for(h, f->buf);
     if (r < 0) return r;
-    const uint64_t b = h->buf_seq[f->buf];
+    const uint64_t b = h->led.seq_of(f->buf);
     if (!b) return 0;                                    // written before any batch (never decoded)
-    const int s = (int) ((b - 1) & 1);
     h->tr.start();
-    if (h->slot_seq[s] == b && (r = check_slot(h, s)) < 0) return r;
+    // the frame's batch and every batch before it (an older batch of its slot was drained
+    // and checked before the slot was reused)
+    if (h->led.unchecked(b) >= 0 && (r = h->led.check_through(h->gpu, b)) < 0) return r;
     h->tr.stop(T_SYNC_WAIT);
-    // an older batch of the slot was drained and checked before its slot was reused
-    return batch_bad(h, b);
+    return h->led.error(h->led.holder(f->buf));
 }
 
 extern "C" int vp9hip_hwframe_sync(vp9hip_hwaccel *h, const vp9hip_hwframe *f)
@@ -471,13 +434,11 @@ extern "C" int vp9hip_hwframe_ready(vp9hip_hwaccel *h, const vp9hip_hwframe *f, 
     if (f->buf < 0 || f->buf >= h->fp.initial_pool_size || !nrefs(h, f->buf)) return VP9HIP_EINVAL;
     int r = launch_for(h, f->buf);
     if (r < 0) return r;
-    const uint64_t b = h->buf_seq[f->buf];
-    if ((r = batch_bad(h, b)) < 0) return r;
+    const uint64_t b = h->led.seq_of(f->buf);
     if (!b) return 0;
-    const int s = (int) ((b - 1) & 1);
-    // the slot's last run is this batch or a later one (which follows it on the context's
+    // the slot's last run is this batch or a later one (which follows it on the slot's
     // stream): ordering the consumer's stream after it orders it after the frame
-    return vp9hip_slot_stream_wait(h->gpu, s, stream);
+    return vp9hip_slot_stream_wait(h->gpu, vp9hip::Ledger::slot_of(b), stream);
 }
 
 extern "C" int vp9hip_hwaccel_uninit(vp9hip_hwaccel *h)
@@ -512,9 +473,7 @@ extern "C" void vp9hip_hwaccel_flush(vp9hip_hwaccel *h)
     drop_job(h);
     h->cur = -1;
     // frames already handed out stay valid: their batch runs, then the slots are dropped
-    if (submit(h) >= 0) {
-        for (int s = 0; s < 2; s++) check_slot(h, s);
-    }
+    if (submit(h) >= 0) h->led.check_through(h->gpu, ~0ull);
     h->batch.clear();
     h->full.clear();
     for (int i = 0; i < 8; i++) h->slot[i] = -1;

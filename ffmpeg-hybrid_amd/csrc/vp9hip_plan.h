@@ -41,7 +41,11 @@ typedef struct PlanFrame {
     uint8_t  lflvl[8][4][2];
 } PlanFrame;
 
-/* Status bits (PlanDev.status[0]); any bit fails the batch with AVERROR_INVALIDDATA. */
+/* Status bits (PlanDev.status[0], and per frame in PlanDev.fbad); any bit fails the frame
+ * that set it with AVERROR_INVALIDDATA. Each frame's records address only its own blocks,
+ * eobs, coefficients and SB slots (offsets rebased on the frame's own ranges, residual jobs
+ * capped at the SB's counts), so a rejected frame leaves the other frames' plans intact;
+ * PLS_BOUNDS (a shared buffer's capacity) cannot be attributed and fails the batch. */
 #define PLS_BLOCK      1u         /* a block field out of range                             */
 #define PLS_ORDER      2u         /* blocks not in decode order / an SB without blocks      */
 #define PLS_EOB        4u         /* eob count or value inconsistent with the packet        */
@@ -73,6 +77,7 @@ typedef struct PlanDev {
     uint32_t *sb_key, *sb_kpos;      /* per slot: intra-step key and position in its list    */
     uint32_t *key_cnt, *key_off;     /* per key: SBs, exclusive scan (+ total)               */
     uint32_t *status;                /* [0] PLS_* bits                                       */
+    uint32_t *fbad;                  /* per frame: the PLS_* bits of that frame              */
     unsigned long long *fbytes;      /* per frame: inter residual pixel bytes, MC bytes     */
     /* products */
     SBRec *sbs; WGRec *wgs; PJob *pjobs; uint32_t *passes; LFRec *lfs; RJob *rjobs; McUnit *mcs;

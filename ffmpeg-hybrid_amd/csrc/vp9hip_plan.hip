@@ -61,6 +61,12 @@ DEV bool inb(const PlanDev &D, uint32_t i, uint32_t cap, uint32_t bit)
     atomicOr(&D.status[0], PLS_BOUNDS);
     return false;
 }
+// A frame's packet is inconsistent: its status bits, for the batch and for the frame.
+DEV void plan_fail(const PlanDev &D, const PlanFrame &F, uint32_t st)
+{
+    atomicOr(D.status, st);
+    if ((uint32_t) F.frame < D.nframes) atomicOr(&D.fbad[F.frame], st);
+}
 // The planner's workgroups are one wave: the LDS unit executes a wave's DS instructions in
 // order, so a wave-scope fence (compiler ordering) replaces the workgroup barrier.
 DEV void wsync()
@@ -171,12 +177,16 @@ DEV Tx sb_tx(const vp9h_block *blk, const uint32_t *pre, int nb, uint32_t t, int
     return sb_tx_at<SSH, SSV>(blk, pre, sb_locate(pre, 3 * nb, t), t, cols, rows);
 }
 
-// The eob of tx t (0 for skipped blocks), range-checked against the packet.
-template <class B> DEV int tx_eob(const PlanDev &D, const B &b, const Tx &tx, const uint32_t *pre, uint32_t b0, uint32_t &st)
+// The eob of tx t (0 for skipped blocks), range-checked against the frame's own eobs: the
+// block scan is rebased on the frame's first block (ebase = blk_eob0[F.blk0]), so a frame
+// whose eob count disagrees with its packet cannot shift another frame's eobs.
+template <class B> DEV int tx_eob(const PlanDev &D, const PlanFrame &F, uint32_t ebase, const B &b, const Tx &tx,
+                                  const uint32_t *pre, uint32_t b0, uint32_t &st)
 {
     if (b.skip) return 0;
-    const uint32_t i = D.blk_eob0[b0 + tx.b] + ((pre[tx.k] & 1023) - (pre[3 * tx.b] & 1023)) + (uint32_t) tx.l;
-    if (i >= D.total_eobs) { st |= PLS_EOB; return 0; }
+    const uint32_t r = D.blk_eob0[b0 + tx.b] - ebase + ((pre[tx.k] & 1023) - (pre[3 * tx.b] & 1023)) + (uint32_t) tx.l;
+    const uint32_t i = F.eob0 + r;
+    if (r >= F.neob || i >= D.total_eobs) { st |= PLS_EOB; return 0; }
     const int e = D.eobs[i];
     if (e > (16 << (2 * tx.g.txs))) { st |= PLS_EOB; return 0; }
     return e;
@@ -263,7 +273,7 @@ __global__ __launch_bounds__(256) void k_pblk(PlanDev D)
             n += (uint32_t) (g.nx * g.ny);
         }
     D.blk_neob[gi] = n;
-    if (st) atomicOr(D.status, st);
+    if (st) plan_fail(D, F, st);
 }
 
 // ------------------------------------------------------------------ k_psb
@@ -297,6 +307,7 @@ __global__ __launch_bounds__(64) void k_psb(PlanDev D)
     wsync();
     const uint32_t tot = sb_prefix<SSH, SSV>(blk, nb, cols, rows, G.mine, pre, lane);
     const uint32_t T = pl_min((int) (tot & 1023), JCAP);
+    const uint32_t ebase = D.blk_eob0[F.blk0];
     uint32_t ncoef = 0, kcnt = 0;
     for (uint32_t t0 = 0; t0 < T; t0 += 64) {
         const uint32_t t = t0 + (uint32_t) lane;
@@ -304,7 +315,7 @@ __global__ __launch_bounds__(64) void k_psb(PlanDev D)
         if (t < T) {
             const Tx tx = sb_tx_at<SSH, SSV>(blk, pre, sb_locate(pre, 3 * nb, t), t, cols, rows);
             const PBlk &b = blk[tx.b];
-            const int e = tx_eob(D, b, tx, pre, b0, st);
+            const int e = tx_eob(D, F, ebase, b, tx, pre, b0, st);
             ncoef += (uint32_t) e;
             int txtp = 0;
             if (b.intra) {
@@ -353,7 +364,7 @@ __global__ __launch_bounds__(64) void k_psb(PlanDev D)
     }
     if (lane < 24 && inb(D, G.slot, D.nslots, 4u)) D.ibits[(size_t) G.slot * 24 + lane] = ib;
     if (lane == 0 && inb(D, G.dord, D.nslots, 8u)) D.sb_ncoef[G.dord] = ncoef;
-    if (st) atomicOr(D.status, st);
+    if (st) plan_fail(D, F, st);
 }
 
 // ------------------------------------------------------------------ k_plan
@@ -455,12 +466,17 @@ __global__ __launch_bounds__(64) void k_pjob(PlanDev D)
     // contiguous in the packet (its coded blocks' tx in decode order): one coalesced load
     // into LDS, then each tx picks its entry (skipped blocks have none)
     {
+        // the block scan rebased on the frame's first block and eob range (tx_eob)
+        const uint32_t ebase = D.blk_eob0[F.blk0];
         const uint32_t be = lane <= nb ? D.blk_eob0[b0 + (uint32_t) lane] : 0u;      // nb + 1 entries
         if (lane < nb) S.eb[lane] = be;
-        const uint32_t E0 = rdl(be, 0), E1 = rdl(be, nb);
+        const uint32_t E0 = rdl(be, 0), E1 = rdl(be, nb), R0 = E0 - ebase;
         uint32_t E = E1 - E0;
-        if (E1 < E0 || E > (uint32_t) JCAP || E1 > D.total_eobs) { st |= PLS_EOB; E = 0; }
-        for (uint32_t i = (uint32_t) lane; i < E; i += 64) S.co[i] = D.eobs[E0 + i];
+        if (E1 < E0 || E > (uint32_t) JCAP || R0 > F.neob || E > F.neob - R0 || F.eob0 + R0 + E > D.total_eobs) {
+            st |= PLS_EOB;
+            E = 0;
+        }
+        for (uint32_t i = (uint32_t) lane; i < E; i += 64) S.co[i] = D.eobs[F.eob0 + R0 + i];
         wsync();
         for (int t = lane; t < T; t += 64) {
             const int k = S.own[t], b = (k * 171) >> 9;
@@ -486,16 +502,20 @@ __global__ __launch_bounds__(64) void k_pjob(PlanDev D)
             carry += rdl(incl, 63);
         }
     }
-    // record bases of the SB: lanes 0..19 residual keys (tcode * 4 + txtp), lane 20 MC units
-    uint32_t rb = 0;
+    // record bases of the SB: lanes 0..19 residual keys (tcode * 4 + txtp), lane 20 MC units;
+    // rl: the end of the key's range (k_psb's count), which no emitted job may pass
+    uint32_t rb = 0, rl = 0;
     if (lane < 20) {
         const uint32_t ci = cnt_idx(D, F, G.seg, slot, lane >> 2, lane & 3);
-        rb = inb(D, ci, D.cap_cnt, 16u) ? D.cnt0[ci] : 0u;
+        if (inb(D, ci, D.cap_cnt, 16u)) { rb = D.cnt0[ci]; rl = rb + D.cnt[ci]; }
     } else if (lane == 20) {
         const uint32_t ci = D.seg_pre1[G.seg] + D.slot_pos[slot];
         rb = inb(D, ci, D.cap_cntm, 16u) ? D.cntm0[ci] : 0u;
     }
-    const uint32_t coef_sb = inb(D, G.dord, D.nslots, 32u) ? D.sb_coef0[G.dord] : 0u;
+    // the SB's first coefficient, rebased on the frame's own coefficient range: the scan's
+    // value at the frame's first SB in decode order (dord = slot0) is the frame's origin
+    const uint32_t coef_sb = inb(D, G.dord, D.nslots, 32u) ? F.coef0 + (D.sb_coef0[G.dord] - D.sb_coef0[F.slot0]) : 0u;
+    const uint32_t coef_end = F.coef0 + F.ncoef;
     const uint32_t rbase = slot * D.rcap;
     unsigned long long ibytes = 0;
     wsync();
@@ -523,7 +543,11 @@ __global__ __launch_bounds__(64) void k_pjob(PlanDev D)
             if (e0 && G.mine) {
                 uint32_t coef = coef_sb + S.co[t];
                 int e = e0;
-                if (coef + (uint32_t) e > D.total_coefs) { st |= PLS_COEF; e = 0; coef = 0; }
+                if (coef < F.coef0 || coef + (uint32_t) e > coef_end || coef_end > D.total_coefs) {
+                    st |= PLS_COEF;
+                    e = 0;
+                    coef = 0;
+                }
                 r.coef = coef;
                 r.eob = (uint16_t) e;
                 r.frame = (uint16_t) F.frame;
@@ -548,16 +572,17 @@ __global__ __launch_bounds__(64) void k_pjob(PlanDev D)
         }
         // ranks within each key, in decode order: one ballot per distinct key of the chunk
         uint64_t pend = __ballot(key >= 0);
-        uint32_t pos = 0;
+        uint32_t pos = 0, lim = 0;
         while (pend) {
             const int l0 = __builtin_ctzll(pend);
             const int kk = rdl(key, l0);
             const uint64_t m = __ballot(key == kk);
-            const uint32_t base = rdl(rb, kk);
-            if (key == kk) pos = base + mbcnt(m);
+            const uint32_t base = rdl(rb, kk), end = rdl(rl, kk);
+            if (key == kk) { pos = base + mbcnt(m); lim = end; }
             if (lane == kk) rb += (uint32_t) __popcll(m);
             pend &= ~m;
         }
+        if (key >= 0 && pos >= lim) { st |= PLS_EOB; key = -1; }   // more jobs than k_psb counted
         if (key >= 0 && inb(D, pos, D.cap_rjobs, 64u)) D.rjobs[pos] = r;
     }
     for (int d = 32; d; d >>= 1) ibytes += __shfl_xor(ibytes, d);
@@ -566,7 +591,7 @@ __global__ __launch_bounds__(64) void k_pjob(PlanDev D)
         if (ibytes && inb(D, (uint32_t) F.frame, D.nframes, 2048u)) atomicAdd(&D.fbytes[2 * F.frame], ibytes);
     }
     st = wor(st);
-    if (lane == 0 && st) atomicOr(D.status, st);
+    if (lane == 0 && st) plan_fail(D, F, st);
     PPT(2);
 }
 
@@ -878,7 +903,7 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
         }
     }
     st = wor(st);
-    if (lane == 0 && st) atomicOr(D.status, st);
+    if (lane == 0 && st) plan_fail(D, F, st);
     PPT(10);
 }
 
@@ -1029,7 +1054,8 @@ __global__ __launch_bounds__(1024) void k_pkeys(PlanDev D, int nk, const uint32_
         fb[2 * i] = (uint32_t) D.fbytes[i];
         fb[2 * i + 1] = (uint32_t) (D.fbytes[i] >> 32);
     }
-    if (t == 0) { out[0] = D.status[0]; out[1 + ng + nk + 1 + 4 * nframes] = D.status[1]; }
+    for (int i = t; i < nframes; i += 1024) fb[4 * nframes + i] = D.fbad[i];     // per-frame status
+    if (t == 0) { out[0] = D.status[0]; out[1 + ng + nk + 1 + 5 * nframes] = D.status[1]; }
 }
 
 // ------------------------------------------------------------------ k_plists
@@ -1048,21 +1074,38 @@ __global__ __launch_bounds__(256) void k_plists(PlanDev D)
 
 // ------------------------------------------------------------------ k_pguard
 // Batches whose launch list is fixed at staging (keyframe batches, runtime "static plan"):
-// their pixel kernels run after the planner without a host check of its status, so a
-// rejected batch (status[0] != 0: the packets are inconsistent) is neutralised here: no
-// intra passes (WGRec), no residual jobs (the summary's ranges); the status is re-copied
-// into the summary (k_plists' bound checks come after k_pkeys), which the host reads when
-// it next waits for the batch (vp9hip_sync / sync_slot: AVERROR_INVALIDDATA).
+// their pixel kernels run after the planner without a host check of its status, so the
+// frames the planner rejected (fbad != 0: the frame's packet is inconsistent) are
+// neutralised here: no intra passes (WGRec), and their residual jobs write nothing but
+// zeros into the spare scratch slot (slot nslots) from no coefficients. The other frames'
+// records address only their own data (k_pjob), so they reconstruct as if alone; a status
+// that names no frame (PLS_BOUNDS) neutralises the whole batch (every WGRec, the summary's
+// residual ranges). The status is re-copied into the summary (k_plists' bound checks come
+// after k_pkeys), which the host reads when it next waits for the batch (vp9hip_sync /
+// sync_slot: AVERROR_INVALIDDATA; vp9hip_batch_frame_status: which frames).
 __global__ __launch_bounds__(256) void k_pguard(PlanDev D, uint32_t *summary, int ng)
 {
     const uint32_t st = __builtin_amdgcn_readfirstlane(D.status[0]);
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) summary[0] = st;
     if (!st) return;
+    const bool all = (st & PLS_BOUNDS) != 0;
     const PlanFrame &F = D.frames[blockIdx.y];
     const int s = blockIdx.x * 256 + threadIdx.x;
-    if (blockIdx.y == 0)
+    if (all && blockIdx.y == 0)
         for (int i = s; i < ng; i += (int) gridDim.x * 256) summary[1 + i] = 0;
-    if (s >= F.sb_cols * F.sb_rows) return;
+    if (!all) {
+        const uint32_t spare = D.nslots * D.rcap;        // resid scratch has nslots + 1 slots
+        const uint32_t nt = gridDim.x * gridDim.y * 256u;
+        for (uint32_t i = (blockIdx.y * gridDim.x + blockIdx.x) * 256u + threadIdx.x; i + 1 < D.cap_rjobs; i += nt) {
+            RJob r = D.rjobs[i];
+            if (r.frame >= D.nframes || !D.fbad[r.frame]) continue;
+            r.coef = 0; r.dst = spare; r.eob = 0; r.nzc = 1; r.nzr = 1;
+            r.ptx &= (uint8_t) ~(1u << 5);                   // scratch, not in place
+            D.rjobs[i] = r;
+        }
+    }
+    const bool bad = all || ((uint32_t) F.frame < D.nframes && D.fbad[F.frame]);
+    if (!bad || s >= F.sb_cols * F.sb_rows) return;
     const uint32_t slot = F.slot0 + (uint32_t) s;
     if (slot < D.nslots) { D.wgs[slot].njobs = 0; D.wgs[slot].npass = 0; }
 }

@@ -179,7 +179,7 @@ struct Staged {
     int plan_flags = 0;                 // device planner kernels: 1 any filtered frame, 2 any inter frame
     size_t o_pf = 0, o_blocks = 0, o_eobs = 0, o_slotpos = 0, o_segpre = 0, o_segsz = 0, o_segpre1 = 0, o_cntm = 0, o_cntm0 = 0, o_gidx = 0, o_bneob = 0,
            o_beob0 = 0, o_sbfirst = 0, o_sbncoef = 0, o_sbcoef0 = 0, o_cnt = 0, o_cnt0 = 0, o_ibits = 0,
-           o_sbinfo = 0, o_sbkey = 0, o_sbkpos = 0, o_keycnt = 0, o_keyoff = 0, o_status = 0, o_fbytes = 0,
+           o_sbinfo = 0, o_sbkey = 0, o_sbkpos = 0, o_keycnt = 0, o_keyoff = 0, o_status = 0, o_fbytes = 0, o_fbad = 0,
            o_summary = 0, o_scan = 0, zero_bytes = 0, o_jobw = 0, o_sbnj = 0;
     size_t scan_bytes = 0, summary_words = 0;
     uint32_t *summary_h = nullptr;                            // pinned readback of the summary
@@ -197,7 +197,12 @@ struct Staged {
     hipEvent_t plan_ev = nullptr;
     bool summary_pending = false;
     int status = 0;                     // sticky until the slot is restaged: the planner rejected
-                                        // the batch (AVERROR_INVALIDDATA; k_pguard neutralised it)
+                                        // frames of the batch (AVERROR_INVALIDDATA; k_pguard
+                                        // neutralised them) or the batch failed (VP9HIP_EBUG)
+    // Per frame (staging order), the outcome of the last stage / run when it failed with
+    // AVERROR_INVALIDDATA (vp9hip_batch_frame_status): 0 reconstructed, AVERROR_INVALIDDATA
+    // rejected, AVERROR(EAGAIN) valid but not run (the batch stopped before its pixel work).
+    std::vector<int> fstat;
     std::vector<uint32_t> exp_ko;       // key offsets the launch list was built with
     std::vector<uint32_t> stat_lists;   // the intra step lists (uploaded with the batch)
     std::vector<int> wr, rd;            // frame buffers the batch writes / reads (sorted)
@@ -284,7 +289,12 @@ struct vp9hip_ctx {
     hipStream_t st = nullptr;           // main stream: uploads, downloads, group 0
     hipStream_t xst[MAX_GROUPS - 1] = {};   // groups 1.. of a batch (joined back into st)
     hipEvent_t fork_ev = nullptr, join_ev[MAX_GROUPS] = {};
-    int max_groups = 2;                 // VP9HIP_STREAMS overrides (1..8); 2 measured best with the device planner and two batch slots (r02k: C3 +3.7 %, C4 +2.7 %, C2 +1.1 % over 3)
+    // frame-group streams per batch slot, VP9HIP_STREAMS overrides (1..8). 1: with 3 or 4
+    // batches in flight (the decoder, the FFHWAccel adapter and the bench rotate 3 slots;
+    // VP9HIP_PIPELINE_SLOTS) the slots' streams then fit the 4 hardware queues (profiles/r05z:
+    // C3 11,205 vs 10,821 fps at 2 groups x 2 slots, C2 at 4 slots 17.6k vs 13.8k). 2 groups
+    // were best with two slots in flight (r02k).
+    int max_groups = 1;
     bool fuse_plf = true;               // VP9HIP_PLF=0: no fused intra + LF launches
     bool level_sched = true;            // VP9HIP_LEVELS=0: inter frames' intra SBs by diagonal
     int lf_rows = 1;                    // VP9HIP_LFROW: 0 LF as diagonal launches only, 1 k_lfr for
@@ -308,7 +318,7 @@ struct vp9hip_ctx {
     KCfg kcfg = { 1, 0 };               // kernel selections (VP9HIP_LFRO, VP9HIP_MCQ_SLICES)
     int host_threads = 16;              // VP9HIP_HOST_THREADS: host planning / staging threads
     uint32_t lfr_spin = 0;              // row-LF hand-off spin bound, 0 = 2^22 polls (test hook)
-    int test_reject = 0;                // the k-th static-plan batch staged is made invalid (test hook)
+    int test_reject = 0;                // k | f << 16: frame f of the k-th batch staged is made invalid (test hook)
     bool static_plan = true;            // VP9HIP_STATIC=0: keyframe batches planned like the others
     bool edge = true;                   // VP9HIP_EDGE=0: no SB edge columns (4:2:0 tile loader)
     bool resid_multi = true;            // VP9HIP_RESID_MULTI=0: one residual launch per tx size
@@ -328,7 +338,7 @@ struct vp9hip_ctx {
     Staged sl[MAX_SLOTS];               // the other slots (sl[slot] is a moved-out placeholder;
                                         // vp9hip_set_batch_slot swaps a slot in and out)
     int slot = 0;
-    int nstat_staged = 0;               // static-plan batches staged (VP9HIP_TEST_REJECT)
+    int nstaged = 0;                    // batches staged (the test_reject hook)
     hipStream_t pst = nullptr;          // device planner stream: a slot's planning overlaps the
                                         // other slot's pixel kernels (VP9HIP_SLOT_STREAMS=0 only)
     // Per-slot streams (default): each batch slot has its own main and group streams, swapped
@@ -458,7 +468,7 @@ extern "C" int vp9hip_open(int device, vp9hip_ctx **out)
               hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) == hipSuccess;
     for (int i = 0; ok && i < c->max_groups - 1; i++)
         ok = hipStreamCreateWithPriority(&c->xst[i], hipStreamNonBlocking, pix_prio) == hipSuccess;
-    if (c->slot_streams) {             // slot 1's set: with 2 groups, 4 streams = the 4 hardware queues
+    if (c->slot_streams) {             // slot 1's set (slots 2.. at their first selection)
         c->sst[0] = c->st;
         for (int i = 0; i < MAX_GROUPS - 1; i++) c->sxst[0][i] = c->xst[i];
         ok = ok && slot_streams_make(c, 1);
@@ -1435,9 +1445,11 @@ static int stage_dev(vp9hip_ctx *c, const DevIn &in)
     s.o_keycnt = o;                                           // zeroed every run: counts, status, byte totals
     s.o_status = al(o + ((size_t) keys + 1) * 4);
     s.o_fbytes = s.o_status + 256;
-    o = al(s.o_fbytes + (size_t) n * 16);
+    s.o_fbad = s.o_fbytes + (size_t) n * 16;                 // per-frame status bits
+    o = al(s.o_fbad + (size_t) n * 4);
     s.zero_bytes = o - s.o_keycnt;
-    s.summary_words = 1 + gidx.size() + keys + 1 + 4 * (size_t) n + 1;      // + status[1]
+    // status, count offsets, key offsets, byte totals, per-frame status, status[1]
+    s.summary_words = 1 + gidx.size() + keys + 1 + 5 * (size_t) n + 1;
     s.o_summary = o; o = al(o + s.summary_words * 4);
     s.o_sbs = o; o = al(o + (size_t) NS * sizeof(SBRec));
     s.o_wgs = o; o = al(o + (size_t) NS * sizeof(WGRec));
@@ -1511,11 +1523,16 @@ static int stage_dev(vp9hip_ctx *c, const DevIn &in)
         worker();
         for (auto &t : pool) t.join();
     }
-    if (s.stat && c->test_reject) {   // test hook (vp9hip_test_hooks): the k-th static-plan batch
-        // of the context gets an intra mode the device planner rejects in its first frame's
-        // first block, so the adapters' handling of a rejected batch can be tested from real
+    if (c->test_reject) {   // test hook (vp9hip_test_hooks): the k-th batch the context stages
+        // gets an intra block with a mode the device planner rejects as the first block of its
+        // frame f, so the front ends' handling of a rejected frame can be tested from real
         // bitstreams
-        if (++c->nstat_staged == c->test_reject && nb) ((vp9h_block *) (img + s.o_blocks))->mode[0] = 20;
+        const int k = c->test_reject & 0xffff, f = c->test_reject >> 16;
+        if (++c->nstaged == k && f < n && pf[f].nblk) {
+            vp9h_block *b = (vp9h_block *) (img + s.o_blocks) + pf[f].blk0;
+            b->intra = 1;
+            for (int m = 0; m < 4; m++) b->mode[m] = 20;
+        }
     }
     // the upload goes on the planner stream: the other batch slot's pixel kernels keep the
     // main stream busy meanwhile
@@ -1534,6 +1551,21 @@ static int stage_dev(vp9hip_ctx *c, const DevIn &in)
     return 0;
 }
 
+// The per-frame verdicts of a rejected batch from its summary: frames whose status bits are
+// set are rejected, the others get `good` (0: reconstructed, EAGAIN: not run). A status that
+// names no frame (PLS_BOUNDS, a shared buffer's capacity) rejects every frame. Returns the
+// number rejected.
+static int frame_verdicts(Staged &s, const uint32_t *sm, int good)
+{
+    const uint32_t *fbad = sm + 1 + s.n_gidx + s.nkey + 1 + 4 * (size_t) s.nframes;
+    const bool all = (sm[0] & PLS_BOUNDS) != 0;
+    s.fstat.assign(s.nframes, good);
+    int nbad = 0;
+    for (int i = 0; i < s.nframes; i++)
+        if (all || fbad[i]) { s.fstat[i] = VP9HIP_EINVALIDDATA; nbad++; }
+    return nbad;
+}
+
 // A static-plan batch's summary, once its run is complete (the caller waited for it):
 // planner status (AVERROR_INVALIDDATA: the batch was neutralised by k_pguard; kept in
 // s.status and returned by every later check until the slot is restaged) and the
@@ -1547,8 +1579,11 @@ static int finish_summary(vp9hip_ctx *c, Staged &s)
     HIPCHK(hipMemcpy(s.summary_h, s.arena + s.o_summary, s.summary_words * 4, hipMemcpyDeviceToHost));
     const uint32_t *sm = s.summary_h;
     if (sm[0]) {
-        fprintf(stderr, "vp9hip: batch rejected by the device planner (status 0x%x, bounds 0x%x)\n", sm[0],
-                sm[s.summary_words - 1]);
+        // k_pguard neutralised the rejected frames only (the whole batch if no frame is named):
+        // the others ran as if alone
+        const int nbad = frame_verdicts(s, sm, 0);
+        fprintf(stderr, "vp9hip: %d of %d frames rejected by the device planner (status 0x%x, bounds 0x%x)\n", nbad,
+                s.nframes, sm[0], sm[s.summary_words - 1]);
         s.status = VP9HIP_EINVALIDDATA;
         return s.status;
     }
@@ -1559,6 +1594,7 @@ static int finish_summary(vp9hip_ctx *c, Staged &s)
             const uint32_t *rng = sm + 1 + L.off;
             if (rng[1] > rng[0] && rng[1] - rng[0] > L.n) {
                 fprintf(stderr, "vp9hip: residual job range %u exceeds its staged bound %u\n", rng[1] - rng[0], (unsigned) L.n);
+                s.fstat.assign(s.nframes, VP9HIP_EBUG);
                 s.status = VP9HIP_EBUG;
                 return s.status;
             }
@@ -1618,6 +1654,7 @@ static int plan_dev(vp9hip_ctx *c)
     D.key_off = (uint32_t *) (A + s.o_keyoff);
     D.status = (uint32_t *) (A + s.o_status);
     D.fbytes = (unsigned long long *) (A + s.o_fbytes);
+    D.fbad = (uint32_t *) (A + s.o_fbad);
     D.sbs = (SBRec *) (A + s.o_sbs);
     D.wgs = (WGRec *) (A + s.o_wgs);
     D.pjobs = (PJob *) (A + s.o_pjobs);
@@ -1683,8 +1720,10 @@ static int plan_dev(vp9hip_ctx *c)
                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - pt0).count());
     const uint32_t *sm = s.summary_h;
     if (sm[0]) {                                              // the packets are inconsistent (PLS_*)
-        fprintf(stderr, "vp9hip: batch rejected by the device planner (status 0x%x, bounds 0x%x)\n", sm[0],
-                sm[s.summary_words - 1]);
+        // nothing was launched: the frames the planner did not reject are valid, not run
+        const int nbad = frame_verdicts(s, sm, VP9HIP_EAGAIN);
+        fprintf(stderr, "vp9hip: %d of %d frames rejected by the device planner (status 0x%x, bounds 0x%x)\n", nbad,
+                s.nframes, sm[0], sm[s.summary_words - 1]);
         return VP9HIP_EINVALIDDATA;
     }
     const uint32_t *gv = sm + 1, *ko = sm + 1 + s.n_gidx, *fb32 = ko + s.nkey + 1;
@@ -1837,6 +1876,7 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
     s.stat = false;
     s.summary_pending = false;
     s.status = 0;
+    s.fstat.assign(n, 0);
     for (int k = 0; k < K_N; k++) s.alg_bytes[k] = 0;
     s.ready = false;
 
@@ -1956,7 +1996,11 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
                 fb.mc.step[r][1] = 16 * fb.mc.scale[r][1] >> 14;
                 valid++;
             }
-            if (!valid) return VP9HIP_EINVALIDDATA;
+            if (!valid) {               // no usable reference scale (vp9.c:845-880): this frame only
+                s.fstat.assign(n, VP9HIP_EAGAIN);
+                s.fstat[i] = VP9HIP_EINVALIDDATA;
+                return VP9HIP_EINVALIDDATA;
+            }
         }
         fb.ss_h = c->ss_h; fb.ss_v = c->ss_v; fb.coef_size = csz;
         fb.pitch[0] = c->pitch[0]; fb.pitch[1] = c->pitch[1];
@@ -2643,8 +2687,20 @@ extern "C" int vp9hip_sync_slot(vp9hip_ctx *c, int slot)
     hipSetDevice(c->dev);
     Staged &g = slot_ref(c, slot);
     if (g.done_ev) HIPCHK(hipEventSynchronize(g.done_ev));
-    if (const int r = finish_summary(c, g)) return r;
-    return check_lfr(g);
+    // a batch with rejected frames still ran the others: their loop-filter hand-offs count
+    const int r = finish_summary(c, g);
+    if (r && r != VP9HIP_EINVALIDDATA) return r;
+    if (const int l = check_lfr(g)) return l;
+    return r;
+}
+
+extern "C" int vp9hip_batch_frame_status(vp9hip_ctx *c, int slot, int *status, int cap)
+{
+    if (!c || slot < 0 || slot >= MAX_SLOTS || cap < 0 || (cap > 0 && !status)) return VP9HIP_EINVAL;
+    const Staged &g = slot_ref(c, slot);
+    const int n = (int) g.fstat.size();
+    for (int i = 0; i < n && i < cap; i++) status[i] = g.fstat[i];
+    return n;
 }
 
 extern "C" int vp9hip_slot_stream_wait(vp9hip_ctx *c, int slot, void *stream)
@@ -2676,7 +2732,8 @@ extern "C" int vp9hip_sync(vp9hip_ctx *c)
     int err = 0;
     for (int k = 0; k < MAX_SLOTS; k++) {
         int r = finish_summary(c, slot_ref(c, k));
-        if (!r) r = check_lfr(slot_ref(c, k));
+        if (!r || r == VP9HIP_EINVALIDDATA)
+            if (const int l = check_lfr(slot_ref(c, k))) r = l;
         if (r && !err) err = r;
     }
     if (err) return err;
@@ -2982,7 +3039,7 @@ extern "C" int vp9hip_plan_stats(const vp9h_frame *f, double *out, int cap)
             r = merge_mixed(s, sbi);
             if (r) return r;
         }
-    for (int i = 0; i < 16; i++) out[i] = 0;
+    for (int i = 0; i < std::min(cap, 23); i++) out[i] = 0;     // every value this writes, some summed
     out[0] = (double) s.sbs.size();
     out[1] = (double) s.passes.size();
     out[2] = (double) s.pjobs.size();

@@ -30,7 +30,10 @@
 extern "C" {
 #endif
 
-#define VP9HIP_ABI_VERSION 1
+/* 2: vp9h_synth_params / vp9h_enc_params end in a vp9h_seg_params; vp9hip_test_hooks,
+ * vp9hip_batch_frame_status and VP9HIP_PIPELINE_SLOTS added. Callers check
+ * vp9hip_abi_version() == VP9HIP_ABI_VERSION before passing structs. */
+#define VP9HIP_ABI_VERSION 2
 
 /* FFmpeg AVERROR values used by the boundary (libavutil/error.h). */
 #define VP9HIP_EINVAL       (-22)          /* AVERROR(EINVAL)   */
@@ -109,9 +112,10 @@ typedef struct vp9hip_ctx vp9hip_ctx;
 int  vp9hip_open(int device, vp9hip_ctx **out);
 void vp9hip_close(vp9hip_ctx *ctx);
 /* Test hooks, copied by every context opened afterwards (0, 0 = off, the default):
- * reject_batch = k makes the k-th static-plan batch the context stages carry an intra mode
- * the device planner rejects; lfr_spin = n bounds the row loop filter's hand-off waits to
- * n polls (forcing its timeout path). No reference counterpart; never called in production. */
+ * reject_batch = k | f << 16 makes frame f of the k-th batch the context stages (k >= 1,
+ * restagings count) start with an intra block whose mode the device planner rejects;
+ * lfr_spin = n bounds the row loop filter's hand-off waits to n polls (forcing its timeout
+ * path). No reference counterpart; never called in production. */
 void vp9hip_test_hooks(int reject_batch, uint32_t lfr_spin);
 
 /* Allocate `nbufs` device frame buffers of w x h (padded to 64 internally). */
@@ -178,6 +182,11 @@ int64_t vp9hip_stripe(vp9hip_ctx *ctx, int frame, int tile_lo, int tile_hi, void
 
 /* Batch slots per context. */
 #define VP9HIP_MAX_SLOTS 4
+/* Batch slots the decoder (vp9hip_decoder_*) and the FFHWAccel adapter rotate: batch k + 3
+ * is staged only after batch k's slot is checked, so three batches are in flight, each on
+ * one frame-group stream (the context default: the slots' streams fit the 4 hardware
+ * queues; bench.py times C3 / C4 / C5 at this depth, C2 at 4). */
+#define VP9HIP_PIPELINE_SLOTS 3
 /* Select batch slot 0 .. VP9HIP_MAX_SLOTS - 1 (default 0): stage_batch*, run_batch,
  * batch_phases, run_phase and stripe act on the current slot. Each slot holds its own
  * staged batch (arena, plan, launch graph) and runs on HIP streams of its own (slots 2..
@@ -189,6 +198,16 @@ int  vp9hip_set_batch_slot(vp9hip_ctx *ctx, int slot);
 /* Wait for the last run of batch slot `slot` only (other slots' work may continue)
  * and check it as vp9hip_sync does (VP9HIP_EBUG: a loop-filter hand-off timed out). */
 int  vp9hip_sync_slot(vp9hip_ctx *ctx, int slot);
+/* Per-frame outcome of the last stage / run of batch slot `slot` after stage_batch*,
+ * run_batch, vp9hip_sync_slot or vp9hip_sync reported AVERROR_INVALIDDATA for it (the device
+ * planner or the staging checks rejected frames): status[i] (staging order, up to cap) is 0
+ * for a frame that was reconstructed, AVERROR_INVALIDDATA for a rejected frame, and
+ * AVERROR(EAGAIN) for a valid frame that was not run (a batch planned on the host's
+ * schedule stops before its pixel launches: stage those frames again). Keyframe batches
+ * (launch lists fixed at staging) reconstruct the frames the planner did not reject; a
+ * rejection that names no frame rejects all. Returns the batch's frame count. No reference
+ * counterpart beyond vp9.c failing only the corrupt frame's decode (:1827-1832). */
+int  vp9hip_batch_frame_status(vp9hip_ctx *ctx, int slot, int *status, int cap);
 /* Make HIP stream `stream` (a hipStream_t; NULL: the null stream) wait for the last run of
  * batch slot `slot`, without a host wait: work enqueued on it afterwards sees that run's
  * frames. The loop-filter hand-off check needs a host wait (vp9hip_sync_slot). */
@@ -502,7 +521,8 @@ typedef struct vp9hip_decoder vp9hip_decoder;
 typedef struct vp9hip_decoder_params {
     int32_t device;
     int32_t max_batch;             /* frames per GPU batch (decoder delay), default 16; the  */
-                                   /* decoder holds 8 + 2 max_batch + extra_bufs buffers      */
+                                   /* decoder holds 8 + (VP9HIP_PIPELINE_SLOTS + 1) max_batch */
+                                   /* + extra_bufs buffers                                    */
     int32_t extra_bufs;            /* output frames the caller may hold at once, default 4     */
     int32_t max_width, max_height; /* buffer size; 0: the first keyframe's (larger inter      */
                                    /* frames, e.g. reference scaling up, need it set)         */

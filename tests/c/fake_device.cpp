@@ -30,6 +30,7 @@ struct Batch {
     std::vector<int> out, refs;
     std::vector<std::pair<int, int>> refwh;     // visible sizes of the references, as staged
     uint64_t seq = 0;
+    int slot = 0;
 };
 }
 
@@ -42,12 +43,13 @@ struct vp9hip_ctx {
     Batch staged[VP9HIP_MAX_SLOTS];
     bool have[VP9HIP_MAX_SLOTS] = {};
     uint64_t slot_last[VP9HIP_MAX_SLOTS] = {};     // sequence of each slot's last launch
+    int serr[VP9HIP_MAX_SLOTS] = {};               // per slot: error of its last run
+    std::vector<int> fstat[VP9HIP_MAX_SLOTS];      // per slot: per-frame outcome of its last run
     // the worker ("device queue")
     std::mutex mu;
     std::condition_variable cv, cv_done;
     std::deque<Batch> q;
     uint64_t launched = 0, finished = 0;
-    int err = 0;
     bool stop = false;
     std::thread worker;
 };
@@ -74,7 +76,8 @@ static void run_worker(vp9hip_ctx *c)
         c->q.pop_front();
         lk.unlock();
         int e = 0;
-        for (size_t i = 0; i < b.pk.size() && !e; i++) {
+        std::vector<int> fst(b.pk.size(), 0);
+        for (size_t i = 0; i < b.pk.size(); i++) {
             const vp9h_frame &f = b.pk[i].f;
             const int o = b.out[i];
             vp9o_planes cur, refs[3];
@@ -83,10 +86,12 @@ static void run_worker(vp9hip_ctx *c)
             for (int r = 0; r < 3; r++) planes_of(c, b.refs[3 * i + r], &refs[r], b.refwh[3 * i + r]);
             // FAKE_NO_RECON=1: no reconstruction (host-side timing of the adapter only)
             static const bool norecon = getenv("FAKE_NO_RECON") && atoi(getenv("FAKE_NO_RECON"));
-            if (!norecon) e = vp9o_decode_frame(&f, &cur, intra ? nullptr : refs);
+            const int fe = norecon ? 0 : vp9o_decode_frame(&f, &cur, intra ? nullptr : refs);
+            if (fe) { fst[i] = VP9HIP_EINVALIDDATA; e = VP9HIP_EINVALIDDATA; }   // that frame only
         }
         lk.lock();
-        if (e && !c->err) c->err = e;
+        c->serr[b.slot] = e;
+        c->fstat[b.slot] = fst;
         c->finished = b.seq;
         c->cv_done.notify_all();
     }
@@ -189,6 +194,9 @@ int vp9hip_run_batch(vp9hip_ctx *c)
         p.f.coefs = p.coefs.data();
     }
     b.seq = ++c->launched;
+    b.slot = c->slot;
+    c->serr[c->slot] = 0;
+    c->fstat[c->slot].assign(b.pk.size(), 0);
     c->slot_last[c->slot] = b.seq;
     c->q.push_back(std::move(b));
     c->cv.notify_one();
@@ -200,7 +208,16 @@ int vp9hip_sync_slot(vp9hip_ctx *c, int slot)
     if (!c || slot < 0 || slot >= VP9HIP_MAX_SLOTS) return VP9HIP_EINVAL;
     wait_seq(c, c->slot_last[slot]);
     std::lock_guard<std::mutex> lk(c->mu);
-    return c->err;
+    return c->serr[slot];
+}
+
+int vp9hip_batch_frame_status(vp9hip_ctx *c, int slot, int *status, int cap)
+{
+    if (!c || slot < 0 || slot >= VP9HIP_MAX_SLOTS || cap < 0 || (cap > 0 && !status)) return VP9HIP_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    const int n = (int) c->fstat[slot].size();
+    for (int i = 0; i < n && i < cap; i++) status[i] = c->fstat[slot][i];
+    return n;
 }
 
 int vp9hip_sync(vp9hip_ctx *c)
@@ -208,7 +225,9 @@ int vp9hip_sync(vp9hip_ctx *c)
     if (!c) return VP9HIP_EINVAL;
     wait_seq(c, c->launched);
     std::lock_guard<std::mutex> lk(c->mu);
-    return c->err;
+    for (int k = 0; k < VP9HIP_MAX_SLOTS; k++)
+        if (c->serr[k]) return c->serr[k];
+    return 0;
 }
 
 int vp9hip_slot_stream_wait(vp9hip_ctx *c, int slot, void *)

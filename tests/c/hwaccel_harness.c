@@ -71,6 +71,9 @@ typedef struct Consumer {
     vp9hip_hwframe q[512];             /* output frames not read yet (av_frame_ref'd) */
     int head, n;
     int frames_out;
+    /* frames whose read failed (transfer / sync: the frame's own decode error, as
+     * av_hwframe_transfer_data reports it for that frame); the decode goes on */
+    int nfailed, failed_idx[1024], failed_err[1024];
     /* MODE "thread": the queue is shared with the consumer thread */
     int threaded, busy, stop, err;
     pthread_t th;
@@ -91,7 +94,12 @@ static int consume_one(Consumer *c)
         pl[1] = malloc((size_t) ls[1] * chh);
         pl[2] = malloc((size_t) ls[2] * chh);
         r = vp9hip_hwframe_transfer(c->h, f, pl, ls);               /* transfer_data_from */
-        if (r >= 0 && c->out) {
+        if (r < 0 && c->out) {           /* a failed frame keeps its place in the output: zeros */
+            memset(pl[0], 0, (size_t) ls[0] * ht);
+            memset(pl[1], 0, (size_t) ls[1] * chh);
+            memset(pl[2], 0, (size_t) ls[2] * chh);
+        }
+        if ((r >= 0 || r == VP9HIP_EINVALIDDATA || r == VP9HIP_EBUG) && c->out) {
             fwrite(pl[0], 1, (size_t) ls[0] * ht, c->out);
             fwrite(pl[1], 1, (size_t) ls[1] * chh, c->out);
             fwrite(pl[2], 1, (size_t) ls[2] * chh, c->out);
@@ -101,6 +109,14 @@ static int consume_one(Consumer *c)
         r = vp9hip_hwframe_sync(c->h, f);                            /* the frame's pixels are final */
     }
     const int u = vp9hip_hwframe_unref(c->h, f);                     /* av_frame_unref */
+    if (r == VP9HIP_EINVALIDDATA || r == VP9HIP_EBUG) {               /* this frame's error */
+        if (c->nfailed < 1024) {
+            c->failed_idx[c->nfailed] = c->frames_out;
+            c->failed_err[c->nfailed] = r;
+        }
+        c->nfailed++;
+        r = 0;
+    }
     if (c->threaded) pthread_mutex_lock(&c->mu);
     c->head = (c->head + 1) % 512;
     c->n--;
@@ -179,7 +195,7 @@ int main(int argc, char **argv)
     const int threaded = argc > 8 && !strcmp(argv[8], "thread");
     const int depth = argc > 9 ? atoi(argv[9]) : 0;
     const int extra = argc > 10 ? atoi(argv[10]) : 2 + lag;
-    if (argc > 11) {                     /* test hooks: reject the k-th static batch, row-LF spin bound */
+    if (argc > 11) {                     /* test hooks: reject a frame of the k-th batch, row-LF spin bound */
         char *e = NULL;
         const int reject = (int) strtol(argv[11], &e, 0);
         vp9hip_test_hooks(reject, e && *e == ',' ? (uint32_t) strtoul(e + 1, NULL, 0) : 0u);
@@ -294,5 +310,11 @@ int main(int argc, char **argv)
     free(buf);
     if (r < 0) { fprintf(stderr, "decode: %d after %d frames\n", r, c.frames_out); return 1; }
     printf("frames %d seconds %.6f\n", c.frames_out, (double) (t1.tv_sec - t0.tv_sec) + 1e-9 * (double) (t1.tv_nsec - t0.tv_nsec));
+    if (c.nfailed) {                     /* rc 3: every other frame was read; these failed */
+        fprintf(stderr, "failed frames:");
+        for (int i = 0; i < c.nfailed && i < 1024; i++) fprintf(stderr, " %d:%d", c.failed_idx[i], c.failed_err[i]);
+        fprintf(stderr, "\n");
+        return 3;
+    }
     return 0;
 }

@@ -64,10 +64,17 @@ def test_default_bound_decodes_bit_exact(v9, orc):
 
 def test_hwaccel_fails_frames_of_a_timed_out_batch(v9, tmp_path):
     """The FFHWAccel path checks the same hand-off words before a frame is read
-    (vp9hip_hwframe_sync / transfer): the harness's decode fails with VP9HIP_EBUG."""
-    from test_hwaccel_harness import run_harness
+    (vp9hip_hwframe_sync / transfer). The consumer reads each frame at once (lag 0), so every
+    read launches the batch holding just that frame: the keyframe's batch times out and the
+    keyframe fails with VP9HIP_EBUG; the P frames, predicted from it, fail with
+    AVERROR_INVALIDDATA without running. The harness reads them all and reports them."""
+    from test_hwaccel_harness import failed_frames, run_harness
     ivf = tmp_path / "t.ivf"
     ivf.write_bytes(v9.ivf_write(_gop(v9), 1920, 1080))
+    want = {0: v9.EBUG, 1: v9.EINVALIDDATA, 2: v9.EINVALIDDATA, 3: v9.EINVALIDDATA}
     for mode in ("download", "device"):
-        rc, _, _, err = run_harness(ivf, "-", 8, 1, 1, 1, 0, mode, 4, hooks=(0, 1))
-        assert rc == 1 and ("decode: %d" % v9.EBUG) in err, (mode, err)
+        rc, n, _, err = run_harness(ivf, "-", 8, 1, 1, 1, 0, mode, 4, hooks=(0, 1))
+        assert rc == 3 and n == 4 and failed_frames(err) == want, (mode, err)
+        # read 4 behind: one batch of 4 launches whole, and all of its frames time out
+        rc, n, _, err = run_harness(ivf, "-", 8, 1, 1, 1, 4, mode, 4, hooks=(0, 1))
+        assert rc == 3 and n == 4 and failed_frames(err) == {i: v9.EBUG for i in range(4)}, (mode, err)

@@ -3,9 +3,11 @@ k_lfro (VP9HIP_LFRO=0), k_mcq's task slices per unit group (VP9HIP_MCQ_SLICES), 
 launch per transform size (VP9HIP_RESID_MULTI=0), and intra SBs reading their left
 neighbour's column from the frame rows instead of the saved SB edges (VP9HIP_EDGE=0, also on
 the C3 keyframe shape); inter frames' intra levels as one k_pred launch per level instead of
-k_predd (VP9HIP_PRED_DF=0), k_predd on the 8K phases too (VP9HIP_PRED_DF_MAX) and with a
-3-workgroup grid that loops over every ticket (VP9HIP_PRED_DF_WGS=3), and the k_predd work
-inside the k_lfro launch (VP9HIP_PRED_LF_FUSE=1; with DF_WGS=4: one intra worker workgroup). Each is switched (read when the context opens) on a key + P chain of
+k_predd (VP9HIP_PRED_DF=0); the k_predd work as a launch of its own instead of intra workers
+inside the phase's k_lfro launch (VP9HIP_PRED_LF_FUSE=0; the default is fused), with its
+default grid, on the 8K phases (VP9HIP_PRED_DF_MAX) and with a 3-workgroup grid that loops
+over every ticket (VP9HIP_PRED_DF_WGS=3); the fused form on the 8K phases and with one
+intra worker workgroup (DF_WGS=4). Each is switched (read when the context opens) on a key + P chain of
 the C2 (1080p 8-bit) or C5 (8K 10-bit) shape, decoded through the bench's batch path and
 compared with the CPU oracle. (The losing alternates of rounds 1-4 -- the single-tile row LF,
 k_mc / k_mcp, MC tickets inside k_lfrd -- were removed in round 5; DESIGN.md §5 keeps
@@ -31,11 +33,14 @@ CASES = [
     ({"VP9HIP_EDGE": "0"}, "C3", 3),
     ({"VP9HIP_EDGE": "0"}, "C2", 3),
     ({"VP9HIP_PRED_DF": "0"}, "C2", 4),
+    # the standalone k_predd launch (intra workers not fused into k_lfro), with its default
+    # grid, on the 8K phases, and with a 3-workgroup grid that loops over every ticket
+    ({"VP9HIP_PRED_LF_FUSE": "0"}, "C2", 4),
+    ({"VP9HIP_PRED_LF_FUSE": "0", "VP9HIP_PRED_DF_MAX": "100000"}, "C5", 2),
+    ({"VP9HIP_PRED_LF_FUSE": "0", "VP9HIP_PRED_DF_WGS": "3"}, "C2", 4),
+    # the default fused form: on the 8K phases, and with one intra worker workgroup
     ({"VP9HIP_PRED_DF_MAX": "100000"}, "C5", 2),
-    ({"VP9HIP_PRED_DF_WGS": "3"}, "C2", 4),
-    ({"VP9HIP_PRED_LF_FUSE": "1"}, "C2", 4),
-    ({"VP9HIP_PRED_LF_FUSE": "1", "VP9HIP_PRED_DF_MAX": "100000"}, "C5", 2),
-    ({"VP9HIP_PRED_LF_FUSE": "1", "VP9HIP_PRED_DF_WGS": "4"}, "C2", 4),
+    ({"VP9HIP_PRED_DF_WGS": "4"}, "C2", 4),
 ]
 
 

@@ -70,7 +70,8 @@ def _read_frames(path, w, h, bpp, ssh, ssv):
 
 def run_harness(ivf, out, bpp, ssh, ssv, passes=2, lag=0, mode="download", depth=0, env=None, timeout=120, extra=None,
                 hooks=None):
-    """The harness binary; returns (returncode, frames, seconds, stderr). extra: the frame
+    """The harness binary; returns (returncode, frames, seconds, stderr): returncode 3 =
+    every frame was read but some failed (failed_frames(stderr)). extra: the frame
     count handed to frame_params (default 2 + lag); hooks: (reject_batch, lfr_spin), the
     vp9hip_test_hooks values the harness sets before it opens the decoder."""
     args = [HARNESS, str(ivf), str(out), str(bpp), str(ssh), str(ssv), str(passes), str(lag), mode, str(depth)]
@@ -80,9 +81,17 @@ def run_harness(ivf, out, bpp, ssh, ssv, passes=2, lag=0, mode="download", depth
         args.append("%d,%d" % hooks)
     r = subprocess.run(args, capture_output=True, text=True, timeout=timeout, env=env)
     f = r.stdout.split()
-    if r.returncode or len(f) < 4:
+    if r.returncode not in (0, 3) or len(f) < 4:
         return r.returncode, None, None, r.stderr
-    return 0, int(f[1]), float(f[3]), r.stderr
+    return r.returncode, int(f[1]), float(f[3]), r.stderr
+
+
+def failed_frames(err):
+    """{output index: error} of the frames the harness could not read (its rc 3 report)."""
+    for line in err.splitlines():
+        if line.startswith("failed frames:"):
+            return {int(a): int(b) for a, b in (t.split(":") for t in line.split(":", 1)[1].split())}
+    return {}
 
 
 # async depth (frames per launch) x consumer lag: 16 / 0 reads each frame at once (every

@@ -7,7 +7,7 @@ TAG=$1; shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
-ARGS=${*:-"--steps 3 --warmup 1 --no-cpu-baseline"}    # the bench workload (C3, 120 frames)
+ARGS=${*:-"--serial-only --steps 10 --warmup 2"}    # the bench workload (C3, 120 frames): its serialised timing steps
 cd /tmp && export TMPDIR=/tmp
 run() { local name=$1; shift
   timeout -k 10 300 rocprofv3 "$@" -d "$OUT/$name" -o run --output-format csv -- python3 "$ROOT/bench.py" $ARGS > "$OUT/$name.log" 2>&1
