@@ -23,6 +23,7 @@ import argparse
 import importlib
 import json
 import os
+import re
 import sys
 import time
 
@@ -298,7 +299,8 @@ def main():
     if os.path.exists(kf) and shape_ok:
         import csv
         for r in csv.DictReader(open(kf)):
-            if r["Name"].split("(")[0].split("<")[0].split()[-1] == dom:
+            m = re.search(r"\b(k_\w+?)\s*[<(]", r["Name"])
+            if m and m.group(1) == dom:
                 t_us = float(r["AverageNs"]) / 1000.0
                 t_frac = bytes_per_launch / (t_us * 1e-6) / 1e9 / HBM_PEAK_GBS
                 trace = {"avg_launch_us": round(t_us, 2), "calls": int(r["Calls"]), "frac": round(t_frac, 5),

@@ -42,10 +42,12 @@ typedef struct PlanFrame {
 } PlanFrame;
 
 /* Status bits (PlanDev.status[0], and per frame in PlanDev.fbad); any bit fails the frame
- * that set it with AVERROR_INVALIDDATA. Each frame's records address only its own blocks,
- * eobs, coefficients and SB slots (offsets rebased on the frame's own ranges, residual jobs
- * capped at the SB's counts), so a rejected frame leaves the other frames' plans intact;
- * PLS_BOUNDS (a shared buffer's capacity) cannot be attributed and fails the batch. */
+ * that set it with AVERROR_INVALIDDATA. A frame's records address only its own blocks and SB
+ * slots, its residual jobs stay inside its SBs' counted ranges, and its eobs / coefficients
+ * are where the batch-wide scans put them as long as every frame's totals match its packet
+ * counts (checked: PLS_TOTAL), so a rejected frame leaves the other frames' plans intact.
+ * PLS_BOUNDS (a shared buffer's capacity) and PLS_TOTAL cannot be attributed and fail the
+ * batch. */
 #define PLS_BLOCK      1u         /* a block field out of range                             */
 #define PLS_ORDER      2u         /* blocks not in decode order / an SB without blocks      */
 #define PLS_EOB        4u         /* eob count or value inconsistent with the packet        */
@@ -54,6 +56,7 @@ typedef struct PlanFrame {
 #define PLS_REF       32u         /* reference index / scale invalid                        */
 #define PLS_SCHED     64u         /* pass scheduling failed (internal)                      */
 #define PLS_BOUNDS   128u         /* a planner index out of its buffer (internal, status[1]) */
+#define PLS_TOTAL    256u         /* a frame's eob / coefficient totals disagree with its counts */
 
 /* Device buffers of a device-planned batch (all in the batch arena). */
 typedef struct PlanDev {
@@ -94,6 +97,7 @@ typedef struct PlanDev {
     int dbg;                         /* diagnostics (VP9HIP_PLAN_DBG): ablation switches, timing only */
     int static_lists;                /* the intra step lists were staged by the host (static plan):  */
                                      /* no step keys; an intra-frame SB without intra jobs fails    */
+    const uint32_t *stat_ko;         /* static plan: the step lists' offsets (nkeys + 1), k_psort    */
 } PlanDev;
 
 #endif

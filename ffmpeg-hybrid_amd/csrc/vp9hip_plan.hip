@@ -177,16 +177,14 @@ DEV Tx sb_tx(const vp9h_block *blk, const uint32_t *pre, int nb, uint32_t t, int
     return sb_tx_at<SSH, SSV>(blk, pre, sb_locate(pre, 3 * nb, t), t, cols, rows);
 }
 
-// The eob of tx t (0 for skipped blocks), range-checked against the frame's own eobs: the
-// block scan is rebased on the frame's first block (ebase = blk_eob0[F.blk0]), so a frame
-// whose eob count disagrees with its packet cannot shift another frame's eobs.
-template <class B> DEV int tx_eob(const PlanDev &D, const PlanFrame &F, uint32_t ebase, const B &b, const Tx &tx,
-                                  const uint32_t *pre, uint32_t b0, uint32_t &st)
+// The eob of tx t (0 for skipped blocks), range-checked against the packet. (A frame whose
+// eob count disagrees with its packet shifts the later frames' eobs: k_pkeys' totals check
+// rejects the batch then, PLS_TOTAL.)
+template <class B> DEV int tx_eob(const PlanDev &D, const B &b, const Tx &tx, const uint32_t *pre, uint32_t b0, uint32_t &st)
 {
     if (b.skip) return 0;
-    const uint32_t r = D.blk_eob0[b0 + tx.b] - ebase + ((pre[tx.k] & 1023) - (pre[3 * tx.b] & 1023)) + (uint32_t) tx.l;
-    const uint32_t i = F.eob0 + r;
-    if (r >= F.neob || i >= D.total_eobs) { st |= PLS_EOB; return 0; }
+    const uint32_t i = D.blk_eob0[b0 + tx.b] + ((pre[tx.k] & 1023) - (pre[3 * tx.b] & 1023)) + (uint32_t) tx.l;
+    if (i >= D.total_eobs) { st |= PLS_EOB; return 0; }
     const int e = D.eobs[i];
     if (e > (16 << (2 * tx.g.txs))) { st |= PLS_EOB; return 0; }
     return e;
@@ -307,7 +305,6 @@ __global__ __launch_bounds__(64) void k_psb(PlanDev D)
     wsync();
     const uint32_t tot = sb_prefix<SSH, SSV>(blk, nb, cols, rows, G.mine, pre, lane);
     const uint32_t T = pl_min((int) (tot & 1023), JCAP);
-    const uint32_t ebase = D.blk_eob0[F.blk0];
     uint32_t ncoef = 0, kcnt = 0;
     for (uint32_t t0 = 0; t0 < T; t0 += 64) {
         const uint32_t t = t0 + (uint32_t) lane;
@@ -315,7 +312,7 @@ __global__ __launch_bounds__(64) void k_psb(PlanDev D)
         if (t < T) {
             const Tx tx = sb_tx_at<SSH, SSV>(blk, pre, sb_locate(pre, 3 * nb, t), t, cols, rows);
             const PBlk &b = blk[tx.b];
-            const int e = tx_eob(D, F, ebase, b, tx, pre, b0, st);
+            const int e = tx_eob(D, b, tx, pre, b0, st);
             ncoef += (uint32_t) e;
             int txtp = 0;
             if (b.intra) {
@@ -403,6 +400,9 @@ template <int JCAP> struct alignas(16) PlanLds {   // 16: jmap rows are stored 1
 };
 static_assert(sizeof(uint16_t[3][256]) <= sizeof(uint32_t[256 + 2 * 64]), "the unit map fits the heights' region");
 #define JA_TRX (1u << 30)
+// unit-map entry: job | units to its right edge << 10 | units to its bottom edge << 13 (0..7
+// each: a job is at most 8 units wide); 0xffff (job 1023 > JCAP) marks a unit no job covers
+#define JM_ENT(j, r, b) ((uint32_t) (j) | (uint32_t) (r) << 10 | (uint32_t) (b) << 13)
 
 // edges the job's (substituted) mode reads: 1 left, 2 top, 4 top-left, 8 top-right (pl_intra_job)
 DEV uint32_t needs_of(uint32_t a)
@@ -466,17 +466,12 @@ __global__ __launch_bounds__(64) void k_pjob(PlanDev D)
     // contiguous in the packet (its coded blocks' tx in decode order): one coalesced load
     // into LDS, then each tx picks its entry (skipped blocks have none)
     {
-        // the block scan rebased on the frame's first block and eob range (tx_eob)
-        const uint32_t ebase = D.blk_eob0[F.blk0];
         const uint32_t be = lane <= nb ? D.blk_eob0[b0 + (uint32_t) lane] : 0u;      // nb + 1 entries
         if (lane < nb) S.eb[lane] = be;
-        const uint32_t E0 = rdl(be, 0), E1 = rdl(be, nb), R0 = E0 - ebase;
+        const uint32_t E0 = rdl(be, 0), E1 = rdl(be, nb);
         uint32_t E = E1 - E0;
-        if (E1 < E0 || E > (uint32_t) JCAP || R0 > F.neob || E > F.neob - R0 || F.eob0 + R0 + E > D.total_eobs) {
-            st |= PLS_EOB;
-            E = 0;
-        }
-        for (uint32_t i = (uint32_t) lane; i < E; i += 64) S.co[i] = D.eobs[F.eob0 + R0 + i];
+        if (E1 < E0 || E > (uint32_t) JCAP || E1 > D.total_eobs) { st |= PLS_EOB; E = 0; }
+        for (uint32_t i = (uint32_t) lane; i < E; i += 64) S.co[i] = D.eobs[E0 + i];
         wsync();
         for (int t = lane; t < T; t += 64) {
             const int k = S.own[t], b = (k * 171) >> 9;
@@ -512,10 +507,7 @@ __global__ __launch_bounds__(64) void k_pjob(PlanDev D)
         const uint32_t ci = D.seg_pre1[G.seg] + D.slot_pos[slot];
         rb = inb(D, ci, D.cap_cntm, 16u) ? D.cntm0[ci] : 0u;
     }
-    // the SB's first coefficient, rebased on the frame's own coefficient range: the scan's
-    // value at the frame's first SB in decode order (dord = slot0) is the frame's origin
-    const uint32_t coef_sb = inb(D, G.dord, D.nslots, 32u) ? F.coef0 + (D.sb_coef0[G.dord] - D.sb_coef0[F.slot0]) : 0u;
-    const uint32_t coef_end = F.coef0 + F.ncoef;
+    const uint32_t coef_sb = inb(D, G.dord, D.nslots, 32u) ? D.sb_coef0[G.dord] : 0u;
     const uint32_t rbase = slot * D.rcap;
     unsigned long long ibytes = 0;
     wsync();
@@ -543,11 +535,7 @@ __global__ __launch_bounds__(64) void k_pjob(PlanDev D)
             if (e0 && G.mine) {
                 uint32_t coef = coef_sb + S.co[t];
                 int e = e0;
-                if (coef < F.coef0 || coef + (uint32_t) e > coef_end || coef_end > D.total_coefs) {
-                    st |= PLS_COEF;
-                    e = 0;
-                    coef = 0;
-                }
+                if (coef + (uint32_t) e > D.total_coefs) { st |= PLS_COEF; e = 0; coef = 0; }
                 r.coef = coef;
                 r.eob = (uint16_t) e;
                 r.frame = (uint16_t) F.frame;
@@ -612,10 +600,13 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
     const uint32_t rbase = slot * D.rcap;
     uint32_t st = 0;
     const int NJ = pl_min((int) D.sb_nj[slot], JCAP);
-    for (int i = lane; i < 3 * 256; i += 64) (&S.u.jmap[0][0])[i] = 0xffff;
+    for (int i = lane; i < 3 * 256 / 8; i += 64) ((uint4 *) &S.u.jmap[0][0])[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
     for (int j = lane; j < NJ; j += 64) S.ja[j] = D.jobw[(size_t) slot * JCAP + (uint32_t) j];
     wsync();
-    for (int j = lane; j < NJ; j += 64) {                  // the unit map: each job's 4x4 units
+    // the unit map: each job's 4x4 units hold JM_ENT(job, units to the job's right edge, units
+    // to its bottom edge), so the producer walk below steps past a producer's extent from the
+    // entry alone (one LDS read per producer instead of the entry and the job's word)
+    for (int j = lane; j < NJ; j += 64) {
         const uint32_t a = S.ja[j];
         const int p = a & 3, step = 1 << ((a >> 2) & 3), ux0 = (a >> 12) & 15, uy0 = (a >> 16) & 15;
         const int units = p ? CW : 16, unitsv = p ? CH : 16;
@@ -623,17 +614,20 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
             // a job is an aligned square inside its plane's 16-unit rows, so each of its unit
             // rows is one aligned 2 / 4 / 8 / 16-byte store: a 32x32 job paints 8 rows, not 64
             // units (the loop's trip count is the largest job's of the chunk)
-            const uint32_t w = (uint32_t) j | (uint32_t) j << 16;
             uint16_t *row = &S.u.jmap[p][uy0 * 16 + ux0];
             for (int v = 0; v < step && uy0 + v < unitsv; v++, row += 16) {
-                if (step == 1) *row = (uint16_t) j;
-                else if (step == 2) *(uint32_t *) row = w;
-                else if (step == 4) *(uint2 *) row = make_uint2(w, w);
-                else *(uint4 *) row = make_uint4(w, w, w, w);
+                const uint32_t b = JM_ENT(j, 0, step - 1 - v);
+                // two units: right distances r and r - 1 (the lower address first)
+                auto e2 = [&](uint32_t r) { return (b | r << 10) | (b | (r - 1) << 10) << 16; };
+                if (step == 1) *row = (uint16_t) b;
+                else if (step == 2) *(uint32_t *) row = e2(1);
+                else if (step == 4) *(uint2 *) row = make_uint2(e2(3), e2(1));
+                else *(uint4 *) row = make_uint4(e2(7), e2(5), e2(3), e2(1));
             }
         } else {
             for (int v = uy0; v < uy0 + step && v < unitsv; v++)
-                for (int u = ux0; u < ux0 + step && u < units; u++) S.u.jmap[p][v * 16 + u] = (uint16_t) j;
+                for (int u = ux0; u < ux0 + step && u < units; u++)
+                    S.u.jmap[p][v * 16 + u] = (uint16_t) JM_ENT(j, ux0 + step - 1 - u, uy0 + step - 1 - v);
         }
     }
     wsync();
@@ -657,12 +651,12 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
             if (u < 0) u = 0;
             const uint16_t *row = S.u.jmap[p] + (uy0 - 1) * 16;
             while (u < u1) {
-                const int d = row[u];
-                if (d == 0xffff) { u++; continue; }
-                const uint32_t ad = S.ja[d];
+                const uint32_t e = row[u];
+                if (e == 0xffff) { u++; continue; }
+                const int d = (int) (e & 1023);
                 if (u == ux0 - 1) tl = d;
                 if (d < j) fn(d);
-                u = pl_max((int) ((ad >> 12) & 15) + (1 << ((ad >> 2) & 3)), u + 1);
+                u += (int) ((e >> 10) & 7) + 1;               // past the producer's right edge
             }
         }
         if (ux0 > 0 && (nd & 1)) {
@@ -670,11 +664,11 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
             int v = uy0;
             const uint16_t *col = S.u.jmap[p] + ux0 - 1;
             while (v < v1) {
-                const int d = col[v * 16];
-                if (d == 0xffff) { v++; continue; }
-                const uint32_t ad = S.ja[d];
+                const uint32_t e = col[v * 16];
+                if (e == 0xffff) { v++; continue; }
+                const int d = (int) (e & 1023);
                 if (d < j && d != tl) fn(d);
-                v = pl_max((int) ((ad >> 16) & 15) + (1 << ((ad >> 2) & 3)), v + 1);
+                v += (int) (e >> 13) + 1;                     // past the producer's bottom edge
             }
         }
     };
@@ -896,6 +890,7 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
         D.sb_info[slot] = has | dmask;
         if (D.static_lists) {
             if (!has && G.mine) st |= PLS_SCHED;          // the staged step list holds every SB
+            D.sb_kpos[slot] = (uint32_t) npass;           // k_psort's key (no step keys here)
         } else if (has && !(F.levels && !F.intra)) {
             const uint32_t key = F.key0 + (uint32_t) ((G.sbx - G.tile_sb0) + G.sby);
             D.sb_key[slot] = key;
@@ -1054,6 +1049,18 @@ __global__ __launch_bounds__(1024) void k_pkeys(PlanDev D, int nk, const uint32_
         fb[2 * i] = (uint32_t) D.fbytes[i];
         fb[2 * i + 1] = (uint32_t) (D.fbytes[i] >> 32);
     }
+    // every frame's eob and coefficient totals as the scans saw them against its packet's
+    // counts: a frame that disagrees shifts the eobs / coefficients of every later frame in
+    // the batch-wide scans, so the batch fails as a whole (PLS_TOTAL names no frame)
+    for (int i = t; i < nframes; i += 1024) {
+        const PlanFrame &F = D.frames[i];
+        const uint32_t ne = D.blk_eob0[F.blk0 + F.nblk] - D.blk_eob0[F.blk0];
+        const uint32_t d0 = F.slot0, d1 = F.slot0 + (uint32_t) (F.sb_cols * F.sb_rows);
+        const uint32_t nc = d1 <= D.nslots ? D.sb_coef0[d1] - D.sb_coef0[d0] : ~0u;
+        if (ne != F.neob || nc != F.ncoef || D.blk_eob0[F.blk0] != F.eob0 || D.sb_coef0[d0] != F.coef0)
+            atomicOr(D.status, PLS_TOTAL);
+    }
+    __syncthreads();
     for (int i = t; i < nframes; i += 1024) fb[4 * nframes + i] = D.fbad[i];     // per-frame status
     if (t == 0) { out[0] = D.status[0]; out[1 + ng + nk + 1 + 5 * nframes] = D.status[1]; }
 }
@@ -1072,6 +1079,55 @@ __global__ __launch_bounds__(256) void k_plists(PlanDev D)
     if (inb(D, i, D.cap_dlists, 16384u)) D.dlists[i] = slot;
 }
 
+// ------------------------------------------------------------------ k_psort
+// Static step lists (keyframe batches): one workgroup per intra step, its SBs reordered by
+// the length of their pass chains, longest first (sb_kpos: the SB's passes, from k_plan; a
+// per-pass row count was measured 2 % slower in k_plan's scheduling loop for the same order).
+// A k_plf launch lasts until its slowest chain ends; chains dispatched in descending length
+// start the long ones first, and the short ones fill the CUs behind them (longest-processing-
+// time order). Counting sort over 256 bins (passes, longest first; more than 255 share the
+// last), each thread's entries held in registers between the histogram and the scatter
+// (one workgroup owns the segment: every read precedes every write); segments of more than
+// PSORT_PER * 1024 entries keep the staged order.
+#define PSORT_PER 8
+__global__ __launch_bounds__(1024) void k_psort(PlanDev D, const uint32_t *ko)
+{
+    __shared__ uint32_t hist[256];
+    const uint32_t k = blockIdx.x, t = threadIdx.x;
+    const uint32_t a = ko[k], e = ko[k + 1];
+    if (e <= a + 1 || e > D.nslots || e - a > PSORT_PER * 1024u) return;
+    if (t < 256) hist[t] = 0;
+    __syncthreads();
+    uint32_t sl[PSORT_PER], bn[PSORT_PER];
+#pragma unroll
+    for (int j = 0; j < PSORT_PER; j++) {
+        const uint32_t i = a + t + (uint32_t) j * 1024u;
+        sl[j] = i < e ? D.dlists[i] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < PSORT_PER; j++) {
+        const uint32_t i = a + t + (uint32_t) j * 1024u;
+        const uint32_t c = i < e ? D.sb_kpos[sl[j]] : 0u;
+        bn[j] = 255u - (c < 255u ? c : 255u);
+        if (i < e) atomicAdd(&hist[bn[j]], 1u);
+    }
+    __syncthreads();
+    const uint32_t v = t < 256 ? hist[t] : 0u;
+    for (uint32_t d = 1; d < 256; d <<= 1) {           // inclusive scan of the bins
+        const uint32_t x = t < 256 && t >= d ? hist[t - d] : 0u;
+        __syncthreads();
+        if (t < 256) hist[t] += x;
+        __syncthreads();
+    }
+    if (t < 256) hist[t] -= v;                         // exclusive: each bin's first position
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PSORT_PER; j++) {
+        const uint32_t i = a + t + (uint32_t) j * 1024u;
+        if (i < e) D.dlists[a + atomicAdd(&hist[bn[j]], 1u)] = sl[j];
+    }
+}
+
 // ------------------------------------------------------------------ k_pguard
 // Batches whose launch list is fixed at staging (keyframe batches, runtime "static plan"):
 // their pixel kernels run after the planner without a host check of its status, so the
@@ -1079,7 +1135,7 @@ __global__ __launch_bounds__(256) void k_plists(PlanDev D)
 // neutralised here: no intra passes (WGRec), and their residual jobs write nothing but
 // zeros into the spare scratch slot (slot nslots) from no coefficients. The other frames'
 // records address only their own data (k_pjob), so they reconstruct as if alone; a status
-// that names no frame (PLS_BOUNDS) neutralises the whole batch (every WGRec, the summary's
+// that names no frame (PLS_BOUNDS, PLS_TOTAL) neutralises the whole batch (every WGRec, the summary's
 // residual ranges). The status is re-copied into the summary (k_plists' bound checks come
 // after k_pkeys), which the host reads when it next waits for the batch (vp9hip_sync /
 // sync_slot: AVERROR_INVALIDDATA; vp9hip_batch_frame_status: which frames).
@@ -1088,7 +1144,7 @@ __global__ __launch_bounds__(256) void k_pguard(PlanDev D, uint32_t *summary, in
     const uint32_t st = __builtin_amdgcn_readfirstlane(D.status[0]);
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) summary[0] = st;
     if (!st) return;
-    const bool all = (st & PLS_BOUNDS) != 0;
+    const bool all = (st & (PLS_BOUNDS | PLS_TOTAL)) != 0;
     const PlanFrame &F = D.frames[blockIdx.y];
     const int s = blockIdx.x * 256 + threadIdx.x;
     if (all && blockIdx.y == 0)
@@ -1165,6 +1221,8 @@ int vp9hip_plan_enqueue(hipStream_t st, const PlanDev *Dp, int ss, int nframes, 
     if (hipcub::DeviceScan::ExclusiveSum(scan_tmp, tb, D.cntm, D.cntm0, (int) nslots + 1, st) != hipSuccess) return -1;
     launch_sb(ss, st, D, max_sb, nframes, 1, flags);
     if (any_levels) hipLaunchKernelGGL(k_plevel, dim3(nframes), dim3(256), 0, st, D);
+    if (D.static_lists && D.stat_ko && !(D.dbg & 4))             // VP9HIP_PLAN_DBG bit 2: staged order
+        hipLaunchKernelGGL(k_psort, dim3(nk), dim3(1024), 0, st, D, D.stat_ko);
     hipLaunchKernelGGL(k_pkeys, dim3(1), dim3(1024), 0, st, D, nk, gidx, ng, nframes, summary);
     if (!D.static_lists) hipLaunchKernelGGL(k_plists, dim3((max_sb + 255) / 256, nframes), dim3(256), 0, st, D);
     if (guard) hipLaunchKernelGGL(k_pguard, dim3((max_sb + 255) / 256, nframes), dim3(256), 0, st, D, summary, ng);

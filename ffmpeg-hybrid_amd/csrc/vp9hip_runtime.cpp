@@ -179,7 +179,7 @@ struct Staged {
     int plan_flags = 0;                 // device planner kernels: 1 any filtered frame, 2 any inter frame
     size_t o_pf = 0, o_blocks = 0, o_eobs = 0, o_slotpos = 0, o_segpre = 0, o_segsz = 0, o_segpre1 = 0, o_cntm = 0, o_cntm0 = 0, o_gidx = 0, o_bneob = 0,
            o_beob0 = 0, o_sbfirst = 0, o_sbncoef = 0, o_sbcoef0 = 0, o_cnt = 0, o_cnt0 = 0, o_ibits = 0,
-           o_sbinfo = 0, o_sbkey = 0, o_sbkpos = 0, o_keycnt = 0, o_keyoff = 0, o_status = 0, o_fbytes = 0, o_fbad = 0,
+           o_sbinfo = 0, o_sbkey = 0, o_sbkpos = 0, o_expko = 0, o_keycnt = 0, o_keyoff = 0, o_status = 0, o_fbytes = 0, o_fbad = 0,
            o_summary = 0, o_scan = 0, zero_bytes = 0, o_jobw = 0, o_sbnj = 0;
     size_t scan_bytes = 0, summary_words = 0;
     uint32_t *summary_h = nullptr;                            // pinned readback of the summary
@@ -1423,6 +1423,7 @@ static int stage_dev(vp9hip_ctx *c, const DevIn &in)
     s.o_segpre1 = o; o = al(o + seg_pre1.size() * 4);
     s.o_gidx = o; o = al(o + gidx.size() * 4);
     s.o_lists = o; o = al(o + (hl.size() + NS) * 4);      // host lists, then the device step lists
+    s.o_expko = o; o = al(o + (s.stat ? s.exp_ko.size() : 0) * 4);   // static lists' offsets (k_psort)
     s.o_ctr = o; o = al(o + (size_t) s.n_ctr * 4);
     s.o_blocks = o; o = al(o + nb * sizeof(vp9h_block));
     s.o_eobs = o; o = al(o + ne * 2);
@@ -1504,6 +1505,7 @@ static int stage_dev(vp9hip_ctx *c, const DevIn &in)
     if (s.stat && !s.stat_lists.empty()) {
         if (s.stat_lists.size() > NS) return VP9HIP_EBUG;
         memcpy(img + s.o_lists + hl.size() * 4, s.stat_lists.data(), s.stat_lists.size() * 4);
+        memcpy(img + s.o_expko, s.exp_ko.data(), s.exp_ko.size() * 4);
     }
     init_lfr_ctr(c, s, (uint32_t *) (img + s.o_ctr));
     {   // packets: blocks, eobs, coefficients (frames copied in parallel)
@@ -1553,12 +1555,12 @@ static int stage_dev(vp9hip_ctx *c, const DevIn &in)
 
 // The per-frame verdicts of a rejected batch from its summary: frames whose status bits are
 // set are rejected, the others get `good` (0: reconstructed, EAGAIN: not run). A status that
-// names no frame (PLS_BOUNDS, a shared buffer's capacity) rejects every frame. Returns the
-// number rejected.
+// names no frame (PLS_BOUNDS: a shared buffer's capacity; PLS_TOTAL: a frame's totals shift
+// the batch-wide scans) rejects every frame. Returns the number rejected.
 static int frame_verdicts(Staged &s, const uint32_t *sm, int good)
 {
     const uint32_t *fbad = sm + 1 + s.n_gidx + s.nkey + 1 + 4 * (size_t) s.nframes;
-    const bool all = (sm[0] & PLS_BOUNDS) != 0;
+    const bool all = (sm[0] & (PLS_BOUNDS | PLS_TOTAL)) != 0;
     s.fstat.assign(s.nframes, good);
     int nbad = 0;
     for (int i = 0; i < s.nframes; i++)
@@ -1572,10 +1574,12 @@ static int frame_verdicts(Staged &s, const uint32_t *sm, int good)
 // algorithmic byte totals. Consistency of the step lists with the staged launch list rests
 // on k_plan's PLS_SCHED check (with static lists k_plan does not count keys, so the summary's
 // key offsets are only used to locate the byte totals).
+static void print_plan_prof(vp9hip_ctx *c, const Staged &s);
 static int finish_summary(vp9hip_ctx *c, Staged &s)
 {
     if (!s.stat || !s.summary_pending) return s.status;
     s.summary_pending = false;
+    if (c->plan_prof_on && c->plan_prof) print_plan_prof(c, s);
     HIPCHK(hipMemcpy(s.summary_h, s.arena + s.o_summary, s.summary_words * 4, hipMemcpyDeviceToHost));
     const uint32_t *sm = s.summary_h;
     if (sm[0]) {
@@ -1607,6 +1611,20 @@ static int finish_summary(vp9hip_ctx *c, Staged &s)
         s.alg_bytes[K_MC] += (double) ((uint64_t) fb32[4 * i + 2] | (uint64_t) fb32[4 * i + 3] << 32);
     }
     return 0;
+}
+
+// VP9HIP_PLAN_PROF=1: the planner's per-SB phase cycles of the last run (k_pjob phases 0-2,
+// k_plan 3-10), summed over the SBs, on stderr. The caller has waited for the planner.
+static void print_plan_prof(vp9hip_ctx *c, const Staged &s)
+{
+    unsigned long long pc[16];
+    if (hipMemcpy(pc, c->plan_prof, sizeof(pc), hipMemcpyDeviceToHost) != hipSuccess) return;
+    double tot = 0;
+    for (int k = 0; k < 11; k++) tot += (double) pc[k];
+    fprintf(stderr, "vp9hip plan phases (%% of planner SB cycles, %.3g cycles/SB%s):", tot / std::max<uint32_t>(1, s.nslots),
+            s.stat ? ", static plan" : "");
+    for (int k = 0; k < 11; k++) fprintf(stderr, " %d:%.1f", k, 100.0 * (double) pc[k] / std::max(1.0, tot));
+    fprintf(stderr, "\n");
 }
 
 // Run the device planner of the staged batch and build its launch list from the summary.
@@ -1679,6 +1697,8 @@ static int plan_dev(vp9hip_ctx *c)
     const bool pprof = c->plan_prof_on;
     D.dbg = c->plan_dbg;
     D.static_lists = s.stat ? 1 : 0;
+    D.stat_ko = s.stat && !s.stat_lists.empty() && s.exp_ko.size() == (size_t) s.nkey + 1 ? (const uint32_t *) (A + s.o_expko)
+                                                                                        : nullptr;
     D.prof = nullptr;
     if (pprof) {
         if (!c->plan_prof && hipMalloc(&c->plan_prof, 16 * sizeof(unsigned long long)) != hipSuccess) return VP9HIP_ENOMEM;
@@ -1706,15 +1726,7 @@ static int plan_dev(vp9hip_ctx *c)
     }
     HIPCHK(hipMemcpyAsync(s.summary_h, A + s.o_summary, s.summary_words * 4, hipMemcpyDeviceToHost, ps));
     HIPCHK(hipStreamSynchronize(ps));          // the pixel kernels, queued after this, read the plan
-    if (pprof) {
-        unsigned long long pc[16];
-        HIPCHK(hipMemcpy(pc, c->plan_prof, sizeof(pc), hipMemcpyDeviceToHost));
-        double tot = 0;
-        for (int k = 0; k < 11; k++) tot += (double) pc[k];
-        fprintf(stderr, "vp9hip plan phases (%% of k_plan SB cycles, %.3g cycles/SB):", tot / std::max<uint32_t>(1, s.nslots));
-        for (int k = 0; k < 11; k++) fprintf(stderr, " %d:%.1f", k, 100.0 * (double) pc[k] / std::max(1.0, tot));
-        fprintf(stderr, "\n");
-    }
+    if (pprof) print_plan_prof(c, s);
     if (plan_trace)
         fprintf(stderr, "vp9hip plan (device): %d frames: %.2f ms host wall\n", s.nframes,
                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - pt0).count());
