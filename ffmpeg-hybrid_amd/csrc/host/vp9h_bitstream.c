@@ -202,6 +202,16 @@ static int bc_tree(BC *c, const int8_t (*t)[2], const uint8_t *probs, int sym)
     return -i;
 }
 
+/* bc_tree with the direction a constant (the walkers' _t forms): the decoder's tree walk inline */
+static inline __attribute__((always_inline)) int bc_tree_e(BC *c, const int enc, const int8_t (*t)[2], const uint8_t *probs,
+                                                           int sym)
+{
+    if (enc) return bc_tree(c, t, probs, sym);
+    int i = 0;
+    do i = t[i][bd_read(&c->d, probs[i])]; while (i > 0);
+    return -i;
+}
+
 /* small context fills (SET_CTXS, vp9block.c:718-745, and the SPLAT / segment-map fills):
  * sizes 1, 2, 4, 8, 16 as one or two stores, as the reference's setctx_2d / AV_WN64A splats do;
  * a libc memset call per fill cost ~30 % of the single-thread parse (tools/parse_bench.c) */
@@ -654,9 +664,15 @@ walk_tokens_t(Walk *w, int n_coeffs, int tx32, const uint8_t (*p)[6][11], int nn
                                       : (int32_t) ((unsigned) vals[k] * (unsigned) qmul[k > 0]);
             if ((csz == 2 ? (int32_t) (int16_t) back : back) != s) { w->err = 1; return 0; }
         }
+    /* the first "more coefficients?" before the output is grown: most tx blocks of a
+     * realistic stream stop here (eob 0) */
+    const int more0 = bc_bool_e(c, enc, tp[0], 0 < eob_in);
+    eobc[0][nnz][more0]++;
+    if (!more0) return 0;
     const size_t c0 = w->nc;
     w->coefs = grow(w->coefs, &w->cc, w->nc + (size_t) n_coeffs * csz, 1, &w->err);
     if (w->err) return 0;
+    goto skip_eob;
     do {
         /* more coefficients? */
         const int more = bc_bool_e(c, enc, tp[0], i < eob_in);
@@ -768,7 +784,7 @@ static void nnz_splat(uint8_t *la, int end, int full, int step)
 }
 
 /* decode_coeffs (vp9block.c:965-1130): returns whether any tx block has coefficients */
-static int walk_coeffs(Walk *w, vp9h_block *b, int row, int col)
+static inline __attribute__((always_inline)) int walk_coeffs_t(Walk *w, vp9h_block *b, int row, int col, const int enc)
 {
     const int csz = w->h->bpp > 8 ? 4 : 2;
     const int lossless = w->h->lossless;
@@ -795,15 +811,15 @@ static int walk_coeffs(Walk *w, vp9h_block *b, int row, int col)
                 const int tcode = lossless ? 4 : t;
                 int eob_in = 0;
                 const uint8_t *cin = NULL;
-                if (w->c->enc) {
+                if (enc) {
                     if (w->ei >= w->in->neobs) { w->err = 1; return 0; }
                     eob_in = w->in->eobs[w->ei++];
                     cin = (const uint8_t *) w->in->coefs + w->ci * csz;
                     w->ci += (uint64_t) eob_in;
                 }
-                const int eob = walk_tokens(w, 16 << (2 * t), t == 3, p, a[x] + l[y], scan_of(tcode, txtp),
+                const int eob = walk_tokens_t(w, 16 << (2 * t), t == 3, p, a[x] + l[y], scan_of(tcode, txtp),
                                             nb_of(tcode, txtp), band_counts[t], qmul[pl > 0], eob_in, cin, csz,
-                                            cnt, eobc);
+                                            cnt, eobc, enc);
                 if (w->err) return 0;
                 w->eobs = grow(w->eobs, &w->ce, w->ne + 1, 2, &w->err);
                 if (w->err) return 0;
@@ -969,7 +985,7 @@ static Mv mv_pred(const Walk *w, const vp9h_block *b, int row, int col, int z, i
 }
 
 /* read_mv_component (vp9mvs.c:277-330): one component of an MV difference, idx 0 = y */
-static int walk_mv_comp(Walk *w, int idx, int hp, int v)
+static inline __attribute__((always_inline)) int walk_mv_comp_t(Walk *w, int idx, int hp, int v, const int enc)
 {
     BC *c = w->c;
     MvProbs *mp = &w->pr.p.mv_comp[idx];
@@ -977,9 +993,9 @@ static int walk_mv_comp(Walk *w, int idx, int hp, int v)
     /* encoder: v = +-(n + 1); n = class0 (n < 16) or (8 << cls) + bits << 3 | fp << 1 | hp */
     const int an = (v < 0 ? -v : v) - 1;
     int cls0 = 0;
-    if (c->enc && an >= 16) { cls0 = 1; while ((8 << (cls0 + 1)) <= an) cls0++; }
-    const int sign = bc_bool(c, mp->sign, v < 0);
-    const int cls = bc_tree(c, mv_class_tree, mp->classes, c->enc ? (an >= 16 ? cls0 : 0) : 0);
+    if (enc && an >= 16) { cls0 = 1; while ((8 << (cls0 + 1)) <= an) cls0++; }
+    const int sign = bc_bool_e(c, enc, mp->sign, v < 0);
+    const int cls = bc_tree_e(c, enc, mv_class_tree, mp->classes, enc ? (an >= 16 ? cls0 : 0) : 0);
     ct->sign[sign]++;
     ct->classes[cls]++;
     int n;
@@ -987,16 +1003,16 @@ static int walk_mv_comp(Walk *w, int idx, int hp, int v)
         const int r = an - (8 << cls);
         n = 0;
         for (int m = 0; m < cls; m++) {
-            const int bit = bc_bool(c, mp->bits[m], (r >> (3 + m)) & 1);
+            const int bit = bc_bool_e(c, enc, mp->bits[m], (r >> (3 + m)) & 1);
             n |= bit << m;
             ct->bits[m][bit]++;
         }
         n <<= 3;
-        const int fp = bc_tree(c, mv_fp_tree, mp->fp, (r >> 1) & 3);
+        const int fp = bc_tree_e(c, enc, mv_fp_tree, mp->fp, (r >> 1) & 3);
         n |= fp << 1;
         ct->fp[fp]++;
         if (hp) {
-            const int bit = bc_bool(c, mp->hp, r & 1);
+            const int bit = bc_bool_e(c, enc, mp->hp, r & 1);
             ct->hp[bit]++;
             n |= bit;
         } else {
@@ -1005,13 +1021,13 @@ static int walk_mv_comp(Walk *w, int idx, int hp, int v)
         }
         n += 8 << cls;
     } else {
-        const int c0 = bc_bool(c, mp->class0, (an >> 3) & 1);
+        const int c0 = bc_bool_e(c, enc, mp->class0, (an >> 3) & 1);
         ct->class0[c0]++;
-        const int fp = bc_tree(c, mv_fp_tree, mp->class0_fp[c0], (an >> 1) & 3);
+        const int fp = bc_tree_e(c, enc, mv_fp_tree, mp->class0_fp[c0], (an >> 1) & 3);
         ct->class0_fp[c0][fp]++;
         n = (c0 << 3) | (fp << 1);
         if (hp) {
-            const int bit = bc_bool(c, mp->class0_hp, an & 1);
+            const int bit = bc_bool_e(c, enc, mp->class0_hp, an & 1);
             ct->class0_hp[bit]++;
             n |= bit;
         } else {
@@ -1025,7 +1041,7 @@ static int walk_mv_comp(Walk *w, int idx, int hp, int v)
 /* ff_vp9_fill_mv (vp9mvs.c:295-365) for sub-block sb (-1: whole block). Encoder: `t` is
  * the packet's MV pair for this sub-block; the coded MV can differ from it only by the
  * odd 1/8-pel step a low-precision difference cannot carry. */
-static void walk_fill_mv(Walk *w, vp9h_block *b, int row, int col, int mode, int sb, Mv out[2], const Mv t[2])
+static inline __attribute__((always_inline)) void walk_fill_mv_t(Walk *w, vp9h_block *b, int row, int col, int mode, int sb, Mv out[2], const Mv t[2], const int enc)
 {
     for (int z = 0; z < 1 + b->comp; z++) {
         if (mode == VP9H_ZEROMV) { out[z].x = out[z].y = 0; continue; }
@@ -1033,14 +1049,14 @@ static void walk_fill_mv(Walk *w, vp9h_block *b, int row, int col, int mode, int
         Mv m = mv_pred(w, b, row, col, z, mode, sb, &hp);
         if (mode == VP9H_NEWMV) {
             int dx = 0, dy = 0;
-            if (w->c->enc) {
+            if (enc) {
                 dx = t[z].x - m.x; dy = t[z].y - m.y;
                 if (!hp) { dx -= (dx & 1) ? (dx > 0 ? 1 : -1) : 0; dy -= (dy & 1) ? (dy > 0 ? 1 : -1) : 0; }
             }
-            const int j = bc_tree(w->c, mv_joint_tree, w->pr.p.mv_joint, (dx != 0) | (dy != 0) << 1);
+            const int j = bc_tree_e(w->c, enc, mv_joint_tree, w->pr.p.mv_joint, (dx != 0) | (dy != 0) << 1);
             w->cnt.mv_joint[j]++;
-            if (j >= 2) m.y = (int16_t) (m.y + walk_mv_comp(w, 0, hp, dy));
-            if (j & 1) m.x = (int16_t) (m.x + walk_mv_comp(w, 1, hp, dx));
+            if (j >= 2) m.y = (int16_t) (m.y + walk_mv_comp_t(w, 0, hp, dy, enc));
+            if (j & 1) m.x = (int16_t) (m.x + walk_mv_comp_t(w, 1, hp, dx, enc));
         }
         out[z] = m;
     }
@@ -1080,7 +1096,7 @@ static const uint8_t inter_mode_ctx[14][14] = {
 };
 
 /* the segment id (decode_mode, vp9block.c:101-141) */
-static void walk_seg_id(Walk *w, vp9h_block *b, const vp9h_block *t, int row, int col, int w4, int h4)
+static inline __attribute__((always_inline)) void walk_seg_id_t(Walk *w, vp9h_block *b, const vp9h_block *t, int row, int col, int w4, int h4, const int enc)
 {
     const Hdr *h = w->h;
     BC *c = w->c;
@@ -1088,7 +1104,7 @@ static void walk_seg_id(Walk *w, vp9h_block *b, const vp9h_block *t, int row, in
     if (!h->seg_enabled) {
         b->seg_id = 0;
     } else if (h->keyframe || h->intraonly) {
-        b->seg_id = h->seg_update_map ? (uint8_t) bc_tree(c, segment_tree, h->seg_prob, t->seg_id) : 0;
+        b->seg_id = h->seg_update_map ? (uint8_t) bc_tree_e(c, enc, segment_tree, h->seg_prob, t->seg_id) : 0;
     } else {
         /* the temporal prediction: the smallest id under the block in the reference map */
         int pred = 0;
@@ -1099,12 +1115,12 @@ static void walk_seg_id(Walk *w, vp9h_block *b, const vp9h_block *t, int row, in
                 for (int x = 0; x < w4; x++) pred = MIN(pred, map[(y + row) * 8 * w->sb_cols + col + x]);
         }
         if (!h->seg_update_map ||
-            (h->seg_temporal && bc_bool(c, h->seg_pred[w->a_segpred[col] + w->l_segpred[row7]], t->seg_id == pred))) {
+            (h->seg_temporal && bc_bool_e(c, enc, h->seg_pred[w->a_segpred[col] + w->l_segpred[row7]], t->seg_id == pred))) {
             b->seg_id = (uint8_t) pred;
             fill_ctx(w->a_segpred + col, 1, w4);
             fill_ctx(w->l_segpred + row7, 1, h4);
         } else {
-            b->seg_id = (uint8_t) bc_tree(c, segment_tree, h->seg_prob, t->seg_id);
+            b->seg_id = (uint8_t) bc_tree_e(c, enc, segment_tree, h->seg_prob, t->seg_id);
             fill_ctx(w->a_segpred + col, 0, w4);
             fill_ctx(w->l_segpred + row7, 0, h4);
         }
@@ -1116,7 +1132,7 @@ static void walk_seg_id(Walk *w, vp9h_block *b, const vp9h_block *t, int row, in
 }
 
 /* the reference frames of an inter block (vp9block.c:333-574) */
-static void walk_refs(Walk *w, vp9h_block *b, const vp9h_block *t, int have_a, int have_l, int col, int row7)
+static inline __attribute__((always_inline)) void walk_refs_t(Walk *w, vp9h_block *b, const vp9h_block *t, int have_a, int have_l, int col, int row7, const int enc)
 {
     const Hdr *h = w->h;
     BC *c = w->c;
@@ -1146,7 +1162,7 @@ static void walk_refs(Walk *w, vp9h_block *b, const vp9h_block *t, int have_a, i
         } else {
             ctx = 1;
         }
-        b->comp = (uint8_t) bc_bool(c, w->pr.p.comp[ctx], t->comp);
+        b->comp = (uint8_t) bc_bool_e(c, enc, w->pr.p.comp[ctx], t->comp);
         w->cnt.comp[ctx][b->comp]++;
     }
     if (b->comp) {
@@ -1177,7 +1193,7 @@ static void walk_refs(Walk *w, vp9h_block *b, const vp9h_block *t, int have_a, i
         } else {
             ctx = 2;
         }
-        const int bit = bc_bool(c, w->pr.p.comp_ref[ctx], t->ref[var_idx] == v1);
+        const int bit = bc_bool_e(c, enc, w->pr.p.comp_ref[ctx], t->ref[var_idx] == v1);
         b->ref[var_idx] = (uint8_t) h->varcompref[bit];
         w->cnt.comp_ref[ctx][bit]++;
         return;
@@ -1200,7 +1216,7 @@ static void walk_refs(Walk *w, vp9h_block *b, const vp9h_block *t, int have_a, i
     } else {
         ctx = 2;
     }
-    int bit = bc_bool(c, w->pr.p.single_ref[ctx][0], t->ref[0] != 0);
+    int bit = bc_bool_e(c, enc, w->pr.p.single_ref[ctx][0], t->ref[0] != 0);
     w->cnt.single_ref[ctx][0][bit]++;
     if (!bit) { b->ref[0] = 0; return; }
     if (have_a) {
@@ -1240,21 +1256,21 @@ static void walk_refs(Walk *w, vp9h_block *b, const vp9h_block *t, int have_a, i
     } else {
         ctx = 2;
     }
-    bit = bc_bool(c, w->pr.p.single_ref[ctx][1], t->ref[0] == 2);
+    bit = bc_bool_e(c, enc, w->pr.p.single_ref[ctx][1], t->ref[0] == 2);
     w->cnt.single_ref[ctx][1][bit]++;
     b->ref[0] = (uint8_t) (1 + bit);
 }
 
 /* one block (decode_mode vp9block.c:80-803 + the coefficient call of
  * ff_vp9_decode_block, vp9block.c:1264-1345). Encoder: `t` is the packet's block. */
-static void walk_block(Walk *w, int row, int col, int bl, int bp)
+static inline __attribute__((always_inline)) void walk_block_t(Walk *w, int row, int col, int bl, int bp, const int enc)
 {
     static const vp9h_block zero_block;
     BC *c = w->c;
     const Hdr *h = w->h;
     const int bs = bl * 3 + bp;
     const vp9h_block *t = &zero_block;
-    if (c->enc) {
+    if (enc) {
         if (w->bi >= w->in->nblocks) { w->err = 1; return; }
         t = &w->in->blocks[w->bi++];
         if (t->row != row || t->col != col || t->bs != bs) { w->err = 1; return; }
@@ -1271,12 +1287,12 @@ static void walk_block(Walk *w, int row, int col, int bl, int bp)
     w->minx = -(128 + col * 64); w->miny = -(128 + row * 64);
     w->maxx = 128 + (w->cols - col - bw4) * 64; w->maxy = 128 + (w->rows - row - bh4) * 64;
 
-    walk_seg_id(w, &b, t, row, col, w4, h4);
+    walk_seg_id_t(w, &b, t, row, col, w4, h4, enc);
     /* skip */
     b.skip = h->seg_enabled && h->seg[b.seg_id].skip;
     if (!b.skip) {
         const int cx = w->l_skip[row7] + w->a_skip[col];
-        b.skip = (uint8_t) bc_bool(c, w->pr.p.skip[cx], t->skip);
+        b.skip = (uint8_t) bc_bool_e(c, enc, w->pr.p.skip[cx], t->skip);
         w->cnt.skip[cx][b.skip]++;
     }
     /* intra / inter */
@@ -1288,7 +1304,7 @@ static void walk_block(Walk *w, int row, int col, int bl, int bp)
         int cx;
         if (have_a && have_l) { cx = w->a_intra[col] + w->l_intra[row7]; cx += cx == 2; }
         else cx = have_a ? 2 * w->a_intra[col] : have_l ? 2 * w->l_intra[row7] : 0;
-        const int bit = bc_bool(c, w->pr.p.intra[cx], !t->intra);
+        const int bit = bc_bool_e(c, enc, w->pr.p.intra[cx], !t->intra);
         w->cnt.intra[cx][bit]++;
         b.intra = !bit;
     }
@@ -1309,17 +1325,17 @@ static void walk_block(Walk *w, int row, int col, int bl, int bp)
         int tx = 0;
         switch (max_tx) {
         case 3:
-            tx = bc_bool(c, pp->tx32p[cx][0], t->tx > 0);
-            if (tx) { tx += bc_bool(c, pp->tx32p[cx][1], t->tx > 1); if (tx == 2) tx += bc_bool(c, pp->tx32p[cx][2], t->tx > 2); }
+            tx = bc_bool_e(c, enc, pp->tx32p[cx][0], t->tx > 0);
+            if (tx) { tx += bc_bool_e(c, enc, pp->tx32p[cx][1], t->tx > 1); if (tx == 2) tx += bc_bool_e(c, enc, pp->tx32p[cx][2], t->tx > 2); }
             w->cnt.tx32p[cx][tx]++;
             break;
         case 2:
-            tx = bc_bool(c, pp->tx16p[cx][0], t->tx > 0);
-            if (tx) tx += bc_bool(c, pp->tx16p[cx][1], t->tx > 1);
+            tx = bc_bool_e(c, enc, pp->tx16p[cx][0], t->tx > 0);
+            if (tx) tx += bc_bool_e(c, enc, pp->tx16p[cx][1], t->tx > 1);
             w->cnt.tx16p[cx][tx]++;
             break;
         case 1:
-            tx = bc_bool(c, pp->tx8p[cx], t->tx > 0);
+            tx = bc_bool_e(c, enc, pp->tx8p[cx], t->tx > 0);
             w->cnt.tx8p[cx][tx]++;
             break;
         default: tx = 0;
@@ -1333,17 +1349,17 @@ static void walk_block(Walk *w, int row, int col, int bl, int bp)
         /* intra modes with above / left 4x4 mode contexts (keyframe probabilities) */
         uint8_t *a = w->a_mode + col * 2, *l = w->l_mode + (row7 << 1);
         if (bs > VP9H_BS_8x8) {
-            b.mode[0] = a[0] = (uint8_t) bc_tree(c, intramode_tree, vp9t_kf_ymode_probs[a[0]][l[0]], t->mode[0]);
+            b.mode[0] = a[0] = (uint8_t) bc_tree_e(c, enc, intramode_tree, vp9t_kf_ymode_probs[a[0]][l[0]], t->mode[0]);
             if (bs != VP9H_BS_8x4) {
-                b.mode[1] = (uint8_t) bc_tree(c, intramode_tree, vp9t_kf_ymode_probs[a[1]][b.mode[0]], t->mode[1]);
+                b.mode[1] = (uint8_t) bc_tree_e(c, enc, intramode_tree, vp9t_kf_ymode_probs[a[1]][b.mode[0]], t->mode[1]);
                 l[0] = a[1] = b.mode[1];
             } else {
                 l[0] = a[1] = b.mode[1] = b.mode[0];
             }
             if (bs != VP9H_BS_4x8) {
-                b.mode[2] = a[0] = (uint8_t) bc_tree(c, intramode_tree, vp9t_kf_ymode_probs[a[0]][l[1]], t->mode[2]);
+                b.mode[2] = a[0] = (uint8_t) bc_tree_e(c, enc, intramode_tree, vp9t_kf_ymode_probs[a[0]][l[1]], t->mode[2]);
                 if (bs != VP9H_BS_8x4) {
-                    b.mode[3] = (uint8_t) bc_tree(c, intramode_tree, vp9t_kf_ymode_probs[a[1]][b.mode[2]], t->mode[3]);
+                    b.mode[3] = (uint8_t) bc_tree_e(c, enc, intramode_tree, vp9t_kf_ymode_probs[a[1]][b.mode[2]], t->mode[3]);
                     l[1] = a[1] = b.mode[3];
                 } else {
                     l[1] = a[1] = b.mode[3] = b.mode[2];
@@ -1353,29 +1369,29 @@ static void walk_block(Walk *w, int row, int col, int bl, int bp)
                 l[1] = a[1] = b.mode[3] = b.mode[1];
             }
         } else {
-            b.mode[0] = (uint8_t) bc_tree(c, intramode_tree, vp9t_kf_ymode_probs[*a][*l], t->mode[0]);
+            b.mode[0] = (uint8_t) bc_tree_e(c, enc, intramode_tree, vp9t_kf_ymode_probs[*a][*l], t->mode[0]);
             b.mode[3] = b.mode[2] = b.mode[1] = b.mode[0];
             fill_ctx(a, b.mode[0], vp9t_bwh[0][bs][0]);
             fill_ctx(l, b.mode[0], vp9t_bwh[0][bs][1]);
         }
-        b.uvmode = (uint8_t) bc_tree(c, intramode_tree, vp9t_kf_uvmode_probs[b.mode[3]], t->uvmode);
+        b.uvmode = (uint8_t) bc_tree_e(c, enc, intramode_tree, vp9t_kf_uvmode_probs[b.mode[3]], t->uvmode);
     } else if (b.intra) {
         /* intra block of an inter frame: adaptive probabilities, no neighbour context */
         static const uint8_t size_group[10] = { 3, 3, 3, 3, 2, 2, 2, 1, 1, 1 };
         if (bs > VP9H_BS_8x8) {
-            b.mode[0] = (uint8_t) bc_tree(c, intramode_tree, w->pr.p.y_mode[0], t->mode[0]);
+            b.mode[0] = (uint8_t) bc_tree_e(c, enc, intramode_tree, w->pr.p.y_mode[0], t->mode[0]);
             w->cnt.y_mode[0][b.mode[0]]++;
             if (bs != VP9H_BS_8x4) {
-                b.mode[1] = (uint8_t) bc_tree(c, intramode_tree, w->pr.p.y_mode[0], t->mode[1]);
+                b.mode[1] = (uint8_t) bc_tree_e(c, enc, intramode_tree, w->pr.p.y_mode[0], t->mode[1]);
                 w->cnt.y_mode[0][b.mode[1]]++;
             } else {
                 b.mode[1] = b.mode[0];
             }
             if (bs != VP9H_BS_4x8) {
-                b.mode[2] = (uint8_t) bc_tree(c, intramode_tree, w->pr.p.y_mode[0], t->mode[2]);
+                b.mode[2] = (uint8_t) bc_tree_e(c, enc, intramode_tree, w->pr.p.y_mode[0], t->mode[2]);
                 w->cnt.y_mode[0][b.mode[2]]++;
                 if (bs != VP9H_BS_8x4) {
-                    b.mode[3] = (uint8_t) bc_tree(c, intramode_tree, w->pr.p.y_mode[0], t->mode[3]);
+                    b.mode[3] = (uint8_t) bc_tree_e(c, enc, intramode_tree, w->pr.p.y_mode[0], t->mode[3]);
                     w->cnt.y_mode[0][b.mode[3]]++;
                 } else {
                     b.mode[3] = b.mode[2];
@@ -1386,14 +1402,14 @@ static void walk_block(Walk *w, int row, int col, int bl, int bp)
             }
         } else {
             const int sz = size_group[bs];
-            b.mode[0] = (uint8_t) bc_tree(c, intramode_tree, w->pr.p.y_mode[sz], t->mode[0]);
+            b.mode[0] = (uint8_t) bc_tree_e(c, enc, intramode_tree, w->pr.p.y_mode[sz], t->mode[0]);
             b.mode[1] = b.mode[2] = b.mode[3] = b.mode[0];
             w->cnt.y_mode[sz][b.mode[3]]++;
         }
-        b.uvmode = (uint8_t) bc_tree(c, intramode_tree, w->pr.p.uv_mode[b.mode[3]], t->uvmode);
+        b.uvmode = (uint8_t) bc_tree_e(c, enc, intramode_tree, w->pr.p.uv_mode[b.mode[3]], t->uvmode);
         w->cnt.uv_mode[b.mode[3]][b.uvmode]++;
     } else {
-        walk_refs(w, &b, t, have_a, have_l, col, row7);
+        walk_refs_t(w, &b, t, have_a, have_l, col, row7, enc);
         Mv tm[4][2], out[2];
         for (int k = 0; k < 4; k++)
             for (int z = 0; z < 2; z++) { tm[k][z].x = t->mv[k][z][0]; tm[k][z].y = t->mv[k][z][1]; }
@@ -1403,8 +1419,8 @@ static void walk_block(Walk *w, int row, int col, int bl, int bp)
             } else {
                 static const uint8_t off[10] = { 3, 0, 0, 1, 0, 0, 0, 0, 0, 0 };
                 const int cx = inter_mode_ctx[w->a_mode[col + off[bs]]][w->l_mode[row7 + off[bs]]];
-                const int want = c->enc ? choose_mode(w, &b, row, col, -1, t->mode[0], tm[0]) : 0;
-                b.mode[0] = (uint8_t) bc_tree(c, inter_mode_tree, w->pr.p.mv_mode[cx], want);
+                const int want = enc ? choose_mode(w, &b, row, col, -1, t->mode[0], tm[0]) : 0;
+                b.mode[0] = (uint8_t) bc_tree_e(c, enc, inter_mode_tree, w->pr.p.mv_mode[cx], want);
                 b.mode[1] = b.mode[2] = b.mode[3] = b.mode[0];
                 w->cnt.mv_mode[cx][b.mode[0] - 10]++;
             }
@@ -1422,7 +1438,7 @@ static void walk_block(Walk *w, int row, int col, int bl, int bp)
             } else {
                 cx = 3;
             }
-            filter_id = bc_tree(c, filter_tree, w->pr.p.filter[cx], t->filter < 3 ? id_of_filter[t->filter] : 0);
+            filter_id = bc_tree_e(c, enc, filter_tree, w->pr.p.filter[cx], t->filter < 3 ? id_of_filter[t->filter] : 0);
             w->cnt.filter[cx][filter_id]++;
             b.filter = filter_of_id[filter_id];
         } else {
@@ -1438,14 +1454,14 @@ static void walk_block(Walk *w, int row, int col, int bl, int bp)
                     memcpy(b.mv[k], b.mv[src], sizeof(b.mv[k]));
                     continue;
                 }
-                const int want = c->enc ? choose_mode(w, &b, row, col, k, t->mode[k], tm[k]) : 0;
-                b.mode[k] = (uint8_t) bc_tree(c, inter_mode_tree, w->pr.p.mv_mode[cx], want);
+                const int want = enc ? choose_mode(w, &b, row, col, k, t->mode[k], tm[k]) : 0;
+                b.mode[k] = (uint8_t) bc_tree_e(c, enc, inter_mode_tree, w->pr.p.mv_mode[cx], want);
                 w->cnt.mv_mode[cx][b.mode[k] - 10]++;
-                walk_fill_mv(w, &b, row, col, b.mode[k], k, out, tm[k]);
+                walk_fill_mv_t(w, &b, row, col, b.mode[k], k, out, tm[k], enc);
                 for (int z = 0; z < 2; z++) { b.mv[k][z][0] = out[z].x; b.mv[k][z][1] = out[z].y; }
             }
         } else {
-            walk_fill_mv(w, &b, row, col, b.mode[0], -1, out, tm[0]);
+            walk_fill_mv_t(w, &b, row, col, b.mode[0], -1, out, tm[0], enc);
             for (int k = 0; k < 4; k++)
                 for (int z = 0; z < 2; z++) { b.mv[k][z][0] = out[z].x; b.mv[k][z][1] = out[z].y; }
         }
@@ -1498,7 +1514,7 @@ static void walk_block(Walk *w, int row, int col, int bl, int bp)
 
     if (!b.skip) {
         const size_t ne0 = w->ne, nc0 = w->nc;
-        if (!walk_coeffs(w, &b, row, col) && !w->err && bs <= VP9H_BS_8x8 && !b.intra) {
+        if (!walk_coeffs_t(w, &b, row, col, enc) && !w->err && bs <= VP9H_BS_8x8 && !b.intra) {
             /* an inter block <= 8x8 without coefficients becomes skip (vp9block.c:1310-1314) */
             b.skip = 1;
             fill_ctx(w->a_skip + col, 1, bw4);
@@ -1519,7 +1535,18 @@ static void walk_block(Walk *w, int row, int col, int bl, int bp)
 }
 
 /* decode_sb (vp9.c:1115-1193) */
-static void walk_sb(Walk *w, int row, int col, int bl)
+/* the walkers per direction: the decoder's carries no encoder branches (tools/parse_bench.c) */
+static __attribute__((noinline)) void walk_block_dec(Walk *w, int row, int col, int bl, int bp)
+{
+    walk_block_t(w, row, col, bl, bp, 0);
+}
+static __attribute__((noinline)) void walk_block_enc(Walk *w, int row, int col, int bl, int bp)
+{
+    walk_block_t(w, row, col, bl, bp, 1);
+}
+static void walk_sb_dec(Walk *w, int row, int col, int bl);
+static void walk_sb_enc(Walk *w, int row, int col, int bl);
+static inline __attribute__((always_inline)) void walk_sb_t(Walk *w, int row, int col, int bl, const int enc)
 {
     BC *c = w->c;
     if (w->err) return;
@@ -1528,41 +1555,48 @@ static void walk_sb(Walk *w, int row, int col, int bl)
                                                             : w->pr.p.partition[bl][ctx];
     const int hbs = 4 >> bl;
     int bp = 0;
-    if (c->enc) {   /* the packet's next block says which partition this node takes */
+    if (enc) {   /* the packet's next block says which partition this node takes */
         if (w->bi >= w->in->nblocks) { w->err = 1; return; }
         const vp9h_block *nb = &w->in->blocks[w->bi];
         const int nbl = nb->bs == VP9H_BS_4x4 ? 3 : nb->bs / 3;
         bp = (nb->row == row && nb->col == col && nbl == bl) ? nb->bs - 3 * bl : 3;
     }
     if (bl == 3) {
-        bp = bc_tree(c, partition_tree, p, bp);
-        walk_block(w, row, col, bl, bp);
+        bp = bc_tree_e(c, enc, partition_tree, p, bp);
+        (enc ? walk_block_enc : walk_block_dec)(w, row, col, bl, bp);
     } else if (col + hbs < w->cols) {
         if (row + hbs < w->rows) {
-            bp = bc_tree(c, partition_tree, p, bp);
+            bp = bc_tree_e(c, enc, partition_tree, p, bp);
             switch (bp) {
-            case 0: walk_block(w, row, col, bl, bp); break;
-            case 1: walk_block(w, row, col, bl, bp); walk_block(w, row + hbs, col, bl, bp); break;
-            case 2: walk_block(w, row, col, bl, bp); walk_block(w, row, col + hbs, bl, bp); break;
+            case 0: (enc ? walk_block_enc : walk_block_dec)(w, row, col, bl, bp); break;
+            case 1: (enc ? walk_block_enc : walk_block_dec)(w, row, col, bl, bp); (enc ? walk_block_enc : walk_block_dec)(w, row + hbs, col, bl, bp); break;
+            case 2: (enc ? walk_block_enc : walk_block_dec)(w, row, col, bl, bp); (enc ? walk_block_enc : walk_block_dec)(w, row, col + hbs, bl, bp); break;
             default:
-                walk_sb(w, row, col, bl + 1); walk_sb(w, row, col + hbs, bl + 1);
-                walk_sb(w, row + hbs, col, bl + 1); walk_sb(w, row + hbs, col + hbs, bl + 1);
+                (enc ? walk_sb_enc : walk_sb_dec)(w, row, col, bl + 1); (enc ? walk_sb_enc : walk_sb_dec)(w, row, col + hbs, bl + 1);
+                (enc ? walk_sb_enc : walk_sb_dec)(w, row + hbs, col, bl + 1); (enc ? walk_sb_enc : walk_sb_dec)(w, row + hbs, col + hbs, bl + 1);
             }
-        } else if (bc_bool(c, p[1], bp == 3)) {
+        } else if (bc_bool_e(c, enc, p[1], bp == 3)) {
             bp = 3;
-            walk_sb(w, row, col, bl + 1); walk_sb(w, row, col + hbs, bl + 1);
+            (enc ? walk_sb_enc : walk_sb_dec)(w, row, col, bl + 1); (enc ? walk_sb_enc : walk_sb_dec)(w, row, col + hbs, bl + 1);
         } else {
             bp = 1;
-            walk_block(w, row, col, bl, 1);
+            (enc ? walk_block_enc : walk_block_dec)(w, row, col, bl, 1);
         }
     } else if (row + hbs < w->rows) {
-        if (bc_bool(c, p[2], bp == 3)) { bp = 3; walk_sb(w, row, col, bl + 1); walk_sb(w, row + hbs, col, bl + 1); }
-        else { bp = 2; walk_block(w, row, col, bl, 2); }
+        if (bc_bool_e(c, enc, p[2], bp == 3)) { bp = 3; (enc ? walk_sb_enc : walk_sb_dec)(w, row, col, bl + 1); (enc ? walk_sb_enc : walk_sb_dec)(w, row + hbs, col, bl + 1); }
+        else { bp = 2; (enc ? walk_block_enc : walk_block_dec)(w, row, col, bl, 2); }
     } else {
         bp = 3;
-        walk_sb(w, row, col, bl + 1);
+        (enc ? walk_sb_enc : walk_sb_dec)(w, row, col, bl + 1);
     }
     w->cnt.partition[bl][ctx][bp]++;
+}
+static void walk_sb_dec(Walk *w, int row, int col, int bl) { walk_sb_t(w, row, col, bl, 0); }
+static void walk_sb_enc(Walk *w, int row, int col, int bl) { walk_sb_t(w, row, col, bl, 1); }
+static void walk_sb(Walk *w, int row, int col, int bl)
+{
+    if (w->c->enc) walk_sb_enc(w, row, col, bl);
+    else walk_sb_dec(w, row, col, bl);
 }
 
 /* ------------------------------------------------------------------ headers */

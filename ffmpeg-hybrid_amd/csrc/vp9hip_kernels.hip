@@ -2191,13 +2191,33 @@ __global__ __launch_bounds__(LfNT<G>::NT + 64) void k_lfrd(const uint32_t *__res
 // interiors written through (the LF loader reads them with sc1 loads in the same launch).
 // The last wave zeroes the tickets; the LF's last workgroup zeroes the done flags (it waited
 // for every one of them).
+// Bounded waits of k_lfro and its intra workers measure time, not polls: a poll's cost
+// differs by orders of magnitude between an LDS counter and an agent-scope flag in HBM under
+// load, so poll counts gave the waits on intra done flags (2^22 global polls) seconds where
+// their sibling waves' LDS waits (2^20 polls) gave up within ~50 ms, and a long intra wait
+// could end in a spurious timeout. Every wait gives up after LFRO_WAIT_TICKS of the 100 MHz
+// realtime clock; waits on intra done flags after half that, and then abort their workgroup,
+// so they give up first. A wait that gives up is counted (ctr[2] / pctr[2]: the batch fails
+// with VP9HIP_EBUG), never hangs. The test hook (ctr[3] / pctr[3] = n) bounds every wait to
+// n polls instead.
+// Dispatch order: an LF workgroup's waits on done flags assume the intra worker workgroups
+// (blockIdx < nblk, dispatched first as the hardware dispatches in blockIdx order) are
+// resident; if they were starved the waits would give up (EBUG) rather than hang.
+#define LFRO_WAIT_TICKS 20000000ull               // 200 ms
+DEV bool wait_expired(uint32_t n, uint32_t spin, uint64_t &t0, uint64_t ticks)
+{
+    if (spin) return n > spin;
+    if (n == 0) { t0 = __builtin_amdgcn_s_memrealtime(); return false; }
+    return (n & 63) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > ticks;
+}
+
 template <typename PIX, class G>
 DEV void lfri_worker(const LfrIntra &li, const FrameDesc *__restrict__ frames, PredLds<PIX, G, true> &S, int lane)
 {
 #if PRED_LTAB_LDS
     load_ltab<PIX>(S.ltab, li.ptab, lane);
 #endif
-    const uint32_t spin = li.pctr[3] ? li.pctr[3] : (1u << 22);
+    const uint32_t spin = li.pctr[3];                 // 0: LFRO_WAIT_TICKS / 2
     for (;;) {
         uint32_t task = 0;
         if (lane == 0) task = atomicAdd(&li.pctr[0], 1u);
@@ -2212,10 +2232,11 @@ DEV void lfri_worker(const LfrIntra &li, const FrameDesc *__restrict__ frames, P
         if (lane == 0 && (info & 2) && sb.sbx > 0) dep = slot - 1;
         if (lane == 1 && (info & 4) && sb.sby > 0) dep = slot - W;
         if (lane == 2 && (info & 8) && sb.sbx > 0 && sb.sby > 0) dep = slot - W - 1;
+        uint64_t tw = 0;
         for (uint32_t t = 0;; t++) {
             const bool ok = dep == ~0u || __hip_atomic_load((gu32 *) &li.done[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
             if (__all(ok)) break;
-            if (t > spin) {
+            if (wait_expired(t, spin, tw, LFRO_WAIT_TICKS / 2)) {
                 if (lane == 0) atomicAdd(&li.pctr[2], 1u);
                 break;
             }
@@ -2246,11 +2267,13 @@ DEV void lfro_pub(uint32_t *f, uint32_t v)
 }
 // (after a wait gives up, `abort` makes every later wait of the workgroup return at once:
 // the task drains in one bounded wait instead of one per SB and counter)
-DEV void lfro_wait(uint32_t *f, uint32_t need, uint32_t *ctr, uint32_t *abort, uint64_t &wc)
+DEV void lfro_wait(uint32_t *f, uint32_t need, uint32_t *ctr, uint32_t *abort, uint64_t &wc, uint32_t spin)
 {
     const uint64_t t0 = LFR_PROF ? clock64() : 0;
+    uint64_t tw = 0;
     for (uint32_t n = 0; __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need; n++) {
-        if (n > (1u << 20) || __hip_atomic_load(abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+        if (wait_expired(n, spin, tw, LFRO_WAIT_TICKS) ||
+            __hip_atomic_load(abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
             if ((threadIdx.x & 63) == 0 && !__hip_atomic_exchange(abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
                 atomicAdd(&ctr[2], 1u);
             break;
@@ -2340,7 +2363,7 @@ __global__ __launch_bounds__(LFRO_NTH) __attribute__((amdgpu_waves_per_eu(4))) v
     __syncthreads();
     const bool tl = LFR_PROF && s_tl;
 #define TLE(e, i) do { if (tl && lane == 0 && (i) >= TL_SB0 && (i) < TL_SB0 + TL_NSB) lfro_tl[e][(i) - TL_SB0] = clock64(); } while (0)
-    const uint32_t spin = ctr[3] ? ctr[3] : (1u << 22);
+    const uint32_t spin = ctr[3];                     // 0: the waits' time budgets (wait_expired)
     const uint32_t *T = tasks + tasks[s_task];
     const uint32_t dep = T[0], ncols = T[1], c0 = T[2];
     const LFRec &rec0 = recs[T[4]];
@@ -2359,10 +2382,10 @@ __global__ __launch_bounds__(LFRO_NTH) __attribute__((amdgpu_waves_per_eu(4))) v
             const int tb = i % LFRO_NTB, tp = tb ? tb - 1 : LFRO_NTB - 1;
             PIX *colp = S.lt[tb] + L::XL + lane;
             const uint64_t wt0 = wc;
-            lfro_wait(&F.ld_top, (uint32_t) i + 1, ctr, &F.abort, wc);
+            lfro_wait(&F.ld_top, (uint32_t) i + 1, ctr, &F.abort, wc, spin);
             if (LFR_PROF) wtop += wc - wt0;
             TLE(0, i);
-            lfro_wait(&F.h0, (uint32_t) i + 1, ctr, &F.abort, wc);
+            lfro_wait(&F.h0, (uint32_t) i + 1, ctr, &F.abort, wc, spin);
             TLE(1, i);
             const uint32_t *pw = S.prog[tb] + (LFP_YR + (lane >> 3) * 16) / 4;
             const uint32_t pw0 = pw[0], pw1 = pw[1], pw2 = pw[2], pw3 = pw[3];
@@ -2377,7 +2400,7 @@ __global__ __launch_bounds__(LFRO_NTH) __attribute__((amdgpu_waves_per_eu(4))) v
 #pragma unroll
             for (int r = 0; r < 8; r++) px[r] = px[32 + r];
             TLE(2, i);
-            lfro_wait(&F.h1, (uint32_t) i + 1, ctr, &F.abort, wc);
+            lfro_wait(&F.h1, (uint32_t) i + 1, ctr, &F.abort, wc, spin);
             TLE(3, i);
 #pragma unroll
             for (int r = 8; r < 40; r++) px[r] = colp[(32 + r) * FLP];
@@ -2402,8 +2425,8 @@ __global__ __launch_bounds__(LFRO_NTH) __attribute__((amdgpu_waves_per_eu(4))) v
             const int row = h * 32 + lane;
             for (int i = 0; i < n; i++) {
                 const int tb = i % LFRO_NTB, tp = tb ? tb - 1 : LFRO_NTB - 1;
-                lfro_wait(&F.ld_int, (uint32_t) i + 1, ctr, &F.abort, wc);
-                if (i > 0) lfro_wait(h ? &F.rb : &F.ra, (uint32_t) i, ctr, &F.abort, wc);
+                lfro_wait(&F.ld_int, (uint32_t) i + 1, ctr, &F.abort, wc, spin);
+                if (i > 0) lfro_wait(h ? &F.rb : &F.ra, (uint32_t) i, ctr, &F.abort, wc, spin);
                 TLE(5 + 2 * h, i);
                 PIX *trow = S.lt[tb] + (row + 8) * FLP;
                 // left halo: SB c - 1's last chunk, final for these rows now
@@ -2424,7 +2447,7 @@ __global__ __launch_bounds__(LFRO_NTH) __attribute__((amdgpu_waves_per_eu(4))) v
         const int p = 1 + (lane >= CH), r = lane & (CH - 1);
         for (int i = 0; i < n; i++) {
             const int tb = i % LFRO_NTB, tp = tb ? tb - 1 : LFRO_NTB - 1;
-            lfro_wait(&F.ld_int, (uint32_t) i + 1, ctr, &F.abort, wc);
+            lfro_wait(&F.ld_int, (uint32_t) i + 1, ctr, &F.abort, wc, spin);
             TLE(9, i);
             PIX *trow = S.ct[tb][p - 1] + (r + 8) * FCP;
             if (i > 0) Chunk16::to_lds(Chunk16::from_lds(S.ct[tp][p - 1] + (r + 8) * FCP + CW), trow);
@@ -2437,7 +2460,7 @@ __global__ __launch_bounds__(LFRO_NTH) __attribute__((amdgpu_waves_per_eu(4))) v
             lf_row_narrow_2<PIX>(rowp, pwc, S.lut, bd, lpx, lev);
             wave_sync();
             TLE(10, i);
-            lfro_wait(&F.ld_top, (uint32_t) i + 1, ctr, &F.abort, wc);
+            lfro_wait(&F.ld_top, (uint32_t) i + 1, ctr, &F.abort, wc, spin);
             TLE(11, i);
             PIX *colp = S.ct[tb][p - 1] + L::XL + r;
             const uint32_t *pwr = S.prog[tb] + (LFP_CR(1, 1) + (r >> 3) * LFP_CSTRIDE(1)) / 4;
@@ -2462,11 +2485,15 @@ __global__ __launch_bounds__(LFRO_NTH) __attribute__((amdgpu_waves_per_eu(4))) v
                     s = T[4 + c - c0] + (uint32_t) (dy * fd.sb_cols + dx);
                     if (!(li.sbinfo[s] & 1)) s = ~0u;
                 }
+                uint64_t tw = 0;
                 for (uint32_t t = 0;; t++) {
                     const bool ok = s == ~0u || __hip_atomic_load((gu32 *) &li.done[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
                     if (__all(ok)) break;
-                    if (t > spin) {
-                        if (lane == 0) atomicAdd(&ctr[2], 1u);
+                    // half the siblings' budget, then the workgroup aborts: its other waves'
+                    // waits on this wave end at once instead of timing out on their own
+                    if (wait_expired(t, spin, tw, LFRO_WAIT_TICKS / 2)) {
+                        if (lane == 0 && !__hip_atomic_exchange(&F.abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+                            atomicAdd(&ctr[2], 1u);
                         break;
                     }
                     __builtin_amdgcn_s_sleep(2);
@@ -2499,13 +2526,13 @@ __global__ __launch_bounds__(LFRO_NTH) __attribute__((amdgpu_waves_per_eu(4))) v
             const int tb = i % LFRO_NTB, tp = tb ? tb - 1 : LFRO_NTB - 1;
             const bool halo = i == 0 && c0 > 0;
             if (i >= LFRO_NTB) {
-                lfro_wait(&F.st1, (uint32_t) (i - LFRO_NTB + 1), ctr, &F.abort, wc);
-                lfro_wait(&F.st2, (uint32_t) (i - LFRO_NTB + 1), ctr, &F.abort, wc);
+                lfro_wait(&F.st1, (uint32_t) (i - LFRO_NTB + 1), ctr, &F.abort, wc, spin);
+                lfro_wait(&F.st2, (uint32_t) (i - LFRO_NTB + 1), ctr, &F.abort, wc, spin);
             }
             if (i >= LFRO_NTB - 1) {
-                lfro_wait(&F.h0x, (uint32_t) (i - LFRO_NTB + 2), ctr, &F.abort, wc);
-                lfro_wait(&F.h1x, (uint32_t) (i - LFRO_NTB + 2), ctr, &F.abort, wc);
-                lfro_wait(&F.cx, (uint32_t) (i - LFRO_NTB + 2), ctr, &F.abort, wc);
+                lfro_wait(&F.h0x, (uint32_t) (i - LFRO_NTB + 2), ctr, &F.abort, wc, spin);
+                lfro_wait(&F.h1x, (uint32_t) (i - LFRO_NTB + 2), ctr, &F.abort, wc, spin);
+                lfro_wait(&F.cx, (uint32_t) (i - LFRO_NTB + 2), ctr, &F.abort, wc, spin);
             }
             TLE(13, i);
 #pragma unroll
@@ -2535,11 +2562,12 @@ __global__ __launch_bounds__(LFRO_NTH) __attribute__((amdgpu_waves_per_eu(4))) v
             if (sby > 0) {
                 if (dep != ~0u && seen < c + 1) {
                     const uint64_t tw0 = LFR_PROF ? clock64() : 0;
+                    uint64_t tw = 0;
                     for (uint32_t k = 0;; k++) {
                         seen = __builtin_amdgcn_readfirstlane(
                             __hip_atomic_load((gu32 *) &progress[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
                         if (seen >= c + 1) break;
-                        if (k > spin) {
+                        if (wait_expired(k, spin, tw, LFRO_WAIT_TICKS)) {
                             if (lane == 0) atomicAdd(&ctr[2], 1u);
                             seen = c + 1;
                             break;
@@ -2561,8 +2589,8 @@ __global__ __launch_bounds__(LFRO_NTH) __attribute__((amdgpu_waves_per_eu(4))) v
                     vt[u] = make_uint4((uint32_t) lo, (uint32_t) (lo >> 32), (uint32_t) hi, (uint32_t) (hi >> 32));
                 }
                 if (i >= LFRO_NTB) {
-                    lfro_wait(&F.st1, (uint32_t) (i - LFRO_NTB + 1), ctr, &F.abort, wc);
-                    lfro_wait(&F.st2, (uint32_t) (i - LFRO_NTB + 1), ctr, &F.abort, wc);
+                    lfro_wait(&F.st1, (uint32_t) (i - LFRO_NTB + 1), ctr, &F.abort, wc, spin);
+                    lfro_wait(&F.st2, (uint32_t) (i - LFRO_NTB + 1), ctr, &F.abort, wc, spin);
                 }
 #pragma unroll
                 for (int u = 0; u < NUT; u++) {
@@ -2584,16 +2612,16 @@ __global__ __launch_bounds__(LFRO_NTH) __attribute__((amdgpu_waves_per_eu(4))) v
             if (c > 0) {
                 // SB c - 1's last columns (this tile's left halo) are final after this SB's
                 // first column edges: its bottom rows are then complete
-                lfro_wait(&F.h1x, (uint32_t) i + 1, ctr, &F.abort, wc);
-                lfro_wait(&F.cx, (uint32_t) i + 1, ctr, &F.abort, wc);
+                lfro_wait(&F.h1x, (uint32_t) i + 1, ctr, &F.abort, wc, spin);
+                lfro_wait(&F.cx, (uint32_t) i + 1, ctr, &F.abort, wc, spin);
                 TLE(17, i);
                 lfro_store<PIX, G>(S, tb, P, c, sby, lane, false, 0);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 if (lane == 0) __hip_atomic_store((gu32 *) &progress[s_task], (uint32_t) c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 TLE(18, i);
             }
-            lfro_wait(&F.rb, (uint32_t) i + 1, ctr, &F.abort, wc);
-            lfro_wait(&F.c, (uint32_t) i + 1, ctr, &F.abort, wc);
+            lfro_wait(&F.rb, (uint32_t) i + 1, ctr, &F.abort, wc, spin);
+            lfro_wait(&F.c, (uint32_t) i + 1, ctr, &F.abort, wc, spin);
             lfro_store<PIX, G>(S, tb, P, c, sby, lane, last, 1);
             if (last) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2607,9 +2635,9 @@ __global__ __launch_bounds__(LFRO_NTH) __attribute__((amdgpu_waves_per_eu(4))) v
         // ---- S2: the tile's other rows
         for (int i = 0; i < n; i++) {
             const int c = (int) c0 + i, tb = i % LFRO_NTB;
-            lfro_wait(&F.rb, (uint32_t) i + 1, ctr, &F.abort, wc);
-            lfro_wait(&F.c, (uint32_t) i + 1, ctr, &F.abort, wc);
-            lfro_wait(&F.h0x, (uint32_t) i + 1, ctr, &F.abort, wc);
+            lfro_wait(&F.rb, (uint32_t) i + 1, ctr, &F.abort, wc, spin);
+            lfro_wait(&F.c, (uint32_t) i + 1, ctr, &F.abort, wc, spin);
+            lfro_wait(&F.h0x, (uint32_t) i + 1, ctr, &F.abort, wc, spin);
             TLE(19, i);
             lfro_store<PIX, G>(S, tb, P, c, sby, lane, i == n - 1, 2);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
