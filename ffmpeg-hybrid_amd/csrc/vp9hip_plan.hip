@@ -586,10 +586,13 @@ __global__ __launch_bounds__(64) void k_pjob(PlanDev D)
 // One wave per SB: producers of every intra job, heights, priority order, list-scheduled
 // passes (the host's merge_mixed), the PJob / pass records, the SB's records, its level
 // dependencies and intra step. Jobs come from k_pjob (D.jobw); the unit map is rebuilt.
+// (Two SBs per wave with the second's job words loaded under the first's scheduling cut the
+// first load's share of a wave's cycles from 31 to 20 %, but not the kernel: 2,880 -> 2,926 us
+// per C3 batch. The waves' time goes to dependent LDS chains at 6 waves per SIMD, LDS-bound.)
 template <int SSH, int SSV>
 __global__ __launch_bounds__(64) void k_plan(PlanDev D)
 {
-    constexpr int CW = 16 >> SSH, CH = 16 >> SSV, JCAP = 256 + 2 * CW * CH;
+    constexpr int CW = 16 >> SSH, CH = 16 >> SSV, JCAP = 256 + 2 * CW * CH, NCH = JCAP / 64;
     __shared__ PlanLds<JCAP> S;
     const PlanFrame &F = D.frames[blockIdx.y];
     const int s = blockIdx.x, lane = threadIdx.x;
@@ -603,6 +606,7 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
     for (int i = lane; i < 3 * 256 / 8; i += 64) ((uint4 *) &S.u.jmap[0][0])[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
     for (int j = lane; j < NJ; j += 64) S.ja[j] = D.jobw[(size_t) slot * JCAP + (uint32_t) j];
     wsync();
+    PPT(8);
     // the unit map: each job's 4x4 units hold JM_ENT(job, units to the job's right edge, units
     // to its bottom edge), so the producer walk below steps past a producer's extent from the
     // entry alone (one LDS read per producer instead of the entry and the job's word)
@@ -631,6 +635,7 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
         }
     }
     wsync();
+    PPT(9);
 
     // ---- producers of every intra job (the pixels its substituted mode reads)
     // The units job j reads are pl_local_reads' runs: the top row (uy0 - 1, from ux0 - 1 with
@@ -719,8 +724,7 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
     }
     PPT(4);
     // ---- priority order: height descending, then decode order. The heights go to registers
-    // first: the order and the pass words overlay them
-    constexpr int NCH = JCAP / 64;
+    // first: the order and the pass words overlay them (NCH = JCAP / 64 chunks)
     int hreg[NCH];
 #pragma unroll
     for (int c = 0; c < NCH; c++) {
