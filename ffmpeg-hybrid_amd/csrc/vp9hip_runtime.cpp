@@ -2495,6 +2495,10 @@ static int launch_one(vp9hip_ctx *c, const Launch &L, hipStream_t st)
     Staged &s = c->stg;
     const FrameDesc *fr = (const FrameDesc *) (s.arena + s.o_frames);
     const uint32_t *lists = (const uint32_t *) (s.arena + s.o_lists);
+    // timing-only ablations (tools/ablate.sh; frames are then wrong): VP9HIP_DEBUG bit 28 skips
+    // the level phases' k_resid_multi launches, bit 29 the k_mcq launches
+    if ((c->dbg >> 28 & 1) && L.kind == K_RESID && L.arg == 5) return 0;
+    if ((c->dbg >> 29 & 1) && L.kind == K_MC) return 0;
     switch (L.kind) {
     case K_MC:
         return vp9hip_launch_mc(c->hb, st, (int) L.n, (const McUnit *) (s.arena + s.o_mcs) + L.off, fr, &c->kcfg);
