@@ -17,6 +17,7 @@ own (MODE "thread": FFmpeg's user thread transferring and unreferencing frames w
 decoder keeps calling the hwaccel). tools/sanitize.sh runs larger inputs and keeps the logs
 under profiles/.
 """
+import fcntl
 import os
 import subprocess
 
@@ -33,8 +34,13 @@ VARIANTS = ("plain", "asan", "tsan")
 
 @pytest.fixture(scope="module")
 def sanbins():
-    r = subprocess.run(["make", "-s", "-j8", "-C", os.path.join(ROOT, "ffmpeg-hybrid_amd", "csrc"), "sanitize"],
-                       capture_output=True, text=True, timeout=600)
+    # one make at a time: pytest-xdist workers each set this fixture up, and a worker linking
+    # while another rewrites a host object links a truncated object
+    os.makedirs(BUILD, exist_ok=True)
+    with open(os.path.join(BUILD, ".make.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        r = subprocess.run(["make", "-s", "-j8", "-C", os.path.join(ROOT, "ffmpeg-hybrid_amd", "csrc"), "sanitize"],
+                           capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
     return BUILD
 
