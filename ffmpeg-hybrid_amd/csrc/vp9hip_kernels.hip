@@ -481,13 +481,9 @@ template <int N, typename COEF> struct RWave { static constexpr int E = (64 / N)
 // launches); the keyframe launches (k_resid_dev) write scratch and keep their registers:
 // they run beside the other slot's k_plf chains, whose co-resident waves the extra
 // registers cost (r04's PREQ everywhere: C3 10,245 -> 9,863 fps on one box, profiles/r05b).
-// gate (k_mcr: gctr non-null): in-place jobs add to pixels another part of the launch writes;
-// the wave waits for gctr[0] >= gneed (mcr_gate) after its transform, before its first pixel load
-DEV void mcr_gate(uint32_t *ctr, uint32_t need, int lane);
 template <int N, int TCODE, typename PIX, class M, typename COEF, bool PREQ = true>
 DEV void resid_wave(const RJob *__restrict__ jobs, int njobs, int wj, int lane, const FrameDesc *__restrict__ frames,
-                    const COEF *__restrict__ coefs, int16_t *__restrict__ resid, COEF *cbw, uint32_t *gctr = nullptr,
-                    uint32_t gneed = 0)
+                    const COEF *__restrict__ coefs, int16_t *__restrict__ resid, COEF *cbw)
 {
     typedef typename M::T T;
     constexpr int CAP = 64 / N;
@@ -593,7 +589,6 @@ DEV void resid_wave(const RJob *__restrict__ jobs, int njobs, int wj, int lane, 
             for (int k = 0; k < N; k++) res[k] = add;
         }
     }
-    if (gctr && __any(act && RJ_INPLACE(r))) mcr_gate(gctr, gneed, lane);
     if (!act) return;
     if (RJ_INPLACE(r)) {
         const int bd = frames[r.frame].bd;
@@ -2981,9 +2976,7 @@ DEV void mcq_h(const uint32_t (&d)[McqW<PIX>::N], const uint32_t (&th)[4], bool 
     }
 }
 
-// SC (k_mcr): the output rows are stored write-through (sc1: agent-scope relaxed atomic
-// stores), so a residual wave of the same launch reads them after one counter hand-off
-template <typename PIX, int R, bool V, bool DIRECT, bool SC = false>
+template <typename PIX, int R, bool V, bool DIRECT>
 DEV void mcq_rows(const McL &u, const McqLds &S, int xx, int yy)
 {
     constexpr int NW = sizeof(PIX) == 1 ? 1 : 2;          // output dwords per row
@@ -3069,15 +3062,7 @@ DEV void mcq_rows(const McL &u, const McqLds &S, int xx, int yy)
     gpo *dst = (gpo *) u.dst + (size_t) (u.y + yy) * pitch + u.x + xx;
 #pragma unroll
     for (int t = 0; t < R; t++) {
-        if constexpr (SC) {
-            typedef __attribute__((address_space(1))) uint32_t g32;
-            typedef __attribute__((address_space(1))) uint64_t g64;
-            if constexpr (sizeof(PIX) == 1)
-                __hip_atomic_store((g32 *) (dst + (size_t) t * pitch), outp[t][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            else
-                __hip_atomic_store((g64 *) (dst + (size_t) t * pitch), (uint64_t) outp[t][0] | (uint64_t) outp[t][1] << 32,
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else if constexpr (sizeof(PIX) == 1) *(__attribute__((address_space(1))) uint32_t *) (dst + (size_t) t * pitch) = outp[t][0];
+        if constexpr (sizeof(PIX) == 1) *(__attribute__((address_space(1))) uint32_t *) (dst + (size_t) t * pitch) = outp[t][0];
         else {
             typedef uint32_t v2u __attribute__((ext_vector_type(2)));
             v2u w2; w2.x = outp[t][0]; w2.y = outp[t][1];
@@ -3086,28 +3071,27 @@ DEV void mcq_rows(const McL &u, const McqLds &S, int xx, int yy)
     }
 }
 
-template <typename PIX, int R, bool SC = false>
+template <typename PIX, int R>
 DEV void mcq_task(const McL &u, const McqLds &S, int xx, int yy)
 {
     const bool v = u.my[0] | (u.nref > 1 ? u.my[1] : 0);
     const bool dir = (u.direct & ((1 << u.nref) - 1)) == ((1 << u.nref) - 1);
     if (__all(dir)) {
-        if (__any(v)) mcq_rows<PIX, R, true, true, SC>(u, S, xx, yy);
-        else mcq_rows<PIX, R, false, true, SC>(u, S, xx, yy);
+        if (__any(v)) mcq_rows<PIX, R, true, true>(u, S, xx, yy);
+        else mcq_rows<PIX, R, false, true>(u, S, xx, yy);
     } else {
-        if (__any(v)) mcq_rows<PIX, R, true, false, SC>(u, S, xx, yy);
-        else mcq_rows<PIX, R, false, false, SC>(u, S, xx, yy);
+        if (__any(v)) mcq_rows<PIX, R, true, false>(u, S, xx, yy);
+        else mcq_rows<PIX, R, false, false>(u, S, xx, yy);
     }
 }
 
-// one k_mcq workgroup: unit group bx (64 units), task slice by of ns; returns whether it
-// ran scaled tasks (their per-pixel stores are plain)
-template <typename PIX, bool SC = false>
-DEV bool mcq_wg(const McUnit *__restrict__ units, int nunits, const FrameDesc *__restrict__ frames, int bx, int by, int ns,
-                McqLds &S)
+template <typename PIX>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_mcq(const McUnit *__restrict__ units, int nunits,
+                                             const FrameDesc *__restrict__ frames)
 {
+    __shared__ McqLds S;
     const int tid = threadIdx.x;
-    const int u0 = bx * MCP_U, nu = nunits - u0 < MCP_U ? nunits - u0 : MCP_U;
+    const int u0 = blockIdx.x * MCP_U, nu = nunits - u0 < MCP_U ? nunits - u0 : MCP_U;
     {
         // filter rows: 3 x 16 8-tap phases, then the bilinear ones as 8-taps; int8 quads of
         // the non-identity phases (every tap of phases 1-15 lies in [-128, 127])
@@ -3149,7 +3133,7 @@ DEV bool mcq_wg(const McUnit *__restrict__ units, int nunits, const FrameDesc *_
     __syncthreads();
     // blockIdx.y: one of gridDim.y slices of the tasks (a workgroup of 64 large units is
     // otherwise the launch's tail: units per workgroup are counted, not their pixels)
-    const int g0 = by * 256, gs = 256 * ns;
+    const int g0 = (int) blockIdx.y * 256, gs = 256 * (int) gridDim.y;
     for (int c = 0; c < 2; c++) {
         const uint32_t T = S.off[c][nu];
         for (uint32_t g = tid + g0; g < T; g += gs) {
@@ -3159,120 +3143,11 @@ DEV bool mcq_wg(const McUnit *__restrict__ units, int nunits, const FrameDesc *_
             const int lq = u.lw - 2;                      // 4-column groups per row: w / 4
             const int xx = (int) (ti & ((1u << lq) - 1)) * 4;
             const int yy = (int) (ti >> lq) << (c ? 2 : 3);
-            if (c == 0) mcq_task<PIX, 8, SC>(u, S, xx, yy);
-            else mcq_task<PIX, 4, SC>(u, S, xx, yy);
+            if (c == 0) mcq_task<PIX, 8>(u, S, xx, yy);
+            else mcq_task<PIX, 4>(u, S, xx, yy);
         }
     }
     mcp_scaled<PIX>(units + u0, S.off[2], nu, frames, tid, g0, gs);
-    return S.off[2][nu] > (uint32_t) g0;
-}
-
-template <typename PIX>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_mcq(const McUnit *__restrict__ units, int nunits,
-                                             const FrameDesc *__restrict__ frames)
-{
-    __shared__ McqLds S;
-    mcq_wg<PIX>(units, nunits, frames, (int) blockIdx.x, (int) blockIdx.y, (int) gridDim.y, S);
-}
-
-// ------------------------------------------------------------- k_mcr
-// k_mcq and k_resid_multi of a level phase (a GOP chain position) in ONE launch.
-// - Roles by ticket: each workgroup takes a ticket b when it starts; tickets [0, nmc) do
-//   k_mcq's work (unit group b % nb, task slice b / nb), the rest k_resid_multi's waves. So a
-//   residual workgroup waits only on MC work that running workgroups hold, whatever the
-//   dispatch order and whatever other launches (the other batch slots' k_mcr) hold the rest
-//   of the chip. With blockIdx roles two concurrent k_mcr launches deadlocked (each one's
-//   waiting residual workgroups holding the CU slots the other's undispatched MC workgroups
-//   needed) until the waits gave up.
-// - A residual wave runs its coefficient scatter and transform at once and waits only before
-//   it adds to MC output (in-place jobs): until every MC workgroup has counted itself.
-// - Producer: the rows are stored sc1 (write-through); every thread drains its stores, the
-//   workgroup meets, and wave 0 adds 1 to each of the MCR_REP replicas of the done count.
-//   A workgroup that ran scaled tasks (plain per-pixel stores; rare: resized references)
-//   releases at agent scope first. That writes back the XCD's L2 (~2-6 us, serialised per
-//   L2), so not for every workgroup.
-// - Consumer: lane 0 polls one replica (relaxed, sleeping between polls, time-bounded:
-//   ctr[2] counts a wait given up; the batch then fails with VP9HIP_EBUG, as after a k_lfro
-//   timeout), then an agent-scope acquire before the pixel loads.
-// - Every counter sits on a 128-byte line of its own. One line for the ticket, the done count
-//   and thousands of polling waves made the launch 10x slower than the two launches.
-// - The last workgroup to finish zeroes the counters for the next launch (graph replay).
-// ctr (32-word aligned; MCR_CTR_WORDS): line 0 {-, workgroups finished, timeouts, spin bound
-// (0: time-based)}, line 1 {ticket}, lines 2 .. 2 + MCR_REP - 1 {MC workgroups done}.
-#define MCR_REP 16
-#define MCR_CTR_WORDS (32 * (2 + MCR_REP))
-struct McrArgs { ResidMulti r; int nunits, nb, ns, nmc; };
-DEV void mcr_gate(uint32_t *ctr, uint32_t need, int lane)
-{
-    if (lane == 0) {
-        const uint32_t spin = ctr[3];
-        const uint32_t rep = (uint32_t) __smid() % MCR_REP;        // spread the pollers
-        uint64_t t0 = 0;
-        for (uint32_t n = 0;; n++) {
-            if (__hip_atomic_load((gu32 *) &ctr[64 + 32 * rep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need) break;
-            if (wait_expired(n, spin, t0, LFRO_WAIT_TICKS)) {
-                atomicAdd(&ctr[2], 1u);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(8);
-        }
-    }
-    wave_sync();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-}
-template <typename PIX, class M, typename COEF>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_mcr(McrArgs a, const McUnit *__restrict__ units, const RJob *__restrict__ jobs,
-                                             const FrameDesc *__restrict__ frames, const COEF *__restrict__ coefs,
-                                             int16_t *__restrict__ resid, uint32_t *ctr)
-{
-    static_assert(RWAVES * 64 == 256, "k_mcr: one block size for both parts");
-    constexpr int E = RWave<32, COEF>::E > RWave<16, COEF>::E ? RWave<32, COEF>::E : RWave<16, COEF>::E;
-    __shared__ union McrLds { McqLds mc; COEF cbs[RWAVES][E]; } U;
-    __shared__ uint32_t s_last, s_ticket;
-    if (threadIdx.x == 0) s_ticket = atomicAdd(&ctr[32], 1u);
-    __syncthreads();
-    const int b = (int) s_ticket;
-    if (b < a.nmc) {
-        const bool scaled = mcq_wg<PIX, true>(units, a.nunits, frames, b % a.nb, b / a.nb, a.ns, U.mc);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x < 64) {                                     // wave 0
-            if (scaled) {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // the compiler may drop it (guide)
-            }
-            if (threadIdx.x < MCR_REP)
-                __hip_atomic_fetch_add((gu32 *) &ctr[64 + 32 * threadIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    } else {
-        const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-        const uint32_t gw = (uint32_t) (b - a.nmc) * RWAVES + wave;
-        if (gw < a.r.w0[5]) {
-            int t = 0;
-#pragma unroll
-            for (int k = 1; k < 5; k++) t += gw >= a.r.w0[k];
-            // selects, not an indexed kernel argument (that is copied to scratch)
-            auto sel = [t](const uint32_t *v) { return t == 0 ? v[0] : t == 1 ? v[1] : t == 2 ? v[2] : t == 3 ? v[3] : v[4]; };
-            const int wj = (int) (gw - sel(a.r.w0));
-            const RJob *j = jobs + sel(a.r.off);
-            const int n = (int) sel(a.r.n);
-            const uint32_t need = (uint32_t) a.nmc;
-            switch (t) {
-            case 0: resid_wave<4, 0, PIX, M, COEF, false>(j, n, wj, lane, frames, coefs, resid, U.cbs[wave], ctr, need); break;
-            case 1: resid_wave<8, 1, PIX, M, COEF, false>(j, n, wj, lane, frames, coefs, resid, U.cbs[wave], ctr, need); break;
-            case 2: resid_wave<16, 2, PIX, M, COEF, false>(j, n, wj, lane, frames, coefs, resid, U.cbs[wave], ctr, need); break;
-            case 3: resid_wave<32, 3, PIX, M, COEF, false>(j, n, wj, lane, frames, coefs, resid, U.cbs[wave], ctr, need); break;
-            default: resid_wave<4, 4, PIX, M, COEF, false>(j, n, wj, lane, frames, coefs, resid, U.cbs[wave], ctr, need); break;
-            }
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) s_last = atomicAdd(&ctr[1], 1u) == gridDim.x - 1;
-    __syncthreads();
-    if (s_last && threadIdx.x < MCR_REP) {
-        ctr[64 + 32 * threadIdx.x] = 0;
-        if (threadIdx.x == 0) { ctr[1] = 0; ctr[32] = 0; }
-    }
 }
 
 // ------------------------------------------------------------ launchers
@@ -3577,36 +3452,6 @@ int vp9hip_launch_plf(int fmt, hipStream_t st, const PlfLaunch *pl, const uint32
 {
     return (fmt & 1 ? vp9hip_launch_plf_16 : vp9hip_launch_plf_8)(fmt >> 1, st, pl, plist, llist, wgs, sbs, jobs, passes,
                                                                   recs, rjobs, frames, coefs, resid, ptab, dbg);
-}
-// k_mcr: the k_mcq grid of vp9hip_launch_mc, then the k_resid_multi waves of
-// vp9hip_launch_resid_multi, one launch; ctr = its counter block (vp9hip_mcr_ctr_words(),
-// 128-byte aligned, zero)
-int vp9hip_mcr_ctr_words(void) { return MCR_CTR_WORDS; }
-int vp9hip_launch_mcr(int hb, hipStream_t st, int n, const McUnit *units, const uint32_t *off, const uint32_t *rn,
-                      const RJob *jobs, const FrameDesc *frames, const void *coefs, int16_t *resid, uint32_t *ctr,
-                      const KCfg *k)
-{
-    if (n <= 0) return -1;
-    static const int tn[5] = { 4, 8, 16, 32, 4 };
-    McrArgs a;
-    a.r.w0[0] = 0;
-    for (int t = 0; t < 5; t++) {
-        a.r.off[t] = off[t]; a.r.n[t] = rn[t];
-        const uint32_t per = 64 / tn[t];
-        a.r.w0[t + 1] = a.r.w0[t] + (rn[t] + per - 1) / per;
-    }
-    a.nunits = n;
-    a.nb = (n + MCP_U - 1) / MCP_U;
-    a.ns = k->mcq_slices > 0 ? std::min(16, k->mcq_slices) : std::max(2, std::min(8, 4096 / a.nb));
-    a.nmc = a.nb * a.ns;
-    const int nr = (int) ((a.r.w0[5] + RWAVES - 1) / RWAVES);
-    if (hb)
-        hipLaunchKernelGGL((k_mcr<uint16_t, M64, int32_t>), dim3(a.nmc + nr), dim3(256), 0, st, a, units, jobs, frames,
-                           (const int32_t *) coefs, resid, ctr);
-    else
-        hipLaunchKernelGGL((k_mcr<uint8_t, M32, int16_t>), dim3(a.nmc + nr), dim3(256), 0, st, a, units, jobs, frames,
-                           (const int16_t *) coefs, resid, ctr);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int vp9hip_launch_mc(int hb, hipStream_t st, int n, const McUnit *units, const FrameDesc *frames, const KCfg *k)
 {

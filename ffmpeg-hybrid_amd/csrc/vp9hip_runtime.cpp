@@ -57,10 +57,6 @@ int vp9hip_launch_predd(int fmt, hipStream_t st, int n, int wgcap, const uint32_
                         const SBRec *sbs, const PJob *jobs, const uint32_t *passes, const FrameDesc *frames,
                         const int16_t *resid, const uint32_t *ptab, uint32_t *ctr, uint32_t *done, int dbg);
 int vp9hip_launch_mc(int hb, hipStream_t st, int n, const McUnit *units, const FrameDesc *frames, const KCfg *k);
-int vp9hip_launch_mcr(int hb, hipStream_t st, int n, const McUnit *units, const uint32_t *off, const uint32_t *rn,
-                      const RJob *jobs, const FrameDesc *frames, const void *coefs, int16_t *resid, uint32_t *ctr,
-                      const KCfg *k);
-int vp9hip_mcr_ctr_words(void);
 size_t vp9hip_plan_scan_bytes(size_t n);
 int vp9hip_plan_enqueue(hipStream_t st, const PlanDev *D, int ss, int nframes, int max_blk, int max_sb, uint32_t nb,
                         uint32_t nslots, uint32_t ncnt, int nk, const uint32_t *gidx, int ng, uint32_t *summary,
@@ -89,8 +85,7 @@ struct Launch { int kind; uint32_t off; uint32_t n; int arg; int grp; int ph; in
                 uint32_t roff[5] = { 0, 0, 0, 0, 0 }, rn[5] = { 0, 0, 0, 0, 0 };   // K_PLF residual jobs by tx code
                 int devr = 0;   // K_RESID of a static plan: off = the summary index of its job range, n = a bound
                 int flow = -1;  // K_PRED of a level phase as one k_predd launch: its counter block;
-                                // K_LFR with the phase's intra SBs inside (off2 / n2 their list);
-                                // K_MC with the phase's residual jobs inside (k_mcr, roff / rn)
+                                // K_LFR with the phase's intra SBs inside (off2 / n2 their list)
 };
 #define PLF_LAG 3   // see the schedule in stage()
 // Residuals run inside the fused launches (one intra diagonal ahead) for phases of fewer
@@ -169,7 +164,6 @@ struct Staged {
         uint32_t lfr_off = 0, lfr_n = 0;                      // k_lfr task table in the host lists
         int lfr_ctr = 0;
         int pred_ctr = -1;                                    // k_predd counter block (level phases)
-        int mcr_ctr = -1;                                     // k_mcr counter block (level phases)
         bool all_lf = false;                                  // every frame of the phase is loop-filtered
         double lfr_bytes = 0;
         int g_res = 0, g_mc = 0;                              // summary gather slots
@@ -328,7 +322,6 @@ struct vp9hip_ctx {
     bool static_plan = true;            // VP9HIP_STATIC=0: keyframe batches planned like the others
     bool edge = true;                   // VP9HIP_EDGE=0: no SB edge columns (4:2:0 tile loader)
     bool resid_multi = true;            // VP9HIP_RESID_MULTI=0: one residual launch per tx size
-    bool mcr = false;                   // VP9HIP_MCR=1: a level phase's MC and residuals in one k_mcr launch
     bool stage_trace = false;           // VP9HIP_STAGE_TRACE=1: host time of staging / planning
     bool plan_prof_on = false;          // VP9HIP_PLAN_PROF=1: k_plan phase cycles
     int plan_dbg = 0;                   // VP9HIP_PLAN_DBG: planner ablations (timing only)
@@ -435,7 +428,6 @@ static void read_config(vp9hip_ctx *c)
     c->static_plan = num("VP9HIP_STATIC", 1) != 0;
     c->edge = num("VP9HIP_EDGE", 1) != 0;
     c->resid_multi = num("VP9HIP_RESID_MULTI", 1) != 0;
-    c->mcr = num("VP9HIP_MCR", 0) != 0;
     c->stage_trace = num("VP9HIP_STAGE_TRACE", 0) != 0;
     c->plan_prof_on = num("VP9HIP_PLAN_PROF", 0) != 0;
     c->plan_dbg = num("VP9HIP_PLAN_DBG", 0);
@@ -1259,13 +1251,6 @@ static int stage_dev(vp9hip_ctx *c, const DevIn &in)
             s.lfr_ctr.push_back(s.n_ctr);
             s.n_ctr += 4;              // ticket, finished, timeouts, spin
         }
-        P.mcr_ctr = -1;
-        if (P.levels && c->mcr && c->resid_multi && !P.fused) {
-            s.n_ctr = (s.n_ctr + 31) & ~31u;                  // its counters on lines of their own
-            P.mcr_ctr = (int) s.n_ctr;
-            s.lfr_ctr.push_back(s.n_ctr);
-            s.n_ctr += (uint32_t) vp9hip_mcr_ctr_words();
-        }
         int nd = 0, nlfd = 0, nk = 0;
         for (int i : P.frames) {
             const FrameBuild &fb = fbs[i];
@@ -1786,14 +1771,9 @@ static int plan_dev(vp9hip_ctx *c)
                 return std::make_pair(a, b - a);
             };
             // level-scheduled (inter chain) phases: every tx size in one launch (arg 5, the
-            // ranges in roff / rn); VP9HIP_RESID_MULTI=0 keeps one launch per size;
-            // VP9HIP_MCR=1 puts them inside the phase's MC launch (k_mcr)
+            // ranges in roff / rn); VP9HIP_RESID_MULTI=0 keeps one launch per size
             const bool rmulti = c->resid_multi;
-            if (P.mcr_ctr >= 0 && m1 > m0) {
-                Launch &L = s.launches.back();
-                for (int tc = 0; tc < 5; tc++) { L.roff[tc] = rr(0, tc).first; L.rn[tc] = rr(0, tc).second; }
-                L.flow = P.mcr_ctr;
-            } else if (!P.fused && P.levels && rmulti) {
+            if (!P.fused && P.levels && rmulti) {
                 Launch L = { K_RESID, 0, 0, 5, g, ph, PART_RECON, 0 };
                 for (int tc = 0; tc < 5; tc++) { L.roff[tc] = rr(0, tc).first; L.rn[tc] = rr(0, tc).second; L.n += L.rn[tc]; }
                 if (L.n) s.launches.push_back(L);
@@ -2521,10 +2501,6 @@ static int launch_one(vp9hip_ctx *c, const Launch &L, hipStream_t st)
     if ((c->dbg >> 29 & 1) && L.kind == K_MC) return 0;
     switch (L.kind) {
     case K_MC:
-        if (L.flow >= 0)
-            return vp9hip_launch_mcr(c->hb, st, (int) L.n, (const McUnit *) (s.arena + s.o_mcs) + L.off, L.roff, L.rn,
-                                     (const RJob *) (s.arena + s.o_rjobs), fr, s.arena + s.o_coefs, s.resid,
-                                     (uint32_t *) (s.arena + s.o_ctr) + L.flow, &c->kcfg);
         return vp9hip_launch_mc(c->hb, st, (int) L.n, (const McUnit *) (s.arena + s.o_mcs) + L.off, fr, &c->kcfg);
     case K_RESID:
         if (L.devr)
