@@ -481,9 +481,7 @@ template <int N, typename COEF> struct RWave { static constexpr int E = (64 / N)
 // launches); the keyframe launches (k_resid_dev) write scratch and keep their registers:
 // they run beside the other slot's k_plf chains, whose co-resident waves the extra
 // registers cost (r04's PREQ everywhere: C3 10,245 -> 9,863 fps on one box, profiles/r05b).
-// RPL (VP9HIP_MCR): in-place jobs store their residual to the frame's residual plane
-// (FrameDesc.rplane, same element offset as the pixel) instead of adding it; k_mcq adds it
-template <int N, int TCODE, typename PIX, class M, typename COEF, bool PREQ = true, bool RPL = false>
+template <int N, int TCODE, typename PIX, class M, typename COEF, bool PREQ = true>
 DEV void resid_wave(const RJob *__restrict__ jobs, int njobs, int wj, int lane, const FrameDesc *__restrict__ frames,
                     const COEF *__restrict__ coefs, int16_t *__restrict__ resid, COEF *cbw)
 {
@@ -513,7 +511,7 @@ DEV void resid_wave(const RJob *__restrict__ jobs, int njobs, int wj, int lane, 
     int pq[PRE ? N : 1];
     PIX *q = nullptr;
     size_t qp = 0;
-    if (!RPL && act && RJ_INPLACE(r)) {
+    if (act && RJ_INPLACE(r)) {
         const FrameDesc &fd = frames[r.frame];
         const int p = RJ_PLANE(r);
         q = (PIX *) fd.plane[p] + r.dst + li;
@@ -592,14 +590,7 @@ DEV void resid_wave(const RJob *__restrict__ jobs, int njobs, int wj, int lane, 
         }
     }
     if (!act) return;
-    if (RPL && RJ_INPLACE(r)) {
-        const FrameDesc &fd = frames[r.frame];
-        const int p = RJ_PLANE(r);
-        int16_t *rp = (int16_t *) fd.rplane + (fd.plane[p] - fd.plane[0]) / sizeof(PIX) + r.dst + li;
-        const size_t rpp = (size_t) fd.pitch[p ? 1 : 0];
-#pragma unroll
-        for (int k = 0; k < N; k++) rp[k * rpp] = (int16_t) (res[k] < -32768 ? -32768 : res[k] > 32767 ? 32767 : res[k]);
-    } else if (RJ_INPLACE(r)) {
+    if (RJ_INPLACE(r)) {
         const int bd = frames[r.frame].bd;
 #pragma unroll
         for (int k = 0; k < N; k++) {
@@ -2804,7 +2795,7 @@ DEV int mc_sample(const PIX *r, int pitch, int w, int h, int X, int Y, int mx, i
 // per-pixel sampler (mc_sample), one pixel per task.
 #define MCP_U 64                                  // units per workgroup
 struct McL {                                      // a unit as its tasks read it (LDS)
-    uint64_t ref[2], dst, rdst;                   // rdst: the unit plane's int16 residual plane (RPL), or 0
+    uint64_t ref[2], dst;
     int32_t ix[2], iy[2];
     int32_t pitch;
     uint16_t x, y, rw[2], rh[2];
@@ -2830,7 +2821,6 @@ DEV void mcp_unit(const McUnit &m, const FrameDesc *__restrict__ frames, McL &L)
     const FrameDesc &fd = frames[m.frame];
     const int p = m.plane, c = p ? 1 : 0;
     L.dst = fd.plane[p];
-    L.rdst = fd.rplane ? fd.rplane + 2 * ((fd.plane[p] - fd.plane[0]) / (fd.bd > 8 ? 2 : 1)) : 0;
     L.pitch = fd.pitch[c];
     L.x = m.x; L.y = m.y;
     L.lw = (uint8_t) (31 - __builtin_clz((unsigned) m.w));
@@ -2873,7 +2863,7 @@ DEV void mcp_offsets(uint32_t (*off)[MCP_U + 1], const uint32_t (&cnt)[3], int t
     }
 }
 // scaled references: one pixel per task (mc_unit_pixels)
-template <typename PIX, bool RPL = false>
+template <typename PIX>
 DEV void mcp_scaled(const McUnit *__restrict__ units, const uint32_t *off, int nu, const FrameDesc *__restrict__ frames, int tid,
                     int g0 = 0, int gs = 256)
 {
@@ -2886,9 +2876,7 @@ DEV void mcp_scaled(const McUnit *__restrict__ units, const uint32_t *off, int n
         const uint32_t ti = g - off[k];
         const int yy = (int) ti / W, xx = (int) ti - yy * W;
         int out = 0;
-#pragma unroll
-        for (int r = 0; r < 2; r++) {                  // constant indices: m stays in registers
-            if (r >= m.nref) break;
+        for (int r = 0; r < m.nref; r++) {
             const int rf = m.ref[r];
             const McRef q = m.r[r];
             const int px = q.mx + xx * q.dx, py = q.my + yy * q.dy;
@@ -2896,13 +2884,7 @@ DEV void mcp_scaled(const McUnit *__restrict__ units, const uint32_t *off, int n
                                          q.ix + (px >> 4), q.iy + (py >> 4), px & 15, py & 15, m.filter, fd.bd);
             out = r ? (out + v + 1) >> 1 : v;
         }
-        const size_t e = (size_t) (m.y + yy) * fd.pitch[c] + m.x + xx;
-        if (RPL && fd.rplane) {
-            int16_t *rp = (int16_t *) fd.rplane + (fd.plane[p] - fd.plane[0]) / sizeof(PIX) + e;
-            const int rv = *rp;
-            if (rv) { out = clipbd(out + rv, fd.bd); *rp = 0; }
-        }
-        ((PIX *) fd.plane[p])[e] = (PIX) out;
+        ((PIX *) fd.plane[p])[(size_t) (m.y + yy) * fd.pitch[c] + m.x + xx] = (PIX) out;
     }
 }
 
@@ -2994,9 +2976,7 @@ DEV void mcq_h(const uint32_t (&d)[McqW<PIX>::N], const uint32_t (&th)[4], bool 
     }
 }
 
-// RPL: the unit's residual (FrameDesc.rplane, written one chain position earlier) is added
-// to the prediction as it is stored, and its elements are zeroed again for the next batch
-template <typename PIX, int R, bool V, bool DIRECT, bool RPL = false>
+template <typename PIX, int R, bool V, bool DIRECT>
 DEV void mcq_rows(const McL &u, const McqLds &S, int xx, int yy)
 {
     constexpr int NW = sizeof(PIX) == 1 ? 1 : 2;          // output dwords per row
@@ -3080,38 +3060,6 @@ DEV void mcq_rows(const McL &u, const McqLds &S, int xx, int yy)
     }
     typedef __attribute__((address_space(1))) PIX gpo;
     gpo *dst = (gpo *) u.dst + (size_t) (u.y + yy) * pitch + u.x + xx;
-    if constexpr (RPL) {
-        if (u.rdst) {
-            typedef uint32_t r2u __attribute__((ext_vector_type(2)));
-            typedef __attribute__((address_space(1))) int16_t gi16;
-            typedef __attribute__((address_space(1))) r2u gr2;
-            gi16 *rr = (gi16 *) u.rdst + (size_t) (u.y + yy) * pitch + u.x + xx;
-#pragma unroll
-            for (int t = 0; t < R; t++) {
-                gr2 *rp = (gr2 *) (rr + (size_t) t * pitch);
-                const r2u rv = *rp;
-                if (rv.x | rv.y) {
-                    const int r4[4] = { (int16_t) rv.x, (int16_t) (rv.x >> 16), (int16_t) rv.y, (int16_t) (rv.y >> 16) };
-                    if constexpr (sizeof(PIX) == 1) {
-                        const uint32_t o = outp[t][0];
-                        uint32_t w = 0;
-#pragma unroll
-                        for (int k = 0; k < 4; k++) w |= (uint32_t) med3_0((int) ((o >> (8 * k)) & 255) + r4[k], pmax) << (8 * k);
-                        outp[t][0] = w;
-                    } else {
-#pragma unroll
-                        for (int i = 0; i < 2; i++) {
-                            const uint32_t o = outp[t][i];
-                            outp[t][i] = (uint32_t) med3_0((int) (o & 0xffff) + r4[2 * i], pmax) |
-                                         (uint32_t) med3_0((int) (o >> 16) + r4[2 * i + 1], pmax) << 16;
-                        }
-                    }
-                    r2u z; z.x = 0u; z.y = 0u;
-                    *rp = z;
-                }
-            }
-        }
-    }
 #pragma unroll
     for (int t = 0; t < R; t++) {
         if constexpr (sizeof(PIX) == 1) *(__attribute__((address_space(1))) uint32_t *) (dst + (size_t) t * pitch) = outp[t][0];
@@ -3123,27 +3071,27 @@ DEV void mcq_rows(const McL &u, const McqLds &S, int xx, int yy)
     }
 }
 
-template <typename PIX, int R, bool RPL = false>
+template <typename PIX, int R>
 DEV void mcq_task(const McL &u, const McqLds &S, int xx, int yy)
 {
     const bool v = u.my[0] | (u.nref > 1 ? u.my[1] : 0);
     const bool dir = (u.direct & ((1 << u.nref) - 1)) == ((1 << u.nref) - 1);
     if (__all(dir)) {
-        if (__any(v)) mcq_rows<PIX, R, true, true, RPL>(u, S, xx, yy);
-        else mcq_rows<PIX, R, false, true, RPL>(u, S, xx, yy);
+        if (__any(v)) mcq_rows<PIX, R, true, true>(u, S, xx, yy);
+        else mcq_rows<PIX, R, false, true>(u, S, xx, yy);
     } else {
-        if (__any(v)) mcq_rows<PIX, R, true, false, RPL>(u, S, xx, yy);
-        else mcq_rows<PIX, R, false, false, RPL>(u, S, xx, yy);
+        if (__any(v)) mcq_rows<PIX, R, true, false>(u, S, xx, yy);
+        else mcq_rows<PIX, R, false, false>(u, S, xx, yy);
     }
 }
 
-// one k_mcq workgroup: unit group bx (64 units), task slice by of ns
-template <typename PIX, bool RPL = false>
-DEV void mcq_wg(const McUnit *__restrict__ units, int nunits, const FrameDesc *__restrict__ frames, int bx, int by, int ns,
-                McqLds &S)
+template <typename PIX>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_mcq(const McUnit *__restrict__ units, int nunits,
+                                             const FrameDesc *__restrict__ frames)
 {
+    __shared__ McqLds S;
     const int tid = threadIdx.x;
-    const int u0 = bx * MCP_U, nu = nunits - u0 < MCP_U ? nunits - u0 : MCP_U;
+    const int u0 = blockIdx.x * MCP_U, nu = nunits - u0 < MCP_U ? nunits - u0 : MCP_U;
     {
         // filter rows: 3 x 16 8-tap phases, then the bilinear ones as 8-taps; int8 quads of
         // the non-identity phases (every tap of phases 1-15 lies in [-128, 127])
@@ -3185,7 +3133,7 @@ DEV void mcq_wg(const McUnit *__restrict__ units, int nunits, const FrameDesc *_
     __syncthreads();
     // blockIdx.y: one of gridDim.y slices of the tasks (a workgroup of 64 large units is
     // otherwise the launch's tail: units per workgroup are counted, not their pixels)
-    const int g0 = by * 256, gs = 256 * ns;
+    const int g0 = (int) blockIdx.y * 256, gs = 256 * (int) gridDim.y;
     for (int c = 0; c < 2; c++) {
         const uint32_t T = S.off[c][nu];
         for (uint32_t g = tid + g0; g < T; g += gs) {
@@ -3195,60 +3143,11 @@ DEV void mcq_wg(const McUnit *__restrict__ units, int nunits, const FrameDesc *_
             const int lq = u.lw - 2;                      // 4-column groups per row: w / 4
             const int xx = (int) (ti & ((1u << lq) - 1)) * 4;
             const int yy = (int) (ti >> lq) << (c ? 2 : 3);
-            if (c == 0) mcq_task<PIX, 8, RPL>(u, S, xx, yy);
-            else mcq_task<PIX, 4, RPL>(u, S, xx, yy);
+            if (c == 0) mcq_task<PIX, 8>(u, S, xx, yy);
+            else mcq_task<PIX, 4>(u, S, xx, yy);
         }
     }
-    mcp_scaled<PIX, RPL>(units + u0, S.off[2], nu, frames, tid, g0, gs);
-}
-
-template <typename PIX>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_mcq(const McUnit *__restrict__ units, int nunits,
-                                             const FrameDesc *__restrict__ frames)
-{
-    __shared__ McqLds S;
-    mcq_wg<PIX>(units, nunits, frames, (int) blockIdx.x, (int) blockIdx.y, (int) gridDim.y, S);
-}
-
-// ------------------------------------------------------------- k_mcr
-// VP9HIP_MCR: a level phase (a GOP chain position) p runs k_mcr = k_mcq's workgroups for p,
-// adding the residual planes (RPL), and k_resid_multi's waves for the NEXT position of the
-// chain, storing their in-place residuals to its frames' residual planes (and the intra
-// residuals to the scratch, as before): two launches per position (k_mcr, k_lfro) instead of
-// three (k_mcq, k_resid_multi, k_lfro), with no dependency inside the launch. A chain's first
-// level position gets its residuals from a k_mcr launch without MC workgroups.
-struct McrArgs { ResidMulti r; int nunits, nb, ns, nmc; };
-template <typename PIX, class M, typename COEF>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_mcr(McrArgs a, const McUnit *__restrict__ units, const RJob *__restrict__ jobs,
-                                             const FrameDesc *__restrict__ frames, const COEF *__restrict__ coefs,
-                                             int16_t *__restrict__ resid)
-{
-    static_assert(RWAVES * 64 == 256, "k_mcr: one block size for both parts");
-    constexpr int E = RWave<32, COEF>::E > RWave<16, COEF>::E ? RWave<32, COEF>::E : RWave<16, COEF>::E;
-    __shared__ union McrLds { McqLds mc; COEF cbs[RWAVES][E]; } U;
-    const int b = (int) blockIdx.x;
-    if (b < a.nmc) {
-        mcq_wg<PIX, true>(units, a.nunits, frames, b % a.nb, b / a.nb, a.ns, U.mc);
-        return;
-    }
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t gw = (uint32_t) (b - a.nmc) * RWAVES + wave;
-    if (gw >= a.r.w0[5]) return;
-    int t = 0;
-#pragma unroll
-    for (int k = 1; k < 5; k++) t += gw >= a.r.w0[k];
-    // selects, not an indexed kernel argument (that is copied to scratch)
-    auto sel = [t](const uint32_t *v) { return t == 0 ? v[0] : t == 1 ? v[1] : t == 2 ? v[2] : t == 3 ? v[3] : v[4]; };
-    const int wj = (int) (gw - sel(a.r.w0));
-    const RJob *j = jobs + sel(a.r.off);
-    const int n = (int) sel(a.r.n);
-    switch (t) {
-    case 0: resid_wave<4, 0, PIX, M, COEF, false, true>(j, n, wj, lane, frames, coefs, resid, U.cbs[wave]); break;
-    case 1: resid_wave<8, 1, PIX, M, COEF, false, true>(j, n, wj, lane, frames, coefs, resid, U.cbs[wave]); break;
-    case 2: resid_wave<16, 2, PIX, M, COEF, false, true>(j, n, wj, lane, frames, coefs, resid, U.cbs[wave]); break;
-    case 3: resid_wave<32, 3, PIX, M, COEF, false, true>(j, n, wj, lane, frames, coefs, resid, U.cbs[wave]); break;
-    default: resid_wave<4, 4, PIX, M, COEF, false, true>(j, n, wj, lane, frames, coefs, resid, U.cbs[wave]); break;
-    }
+    mcp_scaled<PIX>(units + u0, S.off[2], nu, frames, tid, g0, gs);
 }
 
 // ------------------------------------------------------------ launchers
@@ -3553,33 +3452,6 @@ int vp9hip_launch_plf(int fmt, hipStream_t st, const PlfLaunch *pl, const uint32
 {
     return (fmt & 1 ? vp9hip_launch_plf_16 : vp9hip_launch_plf_8)(fmt >> 1, st, pl, plist, llist, wgs, sbs, jobs, passes,
                                                                   recs, rjobs, frames, coefs, resid, ptab, dbg);
-}
-// k_mcr: n MC units (0: none) with the residual planes added, and the residual jobs off / rn
-// (by tx code; the next chain position's) with their in-place residuals to the residual planes
-int vp9hip_launch_mcr(int hb, hipStream_t st, int n, const McUnit *units, const uint32_t *off, const uint32_t *rn,
-                      const RJob *jobs, const FrameDesc *frames, const void *coefs, int16_t *resid, const KCfg *k)
-{
-    static const int tn[5] = { 4, 8, 16, 32, 4 };
-    McrArgs a;
-    a.r.w0[0] = 0;
-    for (int t = 0; t < 5; t++) {
-        a.r.off[t] = off[t]; a.r.n[t] = rn[t];
-        const uint32_t per = 64 / tn[t];
-        a.r.w0[t + 1] = a.r.w0[t] + (rn[t] + per - 1) / per;
-    }
-    a.nunits = n;
-    a.nb = n > 0 ? (n + MCP_U - 1) / MCP_U : 0;
-    a.ns = a.nb ? (k->mcq_slices > 0 ? std::min(16, k->mcq_slices) : std::max(2, std::min(8, 4096 / a.nb))) : 0;
-    a.nmc = a.nb * a.ns;
-    const int nr = (int) ((a.r.w0[5] + RWAVES - 1) / RWAVES);
-    if (a.nmc + nr <= 0) return 0;
-    if (hb)
-        hipLaunchKernelGGL((k_mcr<uint16_t, M64, int32_t>), dim3(a.nmc + nr), dim3(256), 0, st, a, units, jobs, frames,
-                           (const int32_t *) coefs, resid);
-    else
-        hipLaunchKernelGGL((k_mcr<uint8_t, M32, int16_t>), dim3(a.nmc + nr), dim3(256), 0, st, a, units, jobs, frames,
-                           (const int16_t *) coefs, resid);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 int vp9hip_launch_mc(int hb, hipStream_t st, int n, const McUnit *units, const FrameDesc *frames, const KCfg *k)
 {

@@ -57,8 +57,6 @@ int vp9hip_launch_predd(int fmt, hipStream_t st, int n, int wgcap, const uint32_
                         const SBRec *sbs, const PJob *jobs, const uint32_t *passes, const FrameDesc *frames,
                         const int16_t *resid, const uint32_t *ptab, uint32_t *ctr, uint32_t *done, int dbg);
 int vp9hip_launch_mc(int hb, hipStream_t st, int n, const McUnit *units, const FrameDesc *frames, const KCfg *k);
-int vp9hip_launch_mcr(int hb, hipStream_t st, int n, const McUnit *units, const uint32_t *off, const uint32_t *rn,
-                      const RJob *jobs, const FrameDesc *frames, const void *coefs, int16_t *resid, const KCfg *k);
 size_t vp9hip_plan_scan_bytes(size_t n);
 int vp9hip_plan_enqueue(hipStream_t st, const PlanDev *D, int ss, int nframes, int max_blk, int max_sb, uint32_t nb,
                         uint32_t nslots, uint32_t ncnt, int nk, const uint32_t *gidx, int ng, uint32_t *summary,
@@ -87,8 +85,7 @@ struct Launch { int kind; uint32_t off; uint32_t n; int arg; int grp; int ph; in
                 uint32_t roff[5] = { 0, 0, 0, 0, 0 }, rn[5] = { 0, 0, 0, 0, 0 };   // K_PLF residual jobs by tx code
                 int devr = 0;   // K_RESID of a static plan: off = the summary index of its job range, n = a bound
                 int flow = -1;  // K_PRED of a level phase as one k_predd launch: its counter block;
-                                // K_LFR with the phase's intra SBs inside (off2 / n2 their list);
-                                // K_MC 2: k_mcr (VP9HIP_MCR), the next position's residual jobs in roff / rn
+                                // K_LFR with the phase's intra SBs inside (off2 / n2 their list)
 };
 #define PLF_LAG 3   // see the schedule in stage()
 // Residuals run inside the fused launches (one intra diagonal ahead) for phases of fewer
@@ -147,8 +144,6 @@ struct Staged {
            o_coefs = 0, o_ctr = 0;
     int16_t *resid = nullptr;           // intra residual scratch (column-major n x n blocks)
     size_t resid_cap = 0;               // bytes
-    int16_t *rpl = nullptr;             // VP9HIP_MCR: residual planes of the level phases' inter frames
-    size_t rpl_cap = 0;                 // bytes (zero between batches: k_mcq zeroes what it adds)
     uint8_t *edge = nullptr;            // intra frames' SB right columns (FrameDesc.edge)
     size_t edge_cap = 0;                // bytes
     bool ready = false;
@@ -327,7 +322,6 @@ struct vp9hip_ctx {
     bool static_plan = true;            // VP9HIP_STATIC=0: keyframe batches planned like the others
     bool edge = true;                   // VP9HIP_EDGE=0: no SB edge columns (4:2:0 tile loader)
     bool resid_multi = true;            // VP9HIP_RESID_MULTI=0: one residual launch per tx size
-    bool mcr = false;                   // VP9HIP_MCR=1: level phases' residuals one position early, added by MC (k_mcr)
     bool stage_trace = false;           // VP9HIP_STAGE_TRACE=1: host time of staging / planning
     bool plan_prof_on = false;          // VP9HIP_PLAN_PROF=1: k_plan phase cycles
     int plan_dbg = 0;                   // VP9HIP_PLAN_DBG: planner ablations (timing only)
@@ -434,7 +428,6 @@ static void read_config(vp9hip_ctx *c)
     c->static_plan = num("VP9HIP_STATIC", 1) != 0;
     c->edge = num("VP9HIP_EDGE", 1) != 0;
     c->resid_multi = num("VP9HIP_RESID_MULTI", 1) != 0;
-    c->mcr = num("VP9HIP_MCR", 0) != 0;
     c->stage_trace = num("VP9HIP_STAGE_TRACE", 0) != 0;
     c->plan_prof_on = num("VP9HIP_PLAN_PROF", 0) != 0;
     c->plan_dbg = num("VP9HIP_PLAN_DBG", 0);
@@ -525,7 +518,6 @@ extern "C" void vp9hip_close(vp9hip_ctx *c)
         Staged *g = &slot_ref(c, k);
         if (g->arena) hipFree(g->arena);
         if (g->resid) hipFree(g->resid);
-        if (g->rpl) hipFree(g->rpl);
         if (g->edge) hipFree(g->edge);
         if (g->pinned) hipHostFree(g->pinned);
         if (g->graph) hipGraphExecDestroy(g->graph);
@@ -1764,20 +1756,6 @@ static int plan_dev(vp9hip_ctx *c)
     }
     const uint32_t H = s.host_lists;
     const int nph = (int) s.dph.size();
-    // VP9HIP_MCR: a level phase's residual jobs run in the previous position's k_mcr launch
-    // (or a k_mcr launch of their own at a chain's first level position), and its MC adds
-    // the residual planes they wrote; no k_resid_multi launch
-    auto rpl_phase = [&](int ph) {
-        const Staged::DevPhase &P = s.dph[ph];
-        return c->mcr && c->resid_multi && !c->host_plan && !P.fused && P.levels && !P.frames.empty();
-    };
-    auto res_range = [&](int ph, int tc) {
-        const Staged::DevPhase &P = s.dph[ph];
-        const uint32_t a = gv[P.g_res + tc * 2], b = gv[P.g_res + tc * 2 + 1];
-        return std::make_pair(a, b - a);
-    };
-    auto nres = [&](int ph) { uint32_t t = 0; for (int tc = 0; tc < 5; tc++) t += res_range(ph, tc).second; return t; };
-    std::vector<char> attached(nph, 0);
     for (int g = 0; g < s.ngroups; g++)
         for (int ph = 0; ph < nph; ph++) {
             const Staged::DevPhase &P = s.dph[ph];
@@ -1787,25 +1765,7 @@ static int plan_dev(vp9hip_ctx *c)
                 s.launches.push_back(L);
             };
             const uint32_t m0 = gv[P.g_mc], m1 = gv[P.g_mc + 1];
-            if (rpl_phase(ph)) {
-                if (!attached[ph] && nres(ph)) {                    // a chain's first level position
-                    Launch L = { K_MC, 0, 0, 0, g, ph, PART_RECON, 0 };
-                    L.flow = 2;
-                    for (int tc = 0; tc < 5; tc++) { L.roff[tc] = res_range(ph, tc).first; L.rn[tc] = res_range(ph, tc).second; }
-                    s.launches.push_back(L);
-                }
-                if (m1 > m0) {
-                    Launch L = { K_MC, m0, m1 - m0, 0, g, ph, PART_RECON, 0 };
-                    L.flow = 2;
-                    int nx = ph + 1;                                // the next position of the chain
-                    while (nx < nph && (s.dph[nx].frames.empty() || s.dph[nx].group != g)) nx++;
-                    if (nx < nph && rpl_phase(nx) && nres(nx)) {
-                        for (int tc = 0; tc < 5; tc++) { L.roff[tc] = res_range(nx, tc).first; L.rn[tc] = res_range(nx, tc).second; }
-                        attached[nx] = 1;
-                    }
-                    s.launches.push_back(L);
-                }
-            } else if (m1 > m0) push(K_MC, m0, m1 - m0, 0, PART_RECON, 0);
+            if (m1 > m0) push(K_MC, m0, m1 - m0, 0, PART_RECON, 0);
             auto rr = [&](int d, int tc) {
                 const uint32_t a = gv[P.g_res + (d * 5 + tc) * 2], b = gv[P.g_res + (d * 5 + tc) * 2 + 1];
                 return std::make_pair(a, b - a);
@@ -1813,9 +1773,7 @@ static int plan_dev(vp9hip_ctx *c)
             // level-scheduled (inter chain) phases: every tx size in one launch (arg 5, the
             // ranges in roff / rn); VP9HIP_RESID_MULTI=0 keeps one launch per size
             const bool rmulti = c->resid_multi;
-            if (rpl_phase(ph)) {
-                // residuals in k_mcr launches (above)
-            } else if (!P.fused && P.levels && rmulti) {
+            if (!P.fused && P.levels && rmulti) {
                 Launch L = { K_RESID, 0, 0, 5, g, ph, PART_RECON, 0 };
                 for (int tc = 0; tc < 5; tc++) { L.roff[tc] = rr(0, tc).first; L.rn[tc] = rr(0, tc).second; L.n += L.rn[tc]; }
                 if (L.n) s.launches.push_back(L);
@@ -2092,25 +2050,6 @@ static int stage(vp9hip_ctx *c, const vp9h_frame *pkts, int n, const int *out_bu
         }
         for (FrameDesc &fd : s.frames)
             fd.edge = fd.edge && !edge_off ? (uint64_t) (s.edge + (size_t) (fd.edge - 1) * EDGE_PIX * c->bypp) : 0;
-    }
-    // VP9HIP_MCR: a residual plane per inter frame of a level phase (int16, the frame
-    // buffer's element layout), all zero between batches
-    if (c->mcr && c->resid_multi && !c->host_plan && !tiled) {
-        const size_t fe = c->buf_bytes / c->bypp;              // elements per frame
-        size_t nf = 0;
-        for (int i = 0; i < n; i++) nf += fbs[i].levels && !fbs[i].by_diag && !(pkts[i].keyframe || pkts[i].intraonly);
-        if (nf * fe * 2 > s.rpl_cap) {
-            if (s.rpl) hipFree(s.rpl);
-            s.rpl = nullptr;
-            s.rpl_cap = 0;
-            if (hipMalloc(&s.rpl, nf * fe * 2) != hipSuccess) return VP9HIP_ENOMEM;
-            if (hipMemset(s.rpl, 0, nf * fe * 2) != hipSuccess) return VP9HIP_EEXTERNAL;
-            s.rpl_cap = nf * fe * 2;
-        }
-        size_t k = 0;
-        for (int i = 0; i < n; i++)
-            if (fbs[i].levels && !fbs[i].by_diag && !(pkts[i].keyframe || pkts[i].intraonly))
-                s.frames[i].rplane = (uint64_t) (s.rpl + fe * k++);
     }
 
     STAGE_T(0);
@@ -2562,12 +2501,6 @@ static int launch_one(vp9hip_ctx *c, const Launch &L, hipStream_t st)
     if ((c->dbg >> 29 & 1) && L.kind == K_MC) return 0;
     switch (L.kind) {
     case K_MC:
-        if (L.flow == 2) {
-            static const uint32_t none[5] = { 0, 0, 0, 0, 0 };   // bit 27: no residual jobs (timing only)
-            return vp9hip_launch_mcr(c->hb, st, (int) L.n, (const McUnit *) (s.arena + s.o_mcs) + L.off, L.roff,
-                                     (c->dbg >> 27 & 1) ? none : L.rn, (const RJob *) (s.arena + s.o_rjobs), fr,
-                                     s.arena + s.o_coefs, s.resid, &c->kcfg);
-        }
         return vp9hip_launch_mc(c->hb, st, (int) L.n, (const McUnit *) (s.arena + s.o_mcs) + L.off, fr, &c->kcfg);
     case K_RESID:
         if (L.devr)

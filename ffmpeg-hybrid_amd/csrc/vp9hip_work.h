@@ -27,11 +27,6 @@ typedef struct FrameDesc {
                                  EDGE_PIX pixels (luma 64, then the chroma planes' rows),
                                  written by its intra workgroup, read by the SB to its
                                  right instead of 128 one-pixel frame rows; 0: none     */
-    uint64_t rplane;          /* VP9HIP_MCR: int16 residual planes, element for element the
-                                 pixel planes' layout (plane p at (plane[p] - plane[0]) /
-                                 bytes per pixel elements): a level phase's inter residuals,
-                                 written one chain position early, added (and zeroed again)
-                                 by k_mcq; 0: none                                         */
 } FrameDesc;
 #define EDGE_PIX 192          /* pixels per SB in FrameDesc.edge (64 + 2 x 64 at 4:4:4) */
 
