@@ -420,14 +420,15 @@ DEV uint32_t wor(uint32_t v) { return rdl(wscan_dpp<OP_OR>(v), 63); }
 // bucketed by transform), and the intra jobs' words with check_intra_mode resolved, for
 // k_plan. Small LDS (4.8 KB at 4:2:0): a kernel of its own so this per-tx work runs at full
 // occupancy instead of with k_plan's scheduling state.
+// ja: k_pjplan's LDS job words (the intra job words go there, not to D.jobw); returns the
+// SB's intra job count for k_plan's part, -1 past the frame
 template <int SSH, int SSV>
-__global__ __launch_bounds__(64) void k_pjob(PlanDev D)
+DEV int pjob_sb(const PlanDev &D, PJobLds<256 + 2 * (16 >> SSH) * (16 >> SSV)> &S, uint32_t *ja)
 {
     constexpr int CW = 16 >> SSH, CH = 16 >> SSV, JCAP = 256 + 2 * CW * CH;
-    __shared__ PJobLds<JCAP> S;
     const PlanFrame &F = D.frames[blockIdx.y];
     const int s = blockIdx.x, lane = threadIdx.x;
-    if (s >= F.sb_cols * F.sb_rows) return;
+    if (s >= F.sb_cols * F.sb_rows) return -1;
     unsigned long long pt0 = D.prof ? clock64() : 0;
     const SbGeo G = sb_geo(F, s);
     const int cols = F.mc.cols, rows = F.mc.rows;
@@ -555,7 +556,10 @@ __global__ __launch_bounds__(64) void k_pjob(PlanDev D)
                 const int pw8 = p ? cols * 8 >> SSH : cols * 8, ph8 = p ? rows * 8 >> SSV : rows * 8;
                 const PlIntra pi = pl_intra_job(p, txs, mode, e0, tx.g.bx + tx.x * 4, tx.g.by + tx.y * 4, tx.x, tx.g.pw4,
                                                 p ? tx0l >> SSH : tx0l, pw8, ph8, ux0, uy0);
-                if (j < JCAP) D.jobw[(size_t) slot * JCAP + (uint32_t) j] = pi.a | (pi.trx ? JA_TRX : 0u);
+                if (j < JCAP) {
+                    if (ja) ja[j] = pi.a | (pi.trx ? JA_TRX : 0u);
+                    else D.jobw[(size_t) slot * JCAP + (uint32_t) j] = pi.a | (pi.trx ? JA_TRX : 0u);
+                }
             }
         }
         // ranks within each key, in decode order: one ballot per distinct key of the chunk
@@ -575,12 +579,19 @@ __global__ __launch_bounds__(64) void k_pjob(PlanDev D)
     }
     for (int d = 32; d; d >>= 1) ibytes += __shfl_xor(ibytes, d);
     if (lane == 0) {
-        D.sb_nj[slot] = (uint32_t) (G.mine ? NJ : 0);
+        if (!ja) D.sb_nj[slot] = (uint32_t) (G.mine ? NJ : 0);
         if (ibytes && inb(D, (uint32_t) F.frame, D.nframes, 2048u)) atomicAdd(&D.fbytes[2 * F.frame], ibytes);
     }
     st = wor(st);
     if (lane == 0 && st) plan_fail(D, F, st);
     PPT(2);
+    return G.mine ? NJ : 0;
+}
+template <int SSH, int SSV>
+__global__ __launch_bounds__(64) void k_pjob(PlanDev D)
+{
+    __shared__ PJobLds<256 + 2 * (16 >> SSH) * (16 >> SSV)> S;
+    pjob_sb<SSH, SSV>(D, S, nullptr);
 }
 
 // One wave per SB: producers of every intra job, heights, priority order, list-scheduled
@@ -589,11 +600,11 @@ __global__ __launch_bounds__(64) void k_pjob(PlanDev D)
 // (Two SBs per wave with the second's job words loaded under the first's scheduling cut the
 // first load's share of a wave's cycles from 31 to 20 %, but not the kernel: 2,880 -> 2,926 us
 // per C3 batch. The waves' time goes to dependent LDS chains at 6 waves per SIMD, LDS-bound.)
+// nj >= 0 (k_pjplan): the SB's job words are in S.ja already, nj of them
 template <int SSH, int SSV>
-__global__ __launch_bounds__(64) void k_plan(PlanDev D)
+DEV void plan_sb(const PlanDev &D, PlanLds<256 + 2 * (16 >> SSH) * (16 >> SSV)> &S, int nj)
 {
     constexpr int CW = 16 >> SSH, CH = 16 >> SSV, JCAP = 256 + 2 * CW * CH, NCH = JCAP / 64;
-    __shared__ PlanLds<JCAP> S;
     const PlanFrame &F = D.frames[blockIdx.y];
     const int s = blockIdx.x, lane = threadIdx.x;
     if (s >= F.sb_cols * F.sb_rows) return;
@@ -602,9 +613,10 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
     const uint32_t slot = G.slot;
     const uint32_t rbase = slot * D.rcap;
     uint32_t st = 0;
-    const int NJ = pl_min((int) D.sb_nj[slot], JCAP);
+    const int NJ = pl_min(nj >= 0 ? nj : (int) D.sb_nj[slot], JCAP);
     for (int i = lane; i < 3 * 256 / 8; i += 64) ((uint4 *) &S.u.jmap[0][0])[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
-    for (int j = lane; j < NJ; j += 64) S.ja[j] = D.jobw[(size_t) slot * JCAP + (uint32_t) j];
+    if (nj < 0)
+        for (int j = lane; j < NJ; j += 64) S.ja[j] = D.jobw[(size_t) slot * JCAP + (uint32_t) j];
     wsync();
     PPT(8);
     // the unit map: each job's 4x4 units hold JM_ENT(job, units to the job's right edge, units
@@ -905,6 +917,31 @@ __global__ __launch_bounds__(64) void k_plan(PlanDev D)
     if (lane == 0 && st) plan_fail(D, F, st);
     PPT(10);
 }
+template <int SSH, int SSV>
+__global__ __launch_bounds__(64) void k_plan(PlanDev D)
+{
+    __shared__ PlanLds<256 + 2 * (16 >> SSH) * (16 >> SSV)> S;
+    plan_sb<SSH, SSV>(D, S, -1);
+}
+// k_pjob and k_plan of one SB in one wave: the intra job words stay in LDS (no D.jobw round
+// trip through HBM, one wave start instead of two). k_pjob's LDS overlays k_plan's unit
+// map / schedule region, which k_plan writes only after the job words are in place, so the
+// fused wave keeps k_plan's 7.2 KB (4:2:0). VP9HIP_PLAN_DBG bit 3: the two kernels.
+template <int SSH, int SSV>
+__global__ __launch_bounds__(64) void k_pjplan(PlanDev D)
+{
+    constexpr int JCAP = 256 + 2 * (16 >> SSH) * (16 >> SSV);
+    typedef PlanLds<JCAP> PL;
+    __shared__ union alignas(16) {
+        PL pl;
+        struct { uint32_t ja[JCAP]; PJobLds<JCAP> pj; } pjx;   // pj over pl.u
+    } U;
+    static_assert(offsetof(PL, u) == sizeof(uint32_t) * JCAP, "k_pjob's LDS overlays k_plan's union, not its job words");
+    const int nj = pjob_sb<SSH, SSV>(D, U.pjx.pj, U.pl.ja);
+    if (nj < 0) return;
+    wsync();
+    plan_sb<SSH, SSV>(D, U.pl, nj);
+}
 
 // ------------------------------------------------------------------ k_plmc
 // MC units of the SB's inter blocks in decode order (vp9_mc_template.c:30-464), one wave per
@@ -1176,8 +1213,11 @@ void launch_sb_kernels(hipStream_t st, const PlanDev &D, int max_sb, int nframes
 {
     const dim3 g(max_sb, nframes);
     if (stage == 0) { hipLaunchKernelGGL((k_psb<SSH, SSV>), g, dim3(64), 0, st, D); return; }
-    hipLaunchKernelGGL((k_pjob<SSH, SSV>), g, dim3(64), 0, st, D);
-    hipLaunchKernelGGL((k_plan<SSH, SSV>), g, dim3(64), 0, st, D);
+    if (D.dbg & 8) {                                             // VP9HIP_PLAN_DBG bit 3: unfused
+        hipLaunchKernelGGL((k_pjob<SSH, SSV>), g, dim3(64), 0, st, D);
+        hipLaunchKernelGGL((k_plan<SSH, SSV>), g, dim3(64), 0, st, D);
+    } else
+        hipLaunchKernelGGL((k_pjplan<SSH, SSV>), g, dim3(64), 0, st, D);
     if (flags & 1) hipLaunchKernelGGL((k_pllf<SSH, SSV>), g, dim3(64), 0, st, D);
     if (flags & 2) hipLaunchKernelGGL((k_plmc<SSH, SSV>), g, dim3(64), 0, st, D);
 }
