@@ -51,7 +51,7 @@ SEED0 = 0x56503900 + CONFIG_INDEX
 # rocprofv3 passes of the default C3 bench's serialised timing steps (tools/profile.sh with
 # --serial-only): the kernel trace the roofline's launch duration is checked against, and
 # the PMC passes its traffic / issue fields come from
-TRAFFIC_PROFILE = "r06j/C3"
+TRAFFIC_PROFILE = "r06t/C3"
 POISON = 0xA5                  # fill byte of the frame buffers before the timed steps
 
 
