@@ -145,6 +145,13 @@ def aggregate(frames_per_rank, steps, world, elapsed_max):
     return total / elapsed_max, elapsed_max * 1000.0 / steps
 
 
+def dominant_kernel(names, ksum):
+    """The roofline's kernel class: the largest serialised time among the pixel kernels
+    (the planner's span "k_plan" is excluded, see main)."""
+    pix = [k for k in names if k != "k_plan"]
+    return max(pix, key=lambda k: ksum.get(k, [0.0, 0])[0])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -262,11 +269,11 @@ def main():
 
     # dominant kernel (largest device time; the timing steps run every launch on one stream,
     # so these are serialised launch durations, as under a rocprofv3 kernel trace). The
-    # planner's class ("k_plan") is one span over its ~12 kernels (k_pblk, the scans, k_psb,
-    # k_pjob, k_plan, k_pllf, ...; the largest of them, k_plan, is 2.9 ms of its 4.3 per C3
-    # step), not a kernel, and its bytes are not part of BASELINE.md's B: the roofline is taken
-    # for the largest pixel kernel
-    dom = max([k for k in names if k != "k_plan"], key=lambda k: ksum.get(k, [0.0, 0])[0])
+    # planner's class ("k_plan") is one span over its ~10 kernels (k_pblk, the scans, k_psb,
+    # k_pjplan, k_pllf, ...; the largest of them, k_pjplan, is 3.4 ms of its 4.2 per C3 step),
+    # not a kernel, and its bytes are not part of BASELINE.md's B: the roofline is taken for
+    # the largest pixel kernel
+    dom = dominant_kernel(names, ksum)
     kms, kn = ksum[dom]
     launches_per_step = kn / args.steps
     bytes_per_launch = alg[dom] / launches_per_step if launches_per_step else 0.0
